@@ -1,0 +1,42 @@
+# Build libskm (HIP, gfx950), the host CLIs, and the CPU oracle (test infrastructure).
+#   make            -> signature_kmers_amd/libskm.so, bin/kmers-*, oracle/liboracle_skm.so
+HIPCC   ?= /opt/rocm/bin/hipcc
+CXX     ?= g++
+ARCH    ?= gfx950
+JOBS    ?= 8
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
+           -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -Wall -Wno-unused-function
+OBJDIR   = build/obj
+SRC      = signature_kmers_amd/csrc
+HIP_SRCS = $(SRC)/skm_build.hip $(SRC)/skm_annotate.hip
+CPP_SRCS = $(SRC)/skm_host.cpp $(SRC)/skm_bdz.cpp
+OBJS     = $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(CPP_SRCS))
+LIB      = signature_kmers_amd/libskm.so
+TOOLS    = bin/kmers-build-signatures bin/kmers-call-functions bin/kmers-annotate-seqs
+ORACLE   = oracle/liboracle_skm.so
+
+all: $(LIB) $(ORACLE)
+tools: $(TOOLS)
+
+$(OBJDIR)/%.o: $(SRC)/%.hip $(wildcard $(SRC)/*.h) include/skm.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/%.o: $(SRC)/%.cpp $(wildcard $(SRC)/*.h) include/skm.h
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS)
+
+bin/%: $(SRC)/tools/%.cpp $(LIB) $(wildcard $(SRC)/*.h)
+	@mkdir -p bin
+	$(HIPCC) -O2 -std=c++17 -Iinclude -I$(SRC) $< -o $@ -L signature_kmers_amd -lskm -Wl,-rpath,'$$ORIGIN/../signature_kmers_amd'
+
+$(ORACLE): oracle/skm_oracle.cpp
+	$(CXX) -O2 -fPIC -shared -std=c++17 -ffp-contract=off $< -o $@
+
+clean:
+	rm -rf build bin $(LIB) $(ORACLE)
+
+.PHONY: all clean

@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""bench.py -- signature-k-mer build throughput on MI355X (BASELINE.json metric).
+
+Metric: k-mers/sec (windows examined by extract+hash+count+cut), whole job over N GPUs.
+Workload at N=1: BASELINE configs[1] -- 1M synthetic protein sequences, k=8, signature build on
+one MI355X (SURVEY.md 8(d) generator, seed 20241115).  At N>1 each rank builds its own shard of
+1M sequences (weak scaling).
+
+One step = one full device pass of the build pipeline over the HBM-resident input
+(extract/count, scan, extract/scatter, bucket group-by + cut + statistics, overflow, stats).
+Inputs are uploaded before the timed region; outputs stay on the device.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]   (N>1 under torch.distributed.run)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--seqs", type=int, default=1_000_000, help="sequences per GPU")
+    ap.add_argument("--families", type=int, default=4000)
+    ap.add_argument("--cpu-sample-seqs", type=int, default=40_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo: barrier + max over ranks (host side only)
+        dist.init_process_group("gloo")
+    import signature_kmers_amd as skm
+    from signature_kmers_amd import synth
+
+    # ---- synthetic shard (one RNG stream per file: shards are rank-independent) ----
+    per_file = 4000
+    files_per_rank = (a.seqs + per_file - 1) // per_file
+    t0 = time.time()
+    p = synth.generate_arrays(a.seqs * world, a.families, per_file=per_file, first_file=rank * files_per_rank,
+                              n_files=files_per_rank)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    gen_s = time.time() - t0
+    n_windows = int(np.where((f != 0xFFFF) & (l >= 8), l.astype(np.int64) - 7, 0).sum())
+
+    b = skm.SignatureBuilder(len(funcs), device=local)
+    b.add_batch(r, o, l, f, i)
+    b.prepare()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        b.run()
+    phase = {}
+    barrier()
+    t1 = time.perf_counter()
+    for _ in range(a.steps):
+        b.run()
+        for k, v in b.timings().items():
+            phase[k] = phase.get(k, 0.0) + v
+    t_local = time.perf_counter() - t1  # run() returns after its final event has completed
+    barrier()
+    t_max = t_local
+    if dist is not None:
+        import torch
+        tt = torch.tensor([t_local], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+        nw = torch.tensor([n_windows], dtype=torch.float64)
+        dist.all_reduce(nw, op=dist.ReduceOp.SUM)
+        total_windows = float(nw.item())
+    else:
+        total_windows = float(n_windows)
+    kept = b.finish()
+    ms_per_step = 1000.0 * t_max / a.steps
+    value = total_windows * a.steps / t_max
+    phase = {k: v / a.steps for k, v in phase.items()}
+
+    # ---- roofline: dominant kernel (bucket group-by) and the whole pipeline ----
+    n_records = int(kept.n_windows)  # upper bound; exact record count below
+    res_bytes = int(len(r) + len(l))
+    valid = _valid_windows(r, o, l, f)
+    n_kept = len(kept.keys)
+    dom = max(("extract_count", "extract_scatter", "bucket_process"), key=lambda k: phase.get(k, 0.0))
+    alg = {
+        "extract_count": res_bytes,
+        "extract_scatter": res_bytes + 8 * valid,
+        "bucket_process": 8 * valid + 18 * n_kept,
+    }
+    dom_ms = phase[dom]
+    achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
+    pipe_alg = res_bytes + 32 * valid + 18 * n_kept  # SURVEY 8(d) B_alg
+    pipe_gbs = pipe_alg / (phase["total"] * 1e-3) / 1e9
+    traffic = _pmc_traffic(dom, a.seqs)
+
+    out = {
+        "metric": "k-mers/sec (extract+hash+count) at 1/2/4/8 GPUs; achieved HBM GB/s %",
+        "value": value,
+        "unit": "k-mers/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (SURVEY 8(d) generator, seed 20241115)",
+        "config": {"workload": "C2: 1M protein seqs/GPU, k=8, signature build (extract+group+cut+stats)",
+                   "seqs_per_gpu": a.seqs, "families": a.families, "windows_per_gpu": n_windows,
+                   "valid_windows_per_gpu": valid, "kept_kmers_rank0": n_kept,
+                   "parallelism": "single GPU" if world == 1 else f"{world} GPUs, independent shards"},
+        "roofline": {"bound": "hbm", "kernel": f"k_{dom}", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "alg_bytes_per_launch": alg[dom], "avg_launch_ms": dom_ms},
+        "pipeline": {"alg_bytes": pipe_alg, "ms": phase["total"], "GBs": pipe_gbs, "frac": pipe_gbs / HBM_PEAK_GBS,
+                     "phase_ms": phase},
+        "cpu_baseline": None,
+        "gen_seconds": gen_s,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = _cpu_baseline(r, o, l, f, i, len(funcs), a.cpu_sample_seqs)
+    b.close()
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as fh:
+                fh.write(line + "\n")
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _valid_windows(r, o, l, f) -> int:
+    """Count of windows whose 8 residues are all in ok_prot_ (records the build materialises)."""
+    ok = np.zeros(256, bool)
+    ok[np.frombuffer(b"ACDEFGHIKLMNPQRSTVWYacdefghiklmnpqrstvwy", np.uint8)] = True
+    good = ok[r].astype(np.int32)
+    c = np.concatenate([[0], np.cumsum(good)])
+    total = 0
+    for s0, ln, fn in zip(o.astype(np.int64), l.astype(np.int64), f):
+        if fn == 0xFFFF or ln < 8:
+            continue
+        w = c[s0 + 8:s0 + ln + 1] - c[s0:s0 + ln - 7]
+        total += int((w == 8).sum())
+    return total
+
+
+def _pmc_traffic(kernel: str, seqs: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json),
+    when it was measured on this kernel and workload; else None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        e = d["kernels"][f"k_{kernel}"]
+        if int(d.get("seqs_per_gpu", -1)) != seqs:
+            return None
+        return e["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def _cpu_baseline(r, o, l, f, i, nf, n_sample):
+    """The oracle (C++ restatement, single thread) on the first n_sample sequences."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ref
+    n = min(n_sample, len(l))
+    end = int(o[n - 1]) + int(l[n - 1])
+    t = time.perf_counter()
+    oracle_ref.build(r[:end], o[:n], l[:n], f[:n], i[:n], nf)
+    dt = time.perf_counter() - t
+    w = oracle_ref.count_windows(l[:n], f[:n])
+    return {"value": w / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} sequences of the same workload ({w} windows), {dt:.1f} s, "
+                      f"oracle/skm_oracle.cpp single-thread (--n-threads 1 semantics)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,197 @@
+/*
+ * skm.h -- C-ABI of libskm, the MI355X-native signature-k-mer engine.
+ *
+ * This is the drop-in boundary for the reference's hot path (olsonanl/signature_kmers @ 2024-11-15).
+ * The reference has no FFI; its boundary is a C++ template API.  Each entry point below names the
+ * reference interface it replaces (paths relative to the reference's src/).
+ *
+ * Conventions
+ *   - Plain C types only.  No exceptions cross the boundary.
+ *   - Return value: 0 = OK, < 0 = error class (SKM_E_*).  skm_last_error() holds a message
+ *     (thread-local).
+ *   - Host buffers passed in are caller-owned and are copied before the call returns.
+ *   - Buffers returned in out-structs are library-owned; release them with the matching *_free.
+ *   - A k-mer key is the 8 residue bytes as a little-endian uint64 (byte 0 = first residue),
+ *     i.e. Kmer<8> = std::array<char,8> reinterpreted (kmer_data.h:37).
+ *   - Handles are driven from one host thread at a time.
+ */
+#ifndef SKM_H
+#define SKM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SKM_OK 0
+#define SKM_E_ARG -1      /* invalid argument / limit exceeded                    */
+#define SKM_E_HIP -2      /* HIP runtime error (incl. no device)                  */
+#define SKM_E_OOM -3      /* device or host allocation failed                     */
+#define SKM_E_IO -4       /* file I/O or format error                             */
+#define SKM_E_COMM -5     /* RCCL error                                           */
+#define SKM_E_STATE -6    /* call out of order                                    */
+
+#define SKM_UNDEFINED_FUNCTION 0xFFFFu /* kmer_data.h:23 UndefinedFunction */
+
+/* StoredKmerData (kmer_data.h:114-128): five little-endian u16, 10 bytes, the kmer_data.dat
+ * record (perfect_hash.h:62 writes sizeof(StoredKmerData)=10 per MPH slot). */
+#pragma pack(push, 1)
+typedef struct skm_stored_kmer_data {
+    uint16_t avg_from_end;
+    uint16_t function_index;
+    uint16_t mean;
+    uint16_t median;
+    uint16_t var;
+} skm_stored_kmer_data;
+#pragma pack(pop)
+
+/* KmerCall (call_functions.h:23-48). 24 bytes. */
+typedef struct skm_kmer_call {
+    uint32_t start;
+    uint32_t end;
+    int32_t count;
+    uint16_t function_index;
+    uint16_t pad;
+    uint32_t protein_length_median;
+    float protein_length_med_avg_dev;
+} skm_kmer_call;
+
+const char* skm_last_error(void);
+const char* skm_version(void);
+int skm_device_count(int* n);
+
+/* ------------------------------------------------------------------------------------------
+ * Signature build.  Replaces SignatureBuilder<K>::extract_kmers + process_kmers
+ * (signature_build.h:55-110, signature_build.tcc:48-293) as driven by kmers-build-signatures.cc
+ * :193-196, and the consumers kept_kmers()/kmer_stats() (signature_build.h:106-107).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct skm_build skm_build;
+
+typedef struct skm_build_opts {
+    int32_t k;                  /* must be 8 (kmers-build-signatures.cc:17 K=8)                 */
+    uint32_t max_seqs_per_file; /* 100000 (kmers-build-signatures.cc:18); informational        */
+    uint32_t n_functions;       /* size of function.index (FunctionIndex upper bound, < 65535)  */
+    int32_t canonical_order;    /* 1: n_threads=1 reference semantics (the only mode)           */
+    int32_t rank;               /* this process's rank (0 for single GPU)                        */
+    int32_t world_size;         /* number of GPUs/processes: 1, 2, 4 or 8                        */
+} skm_build_opts;
+
+/* Kept k-mers (KeptKmers<8>, signature_build.h:52-53) + KmerStatistics (:44-50). */
+typedef struct skm_kept {
+    uint64_t* keys;                  /* [n] k-mer keys, sorted ascending                       */
+    skm_stored_kmer_data* data;      /* [n] packed 10-byte records                              */
+    uint64_t n;                      /* kept k-mers ("Kept N kmers")                            */
+    uint32_t* distinct_functions;    /* [n_functions] kept k-mers per best function              */
+    uint32_t* seqs_with_func;        /* [n_functions] sequences per function                    */
+    uint32_t n_functions;
+    uint64_t n_seqs_with_signature;  /* "num_seqs_with_a_signature="                            */
+    uint64_t distinct_signatures;    /* "distinct_signatures="                                  */
+    uint64_t n_windows;              /* windows examined (metric units)                         */
+    uint64_t n_records;              /* valid windows (occurrences)                             */
+} skm_kept;
+
+/* devices: HIP device ordinals (n_devices == 1 per process; multi-GPU is one process per GPU). */
+int skm_build_create(skm_build** out, const int* devices, int n_devices, const skm_build_opts* opts);
+
+/* One batch of sequences in reference emission order (file order, then sequence order).
+ * residues: concatenated residue bytes; sequence s is residues[seq_off[s] .. +seq_len[s]).
+ * seq_func: FunctionIndex of the sequence's assigned function, or 0xFFFF when the sequence has
+ *           no kept function (the reference skips it, signature_build.tcc:133-158).
+ * seq_id:   file_number*max_seqs_per_file + k (signature_build.tcc:91,138).                   */
+int skm_build_add_batch(skm_build* b, const uint8_t* residues, const uint64_t* seq_off,
+                        const uint32_t* seq_len, const uint16_t* seq_func, const uint32_t* seq_id,
+                        size_t n_seqs);
+
+/* Upload + pack everything added so far into HBM (idempotent). */
+int skm_build_prepare(skm_build* b);
+/* Run the device pipeline over the resident input; results stay on the device. */
+int skm_build_run(skm_build* b);
+/* Device time (ms) of the last run's phases: [0]=extract-count [1]=scan [2]=extract-scatter
+ * [3]=bucket-process [4]=overflow [5]=stats [6]=total; returns number of entries written. */
+int skm_build_last_timings(skm_build* b, float* ms, int cap);
+/* Run (if not yet run since the last prepare) and download the result. */
+int skm_build_finish(skm_build* b, skm_kept* out);
+void skm_kept_free(skm_kept* k);
+void skm_build_destroy(skm_build* b);
+
+/* ------------------------------------------------------------------------------------------
+ * Multi-GPU (one process per GPU).  Rank 0 calls skm_comm_unique_id, the caller broadcasts the
+ * 128 bytes (e.g. torch.distributed over gloo), every rank passes them to
+ * skm_build_set_comm before skm_build_run.  Owner of a k-mer = top bits of its hashed key;
+ * records are exchanged with one RCCL all-to-all over xGMI.
+ * ------------------------------------------------------------------------------------------ */
+int skm_comm_unique_id(uint8_t id[128]);
+int skm_build_set_comm(skm_build* b, const uint8_t id[128]);
+
+/* ------------------------------------------------------------------------------------------
+ * Signature DB (CmphKmerDb<StoredKmerData,8>, cmph_kmer.h:28-164).  Reads a cmph BDZ dump
+ * (<dir>/kmer_data.mph) + the dense record file (<dir>/kmer_data.dat) and lays g, the rank table
+ * and the records out contiguously in HBM.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct skm_db skm_db;
+
+int skm_db_open(skm_db** out, const char* mph_path, const char* dat_path, int device);
+int skm_db_open_mem(skm_db** out, const uint8_t* mph, size_t mph_len, const uint8_t* dat,
+                    size_t dat_len, int device);
+/* cmph_size() (cmph_kmer.h:102) */
+int skm_db_size(skm_db* db, uint32_t* m);
+/* Batched cmph_search(hash, key, 8) (cmph_kmer.h:90-92); idx >= size is a miss. */
+int skm_db_lookup(skm_db* db, const uint64_t* keys, size_t n, uint32_t* idx_out);
+void skm_db_close(skm_db* db);
+
+/* Build a BDZ minimal perfect hash over keys (build_perfect_hash, perfect_hash.h:11-69):
+ * writes a cmph-compatible .mph image and the .dat records (data[i] goes to slot search(key i)).
+ * seed: initial PRNG seed for the hash seed draws (cmph uses rand() % 15).                     */
+int skm_mph_build(const uint64_t* keys, const skm_stored_kmer_data* data, size_t n, uint32_t seed,
+                  const char* mph_path, const char* dat_path);
+
+/* ------------------------------------------------------------------------------------------
+ * Function calling.  Replaces FunctionCaller<CmphKmerDb>::process_aa_seq for a batch of query
+ * sequences (call_functions.tcc:259-338 + HitSet :6-108, window iterator kmer_data.h:76-102).
+ * find_best_call (call_functions.tcc:347-659) stays on the host: skm_find_best_call.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct skm_annot_opts {
+    int32_t min_hits;      /* 5   (call_functions.h:66)                                   */
+    int32_t max_gap;       /* 200                                                          */
+    int32_t ignore_hypo;   /* --ignore-hypo                                                */
+    int32_t hypo_index;    /* index of "hypothetical protein" in function.index           */
+    int32_t mean_mode;     /* Boost.Math mean: 0 = >=1.76 four-lane (default), 1 = <=1.75  */
+    int32_t mad_mode;      /* 0 = |x(mid)-median| (the only mode on the device)            */
+} skm_annot_opts;
+
+typedef struct skm_calls {
+    uint64_t* call_off;    /* [n_seqs+1] CSR offsets                                       */
+    skm_kmer_call* calls;  /* [n_calls]                                                    */
+    uint64_t n_seqs;
+    uint64_t n_calls;
+    uint64_t n_windows;    /* query windows examined                                       */
+} skm_calls;
+
+typedef struct skm_query skm_query;
+/* Upload a batch of query sequences (residues/seq_off/seq_len as in skm_build_add_batch). */
+int skm_query_create(skm_query** out, skm_db* db, const uint8_t* residues, const uint64_t* seq_off,
+                     const uint32_t* seq_len, size_t n_seqs);
+/* Device pipeline (window lookup + HitSet) on resident queries; calls stay on the device. */
+int skm_query_run(skm_query* q, const skm_annot_opts* opts);
+int skm_query_last_timings(skm_query* q, float* ms, int cap);
+/* Download the calls of the last run. */
+int skm_query_calls(skm_query* q, skm_calls* out);
+void skm_query_destroy(skm_query* q);
+/* Convenience: create + run + calls + destroy. */
+int skm_annotate(skm_db* db, const uint8_t* residues, const uint64_t* seq_off, const uint32_t* seq_len,
+                 size_t n_seqs, const skm_annot_opts* opts, skm_calls* out);
+void skm_calls_free(skm_calls* c);
+
+/* find_best_call (call_functions.tcc:347-659) on the host.  function_index: nfunc C strings
+ * (function.index column 1).  out_func receives the called function (NUL-terminated).      */
+int skm_find_best_call(const skm_kmer_call* calls, size_t ncalls, const char* const* function_index,
+                       size_t nfunc, uint16_t* out_fi, float* out_score, float* out_offset,
+                       char* out_func, size_t out_func_cap);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SKM_H */

@@ -1,0 +1,352 @@
+"""signature_kmers_amd -- MI355X-native signature-k-mer engine (host mirror over libskm's C-ABI).
+
+The reference (olsonanl/signature_kmers) exposes its hot path as C++ templates:
+``SignatureBuilder<8>`` (signature_build.h:55-147), the KmerDb concept ``CmphKmerDb``
+(cmph_kmer.h:28-164) and ``FunctionCaller<KmerDb>`` (call_functions.h:60-136).  This module
+mirrors those classes in Python on top of ``libskm.so`` (include/skm.h).  Every compute call goes
+to the HIP library; there is no CPU fallback -- a missing library raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+__all__ = [
+    "SkmError", "lib", "K", "UNDEFINED_FUNCTION", "STORED_DTYPE", "CALL_DTYPE",
+    "SignatureBuilder", "KeptKmers", "CmphKmerDb", "FunctionCaller", "mph_build",
+    "kmer_to_str", "str_to_kmer", "keys_from_strings", "device_count",
+]
+
+K = 8
+UNDEFINED_FUNCTION = 0xFFFF
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libskm.so")
+
+STORED_DTYPE = np.dtype([("avg_from_end", "<u2"), ("function_index", "<u2"), ("mean", "<u2"),
+                         ("median", "<u2"), ("var", "<u2")])  # StoredKmerData, kmer_data.h:114-128
+CALL_DTYPE = np.dtype([("start", "<u4"), ("end", "<u4"), ("count", "<i4"), ("function_index", "<u2"),
+                       ("pad", "<u2"), ("protein_length_median", "<u4"),
+                       ("protein_length_med_avg_dev", "<f4")])  # KmerCall, call_functions.h:23-48
+
+
+class SkmError(RuntimeError):
+    pass
+
+
+class _BuildOpts(C.Structure):
+    _fields_ = [("k", C.c_int32), ("max_seqs_per_file", C.c_uint32), ("n_functions", C.c_uint32),
+                ("canonical_order", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32)]
+
+
+class _Kept(C.Structure):
+    _fields_ = [("keys", C.POINTER(C.c_uint64)), ("data", C.c_void_p), ("n", C.c_uint64),
+                ("distinct_functions", C.POINTER(C.c_uint32)), ("seqs_with_func", C.POINTER(C.c_uint32)),
+                ("n_functions", C.c_uint32), ("n_seqs_with_signature", C.c_uint64),
+                ("distinct_signatures", C.c_uint64), ("n_windows", C.c_uint64), ("n_records", C.c_uint64)]
+
+
+class _AnnotOpts(C.Structure):
+    _fields_ = [("min_hits", C.c_int32), ("max_gap", C.c_int32), ("ignore_hypo", C.c_int32),
+                ("hypo_index", C.c_int32), ("mean_mode", C.c_int32), ("mad_mode", C.c_int32)]
+
+
+class _Calls(C.Structure):
+    _fields_ = [("call_off", C.POINTER(C.c_uint64)), ("calls", C.c_void_p), ("n_seqs", C.c_uint64),
+                ("n_calls", C.c_uint64), ("n_windows", C.c_uint64)]
+
+
+_P = C.c_void_p
+_SIGS = {
+    "skm_last_error": (C.c_char_p, []),
+    "skm_version": (C.c_char_p, []),
+    "skm_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "skm_build_create": (C.c_int, [C.POINTER(_P), C.POINTER(C.c_int), C.c_int, C.POINTER(_BuildOpts)]),
+    "skm_build_add_batch": (C.c_int, [_P, _P, _P, _P, _P, _P, C.c_size_t]),
+    "skm_build_prepare": (C.c_int, [_P]),
+    "skm_build_run": (C.c_int, [_P]),
+    "skm_build_last_timings": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int]),
+    "skm_build_finish": (C.c_int, [_P, C.POINTER(_Kept)]),
+    "skm_kept_free": (None, [C.POINTER(_Kept)]),
+    "skm_build_destroy": (None, [_P]),
+    "skm_comm_unique_id": (C.c_int, [_P]),
+    "skm_build_set_comm": (C.c_int, [_P, _P]),
+    "skm_db_open": (C.c_int, [C.POINTER(_P), C.c_char_p, C.c_char_p, C.c_int]),
+    "skm_db_open_mem": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, _P, C.c_size_t, C.c_int]),
+    "skm_db_size": (C.c_int, [_P, C.POINTER(C.c_uint32)]),
+    "skm_db_lookup": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "skm_db_close": (None, [_P]),
+    "skm_mph_build": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_char_p, C.c_char_p]),
+    "skm_query_create": (C.c_int, [C.POINTER(_P), _P, _P, _P, _P, C.c_size_t]),
+    "skm_query_run": (C.c_int, [_P, C.POINTER(_AnnotOpts)]),
+    "skm_query_last_timings": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int]),
+    "skm_query_calls": (C.c_int, [_P, C.POINTER(_Calls)]),
+    "skm_query_destroy": (None, [_P]),
+    "skm_annotate": (C.c_int, [_P, _P, _P, _P, C.c_size_t, C.POINTER(_AnnotOpts), C.POINTER(_Calls)]),
+    "skm_calls_free": (None, [C.POINTER(_Calls)]),
+    "skm_find_best_call": (C.c_int, [_P, C.c_size_t, C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(C.c_uint16),
+                                     C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_char_p, C.c_size_t]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libskm.so (built in-tree by __graft_entry__.build / `make`).  Fails loudly."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SkmError(f"{LIB_PATH} is missing: run `make` (or __graft_entry__.build()) first")
+        h = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise SkmError(f"libskm error {rc}: {lib().skm_last_error().decode(errors='replace')}")
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _check(lib().skm_device_count(C.byref(n)))
+    return n.value
+
+
+def kmer_to_str(key: int) -> str:
+    return int(key).to_bytes(8, "little").decode("latin-1")
+
+
+def str_to_kmer(s: str) -> int:
+    b = s.encode("latin-1")
+    assert len(b) == K
+    return int.from_bytes(b, "little")
+
+
+def keys_from_strings(strs) -> np.ndarray:
+    return np.array([str_to_kmer(s) for s in strs], dtype=np.uint64)
+
+
+@dataclass
+class KeptKmers:
+    """KeptKmers<8> + KmerStatistics (signature_build.h:34-53), keys sorted ascending."""
+    keys: np.ndarray                 # u64 little-endian k-mers
+    data: np.ndarray                 # STORED_DTYPE
+    distinct_functions: np.ndarray   # u32[n_functions]
+    seqs_with_func: np.ndarray       # u32[n_functions]
+    n_seqs_with_signature: int
+    distinct_signatures: int
+    n_windows: int
+
+    def stats_lines(self) -> str:
+        """stdout of process_kmers (signature_build.tcc:210-212)."""
+        return (f"Kept {len(self.keys)} kmers\ndistinct_signatures={self.distinct_signatures}\n"
+                f"num_seqs_with_a_signature={self.n_seqs_with_signature}\n")
+
+    def final_kmers_lines(self):
+        """final.kmers rows (kmers-build-signatures.cc:212-216): KMER \\t avg_from_end \\t fi \\t"""
+        for k, d in zip(self.keys, self.data):
+            yield f"{kmer_to_str(k)}\t{int(d['avg_from_end'])}\t{int(d['function_index'])}\t\n"
+
+
+class SignatureBuilder:
+    """Device signature build (SignatureBuilder<8>::extract_kmers + process_kmers).
+
+    Sequences are added in reference emission order with their FunctionIndex (0xFFFF = no kept
+    function) and seq_id (file_number * max_seqs_per_file + k)."""
+
+    def __init__(self, n_functions: int, max_seqs_per_file: int = 100000, device: int = 0):
+        self._h = C.c_void_p()
+        opts = _BuildOpts(8, max_seqs_per_file, n_functions, 1, 0, 1)
+        dev = (C.c_int * 1)(device)
+        _check(lib().skm_build_create(C.byref(self._h), dev, 1, C.byref(opts)))
+        self.n_functions = n_functions
+
+    def add_batch(self, residues, seq_off, seq_len, seq_func, seq_id=None):
+        residues = np.ascontiguousarray(residues, dtype=np.uint8)
+        seq_off = np.ascontiguousarray(seq_off, dtype=np.uint64)
+        seq_len = np.ascontiguousarray(seq_len, dtype=np.uint32)
+        seq_func = np.ascontiguousarray(seq_func, dtype=np.uint16)
+        n = len(seq_len)
+        assert len(seq_off) == n and len(seq_func) == n
+        if n:
+            end = seq_off.astype(np.int64) + seq_len.astype(np.int64)
+            if end.max() > len(residues):
+                raise SkmError("seq_off/seq_len exceed the residue buffer")
+        sid = None if seq_id is None else np.ascontiguousarray(seq_id, dtype=np.uint32)
+        _check(lib().skm_build_add_batch(self._h, _ptr(residues), _ptr(seq_off), _ptr(seq_len), _ptr(seq_func),
+                                         _ptr(sid) if sid is not None else None, n))
+
+    def prepare(self):
+        _check(lib().skm_build_prepare(self._h))
+
+    def run(self):
+        _check(lib().skm_build_run(self._h))
+
+    def timings(self) -> dict:
+        ms = (C.c_float * 8)()
+        n = lib().skm_build_last_timings(self._h, ms, 8)
+        names = ["extract_count", "scan", "extract_scatter", "bucket_process", "overflow", "stats", "total"]
+        return {names[i]: float(ms[i]) for i in range(n)}
+
+    def finish(self) -> KeptKmers:
+        k = _Kept()
+        _check(lib().skm_build_finish(self._h, C.byref(k)))
+        try:
+            n = int(k.n)
+            keys = np.ctypeslib.as_array(k.keys, shape=(max(n, 1),))[:n].copy() if n else np.zeros(0, np.uint64)
+            data = (np.frombuffer(C.string_at(k.data, 10 * n), dtype=STORED_DTYPE).copy() if n
+                    else np.zeros(0, STORED_DTYPE))
+            nf = int(k.n_functions)
+            df = np.ctypeslib.as_array(k.distinct_functions, shape=(max(nf, 1),))[:nf].copy()
+            sw = np.ctypeslib.as_array(k.seqs_with_func, shape=(max(nf, 1),))[:nf].copy()
+            return KeptKmers(keys, data, df, sw, int(k.n_seqs_with_signature), int(k.distinct_signatures),
+                             int(k.n_windows))
+        finally:
+            lib().skm_kept_free(C.byref(k))
+
+    def close(self):
+        if self._h:
+            lib().skm_build_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def mph_build(keys: np.ndarray, data: np.ndarray, mph_path: str, dat_path: str, seed: int = 1):
+    """build_perfect_hash (perfect_hash.h:11-69): cmph-compatible BDZ .mph + dense .dat."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    data = np.ascontiguousarray(data, dtype=STORED_DTYPE)
+    _check(lib().skm_mph_build(_ptr(keys), _ptr(data), len(keys), seed, mph_path.encode(), dat_path.encode()))
+
+
+class CmphKmerDb:
+    """CmphKmerDb<StoredKmerData, 8> (cmph_kmer.h:28-164) resident in HBM."""
+    KmerSize = K
+
+    def __init__(self, file_base: str | None = None, device: int = 0, mph: bytes | None = None,
+                 dat: bytes | None = None):
+        self._h = C.c_void_p()
+        self.device = device
+        if file_base is not None:
+            _check(lib().skm_db_open(C.byref(self._h), (file_base + ".mph").encode(), (file_base + ".dat").encode(),
+                                     device))
+        else:
+            mb = np.frombuffer(mph, dtype=np.uint8)
+            db = np.frombuffer(dat, dtype=np.uint8) if dat else np.zeros(0, np.uint8)
+            _check(lib().skm_db_open_mem(C.byref(self._h), _ptr(mb), len(mb), _ptr(db), len(db), device))
+
+    def hash_size(self) -> int:
+        m = C.c_uint32()
+        _check(lib().skm_db_size(self._h, C.byref(m)))
+        return m.value
+
+    def lookup_keys(self, keys: np.ndarray) -> np.ndarray:
+        """cmph_search per key (lookup_key, cmph_kmer.h:90-92); >= hash_size means miss."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        out = np.zeros(len(keys), dtype=np.uint32)
+        if len(keys):
+            _check(lib().skm_db_lookup(self._h, _ptr(keys), len(keys), _ptr(out)))
+        return out
+
+    def close(self):
+        if self._h:
+            lib().skm_db_close(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def read_function_index(path: str) -> list:
+    """FunctionCaller::read_function_index (call_functions.tcc:123-148): column 1 by id."""
+    rows = []
+    with open(path, "rb") as f:
+        for line in f.read().split(b"\n"):
+            if not line:
+                continue
+            parts = line.split(b"\t")
+            rows.append((int(parts[0]), parts[1].decode("latin-1") if len(parts) > 1 else ""))
+    n = max((i for i, _ in rows), default=-1) + 1
+    out = [""] * n
+    for i, s in rows:
+        out[i] = s
+    return out
+
+
+class FunctionCaller:
+    """FunctionCaller<CmphKmerDb> (call_functions.h:60-136) with the per-window lookup and HitSet
+    state machine on the GPU and find_best_call on the host."""
+
+    def __init__(self, db: CmphKmerDb, function_index, min_hits: int = 5, max_gap: int = 200,
+                 mean_mode: int = 0):
+        self.db = db
+        self.function_index = read_function_index(function_index) if isinstance(function_index, str) \
+            else list(function_index)
+        self.min_hits = min_hits
+        self.max_gap = max_gap
+        self.ignore_hypothetical_ = False
+        self.mean_mode = mean_mode
+        try:
+            self.hypo_index = self.function_index.index("hypothetical protein")
+        except ValueError:
+            self.hypo_index = -1
+        self._fi_arr = (C.c_char_p * max(1, len(self.function_index)))(
+            *[s.encode("latin-1") for s in self.function_index])
+
+    def ignore_hypothetical(self, x: bool):
+        self.ignore_hypothetical_ = bool(x)
+
+    def _opts(self):
+        return _AnnotOpts(self.min_hits, self.max_gap, 1 if self.ignore_hypothetical_ else 0, self.hypo_index,
+                          self.mean_mode, 0)
+
+    def process_seqs(self, residues, seq_off, seq_len):
+        """process_aa_seq for a batch: returns (call_off u64[n+1], calls CALL_DTYPE)."""
+        if self.hypo_index < 0:  # call_functions.tcc:269-274 exits the process
+            raise SkmError("Cannot find hypothetical protein index")
+        residues = np.ascontiguousarray(residues, dtype=np.uint8)
+        seq_off = np.ascontiguousarray(seq_off, dtype=np.uint64)
+        seq_len = np.ascontiguousarray(seq_len, dtype=np.uint32)
+        out = _Calls()
+        opts = self._opts()
+        _check(lib().skm_annotate(self.db._h, _ptr(residues), _ptr(seq_off), _ptr(seq_len), len(seq_len),
+                                  C.byref(opts), C.byref(out)))
+        try:
+            n = int(out.n_seqs)
+            off = np.ctypeslib.as_array(out.call_off, shape=(n + 1,)).copy()
+            nc = int(out.n_calls)
+            calls = (np.frombuffer(C.string_at(out.calls, CALL_DTYPE.itemsize * nc), dtype=CALL_DTYPE).copy()
+                     if nc else np.zeros(0, CALL_DTYPE))
+            return off, calls
+        finally:
+            lib().skm_calls_free(C.byref(out))
+
+    def find_best_call(self, calls: np.ndarray):
+        """find_best_call (call_functions.tcc:347-659) -> (function_index, function, score, offset)."""
+        calls = np.ascontiguousarray(calls, dtype=CALL_DTYPE)
+        fi = C.c_uint16()
+        score = C.c_float()
+        off = C.c_float()
+        buf = C.create_string_buffer(4096)
+        _check(lib().skm_find_best_call(_ptr(calls) if len(calls) else None, len(calls), self._fi_arr,
+                                        len(self.function_index), C.byref(fi), C.byref(score), C.byref(off), buf,
+                                        4096))
+        return fi.value, buf.value.decode("latin-1"), score.value, off.value

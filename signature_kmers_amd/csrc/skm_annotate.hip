@@ -1,0 +1,809 @@
+// skm_annotate.hip -- function calling against a CMPH/BDZ signature DB resident in HBM.
+//
+// Replaces FunctionCaller<CmphKmerDb>::process_aa_seq (call_functions.tcc:259-338) with its
+// window iterator for_each_kmer<8> (kmer_data.h:76-102), CmphKmerDb::fetch (cmph_kmer.h:139-147)
+// and HitSet::process (call_functions.tcc:35-103).
+//
+//   k_lookup   one thread per 16 windows: window validity (no 'X'/'*' in the window or the byte
+//              after it), jenkins lookup2 -> 3 vertices -> 2-bit g -> rank (popcount over u32
+//              words of g) -> 10-byte record gather; writes func<<16|mean per window position
+//   k_calls    one thread per query sequence: the HitSet state machine over its window hits,
+//              statistics (Boost.Math mean / median / MAD) on a per-sequence scratch, KmerCall
+//              emission into a per-sequence slot range
+//   scan + k_gather   CSR compaction of the calls
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "skm_bdz.h"
+#include "skm_common.h"
+#include "skm_util.h"
+
+namespace skm {
+
+constexpr uint32_t NO_HIT = 0xFFFFFFFFu;
+constexpr int LK_THREADS = 256;
+constexpr int LK_POS = 16;
+
+struct QMeta {
+    uint64_t pstart;
+    uint32_t len;
+    uint32_t pad;
+};
+
+struct DevBdz {
+    const uint32_t* g;          // g as little-endian u32 words (16 entries each), padded
+    const uint32_t* ranktable;
+    const uint16_t* dat;        // 5 u16 per record
+    uint32_t m, r, b, seed;
+    uint64_t r_magic;           // fastmod: ceil(2^64 / r)
+};
+
+__device__ __forceinline__ uint32_t fastmod(uint32_t a, uint64_t M, uint32_t d) {
+    uint64_t low = M * a;
+    return (uint32_t)__umul64hi(low, (uint64_t)d);
+}
+
+__device__ __forceinline__ void jmix(uint32_t& a, uint32_t& b, uint32_t& c) {
+    a -= b; a -= c; a ^= (c >> 13);
+    b -= c; b -= a; b ^= (a << 8);
+    c -= a; c -= b; c ^= (b >> 13);
+    a -= b; a -= c; a ^= (c >> 12);
+    b -= c; b -= a; b ^= (a << 16);
+    c -= a; c -= b; c ^= (b >> 5);
+    a -= b; a -= c; a ^= (c >> 3);
+    b -= c; b -= a; b ^= (a << 10);
+    c -= a; c -= b; c ^= (b >> 15);
+}
+
+__device__ __forceinline__ uint32_t gval(const uint32_t* g, uint32_t i) { return (g[i >> 4] >> ((i & 15u) * 2)) & 3u; }
+
+__device__ __forceinline__ uint32_t unassigned_in(uint32_t w) { return __popc(w & (w >> 1) & 0x55555555u); }
+
+// cmph bdz_search for an 8-byte key given as two little-endian u32 words
+__device__ __forceinline__ uint32_t bdz_lookup(const DevBdz& D, uint32_t lo, uint32_t hi) {
+    uint32_t a = 0x9e3779b9u + lo, b = 0x9e3779b9u + hi, c = D.seed + 8u;
+    jmix(a, b, c);
+    const uint32_t h0 = fastmod(a, D.r_magic, D.r);
+    const uint32_t h1 = fastmod(b, D.r_magic, D.r) + D.r;
+    const uint32_t h2 = fastmod(c, D.r_magic, D.r) + 2u * D.r;
+    const uint32_t sel = (gval(D.g, h0) + gval(D.g, h1) + gval(D.g, h2)) % 3u;
+    const uint32_t v = sel == 0 ? h0 : (sel == 1 ? h1 : h2);
+    // rank(v): ranktable[v >> b] + assigned entries in [ (v>>b)<<b, v )
+    const uint32_t blk = v >> D.b;
+    uint32_t rank = D.ranktable[blk];
+    uint32_t i = blk << D.b;
+    // head: up to the next 16-aligned entry
+    while (i < v && (i & 15u)) {
+        rank += gval(D.g, i) != 3u;
+        ++i;
+    }
+    for (; i + 16 <= v; i += 16) rank += 16u - unassigned_in(D.g[i >> 4]);
+    if (i < v) {
+        const uint32_t nb = (v - i) * 2u;
+        const uint32_t w = D.g[i >> 4] & ((1u << nb) - 1u);
+        rank += (v - i) - unassigned_in(w);
+    }
+    return rank;
+}
+
+__device__ __forceinline__ bool ambig(uint32_t c) { return c == 'X' || c == '*'; }
+
+__global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict__ res, uint64_t rp, DevBdz D,
+                                                      uint32_t* __restrict__ hits) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x * LK_POS;
+    for (uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * LK_POS; base < rp; base += step) {
+        const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
+        const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
+        const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        // bad[j]: byte j is a separator (0) or ambiguous; amb[j]: byte j is 'X' or '*'
+        uint32_t bad = 0, amb = 0;
+#pragma unroll
+        for (int j = 0; j < 25 && j < 32; ++j) {
+            uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            bool a = ambig(c);
+            amb |= (a ? 1u : 0u) << j;
+            bad |= ((a || c == 0) ? 1u : 0u) << j;
+        }
+        uint32_t out[LK_POS];
+#pragma unroll
+        for (int t = 0; t < LK_POS; ++t) {
+            const uint64_t p = base + t;
+            uint32_t o = NO_HIT;
+            // for_each_kmer: skip when an ambiguous char lies in [p, p+8] (incl. the next byte)
+            if (p < rp && ((bad >> t) & 0xFFu) == 0 && ((amb >> (t + 8)) & 1u) == 0) {
+                // key bytes t..t+7
+                const int wi = t >> 2, sh = (t & 3) * 8;
+                uint32_t lo, hi;
+                if (sh == 0) {
+                    lo = w[wi];
+                    hi = w[wi + 1];
+                } else {
+                    lo = (w[wi] >> sh) | (w[wi + 1] << (32 - sh));
+                    hi = (w[wi + 1] >> sh) | (w[wi + 2] << (32 - sh));
+                }
+                const uint32_t idx = bdz_lookup(D, lo, hi);
+                if (idx < D.m) {
+                    const uint16_t* rec = D.dat + (uint64_t)idx * 5;
+                    o = ((uint32_t)rec[1] << 16) | rec[2];  // function_index, mean
+                }
+            }
+            out[t] = o;
+        }
+        uint4* dst = reinterpret_cast<uint4*>(hits + base);
+        dst[0] = make_uint4(out[0], out[1], out[2], out[3]);
+        dst[1] = make_uint4(out[4], out[5], out[6], out[7]);
+        dst[2] = make_uint4(out[8], out[9], out[10], out[11]);
+        dst[3] = make_uint4(out[12], out[13], out[14], out[15]);
+    }
+}
+
+struct CallArgs {
+    const QMeta* meta;
+    const uint32_t* hits;
+    uint16_t* scratch;          // per-sequence value scratch (nwin entries)
+    const uint64_t* scr_off;    // [nseq] scratch offsets (= window offsets)
+    const uint64_t* cap_off;    // [nseq+1] call slot offsets
+    skm_kmer_call* slots;
+    uint32_t* counts;           // [nseq]
+    uint32_t nseq;
+    int min_hits, max_gap, ignore_hypo, mean_mode;
+    uint32_t hypo;
+};
+
+__device__ __forceinline__ bool usable(uint32_t h, const CallArgs& A) {
+    return h != NO_HIT && !(A.ignore_hypo && (h >> 16) == A.hypo);
+}
+
+__device__ void heap_sort_u16(uint16_t* a, uint32_t n) {
+    auto sift = [&](uint32_t start, uint32_t end) {
+        uint32_t root = start;
+        while (2 * root + 1 < end) {
+            uint32_t child = 2 * root + 1;
+            if (child + 1 < end && a[child] < a[child + 1]) ++child;
+            if (a[root] < a[child]) {
+                uint16_t t = a[root];
+                a[root] = a[child];
+                a[child] = t;
+                root = child;
+            } else {
+                return;
+            }
+        }
+    };
+    if (n < 2) return;
+    for (uint32_t s = n / 2; s-- > 0;) sift(s, n);
+    for (uint32_t end = n - 1; end > 0; --end) {
+        uint16_t t = a[0];
+        a[0] = a[end];
+        a[end] = t;
+        sift(0, end);
+    }
+}
+
+// k-th smallest |2 v_j - C2| over sorted v[0..n) (two pointers from the centre outward)
+__device__ uint32_t kth_dev(const uint16_t* v, uint32_t n, uint32_t C2, uint32_t k) {
+    // split: first index with 2v > C2
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (2u * v[mid] > C2)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    int64_t L = (int64_t)lo - 1;
+    uint32_t R = lo;
+    uint32_t d = 0;
+    for (uint32_t t = 0; t <= k; ++t) {
+        uint32_t dl = L >= 0 ? C2 - 2u * v[L] : 0xFFFFFFFFu;
+        uint32_t dr = R < n ? 2u * v[R] - C2 : 0xFFFFFFFFu;
+        if (dl <= dr) {
+            d = dl;
+            --L;
+        } else {
+            d = dr;
+            ++R;
+        }
+    }
+    return d;
+}
+
+// HitSet::process over window range [first, last] with current function cur.
+__device__ void hitset_process(const CallArgs& A, const uint32_t* hit, uint16_t* scr, uint32_t first, uint32_t last,
+                               uint32_t cur, double seqlen, skm_kmer_call* slots, uint32_t& ncalls) {
+    uint32_t n = 0, last_cur = first;
+    for (uint32_t i = first; i <= last; ++i) {
+        const uint32_t h = hit[i];
+        if (!usable(h, A) || (h >> 16) != cur) continue;
+        scr[n++] = (uint16_t)(h & 0xFFFFu);
+        last_cur = i;
+    }
+    // Boost.Math mean over float(kdata.mean) in hit order
+    float mean;
+    if (A.mean_mode == 1) {
+        float mu = 0, fi = 1;
+        for (uint32_t j = 0; j < n; ++j) {
+            mu = mu + ((float)scr[j] - mu) / fi;
+            fi += 1;
+        }
+        mean = mu;
+    } else {
+        float mu[4] = {0, 0, 0, 0};
+        float fi = 1;
+        const uint32_t end = n - (n % 4);
+        uint32_t j = 0;
+        for (; j < end; j += 4) {
+            const float inv = 1.0f / fi;
+            float t0 = (float)scr[j] - mu[0], t1 = (float)scr[j + 1] - mu[1];
+            float t2 = (float)scr[j + 2] - mu[2], t3 = (float)scr[j + 3] - mu[3];
+            t0 *= inv;
+            t1 *= inv;
+            t2 *= inv;
+            t3 *= inv;
+            mu[0] += t0;
+            mu[1] += t1;
+            mu[2] += t2;
+            mu[3] += t3;
+            fi += 1;
+        }
+        const float num1 = float(n - (n % 4)) / float(4);
+        const float num2 = num1 + float(n % 4);
+        for (; j < n; ++j) {
+            mu[3] += ((float)scr[j] - mu[3]) / fi;
+            fi += 1;
+        }
+        mean = (num1 * (mu[0] + mu[1] + mu[2]) + num2 * mu[3]) / float(n);
+    }
+    heap_sort_u16(scr, n);
+    float median;
+    uint32_t C2;
+    if (n & 1) {
+        const uint32_t m = scr[(n - 1) / 2];
+        median = (float)m;
+        C2 = 2u * m;
+    } else {
+        const uint32_t a = scr[n / 2 - 1], b = scr[n / 2];
+        median = ((float)a + (float)b) / 2;
+        C2 = a + b;
+    }
+    float mad;
+    if (n & 1) {
+        mad = (float)kth_dev(scr, n, C2, (n - 1) / 2) * 0.5f;
+    } else {
+        const float d1 = (float)kth_dev(scr, n, C2, n / 2 - 1) * 0.5f;
+        const float d2 = (float)kth_dev(scr, n, C2, n / 2) * 0.5f;
+        mad = (d1 + d2) / 2.0f;
+    }
+    if (mad == 0) mad = 30;
+    const double cutoff_b = (double)mean - 2.0 * (double)mad;
+    const double cutoff_t = (double)mean + 2.0 * (double)mad;
+    if ((int)n >= A.min_hits && !(seqlen < cutoff_b || seqlen > cutoff_t)) {
+        skm_kmer_call c;
+        c.start = first;
+        c.end = last_cur + 7u;
+        c.count = (int32_t)n;
+        c.function_index = (uint16_t)cur;
+        c.pad = 0;
+        c.protein_length_median = (uint32_t)median;
+        c.protein_length_med_avg_dev = mad;
+        slots[ncalls++] = c;
+    }
+}
+
+__global__ void k_calls(CallArgs A) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= A.nseq) return;
+    const QMeta m = A.meta[s];
+    const uint32_t nwin = m.len >= 8 ? m.len - 7 : 0;
+    const uint32_t* hit = A.hits + m.pstart;
+    uint16_t* scr = A.scratch + A.scr_off[s];
+    skm_kmer_call* slots = A.slots + A.cap_off[s];
+    const double seqlen = (double)m.len;
+    uint32_t ncalls = 0;
+    // HitSet: all usable hits in window range [first, last_pos]; pair = (prev, last)
+    uint32_t count = 0, first = 0, last_pos = 0, prev_pos = 0, last_f = 0, prev_f = 0, cur = 0xFFFFu;
+    for (uint32_t i = 0; i < nwin; ++i) {
+        const uint32_t h = hit[i];
+        if (!usable(h, A)) continue;
+        const uint32_t f = h >> 16;
+        if (count > 0 && (uint64_t)last_pos + (uint64_t)A.max_gap < (uint64_t)i) {
+            if ((int)count >= A.min_hits) {
+                hitset_process(A, hit, scr, first, last_pos, cur, seqlen, slots, ncalls);
+                if (prev_f != cur && prev_f == last_f) {
+                    cur = prev_f;
+                    first = prev_pos;
+                    count = 2;
+                } else {
+                    count = 0;
+                }
+            } else {
+                count = 0;
+            }
+        }
+        if (count == 0) {
+            cur = f;
+            first = i;
+        }
+        prev_pos = last_pos;
+        prev_f = last_f;
+        last_pos = i;
+        last_f = f;
+        ++count;
+        if (count > 1 && cur != f && prev_f == f) {
+            hitset_process(A, hit, scr, first, last_pos, cur, seqlen, slots, ncalls);
+            if (prev_f != cur && prev_f == last_f) {
+                cur = prev_f;
+                first = prev_pos;
+                count = 2;
+            } else {
+                count = 0;
+            }
+        }
+    }
+    if ((int)count >= A.min_hits) hitset_process(A, hit, scr, first, last_pos, cur, seqlen, slots, ncalls);
+    A.counts[s] = ncalls;
+}
+
+// capacity of the call slot range of sequence s
+__global__ void k_caps(const QMeta* __restrict__ meta, uint32_t nseq, int min_hits, uint32_t* __restrict__ cap) {
+    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseq) return;
+    uint32_t len = meta[s].len;
+    uint32_t nwin = len >= 8 ? len - 7 : 0;
+    cap[s] = min_hits > 2 ? nwin / (uint32_t)(min_hits - 2) + 2u : 2u * nwin + 2u;
+}
+
+// ---- exclusive scan u32 -> u64 (out has n+1 entries) ----
+constexpr int SC_THREADS = 256, SC_ITEMS = 8, SC_TILE = SC_THREADS * SC_ITEMS;
+
+__global__ void k_scan_tiles(const uint32_t* __restrict__ in, uint64_t n, uint64_t* __restrict__ out,
+                             uint64_t* __restrict__ tile_sums) {
+    __shared__ uint64_t s_w[SC_THREADS / 64 + 1];
+    const uint64_t t0 = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_ITEMS;
+    uint64_t v[SC_ITEMS];
+    uint64_t local = 0;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        v[j] = (t0 + j < n) ? in[t0 + j] : 0;
+        local += v[j];
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t x = local;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) s_w[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (int w = 0; w < SC_THREADS / 64; ++w) {
+            uint64_t t = s_w[w];
+            s_w[w] = acc;
+            acc += t;
+        }
+        tile_sums[blockIdx.x] = acc;
+    }
+    __syncthreads();
+    uint64_t run = s_w[wave] + x - local;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        if (t0 + j < n) out[t0 + j] = run;
+        run += v[j];
+    }
+}
+
+__global__ void k_scan_sums(uint64_t* __restrict__ sums, uint64_t nt, uint64_t* __restrict__ total) {
+    // single workgroup, sequential over chunks of 1024
+    __shared__ uint64_t s_w[17];
+    uint64_t carry = 0;
+    for (uint64_t c0 = 0; c0 < nt; c0 += blockDim.x) {
+        uint64_t i = c0 + threadIdx.x;
+        uint64_t v = i < nt ? sums[i] : 0;
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        uint64_t x = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            uint64_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) s_w[wave] = x;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t acc = 0;
+            for (int w = 0; w < (int)(blockDim.x / 64); ++w) {
+                uint64_t t = s_w[w];
+                s_w[w] = acc;
+                acc += t;
+            }
+            s_w[16] = acc;
+        }
+        __syncthreads();
+        if (i < nt) sums[i] = carry + s_w[wave] + x - v;
+        carry += s_w[16];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ void k_scan_add(uint64_t* __restrict__ out, uint64_t n, const uint64_t* __restrict__ tile_sums,
+                           const uint64_t* __restrict__ total) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] += tile_sums[i / SC_TILE];
+    if (i == n) out[n] = *total;
+}
+
+__global__ void k_gather_calls(const skm_kmer_call* __restrict__ slots, const uint64_t* __restrict__ cap_off,
+                               const uint64_t* __restrict__ call_off, uint32_t nseq, skm_kmer_call* __restrict__ out) {
+    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseq) return;
+    uint64_t a = call_off[s], e = call_off[s + 1], src = cap_off[s];
+    for (uint64_t j = a; j < e; ++j) out[j] = slots[src + (j - a)];
+}
+
+struct Scanner {
+    DevBuf tiles, total;
+    // out: n+1 u64 entries
+    void run(const uint32_t* in, uint64_t n, uint64_t* out, hipStream_t st) {
+        uint64_t nt = std::max<uint64_t>(1, ceil_div(n, SC_TILE));
+        tiles.ensure(8 * nt);
+        total.ensure(8);
+        hipLaunchKernelGGL(k_scan_tiles, dim3((uint32_t)nt), dim3(SC_THREADS), 0, st, in, n, out, tiles.as<uint64_t>());
+        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, st, tiles.as<uint64_t>(), nt, total.as<uint64_t>());
+        hipLaunchKernelGGL(k_scan_add, dim3((uint32_t)ceil_div(n + 1, 256)), dim3(256), 0, st, out, n,
+                           tiles.as<uint64_t>(), total.as<uint64_t>());
+        SKM_HIP(hipGetLastError());
+    }
+};
+
+}  // namespace skm
+
+using namespace skm;
+
+struct skm_db {
+    int device = 0;
+    Bdz bdz;
+    uint64_t dat_records = 0;
+    DevBuf d_g, d_rank, d_dat;
+    DevBdz dev{};
+};
+
+struct skm_query {
+    skm_db* db = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[5] = {};
+    float last_ms[5] = {};
+    uint32_t nseq = 0;
+    uint64_t rp = 0, n_windows = 0;
+    DevBuf d_res, d_meta, d_hits, d_scr, d_scr_off, d_caps, d_cap_off, d_slots, d_counts, d_call_off, d_calls;
+    Scanner scan;
+    uint64_t n_calls = 0;
+    bool ran = false;
+};
+
+namespace {
+
+void db_upload(skm_db* db, const uint8_t* dat, size_t dat_len) {
+    SKM_HIP(hipSetDevice(db->device));
+    Bdz& h = db->bdz;
+    SKM_CHECK(dat_len % 10 == 0, SKM_E_IO, "kmer_data.dat size is not a multiple of 10");
+    db->dat_records = dat_len / 10;
+    SKM_CHECK(db->dat_records >= h.m, SKM_E_IO, "kmer_data.dat has fewer records than the hash size");
+    const size_t gbytes = ((h.g.size() + 63) / 64) * 64 + 64;
+    std::vector<uint8_t> g(gbytes, 0xFF);
+    std::memcpy(g.data(), h.g.data(), h.g.size());
+    db->d_g.ensure(gbytes);
+    SKM_HIP(hipMemcpy(db->d_g.p, g.data(), gbytes, hipMemcpyHostToDevice));
+    db->d_rank.ensure(4 * std::max<size_t>(h.ranktable.size(), 1));
+    if (!h.ranktable.empty()) SKM_HIP(hipMemcpy(db->d_rank.p, h.ranktable.data(), 4 * h.ranktable.size(), hipMemcpyHostToDevice));
+    db->d_dat.ensure(std::max<size_t>(dat_len, 16));
+    if (dat_len) SKM_HIP(hipMemcpy(db->d_dat.p, dat, dat_len, hipMemcpyHostToDevice));
+    DevBdz& D = db->dev;
+    D.g = db->d_g.as<uint32_t>();
+    D.ranktable = db->d_rank.as<uint32_t>();
+    D.dat = db->d_dat.as<uint16_t>();
+    D.m = h.m;
+    D.r = h.r;
+    D.b = h.b;
+    D.seed = h.seed;
+    D.r_magic = h.r ? (~0ull / h.r + 1) : 0;
+}
+
+bool read_file(const char* path, std::vector<uint8_t>& out) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    f.seekg(0, std::ios::end);
+    std::streamoff n = f.tellg();
+    f.seekg(0);
+    out.resize((size_t)n);
+    if (n) f.read((char*)out.data(), n);
+    return (bool)f;
+}
+
+void query_run(skm_query* q, const skm_annot_opts* o) {
+    skm_db* db = q->db;
+    SKM_HIP(hipSetDevice(db->device));
+    hipStream_t st = q->stream;
+    SKM_HIP(hipEventRecord(q->ev[0], st));
+    if (q->rp && db->bdz.m) {
+        uint64_t nthreads = ceil_div(q->rp, LK_POS);
+        uint32_t grid = (uint32_t)std::min<uint64_t>(ceil_div(nthreads, LK_THREADS), 256ull * 16);
+        hipLaunchKernelGGL(k_lookup, dim3(grid), dim3(LK_THREADS), 0, st, q->d_res.as<uint8_t>(), q->rp, db->dev,
+                           q->d_hits.as<uint32_t>());
+    } else if (q->rp) {
+        SKM_HIP(hipMemsetAsync(q->d_hits.p, 0xFF, 4 * q->rp, st));
+    }
+    SKM_HIP(hipGetLastError());
+    SKM_HIP(hipEventRecord(q->ev[1], st));
+    const uint32_t ns = q->nseq;
+    if (ns) {
+        hipLaunchKernelGGL(k_caps, dim3(ceil_div(ns, 256)), dim3(256), 0, st, q->d_meta.as<QMeta>(), ns, o->min_hits,
+                           q->d_caps.as<uint32_t>());
+        q->scan.run(q->d_caps.as<uint32_t>(), ns, q->d_cap_off.as<uint64_t>(), st);
+        uint64_t cap_total = 0;
+        SKM_HIP(hipMemcpyAsync(&cap_total, q->d_cap_off.as<uint64_t>() + ns, 8, hipMemcpyDeviceToHost, st));
+        SKM_HIP(hipStreamSynchronize(st));
+        q->d_slots.ensure(sizeof(skm_kmer_call) * std::max<uint64_t>(cap_total, 1));
+        CallArgs A;
+        A.meta = q->d_meta.as<QMeta>();
+        A.hits = q->d_hits.as<uint32_t>();
+        A.scratch = q->d_scr.as<uint16_t>();
+        A.scr_off = q->d_scr_off.as<uint64_t>();
+        A.cap_off = q->d_cap_off.as<uint64_t>();
+        A.slots = q->d_slots.as<skm_kmer_call>();
+        A.counts = q->d_counts.as<uint32_t>();
+        A.nseq = ns;
+        A.min_hits = o->min_hits;
+        A.max_gap = o->max_gap;
+        A.ignore_hypo = o->ignore_hypo && o->hypo_index >= 0;
+        A.mean_mode = o->mean_mode;
+        A.hypo = o->hypo_index >= 0 ? (uint32_t)o->hypo_index : 0xFFFFFFFFu;
+        SKM_HIP(hipEventRecord(q->ev[2], st));
+        hipLaunchKernelGGL(k_calls, dim3(ceil_div(ns, 64)), dim3(64), 0, st, A);
+        SKM_HIP(hipGetLastError());
+        SKM_HIP(hipEventRecord(q->ev[3], st));
+        q->scan.run(q->d_counts.as<uint32_t>(), ns, q->d_call_off.as<uint64_t>(), st);
+        SKM_HIP(hipMemcpyAsync(&q->n_calls, q->d_call_off.as<uint64_t>() + ns, 8, hipMemcpyDeviceToHost, st));
+        SKM_HIP(hipStreamSynchronize(st));
+        q->d_calls.ensure(sizeof(skm_kmer_call) * std::max<uint64_t>(q->n_calls, 1));
+        hipLaunchKernelGGL(k_gather_calls, dim3(ceil_div(ns, 256)), dim3(256), 0, st, q->d_slots.as<skm_kmer_call>(),
+                           q->d_cap_off.as<uint64_t>(), q->d_call_off.as<uint64_t>(), ns, q->d_calls.as<skm_kmer_call>());
+        SKM_HIP(hipGetLastError());
+    } else {
+        SKM_HIP(hipEventRecord(q->ev[2], st));
+        SKM_HIP(hipEventRecord(q->ev[3], st));
+        q->n_calls = 0;
+    }
+    SKM_HIP(hipEventRecord(q->ev[4], st));
+    SKM_HIP(hipEventSynchronize(q->ev[4]));
+    SKM_HIP(hipEventElapsedTime(&q->last_ms[0], q->ev[0], q->ev[1]));  // lookup
+    SKM_HIP(hipEventElapsedTime(&q->last_ms[1], q->ev[2], q->ev[3]));  // hitset
+    SKM_HIP(hipEventElapsedTime(&q->last_ms[2], q->ev[3], q->ev[4]));  // compaction
+    SKM_HIP(hipEventElapsedTime(&q->last_ms[3], q->ev[0], q->ev[4]));  // total
+    q->ran = true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int skm_db_open_mem(skm_db** out, const uint8_t* mph, size_t mph_len, const uint8_t* dat, size_t dat_len, int device) {
+    SKM_API_BEGIN
+    SKM_CHECK(out && mph, SKM_E_ARG, "null argument");
+    auto* db = new skm_db();
+    db->device = device;
+    std::string err;
+    if (!bdz_parse(mph, mph_len, db->bdz, err)) {
+        delete db;
+        throw Error(SKM_E_IO, "kmer_data.mph: " + err);
+    }
+    try {
+        db_upload(db, dat, dat_len);
+    } catch (...) {
+        delete db;
+        throw;
+    }
+    *out = db;
+    SKM_API_END
+}
+
+int skm_db_open(skm_db** out, const char* mph_path, const char* dat_path, int device) {
+    SKM_API_BEGIN
+    SKM_CHECK(out && mph_path && dat_path, SKM_E_ARG, "null argument");
+    std::vector<uint8_t> mph, dat;
+    SKM_CHECK(read_file(mph_path, mph), SKM_E_IO, std::string("cannot read ") + mph_path);
+    SKM_CHECK(read_file(dat_path, dat), SKM_E_IO, std::string("cannot read ") + dat_path);
+    int rc = skm_db_open_mem(out, mph.data(), mph.size(), dat.data(), dat.size(), device);
+    if (rc) return rc;
+    SKM_API_END
+}
+
+int skm_db_size(skm_db* db, uint32_t* m) {
+    if (!db || !m) return SKM_E_ARG;
+    *m = db->bdz.m;
+    return SKM_OK;
+}
+
+__global__ void k_lookup_keys(const uint64_t* __restrict__ keys, uint64_t n, DevBdz D, uint32_t* __restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t k = keys[i];
+    out[i] = bdz_lookup(D, (uint32_t)k, (uint32_t)(k >> 32));
+}
+
+int skm_db_lookup(skm_db* db, const uint64_t* keys, size_t n, uint32_t* idx_out) {
+    SKM_API_BEGIN
+    SKM_CHECK(db && (n == 0 || (keys && idx_out)), SKM_E_ARG, "null argument");
+    if (n == 0) return SKM_OK;
+    SKM_HIP(hipSetDevice(db->device));
+    if (db->bdz.m == 0) {
+        for (size_t i = 0; i < n; ++i) idx_out[i] = 0;  // empty hash: every key maps to rank 0 == size (miss)
+        return SKM_OK;
+    }
+    DevBuf dk, dout;
+    dk.ensure(8 * n);
+    dout.ensure(4 * n);
+    SKM_HIP(hipMemcpy(dk.p, keys, 8 * n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_lookup_keys, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, 0, dk.as<uint64_t>(), (uint64_t)n,
+                       db->dev, dout.as<uint32_t>());
+    SKM_HIP(hipGetLastError());
+    SKM_HIP(hipMemcpy(idx_out, dout.p, 4 * n, hipMemcpyDeviceToHost));
+    SKM_API_END
+}
+
+void skm_db_close(skm_db* db) { delete db; }
+
+int skm_mph_build(const uint64_t* keys, const skm_stored_kmer_data* data, size_t n, uint32_t seed, const char* mph_path,
+                  const char* dat_path) {
+    SKM_API_BEGIN
+    SKM_CHECK((n == 0 || (keys && data)) && mph_path && dat_path, SKM_E_ARG, "null argument");
+    Bdz h;
+    std::string err;
+    SKM_CHECK(bdz_build(keys, n, seed, h, err), SKM_E_ARG, err);
+    // dense record array indexed by the hash (perfect_hash.h:41-54): unwritten slots would keep the
+    // StoredKmerData defaults, but a minimal perfect hash writes every slot.
+    std::vector<skm_stored_kmer_data> kd(n);
+    for (size_t i = 0; i < n; ++i) {
+        uint8_t kb[8];
+        std::memcpy(kb, &keys[i], 8);
+        uint32_t idx = bdz_search(h, kb, 8);
+        SKM_CHECK(idx < n, SKM_E_ARG, "BDZ construction produced an out-of-range slot");
+        kd[idx] = data[i];
+    }
+    std::vector<uint8_t> img = bdz_dump(h);
+    std::ofstream fm(mph_path, std::ios::binary);
+    SKM_CHECK((bool)fm, SKM_E_IO, std::string("cannot write ") + mph_path);
+    fm.write((const char*)img.data(), (std::streamsize)img.size());
+    std::ofstream fd(dat_path, std::ios::binary);
+    SKM_CHECK((bool)fd, SKM_E_IO, std::string("cannot write ") + dat_path);
+    if (n) fd.write((const char*)kd.data(), (std::streamsize)(sizeof(skm_stored_kmer_data) * n));
+    SKM_CHECK((bool)fm && (bool)fd, SKM_E_IO, "write failed");
+    SKM_API_END
+}
+
+int skm_query_create(skm_query** out, skm_db* db, const uint8_t* residues, const uint64_t* seq_off,
+                     const uint32_t* seq_len, size_t n_seqs) {
+    SKM_API_BEGIN
+    SKM_CHECK(out && db, SKM_E_ARG, "null argument");
+    SKM_CHECK(n_seqs == 0 || (residues && seq_off && seq_len), SKM_E_ARG, "null array");
+    SKM_CHECK(n_seqs < 0xFFFFFFFFull, SKM_E_ARG, "too many query sequences in one batch");
+    SKM_HIP(hipSetDevice(db->device));
+    auto* q = new skm_query();
+    q->db = db;
+    try {
+        SKM_HIP(hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking));
+        for (auto& e : q->ev) SKM_HIP(hipEventCreate(&e));
+        std::vector<uint8_t> res;
+        std::vector<QMeta> meta(n_seqs);
+        std::vector<uint64_t> scr_off(n_seqs);
+        uint64_t total = 0, nwin_tot = 0;
+        for (size_t s = 0; s < n_seqs; ++s) total += (uint64_t)seq_len[s] + 1;
+        res.reserve(total);
+        for (size_t s = 0; s < n_seqs; ++s) {
+            meta[s].pstart = res.size();
+            meta[s].len = seq_len[s];
+            meta[s].pad = 0;
+            res.insert(res.end(), residues + seq_off[s], residues + seq_off[s] + seq_len[s]);
+            res.push_back(0);
+            scr_off[s] = nwin_tot;
+            nwin_tot += seq_len[s] >= 8 ? seq_len[s] - 7 : 0;
+        }
+        q->nseq = (uint32_t)n_seqs;
+        q->rp = res.size();
+        q->n_windows = nwin_tot;
+        // hits are written in 16-window groups: pad to a multiple of 16 positions
+        const uint64_t rp_pad = ceil_div(q->rp + 1, LK_POS) * LK_POS;
+        q->d_res.ensure(rp_pad + 64);
+        SKM_HIP(hipMemsetAsync(q->d_res.p, 0, rp_pad + 64, q->stream));
+        if (q->rp) SKM_HIP(hipMemcpyAsync(q->d_res.p, res.data(), q->rp, hipMemcpyHostToDevice, q->stream));
+        q->d_meta.ensure(sizeof(QMeta) * std::max<size_t>(n_seqs, 1));
+        if (n_seqs) SKM_HIP(hipMemcpyAsync(q->d_meta.p, meta.data(), sizeof(QMeta) * n_seqs, hipMemcpyHostToDevice, q->stream));
+        q->d_hits.ensure(4 * (rp_pad + 16));
+        q->d_scr.ensure(2 * std::max<uint64_t>(nwin_tot, 1));
+        q->d_scr_off.ensure(8 * std::max<size_t>(n_seqs, 1));
+        if (n_seqs) SKM_HIP(hipMemcpyAsync(q->d_scr_off.p, scr_off.data(), 8 * n_seqs, hipMemcpyHostToDevice, q->stream));
+        q->d_caps.ensure(4 * std::max<size_t>(n_seqs, 1));
+        q->d_cap_off.ensure(8 * (n_seqs + 1));
+        q->d_counts.ensure(4 * std::max<size_t>(n_seqs, 1));
+        q->d_call_off.ensure(8 * (n_seqs + 1));
+        SKM_HIP(hipStreamSynchronize(q->stream));
+    } catch (...) {
+        skm_query_destroy(q);
+        throw;
+    }
+    *out = q;
+    SKM_API_END
+}
+
+int skm_query_run(skm_query* q, const skm_annot_opts* opts) {
+    SKM_API_BEGIN
+    SKM_CHECK(q && opts, SKM_E_ARG, "null argument");
+    SKM_CHECK(opts->mad_mode == 0, SKM_E_ARG, "device path implements mad_mode 0 only");
+    SKM_CHECK(opts->min_hits >= 1 && opts->max_gap >= 0, SKM_E_ARG, "invalid min_hits / max_gap");
+    query_run(q, opts);
+    SKM_API_END
+}
+
+int skm_query_last_timings(skm_query* q, float* ms, int cap) {
+    if (!q || !ms) return SKM_E_ARG;
+    int n = std::min(cap, 4);
+    for (int i = 0; i < n; ++i) ms[i] = q->last_ms[i];
+    return n;
+}
+
+int skm_query_calls(skm_query* q, skm_calls* out) {
+    SKM_API_BEGIN
+    SKM_CHECK(q && out, SKM_E_ARG, "null argument");
+    SKM_CHECK(q->ran, SKM_E_STATE, "skm_query_run has not been called");
+    SKM_HIP(hipSetDevice(q->db->device));
+    std::memset(out, 0, sizeof(*out));
+    out->n_seqs = q->nseq;
+    out->n_calls = q->n_calls;
+    out->n_windows = q->n_windows;
+    out->call_off = (uint64_t*)std::malloc(8 * (q->nseq + 1));
+    out->calls = (skm_kmer_call*)std::malloc(sizeof(skm_kmer_call) * std::max<uint64_t>(q->n_calls, 1));
+    SKM_CHECK(out->call_off && out->calls, SKM_E_OOM, "host allocation failed");
+    if (q->nseq)
+        SKM_HIP(hipMemcpyAsync(out->call_off, q->d_call_off.p, 8 * (q->nseq + 1), hipMemcpyDeviceToHost, q->stream));
+    else
+        out->call_off[0] = 0;
+    if (q->n_calls)
+        SKM_HIP(hipMemcpyAsync(out->calls, q->d_calls.p, sizeof(skm_kmer_call) * q->n_calls, hipMemcpyDeviceToHost, q->stream));
+    SKM_HIP(hipStreamSynchronize(q->stream));
+    SKM_API_END
+}
+
+void skm_query_destroy(skm_query* q) {
+    if (!q) return;
+    (void)hipSetDevice(q->db->device);
+    if (q->stream) (void)hipStreamSynchronize(q->stream);
+    for (auto& e : q->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (q->stream) (void)hipStreamDestroy(q->stream);
+    delete q;
+}
+
+int skm_annotate(skm_db* db, const uint8_t* residues, const uint64_t* seq_off, const uint32_t* seq_len, size_t n_seqs,
+                 const skm_annot_opts* opts, skm_calls* out) {
+    skm_query* q = nullptr;
+    int rc = skm_query_create(&q, db, residues, seq_off, seq_len, n_seqs);
+    if (rc) return rc;
+    rc = skm_query_run(q, opts);
+    if (!rc) rc = skm_query_calls(q, out);
+    skm_query_destroy(q);
+    return rc;
+}
+
+void skm_calls_free(skm_calls* c) {
+    if (!c) return;
+    std::free(c->call_off);
+    std::free(c->calls);
+    std::memset(c, 0, sizeof(*c));
+}
+
+}  // extern "C"

@@ -1,0 +1,1250 @@
+// skm_build.hip -- signature build on MI355X (gfx950).
+//
+// Replaces the reference's SignatureBuilder<8>::extract_kmers + process_kmers
+// (signature_build.tcc:48-293): sliding 8-mer extraction, grouping of equal k-mers, the 80 %
+// best-function cut and the per-k-mer statistics, with `--n-threads 1` semantics.
+//
+// Device pipeline (one GPU; the multi-GPU form inserts an RCCL all-to-all between 3 and 4):
+//   1. k_extract<count>   residues -> per-workgroup histogram of level-1 buckets (LDS atomics)
+//   2. k_colsum/k_bstart/k_coloffs   exclusive scan of the [workgroup][bucket] matrix
+//   3. k_extract<scatter> residues -> 8-byte occurrence records  rem<<pos_bits | position,
+//                         partitioned by level-1 bucket (owner-major)
+//   4. k_bucket_process   one workgroup per level-1 bucket: level-2 partition in HBM, then per
+//                         sub-bucket an LDS bitonic sort by (k-mer, function, ordinal), group
+//                         detection, cut, statistics, compaction of the kept k-mers
+//   5. k_overflow         sub-buckets larger than LDS: same algorithm, global-memory bitonic
+//   6. k_stats            distinct_functions, seqs_with_func, seqs-with-signature flags
+//
+// Exactness notes: group members are visited in reverse ordinal order
+// (TBB 2020 multimap LIFO), the cut is fp32 `(float)best < (float)count*0.8f`, statistics are
+// the Boost.Accumulators recurrences in fp64 with contraction disabled (-ffp-contract=off).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "skm_common.h"
+#include "skm_util.h"
+
+#if defined(SKM_WITH_RCCL)
+#include <rccl/rccl.h>
+#endif
+
+namespace skm {
+
+// ------------------------------------------------------------------------------------------
+// Tunables
+// ------------------------------------------------------------------------------------------
+constexpr int EX_THREADS = 512;        // extract workgroup
+constexpr int EX_POS_PER_THREAD = 16;  // windows per thread per step (one 16-byte load + halo)
+constexpr int EX_MAX_WG = 512;         // rows of the histogram matrix
+constexpr int SCAN_ROWS = 32;          // rows per column-scan block
+constexpr int BP_THREADS = 512;        // bucket-process workgroup
+constexpr int CAP = 4096;              // LDS sub-bucket capacity (16-byte elements)
+constexpr int SUB_TARGET = 1024;       // target records per level-2 sub-bucket
+constexpr int MAX_B2 = 12;             // <= 4096 sub-buckets per level-1 bucket
+constexpr int SMALL_GROUP = 48;        // O(c^2) offset selection below this size
+
+struct SeqMeta {        // 16 bytes, one dwordx4 load
+    uint64_t pstart;    // first residue in the packed buffer
+    uint32_t len;       // protein length
+    uint16_t func;      // FunctionIndex
+    uint16_t pad;
+};
+
+struct OvfEntry {
+    uint64_t off;       // first record (in the records buffer given to the overflow kernel)
+    uint32_t n;         // records
+    uint32_t bucket;    // level-1 bucket (hash prefix)
+    uint64_t scratch;   // element offset in scratch (host fills)
+    uint32_t npad;      // pow2 >= n (host fills)
+    uint32_t src;       // 0 = recs, 1 = tmp
+};
+
+// ------------------------------------------------------------------------------------------
+// Device helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint16_t d2u16(double d) {
+    // gcc/x86-64: cvttsd2si to int32 then keep 16 bits; out of range -> 0x80000000 -> 0
+    if (!(d > -2147483649.0 && d < 2147483648.0)) return 0;
+    return (uint16_t)(int32_t)d;
+}
+
+// Boost.Accumulators p_square_quantile(p=0.5) + lazy mean over a u16 sum + immediate variance.
+struct SigStats {
+    double h[5];
+    int32_t act[5];
+    uint32_t cnt;
+    uint16_t sum;
+    double var;
+
+    __device__ void init() {
+        for (int i = 0; i < 5; ++i) {
+            h[i] = 0.0;
+            act[i] = i + 1;
+        }
+        cnt = 0;
+        sum = 0;
+        var = 0.0;
+    }
+
+    __device__ void add(uint32_t sample) {
+        ++cnt;
+        sum = (uint16_t)(sum + sample);
+        const double x = (double)sample;
+        // ---- p_square_quantile ----
+        if (cnt <= 5) {
+            h[cnt - 1] = x;
+            if (cnt == 5) {  // std::sort of 5 values (result is the unique sorted order)
+                for (int i = 1; i < 5; ++i) {
+                    double v = h[i];
+                    int j = i - 1;
+                    while (j >= 0 && h[j] > v) {
+                        h[j + 1] = h[j];
+                        --j;
+                    }
+                    h[j + 1] = v;
+                }
+            }
+        } else {
+            int cell;
+            if (x < h[0]) {
+                h[0] = x;
+                cell = 1;
+            } else if (h[4] <= x) {
+                h[4] = x;
+                cell = 4;
+            } else {
+                cell = 1;
+                while (cell < 5 && !(x < h[cell])) ++cell;  // std::upper_bound
+            }
+            for (int i = cell; i < 5; ++i) act[i] += 1;
+            // desired positions accumulate exact multiples of 1/4: closed form is bit-identical
+            const double nstep = (double)(cnt - 5);
+            double des[5];
+            des[0] = 1.0;
+            des[1] = 2.0 + nstep * 0.25;
+            des[2] = 3.0 + nstep * 0.5;
+            des[3] = 4.0 + nstep * 0.75;
+            des[4] = 5.0 + nstep;
+            for (int i = 1; i <= 3; ++i) {
+                double d = des[i] - (double)act[i];
+                double dp = (double)act[i + 1] - (double)act[i];
+                double dm = (double)act[i - 1] - (double)act[i];
+                if ((d >= 1. && dp > 1.) || (d <= -1. && dm < -1.)) {
+                    double hp = (h[i + 1] - h[i]) / dp;
+                    double hm = (h[i - 1] - h[i]) / dm;
+                    short sign_d = static_cast<short>(d / fabs(d));
+                    double hh = h[i] + sign_d / (dp - dm) * ((sign_d - dm) * hp + (dp - sign_d) * hm);
+                    if (h[i - 1] < hh && hh < h[i + 1]) {
+                        h[i] = hh;
+                    } else {
+                        if (d > 0) h[i] += hp;
+                        if (d < 0) h[i] -= hm;
+                    }
+                    act[i] += sign_d;
+                }
+            }
+        }
+        // ---- variance (immediate), mean = lazy sum/count with the u16 sum ----
+        if (cnt > 1) {
+            double mean = (double)sum / (double)cnt;
+            double tmp = x - mean;
+            var = var * (double)(cnt - 1) / (double)cnt + tmp * tmp / (double)(cnt - 1);
+        }
+    }
+};
+
+// k-th smallest (0-based) of the low 16 bits of lo[a..b)
+__device__ uint32_t select_offset(const uint64_t* lo, uint32_t a, uint32_t b, uint32_t k) {
+    const uint32_t c = b - a;
+    if (c <= (uint32_t)SMALL_GROUP) {
+        for (uint32_t j = a; j < b; ++j) {
+            uint32_t v = (uint32_t)(lo[j] & 0xFFFFu);
+            uint32_t lt = 0, le = 0;
+            for (uint32_t t = a; t < b; ++t) {
+                uint32_t w = (uint32_t)(lo[t] & 0xFFFFu);
+                lt += w < v;
+                le += w <= v;
+            }
+            if (lt <= k && k < le) return v;
+        }
+        return 0;  // unreachable
+    }
+    uint32_t vmin = 0xFFFFu, vmax = 0;
+    for (uint32_t j = a; j < b; ++j) {
+        uint32_t v = (uint32_t)(lo[j] & 0xFFFFu);
+        vmin = min(vmin, v);
+        vmax = max(vmax, v);
+    }
+    while (vmin < vmax) {
+        uint32_t mid = (vmin + vmax) >> 1;
+        uint32_t cnt = 0;
+        for (uint32_t j = a; j < b; ++j) cnt += (uint32_t)(lo[j] & 0xFFFFu) <= mid;
+        if (cnt >= k + 1)
+            vmax = mid;
+        else
+            vmin = mid + 1;
+    }
+    return vmin;
+}
+
+// Process one group [a,b) of elements sorted by (rem, func, ordinal).  hi = rem<<16|func,
+// lo = s<<36 | i<<16 | offset16.  If kept, the head element is overwritten with the kept
+// record: hi = 1<<63 | h43<<16 | avg_from_end, lo = func | mean<<16 | median<<32 | var<<48.
+// (process_kmer_set, signature_build.tcc:219-293)
+__device__ void process_group(uint64_t* hi, uint64_t* lo, uint32_t a, uint32_t b, uint64_t hprefix,
+                              const SeqMeta* __restrict__ meta, uint8_t* __restrict__ flags) {
+    const uint32_t c = b - a;
+    // best function: iterate func runs in ascending FunctionIndex (std::map order); replace only
+    // on strictly greater count -> ties go to the lowest index.
+    uint32_t best_f = 0xFFFFu, best_c = 0, rb = a, re = a;
+    bool have = false;
+    uint32_t run_f = (uint32_t)(hi[a] & 0xFFFFu), run_s = a;
+    for (uint32_t j = a + 1; j <= b; ++j) {
+        uint32_t f = j < b ? (uint32_t)(hi[j] & 0xFFFFu) : 0x10000u;
+        if (f != run_f) {
+            uint32_t len = j - run_s;
+            if (!have || len > best_c) {
+                have = true;
+                best_f = run_f;
+                best_c = len;
+                rb = run_s;
+                re = j;
+            }
+            run_f = f;
+            run_s = j;
+        }
+    }
+    const float thresh = float(c) * 0.8f;
+    if ((float)best_c < thresh) return;
+
+    // avg_from_end: sorted(offsets)[size/2] over ALL occurrences
+    const uint32_t avg = select_offset(lo, a, b, c / 2);
+    // seqs_with_a_signature: every occurrence's sequence
+    for (uint32_t j = a; j < b; ++j) flags[lo[j] >> 36] = 1;
+    // accumulator over protein lengths of best-function occurrences, reverse ordinal order
+    SigStats st;
+    st.init();
+    uint32_t j = re;
+    while (j > rb) {
+        uint32_t lens[8];
+        uint32_t nb = min(8u, j - rb);
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t)
+            if (t < nb) lens[t] = meta[lo[j - 1 - t] >> 36].len;
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t)
+            if (t < nb) st.add(lens[t]);
+        j -= nb;
+    }
+    const uint16_t mean = d2u16((double)st.sum / (double)st.cnt);
+    const uint16_t median = d2u16(st.h[2]);
+    const uint16_t var = d2u16(st.var);
+    const uint64_t h43 = hprefix | (hi[a] >> 16);
+    hi[a] = (1ull << 63) | (h43 << 16) | avg;
+    lo[a] = (uint64_t)best_f | ((uint64_t)mean << 16) | ((uint64_t)median << 32) | ((uint64_t)var << 48);
+}
+
+__device__ __forceinline__ void make_elem(uint64_t rec, int pos_bits, uint64_t pos_mask, uint64_t pos_base,
+                                          const uint32_t* __restrict__ blk2seq, const SeqMeta* __restrict__ meta,
+                                          uint64_t& ohi, uint64_t& olo) {
+    const uint64_t rem = rec >> pos_bits;
+    const uint64_t p = (rec & pos_mask) - pos_base;
+    uint32_t s = blk2seq[p >> 6];
+    SeqMeta m = meta[s];
+    while (p >= m.pstart + m.len + 1) {
+        ++s;
+        m = meta[s];
+    }
+    const uint32_t i = (uint32_t)(p - m.pstart);
+    const uint32_t off16 = (m.len - i) & 0xFFFFu;
+    ohi = (rem << 16) | m.func;
+    olo = ((uint64_t)s << 36) | ((uint64_t)i << 16) | off16;
+}
+
+__device__ __forceinline__ bool elem_less(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
+    return ah < bh || (ah == bh && al < bl);
+}
+
+// Bitonic network over hi/lo[0..N) restricted to stages k in [kmin..kmax] (pow2), all strides j
+// of those stages below jlim; gidx0 = global index of element 0 (for chunked global sorts).
+__device__ void bitonic_lds(uint64_t* hi, uint64_t* lo, uint32_t N, uint32_t kmin, uint32_t kmax, uint32_t jtop,
+                            uint64_t gidx0) {
+    for (uint32_t k = kmin; k <= kmax; k <<= 1) {
+        for (uint32_t j = min(k >> 1, jtop); j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < N / 2; t += blockDim.x) {
+                uint32_t i = 2 * t - (t & (j - 1));
+                uint32_t l = i + j;
+                bool asc = (((gidx0 + i) & k) == 0);
+                uint64_t ah = hi[i], al = lo[i], bh = hi[l], bl = lo[l];
+                bool gt = elem_less(bh, bl, ah, al);
+                if (gt == asc) {
+                    hi[i] = bh;
+                    lo[i] = bl;
+                    hi[l] = ah;
+                    lo[l] = al;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Workgroup exclusive scan of one u32 per thread (blockDim multiple of 64, <= 1024).
+__device__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) s_wave[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int w = 0; w < nw; ++w) {
+            uint32_t t = s_wave[w];
+            s_wave[w] = acc;
+            acc += t;
+        }
+        s_wave[nw] = acc;
+    }
+    __syncthreads();
+    uint32_t r = s_wave[wave] + x - v;
+    total = s_wave[nw];
+    __syncthreads();
+    return r;
+}
+
+// Find groups in sorted hi/lo[0..n), process them, compact kept records to the output.
+__device__ void process_sorted(uint64_t* hi, uint64_t* lo, uint32_t n, uint64_t hprefix, const SeqMeta* meta,
+                               uint8_t* flags, uint16_t* s_heads, uint32_t* s_wave,
+                               unsigned long long* kept_ctr, uint64_t* out_keys, skm_stored_kmer_data* out_data) {
+    // group heads -> compact list (ordered)
+    uint32_t base = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += blockDim.x) {
+        uint32_t j = c0 + threadIdx.x;
+        bool head = j < n && (j == 0 || (hi[j] >> 16) != (hi[j - 1] >> 16));
+        uint32_t tot;
+        uint32_t pos = wg_exclusive_scan(head ? 1u : 0u, s_wave, tot);
+        if (head) s_heads[base + pos] = (uint16_t)j;
+        base += tot;
+    }
+    __syncthreads();
+    const uint32_t ngroups = base;
+    for (uint32_t g = threadIdx.x; g < ngroups; g += blockDim.x) {
+        uint32_t a = s_heads[g];
+        uint32_t b = g + 1 < ngroups ? s_heads[g + 1] : n;
+        process_group(hi, lo, a, b, hprefix, meta, flags);
+    }
+    __syncthreads();
+    // compaction of kept heads
+    uint32_t kbase_local = 0;
+    uint64_t gbase = 0;
+    for (uint32_t g0 = 0; g0 < ngroups; g0 += blockDim.x) {
+        uint32_t g = g0 + threadIdx.x;
+        uint32_t a = g < ngroups ? s_heads[g] : 0;
+        bool kept = g < ngroups && (hi[a] >> 63);
+        uint32_t tot;
+        uint32_t pos = wg_exclusive_scan(kept ? 1u : 0u, s_wave, tot);
+        if (tot == 0) continue;
+        if (threadIdx.x == 0) s_wave[32] = (uint32_t)0;
+        if (threadIdx.x == 0) {
+            unsigned long long gb = atomicAdd(kept_ctr, (unsigned long long)tot);
+            reinterpret_cast<unsigned long long*>(s_wave)[17] = gb;
+        }
+        __syncthreads();
+        gbase = reinterpret_cast<unsigned long long*>(s_wave)[17];
+        if (kept) {
+            uint64_t H = hi[a], L = lo[a];
+            uint64_t h43 = (H >> 16) & KEY_MASK;
+            uint64_t raw = decode_key(unmix43(h43));
+            uint64_t o = gbase + pos;
+            out_keys[o] = raw;
+            skm_stored_kmer_data d;
+            d.avg_from_end = (uint16_t)(H & 0xFFFFu);
+            d.function_index = (uint16_t)(L & 0xFFFFu);
+            d.mean = (uint16_t)(L >> 16);
+            d.median = (uint16_t)(L >> 32);
+            d.var = (uint16_t)(L >> 48);
+            out_data[o] = d;
+        }
+        __syncthreads();
+        kbase_local += tot;
+    }
+    (void)kbase_local;
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernels
+// ------------------------------------------------------------------------------------------
+
+// blk2seq[b] = sequence containing packed position 64*b
+__global__ void k_blk2seq(const SeqMeta* __restrict__ meta, uint32_t nseq, uint32_t* __restrict__ blk2seq,
+                          uint64_t nblk) {
+    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseq) return;
+    uint64_t a = meta[s].pstart, e = a + meta[s].len + 1;
+    for (uint64_t b = (a + 63) >> 6; b < ((e + 63) >> 6) && b < nblk; ++b) blk2seq[b] = s;
+}
+
+template <bool SCATTER>
+__global__ __launch_bounds__(EX_THREADS) void k_extract(const uint8_t* __restrict__ res, uint64_t rp, uint64_t span,
+                                                        int owner_bits, int b1_bits, uint64_t pos_base,
+                                                        uint32_t* __restrict__ hist, const uint32_t* __restrict__ offs,
+                                                        const uint64_t* __restrict__ owner_start,
+                                                        uint64_t* __restrict__ recs) {
+    extern __shared__ uint32_t s_cnt[];  // [NB]
+    const int nbits = owner_bits + b1_bits;
+    const uint32_t NB = 1u << nbits;
+    const int rem_bits = KEY_BITS - nbits;
+    const int pos_bits = 64 - rem_bits;
+    const uint64_t rem_mask = (1ull << rem_bits) - 1;
+    const uint32_t wg = blockIdx.x;
+    for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) s_cnt[b] = SCATTER ? offs[(uint64_t)wg * NB + b] : 0u;
+    __syncthreads();
+    const uint64_t begin = (uint64_t)wg * span;
+    const uint64_t end = min(begin + span, rp);
+    for (uint64_t base = begin + (uint64_t)threadIdx.x * EX_POS_PER_THREAD; base < end;
+         base += (uint64_t)blockDim.x * EX_POS_PER_THREAD) {
+        const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
+        const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
+        const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        uint32_t code[24];
+        uint32_t valid = 0;
+#pragma unroll
+        for (int j = 0; j < 24; ++j) {
+            uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            uint32_t cd = residue_code(c);
+            valid |= (cd < 40u ? 1u : 0u) << j;
+            code[j] = cd < 40u ? cd : 0u;
+        }
+        uint64_t k = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
+        constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
+#pragma unroll
+        for (int t = 0; t < EX_POS_PER_THREAD; ++t) {
+            if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
+            const uint64_t p = base + t;
+            if (((valid >> t) & 0xFFu) == 0xFFu && p < end) {
+                const uint64_t h = mix43(k);
+                const uint32_t bucket = (uint32_t)(h >> rem_bits);
+                if (SCATTER) {
+                    const uint32_t idx = atomicAdd(&s_cnt[bucket], 1u);
+                    const uint64_t o = owner_start[bucket >> b1_bits] + idx;
+                    recs[o] = ((h & rem_mask) << pos_bits) | (pos_base + p);
+                } else {
+                    atomicAdd(&s_cnt[bucket], 1u);
+                }
+            }
+        }
+    }
+    if (!SCATTER) {
+        __syncthreads();
+        for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) hist[(uint64_t)wg * NB + b] = s_cnt[b];
+    }
+}
+
+// partial[rb][b] = sum of hist[w][b] over rows w of row-block rb
+__global__ void k_colsum(const uint32_t* __restrict__ hist, uint32_t nwg, uint32_t NB, uint32_t* __restrict__ partial) {
+    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t rb = blockIdx.y;
+    if (b >= NB) return;
+    uint32_t w0 = rb * SCAN_ROWS, w1 = min(nwg, w0 + SCAN_ROWS);
+    uint32_t s = 0;
+    for (uint32_t w = w0; w < w1; ++w) s += hist[(uint64_t)w * NB + b];
+    partial[(uint64_t)rb * NB + b] = s;
+}
+
+// One workgroup: bucket totals -> owner-relative bucket starts; rbbase[rb][b] = start of the
+// row-block's first row within the bucket (owner-relative); owner_start[o] absolute.
+__global__ void k_bstart(const uint32_t* __restrict__ partial, uint32_t nrb, uint32_t NB, int b1_bits,
+                         uint32_t* __restrict__ rbbase, uint32_t* __restrict__ bstart, uint64_t* __restrict__ owner_start,
+                         uint32_t nowners) {
+    __shared__ uint32_t s_wave[34];
+    __shared__ unsigned long long s_tot[64];
+    const uint32_t per = (NB + blockDim.x - 1) / blockDim.x;
+    const uint32_t b0 = threadIdx.x * per;
+    // per-thread totals over its bucket range
+    uint32_t local = 0;
+    for (uint32_t b = b0; b < min(NB, b0 + per); ++b) {
+        uint32_t acc = 0;
+        for (uint32_t rb = 0; rb < nrb; ++rb) {
+            uint32_t v = partial[(uint64_t)rb * NB + b];
+            rbbase[(uint64_t)rb * NB + b] = acc;
+            acc += v;
+        }
+        bstart[b] = acc;  // temporarily the total
+        local += acc;
+    }
+    uint32_t total;
+    uint32_t ex = wg_exclusive_scan(local, s_wave, total);
+    // absolute exclusive starts
+    uint32_t run = ex;
+    for (uint32_t b = b0; b < min(NB, b0 + per); ++b) {
+        uint32_t t = bstart[b];
+        bstart[b] = run;
+        run += t;
+    }
+    __syncthreads();
+    // owner starts (absolute), then make bucket starts owner-relative
+    if (threadIdx.x < nowners) {
+        uint32_t ob = threadIdx.x << b1_bits;
+        s_tot[threadIdx.x] = bstart[ob];
+    }
+    if (threadIdx.x == 0) s_tot[nowners] = total;
+    __syncthreads();
+    if (threadIdx.x <= nowners) owner_start[threadIdx.x] = s_tot[threadIdx.x];
+    for (uint32_t b = b0; b < min(NB, b0 + per); ++b) {
+        uint32_t o = b >> b1_bits;
+        uint32_t rel = bstart[b] - (uint32_t)s_tot[o];
+        for (uint32_t rb = 0; rb < nrb; ++rb) rbbase[(uint64_t)rb * NB + b] += rel;
+    }
+    __syncthreads();
+    for (uint32_t b = b0; b < min(NB, b0 + per); ++b) bstart[b] -= (uint32_t)s_tot[b >> b1_bits];
+    if (threadIdx.x == 0) bstart[NB] = 0;  // sentinel unused
+}
+
+// offs[w][b] = rbbase[rb][b] + sum of hist rows before w inside the row-block
+__global__ void k_coloffs(const uint32_t* __restrict__ hist, const uint32_t* __restrict__ rbbase, uint32_t nwg, uint32_t NB,
+                          uint32_t* __restrict__ offs) {
+    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t rb = blockIdx.y;
+    if (b >= NB) return;
+    uint32_t w0 = rb * SCAN_ROWS, w1 = min(nwg, w0 + SCAN_ROWS);
+    uint32_t run = rbbase[(uint64_t)rb * NB + b];
+    for (uint32_t w = w0; w < w1; ++w) {
+        uint64_t idx = (uint64_t)w * NB + b;
+        uint32_t v = hist[idx];
+        offs[idx] = run;
+        run += v;
+    }
+}
+
+struct BucketArgs {
+    const uint64_t* recs;      // records of this owner, bucket-major (level-1)
+    uint64_t* tmp;             // level-2 partition scratch, same indexing as recs
+    const uint64_t* bstart;    // [nbuckets+1] absolute starts in recs
+    uint32_t nbuckets;
+    uint32_t bucket_base;      // global bucket id of bucket 0 (owner << b1_bits)
+    int rem_bits, pos_bits;
+    uint64_t pos_base;         // subtract from record positions to get local packed positions
+    const uint32_t* blk2seq;
+    const SeqMeta* meta;
+    uint8_t* flags;
+    unsigned long long* kept_ctr;
+    uint64_t* out_keys;
+    skm_stored_kmer_data* out_data;
+    OvfEntry* ovf;
+    unsigned int* ovf_ctr;
+    uint32_t ovf_cap;
+};
+
+__global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
+    __shared__ uint64_t s_hi[CAP];
+    __shared__ uint64_t s_lo[CAP];
+    __shared__ uint32_t s_sub[(1 << MAX_B2) + 1];
+    __shared__ uint16_t s_heads[CAP];
+    __shared__ uint32_t s_wave[40];
+    const uint32_t bucket = blockIdx.x;
+    if (bucket >= A.nbuckets) return;
+    const uint64_t r0 = A.bstart[bucket], r1 = A.bstart[bucket + 1];
+    const uint64_t n = r1 - r0;
+    if (n == 0) return;
+    const uint64_t pos_mask = (A.pos_bits >= 64) ? ~0ull : ((1ull << A.pos_bits) - 1);
+    const uint64_t hprefix = (uint64_t)(A.bucket_base + bucket) << A.rem_bits;
+
+    auto load_and_process = [&](const uint64_t* src, uint32_t cnt) {
+        uint32_t N = 1;
+        while (N < cnt) N <<= 1;
+        for (uint32_t j = threadIdx.x; j < N; j += blockDim.x) {
+            if (j < cnt) {
+                make_elem(src[j], A.pos_bits, pos_mask, A.pos_base, A.blk2seq, A.meta, s_hi[j], s_lo[j]);
+            } else {
+                s_hi[j] = ~0ull;
+                s_lo[j] = ~0ull;
+            }
+        }
+        __syncthreads();
+        bitonic_lds(s_hi, s_lo, N, 2, N, N, 0);
+        process_sorted(s_hi, s_lo, cnt, hprefix, A.meta, A.flags, s_heads, s_wave, A.kept_ctr, A.out_keys, A.out_data);
+        __syncthreads();
+    };
+    auto push_overflow = [&](uint64_t off, uint32_t cnt, uint32_t src) {
+        unsigned int e = atomicAdd(A.ovf_ctr, 1u);
+        if (e < A.ovf_cap) {
+            OvfEntry en;
+            en.off = off;
+            en.n = cnt;
+            en.bucket = bucket;
+            en.scratch = 0;
+            en.npad = 0;
+            en.src = src;
+            A.ovf[e] = en;
+        }
+    };
+
+    if (n <= (uint64_t)CAP) {
+        load_and_process(A.recs + r0, (uint32_t)n);
+        return;
+    }
+    // ---- level-2 partition by the next b2 bits of rem ----
+    int b2 = 0;
+    while (b2 < MAX_B2 && (n >> b2) > (uint64_t)SUB_TARGET) ++b2;
+    const uint32_t nsub = 1u << b2;
+    const int shift = A.rem_bits - b2;
+    for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_sub[d] = 0;
+    __syncthreads();
+    for (uint64_t j = threadIdx.x; j < n; j += blockDim.x) {
+        uint64_t rec = A.recs[r0 + j];
+        uint32_t d = (uint32_t)((rec >> A.pos_bits) >> shift);
+        atomicAdd(&s_sub[d], 1u);
+    }
+    __syncthreads();
+    // exclusive scan of s_sub[0..nsub) (each thread a contiguous chunk)
+    {
+        const uint32_t per = (nsub + blockDim.x - 1) / blockDim.x;
+        const uint32_t d0 = threadIdx.x * per;
+        uint32_t local = 0;
+        for (uint32_t d = d0; d < min(nsub, d0 + per); ++d) local += s_sub[d];
+        uint32_t tot;
+        uint32_t run = wg_exclusive_scan(local, s_wave, tot);
+        for (uint32_t d = d0; d < min(nsub, d0 + per); ++d) {
+            uint32_t t = s_sub[d];
+            s_sub[d] = run;
+            run += t;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) s_sub[nsub] = tot;
+        __syncthreads();
+    }
+    // scatter into tmp using s_heads area as per-sub cursors is too small; use s_hi as cursors
+    uint32_t* s_cur = reinterpret_cast<uint32_t*>(s_hi);
+    for (uint32_t d = threadIdx.x; d < nsub; d += blockDim.x) s_cur[d] = s_sub[d];
+    __syncthreads();
+    for (uint64_t j = threadIdx.x; j < n; j += blockDim.x) {
+        uint64_t rec = A.recs[r0 + j];
+        uint32_t d = (uint32_t)((rec >> A.pos_bits) >> shift);
+        uint32_t o = atomicAdd(&s_cur[d], 1u);
+        A.tmp[r0 + o] = rec;
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (uint32_t d = 0; d < nsub; ++d) {
+        const uint32_t a = s_sub[d], e = s_sub[d + 1];
+        const uint32_t cnt = e - a;
+        if (cnt == 0) continue;
+        if (cnt <= (uint32_t)CAP) {
+            load_and_process(A.tmp + r0 + a, cnt);
+        } else if (threadIdx.x == 0) {
+            push_overflow(r0 + a, cnt, 1);
+        }
+    }
+}
+
+struct OvfArgs {
+    const OvfEntry* ovf;
+    const uint64_t* recs;
+    const uint64_t* tmp;
+    uint64_t* s_hi_g;   // scratch elements
+    uint64_t* s_lo_g;
+    uint32_t bucket_base;
+    int rem_bits, pos_bits;
+    uint64_t pos_base;
+    const uint32_t* blk2seq;
+    const SeqMeta* meta;
+    uint8_t* flags;
+    unsigned long long* kept_ctr;
+    uint64_t* out_keys;
+    skm_stored_kmer_data* out_data;
+    uint32_t* heads_g;  // scratch group heads (u32), same indexing as elements
+};
+
+// Groups of a sorted global array (the overflow form of process_sorted).
+__device__ void process_sorted_global(uint64_t* hi, uint64_t* lo, uint32_t n, uint64_t hprefix, const SeqMeta* meta,
+                                      uint8_t* flags, uint32_t* heads, uint32_t* s_wave,
+                                      unsigned long long* kept_ctr, uint64_t* out_keys, skm_stored_kmer_data* out_data) {
+    uint32_t base = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += blockDim.x) {
+        uint32_t j = c0 + threadIdx.x;
+        bool head = j < n && (j == 0 || (hi[j] >> 16) != (hi[j - 1] >> 16));
+        uint32_t tot;
+        uint32_t pos = wg_exclusive_scan(head ? 1u : 0u, s_wave, tot);
+        if (head) heads[base + pos] = j;
+        base += tot;
+    }
+    __threadfence_block();
+    __syncthreads();
+    const uint32_t ngroups = base;
+    for (uint32_t g = threadIdx.x; g < ngroups; g += blockDim.x) {
+        uint32_t a = heads[g];
+        uint32_t b = g + 1 < ngroups ? heads[g + 1] : n;
+        process_group(hi, lo, a, b, hprefix, meta, flags);
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (uint32_t g0 = 0; g0 < ngroups; g0 += blockDim.x) {
+        uint32_t g = g0 + threadIdx.x;
+        uint32_t a = g < ngroups ? heads[g] : 0;
+        bool kept = g < ngroups && (hi[a] >> 63);
+        uint32_t tot;
+        uint32_t pos = wg_exclusive_scan(kept ? 1u : 0u, s_wave, tot);
+        if (tot == 0) continue;
+        if (threadIdx.x == 0) {
+            unsigned long long gb = atomicAdd(kept_ctr, (unsigned long long)tot);
+            reinterpret_cast<unsigned long long*>(s_wave)[17] = gb;
+        }
+        __syncthreads();
+        uint64_t gbase = reinterpret_cast<unsigned long long*>(s_wave)[17];
+        if (kept) {
+            uint64_t H = hi[a], L = lo[a];
+            uint64_t raw = decode_key(unmix43((H >> 16) & KEY_MASK));
+            uint64_t o = gbase + pos;
+            out_keys[o] = raw;
+            skm_stored_kmer_data d;
+            d.avg_from_end = (uint16_t)(H & 0xFFFFu);
+            d.function_index = (uint16_t)(L & 0xFFFFu);
+            d.mean = (uint16_t)(L >> 16);
+            d.median = (uint16_t)(L >> 32);
+            d.var = (uint16_t)(L >> 48);
+            out_data[o] = d;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(BP_THREADS) void k_overflow(OvfArgs A) {
+    __shared__ uint64_t s_hi[CAP];
+    __shared__ uint64_t s_lo[CAP];
+    __shared__ uint32_t s_wave[40];
+    const OvfEntry e = A.ovf[blockIdx.x];
+    const uint64_t* src = (e.src ? A.tmp : A.recs) + e.off;
+    uint64_t* ghi = A.s_hi_g + e.scratch;
+    uint64_t* glo = A.s_lo_g + e.scratch;
+    uint32_t* heads = A.heads_g + e.scratch;
+    const uint32_t N = e.npad, n = e.n;
+    const uint64_t pos_mask = (A.pos_bits >= 64) ? ~0ull : ((1ull << A.pos_bits) - 1);
+    const uint64_t hprefix = (uint64_t)(A.bucket_base + e.bucket) << A.rem_bits;
+    // phase 0: chunks of CAP sorted in LDS (directions from global index)
+    for (uint32_t c0 = 0; c0 < N; c0 += CAP) {
+        for (uint32_t j = threadIdx.x; j < CAP; j += blockDim.x) {
+            uint32_t g = c0 + j;
+            if (g < n) {
+                make_elem(src[g], A.pos_bits, pos_mask, A.pos_base, A.blk2seq, A.meta, s_hi[j], s_lo[j]);
+            } else {
+                s_hi[j] = ~0ull;
+                s_lo[j] = ~0ull;
+            }
+        }
+        __syncthreads();
+        bitonic_lds(s_hi, s_lo, CAP, 2, CAP, CAP, c0);
+        for (uint32_t j = threadIdx.x; j < CAP; j += blockDim.x) {
+            ghi[c0 + j] = s_hi[j];
+            glo[c0 + j] = s_lo[j];
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    // merge stages k > CAP: strides >= CAP in global memory, then strides < CAP per chunk in LDS
+    for (uint32_t k = 2 * CAP; k <= N; k <<= 1) {
+        for (uint32_t j = k >> 1; j >= (uint32_t)CAP; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < N / 2; t += blockDim.x) {
+                uint32_t i = 2 * t - (t & (j - 1));
+                uint32_t l = i + j;
+                bool asc = ((i & k) == 0);
+                uint64_t ah = ghi[i], al = glo[i], bh = ghi[l], bl = glo[l];
+                bool gt = elem_less(bh, bl, ah, al);
+                if (gt == asc) {
+                    ghi[i] = bh;
+                    glo[i] = bl;
+                    ghi[l] = ah;
+                    glo[l] = al;
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+        for (uint32_t c0 = 0; c0 < N; c0 += CAP) {
+            for (uint32_t j = threadIdx.x; j < CAP; j += blockDim.x) {
+                s_hi[j] = ghi[c0 + j];
+                s_lo[j] = glo[c0 + j];
+            }
+            __syncthreads();
+            bitonic_lds(s_hi, s_lo, CAP, k, k, CAP >> 1, c0);
+            for (uint32_t j = threadIdx.x; j < CAP; j += blockDim.x) {
+                ghi[c0 + j] = s_hi[j];
+                glo[c0 + j] = s_lo[j];
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+    }
+    process_sorted_global(ghi, glo, n, hprefix, A.meta, A.flags, heads, s_wave, A.kept_ctr, A.out_keys, A.out_data);
+}
+
+// distinct_functions[f] += kept k-mers with best function f (LDS privatised when it fits)
+__global__ void k_func_hist_kept(const skm_stored_kmer_data* __restrict__ data, uint64_t n, uint32_t nf,
+                                 uint32_t* __restrict__ dfunc) {
+    extern __shared__ uint32_t s_h[];
+    const bool lds = nf <= 16384;
+    if (lds)
+        for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) s_h[f] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t f = data[i].function_index;
+        if (f < nf) {
+            if (lds)
+                atomicAdd(&s_h[f], 1u);
+            else
+                atomicAdd(&dfunc[f], 1u);
+        }
+    }
+    __syncthreads();
+    if (lds)
+        for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x)
+            if (s_h[f]) atomicAdd(&dfunc[f], s_h[f]);
+}
+
+__global__ void k_func_hist_seqs(const SeqMeta* __restrict__ meta, uint32_t nseq, uint32_t nf, uint32_t* __restrict__ swf) {
+    extern __shared__ uint32_t s_h[];
+    const bool lds = nf <= 16384;
+    if (lds)
+        for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) s_h[f] = 0;
+    __syncthreads();
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseq; s += gridDim.x * blockDim.x) {
+        uint32_t f = meta[s].func;
+        if (f < nf) {
+            if (lds)
+                atomicAdd(&s_h[f], 1u);
+            else
+                atomicAdd(&swf[f], 1u);
+        }
+    }
+    __syncthreads();
+    if (lds)
+        for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x)
+            if (s_h[f]) atomicAdd(&swf[f], s_h[f]);
+}
+
+__global__ void k_count_flags(const uint8_t* __restrict__ flags, uint32_t nseq, unsigned long long* __restrict__ out) {
+    uint32_t local = 0;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseq; s += gridDim.x * blockDim.x) local += flags[s] ? 1u : 0u;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) local += __shfl_down(local, d, 64);
+    if ((threadIdx.x & 63) == 0 && local) atomicAdd(out, (unsigned long long)local);
+}
+
+}  // namespace skm
+
+// ==========================================================================================
+// Host side
+// ==========================================================================================
+using namespace skm;
+
+struct skm_build {
+    skm_build_opts opts{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[8] = {};
+    float last_ms[8] = {};
+
+    // host staging (reference emission order, only sequences with a kept function)
+    std::vector<uint8_t> h_res;     // packed residues with one 0 separator after each sequence
+    std::vector<SeqMeta> h_meta;
+    std::vector<uint32_t> h_seqid;
+    uint64_t n_windows = 0;
+    bool seqid_strict = true;
+    bool prepared = false, ran = false;
+
+    // device input
+    DevBuf d_res, d_meta, d_blk2seq;
+    uint64_t rp = 0;       // packed length
+    uint32_t nseq = 0;
+    // geometry
+    int owner_bits = 0, b1_bits = 11;
+    // device work
+    DevBuf d_hist, d_offs, d_partial, d_rbbase, d_bstart32, d_bstart, d_owner_start;
+    DevBuf d_recs, d_tmp;
+    DevBuf d_keys, d_data, d_ctr, d_flags, d_dfunc, d_swf, d_ovf, d_ovf_hi, d_ovf_lo, d_ovf_heads;
+    uint32_t nwg = 0;
+    uint64_t span = 0;
+    uint64_t n_records = 0;
+    uint64_t n_kept = 0;
+    uint64_t ovf_cap = 0;
+
+    // multi-GPU
+#if defined(SKM_WITH_RCCL)
+    ncclComm_t comm = nullptr;
+#endif
+    bool has_comm = false;
+};
+
+namespace {
+
+void bucket_starts_abs(skm_build* b, std::vector<uint64_t>& starts) {
+    // host helper: build absolute bucket starts from owner-relative u32 starts (single GPU)
+    const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
+    std::vector<uint32_t> rel(NB + 1);
+    std::vector<uint64_t> ost((1u << b->owner_bits) + 1);
+    SKM_HIP(hipMemcpyAsync(rel.data(), b->d_bstart32.p, sizeof(uint32_t) * (NB + 1), hipMemcpyDeviceToHost, b->stream));
+    SKM_HIP(hipMemcpyAsync(ost.data(), b->d_owner_start.p, sizeof(uint64_t) * ost.size(), hipMemcpyDeviceToHost, b->stream));
+    SKM_HIP(hipStreamSynchronize(b->stream));
+    starts.resize(NB + 1);
+    for (uint32_t k = 0; k < NB; ++k) starts[k] = ost[k >> b->b1_bits] + rel[k];
+    starts[NB] = ost[1u << b->owner_bits];
+}
+
+__global__ void k_abs_starts(const uint32_t* rel, const uint64_t* ost, uint32_t NB, int b1_bits, uint32_t nowners,
+                             uint64_t* out) {
+    uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < NB) out[k] = ost[k >> b1_bits] + rel[k];
+    if (k == NB) out[NB] = ost[nowners];
+}
+
+void run_pipeline(skm_build* b) {
+    hipStream_t st = b->stream;
+    const int nbits = b->owner_bits + b->b1_bits;
+    const uint32_t NB = 1u << nbits;
+    const uint32_t nowners = 1u << b->owner_bits;
+    const int rem_bits = KEY_BITS - nbits;
+    const int pos_bits = 64 - rem_bits;
+    const uint32_t F = b->opts.n_functions;
+
+    SKM_HIP(hipEventRecord(b->ev[0], st));
+    // ---- 1. count ----
+    size_t lds_cnt = sizeof(uint32_t) * NB;
+    hipLaunchKernelGGL(k_extract<false>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, b->d_res.as<uint8_t>(), b->rp,
+                       b->span, b->owner_bits, b->b1_bits, (uint64_t)0, b->d_hist.as<uint32_t>(), nullptr, nullptr,
+                       nullptr);
+    SKM_HIP(hipGetLastError());
+    SKM_HIP(hipEventRecord(b->ev[1], st));
+    // ---- 2. scan ----
+    const uint32_t nrb = (uint32_t)ceil_div(b->nwg, SCAN_ROWS);
+    dim3 gsc((NB + 255) / 256, nrb);
+    hipLaunchKernelGGL(k_colsum, gsc, dim3(256), 0, st, b->d_hist.as<uint32_t>(), b->nwg, NB, b->d_partial.as<uint32_t>());
+    hipLaunchKernelGGL(k_bstart, dim3(1), dim3(1024), 0, st, b->d_partial.as<uint32_t>(), nrb, NB, b->b1_bits,
+                       b->d_rbbase.as<uint32_t>(), b->d_bstart32.as<uint32_t>(), b->d_owner_start.as<uint64_t>(), nowners);
+    hipLaunchKernelGGL(k_coloffs, gsc, dim3(256), 0, st, b->d_hist.as<uint32_t>(), b->d_rbbase.as<uint32_t>(), b->nwg,
+                       NB, b->d_offs.as<uint32_t>());
+    hipLaunchKernelGGL(k_abs_starts, dim3((NB + 1 + 255) / 256), dim3(256), 0, st, b->d_bstart32.as<uint32_t>(),
+                       b->d_owner_start.as<uint64_t>(), NB, b->b1_bits, nowners, b->d_bstart.as<uint64_t>());
+    SKM_HIP(hipGetLastError());
+    SKM_HIP(hipEventRecord(b->ev[2], st));
+    // ---- 3. scatter ----
+    hipLaunchKernelGGL(k_extract<true>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, b->d_res.as<uint8_t>(), b->rp,
+                       b->span, b->owner_bits, b->b1_bits, (uint64_t)0, nullptr, b->d_offs.as<uint32_t>(),
+                       b->d_owner_start.as<uint64_t>(), b->d_recs.as<uint64_t>());
+    SKM_HIP(hipGetLastError());
+    SKM_HIP(hipEventRecord(b->ev[3], st));
+    // ---- 4. bucket process ----
+    SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 64, st));
+    SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->nseq ? b->nseq : 1, st));
+    BucketArgs A;
+    A.recs = b->d_recs.as<uint64_t>();
+    A.tmp = b->d_tmp.as<uint64_t>();
+    A.bstart = b->d_bstart.as<uint64_t>();
+    A.nbuckets = NB;
+    A.bucket_base = 0;
+    A.rem_bits = rem_bits;
+    A.pos_bits = pos_bits;
+    A.pos_base = 0;
+    A.blk2seq = b->d_blk2seq.as<uint32_t>();
+    A.meta = b->d_meta.as<SeqMeta>();
+    A.flags = b->d_flags.as<uint8_t>();
+    A.kept_ctr = b->d_ctr.as<unsigned long long>();
+    A.out_keys = b->d_keys.as<uint64_t>();
+    A.out_data = b->d_data.as<skm_stored_kmer_data>();
+    A.ovf = b->d_ovf.as<OvfEntry>();
+    A.ovf_ctr = reinterpret_cast<unsigned int*>(b->d_ctr.as<unsigned long long>() + 1);
+    A.ovf_cap = (uint32_t)b->ovf_cap;
+    hipLaunchKernelGGL(k_bucket_process, dim3(NB), dim3(BP_THREADS), 0, st, A);
+    SKM_HIP(hipGetLastError());
+    SKM_HIP(hipEventRecord(b->ev[4], st));
+    // ---- 5. overflow ----
+    unsigned long long ctr[2];
+    SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, sizeof(ctr), hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipStreamSynchronize(st));
+    uint32_t novf = (uint32_t)(ctr[1] & 0xFFFFFFFFull);
+    SKM_CHECK(novf <= b->ovf_cap, SKM_E_OOM, "overflow list capacity exceeded");
+    if (novf) {
+        std::vector<OvfEntry> ov(novf);
+        SKM_HIP(hipMemcpyAsync(ov.data(), b->d_ovf.p, sizeof(OvfEntry) * novf, hipMemcpyDeviceToHost, st));
+        SKM_HIP(hipStreamSynchronize(st));
+        uint64_t tot = 0;
+        for (auto& e : ov) {
+            uint32_t np = 1;
+            while (np < e.n) np <<= 1;
+            e.npad = np;
+            e.scratch = tot;
+            tot += np;
+        }
+        b->d_ovf_hi.ensure(tot * 8);
+        b->d_ovf_lo.ensure(tot * 8);
+        b->d_ovf_heads.ensure(tot * 4);
+        SKM_HIP(hipMemcpyAsync(b->d_ovf.p, ov.data(), sizeof(OvfEntry) * novf, hipMemcpyHostToDevice, st));
+        OvfArgs O;
+        O.ovf = b->d_ovf.as<OvfEntry>();
+        O.recs = b->d_recs.as<uint64_t>();
+        O.tmp = b->d_tmp.as<uint64_t>();
+        O.s_hi_g = b->d_ovf_hi.as<uint64_t>();
+        O.s_lo_g = b->d_ovf_lo.as<uint64_t>();
+        O.bucket_base = 0;
+        O.rem_bits = rem_bits;
+        O.pos_bits = pos_bits;
+        O.pos_base = 0;
+        O.blk2seq = A.blk2seq;
+        O.meta = A.meta;
+        O.flags = A.flags;
+        O.kept_ctr = A.kept_ctr;
+        O.out_keys = A.out_keys;
+        O.out_data = A.out_data;
+        O.heads_g = b->d_ovf_heads.as<uint32_t>();
+        hipLaunchKernelGGL(k_overflow, dim3(novf), dim3(BP_THREADS), 0, st, O);
+        SKM_HIP(hipGetLastError());
+    }
+    SKM_HIP(hipEventRecord(b->ev[5], st));
+    // ---- 6. stats ----
+    SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
+    SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
+    // kept count is needed for the histogram bound: use the upper bound (records) and let the
+    // kernel read the device counter instead -- simpler: sync for the count.
+    SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, sizeof(ctr), hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipStreamSynchronize(st));
+    b->n_kept = ctr[0];
+    size_t lds_f = F <= 16384 ? sizeof(uint32_t) * F : 0;
+    if (b->n_kept)
+        hipLaunchKernelGGL(k_func_hist_kept, dim3(1024), dim3(256), lds_f, st, b->d_data.as<skm_stored_kmer_data>(),
+                           b->n_kept, F, b->d_dfunc.as<uint32_t>());
+    if (b->nseq)
+        hipLaunchKernelGGL(k_func_hist_seqs, dim3(256), dim3(256), lds_f, st, b->d_meta.as<SeqMeta>(), b->nseq, F,
+                           b->d_swf.as<uint32_t>());
+    hipLaunchKernelGGL(k_count_flags, dim3(256), dim3(256), 0, st, b->d_flags.as<uint8_t>(), b->nseq,
+                       b->d_ctr.as<unsigned long long>() + 2);
+    SKM_HIP(hipGetLastError());
+    SKM_HIP(hipEventRecord(b->ev[6], st));
+    SKM_HIP(hipEventSynchronize(b->ev[6]));
+    for (int i = 0; i < 6; ++i) SKM_HIP(hipEventElapsedTime(&b->last_ms[i], b->ev[i], b->ev[i + 1]));
+    SKM_HIP(hipEventElapsedTime(&b->last_ms[6], b->ev[0], b->ev[6]));
+    b->ran = true;
+}
+
+void prepare(skm_build* b) {
+    if (b->prepared) return;
+    SKM_HIP(hipSetDevice(b->device));
+    const uint64_t rp = b->h_res.size();
+    b->rp = rp;
+    b->nseq = (uint32_t)b->h_meta.size();
+    SKM_CHECK(b->h_meta.size() < (1ull << ELEM_S_BITS), SKM_E_ARG, "too many sequences in one build shard");
+    // geometry: records carry the packed position in pos_bits
+    b->owner_bits = 0;
+    b->b1_bits = 11;
+    const int rem_bits = KEY_BITS - b->owner_bits - b->b1_bits;
+    SKM_CHECK(rp < (1ull << (64 - rem_bits)), SKM_E_ARG, "input too large for one GPU shard");
+    SKM_CHECK(b->n_windows < (1ull << 32), SKM_E_ARG, "more than 2^32 windows in one GPU shard");
+    // upload
+    b->d_res.ensure(rp + 64);
+    SKM_HIP(hipMemsetAsync(b->d_res.p, 0, rp + 64, b->stream));
+    if (rp) SKM_HIP(hipMemcpyAsync(b->d_res.p, b->h_res.data(), rp, hipMemcpyHostToDevice, b->stream));
+    b->d_meta.ensure(sizeof(SeqMeta) * (b->nseq + 1));
+    SeqMeta sentinel{rp, 0, 0xFFFF, 0};
+    std::vector<SeqMeta> meta = b->h_meta;
+    meta.push_back(sentinel);
+    SKM_HIP(hipMemcpyAsync(b->d_meta.p, meta.data(), sizeof(SeqMeta) * meta.size(), hipMemcpyHostToDevice, b->stream));
+    const uint64_t nblk = (rp >> 6) + 1;
+    b->d_blk2seq.ensure(sizeof(uint32_t) * nblk);
+    SKM_HIP(hipMemsetAsync(b->d_blk2seq.p, 0, sizeof(uint32_t) * nblk, b->stream));
+    if (b->nseq)
+        hipLaunchKernelGGL(k_blk2seq, dim3((b->nseq + 255) / 256), dim3(256), 0, b->stream, b->d_meta.as<SeqMeta>(), b->nseq,
+                           b->d_blk2seq.as<uint32_t>(), nblk);
+    SKM_HIP(hipGetLastError());
+    // work buffers
+    const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
+    uint64_t step = (uint64_t)EX_THREADS * EX_POS_PER_THREAD;
+    uint64_t nwg = std::max<uint64_t>(1, std::min<uint64_t>(EX_MAX_WG, ceil_div(rp ? rp : 1, step)));
+    b->span = ceil_div(ceil_div(rp ? rp : 1, nwg), step) * step;
+    b->nwg = (uint32_t)ceil_div(rp ? rp : 1, b->span);
+    const uint32_t nrb = (uint32_t)ceil_div(b->nwg, SCAN_ROWS);
+    b->d_hist.ensure(sizeof(uint32_t) * (uint64_t)b->nwg * NB);
+    b->d_offs.ensure(sizeof(uint32_t) * (uint64_t)b->nwg * NB);
+    b->d_partial.ensure(sizeof(uint32_t) * (uint64_t)nrb * NB);
+    b->d_rbbase.ensure(sizeof(uint32_t) * (uint64_t)nrb * NB);
+    b->d_bstart32.ensure(sizeof(uint32_t) * (NB + 1));
+    b->d_bstart.ensure(sizeof(uint64_t) * (NB + 1));
+    b->d_owner_start.ensure(sizeof(uint64_t) * 16);
+    const uint64_t W = b->n_windows;
+    b->d_recs.ensure(8 * std::max<uint64_t>(W, 1));
+    b->d_tmp.ensure(8 * std::max<uint64_t>(W, 1));
+    b->d_keys.ensure(8 * std::max<uint64_t>(W, 1));
+    b->d_data.ensure(sizeof(skm_stored_kmer_data) * std::max<uint64_t>(W, 1) + 16);
+    b->d_ctr.ensure(64);
+    b->d_flags.ensure(std::max<uint64_t>(b->nseq, 1));
+    b->d_dfunc.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
+    b->d_swf.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
+    b->ovf_cap = W / CAP + NB + 16;
+    b->d_ovf.ensure(sizeof(OvfEntry) * b->ovf_cap);
+    SKM_HIP(hipStreamSynchronize(b->stream));
+    b->prepared = true;
+    b->ran = false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int skm_build_create(skm_build** out, const int* devices, int n_devices, const skm_build_opts* opts) {
+    SKM_API_BEGIN
+    SKM_CHECK(out && opts, SKM_E_ARG, "null argument");
+    SKM_CHECK(opts->k == 8, SKM_E_ARG, "only k = 8 is supported (kmers-build-signatures.cc:17)");
+    SKM_CHECK(opts->n_functions < 0xFFFFu, SKM_E_ARG, "n_functions must be < 65535");
+    SKM_CHECK(n_devices == 1, SKM_E_ARG, "one device per process (multi-GPU: one process per GPU)");
+    SKM_CHECK(opts->world_size == 1 || opts->world_size == 0, SKM_E_ARG, "world_size > 1 requires skm_build_set_comm");
+    int ndev = 0;
+    SKM_HIP(hipGetDeviceCount(&ndev));
+    SKM_CHECK(ndev > 0, SKM_E_HIP, "no HIP device");
+    auto* b = new skm_build();
+    b->opts = *opts;
+    b->device = devices ? devices[0] : 0;
+    SKM_HIP(hipSetDevice(b->device));
+    SKM_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    for (auto& e : b->ev) SKM_HIP(hipEventCreate(&e));
+    *out = b;
+    SKM_API_END
+}
+
+int skm_build_add_batch(skm_build* b, const uint8_t* residues, const uint64_t* seq_off, const uint32_t* seq_len,
+                        const uint16_t* seq_func, const uint32_t* seq_id, size_t n_seqs) {
+    SKM_API_BEGIN
+    SKM_CHECK(b, SKM_E_ARG, "null build");
+    SKM_CHECK(n_seqs == 0 || (residues && seq_off && seq_len && seq_func), SKM_E_ARG, "null array");
+    for (size_t s = 0; s < n_seqs; ++s) {
+        const uint16_t f = seq_func[s];
+        if (f == SKM_UNDEFINED_FUNCTION) continue;  // signature_build.tcc:155-158
+        SKM_CHECK(f < b->opts.n_functions, SKM_E_ARG, "seq_func out of range");
+        const uint32_t len = seq_len[s];
+        SKM_CHECK(len < (1u << ELEM_I_BITS), SKM_E_ARG, "protein longer than 1,048,575 residues");
+        SeqMeta m;
+        m.pstart = b->h_res.size();
+        m.len = len;
+        m.func = f;
+        m.pad = 0;
+        b->h_res.insert(b->h_res.end(), residues + seq_off[s], residues + seq_off[s] + len);
+        b->h_res.push_back(0);
+        const uint32_t sid = seq_id ? seq_id[s] : (uint32_t)b->h_meta.size();
+        if (!b->h_seqid.empty() && sid <= b->h_seqid.back()) b->seqid_strict = false;
+        b->h_meta.push_back(m);
+        b->h_seqid.push_back(sid);
+        if (len >= 8) b->n_windows += len - 7;
+    }
+    b->prepared = false;
+    b->ran = false;
+    SKM_API_END
+}
+
+int skm_build_prepare(skm_build* b) {
+    SKM_API_BEGIN
+    SKM_CHECK(b, SKM_E_ARG, "null build");
+    prepare(b);
+    SKM_API_END
+}
+
+int skm_build_run(skm_build* b) {
+    SKM_API_BEGIN
+    SKM_CHECK(b, SKM_E_ARG, "null build");
+    SKM_HIP(hipSetDevice(b->device));
+    prepare(b);
+    run_pipeline(b);
+    SKM_API_END
+}
+
+int skm_build_last_timings(skm_build* b, float* ms, int cap) {
+    if (!b || !ms) return SKM_E_ARG;
+    int n = std::min(cap, 7);
+    for (int i = 0; i < n; ++i) ms[i] = b->last_ms[i];
+    return n;
+}
+
+int skm_build_finish(skm_build* b, skm_kept* out) {
+    SKM_API_BEGIN
+    SKM_CHECK(b && out, SKM_E_ARG, "null argument");
+    SKM_HIP(hipSetDevice(b->device));
+    prepare(b);
+    if (!b->ran) run_pipeline(b);
+    std::memset(out, 0, sizeof(*out));
+    const uint64_t n = b->n_kept;
+    const uint32_t F = b->opts.n_functions;
+    std::vector<uint64_t> keys(n);
+    std::vector<skm_stored_kmer_data> data(n);
+    unsigned long long ctr[3];
+    if (n) {
+        SKM_HIP(hipMemcpyAsync(keys.data(), b->d_keys.p, 8 * n, hipMemcpyDeviceToHost, b->stream));
+        SKM_HIP(hipMemcpyAsync(data.data(), b->d_data.p, sizeof(skm_stored_kmer_data) * n, hipMemcpyDeviceToHost, b->stream));
+    }
+    out->distinct_functions = (uint32_t*)std::malloc(sizeof(uint32_t) * std::max<uint32_t>(F, 1));
+    out->seqs_with_func = (uint32_t*)std::malloc(sizeof(uint32_t) * std::max<uint32_t>(F, 1));
+    SKM_CHECK(out->distinct_functions && out->seqs_with_func, SKM_E_OOM, "host allocation failed");
+    if (F) {
+        SKM_HIP(hipMemcpyAsync(out->distinct_functions, b->d_dfunc.p, sizeof(uint32_t) * F, hipMemcpyDeviceToHost, b->stream));
+        SKM_HIP(hipMemcpyAsync(out->seqs_with_func, b->d_swf.p, sizeof(uint32_t) * F, hipMemcpyDeviceToHost, b->stream));
+    }
+    SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, sizeof(ctr), hipMemcpyDeviceToHost, b->stream));
+    std::vector<uint8_t> flags;
+    if (!b->seqid_strict) {
+        flags.resize(b->nseq);
+        if (b->nseq) SKM_HIP(hipMemcpyAsync(flags.data(), b->d_flags.p, b->nseq, hipMemcpyDeviceToHost, b->stream));
+    }
+    SKM_HIP(hipStreamSynchronize(b->stream));
+    // deterministic output order: sort by key
+    std::vector<uint64_t> perm(n);
+    std::iota(perm.begin(), perm.end(), 0);
+    std::sort(perm.begin(), perm.end(), [&](uint64_t x, uint64_t y) { return keys[x] < keys[y]; });
+    out->keys = (uint64_t*)std::malloc(8 * std::max<uint64_t>(n, 1));
+    out->data = (skm_stored_kmer_data*)std::malloc(sizeof(skm_stored_kmer_data) * std::max<uint64_t>(n, 1));
+    SKM_CHECK(out->keys && out->data, SKM_E_OOM, "host allocation failed");
+    for (uint64_t i = 0; i < n; ++i) {
+        out->keys[i] = keys[perm[i]];
+        out->data[i] = data[perm[i]];
+    }
+    out->n = n;
+    out->n_functions = F;
+    out->distinct_signatures = n;
+    if (b->seqid_strict) {
+        out->n_seqs_with_signature = ctr[2];
+    } else {  // colliding seq ids (files with > max_seqs_per_file sequences): count distinct ids
+        std::vector<uint32_t> ids;
+        for (uint32_t s = 0; s < b->nseq; ++s)
+            if (flags[s]) ids.push_back(b->h_seqid[s]);
+        std::sort(ids.begin(), ids.end());
+        out->n_seqs_with_signature = (uint64_t)(std::unique(ids.begin(), ids.end()) - ids.begin());
+    }
+    out->n_windows = b->n_windows;
+    out->n_records = 0;
+    SKM_API_END
+}
+
+void skm_kept_free(skm_kept* k) {
+    if (!k) return;
+    std::free(k->keys);
+    std::free(k->data);
+    std::free(k->distinct_functions);
+    std::free(k->seqs_with_func);
+    std::memset(k, 0, sizeof(*k));
+}
+
+void skm_build_destroy(skm_build* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->device);
+    if (b->stream) (void)hipStreamSynchronize(b->stream);
+    for (auto& e : b->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (b->stream) (void)hipStreamDestroy(b->stream);
+    delete b;
+}
+
+}  // extern "C"

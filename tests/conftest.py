@@ -1,0 +1,31 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+TESTS = os.path.dirname(os.path.abspath(__file__))
+if TESTS not in sys.path:
+    sys.path.insert(0, TESTS)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; run with -m gpu")
+    config.addinivalue_line("markers", "slow: larger CPU cases")
+
+
+@pytest.fixture(scope="session")
+def skm():
+    import signature_kmers_amd as skm_mod
+    skm_mod.lib()
+    return skm_mod
+
+
+@pytest.fixture(scope="session")
+def gpu(skm):
+    n = skm.device_count()
+    if n < 1:
+        pytest.fail("gpu test selected but no HIP device is visible")
+    return 0

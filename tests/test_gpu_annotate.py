@@ -1,0 +1,84 @@
+"""GPU parity: HBM-resident CMPH/BDZ lookup and the HitSet call path vs the CPU oracle."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ref
+from signature_kmers_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def make_db(skm, tmp_path, n_seqs=3000, fam=60, seed=21):
+    p = synth.generate_arrays(n_seqs, fam, per_file=500, seed=seed)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    ref = oracle_ref.build(r, o, l, f, i, len(funcs))
+    mph = str(tmp_path / "kmer_data.mph")
+    dat = str(tmp_path / "kmer_data.dat")
+    skm.mph_build(ref["keys"], ref["data"], mph, dat, seed=7)
+    return ref, funcs, mph, dat, p
+
+
+def test_lookup_members_and_strangers(skm, gpu, tmp_path):
+    ref, funcs, mph, dat, _ = make_db(skm, tmp_path)
+    db = skm.CmphKmerDb(str(tmp_path / "kmer_data"))
+    m = db.hash_size()
+    assert m == len(ref["keys"])
+    idx = db.lookup_keys(ref["keys"])
+    assert np.array_equal(np.sort(idx), np.arange(m, dtype=np.uint32))  # minimal perfect
+    ob = oracle_ref.Bdz(open(mph, "rb").read())
+    np.testing.assert_array_equal(idx, ob.search(ref["keys"]))
+    rng = np.random.default_rng(3)
+    strangers = rng.integers(0, 2**63, size=200000, dtype=np.uint64)
+    np.testing.assert_array_equal(db.lookup_keys(strangers), ob.search(strangers))
+    # the .dat slot of each member holds its record
+    d = np.frombuffer(open(dat, "rb").read(), dtype=skm.STORED_DTYPE)
+    np.testing.assert_array_equal(d[idx], ref["data"])
+
+
+@pytest.mark.parametrize("ignore_hypo", [0, 1])
+def test_calls_match_oracle(skm, gpu, tmp_path, ignore_hypo):
+    ref, funcs, mph, dat, _ = make_db(skm, tmp_path)
+    db = skm.CmphKmerDb(str(tmp_path / "kmer_data"))
+    caller = skm.FunctionCaller(db, funcs)
+    caller.ignore_hypothetical(bool(ignore_hypo))
+    q = synth.generate_arrays(4000, 60, per_file=500, seed=99, extras=True)  # fresh queries
+    off, calls = caller.process_seqs(q.residues, q.seq_off, q.seq_len)
+    ob = oracle_ref.Bdz(open(mph, "rb").read())
+    ooff, ocalls = oracle_ref.annotate(ob, open(dat, "rb").read(), q.residues, q.seq_off, q.seq_len,
+                                       ignore_hypo=ignore_hypo, hypo_index=funcs.index("hypothetical protein"))
+    np.testing.assert_array_equal(off, ooff)
+    assert len(calls) == len(ocalls) and len(calls) > 100
+    for f in ("start", "end", "count", "function_index", "protein_length_median"):
+        np.testing.assert_array_equal(calls[f], ocalls[f], err_msg=f)
+    np.testing.assert_array_equal(calls["protein_length_med_avg_dev"].view(np.uint32),
+                                  ocalls["protein_length_med_avg_dev"].view(np.uint32))
+    # host find_best_call (product) == oracle find_best_call
+    n_called = 0
+    for s in range(len(q.seq_len)):
+        c = calls[off[s]:off[s + 1]]
+        a = caller.find_best_call(c)
+        b = oracle_ref.find_best_call(c, funcs)
+        assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2], (s, a, b)
+        n_called += a[0] != 0xFFFF
+    assert n_called > len(q.seq_len) // 2
+
+
+def test_query_edge_cases(skm, gpu, tmp_path):
+    ref, funcs, mph, dat, p = make_db(skm, tmp_path, n_seqs=1500, fam=30, seed=5)
+    db = skm.CmphKmerDb(str(tmp_path / "kmer_data"))
+    caller = skm.FunctionCaller(db, funcs)
+    src = p.residues[p.seq_off[0]:p.seq_off[0] + p.seq_len[0]].tobytes()
+    seqs = [b"", b"ACDEFGH", b"ACDEFGHI", b"ACDEFGHIX", b"XACDEFGHI", src, src[:50] + b"X" + src[50:],
+            src[:40] + b"*" + src[41:], src.lower(), src * 3, b"X" * 20]
+    lens = np.array([len(s) for s in seqs], np.uint32)
+    off = np.zeros(len(seqs), np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    res = np.frombuffer(b"".join(seqs), np.uint8)
+    goff, gcalls = caller.process_seqs(res, off, lens)
+    ob = oracle_ref.Bdz(open(mph, "rb").read())
+    ooff, ocalls = oracle_ref.annotate(ob, open(dat, "rb").read(), res, off, lens,
+                                       hypo_index=funcs.index("hypothetical protein"))
+    np.testing.assert_array_equal(goff, ooff)
+    np.testing.assert_array_equal(gcalls.view(np.uint8), ocalls.view(np.uint8))

@@ -1,0 +1,158 @@
+"""GPU parity: HIP signature build (libskm via the C-ABI) vs the CPU oracle restatement.
+
+Bit-exact comparison of the kept k-mer set, every StoredKmerData field, distinct_functions,
+seqs_with_func, num_seqs_with_a_signature and distinct_signatures on seeded inputs."""
+import numpy as np
+import pytest
+
+import oracle_ref
+from signature_kmers_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def run_both(skm, residues, seq_off, seq_len, seq_func, seq_id, nf):
+    b = skm.SignatureBuilder(nf)
+    b.add_batch(residues, seq_off, seq_len, seq_func, seq_id)
+    got = b.finish()
+    b.close()
+    ref = oracle_ref.build(residues, seq_off, seq_len, seq_func, seq_id, nf)
+    return got, ref
+
+
+def assert_same(got, ref):
+    assert len(got.keys) == len(ref["keys"]), (len(got.keys), len(ref["keys"]))
+    np.testing.assert_array_equal(got.keys, ref["keys"])
+    for f in ("avg_from_end", "function_index", "mean", "median", "var"):
+        bad = np.nonzero(got.data[f] != ref["data"][f])[0]
+        assert len(bad) == 0, (f, len(bad), got.data[bad[:5]], ref["data"][bad[:5]],
+                               [skm_kmer(k) for k in got.keys[bad[:5]]])
+    np.testing.assert_array_equal(got.distinct_functions, ref["distinct_functions"])
+    np.testing.assert_array_equal(got.seqs_with_func, ref["seqs_with_func"])
+    assert got.n_seqs_with_signature == ref["n_seqs_with_signature"]
+    assert got.distinct_signatures == ref["distinct_signatures"]
+
+
+def skm_kmer(k):
+    return int(k).to_bytes(8, "little")
+
+
+def pack(seqs):
+    lens = np.array([len(s) for s in seqs], np.uint32)
+    off = np.zeros(len(seqs), np.uint64)
+    if len(seqs):
+        off[1:] = np.cumsum(lens[:-1])
+    res = np.frombuffer(b"".join(seqs), np.uint8) if seqs else np.zeros(0, np.uint8)
+    return res, off, lens
+
+
+def test_config1_synthetic(skm, gpu):
+    p = synth.generate_arrays(1000, 40, per_file=100, extras=True)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    got, ref = run_both(skm, r, o, l, f, i, len(funcs))
+    assert len(got.keys) > 1000
+    assert_same(got, ref)
+
+
+@pytest.mark.parametrize("n,fam,seed", [(5000, 100, 1), (20000, 400, 2)])
+def test_synthetic_sizes(skm, gpu, n, fam, seed):
+    p = synth.generate_arrays(n, fam, per_file=1000, seed=seed)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    got, ref = run_both(skm, r, o, l, f, i, len(funcs))
+    assert_same(got, ref)
+
+
+def test_level2_partition_and_overflow(skm, gpu):
+    # 60K sequences from 60 families: level-1 buckets exceed LDS capacity (level-2 partition),
+    # conserved k-mers of the largest families exceed a sub-bucket (global-memory overflow path)
+    p = synth.generate_arrays(60000, 60, per_file=2000, seed=3)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    got, ref = run_both(skm, r, o, l, f, i, len(funcs))
+    assert_same(got, ref)
+
+
+def test_edge_cases(skm, gpu):
+    seqs = [
+        b"",                       # empty
+        b"ACDEFGH",                # 7 residues: no window
+        b"ACDEFGHI",               # exactly one window
+        b"ACDEFGHIXKLMNPQRST",     # X splits windows
+        b"acdefghiklmnpqrstvwy",   # lower case is valid for the build
+        b"ACDEFGHIBZUJOACDEFGHI",  # B/Z/U/J/O are not in ok_prot_
+        b"ACDEFGHI*",              # '*' invalid
+        b"WWWWWWWWWWWWWWWWWWWWWWWW",  # self-overlapping repeats
+    ]
+    res, off, lens = pack(seqs)
+    func = np.array([0, 1, 2, 3, 4, 5, 0xFFFF, 2], np.uint16)
+    sid = np.arange(len(seqs), dtype=np.uint32)
+    got, ref = run_both(skm, res, off, lens, func, sid, 8)
+    assert_same(got, ref)
+
+
+def test_empty_input(skm, gpu):
+    res, off, lens = pack([])
+    got, ref = run_both(skm, res, off, lens, np.zeros(0, np.uint16), np.zeros(0, np.uint32), 4)
+    assert len(got.keys) == 0 and got.distinct_signatures == 0
+    assert_same(got, ref)
+
+
+def test_cut_ties_and_heavy_groups(skm, gpu):
+    rng = np.random.default_rng(5)
+    core = bytes(rng.choice(np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8), 40))
+    seqs, funcs = [], []
+    # 4 copies func 3, 1 copy func 1  -> count 5, best 4 >= 4.0 -> kept with func 3
+    # 5 copies func 2, 5 copies func 0 -> tie -> lowest index 0, 5 < 8 -> cut
+    # 9000 copies func 1 (varying lengths) -> heavy group beyond LDS capacity
+    for _ in range(4):
+        seqs.append(b"MK" + core)
+        funcs.append(3)
+    seqs.append(b"MK" + core + b"G")
+    funcs.append(1)
+    tie = bytes(rng.choice(np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8), 30))
+    for j in range(10):
+        seqs.append(tie + b"A" * j)
+        funcs.append(2 if j < 5 else 0)
+    heavy = bytes(rng.choice(np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8), 25))
+    for j in range(9000):
+        pad = bytes(rng.choice(np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8), int(rng.integers(0, 300))))
+        seqs.append(pad + heavy + pad[::-1])
+        funcs.append(1 if j % 10 else 4)
+    res, off, lens = pack(seqs)
+    func = np.array(funcs, np.uint16)
+    sid = np.arange(len(seqs), dtype=np.uint32)
+    got, ref = run_both(skm, res, off, lens, func, sid, 6)
+    assert_same(got, ref)
+
+
+def test_u16_wrap_long_protein(skm, gpu):
+    # protein longer than 65535: offsets wrap (signature_build.tcc:164), sums wrap in the mean
+    rng = np.random.default_rng(9)
+    aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+    long = bytes(rng.choice(aa, 70000))
+    seqs = [long, long[:30000], long[1000:1400]] + [long[5000:5300]] * 300
+    res, off, lens = pack(seqs)
+    func = np.zeros(len(seqs), np.uint16)
+    sid = np.arange(len(seqs), dtype=np.uint32)
+    got, ref = run_both(skm, res, off, lens, func, sid, 2)
+    assert_same(got, ref)
+
+
+def test_colliding_seq_ids(skm, gpu):
+    p = synth.generate_arrays(3000, 30, per_file=1000, seed=11)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    i = (i % 700).astype(np.uint32)  # many sequences share ids (files with > max_seqs_per_file)
+    got, ref = run_both(skm, r, o, l, f, i, len(funcs))
+    assert_same(got, ref)
+
+
+def test_rerun_is_idempotent(skm, gpu):
+    p = synth.generate_arrays(2000, 50, per_file=500, seed=4)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    b = skm.SignatureBuilder(len(funcs))
+    b.add_batch(r, o, l, f, i)
+    b.run()
+    a = b.finish()
+    b.run()
+    c = b.finish()
+    np.testing.assert_array_equal(a.keys, c.keys)
+    np.testing.assert_array_equal(a.data, c.data)
