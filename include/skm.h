@@ -109,7 +109,7 @@ int skm_build_prepare(skm_build* b);
 /* Run the device pipeline over the resident input; results stay on the device. */
 int skm_build_run(skm_build* b);
 /* Device time (ms) of the last run's phases: [0]=extract-count [1]=scan [2]=extract-scatter
- * [3]=bucket-process [4]=overflow [5]=stats [6]=total; returns number of entries written. */
+ * [3]=bucket-process [4]=overflow [5]=chains [6]=stats [7]=total; returns entries written. */
 int skm_build_last_timings(skm_build* b, float* ms, int cap);
 /* Run (if not yet run since the last prepare) and download the result. */
 int skm_build_finish(skm_build* b, skm_kept* out);

@@ -196,7 +196,7 @@ class SignatureBuilder:
     def timings(self) -> dict:
         ms = (C.c_float * 8)()
         n = lib().skm_build_last_timings(self._h, ms, 8)
-        names = ["extract_count", "scan", "extract_scatter", "bucket_process", "overflow", "stats", "total"]
+        names = ["extract_count", "scan", "extract_scatter", "bucket_process", "overflow", "chains", "stats", "total"]
         return {names[i]: float(ms[i]) for i in range(n)}
 
     def finish(self) -> KeptKmers:

@@ -43,11 +43,12 @@ constexpr int EX_THREADS = 512;        // extract workgroup
 constexpr int EX_POS_PER_THREAD = 16;  // windows per thread per step (one 16-byte load + halo)
 constexpr int EX_MAX_WG = 512;         // rows of the histogram matrix
 constexpr int SCAN_ROWS = 32;          // rows per column-scan block
-constexpr int BP_THREADS = 512;        // bucket-process workgroup
-constexpr int CAP = 4096;              // LDS sub-bucket capacity (16-byte elements)
-constexpr int SUB_TARGET = 1024;       // target records per level-2 sub-bucket
+constexpr int BP_THREADS = 1024;       // bucket-process workgroup (one per CU: LDS ~150 KB)
+constexpr int CAP = 4096;              // LDS sub-bucket capacity (records)
+constexpr int TAB_BITS = 13;
+constexpr int TAB = 1 << TAB_BITS;     // LDS hash slots per sub-bucket (load <= 0.5)
+constexpr int SUB_TARGET = 2048;       // target records per level-2 sub-bucket
 constexpr int MAX_B2 = 12;             // <= 4096 sub-buckets per level-1 bucket
-constexpr int SMALL_GROUP = 48;        // O(c^2) offset selection below this size
 
 struct SeqMeta {        // 16 bytes, one dwordx4 load
     uint64_t pstart;    // first residue in the packed buffer
@@ -98,19 +99,21 @@ struct SigStats {
         const double x = (double)sample;
         // ---- p_square_quantile ----
         if (cnt <= 5) {
-            h[cnt - 1] = x;
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+                if ((uint32_t)i == cnt - 1) h[i] = x;
             if (cnt == 5) {  // std::sort of 5 values (result is the unique sorted order)
-                for (int i = 1; i < 5; ++i) {
-                    double v = h[i];
-                    int j = i - 1;
-                    while (j >= 0 && h[j] > v) {
-                        h[j + 1] = h[j];
-                        --j;
+#pragma unroll
+                for (int i = 0; i < 5; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4 - i; ++j) {  // bubble network: same sorted values as std::sort
+                        const double a = h[j], b = h[j + 1];
+                        h[j] = a > b ? b : a;
+                        h[j + 1] = a > b ? a : b;
                     }
-                    h[j + 1] = v;
-                }
             }
         } else {
+            // cell k with heights[k-1] <= x < heights[k] (std::upper_bound), extremes adjusted
             int cell;
             if (x < h[0]) {
                 h[0] = x;
@@ -119,27 +122,24 @@ struct SigStats {
                 h[4] = x;
                 cell = 4;
             } else {
-                cell = 1;
-                while (cell < 5 && !(x < h[cell])) ++cell;  // std::upper_bound
+                cell = x < h[1] ? 1 : (x < h[2] ? 2 : (x < h[3] ? 3 : 4));
             }
-            for (int i = cell; i < 5; ++i) act[i] += 1;
+#pragma unroll
+            for (int i = 1; i < 5; ++i)
+                if (i >= cell) act[i] += 1;
             // desired positions accumulate exact multiples of 1/4: closed form is bit-identical
             const double nstep = (double)(cnt - 5);
-            double des[5];
-            des[0] = 1.0;
-            des[1] = 2.0 + nstep * 0.25;
-            des[2] = 3.0 + nstep * 0.5;
-            des[3] = 4.0 + nstep * 0.75;
-            des[4] = 5.0 + nstep;
+            const double des[4] = {0.0, 2.0 + nstep * 0.25, 3.0 + nstep * 0.5, 4.0 + nstep * 0.75};
+#pragma unroll
             for (int i = 1; i <= 3; ++i) {
-                double d = des[i] - (double)act[i];
-                double dp = (double)act[i + 1] - (double)act[i];
-                double dm = (double)act[i - 1] - (double)act[i];
+                const double d = des[i] - (double)act[i];
+                const double dp = (double)act[i + 1] - (double)act[i];
+                const double dm = (double)act[i - 1] - (double)act[i];
                 if ((d >= 1. && dp > 1.) || (d <= -1. && dm < -1.)) {
-                    double hp = (h[i + 1] - h[i]) / dp;
-                    double hm = (h[i - 1] - h[i]) / dm;
-                    short sign_d = static_cast<short>(d / fabs(d));
-                    double hh = h[i] + sign_d / (dp - dm) * ((sign_d - dm) * hp + (dp - sign_d) * hm);
+                    const double hp = (h[i + 1] - h[i]) / dp;
+                    const double hm = (h[i - 1] - h[i]) / dm;
+                    const short sign_d = static_cast<short>(d / fabs(d));
+                    const double hh = h[i] + sign_d / (dp - dm) * ((sign_d - dm) * hp + (dp - sign_d) * hm);
                     if (h[i - 1] < hh && hh < h[i + 1]) {
                         h[i] = hh;
                     } else {
@@ -158,97 +158,6 @@ struct SigStats {
         }
     }
 };
-
-// k-th smallest (0-based) of the low 16 bits of lo[a..b)
-__device__ uint32_t select_offset(const uint64_t* lo, uint32_t a, uint32_t b, uint32_t k) {
-    const uint32_t c = b - a;
-    if (c <= (uint32_t)SMALL_GROUP) {
-        for (uint32_t j = a; j < b; ++j) {
-            uint32_t v = (uint32_t)(lo[j] & 0xFFFFu);
-            uint32_t lt = 0, le = 0;
-            for (uint32_t t = a; t < b; ++t) {
-                uint32_t w = (uint32_t)(lo[t] & 0xFFFFu);
-                lt += w < v;
-                le += w <= v;
-            }
-            if (lt <= k && k < le) return v;
-        }
-        return 0;  // unreachable
-    }
-    uint32_t vmin = 0xFFFFu, vmax = 0;
-    for (uint32_t j = a; j < b; ++j) {
-        uint32_t v = (uint32_t)(lo[j] & 0xFFFFu);
-        vmin = min(vmin, v);
-        vmax = max(vmax, v);
-    }
-    while (vmin < vmax) {
-        uint32_t mid = (vmin + vmax) >> 1;
-        uint32_t cnt = 0;
-        for (uint32_t j = a; j < b; ++j) cnt += (uint32_t)(lo[j] & 0xFFFFu) <= mid;
-        if (cnt >= k + 1)
-            vmax = mid;
-        else
-            vmin = mid + 1;
-    }
-    return vmin;
-}
-
-// Process one group [a,b) of elements sorted by (rem, func, ordinal).  hi = rem<<16|func,
-// lo = s<<36 | i<<16 | offset16.  If kept, the head element is overwritten with the kept
-// record: hi = 1<<63 | h43<<16 | avg_from_end, lo = func | mean<<16 | median<<32 | var<<48.
-// (process_kmer_set, signature_build.tcc:219-293)
-__device__ void process_group(uint64_t* hi, uint64_t* lo, uint32_t a, uint32_t b, uint64_t hprefix,
-                              const SeqMeta* __restrict__ meta, uint8_t* __restrict__ flags) {
-    const uint32_t c = b - a;
-    // best function: iterate func runs in ascending FunctionIndex (std::map order); replace only
-    // on strictly greater count -> ties go to the lowest index.
-    uint32_t best_f = 0xFFFFu, best_c = 0, rb = a, re = a;
-    bool have = false;
-    uint32_t run_f = (uint32_t)(hi[a] & 0xFFFFu), run_s = a;
-    for (uint32_t j = a + 1; j <= b; ++j) {
-        uint32_t f = j < b ? (uint32_t)(hi[j] & 0xFFFFu) : 0x10000u;
-        if (f != run_f) {
-            uint32_t len = j - run_s;
-            if (!have || len > best_c) {
-                have = true;
-                best_f = run_f;
-                best_c = len;
-                rb = run_s;
-                re = j;
-            }
-            run_f = f;
-            run_s = j;
-        }
-    }
-    const float thresh = float(c) * 0.8f;
-    if ((float)best_c < thresh) return;
-
-    // avg_from_end: sorted(offsets)[size/2] over ALL occurrences
-    const uint32_t avg = select_offset(lo, a, b, c / 2);
-    // seqs_with_a_signature: every occurrence's sequence
-    for (uint32_t j = a; j < b; ++j) flags[lo[j] >> 36] = 1;
-    // accumulator over protein lengths of best-function occurrences, reverse ordinal order
-    SigStats st;
-    st.init();
-    uint32_t j = re;
-    while (j > rb) {
-        uint32_t lens[8];
-        uint32_t nb = min(8u, j - rb);
-#pragma unroll
-        for (uint32_t t = 0; t < 8; ++t)
-            if (t < nb) lens[t] = meta[lo[j - 1 - t] >> 36].len;
-#pragma unroll
-        for (uint32_t t = 0; t < 8; ++t)
-            if (t < nb) st.add(lens[t]);
-        j -= nb;
-    }
-    const uint16_t mean = d2u16((double)st.sum / (double)st.cnt);
-    const uint16_t median = d2u16(st.h[2]);
-    const uint16_t var = d2u16(st.var);
-    const uint64_t h43 = hprefix | (hi[a] >> 16);
-    hi[a] = (1ull << 63) | (h43 << 16) | avg;
-    lo[a] = (uint64_t)best_f | ((uint64_t)mean << 16) | ((uint64_t)median << 32) | ((uint64_t)var << 48);
-}
 
 __device__ __forceinline__ void make_elem(uint64_t rec, int pos_bits, uint64_t pos_mask, uint64_t pos_base,
                                           const uint32_t* __restrict__ blk2seq, const SeqMeta* __restrict__ meta,
@@ -322,63 +231,260 @@ __device__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t& to
     return r;
 }
 
-// Find groups in sorted hi/lo[0..n), process them, compact kept records to the output.
-__device__ void process_sorted(uint64_t* hi, uint64_t* lo, uint32_t n, uint64_t hprefix, const SeqMeta* meta,
-                               uint8_t* flags, uint16_t* s_heads, uint32_t* s_wave,
-                               unsigned long long* kept_ctr, uint64_t* out_keys, skm_stored_kmer_data* out_data) {
-    // group heads -> compact list (ordered)
-    uint32_t base = 0;
-    for (uint32_t c0 = 0; c0 < n; c0 += blockDim.x) {
-        uint32_t j = c0 + threadIdx.x;
-        bool head = j < n && (j == 0 || (hi[j] >> 16) != (hi[j - 1] >> 16));
-        uint32_t tot;
-        uint32_t pos = wg_exclusive_scan(head ? 1u : 0u, s_wave, tot);
-        if (head) s_heads[base + pos] = (uint16_t)j;
-        base += tot;
+// ------------------------------------------------------------------------------------------
+// Group processing (process_kmer_set, signature_build.tcc:219-293).
+//
+// A group is the set of occurrences of one k-mer.  Groups arrive sorted by (func, ordinal), so
+// function runs are contiguous in ascending FunctionIndex (the std::map order of func_count)
+// and the best-function run is in ascending ordinal order.  Order-dependent statistics (P^2
+// median, running variance) need the run in REVERSE ordinal order; when the run has >= 3
+// members they are deferred to k_chains (one thread per chain), everything else is done here.
+// ------------------------------------------------------------------------------------------
+constexpr int SMALLC = 16;   // thread-level groups up to this size, wave-level above
+
+struct Job {                 // one deferred P^2 / variance chain
+    uint64_t lens_off;       // protein lengths in visit order (reverse ordinal) at lens[lens_off..]
+    uint32_t n;
+    uint32_t out_idx;        // kept-k-mer output slot receiving median / var
+};
+
+struct GRes {
+    uint32_t best_f, avg, cbest, rb;   // rb: first element of the best run (group-relative)
+    uint16_t mean, median, var;
+    bool kept;
+};
+
+// Sorted multi-occurrence array in LDS: key = rep<<16 | func, element index -> lo
+struct LdsView {
+    const uint32_t* mkey;
+    const uint16_t* midx;
+    const uint64_t* lo;
+    __device__ __forceinline__ uint32_t func(uint32_t j) const { return mkey[j] & 0xFFFFu; }
+    __device__ __forceinline__ uint64_t lov(uint32_t j) const { return lo[midx[j]]; }
+};
+
+// Sorted 16-byte elements in global memory (overflow path): hi = rem<<16|func
+struct GlbView {
+    const uint64_t* hi;
+    const uint64_t* lo;
+    __device__ __forceinline__ uint32_t func(uint64_t j) const { return (uint32_t)(hi[j] & 0xFFFFu); }
+    __device__ __forceinline__ uint64_t lov(uint64_t j) const { return lo[j]; }
+};
+
+template <int N>
+__device__ __forceinline__ void reg_sort(uint32_t* v) {
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const bool asc = (i & k) == 0;
+                    const uint32_t a = v[i], b = v[l];
+                    v[i] = asc ? min(a, b) : max(a, b);
+                    v[l] = asc ? max(a, b) : min(a, b);
+                }
+            }
+}
+
+__device__ __forceinline__ void stats_small(GRes& r, const uint32_t* lens_rev, uint32_t n) {
+    // n <= 2 samples in visit order: P^2 heights[2] is still 0; the variance recurrence of SigStats
+    // after two samples is 0*(1)/2 + (x2 - mean2)^2 / 1 with mean2 over the u16 sum.
+    r.median = 0;
+    r.var = 0;
+    if (n == 2) {
+        const uint16_t sum = (uint16_t)(lens_rev[0] + lens_rev[1]);
+        const double mean = (double)sum / 2.0;
+        const double tmp = (double)lens_rev[1] - mean;
+        const double v = 0.0 * 1.0 / 2.0 + tmp * tmp / 1.0;
+        r.var = d2u16(v);
     }
-    __syncthreads();
-    const uint32_t ngroups = base;
-    for (uint32_t g = threadIdx.x; g < ngroups; g += blockDim.x) {
-        uint32_t a = s_heads[g];
-        uint32_t b = g + 1 < ngroups ? s_heads[g + 1] : n;
-        process_group(hi, lo, a, b, hprefix, meta, flags);
-    }
-    __syncthreads();
-    // compaction of kept heads
-    uint32_t kbase_local = 0;
-    uint64_t gbase = 0;
-    for (uint32_t g0 = 0; g0 < ngroups; g0 += blockDim.x) {
-        uint32_t g = g0 + threadIdx.x;
-        uint32_t a = g < ngroups ? s_heads[g] : 0;
-        bool kept = g < ngroups && (hi[a] >> 63);
-        uint32_t tot;
-        uint32_t pos = wg_exclusive_scan(kept ? 1u : 0u, s_wave, tot);
-        if (tot == 0) continue;
-        if (threadIdx.x == 0) s_wave[32] = (uint32_t)0;
-        if (threadIdx.x == 0) {
-            unsigned long long gb = atomicAdd(kept_ctr, (unsigned long long)tot);
-            reinterpret_cast<unsigned long long*>(s_wave)[17] = gb;
+}
+
+// Thread-level group of c <= N members starting at a.
+template <int N, class V>
+__device__ GRes group_thread(const V& v, uint64_t a, uint32_t c, const SeqMeta* __restrict__ meta,
+                             uint8_t* __restrict__ flags) {
+    GRes r;
+    r.kept = false;
+    uint32_t fn[N], of[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+        if ((uint32_t)t < c) {
+            fn[t] = v.func(a + t);
+            of[t] = (uint32_t)(v.lov(a + t) & 0xFFFFu);
+        } else {
+            fn[t] = 0x10000u;
+            of[t] = 0x10000u;  // sorts after every real offset
         }
-        __syncthreads();
-        gbase = reinterpret_cast<unsigned long long*>(s_wave)[17];
-        if (kept) {
-            uint64_t H = hi[a], L = lo[a];
-            uint64_t h43 = (H >> 16) & KEY_MASK;
-            uint64_t raw = decode_key(unmix43(h43));
-            uint64_t o = gbase + pos;
-            out_keys[o] = raw;
-            skm_stored_kmer_data d;
-            d.avg_from_end = (uint16_t)(H & 0xFFFFu);
-            d.function_index = (uint16_t)(L & 0xFFFFu);
-            d.mean = (uint16_t)(L >> 16);
-            d.median = (uint16_t)(L >> 32);
-            d.var = (uint16_t)(L >> 48);
-            out_data[o] = d;
-        }
-        __syncthreads();
-        kbase_local += tot;
     }
-    (void)kbase_local;
+    uint32_t best_f = fn[0], best_c = 0, rb = 0, run_s = 0;
+#pragma unroll
+    for (int t = 1; t <= N; ++t) {
+        if ((uint32_t)t <= c) {
+            const bool end = ((uint32_t)t == c) || fn[t < N ? t : N - 1] != fn[t - 1];
+            if (end) {
+                const uint32_t len = t - run_s;
+                if (len > best_c) {
+                    best_c = len;
+                    best_f = fn[t - 1];
+                    rb = run_s;
+                }
+                run_s = t;
+            }
+        }
+    }
+    if ((float)best_c < float(c) * 0.8f) return r;
+    r.kept = true;
+    r.best_f = best_f;
+    r.cbest = best_c;
+    r.rb = rb;
+    reg_sort<N>(of);
+    const uint32_t k = c / 2;
+    uint32_t avg = 0;
+#pragma unroll
+    for (int t = 0; t < N; ++t)
+        if ((uint32_t)t == k) avg = of[t];
+    r.avg = avg;
+    uint32_t sum = 0;
+    uint32_t lr0 = 0, lr1 = 0;
+    for (uint32_t t = 0; t < c; ++t) {
+        const uint64_t lo = v.lov(a + t);
+        const uint32_t s = (uint32_t)(lo >> 36);
+        flags[s] = 1;
+        if (t >= rb && t < rb + best_c) {
+            const uint32_t len = meta[s].len;
+            sum += len;
+            const uint32_t q = rb + best_c - 1 - t;  // visit position (reverse ordinal)
+            if (q == 0) lr0 = len;
+            if (q == 1) lr1 = len;
+        }
+    }
+    r.mean = d2u16((double)(uint16_t)sum / (double)best_c);
+    r.median = 0;
+    r.var = 0;
+    if (best_c <= 2) {
+        const uint32_t lr[2] = {lr0, lr1};
+        stats_small(r, lr, best_c);
+    }
+    return r;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_min(uint32_t x) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x = min(x, (uint32_t)__shfl_xor(x, d, 64));
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x = max(x, (uint32_t)__shfl_xor(x, d, 64));
+    return x;
+}
+
+// Wave-level group (all 64 lanes, same a/c).  Only used for c > SMALLC, so the best run always
+// has >= 3 members and its median/var are deferred.
+template <class V>
+__device__ GRes group_wave(const V& v, uint64_t a, uint32_t c, const SeqMeta* __restrict__ meta,
+                           uint8_t* __restrict__ flags) {
+    const uint32_t lane = threadIdx.x & 63u;
+    GRes r;
+    r.kept = false;
+    uint32_t best_f = 0, best_c = 0, rb = 0, run_s = 0;
+    uint32_t run_f = v.func(a);
+    for (uint32_t base = 0; base < c; base += 64) {
+        const uint32_t t = base + lane;
+        const bool valid = t < c;
+        const uint32_t f = valid ? v.func(a + t) : 0xFFFFFFFFu;
+        const uint32_t fp = (valid && t > 0) ? v.func(a + t - 1) : 0xFFFFFFFFu;
+        uint64_t m = __ballot(valid && t > 0 && f != fp);
+        while (m) {
+            const int q = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const uint32_t pos = base + (uint32_t)q;
+            const uint32_t len = pos - run_s;
+            if (len > best_c) {
+                best_c = len;
+                best_f = run_f;
+                rb = run_s;
+            }
+            run_s = pos;
+            run_f = (uint32_t)__shfl((int)f, q, 64);
+        }
+    }
+    {
+        const uint32_t len = c - run_s;
+        if (len > best_c) {
+            best_c = len;
+            best_f = run_f;
+            rb = run_s;
+        }
+    }
+    if ((float)best_c < float(c) * 0.8f) return r;
+    r.kept = true;
+    r.best_f = best_f;
+    r.cbest = best_c;
+    r.rb = rb;
+    // avg_from_end: k-th smallest offset by binary search over the value range
+    uint32_t vmin = 0xFFFFu, vmax = 0;
+    for (uint32_t t = lane; t < c; t += 64) {
+        const uint32_t o = (uint32_t)(v.lov(a + t) & 0xFFFFu);
+        vmin = min(vmin, o);
+        vmax = max(vmax, o);
+    }
+    vmin = wave_min(vmin);
+    vmax = wave_max(vmax);
+    const uint32_t k = c / 2;
+    while (vmin < vmax) {
+        const uint32_t mid = (vmin + vmax) >> 1;
+        uint32_t cnt = 0;
+        for (uint32_t t = lane; t < c; t += 64) cnt += (uint32_t)(v.lov(a + t) & 0xFFFFu) <= mid;
+        cnt = wave_sum(cnt);
+        if (cnt >= k + 1)
+            vmax = mid;
+        else
+            vmin = mid + 1;
+    }
+    r.avg = vmin;
+    uint32_t sum = 0;
+    for (uint32_t t = lane; t < c; t += 64) {
+        const uint32_t s = (uint32_t)(v.lov(a + t) >> 36);
+        flags[s] = 1;
+        if (t >= rb && t < rb + best_c) sum += meta[s].len;
+    }
+    sum = wave_sum(sum);
+    r.mean = d2u16((double)(uint16_t)sum / (double)best_c);
+    r.median = 0;
+    r.var = 0;
+    return r;
+}
+
+// P^2 median + variance chains, one thread per job (visit order = lens order).
+__global__ void k_chains(const Job* __restrict__ jobs, uint64_t njobs, const uint32_t* __restrict__ lens,
+                         skm_stored_kmer_data* __restrict__ out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= njobs) return;
+    const Job jb = jobs[j];
+    const uint32_t* x = lens + jb.lens_off;
+    SigStats st;
+    st.init();
+    uint32_t t = 0;
+    for (; t + 4 <= jb.n; t += 4) {
+        const uint4 q = make_uint4(x[t], x[t + 1], x[t + 2], x[t + 3]);
+        st.add(q.x);
+        st.add(q.y);
+        st.add(q.z);
+        st.add(q.w);
+    }
+    for (; t < jb.n; ++t) st.add(x[t]);
+    out[jb.out_idx].median = d2u16(st.h[2]);
+    out[jb.out_idx].var = d2u16(st.var);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -529,7 +635,7 @@ __global__ void k_coloffs(const uint32_t* __restrict__ hist, const uint32_t* __r
 }
 
 struct BucketArgs {
-    const uint64_t* recs;      // records of this owner, bucket-major (level-1)
+    const uint64_t* recs;      // records of this owner, level-1 bucket-major
     uint64_t* tmp;             // level-2 partition scratch, same indexing as recs
     const uint64_t* bstart;    // [nbuckets+1] absolute starts in recs
     uint32_t nbuckets;
@@ -539,20 +645,250 @@ struct BucketArgs {
     const uint32_t* blk2seq;
     const SeqMeta* meta;
     uint8_t* flags;
-    unsigned long long* kept_ctr;
+    unsigned long long* ctr;   // [0] kept [1] overflow entries [2] flagged seqs [3] jobs [4] lens
     uint64_t* out_keys;
     skm_stored_kmer_data* out_data;
+    Job* jobs;
+    uint32_t* lens;
     OvfEntry* ovf;
-    unsigned int* ovf_ctr;
     uint32_t ovf_cap;
 };
+
+struct SubLds {
+    uint64_t* hi;      // [CAP] element: rem<<16|func   (kept: 1<<63 | h43<<16 | avg)
+    uint64_t* lo;      // [CAP] element: s<<36|i<<16|off (kept, no job: func|mean|median|var)
+    uint32_t* tab;     // [TAB] hash slot: rep<<16 | count; later jobinfo[CAP] + func|mean[CAP]
+    uint16_t* slot;    // [CAP] record -> slot; later group heads
+    uint32_t* mkey;    // [CAP] sorted multi records: rep<<16 | func
+    uint16_t* midx;    // [CAP] sorted multi records: element index
+    uint16_t* big;     // [CAP/2] wave-level group list
+    uint32_t* wave;    // scan scratch (>= 40 words, 16-byte aligned)
+    uint32_t* nbig;
+};
+
+__device__ __forceinline__ uint64_t kept_hi(uint64_t h43, uint32_t avg) { return (1ull << 63) | (h43 << 16) | avg; }
+__device__ __forceinline__ uint64_t kept_lo(uint32_t f, uint32_t mean, uint32_t med, uint32_t var) {
+    return (uint64_t)f | ((uint64_t)mean << 16) | ((uint64_t)med << 32) | ((uint64_t)var << 48);
+}
+
+__device__ __forceinline__ void write_kept(const BucketArgs& A, uint64_t o, uint64_t H, uint64_t L) {
+    A.out_keys[o] = decode_key(unmix43((H >> 16) & KEY_MASK));
+    skm_stored_kmer_data d;
+    d.avg_from_end = (uint16_t)(H & 0xFFFFu);
+    d.function_index = (uint16_t)(L & 0xFFFFu);
+    d.mean = (uint16_t)(L >> 16);
+    d.median = (uint16_t)(L >> 32);
+    d.var = (uint16_t)(L >> 48);
+    A.out_data[o] = d;
+}
+
+// One sub-bucket of n <= CAP records: LDS hash grouping, singletons immediately, multi-occurrence
+// groups sorted by (group, func, ordinal) and processed by threads (small) or waves (large).
+__device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const BucketArgs& A, uint64_t hprefix,
+                            uint64_t pos_mask, const SubLds& L) {
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t EMPTY = 0xFFFFFFFFu;
+    // 1. load + resolve each record to (sequence, window, function, offset)
+    for (uint32_t j = tid; j < n; j += nt)
+        make_elem(src[j], A.pos_bits, pos_mask, A.pos_base, A.blk2seq, A.meta, L.hi[j], L.lo[j]);
+    for (uint32_t t = tid; t < (uint32_t)TAB; t += nt) L.tab[t] = EMPTY;
+    if (tid == 0) *L.nbig = 0;
+    __syncthreads();
+    // 2. hash insert: slot value = representative element << 16 | occurrence count
+    for (uint32_t j = tid; j < n; j += nt) {
+        const uint32_t rem = (uint32_t)(L.hi[j] >> 16);
+        uint32_t slot = (rem * 0x9E3779B1u) >> (32 - TAB_BITS);
+        while (true) {
+            const uint32_t cur = atomicCAS(&L.tab[slot], EMPTY, (j << 16) | 1u);
+            if (cur == EMPTY) break;
+            if ((uint32_t)(L.hi[cur >> 16] >> 16) == rem) {
+                atomicAdd(&L.tab[slot], 1u);
+                break;
+            }
+            slot = (slot + 1) & (TAB - 1);
+        }
+        L.slot[j] = (uint16_t)slot;
+    }
+    __syncthreads();
+    // 3. singletons resolved in place; multi-occurrence records compacted
+    uint32_t M = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += nt) {
+        const uint32_t j = c0 + tid;
+        const bool in = j < n;
+        const uint32_t e = in ? L.tab[L.slot[j]] : 0u;
+        const bool multi = in && (e & 0xFFFFu) > 1u;
+        uint32_t tot;
+        const uint32_t pos = wg_exclusive_scan(multi ? 1u : 0u, L.wave, tot);
+        if (multi) {
+            L.midx[M + pos] = (uint16_t)j;
+            L.mkey[M + pos] = (e & 0xFFFF0000u) | (uint32_t)(L.hi[j] & 0xFFFFu);
+        } else if (in) {  // group of one: always kept (1 >= 0.8), median 0, var 0
+            const uint64_t H = L.hi[j], Lo = L.lo[j];
+            const uint32_t s = (uint32_t)(Lo >> 36);
+            const uint32_t len = A.meta[s].len;
+            A.flags[s] = 1;
+            L.hi[j] = kept_hi(hprefix | (H >> 16), (uint32_t)(Lo & 0xFFFFu));
+            L.lo[j] = kept_lo((uint32_t)(H & 0xFFFFu), d2u16((double)(uint16_t)len / 1.0), 0, 0);
+        }
+        M += tot;
+    }
+    __syncthreads();
+    uint32_t* jobinfo = L.tab;        // per representative: best-run start << 16 | best count
+    uint32_t* fmean = L.tab + CAP;    // per representative: func | mean << 16
+    for (uint32_t j = tid; j < n; j += nt) jobinfo[j] = 0;
+    uint32_t NP = 1;
+    while (NP < M) NP <<= 1;
+    for (uint32_t t = M + tid; t < NP; t += nt) {
+        L.mkey[t] = 0xFFFFFFFFu;
+        L.midx[t] = 0;
+    }
+    __syncthreads();
+    // 4. bitonic sort of the multi records by (representative, func, ordinal)
+    if (M > 1) {
+        for (uint32_t k = 2; k <= NP; k <<= 1) {
+            for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+                for (uint32_t t = tid; t < NP / 2; t += nt) {
+                    const uint32_t i = 2 * t - (t & (jj - 1));
+                    const uint32_t l = i + jj;
+                    const bool asc = (i & k) == 0;
+                    const uint32_t ka = L.mkey[i], kb = L.mkey[l];
+                    const uint16_t ia = L.midx[i], ib = L.midx[l];
+                    const bool gt = ka > kb || (ka == kb && L.lo[ia] > L.lo[ib]);
+                    if (gt == asc) {
+                        L.mkey[i] = kb;
+                        L.mkey[l] = ka;
+                        L.midx[i] = ib;
+                        L.midx[l] = ia;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+    // 5. group heads of the sorted multi records
+    uint16_t* heads = L.slot;
+    uint32_t G = 0;
+    for (uint32_t c0 = 0; c0 < M; c0 += nt) {
+        const uint32_t t = c0 + tid;
+        const bool head = t < M && (t == 0 || (L.mkey[t] >> 16) != (L.mkey[t - 1] >> 16));
+        uint32_t tot;
+        const uint32_t pos = wg_exclusive_scan(head ? 1u : 0u, L.wave, tot);
+        if (head) heads[G + pos] = (uint16_t)t;
+        G += tot;
+    }
+    __syncthreads();
+    const LdsView V{L.mkey, L.midx, L.lo};
+    auto stage = [&](const GRes& r, uint32_t a) {
+        if (!r.kept) return;
+        const uint32_t rep = L.mkey[a] >> 16;
+        const uint64_t h43 = hprefix | (L.hi[rep] >> 16);
+        L.hi[rep] = kept_hi(h43, r.avg);
+        if (r.cbest >= 3) {
+            jobinfo[rep] = ((a + r.rb) << 16) | r.cbest;
+            fmean[rep] = r.best_f | ((uint32_t)r.mean << 16);
+        } else {
+            L.lo[rep] = kept_lo(r.best_f, r.mean, r.median, r.var);
+        }
+    };
+    // 6. thread-level groups; large ones queued for waves
+    for (uint32_t g = tid; g < G; g += nt) {
+        const uint32_t a = heads[g];
+        const uint32_t b = g + 1 < G ? heads[g + 1] : M;
+        const uint32_t c = b - a;
+        if (c > (uint32_t)SMALLC) {
+            const uint32_t bi = atomicAdd(L.nbig, 1u);
+            L.big[bi] = (uint16_t)g;
+            continue;
+        }
+        GRes r;
+        if (c <= 4)
+            r = group_thread<4>(V, a, c, A.meta, A.flags);
+        else if (c <= 8)
+            r = group_thread<8>(V, a, c, A.meta, A.flags);
+        else
+            r = group_thread<16>(V, a, c, A.meta, A.flags);
+        stage(r, a);
+    }
+    __syncthreads();
+    // 7. wave-level groups
+    {
+        const uint32_t nbig = *L.nbig;
+        const uint32_t wave = tid >> 6, nwaves = nt >> 6;
+        for (uint32_t bi = wave; bi < nbig; bi += nwaves) {
+            const uint32_t g = L.big[bi];
+            const uint32_t a = heads[g];
+            const uint32_t b = g + 1 < G ? heads[g + 1] : M;
+            const GRes r = group_wave(V, a, b - a, A.meta, A.flags);
+            if ((tid & 63u) == 0) stage(r, a);
+        }
+    }
+    __syncthreads();
+    // 8. emit kept k-mers (one atomic per chunk) and chain jobs with their protein lengths
+    unsigned long long* s_base = reinterpret_cast<unsigned long long*>(L.wave + 36);
+    for (uint32_t c0 = 0; c0 < n; c0 += nt) {
+        const uint32_t j = c0 + tid;
+        const uint64_t H = j < n ? L.hi[j] : 0;
+        const bool kept = (H >> 63) != 0;
+        const uint32_t jb = kept ? jobinfo[j] : 0u;
+        const uint32_t jn = jb & 0xFFFFu;
+        uint32_t K, JL;
+        const uint32_t kpos = wg_exclusive_scan(kept ? 1u : 0u, L.wave, K);
+        const uint32_t jl = wg_exclusive_scan(jn ? ((jn << 11) | 1u) : 0u, L.wave, JL);
+        if (K == 0) continue;
+        if (tid == 0) {
+            s_base[0] = atomicAdd(&A.ctr[0], (unsigned long long)K);
+            if (JL) {
+                s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)(JL & 0x7FFu));
+                s_base[2] = atomicAdd(&A.ctr[4], (unsigned long long)(JL >> 11));
+            }
+        }
+        __syncthreads();
+        if (kept) {
+            const uint64_t o = s_base[0] + kpos;
+            if (jn) {
+                const uint32_t fm = fmean[j];
+                write_kept(A, o, H, kept_lo(fm & 0xFFFFu, fm >> 16, 0, 0));
+                const uint64_t loff = s_base[2] + (jl >> 11);
+                Job jbr;
+                jbr.lens_off = loff;
+                jbr.n = jn;
+                jbr.out_idx = (uint32_t)o;
+                A.jobs[s_base[1] + (jl & 0x7FFu)] = jbr;
+                const uint32_t start = jb >> 16;
+                for (uint32_t t = 0; t < jn; ++t) {
+                    const uint32_t e = start + jn - 1 - t;  // reverse ordinal order
+                    A.lens[loff + t] = A.meta[L.lo[L.midx[e]] >> 36].len;
+                }
+            } else {
+                write_kept(A, o, H, L.lo[j]);
+            }
+        }
+        __syncthreads();
+    }
+}
 
 __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
     __shared__ uint64_t s_hi[CAP];
     __shared__ uint64_t s_lo[CAP];
+    __shared__ uint32_t s_tab[TAB];
+    __shared__ uint16_t s_slot[CAP];
+    __shared__ uint32_t s_mkey[CAP];
+    __shared__ uint16_t s_midx[CAP];
     __shared__ uint32_t s_sub[(1 << MAX_B2) + 1];
-    __shared__ uint16_t s_heads[CAP];
-    __shared__ uint32_t s_wave[40];
+    __shared__ uint16_t s_big[CAP / 2];
+    __shared__ __align__(16) uint32_t s_wave[48];
+    __shared__ uint32_t s_nbig;
+    SubLds L;
+    L.hi = s_hi;
+    L.lo = s_lo;
+    L.tab = s_tab;
+    L.slot = s_slot;
+    L.mkey = s_mkey;
+    L.midx = s_midx;
+    L.big = s_big;
+    L.wave = s_wave;
+    L.nbig = &s_nbig;
+
     const uint32_t bucket = blockIdx.x;
     if (bucket >= A.nbuckets) return;
     const uint64_t r0 = A.bstart[bucket], r1 = A.bstart[bucket + 1];
@@ -561,38 +897,8 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
     const uint64_t pos_mask = (A.pos_bits >= 64) ? ~0ull : ((1ull << A.pos_bits) - 1);
     const uint64_t hprefix = (uint64_t)(A.bucket_base + bucket) << A.rem_bits;
 
-    auto load_and_process = [&](const uint64_t* src, uint32_t cnt) {
-        uint32_t N = 1;
-        while (N < cnt) N <<= 1;
-        for (uint32_t j = threadIdx.x; j < N; j += blockDim.x) {
-            if (j < cnt) {
-                make_elem(src[j], A.pos_bits, pos_mask, A.pos_base, A.blk2seq, A.meta, s_hi[j], s_lo[j]);
-            } else {
-                s_hi[j] = ~0ull;
-                s_lo[j] = ~0ull;
-            }
-        }
-        __syncthreads();
-        bitonic_lds(s_hi, s_lo, N, 2, N, N, 0);
-        process_sorted(s_hi, s_lo, cnt, hprefix, A.meta, A.flags, s_heads, s_wave, A.kept_ctr, A.out_keys, A.out_data);
-        __syncthreads();
-    };
-    auto push_overflow = [&](uint64_t off, uint32_t cnt, uint32_t src) {
-        unsigned int e = atomicAdd(A.ovf_ctr, 1u);
-        if (e < A.ovf_cap) {
-            OvfEntry en;
-            en.off = off;
-            en.n = cnt;
-            en.bucket = bucket;
-            en.scratch = 0;
-            en.npad = 0;
-            en.src = src;
-            A.ovf[e] = en;
-        }
-    };
-
     if (n <= (uint64_t)CAP) {
-        load_and_process(A.recs + r0, (uint32_t)n);
+        process_sub(A.recs + r0, (uint32_t)n, A, hprefix, pos_mask, L);
         return;
     }
     // ---- level-2 partition by the next b2 bits of rem ----
@@ -603,12 +909,10 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
     for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_sub[d] = 0;
     __syncthreads();
     for (uint64_t j = threadIdx.x; j < n; j += blockDim.x) {
-        uint64_t rec = A.recs[r0 + j];
-        uint32_t d = (uint32_t)((rec >> A.pos_bits) >> shift);
-        atomicAdd(&s_sub[d], 1u);
+        const uint64_t rec = A.recs[r0 + j];
+        atomicAdd(&s_sub[(uint32_t)((rec >> A.pos_bits) >> shift)], 1u);
     }
     __syncthreads();
-    // exclusive scan of s_sub[0..nsub) (each thread a contiguous chunk)
     {
         const uint32_t per = (nsub + blockDim.x - 1) / blockDim.x;
         const uint32_t d0 = threadIdx.x * per;
@@ -617,7 +921,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
         uint32_t tot;
         uint32_t run = wg_exclusive_scan(local, s_wave, tot);
         for (uint32_t d = d0; d < min(nsub, d0 + per); ++d) {
-            uint32_t t = s_sub[d];
+            const uint32_t t = s_sub[d];
             s_sub[d] = run;
             run += t;
         }
@@ -625,14 +929,12 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
         if (threadIdx.x == 0) s_sub[nsub] = tot;
         __syncthreads();
     }
-    // scatter into tmp using s_heads area as per-sub cursors is too small; use s_hi as cursors
     uint32_t* s_cur = reinterpret_cast<uint32_t*>(s_hi);
     for (uint32_t d = threadIdx.x; d < nsub; d += blockDim.x) s_cur[d] = s_sub[d];
     __syncthreads();
     for (uint64_t j = threadIdx.x; j < n; j += blockDim.x) {
-        uint64_t rec = A.recs[r0 + j];
-        uint32_t d = (uint32_t)((rec >> A.pos_bits) >> shift);
-        uint32_t o = atomicAdd(&s_cur[d], 1u);
+        const uint64_t rec = A.recs[r0 + j];
+        const uint32_t o = atomicAdd(&s_cur[(uint32_t)((rec >> A.pos_bits) >> shift)], 1u);
         A.tmp[r0 + o] = rec;
     }
     __threadfence_block();
@@ -642,100 +944,55 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
         const uint32_t cnt = e - a;
         if (cnt == 0) continue;
         if (cnt <= (uint32_t)CAP) {
-            load_and_process(A.tmp + r0 + a, cnt);
+            process_sub(A.tmp + r0 + a, cnt, A, hprefix, pos_mask, L);
+            __syncthreads();
         } else if (threadIdx.x == 0) {
-            push_overflow(r0 + a, cnt, 1);
+            const unsigned int en = atomicAdd(reinterpret_cast<unsigned int*>(&A.ctr[1]), 1u);
+            if (en < A.ovf_cap) {
+                OvfEntry o;
+                o.off = r0 + a;
+                o.n = cnt;
+                o.bucket = bucket;
+                o.scratch = 0;
+                o.npad = 0;
+                o.src = 1;
+                A.ovf[en] = o;
+            }
         }
     }
 }
 
-struct OvfArgs {
-    const OvfEntry* ovf;
-    const uint64_t* recs;
-    const uint64_t* tmp;
-    uint64_t* s_hi_g;   // scratch elements
-    uint64_t* s_lo_g;
-    uint32_t bucket_base;
-    int rem_bits, pos_bits;
-    uint64_t pos_base;
-    const uint32_t* blk2seq;
-    const SeqMeta* meta;
-    uint8_t* flags;
-    unsigned long long* kept_ctr;
-    uint64_t* out_keys;
-    skm_stored_kmer_data* out_data;
-    uint32_t* heads_g;  // scratch group heads (u32), same indexing as elements
+struct OvfScratch {
+    uint64_t* hi;       // sorted elements
+    uint64_t* lo;
+    uint32_t* heads;    // group heads
+    uint64_t* jobinfo;  // per head: best-run start << 32 | best count
+    uint32_t* fmean;    // per head: func | mean << 16
 };
 
-// Groups of a sorted global array (the overflow form of process_sorted).
-__device__ void process_sorted_global(uint64_t* hi, uint64_t* lo, uint32_t n, uint64_t hprefix, const SeqMeta* meta,
-                                      uint8_t* flags, uint32_t* heads, uint32_t* s_wave,
-                                      unsigned long long* kept_ctr, uint64_t* out_keys, skm_stored_kmer_data* out_data) {
-    uint32_t base = 0;
-    for (uint32_t c0 = 0; c0 < n; c0 += blockDim.x) {
-        uint32_t j = c0 + threadIdx.x;
-        bool head = j < n && (j == 0 || (hi[j] >> 16) != (hi[j - 1] >> 16));
-        uint32_t tot;
-        uint32_t pos = wg_exclusive_scan(head ? 1u : 0u, s_wave, tot);
-        if (head) heads[base + pos] = j;
-        base += tot;
-    }
-    __threadfence_block();
-    __syncthreads();
-    const uint32_t ngroups = base;
-    for (uint32_t g = threadIdx.x; g < ngroups; g += blockDim.x) {
-        uint32_t a = heads[g];
-        uint32_t b = g + 1 < ngroups ? heads[g + 1] : n;
-        process_group(hi, lo, a, b, hprefix, meta, flags);
-    }
-    __threadfence_block();
-    __syncthreads();
-    for (uint32_t g0 = 0; g0 < ngroups; g0 += blockDim.x) {
-        uint32_t g = g0 + threadIdx.x;
-        uint32_t a = g < ngroups ? heads[g] : 0;
-        bool kept = g < ngroups && (hi[a] >> 63);
-        uint32_t tot;
-        uint32_t pos = wg_exclusive_scan(kept ? 1u : 0u, s_wave, tot);
-        if (tot == 0) continue;
-        if (threadIdx.x == 0) {
-            unsigned long long gb = atomicAdd(kept_ctr, (unsigned long long)tot);
-            reinterpret_cast<unsigned long long*>(s_wave)[17] = gb;
-        }
-        __syncthreads();
-        uint64_t gbase = reinterpret_cast<unsigned long long*>(s_wave)[17];
-        if (kept) {
-            uint64_t H = hi[a], L = lo[a];
-            uint64_t raw = decode_key(unmix43((H >> 16) & KEY_MASK));
-            uint64_t o = gbase + pos;
-            out_keys[o] = raw;
-            skm_stored_kmer_data d;
-            d.avg_from_end = (uint16_t)(H & 0xFFFFu);
-            d.function_index = (uint16_t)(L & 0xFFFFu);
-            d.mean = (uint16_t)(L >> 16);
-            d.median = (uint16_t)(L >> 32);
-            d.var = (uint16_t)(L >> 48);
-            out_data[o] = d;
-        }
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(BP_THREADS) void k_overflow(OvfArgs A) {
+// Overflow sub-buckets (n > CAP): global-memory bitonic sort (LDS for strides < CAP), then the
+// same group processing on the global arrays.
+__global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratch S) {
     __shared__ uint64_t s_hi[CAP];
     __shared__ uint64_t s_lo[CAP];
-    __shared__ uint32_t s_wave[40];
+    __shared__ __align__(16) uint32_t s_wave[48];
+    __shared__ uint32_t s_nbig;
+    __shared__ uint32_t s_big[BP_THREADS];
     const OvfEntry e = A.ovf[blockIdx.x];
     const uint64_t* src = (e.src ? A.tmp : A.recs) + e.off;
-    uint64_t* ghi = A.s_hi_g + e.scratch;
-    uint64_t* glo = A.s_lo_g + e.scratch;
-    uint32_t* heads = A.heads_g + e.scratch;
+    uint64_t* ghi = S.hi + e.scratch;
+    uint64_t* glo = S.lo + e.scratch;
+    uint32_t* heads = S.heads + e.scratch;
+    uint64_t* jobinfo = S.jobinfo + e.scratch;
+    uint32_t* fmean = S.fmean + e.scratch;
     const uint32_t N = e.npad, n = e.n;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint64_t pos_mask = (A.pos_bits >= 64) ? ~0ull : ((1ull << A.pos_bits) - 1);
     const uint64_t hprefix = (uint64_t)(A.bucket_base + e.bucket) << A.rem_bits;
-    // phase 0: chunks of CAP sorted in LDS (directions from global index)
+    // phase 0: chunks of CAP sorted in LDS (directions from the global index)
     for (uint32_t c0 = 0; c0 < N; c0 += CAP) {
-        for (uint32_t j = threadIdx.x; j < CAP; j += blockDim.x) {
-            uint32_t g = c0 + j;
+        for (uint32_t j = tid; j < CAP; j += nt) {
+            const uint32_t g = c0 + j;
             if (g < n) {
                 make_elem(src[g], A.pos_bits, pos_mask, A.pos_base, A.blk2seq, A.meta, s_hi[j], s_lo[j]);
             } else {
@@ -745,23 +1002,21 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(OvfArgs A) {
         }
         __syncthreads();
         bitonic_lds(s_hi, s_lo, CAP, 2, CAP, CAP, c0);
-        for (uint32_t j = threadIdx.x; j < CAP; j += blockDim.x) {
+        for (uint32_t j = tid; j < CAP; j += nt) {
             ghi[c0 + j] = s_hi[j];
             glo[c0 + j] = s_lo[j];
         }
         __threadfence_block();
         __syncthreads();
     }
-    // merge stages k > CAP: strides >= CAP in global memory, then strides < CAP per chunk in LDS
     for (uint32_t k = 2 * CAP; k <= N; k <<= 1) {
         for (uint32_t j = k >> 1; j >= (uint32_t)CAP; j >>= 1) {
-            for (uint32_t t = threadIdx.x; t < N / 2; t += blockDim.x) {
-                uint32_t i = 2 * t - (t & (j - 1));
-                uint32_t l = i + j;
-                bool asc = ((i & k) == 0);
-                uint64_t ah = ghi[i], al = glo[i], bh = ghi[l], bl = glo[l];
-                bool gt = elem_less(bh, bl, ah, al);
-                if (gt == asc) {
+            for (uint32_t t = tid; t < N / 2; t += nt) {
+                const uint32_t i = 2 * t - (t & (j - 1));
+                const uint32_t l = i + j;
+                const bool asc = ((i & k) == 0);
+                const uint64_t ah = ghi[i], al = glo[i], bh = ghi[l], bl = glo[l];
+                if (elem_less(bh, bl, ah, al) == asc) {
                     ghi[i] = bh;
                     glo[i] = bl;
                     ghi[l] = ah;
@@ -772,13 +1027,13 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(OvfArgs A) {
             __syncthreads();
         }
         for (uint32_t c0 = 0; c0 < N; c0 += CAP) {
-            for (uint32_t j = threadIdx.x; j < CAP; j += blockDim.x) {
+            for (uint32_t j = tid; j < CAP; j += nt) {
                 s_hi[j] = ghi[c0 + j];
                 s_lo[j] = glo[c0 + j];
             }
             __syncthreads();
             bitonic_lds(s_hi, s_lo, CAP, k, k, CAP >> 1, c0);
-            for (uint32_t j = threadIdx.x; j < CAP; j += blockDim.x) {
+            for (uint32_t j = tid; j < CAP; j += nt) {
                 ghi[c0 + j] = s_hi[j];
                 glo[c0 + j] = s_lo[j];
             }
@@ -786,7 +1041,126 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(OvfArgs A) {
             __syncthreads();
         }
     }
-    process_sorted_global(ghi, glo, n, hprefix, A.meta, A.flags, heads, s_wave, A.kept_ctr, A.out_keys, A.out_data);
+    // group heads
+    uint32_t G = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += nt) {
+        const uint32_t t = c0 + tid;
+        const bool head = t < n && (t == 0 || (ghi[t] >> 16) != (ghi[t - 1] >> 16));
+        uint32_t tot;
+        const uint32_t pos = wg_exclusive_scan(head ? 1u : 0u, s_wave, tot);
+        if (head) {
+            heads[G + pos] = t;
+            jobinfo[t] = 0;
+        }
+        G += tot;
+    }
+    __threadfence_block();
+    __syncthreads();
+    const GlbView V{ghi, glo};
+    auto stage = [&](const GRes& r, uint32_t a) {
+        if (!r.kept) return;
+        const uint64_t h43 = hprefix | (ghi[a] >> 16);
+        if (r.cbest >= 3) {
+            jobinfo[a] = ((uint64_t)(a + r.rb) << 32) | r.cbest;
+            fmean[a] = r.best_f | ((uint32_t)r.mean << 16);
+        } else {
+            glo[a] = kept_lo(r.best_f, r.mean, r.median, r.var);
+        }
+        ghi[a] = kept_hi(h43, r.avg);
+    };
+    for (uint32_t g0 = 0; g0 < G; g0 += nt) {
+        if (tid == 0) s_nbig = 0;
+        __syncthreads();
+        const uint32_t g = g0 + tid;
+        if (g < G) {
+            const uint32_t a = heads[g];
+            const uint32_t b = g + 1 < G ? heads[g + 1] : n;
+            const uint32_t c = b - a;
+            if (c > (uint32_t)SMALLC) {
+                s_big[atomicAdd(&s_nbig, 1u)] = g;
+            } else {
+                GRes r;
+                if (c <= 4)
+                    r = group_thread<4>(V, a, c, A.meta, A.flags);
+                else if (c <= 8)
+                    r = group_thread<8>(V, a, c, A.meta, A.flags);
+                else
+                    r = group_thread<16>(V, a, c, A.meta, A.flags);
+                stage(r, a);
+            }
+        }
+        __syncthreads();
+        const uint32_t nbig = s_nbig;
+        for (uint32_t bi = tid >> 6; bi < nbig; bi += nt >> 6) {
+            const uint32_t gg = s_big[bi];
+            const uint32_t a = heads[gg];
+            const uint32_t b = gg + 1 < G ? heads[gg + 1] : n;
+            const GRes r = group_wave(V, a, b - a, A.meta, A.flags);
+            if ((tid & 63u) == 0) stage(r, a);
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    // emit over groups
+    unsigned long long* s_base = reinterpret_cast<unsigned long long*>(s_wave + 36);
+    for (uint32_t g0 = 0; g0 < G; g0 += nt) {
+        const uint32_t g = g0 + tid;
+        const uint32_t a = g < G ? heads[g] : 0u;
+        const uint64_t H = g < G ? ghi[a] : 0ull;
+        const bool kept = (H >> 63) != 0;
+        const uint64_t jb = kept ? jobinfo[a] : 0ull;
+        const uint32_t jn = (uint32_t)(jb & 0xFFFFFFFFu);
+        uint32_t K, J, Lt;
+        const uint32_t kpos = wg_exclusive_scan(kept ? 1u : 0u, s_wave, K);
+        const uint32_t jpos = wg_exclusive_scan(jn ? 1u : 0u, s_wave, J);
+        const uint32_t lpos = wg_exclusive_scan(jn, s_wave, Lt);
+        if (K == 0) continue;
+        if (tid == 0) {
+            s_base[0] = atomicAdd(&A.ctr[0], (unsigned long long)K);
+            if (J) {
+                s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)J);
+                s_base[2] = atomicAdd(&A.ctr[4], (unsigned long long)Lt);
+            }
+            s_nbig = 0;
+        }
+        __syncthreads();
+        if (kept) {
+            const uint64_t o = s_base[0] + kpos;
+            if (jn) {
+                const uint32_t fm = fmean[a];
+                write_kept(A, o, H, kept_lo(fm & 0xFFFFu, fm >> 16, 0, 0));
+                Job jbr;
+                jbr.lens_off = s_base[2] + lpos;
+                jbr.n = jn;
+                jbr.out_idx = (uint32_t)o;
+                A.jobs[s_base[1] + jpos] = jbr;
+                if (jn <= 64) {
+                    const uint64_t start = jb >> 32;
+                    for (uint32_t t = 0; t < jn; ++t)
+                        A.lens[jbr.lens_off + t] = A.meta[glo[start + jn - 1 - t] >> 36].len;
+                } else {
+                    const uint32_t bi = atomicAdd(&s_nbig, 1u);
+                    s_big[bi] = g;
+                    s_lo[bi] = jbr.lens_off;
+                }
+            } else {
+                write_kept(A, o, H, glo[a]);
+            }
+        }
+        __syncthreads();
+        // long chains: the whole workgroup writes their lengths
+        const uint32_t nb = s_nbig;
+        for (uint32_t q = 0; q < nb; ++q) {
+            const uint32_t gg = s_big[q];
+            const uint32_t aa = heads[gg];
+            const uint64_t jbq = jobinfo[aa];
+            const uint32_t nq = (uint32_t)(jbq & 0xFFFFFFFFu);
+            const uint64_t start = jbq >> 32;
+            const uint64_t loff = s_lo[q];
+            for (uint32_t t = tid; t < nq; t += nt) A.lens[loff + t] = A.meta[glo[start + nq - 1 - t] >> 36].len;
+        }
+        __syncthreads();
+    }
 }
 
 // distinct_functions[f] += kept k-mers with best function f (LDS privatised when it fits)
@@ -852,8 +1226,8 @@ struct skm_build {
     skm_build_opts opts{};
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[8] = {};
-    float last_ms[8] = {};
+    hipEvent_t ev[9] = {};
+    float last_ms[9] = {};
 
     // host staging (reference emission order, only sequences with a kept function)
     std::vector<uint8_t> h_res;     // packed residues with one 0 separator after each sequence
@@ -872,7 +1246,10 @@ struct skm_build {
     // device work
     DevBuf d_hist, d_offs, d_partial, d_rbbase, d_bstart32, d_bstart, d_owner_start;
     DevBuf d_recs, d_tmp;
-    DevBuf d_keys, d_data, d_ctr, d_flags, d_dfunc, d_swf, d_ovf, d_ovf_hi, d_ovf_lo, d_ovf_heads;
+    DevBuf d_keys, d_data, d_ctr, d_flags, d_dfunc, d_swf, d_ovf, d_ovf_hi, d_ovf_lo, d_ovf_heads, d_ovf_job, d_ovf_fm;
+    DevBuf d_jobs, d_lens;
+    uint64_t jobs_cap = 0, lens_cap = 0, n_jobs = 0;
+    uint32_t n_overflow = 0;
     uint32_t nwg = 0;
     uint64_t span = 0;
     uint64_t n_records = 0;
@@ -944,7 +1321,7 @@ void run_pipeline(skm_build* b) {
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[3], st));
     // ---- 4. bucket process ----
-    SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 64, st));
+    SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 128, st));
     SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->nseq ? b->nseq : 1, st));
     BucketArgs A;
     A.recs = b->d_recs.as<uint64_t>();
@@ -958,21 +1335,23 @@ void run_pipeline(skm_build* b) {
     A.blk2seq = b->d_blk2seq.as<uint32_t>();
     A.meta = b->d_meta.as<SeqMeta>();
     A.flags = b->d_flags.as<uint8_t>();
-    A.kept_ctr = b->d_ctr.as<unsigned long long>();
+    A.ctr = b->d_ctr.as<unsigned long long>();
     A.out_keys = b->d_keys.as<uint64_t>();
     A.out_data = b->d_data.as<skm_stored_kmer_data>();
+    A.jobs = b->d_jobs.as<Job>();
+    A.lens = b->d_lens.as<uint32_t>();
     A.ovf = b->d_ovf.as<OvfEntry>();
-    A.ovf_ctr = reinterpret_cast<unsigned int*>(b->d_ctr.as<unsigned long long>() + 1);
     A.ovf_cap = (uint32_t)b->ovf_cap;
     hipLaunchKernelGGL(k_bucket_process, dim3(NB), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[4], st));
     // ---- 5. overflow ----
-    unsigned long long ctr[2];
+    unsigned long long ctr[5];
     SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, sizeof(ctr), hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
-    uint32_t novf = (uint32_t)(ctr[1] & 0xFFFFFFFFull);
+    const uint32_t novf = (uint32_t)(ctr[1] & 0xFFFFFFFFull);
     SKM_CHECK(novf <= b->ovf_cap, SKM_E_OOM, "overflow list capacity exceeded");
+    b->n_overflow = novf;
     if (novf) {
         std::vector<OvfEntry> ov(novf);
         SKM_HIP(hipMemcpyAsync(ov.data(), b->d_ovf.p, sizeof(OvfEntry) * novf, hipMemcpyDeviceToHost, st));
@@ -988,37 +1367,34 @@ void run_pipeline(skm_build* b) {
         b->d_ovf_hi.ensure(tot * 8);
         b->d_ovf_lo.ensure(tot * 8);
         b->d_ovf_heads.ensure(tot * 4);
+        b->d_ovf_job.ensure(tot * 8);
+        b->d_ovf_fm.ensure(tot * 4);
         SKM_HIP(hipMemcpyAsync(b->d_ovf.p, ov.data(), sizeof(OvfEntry) * novf, hipMemcpyHostToDevice, st));
-        OvfArgs O;
-        O.ovf = b->d_ovf.as<OvfEntry>();
-        O.recs = b->d_recs.as<uint64_t>();
-        O.tmp = b->d_tmp.as<uint64_t>();
-        O.s_hi_g = b->d_ovf_hi.as<uint64_t>();
-        O.s_lo_g = b->d_ovf_lo.as<uint64_t>();
-        O.bucket_base = 0;
-        O.rem_bits = rem_bits;
-        O.pos_bits = pos_bits;
-        O.pos_base = 0;
-        O.blk2seq = A.blk2seq;
-        O.meta = A.meta;
-        O.flags = A.flags;
-        O.kept_ctr = A.kept_ctr;
-        O.out_keys = A.out_keys;
-        O.out_data = A.out_data;
-        O.heads_g = b->d_ovf_heads.as<uint32_t>();
-        hipLaunchKernelGGL(k_overflow, dim3(novf), dim3(BP_THREADS), 0, st, O);
+        OvfScratch S;
+        S.hi = b->d_ovf_hi.as<uint64_t>();
+        S.lo = b->d_ovf_lo.as<uint64_t>();
+        S.heads = b->d_ovf_heads.as<uint32_t>();
+        S.jobinfo = b->d_ovf_job.as<uint64_t>();
+        S.fmean = b->d_ovf_fm.as<uint32_t>();
+        hipLaunchKernelGGL(k_overflow, dim3(novf), dim3(BP_THREADS), 0, st, A, S);
         SKM_HIP(hipGetLastError());
     }
     SKM_HIP(hipEventRecord(b->ev[5], st));
-    // ---- 6. stats ----
-    SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
-    SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
-    // kept count is needed for the histogram bound: use the upper bound (records) and let the
-    // kernel read the device counter instead -- simpler: sync for the count.
+    // ---- 6. deferred P^2 / variance chains ----
     SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, sizeof(ctr), hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
     b->n_kept = ctr[0];
-    size_t lds_f = F <= 16384 ? sizeof(uint32_t) * F : 0;
+    b->n_jobs = ctr[3];
+    SKM_CHECK(ctr[3] <= b->jobs_cap && ctr[4] <= b->lens_cap, SKM_E_OOM, "chain buffers overflowed");
+    if (b->n_jobs)
+        hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(b->n_jobs, 256)), dim3(256), 0, st, b->d_jobs.as<Job>(),
+                           (uint64_t)b->n_jobs, b->d_lens.as<uint32_t>(), b->d_data.as<skm_stored_kmer_data>());
+    SKM_HIP(hipGetLastError());
+    SKM_HIP(hipEventRecord(b->ev[6], st));
+    // ---- 7. stats ----
+    SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
+    SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
+    const size_t lds_f = F <= 16384 ? sizeof(uint32_t) * F : 0;
     if (b->n_kept)
         hipLaunchKernelGGL(k_func_hist_kept, dim3(1024), dim3(256), lds_f, st, b->d_data.as<skm_stored_kmer_data>(),
                            b->n_kept, F, b->d_dfunc.as<uint32_t>());
@@ -1028,10 +1404,10 @@ void run_pipeline(skm_build* b) {
     hipLaunchKernelGGL(k_count_flags, dim3(256), dim3(256), 0, st, b->d_flags.as<uint8_t>(), b->nseq,
                        b->d_ctr.as<unsigned long long>() + 2);
     SKM_HIP(hipGetLastError());
-    SKM_HIP(hipEventRecord(b->ev[6], st));
-    SKM_HIP(hipEventSynchronize(b->ev[6]));
-    for (int i = 0; i < 6; ++i) SKM_HIP(hipEventElapsedTime(&b->last_ms[i], b->ev[i], b->ev[i + 1]));
-    SKM_HIP(hipEventElapsedTime(&b->last_ms[6], b->ev[0], b->ev[6]));
+    SKM_HIP(hipEventRecord(b->ev[7], st));
+    SKM_HIP(hipEventSynchronize(b->ev[7]));
+    for (int i = 0; i < 7; ++i) SKM_HIP(hipEventElapsedTime(&b->last_ms[i], b->ev[i], b->ev[i + 1]));
+    SKM_HIP(hipEventElapsedTime(&b->last_ms[7], b->ev[0], b->ev[7]));
     b->ran = true;
 }
 
@@ -1083,11 +1459,15 @@ void prepare(skm_build* b) {
     b->d_tmp.ensure(8 * std::max<uint64_t>(W, 1));
     b->d_keys.ensure(8 * std::max<uint64_t>(W, 1));
     b->d_data.ensure(sizeof(skm_stored_kmer_data) * std::max<uint64_t>(W, 1) + 16);
-    b->d_ctr.ensure(64);
+    b->d_ctr.ensure(128);
     b->d_flags.ensure(std::max<uint64_t>(b->nseq, 1));
     b->d_dfunc.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
     b->d_swf.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
     b->ovf_cap = W / CAP + NB + 16;
+    b->jobs_cap = W / 3 + 16;
+    b->lens_cap = W + 16;
+    b->d_jobs.ensure(sizeof(Job) * b->jobs_cap);
+    b->d_lens.ensure(sizeof(uint32_t) * b->lens_cap);
     b->d_ovf.ensure(sizeof(OvfEntry) * b->ovf_cap);
     SKM_HIP(hipStreamSynchronize(b->stream));
     b->prepared = true;
@@ -1165,7 +1545,7 @@ int skm_build_run(skm_build* b) {
 
 int skm_build_last_timings(skm_build* b, float* ms, int cap) {
     if (!b || !ms) return SKM_E_ARG;
-    int n = std::min(cap, 7);
+    int n = std::min(cap, 8);
     for (int i = 0; i < n; ++i) ms[i] = b->last_ms[i];
     return n;
 }

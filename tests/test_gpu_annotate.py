@@ -43,7 +43,8 @@ def test_calls_match_oracle(skm, gpu, tmp_path, ignore_hypo):
     db = skm.CmphKmerDb(str(tmp_path / "kmer_data"))
     caller = skm.FunctionCaller(db, funcs)
     caller.ignore_hypothetical(bool(ignore_hypo))
-    q = synth.generate_arrays(4000, 60, per_file=500, seed=99, extras=True)  # fresh queries
+    # fresh queries from the same families (files the DB never saw)
+    q = synth.generate_arrays(100000, 60, per_file=500, first_file=40, n_files=8, seed=21, extras=True)
     off, calls = caller.process_seqs(q.residues, q.seq_off, q.seq_len)
     ob = oracle_ref.Bdz(open(mph, "rb").read())
     ooff, ocalls = oracle_ref.annotate(ob, open(dat, "rb").read(), q.residues, q.seq_off, q.seq_len,
