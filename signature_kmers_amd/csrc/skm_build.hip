@@ -93,9 +93,8 @@ struct SigStats {
         var = 0.0;
     }
 
-    __device__ void add(uint32_t sample) {
+    __device__ void add_p2(uint32_t sample) {
         ++cnt;
-        sum = (uint16_t)(sum + sample);
         const double x = (double)sample;
         // ---- p_square_quantile ----
         if (cnt <= 5) {
@@ -138,7 +137,7 @@ struct SigStats {
                 if ((d >= 1. && dp > 1.) || (d <= -1. && dm < -1.)) {
                     const double hp = (h[i + 1] - h[i]) / dp;
                     const double hm = (h[i - 1] - h[i]) / dm;
-                    const short sign_d = static_cast<short>(d / fabs(d));
+                    const short sign_d = d > 0 ? 1 : -1;  // d / |d| with |d| >= 1: exactly +-1
                     const double hh = h[i] + sign_d / (dp - dm) * ((sign_d - dm) * hp + (dp - sign_d) * hm);
                     if (h[i - 1] < hh && hh < h[i + 1]) {
                         h[i] = hh;
@@ -150,7 +149,12 @@ struct SigStats {
                 }
             }
         }
-        // ---- variance (immediate), mean = lazy sum/count with the u16 sum ----
+    }
+    // variance (immediate); its mean is the lazy sum/count over the u16 sum
+    __device__ void add_var(uint32_t sample) {
+        ++cnt;
+        sum = (uint16_t)(sum + sample);
+        const double x = (double)sample;
         if (cnt > 1) {
             double mean = (double)sum / (double)cnt;
             double tmp = x - mean;
@@ -465,26 +469,42 @@ __device__ GRes group_wave(const V& v, uint64_t a, uint32_t c, const SeqMeta* __
     return r;
 }
 
-// P^2 median + variance chains, one thread per job (visit order = lens order).
-__global__ void k_chains(const Job* __restrict__ jobs, uint64_t njobs, const uint32_t* __restrict__ lens,
-                         skm_stored_kmer_data* __restrict__ out) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// P^2 median (even thread) and variance (odd thread) chains of one job; lens in visit order.
+__global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, uint64_t njobs,
+                                                const uint32_t* __restrict__ lens, skm_stored_kmer_data* __restrict__ out) {
+    const uint64_t tj = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t j = tj >> 1;
     if (j >= njobs) return;
+    const bool var_thread = (tj & 1u) != 0;
     const Job jb = jobs[j];
     const uint32_t* x = lens + jb.lens_off;
+    const uint32_t n = jb.n;
     SigStats st;
     st.init();
-    uint32_t t = 0;
-    for (; t + 4 <= jb.n; t += 4) {
-        const uint4 q = make_uint4(x[t], x[t + 1], x[t + 2], x[t + 3]);
-        st.add(q.x);
-        st.add(q.y);
-        st.add(q.z);
-        st.add(q.w);
+    constexpr uint32_t B = 16;
+    uint32_t cur[B], nxt[B];
+#pragma unroll
+    for (uint32_t t = 0; t < B; ++t) cur[t] = t < n ? x[t] : 0u;
+    for (uint32_t base = 0; base < n; base += B) {
+#pragma unroll
+        for (uint32_t t = 0; t < B; ++t) nxt[t] = base + B + t < n ? x[base + B + t] : 0u;
+        const uint32_t m = min(B, n - base);
+        if (var_thread) {
+#pragma unroll
+            for (uint32_t t = 0; t < B; ++t)
+                if (t < m) st.add_var(cur[t]);
+        } else {
+#pragma unroll
+            for (uint32_t t = 0; t < B; ++t)
+                if (t < m) st.add_p2(cur[t]);
+        }
+#pragma unroll
+        for (uint32_t t = 0; t < B; ++t) cur[t] = nxt[t];
     }
-    for (; t < jb.n; ++t) st.add(x[t]);
-    out[jb.out_idx].median = d2u16(st.h[2]);
-    out[jb.out_idx].var = d2u16(st.var);
+    if (var_thread)
+        out[jb.out_idx].var = d2u16(st.var);
+    else
+        out[jb.out_idx].median = d2u16(st.h[2]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -658,9 +678,11 @@ struct SubLds {
     uint64_t* hi;      // [CAP] element: rem<<16|func   (kept: 1<<63 | h43<<16 | avg)
     uint64_t* lo;      // [CAP] element: s<<36|i<<16|off (kept, no job: func|mean|median|var)
     uint32_t* tab;     // [TAB] hash slot: rep<<16 | count; later jobinfo[CAP] + func|mean[CAP]
-    uint16_t* slot;    // [CAP] record -> slot; later group heads
-    uint32_t* mkey;    // [CAP] sorted multi records: rep<<16 | func
-    uint16_t* midx;    // [CAP] sorted multi records: element index
+    uint16_t* slot;    // [CAP] element -> hash slot
+    uint16_t* rank;    // [CAP] element -> rank within its group (insertion order)
+    uint16_t* goff;    // [CAP] representative -> first slot of its group in `order`
+    uint16_t* glist;   // [CAP] group -> representative
+    uint16_t* order;   // [CAP] multi-occurrence elements grouped by representative
     uint16_t* big;     // [CAP/2] wave-level group list
     uint32_t* wave;    // scan scratch (>= 40 words, 16-byte aligned)
     uint32_t* nbig;
@@ -682,8 +704,226 @@ __device__ __forceinline__ void write_kept(const BucketArgs& A, uint64_t o, uint
     A.out_data[o] = d;
 }
 
-// One sub-bucket of n <= CAP records: LDS hash grouping, singletons immediately, multi-occurrence
-// groups sorted by (group, func, ordinal) and processed by threads (small) or waves (large).
+template <int N>
+__device__ __forceinline__ void reg_sort_pairs(uint64_t* k, uint32_t* v) {
+#pragma unroll
+    for (int kk = 2; kk <= N; kk <<= 1)
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const bool asc = (i & kk) == 0;
+                    const bool sw = asc ? (k[i] > k[l]) : (k[i] < k[l]);
+                    const uint64_t ka = k[i], kb = k[l];
+                    const uint32_t va = v[i], vb = v[l];
+                    k[i] = sw ? kb : ka;
+                    k[l] = sw ? ka : kb;
+                    v[i] = sw ? vb : va;
+                    v[l] = sw ? va : vb;
+                }
+            }
+}
+
+// Thread-level group (c <= N members at order[a..a+c)): members sorted in registers by
+// (func, ordinal); the sorted member list is written back so the best run is contiguous.
+template <int N>
+__device__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint32_t c, const SeqMeta* __restrict__ meta,
+                              uint8_t* __restrict__ flags) {
+    GRes r;
+    r.kept = false;
+    uint64_t key[N];
+    uint32_t idx[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+        if ((uint32_t)t < c) {
+            const uint32_t j = L.order[a + t];
+            key[t] = ((L.hi[j] & 0xFFFFull) << 48) | (L.lo[j] >> 16);
+            idx[t] = j;
+        } else {
+            key[t] = ~0ull;
+            idx[t] = 0xFFFFu;
+        }
+    }
+    reg_sort_pairs<N>(key, idx);
+#pragma unroll
+    for (int t = 0; t < N; ++t)
+        if ((uint32_t)t < c) L.order[a + t] = (uint16_t)idx[t];
+    uint32_t best_f = (uint32_t)(key[0] >> 48), best_c = 0, rb = 0, run_s = 0;
+#pragma unroll
+    for (int t = 1; t <= N; ++t) {
+        if ((uint32_t)t <= c) {
+            const bool end = ((uint32_t)t == c) || (key[t < N ? t : N - 1] >> 48) != (key[t - 1] >> 48);
+            if (end) {
+                const uint32_t len = t - run_s;
+                if (len > best_c) {
+                    best_c = len;
+                    best_f = (uint32_t)(key[t - 1] >> 48);
+                    rb = run_s;
+                }
+                run_s = t;
+            }
+        }
+    }
+    if ((float)best_c < float(c) * 0.8f) return r;
+    r.kept = true;
+    r.best_f = best_f;
+    r.cbest = best_c;
+    r.rb = rb;
+    uint32_t of[N];
+    uint32_t sum = 0, lr0 = 0, lr1 = 0;
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+        of[t] = 0x10000u;
+        if ((uint32_t)t < c) {
+            const uint64_t lo = L.lo[idx[t]];
+            of[t] = (uint32_t)(lo & 0xFFFFu);
+            const uint32_t s = (uint32_t)(lo >> 36);
+            flags[s] = 1;
+            if ((uint32_t)t >= rb && (uint32_t)t < rb + best_c) {
+                const uint32_t len = meta[s].len;
+                sum += len;
+                const uint32_t q = rb + best_c - 1 - t;  // visit position (reverse ordinal)
+                if (q == 0) lr0 = len;
+                if (q == 1) lr1 = len;
+            }
+        }
+    }
+    reg_sort<N>(of);
+    const uint32_t k = c / 2;
+    uint32_t avg = 0;
+#pragma unroll
+    for (int t = 0; t < N; ++t)
+        if ((uint32_t)t == k) avg = of[t];
+    r.avg = avg;
+    r.mean = d2u16((double)(uint16_t)sum / (double)best_c);
+    r.median = 0;
+    r.var = 0;
+    if (best_c <= 2) {
+        const uint32_t lr[2] = {lr0, lr1};
+        stats_small(r, lr, best_c);
+    }
+    return r;
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave-level group (c > SMALLC).  Best function by Boyer-Moore majority: if any function has
+// >= 80 % of the occurrences it is the strict majority, otherwise the group is cut anyway.
+// The best-function members are compacted to order[a..a+cbest) and sorted by ordinal.
+__device__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const SeqMeta* __restrict__ meta,
+                            uint8_t* __restrict__ flags) {
+    const uint32_t lane = threadIdx.x & 63u;
+    GRes r;
+    r.kept = false;
+    // majority candidate
+    uint32_t cand = 0xFFFFFFFFu, cc = 0;
+    for (uint32_t t = lane; t < c; t += 64) {
+        const uint32_t f = (uint32_t)(L.hi[L.order[a + t]] & 0xFFFFu);
+        if (cc == 0) {
+            cand = f;
+            cc = 1;
+        } else if (f == cand) {
+            ++cc;
+        } else {
+            --cc;
+        }
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t oc = (uint32_t)__shfl_xor((int)cand, d, 64), on = (uint32_t)__shfl_xor((int)cc, d, 64);
+        if (oc == cand) {
+            cc += on;
+        } else if (cc >= on) {
+            cc -= on;
+        } else {
+            cand = oc;
+            cc = on - cc;
+        }
+    }
+    cand = (uint32_t)__shfl((int)cand, 0, 64);
+    uint32_t nb = 0;
+    for (uint32_t t = lane; t < c; t += 64) nb += (uint32_t)(L.hi[L.order[a + t]] & 0xFFFFu) == cand;
+    nb = wave_sum(nb);
+    if ((float)nb < float(c) * 0.8f) return r;
+    r.kept = true;
+    r.best_f = cand;
+    r.cbest = nb;
+    r.rb = 0;
+    // avg_from_end over all members: k-th smallest offset by binary search on the value
+    uint32_t vmin = 0xFFFFu, vmax = 0, sum = 0;
+    for (uint32_t t = lane; t < c; t += 64) {
+        const uint32_t j = L.order[a + t];
+        const uint64_t lo = L.lo[j];
+        const uint32_t o = (uint32_t)(lo & 0xFFFFu);
+        vmin = min(vmin, o);
+        vmax = max(vmax, o);
+        const uint32_t s = (uint32_t)(lo >> 36);
+        flags[s] = 1;
+        if ((uint32_t)(L.hi[j] & 0xFFFFu) == cand) sum += meta[s].len;
+    }
+    vmin = wave_min(vmin);
+    vmax = wave_max(vmax);
+    sum = wave_sum(sum);
+    const uint32_t k = c / 2;
+    while (vmin < vmax) {
+        const uint32_t mid = (vmin + vmax) >> 1;
+        uint32_t cnt = 0;
+        for (uint32_t t = lane; t < c; t += 64) cnt += (uint32_t)(L.lo[L.order[a + t]] & 0xFFFFu) <= mid;
+        cnt = wave_sum(cnt);
+        if (cnt >= k + 1)
+            vmax = mid;
+        else
+            vmin = mid + 1;
+    }
+    r.avg = vmin;
+    r.mean = d2u16((double)(uint16_t)sum / (double)nb);
+    r.median = 0;
+    r.var = 0;
+    // compact the best-function members to the front (writes never pass the read position)
+    uint32_t w = 0;
+    for (uint32_t base = 0; base < c; base += 64) {
+        const uint32_t t = base + lane;
+        const uint32_t j = t < c ? L.order[a + t] : 0u;
+        const bool keep = t < c && (uint32_t)(L.hi[j] & 0xFFFFu) == cand;
+        const uint64_t m = __ballot(keep);
+        wave_sync();
+        if (keep) L.order[a + w + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)j;
+        w += (uint32_t)__popcll(m);
+        wave_sync();
+    }
+    // sort order[a..a+nb) by ordinal: bitonic for arbitrary n (only ascending compare-exchanges,
+    // missing partners act as +infinity)
+    uint32_t Np = 1;
+    while (Np < nb) Np <<= 1;
+    for (uint32_t kk = 2; kk <= Np; kk <<= 1) {
+        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+            const bool flip = jj == (kk >> 1);
+            for (uint32_t t = lane; t < Np / 2; t += 64) {
+                const uint32_t i = 2 * t - (t & (jj - 1));
+                const uint32_t l = flip ? (i ^ (kk - 1)) : (i + jj);
+                if (l < nb) {
+                    const uint16_t ia = L.order[a + i], ib = L.order[a + l];
+                    if (L.lo[ia] > L.lo[ib]) {
+                        L.order[a + i] = ib;
+                        L.order[a + l] = ia;
+                    }
+                }
+            }
+            wave_sync();
+        }
+    }
+    return r;
+}
+
+// One sub-bucket of n <= CAP records: LDS hash grouping (ranks from the insert atomics give a
+// counting sort by group), singletons resolved immediately, multi-occurrence groups by threads
+// (small) or waves (large); no workgroup-wide sort.
 __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const BucketArgs& A, uint64_t hprefix,
                             uint64_t pos_mask, const SubLds& L) {
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -694,35 +934,38 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
     for (uint32_t t = tid; t < (uint32_t)TAB; t += nt) L.tab[t] = EMPTY;
     if (tid == 0) *L.nbig = 0;
     __syncthreads();
-    // 2. hash insert: slot value = representative element << 16 | occurrence count
+    // 2. hash insert: slot = representative << 16 | count; the pre-increment count is the rank
     for (uint32_t j = tid; j < n; j += nt) {
         const uint32_t rem = (uint32_t)(L.hi[j] >> 16);
         uint32_t slot = (rem * 0x9E3779B1u) >> (32 - TAB_BITS);
+        uint32_t rk = 0;
         while (true) {
             const uint32_t cur = atomicCAS(&L.tab[slot], EMPTY, (j << 16) | 1u);
             if (cur == EMPTY) break;
             if ((uint32_t)(L.hi[cur >> 16] >> 16) == rem) {
-                atomicAdd(&L.tab[slot], 1u);
+                rk = atomicAdd(&L.tab[slot], 1u) & 0xFFFFu;
                 break;
             }
             slot = (slot + 1) & (TAB - 1);
         }
         L.slot[j] = (uint16_t)slot;
+        L.rank[j] = (uint16_t)rk;
     }
     __syncthreads();
-    // 3. singletons resolved in place; multi-occurrence records compacted
-    uint32_t M = 0;
+    // 3. singletons resolved in place; multi-occurrence groups get a slice of `order`
+    uint32_t M = 0, G = 0;
     for (uint32_t c0 = 0; c0 < n; c0 += nt) {
         const uint32_t j = c0 + tid;
         const bool in = j < n;
         const uint32_t e = in ? L.tab[L.slot[j]] : 0u;
-        const bool multi = in && (e & 0xFFFFu) > 1u;
+        const uint32_t cnt = e & 0xFFFFu;
+        const bool grp = in && cnt > 1 && (e >> 16) == j;
         uint32_t tot;
-        const uint32_t pos = wg_exclusive_scan(multi ? 1u : 0u, L.wave, tot);
-        if (multi) {
-            L.midx[M + pos] = (uint16_t)j;
-            L.mkey[M + pos] = (e & 0xFFFF0000u) | (uint32_t)(L.hi[j] & 0xFFFFu);
-        } else if (in) {  // group of one: always kept (1 >= 0.8), median 0, var 0
+        const uint32_t v = wg_exclusive_scan(grp ? ((cnt << 13) | 1u) : 0u, L.wave, tot);
+        if (grp) {
+            L.goff[j] = (uint16_t)(M + (v >> 13));
+            L.glist[G + (v & 0x1FFFu)] = (uint16_t)j;
+        } else if (in && cnt == 1) {  // group of one: always kept (1 >= 0.8), median 0, var 0
             const uint64_t H = L.hi[j], Lo = L.lo[j];
             const uint32_t s = (uint32_t)(Lo >> 36);
             const uint32_t len = A.meta[s].len;
@@ -730,57 +973,22 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
             L.hi[j] = kept_hi(hprefix | (H >> 16), (uint32_t)(Lo & 0xFFFFu));
             L.lo[j] = kept_lo((uint32_t)(H & 0xFFFFu), d2u16((double)(uint16_t)len / 1.0), 0, 0);
         }
-        M += tot;
+        M += tot >> 13;
+        G += tot & 0x1FFFu;
+    }
+    __syncthreads();
+    // 4. counting-sort scatter of the multi-occurrence elements
+    for (uint32_t j = tid; j < n; j += nt) {
+        const uint32_t e = L.tab[L.slot[j]];
+        if ((e & 0xFFFFu) > 1) L.order[L.goff[e >> 16] + L.rank[j]] = (uint16_t)j;
     }
     __syncthreads();
     uint32_t* jobinfo = L.tab;        // per representative: best-run start << 16 | best count
     uint32_t* fmean = L.tab + CAP;    // per representative: func | mean << 16
     for (uint32_t j = tid; j < n; j += nt) jobinfo[j] = 0;
-    uint32_t NP = 1;
-    while (NP < M) NP <<= 1;
-    for (uint32_t t = M + tid; t < NP; t += nt) {
-        L.mkey[t] = 0xFFFFFFFFu;
-        L.midx[t] = 0;
-    }
     __syncthreads();
-    // 4. bitonic sort of the multi records by (representative, func, ordinal)
-    if (M > 1) {
-        for (uint32_t k = 2; k <= NP; k <<= 1) {
-            for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-                for (uint32_t t = tid; t < NP / 2; t += nt) {
-                    const uint32_t i = 2 * t - (t & (jj - 1));
-                    const uint32_t l = i + jj;
-                    const bool asc = (i & k) == 0;
-                    const uint32_t ka = L.mkey[i], kb = L.mkey[l];
-                    const uint16_t ia = L.midx[i], ib = L.midx[l];
-                    const bool gt = ka > kb || (ka == kb && L.lo[ia] > L.lo[ib]);
-                    if (gt == asc) {
-                        L.mkey[i] = kb;
-                        L.mkey[l] = ka;
-                        L.midx[i] = ib;
-                        L.midx[l] = ia;
-                    }
-                }
-                __syncthreads();
-            }
-        }
-    }
-    // 5. group heads of the sorted multi records
-    uint16_t* heads = L.slot;
-    uint32_t G = 0;
-    for (uint32_t c0 = 0; c0 < M; c0 += nt) {
-        const uint32_t t = c0 + tid;
-        const bool head = t < M && (t == 0 || (L.mkey[t] >> 16) != (L.mkey[t - 1] >> 16));
-        uint32_t tot;
-        const uint32_t pos = wg_exclusive_scan(head ? 1u : 0u, L.wave, tot);
-        if (head) heads[G + pos] = (uint16_t)t;
-        G += tot;
-    }
-    __syncthreads();
-    const LdsView V{L.mkey, L.midx, L.lo};
-    auto stage = [&](const GRes& r, uint32_t a) {
+    auto stage = [&](const GRes& r, uint32_t rep, uint32_t a) {
         if (!r.kept) return;
-        const uint32_t rep = L.mkey[a] >> 16;
         const uint64_t h43 = hprefix | (L.hi[rep] >> 16);
         L.hi[rep] = kept_hi(h43, r.avg);
         if (r.cbest >= 3) {
@@ -790,40 +998,39 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
             L.lo[rep] = kept_lo(r.best_f, r.mean, r.median, r.var);
         }
     };
-    // 6. thread-level groups; large ones queued for waves
+    // 5. thread-level groups; large ones queued for waves
     for (uint32_t g = tid; g < G; g += nt) {
-        const uint32_t a = heads[g];
-        const uint32_t b = g + 1 < G ? heads[g + 1] : M;
-        const uint32_t c = b - a;
+        const uint32_t rep = L.glist[g];
+        const uint32_t a = L.goff[rep];
+        const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
         if (c > (uint32_t)SMALLC) {
-            const uint32_t bi = atomicAdd(L.nbig, 1u);
-            L.big[bi] = (uint16_t)g;
+            L.big[atomicAdd(L.nbig, 1u)] = (uint16_t)g;
             continue;
         }
         GRes r;
         if (c <= 4)
-            r = group_thread<4>(V, a, c, A.meta, A.flags);
+            r = lgroup_thread<4>(L, a, c, A.meta, A.flags);
         else if (c <= 8)
-            r = group_thread<8>(V, a, c, A.meta, A.flags);
+            r = lgroup_thread<8>(L, a, c, A.meta, A.flags);
         else
-            r = group_thread<16>(V, a, c, A.meta, A.flags);
-        stage(r, a);
+            r = lgroup_thread<16>(L, a, c, A.meta, A.flags);
+        stage(r, rep, a);
     }
     __syncthreads();
-    // 7. wave-level groups
     {
         const uint32_t nbig = *L.nbig;
         const uint32_t wave = tid >> 6, nwaves = nt >> 6;
         for (uint32_t bi = wave; bi < nbig; bi += nwaves) {
             const uint32_t g = L.big[bi];
-            const uint32_t a = heads[g];
-            const uint32_t b = g + 1 < G ? heads[g + 1] : M;
-            const GRes r = group_wave(V, a, b - a, A.meta, A.flags);
-            if ((tid & 63u) == 0) stage(r, a);
+            const uint32_t rep = L.glist[g];
+            const uint32_t a = L.goff[rep];
+            const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
+            const GRes r = lgroup_wave(L, a, c, A.meta, A.flags);
+            if ((tid & 63u) == 0) stage(r, rep, a);
         }
     }
     __syncthreads();
-    // 8. emit kept k-mers (one atomic per chunk) and chain jobs with their protein lengths
+    // 6. emit kept k-mers (one atomic per chunk) and chain jobs with their protein lengths
     unsigned long long* s_base = reinterpret_cast<unsigned long long*>(L.wave + 36);
     for (uint32_t c0 = 0; c0 < n; c0 += nt) {
         const uint32_t j = c0 + tid;
@@ -855,10 +1062,8 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
                 jbr.out_idx = (uint32_t)o;
                 A.jobs[s_base[1] + (jl & 0x7FFu)] = jbr;
                 const uint32_t start = jb >> 16;
-                for (uint32_t t = 0; t < jn; ++t) {
-                    const uint32_t e = start + jn - 1 - t;  // reverse ordinal order
-                    A.lens[loff + t] = A.meta[L.lo[L.midx[e]] >> 36].len;
-                }
+                for (uint32_t t = 0; t < jn; ++t)  // reverse ordinal order
+                    A.lens[loff + t] = A.meta[L.lo[L.order[start + jn - 1 - t]] >> 36].len;
             } else {
                 write_kept(A, o, H, L.lo[j]);
             }
@@ -872,8 +1077,10 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
     __shared__ uint64_t s_lo[CAP];
     __shared__ uint32_t s_tab[TAB];
     __shared__ uint16_t s_slot[CAP];
-    __shared__ uint32_t s_mkey[CAP];
-    __shared__ uint16_t s_midx[CAP];
+    __shared__ uint16_t s_rank[CAP];
+    __shared__ uint16_t s_goff[CAP];
+    __shared__ uint16_t s_glist[CAP];
+    __shared__ uint16_t s_order[CAP];
     __shared__ uint32_t s_sub[(1 << MAX_B2) + 1];
     __shared__ uint16_t s_big[CAP / 2];
     __shared__ __align__(16) uint32_t s_wave[48];
@@ -883,8 +1090,10 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
     L.lo = s_lo;
     L.tab = s_tab;
     L.slot = s_slot;
-    L.mkey = s_mkey;
-    L.midx = s_midx;
+    L.rank = s_rank;
+    L.goff = s_goff;
+    L.glist = s_glist;
+    L.order = s_order;
     L.big = s_big;
     L.wave = s_wave;
     L.nbig = &s_nbig;
