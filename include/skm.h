@@ -111,6 +111,12 @@ int skm_build_run(skm_build* b);
 /* Device time (ms) of the last run's phases: [0]=extract-count [1]=scan [2]=extract-scatter
  * [3]=bucket-process [4]=overflow [5]=chains [6]=stats [7]=total; returns entries written. */
 int skm_build_last_timings(skm_build* b, float* ms, int cap);
+/* Counters of the last run: [0]=windows [1]=kept [2]=overflow sub-buckets [3]=chain jobs
+ * [4]=chain samples [5]=sequences; returns entries written. */
+int skm_build_counters(skm_build* b, uint64_t* out, int cap);
+/* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then
+ * enable/disable stamping for subsequent runs. */
+int skm_build_debug_stamps(skm_build* b, int enable, uint64_t* out, int cap);
 /* Run (if not yet run since the last prepare) and download the result. */
 int skm_build_finish(skm_build* b, skm_kept* out);
 void skm_kept_free(skm_kept* k);

@@ -69,6 +69,8 @@ _SIGS = {
     "skm_build_run": (C.c_int, [_P]),
     "skm_build_last_timings": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int]),
     "skm_build_finish": (C.c_int, [_P, C.POINTER(_Kept)]),
+    "skm_build_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
+    "skm_build_debug_stamps": (C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64), C.c_int]),
     "skm_kept_free": (None, [C.POINTER(_Kept)]),
     "skm_build_destroy": (None, [_P]),
     "skm_comm_unique_id": (C.c_int, [_P]),
@@ -198,6 +200,17 @@ class SignatureBuilder:
         n = lib().skm_build_last_timings(self._h, ms, 8)
         names = ["extract_count", "scan", "extract_scatter", "bucket_process", "overflow", "chains", "stats", "total"]
         return {names[i]: float(ms[i]) for i in range(n)}
+
+    def counters(self) -> dict:
+        v = (C.c_uint64 * 8)()
+        n = lib().skm_build_counters(self._h, v, 8)
+        names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences"]
+        return {names[i]: int(v[i]) for i in range(n)}
+
+    def debug_stamps(self, enable: bool) -> list:
+        v = (C.c_uint64 * 16)()
+        _check(lib().skm_build_debug_stamps(self._h, 1 if enable else 0, v, 16))
+        return [int(x) for x in v]
 
     def finish(self) -> KeptKmers:
         k = _Kept()

@@ -672,7 +672,17 @@ struct BucketArgs {
     uint32_t* lens;
     OvfEntry* ovf;
     uint32_t ovf_cap;
+    unsigned long long* stamps;   // optional [16] per-phase cycle sums (diagnostics)
 };
+
+#define SKM_STAMP(i)                                                          \
+    do {                                                                      \
+        if (A.stamps && threadIdx.x == 0) {                                   \
+            const uint64_t _t = __builtin_amdgcn_s_memtime();                 \
+            atomicAdd(&A.stamps[(i)], (unsigned long long)(_t - *L.tlast));   \
+            *L.tlast = _t;                                                    \
+        }                                                                     \
+    } while (0)
 
 struct SubLds {
     uint64_t* hi;      // [CAP] element: rem<<16|func   (kept: 1<<63 | h43<<16 | avg)
@@ -686,6 +696,7 @@ struct SubLds {
     uint16_t* big;     // [CAP/2] wave-level group list
     uint32_t* wave;    // scan scratch (>= 40 words, 16-byte aligned)
     uint32_t* nbig;
+    uint64_t* tlast;   // stamp scratch
 };
 
 __device__ __forceinline__ uint64_t kept_hi(uint64_t h43, uint32_t avg) { return (1ull << 63) | (h43 << 16) | avg; }
@@ -934,6 +945,7 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
     for (uint32_t t = tid; t < (uint32_t)TAB; t += nt) L.tab[t] = EMPTY;
     if (tid == 0) *L.nbig = 0;
     __syncthreads();
+    SKM_STAMP(2);
     // 2. hash insert: slot = representative << 16 | count; the pre-increment count is the rank
     for (uint32_t j = tid; j < n; j += nt) {
         const uint32_t rem = (uint32_t)(L.hi[j] >> 16);
@@ -952,6 +964,7 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
         L.rank[j] = (uint16_t)rk;
     }
     __syncthreads();
+    SKM_STAMP(3);
     // 3. singletons resolved in place; multi-occurrence groups get a slice of `order`
     uint32_t M = 0, G = 0;
     for (uint32_t c0 = 0; c0 < n; c0 += nt) {
@@ -977,6 +990,7 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
         G += tot & 0x1FFFu;
     }
     __syncthreads();
+    SKM_STAMP(4);
     // 4. counting-sort scatter of the multi-occurrence elements
     for (uint32_t j = tid; j < n; j += nt) {
         const uint32_t e = L.tab[L.slot[j]];
@@ -987,6 +1001,7 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
     uint32_t* fmean = L.tab + CAP;    // per representative: func | mean << 16
     for (uint32_t j = tid; j < n; j += nt) jobinfo[j] = 0;
     __syncthreads();
+    SKM_STAMP(5);
     auto stage = [&](const GRes& r, uint32_t rep, uint32_t a) {
         if (!r.kept) return;
         const uint64_t h43 = hprefix | (L.hi[rep] >> 16);
@@ -1017,6 +1032,7 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
         stage(r, rep, a);
     }
     __syncthreads();
+    SKM_STAMP(6);
     {
         const uint32_t nbig = *L.nbig;
         const uint32_t wave = tid >> 6, nwaves = nt >> 6;
@@ -1030,6 +1046,7 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
         }
     }
     __syncthreads();
+    SKM_STAMP(7);
     // 6. emit kept k-mers (one atomic per chunk) and chain jobs with their protein lengths
     unsigned long long* s_base = reinterpret_cast<unsigned long long*>(L.wave + 36);
     for (uint32_t c0 = 0; c0 < n; c0 += nt) {
@@ -1070,6 +1087,7 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
         }
         __syncthreads();
     }
+    SKM_STAMP(8);
 }
 
 __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
@@ -1085,7 +1103,10 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
     __shared__ uint16_t s_big[CAP / 2];
     __shared__ __align__(16) uint32_t s_wave[48];
     __shared__ uint32_t s_nbig;
+    __shared__ uint64_t s_tlast;
     SubLds L;
+    L.tlast = &s_tlast;
+    if (threadIdx.x == 0) s_tlast = __builtin_amdgcn_s_memtime();
     L.hi = s_hi;
     L.lo = s_lo;
     L.tab = s_tab;
@@ -1110,6 +1131,8 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
         process_sub(A.recs + r0, (uint32_t)n, A, hprefix, pos_mask, L);
         return;
     }
+    __syncthreads();
+    SKM_STAMP(9);
     // ---- level-2 partition by the next b2 bits of rem ----
     int b2 = 0;
     while (b2 < MAX_B2 && (n >> b2) > (uint64_t)SUB_TARGET) ++b2;
@@ -1122,6 +1145,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
         atomicAdd(&s_sub[(uint32_t)((rec >> A.pos_bits) >> shift)], 1u);
     }
     __syncthreads();
+    SKM_STAMP(0);
     {
         const uint32_t per = (nsub + blockDim.x - 1) / blockDim.x;
         const uint32_t d0 = threadIdx.x * per;
@@ -1148,6 +1172,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
     }
     __threadfence_block();
     __syncthreads();
+    SKM_STAMP(1);
     for (uint32_t d = 0; d < nsub; ++d) {
         const uint32_t a = s_sub[d], e = s_sub[d + 1];
         const uint32_t cnt = e - a;
@@ -1155,6 +1180,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
         if (cnt <= (uint32_t)CAP) {
             process_sub(A.tmp + r0 + a, cnt, A, hprefix, pos_mask, L);
             __syncthreads();
+            SKM_STAMP(10);
         } else if (threadIdx.x == 0) {
             const unsigned int en = atomicAdd(reinterpret_cast<unsigned int*>(&A.ctr[1]), 1u);
             if (en < A.ovf_cap) {
@@ -1456,8 +1482,9 @@ struct skm_build {
     DevBuf d_hist, d_offs, d_partial, d_rbbase, d_bstart32, d_bstart, d_owner_start;
     DevBuf d_recs, d_tmp;
     DevBuf d_keys, d_data, d_ctr, d_flags, d_dfunc, d_swf, d_ovf, d_ovf_hi, d_ovf_lo, d_ovf_heads, d_ovf_job, d_ovf_fm;
-    DevBuf d_jobs, d_lens;
-    uint64_t jobs_cap = 0, lens_cap = 0, n_jobs = 0;
+    DevBuf d_jobs, d_lens, d_stamps;
+    bool stamps = false;
+    uint64_t jobs_cap = 0, lens_cap = 0, n_jobs = 0, n_lens = 0;
     uint32_t n_overflow = 0;
     uint32_t nwg = 0;
     uint64_t span = 0;
@@ -1551,6 +1578,12 @@ void run_pipeline(skm_build* b) {
     A.lens = b->d_lens.as<uint32_t>();
     A.ovf = b->d_ovf.as<OvfEntry>();
     A.ovf_cap = (uint32_t)b->ovf_cap;
+    A.stamps = nullptr;
+    if (b->stamps) {
+        b->d_stamps.ensure(16 * 8);
+        SKM_HIP(hipMemsetAsync(b->d_stamps.p, 0, 16 * 8, st));
+        A.stamps = b->d_stamps.as<unsigned long long>();
+    }
     hipLaunchKernelGGL(k_bucket_process, dim3(NB), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[4], st));
@@ -1594,9 +1627,10 @@ void run_pipeline(skm_build* b) {
     SKM_HIP(hipStreamSynchronize(st));
     b->n_kept = ctr[0];
     b->n_jobs = ctr[3];
+    b->n_lens = ctr[4];
     SKM_CHECK(ctr[3] <= b->jobs_cap && ctr[4] <= b->lens_cap, SKM_E_OOM, "chain buffers overflowed");
     if (b->n_jobs)
-        hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(b->n_jobs, 256)), dim3(256), 0, st, b->d_jobs.as<Job>(),
+        hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(2 * b->n_jobs, 256)), dim3(256), 0, st, b->d_jobs.as<Job>(),
                            (uint64_t)b->n_jobs, b->d_lens.as<uint32_t>(), b->d_data.as<skm_stored_kmer_data>());
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[6], st));
@@ -1750,6 +1784,27 @@ int skm_build_run(skm_build* b) {
     prepare(b);
     run_pipeline(b);
     SKM_API_END
+}
+
+// Diagnostics: enable per-phase s_memtime sums in k_bucket_process (returned by the next call).
+int skm_build_debug_stamps(skm_build* b, int enable, uint64_t* out, int cap) {
+    SKM_API_BEGIN
+    SKM_CHECK(b, SKM_E_ARG, "null build");
+    if (out && cap > 0 && b->stamps && b->d_stamps.p) {
+        uint64_t tmp[16];
+        SKM_HIP(hipMemcpy(tmp, b->d_stamps.p, sizeof(tmp), hipMemcpyDeviceToHost));
+        for (int i = 0; i < cap && i < 16; ++i) out[i] = tmp[i];
+    }
+    b->stamps = enable != 0;
+    SKM_API_END
+}
+
+int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
+    if (!b || !out) return SKM_E_ARG;
+    const uint64_t v[6] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq};
+    int n = std::min(cap, 6);
+    for (int i = 0; i < n; ++i) out[i] = v[i];
+    return n;
 }
 
 int skm_build_last_timings(skm_build* b, float* ms, int cap) {

@@ -1,0 +1,41 @@
+"""Diagnostics for the device build: phase timings, counters and k_bucket_process phase stamps."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import signature_kmers_amd as skm  # noqa: E402
+from signature_kmers_amd import synth  # noqa: E402
+
+STAMP_NAMES = {0: "l2_count", 1: "l2_scatter", 9: "l2_setup", 2: "sub_load", 3: "sub_hash", 4: "sub_classify",
+               5: "sub_scatter", 6: "sub_thread_groups", 7: "sub_wave_groups", 8: "sub_emit", 10: "sub_loop_tail"}
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--seqs", type=int, default=1_000_000)
+ap.add_argument("--families", type=int, default=4000)
+ap.add_argument("--steps", type=int, default=2)
+a = ap.parse_args()
+t = time.time()
+p = synth.generate_arrays(a.seqs, a.families)
+r, o, l, f, i, funcs = synth.build_inputs(p)
+print("gen", round(time.time() - t, 1), "s", flush=True)
+b = skm.SignatureBuilder(len(funcs))
+b.add_batch(r, o, l, f, i)
+b.prepare()
+b.run()
+print("timings", json.dumps(b.timings()))
+b.debug_stamps(True)
+b.run()
+st = b.debug_stamps(False)
+tot = sum(st)
+print("stamps (cycles summed over workgroups):")
+for k in sorted(STAMP_NAMES):
+    print(f"  {STAMP_NAMES[k]:>20s} {st[k]:>16d} {100.0 * st[k] / max(tot, 1):6.1f}%")
+print("timings(stamped)", json.dumps(b.timings()))
+print("counters", json.dumps(b.counters()))
+for _ in range(a.steps):
+    b.run()
+    print("timings", json.dumps(b.timings()))
