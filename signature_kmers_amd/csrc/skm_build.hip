@@ -176,7 +176,7 @@ __device__ __forceinline__ void make_elem(uint64_t rec, int pos_bits, uint64_t p
     }
     const uint32_t i = (uint32_t)(p - m.pstart);
     const uint32_t off16 = (m.len - i) & 0xFFFFu;
-    ohi = (rem << 16) | m.func;
+    ohi = ((uint64_t)(m.len & 0xFFFFu) << 48) | (rem << 16) | m.func;  // len mod 2^16 rides along
     olo = ((uint64_t)s << 36) | ((uint64_t)i << 16) | off16;
 }
 
@@ -469,13 +469,64 @@ __device__ GRes group_wave(const V& v, uint64_t a, uint32_t c, const SeqMeta* __
     return r;
 }
 
-// P^2 median (even thread) and variance (odd thread) chains of one job; lens in visit order.
+// Chains run longest-first: jobs are counting-sorted by length class (floor(log2 n), descending)
+// so a wave's 64 jobs have similar lengths.  Waves 2w and 2w+1 run the P^2 median and the
+// variance recurrence of the same 64 jobs (wave-uniform branch).
+constexpr int JOB_CLASSES = 32;
+constexpr int JOB_WG = 256;
+
+__device__ __forceinline__ uint32_t job_class(uint32_t n) { return 31u - (uint32_t)__clz(n | 1u); }
+
+__global__ __launch_bounds__(JOB_WG) void k_job_count(const Job* __restrict__ jobs, uint64_t njobs, uint64_t chunk,
+                                                      uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[JOB_CLASSES];
+    if (threadIdx.x < JOB_CLASSES) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t a = (uint64_t)blockIdx.x * chunk, e = min(njobs, a + chunk);
+    for (uint64_t j = a + threadIdx.x; j < e; j += blockDim.x) atomicAdd(&h[job_class(jobs[j].n)], 1u);
+    __syncthreads();
+    if (threadIdx.x < JOB_CLASSES) hist[blockIdx.x * JOB_CLASSES + threadIdx.x] = h[threadIdx.x];
+}
+
+// one workgroup: offs[w][c] = start of (class c, workgroup w), classes in descending order
+__global__ void k_job_scan(const uint32_t* __restrict__ hist, uint32_t nwg, uint64_t* __restrict__ offs) {
+    __shared__ uint64_t tot[JOB_CLASSES];
+    const uint32_t c = threadIdx.x;
+    if (c < JOB_CLASSES) {
+        uint64_t t = 0;
+        for (uint32_t w = 0; w < nwg; ++w) t += hist[w * JOB_CLASSES + c];
+        tot[c] = t;
+    }
+    __syncthreads();
+    if (c < JOB_CLASSES) {
+        uint64_t base = 0;
+        for (uint32_t cc = JOB_CLASSES - 1; cc > c; --cc) base += tot[cc];
+        for (uint32_t w = 0; w < nwg; ++w) {
+            offs[w * JOB_CLASSES + c] = base;
+            base += hist[w * JOB_CLASSES + c];
+        }
+    }
+}
+
+__global__ __launch_bounds__(JOB_WG) void k_job_scatter(const Job* __restrict__ jobs, uint64_t njobs, uint64_t chunk,
+                                                        const uint64_t* __restrict__ offs, Job* __restrict__ sorted) {
+    __shared__ unsigned long long cur[JOB_CLASSES];
+    if (threadIdx.x < JOB_CLASSES) cur[threadIdx.x] = offs[blockIdx.x * JOB_CLASSES + threadIdx.x];
+    __syncthreads();
+    const uint64_t a = (uint64_t)blockIdx.x * chunk, e = min(njobs, a + chunk);
+    for (uint64_t j = a + threadIdx.x; j < e; j += blockDim.x) {
+        const Job jb = jobs[j];
+        sorted[atomicAdd(&cur[job_class(jb.n)], 1ull)] = jb;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, uint64_t njobs,
                                                 const uint32_t* __restrict__ lens, skm_stored_kmer_data* __restrict__ out) {
-    const uint64_t tj = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t j = tj >> 1;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t wave = t >> 6;
+    const uint64_t j = (wave >> 1) * 64 + (t & 63u);
+    const bool var_wave = (wave & 1u) != 0;
     if (j >= njobs) return;
-    const bool var_thread = (tj & 1u) != 0;
     const Job jb = jobs[j];
     const uint32_t* x = lens + jb.lens_off;
     const uint32_t n = jb.n;
@@ -484,24 +535,24 @@ __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, ui
     constexpr uint32_t B = 16;
     uint32_t cur[B], nxt[B];
 #pragma unroll
-    for (uint32_t t = 0; t < B; ++t) cur[t] = t < n ? x[t] : 0u;
+    for (uint32_t q = 0; q < B; ++q) cur[q] = q < n ? x[q] : 0u;
     for (uint32_t base = 0; base < n; base += B) {
 #pragma unroll
-        for (uint32_t t = 0; t < B; ++t) nxt[t] = base + B + t < n ? x[base + B + t] : 0u;
+        for (uint32_t q = 0; q < B; ++q) nxt[q] = base + B + q < n ? x[base + B + q] : 0u;
         const uint32_t m = min(B, n - base);
-        if (var_thread) {
+        if (var_wave) {
 #pragma unroll
-            for (uint32_t t = 0; t < B; ++t)
-                if (t < m) st.add_var(cur[t]);
+            for (uint32_t q = 0; q < B; ++q)
+                if (q < m) st.add_var(cur[q]);
         } else {
 #pragma unroll
-            for (uint32_t t = 0; t < B; ++t)
-                if (t < m) st.add_p2(cur[t]);
+            for (uint32_t q = 0; q < B; ++q)
+                if (q < m) st.add_p2(cur[q]);
         }
 #pragma unroll
-        for (uint32_t t = 0; t < B; ++t) cur[t] = nxt[t];
+        for (uint32_t q = 0; q < B; ++q) cur[q] = nxt[q];
     }
-    if (var_thread)
+    if (var_wave)
         out[jb.out_idx].var = d2u16(st.var);
     else
         out[jb.out_idx].median = d2u16(st.h[2]);
@@ -684,6 +735,9 @@ struct BucketArgs {
         }                                                                     \
     } while (0)
 
+constexpr uint32_t JOB_KEPT = 0x8000u;        // jobinfo flag: the representative's group is kept
+constexpr uint32_t JOB_COUNT_MASK = 0x1FFFu;  // jobinfo: best-run length (<= CAP)
+
 struct SubLds {
     uint64_t* hi;      // [CAP] element: rem<<16|func   (kept: 1<<63 | h43<<16 | avg)
     uint64_t* lo;      // [CAP] element: s<<36|i<<16|off (kept, no job: func|mean|median|var)
@@ -793,11 +847,10 @@ __device__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint32_t c, const Seq
             const uint32_t s = (uint32_t)(lo >> 36);
             flags[s] = 1;
             if ((uint32_t)t >= rb && (uint32_t)t < rb + best_c) {
-                const uint32_t len = meta[s].len;
-                sum += len;
+                sum += (uint32_t)(L.hi[idx[t]] >> 48);  // len mod 2^16 is all the u16 sum keeps
                 const uint32_t q = rb + best_c - 1 - t;  // visit position (reverse ordinal)
-                if (q == 0) lr0 = len;
-                if (q == 1) lr1 = len;
+                if (q == 0) lr0 = s;
+                if (q == 1) lr1 = s;
             }
         }
     }
@@ -812,7 +865,7 @@ __device__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint32_t c, const Seq
     r.median = 0;
     r.var = 0;
     if (best_c <= 2) {
-        const uint32_t lr[2] = {lr0, lr1};
+        const uint32_t lr[2] = {meta[lr0].len, best_c == 2 ? meta[lr1].len : 0u};
         stats_small(r, lr, best_c);
     }
     return r;
@@ -874,9 +927,9 @@ __device__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const SeqMe
         const uint32_t o = (uint32_t)(lo & 0xFFFFu);
         vmin = min(vmin, o);
         vmax = max(vmax, o);
-        const uint32_t s = (uint32_t)(lo >> 36);
-        flags[s] = 1;
-        if ((uint32_t)(L.hi[j] & 0xFFFFu) == cand) sum += meta[s].len;
+        flags[lo >> 36] = 1;
+        const uint64_t hj = L.hi[j];
+        if ((uint32_t)(hj & 0xFFFFu) == cand) sum += (uint32_t)(hj >> 48);
     }
     vmin = wave_min(vmin);
     vmax = wave_max(vmax);
@@ -980,11 +1033,10 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
             L.glist[G + (v & 0x1FFFu)] = (uint16_t)j;
         } else if (in && cnt == 1) {  // group of one: always kept (1 >= 0.8), median 0, var 0
             const uint64_t H = L.hi[j], Lo = L.lo[j];
-            const uint32_t s = (uint32_t)(Lo >> 36);
-            const uint32_t len = A.meta[s].len;
-            A.flags[s] = 1;
-            L.hi[j] = kept_hi(hprefix | (H >> 16), (uint32_t)(Lo & 0xFFFFu));
-            L.lo[j] = kept_lo((uint32_t)(H & 0xFFFFu), d2u16((double)(uint16_t)len / 1.0), 0, 0);
+            A.flags[Lo >> 36] = 1;
+            L.hi[j] = kept_hi(hprefix | ((H >> 16) & 0xFFFFFFFFull), (uint32_t)(Lo & 0xFFFFu));
+            L.lo[j] = kept_lo((uint32_t)(H & 0xFFFFu), d2u16((double)(uint16_t)(H >> 48) / 1.0), 0, 0);
+            L.rank[j] = 0xFFFFu;  // singleton marker
         }
         M += tot >> 13;
         G += tot & 0x1FFFu;
@@ -997,19 +1049,20 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
         if ((e & 0xFFFFu) > 1) L.order[L.goff[e >> 16] + L.rank[j]] = (uint16_t)j;
     }
     __syncthreads();
-    uint32_t* jobinfo = L.tab;        // per representative: best-run start << 16 | best count
+    uint32_t* jobinfo = L.tab;        // per representative: best-run start << 16 | KEPT | best count
     uint32_t* fmean = L.tab + CAP;    // per representative: func | mean << 16
-    for (uint32_t j = tid; j < n; j += nt) jobinfo[j] = 0;
+    for (uint32_t j = tid; j < n; j += nt) jobinfo[j] = L.rank[j] == 0xFFFFu ? JOB_KEPT : 0u;
     __syncthreads();
     SKM_STAMP(5);
     auto stage = [&](const GRes& r, uint32_t rep, uint32_t a) {
         if (!r.kept) return;
-        const uint64_t h43 = hprefix | (L.hi[rep] >> 16);
+        const uint64_t h43 = hprefix | ((L.hi[rep] >> 16) & 0xFFFFFFFFull);
         L.hi[rep] = kept_hi(h43, r.avg);
         if (r.cbest >= 3) {
-            jobinfo[rep] = ((a + r.rb) << 16) | r.cbest;
+            jobinfo[rep] = ((a + r.rb) << 16) | JOB_KEPT | r.cbest;
             fmean[rep] = r.best_f | ((uint32_t)r.mean << 16);
         } else {
+            jobinfo[rep] = JOB_KEPT;
             L.lo[rep] = kept_lo(r.best_f, r.mean, r.median, r.var);
         }
     };
@@ -1047,23 +1100,26 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
     }
     __syncthreads();
     SKM_STAMP(7);
-    // 6. emit kept k-mers (one atomic per chunk) and chain jobs with their protein lengths
+    // 6. emit kept k-mers (one atomic per chunk) and chain jobs; the chunk's protein lengths are
+    //    gathered by the whole workgroup (job table: lens prefix | representative, in glist)
     unsigned long long* s_base = reinterpret_cast<unsigned long long*>(L.wave + 36);
+    uint32_t* jtab = reinterpret_cast<uint32_t*>(L.glist);
     for (uint32_t c0 = 0; c0 < n; c0 += nt) {
         const uint32_t j = c0 + tid;
-        const uint64_t H = j < n ? L.hi[j] : 0;
-        const bool kept = (H >> 63) != 0;
-        const uint32_t jb = kept ? jobinfo[j] : 0u;
-        const uint32_t jn = jb & 0xFFFFu;
+        const uint32_t jb = j < n ? jobinfo[j] : 0u;
+        const bool kept = (jb & JOB_KEPT) != 0;
+        const uint64_t H = kept ? L.hi[j] : 0;
+        const uint32_t jn = jb & JOB_COUNT_MASK;
         uint32_t K, JL;
         const uint32_t kpos = wg_exclusive_scan(kept ? 1u : 0u, L.wave, K);
         const uint32_t jl = wg_exclusive_scan(jn ? ((jn << 11) | 1u) : 0u, L.wave, JL);
         if (K == 0) continue;
+        const uint32_t njob = JL & 0x7FFu, nlens = JL >> 11;
         if (tid == 0) {
             s_base[0] = atomicAdd(&A.ctr[0], (unsigned long long)K);
-            if (JL) {
-                s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)(JL & 0x7FFu));
-                s_base[2] = atomicAdd(&A.ctr[4], (unsigned long long)(JL >> 11));
+            if (njob) {
+                s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)njob);
+                s_base[2] = atomicAdd(&A.ctr[4], (unsigned long long)nlens);
             }
         }
         __syncthreads();
@@ -1072,18 +1128,31 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
             if (jn) {
                 const uint32_t fm = fmean[j];
                 write_kept(A, o, H, kept_lo(fm & 0xFFFFu, fm >> 16, 0, 0));
-                const uint64_t loff = s_base[2] + (jl >> 11);
                 Job jbr;
-                jbr.lens_off = loff;
+                jbr.lens_off = s_base[2] + (jl >> 11);
                 jbr.n = jn;
                 jbr.out_idx = (uint32_t)o;
                 A.jobs[s_base[1] + (jl & 0x7FFu)] = jbr;
-                const uint32_t start = jb >> 16;
-                for (uint32_t t = 0; t < jn; ++t)  // reverse ordinal order
-                    A.lens[loff + t] = A.meta[L.lo[L.order[start + jn - 1 - t]] >> 36].len;
+                jtab[jl & 0x7FFu] = ((jl >> 11) << 16) | j;
             } else {
                 write_kept(A, o, H, L.lo[j]);
             }
+        }
+        __syncthreads();
+        for (uint32_t q = tid; q < nlens; q += nt) {
+            uint32_t lo_j = 0, hi_j = njob;  // last job whose lens prefix <= q
+            while (hi_j - lo_j > 1) {
+                const uint32_t mid = (lo_j + hi_j) >> 1;
+                if ((jtab[mid] >> 16) <= q)
+                    lo_j = mid;
+                else
+                    hi_j = mid;
+            }
+            const uint32_t ent = jtab[lo_j];
+            const uint32_t jbq = jobinfo[ent & 0xFFFFu];
+            const uint32_t jnq = jbq & JOB_COUNT_MASK, start = jbq >> 16;
+            const uint32_t t = q - (ent >> 16);
+            A.lens[s_base[2] + q] = A.meta[L.lo[L.order[start + jnq - 1 - t]] >> 36].len;  // reverse ordinal
         }
         __syncthreads();
     }
@@ -1094,13 +1163,13 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
     __shared__ uint64_t s_hi[CAP];
     __shared__ uint64_t s_lo[CAP];
     __shared__ uint32_t s_tab[TAB];
-    __shared__ uint16_t s_slot[CAP];
-    __shared__ uint16_t s_rank[CAP];
-    __shared__ uint16_t s_goff[CAP];
-    __shared__ uint16_t s_glist[CAP];
-    __shared__ uint16_t s_order[CAP];
+    __align__(16) __shared__ uint16_t s_slot[CAP];
+    __align__(16) __shared__ uint16_t s_rank[CAP];
+    __align__(16) __shared__ uint16_t s_goff[CAP];
+    __align__(16) __shared__ uint16_t s_glist[CAP];
+    __align__(16) __shared__ uint16_t s_order[CAP];
     __shared__ uint32_t s_sub[(1 << MAX_B2) + 1];
-    __shared__ uint16_t s_big[CAP / 2];
+    __align__(16) __shared__ uint16_t s_big[CAP / 2];
     __shared__ __align__(16) uint32_t s_wave[48];
     __shared__ uint32_t s_nbig;
     __shared__ uint64_t s_tlast;
@@ -1230,6 +1299,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
             const uint32_t g = c0 + j;
             if (g < n) {
                 make_elem(src[g], A.pos_bits, pos_mask, A.pos_base, A.blk2seq, A.meta, s_hi[j], s_lo[j]);
+                s_hi[j] &= 0x0000FFFFFFFFFFFFull;
             } else {
                 s_hi[j] = ~0ull;
                 s_lo[j] = ~0ull;
@@ -1482,7 +1552,7 @@ struct skm_build {
     DevBuf d_hist, d_offs, d_partial, d_rbbase, d_bstart32, d_bstart, d_owner_start;
     DevBuf d_recs, d_tmp;
     DevBuf d_keys, d_data, d_ctr, d_flags, d_dfunc, d_swf, d_ovf, d_ovf_hi, d_ovf_lo, d_ovf_heads, d_ovf_job, d_ovf_fm;
-    DevBuf d_jobs, d_lens, d_stamps;
+    DevBuf d_jobs, d_lens, d_stamps, d_job_hist, d_job_offs, d_jobs_sorted;
     bool stamps = false;
     uint64_t jobs_cap = 0, lens_cap = 0, n_jobs = 0, n_lens = 0;
     uint32_t n_overflow = 0;
@@ -1629,9 +1699,24 @@ void run_pipeline(skm_build* b) {
     b->n_jobs = ctr[3];
     b->n_lens = ctr[4];
     SKM_CHECK(ctr[3] <= b->jobs_cap && ctr[4] <= b->lens_cap, SKM_E_OOM, "chain buffers overflowed");
-    if (b->n_jobs)
-        hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(2 * b->n_jobs, 256)), dim3(256), 0, st, b->d_jobs.as<Job>(),
-                           (uint64_t)b->n_jobs, b->d_lens.as<uint32_t>(), b->d_data.as<skm_stored_kmer_data>());
+    if (b->n_jobs) {
+        const uint64_t nj = b->n_jobs;
+        const uint32_t nwg = (uint32_t)std::min<uint64_t>(1024, ceil_div(nj, 4096));
+        const uint64_t chunk = ceil_div(nj, nwg);
+        b->d_job_hist.ensure(4ull * nwg * JOB_CLASSES);
+        b->d_job_offs.ensure(8ull * nwg * JOB_CLASSES);
+        b->d_jobs_sorted.ensure(sizeof(Job) * nj);
+        hipLaunchKernelGGL(k_job_count, dim3(nwg), dim3(JOB_WG), 0, st, b->d_jobs.as<Job>(), nj, chunk,
+                           b->d_job_hist.as<uint32_t>());
+        hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(64), 0, st, b->d_job_hist.as<uint32_t>(), nwg,
+                           b->d_job_offs.as<uint64_t>());
+        hipLaunchKernelGGL(k_job_scatter, dim3(nwg), dim3(JOB_WG), 0, st, b->d_jobs.as<Job>(), nj, chunk,
+                           b->d_job_offs.as<uint64_t>(), b->d_jobs_sorted.as<Job>());
+        const uint64_t threads = ceil_div(nj, 64) * 128;
+        hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, st,
+                           b->d_jobs_sorted.as<Job>(), nj, b->d_lens.as<uint32_t>(),
+                           b->d_data.as<skm_stored_kmer_data>());
+    }
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[6], st));
     // ---- 7. stats ----
