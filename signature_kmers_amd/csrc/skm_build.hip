@@ -43,12 +43,12 @@ constexpr int EX_THREADS = 512;        // extract workgroup
 constexpr int EX_POS_PER_THREAD = 16;  // windows per thread per step (one 16-byte load + halo)
 constexpr int EX_MAX_WG = 512;         // rows of the histogram matrix
 constexpr int SCAN_ROWS = 32;          // rows per column-scan block
-constexpr int BP_THREADS = 1024;       // bucket-process workgroup (one per CU: LDS ~150 KB)
-constexpr int CAP = 4096;              // LDS sub-bucket capacity (records)
-constexpr int TAB_BITS = 13;
+constexpr int BP_THREADS = 512;        // bucket-process workgroup: two per CU (LDS ~79 KB each)
+constexpr int CAP = 2048;              // LDS sub-bucket capacity (records)
+constexpr int TAB_BITS = 12;
 constexpr int TAB = 1 << TAB_BITS;     // LDS hash slots per sub-bucket (load <= 0.5)
-constexpr int SUB_TARGET = 2048;       // target records per level-2 sub-bucket
-constexpr int MAX_B2 = 12;             // <= 4096 sub-buckets per level-1 bucket
+constexpr int SUB_TARGET = 1024;       // target records per level-2 sub-bucket
+constexpr int MAX_B2 = 11;             // <= 2048 sub-buckets per level-1 bucket
 
 struct SeqMeta {        // 16 bytes, one dwordx4 load
     uint64_t pstart;    // first residue in the packed buffer
@@ -244,7 +244,7 @@ __device__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t& to
 // median, running variance) need the run in REVERSE ordinal order; when the run has >= 3
 // members they are deferred to k_chains (one thread per chain), everything else is done here.
 // ------------------------------------------------------------------------------------------
-constexpr int SMALLC = 16;   // thread-level groups up to this size, wave-level above
+constexpr int SMALLC = 8;    // thread-level groups up to this size, wave-level above
 
 struct Job {                 // one deferred P^2 / variance chain
     uint64_t lens_off;       // protein lengths in visit order (reverse ordinal) at lens[lens_off..]
@@ -736,7 +736,7 @@ struct BucketArgs {
     } while (0)
 
 constexpr uint32_t JOB_KEPT = 0x8000u;        // jobinfo flag: the representative's group is kept
-constexpr uint32_t JOB_COUNT_MASK = 0x1FFFu;  // jobinfo: best-run length (<= CAP)
+constexpr uint32_t JOB_COUNT_MASK = 0x0FFFu;  // jobinfo: best-run length (<= CAP)
 
 struct SubLds {
     uint64_t* hi;      // [CAP] element: rem<<16|func   (kept: 1<<63 | h43<<16 | avg)
@@ -751,6 +751,7 @@ struct SubLds {
     uint32_t* wave;    // scan scratch (>= 40 words, 16-byte aligned)
     uint32_t* nbig;
     uint64_t* tlast;   // stamp scratch
+    uint32_t* ccnt;    // [8] size-class counters
 };
 
 __device__ __forceinline__ uint64_t kept_hi(uint64_t h43, uint32_t avg) { return (1ull << 63) | (h43 << 16) | avg; }
@@ -935,15 +936,34 @@ __device__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const SeqMe
     vmax = wave_max(vmax);
     sum = wave_sum(sum);
     const uint32_t k = c / 2;
+    // invariant: answer in [vmin, vmax]; each pass counts 8 pivots at once (9-way split)
     while (vmin < vmax) {
-        const uint32_t mid = (vmin + vmax) >> 1;
-        uint32_t cnt = 0;
-        for (uint32_t t = lane; t < c; t += 64) cnt += (uint32_t)(L.lo[L.order[a + t]] & 0xFFFFu) <= mid;
-        cnt = wave_sum(cnt);
-        if (cnt >= k + 1)
-            vmax = mid;
-        else
-            vmin = mid + 1;
+        const uint32_t span = vmax - vmin;
+        uint32_t piv[8], cnt[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            piv[q] = vmin + (uint32_t)(((uint64_t)span * (uint64_t)(q + 1)) / 9u);
+            cnt[q] = 0;
+        }
+        for (uint32_t t = lane; t < c; t += 64) {
+            const uint32_t o = (uint32_t)(L.lo[L.order[a + t]] & 0xFFFFu);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) cnt[q] += o <= piv[q];
+        }
+        uint32_t nlo = vmin, nhi = vmax;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            cnt[q] = wave_sum(cnt[q]);
+        }
+        // smallest pivot with count >= k+1 bounds from above; the previous pivot from below
+#pragma unroll
+        for (int q = 7; q >= 0; --q)
+            if (cnt[q] >= k + 1) nhi = min(nhi, piv[q]);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (cnt[q] < k + 1) nlo = max(nlo, piv[q] + 1);
+        vmin = nlo;
+        vmax = nhi;
     }
     r.avg = vmin;
     r.mean = d2u16((double)(uint16_t)sum / (double)nb);
@@ -961,25 +981,55 @@ __device__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const SeqMe
         w += (uint32_t)__popcll(m);
         wave_sync();
     }
-    // sort order[a..a+nb) by ordinal: bitonic for arbitrary n (only ascending compare-exchanges,
-    // missing partners act as +infinity)
-    uint32_t Np = 1;
-    while (Np < nb) Np <<= 1;
-    for (uint32_t kk = 2; kk <= Np; kk <<= 1) {
-        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-            const bool flip = jj == (kk >> 1);
-            for (uint32_t t = lane; t < Np / 2; t += 64) {
-                const uint32_t i = 2 * t - (t & (jj - 1));
-                const uint32_t l = flip ? (i ^ (kk - 1)) : (i + jj);
-                if (l < nb) {
-                    const uint16_t ia = L.order[a + i], ib = L.order[a + l];
-                    if (L.lo[ia] > L.lo[ib]) {
-                        L.order[a + i] = ib;
-                        L.order[a + l] = ia;
-                    }
+    // sort order[a..a+nb) by ordinal
+    if (nb <= 64) {
+        // one element per lane, bitonic network over shuffles; missing lanes hold +inf
+        uint64_t key = ~0ull;
+        uint32_t idx = 0;
+        if (lane < nb) {
+            idx = L.order[a + lane];
+            key = L.lo[idx];
+        }
+#pragma unroll
+        for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                const uint64_t ok = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), jj, 64) << 32) |
+                                    (uint32_t)__shfl_xor((int)(uint32_t)key, jj, 64);
+                const uint32_t oi = (uint32_t)__shfl_xor((int)idx, jj, 64);
+                const bool lower = (lane & jj) == 0;
+                const bool asc = (lane & kk) == 0;
+                const bool take_min = lower == asc;
+                const bool other_smaller = ok < key;
+                if (take_min ? other_smaller : !other_smaller && ok != key) {
+                    key = ok;
+                    idx = oi;
                 }
             }
-            wave_sync();
+        }
+        wave_sync();
+        if (lane < nb) L.order[a + lane] = (uint16_t)idx;
+        wave_sync();
+    } else {
+        // bitonic for arbitrary n (only ascending compare-exchanges; missing partners = +inf)
+        uint32_t Np = 1;
+        while (Np < nb) Np <<= 1;
+        for (uint32_t kk = 2; kk <= Np; kk <<= 1) {
+            for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                const bool flip = jj == (kk >> 1);
+                for (uint32_t t = lane; t < Np / 2; t += 64) {
+                    const uint32_t i = 2 * t - (t & (jj - 1));
+                    const uint32_t l = flip ? (i ^ (kk - 1)) : (i + jj);
+                    if (l < nb) {
+                        const uint16_t ia = L.order[a + i], ib = L.order[a + l];
+                        if (L.lo[ia] > L.lo[ib]) {
+                            L.order[a + i] = ib;
+                            L.order[a + l] = ia;
+                        }
+                    }
+                }
+                wave_sync();
+            }
         }
     }
     return r;
@@ -1066,22 +1116,48 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
             L.lo[rep] = kept_lo(r.best_f, r.mean, r.median, r.var);
         }
     };
-    // 5. thread-level groups; large ones queued for waves
+    // 5. groups by size class so that a wave runs one code path: [2], [3,4], [5,8] by threads,
+    //    (8, CAP] by waves.  `big` holds the class-ordered group list.
+    uint32_t* ccnt = L.ccnt;
+    if (tid < 8) ccnt[tid] = 0;
+    __syncthreads();
     for (uint32_t g = tid; g < G; g += nt) {
+        const uint32_t a = L.goff[L.glist[g]];
+        const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
+        const uint32_t cls = c <= 2 ? 0 : c <= 4 ? 1 : c <= (uint32_t)SMALLC ? 2 : 4;
+        atomicAdd(&ccnt[cls], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (int q = 0; q < 5; ++q) {
+            const uint32_t t = ccnt[q];
+            ccnt[q] = run;
+            run += t;
+        }
+        *L.nbig = G - ccnt[4];  // start of the wave-level class
+    }
+    __syncthreads();
+    for (uint32_t g = tid; g < G; g += nt) {
+        const uint32_t a = L.goff[L.glist[g]];
+        const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
+        const uint32_t cls = c <= 2 ? 0 : c <= 4 ? 1 : c <= (uint32_t)SMALLC ? 2 : 4;
+        L.big[atomicAdd(&ccnt[cls], 1u)] = (uint16_t)g;
+    }
+    __syncthreads();
+    const uint32_t nsmall = G - *L.nbig;  // groups handled by threads (classes 0..3)
+    for (uint32_t q = tid; q < nsmall; q += nt) {
+        const uint32_t g = L.big[q];
         const uint32_t rep = L.glist[g];
         const uint32_t a = L.goff[rep];
         const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
-        if (c > (uint32_t)SMALLC) {
-            L.big[atomicAdd(L.nbig, 1u)] = (uint16_t)g;
-            continue;
-        }
         GRes r;
-        if (c <= 4)
+        if (c <= 2)
+            r = lgroup_thread<2>(L, a, c, A.meta, A.flags);
+        else if (c <= 4)
             r = lgroup_thread<4>(L, a, c, A.meta, A.flags);
-        else if (c <= 8)
-            r = lgroup_thread<8>(L, a, c, A.meta, A.flags);
         else
-            r = lgroup_thread<16>(L, a, c, A.meta, A.flags);
+            r = lgroup_thread<8>(L, a, c, A.meta, A.flags);
         stage(r, rep, a);
     }
     __syncthreads();
@@ -1090,7 +1166,7 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
         const uint32_t nbig = *L.nbig;
         const uint32_t wave = tid >> 6, nwaves = nt >> 6;
         for (uint32_t bi = wave; bi < nbig; bi += nwaves) {
-            const uint32_t g = L.big[bi];
+            const uint32_t g = L.big[nsmall + bi];
             const uint32_t rep = L.glist[g];
             const uint32_t a = L.goff[rep];
             const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
@@ -1159,7 +1235,7 @@ __device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const 
     SKM_STAMP(8);
 }
 
-__global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
+__global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) {
     __shared__ uint64_t s_hi[CAP];
     __shared__ uint64_t s_lo[CAP];
     __shared__ uint32_t s_tab[TAB];
@@ -1173,7 +1249,9 @@ __global__ __launch_bounds__(BP_THREADS) void k_bucket_process(BucketArgs A) {
     __shared__ __align__(16) uint32_t s_wave[48];
     __shared__ uint32_t s_nbig;
     __shared__ uint64_t s_tlast;
+    __shared__ uint32_t s_ccnt[8];
     SubLds L;
+    L.ccnt = s_ccnt;
     L.tlast = &s_tlast;
     if (threadIdx.x == 0) s_tlast = __builtin_amdgcn_s_memtime();
     L.hi = s_hi;
