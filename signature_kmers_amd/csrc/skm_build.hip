@@ -126,24 +126,26 @@ struct SigStats {
 #pragma unroll
             for (int i = 1; i < 5; ++i)
                 if (i >= cell) act[i] += 1;
-            // desired positions accumulate exact multiples of 1/4: closed form is bit-identical
-            const double nstep = (double)(cnt - 5);
-            const double des[4] = {0.0, 2.0 + nstep * 0.25, 3.0 + nstep * 0.5, 4.0 + nstep * 0.75};
+            // Desired positions accumulate exact multiples of 1/4 (desired_i = i+1 + (cnt-5)*i/4),
+            // actual positions are integers: d, dp, dm and the adjust decision are exact in
+            // quarter units, so only the height update itself needs fp64 (bit-identical).
+            const int32_t k4 = (int32_t)(cnt - 5);
 #pragma unroll
             for (int i = 1; i <= 3; ++i) {
-                const double d = des[i] - (double)act[i];
-                const double dp = (double)act[i + 1] - (double)act[i];
-                const double dm = (double)act[i - 1] - (double)act[i];
-                if ((d >= 1. && dp > 1.) || (d <= -1. && dm < -1.)) {
+                const int32_t d4 = 4 * (i + 1) + k4 * i - 4 * act[i];  // 4*d
+                const int32_t dpi = act[i + 1] - act[i];
+                const int32_t dmi = act[i - 1] - act[i];
+                if ((d4 >= 4 && dpi > 1) || (d4 <= -4 && dmi < -1)) {
+                    const double dp = (double)dpi, dm = (double)dmi;
                     const double hp = (h[i + 1] - h[i]) / dp;
                     const double hm = (h[i - 1] - h[i]) / dm;
-                    const short sign_d = d > 0 ? 1 : -1;  // d / |d| with |d| >= 1: exactly +-1
+                    const short sign_d = d4 > 0 ? 1 : -1;  // d / |d|, exactly +-1
                     const double hh = h[i] + sign_d / (dp - dm) * ((sign_d - dm) * hp + (dp - sign_d) * hm);
                     if (h[i - 1] < hh && hh < h[i + 1]) {
                         h[i] = hh;
                     } else {
-                        if (d > 0) h[i] += hp;
-                        if (d < 0) h[i] -= hm;
+                        if (d4 > 0) h[i] += hp;
+                        if (d4 < 0) h[i] -= hm;
                     }
                     act[i] += sign_d;
                 }
@@ -293,15 +295,15 @@ __device__ __forceinline__ void reg_sort(uint32_t* v) {
             }
 }
 
-__device__ __forceinline__ void stats_small(GRes& r, const uint32_t* lens_rev, uint32_t n) {
+__device__ __forceinline__ void stats_small(GRes& r, uint32_t x0, uint32_t x1, uint32_t n) {
     // n <= 2 samples in visit order: P^2 heights[2] is still 0; the variance recurrence of SigStats
     // after two samples is 0*(1)/2 + (x2 - mean2)^2 / 1 with mean2 over the u16 sum.
     r.median = 0;
     r.var = 0;
     if (n == 2) {
-        const uint16_t sum = (uint16_t)(lens_rev[0] + lens_rev[1]);
+        const uint16_t sum = (uint16_t)(x0 + x1);
         const double mean = (double)sum / 2.0;
-        const double tmp = (double)lens_rev[1] - mean;
+        const double tmp = (double)x1 - mean;
         const double v = 0.0 * 1.0 / 2.0 + tmp * tmp / 1.0;
         r.var = d2u16(v);
     }
@@ -369,10 +371,7 @@ __device__ GRes group_thread(const V& v, uint64_t a, uint32_t c, const SeqMeta* 
     r.mean = d2u16((double)(uint16_t)sum / (double)best_c);
     r.median = 0;
     r.var = 0;
-    if (best_c <= 2) {
-        const uint32_t lr[2] = {lr0, lr1};
-        stats_small(r, lr, best_c);
-    }
+    if (best_c <= 2) stats_small(r, lr0, lr1, best_c);
     return r;
 }
 
@@ -795,7 +794,7 @@ __device__ __forceinline__ void reg_sort_pairs(uint64_t* k, uint32_t* v) {
 // Thread-level group (c <= N members at order[a..a+c)): members sorted in registers by
 // (func, ordinal); the sorted member list is written back so the best run is contiguous.
 template <int N>
-__device__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint32_t c, const SeqMeta* __restrict__ meta,
+__device__ __forceinline__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint32_t c, const SeqMeta* __restrict__ meta,
                               uint8_t* __restrict__ flags) {
     GRes r;
     r.kept = false;
@@ -865,10 +864,7 @@ __device__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint32_t c, const Seq
     r.mean = d2u16((double)(uint16_t)sum / (double)best_c);
     r.median = 0;
     r.var = 0;
-    if (best_c <= 2) {
-        const uint32_t lr[2] = {meta[lr0].len, best_c == 2 ? meta[lr1].len : 0u};
-        stats_small(r, lr, best_c);
-    }
+    if (best_c <= 2) stats_small(r, meta[lr0].len, best_c == 2 ? meta[lr1].len : 0u, best_c);
     return r;
 }
 
@@ -881,8 +877,87 @@ __device__ __forceinline__ void wave_sync() {
 // Wave-level group (c > SMALLC).  Best function by Boyer-Moore majority: if any function has
 // >= 80 % of the occurrences it is the strict majority, otherwise the group is cut anyway.
 // The best-function members are compacted to order[a..a+cbest) and sorted by ordinal.
-__device__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const SeqMeta* __restrict__ meta,
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    return ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64) << 32) |
+           (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
+}
+
+// Ascending bitonic sort of one (key, val) per lane across the 64 lanes.
+__device__ __forceinline__ void wave_sort64(uint64_t& key, uint32_t& val) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+            const uint64_t ok = shfl_xor_u64(key, jj);
+            const uint32_t ov = (uint32_t)__shfl_xor((int)val, jj, 64);
+            const bool take_min = ((lane & jj) == 0) == ((lane & kk) == 0);
+            const bool sw = take_min ? (ok < key) : (ok > key);
+            if (sw) {
+                key = ok;
+                val = ov;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void bm_combine(uint32_t& cand, uint32_t& cc) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t oc = (uint32_t)__shfl_xor((int)cand, d, 64), on = (uint32_t)__shfl_xor((int)cc, d, 64);
+        if (oc == cand) {
+            cc += on;
+        } else if (cc >= on) {
+            cc -= on;
+        } else {
+            cand = oc;
+            cc = on - cc;
+        }
+    }
+    cand = (uint32_t)__shfl((int)cand, 0, 64);
+}
+
+// Wave-level group with c <= 64: one member per lane, everything in registers.
+__device__ __forceinline__ GRes lgroup_wave64(const SubLds& L, uint32_t a, uint32_t c, uint8_t* __restrict__ flags) {
+    const uint32_t lane = threadIdx.x & 63u;
+    GRes r;
+    r.kept = false;
+    const bool v = lane < c;
+    const uint32_t j = v ? L.order[a + lane] : 0u;
+    const uint64_t hj = v ? L.hi[j] : 0ull, lj = v ? L.lo[j] : 0ull;
+    const uint32_t f = v ? (uint32_t)(hj & 0xFFFFu) : 0xFFFFFFFFu;
+    uint32_t cand = f, cc = v ? 1u : 0u;
+    bm_combine(cand, cc);
+    const bool best = v && f == cand;
+    const uint32_t nb = (uint32_t)__popcll(__ballot(best));
+    if ((float)nb < float(c) * 0.8f) return r;
+    r.kept = true;
+    r.best_f = cand;
+    r.cbest = nb;
+    r.rb = 0;
+    if (v) flags[lj >> 36] = 1;
+    const uint32_t sum = wave_sum(best ? (uint32_t)(hj >> 48) : 0u);
+    r.mean = d2u16((double)(uint16_t)sum / (double)nb);
+    r.median = 0;
+    r.var = 0;
+    // avg_from_end: sort the offsets across lanes, take element c/2
+    uint64_t ok = v ? (lj & 0xFFFFull) : 0x10000ull;
+    uint32_t dummy = 0;
+    wave_sort64(ok, dummy);
+    r.avg = (uint32_t)__shfl((int)(uint32_t)ok, (int)(c / 2), 64);
+    // best-function members by ordinal
+    uint64_t key = best ? lj : ~0ull;
+    uint32_t idx = j;
+    wave_sort64(key, idx);
+    wave_sync();
+    if (lane < nb) L.order[a + lane] = (uint16_t)idx;
+    wave_sync();
+    return r;
+}
+
+__device__ __forceinline__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const SeqMeta* __restrict__ meta,
                             uint8_t* __restrict__ flags) {
+    if (c <= 64) return lgroup_wave64(L, a, c, flags);
     const uint32_t lane = threadIdx.x & 63u;
     GRes r;
     r.kept = false;
@@ -899,19 +974,7 @@ __device__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const SeqMe
             --cc;
         }
     }
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t oc = (uint32_t)__shfl_xor((int)cand, d, 64), on = (uint32_t)__shfl_xor((int)cc, d, 64);
-        if (oc == cand) {
-            cc += on;
-        } else if (cc >= on) {
-            cc -= on;
-        } else {
-            cand = oc;
-            cc = on - cc;
-        }
-    }
-    cand = (uint32_t)__shfl((int)cand, 0, 64);
+    bm_combine(cand, cc);
     uint32_t nb = 0;
     for (uint32_t t = lane; t < c; t += 64) nb += (uint32_t)(L.hi[L.order[a + t]] & 0xFFFFu) == cand;
     nb = wave_sum(nb);
@@ -1038,7 +1101,7 @@ __device__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const SeqMe
 // One sub-bucket of n <= CAP records: LDS hash grouping (ranks from the insert atomics give a
 // counting sort by group), singletons resolved immediately, multi-occurrence groups by threads
 // (small) or waves (large); no workgroup-wide sort.
-__device__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const BucketArgs& A, uint64_t hprefix,
+__device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const BucketArgs& A, uint64_t hprefix,
                             uint64_t pos_mask, const SubLds& L) {
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t EMPTY = 0xFFFFFFFFu;

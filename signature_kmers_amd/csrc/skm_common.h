@@ -72,13 +72,20 @@ SKM_HD uint8_t code_residue(uint32_t code) {
 }
 
 // base-40 code -> little-endian raw key (byte 0 = first residue, the most significant digit).
+// Split at 40^4 so the digit loop runs in 32-bit arithmetic.
 SKM_HD uint64_t decode_key(uint64_t k) {
+    const uint64_t q = k / 2560000u;                       // 40^4
+    uint32_t hi4 = (uint32_t)q, lo4 = (uint32_t)(k - q * 2560000u);
     uint64_t raw = 0;
-    for (int j = 7; j >= 0; --j) {
-        uint64_t q = k / 40u;
-        uint32_t d = (uint32_t)(k - q * 40u);
-        k = q;
-        raw |= (uint64_t)code_residue(d) << (8 * j);
+    for (int j = 7; j >= 4; --j) {
+        const uint32_t qq = lo4 / 40u;
+        raw |= (uint64_t)code_residue(lo4 - qq * 40u) << (8 * j);
+        lo4 = qq;
+    }
+    for (int j = 3; j >= 0; --j) {
+        const uint32_t qq = hi4 / 40u;
+        raw |= (uint64_t)code_residue(hi4 - qq * 40u) << (8 * j);
+        hi4 = qq;
     }
     return raw;
 }
