@@ -246,6 +246,11 @@ __device__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t& to
 // median, running variance) need the run in REVERSE ordinal order; when the run has >= 3
 // members they are deferred to k_chains (one thread per chain), everything else is done here.
 // ------------------------------------------------------------------------------------------
+// Job.lens_off selector (top 2 bits): protein lengths live in the chain-lengths buffer, or in the
+// (already consumed) record slots of the sub-bucket that produced the job, viewed as u32.
+constexpr uint64_t LENS_SEL_SHIFT = 62;
+constexpr uint64_t LENS_IN_RECS = 1, LENS_IN_TMP = 2;  // 0: chain-lengths buffer (overflow path)
+constexpr uint64_t LENS_OFF_MASK = (1ull << LENS_SEL_SHIFT) - 1;
 constexpr int SMALLC = 8;    // thread-level groups up to this size, wave-level above
 
 struct Job {                 // one deferred P^2 / variance chain
@@ -520,36 +525,33 @@ __global__ __launch_bounds__(JOB_WG) void k_job_scatter(const Job* __restrict__ 
 }
 
 __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, uint64_t njobs,
-                                                const uint32_t* __restrict__ lens, skm_stored_kmer_data* __restrict__ out) {
+                                                const uint32_t* __restrict__ lens, const uint32_t* __restrict__ recs32,
+                                                const uint32_t* __restrict__ tmp32,
+                                                skm_stored_kmer_data* __restrict__ out) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t wave = t >> 6;
     const uint64_t j = (wave >> 1) * 64 + (t & 63u);
     const bool var_wave = (wave & 1u) != 0;
     if (j >= njobs) return;
     const Job jb = jobs[j];
-    const uint32_t* x = lens + jb.lens_off;
+    const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
+    const uint32_t* x = (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : lens) + (jb.lens_off & LENS_OFF_MASK);
     const uint32_t n = jb.n;
     SigStats st;
     st.init();
-    constexpr uint32_t B = 16;
-    uint32_t cur[B], nxt[B];
+    constexpr uint32_t B = 16;  // prefetch distance (shift-register queue keeps the loop body small)
+    uint32_t q[B];
 #pragma unroll
-    for (uint32_t q = 0; q < B; ++q) cur[q] = q < n ? x[q] : 0u;
-    for (uint32_t base = 0; base < n; base += B) {
+    for (uint32_t i = 0; i < B; ++i) q[i] = i < n ? x[i] : 0u;
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t v = q[0];
 #pragma unroll
-        for (uint32_t q = 0; q < B; ++q) nxt[q] = base + B + q < n ? x[base + B + q] : 0u;
-        const uint32_t m = min(B, n - base);
-        if (var_wave) {
-#pragma unroll
-            for (uint32_t q = 0; q < B; ++q)
-                if (q < m) st.add_var(cur[q]);
-        } else {
-#pragma unroll
-            for (uint32_t q = 0; q < B; ++q)
-                if (q < m) st.add_p2(cur[q]);
-        }
-#pragma unroll
-        for (uint32_t q = 0; q < B; ++q) cur[q] = nxt[q];
+        for (uint32_t i = 0; i + 1 < B; ++i) q[i] = q[i + 1];
+        q[B - 1] = k + B < n ? x[k + B] : 0u;
+        if (var_wave)
+            st.add_var(v);
+        else
+            st.add_p2(v);
     }
     if (var_wave)
         out[jb.out_idx].var = d2u16(st.var);
@@ -751,6 +753,8 @@ struct SubLds {
     uint32_t* nbig;
     uint64_t* tlast;   // stamp scratch
     uint32_t* ccnt;    // [8] size-class counters
+    uint32_t* lens32;  // the sub-bucket's consumed record slots viewed as u32 (chain lengths)
+    uint64_t lens_sel; // selector | u32 offset of lens32 in its buffer
 };
 
 __device__ __forceinline__ uint64_t kept_hi(uint64_t h43, uint32_t avg) { return (1ull << 63) | (h43 << 16) | avg; }
@@ -864,7 +868,14 @@ __device__ __forceinline__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint3
     r.mean = d2u16((double)(uint16_t)sum / (double)best_c);
     r.median = 0;
     r.var = 0;
-    if (best_c <= 2) stats_small(r, meta[lr0].len, best_c == 2 ? meta[lr1].len : 0u, best_c);
+    if (best_c <= 2) {
+        stats_small(r, meta[lr0].len, best_c == 2 ? meta[lr1].len : 0u, best_c);
+    } else {
+#pragma unroll
+        for (int t = 0; t < N; ++t)
+            if ((uint32_t)t >= rb && (uint32_t)t < rb + best_c)
+                L.lens32[a + (rb + best_c - 1 - t)] = meta[L.lo[idx[t]] >> 36].len;  // visit order
+    }
     return r;
 }
 
@@ -918,7 +929,8 @@ __device__ __forceinline__ void bm_combine(uint32_t& cand, uint32_t& cc) {
 }
 
 // Wave-level group with c <= 64: one member per lane, everything in registers.
-__device__ __forceinline__ GRes lgroup_wave64(const SubLds& L, uint32_t a, uint32_t c, uint8_t* __restrict__ flags) {
+__device__ __forceinline__ GRes lgroup_wave64(const SubLds& L, uint32_t a, uint32_t c, const SeqMeta* __restrict__ meta,
+                                              uint8_t* __restrict__ flags) {
     const uint32_t lane = threadIdx.x & 63u;
     GRes r;
     r.kept = false;
@@ -949,15 +961,13 @@ __device__ __forceinline__ GRes lgroup_wave64(const SubLds& L, uint32_t a, uint3
     uint64_t key = best ? lj : ~0ull;
     uint32_t idx = j;
     wave_sort64(key, idx);
-    wave_sync();
-    if (lane < nb) L.order[a + lane] = (uint16_t)idx;
-    wave_sync();
+    if (lane < nb) L.lens32[a + (nb - 1 - lane)] = meta[key >> 36].len;  // reverse ordinal
     return r;
 }
 
 __device__ __forceinline__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const SeqMeta* __restrict__ meta,
                             uint8_t* __restrict__ flags) {
-    if (c <= 64) return lgroup_wave64(L, a, c, flags);
+    if (c <= 64) return lgroup_wave64(L, a, c, meta, flags);
     const uint32_t lane = threadIdx.x & 63u;
     GRes r;
     r.kept = false;
@@ -1095,6 +1105,8 @@ __device__ __forceinline__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_
             }
         }
     }
+    for (uint32_t t = lane; t < nb; t += 64)
+        L.lens32[a + (nb - 1 - t)] = meta[L.lo[L.order[a + t]] >> 36].len;  // reverse ordinal
     return r;
 }
 
@@ -1172,7 +1184,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src, ui
         const uint64_t h43 = hprefix | ((L.hi[rep] >> 16) & 0xFFFFFFFFull);
         L.hi[rep] = kept_hi(h43, r.avg);
         if (r.cbest >= 3) {
-            jobinfo[rep] = ((a + r.rb) << 16) | JOB_KEPT | r.cbest;
+            jobinfo[rep] = (a << 16) | JOB_KEPT | r.cbest;  // chain lengths at lens32[a..a+cbest)
             fmean[rep] = r.best_f | ((uint32_t)r.mean << 16);
         } else {
             jobinfo[rep] = JOB_KEPT;
@@ -1239,27 +1251,21 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src, ui
     }
     __syncthreads();
     SKM_STAMP(7);
-    // 6. emit kept k-mers (one atomic per chunk) and chain jobs; the chunk's protein lengths are
-    //    gathered by the whole workgroup (job table: lens prefix | representative, in glist)
+    // 6. emit kept k-mers and chain jobs (one atomic each per chunk)
     unsigned long long* s_base = reinterpret_cast<unsigned long long*>(L.wave + 36);
-    uint32_t* jtab = reinterpret_cast<uint32_t*>(L.glist);
     for (uint32_t c0 = 0; c0 < n; c0 += nt) {
         const uint32_t j = c0 + tid;
         const uint32_t jb = j < n ? jobinfo[j] : 0u;
         const bool kept = (jb & JOB_KEPT) != 0;
         const uint64_t H = kept ? L.hi[j] : 0;
         const uint32_t jn = jb & JOB_COUNT_MASK;
-        uint32_t K, JL;
+        uint32_t K, J;
         const uint32_t kpos = wg_exclusive_scan(kept ? 1u : 0u, L.wave, K);
-        const uint32_t jl = wg_exclusive_scan(jn ? ((jn << 11) | 1u) : 0u, L.wave, JL);
+        const uint32_t jpos = wg_exclusive_scan(jn ? 1u : 0u, L.wave, J);
         if (K == 0) continue;
-        const uint32_t njob = JL & 0x7FFu, nlens = JL >> 11;
         if (tid == 0) {
             s_base[0] = atomicAdd(&A.ctr[0], (unsigned long long)K);
-            if (njob) {
-                s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)njob);
-                s_base[2] = atomicAdd(&A.ctr[4], (unsigned long long)nlens);
-            }
+            if (J) s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)J);
         }
         __syncthreads();
         if (kept) {
@@ -1268,30 +1274,13 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src, ui
                 const uint32_t fm = fmean[j];
                 write_kept(A, o, H, kept_lo(fm & 0xFFFFu, fm >> 16, 0, 0));
                 Job jbr;
-                jbr.lens_off = s_base[2] + (jl >> 11);
+                jbr.lens_off = L.lens_sel + (jb >> 16);
                 jbr.n = jn;
                 jbr.out_idx = (uint32_t)o;
-                A.jobs[s_base[1] + (jl & 0x7FFu)] = jbr;
-                jtab[jl & 0x7FFu] = ((jl >> 11) << 16) | j;
+                A.jobs[s_base[1] + jpos] = jbr;
             } else {
                 write_kept(A, o, H, L.lo[j]);
             }
-        }
-        __syncthreads();
-        for (uint32_t q = tid; q < nlens; q += nt) {
-            uint32_t lo_j = 0, hi_j = njob;  // last job whose lens prefix <= q
-            while (hi_j - lo_j > 1) {
-                const uint32_t mid = (lo_j + hi_j) >> 1;
-                if ((jtab[mid] >> 16) <= q)
-                    lo_j = mid;
-                else
-                    hi_j = mid;
-            }
-            const uint32_t ent = jtab[lo_j];
-            const uint32_t jbq = jobinfo[ent & 0xFFFFu];
-            const uint32_t jnq = jbq & JOB_COUNT_MASK, start = jbq >> 16;
-            const uint32_t t = q - (ent >> 16);
-            A.lens[s_base[2] + q] = A.meta[L.lo[L.order[start + jnq - 1 - t]] >> 36].len;  // reverse ordinal
         }
         __syncthreads();
     }
@@ -1338,6 +1327,8 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     const uint64_t hprefix = (uint64_t)(A.bucket_base + bucket) << A.rem_bits;
 
     if (n <= (uint64_t)CAP) {
+        L.lens32 = reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(A.recs + r0));
+        L.lens_sel = (LENS_IN_RECS << LENS_SEL_SHIFT) | (2 * r0);
         process_sub(A.recs + r0, (uint32_t)n, A, hprefix, pos_mask, L);
         return;
     }
@@ -1388,6 +1379,8 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
         const uint32_t cnt = e - a;
         if (cnt == 0) continue;
         if (cnt <= (uint32_t)CAP) {
+            L.lens32 = reinterpret_cast<uint32_t*>(A.tmp + r0 + a);
+            L.lens_sel = (LENS_IN_TMP << LENS_SEL_SHIFT) | (2 * (r0 + a));
             process_sub(A.tmp + r0 + a, cnt, A, hprefix, pos_mask, L);
             __syncthreads();
             SKM_STAMP(10);
@@ -1855,8 +1848,8 @@ void run_pipeline(skm_build* b) {
                            b->d_job_offs.as<uint64_t>(), b->d_jobs_sorted.as<Job>());
         const uint64_t threads = ceil_div(nj, 64) * 128;
         hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, st,
-                           b->d_jobs_sorted.as<Job>(), nj, b->d_lens.as<uint32_t>(),
-                           b->d_data.as<skm_stored_kmer_data>());
+                           b->d_jobs_sorted.as<Job>(), nj, b->d_lens.as<uint32_t>(), b->d_recs.as<uint32_t>(),
+                           b->d_tmp.as<uint32_t>(), b->d_data.as<skm_stored_kmer_data>());
     }
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[6], st));
