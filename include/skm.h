@@ -117,6 +117,10 @@ int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then
  * enable/disable stamping for subsequent runs. */
 int skm_build_debug_stamps(skm_build* b, int enable, uint64_t* out, int cap);
+/* Diagnostics: lengths of the first cap chain jobs in execution order (longest first). */
+int skm_build_debug_jobs(skm_build* b, uint32_t* out, int cap);
+/* Diagnostics: device time of the chain kernel on njobs synthetic jobs of length n. */
+int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms);
 /* Run (if not yet run since the last prepare) and download the result. */
 int skm_build_finish(skm_build* b, skm_kept* out);
 void skm_kept_free(skm_kept* k);

@@ -70,6 +70,8 @@ _SIGS = {
     "skm_build_last_timings": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int]),
     "skm_build_finish": (C.c_int, [_P, C.POINTER(_Kept)]),
     "skm_build_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
+    "skm_build_debug_jobs": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int]),
+    "skm_debug_chain_bench": (C.c_int, [C.c_uint32, C.c_uint32, C.POINTER(C.c_float)]),
     "skm_build_debug_stamps": (C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64), C.c_int]),
     "skm_kept_free": (None, [C.POINTER(_Kept)]),
     "skm_build_destroy": (None, [_P]),
@@ -117,6 +119,12 @@ def _check(rc: int):
 
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
+
+
+def debug_chain_bench(n: int, njobs: int) -> float:
+    ms = C.c_float()
+    _check(lib().skm_debug_chain_bench(n, njobs, C.byref(ms)))
+    return ms.value
 
 
 def device_count() -> int:
@@ -206,6 +214,11 @@ class SignatureBuilder:
         n = lib().skm_build_counters(self._h, v, 8)
         names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences"]
         return {names[i]: int(v[i]) for i in range(n)}
+
+    def debug_jobs(self, k: int = 64) -> list:
+        v = (C.c_uint32 * k)()
+        _check(lib().skm_build_debug_jobs(self._h, v, k))
+        return [int(x) for x in v]
 
     def debug_stamps(self, enable: bool) -> list:
         v = (C.c_uint64 * 16)()

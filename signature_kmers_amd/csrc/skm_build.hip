@@ -165,6 +165,13 @@ struct SigStats {
     }
 };
 
+constexpr uint32_t REM_MASK = 0x7FFFFFFFu;   // rem <= 31 bits; bit 47 of hi is the big-length flag
+
+// protein length of an element: carried mod 2^16 unless the big-length flag is set
+__device__ __forceinline__ uint32_t elem_len(uint64_t hi, uint64_t lo, const SeqMeta* __restrict__ meta) {
+    return ((hi >> 47) & 1u) ? meta[lo >> 36].len : (uint32_t)(hi >> 48);
+}
+
 __device__ __forceinline__ void make_elem(uint64_t rec, int pos_bits, uint64_t pos_mask, uint64_t pos_base,
                                           const uint32_t* __restrict__ blk2seq, const SeqMeta* __restrict__ meta,
                                           uint64_t& ohi, uint64_t& olo) {
@@ -178,7 +185,8 @@ __device__ __forceinline__ void make_elem(uint64_t rec, int pos_bits, uint64_t p
     }
     const uint32_t i = (uint32_t)(p - m.pstart);
     const uint32_t off16 = (m.len - i) & 0xFFFFu;
-    ohi = ((uint64_t)(m.len & 0xFFFFu) << 48) | (rem << 16) | m.func;  // len mod 2^16 rides along
+    // len mod 2^16 rides along in [63:48]; bit 47 flags proteins >= 65536 (rem is <= 31 bits)
+    ohi = ((uint64_t)(m.len & 0xFFFFu) << 48) | ((uint64_t)(m.len > 0xFFFFu) << 47) | (rem << 16) | m.func;
     olo = ((uint64_t)s << 36) | ((uint64_t)i << 16) | off16;
 }
 
@@ -539,19 +547,26 @@ __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, ui
     const uint32_t n = jb.n;
     SigStats st;
     st.init();
-    constexpr uint32_t B = 16;  // prefetch distance (shift-register queue keeps the loop body small)
-    uint32_t q[B];
+    constexpr uint32_t B = 16;  // samples per block; the next block is in flight meanwhile
+    uint32_t cur[B], nxt[B];
 #pragma unroll
-    for (uint32_t i = 0; i < B; ++i) q[i] = i < n ? x[i] : 0u;
-    for (uint32_t k = 0; k < n; ++k) {
-        const uint32_t v = q[0];
+    for (uint32_t i = 0; i < B; ++i) cur[i] = i < n ? x[i] : 0u;
+    for (uint32_t base = 0; base < n; base += B) {
 #pragma unroll
-        for (uint32_t i = 0; i + 1 < B; ++i) q[i] = q[i + 1];
-        q[B - 1] = k + B < n ? x[k + B] : 0u;
-        if (var_wave)
-            st.add_var(v);
-        else
-            st.add_p2(v);
+        for (uint32_t i = 0; i < B; ++i) nxt[i] = base + B + i < n ? x[base + B + i] : 0u;
+        const uint32_t m = min(B, n - base);
+        for (uint32_t i = 0; i < m; ++i) {
+            // rotate the block through cur[0] without dynamic register indexing
+            const uint32_t v = cur[0];
+#pragma unroll
+            for (uint32_t q = 0; q + 1 < B; ++q) cur[q] = cur[q + 1];
+            if (var_wave)
+                st.add_var(v);
+            else
+                st.add_p2(v);
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < B; ++i) cur[i] = nxt[i];
     }
     if (var_wave)
         out[jb.out_idx].var = d2u16(st.var);
@@ -851,10 +866,11 @@ __device__ __forceinline__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint3
             const uint32_t s = (uint32_t)(lo >> 36);
             flags[s] = 1;
             if ((uint32_t)t >= rb && (uint32_t)t < rb + best_c) {
-                sum += (uint32_t)(L.hi[idx[t]] >> 48);  // len mod 2^16 is all the u16 sum keeps
+                const uint64_t hj = L.hi[idx[t]];
+                sum += (uint32_t)(hj >> 48);  // len mod 2^16 is all the u16 sum keeps
                 const uint32_t q = rb + best_c - 1 - t;  // visit position (reverse ordinal)
-                if (q == 0) lr0 = s;
-                if (q == 1) lr1 = s;
+                if (q == 0) lr0 = elem_len(hj, lo, meta);
+                if (q == 1) lr1 = elem_len(hj, lo, meta);
             }
         }
     }
@@ -869,12 +885,12 @@ __device__ __forceinline__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint3
     r.median = 0;
     r.var = 0;
     if (best_c <= 2) {
-        stats_small(r, meta[lr0].len, best_c == 2 ? meta[lr1].len : 0u, best_c);
+        stats_small(r, lr0, best_c == 2 ? lr1 : 0u, best_c);
     } else {
 #pragma unroll
         for (int t = 0; t < N; ++t)
             if ((uint32_t)t >= rb && (uint32_t)t < rb + best_c)
-                L.lens32[a + (rb + best_c - 1 - t)] = meta[L.lo[idx[t]] >> 36].len;  // visit order
+                L.lens32[a + (rb + best_c - 1 - t)] = elem_len(L.hi[idx[t]], L.lo[idx[t]], meta);  // visit order
     }
     return r;
 }
@@ -961,7 +977,7 @@ __device__ __forceinline__ GRes lgroup_wave64(const SubLds& L, uint32_t a, uint3
     uint64_t key = best ? lj : ~0ull;
     uint32_t idx = j;
     wave_sort64(key, idx);
-    if (lane < nb) L.lens32[a + (nb - 1 - lane)] = meta[key >> 36].len;  // reverse ordinal
+    if (lane < nb) L.lens32[a + (nb - 1 - lane)] = elem_len(L.hi[idx], key, meta);  // reverse ordinal
     return r;
 }
 
@@ -1105,8 +1121,10 @@ __device__ __forceinline__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_
             }
         }
     }
-    for (uint32_t t = lane; t < nb; t += 64)
-        L.lens32[a + (nb - 1 - t)] = meta[L.lo[L.order[a + t]] >> 36].len;  // reverse ordinal
+    for (uint32_t t = lane; t < nb; t += 64) {
+        const uint32_t jj = L.order[a + t];
+        L.lens32[a + (nb - 1 - t)] = elem_len(L.hi[jj], L.lo[jj], meta);  // reverse ordinal
+    }
     return r;
 }
 
@@ -1126,13 +1144,13 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src, ui
     SKM_STAMP(2);
     // 2. hash insert: slot = representative << 16 | count; the pre-increment count is the rank
     for (uint32_t j = tid; j < n; j += nt) {
-        const uint32_t rem = (uint32_t)(L.hi[j] >> 16);
+        const uint32_t rem = (uint32_t)(L.hi[j] >> 16) & REM_MASK;
         uint32_t slot = (rem * 0x9E3779B1u) >> (32 - TAB_BITS);
         uint32_t rk = 0;
         while (true) {
             const uint32_t cur = atomicCAS(&L.tab[slot], EMPTY, (j << 16) | 1u);
             if (cur == EMPTY) break;
-            if ((uint32_t)(L.hi[cur >> 16] >> 16) == rem) {
+            if (((uint32_t)(L.hi[cur >> 16] >> 16) & REM_MASK) == rem) {
                 rk = atomicAdd(&L.tab[slot], 1u) & 0xFFFFu;
                 break;
             }
@@ -1159,7 +1177,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src, ui
         } else if (in && cnt == 1) {  // group of one: always kept (1 >= 0.8), median 0, var 0
             const uint64_t H = L.hi[j], Lo = L.lo[j];
             A.flags[Lo >> 36] = 1;
-            L.hi[j] = kept_hi(hprefix | ((H >> 16) & 0xFFFFFFFFull), (uint32_t)(Lo & 0xFFFFu));
+            L.hi[j] = kept_hi(hprefix | ((H >> 16) & REM_MASK), (uint32_t)(Lo & 0xFFFFu));
             L.lo[j] = kept_lo((uint32_t)(H & 0xFFFFu), d2u16((double)(uint16_t)(H >> 48) / 1.0), 0, 0);
             L.rank[j] = 0xFFFFu;  // singleton marker
         }
@@ -1181,7 +1199,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src, ui
     SKM_STAMP(5);
     auto stage = [&](const GRes& r, uint32_t rep, uint32_t a) {
         if (!r.kept) return;
-        const uint64_t h43 = hprefix | ((L.hi[rep] >> 16) & 0xFFFFFFFFull);
+        const uint64_t h43 = hprefix | ((L.hi[rep] >> 16) & REM_MASK);
         L.hi[rep] = kept_hi(h43, r.avg);
         if (r.cbest >= 3) {
             jobinfo[rep] = (a << 16) | JOB_KEPT | r.cbest;  // chain lengths at lens32[a..a+cbest)
@@ -1433,7 +1451,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
             const uint32_t g = c0 + j;
             if (g < n) {
                 make_elem(src[g], A.pos_bits, pos_mask, A.pos_base, A.blk2seq, A.meta, s_hi[j], s_lo[j]);
-                s_hi[j] &= 0x0000FFFFFFFFFFFFull;
+                s_hi[j] &= 0x00007FFFFFFFFFFFull;
             } else {
                 s_hi[j] = ~0ull;
                 s_lo[j] = ~0ull;
@@ -1681,7 +1699,7 @@ struct skm_build {
     uint64_t rp = 0;       // packed length
     uint32_t nseq = 0;
     // geometry
-    int owner_bits = 0, b1_bits = 11;
+    int owner_bits = 0, b1_bits = 12;
     // device work
     DevBuf d_hist, d_offs, d_partial, d_rbbase, d_bstart32, d_bstart, d_owner_start;
     DevBuf d_recs, d_tmp;
@@ -1882,7 +1900,7 @@ void prepare(skm_build* b) {
     SKM_CHECK(b->h_meta.size() < (1ull << ELEM_S_BITS), SKM_E_ARG, "too many sequences in one build shard");
     // geometry: records carry the packed position in pos_bits
     b->owner_bits = 0;
-    b->b1_bits = 11;
+    b->b1_bits = 12;  // rem = 31 bits: leaves the big-length flag bit in the element
     const int rem_bits = KEY_BITS - b->owner_bits - b->b1_bits;
     SKM_CHECK(rp < (1ull << (64 - rem_bits)), SKM_E_ARG, "input too large for one GPU shard");
     SKM_CHECK(b->n_windows < (1ull << 32), SKM_E_ARG, "more than 2^32 windows in one GPU shard");
@@ -2015,6 +2033,53 @@ int skm_build_debug_stamps(skm_build* b, int enable, uint64_t* out, int cap) {
         for (int i = 0; i < cap && i < 16; ++i) out[i] = tmp[i];
     }
     b->stamps = enable != 0;
+    SKM_API_END
+}
+
+// Diagnostics: lengths of the first `cap` chain jobs in execution order (longest class first).
+int skm_build_debug_jobs(skm_build* b, uint32_t* out, int cap) {
+    SKM_API_BEGIN
+    SKM_CHECK(b && out, SKM_E_ARG, "null argument");
+    const uint64_t n = std::min<uint64_t>((uint64_t)cap, b->n_jobs);
+    std::vector<Job> j(n);
+    if (n) SKM_HIP(hipMemcpy(j.data(), b->d_jobs_sorted.p, sizeof(Job) * n, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < (uint64_t)cap; ++i) out[i] = i < n ? j[i].n : 0u;
+    SKM_API_END
+}
+
+// Diagnostics: time k_chains on `njobs` synthetic jobs of length n (lengths 300 +- 60).
+int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms) {
+    SKM_API_BEGIN
+    SKM_CHECK(ms && n && njobs, SKM_E_ARG, "bad argument");
+    std::vector<uint32_t> lens((size_t)n * njobs);
+    uint32_t x = 12345;
+    for (auto& v : lens) {
+        x = x * 1664525u + 1013904223u;
+        v = 240 + (x >> 16) % 121;
+    }
+    std::vector<Job> jobs(njobs);
+    for (uint32_t i = 0; i < njobs; ++i) jobs[i] = Job{(uint64_t)i * n, n, i};
+    DevBuf dl, dj, dout;
+    dl.ensure(4 * lens.size());
+    dj.ensure(sizeof(Job) * njobs);
+    dout.ensure(sizeof(skm_stored_kmer_data) * njobs);
+    SKM_HIP(hipMemcpy(dl.p, lens.data(), 4 * lens.size(), hipMemcpyHostToDevice));
+    SKM_HIP(hipMemcpy(dj.p, jobs.data(), sizeof(Job) * njobs, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    SKM_HIP(hipEventCreate(&e0));
+    SKM_HIP(hipEventCreate(&e1));
+    const uint64_t threads = ceil_div(njobs, 64) * 128;
+    for (int it = 0; it < 2; ++it) {
+        SKM_HIP(hipEventRecord(e0, 0));
+        hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, 0, dj.as<Job>(),
+                           (uint64_t)njobs, dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(),
+                           dout.as<skm_stored_kmer_data>());
+        SKM_HIP(hipEventRecord(e1, 0));
+        SKM_HIP(hipEventSynchronize(e1));
+        SKM_HIP(hipEventElapsedTime(ms, e0, e1));
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     SKM_API_END
 }
 

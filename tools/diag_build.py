@@ -36,6 +36,9 @@ for k in sorted(STAMP_NAMES):
     print(f"  {STAMP_NAMES[k]:>20s} {st[k]:>16d} {100.0 * st[k] / max(tot, 1):6.1f}%")
 print("timings(stamped)", json.dumps(b.timings()))
 print("counters", json.dumps(b.counters()))
+print("longest jobs", b.debug_jobs(16))
+for n, nj in [(1000, 1), (1000, 64), (1000, 4096), (16000, 1), (16000, 64), (100, 100000), (10, 1000000)]:
+    print("chain bench n=%d jobs=%d: %.3f ms" % (n, nj, skm.debug_chain_bench(n, nj)))
 for _ in range(a.steps):
     b.run()
     print("timings", json.dumps(b.timings()))
