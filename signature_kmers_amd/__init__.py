@@ -334,8 +334,7 @@ class FunctionCaller:
             self.hypo_index = self.function_index.index("hypothetical protein")
         except ValueError:
             self.hypo_index = -1
-        self._fi_arr = (C.c_char_p * max(1, len(self.function_index)))(
-            *[s.encode("latin-1") for s in self.function_index])
+        self._fi_arr = _fi_array(self.function_index)
 
     def ignore_hypothetical(self, x: bool):
         self.ignore_hypothetical_ = bool(x)
@@ -367,12 +366,25 @@ class FunctionCaller:
 
     def find_best_call(self, calls: np.ndarray):
         """find_best_call (call_functions.tcc:347-659) -> (function_index, function, score, offset)."""
-        calls = np.ascontiguousarray(calls, dtype=CALL_DTYPE)
-        fi = C.c_uint16()
-        score = C.c_float()
-        off = C.c_float()
-        buf = C.create_string_buffer(4096)
-        _check(lib().skm_find_best_call(_ptr(calls) if len(calls) else None, len(calls), self._fi_arr,
-                                        len(self.function_index), C.byref(fi), C.byref(score), C.byref(off), buf,
-                                        4096))
-        return fi.value, buf.value.decode("latin-1"), score.value, off.value
+        return _find_best_call(calls, self._fi_arr, len(self.function_index))
+
+
+def _fi_array(function_index):
+    return (C.c_char_p * max(1, len(function_index)))(*[s.encode("latin-1") for s in function_index])
+
+
+def _find_best_call(calls, fi_arr, nfunc):
+    calls = np.ascontiguousarray(calls, dtype=CALL_DTYPE)
+    fi = C.c_uint16()
+    score = C.c_float()
+    off = C.c_float()
+    buf = C.create_string_buffer(4096)
+    _check(lib().skm_find_best_call(_ptr(calls) if len(calls) else None, len(calls), fi_arr, nfunc, C.byref(fi),
+                                    C.byref(score), C.byref(off), buf, 4096))
+    return fi.value, buf.value.decode("latin-1"), score.value, off.value
+
+
+def find_best_call(calls: np.ndarray, function_index):
+    """Host find_best_call (call_functions.tcc:347-659) over one sequence's calls, without a DB:
+    -> (function_index, function, score, offset)."""
+    return _find_best_call(calls, _fi_array(function_index), len(function_index))

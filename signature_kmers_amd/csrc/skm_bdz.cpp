@@ -152,18 +152,29 @@ bool bdz_build(const uint64_t* keys, size_t nkeys, uint32_t seed, Bdz& h, std::s
     h.m = (uint32_t)nkeys;
     h.r = (uint32_t)std::ceil((c * nkeys) / 3);
     if (h.r % 2 == 0) h.r += 1;
-    h.n = 3 * h.r;
     h.b = 7;
     h.k = 1u << h.b;
-    h.ranktablesize = (uint32_t)std::ceil(h.n / (double)h.k);
+    {   // duplicate keys never give an acyclic 3-graph: report them instead of retrying
+        std::vector<uint64_t> sk(keys, keys + nkeys);
+        std::sort(sk.begin(), sk.end());
+        if (std::adjacent_find(sk.begin(), sk.end()) != sk.end()) {
+            err = "BDZ construction failed: duplicate keys";
+            return false;
+        }
+    }
     std::mt19937 rng(seed);
     std::vector<uint32_t> ev((size_t)3 * nkeys);
-    std::vector<uint32_t> deg(h.n), xor_edge(h.n), queue;
+    std::vector<uint32_t> deg, xor_edge, queue;
     std::vector<uint8_t> removed;
     for (int attempt = 0; attempt < 1000; ++attempt) {
+        // tiny key sets (r = 1 or 3) can be cyclic for every seed: widen r (kept odd) every 20
+        // failed attempts.  Readers take r from the image, so any odd r stays cmph-compatible.
+        if (attempt > 0 && attempt % 20 == 0) h.r += 2;
+        h.n = 3 * h.r;
+        h.ranktablesize = (uint32_t)std::ceil(h.n / (double)h.k);
+        deg.assign(h.n, 0);
+        xor_edge.assign(h.n, 0);
         h.seed = rng();
-        std::fill(deg.begin(), deg.end(), 0);
-        std::fill(xor_edge.begin(), xor_edge.end(), 0);
         for (size_t e = 0; e < nkeys; ++e) {
             uint8_t kb[8];
             std::memcpy(kb, &keys[e], 8);
@@ -239,7 +250,7 @@ bool bdz_build(const uint64_t* keys, size_t nkeys, uint32_t seed, Bdz& h, std::s
         }
         return true;
     }
-    err = "BDZ construction failed: no acyclic 3-graph in 1000 attempts (duplicate keys?)";
+    err = "BDZ construction failed: no acyclic 3-graph in 1000 attempts";
     return false;
 }
 

@@ -19,6 +19,9 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def skm():
     import signature_kmers_amd as skm_mod
+    if not os.path.exists(skm_mod.LIB_PATH):  # fresh checkout: build libskm.so + the oracle in-tree
+        import subprocess
+        subprocess.check_call(["make", "-C", ROOT, "-j", str(min(16, os.cpu_count() or 8)), "all"])
     skm_mod.lib()
     return skm_mod
 
