@@ -7,13 +7,15 @@
 // Device pipeline (one GPU; the multi-GPU form inserts an RCCL all-to-all between 3 and 4):
 //   1. k_extract<count>   residues -> per-workgroup histogram of level-1 buckets (LDS atomics)
 //   2. k_colsum/k_bstart/k_coloffs   exclusive scan of the [workgroup][bucket] matrix
-//   3. k_extract<scatter> residues -> 8-byte occurrence records  rem<<pos_bits | position,
+//   3. k_extract<scatter> residues -> 16-byte occurrence elements (SoA hi/lo, see make_elem),
 //                         partitioned by level-1 bucket (owner-major)
 //   4. k_bucket_process   one workgroup per level-1 bucket: level-2 partition in HBM, then per
-//                         sub-bucket an LDS bitonic sort by (k-mer, function, ordinal), group
-//                         detection, cut, statistics, compaction of the kept k-mers
-//   5. k_overflow         sub-buckets larger than LDS: same algorithm, global-memory bitonic
-//   6. k_stats            distinct_functions, seqs_with_func, seqs-with-signature flags
+//                         sub-bucket LDS hash grouping, cut, statistics (short P^2/variance
+//                         chains inline, long ones deferred as jobs), compaction of kept k-mers
+//   5. k_overflow         sub-buckets larger than LDS: global-memory bitonic sort + the same
+//                         group processing
+//   6. k_job_* / k_chains deferred P^2 median / variance recurrences, longest first
+//   7. k_func_hist_* / k_count_flags   distinct_functions, seqs_with_func, signature flags
 //
 // Exactness notes: group members are visited in reverse ordinal order
 // (TBB 2020 multimap LIFO), the cut is fp32 `(float)best < (float)count*0.8f`, statistics are
@@ -172,20 +174,14 @@ __device__ __forceinline__ uint32_t elem_len(uint64_t hi, uint64_t lo, const Seq
     return ((hi >> 47) & 1u) ? meta[lo >> 36].len : (uint32_t)(hi >> 48);
 }
 
-__device__ __forceinline__ void make_elem(uint64_t rec, int pos_bits, uint64_t pos_mask, uint64_t pos_base,
-                                          const uint32_t* __restrict__ blk2seq, const SeqMeta* __restrict__ meta,
-                                          uint64_t& ohi, uint64_t& olo) {
-    const uint64_t rem = rec >> pos_bits;
-    const uint64_t p = (rec & pos_mask) - pos_base;
-    uint32_t s = blk2seq[p >> 6];
-    SeqMeta m = meta[s];
-    while (p >= m.pstart + m.len + 1) {
-        ++s;
-        m = meta[s];
-    }
-    const uint32_t i = (uint32_t)(p - m.pstart);
+// 16-byte occurrence element (written by the extract-scatter kernel, read by the bucket kernel):
+//   hi = len mod 2^16 << 48 | (len > 65535) << 47 | rem << 16 | func     (rem <= 31 bits)
+//   lo = s << 36 | i << 16 | (len - i) mod 2^16                           (s = global sequence index)
+// Everything the group-by needs rides in the element, so the bucket kernel never gathers
+// per-sequence metadata (lo order = insertion order: sequence, then window).
+__device__ __forceinline__ void make_elem(uint64_t rem, uint32_t s, uint32_t i, const SeqMeta& m, uint64_t& ohi,
+                                          uint64_t& olo) {
     const uint32_t off16 = (m.len - i) & 0xFFFFu;
-    // len mod 2^16 rides along in [63:48]; bit 47 flags proteins >= 65536 (rem is <= 31 bits)
     ohi = ((uint64_t)(m.len & 0xFFFFu) << 48) | ((uint64_t)(m.len > 0xFFFFu) << 47) | (rem << 16) | m.func;
     olo = ((uint64_t)s << 36) | ((uint64_t)i << 16) | off16;
 }
@@ -587,20 +583,32 @@ __global__ void k_blk2seq(const SeqMeta* __restrict__ meta, uint32_t nseq, uint3
     for (uint64_t b = (a + 63) >> 6; b < ((e + 63) >> 6) && b < nblk; ++b) blk2seq[b] = s;
 }
 
+struct ExtractArgs {
+    const uint8_t* res;
+    uint64_t rp, span;
+    int owner_bits, b1_bits;
+    uint32_t* hist;                 // count pass: [wg][bucket]
+    const uint32_t* offs;           // scatter pass: [wg][bucket] element offsets within the owner
+    const uint64_t* owner_start;    // [owners+1]
+    const uint32_t* blk2seq;        // sequence containing packed position 64*b
+    const SeqMeta* meta;
+    uint32_t s_base;                // global index of this shard's first sequence
+    uint64_t* out_hi;
+    uint64_t* out_lo;
+};
+
 template <bool SCATTER>
-__global__ __launch_bounds__(EX_THREADS) void k_extract(const uint8_t* __restrict__ res, uint64_t rp, uint64_t span,
-                                                        int owner_bits, int b1_bits, uint64_t pos_base,
-                                                        uint32_t* __restrict__ hist, const uint32_t* __restrict__ offs,
-                                                        const uint64_t* __restrict__ owner_start,
-                                                        uint64_t* __restrict__ recs) {
+__global__ __launch_bounds__(EX_THREADS) void k_extract(ExtractArgs X) {
+    const uint8_t* __restrict__ res = X.res;
+    const uint64_t rp = X.rp, span = X.span;
+    const int owner_bits = X.owner_bits, b1_bits = X.b1_bits;
     extern __shared__ uint32_t s_cnt[];  // [NB]
     const int nbits = owner_bits + b1_bits;
     const uint32_t NB = 1u << nbits;
     const int rem_bits = KEY_BITS - nbits;
-    const int pos_bits = 64 - rem_bits;
     const uint64_t rem_mask = (1ull << rem_bits) - 1;
     const uint32_t wg = blockIdx.x;
-    for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) s_cnt[b] = SCATTER ? offs[(uint64_t)wg * NB + b] : 0u;
+    for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) s_cnt[b] = SCATTER ? X.offs[(uint64_t)wg * NB + b] : 0u;
     __syncthreads();
     const uint64_t begin = (uint64_t)wg * span;
     const uint64_t end = min(begin + span, rp);
@@ -622,6 +630,12 @@ __global__ __launch_bounds__(EX_THREADS) void k_extract(const uint8_t* __restric
 #pragma unroll
         for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
         constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
+        uint32_t s = 0;
+        SeqMeta m{};
+        if (SCATTER && valid) {
+            s = X.blk2seq[base >> 6];
+            m = X.meta[s];
+        }
 #pragma unroll
         for (int t = 0; t < EX_POS_PER_THREAD; ++t) {
             if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
@@ -630,9 +644,13 @@ __global__ __launch_bounds__(EX_THREADS) void k_extract(const uint8_t* __restric
                 const uint64_t h = mix43(k);
                 const uint32_t bucket = (uint32_t)(h >> rem_bits);
                 if (SCATTER) {
+                    while (p > m.pstart + m.len) m = X.meta[++s];  // valid windows never span a separator
                     const uint32_t idx = atomicAdd(&s_cnt[bucket], 1u);
-                    const uint64_t o = owner_start[bucket >> b1_bits] + idx;
-                    recs[o] = ((h & rem_mask) << pos_bits) | (pos_base + p);
+                    const uint64_t o = X.owner_start[bucket >> b1_bits] + idx;
+                    uint64_t eh, el;
+                    make_elem(h & rem_mask, X.s_base + s, (uint32_t)(p - m.pstart), m, eh, el);
+                    X.out_hi[o] = eh;
+                    X.out_lo[o] = el;
                 } else {
                     atomicAdd(&s_cnt[bucket], 1u);
                 }
@@ -641,7 +659,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_extract(const uint8_t* __restric
     }
     if (!SCATTER) {
         __syncthreads();
-        for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) hist[(uint64_t)wg * NB + b] = s_cnt[b];
+        for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) X.hist[(uint64_t)wg * NB + b] = s_cnt[b];
     }
 }
 
@@ -722,15 +740,15 @@ __global__ void k_coloffs(const uint32_t* __restrict__ hist, const uint32_t* __r
 }
 
 struct BucketArgs {
-    const uint64_t* recs;      // records of this owner, level-1 bucket-major
-    uint64_t* tmp;             // level-2 partition scratch, same indexing as recs
+    uint64_t* recs_hi;         // elements of this owner, level-1 bucket-major (SoA hi / lo)
+    const uint64_t* recs_lo;
+    uint64_t* tmp_hi;          // level-2 partition scratch, same indexing as recs
+    uint64_t* tmp_lo;
     const uint64_t* bstart;    // [nbuckets+1] absolute starts in recs
     uint32_t nbuckets;
     uint32_t bucket_base;      // global bucket id of bucket 0 (owner << b1_bits)
-    int rem_bits, pos_bits;
-    uint64_t pos_base;         // subtract from record positions to get local packed positions
-    const uint32_t* blk2seq;
-    const SeqMeta* meta;
+    int rem_bits;
+    const SeqMeta* meta;       // indexed by global sequence (only proteins >= 65536 residues read it)
     uint8_t* flags;
     unsigned long long* ctr;   // [0] kept [1] overflow entries [2] flagged seqs [3] jobs [4] lens
     uint64_t* out_keys;
@@ -1131,13 +1149,15 @@ __device__ __forceinline__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_
 // One sub-bucket of n <= CAP records: LDS hash grouping (ranks from the insert atomics give a
 // counting sort by group), singletons resolved immediately, multi-occurrence groups by threads
 // (small) or waves (large); no workgroup-wide sort.
-__device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src, uint32_t n, const BucketArgs& A, uint64_t hprefix,
-                            uint64_t pos_mask, const SubLds& L) {
+__device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi, const uint64_t* __restrict__ src_lo,
+                                            uint32_t n, const BucketArgs& A, uint64_t hprefix, const SubLds& L) {
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t EMPTY = 0xFFFFFFFFu;
-    // 1. load + resolve each record to (sequence, window, function, offset)
-    for (uint32_t j = tid; j < n; j += nt)
-        make_elem(src[j], A.pos_bits, pos_mask, A.pos_base, A.blk2seq, A.meta, L.hi[j], L.lo[j]);
+    // 1. load the elements
+    for (uint32_t j = tid; j < n; j += nt) {
+        L.hi[j] = src_hi[j];
+        L.lo[j] = src_lo[j];
+    }
     for (uint32_t t = tid; t < (uint32_t)TAB; t += nt) L.tab[t] = EMPTY;
     if (tid == 0) *L.nbig = 0;
     __syncthreads();
@@ -1341,13 +1361,13 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     const uint64_t r0 = A.bstart[bucket], r1 = A.bstart[bucket + 1];
     const uint64_t n = r1 - r0;
     if (n == 0) return;
-    const uint64_t pos_mask = (A.pos_bits >= 64) ? ~0ull : ((1ull << A.pos_bits) - 1);
     const uint64_t hprefix = (uint64_t)(A.bucket_base + bucket) << A.rem_bits;
+    const uint64_t rem_mask = (1ull << A.rem_bits) - 1;
 
     if (n <= (uint64_t)CAP) {
-        L.lens32 = reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(A.recs + r0));
+        L.lens32 = reinterpret_cast<uint32_t*>(A.recs_hi + r0);
         L.lens_sel = (LENS_IN_RECS << LENS_SEL_SHIFT) | (2 * r0);
-        process_sub(A.recs + r0, (uint32_t)n, A, hprefix, pos_mask, L);
+        process_sub(A.recs_hi + r0, A.recs_lo + r0, (uint32_t)n, A, hprefix, L);
         return;
     }
     __syncthreads();
@@ -1360,8 +1380,8 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_sub[d] = 0;
     __syncthreads();
     for (uint64_t j = threadIdx.x; j < n; j += blockDim.x) {
-        const uint64_t rec = A.recs[r0 + j];
-        atomicAdd(&s_sub[(uint32_t)((rec >> A.pos_bits) >> shift)], 1u);
+        const uint64_t h = A.recs_hi[r0 + j];
+        atomicAdd(&s_sub[(uint32_t)(((h >> 16) & rem_mask) >> shift)], 1u);
     }
     __syncthreads();
     SKM_STAMP(0);
@@ -1385,9 +1405,11 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     for (uint32_t d = threadIdx.x; d < nsub; d += blockDim.x) s_cur[d] = s_sub[d];
     __syncthreads();
     for (uint64_t j = threadIdx.x; j < n; j += blockDim.x) {
-        const uint64_t rec = A.recs[r0 + j];
-        const uint32_t o = atomicAdd(&s_cur[(uint32_t)((rec >> A.pos_bits) >> shift)], 1u);
-        A.tmp[r0 + o] = rec;
+        const uint64_t h = A.recs_hi[r0 + j];
+        const uint64_t l = A.recs_lo[r0 + j];
+        const uint32_t o = atomicAdd(&s_cur[(uint32_t)(((h >> 16) & rem_mask) >> shift)], 1u);
+        A.tmp_hi[r0 + o] = h;
+        A.tmp_lo[r0 + o] = l;
     }
     __threadfence_block();
     __syncthreads();
@@ -1397,9 +1419,9 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
         const uint32_t cnt = e - a;
         if (cnt == 0) continue;
         if (cnt <= (uint32_t)CAP) {
-            L.lens32 = reinterpret_cast<uint32_t*>(A.tmp + r0 + a);
+            L.lens32 = reinterpret_cast<uint32_t*>(A.tmp_hi + r0 + a);
             L.lens_sel = (LENS_IN_TMP << LENS_SEL_SHIFT) | (2 * (r0 + a));
-            process_sub(A.tmp + r0 + a, cnt, A, hprefix, pos_mask, L);
+            process_sub(A.tmp_hi + r0 + a, A.tmp_lo + r0 + a, cnt, A, hprefix, L);
             __syncthreads();
             SKM_STAMP(10);
         } else if (threadIdx.x == 0) {
@@ -1435,7 +1457,8 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
     __shared__ uint32_t s_nbig;
     __shared__ uint32_t s_big[BP_THREADS];
     const OvfEntry e = A.ovf[blockIdx.x];
-    const uint64_t* src = (e.src ? A.tmp : A.recs) + e.off;
+    const uint64_t* src_hi = (e.src ? A.tmp_hi : A.recs_hi) + e.off;
+    const uint64_t* src_lo = (e.src ? A.tmp_lo : A.recs_lo) + e.off;
     uint64_t* ghi = S.hi + e.scratch;
     uint64_t* glo = S.lo + e.scratch;
     uint32_t* heads = S.heads + e.scratch;
@@ -1443,15 +1466,14 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
     uint32_t* fmean = S.fmean + e.scratch;
     const uint32_t N = e.npad, n = e.n;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    const uint64_t pos_mask = (A.pos_bits >= 64) ? ~0ull : ((1ull << A.pos_bits) - 1);
     const uint64_t hprefix = (uint64_t)(A.bucket_base + e.bucket) << A.rem_bits;
     // phase 0: chunks of CAP sorted in LDS (directions from the global index)
     for (uint32_t c0 = 0; c0 < N; c0 += CAP) {
         for (uint32_t j = tid; j < CAP; j += nt) {
             const uint32_t g = c0 + j;
             if (g < n) {
-                make_elem(src[g], A.pos_bits, pos_mask, A.pos_base, A.blk2seq, A.meta, s_hi[j], s_lo[j]);
-                s_hi[j] &= 0x00007FFFFFFFFFFFull;
+                s_hi[j] = src_hi[g] & 0x00007FFFFFFFFFFFull;  // group key = rem | func (length bits dropped)
+                s_lo[j] = src_lo[g];
             } else {
                 s_hi[j] = ~0ull;
                 s_lo[j] = ~0ull;
@@ -1702,7 +1724,8 @@ struct skm_build {
     int owner_bits = 0, b1_bits = 12;
     // device work
     DevBuf d_hist, d_offs, d_partial, d_rbbase, d_bstart32, d_bstart, d_owner_start;
-    DevBuf d_recs, d_tmp;
+    DevBuf d_recs_hi, d_recs_lo, d_tmp_hi, d_tmp_lo;
+    uint32_t s_base = 0;   // global index of this shard's first sequence
     DevBuf d_keys, d_data, d_ctr, d_flags, d_dfunc, d_swf, d_ovf, d_ovf_hi, d_ovf_lo, d_ovf_heads, d_ovf_job, d_ovf_fm;
     DevBuf d_jobs, d_lens, d_stamps, d_job_hist, d_job_offs, d_jobs_sorted;
     bool stamps = false;
@@ -1749,15 +1772,26 @@ void run_pipeline(skm_build* b) {
     const uint32_t NB = 1u << nbits;
     const uint32_t nowners = 1u << b->owner_bits;
     const int rem_bits = KEY_BITS - nbits;
-    const int pos_bits = 64 - rem_bits;
     const uint32_t F = b->opts.n_functions;
 
     SKM_HIP(hipEventRecord(b->ev[0], st));
     // ---- 1. count ----
     size_t lds_cnt = sizeof(uint32_t) * NB;
-    hipLaunchKernelGGL(k_extract<false>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, b->d_res.as<uint8_t>(), b->rp,
-                       b->span, b->owner_bits, b->b1_bits, (uint64_t)0, b->d_hist.as<uint32_t>(), nullptr, nullptr,
-                       nullptr);
+    ExtractArgs X;
+    X.res = b->d_res.as<uint8_t>();
+    X.rp = b->rp;
+    X.span = b->span;
+    X.owner_bits = b->owner_bits;
+    X.b1_bits = b->b1_bits;
+    X.hist = b->d_hist.as<uint32_t>();
+    X.offs = b->d_offs.as<uint32_t>();
+    X.owner_start = b->d_owner_start.as<uint64_t>();
+    X.blk2seq = b->d_blk2seq.as<uint32_t>();
+    X.meta = b->d_meta.as<SeqMeta>();
+    X.s_base = b->s_base;
+    X.out_hi = b->d_recs_hi.as<uint64_t>();
+    X.out_lo = b->d_recs_lo.as<uint64_t>();
+    hipLaunchKernelGGL(k_extract<false>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, X);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[1], st));
     // ---- 2. scan ----
@@ -1773,24 +1807,21 @@ void run_pipeline(skm_build* b) {
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[2], st));
     // ---- 3. scatter ----
-    hipLaunchKernelGGL(k_extract<true>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, b->d_res.as<uint8_t>(), b->rp,
-                       b->span, b->owner_bits, b->b1_bits, (uint64_t)0, nullptr, b->d_offs.as<uint32_t>(),
-                       b->d_owner_start.as<uint64_t>(), b->d_recs.as<uint64_t>());
+    hipLaunchKernelGGL(k_extract<true>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, X);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[3], st));
     // ---- 4. bucket process ----
     SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 128, st));
     SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->nseq ? b->nseq : 1, st));
     BucketArgs A;
-    A.recs = b->d_recs.as<uint64_t>();
-    A.tmp = b->d_tmp.as<uint64_t>();
+    A.recs_hi = b->d_recs_hi.as<uint64_t>();
+    A.recs_lo = b->d_recs_lo.as<uint64_t>();
+    A.tmp_hi = b->d_tmp_hi.as<uint64_t>();
+    A.tmp_lo = b->d_tmp_lo.as<uint64_t>();
     A.bstart = b->d_bstart.as<uint64_t>();
     A.nbuckets = NB;
     A.bucket_base = 0;
     A.rem_bits = rem_bits;
-    A.pos_bits = pos_bits;
-    A.pos_base = 0;
-    A.blk2seq = b->d_blk2seq.as<uint32_t>();
     A.meta = b->d_meta.as<SeqMeta>();
     A.flags = b->d_flags.as<uint8_t>();
     A.ctr = b->d_ctr.as<unsigned long long>();
@@ -1866,8 +1897,8 @@ void run_pipeline(skm_build* b) {
                            b->d_job_offs.as<uint64_t>(), b->d_jobs_sorted.as<Job>());
         const uint64_t threads = ceil_div(nj, 64) * 128;
         hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, st,
-                           b->d_jobs_sorted.as<Job>(), nj, b->d_lens.as<uint32_t>(), b->d_recs.as<uint32_t>(),
-                           b->d_tmp.as<uint32_t>(), b->d_data.as<skm_stored_kmer_data>());
+                           b->d_jobs_sorted.as<Job>(), nj, b->d_lens.as<uint32_t>(), b->d_recs_hi.as<uint32_t>(),
+                           b->d_tmp_hi.as<uint32_t>(), b->d_data.as<skm_stored_kmer_data>());
     }
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[6], st));
@@ -1898,11 +1929,9 @@ void prepare(skm_build* b) {
     b->rp = rp;
     b->nseq = (uint32_t)b->h_meta.size();
     SKM_CHECK(b->h_meta.size() < (1ull << ELEM_S_BITS), SKM_E_ARG, "too many sequences in one build shard");
-    // geometry: records carry the packed position in pos_bits
+    // geometry: 4096 level-1 buckets; rem = 31 bits leaves element bit 47 for the big-length flag
     b->owner_bits = 0;
-    b->b1_bits = 12;  // rem = 31 bits: leaves the big-length flag bit in the element
-    const int rem_bits = KEY_BITS - b->owner_bits - b->b1_bits;
-    SKM_CHECK(rp < (1ull << (64 - rem_bits)), SKM_E_ARG, "input too large for one GPU shard");
+    b->b1_bits = 12;
     SKM_CHECK(b->n_windows < (1ull << 32), SKM_E_ARG, "more than 2^32 windows in one GPU shard");
     // upload
     b->d_res.ensure(rp + 64);
@@ -1935,8 +1964,10 @@ void prepare(skm_build* b) {
     b->d_bstart.ensure(sizeof(uint64_t) * (NB + 1));
     b->d_owner_start.ensure(sizeof(uint64_t) * 16);
     const uint64_t W = b->n_windows;
-    b->d_recs.ensure(8 * std::max<uint64_t>(W, 1));
-    b->d_tmp.ensure(8 * std::max<uint64_t>(W, 1));
+    b->d_recs_hi.ensure(8 * std::max<uint64_t>(W, 1));
+    b->d_recs_lo.ensure(8 * std::max<uint64_t>(W, 1));
+    b->d_tmp_hi.ensure(8 * std::max<uint64_t>(W, 1));
+    b->d_tmp_lo.ensure(8 * std::max<uint64_t>(W, 1));
     b->d_keys.ensure(8 * std::max<uint64_t>(W, 1));
     b->d_data.ensure(sizeof(skm_stored_kmer_data) * std::max<uint64_t>(W, 1) + 16);
     b->d_ctr.ensure(128);
