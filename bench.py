@@ -106,8 +106,8 @@ def main():
     dom = max(("extract_count", "extract_scatter", "bucket_process"), key=lambda k: phase.get(k, 0.0))
     alg = {
         "extract_count": res_bytes,
-        "extract_scatter": res_bytes + 8 * valid,
-        "bucket_process": 8 * valid + 18 * n_kept,
+        "extract_scatter": res_bytes + 16 * valid,   # 16-byte occurrence elements written once
+        "bucket_process": 16 * valid + 18 * n_kept,  # ... read once; kept keys + records written
     }
     dom_ms = phase[dom]
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
