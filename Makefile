@@ -4,7 +4,7 @@ HIPCC   ?= /opt/rocm/bin/hipcc
 CXX     ?= g++
 ARCH    ?= gfx950
 JOBS    ?= 8
-HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -DSKM_WITH_RCCL \
            -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -Wall -Wno-unused-function
 OBJDIR   = build/obj
 SRC      = signature_kmers_amd/csrc
@@ -27,7 +27,7 @@ $(OBJDIR)/%.o: $(SRC)/%.cpp $(wildcard $(SRC)/*.h) include/skm.h
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 bin/%: $(SRC)/tools/%.cpp $(LIB) $(wildcard $(SRC)/*.h)
 	@mkdir -p bin

@@ -3,8 +3,10 @@
 
 Metric: k-mers/sec (windows examined by extract+hash+count+cut), whole job over N GPUs.
 Workload at N=1: BASELINE configs[1] -- 1M synthetic protein sequences, k=8, signature build on
-one MI355X (SURVEY.md 8(d) generator, seed 20241115).  At N>1 each rank builds its own shard of
-1M sequences (weak scaling).
+one MI355X (SURVEY.md 8(d) generator, seed 20241115).  At N>1 (weak scaling) rank r holds the
+r-th contiguous range of files of an N x 1M proteome and the ranks run ONE build over the union:
+occurrence elements go to the owner GPU of their k-mer with an RCCL all-to-all over xGMI, then
+per-function counts and signature flags are all-reduced.
 
 One step = one full device pass of the build pipeline over the HBM-resident input
 (extract/count, scan, extract/scatter, bucket group-by + cut + statistics, overflow, stats).
@@ -47,11 +49,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
-        import torch.distributed as dist  # gloo: barrier + max over ranks (host side only)
-        dist.init_process_group("gloo")
     import signature_kmers_amd as skm
     from signature_kmers_amd import synth
+    uid = None
+    if world > 1:
+        import torch.distributed as dist  # gloo: rendezvous, barrier, max over ranks (host side)
+        dist.init_process_group("gloo")
+        box = [skm.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
 
     # ---- synthetic shard (one RNG stream per file: shards are rank-independent) ----
     per_file = 4000
@@ -63,8 +69,10 @@ def main():
     gen_s = time.time() - t0
     n_windows = int(np.where((f != 0xFFFF) & (l >= 8), l.astype(np.int64) - 7, 0).sum())
 
-    b = skm.SignatureBuilder(len(funcs), device=local)
+    b = skm.SignatureBuilder(len(funcs), device=local, rank=rank, world_size=world)
     b.add_batch(r, o, l, f, i)
+    if uid is not None:
+        b.set_comm(uid)  # RCCL communicator over the world (data-path exchange)
     b.prepare()
 
     def barrier():
@@ -93,25 +101,25 @@ def main():
         total_windows = float(nw.item())
     else:
         total_windows = float(n_windows)
-    kept = b.finish()
     ms_per_step = 1000.0 * t_max / a.steps
     value = total_windows * a.steps / t_max
     phase = {k: v / a.steps for k, v in phase.items()}
 
     # ---- roofline: dominant kernel (bucket group-by) and the whole pipeline ----
-    n_records = int(kept.n_windows)  # upper bound; exact record count below
     res_bytes = int(len(r) + len(l))
-    valid = _valid_windows(r, o, l, f)
-    n_kept = len(kept.keys)
+    valid = _valid_windows(r, o, l, f)          # occurrence elements this rank extracts
+    ctrs = b.counters()
+    grouped = ctrs["grouped"]                   # elements this rank groups (after the exchange)
+    n_kept = ctrs["kept"]                       # kept k-mers this rank owns
     dom = max(("extract_count", "extract_scatter", "bucket_process"), key=lambda k: phase.get(k, 0.0))
     alg = {
         "extract_count": res_bytes,
         "extract_scatter": res_bytes + 16 * valid,   # 16-byte occurrence elements written once
-        "bucket_process": 16 * valid + 18 * n_kept,  # ... read once; kept keys + records written
+        "bucket_process": 16 * grouped + 18 * n_kept,  # ... read once; kept keys + records written
     }
     dom_ms = phase[dom]
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
-    pipe_alg = res_bytes + 32 * valid + 18 * n_kept  # SURVEY 8(d) B_alg
+    pipe_alg = res_bytes + 16 * valid + 16 * grouped + 18 * n_kept  # SURVEY 8(d) B_alg
     pipe_gbs = pipe_alg / (phase["total"] * 1e-3) / 1e9
     traffic = _pmc_traffic(dom, a.seqs)
 
@@ -130,8 +138,9 @@ def main():
         "data": "synthetic (SURVEY 8(d) generator, seed 20241115)",
         "config": {"workload": "C2: 1M protein seqs/GPU, k=8, signature build (extract+group+cut+stats)",
                    "seqs_per_gpu": a.seqs, "families": a.families, "windows_per_gpu": n_windows,
-                   "valid_windows_per_gpu": valid, "kept_kmers_rank0": n_kept,
-                   "parallelism": "single GPU" if world == 1 else f"{world} GPUs, independent shards"},
+                   "valid_windows_per_gpu": valid, "kept_kmers_rank0": n_kept, "grouped_elements_rank0": grouped,
+                   "parallelism": "single GPU" if world == 1 else
+                   f"{world} GPUs, owner-partitioned RCCL all-to-all + all-reduce"},
         "roofline": {"bound": "hbm", "kernel": f"k_{dom}", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "alg_bytes_per_launch": alg[dom], "avg_launch_ms": dom_ms},

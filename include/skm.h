@@ -109,10 +109,12 @@ int skm_build_prepare(skm_build* b);
 /* Run the device pipeline over the resident input; results stay on the device. */
 int skm_build_run(skm_build* b);
 /* Device time (ms) of the last run's phases: [0]=extract-count [1]=scan [2]=extract-scatter
- * [3]=bucket-process [4]=overflow [5]=chains [6]=stats [7]=total; returns entries written. */
+ * [3]=bucket-process [4]=overflow [5]=chains [6]=stats (+ reductions) [7]=total
+ * [8]=exchange (world_size > 1); returns entries written. */
 int skm_build_last_timings(skm_build* b, float* ms, int cap);
-/* Counters of the last run: [0]=windows [1]=kept [2]=overflow sub-buckets [3]=chain jobs
- * [4]=chain samples [5]=sequences; returns entries written. */
+/* Counters of the last run: [0]=windows [1]=kept (owned by this rank) [2]=overflow sub-buckets
+ * [3]=chain jobs [4]=chain samples [5]=sequences [6]=occurrences grouped on this rank;
+ * returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then
  * enable/disable stamping for subsequent runs. */
@@ -121,19 +123,27 @@ int skm_build_debug_stamps(skm_build* b, int enable, uint64_t* out, int cap);
 int skm_build_debug_jobs(skm_build* b, uint32_t* out, int cap);
 /* Diagnostics: device time of the chain kernel on njobs synthetic jobs of length n. */
 int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms);
-/* Run (if not yet run since the last prepare) and download the result. */
+/* Run (if not yet run since the last prepare) and download the result.  With world_size > 1
+ * this is collective: rank 0 receives every rank's kept k-mers (keys sorted), the other ranks
+ * the k-mers they own; the statistics are global on every rank. */
 int skm_build_finish(skm_build* b, skm_kept* out);
 void skm_kept_free(skm_kept* k);
 void skm_build_destroy(skm_build* b);
 
 /* ------------------------------------------------------------------------------------------
- * Multi-GPU (one process per GPU).  Rank 0 calls skm_comm_unique_id, the caller broadcasts the
- * 128 bytes (e.g. torch.distributed over gloo), every rank passes them to
- * skm_build_set_comm before skm_build_run.  Owner of a k-mer = top bits of its hashed key;
- * records are exchanged with one RCCL all-to-all over xGMI.
+ * Multi-GPU (one process per GPU; opts.rank / opts.world_size, a power of two).  Rank r adds
+ * the r-th contiguous range of files (emission order is rank order).  Rank 0 calls
+ * skm_comm_unique_id, the caller broadcasts the 128 bytes (e.g. torch.distributed over gloo),
+ * every rank passes them to skm_build_set_comm (collective) before prepare/run.  Owner of a
+ * k-mer = top bits of its hashed key; occurrence elements are exchanged with one RCCL
+ * all-to-all over xGMI, then per-function counts (sum) and signature flags (max) are
+ * all-reduced.  prepare / run / finish are collective.
  * ------------------------------------------------------------------------------------------ */
 int skm_comm_unique_id(uint8_t id[128]);
 int skm_build_set_comm(skm_build* b, const uint8_t id[128]);
+/* Test/diagnostic transport: run n handles of ranks 0..n-1 (world_size n) in this process,
+ * exchanging through device copies instead of RCCL; skm_build_finish on any member afterwards. */
+int skm_build_group_run(skm_build* const* bs, int n);
 
 /* ------------------------------------------------------------------------------------------
  * Signature DB (CmphKmerDb<StoredKmerData,8>, cmph_kmer.h:28-164).  Reads a cmph BDZ dump

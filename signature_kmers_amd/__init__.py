@@ -77,6 +77,7 @@ _SIGS = {
     "skm_build_destroy": (None, [_P]),
     "skm_comm_unique_id": (C.c_int, [_P]),
     "skm_build_set_comm": (C.c_int, [_P, _P]),
+    "skm_build_group_run": (C.c_int, [C.POINTER(_P), C.c_int]),
     "skm_db_open": (C.c_int, [C.POINTER(_P), C.c_char_p, C.c_char_p, C.c_int]),
     "skm_db_open_mem": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, _P, C.c_size_t, C.c_int]),
     "skm_db_size": (C.c_int, [_P, C.POINTER(C.c_uint32)]),
@@ -175,9 +176,11 @@ class SignatureBuilder:
     Sequences are added in reference emission order with their FunctionIndex (0xFFFF = no kept
     function) and seq_id (file_number * max_seqs_per_file + k)."""
 
-    def __init__(self, n_functions: int, max_seqs_per_file: int = 100000, device: int = 0):
+    def __init__(self, n_functions: int, max_seqs_per_file: int = 100000, device: int = 0, rank: int = 0,
+                 world_size: int = 1):
         self._h = C.c_void_p()
-        opts = _BuildOpts(8, max_seqs_per_file, n_functions, 1, 0, 1)
+        opts = _BuildOpts(8, max_seqs_per_file, n_functions, 1, rank, world_size)
+        self.rank, self.world_size = rank, world_size
         dev = (C.c_int * 1)(device)
         _check(lib().skm_build_create(C.byref(self._h), dev, 1, C.byref(opts)))
         self.n_functions = n_functions
@@ -197,6 +200,11 @@ class SignatureBuilder:
         _check(lib().skm_build_add_batch(self._h, _ptr(residues), _ptr(seq_off), _ptr(seq_len), _ptr(seq_func),
                                          _ptr(sid) if sid is not None else None, n))
 
+    def set_comm(self, unique_id: bytes):
+        """Join the RCCL communicator (collective over the world_size ranks)."""
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
+        _check(lib().skm_build_set_comm(self._h, buf))
+
     def prepare(self):
         _check(lib().skm_build_prepare(self._h))
 
@@ -204,15 +212,16 @@ class SignatureBuilder:
         _check(lib().skm_build_run(self._h))
 
     def timings(self) -> dict:
-        ms = (C.c_float * 8)()
-        n = lib().skm_build_last_timings(self._h, ms, 8)
-        names = ["extract_count", "scan", "extract_scatter", "bucket_process", "overflow", "chains", "stats", "total"]
+        ms = (C.c_float * 9)()
+        n = lib().skm_build_last_timings(self._h, ms, 9)
+        names = ["extract_count", "scan", "extract_scatter", "bucket_process", "overflow", "chains", "stats", "total",
+                 "exchange"]
         return {names[i]: float(ms[i]) for i in range(n)}
 
     def counters(self) -> dict:
         v = (C.c_uint64 * 8)()
         n = lib().skm_build_counters(self._h, v, 8)
-        names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences"]
+        names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped"]
         return {names[i]: int(v[i]) for i in range(n)}
 
     def debug_jobs(self, k: int = 64) -> list:
@@ -251,6 +260,20 @@ class SignatureBuilder:
             self.close()
         except Exception:
             pass
+
+
+def comm_unique_id() -> bytes:
+    """128-byte RCCL unique id (rank 0 creates it; broadcast it to every rank's set_comm)."""
+    buf = (C.c_uint8 * 128)()
+    _check(lib().skm_comm_unique_id(buf))
+    return bytes(buf)
+
+
+def group_run(builders) -> None:
+    """Run ranks 0..n-1 of one build inside this process (device-copy exchange instead of RCCL);
+    used to test the multi-GPU path on one device."""
+    arr = (C.c_void_p * len(builders))(*[b._h.value for b in builders])
+    _check(lib().skm_build_group_run(arr, len(builders)))
 
 
 def mph_build(keys: np.ndarray, data: np.ndarray, mph_path: str, dat_path: str, seed: int = 1):

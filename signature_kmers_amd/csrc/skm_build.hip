@@ -170,8 +170,8 @@ struct SigStats {
 constexpr uint32_t REM_MASK = 0x7FFFFFFFu;   // rem <= 31 bits; bit 47 of hi is the big-length flag
 
 // protein length of an element: carried mod 2^16 unless the big-length flag is set
-__device__ __forceinline__ uint32_t elem_len(uint64_t hi, uint64_t lo, const SeqMeta* __restrict__ meta) {
-    return ((hi >> 47) & 1u) ? meta[lo >> 36].len : (uint32_t)(hi >> 48);
+__device__ __forceinline__ uint32_t elem_len(uint64_t hi, uint64_t lo, const uint32_t* __restrict__ glen) {
+    return ((hi >> 47) & 1u) ? glen[lo >> 36] : (uint32_t)(hi >> 48);
 }
 
 // 16-byte occurrence element (written by the extract-scatter kernel, read by the bucket kernel):
@@ -320,7 +320,7 @@ __device__ __forceinline__ void stats_small(GRes& r, uint32_t x0, uint32_t x1, u
 
 // Thread-level group of c <= N members starting at a.
 template <int N, class V>
-__device__ GRes group_thread(const V& v, uint64_t a, uint32_t c, const SeqMeta* __restrict__ meta,
+__device__ GRes group_thread(const V& v, uint64_t a, uint32_t c, const uint32_t* __restrict__ glen,
                              uint8_t* __restrict__ flags) {
     GRes r;
     r.kept = false;
@@ -370,7 +370,7 @@ __device__ GRes group_thread(const V& v, uint64_t a, uint32_t c, const SeqMeta* 
         const uint32_t s = (uint32_t)(lo >> 36);
         flags[s] = 1;
         if (t >= rb && t < rb + best_c) {
-            const uint32_t len = meta[s].len;
+            const uint32_t len = glen[s];
             sum += len;
             const uint32_t q = rb + best_c - 1 - t;  // visit position (reverse ordinal)
             if (q == 0) lr0 = len;
@@ -403,7 +403,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 // Wave-level group (all 64 lanes, same a/c).  Only used for c > SMALLC, so the best run always
 // has >= 3 members and its median/var are deferred.
 template <class V>
-__device__ GRes group_wave(const V& v, uint64_t a, uint32_t c, const SeqMeta* __restrict__ meta,
+__device__ GRes group_wave(const V& v, uint64_t a, uint32_t c, const uint32_t* __restrict__ glen,
                            uint8_t* __restrict__ flags) {
     const uint32_t lane = threadIdx.x & 63u;
     GRes r;
@@ -468,7 +468,7 @@ __device__ GRes group_wave(const V& v, uint64_t a, uint32_t c, const SeqMeta* __
     for (uint32_t t = lane; t < c; t += 64) {
         const uint32_t s = (uint32_t)(v.lov(a + t) >> 36);
         flags[s] = 1;
-        if (t >= rb && t < rb + best_c) sum += meta[s].len;
+        if (t >= rb && t < rb + best_c) sum += glen[s];
     }
     sum = wave_sum(sum);
     r.mean = d2u16((double)(uint16_t)sum / (double)best_c);
@@ -744,11 +744,15 @@ struct BucketArgs {
     const uint64_t* recs_lo;
     uint64_t* tmp_hi;          // level-2 partition scratch, same indexing as recs
     uint64_t* tmp_lo;
-    const uint64_t* bstart;    // [nbuckets+1] absolute starts in recs
+    const uint64_t* bstart;    // [nbuckets+1] bucket starts (in recs when nsrc == 1; in tmp always)
+    const uint64_t* seg_start; // nsrc > 1: [nsrc][nbuckets] start of each source rank's piece in recs
+    const uint32_t* seg_len;   // nsrc > 1: [nsrc][nbuckets] its length
+    uint32_t nsrc;             // 1, or the world size after the all-to-all exchange
     uint32_t nbuckets;
     uint32_t bucket_base;      // global bucket id of bucket 0 (owner << b1_bits)
     int rem_bits;
-    const SeqMeta* meta;       // indexed by global sequence (only proteins >= 65536 residues read it)
+    const uint32_t* glen;      // protein length by global sequence index (read only for lengths >= 65536
+                               // and by overflow sub-buckets)
     uint8_t* flags;
     unsigned long long* ctr;   // [0] kept [1] overflow entries [2] flagged seqs [3] jobs [4] lens
     uint64_t* out_keys;
@@ -831,7 +835,7 @@ __device__ __forceinline__ void reg_sort_pairs(uint64_t* k, uint32_t* v) {
 // Thread-level group (c <= N members at order[a..a+c)): members sorted in registers by
 // (func, ordinal); the sorted member list is written back so the best run is contiguous.
 template <int N>
-__device__ __forceinline__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint32_t c, const SeqMeta* __restrict__ meta,
+__device__ __forceinline__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint32_t c, const uint32_t* __restrict__ glen,
                               uint8_t* __restrict__ flags) {
     GRes r;
     r.kept = false;
@@ -887,8 +891,8 @@ __device__ __forceinline__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint3
                 const uint64_t hj = L.hi[idx[t]];
                 sum += (uint32_t)(hj >> 48);  // len mod 2^16 is all the u16 sum keeps
                 const uint32_t q = rb + best_c - 1 - t;  // visit position (reverse ordinal)
-                if (q == 0) lr0 = elem_len(hj, lo, meta);
-                if (q == 1) lr1 = elem_len(hj, lo, meta);
+                if (q == 0) lr0 = elem_len(hj, lo, glen);
+                if (q == 1) lr1 = elem_len(hj, lo, glen);
             }
         }
     }
@@ -908,7 +912,7 @@ __device__ __forceinline__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint3
 #pragma unroll
         for (int t = 0; t < N; ++t)
             if ((uint32_t)t >= rb && (uint32_t)t < rb + best_c)
-                L.lens32[a + (rb + best_c - 1 - t)] = elem_len(L.hi[idx[t]], L.lo[idx[t]], meta);  // visit order
+                L.lens32[a + (rb + best_c - 1 - t)] = elem_len(L.hi[idx[t]], L.lo[idx[t]], glen);  // visit order
     }
     return r;
 }
@@ -963,7 +967,7 @@ __device__ __forceinline__ void bm_combine(uint32_t& cand, uint32_t& cc) {
 }
 
 // Wave-level group with c <= 64: one member per lane, everything in registers.
-__device__ __forceinline__ GRes lgroup_wave64(const SubLds& L, uint32_t a, uint32_t c, const SeqMeta* __restrict__ meta,
+__device__ __forceinline__ GRes lgroup_wave64(const SubLds& L, uint32_t a, uint32_t c, const uint32_t* __restrict__ glen,
                                               uint8_t* __restrict__ flags) {
     const uint32_t lane = threadIdx.x & 63u;
     GRes r;
@@ -995,13 +999,13 @@ __device__ __forceinline__ GRes lgroup_wave64(const SubLds& L, uint32_t a, uint3
     uint64_t key = best ? lj : ~0ull;
     uint32_t idx = j;
     wave_sort64(key, idx);
-    if (lane < nb) L.lens32[a + (nb - 1 - lane)] = elem_len(L.hi[idx], key, meta);  // reverse ordinal
+    if (lane < nb) L.lens32[a + (nb - 1 - lane)] = elem_len(L.hi[idx], key, glen);  // reverse ordinal
     return r;
 }
 
-__device__ __forceinline__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const SeqMeta* __restrict__ meta,
+__device__ __forceinline__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const uint32_t* __restrict__ glen,
                             uint8_t* __restrict__ flags) {
-    if (c <= 64) return lgroup_wave64(L, a, c, meta, flags);
+    if (c <= 64) return lgroup_wave64(L, a, c, glen, flags);
     const uint32_t lane = threadIdx.x & 63u;
     GRes r;
     r.kept = false;
@@ -1141,7 +1145,7 @@ __device__ __forceinline__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_
     }
     for (uint32_t t = lane; t < nb; t += 64) {
         const uint32_t jj = L.order[a + t];
-        L.lens32[a + (nb - 1 - t)] = elem_len(L.hi[jj], L.lo[jj], meta);  // reverse ordinal
+        L.lens32[a + (nb - 1 - t)] = elem_len(L.hi[jj], L.lo[jj], glen);  // reverse ordinal
     }
     return r;
 }
@@ -1266,11 +1270,11 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
         GRes r;
         if (c <= 2)
-            r = lgroup_thread<2>(L, a, c, A.meta, A.flags);
+            r = lgroup_thread<2>(L, a, c, A.glen, A.flags);
         else if (c <= 4)
-            r = lgroup_thread<4>(L, a, c, A.meta, A.flags);
+            r = lgroup_thread<4>(L, a, c, A.glen, A.flags);
         else
-            r = lgroup_thread<8>(L, a, c, A.meta, A.flags);
+            r = lgroup_thread<8>(L, a, c, A.glen, A.flags);
         stage(r, rep, a);
     }
     __syncthreads();
@@ -1283,7 +1287,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
             const uint32_t rep = L.glist[g];
             const uint32_t a = L.goff[rep];
             const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
-            const GRes r = lgroup_wave(L, a, c, A.meta, A.flags);
+            const GRes r = lgroup_wave(L, a, c, A.glen, A.flags);
             if ((tid & 63u) == 0) stage(r, rep, a);
         }
     }
@@ -1364,7 +1368,7 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     const uint64_t hprefix = (uint64_t)(A.bucket_base + bucket) << A.rem_bits;
     const uint64_t rem_mask = (1ull << A.rem_bits) - 1;
 
-    if (n <= (uint64_t)CAP) {
+    if (n <= (uint64_t)CAP && A.nsrc == 1) {
         L.lens32 = reinterpret_cast<uint32_t*>(A.recs_hi + r0);
         L.lens_sel = (LENS_IN_RECS << LENS_SEL_SHIFT) | (2 * r0);
         process_sub(A.recs_hi + r0, A.recs_lo + r0, (uint32_t)n, A, hprefix, L);
@@ -1379,9 +1383,24 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     const int shift = A.rem_bits - b2;
     for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_sub[d] = 0;
     __syncthreads();
-    for (uint64_t j = threadIdx.x; j < n; j += blockDim.x) {
-        const uint64_t h = A.recs_hi[r0 + j];
-        atomicAdd(&s_sub[(uint32_t)(((h >> 16) & rem_mask) >> shift)], 1u);
+    // the bucket's elements: one contiguous range, or one piece per source rank after the exchange
+    const uint32_t nseg = A.nsrc;
+    auto seg = [&](uint32_t p, uint64_t& base, uint64_t& len) {
+        if (nseg == 1) {
+            base = r0;
+            len = n;
+        } else {
+            base = A.seg_start[(uint64_t)p * A.nbuckets + bucket];
+            len = A.seg_len[(uint64_t)p * A.nbuckets + bucket];
+        }
+    };
+    for (uint32_t p = 0; p < nseg; ++p) {
+        uint64_t base, len;
+        seg(p, base, len);
+        for (uint64_t j = threadIdx.x; j < len; j += blockDim.x) {
+            const uint64_t h = A.recs_hi[base + j];
+            atomicAdd(&s_sub[(uint32_t)(((h >> 16) & rem_mask) >> shift)], 1u);
+        }
     }
     __syncthreads();
     SKM_STAMP(0);
@@ -1404,12 +1423,16 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     uint32_t* s_cur = reinterpret_cast<uint32_t*>(s_hi);
     for (uint32_t d = threadIdx.x; d < nsub; d += blockDim.x) s_cur[d] = s_sub[d];
     __syncthreads();
-    for (uint64_t j = threadIdx.x; j < n; j += blockDim.x) {
-        const uint64_t h = A.recs_hi[r0 + j];
-        const uint64_t l = A.recs_lo[r0 + j];
-        const uint32_t o = atomicAdd(&s_cur[(uint32_t)(((h >> 16) & rem_mask) >> shift)], 1u);
-        A.tmp_hi[r0 + o] = h;
-        A.tmp_lo[r0 + o] = l;
+    for (uint32_t p = 0; p < nseg; ++p) {
+        uint64_t base, len;
+        seg(p, base, len);
+        for (uint64_t j = threadIdx.x; j < len; j += blockDim.x) {
+            const uint64_t h = A.recs_hi[base + j];
+            const uint64_t l = A.recs_lo[base + j];
+            const uint32_t o = atomicAdd(&s_cur[(uint32_t)(((h >> 16) & rem_mask) >> shift)], 1u);
+            A.tmp_hi[r0 + o] = h;
+            A.tmp_lo[r0 + o] = l;
+        }
     }
     __threadfence_block();
     __syncthreads();
@@ -1560,11 +1583,11 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
             } else {
                 GRes r;
                 if (c <= 4)
-                    r = group_thread<4>(V, a, c, A.meta, A.flags);
+                    r = group_thread<4>(V, a, c, A.glen, A.flags);
                 else if (c <= 8)
-                    r = group_thread<8>(V, a, c, A.meta, A.flags);
+                    r = group_thread<8>(V, a, c, A.glen, A.flags);
                 else
-                    r = group_thread<16>(V, a, c, A.meta, A.flags);
+                    r = group_thread<16>(V, a, c, A.glen, A.flags);
                 stage(r, a);
             }
         }
@@ -1574,7 +1597,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
             const uint32_t gg = s_big[bi];
             const uint32_t a = heads[gg];
             const uint32_t b = gg + 1 < G ? heads[gg + 1] : n;
-            const GRes r = group_wave(V, a, b - a, A.meta, A.flags);
+            const GRes r = group_wave(V, a, b - a, A.glen, A.flags);
             if ((tid & 63u) == 0) stage(r, a);
         }
         __threadfence_block();
@@ -1616,7 +1639,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
                 if (jn <= 64) {
                     const uint64_t start = jb >> 32;
                     for (uint32_t t = 0; t < jn; ++t)
-                        A.lens[jbr.lens_off + t] = A.meta[glo[start + jn - 1 - t] >> 36].len;
+                        A.lens[jbr.lens_off + t] = A.glen[glo[start + jn - 1 - t] >> 36];
                 } else {
                     const uint32_t bi = atomicAdd(&s_nbig, 1u);
                     s_big[bi] = g;
@@ -1636,7 +1659,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
             const uint32_t nq = (uint32_t)(jbq & 0xFFFFFFFFu);
             const uint64_t start = jbq >> 32;
             const uint64_t loff = s_lo[q];
-            for (uint32_t t = tid; t < nq; t += nt) A.lens[loff + t] = A.meta[glo[start + nq - 1 - t] >> 36].len;
+            for (uint32_t t = tid; t < nq; t += nt) A.lens[loff + t] = A.glen[glo[start + nq - 1 - t] >> 36];
         }
         __syncthreads();
     }
@@ -1705,7 +1728,7 @@ struct skm_build {
     skm_build_opts opts{};
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[9] = {};
+    hipEvent_t ev[10] = {};
     float last_ms[9] = {};
 
     // host staging (reference emission order, only sequences with a kept function)
@@ -1717,15 +1740,19 @@ struct skm_build {
     bool prepared = false, ran = false;
 
     // device input
-    DevBuf d_res, d_meta, d_blk2seq;
+    DevBuf d_res, d_meta, d_blk2seq, d_glen;
     uint64_t rp = 0;       // packed length
     uint32_t nseq = 0;
-    // geometry
+    // geometry / ranks
+    int world = 1, rank = 0;
     int owner_bits = 0, b1_bits = 12;
+    uint32_t s_base = 0;   // global index of this shard's first sequence
+    uint32_t n_total = 0;  // sequences over all ranks
+    std::vector<uint32_t> g_seqid;  // world > 1: all ranks' seq ids in global order (finish)
+    bool g_strict = true;
     // device work
     DevBuf d_hist, d_offs, d_partial, d_rbbase, d_bstart32, d_bstart, d_owner_start;
     DevBuf d_recs_hi, d_recs_lo, d_tmp_hi, d_tmp_lo;
-    uint32_t s_base = 0;   // global index of this shard's first sequence
     DevBuf d_keys, d_data, d_ctr, d_flags, d_dfunc, d_swf, d_ovf, d_ovf_hi, d_ovf_lo, d_ovf_heads, d_ovf_job, d_ovf_fm;
     DevBuf d_jobs, d_lens, d_stamps, d_job_hist, d_job_offs, d_jobs_sorted;
     bool stamps = false;
@@ -1733,31 +1760,25 @@ struct skm_build {
     uint32_t n_overflow = 0;
     uint32_t nwg = 0;
     uint64_t span = 0;
-    uint64_t n_records = 0;
     uint64_t n_kept = 0;
     uint64_t ovf_cap = 0;
 
-    // multi-GPU
+    // world > 1: owner-partitioned exchange
+    DevBuf d_rhi, d_rlo;                 // received elements, [source rank][level-1 bucket]
+    DevBuf d_cnt_send, d_cnt_recv;       // [world][NB1] element counts
+    DevBuf d_seg_start, d_seg_len, d_vstart;
+    std::vector<uint64_t> send_off, send_cnt, recv_off, recv_cnt;
+    uint64_t n_local = 0;                // elements this rank groups (received, or extracted at world 1)
+    uint64_t cap_local = 0;
+
+    // transport: RCCL communicator, or the in-process rank group used by the tests
 #if defined(SKM_WITH_RCCL)
     ncclComm_t comm = nullptr;
 #endif
-    bool has_comm = false;
+    std::vector<skm_build*> group;
 };
 
 namespace {
-
-void bucket_starts_abs(skm_build* b, std::vector<uint64_t>& starts) {
-    // host helper: build absolute bucket starts from owner-relative u32 starts (single GPU)
-    const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
-    std::vector<uint32_t> rel(NB + 1);
-    std::vector<uint64_t> ost((1u << b->owner_bits) + 1);
-    SKM_HIP(hipMemcpyAsync(rel.data(), b->d_bstart32.p, sizeof(uint32_t) * (NB + 1), hipMemcpyDeviceToHost, b->stream));
-    SKM_HIP(hipMemcpyAsync(ost.data(), b->d_owner_start.p, sizeof(uint64_t) * ost.size(), hipMemcpyDeviceToHost, b->stream));
-    SKM_HIP(hipStreamSynchronize(b->stream));
-    starts.resize(NB + 1);
-    for (uint32_t k = 0; k < NB; ++k) starts[k] = ost[k >> b->b1_bits] + rel[k];
-    starts[NB] = ost[1u << b->owner_bits];
-}
 
 __global__ void k_abs_starts(const uint32_t* rel, const uint64_t* ost, uint32_t NB, int b1_bits, uint32_t nowners,
                              uint64_t* out) {
@@ -1766,17 +1787,311 @@ __global__ void k_abs_starts(const uint32_t* rel, const uint64_t* ost, uint32_t 
     if (k == NB) out[NB] = ost[nowners];
 }
 
-void run_pipeline(skm_build* b) {
+// ------------------------------------------------------------------------------------------
+// Collectives over the ranks of one build.  `bs` lists the handles this process drives: {b}
+// with an RCCL communicator (one process per GPU), or every rank of an in-process group
+// (skm_build_group_run; the exchange is then plain device copies).  All are stream-ordered on
+// each handle's stream; the group form synchronises around each step.
+// ------------------------------------------------------------------------------------------
+using Ranks = std::vector<skm_build*>;
+
+bool is_group(const Ranks& bs) { return bs.size() > 1 || (bs[0]->world > 1 && !bs[0]->group.empty()); }
+
+void sync_all(const Ranks& bs) {
+    for (auto* b : bs) SKM_HIP(hipStreamSynchronize(b->stream));
+}
+
+#if defined(SKM_WITH_RCCL)
+#define SKM_NCCL(x)                                                                              \
+    do {                                                                                         \
+        ncclResult_t _r = (x);                                                                   \
+        if (_r != ncclSuccess) throw skm::Error(SKM_E_COMM, std::string("RCCL: ") + ncclGetErrorString(_r)); \
+    } while (0)
+#endif
+
+// all-to-all with variable counts: rank p sends send[p] + soff[p][q] (scnt[p][q] bytes) to rank q,
+// which receives it at recv[q] + roff[q][p].
+struct A2A {
+    std::vector<const uint8_t*> send;
+    std::vector<uint8_t*> recv;
+    std::vector<std::vector<uint64_t>> soff, scnt, roff, rcnt;  // bytes, [local handle][peer]
+};
+
+void alltoallv(const Ranks& bs, const A2A& x) {
+    if (is_group(bs)) {
+        sync_all(bs);
+        const size_t W = bs.size();
+        for (size_t p = 0; p < W; ++p)
+            for (size_t q = 0; q < W; ++q)
+                if (x.scnt[p][q])
+                    SKM_HIP(hipMemcpyAsync(x.recv[q] + x.roff[q][p], x.send[p] + x.soff[p][q], x.scnt[p][q],
+                                           hipMemcpyDeviceToDevice, bs[q]->stream));
+        sync_all(bs);
+        return;
+    }
+#if defined(SKM_WITH_RCCL)
+    skm_build* b = bs[0];
+    const int W = b->world, me = b->rank;
+    if (x.scnt[0][me])
+        SKM_HIP(hipMemcpyAsync(x.recv[0] + x.roff[0][me], x.send[0] + x.soff[0][me], x.scnt[0][me],
+                               hipMemcpyDeviceToDevice, b->stream));
+    SKM_NCCL(ncclGroupStart());
+    for (int q = 0; q < W; ++q) {
+        if (q == me) continue;
+        if (x.scnt[0][q]) SKM_NCCL(ncclSend(x.send[0] + x.soff[0][q], x.scnt[0][q], ncclUint8, q, b->comm, b->stream));
+        if (x.rcnt[0][q]) SKM_NCCL(ncclRecv(x.recv[0] + x.roff[0][q], x.rcnt[0][q], ncclUint8, q, b->comm, b->stream));
+    }
+    SKM_NCCL(ncclGroupEnd());
+#else
+    throw Error(SKM_E_COMM, "libskm was built without RCCL");
+#endif
+}
+
+// element-wise reduction of a device array across ranks (in place): u32 sum or u8 max
+enum class Red { SumU32, MaxU8 };
+
+void allreduce(const Ranks& bs, const std::vector<void*>& ptr, size_t count, Red op) {
+    if (count == 0) return;
+    if (is_group(bs)) {
+        sync_all(bs);
+        const size_t es = op == Red::SumU32 ? 4 : 1;
+        std::vector<uint8_t> acc(count * es, 0), tmp(count * es);
+        for (size_t r = 0; r < bs.size(); ++r) {
+            SKM_HIP(hipMemcpy(tmp.data(), ptr[r], count * es, hipMemcpyDeviceToHost));
+            if (op == Red::SumU32) {
+                auto* a = reinterpret_cast<uint32_t*>(acc.data());
+                auto* t = reinterpret_cast<const uint32_t*>(tmp.data());
+                for (size_t i = 0; i < count; ++i) a[i] += t[i];
+            } else {
+                for (size_t i = 0; i < count; ++i) acc[i] = std::max(acc[i], tmp[i]);
+            }
+        }
+        for (size_t r = 0; r < bs.size(); ++r) SKM_HIP(hipMemcpy(ptr[r], acc.data(), count * es, hipMemcpyHostToDevice));
+        return;
+    }
+#if defined(SKM_WITH_RCCL)
+    skm_build* b = bs[0];
+    if (op == Red::SumU32)
+        SKM_NCCL(ncclAllReduce(ptr[0], ptr[0], count, ncclUint32, ncclSum, b->comm, b->stream));
+    else
+        SKM_NCCL(ncclAllReduce(ptr[0], ptr[0], count, ncclUint8, ncclMax, b->comm, b->stream));
+#else
+    throw Error(SKM_E_COMM, "libskm was built without RCCL");
+#endif
+}
+
+// gather one u64 per rank to every rank (host values)
+std::vector<uint64_t> allgather_u64(const Ranks& bs, const std::vector<uint64_t>& mine) {
+    if (is_group(bs)) return mine;  // one value per handle, already in rank order
+#if defined(SKM_WITH_RCCL)
+    skm_build* b = bs[0];
+    DevBuf d;
+    d.ensure(8 * (b->world + 1));
+    SKM_HIP(hipMemcpyAsync(d.as<uint64_t>() + b->rank, &mine[0], 8, hipMemcpyHostToDevice, b->stream));
+    SKM_NCCL(ncclAllGather(d.as<uint64_t>() + b->rank, d.p, 1, ncclUint64, b->comm, b->stream));
+    std::vector<uint64_t> out(b->world);
+    SKM_HIP(hipMemcpyAsync(out.data(), d.p, 8 * b->world, hipMemcpyDeviceToHost, b->stream));
+    SKM_HIP(hipStreamSynchronize(b->stream));
+    return out;
+#else
+    throw Error(SKM_E_COMM, "libskm was built without RCCL");
+#endif
+}
+
+// every rank receives the rank-ordered concatenation of all ranks' device arrays
+void allgatherv(const Ranks& bs, const std::vector<const void*>& src, const std::vector<void*>& dst,
+                const std::vector<uint64_t>& bytes_per_rank) {
+    const size_t W = bytes_per_rank.size();
+    std::vector<uint64_t> off(W + 1, 0);
+    for (size_t r = 0; r < W; ++r) off[r + 1] = off[r] + bytes_per_rank[r];
+    if (is_group(bs)) {
+        sync_all(bs);
+        for (size_t q = 0; q < bs.size(); ++q)
+            for (size_t r = 0; r < W; ++r)
+                if (bytes_per_rank[r])
+                    SKM_HIP(hipMemcpy(static_cast<uint8_t*>(dst[q]) + off[r], src[r], bytes_per_rank[r],
+                                      hipMemcpyDeviceToDevice));
+        return;
+    }
+#if defined(SKM_WITH_RCCL)
+    skm_build* b = bs[0];
+    SKM_NCCL(ncclGroupStart());
+    for (int r = 0; r < b->world; ++r)
+        if (bytes_per_rank[r])
+            SKM_NCCL(ncclBroadcast(r == b->rank ? src[0] : nullptr, static_cast<uint8_t*>(dst[0]) + off[r],
+                                   bytes_per_rank[r], ncclUint8, r, b->comm, b->stream));
+    SKM_NCCL(ncclGroupEnd());
+#else
+    throw Error(SKM_E_COMM, "libskm was built without RCCL");
+#endif
+}
+
+// ------------------------------------------------------------------------------------------
+// prepare: pack + upload; with world > 1 also the global sequence numbering
+// ------------------------------------------------------------------------------------------
+void set_geometry(skm_build* b) {
+    b->world = std::max(1, b->opts.world_size);
+    b->rank = b->opts.rank;
+    int ob = 0;
+    while ((1 << ob) < b->world) ++ob;
+    b->owner_bits = ob;
+    // 4096 level-1 buckets in total (8192 from 4 ranks up); rem <= 31 bits leaves element bit 47
+    // for the big-length flag
+    const int total = 12 + (ob >= 2 ? 1 : 0);
+    b->b1_bits = total - ob;
+}
+
+void prepare_local(skm_build* b) {
+    SKM_HIP(hipSetDevice(b->device));
+    set_geometry(b);
+    const uint64_t rp = b->h_res.size();
+    b->rp = rp;
+    b->nseq = (uint32_t)b->h_meta.size();
+    SKM_CHECK(b->h_meta.size() < (1ull << ELEM_S_BITS), SKM_E_ARG, "too many sequences in one build shard");
+    SKM_CHECK(b->n_windows < (1ull << 32), SKM_E_ARG, "more than 2^32 windows in one GPU shard");
+    // upload
+    b->d_res.ensure(rp + 64);
+    SKM_HIP(hipMemsetAsync(b->d_res.p, 0, rp + 64, b->stream));
+    if (rp) SKM_HIP(hipMemcpyAsync(b->d_res.p, b->h_res.data(), rp, hipMemcpyHostToDevice, b->stream));
+    b->d_meta.ensure(sizeof(SeqMeta) * (b->nseq + 1));
+    SeqMeta sentinel{rp, 0, 0xFFFF, 0};
+    std::vector<SeqMeta> meta = b->h_meta;
+    meta.push_back(sentinel);
+    SKM_HIP(hipMemcpyAsync(b->d_meta.p, meta.data(), sizeof(SeqMeta) * meta.size(), hipMemcpyHostToDevice, b->stream));
+    const uint64_t nblk = (rp >> 6) + 1;
+    b->d_blk2seq.ensure(sizeof(uint32_t) * nblk);
+    SKM_HIP(hipMemsetAsync(b->d_blk2seq.p, 0, sizeof(uint32_t) * nblk, b->stream));
+    if (b->nseq)
+        hipLaunchKernelGGL(k_blk2seq, dim3((b->nseq + 255) / 256), dim3(256), 0, b->stream, b->d_meta.as<SeqMeta>(), b->nseq,
+                           b->d_blk2seq.as<uint32_t>(), nblk);
+    SKM_HIP(hipGetLastError());
+    // extract geometry + work buffers
+    const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
+    uint64_t step = (uint64_t)EX_THREADS * EX_POS_PER_THREAD;
+    uint64_t nwg = std::max<uint64_t>(1, std::min<uint64_t>(EX_MAX_WG, ceil_div(rp ? rp : 1, step)));
+    b->span = ceil_div(ceil_div(rp ? rp : 1, nwg), step) * step;
+    b->nwg = (uint32_t)ceil_div(rp ? rp : 1, b->span);
+    const uint32_t nrb = (uint32_t)ceil_div(b->nwg, SCAN_ROWS);
+    b->d_hist.ensure(sizeof(uint32_t) * (uint64_t)b->nwg * NB);
+    b->d_offs.ensure(sizeof(uint32_t) * (uint64_t)b->nwg * NB);
+    b->d_partial.ensure(sizeof(uint32_t) * (uint64_t)nrb * NB);
+    b->d_rbbase.ensure(sizeof(uint32_t) * (uint64_t)nrb * NB);
+    b->d_bstart32.ensure(sizeof(uint32_t) * (NB + 1));
+    b->d_bstart.ensure(sizeof(uint64_t) * (NB + 1));
+    b->d_owner_start.ensure(sizeof(uint64_t) * 80);
+    const uint64_t W = b->n_windows;
+    b->d_recs_hi.ensure(8 * std::max<uint64_t>(W, 1));
+    b->d_recs_lo.ensure(8 * std::max<uint64_t>(W, 1));
+    b->d_ctr.ensure(128);
+    b->d_dfunc.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
+    b->d_swf.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
+}
+
+// buffers sized by the number of elements this rank groups
+void ensure_local(skm_build* b, uint64_t n) {
+    if (n <= b->cap_local && b->cap_local) return;
+    const uint64_t c = std::max<uint64_t>(n + n / 16, 1);
+    if (b->world > 1) {
+        b->d_rhi.ensure(8 * c);
+        b->d_rlo.ensure(8 * c);
+    }
+    b->d_tmp_hi.ensure(8 * c);
+    b->d_tmp_lo.ensure(8 * c);
+    b->d_keys.ensure(8 * c);
+    b->d_data.ensure(sizeof(skm_stored_kmer_data) * c + 16);
+    const uint32_t NB1 = 1u << b->b1_bits;
+    b->ovf_cap = c / CAP + NB1 + 16;
+    b->jobs_cap = c / 3 + 16;
+    b->lens_cap = c + 16;
+    b->d_jobs.ensure(sizeof(Job) * b->jobs_cap);
+    b->d_lens.ensure(sizeof(uint32_t) * b->lens_cap);
+    b->d_ovf.ensure(sizeof(OvfEntry) * b->ovf_cap);
+    b->cap_local = c;
+}
+
+void prepare(const Ranks& bs) {
+    bool need = false;
+    for (auto* b : bs) need |= !b->prepared;
+    if (!need) return;
+    for (auto* b : bs) prepare_local(b);
+    skm_build* b0 = bs[0];
+    if (b0->world == 1) {
+        b0->s_base = 0;
+        b0->n_total = b0->nseq;
+        b0->d_glen.ensure(4 * (b0->nseq + 1));
+        std::vector<uint32_t> len(b0->nseq);
+        for (uint32_t s = 0; s < b0->nseq; ++s) len[s] = b0->h_meta[s].len;
+        if (b0->nseq) SKM_HIP(hipMemcpyAsync(b0->d_glen.p, len.data(), 4 * b0->nseq, hipMemcpyHostToDevice, b0->stream));
+        ensure_local(b0, b0->n_windows);
+    } else {
+        // global sequence numbering: ranks hold contiguous file ranges in rank order
+        std::vector<uint64_t> mine;
+        for (auto* b : bs) mine.push_back(b->nseq);
+        const std::vector<uint64_t> ns = allgather_u64(bs, mine);
+        uint64_t tot = 0;
+        for (auto v : ns) tot += v;
+        SKM_CHECK(tot < (1ull << ELEM_S_BITS), SKM_E_ARG, "too many sequences in one build");
+        std::vector<uint64_t> bytes(ns.size());
+        for (size_t r = 0; r < ns.size(); ++r) bytes[r] = 4 * ns[r];
+        std::vector<DevBuf> lens_src(bs.size()), ids_src(bs.size()), ids_all(bs.size());
+        std::vector<const void*> src_l, src_i;
+        std::vector<void*> dst_l, dst_i;
+        for (size_t k = 0; k < bs.size(); ++k) {
+            skm_build* b = bs[k];
+            uint64_t base = 0;
+            for (int r = 0; r < b->rank; ++r) base += ns[r];
+            b->s_base = (uint32_t)base;
+            b->n_total = (uint32_t)tot;
+            std::vector<uint32_t> len(b->nseq);
+            for (uint32_t s = 0; s < b->nseq; ++s) len[s] = b->h_meta[s].len;
+            lens_src[k].ensure(4 * (b->nseq + 1));
+            ids_src[k].ensure(4 * (b->nseq + 1));
+            ids_all[k].ensure(4 * (tot + 1));
+            b->d_glen.ensure(4 * (tot + 1));
+            SKM_HIP(hipMemcpy(lens_src[k].p, len.data(), 4 * b->nseq, hipMemcpyHostToDevice));
+            SKM_HIP(hipMemcpy(ids_src[k].p, b->h_seqid.data(), 4 * b->nseq, hipMemcpyHostToDevice));
+            src_l.push_back(lens_src[k].p);
+            src_i.push_back(ids_src[k].p);
+            dst_l.push_back(b->d_glen.p);
+            dst_i.push_back(ids_all[k].p);
+        }
+        if (is_group(bs)) {  // allgatherv takes every rank's source in the group form
+            allgatherv(bs, src_l, dst_l, bytes);
+            allgatherv(bs, src_i, dst_i, bytes);
+        } else {
+            allgatherv(bs, {src_l[0]}, {dst_l[0]}, bytes);
+            allgatherv(bs, {src_i[0]}, {dst_i[0]}, bytes);
+        }
+        sync_all(bs);
+        for (size_t k = 0; k < bs.size(); ++k) {
+            skm_build* b = bs[k];
+            b->g_seqid.resize(tot);
+            if (tot) SKM_HIP(hipMemcpy(b->g_seqid.data(), ids_all[k].p, 4 * tot, hipMemcpyDeviceToHost));
+            b->g_strict = true;
+            for (uint64_t s = 1; s < tot; ++s)
+                if (b->g_seqid[s] <= b->g_seqid[s - 1]) b->g_strict = false;
+            ensure_local(b, b->n_windows);  // first guess; grown at run time if the exchange brings more
+        }
+    }
+    for (auto* b : bs) {
+        b->d_flags.ensure(std::max<uint64_t>(b->n_total, 1));
+        SKM_HIP(hipStreamSynchronize(b->stream));
+        b->prepared = true;
+        b->ran = false;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// run: extract -> [exchange] -> group-by -> chains -> statistics [-> reductions]
+// ------------------------------------------------------------------------------------------
+void phase_extract(skm_build* b) {
     hipStream_t st = b->stream;
     const int nbits = b->owner_bits + b->b1_bits;
     const uint32_t NB = 1u << nbits;
     const uint32_t nowners = 1u << b->owner_bits;
-    const int rem_bits = KEY_BITS - nbits;
-    const uint32_t F = b->opts.n_functions;
-
     SKM_HIP(hipEventRecord(b->ev[0], st));
     // ---- 1. count ----
-    size_t lds_cnt = sizeof(uint32_t) * NB;
+    const size_t lds_cnt = sizeof(uint32_t) * NB;
     ExtractArgs X;
     X.res = b->d_res.as<uint8_t>();
     X.rp = b->rp;
@@ -1810,19 +2125,115 @@ void run_pipeline(skm_build* b) {
     hipLaunchKernelGGL(k_extract<true>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, X);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[3], st));
+}
+
+// world > 1: send layout from the local bucket starts, counts all-to-all, receive layout
+void exchange(const Ranks& bs) {
+    const int W = bs[0]->world;
+    const uint32_t NB1 = 1u << bs[0]->b1_bits;
+    const uint32_t NB = NB1 * (uint32_t)W;
+    // 1. per-peer counts of its buckets
+    A2A cx;
+    for (auto* b : bs) {
+        std::vector<uint64_t> abs(NB + 1);
+        SKM_HIP(hipMemcpyAsync(abs.data(), b->d_bstart.p, 8 * (NB + 1), hipMemcpyDeviceToHost, b->stream));
+        SKM_HIP(hipStreamSynchronize(b->stream));
+        std::vector<uint32_t> cnt(NB);
+        for (uint32_t k = 0; k < NB; ++k) cnt[k] = (uint32_t)(abs[k + 1] - abs[k]);
+        b->send_off.assign(W, 0);
+        b->send_cnt.assign(W, 0);
+        for (int q = 0; q < W; ++q) {
+            b->send_off[q] = abs[(uint64_t)q * NB1];
+            b->send_cnt[q] = abs[(uint64_t)(q + 1) * NB1] - abs[(uint64_t)q * NB1];
+        }
+        b->d_cnt_send.ensure(4ull * NB);
+        b->d_cnt_recv.ensure(4ull * NB);
+        SKM_HIP(hipMemcpyAsync(b->d_cnt_send.p, cnt.data(), 4ull * NB, hipMemcpyHostToDevice, b->stream));
+        cx.send.push_back(b->d_cnt_send.as<uint8_t>());
+        cx.recv.push_back(b->d_cnt_recv.as<uint8_t>());
+        std::vector<uint64_t> off(W), c(W, 4ull * NB1);
+        for (int q = 0; q < W; ++q) off[q] = 4ull * NB1 * q;
+        cx.soff.push_back(off);
+        cx.scnt.push_back(c);
+        cx.roff.push_back(off);
+        cx.rcnt.push_back(c);
+    }
+    alltoallv(bs, cx);
+    // 2. receive layout: source-major pieces, bucket-major virtual numbering for tmp
+    A2A ex_hi, ex_lo;
+    for (auto* b : bs) {
+        std::vector<uint32_t> rc(NB);  // [source][bucket]
+        SKM_HIP(hipMemcpyAsync(rc.data(), b->d_cnt_recv.p, 4ull * NB, hipMemcpyDeviceToHost, b->stream));
+        SKM_HIP(hipStreamSynchronize(b->stream));
+        b->recv_off.assign(W, 0);
+        b->recv_cnt.assign(W, 0);
+        std::vector<uint64_t> seg_start(NB), bucket_tot(NB1, 0), vstart(NB1 + 1, 0);
+        std::vector<uint32_t> seg_len(NB);
+        uint64_t run = 0;
+        for (int p = 0; p < W; ++p) {
+            b->recv_off[p] = run;
+            for (uint32_t k = 0; k < NB1; ++k) {
+                const uint32_t c = rc[(uint64_t)p * NB1 + k];
+                seg_start[(uint64_t)p * NB1 + k] = run;
+                seg_len[(uint64_t)p * NB1 + k] = c;
+                bucket_tot[k] += c;
+                run += c;
+            }
+            b->recv_cnt[p] = run - b->recv_off[p];
+        }
+        for (uint32_t k = 0; k < NB1; ++k) vstart[k + 1] = vstart[k] + bucket_tot[k];
+        b->n_local = run;
+        ensure_local(b, run);
+        b->d_seg_start.ensure(8ull * NB);
+        b->d_seg_len.ensure(4ull * NB);
+        b->d_vstart.ensure(8ull * (NB1 + 1));
+        SKM_HIP(hipMemcpyAsync(b->d_seg_start.p, seg_start.data(), 8ull * NB, hipMemcpyHostToDevice, b->stream));
+        SKM_HIP(hipMemcpyAsync(b->d_seg_len.p, seg_len.data(), 4ull * NB, hipMemcpyHostToDevice, b->stream));
+        SKM_HIP(hipMemcpyAsync(b->d_vstart.p, vstart.data(), 8ull * (NB1 + 1), hipMemcpyHostToDevice, b->stream));
+        std::vector<uint64_t> so(W), sc(W), ro(W), rcn(W);
+        for (int q = 0; q < W; ++q) {
+            so[q] = 8 * b->send_off[q];
+            sc[q] = 8 * b->send_cnt[q];
+            ro[q] = 8 * b->recv_off[q];
+            rcn[q] = 8 * b->recv_cnt[q];
+        }
+        ex_hi.send.push_back(b->d_recs_hi.as<uint8_t>());
+        ex_hi.recv.push_back(b->d_rhi.as<uint8_t>());
+        ex_lo.send.push_back(b->d_recs_lo.as<uint8_t>());
+        ex_lo.recv.push_back(b->d_rlo.as<uint8_t>());
+        for (A2A* e : {&ex_hi, &ex_lo}) {
+            e->soff.push_back(so);
+            e->scnt.push_back(sc);
+            e->roff.push_back(ro);
+            e->rcnt.push_back(rcn);
+        }
+    }
+    alltoallv(bs, ex_hi);
+    alltoallv(bs, ex_lo);
+}
+
+void phase_group(skm_build* b) {
+    hipStream_t st = b->stream;
+    const uint32_t F = b->opts.n_functions;
+    const bool multi = b->world > 1;
+    const uint32_t NB1 = 1u << b->b1_bits;
+    SKM_HIP(hipEventRecord(b->ev[4], st));
     // ---- 4. bucket process ----
     SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 128, st));
-    SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->nseq ? b->nseq : 1, st));
+    SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->n_total ? b->n_total : 1, st));
     BucketArgs A;
-    A.recs_hi = b->d_recs_hi.as<uint64_t>();
-    A.recs_lo = b->d_recs_lo.as<uint64_t>();
+    A.recs_hi = multi ? b->d_rhi.as<uint64_t>() : b->d_recs_hi.as<uint64_t>();
+    A.recs_lo = multi ? b->d_rlo.as<uint64_t>() : b->d_recs_lo.as<uint64_t>();
     A.tmp_hi = b->d_tmp_hi.as<uint64_t>();
     A.tmp_lo = b->d_tmp_lo.as<uint64_t>();
-    A.bstart = b->d_bstart.as<uint64_t>();
-    A.nbuckets = NB;
-    A.bucket_base = 0;
-    A.rem_bits = rem_bits;
-    A.meta = b->d_meta.as<SeqMeta>();
+    A.bstart = multi ? b->d_vstart.as<uint64_t>() : b->d_bstart.as<uint64_t>();
+    A.seg_start = multi ? b->d_seg_start.as<uint64_t>() : nullptr;
+    A.seg_len = multi ? b->d_seg_len.as<uint32_t>() : nullptr;
+    A.nsrc = multi ? (uint32_t)b->world : 1u;
+    A.nbuckets = NB1;
+    A.bucket_base = (uint32_t)b->rank << b->b1_bits;
+    A.rem_bits = KEY_BITS - b->owner_bits - b->b1_bits;
+    A.glen = b->d_glen.as<uint32_t>();
     A.flags = b->d_flags.as<uint8_t>();
     A.ctr = b->d_ctr.as<unsigned long long>();
     A.out_keys = b->d_keys.as<uint64_t>();
@@ -1837,12 +2248,13 @@ void run_pipeline(skm_build* b) {
         SKM_HIP(hipMemsetAsync(b->d_stamps.p, 0, 16 * 8, st));
         A.stamps = b->d_stamps.as<unsigned long long>();
     }
-    hipLaunchKernelGGL(k_bucket_process, dim3(NB), dim3(BP_THREADS), 0, st, A);
+    hipLaunchKernelGGL(k_bucket_process, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
-    SKM_HIP(hipEventRecord(b->ev[4], st));
+    SKM_HIP(hipEventRecord(b->ev[5], st));
     // ---- 5. overflow ----
     unsigned long long ctr[5];
     SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, sizeof(ctr), hipMemcpyDeviceToHost, st));
+    if (!multi) SKM_HIP(hipMemcpyAsync(&b->n_local, b->d_bstart.as<uint64_t>() + NB1, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
     const uint32_t novf = (uint32_t)(ctr[1] & 0xFFFFFFFFull);
     SKM_CHECK(novf <= b->ovf_cap, SKM_E_OOM, "overflow list capacity exceeded");
@@ -1874,7 +2286,7 @@ void run_pipeline(skm_build* b) {
         hipLaunchKernelGGL(k_overflow, dim3(novf), dim3(BP_THREADS), 0, st, A, S);
         SKM_HIP(hipGetLastError());
     }
-    SKM_HIP(hipEventRecord(b->ev[5], st));
+    SKM_HIP(hipEventRecord(b->ev[6], st));
     // ---- 6. deferred P^2 / variance chains ----
     SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, sizeof(ctr), hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
@@ -1897,12 +2309,12 @@ void run_pipeline(skm_build* b) {
                            b->d_job_offs.as<uint64_t>(), b->d_jobs_sorted.as<Job>());
         const uint64_t threads = ceil_div(nj, 64) * 128;
         hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, st,
-                           b->d_jobs_sorted.as<Job>(), nj, b->d_lens.as<uint32_t>(), b->d_recs_hi.as<uint32_t>(),
+                           b->d_jobs_sorted.as<Job>(), nj, b->d_lens.as<uint32_t>(), A.recs_hi ? reinterpret_cast<const uint32_t*>(A.recs_hi) : nullptr,
                            b->d_tmp_hi.as<uint32_t>(), b->d_data.as<skm_stored_kmer_data>());
     }
     SKM_HIP(hipGetLastError());
-    SKM_HIP(hipEventRecord(b->ev[6], st));
-    // ---- 7. stats ----
+    SKM_HIP(hipEventRecord(b->ev[7], st));
+    // ---- 7. per-rank statistics ----
     SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     const size_t lds_f = F <= 16384 ? sizeof(uint32_t) * F : 0;
@@ -1912,77 +2324,48 @@ void run_pipeline(skm_build* b) {
     if (b->nseq)
         hipLaunchKernelGGL(k_func_hist_seqs, dim3(256), dim3(256), lds_f, st, b->d_meta.as<SeqMeta>(), b->nseq, F,
                            b->d_swf.as<uint32_t>());
-    hipLaunchKernelGGL(k_count_flags, dim3(256), dim3(256), 0, st, b->d_flags.as<uint8_t>(), b->nseq,
+    SKM_HIP(hipGetLastError());
+}
+
+void phase_final(skm_build* b) {
+    hipStream_t st = b->stream;
+    hipLaunchKernelGGL(k_count_flags, dim3(256), dim3(256), 0, st, b->d_flags.as<uint8_t>(), b->n_total,
                        b->d_ctr.as<unsigned long long>() + 2);
     SKM_HIP(hipGetLastError());
-    SKM_HIP(hipEventRecord(b->ev[7], st));
-    SKM_HIP(hipEventSynchronize(b->ev[7]));
-    for (int i = 0; i < 7; ++i) SKM_HIP(hipEventElapsedTime(&b->last_ms[i], b->ev[i], b->ev[i + 1]));
-    SKM_HIP(hipEventElapsedTime(&b->last_ms[7], b->ev[0], b->ev[7]));
+    SKM_HIP(hipEventRecord(b->ev[8], st));
+    SKM_HIP(hipEventSynchronize(b->ev[8]));
+    // [0] extract-count [1] scan [2] extract-scatter [3] bucket [4] overflow [5] chains
+    // [6] stats (+ reductions) [7] total [8] exchange
+    const int from[7] = {0, 1, 2, 4, 5, 6, 7}, to[7] = {1, 2, 3, 5, 6, 7, 8};
+    for (int i = 0; i < 7; ++i) SKM_HIP(hipEventElapsedTime(&b->last_ms[i], b->ev[from[i]], b->ev[to[i]]));
+    SKM_HIP(hipEventElapsedTime(&b->last_ms[7], b->ev[0], b->ev[8]));
+    SKM_HIP(hipEventElapsedTime(&b->last_ms[8], b->ev[3], b->ev[4]));
     b->ran = true;
 }
 
-void prepare(skm_build* b) {
-    if (b->prepared) return;
-    SKM_HIP(hipSetDevice(b->device));
-    const uint64_t rp = b->h_res.size();
-    b->rp = rp;
-    b->nseq = (uint32_t)b->h_meta.size();
-    SKM_CHECK(b->h_meta.size() < (1ull << ELEM_S_BITS), SKM_E_ARG, "too many sequences in one build shard");
-    // geometry: 4096 level-1 buckets; rem = 31 bits leaves element bit 47 for the big-length flag
-    b->owner_bits = 0;
-    b->b1_bits = 12;
-    SKM_CHECK(b->n_windows < (1ull << 32), SKM_E_ARG, "more than 2^32 windows in one GPU shard");
-    // upload
-    b->d_res.ensure(rp + 64);
-    SKM_HIP(hipMemsetAsync(b->d_res.p, 0, rp + 64, b->stream));
-    if (rp) SKM_HIP(hipMemcpyAsync(b->d_res.p, b->h_res.data(), rp, hipMemcpyHostToDevice, b->stream));
-    b->d_meta.ensure(sizeof(SeqMeta) * (b->nseq + 1));
-    SeqMeta sentinel{rp, 0, 0xFFFF, 0};
-    std::vector<SeqMeta> meta = b->h_meta;
-    meta.push_back(sentinel);
-    SKM_HIP(hipMemcpyAsync(b->d_meta.p, meta.data(), sizeof(SeqMeta) * meta.size(), hipMemcpyHostToDevice, b->stream));
-    const uint64_t nblk = (rp >> 6) + 1;
-    b->d_blk2seq.ensure(sizeof(uint32_t) * nblk);
-    SKM_HIP(hipMemsetAsync(b->d_blk2seq.p, 0, sizeof(uint32_t) * nblk, b->stream));
-    if (b->nseq)
-        hipLaunchKernelGGL(k_blk2seq, dim3((b->nseq + 255) / 256), dim3(256), 0, b->stream, b->d_meta.as<SeqMeta>(), b->nseq,
-                           b->d_blk2seq.as<uint32_t>(), nblk);
-    SKM_HIP(hipGetLastError());
-    // work buffers
-    const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
-    uint64_t step = (uint64_t)EX_THREADS * EX_POS_PER_THREAD;
-    uint64_t nwg = std::max<uint64_t>(1, std::min<uint64_t>(EX_MAX_WG, ceil_div(rp ? rp : 1, step)));
-    b->span = ceil_div(ceil_div(rp ? rp : 1, nwg), step) * step;
-    b->nwg = (uint32_t)ceil_div(rp ? rp : 1, b->span);
-    const uint32_t nrb = (uint32_t)ceil_div(b->nwg, SCAN_ROWS);
-    b->d_hist.ensure(sizeof(uint32_t) * (uint64_t)b->nwg * NB);
-    b->d_offs.ensure(sizeof(uint32_t) * (uint64_t)b->nwg * NB);
-    b->d_partial.ensure(sizeof(uint32_t) * (uint64_t)nrb * NB);
-    b->d_rbbase.ensure(sizeof(uint32_t) * (uint64_t)nrb * NB);
-    b->d_bstart32.ensure(sizeof(uint32_t) * (NB + 1));
-    b->d_bstart.ensure(sizeof(uint64_t) * (NB + 1));
-    b->d_owner_start.ensure(sizeof(uint64_t) * 16);
-    const uint64_t W = b->n_windows;
-    b->d_recs_hi.ensure(8 * std::max<uint64_t>(W, 1));
-    b->d_recs_lo.ensure(8 * std::max<uint64_t>(W, 1));
-    b->d_tmp_hi.ensure(8 * std::max<uint64_t>(W, 1));
-    b->d_tmp_lo.ensure(8 * std::max<uint64_t>(W, 1));
-    b->d_keys.ensure(8 * std::max<uint64_t>(W, 1));
-    b->d_data.ensure(sizeof(skm_stored_kmer_data) * std::max<uint64_t>(W, 1) + 16);
-    b->d_ctr.ensure(128);
-    b->d_flags.ensure(std::max<uint64_t>(b->nseq, 1));
-    b->d_dfunc.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
-    b->d_swf.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
-    b->ovf_cap = W / CAP + NB + 16;
-    b->jobs_cap = W / 3 + 16;
-    b->lens_cap = W + 16;
-    b->d_jobs.ensure(sizeof(Job) * b->jobs_cap);
-    b->d_lens.ensure(sizeof(uint32_t) * b->lens_cap);
-    b->d_ovf.ensure(sizeof(OvfEntry) * b->ovf_cap);
-    SKM_HIP(hipStreamSynchronize(b->stream));
-    b->prepared = true;
-    b->ran = false;
+void run_ranks(const Ranks& bs) {
+    prepare(bs);
+    for (auto* b : bs) phase_extract(b);
+    if (bs[0]->world > 1) exchange(bs);
+    for (auto* b : bs) phase_group(b);
+    if (bs[0]->world > 1) {
+        std::vector<void*> df, sw, fl;
+        for (auto* b : bs) {
+            df.push_back(b->d_dfunc.p);
+            sw.push_back(b->d_swf.p);
+            fl.push_back(b->d_flags.p);
+        }
+        const uint32_t F = bs[0]->opts.n_functions;
+        allreduce(bs, df, F, Red::SumU32);
+        allreduce(bs, sw, F, Red::SumU32);
+        allreduce(bs, fl, bs[0]->n_total, Red::MaxU8);
+    }
+    for (auto* b : bs) phase_final(b);
+}
+
+Ranks ranks_of(skm_build* b) {
+    if (!b->group.empty()) return b->group;
+    return Ranks{b};
 }
 
 }  // namespace
@@ -1995,16 +2378,20 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     SKM_CHECK(opts->k == 8, SKM_E_ARG, "only k = 8 is supported (kmers-build-signatures.cc:17)");
     SKM_CHECK(opts->n_functions < 0xFFFFu, SKM_E_ARG, "n_functions must be < 65535");
     SKM_CHECK(n_devices == 1, SKM_E_ARG, "one device per process (multi-GPU: one process per GPU)");
-    SKM_CHECK(opts->world_size == 1 || opts->world_size == 0, SKM_E_ARG, "world_size > 1 requires skm_build_set_comm");
+    const int ws = std::max(1, opts->world_size);
+    SKM_CHECK(ws <= 64 && (ws & (ws - 1)) == 0, SKM_E_ARG, "world_size must be a power of two <= 64");
+    SKM_CHECK(opts->rank >= 0 && opts->rank < ws, SKM_E_ARG, "rank out of range");
     int ndev = 0;
     SKM_HIP(hipGetDeviceCount(&ndev));
     SKM_CHECK(ndev > 0, SKM_E_HIP, "no HIP device");
     auto* b = new skm_build();
     b->opts = *opts;
+    b->opts.world_size = ws;
     b->device = devices ? devices[0] : 0;
     SKM_HIP(hipSetDevice(b->device));
     SKM_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
     for (auto& e : b->ev) SKM_HIP(hipEventCreate(&e));
+    set_geometry(b);
     *out = b;
     SKM_API_END
 }
@@ -2038,19 +2425,76 @@ int skm_build_add_batch(skm_build* b, const uint8_t* residues, const uint64_t* s
     SKM_API_END
 }
 
+static void check_transport(skm_build* b) {
+#if defined(SKM_WITH_RCCL)
+    const bool comm = b->comm != nullptr;
+#else
+    const bool comm = false;
+#endif
+    SKM_CHECK(b->world == 1 || comm || !b->group.empty(), SKM_E_STATE,
+              "world_size > 1 needs skm_build_set_comm (or skm_build_group_run) first");
+}
+
 int skm_build_prepare(skm_build* b) {
     SKM_API_BEGIN
     SKM_CHECK(b, SKM_E_ARG, "null build");
-    prepare(b);
+    check_transport(b);
+    SKM_HIP(hipSetDevice(b->device));
+    prepare(ranks_of(b));
     SKM_API_END
 }
 
 int skm_build_run(skm_build* b) {
     SKM_API_BEGIN
     SKM_CHECK(b, SKM_E_ARG, "null build");
+    check_transport(b);
     SKM_HIP(hipSetDevice(b->device));
-    prepare(b);
-    run_pipeline(b);
+    run_ranks(ranks_of(b));
+    SKM_API_END
+}
+
+int skm_build_group_run(skm_build* const* bs, int n) {
+    SKM_API_BEGIN
+    SKM_CHECK(bs && n >= 1, SKM_E_ARG, "null argument");
+    Ranks g(bs, bs + n);
+    for (int r = 0; r < n; ++r) {
+        SKM_CHECK(g[r], SKM_E_ARG, "null build");
+        SKM_CHECK(g[r]->world == n && g[r]->rank == r, SKM_E_ARG, "group member r must have rank r and world_size n");
+    }
+    for (auto* b : g) b->group = n > 1 ? g : Ranks{};
+    SKM_HIP(hipSetDevice(g[0]->device));
+    run_ranks(n > 1 ? g : Ranks{g[0]});
+    SKM_API_END
+}
+
+int skm_comm_unique_id(uint8_t id[128]) {
+    SKM_API_BEGIN
+    SKM_CHECK(id, SKM_E_ARG, "null argument");
+#if defined(SKM_WITH_RCCL)
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId must be 128 bytes");
+    ncclUniqueId u;
+    SKM_NCCL(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, 128);
+#else
+    std::memset(id, 0, 128);
+    throw Error(SKM_E_COMM, "libskm was built without RCCL");
+#endif
+    SKM_API_END
+}
+
+int skm_build_set_comm(skm_build* b, const uint8_t id[128]) {
+    SKM_API_BEGIN
+    SKM_CHECK(b && id, SKM_E_ARG, "null argument");
+#if defined(SKM_WITH_RCCL)
+    SKM_CHECK(b->comm == nullptr, SKM_E_STATE, "communicator already set");
+    SKM_HIP(hipSetDevice(b->device));
+    if (b->world == 1) return SKM_OK;
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    SKM_NCCL(ncclCommInitRank(&b->comm, b->world, u, b->rank));
+#else
+    throw Error(SKM_E_COMM, "libskm was built without RCCL");
+#endif
     SKM_API_END
 }
 
@@ -2116,15 +2560,15 @@ int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms) {
 
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
-    const uint64_t v[6] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq};
-    int n = std::min(cap, 6);
+    const uint64_t v[7] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local};
+    int n = std::min(cap, 7);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }
 
 int skm_build_last_timings(skm_build* b, float* ms, int cap) {
     if (!b || !ms) return SKM_E_ARG;
-    int n = std::min(cap, 8);
+    int n = std::min(cap, 9);
     for (int i = 0; i < n; ++i) ms[i] = b->last_ms[i];
     return n;
 }
@@ -2132,18 +2576,83 @@ int skm_build_last_timings(skm_build* b, float* ms, int cap) {
 int skm_build_finish(skm_build* b, skm_kept* out) {
     SKM_API_BEGIN
     SKM_CHECK(b && out, SKM_E_ARG, "null argument");
+    check_transport(b);
     SKM_HIP(hipSetDevice(b->device));
-    prepare(b);
-    if (!b->ran) run_pipeline(b);
+    const Ranks bs = ranks_of(b);
+    bool need = false;
+    for (auto* x : bs) need |= !x->prepared || !x->ran;
+    if (need) run_ranks(bs);
     std::memset(out, 0, sizeof(*out));
-    const uint64_t n = b->n_kept;
     const uint32_t F = b->opts.n_functions;
+    // kept k-mers: rank 0 gathers every rank's owned k-mers; other ranks return their own
+    std::vector<uint64_t> mine;
+    for (auto* x : bs) mine.push_back(x->n_kept);
+    const std::vector<uint64_t> nk = b->world > 1 ? allgather_u64(bs, mine) : mine;
+    uint64_t total = 0;
+    for (auto v : nk) total += v;
+    const bool gather = b->world > 1 && b->rank == 0;
+    const uint64_t n = gather ? total : b->n_kept;
     std::vector<uint64_t> keys(n);
     std::vector<skm_stored_kmer_data> data(n);
-    unsigned long long ctr[3];
-    if (n) {
+    if (b->world > 1 && !bs.empty() && bs.size() > 1) {  // in-process group: plain copies
+        if (gather) {
+            uint64_t o = 0;
+            for (auto* x : bs) {
+                if (x->n_kept) {
+                    SKM_HIP(hipMemcpy(keys.data() + o, x->d_keys.p, 8 * x->n_kept, hipMemcpyDeviceToHost));
+                    SKM_HIP(hipMemcpy(data.data() + o, x->d_data.p, sizeof(skm_stored_kmer_data) * x->n_kept,
+                                      hipMemcpyDeviceToHost));
+                }
+                o += x->n_kept;
+            }
+        } else if (n) {
+            SKM_HIP(hipMemcpy(keys.data(), b->d_keys.p, 8 * n, hipMemcpyDeviceToHost));
+            SKM_HIP(hipMemcpy(data.data(), b->d_data.p, sizeof(skm_stored_kmer_data) * n, hipMemcpyDeviceToHost));
+        }
+    } else if (b->world > 1) {  // RCCL: every rank sends its k-mers to rank 0
+        const int W = b->world;
+        DevBuf gk, gd;
+        A2A xk, xd;
+        std::vector<uint64_t> so(W, 0), sck(W, 0), scd(W, 0), rok(W, 0), rod(W, 0), rck(W, 0), rcd(W, 0);
+        sck[0] = 8 * b->n_kept;
+        scd[0] = sizeof(skm_stored_kmer_data) * b->n_kept;
+        if (gather) {
+            gk.ensure(8 * (total + 1));
+            gd.ensure(sizeof(skm_stored_kmer_data) * (total + 1));
+            uint64_t o = 0;
+            for (int r = 0; r < W; ++r) {
+                rok[r] = 8 * o;
+                rod[r] = sizeof(skm_stored_kmer_data) * o;
+                rck[r] = 8 * nk[r];
+                rcd[r] = sizeof(skm_stored_kmer_data) * nk[r];
+                o += nk[r];
+            }
+        }
+        xk.send = {b->d_keys.as<uint8_t>()};
+        xk.recv = {gather ? gk.as<uint8_t>() : nullptr};
+        xk.soff = {so};
+        xk.scnt = {sck};
+        xk.roff = {rok};
+        xk.rcnt = {rck};
+        xd.send = {b->d_data.as<uint8_t>()};
+        xd.recv = {gather ? gd.as<uint8_t>() : nullptr};
+        xd.soff = {so};
+        xd.scnt = {scd};
+        xd.roff = {rod};
+        xd.rcnt = {rcd};
+        alltoallv(bs, xk);
+        alltoallv(bs, xd);
+        SKM_HIP(hipStreamSynchronize(b->stream));
+        const void* sk = gather ? gk.p : b->d_keys.p;
+        const void* sd = gather ? gd.p : b->d_data.p;
+        if (n) {
+            SKM_HIP(hipMemcpy(keys.data(), sk, 8 * n, hipMemcpyDeviceToHost));
+            SKM_HIP(hipMemcpy(data.data(), sd, sizeof(skm_stored_kmer_data) * n, hipMemcpyDeviceToHost));
+        }
+    } else if (n) {
         SKM_HIP(hipMemcpyAsync(keys.data(), b->d_keys.p, 8 * n, hipMemcpyDeviceToHost, b->stream));
-        SKM_HIP(hipMemcpyAsync(data.data(), b->d_data.p, sizeof(skm_stored_kmer_data) * n, hipMemcpyDeviceToHost, b->stream));
+        SKM_HIP(hipMemcpyAsync(data.data(), b->d_data.p, sizeof(skm_stored_kmer_data) * n, hipMemcpyDeviceToHost,
+                               b->stream));
     }
     out->distinct_functions = (uint32_t*)std::malloc(sizeof(uint32_t) * std::max<uint32_t>(F, 1));
     out->seqs_with_func = (uint32_t*)std::malloc(sizeof(uint32_t) * std::max<uint32_t>(F, 1));
@@ -2152,11 +2661,13 @@ int skm_build_finish(skm_build* b, skm_kept* out) {
         SKM_HIP(hipMemcpyAsync(out->distinct_functions, b->d_dfunc.p, sizeof(uint32_t) * F, hipMemcpyDeviceToHost, b->stream));
         SKM_HIP(hipMemcpyAsync(out->seqs_with_func, b->d_swf.p, sizeof(uint32_t) * F, hipMemcpyDeviceToHost, b->stream));
     }
+    unsigned long long ctr[3];
     SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, sizeof(ctr), hipMemcpyDeviceToHost, b->stream));
+    const bool strict = b->world > 1 ? b->g_strict : b->seqid_strict;
     std::vector<uint8_t> flags;
-    if (!b->seqid_strict) {
-        flags.resize(b->nseq);
-        if (b->nseq) SKM_HIP(hipMemcpyAsync(flags.data(), b->d_flags.p, b->nseq, hipMemcpyDeviceToHost, b->stream));
+    if (!strict) {
+        flags.resize(b->n_total);
+        if (b->n_total) SKM_HIP(hipMemcpyAsync(flags.data(), b->d_flags.p, b->n_total, hipMemcpyDeviceToHost, b->stream));
     }
     SKM_HIP(hipStreamSynchronize(b->stream));
     // deterministic output order: sort by key
@@ -2172,18 +2683,19 @@ int skm_build_finish(skm_build* b, skm_kept* out) {
     }
     out->n = n;
     out->n_functions = F;
-    out->distinct_signatures = n;
-    if (b->seqid_strict) {
+    out->distinct_signatures = total;
+    if (strict) {
         out->n_seqs_with_signature = ctr[2];
     } else {  // colliding seq ids (files with > max_seqs_per_file sequences): count distinct ids
+        const std::vector<uint32_t>& sid = b->world > 1 ? b->g_seqid : b->h_seqid;
         std::vector<uint32_t> ids;
-        for (uint32_t s = 0; s < b->nseq; ++s)
-            if (flags[s]) ids.push_back(b->h_seqid[s]);
+        for (uint32_t s = 0; s < b->n_total; ++s)
+            if (flags[s]) ids.push_back(sid[s]);
         std::sort(ids.begin(), ids.end());
         out->n_seqs_with_signature = (uint64_t)(std::unique(ids.begin(), ids.end()) - ids.begin());
     }
     out->n_windows = b->n_windows;
-    out->n_records = 0;
+    out->n_records = b->n_local;
     SKM_API_END
 }
 
@@ -2200,6 +2712,11 @@ void skm_build_destroy(skm_build* b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
+#if defined(SKM_WITH_RCCL)
+    if (b->comm) (void)ncclCommDestroy(b->comm);
+#endif
+    for (auto* x : b->group)  // leave the other members usable on their own
+        if (x != b) x->group.clear();
     for (auto& e : b->ev)
         if (e) (void)hipEventDestroy(e);
     if (b->stream) (void)hipStreamDestroy(b->stream);

@@ -223,20 +223,4 @@ int skm_find_best_call(const skm_kmer_call* calls_in, size_t ncalls, const char*
     SKM_API_END
 }
 
-// Multi-GPU communicator (RCCL).  The exchange path is compiled in only with SKM_WITH_RCCL.
-int skm_comm_unique_id(uint8_t id[128]) {
-    SKM_API_BEGIN
-    SKM_CHECK(id, SKM_E_ARG, "null argument");
-    std::memset(id, 0, 128);
-    throw Error(SKM_E_COMM, "libskm was built without RCCL support");
-    SKM_API_END
-}
-
-int skm_build_set_comm(skm_build* b, const uint8_t id[128]) {
-    SKM_API_BEGIN
-    SKM_CHECK(b && id, SKM_E_ARG, "null argument");
-    throw Error(SKM_E_COMM, "libskm was built without RCCL support");
-    SKM_API_END
-}
-
 }  // extern "C"
