@@ -51,6 +51,7 @@ constexpr int TAB_BITS = 12;
 constexpr int TAB = 1 << TAB_BITS;     // LDS hash slots per sub-bucket (load <= 0.5)
 constexpr int SUB_TARGET = 1024;       // target records per level-2 sub-bucket
 constexpr int MAX_B2 = 11;             // <= 2048 sub-buckets per level-1 bucket
+constexpr int SUB_TAB = (1 << MAX_B2) + 2;  // per-bucket sub-bucket table: count + offsets
 
 struct SeqMeta {        // 16 bytes, one dwordx4 load
     uint64_t pstart;    // first residue in the packed buffer
@@ -748,6 +749,8 @@ struct BucketArgs {
     const uint64_t* seg_start; // nsrc > 1: [nsrc][nbuckets] start of each source rank's piece in recs
     const uint32_t* seg_len;   // nsrc > 1: [nsrc][nbuckets] its length
     uint32_t nsrc;             // 1, or the world size after the all-to-all exchange
+    uint32_t* sub_tab;         // [nbuckets][SUB_TAB]: number of level-2 sub-buckets, then their offsets
+    unsigned long long* kept_ctr;  // kept k-mer counter (shared by k_bucket_process and k_overflow)
     uint32_t nbuckets;
     uint32_t bucket_base;      // global bucket id of bucket 0 (owner << b1_bits)
     int rem_bits;
@@ -1306,7 +1309,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         const uint32_t jpos = wg_exclusive_scan(jn ? 1u : 0u, L.wave, J);
         if (K == 0) continue;
         if (tid == 0) {
-            s_base[0] = atomicAdd(&A.ctr[0], (unsigned long long)K);
+            s_base[0] = atomicAdd(A.kept_ctr, (unsigned long long)K);
             if (J) s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)J);
         }
         __syncthreads();
@@ -1366,7 +1369,6 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     const uint64_t n = r1 - r0;
     if (n == 0) return;
     const uint64_t hprefix = (uint64_t)(A.bucket_base + bucket) << A.rem_bits;
-    const uint64_t rem_mask = (1ull << A.rem_bits) - 1;
 
     if (n <= (uint64_t)CAP && A.nsrc == 1) {
         L.lens32 = reinterpret_cast<uint32_t*>(A.recs_hi + r0);
@@ -1374,9 +1376,42 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
         process_sub(A.recs_hi + r0, A.recs_lo + r0, (uint32_t)n, A, hprefix, L);
         return;
     }
+    // ---- sub-buckets from the partition pass (k_partition) ----
+    const uint32_t* tab = A.sub_tab + (uint64_t)bucket * SUB_TAB;
+    const uint32_t nsub = tab[0];
+    for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_sub[d] = tab[1 + d];
     __syncthreads();
     SKM_STAMP(9);
-    // ---- level-2 partition by the next b2 bits of rem ----
+    for (uint32_t d = 0; d < nsub; ++d) {
+        const uint32_t a = s_sub[d], e = s_sub[d + 1];
+        const uint32_t cnt = e - a;
+        if (cnt == 0 || cnt > (uint32_t)CAP) continue;  // empty, or an overflow sub-bucket (k_overflow)
+        L.lens32 = reinterpret_cast<uint32_t*>(A.tmp_hi + r0 + a);
+        L.lens_sel = (LENS_IN_TMP << LENS_SEL_SHIFT) | (2 * (r0 + a));
+        process_sub(A.tmp_hi + r0 + a, A.tmp_lo + r0 + a, cnt, A, hprefix, L);
+        __syncthreads();
+        SKM_STAMP(10);
+    }
+}
+
+// Level-2 partition of every level-1 bucket that does not fit LDS (or arrives in pieces from
+// several ranks): count by the next b2 bits of rem, exclusive scan, scatter into tmp.  Writes the
+// sub-bucket table for k_bucket_process and queues sub-buckets larger than CAP for k_overflow,
+// so the overflow path (and its long P^2 chains) can run concurrently with the group-by.
+__global__ __launch_bounds__(BP_THREADS) void k_partition(BucketArgs A) {
+    __shared__ uint32_t s_sub[(1 << MAX_B2) + 1];
+    __shared__ uint32_t s_cur[1 << MAX_B2];
+    __shared__ __align__(16) uint32_t s_wave[48];
+    const uint32_t bucket = blockIdx.x;
+    if (bucket >= A.nbuckets) return;
+    const uint64_t r0 = A.bstart[bucket], r1 = A.bstart[bucket + 1];
+    const uint64_t n = r1 - r0;
+    uint32_t* tab = A.sub_tab + (uint64_t)bucket * SUB_TAB;
+    if (n == 0 || (n <= (uint64_t)CAP && A.nsrc == 1)) {  // processed in place by k_bucket_process
+        if (threadIdx.x == 0) tab[0] = 0;
+        return;
+    }
+    const uint64_t rem_mask = (1ull << A.rem_bits) - 1;
     int b2 = 0;
     while (b2 < MAX_B2 && (n >> b2) > (uint64_t)SUB_TARGET) ++b2;
     const uint32_t nsub = 1u << b2;
@@ -1403,7 +1438,6 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
         }
     }
     __syncthreads();
-    SKM_STAMP(0);
     {
         const uint32_t per = (nsub + blockDim.x - 1) / blockDim.x;
         const uint32_t d0 = threadIdx.x * per;
@@ -1420,8 +1454,9 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
         if (threadIdx.x == 0) s_sub[nsub] = tot;
         __syncthreads();
     }
-    uint32_t* s_cur = reinterpret_cast<uint32_t*>(s_hi);
     for (uint32_t d = threadIdx.x; d < nsub; d += blockDim.x) s_cur[d] = s_sub[d];
+    if (threadIdx.x == 0) tab[0] = nsub;
+    for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) tab[1 + d] = s_sub[d];
     __syncthreads();
     for (uint32_t p = 0; p < nseg; ++p) {
         uint64_t base, len;
@@ -1434,24 +1469,13 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
             A.tmp_lo[r0 + o] = l;
         }
     }
-    __threadfence_block();
-    __syncthreads();
-    SKM_STAMP(1);
-    for (uint32_t d = 0; d < nsub; ++d) {
-        const uint32_t a = s_sub[d], e = s_sub[d + 1];
-        const uint32_t cnt = e - a;
-        if (cnt == 0) continue;
-        if (cnt <= (uint32_t)CAP) {
-            L.lens32 = reinterpret_cast<uint32_t*>(A.tmp_hi + r0 + a);
-            L.lens_sel = (LENS_IN_TMP << LENS_SEL_SHIFT) | (2 * (r0 + a));
-            process_sub(A.tmp_hi + r0 + a, A.tmp_lo + r0 + a, cnt, A, hprefix, L);
-            __syncthreads();
-            SKM_STAMP(10);
-        } else if (threadIdx.x == 0) {
+    for (uint32_t d = threadIdx.x; d < nsub; d += blockDim.x) {
+        const uint32_t cnt = s_sub[d + 1] - s_sub[d];
+        if (cnt > (uint32_t)CAP) {
             const unsigned int en = atomicAdd(reinterpret_cast<unsigned int*>(&A.ctr[1]), 1u);
             if (en < A.ovf_cap) {
                 OvfEntry o;
-                o.off = r0 + a;
+                o.off = r0 + s_sub[d];
                 o.n = cnt;
                 o.bucket = bucket;
                 o.scratch = 0;
@@ -1618,7 +1642,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
         const uint32_t lpos = wg_exclusive_scan(jn, s_wave, Lt);
         if (K == 0) continue;
         if (tid == 0) {
-            s_base[0] = atomicAdd(&A.ctr[0], (unsigned long long)K);
+            s_base[0] = atomicAdd(A.kept_ctr, (unsigned long long)K);
             if (J) {
                 s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)J);
                 s_base[2] = atomicAdd(&A.ctr[4], (unsigned long long)Lt);
@@ -1724,6 +1748,10 @@ __global__ void k_count_flags(const uint8_t* __restrict__ flags, uint32_t nseq, 
 // ==========================================================================================
 using namespace skm;
 
+struct ChainSet {            // job sort scratch + sorted jobs of one chain launch
+    DevBuf hist, offs, sorted;
+};
+
 struct skm_build {
     skm_build_opts opts{};
     int device = 0;
@@ -1754,7 +1782,7 @@ struct skm_build {
     DevBuf d_hist, d_offs, d_partial, d_rbbase, d_bstart32, d_bstart, d_owner_start;
     DevBuf d_recs_hi, d_recs_lo, d_tmp_hi, d_tmp_lo;
     DevBuf d_keys, d_data, d_ctr, d_flags, d_dfunc, d_swf, d_ovf, d_ovf_hi, d_ovf_lo, d_ovf_heads, d_ovf_job, d_ovf_fm;
-    DevBuf d_jobs, d_lens, d_stamps, d_job_hist, d_job_offs, d_jobs_sorted;
+    DevBuf d_jobs, d_lens, d_stamps;
     bool stamps = false;
     uint64_t jobs_cap = 0, lens_cap = 0, n_jobs = 0, n_lens = 0;
     uint32_t n_overflow = 0;
@@ -1776,6 +1804,13 @@ struct skm_build {
     ncclComm_t comm = nullptr;
 #endif
     std::vector<skm_build*> group;
+
+    // second stream: overflow sub-buckets + their chains, concurrent with the group-by
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_part = nullptr, ev_o[3] = {};
+    DevBuf d_sub_tab, d_jobs2;
+    uint64_t jobs2_cap = 0;
+    ChainSet cs_main, cs_ovf;
 };
 
 namespace {
@@ -2212,15 +2247,37 @@ void exchange(const Ranks& bs) {
     alltoallv(bs, ex_lo);
 }
 
+// job sort by length class (longest first) + the chain kernel, on stream st
+void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, const uint32_t* lens,
+                   const uint32_t* recs32, const uint32_t* tmp32, skm_stored_kmer_data* out) {
+    if (!nj) return;
+    const uint32_t nwg = (uint32_t)std::min<uint64_t>(1024, ceil_div(nj, 4096));
+    const uint64_t chunk = ceil_div(nj, nwg);
+    cs.hist.ensure(4ull * nwg * JOB_CLASSES);
+    cs.offs.ensure(8ull * nwg * JOB_CLASSES);
+    cs.sorted.ensure(sizeof(Job) * nj);
+    hipLaunchKernelGGL(k_job_count, dim3(nwg), dim3(JOB_WG), 0, st, jobs, nj, chunk, cs.hist.as<uint32_t>());
+    hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(64), 0, st, cs.hist.as<uint32_t>(), nwg, cs.offs.as<uint64_t>());
+    hipLaunchKernelGGL(k_job_scatter, dim3(nwg), dim3(JOB_WG), 0, st, jobs, nj, chunk, cs.offs.as<uint64_t>(),
+                       cs.sorted.as<Job>());
+    const uint64_t threads = ceil_div(nj, 64) * 128;
+    hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, st, cs.sorted.as<Job>(), nj,
+                       lens, recs32, tmp32, out);
+    SKM_HIP(hipGetLastError());
+}
+
+// Group-by.  k_partition splits the oversized level-1 buckets; the overflow sub-buckets (the
+// heaviest k-mers and their long P^2 chains) then run on a second stream, concurrently with
+// k_bucket_process on the first.
 void phase_group(skm_build* b) {
-    hipStream_t st = b->stream;
+    hipStream_t st = b->stream, st2 = b->stream2;
     const uint32_t F = b->opts.n_functions;
     const bool multi = b->world > 1;
     const uint32_t NB1 = 1u << b->b1_bits;
     SKM_HIP(hipEventRecord(b->ev[4], st));
-    // ---- 4. bucket process ----
     SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 128, st));
     SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->n_total ? b->n_total : 1, st));
+    unsigned long long* ctr_d = b->d_ctr.as<unsigned long long>();
     BucketArgs A;
     A.recs_hi = multi ? b->d_rhi.as<uint64_t>() : b->d_recs_hi.as<uint64_t>();
     A.recs_lo = multi ? b->d_rlo.as<uint64_t>() : b->d_recs_lo.as<uint64_t>();
@@ -2230,12 +2287,15 @@ void phase_group(skm_build* b) {
     A.seg_start = multi ? b->d_seg_start.as<uint64_t>() : nullptr;
     A.seg_len = multi ? b->d_seg_len.as<uint32_t>() : nullptr;
     A.nsrc = multi ? (uint32_t)b->world : 1u;
+    b->d_sub_tab.ensure(4ull * NB1 * SUB_TAB);
+    A.sub_tab = b->d_sub_tab.as<uint32_t>();
+    A.kept_ctr = ctr_d;
     A.nbuckets = NB1;
     A.bucket_base = (uint32_t)b->rank << b->b1_bits;
     A.rem_bits = KEY_BITS - b->owner_bits - b->b1_bits;
     A.glen = b->d_glen.as<uint32_t>();
     A.flags = b->d_flags.as<uint8_t>();
-    A.ctr = b->d_ctr.as<unsigned long long>();
+    A.ctr = ctr_d;
     A.out_keys = b->d_keys.as<uint64_t>();
     A.out_data = b->d_data.as<skm_stored_kmer_data>();
     A.jobs = b->d_jobs.as<Job>();
@@ -2248,17 +2308,19 @@ void phase_group(skm_build* b) {
         SKM_HIP(hipMemsetAsync(b->d_stamps.p, 0, 16 * 8, st));
         A.stamps = b->d_stamps.as<unsigned long long>();
     }
-    hipLaunchKernelGGL(k_bucket_process, dim3(NB1), dim3(BP_THREADS), 0, st, A);
+    // ---- 4a. level-2 partition ----
+    hipLaunchKernelGGL(k_partition, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
-    SKM_HIP(hipEventRecord(b->ev[5], st));
-    // ---- 5. overflow ----
-    unsigned long long ctr[5];
-    SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, sizeof(ctr), hipMemcpyDeviceToHost, st));
+    unsigned long long ctr[16];
+    SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, 8 * 5, hipMemcpyDeviceToHost, st));
     if (!multi) SKM_HIP(hipMemcpyAsync(&b->n_local, b->d_bstart.as<uint64_t>() + NB1, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
     const uint32_t novf = (uint32_t)(ctr[1] & 0xFFFFFFFFull);
     SKM_CHECK(novf <= b->ovf_cap, SKM_E_OOM, "overflow list capacity exceeded");
     b->n_overflow = novf;
+    // ---- 5. overflow sub-buckets on the second stream ----
+    BucketArgs A2 = A;
+    uint64_t ovf_elems = 0;
     if (novf) {
         std::vector<OvfEntry> ov(novf);
         SKM_HIP(hipMemcpyAsync(ov.data(), b->d_ovf.p, sizeof(OvfEntry) * novf, hipMemcpyDeviceToHost, st));
@@ -2270,51 +2332,59 @@ void phase_group(skm_build* b) {
             e.npad = np;
             e.scratch = tot;
             tot += np;
+            ovf_elems += e.n;
         }
         b->d_ovf_hi.ensure(tot * 8);
         b->d_ovf_lo.ensure(tot * 8);
         b->d_ovf_heads.ensure(tot * 4);
         b->d_ovf_job.ensure(tot * 8);
         b->d_ovf_fm.ensure(tot * 4);
+        b->jobs2_cap = ovf_elems / 3 + 16;
+        b->d_jobs2.ensure(sizeof(Job) * b->jobs2_cap);
         SKM_HIP(hipMemcpyAsync(b->d_ovf.p, ov.data(), sizeof(OvfEntry) * novf, hipMemcpyHostToDevice, st));
+        SKM_HIP(hipEventRecord(b->ev_part, st));
+        SKM_HIP(hipStreamWaitEvent(st2, b->ev_part, 0));
         OvfScratch S;
         S.hi = b->d_ovf_hi.as<uint64_t>();
         S.lo = b->d_ovf_lo.as<uint64_t>();
         S.heads = b->d_ovf_heads.as<uint32_t>();
         S.jobinfo = b->d_ovf_job.as<uint64_t>();
         S.fmean = b->d_ovf_fm.as<uint32_t>();
-        hipLaunchKernelGGL(k_overflow, dim3(novf), dim3(BP_THREADS), 0, st, A, S);
+        A2.ctr = ctr_d + 8;  // own job / length counters; the kept counter stays shared
+        A2.jobs = b->d_jobs2.as<Job>();
+        A2.lens = b->d_lens.as<uint32_t>();
+        SKM_HIP(hipEventRecord(b->ev_o[0], st2));
+        hipLaunchKernelGGL(k_overflow, dim3(novf), dim3(BP_THREADS), 0, st2, A2, S);
         SKM_HIP(hipGetLastError());
+        SKM_HIP(hipEventRecord(b->ev_o[1], st2));
     }
-    SKM_HIP(hipEventRecord(b->ev[6], st));
-    // ---- 6. deferred P^2 / variance chains ----
-    SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, sizeof(ctr), hipMemcpyDeviceToHost, st));
-    SKM_HIP(hipStreamSynchronize(st));
-    b->n_kept = ctr[0];
-    b->n_jobs = ctr[3];
-    b->n_lens = ctr[4];
-    SKM_CHECK(ctr[3] <= b->jobs_cap && ctr[4] <= b->lens_cap, SKM_E_OOM, "chain buffers overflowed");
-    if (b->n_jobs) {
-        const uint64_t nj = b->n_jobs;
-        const uint32_t nwg = (uint32_t)std::min<uint64_t>(1024, ceil_div(nj, 4096));
-        const uint64_t chunk = ceil_div(nj, nwg);
-        b->d_job_hist.ensure(4ull * nwg * JOB_CLASSES);
-        b->d_job_offs.ensure(8ull * nwg * JOB_CLASSES);
-        b->d_jobs_sorted.ensure(sizeof(Job) * nj);
-        hipLaunchKernelGGL(k_job_count, dim3(nwg), dim3(JOB_WG), 0, st, b->d_jobs.as<Job>(), nj, chunk,
-                           b->d_job_hist.as<uint32_t>());
-        hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(64), 0, st, b->d_job_hist.as<uint32_t>(), nwg,
-                           b->d_job_offs.as<uint64_t>());
-        hipLaunchKernelGGL(k_job_scatter, dim3(nwg), dim3(JOB_WG), 0, st, b->d_jobs.as<Job>(), nj, chunk,
-                           b->d_job_offs.as<uint64_t>(), b->d_jobs_sorted.as<Job>());
-        const uint64_t threads = ceil_div(nj, 64) * 128;
-        hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, st,
-                           b->d_jobs_sorted.as<Job>(), nj, b->d_lens.as<uint32_t>(), A.recs_hi ? reinterpret_cast<const uint32_t*>(A.recs_hi) : nullptr,
-                           b->d_tmp_hi.as<uint32_t>(), b->d_data.as<skm_stored_kmer_data>());
-    }
+    // ---- 4b. group-by of the sub-buckets that fit LDS ----
+    hipLaunchKernelGGL(k_bucket_process, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
+    SKM_HIP(hipEventRecord(b->ev[5], st));
+    // ---- 6. deferred P^2 / variance chains: the overflow's as soon as it is done ----
+    b->n_jobs = b->n_lens = 0;
+    if (novf) {
+        SKM_HIP(hipMemcpyAsync(ctr + 8, ctr_d + 8, 8 * 5, hipMemcpyDeviceToHost, st2));
+        SKM_HIP(hipStreamSynchronize(st2));
+        SKM_CHECK(ctr[8 + 3] <= b->jobs2_cap && ctr[8 + 4] <= b->lens_cap, SKM_E_OOM, "overflow chain buffers overflowed");
+        launch_chains(st2, A2.jobs, ctr[8 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, A.out_data);
+        SKM_HIP(hipEventRecord(b->ev_o[2], st2));
+        b->n_jobs += ctr[8 + 3];
+        b->n_lens += ctr[8 + 4];
+    }
+    SKM_HIP(hipMemcpyAsync(ctr, ctr_d, 8 * 5, hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipStreamSynchronize(st));
+    SKM_CHECK(ctr[3] <= b->jobs_cap, SKM_E_OOM, "chain buffers overflowed");
+    launch_chains(st, A.jobs, ctr[3], b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
+                  reinterpret_cast<const uint32_t*>(A.tmp_hi), A.out_data);
+    b->n_jobs += ctr[3];
+    if (novf) SKM_HIP(hipStreamWaitEvent(st, b->ev_o[2], 0));
+    SKM_HIP(hipEventRecord(b->ev[6], st));
     SKM_HIP(hipEventRecord(b->ev[7], st));
     // ---- 7. per-rank statistics ----
+    SKM_HIP(hipMemcpyAsync(&b->n_kept, ctr_d, 8, hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipStreamSynchronize(st));
     SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     const size_t lds_f = F <= 16384 ? sizeof(uint32_t) * F : 0;
@@ -2336,8 +2406,11 @@ void phase_final(skm_build* b) {
     SKM_HIP(hipEventSynchronize(b->ev[8]));
     // [0] extract-count [1] scan [2] extract-scatter [3] bucket [4] overflow [5] chains
     // [6] stats (+ reductions) [7] total [8] exchange
-    const int from[7] = {0, 1, 2, 4, 5, 6, 7}, to[7] = {1, 2, 3, 5, 6, 7, 8};
+    // [4] overflow: its own kernel time on the second stream (it overlaps [3])
+    const int from[7] = {0, 1, 2, 4, 5, 5, 7}, to[7] = {1, 2, 3, 5, 6, 6, 8};
     for (int i = 0; i < 7; ++i) SKM_HIP(hipEventElapsedTime(&b->last_ms[i], b->ev[from[i]], b->ev[to[i]]));
+    b->last_ms[4] = 0.f;
+    if (b->n_overflow) SKM_HIP(hipEventElapsedTime(&b->last_ms[4], b->ev_o[0], b->ev_o[1]));
     SKM_HIP(hipEventElapsedTime(&b->last_ms[7], b->ev[0], b->ev[8]));
     SKM_HIP(hipEventElapsedTime(&b->last_ms[8], b->ev[3], b->ev[4]));
     b->ran = true;
@@ -2390,7 +2463,10 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     b->device = devices ? devices[0] : 0;
     SKM_HIP(hipSetDevice(b->device));
     SKM_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    SKM_HIP(hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking));
     for (auto& e : b->ev) SKM_HIP(hipEventCreate(&e));
+    SKM_HIP(hipEventCreateWithFlags(&b->ev_part, hipEventDisableTiming));
+    for (auto& e : b->ev_o) SKM_HIP(hipEventCreate(&e));
     set_geometry(b);
     *out = b;
     SKM_API_END
@@ -2517,7 +2593,12 @@ int skm_build_debug_jobs(skm_build* b, uint32_t* out, int cap) {
     SKM_CHECK(b && out, SKM_E_ARG, "null argument");
     const uint64_t n = std::min<uint64_t>((uint64_t)cap, b->n_jobs);
     std::vector<Job> j(n);
-    if (n) SKM_HIP(hipMemcpy(j.data(), b->d_jobs_sorted.p, sizeof(Job) * n, hipMemcpyDeviceToHost));
+    const uint64_t n2 = std::min<uint64_t>(n, b->cs_ovf.sorted.bytes / sizeof(Job));
+    if (b->n_overflow && n2) {  // the overflow's chains (the longest) first
+        SKM_HIP(hipMemcpy(j.data(), b->cs_ovf.sorted.p, sizeof(Job) * n2, hipMemcpyDeviceToHost));
+    } else if (n) {
+        SKM_HIP(hipMemcpy(j.data(), b->cs_main.sorted.p, sizeof(Job) * n, hipMemcpyDeviceToHost));
+    }
     for (uint64_t i = 0; i < (uint64_t)cap; ++i) out[i] = i < n ? j[i].n : 0u;
     SKM_API_END
 }
@@ -2717,9 +2798,14 @@ void skm_build_destroy(skm_build* b) {
 #endif
     for (auto* x : b->group)  // leave the other members usable on their own
         if (x != b) x->group.clear();
+    if (b->stream2) (void)hipStreamSynchronize(b->stream2);
     for (auto& e : b->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : b->ev_o)
+        if (e) (void)hipEventDestroy(e);
+    if (b->ev_part) (void)hipEventDestroy(b->ev_part);
     if (b->stream) (void)hipStreamDestroy(b->stream);
+    if (b->stream2) (void)hipStreamDestroy(b->stream2);
     delete b;
 }
 
