@@ -664,6 +664,219 @@ __global__ __launch_bounds__(EX_THREADS) void k_extract(ExtractArgs X) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Two-pass LDS-staged scatter of the occurrence elements (replaces a direct 4096-way scatter,
+// whose 16-byte stores from every workgroup into every bucket left partial lines in L2:
+// ~4x write amplification measured).  Pass 1 partitions by the top 6 bucket bits (64-way) as
+// the windows are extracted; pass 2 splits each of those ranges by the remaining bits.  Each
+// pass stages 4096 elements per round in LDS, sorted by destination, reserves one global range
+// per destination per round with one atomic, and writes runs of ~64 / ~32 contiguous elements.
+// Element order inside a bucket is immaterial (elements carry their ordinal).  Between the
+// passes the low 16 bits of lo hold the full bucket id instead of (len - i) mod 2^16, which
+// pass 2 restores from len mod 2^16 (hi[63:48]) and i.
+// ------------------------------------------------------------------------------------------
+constexpr int SC_ROUND = 4096;        // elements staged per round (64 KB of LDS)
+constexpr int SC_L0_BITS = 6;         // pass-1 fan-out
+constexpr int SC_POS = SC_ROUND / EX_THREADS;  // windows per thread per round (8)
+constexpr uint64_t SC_SLICE = 65536;  // pass-2 elements per workgroup
+
+struct StageLds {
+    uint64_t hi[SC_ROUND];
+    uint64_t lo[SC_ROUND];
+    uint8_t dst[SC_ROUND];
+    uint32_t cnt[128];
+    uint32_t off[129];
+    unsigned long long base[128];
+    uint32_t wave[48];
+};
+
+// counts already in L.cnt[0..nd): exclusive offsets, then one global reservation per destination
+__device__ __forceinline__ uint32_t stage_reserve(StageLds& L, uint32_t nd, unsigned long long* __restrict__ cur,
+                                                  uint32_t cur_base) {
+    const uint32_t t = threadIdx.x;
+    uint32_t tot;
+    const uint32_t c = t < nd ? L.cnt[t] : 0u;
+    const uint32_t ex = wg_exclusive_scan(c, L.wave, tot);
+    if (t < nd) {
+        L.off[t] = ex;
+        L.base[t] = c ? atomicAdd(&cur[cur_base + t], (unsigned long long)c) : 0ull;
+    }
+    if (t == 0) L.off[nd] = tot;
+    __syncthreads();
+    return tot;
+}
+
+__global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, unsigned long long* __restrict__ cur0,
+                                                                 uint64_t* __restrict__ out_hi,
+                                                                 uint64_t* __restrict__ out_lo) {
+    __shared__ StageLds L;
+    const uint8_t* __restrict__ res = X.res;
+    const int nbits = X.owner_bits + X.b1_bits;
+    const int rem_bits = KEY_BITS - nbits;
+    const uint64_t rem_mask = (1ull << rem_bits) - 1;
+    const int l0_shift = nbits - SC_L0_BITS;
+    const uint64_t begin = (uint64_t)blockIdx.x * X.span;
+    const uint64_t end = min(begin + X.span, X.rp);
+    for (uint64_t base = begin; base < end; base += SC_ROUND) {
+        if (threadIdx.x < 128) L.cnt[threadIdx.x] = 0;
+        __syncthreads();
+        const uint64_t p0 = base + (uint64_t)threadIdx.x * SC_POS;
+        const bool live = p0 < end;  // the residue buffer is padded by 64 bytes past rp, not more
+        const uint2 v0 = live ? *reinterpret_cast<const uint2*>(res + p0) : make_uint2(0u, 0u);
+        const uint2 v1 = live ? *reinterpret_cast<const uint2*>(res + p0 + 8) : make_uint2(0u, 0u);
+        const uint32_t w[4] = {v0.x, v0.y, v1.x, v1.y};
+        uint32_t code[16];
+        uint32_t valid = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t cd = residue_code((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+            valid |= (cd < 40u ? 1u : 0u) << j;
+            code[j] = cd < 40u ? cd : 0u;
+        }
+        uint64_t k = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
+        constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
+        uint32_t s = 0;
+        SeqMeta m{};
+        if (valid) {
+            s = X.blk2seq[p0 >> 6];
+            m = X.meta[s];
+        }
+        uint64_t eh[SC_POS], el[SC_POS];
+        uint32_t rk[SC_POS], l0[SC_POS];
+        uint32_t ok = 0;
+#pragma unroll
+        for (int t = 0; t < SC_POS; ++t) {
+            if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
+            const uint64_t p = p0 + t;
+            eh[t] = el[t] = 0;
+            rk[t] = l0[t] = 0;
+            if (((valid >> t) & 0xFFu) == 0xFFu && p < end) {
+                while (p > m.pstart + m.len) m = X.meta[++s];  // valid windows never span a separator
+                const uint64_t h = mix43(k);
+                const uint32_t bucket = (uint32_t)(h >> rem_bits);
+                make_elem(h & rem_mask, X.s_base + s, (uint32_t)(p - m.pstart), m, eh[t], el[t]);
+                el[t] = (el[t] & ~0xFFFFull) | bucket;  // bucket id rides in the offset field until pass 2
+                l0[t] = bucket >> l0_shift;
+                rk[t] = atomicAdd(&L.cnt[l0[t]], 1u);
+                ok |= 1u << t;
+            }
+        }
+        __syncthreads();
+        const uint32_t tot = stage_reserve(L, 1u << SC_L0_BITS, cur0, 0);
+#pragma unroll
+        for (int t = 0; t < SC_POS; ++t)
+            if ((ok >> t) & 1u) {
+                const uint32_t slot = L.off[l0[t]] + rk[t];
+                L.hi[slot] = eh[t];
+                L.lo[slot] = el[t];
+                L.dst[slot] = (uint8_t)l0[t];
+            }
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < tot; j += blockDim.x) {
+            const uint32_t d = L.dst[j];
+            const uint64_t o = L.base[d] + (j - L.off[d]);
+            out_hi[o] = L.hi[j];
+            out_lo[o] = L.lo[j];
+        }
+        __syncthreads();
+    }
+}
+
+// cur0[b0] = start of pass-1 range b0; cur1[b] = start of bucket b; slice prefix for pass 2
+__global__ void k_stage_init(const uint64_t* __restrict__ bstart, uint32_t NB, int l0_shift,
+                             unsigned long long* __restrict__ cur0, unsigned long long* __restrict__ cur1,
+                             uint32_t* __restrict__ slice_base) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < NB) cur1[t] = bstart[t];
+    if (blockIdx.x == 0) {
+        __shared__ uint32_t s_n[(1 << SC_L0_BITS) + 1];
+        const uint32_t n0 = 1u << SC_L0_BITS;
+        if (threadIdx.x < n0) {
+            const uint64_t a = bstart[(uint64_t)threadIdx.x << l0_shift];
+            const uint64_t e = bstart[(uint64_t)(threadIdx.x + 1) << l0_shift];
+            cur0[threadIdx.x] = a;
+            s_n[threadIdx.x] = (uint32_t)((e - a + SC_SLICE - 1) / SC_SLICE);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (uint32_t b = 0; b < n0; ++b) {
+                slice_base[b] = acc;
+                acc += s_n[b];
+            }
+            slice_base[n0] = acc;
+        }
+    }
+}
+
+__global__ __launch_bounds__(EX_THREADS, 2) void k_split_stage(const uint64_t* __restrict__ in_hi,
+                                                               const uint64_t* __restrict__ in_lo,
+                                                               const uint64_t* __restrict__ bstart, int nbits,
+                                                               const uint32_t* __restrict__ slice_base,
+                                                               unsigned long long* __restrict__ cur1,
+                                                               uint64_t* __restrict__ out_hi,
+                                                               uint64_t* __restrict__ out_lo) {
+    __shared__ StageLds L;
+    const uint32_t n0 = 1u << SC_L0_BITS;
+    const int sub_bits = nbits - SC_L0_BITS;
+    const uint32_t nsub = 1u << sub_bits;
+    const uint32_t w = blockIdx.x;
+    if (w >= slice_base[n0]) return;
+    uint32_t b0 = 0;
+    while (b0 + 1 < n0 && slice_base[b0 + 1] <= w) ++b0;
+    const uint64_t a0 = bstart[(uint64_t)b0 << sub_bits], e0 = bstart[(uint64_t)(b0 + 1) << sub_bits];
+    const uint64_t begin = a0 + (uint64_t)(w - slice_base[b0]) * SC_SLICE;
+    const uint64_t end = min(begin + SC_SLICE, e0);
+    for (uint64_t base = begin; base < end; base += SC_ROUND) {
+        if (threadIdx.x < 128) L.cnt[threadIdx.x] = 0;
+        __syncthreads();
+        uint64_t eh[SC_POS], el[SC_POS];
+        uint32_t rk[SC_POS], sb[SC_POS];
+#pragma unroll
+        for (int t = 0; t < SC_POS; ++t) {
+            const uint64_t j = base + threadIdx.x + (uint64_t)t * EX_THREADS;
+            rk[t] = sb[t] = 0;
+            eh[t] = el[t] = 0;
+            if (j < end) {
+                eh[t] = in_hi[j];
+                el[t] = in_lo[j];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < SC_POS; ++t) {
+            const uint64_t j = base + threadIdx.x + (uint64_t)t * EX_THREADS;
+            if (j < end) {
+                sb[t] = (uint32_t)(el[t] & 0xFFFFu) & (nsub - 1);
+                const uint32_t i = (uint32_t)(el[t] >> 16) & ((1u << ELEM_I_BITS) - 1);
+                el[t] = (el[t] & ~0xFFFFull) | (((uint32_t)(eh[t] >> 48) - i) & 0xFFFFu);  // restore (len - i) mod 2^16
+                rk[t] = atomicAdd(&L.cnt[sb[t]], 1u);
+            }
+        }
+        __syncthreads();
+        const uint32_t tot = stage_reserve(L, nsub, cur1, b0 << sub_bits);
+#pragma unroll
+        for (int t = 0; t < SC_POS; ++t) {
+            const uint64_t j = base + threadIdx.x + (uint64_t)t * EX_THREADS;
+            if (j < end) {
+                const uint32_t slot = L.off[sb[t]] + rk[t];
+                L.hi[slot] = eh[t];
+                L.lo[slot] = el[t];
+                L.dst[slot] = (uint8_t)sb[t];
+            }
+        }
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < tot; j += blockDim.x) {
+            const uint32_t d = L.dst[j];
+            const uint64_t o = L.base[d] + (j - L.off[d]);
+            out_hi[o] = L.hi[j];
+            out_lo[o] = L.lo[j];
+        }
+        __syncthreads();
+    }
+}
+
 // partial[rb][b] = sum of hist[w][b] over rows w of row-block rb
 __global__ void k_colsum(const uint32_t* __restrict__ hist, uint32_t nwg, uint32_t NB, uint32_t* __restrict__ partial) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1781,6 +1994,7 @@ struct skm_build {
     // device work
     DevBuf d_hist, d_offs, d_partial, d_rbbase, d_bstart32, d_bstart, d_owner_start;
     DevBuf d_recs_hi, d_recs_lo, d_tmp_hi, d_tmp_lo;
+    DevBuf d_cur0, d_cur1, d_slices;   // staged scatter cursors
     DevBuf d_keys, d_data, d_ctr, d_flags, d_dfunc, d_swf, d_ovf, d_ovf_hi, d_ovf_lo, d_ovf_heads, d_ovf_job, d_ovf_fm;
     DevBuf d_jobs, d_lens, d_stamps;
     bool stamps = false;
@@ -2156,8 +2370,19 @@ void phase_extract(skm_build* b) {
                        b->d_owner_start.as<uint64_t>(), NB, b->b1_bits, nowners, b->d_bstart.as<uint64_t>());
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[2], st));
-    // ---- 3. scatter ----
-    hipLaunchKernelGGL(k_extract<true>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, X);
+    // ---- 3. scatter: 64-way staged pass into tmp, then the split into the final buckets ----
+    const int l0_shift = nbits - SC_L0_BITS;
+    b->d_cur0.ensure(8 * 64);
+    b->d_cur1.ensure(8ull * NB);
+    b->d_slices.ensure(4 * 80);
+    hipLaunchKernelGGL(k_stage_init, dim3((NB + 255) / 256), dim3(256), 0, st, b->d_bstart.as<uint64_t>(), NB, l0_shift,
+                       b->d_cur0.as<unsigned long long>(), b->d_cur1.as<unsigned long long>(), b->d_slices.as<uint32_t>());
+    hipLaunchKernelGGL(k_extract_stage, dim3(b->nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
+                       b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
+    const uint32_t nsl = (uint32_t)(ceil_div(b->n_windows, SC_SLICE) + (1u << SC_L0_BITS));
+    hipLaunchKernelGGL(k_split_stage, dim3(nsl), dim3(EX_THREADS), 0, st, b->d_tmp_hi.as<uint64_t>(),
+                       b->d_tmp_lo.as<uint64_t>(), b->d_bstart.as<uint64_t>(), nbits, b->d_slices.as<uint32_t>(),
+                       b->d_cur1.as<unsigned long long>(), b->d_recs_hi.as<uint64_t>(), b->d_recs_lo.as<uint64_t>());
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[3], st));
 }
