@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -45,7 +46,7 @@ constexpr int EX_THREADS = 512;        // extract workgroup
 constexpr int EX_POS_PER_THREAD = 16;  // windows per thread per step (one 16-byte load + halo)
 constexpr int EX_MAX_WG = 512;         // rows of the histogram matrix
 constexpr int SCAN_ROWS = 32;          // rows per column-scan block
-constexpr int BP_THREADS = 512;        // bucket-process workgroup: two per CU (LDS ~79 KB each)
+constexpr int BP_THREADS = 512;        // bucket-process workgroup: two per CU (LDS ~72 KB each)
 constexpr int CAP = 2048;              // LDS sub-bucket capacity (records)
 constexpr int TAB_BITS = 12;
 constexpr int TAB = 1 << TAB_BITS;     // LDS hash slots per sub-bucket (load <= 0.5)
@@ -964,6 +965,7 @@ struct BucketArgs {
     uint32_t nsrc;             // 1, or the world size after the all-to-all exchange
     uint32_t* sub_tab;         // [nbuckets][SUB_TAB]: number of level-2 sub-buckets, then their offsets
     unsigned long long* kept_ctr;  // kept k-mer counter (shared by k_bucket_process and k_overflow)
+    int experiment;                // diagnostics only (SKM_EXPERIMENT)
     uint32_t nbuckets;
     uint32_t bucket_base;      // global bucket id of bucket 0 (owner << b1_bits)
     int rem_bits;
@@ -1366,6 +1368,138 @@ __device__ __forceinline__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_
     return r;
 }
 
+// ------------------------------------------------------------------------------------------
+// Groups of 2..64 members, packed 64/S to a wave in aligned segments of S lanes (S = 2..64, the
+// next power of two >= c), one member per lane.  Every step is a segment-local shuffle network,
+// so a wave resolves up to 32 groups at once with one code path:
+//   sort by (function, ordinal) -> function runs by ballot -> best run by segmented max (ties to
+//   the lowest FunctionIndex) -> fp32 cut -> u16 mean over the run -> upper-median offset by a
+//   second segment sort -> chain lengths of the best run in visit (reverse ordinal) order.
+// ------------------------------------------------------------------------------------------
+template <int S>
+__device__ __forceinline__ uint64_t seg_bitonic64(uint64_t key, uint32_t& pay, uint32_t m) {
+#pragma unroll
+    for (int k = 2; k <= S; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t ok = shfl_xor_u64(key, j);
+            const uint32_t op = (uint32_t)__shfl_xor((int)pay, j, 64);
+            const bool take_min = ((m & (uint32_t)j) == 0) == ((m & (uint32_t)k) == 0);
+            if (take_min ? (ok < key) : (ok > key)) {
+                key = ok;
+                pay = op;
+            }
+        }
+    }
+    return key;
+}
+
+template <int S>
+__device__ __forceinline__ uint32_t seg_bitonic32(uint32_t key, uint32_t m) {
+#pragma unroll
+    for (int k = 2; k <= S; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t ok = (uint32_t)__shfl_xor((int)key, j, 64);
+            const bool take_min = ((m & (uint32_t)j) == 0) == ((m & (uint32_t)k) == 0);
+            key = take_min ? min(key, ok) : max(key, ok);
+        }
+    }
+    return key;
+}
+
+template <int S>
+__device__ __forceinline__ uint32_t seg_reduce_max(uint32_t x) {
+#pragma unroll
+    for (int d = 1; d < S; d <<= 1) x = max(x, (uint32_t)__shfl_xor((int)x, d, 64));
+    return x;
+}
+
+template <int S>
+__device__ __forceinline__ uint32_t seg_reduce_sum(uint32_t x) {
+#pragma unroll
+    for (int d = 1; d < S; d <<= 1) x += (uint32_t)__shfl_xor((int)x, d, 64);
+    return x;
+}
+
+// One wave task: groups big[q0 .. q0 + 64/S) of the class with segment size S.
+template <int S>
+__device__ __forceinline__ void seg_groups(const SubLds& L, uint32_t q0, uint32_t qend, uint32_t G, uint32_t M,
+                                           const BucketArgs& A, uint64_t hprefix, uint32_t* jobinfo,
+                                           uint32_t* fmean) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t m = lane & (uint32_t)(S - 1);
+    const uint32_t sbase = lane - m;
+    const uint32_t q = q0 + lane / (uint32_t)S;
+    const bool gv = q < qend;
+    uint32_t rep = 0, a = 0, c = 0;
+    if (gv) {
+        const uint32_t g = L.big[q];
+        rep = L.glist[g];
+        a = L.goff[rep];
+        c = (g + 1 < G ? L.goff[L.glist[g + 1]] : M) - a;
+    }
+    const bool real = gv && m < c;
+    uint64_t key = ~0ull;
+    uint32_t pay = 0;
+    if (real) {
+        const uint32_t j = L.order[a + m];
+        const uint64_t hj = L.hi[j], lj = L.lo[j];
+        key = ((hj & 0xFFFFull) << 48) | (lj >> 16);  // function, then ordinal (s << 20 | i)
+        pay = (uint32_t)(hj >> 47);                    // len mod 2^16 << 1 | big-length flag
+    }
+    key = seg_bitonic64<S>(key, pay, m);
+    // function runs (padding lanes are heads of empty runs)
+    const uint32_t f = (uint32_t)(key >> 48);
+    const uint32_t fprev = (uint32_t)__shfl_up((int)f, 1, 64);
+    const bool head = !real || m == 0 || f != fprev;
+    const uint64_t H = __ballot(head);
+    const uint64_t above = lane == 63 ? 0ull : (H & ~((2ull << lane) - 1ull));
+    const uint32_t nh = above ? (uint32_t)__ffsll((long long)above) - 1u : 64u;
+    const uint32_t rlen = min(nh, sbase + c) - lane;
+    const uint32_t v = (real && head) ? ((rlen << 16) | (0xFFFFu - f)) : 0u;
+    const uint32_t best = seg_reduce_max<S>(v);
+    const uint32_t cbest = best >> 16, bf = 0xFFFFu - (best & 0xFFFFu);
+    const bool kept = gv && !((float)cbest < float(c) * 0.8f);
+    const bool inrun = real && f == bf;
+    const uint32_t len16 = pay >> 1;
+    const uint32_t sum = seg_reduce_sum<S>(inrun ? len16 : 0u);
+    // upper median of the offsets (len - i) mod 2^16 over all members
+    const uint32_t i = (uint32_t)(key & ((1u << ELEM_I_BITS) - 1));
+    const uint32_t off = real ? ((len16 - i) & 0xFFFFu) : 0x10000u;
+    const uint32_t osort = seg_bitonic32<S>(off, m);
+    const uint32_t avg = (uint32_t)__shfl((int)osort, (int)(sbase + (c >> 1)), 64);
+    // best run: lanes [rs, rs + cbest), ascending ordinal
+    const uint64_t R = __ballot(inrun);
+    const uint64_t segmask = (S == 64) ? ~0ull : (((1ull << S) - 1ull) << sbase);
+    const uint64_t Rs = R & segmask;
+    const uint32_t rs = Rs ? (uint32_t)__ffsll((long long)Rs) - 1u : sbase;
+    const uint32_t s = (uint32_t)(key >> ELEM_I_BITS) & ((1u << ELEM_S_BITS) - 1u);
+    const uint32_t len = (pay & 1u) ? A.glen[s] : len16;
+    if (kept && real) A.flags[s] = 1;
+    const uint32_t x0 = (uint32_t)__shfl((int)len, (int)(rs + cbest - 1), 64);  // first visited
+    const uint32_t x1 = (uint32_t)__shfl((int)len, (int)rs, 64);                // second when cbest == 2
+    if (kept && inrun && cbest >= 3) L.lens32[a + (rs + cbest - 1 - lane)] = len;  // visit order
+    if (kept && m == 0) {
+        GRes r;
+        r.kept = true;
+        r.best_f = bf;
+        r.cbest = cbest;
+        r.avg = avg;
+        r.mean = d2u16((double)(uint16_t)sum / (double)cbest);
+        stats_small(r, x0, cbest == 2 ? x1 : 0u, cbest);
+        const uint64_t h43 = hprefix | ((L.hi[rep] >> 16) & REM_MASK);
+        L.hi[rep] = kept_hi(h43, r.avg);
+        if (cbest >= 3) {
+            jobinfo[rep] = (a << 16) | JOB_KEPT | cbest;  // chain lengths at lens32[a..a+cbest)
+            fmean[rep] = bf | ((uint32_t)r.mean << 16);
+        } else {
+            jobinfo[rep] = JOB_KEPT;
+            L.lo[rep] = kept_lo(bf, r.mean, r.median, r.var);
+        }
+    }
+}
+
 // One sub-bucket of n <= CAP records: LDS hash grouping (ranks from the insert atomics give a
 // counting sort by group), singletons resolved immediately, multi-occurrence groups by threads
 // (small) or waves (large); no workgroup-wide sort.
@@ -1449,57 +1583,71 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
             L.lo[rep] = kept_lo(r.best_f, r.mean, r.median, r.var);
         }
     };
-    // 5. groups by size class so that a wave runs one code path: [2], [3,4], [5,8] by threads,
-    //    (8, CAP] by waves.  `big` holds the class-ordered group list.
+    // 5. groups by size class: classes 0..5 = segment size 2,4,..,64 (packed 64/S per wave),
+    //    class 6 = more than 64 members (one wave per group).  `big` holds the class-ordered list.
     uint32_t* ccnt = L.ccnt;
     if (tid < 8) ccnt[tid] = 0;
     __syncthreads();
+    auto cls_of = [](uint32_t c) -> uint32_t {
+        return c > 64u ? 6u : 31u - (uint32_t)__clz(c - 1u) - 0u;  // c in [2,64]: ceil(log2 c) - 1
+    };
     for (uint32_t g = tid; g < G; g += nt) {
         const uint32_t a = L.goff[L.glist[g]];
         const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
-        const uint32_t cls = c <= 2 ? 0 : c <= 4 ? 1 : c <= (uint32_t)SMALLC ? 2 : 4;
-        atomicAdd(&ccnt[cls], 1u);
+        atomicAdd(&ccnt[cls_of(c)], 1u);
     }
     __syncthreads();
+    // ccnt[0..7]: cursors, [8..15]: class starts in big[], [16..23]: first wave task of each class
+    uint32_t* cstart = ccnt + 8;
+    uint32_t* tstart = ccnt + 16;
     if (tid == 0) {
-        uint32_t run = 0;
-        for (int q = 0; q < 5; ++q) {
+        uint32_t run = 0, acc = 0;
+        for (int q = 0; q < 7; ++q) {
             const uint32_t t = ccnt[q];
             ccnt[q] = run;
+            cstart[q] = run;
+            tstart[q] = acc;
+            const uint32_t per = q < 6 ? (64u >> (q + 1)) : 1u;
+            acc += (t + per - 1) / per;
             run += t;
         }
-        *L.nbig = G - ccnt[4];  // start of the wave-level class
+        cstart[7] = run;
+        tstart[7] = acc;
     }
     __syncthreads();
     for (uint32_t g = tid; g < G; g += nt) {
         const uint32_t a = L.goff[L.glist[g]];
         const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
-        const uint32_t cls = c <= 2 ? 0 : c <= 4 ? 1 : c <= (uint32_t)SMALLC ? 2 : 4;
-        L.big[atomicAdd(&ccnt[cls], 1u)] = (uint16_t)g;
-    }
-    __syncthreads();
-    const uint32_t nsmall = G - *L.nbig;  // groups handled by threads (classes 0..3)
-    for (uint32_t q = tid; q < nsmall; q += nt) {
-        const uint32_t g = L.big[q];
-        const uint32_t rep = L.glist[g];
-        const uint32_t a = L.goff[rep];
-        const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
-        GRes r;
-        if (c <= 2)
-            r = lgroup_thread<2>(L, a, c, A.glen, A.flags);
-        else if (c <= 4)
-            r = lgroup_thread<4>(L, a, c, A.glen, A.flags);
-        else
-            r = lgroup_thread<8>(L, a, c, A.glen, A.flags);
-        stage(r, rep, a);
+        L.big[atomicAdd(&ccnt[cls_of(c)], 1u)] = (uint16_t)g;
     }
     __syncthreads();
     SKM_STAMP(6);
     {
-        const uint32_t nbig = *L.nbig;
+        // wave tasks: class k packs 64 >> (k + 1) groups per task
+        const uint32_t ntask = tstart[6];
+        const uint32_t wave = tid >> 6, nwaves = nt >> 6;
+        for (uint32_t t = wave; t < ntask; t += nwaves) {
+            uint32_t k = 0;
+            while (k < 5 && t >= tstart[k + 1]) ++k;
+            const uint32_t per = 64u >> (k + 1);
+            const uint32_t q0 = cstart[k] + (t - tstart[k]) * per, qe = cstart[k + 1];
+            switch (k) {
+                case 0: seg_groups<2>(L, q0, qe, G, M, A, hprefix, jobinfo, fmean); break;
+                case 1: seg_groups<4>(L, q0, qe, G, M, A, hprefix, jobinfo, fmean); break;
+                case 2: seg_groups<8>(L, q0, qe, G, M, A, hprefix, jobinfo, fmean); break;
+                case 3: seg_groups<16>(L, q0, qe, G, M, A, hprefix, jobinfo, fmean); break;
+                case 4: seg_groups<32>(L, q0, qe, G, M, A, hprefix, jobinfo, fmean); break;
+                default: seg_groups<64>(L, q0, qe, G, M, A, hprefix, jobinfo, fmean); break;
+            }
+        }
+    }
+    __syncthreads();
+    SKM_STAMP(11);
+    {   // groups of more than 64 members: one wave each
+        const uint32_t nbig = cstart[7] - cstart[6];
         const uint32_t wave = tid >> 6, nwaves = nt >> 6;
         for (uint32_t bi = wave; bi < nbig; bi += nwaves) {
-            const uint32_t g = L.big[nsmall + bi];
+            const uint32_t g = L.big[cstart[6] + bi];
             const uint32_t rep = L.glist[g];
             const uint32_t a = L.goff[rep];
             const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
@@ -1509,25 +1657,40 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     }
     __syncthreads();
     SKM_STAMP(7);
-    // 6. emit kept k-mers and chain jobs (one atomic each per chunk)
+    // 6. emit kept k-mers and chain jobs: one scan and one reservation per sub-bucket; each
+    //    thread owns EMIT_PER consecutive elements so its outputs are consecutive
+    constexpr uint32_t EMIT_PER = CAP / BP_THREADS;
     unsigned long long* s_base = reinterpret_cast<unsigned long long*>(L.wave + 36);
-    for (uint32_t c0 = 0; c0 < n; c0 += nt) {
-        const uint32_t j = c0 + tid;
+    const uint32_t j0 = tid * EMIT_PER;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < EMIT_PER; ++u) {
+        const uint32_t j = j0 + u;
         const uint32_t jb = j < n ? jobinfo[j] : 0u;
-        const bool kept = (jb & JOB_KEPT) != 0;
-        const uint64_t H = kept ? L.hi[j] : 0;
-        const uint32_t jn = jb & JOB_COUNT_MASK;
-        uint32_t K, J;
-        const uint32_t kpos = wg_exclusive_scan(kept ? 1u : 0u, L.wave, K);
-        const uint32_t jpos = wg_exclusive_scan(jn ? 1u : 0u, L.wave, J);
-        if (K == 0) continue;
-        if (tid == 0) {
-            s_base[0] = atomicAdd(A.kept_ctr, (unsigned long long)K);
-            if (J) s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)J);
+        cnt += ((jb & JOB_KEPT) ? 1u : 0u) | ((jb & JOB_COUNT_MASK) ? 0x10000u : 0u);
+    }
+    uint32_t tot;
+    const uint32_t pos = wg_exclusive_scan(cnt, L.wave, tot);
+    if (tid == 0 && (tot & 0xFFFFu)) {
+        if (A.experiment) {  // diagnostic: no global reservation (outputs overwrite each other)
+            s_base[0] = (uint64_t)blockIdx.x * 16;
+            s_base[1] = (uint64_t)blockIdx.x * 8;
+        } else {
+            s_base[0] = atomicAdd(A.kept_ctr, (unsigned long long)(tot & 0xFFFFu));
+            if (tot >> 16) s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)(tot >> 16));
         }
-        __syncthreads();
-        if (kept) {
-            const uint64_t o = s_base[0] + kpos;
+    }
+    __syncthreads();
+    if (tot & 0xFFFFu) {
+        uint64_t o = s_base[0] + (pos & 0xFFFFu);
+        uint64_t oj = s_base[1] + (pos >> 16);
+#pragma unroll
+        for (uint32_t u = 0; u < EMIT_PER; ++u) {
+            const uint32_t j = j0 + u;
+            const uint32_t jb = j < n ? jobinfo[j] : 0u;
+            if (!(jb & JOB_KEPT)) continue;
+            const uint64_t H = L.hi[j];
+            const uint32_t jn = jb & JOB_COUNT_MASK;
             if (jn) {
                 const uint32_t fm = fmean[j];
                 write_kept(A, o, H, kept_lo(fm & 0xFFFFu, fm >> 16, 0, 0));
@@ -1535,17 +1698,19 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
                 jbr.lens_off = L.lens_sel + (jb >> 16);
                 jbr.n = jn;
                 jbr.out_idx = (uint32_t)o;
-                A.jobs[s_base[1] + jpos] = jbr;
+                A.jobs[oj++] = jbr;
             } else {
                 write_kept(A, o, H, L.lo[j]);
             }
+            ++o;
         }
-        __syncthreads();
     }
+    __syncthreads();
     SKM_STAMP(8);
 }
 
 __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) {
+    static_assert(CAP % BP_THREADS == 0, "emit assigns CAP / BP_THREADS elements per thread");
     __shared__ uint64_t s_hi[CAP];
     __shared__ uint64_t s_lo[CAP];
     __shared__ uint32_t s_tab[TAB];
@@ -1554,12 +1719,11 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     __align__(16) __shared__ uint16_t s_goff[CAP];
     __align__(16) __shared__ uint16_t s_glist[CAP];
     __align__(16) __shared__ uint16_t s_order[CAP];
-    __shared__ uint32_t s_sub[(1 << MAX_B2) + 1];
     __align__(16) __shared__ uint16_t s_big[CAP / 2];
     __shared__ __align__(16) uint32_t s_wave[48];
     __shared__ uint32_t s_nbig;
     __shared__ uint64_t s_tlast;
-    __shared__ uint32_t s_ccnt[8];
+    __shared__ uint32_t s_ccnt[24];
     SubLds L;
     L.ccnt = s_ccnt;
     L.tlast = &s_tlast;
@@ -1592,11 +1756,9 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     // ---- sub-buckets from the partition pass (k_partition) ----
     const uint32_t* tab = A.sub_tab + (uint64_t)bucket * SUB_TAB;
     const uint32_t nsub = tab[0];
-    for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_sub[d] = tab[1 + d];
-    __syncthreads();
     SKM_STAMP(9);
     for (uint32_t d = 0; d < nsub; ++d) {
-        const uint32_t a = s_sub[d], e = s_sub[d + 1];
+        const uint32_t a = tab[1 + d], e = tab[2 + d];
         const uint32_t cnt = e - a;
         if (cnt == 0 || cnt > (uint32_t)CAP) continue;  // empty, or an overflow sub-bucket (k_overflow)
         L.lens32 = reinterpret_cast<uint32_t*>(A.tmp_hi + r0 + a);
@@ -2515,6 +2677,7 @@ void phase_group(skm_build* b) {
     b->d_sub_tab.ensure(4ull * NB1 * SUB_TAB);
     A.sub_tab = b->d_sub_tab.as<uint32_t>();
     A.kept_ctr = ctr_d;
+    A.experiment = getenv("SKM_EXPERIMENT") ? atoi(getenv("SKM_EXPERIMENT")) : 0;
     A.nbuckets = NB1;
     A.bucket_base = (uint32_t)b->rank << b->b1_bits;
     A.rem_bits = KEY_BITS - b->owner_bits - b->b1_bits;

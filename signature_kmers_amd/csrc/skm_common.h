@@ -65,16 +65,26 @@ SKM_HD uint32_t residue_code(uint32_t c) {
     return valid ? rank + ((c & 0x20u) ? 20u : 0u) : 0xFFu;
 }
 
-// code -> residue byte
+// code -> residue byte.  Arithmetic (no table in memory: on the device a string table costs a
+// dependent global byte load per digit): 5-bit offsets from 'A' of ACDEFGHIKLMNPQRSTVWY packed
+// 12 + 8 into two constants; codes 20..39 are the lower-case letters.
 SKM_HD uint8_t code_residue(uint32_t code) {
-    const char* s = "ACDEFGHIKLMNPQRSTVWYacdefghiklmnpqrstvwy";
-    return (uint8_t)s[code];
+    const uint32_t c = code >= 20u ? code - 20u : code;
+    const uint64_t w = c < 12u ? 0x6b16a41cc520c40ull : 0xc5ab39460full;
+    const uint32_t sh = 5u * (c < 12u ? c : c - 12u);
+    return (uint8_t)(65u + (uint32_t)((w >> sh) & 31u) + (code >= 20u ? 32u : 0u));
 }
 
 // base-40 code -> little-endian raw key (byte 0 = first residue, the most significant digit).
 // Split at 40^4 so the digit loop runs in 32-bit arithmetic.
 SKM_HD uint64_t decode_key(uint64_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // k < 2^43 is exact in fp64; the product can only fall short of an exact multiple of 40^4
+    uint64_t q = (uint64_t)((double)k * (1.0 / 2560000.0));
+    if (k - q * 2560000u >= 2560000u) ++q;
+#else
     const uint64_t q = k / 2560000u;                       // 40^4
+#endif
     uint32_t hi4 = (uint32_t)q, lo4 = (uint32_t)(k - q * 2560000u);
     uint64_t raw = 0;
     for (int j = 7; j >= 4; --j) {

@@ -11,7 +11,8 @@ import signature_kmers_amd as skm  # noqa: E402
 from signature_kmers_amd import synth  # noqa: E402
 
 STAMP_NAMES = {0: "l2_count", 1: "l2_scatter", 9: "l2_setup", 2: "sub_load", 3: "sub_hash", 4: "sub_classify",
-               5: "sub_scatter", 6: "sub_thread_groups", 7: "sub_wave_groups", 8: "sub_emit", 10: "sub_loop_tail"}
+               5: "sub_scatter", 6: "sub_class_sort", 11: "sub_seg_groups", 7: "sub_big_groups", 8: "sub_emit",
+               10: "sub_loop_tail"}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--seqs", type=int, default=1_000_000)
