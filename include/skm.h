@@ -123,6 +123,9 @@ int skm_build_debug_stamps(skm_build* b, int enable, uint64_t* out, int cap);
 int skm_build_debug_jobs(skm_build* b, uint32_t* out, int cap);
 /* Diagnostics: device time of the chain kernel on njobs synthetic jobs of length n. */
 int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms);
+/* Diagnostics: device exact-division helpers (reciprocal + corrected quotient used by the
+ * statistics recurrences) against IEEE division: m = 1..nm, then nm*per random pairs. */
+int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches);
 /* Run (if not yet run since the last prepare) and download the result.  With world_size > 1
  * this is collective: rank 0 receives every rank's kept k-mers (keys sorted), the other ranks
  * the k-mers they own; the statistics are global on every rank. */

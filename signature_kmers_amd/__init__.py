@@ -78,6 +78,7 @@ _SIGS = {
     "skm_comm_unique_id": (C.c_int, [_P]),
     "skm_build_set_comm": (C.c_int, [_P, _P]),
     "skm_build_group_run": (C.c_int, [C.POINTER(_P), C.c_int]),
+    "skm_debug_div_check": (C.c_int, [C.c_uint64, C.c_uint32, C.POINTER(C.c_uint64)]),
     "skm_db_open": (C.c_int, [C.POINTER(_P), C.c_char_p, C.c_char_p, C.c_int]),
     "skm_db_open_mem": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, _P, C.c_size_t, C.c_int]),
     "skm_db_size": (C.c_int, [_P, C.POINTER(C.c_uint32)]),
@@ -126,6 +127,13 @@ def debug_chain_bench(n: int, njobs: int) -> float:
     ms = C.c_float()
     _check(lib().skm_debug_chain_bench(n, njobs, C.byref(ms)))
     return ms.value
+
+
+def debug_div_check(nm: int, per: int) -> int:
+    """Mismatches of the device exact-division helpers against IEEE division."""
+    v = C.c_uint64(0)
+    _check(lib().skm_debug_div_check(nm, per, C.byref(v)))
+    return v.value
 
 
 def device_count() -> int:

@@ -23,7 +23,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -79,6 +81,29 @@ __device__ __forceinline__ uint16_t d2u16(double d) {
     return (uint16_t)(int32_t)d;
 }
 
+// ------------------------------------------------------------------------------------------
+// Exact fp64 division without the division on the dependent chain.  Every divisor in the
+// statistics recurrences is an integer m (marker position differences, sample counts), so
+//   y = RN(1/m): v_rcp_f64 + two Newton steps (error ~2^-92 relative; 1/m of an integer below
+//                2^45 is never within 2^-75 of a rounding midpoint, so the last FMA rounds to
+//                RN(1/m) exactly), computed as soon as m is known, off the height chain;
+//   RN(a/m) = fma(fma(-q, m, a), y, q) with q = RN(a*y)  (Markstein's correction theorem:
+//                y within 1/2 ulp of 1/m and q within 1 ulp of a/m give the correctly
+//                rounded quotient).
+// Bit-identical to IEEE division (checked against the CPU oracle by the parity tests and by
+// skm_debug_div_check on the device).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double rcp_int(double m) {
+    double y = __builtin_amdgcn_rcp(m);
+    y = __builtin_fma(__builtin_fma(-m, y, 1.0), y, y);
+    y = __builtin_fma(__builtin_fma(-m, y, 1.0), y, y);
+    return y;
+}
+__device__ __forceinline__ double div_by(double a, double m, double y) {
+    const double q = a * y;
+    return __builtin_fma(__builtin_fma(-q, m, a), y, q);
+}
+
 // Boost.Accumulators p_square_quantile(p=0.5) + lazy mean over a u16 sum + immediate variance.
 struct SigStats {
     double h[5];
@@ -116,23 +141,19 @@ struct SigStats {
                     }
             }
         } else {
-            // cell k with heights[k-1] <= x < heights[k] (std::upper_bound), extremes adjusted
-            int cell;
-            if (x < h[0]) {
-                h[0] = x;
-                cell = 1;
-            } else if (h[4] <= x) {
-                h[4] = x;
-                cell = 4;
-            } else {
-                cell = x < h[1] ? 1 : (x < h[2] ? 2 : (x < h[3] ? 3 : 4));
-            }
+            // cell k with heights[k-1] <= x < heights[k] (std::upper_bound), extremes adjusted.
+            // Branch-free: with sorted heights the cell is 1 + #{k in 1..3 : heights[k] <= x} in
+            // all three cases (x < h0 -> 1, h4 <= x -> 4).
+            const int cell = 1 + (h[1] <= x ? 1 : 0) + (h[2] <= x ? 1 : 0) + (h[3] <= x ? 1 : 0);
+            h[0] = x < h[0] ? x : h[0];
+            h[4] = h[4] <= x ? x : h[4];
 #pragma unroll
             for (int i = 1; i < 5; ++i)
                 if (i >= cell) act[i] += 1;
             // Desired positions accumulate exact multiples of 1/4 (desired_i = i+1 + (cnt-5)*i/4),
             // actual positions are integers: d, dp, dm and the adjust decision are exact in
-            // quarter units, so only the height update itself needs fp64 (bit-identical).
+            // quarter units, so only the height update itself needs fp64 (bit-identical).  Its
+            // three divisions by integers take the reciprocal + corrected-quotient route.
             const int32_t k4 = (int32_t)(cnt - 5);
 #pragma unroll
             for (int i = 1; i <= 3; ++i) {
@@ -140,18 +161,21 @@ struct SigStats {
                 const int32_t dpi = act[i + 1] - act[i];
                 const int32_t dmi = act[i - 1] - act[i];
                 if ((d4 >= 4 && dpi > 1) || (d4 <= -4 && dmi < -1)) {
+                    const int32_t sgi = d4 > 0 ? 1 : -1;  // d / |d|, exactly +-1
                     const double dp = (double)dpi, dm = (double)dmi;
-                    const double hp = (h[i + 1] - h[i]) / dp;
-                    const double hm = (h[i - 1] - h[i]) / dm;
-                    const short sign_d = d4 > 0 ? 1 : -1;  // d / |d|, exactly +-1
-                    const double hh = h[i] + sign_d / (dp - dm) * ((sign_d - dm) * hp + (dp - sign_d) * hm);
+                    const double ydp = rcp_int(dp), ydm = rcp_int(dm), ym = rcp_int((double)(dpi - dmi));
+                    const double hp = div_by(h[i + 1] - h[i], dp, ydp);
+                    const double hm = div_by(h[i - 1] - h[i], dm, ydm);
+                    const double sgd = (double)sgi;
+                    const double so = sgi > 0 ? ym : -ym;  // sign_d / (dp - dm)
+                    const double hh = h[i] + so * ((sgd - dm) * hp + (dp - sgd) * hm);
                     if (h[i - 1] < hh && hh < h[i + 1]) {
                         h[i] = hh;
                     } else {
-                        if (d4 > 0) h[i] += hp;
-                        if (d4 < 0) h[i] -= hm;
+                        if (sgi > 0) h[i] += hp;
+                        if (sgi < 0) h[i] -= hm;
                     }
-                    act[i] += sign_d;
+                    act[i] += sgi;
                 }
             }
         }
@@ -162,9 +186,12 @@ struct SigStats {
         sum = (uint16_t)(sum + sample);
         const double x = (double)sample;
         if (cnt > 1) {
-            double mean = (double)sum / (double)cnt;
-            double tmp = x - mean;
-            var = var * (double)(cnt - 1) / (double)cnt + tmp * tmp / (double)(cnt - 1);
+            const double c = (double)cnt, c1 = (double)(cnt - 1);
+            const double yc = rcp_int(c), yc1 = rcp_int(c1);
+            const double mean = div_by((double)sum, c, yc);
+            const double tmp = x - mean;
+            const double t2 = div_by(tmp * tmp, c1, yc1);
+            var = div_by(var * c1, c, yc) + t2;
         }
     }
 };
@@ -255,7 +282,7 @@ __device__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t& to
 // Job.lens_off selector (top 2 bits): protein lengths live in the chain-lengths buffer, or in the
 // (already consumed) record slots of the sub-bucket that produced the job, viewed as u32.
 constexpr uint64_t LENS_SEL_SHIFT = 62;
-constexpr uint64_t LENS_IN_RECS = 1, LENS_IN_TMP = 2;  // 0: chain-lengths buffer (overflow path)
+constexpr uint64_t LENS_IN_RECS = 1, LENS_IN_TMP = 2, LENS_IN_BIG = 3;  // 0: chain-lengths buffer (overflow)
 constexpr uint64_t LENS_OFF_MASK = (1ull << LENS_SEL_SHIFT) - 1;
 constexpr int SMALLC = 8;    // thread-level groups up to this size, wave-level above
 
@@ -271,14 +298,6 @@ struct GRes {
     bool kept;
 };
 
-// Sorted multi-occurrence array in LDS: key = rep<<16 | func, element index -> lo
-struct LdsView {
-    const uint32_t* mkey;
-    const uint16_t* midx;
-    const uint64_t* lo;
-    __device__ __forceinline__ uint32_t func(uint32_t j) const { return mkey[j] & 0xFFFFu; }
-    __device__ __forceinline__ uint64_t lov(uint32_t j) const { return lo[midx[j]]; }
-};
 
 // Sorted 16-byte elements in global memory (overflow path): hi = rem<<16|func
 struct GlbView {
@@ -499,7 +518,10 @@ __global__ __launch_bounds__(JOB_WG) void k_job_count(const Job* __restrict__ jo
 }
 
 // one workgroup: offs[w][c] = start of (class c, workgroup w), classes in descending order
-__global__ void k_job_scan(const uint32_t* __restrict__ hist, uint32_t nwg, uint64_t* __restrict__ offs) {
+constexpr uint32_t LONG_CLASS = 14;  // chains of >= 16384 samples get a wave pair each (k_chain_long)
+
+__global__ void k_job_scan(const uint32_t* __restrict__ hist, uint32_t nwg, uint64_t* __restrict__ offs,
+                           uint32_t long_class) {
     __shared__ uint64_t tot[JOB_CLASSES];
     const uint32_t c = threadIdx.x;
     if (c < JOB_CLASSES) {
@@ -508,6 +530,11 @@ __global__ void k_job_scan(const uint32_t* __restrict__ hist, uint32_t nwg, uint
         tot[c] = t;
     }
     __syncthreads();
+    if (c == 0) {  // jobs of the long classes lead the sorted order
+        uint64_t nl = 0;
+        for (uint32_t cc = long_class; cc < JOB_CLASSES; ++cc) nl += tot[cc];
+        offs[(uint64_t)nwg * JOB_CLASSES] = nl;
+    }
     if (c < JOB_CLASSES) {
         uint64_t base = 0;
         for (uint32_t cc = JOB_CLASSES - 1; cc > c; --cc) base += tot[cc];
@@ -530,9 +557,197 @@ __global__ __launch_bounds__(JOB_WG) void k_job_scatter(const Job* __restrict__ 
     }
 }
 
+// One chain over x[0..n): blocks of 16 samples; the next block's loads (index clamped, so no
+// per-element branch) are in flight while the current block is consumed.
+template <bool VAR>
+__device__ __forceinline__ void chain_run(SigStats& st, const uint32_t* __restrict__ x, uint32_t n) {
+    constexpr uint32_t B = 16;
+    const uint32_t last = n - 1;
+    uint32_t cur[B], nxt[B];
+#pragma unroll
+    for (uint32_t i = 0; i < B; ++i) cur[i] = x[min(i, last)];
+    for (uint32_t base = 0; base < n; base += B) {
+#pragma unroll
+        for (uint32_t i = 0; i < B; ++i) nxt[i] = x[min(base + B + i, last)];
+        const uint32_t m = min(B, n - base);
+        for (uint32_t i = 0; i < m; ++i) {
+            // rotate the block through cur[0] without dynamic register indexing
+            const uint32_t v = cur[0];
+#pragma unroll
+            for (uint32_t q = 0; q + 1 < B; ++q) cur[q] = cur[q + 1];
+            if (VAR)
+                st.add_var(v);
+            else
+                st.add_p2(v);
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < B; ++i) cur[i] = nxt[i];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Long chains: one wave pair per job (wave 0: P^2 median, wave 1: variance), 64 samples per
+// round held one per lane.
+//   P^2: the cells of all 64 samples come from three ballots of (height <= x) against the
+//   current heights; the extremes h0/h4 are lane prefix min/max (they never feed the cell).
+//   The walk over the round is scalar integer work (positions, quarter-unit decisions); only a
+//   marker adjustment runs fp64, after which the three ballots are re-taken.
+//   Variance: the sample-independent terms (u16 prefix sum, mean, (x-mean)^2/(n-1), 1/n) are
+//   computed per lane; the walk is the 5-op recurrence var = var*(n-1)/n + t.
+// Both give the bit-identical result of the one-lane recurrences in SigStats.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t incl_scan_min(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)v, d, 64);
+        if (lane >= (uint32_t)d) v = min(v, o);
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t incl_scan_max(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)v, d, 64);
+        if (lane >= (uint32_t)d) v = max(v, o);
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t incl_scan_add(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)v, d, 64);
+        if (lane >= (uint32_t)d) v += o;
+    }
+    return v;
+}
+__device__ __forceinline__ double readlane_f64(double v, uint32_t l) {
+    const uint64_t b = __double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, (int)l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), (int)l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ double chain_long_p2(const uint32_t* __restrict__ x, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63u;
+    SigStats st;
+    st.init();
+    const uint32_t n0 = min(n, 5u);
+    for (uint32_t i = 0; i < n0; ++i) st.add_p2(x[i]);  // uniform: every lane runs the same start
+    if (n <= 5) return st.h[2];
+    double h1 = st.h[1], h2 = st.h[2], h3 = st.h[3];
+    uint32_t h0i = (uint32_t)st.h[0], h4i = (uint32_t)st.h[4];  // extremes are always samples
+    int32_t a1 = st.act[1], a2 = st.act[2], a3 = st.act[3], a4 = st.act[4];
+    uint32_t cnt = 5;
+    uint32_t xn = 5 + lane < n ? x[5 + lane] : 0u;
+    for (uint32_t base = 5; base < n; base += 64) {
+        const uint32_t m = min(64u, n - base);
+        const uint32_t xl = xn;
+        const bool live = lane < m;
+        xn = base + 64 + lane < n ? x[base + 64 + lane] : 0u;  // next round in flight
+        const uint32_t imin = min(h0i, incl_scan_min(live ? xl : 0xFFFFFFFFu));
+        const uint32_t imax = max(h4i, incl_scan_max(live ? xl : 0u));
+        const double xd = (double)xl;
+        uint64_t B1 = __ballot(live && h1 <= xd), B2 = __ballot(live && h2 <= xd), B3 = __ballot(live && h3 <= xd);
+        for (uint32_t l = 0; l < m; ++l) {
+            const int32_t cell = 1 + (int32_t)((B1 >> l) & 1u) + (int32_t)((B2 >> l) & 1u) + (int32_t)((B3 >> l) & 1u);
+            a1 += cell <= 1;
+            a2 += cell <= 2;
+            a3 += cell <= 3;
+            a4 += 1;
+            ++cnt;
+            const int32_t k4 = (int32_t)(cnt - 5);
+            bool moved = false;
+            // marker i: d4 = 4*(desired - actual), exact; heights only when it adjusts
+#define SKM_P2_MARKER(I, AM, A, AP, HM, H, HP)                                                      \
+            {                                                                                      \
+                const int32_t d4 = 4 * ((I) + 1) + k4 * (I) - 4 * (A);                             \
+                const int32_t dpi = (AP) - (A), dmi = (AM) - (A);                                  \
+                if ((d4 >= 4 && dpi > 1) || (d4 <= -4 && dmi < -1)) {                             \
+                    const int32_t sgi = d4 > 0 ? 1 : -1;                                           \
+                    const double hm_ = (HM), hp_ = (HP);                                           \
+                    const double dp = (double)dpi, dm = (double)dmi;                               \
+                    const double ydp = rcp_int(dp), ydm = rcp_int(dm), ym = rcp_int((double)(dpi - dmi)); \
+                    const double hp = div_by(hp_ - (H), dp, ydp);                                  \
+                    const double hm = div_by(hm_ - (H), dm, ydm);                                  \
+                    const double sgd = (double)sgi;                                                \
+                    const double so = sgi > 0 ? ym : -ym;                                          \
+                    const double hh = (H) + so * ((sgd - dm) * hp + (dp - sgd) * hm);              \
+                    if (hm_ < hh && hh < hp_)                                                      \
+                        (H) = hh;                                                                  \
+                    else                                                                           \
+                        (H) = sgi > 0 ? (H) + hp : (H) - hm;                                       \
+                    (A) += sgi;                                                                    \
+                    moved = true;                                                                  \
+                }                                                                                  \
+            }
+            SKM_P2_MARKER(1, 1, a1, a2, (double)(uint32_t)__builtin_amdgcn_readlane((int)imin, (int)l), h1, h2)
+            SKM_P2_MARKER(2, a1, a2, a3, h1, h2, h3)
+            SKM_P2_MARKER(3, a2, a3, a4, h2, h3, (double)(uint32_t)__builtin_amdgcn_readlane((int)imax, (int)l))
+#undef SKM_P2_MARKER
+            if (moved) {
+                B1 = __ballot(live && h1 <= xd);
+                B2 = __ballot(live && h2 <= xd);
+                B3 = __ballot(live && h3 <= xd);
+            }
+        }
+        h0i = (uint32_t)__builtin_amdgcn_readlane((int)imin, (int)(m - 1));
+        h4i = (uint32_t)__builtin_amdgcn_readlane((int)imax, (int)(m - 1));
+    }
+    return h2;
+}
+
+__device__ double chain_long_var(const uint32_t* __restrict__ x, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63u;
+    double var = 0.0;
+    uint32_t sum = 0;  // running u32 sum; only its low 16 bits are the accumulator's sum
+    uint32_t xn = lane < n ? x[lane] : 0u;
+    for (uint32_t base = 0; base < n; base += 64) {
+        const uint32_t m = min(64u, n - base);
+        const uint32_t xl = xn;
+        const bool live = lane < m;
+        xn = base + 64 + lane < n ? x[base + 64 + lane] : 0u;
+        const uint32_t ps = sum + incl_scan_add(live ? xl : 0u);
+        const uint32_t c = base + lane + 1;  // count after this sample
+        double cd = (double)c, c1d = (double)(c - 1), yc = 0.0, t2 = 0.0;
+        if (live && c > 1) {
+            yc = rcp_int(cd);
+            const double mean = div_by((double)(ps & 0xFFFFu), cd, yc);
+            const double tmp = (double)xl - mean;
+            t2 = div_by(tmp * tmp, c1d, rcp_int(c1d));
+        }
+        for (uint32_t l = (base == 0 ? 1u : 0u); l < m; ++l)
+            var = div_by(var * readlane_f64(c1d, l), readlane_f64(cd, l), readlane_f64(yc, l)) + readlane_f64(t2, l);
+        sum = (uint32_t)__builtin_amdgcn_readlane((int)ps, (int)(m - 1));
+    }
+    return var;
+}
+
+__global__ __launch_bounds__(128) void k_chain_long(const Job* __restrict__ jobs, uint64_t njobs,
+                                                    const uint32_t* __restrict__ lens,
+                                                    const uint32_t* __restrict__ recs32,
+                                                    const uint32_t* __restrict__ tmp32,
+                                                    const uint32_t* __restrict__ big32,
+                                                    skm_stored_kmer_data* __restrict__ out) {
+    if (blockIdx.x >= njobs) return;
+    const Job jb = jobs[blockIdx.x];
+    const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
+    const uint32_t* x = (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
+                        (jb.lens_off & LENS_OFF_MASK);
+    if (threadIdx.x < 64) {
+        const double med = chain_long_p2(x, jb.n);
+        if (threadIdx.x == 0) out[jb.out_idx].median = d2u16(med);
+    } else {
+        const double v = chain_long_var(x, jb.n);
+        if (threadIdx.x == 64) out[jb.out_idx].var = d2u16(v);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, uint64_t njobs,
                                                 const uint32_t* __restrict__ lens, const uint32_t* __restrict__ recs32,
-                                                const uint32_t* __restrict__ tmp32,
+                                                const uint32_t* __restrict__ tmp32, const uint32_t* __restrict__ big32,
                                                 skm_stored_kmer_data* __restrict__ out) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t wave = t >> 6;
@@ -541,35 +756,42 @@ __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, ui
     if (j >= njobs) return;
     const Job jb = jobs[j];
     const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
-    const uint32_t* x = (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : lens) + (jb.lens_off & LENS_OFF_MASK);
+    const uint32_t* x = (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
+                        (jb.lens_off & LENS_OFF_MASK);
     const uint32_t n = jb.n;
     SigStats st;
     st.init();
-    constexpr uint32_t B = 16;  // samples per block; the next block is in flight meanwhile
-    uint32_t cur[B], nxt[B];
-#pragma unroll
-    for (uint32_t i = 0; i < B; ++i) cur[i] = i < n ? x[i] : 0u;
-    for (uint32_t base = 0; base < n; base += B) {
-#pragma unroll
-        for (uint32_t i = 0; i < B; ++i) nxt[i] = base + B + i < n ? x[base + B + i] : 0u;
-        const uint32_t m = min(B, n - base);
-        for (uint32_t i = 0; i < m; ++i) {
-            // rotate the block through cur[0] without dynamic register indexing
-            const uint32_t v = cur[0];
-#pragma unroll
-            for (uint32_t q = 0; q + 1 < B; ++q) cur[q] = cur[q + 1];
-            if (var_wave)
-                st.add_var(v);
-            else
-                st.add_p2(v);
-        }
-#pragma unroll
-        for (uint32_t i = 0; i < B; ++i) cur[i] = nxt[i];
-    }
+    if (var_wave)
+        chain_run<true>(st, x, n);
+    else
+        chain_run<false>(st, x, n);
     if (var_wave)
         out[jb.out_idx].var = d2u16(st.var);
     else
         out[jb.out_idx].median = d2u16(st.h[2]);
+}
+
+// Diagnostics: rcp_int / div_by against IEEE division.  Thread t checks m = t + 1 (and -m), then
+// `per` pseudo-random (a, m) pairs with m up to 2^22 and a spanning heights and differences.
+__global__ void k_div_check(uint64_t nm, uint32_t per, unsigned long long* __restrict__ bad) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nm) return;
+    uint32_t nb = 0;
+    const double m = (double)(t + 1);
+    nb += rcp_int(m) != 1.0 / m;
+    nb += rcp_int(-m) != 1.0 / -m;
+    uint64_t x = t * 0x9E3779B97F4A7C15ull + 12345;
+    for (uint32_t k = 0; k < per; ++k) {
+        x ^= x >> 12;
+        x ^= x << 25;
+        x ^= x >> 27;
+        const uint64_t r = x * 0x2545F4914F6CDD1Dull;
+        const double b = (double)(1 + (r & 0x3FFFFFu)) * ((r >> 22) & 1 ? -1.0 : 1.0);
+        const double a = ((double)(r >> 11) * (1.0 / 9007199254740992.0) - 0.5) *
+                         (double)(1ull << ((r >> 23) & 31)) + (double)((r >> 40) & 0xFFFF);
+        nb += div_by(a, b, rcp_int(b)) != a / b;
+    }
+    if (nb) atomicAdd(bad, (unsigned long long)nb);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -965,7 +1187,7 @@ struct BucketArgs {
     uint32_t nsrc;             // 1, or the world size after the all-to-all exchange
     uint32_t* sub_tab;         // [nbuckets][SUB_TAB]: number of level-2 sub-buckets, then their offsets
     unsigned long long* kept_ctr;  // kept k-mer counter (shared by k_bucket_process and k_overflow)
-    int experiment;                // diagnostics only (SKM_EXPERIMENT)
+
     uint32_t nbuckets;
     uint32_t bucket_base;      // global bucket id of bucket 0 (owner << b1_bits)
     int rem_bits;
@@ -1028,118 +1250,9 @@ __device__ __forceinline__ void write_kept(const BucketArgs& A, uint64_t o, uint
     A.out_data[o] = d;
 }
 
-template <int N>
-__device__ __forceinline__ void reg_sort_pairs(uint64_t* k, uint32_t* v) {
-#pragma unroll
-    for (int kk = 2; kk <= N; kk <<= 1)
-#pragma unroll
-        for (int j = kk >> 1; j > 0; j >>= 1)
-#pragma unroll
-            for (int i = 0; i < N; ++i) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const bool asc = (i & kk) == 0;
-                    const bool sw = asc ? (k[i] > k[l]) : (k[i] < k[l]);
-                    const uint64_t ka = k[i], kb = k[l];
-                    const uint32_t va = v[i], vb = v[l];
-                    k[i] = sw ? kb : ka;
-                    k[l] = sw ? ka : kb;
-                    v[i] = sw ? vb : va;
-                    v[l] = sw ? va : vb;
-                }
-            }
-}
 
 // Thread-level group (c <= N members at order[a..a+c)): members sorted in registers by
 // (func, ordinal); the sorted member list is written back so the best run is contiguous.
-template <int N>
-__device__ __forceinline__ GRes lgroup_thread(const SubLds& L, uint32_t a, uint32_t c, const uint32_t* __restrict__ glen,
-                              uint8_t* __restrict__ flags) {
-    GRes r;
-    r.kept = false;
-    uint64_t key[N];
-    uint32_t idx[N];
-#pragma unroll
-    for (int t = 0; t < N; ++t) {
-        if ((uint32_t)t < c) {
-            const uint32_t j = L.order[a + t];
-            key[t] = ((L.hi[j] & 0xFFFFull) << 48) | (L.lo[j] >> 16);
-            idx[t] = j;
-        } else {
-            key[t] = ~0ull;
-            idx[t] = 0xFFFFu;
-        }
-    }
-    reg_sort_pairs<N>(key, idx);
-#pragma unroll
-    for (int t = 0; t < N; ++t)
-        if ((uint32_t)t < c) L.order[a + t] = (uint16_t)idx[t];
-    uint32_t best_f = (uint32_t)(key[0] >> 48), best_c = 0, rb = 0, run_s = 0;
-#pragma unroll
-    for (int t = 1; t <= N; ++t) {
-        if ((uint32_t)t <= c) {
-            const bool end = ((uint32_t)t == c) || (key[t < N ? t : N - 1] >> 48) != (key[t - 1] >> 48);
-            if (end) {
-                const uint32_t len = t - run_s;
-                if (len > best_c) {
-                    best_c = len;
-                    best_f = (uint32_t)(key[t - 1] >> 48);
-                    rb = run_s;
-                }
-                run_s = t;
-            }
-        }
-    }
-    if ((float)best_c < float(c) * 0.8f) return r;
-    r.kept = true;
-    r.best_f = best_f;
-    r.cbest = best_c;
-    r.rb = rb;
-    uint32_t of[N];
-    uint32_t sum = 0, lr0 = 0, lr1 = 0;
-#pragma unroll
-    for (int t = 0; t < N; ++t) {
-        of[t] = 0x10000u;
-        if ((uint32_t)t < c) {
-            const uint64_t lo = L.lo[idx[t]];
-            of[t] = (uint32_t)(lo & 0xFFFFu);
-            const uint32_t s = (uint32_t)(lo >> 36);
-            flags[s] = 1;
-            if ((uint32_t)t >= rb && (uint32_t)t < rb + best_c) {
-                const uint64_t hj = L.hi[idx[t]];
-                sum += (uint32_t)(hj >> 48);  // len mod 2^16 is all the u16 sum keeps
-                const uint32_t q = rb + best_c - 1 - t;  // visit position (reverse ordinal)
-                if (q == 0) lr0 = elem_len(hj, lo, glen);
-                if (q == 1) lr1 = elem_len(hj, lo, glen);
-            }
-        }
-    }
-    reg_sort<N>(of);
-    const uint32_t k = c / 2;
-    uint32_t avg = 0;
-#pragma unroll
-    for (int t = 0; t < N; ++t)
-        if ((uint32_t)t == k) avg = of[t];
-    r.avg = avg;
-    r.mean = d2u16((double)(uint16_t)sum / (double)best_c);
-    r.median = 0;
-    r.var = 0;
-    if (best_c <= 2) {
-        stats_small(r, lr0, best_c == 2 ? lr1 : 0u, best_c);
-    } else {
-#pragma unroll
-        for (int t = 0; t < N; ++t)
-            if ((uint32_t)t >= rb && (uint32_t)t < rb + best_c)
-                L.lens32[a + (rb + best_c - 1 - t)] = elem_len(L.hi[idx[t]], L.lo[idx[t]], glen);  // visit order
-    }
-    return r;
-}
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // Wave-level group (c > SMALLC).  Best function by Boyer-Moore majority: if any function has
 // >= 80 % of the occurrences it is the strict majority, otherwise the group is cut anyway.
@@ -1149,24 +1262,6 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
            (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
 }
 
-// Ascending bitonic sort of one (key, val) per lane across the 64 lanes.
-__device__ __forceinline__ void wave_sort64(uint64_t& key, uint32_t& val) {
-    const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-    for (int kk = 2; kk <= 64; kk <<= 1) {
-#pragma unroll
-        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-            const uint64_t ok = shfl_xor_u64(key, jj);
-            const uint32_t ov = (uint32_t)__shfl_xor((int)val, jj, 64);
-            const bool take_min = ((lane & jj) == 0) == ((lane & kk) == 0);
-            const bool sw = take_min ? (ok < key) : (ok > key);
-            if (sw) {
-                key = ok;
-                val = ov;
-            }
-        }
-    }
-}
 
 __device__ __forceinline__ void bm_combine(uint32_t& cand, uint32_t& cc) {
 #pragma unroll
@@ -1184,46 +1279,18 @@ __device__ __forceinline__ void bm_combine(uint32_t& cand, uint32_t& cc) {
     cand = (uint32_t)__shfl((int)cand, 0, 64);
 }
 
-// Wave-level group with c <= 64: one member per lane, everything in registers.
-__device__ __forceinline__ GRes lgroup_wave64(const SubLds& L, uint32_t a, uint32_t c, const uint32_t* __restrict__ glen,
-                                              uint8_t* __restrict__ flags) {
-    const uint32_t lane = threadIdx.x & 63u;
-    GRes r;
-    r.kept = false;
-    const bool v = lane < c;
-    const uint32_t j = v ? L.order[a + lane] : 0u;
-    const uint64_t hj = v ? L.hi[j] : 0ull, lj = v ? L.lo[j] : 0ull;
-    const uint32_t f = v ? (uint32_t)(hj & 0xFFFFu) : 0xFFFFFFFFu;
-    uint32_t cand = f, cc = v ? 1u : 0u;
-    bm_combine(cand, cc);
-    const bool best = v && f == cand;
-    const uint32_t nb = (uint32_t)__popcll(__ballot(best));
-    if ((float)nb < float(c) * 0.8f) return r;
-    r.kept = true;
-    r.best_f = cand;
-    r.cbest = nb;
-    r.rb = 0;
-    if (v) flags[lj >> 36] = 1;
-    const uint32_t sum = wave_sum(best ? (uint32_t)(hj >> 48) : 0u);
-    r.mean = d2u16((double)(uint16_t)sum / (double)nb);
-    r.median = 0;
-    r.var = 0;
-    // avg_from_end: sort the offsets across lanes, take element c/2
-    uint64_t ok = v ? (lj & 0xFFFFull) : 0x10000ull;
-    uint32_t dummy = 0;
-    wave_sort64(ok, dummy);
-    r.avg = (uint32_t)__shfl((int)(uint32_t)ok, (int)(c / 2), 64);
-    // best-function members by ordinal
-    uint64_t key = best ? lj : ~0ull;
-    uint32_t idx = j;
-    wave_sort64(key, idx);
-    if (lane < nb) L.lens32[a + (nb - 1 - lane)] = elem_len(L.hi[idx], key, glen);  // reverse ordinal
-    return r;
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Wave-level group of 65..CAP members in LDS (order[a..a+c)).  Best function by Boyer-Moore
+// majority (a function with >= 80 % of the occurrences is the strict majority, otherwise the
+// group is cut anyway), upper-median offset by 9-way pivot selection, best-function members
+// compacted to the front and sorted by ordinal, chain lengths in visit order.
 __device__ __forceinline__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const uint32_t* __restrict__ glen,
                             uint8_t* __restrict__ flags) {
-    if (c <= 64) return lgroup_wave64(L, a, c, glen, flags);
     const uint32_t lane = threadIdx.x & 63u;
     GRes r;
     r.kept = false;
@@ -1571,18 +1638,6 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     for (uint32_t j = tid; j < n; j += nt) jobinfo[j] = L.rank[j] == 0xFFFFu ? JOB_KEPT : 0u;
     __syncthreads();
     SKM_STAMP(5);
-    auto stage = [&](const GRes& r, uint32_t rep, uint32_t a) {
-        if (!r.kept) return;
-        const uint64_t h43 = hprefix | ((L.hi[rep] >> 16) & REM_MASK);
-        L.hi[rep] = kept_hi(h43, r.avg);
-        if (r.cbest >= 3) {
-            jobinfo[rep] = (a << 16) | JOB_KEPT | r.cbest;  // chain lengths at lens32[a..a+cbest)
-            fmean[rep] = r.best_f | ((uint32_t)r.mean << 16);
-        } else {
-            jobinfo[rep] = JOB_KEPT;
-            L.lo[rep] = kept_lo(r.best_f, r.mean, r.median, r.var);
-        }
-    };
     // 5. groups by size class: classes 0..5 = segment size 2,4,..,64 (packed 64/S per wave),
     //    class 6 = more than 64 members (one wave per group).  `big` holds the class-ordered list.
     uint32_t* ccnt = L.ccnt;
@@ -1652,7 +1707,12 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
             const uint32_t a = L.goff[rep];
             const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
             const GRes r = lgroup_wave(L, a, c, A.glen, A.flags);
-            if ((tid & 63u) == 0) stage(r, rep, a);
+            if ((tid & 63u) == 0 && r.kept) {
+                const uint64_t h43 = hprefix | ((L.hi[rep] >> 16) & REM_MASK);
+                L.hi[rep] = kept_hi(h43, r.avg);
+                jobinfo[rep] = (a << 16) | JOB_KEPT | r.cbest;  // cbest > 51: always a chain job
+                fmean[rep] = r.best_f | ((uint32_t)r.mean << 16);
+            }
         }
     }
     __syncthreads();
@@ -1672,13 +1732,8 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     uint32_t tot;
     const uint32_t pos = wg_exclusive_scan(cnt, L.wave, tot);
     if (tid == 0 && (tot & 0xFFFFu)) {
-        if (A.experiment) {  // diagnostic: no global reservation (outputs overwrite each other)
-            s_base[0] = (uint64_t)blockIdx.x * 16;
-            s_base[1] = (uint64_t)blockIdx.x * 8;
-        } else {
-            s_base[0] = atomicAdd(A.kept_ctr, (unsigned long long)(tot & 0xFFFFu));
-            if (tot >> 16) s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)(tot >> 16));
-        }
+        s_base[0] = atomicAdd(A.kept_ctr, (unsigned long long)(tot & 0xFFFFu));
+        if (tot >> 16) s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)(tot >> 16));
     }
     __syncthreads();
     if (tot & 0xFFFFu) {
@@ -1714,6 +1769,7 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     __shared__ uint64_t s_hi[CAP];
     __shared__ uint64_t s_lo[CAP];
     __shared__ uint32_t s_tab[TAB];
+    __shared__ uint32_t s_sub[(1 << MAX_B2) + 1];
     __align__(16) __shared__ uint16_t s_slot[CAP];
     __align__(16) __shared__ uint16_t s_rank[CAP];
     __align__(16) __shared__ uint16_t s_goff[CAP];
@@ -1756,9 +1812,11 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     // ---- sub-buckets from the partition pass (k_partition) ----
     const uint32_t* tab = A.sub_tab + (uint64_t)bucket * SUB_TAB;
     const uint32_t nsub = tab[0];
+    for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_sub[d] = tab[1 + d];
+    __syncthreads();
     SKM_STAMP(9);
     for (uint32_t d = 0; d < nsub; ++d) {
-        const uint32_t a = tab[1 + d], e = tab[2 + d];
+        const uint32_t a = s_sub[d], e = s_sub[d + 1];
         const uint32_t cnt = e - a;
         if (cnt == 0 || cnt > (uint32_t)CAP) continue;  // empty, or an overflow sub-bucket (k_overflow)
         L.lens32 = reinterpret_cast<uint32_t*>(A.tmp_hi + r0 + a);
@@ -2185,6 +2243,7 @@ struct skm_build {
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_part = nullptr, ev_o[3] = {};
     DevBuf d_sub_tab, d_jobs2;
+
     uint64_t jobs2_cap = 0;
     ChainSet cs_main, cs_ovf;
 };
@@ -2408,6 +2467,7 @@ void ensure_local(skm_build* b, uint64_t n) {
     }
     b->d_tmp_hi.ensure(8 * c);
     b->d_tmp_lo.ensure(8 * c);
+
     b->d_keys.ensure(8 * c);
     b->d_data.ensure(sizeof(skm_stored_kmer_data) * c + 16);
     const uint32_t NB1 = 1u << b->b1_bits;
@@ -2636,20 +2696,29 @@ void exchange(const Ranks& bs) {
 
 // job sort by length class (longest first) + the chain kernel, on stream st
 void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, const uint32_t* lens,
-                   const uint32_t* recs32, const uint32_t* tmp32, skm_stored_kmer_data* out) {
+                   const uint32_t* recs32, const uint32_t* tmp32, const uint32_t* big32, skm_stored_kmer_data* out,
+                   uint32_t long_class) {
     if (!nj) return;
     const uint32_t nwg = (uint32_t)std::min<uint64_t>(1024, ceil_div(nj, 4096));
     const uint64_t chunk = ceil_div(nj, nwg);
     cs.hist.ensure(4ull * nwg * JOB_CLASSES);
-    cs.offs.ensure(8ull * nwg * JOB_CLASSES);
+    cs.offs.ensure(8ull * nwg * JOB_CLASSES + 8);
     cs.sorted.ensure(sizeof(Job) * nj);
     hipLaunchKernelGGL(k_job_count, dim3(nwg), dim3(JOB_WG), 0, st, jobs, nj, chunk, cs.hist.as<uint32_t>());
-    hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(64), 0, st, cs.hist.as<uint32_t>(), nwg, cs.offs.as<uint64_t>());
+    hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(64), 0, st, cs.hist.as<uint32_t>(), nwg, cs.offs.as<uint64_t>(), long_class);
     hipLaunchKernelGGL(k_job_scatter, dim3(nwg), dim3(JOB_WG), 0, st, jobs, nj, chunk, cs.offs.as<uint64_t>(),
                        cs.sorted.as<Job>());
-    const uint64_t threads = ceil_div(nj, 64) * 128;
-    hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, st, cs.sorted.as<Job>(), nj,
-                       lens, recs32, tmp32, out);
+    uint64_t nlong = 0;
+    SKM_HIP(hipMemcpyAsync(&nlong, cs.offs.as<uint64_t>() + (uint64_t)nwg * JOB_CLASSES, 8, hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipStreamSynchronize(st));
+    if (nlong)
+        hipLaunchKernelGGL(k_chain_long, dim3((uint32_t)nlong), dim3(128), 0, st, cs.sorted.as<Job>(), nlong, lens, recs32,
+                           tmp32, big32, out);
+    if (nj > nlong) {
+        const uint64_t threads = ceil_div(nj - nlong, 64) * 128;
+        hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, st,
+                           cs.sorted.as<Job>() + nlong, nj - nlong, lens, recs32, tmp32, big32, out);
+    }
     SKM_HIP(hipGetLastError());
 }
 
@@ -2657,6 +2726,12 @@ void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, c
 // heaviest k-mers and their long P^2 chains) then run on a second stream, concurrently with
 // k_bucket_process on the first.
 void phase_group(skm_build* b) {
+    // host-side timeline (SKM_HOST_TIMING=1): where the host waits between launches
+    static const bool host_timing = getenv("SKM_HOST_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    double tm[8] = {0};
+#define T(i) \
+    if (host_timing) tm[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count()
     hipStream_t st = b->stream, st2 = b->stream2;
     const uint32_t F = b->opts.n_functions;
     const bool multi = b->world > 1;
@@ -2677,7 +2752,7 @@ void phase_group(skm_build* b) {
     b->d_sub_tab.ensure(4ull * NB1 * SUB_TAB);
     A.sub_tab = b->d_sub_tab.as<uint32_t>();
     A.kept_ctr = ctr_d;
-    A.experiment = getenv("SKM_EXPERIMENT") ? atoi(getenv("SKM_EXPERIMENT")) : 0;
+
     A.nbuckets = NB1;
     A.bucket_base = (uint32_t)b->rank << b->b1_bits;
     A.rem_bits = KEY_BITS - b->owner_bits - b->b1_bits;
@@ -2696,6 +2771,7 @@ void phase_group(skm_build* b) {
         SKM_HIP(hipMemsetAsync(b->d_stamps.p, 0, 16 * 8, st));
         A.stamps = b->d_stamps.as<unsigned long long>();
     }
+    T(0);
     // ---- 4a. level-2 partition ----
     hipLaunchKernelGGL(k_partition, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
@@ -2703,6 +2779,7 @@ void phase_group(skm_build* b) {
     SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, 8 * 5, hipMemcpyDeviceToHost, st));
     if (!multi) SKM_HIP(hipMemcpyAsync(&b->n_local, b->d_bstart.as<uint64_t>() + NB1, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
+    T(1);
     const uint32_t novf = (uint32_t)(ctr[1] & 0xFFFFFFFFull);
     SKM_CHECK(novf <= b->ovf_cap, SKM_E_OOM, "overflow list capacity exceeded");
     b->n_overflow = novf;
@@ -2746,30 +2823,34 @@ void phase_group(skm_build* b) {
         SKM_HIP(hipGetLastError());
         SKM_HIP(hipEventRecord(b->ev_o[1], st2));
     }
+    T(2);
     // ---- 4b. group-by of the sub-buckets that fit LDS ----
     hipLaunchKernelGGL(k_bucket_process, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[5], st));
+    T(3);
     // ---- 6. deferred P^2 / variance chains: the overflow's as soon as it is done ----
     b->n_jobs = b->n_lens = 0;
     if (novf) {
         SKM_HIP(hipMemcpyAsync(ctr + 8, ctr_d + 8, 8 * 5, hipMemcpyDeviceToHost, st2));
         SKM_HIP(hipStreamSynchronize(st2));
         SKM_CHECK(ctr[8 + 3] <= b->jobs2_cap && ctr[8 + 4] <= b->lens_cap, SKM_E_OOM, "overflow chain buffers overflowed");
-        launch_chains(st2, A2.jobs, ctr[8 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, A.out_data);
+        launch_chains(st2, A2.jobs, ctr[8 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, nullptr, A.out_data, LONG_CLASS);
         SKM_HIP(hipEventRecord(b->ev_o[2], st2));
         b->n_jobs += ctr[8 + 3];
         b->n_lens += ctr[8 + 4];
     }
+    T(4);
     SKM_HIP(hipMemcpyAsync(ctr, ctr_d, 8 * 5, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
     SKM_CHECK(ctr[3] <= b->jobs_cap, SKM_E_OOM, "chain buffers overflowed");
     launch_chains(st, A.jobs, ctr[3], b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
-                  reinterpret_cast<const uint32_t*>(A.tmp_hi), A.out_data);
+                  reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, LONG_CLASS);
     b->n_jobs += ctr[3];
     if (novf) SKM_HIP(hipStreamWaitEvent(st, b->ev_o[2], 0));
     SKM_HIP(hipEventRecord(b->ev[6], st));
     SKM_HIP(hipEventRecord(b->ev[7], st));
+    T(5);
     // ---- 7. per-rank statistics ----
     SKM_HIP(hipMemcpyAsync(&b->n_kept, ctr_d, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
@@ -2783,6 +2864,11 @@ void phase_group(skm_build* b) {
         hipLaunchKernelGGL(k_func_hist_seqs, dim3(256), dim3(256), lds_f, st, b->d_meta.as<SeqMeta>(), b->nseq, F,
                            b->d_swf.as<uint32_t>());
     SKM_HIP(hipGetLastError());
+    T(6);
+    if (host_timing)
+        fprintf(stderr, "host ms: part %.3f ovf-read %.3f launches %.3f ovf-chains %.3f main-chains %.3f stats %.3f end %.3f\n",
+                tm[0], tm[1], tm[2], tm[3], tm[4], tm[5], tm[6]);
+#undef T
 }
 
 void phase_final(skm_build* b) {
@@ -3015,8 +3101,13 @@ int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms) {
     const uint64_t threads = ceil_div(njobs, 64) * 128;
     for (int it = 0; it < 2; ++it) {
         SKM_HIP(hipEventRecord(e0, 0));
+        if (n >= (1u << LONG_CLASS))
+            hipLaunchKernelGGL(k_chain_long, dim3(njobs), dim3(128), 0, 0, dj.as<Job>(), (uint64_t)njobs,
+                               dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(),
+                               dout.as<skm_stored_kmer_data>());
+        else
         hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, 0, dj.as<Job>(),
-                           (uint64_t)njobs, dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(),
+                           (uint64_t)njobs, dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(),
                            dout.as<skm_stored_kmer_data>());
         SKM_HIP(hipEventRecord(e1, 0));
         SKM_HIP(hipEventSynchronize(e1));
@@ -3024,6 +3115,20 @@ int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms) {
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    SKM_API_END
+}
+
+// Diagnostics: device reciprocal / corrected-quotient check against IEEE division.
+int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
+    SKM_API_BEGIN
+    SKM_CHECK(mismatches && nm, SKM_E_ARG, "bad argument");
+    DevBuf d;
+    d.ensure(8);
+    SKM_HIP(hipMemset(d.p, 0, 8));
+    hipLaunchKernelGGL(k_div_check, dim3((uint32_t)ceil_div(nm, 256)), dim3(256), 0, 0, nm, per,
+                       d.as<unsigned long long>());
+    SKM_HIP(hipGetLastError());
+    SKM_HIP(hipMemcpy(mismatches, d.p, 8, hipMemcpyDeviceToHost));
     SKM_API_END
 }
 

@@ -156,3 +156,8 @@ def test_rerun_is_idempotent(skm, gpu):
     c = b.finish()
     np.testing.assert_array_equal(a.keys, c.keys)
     np.testing.assert_array_equal(a.data, c.data)
+
+
+def test_device_exact_division(skm, gpu):
+    # reciprocal of every integer up to 2^22 (both signs) and 2^22 * 64 random quotients
+    assert skm.debug_div_check(1 << 22, 64) == 0
