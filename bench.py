@@ -69,7 +69,8 @@ def main():
     gen_s = time.time() - t0
     n_windows = int(np.where((f != 0xFFFF) & (l >= 8), l.astype(np.int64) - 7, 0).sum())
 
-    b = skm.SignatureBuilder(len(funcs), device=local, rank=rank, world_size=world)
+    ndev = max(1, skm.device_count())
+    b = skm.SignatureBuilder(len(funcs), device=local % ndev, rank=rank, world_size=world)
     b.add_batch(r, o, l, f, i)
     if uid is not None:
         b.set_comm(uid)  # RCCL communicator over the world (data-path exchange)

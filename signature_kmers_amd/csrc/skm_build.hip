@@ -1815,15 +1815,24 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_sub[d] = tab[1 + d];
     __syncthreads();
     SKM_STAMP(9);
-    for (uint32_t d = 0; d < nsub; ++d) {
-        const uint32_t a = s_sub[d], e = s_sub[d + 1];
-        const uint32_t cnt = e - a;
-        if (cnt == 0 || cnt > (uint32_t)CAP) continue;  // empty, or an overflow sub-bucket (k_overflow)
+    // consecutive sub-buckets are contiguous in tmp and hold disjoint keys: batch as many as fit
+    // in LDS into one pass, so the per-pass fixed costs (load latency, barriers, reservations)
+    // are paid once per ~CAP elements
+    for (uint32_t d = 0; d < nsub;) {
+        const uint32_t a = s_sub[d];
+        if (s_sub[d + 1] - a == 0 || s_sub[d + 1] - a > (uint32_t)CAP) {  // empty, or k_overflow's
+            ++d;
+            continue;
+        }
+        uint32_t d2 = d + 1;
+        while (d2 < nsub && s_sub[d2 + 1] - a <= (uint32_t)CAP) ++d2;
+        const uint32_t cnt = s_sub[d2] - a;
         L.lens32 = reinterpret_cast<uint32_t*>(A.tmp_hi + r0 + a);
         L.lens_sel = (LENS_IN_TMP << LENS_SEL_SHIFT) | (2 * (r0 + a));
         process_sub(A.tmp_hi + r0 + a, A.tmp_lo + r0 + a, cnt, A, hprefix, L);
         __syncthreads();
         SKM_STAMP(10);
+        d = d2;
     }
 }
 
@@ -2243,6 +2252,24 @@ struct skm_build {
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_part = nullptr, ev_o[3] = {};
     DevBuf d_sub_tab, d_jobs2;
+
+    // pinned host staging for the pipeline's small readbacks
+    unsigned long long* h_pin = nullptr;   // [32] counters
+    OvfEntry* h_ovf = nullptr;
+    size_t h_ovf_cap = 0;
+    unsigned long long* pinned_ctr() {
+        if (!h_pin) SKM_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_pin), 32 * 8, hipHostMallocDefault));
+        return h_pin;
+    }
+    OvfEntry* pinned_ovf(size_t n) {
+        if (n > h_ovf_cap) {
+            if (h_ovf) SKM_HIP(hipHostFree(h_ovf));
+            h_ovf = nullptr;
+            h_ovf_cap = std::max<size_t>(n, 1024);
+            SKM_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_ovf), sizeof(OvfEntry) * h_ovf_cap, hipHostMallocDefault));
+        }
+        return h_ovf;
+    }
 
     uint64_t jobs2_cap = 0;
     ChainSet cs_main, cs_ovf;
@@ -2697,7 +2724,7 @@ void exchange(const Ranks& bs) {
 // job sort by length class (longest first) + the chain kernel, on stream st
 void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, const uint32_t* lens,
                    const uint32_t* recs32, const uint32_t* tmp32, const uint32_t* big32, skm_stored_kmer_data* out,
-                   uint32_t long_class) {
+                   uint32_t long_class, unsigned long long* pin) {
     if (!nj) return;
     const uint32_t nwg = (uint32_t)std::min<uint64_t>(1024, ceil_div(nj, 4096));
     const uint64_t chunk = ceil_div(nj, nwg);
@@ -2708,9 +2735,9 @@ void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, c
     hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(64), 0, st, cs.hist.as<uint32_t>(), nwg, cs.offs.as<uint64_t>(), long_class);
     hipLaunchKernelGGL(k_job_scatter, dim3(nwg), dim3(JOB_WG), 0, st, jobs, nj, chunk, cs.offs.as<uint64_t>(),
                        cs.sorted.as<Job>());
-    uint64_t nlong = 0;
-    SKM_HIP(hipMemcpyAsync(&nlong, cs.offs.as<uint64_t>() + (uint64_t)nwg * JOB_CLASSES, 8, hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipMemcpyAsync(pin, cs.offs.as<uint64_t>() + (uint64_t)nwg * JOB_CLASSES, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
+    const uint64_t nlong = *pin;
     if (nlong)
         hipLaunchKernelGGL(k_chain_long, dim3((uint32_t)nlong), dim3(128), 0, st, cs.sorted.as<Job>(), nlong, lens, recs32,
                            tmp32, big32, out);
@@ -2775,11 +2802,13 @@ void phase_group(skm_build* b) {
     // ---- 4a. level-2 partition ----
     hipLaunchKernelGGL(k_partition, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
-    unsigned long long ctr[16];
+    // readbacks go through pinned host memory (no staging copies, no pageable-copy stalls)
+    unsigned long long* ctr = b->pinned_ctr();
     SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, 8 * 5, hipMemcpyDeviceToHost, st));
-    if (!multi) SKM_HIP(hipMemcpyAsync(&b->n_local, b->d_bstart.as<uint64_t>() + NB1, 8, hipMemcpyDeviceToHost, st));
+    if (!multi) SKM_HIP(hipMemcpyAsync(ctr + 16, b->d_bstart.as<uint64_t>() + NB1, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
     T(1);
+    if (!multi) b->n_local = ctr[16];
     const uint32_t novf = (uint32_t)(ctr[1] & 0xFFFFFFFFull);
     SKM_CHECK(novf <= b->ovf_cap, SKM_E_OOM, "overflow list capacity exceeded");
     b->n_overflow = novf;
@@ -2787,11 +2816,12 @@ void phase_group(skm_build* b) {
     BucketArgs A2 = A;
     uint64_t ovf_elems = 0;
     if (novf) {
-        std::vector<OvfEntry> ov(novf);
-        SKM_HIP(hipMemcpyAsync(ov.data(), b->d_ovf.p, sizeof(OvfEntry) * novf, hipMemcpyDeviceToHost, st));
+        OvfEntry* ov = b->pinned_ovf(novf);
+        SKM_HIP(hipMemcpyAsync(ov, b->d_ovf.p, sizeof(OvfEntry) * novf, hipMemcpyDeviceToHost, st));
         SKM_HIP(hipStreamSynchronize(st));
         uint64_t tot = 0;
-        for (auto& e : ov) {
+        for (uint32_t q = 0; q < novf; ++q) {
+            OvfEntry& e = ov[q];
             uint32_t np = 1;
             while (np < e.n) np <<= 1;
             e.npad = np;
@@ -2806,7 +2836,7 @@ void phase_group(skm_build* b) {
         b->d_ovf_fm.ensure(tot * 4);
         b->jobs2_cap = ovf_elems / 3 + 16;
         b->d_jobs2.ensure(sizeof(Job) * b->jobs2_cap);
-        SKM_HIP(hipMemcpyAsync(b->d_ovf.p, ov.data(), sizeof(OvfEntry) * novf, hipMemcpyHostToDevice, st));
+        SKM_HIP(hipMemcpyAsync(b->d_ovf.p, ov, sizeof(OvfEntry) * novf, hipMemcpyHostToDevice, st));
         SKM_HIP(hipEventRecord(b->ev_part, st));
         SKM_HIP(hipStreamWaitEvent(st2, b->ev_part, 0));
         OvfScratch S;
@@ -2835,7 +2865,9 @@ void phase_group(skm_build* b) {
         SKM_HIP(hipMemcpyAsync(ctr + 8, ctr_d + 8, 8 * 5, hipMemcpyDeviceToHost, st2));
         SKM_HIP(hipStreamSynchronize(st2));
         SKM_CHECK(ctr[8 + 3] <= b->jobs2_cap && ctr[8 + 4] <= b->lens_cap, SKM_E_OOM, "overflow chain buffers overflowed");
-        launch_chains(st2, A2.jobs, ctr[8 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, nullptr, A.out_data, LONG_CLASS);
+        // the overflow's chains are the longest: wave pairs from 8192 samples up
+        launch_chains(st2, A2.jobs, ctr[8 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, nullptr, A.out_data, 13,
+                      ctr + 21);
         SKM_HIP(hipEventRecord(b->ev_o[2], st2));
         b->n_jobs += ctr[8 + 3];
         b->n_lens += ctr[8 + 4];
@@ -2845,15 +2877,16 @@ void phase_group(skm_build* b) {
     SKM_HIP(hipStreamSynchronize(st));
     SKM_CHECK(ctr[3] <= b->jobs_cap, SKM_E_OOM, "chain buffers overflowed");
     launch_chains(st, A.jobs, ctr[3], b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
-                  reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, LONG_CLASS);
+                  reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, LONG_CLASS, ctr + 20);
     b->n_jobs += ctr[3];
     if (novf) SKM_HIP(hipStreamWaitEvent(st, b->ev_o[2], 0));
     SKM_HIP(hipEventRecord(b->ev[6], st));
     SKM_HIP(hipEventRecord(b->ev[7], st));
     T(5);
     // ---- 7. per-rank statistics ----
-    SKM_HIP(hipMemcpyAsync(&b->n_kept, ctr_d, 8, hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipMemcpyAsync(ctr + 17, ctr_d, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
+    b->n_kept = ctr[17];
     SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     const size_t lds_f = F <= 16384 ? sizeof(uint32_t) * F : 0;
@@ -3297,6 +3330,8 @@ void skm_build_destroy(skm_build* b) {
     for (auto& e : b->ev_o)
         if (e) (void)hipEventDestroy(e);
     if (b->ev_part) (void)hipEventDestroy(b->ev_part);
+    if (b->h_pin) (void)hipHostFree(b->h_pin);
+    if (b->h_ovf) (void)hipHostFree(b->h_ovf);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     if (b->stream2) (void)hipStreamDestroy(b->stream2);
     delete b;
