@@ -730,8 +730,11 @@ __global__ __launch_bounds__(128) void k_chain_long(const Job* __restrict__ jobs
                                                     const uint32_t* __restrict__ recs32,
                                                     const uint32_t* __restrict__ tmp32,
                                                     const uint32_t* __restrict__ big32,
-                                                    skm_stored_kmer_data* __restrict__ out) {
+                                                    skm_stored_kmer_data* __restrict__ out, int prio) {
     if (blockIdx.x >= njobs) return;
+    if (prio == 1) __builtin_amdgcn_s_setprio(1);
+    if (prio == 2) __builtin_amdgcn_s_setprio(2);
+    if (prio >= 3) __builtin_amdgcn_s_setprio(3);
     const Job jb = jobs[blockIdx.x];
     const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
     const uint32_t* x = (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
@@ -1840,9 +1843,16 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
 // several ranks): count by the next b2 bits of rem, exclusive scan, scatter into tmp.  Writes the
 // sub-bucket table for k_bucket_process and queues sub-buckets larger than CAP for k_overflow,
 // so the overflow path (and its long P^2 chains) can run concurrently with the group-by.
-__global__ __launch_bounds__(BP_THREADS) void k_partition(BucketArgs A) {
+constexpr uint32_t PT_ROUND = 2048;  // elements staged per round of the level-2 scatter
+
+__global__ __launch_bounds__(BP_THREADS, 2) void k_partition(BucketArgs A) {
     __shared__ uint32_t s_sub[(1 << MAX_B2) + 1];
     __shared__ uint32_t s_cur[1 << MAX_B2];
+    __shared__ uint32_t s_rc[1 << MAX_B2];          // this round's count per sub-bucket
+    __shared__ uint32_t s_ro[(1 << MAX_B2) + 1];    // ... and its staging offset
+    __shared__ uint64_t s_sh[PT_ROUND];
+    __shared__ uint64_t s_sl[PT_ROUND];
+    __shared__ uint16_t s_sd[PT_ROUND];
     __shared__ __align__(16) uint32_t s_wave[48];
     const uint32_t bucket = blockIdx.x;
     if (bucket >= A.nbuckets) return;
@@ -1900,15 +1910,68 @@ __global__ __launch_bounds__(BP_THREADS) void k_partition(BucketArgs A) {
     if (threadIdx.x == 0) tab[0] = nsub;
     for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) tab[1 + d] = s_sub[d];
     __syncthreads();
+    // staged scatter: each round sorts PT_ROUND elements by sub-bucket in LDS, then writes each
+    // sub-bucket's run contiguously (whole lines instead of scattered 8-byte stores)
+    constexpr uint32_t PER = PT_ROUND / BP_THREADS;
     for (uint32_t p = 0; p < nseg; ++p) {
         uint64_t base, len;
         seg(p, base, len);
-        for (uint64_t j = threadIdx.x; j < len; j += blockDim.x) {
-            const uint64_t h = A.recs_hi[base + j];
-            const uint64_t l = A.recs_lo[base + j];
-            const uint32_t o = atomicAdd(&s_cur[(uint32_t)(((h >> 16) & rem_mask) >> shift)], 1u);
-            A.tmp_hi[r0 + o] = h;
-            A.tmp_lo[r0 + o] = l;
+        for (uint64_t rb = 0; rb < len; rb += PT_ROUND) {
+            for (uint32_t d = threadIdx.x; d < nsub; d += blockDim.x) s_rc[d] = 0;
+            __syncthreads();
+            uint64_t eh[PER], el[PER];
+            uint32_t sb[PER], rk[PER];
+#pragma unroll
+            for (uint32_t u = 0; u < PER; ++u) {
+                const uint64_t j = rb + threadIdx.x + (uint64_t)u * BP_THREADS;
+                sb[u] = 0xFFFFFFFFu;
+                if (j < len) {
+                    eh[u] = A.recs_hi[base + j];
+                    el[u] = A.recs_lo[base + j];
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < PER; ++u) {
+                const uint64_t j = rb + threadIdx.x + (uint64_t)u * BP_THREADS;
+                if (j < len) {
+                    sb[u] = (uint32_t)(((eh[u] >> 16) & rem_mask) >> shift);
+                    rk[u] = atomicAdd(&s_rc[sb[u]], 1u);
+                }
+            }
+            __syncthreads();
+            {   // exclusive scan of the round counts over the sub-buckets
+                const uint32_t per = (nsub + blockDim.x - 1) / blockDim.x;
+                const uint32_t d0 = threadIdx.x * per;
+                uint32_t local = 0;
+                for (uint32_t d = d0; d < min(nsub, d0 + per); ++d) local += s_rc[d];
+                uint32_t tot;
+                uint32_t run = wg_exclusive_scan(local, s_wave, tot);
+                for (uint32_t d = d0; d < min(nsub, d0 + per); ++d) {
+                    s_ro[d] = run;
+                    run += s_rc[d];
+                }
+                if (threadIdx.x == 0) s_ro[nsub] = tot;
+                __syncthreads();
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < PER; ++u)
+                if (sb[u] != 0xFFFFFFFFu) {
+                    const uint32_t slot = s_ro[sb[u]] + rk[u];
+                    s_sh[slot] = eh[u];
+                    s_sl[slot] = el[u];
+                    s_sd[slot] = (uint16_t)sb[u];
+                }
+            __syncthreads();
+            const uint32_t tot = s_ro[nsub];
+            for (uint32_t k = threadIdx.x; k < tot; k += blockDim.x) {
+                const uint32_t d = s_sd[k];
+                const uint64_t o = r0 + s_cur[d] + (k - s_ro[d]);
+                A.tmp_hi[o] = s_sh[k];
+                A.tmp_lo[o] = s_sl[k];
+            }
+            __syncthreads();
+            for (uint32_t d = threadIdx.x; d < nsub; d += blockDim.x) s_cur[d] += s_rc[d];
+            __syncthreads();
         }
     }
     for (uint32_t d = threadIdx.x; d < nsub; d += blockDim.x) {
@@ -2721,6 +2784,12 @@ void exchange(const Ranks& bs) {
     alltoallv(bs, ex_lo);
 }
 
+// tuning knobs for experiments (defaults are the tuned values)
+int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+
 // job sort by length class (longest first) + the chain kernel, on stream st
 void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, const uint32_t* lens,
                    const uint32_t* recs32, const uint32_t* tmp32, const uint32_t* big32, skm_stored_kmer_data* out,
@@ -2740,7 +2809,7 @@ void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, c
     const uint64_t nlong = *pin;
     if (nlong)
         hipLaunchKernelGGL(k_chain_long, dim3((uint32_t)nlong), dim3(128), 0, st, cs.sorted.as<Job>(), nlong, lens, recs32,
-                           tmp32, big32, out);
+                           tmp32, big32, out, env_int("SKM_CHAIN_PRIO", 0));
     if (nj > nlong) {
         const uint64_t threads = ceil_div(nj - nlong, 64) * 128;
         hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, st,
@@ -2865,9 +2934,10 @@ void phase_group(skm_build* b) {
         SKM_HIP(hipMemcpyAsync(ctr + 8, ctr_d + 8, 8 * 5, hipMemcpyDeviceToHost, st2));
         SKM_HIP(hipStreamSynchronize(st2));
         SKM_CHECK(ctr[8 + 3] <= b->jobs2_cap && ctr[8 + 4] <= b->lens_cap, SKM_E_OOM, "overflow chain buffers overflowed");
-        // the overflow's chains are the longest: wave pairs from 8192 samples up
-        launch_chains(st2, A2.jobs, ctr[8 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, nullptr, A.out_data, 13,
-                      ctr + 21);
+        // the overflow holds the longest chains: per-lane below 32768 samples (fewer waves beside
+        // the group-by), a wave pair each from there (latency-bound, grows with the world size)
+        launch_chains(st2, A2.jobs, ctr[8 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, nullptr, A.out_data,
+                      (uint32_t)env_int("SKM_OVF_LONG_CLASS", 15), ctr + 21);
         SKM_HIP(hipEventRecord(b->ev_o[2], st2));
         b->n_jobs += ctr[8 + 3];
         b->n_lens += ctr[8 + 4];
@@ -3137,7 +3207,7 @@ int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms) {
         if (n >= (1u << LONG_CLASS))
             hipLaunchKernelGGL(k_chain_long, dim3(njobs), dim3(128), 0, 0, dj.as<Job>(), (uint64_t)njobs,
                                dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(),
-                               dout.as<skm_stored_kmer_data>());
+                               dout.as<skm_stored_kmer_data>(), 0);
         else
         hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, 0, dj.as<Job>(),
                            (uint64_t)njobs, dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(),

@@ -9,6 +9,6 @@ r, o, l, f, i, funcs = synth.build_inputs(p)
 b = skm.SignatureBuilder(len(funcs))
 b.add_batch(r, o, l, f, i)
 b.prepare()
-b.run()
-b.run()
+for _ in range(int(os.environ.get('SKM_PROBE_RUNS', '2'))):
+    b.run()
 print(b.timings())
