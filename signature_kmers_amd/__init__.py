@@ -220,16 +220,17 @@ class SignatureBuilder:
         _check(lib().skm_build_run(self._h))
 
     def timings(self) -> dict:
-        ms = (C.c_float * 9)()
-        n = lib().skm_build_last_timings(self._h, ms, 9)
+        ms = (C.c_float * 11)()
+        n = lib().skm_build_last_timings(self._h, ms, 11)
         names = ["extract_count", "scan", "extract_scatter", "bucket_process", "overflow", "chains", "stats", "total",
-                 "exchange"]
+                 "exchange", "partition", "bucket_kernel"]
         return {names[i]: float(ms[i]) for i in range(n)}
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 8)()
-        n = lib().skm_build_counters(self._h, v, 8)
-        names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped"]
+        v = (C.c_uint64 * 9)()
+        n = lib().skm_build_counters(self._h, v, 9)
+        names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped",
+                 "overflow_elements", "overflow_kept"]
         return {names[i]: int(v[i]) for i in range(n)}
 
     def debug_jobs(self, k: int = 64) -> list:

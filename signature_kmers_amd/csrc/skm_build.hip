@@ -2148,6 +2148,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
         if (K == 0) continue;
         if (tid == 0) {
             s_base[0] = atomicAdd(A.kept_ctr, (unsigned long long)K);
+            atomicAdd(&A.ctr[0], (unsigned long long)K);  // the overflow's own kept count
             if (J) {
                 s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)J);
                 s_base[2] = atomicAdd(&A.ctr[4], (unsigned long long)Lt);
@@ -2261,8 +2262,9 @@ struct skm_build {
     skm_build_opts opts{};
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[10] = {};
-    float last_ms[9] = {};
+    hipEvent_t ev[12] = {};
+    float last_ms[11] = {};
+    uint64_t ovf_elems = 0, ovf_kept = 0;
 
     // host staging (reference emission order, only sequences with a kept function)
     std::vector<uint8_t> h_res;     // packed residues with one 0 separator after each sequence
@@ -2871,6 +2873,7 @@ void phase_group(skm_build* b) {
     // ---- 4a. level-2 partition ----
     hipLaunchKernelGGL(k_partition, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
+    SKM_HIP(hipEventRecord(b->ev[10], st));
     // readbacks go through pinned host memory (no staging copies, no pageable-copy stalls)
     unsigned long long* ctr = b->pinned_ctr();
     SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, 8 * 5, hipMemcpyDeviceToHost, st));
@@ -2904,6 +2907,7 @@ void phase_group(skm_build* b) {
         b->d_ovf_job.ensure(tot * 8);
         b->d_ovf_fm.ensure(tot * 4);
         b->jobs2_cap = ovf_elems / 3 + 16;
+        b->ovf_elems = ovf_elems;
         b->d_jobs2.ensure(sizeof(Job) * b->jobs2_cap);
         SKM_HIP(hipMemcpyAsync(b->d_ovf.p, ov, sizeof(OvfEntry) * novf, hipMemcpyHostToDevice, st));
         SKM_HIP(hipEventRecord(b->ev_part, st));
@@ -2924,12 +2928,15 @@ void phase_group(skm_build* b) {
     }
     T(2);
     // ---- 4b. group-by of the sub-buckets that fit LDS ----
+    SKM_HIP(hipEventRecord(b->ev[11], st));
     hipLaunchKernelGGL(k_bucket_process, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[5], st));
     T(3);
     // ---- 6. deferred P^2 / variance chains: the overflow's as soon as it is done ----
     b->n_jobs = b->n_lens = 0;
+    b->ovf_kept = 0;
+    if (!novf) b->ovf_elems = 0;
     if (novf) {
         SKM_HIP(hipMemcpyAsync(ctr + 8, ctr_d + 8, 8 * 5, hipMemcpyDeviceToHost, st2));
         SKM_HIP(hipStreamSynchronize(st2));
@@ -2940,6 +2947,7 @@ void phase_group(skm_build* b) {
                       (uint32_t)env_int("SKM_OVF_LONG_CLASS", 15), ctr + 21);
         SKM_HIP(hipEventRecord(b->ev_o[2], st2));
         b->n_jobs += ctr[8 + 3];
+        b->ovf_kept = ctr[8 + 0];
         b->n_lens += ctr[8 + 4];
     }
     T(4);
@@ -2990,6 +2998,8 @@ void phase_final(skm_build* b) {
     if (b->n_overflow) SKM_HIP(hipEventElapsedTime(&b->last_ms[4], b->ev_o[0], b->ev_o[1]));
     SKM_HIP(hipEventElapsedTime(&b->last_ms[7], b->ev[0], b->ev[8]));
     SKM_HIP(hipEventElapsedTime(&b->last_ms[8], b->ev[3], b->ev[4]));
+    SKM_HIP(hipEventElapsedTime(&b->last_ms[9], b->ev[4], b->ev[10]));   // level-2 partition kernel
+    SKM_HIP(hipEventElapsedTime(&b->last_ms[10], b->ev[11], b->ev[5]));  // group-by kernel alone
     b->ran = true;
 }
 
@@ -3237,15 +3247,16 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
-    const uint64_t v[7] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local};
-    int n = std::min(cap, 7);
+    const uint64_t v[9] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+                           b->ovf_elems, b->ovf_kept};
+    int n = std::min(cap, 9);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }
 
 int skm_build_last_timings(skm_build* b, float* ms, int cap) {
     if (!b || !ms) return SKM_E_ARG;
-    int n = std::min(cap, 9);
+    int n = std::min(cap, 11);
     for (int i = 0; i < n; ++i) ms[i] = b->last_ms[i];
     return n;
 }
