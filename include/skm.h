@@ -111,11 +111,13 @@ int skm_build_run(skm_build* b);
 /* Device time (ms) of the last run's phases: [0]=extract-count [1]=scan [2]=extract-scatter
  * [3]=bucket-process (partition + group-by) [4]=overflow (own stream, overlaps [3]) [5]=chains
  * [6]=stats (+ reductions) [7]=total [8]=exchange (world_size > 1) [9]=level-2 partition kernel
- * [10]=group-by kernel alone; returns entries written. */
+ * [10]=group-by kernel alone [11]=groups of > 64 members (k_big_groups + append);
+ * returns entries written. */
 int skm_build_last_timings(skm_build* b, float* ms, int cap);
 /* Counters of the last run: [0]=windows [1]=kept (owned by this rank) [2]=overflow sub-buckets
  * [3]=chain jobs [4]=chain samples [5]=sequences [6]=occurrences grouped on this rank
- * [7]=occurrences in overflow sub-buckets [8]=k-mers kept by the overflow path;
+ * [7]=occurrences in overflow sub-buckets [8]=k-mers kept by the overflow path
+ * [9]=groups of > 64 members handed to k_big_groups [10]=k-mers kept among them;
  * returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then

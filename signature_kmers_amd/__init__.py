@@ -220,17 +220,17 @@ class SignatureBuilder:
         _check(lib().skm_build_run(self._h))
 
     def timings(self) -> dict:
-        ms = (C.c_float * 11)()
-        n = lib().skm_build_last_timings(self._h, ms, 11)
+        ms = (C.c_float * 12)()
+        n = lib().skm_build_last_timings(self._h, ms, 12)
         names = ["extract_count", "scan", "extract_scatter", "bucket_process", "overflow", "chains", "stats", "total",
-                 "exchange", "partition", "bucket_kernel"]
+                 "exchange", "partition", "bucket_kernel", "big_groups"]
         return {names[i]: float(ms[i]) for i in range(n)}
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 9)()
-        n = lib().skm_build_counters(self._h, v, 9)
+        v = (C.c_uint64 * 11)()
+        n = lib().skm_build_counters(self._h, v, 11)
         names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped",
-                 "overflow_elements", "overflow_kept"]
+                 "overflow_elements", "overflow_kept", "big_groups", "big_kept"]
         return {names[i]: int(v[i]) for i in range(n)}
 
     def debug_jobs(self, k: int = 64) -> list:
@@ -239,8 +239,8 @@ class SignatureBuilder:
         return [int(x) for x in v]
 
     def debug_stamps(self, enable: bool) -> list:
-        v = (C.c_uint64 * 16)()
-        _check(lib().skm_build_debug_stamps(self._h, 1 if enable else 0, v, 16))
+        v = (C.c_uint64 * 32)()
+        _check(lib().skm_build_debug_stamps(self._h, 1 if enable else 0, v, 32))
         return [int(x) for x in v]
 
     def finish(self) -> KeptKmers:

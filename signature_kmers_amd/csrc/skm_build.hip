@@ -243,15 +243,98 @@ __device__ void bitonic_lds(uint64_t* hi, uint64_t* lo, uint32_t N, uint32_t kmi
     }
 }
 
+// Exchange with lane ^ D without LDS addressing: DPP quad_perm (1, 2) and row_ror:8 (8) on the
+// VALU, ds_swizzle bitmask mode (4, 16), v_permlane32_swap (32, CDNA4).
+template <int D>
+__device__ __forceinline__ uint32_t xshfl(uint32_t x) {
+    static_assert(D == 1 || D == 2 || D == 4 || D == 8 || D == 16 || D == 32, "xor distance");
+    if constexpr (D == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+    } else if constexpr (D == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+    } else if constexpr (D == 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
+    } else if constexpr (D == 4 || D == 16) {
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (D << 10));
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (threadIdx.x & 32u) ? (uint32_t)r[0] : (uint32_t)r[1];
+    }
+}
+template <int D>
+__device__ __forceinline__ uint64_t xshfl64(uint64_t v) {
+    return ((uint64_t)xshfl<D>((uint32_t)(v >> 32)) << 32) | xshfl<D>((uint32_t)v);
+}
+// run-time (wave-uniform) distance
+__device__ __forceinline__ uint64_t xshfl64_rt(uint64_t v, uint32_t d) {
+    switch (d) {
+        case 1: return xshfl64<1>(v);
+        case 2: return xshfl64<2>(v);
+        case 4: return xshfl64<4>(v);
+        case 8: return xshfl64<8>(v);
+        case 16: return xshfl64<16>(v);
+        default: return xshfl64<32>(v);
+    }
+}
+
+// distance known after unrolling (the switch folds away)
+__device__ __forceinline__ uint32_t xs(uint32_t x, int d) {
+    switch (d) {
+        case 1: return xshfl<1>(x);
+        case 2: return xshfl<2>(x);
+        case 4: return xshfl<4>(x);
+        case 8: return xshfl<8>(x);
+        case 16: return xshfl<16>(x);
+        default: return xshfl<32>(x);
+    }
+}
+__device__ __forceinline__ uint64_t xs64(uint64_t v, int d) {
+    return ((uint64_t)xs((uint32_t)(v >> 32), d) << 32) | xs((uint32_t)v, d);
+}
+
+// Inclusive wave scan on DPP: row_shr 1/2/4/8 within rows of 16, then row_bcast 15 / 31.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+    x += xshfl<1>(x);
+    x += xshfl<2>(x);
+    x += xshfl<4>(x);
+    x += xshfl<8>(x);
+    x += xshfl<16>(x);
+    x += xshfl<32>(x);
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_min(uint32_t x) {
+    x = min(x, xshfl<1>(x));
+    x = min(x, xshfl<2>(x));
+    x = min(x, xshfl<4>(x));
+    x = min(x, xshfl<8>(x));
+    x = min(x, xshfl<16>(x));
+    x = min(x, xshfl<32>(x));
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+    x = max(x, xshfl<1>(x));
+    x = max(x, xshfl<2>(x));
+    x = max(x, xshfl<4>(x));
+    x = max(x, xshfl<8>(x));
+    x = max(x, xshfl<16>(x));
+    x = max(x, xshfl<32>(x));
+    return x;
+}
+
 // Workgroup exclusive scan of one u32 per thread (blockDim multiple of 64, <= 1024).
 __device__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
+    const uint32_t x = wave_incl_scan(v);
     if (lane == 63) s_wave[wave] = x;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -403,22 +486,6 @@ __device__ GRes group_thread(const V& v, uint64_t a, uint32_t c, const uint32_t*
     r.var = 0;
     if (best_c <= 2) stats_small(r, lr0, lr1, best_c);
     return r;
-}
-
-__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
-    return x;
-}
-__device__ __forceinline__ uint32_t wave_min(uint32_t x) {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) x = min(x, (uint32_t)__shfl_xor(x, d, 64));
-    return x;
-}
-__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) x = max(x, (uint32_t)__shfl_xor(x, d, 64));
-    return x;
 }
 
 // Wave-level group (all 64 lanes, same a/c).  Only used for c > SMALLC, so the best run always
@@ -1204,7 +1271,9 @@ struct BucketArgs {
     uint32_t* lens;
     OvfEntry* ovf;
     uint32_t ovf_cap;
-    unsigned long long* stamps;   // optional [16] per-phase cycle sums (diagnostics)
+    unsigned long long* stamps;   // optional [32] per-phase cycle sums (diagnostics)
+    uint64_t* big_desc;        // [big_cap][2] groups of > 64 members handed to k_big_groups
+    uint32_t big_cap;
 };
 
 #define SKM_STAMP(i)                                                          \
@@ -1269,7 +1338,7 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
 __device__ __forceinline__ void bm_combine(uint32_t& cand, uint32_t& cc) {
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t oc = (uint32_t)__shfl_xor((int)cand, d, 64), on = (uint32_t)__shfl_xor((int)cc, d, 64);
+        const uint32_t oc = xs(cand, d), on = xs(cc, d);
         if (oc == cand) {
             cc += on;
         } else if (cc >= on) {
@@ -1288,156 +1357,6 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Wave-level group of 65..CAP members in LDS (order[a..a+c)).  Best function by Boyer-Moore
-// majority (a function with >= 80 % of the occurrences is the strict majority, otherwise the
-// group is cut anyway), upper-median offset by 9-way pivot selection, best-function members
-// compacted to the front and sorted by ordinal, chain lengths in visit order.
-__device__ __forceinline__ GRes lgroup_wave(const SubLds& L, uint32_t a, uint32_t c, const uint32_t* __restrict__ glen,
-                            uint8_t* __restrict__ flags) {
-    const uint32_t lane = threadIdx.x & 63u;
-    GRes r;
-    r.kept = false;
-    // majority candidate
-    uint32_t cand = 0xFFFFFFFFu, cc = 0;
-    for (uint32_t t = lane; t < c; t += 64) {
-        const uint32_t f = (uint32_t)(L.hi[L.order[a + t]] & 0xFFFFu);
-        if (cc == 0) {
-            cand = f;
-            cc = 1;
-        } else if (f == cand) {
-            ++cc;
-        } else {
-            --cc;
-        }
-    }
-    bm_combine(cand, cc);
-    uint32_t nb = 0;
-    for (uint32_t t = lane; t < c; t += 64) nb += (uint32_t)(L.hi[L.order[a + t]] & 0xFFFFu) == cand;
-    nb = wave_sum(nb);
-    if ((float)nb < float(c) * 0.8f) return r;
-    r.kept = true;
-    r.best_f = cand;
-    r.cbest = nb;
-    r.rb = 0;
-    // avg_from_end over all members: k-th smallest offset by binary search on the value
-    uint32_t vmin = 0xFFFFu, vmax = 0, sum = 0;
-    for (uint32_t t = lane; t < c; t += 64) {
-        const uint32_t j = L.order[a + t];
-        const uint64_t lo = L.lo[j];
-        const uint32_t o = (uint32_t)(lo & 0xFFFFu);
-        vmin = min(vmin, o);
-        vmax = max(vmax, o);
-        flags[lo >> 36] = 1;
-        const uint64_t hj = L.hi[j];
-        if ((uint32_t)(hj & 0xFFFFu) == cand) sum += (uint32_t)(hj >> 48);
-    }
-    vmin = wave_min(vmin);
-    vmax = wave_max(vmax);
-    sum = wave_sum(sum);
-    const uint32_t k = c / 2;
-    // invariant: answer in [vmin, vmax]; each pass counts 8 pivots at once (9-way split)
-    while (vmin < vmax) {
-        const uint32_t span = vmax - vmin;
-        uint32_t piv[8], cnt[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            piv[q] = vmin + (uint32_t)(((uint64_t)span * (uint64_t)(q + 1)) / 9u);
-            cnt[q] = 0;
-        }
-        for (uint32_t t = lane; t < c; t += 64) {
-            const uint32_t o = (uint32_t)(L.lo[L.order[a + t]] & 0xFFFFu);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) cnt[q] += o <= piv[q];
-        }
-        uint32_t nlo = vmin, nhi = vmax;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            cnt[q] = wave_sum(cnt[q]);
-        }
-        // smallest pivot with count >= k+1 bounds from above; the previous pivot from below
-#pragma unroll
-        for (int q = 7; q >= 0; --q)
-            if (cnt[q] >= k + 1) nhi = min(nhi, piv[q]);
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (cnt[q] < k + 1) nlo = max(nlo, piv[q] + 1);
-        vmin = nlo;
-        vmax = nhi;
-    }
-    r.avg = vmin;
-    r.mean = d2u16((double)(uint16_t)sum / (double)nb);
-    r.median = 0;
-    r.var = 0;
-    // compact the best-function members to the front (writes never pass the read position)
-    uint32_t w = 0;
-    for (uint32_t base = 0; base < c; base += 64) {
-        const uint32_t t = base + lane;
-        const uint32_t j = t < c ? L.order[a + t] : 0u;
-        const bool keep = t < c && (uint32_t)(L.hi[j] & 0xFFFFu) == cand;
-        const uint64_t m = __ballot(keep);
-        wave_sync();
-        if (keep) L.order[a + w + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)j;
-        w += (uint32_t)__popcll(m);
-        wave_sync();
-    }
-    // sort order[a..a+nb) by ordinal
-    if (nb <= 64) {
-        // one element per lane, bitonic network over shuffles; missing lanes hold +inf
-        uint64_t key = ~0ull;
-        uint32_t idx = 0;
-        if (lane < nb) {
-            idx = L.order[a + lane];
-            key = L.lo[idx];
-        }
-#pragma unroll
-        for (int kk = 2; kk <= 64; kk <<= 1) {
-#pragma unroll
-            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-                const uint64_t ok = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), jj, 64) << 32) |
-                                    (uint32_t)__shfl_xor((int)(uint32_t)key, jj, 64);
-                const uint32_t oi = (uint32_t)__shfl_xor((int)idx, jj, 64);
-                const bool lower = (lane & jj) == 0;
-                const bool asc = (lane & kk) == 0;
-                const bool take_min = lower == asc;
-                const bool other_smaller = ok < key;
-                if (take_min ? other_smaller : !other_smaller && ok != key) {
-                    key = ok;
-                    idx = oi;
-                }
-            }
-        }
-        wave_sync();
-        if (lane < nb) L.order[a + lane] = (uint16_t)idx;
-        wave_sync();
-    } else {
-        // bitonic for arbitrary n (only ascending compare-exchanges; missing partners = +inf)
-        uint32_t Np = 1;
-        while (Np < nb) Np <<= 1;
-        for (uint32_t kk = 2; kk <= Np; kk <<= 1) {
-            for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-                const bool flip = jj == (kk >> 1);
-                for (uint32_t t = lane; t < Np / 2; t += 64) {
-                    const uint32_t i = 2 * t - (t & (jj - 1));
-                    const uint32_t l = flip ? (i ^ (kk - 1)) : (i + jj);
-                    if (l < nb) {
-                        const uint16_t ia = L.order[a + i], ib = L.order[a + l];
-                        if (L.lo[ia] > L.lo[ib]) {
-                            L.order[a + i] = ib;
-                            L.order[a + l] = ia;
-                        }
-                    }
-                }
-                wave_sync();
-            }
-        }
-    }
-    for (uint32_t t = lane; t < nb; t += 64) {
-        const uint32_t jj = L.order[a + t];
-        L.lens32[a + (nb - 1 - t)] = elem_len(L.hi[jj], L.lo[jj], glen);  // reverse ordinal
-    }
-    return r;
-}
-
 // ------------------------------------------------------------------------------------------
 // Groups of 2..64 members, packed 64/S to a wave in aligned segments of S lanes (S = 2..64, the
 // next power of two >= c), one member per lane.  Every step is a segment-local shuffle network,
@@ -1452,8 +1371,8 @@ __device__ __forceinline__ uint64_t seg_bitonic64(uint64_t key, uint32_t& pay, u
     for (int k = 2; k <= S; k <<= 1) {
 #pragma unroll
         for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint64_t ok = shfl_xor_u64(key, j);
-            const uint32_t op = (uint32_t)__shfl_xor((int)pay, j, 64);
+            const uint64_t ok = xs64(key, j);
+            const uint32_t op = xs(pay, j);
             const bool take_min = ((m & (uint32_t)j) == 0) == ((m & (uint32_t)k) == 0);
             if (take_min ? (ok < key) : (ok > key)) {
                 key = ok;
@@ -1470,7 +1389,7 @@ __device__ __forceinline__ uint32_t seg_bitonic32(uint32_t key, uint32_t m) {
     for (int k = 2; k <= S; k <<= 1) {
 #pragma unroll
         for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint32_t ok = (uint32_t)__shfl_xor((int)key, j, 64);
+            const uint32_t ok = xs(key, j);
             const bool take_min = ((m & (uint32_t)j) == 0) == ((m & (uint32_t)k) == 0);
             key = take_min ? min(key, ok) : max(key, ok);
         }
@@ -1481,14 +1400,14 @@ __device__ __forceinline__ uint32_t seg_bitonic32(uint32_t key, uint32_t m) {
 template <int S>
 __device__ __forceinline__ uint32_t seg_reduce_max(uint32_t x) {
 #pragma unroll
-    for (int d = 1; d < S; d <<= 1) x = max(x, (uint32_t)__shfl_xor((int)x, d, 64));
+    for (int d = 1; d < S; d <<= 1) x = max(x, xs(x, d));
     return x;
 }
 
 template <int S>
 __device__ __forceinline__ uint32_t seg_reduce_sum(uint32_t x) {
 #pragma unroll
-    for (int d = 1; d < S; d <<= 1) x += (uint32_t)__shfl_xor((int)x, d, 64);
+    for (int d = 1; d < S; d <<= 1) x += xs(x, d);
     return x;
 }
 
@@ -1549,7 +1468,7 @@ __device__ __forceinline__ void seg_groups(const SubLds& L, uint32_t q0, uint32_
     if (kept && real) A.flags[s] = 1;
     const uint32_t x0 = (uint32_t)__shfl((int)len, (int)(rs + cbest - 1), 64);  // first visited
     const uint32_t x1 = (uint32_t)__shfl((int)len, (int)rs, 64);                // second when cbest == 2
-    if (kept && inrun && cbest >= 3) L.lens32[a + (rs + cbest - 1 - lane)] = len;  // visit order
+    if (kept && inrun && cbest >= 3) L.lens32[2 * a + (rs + cbest - 1 - lane)] = len;  // visit order
     if (kept && m == 0) {
         GRes r;
         r.kept = true;
@@ -1561,7 +1480,7 @@ __device__ __forceinline__ void seg_groups(const SubLds& L, uint32_t q0, uint32_
         const uint64_t h43 = hprefix | ((L.hi[rep] >> 16) & REM_MASK);
         L.hi[rep] = kept_hi(h43, r.avg);
         if (cbest >= 3) {
-            jobinfo[rep] = (a << 16) | JOB_KEPT | cbest;  // chain lengths at lens32[a..a+cbest)
+            jobinfo[rep] = (a << 16) | JOB_KEPT | cbest;  // chain lengths at lens32[2a..2a+cbest)
             fmean[rep] = bf | ((uint32_t)r.mean << 16);
         } else {
             jobinfo[rep] = JOB_KEPT;
@@ -1672,6 +1591,10 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         cstart[7] = run;
         tstart[7] = acc;
     }
+    // groups of more than 64 members go to k_big_groups: reserve their descriptors now, the
+    // atomic's latency hides behind the packed-group phase
+    unsigned long long big_base = 0;
+    if (tid == 0 && cstart[7] > cstart[6]) big_base = atomicAdd(&A.ctr[5], (unsigned long long)(cstart[7] - cstart[6]));
     __syncthreads();
     for (uint32_t g = tid; g < G; g += nt) {
         const uint32_t a = L.goff[L.glist[g]];
@@ -1699,22 +1622,28 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
             }
         }
     }
+    if (tid == 0) *reinterpret_cast<unsigned long long*>(L.wave + 44) = big_base;
     __syncthreads();
     SKM_STAMP(11);
-    {   // groups of more than 64 members: one wave each
+    {   // groups of more than 64 members: members (func << 48 | ordinal) into the group's own
+        // consumed slots, one descriptor each; k_big_groups resolves them register-resident
         const uint32_t nbig = cstart[7] - cstart[6];
-        const uint32_t wave = tid >> 6, nwaves = nt >> 6;
+        const uint64_t bbase = *reinterpret_cast<const unsigned long long*>(L.wave + 44);
+        const uint32_t wave = tid >> 6, nwaves = nt >> 6, lane = tid & 63u;
+        uint64_t* slots = reinterpret_cast<uint64_t*>(L.lens32);
         for (uint32_t bi = wave; bi < nbig; bi += nwaves) {
             const uint32_t g = L.big[cstart[6] + bi];
             const uint32_t rep = L.glist[g];
             const uint32_t a = L.goff[rep];
             const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
-            const GRes r = lgroup_wave(L, a, c, A.glen, A.flags);
-            if ((tid & 63u) == 0 && r.kept) {
-                const uint64_t h43 = hprefix | ((L.hi[rep] >> 16) & REM_MASK);
-                L.hi[rep] = kept_hi(h43, r.avg);
-                jobinfo[rep] = (a << 16) | JOB_KEPT | r.cbest;  // cbest > 51: always a chain job
-                fmean[rep] = r.best_f | ((uint32_t)r.mean << 16);
+            for (uint32_t t = lane; t < c; t += 64) {
+                const uint32_t j = L.order[a + t];
+                slots[a + t] = ((L.hi[j] & 0xFFFFull) << 48) | (L.lo[j] >> 16);
+            }
+            const uint64_t q = bbase + bi;
+            if (lane == 0 && q < A.big_cap) {
+                A.big_desc[2 * q] = (hprefix | ((L.hi[rep] >> 16) & REM_MASK)) | ((uint64_t)c << KEY_BITS);
+                A.big_desc[2 * q + 1] = L.lens_sel + 2 * a;
             }
         }
     }
@@ -1753,7 +1682,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
                 const uint32_t fm = fmean[j];
                 write_kept(A, o, H, kept_lo(fm & 0xFFFFu, fm >> 16, 0, 0));
                 Job jbr;
-                jbr.lens_off = L.lens_sel + (jb >> 16);
+                jbr.lens_off = L.lens_sel + 2 * (jb >> 16);
                 jbr.n = jn;
                 jbr.out_idx = (uint32_t)o;
                 A.jobs[oj++] = jbr;
@@ -1806,36 +1735,280 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     if (n == 0) return;
     const uint64_t hprefix = (uint64_t)(A.bucket_base + bucket) << A.rem_bits;
 
-    if (n <= (uint64_t)CAP && A.nsrc == 1) {
-        L.lens32 = reinterpret_cast<uint32_t*>(A.recs_hi + r0);
-        L.lens_sel = (LENS_IN_RECS << LENS_SEL_SHIFT) | (2 * r0);
-        process_sub(A.recs_hi + r0, A.recs_lo + r0, (uint32_t)n, A, hprefix, L);
-        return;
+    // a bucket that fits LDS is one batch straight from recs; otherwise the sub-buckets of the
+    // partition pass (k_partition) in tmp: consecutive sub-buckets are contiguous and hold
+    // disjoint keys, so as many as fit in LDS form one batch (the per-pass fixed costs -- load
+    // latency, barriers, reservations -- are paid once per ~CAP elements).  One call site of
+    // process_sub keeps the kernel's code footprint small.
+    const bool direct = n <= (uint64_t)CAP && A.nsrc == 1;
+    uint32_t nsub = 1;
+    if (!direct) {
+        const uint32_t* tab = A.sub_tab + (uint64_t)bucket * SUB_TAB;
+        nsub = tab[0];
+        for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_sub[d] = tab[1 + d];
+        __syncthreads();
+        SKM_STAMP(9);
     }
-    // ---- sub-buckets from the partition pass (k_partition) ----
-    const uint32_t* tab = A.sub_tab + (uint64_t)bucket * SUB_TAB;
-    const uint32_t nsub = tab[0];
-    for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_sub[d] = tab[1 + d];
-    __syncthreads();
-    SKM_STAMP(9);
-    // consecutive sub-buckets are contiguous in tmp and hold disjoint keys: batch as many as fit
-    // in LDS into one pass, so the per-pass fixed costs (load latency, barriers, reservations)
-    // are paid once per ~CAP elements
     for (uint32_t d = 0; d < nsub;) {
-        const uint32_t a = s_sub[d];
-        if (s_sub[d + 1] - a == 0 || s_sub[d + 1] - a > (uint32_t)CAP) {  // empty, or k_overflow's
-            ++d;
-            continue;
+        const uint64_t* src_hi;
+        const uint64_t* src_lo;
+        uint32_t cnt;
+        if (direct) {
+            src_hi = A.recs_hi + r0;
+            src_lo = A.recs_lo + r0;
+            cnt = (uint32_t)n;
+            L.lens_sel = (LENS_IN_RECS << LENS_SEL_SHIFT) | (2 * r0);
+            d = 1;
+        } else {
+            const uint32_t a = s_sub[d];
+            if (s_sub[d + 1] - a == 0 || s_sub[d + 1] - a > (uint32_t)CAP) {  // empty, or k_overflow's
+                ++d;
+                continue;
+            }
+            uint32_t d2 = d + 1;
+            while (d2 < nsub && s_sub[d2 + 1] - a <= (uint32_t)CAP) ++d2;
+            cnt = s_sub[d2] - a;
+            src_hi = A.tmp_hi + r0 + a;
+            src_lo = A.tmp_lo + r0 + a;
+            L.lens_sel = (LENS_IN_TMP << LENS_SEL_SHIFT) | (2 * (r0 + a));
+            d = d2;
         }
-        uint32_t d2 = d + 1;
-        while (d2 < nsub && s_sub[d2 + 1] - a <= (uint32_t)CAP) ++d2;
-        const uint32_t cnt = s_sub[d2] - a;
-        L.lens32 = reinterpret_cast<uint32_t*>(A.tmp_hi + r0 + a);
-        L.lens_sel = (LENS_IN_TMP << LENS_SEL_SHIFT) | (2 * (r0 + a));
-        process_sub(A.tmp_hi + r0 + a, A.tmp_lo + r0 + a, cnt, A, hprefix, L);
+        L.lens32 = reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(src_hi));
+        process_sub(src_hi, src_lo, cnt, A, hprefix, L);
         __syncthreads();
         SKM_STAMP(10);
-        d = d2;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Groups of 65..CAP members (k_bucket_process hands them over as descriptors): one wave per group,
+// no workgroup barriers, every member register-resident (E = 2..32 per lane).  Counting is done
+// on ballots (v_cmp + s_bcnt1, no cross-lane latency): the best-function count and the
+// upper-median offset by a 16-step radix select.  The best-function members are sorted by
+// ordinal with a bitonic network over 64 E keys (compare-exchanges within a lane below distance
+// E, DPP / swizzle / permlane exchanges above) and their lengths written in visit order into
+// the group's own slots (the chain job's input).
+// ------------------------------------------------------------------------------------------
+struct BigOut {              // one per descriptor; n == 0: group cut
+    uint64_t h43;            // hashed key
+    uint64_t lens_off;       // chain input (selector | u32 offset)
+    uint32_t n;              // best-function members (chain length)
+    uint16_t avg, func, mean, pad0;
+    uint32_t pad1;
+};
+static_assert(sizeof(BigOut) == 32, "BigOut layout");
+
+struct BigArgs {
+    const uint64_t* desc;
+    const unsigned long long* ndesc;   // device counter (k_bucket_process)
+    uint32_t cap;
+    const uint64_t* recs_hi;
+    const uint64_t* tmp_hi;
+    const uint32_t* glen;
+    uint8_t* flags;
+    BigOut* out;
+};
+
+template <int E>
+__device__ __forceinline__ uint32_t ballot_count(const bool (&p)[E]) {
+    uint32_t n = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) n += (uint32_t)__popcll(__ballot(p[e]));
+    return n;
+}
+
+template <int E, int D>
+__device__ __forceinline__ void bitonic_cross(uint64_t (&ky)[E], bool take_min) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint64_t o = xshfl64<D>(ky[e]);
+        ky[e] = take_min ? (o < ky[e] ? o : ky[e]) : (o > ky[e] ? o : ky[e]);
+    }
+}
+
+template <int E>
+__device__ __forceinline__ void big_group(const BigArgs& B, uint64_t g, uint64_t* mem, uint32_t c, uint64_t h43,
+                                          uint64_t lens_off) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t fo[E];  // func << 16 | offset (padding: 0xFFFFFFFF)
+    uint64_t ky[E];  // ordinal (s << 20 | i) << 16
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t t = lane * E + (uint32_t)e;
+        fo[e] = 0xFFFFFFFFu;
+        ky[e] = ~0ull;
+        if (t < c) {
+            const uint64_t v = mem[t];
+            const uint32_t s = (uint32_t)(v >> ELEM_I_BITS) & ((1u << ELEM_S_BITS) - 1u);
+            const uint32_t i = (uint32_t)v & ((1u << ELEM_I_BITS) - 1u);
+            fo[e] = ((uint32_t)(v >> 48) << 16) | ((B.glen[s] - i) & 0xFFFFu);
+            ky[e] = v << 16;
+        }
+    }
+    // majority candidate (a function with >= 80 % of the members is the strict majority)
+    uint32_t cand = 0xFFFFFFFFu, cc = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if (fo[e] != 0xFFFFFFFFu) {
+            const uint32_t f = fo[e] >> 16;
+            if (cc == 0) {
+                cand = f;
+                cc = 1;
+            } else if (f == cand) {
+                ++cc;
+            } else {
+                --cc;
+            }
+        }
+    }
+    bm_combine(cand, cc);
+    bool p[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) p[e] = (fo[e] >> 16) == cand;  // padding has func 0xFFFF != cand
+    const uint32_t nb = ballot_count<E>(p);
+    BigOut o;
+    o.h43 = h43;
+    o.lens_off = lens_off;
+    o.n = 0;
+    o.avg = o.func = o.mean = 0;
+    o.pad0 = 0;
+    o.pad1 = 0;
+    if ((float)nb < float(c) * 0.8f) {
+        if (lane == 0) B.out[g] = o;
+        return;
+    }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if (fo[e] != 0xFFFFFFFFu) {
+            const uint32_t s = (uint32_t)(ky[e] >> (16 + ELEM_I_BITS));
+            B.flags[s] = 1;
+            if (p[e]) sum += B.glen[s];
+        }
+        if (!p[e]) ky[e] = ~0ull;  // sort key: best-function members only
+    }
+    sum = wave_sum(sum);
+    // upper median offset: the (c/2)-th smallest (0-based) by radix select, bit 15 down to 0
+    uint32_t k = c / 2, pre = 0;
+#pragma unroll 1
+    for (int b = 15; b >= 0; --b) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t v = fo[e] == 0xFFFFFFFFu ? 0x10000u : (fo[e] & 0xFFFFu);
+            p[e] = ((v >> b) ^ (pre >> b)) == 0u;  // bits above b match the prefix, bit b clear
+        }
+        const uint32_t n0 = ballot_count<E>(p);
+        if (k >= n0) {
+            k -= n0;
+            pre |= 1u << b;
+        }
+    }
+    // ascending bitonic sort of the 64 E keys (blocked: lane holds keys lane*E .. lane*E+E-1)
+#pragma unroll 1
+    for (uint32_t kk = 2; kk <= 64u * E; kk <<= 1) {
+        const bool asc_lane = ((lane * (uint32_t)E) & kk) == 0;  // valid when kk >= 2E
+#pragma unroll 1
+        for (uint32_t jj = kk >> 1; jj >= (uint32_t)E; jj >>= 1) {
+            const uint32_t d = jj / (uint32_t)E;
+            const bool take_min = ((lane & d) == 0) == asc_lane;
+            switch (d) {  // wave-uniform
+                case 1: bitonic_cross<E, 1>(ky, take_min); break;
+                case 2: bitonic_cross<E, 2>(ky, take_min); break;
+                case 4: bitonic_cross<E, 4>(ky, take_min); break;
+                case 8: bitonic_cross<E, 8>(ky, take_min); break;
+                case 16: bitonic_cross<E, 16>(ky, take_min); break;
+                default: bitonic_cross<E, 32>(ky, take_min); break;
+            }
+        }
+#pragma unroll
+        for (int jj = E / 2; jj > 0; jj >>= 1) {
+            if ((uint32_t)jj < kk) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int l = e ^ jj;
+                    if (l > e) {
+                        const bool asc = (((lane * (uint32_t)E) + (uint32_t)e) & kk) == 0;
+                        const uint64_t x = ky[e], y = ky[l];
+                        const bool sw = asc ? (y < x) : (x < y);
+                        ky[e] = sw ? y : x;
+                        ky[l] = sw ? x : y;
+                    }
+                }
+            }
+        }
+    }
+    // chain input: best-function lengths in visit (reverse ordinal) order, over the group's own
+    // slots (every member is in registers by now)
+    uint32_t* lens = reinterpret_cast<uint32_t*>(mem);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t t = lane * E + (uint32_t)e;
+        if (t < nb) lens[nb - 1 - t] = B.glen[(uint32_t)(ky[e] >> (16 + ELEM_I_BITS))];
+    }
+    o.n = nb;
+    o.avg = (uint16_t)pre;
+    o.func = (uint16_t)cand;
+    o.mean = d2u16((double)(uint16_t)sum / (double)nb);
+    if (lane == 0) B.out[g] = o;
+}
+
+constexpr int BIG_WG = 256;
+
+// LARGE = false: groups of 65..1024 members (E <= 16, 128 VGPRs, 2 waves per SIMD);
+// LARGE = true: 1025..CAP (E = 32), a separate launch so the common case keeps its occupancy.
+template <bool LARGE>
+__global__ __launch_bounds__(BIG_WG, LARGE ? 1 : 2) void k_big_groups(BigArgs B) {
+    const uint64_t nd = min((uint64_t)*B.ndesc, (uint64_t)B.cap);
+    const uint64_t nw = (uint64_t)gridDim.x * (BIG_WG / 64);
+    for (uint64_t g = (uint64_t)blockIdx.x * (BIG_WG / 64) + (threadIdx.x >> 6); g < nd; g += nw) {
+        const uint64_t d0 = B.desc[2 * g], d1 = B.desc[2 * g + 1];
+        const uint32_t c = (uint32_t)(d0 >> KEY_BITS);
+        if (LARGE != (c > 1024u)) continue;
+        const uint64_t h43 = d0 & KEY_MASK;
+        const uint64_t sel = d1 >> LENS_SEL_SHIFT, off = d1 & LENS_OFF_MASK;
+        uint64_t* mem = const_cast<uint64_t*>(sel == LENS_IN_RECS ? B.recs_hi : B.tmp_hi) + off / 2;
+        if constexpr (LARGE) {
+            big_group<32>(B, g, mem, c, h43, d1);
+        } else {
+            if (c <= 128u) big_group<2>(B, g, mem, c, h43, d1);
+            else if (c <= 256u) big_group<4>(B, g, mem, c, h43, d1);
+            else if (c <= 512u) big_group<8>(B, g, mem, c, h43, d1);
+            else big_group<16>(B, g, mem, c, h43, d1);
+        }
+    }
+}
+
+// Kept big groups appended to the kept k-mers and chain jobs: one reservation per round of
+// BIG_WG descriptors per workgroup.
+__global__ __launch_bounds__(BIG_WG) void k_big_append(const BigOut* __restrict__ out, BigArgs B, BucketArgs A) {
+    __shared__ __align__(16) uint32_t s_wave[48];
+    __shared__ unsigned long long s_base[2];
+    const uint64_t nd = min((uint64_t)*B.ndesc, (uint64_t)B.cap);
+    const uint64_t per = (nd + gridDim.x - 1) / gridDim.x;
+    const uint64_t g0 = (uint64_t)blockIdx.x * per, g1 = min(nd, g0 + per);
+    for (uint64_t r = g0; r < g1; r += BIG_WG) {
+        const uint64_t g = r + threadIdx.x;
+        const bool kept = g < g1 && out[g].n != 0;
+        uint32_t tot;
+        const uint32_t pos = wg_exclusive_scan(kept ? 1u : 0u, s_wave, tot);
+        if (tot == 0) continue;
+        if (threadIdx.x == 0) {
+            s_base[0] = atomicAdd(A.kept_ctr, (unsigned long long)tot);
+            s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)tot);
+            atomicAdd(&A.ctr[6], (unsigned long long)tot);  // kept big groups (diagnostics)
+        }
+        __syncthreads();
+        if (kept) {
+            const BigOut o = out[g];
+            const uint64_t w = s_base[0] + pos;
+            write_kept(A, w, kept_hi(o.h43, o.avg), kept_lo(o.func, o.mean, 0, 0));
+            Job jb;
+            jb.lens_off = o.lens_off;
+            jb.n = o.n;
+            jb.out_idx = (uint32_t)w;
+            A.jobs[s_base[1] + pos] = jb;
+        }
+        __syncthreads();
     }
 }
 
@@ -2262,8 +2435,8 @@ struct skm_build {
     skm_build_opts opts{};
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[12] = {};
-    float last_ms[11] = {};
+    hipEvent_t ev[13] = {};
+    float last_ms[12] = {};
     uint64_t ovf_elems = 0, ovf_kept = 0;
 
     // host staging (reference emission order, only sequences with a kept function)
@@ -2290,7 +2463,8 @@ struct skm_build {
     DevBuf d_recs_hi, d_recs_lo, d_tmp_hi, d_tmp_lo;
     DevBuf d_cur0, d_cur1, d_slices;   // staged scatter cursors
     DevBuf d_keys, d_data, d_ctr, d_flags, d_dfunc, d_swf, d_ovf, d_ovf_hi, d_ovf_lo, d_ovf_heads, d_ovf_job, d_ovf_fm;
-    DevBuf d_jobs, d_lens, d_stamps;
+    DevBuf d_jobs, d_lens, d_stamps, d_big_desc, d_big_out;
+    uint64_t big_cap = 0, n_big = 0, big_kept = 0;
     bool stamps = false;
     uint64_t jobs_cap = 0, lens_cap = 0, n_jobs = 0, n_lens = 0;
     uint32_t n_overflow = 0;
@@ -2865,8 +3039,8 @@ void phase_group(skm_build* b) {
     A.ovf_cap = (uint32_t)b->ovf_cap;
     A.stamps = nullptr;
     if (b->stamps) {
-        b->d_stamps.ensure(16 * 8);
-        SKM_HIP(hipMemsetAsync(b->d_stamps.p, 0, 16 * 8, st));
+        b->d_stamps.ensure(32 * 8);
+        SKM_HIP(hipMemsetAsync(b->d_stamps.p, 0, 32 * 8, st));
         A.stamps = b->d_stamps.as<unsigned long long>();
     }
     T(0);
@@ -2927,11 +3101,31 @@ void phase_group(skm_build* b) {
         SKM_HIP(hipEventRecord(b->ev_o[1], st2));
     }
     T(2);
-    // ---- 4b. group-by of the sub-buckets that fit LDS ----
+    // ---- 4b. group-by of the sub-buckets that fit LDS; groups of > 64 members are handed to
+    //      k_big_groups (one wave each) and appended ----
+    b->big_cap = b->n_local / 65 + 64;
+    b->d_big_desc.ensure(16 * b->big_cap);
+    b->d_big_out.ensure(sizeof(BigOut) * b->big_cap);
+    A.big_desc = b->d_big_desc.as<uint64_t>();
+    A.big_cap = (uint32_t)std::min<uint64_t>(b->big_cap, 0xFFFFFFFFull);
+    BigArgs BA;
+    BA.desc = A.big_desc;
+    BA.ndesc = ctr_d + 5;
+    BA.cap = A.big_cap;
+    BA.recs_hi = A.recs_hi;
+    BA.tmp_hi = A.tmp_hi;
+    BA.glen = A.glen;
+    BA.flags = A.flags;
+    BA.out = b->d_big_out.as<BigOut>();
     SKM_HIP(hipEventRecord(b->ev[11], st));
     hipLaunchKernelGGL(k_bucket_process, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[5], st));
+    hipLaunchKernelGGL(k_big_groups<false>, dim3(2048), dim3(BIG_WG), 0, st, BA);
+    hipLaunchKernelGGL(k_big_groups<true>, dim3(512), dim3(BIG_WG), 0, st, BA);
+    hipLaunchKernelGGL(k_big_append, dim3(256), dim3(BIG_WG), 0, st, BA.out, BA, A);
+    SKM_HIP(hipGetLastError());
+    SKM_HIP(hipEventRecord(b->ev[12], st));
     T(3);
     // ---- 6. deferred P^2 / variance chains: the overflow's as soon as it is done ----
     b->n_jobs = b->n_lens = 0;
@@ -2951,9 +3145,12 @@ void phase_group(skm_build* b) {
         b->n_lens += ctr[8 + 4];
     }
     T(4);
-    SKM_HIP(hipMemcpyAsync(ctr, ctr_d, 8 * 5, hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipMemcpyAsync(ctr, ctr_d, 8 * 7, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
     SKM_CHECK(ctr[3] <= b->jobs_cap, SKM_E_OOM, "chain buffers overflowed");
+    SKM_CHECK(ctr[5] <= b->big_cap, SKM_E_OOM, "big-group descriptor capacity exceeded");
+    b->n_big = ctr[5];
+    b->big_kept = ctr[6];
     launch_chains(st, A.jobs, ctr[3], b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
                   reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, LONG_CLASS, ctr + 20);
     b->n_jobs += ctr[3];
@@ -2992,7 +3189,7 @@ void phase_final(skm_build* b) {
     // [0] extract-count [1] scan [2] extract-scatter [3] bucket [4] overflow [5] chains
     // [6] stats (+ reductions) [7] total [8] exchange
     // [4] overflow: its own kernel time on the second stream (it overlaps [3])
-    const int from[7] = {0, 1, 2, 4, 5, 5, 7}, to[7] = {1, 2, 3, 5, 6, 6, 8};
+    const int from[7] = {0, 1, 2, 4, 5, 12, 7}, to[7] = {1, 2, 3, 12, 6, 6, 8};
     for (int i = 0; i < 7; ++i) SKM_HIP(hipEventElapsedTime(&b->last_ms[i], b->ev[from[i]], b->ev[to[i]]));
     b->last_ms[4] = 0.f;
     if (b->n_overflow) SKM_HIP(hipEventElapsedTime(&b->last_ms[4], b->ev_o[0], b->ev_o[1]));
@@ -3000,6 +3197,7 @@ void phase_final(skm_build* b) {
     SKM_HIP(hipEventElapsedTime(&b->last_ms[8], b->ev[3], b->ev[4]));
     SKM_HIP(hipEventElapsedTime(&b->last_ms[9], b->ev[4], b->ev[10]));   // level-2 partition kernel
     SKM_HIP(hipEventElapsedTime(&b->last_ms[10], b->ev[11], b->ev[5]));  // group-by kernel alone
+    SKM_HIP(hipEventElapsedTime(&b->last_ms[11], b->ev[5], b->ev[12]));  // big groups + append
     b->ran = true;
 }
 
@@ -3166,9 +3364,9 @@ int skm_build_debug_stamps(skm_build* b, int enable, uint64_t* out, int cap) {
     SKM_API_BEGIN
     SKM_CHECK(b, SKM_E_ARG, "null build");
     if (out && cap > 0 && b->stamps && b->d_stamps.p) {
-        uint64_t tmp[16];
+        uint64_t tmp[32];
         SKM_HIP(hipMemcpy(tmp, b->d_stamps.p, sizeof(tmp), hipMemcpyDeviceToHost));
-        for (int i = 0; i < cap && i < 16; ++i) out[i] = tmp[i];
+        for (int i = 0; i < cap && i < 32; ++i) out[i] = tmp[i];
     }
     b->stamps = enable != 0;
     SKM_API_END
@@ -3247,16 +3445,16 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
-    const uint64_t v[9] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
-                           b->ovf_elems, b->ovf_kept};
-    int n = std::min(cap, 9);
+    const uint64_t v[11] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+                            b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept};
+    int n = std::min(cap, 11);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }
 
 int skm_build_last_timings(skm_build* b, float* ms, int cap) {
     if (!b || !ms) return SKM_E_ARG;
-    int n = std::min(cap, 11);
+    int n = std::min(cap, 12);
     for (int i = 0; i < n; ++i) ms[i] = b->last_ms[i];
     return n;
 }

@@ -31,10 +31,14 @@ print("timings", json.dumps(b.timings()))
 b.debug_stamps(True)
 b.run()
 st = b.debug_stamps(False)
-tot = sum(st)
+tot = sum(st[:16])
 print("stamps (cycles summed over workgroups):")
-for k in sorted(STAMP_NAMES):
+for k in sorted(STAMP_NAMES):  # noqa
     print(f"  {STAMP_NAMES[k]:>20s} {st[k]:>16d} {100.0 * st[k] / max(tot, 1):6.1f}%")
+for q, nm in enumerate(["65-128", "129-256", "257-512", "513-2048"]):
+    ng = st[20 + q]
+    print(f"  big groups {nm:>9s}: {ng:>9d} groups, {st[16 + q] / max(ng, 1):10.0f} cycles/group (wave), "
+          f"{100.0 * st[16 + q] / max(tot, 1):5.1f}% of stamped WG cycles")
 print("timings(stamped)", json.dumps(b.timings()))
 print("counters", json.dumps(b.counters()))
 print("longest jobs", b.debug_jobs(16))
