@@ -125,8 +125,12 @@ int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 int skm_build_debug_stamps(skm_build* b, int enable, uint64_t* out, int cap);
 /* Diagnostics: lengths of the first cap chain jobs in execution order (longest first). */
 int skm_build_debug_jobs(skm_build* b, uint32_t* out, int cap);
-/* Diagnostics: device time of the chain kernel on njobs synthetic jobs of length n. */
-int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms);
+/* Diagnostics: device time of the chain kernel on njobs synthetic jobs of length n
+ * (mode 0: the build's choice by length, 1: one lane per chain, 2: one wave pair per chain). */
+int skm_debug_chain_bench(uint32_t n, uint32_t njobs, int mode, float* ms);
+/* Diagnostics: the P^2 median and the variance (raw doubles) of one chain of n samples in visit
+ * order, by the per-lane (mode 1) or the wave-pair (mode 2) chain code. */
+int skm_debug_chain_eval(const uint32_t* samples, uint32_t n, int mode, double* median, double* var);
 /* Diagnostics: device exact-division helpers (reciprocal + corrected quotient used by the
  * statistics recurrences) against IEEE division: m = 1..nm, then nm*per random pairs. */
 int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches);

@@ -71,7 +71,8 @@ _SIGS = {
     "skm_build_finish": (C.c_int, [_P, C.POINTER(_Kept)]),
     "skm_build_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
     "skm_build_debug_jobs": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int]),
-    "skm_debug_chain_bench": (C.c_int, [C.c_uint32, C.c_uint32, C.POINTER(C.c_float)]),
+    "skm_debug_chain_bench": (C.c_int, [C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_float)]),
+    "skm_debug_chain_eval": (C.c_int, [_P, C.c_uint32, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "skm_build_debug_stamps": (C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64), C.c_int]),
     "skm_kept_free": (None, [C.POINTER(_Kept)]),
     "skm_build_destroy": (None, [_P]),
@@ -123,10 +124,18 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
 
 
-def debug_chain_bench(n: int, njobs: int) -> float:
+def debug_chain_bench(n: int, njobs: int, mode: int = 0) -> float:
     ms = C.c_float()
-    _check(lib().skm_debug_chain_bench(n, njobs, C.byref(ms)))
+    _check(lib().skm_debug_chain_bench(n, njobs, mode, C.byref(ms)))
     return ms.value
+
+
+def debug_chain_eval(samples, mode: int):
+    """(P^2 median, variance) as raw doubles for one chain (samples in visit order)."""
+    x = np.ascontiguousarray(samples, dtype=np.uint32)
+    med, var = C.c_double(), C.c_double()
+    _check(lib().skm_debug_chain_eval(_ptr(x), len(x), mode, C.byref(med), C.byref(var)))
+    return med.value, var.value
 
 
 def debug_div_check(nm: int, per: int) -> int:

@@ -105,6 +105,25 @@ __device__ __forceinline__ double div_by(double a, double m, double y) {
 }
 
 // Boost.Accumulators p_square_quantile(p=0.5) + lazy mean over a u16 sum + immediate variance.
+// P^2 parabolic height update of one marker (Boost p_square_quantile): neighbours
+// hm_ / hp_, actual-position gaps dp = n[i+1]-n[i] > 1 or dm = n[i-1]-n[i] < -1, direction
+// sg = +-1.  Quotients by integers take the reciprocal + corrected-quotient route; sg / (dp - dm)
+// is exactly +-RN(1/(dp - dm)), so the product by it is +-RN(ym * S) (same rounding).
+__device__ __forceinline__ double p2_height_y(double hm_, double H, double hp_, int32_t dpi, int32_t dmi, int32_t sgi,
+                                              double ydp, double ydm, double ym) {
+    const double dp = (double)dpi, dm = (double)dmi;
+    const double hp = div_by(hp_ - H, dp, ydp);
+    const double hm = div_by(hm_ - H, dm, ydm);
+    const double t = ym * ((double)(sgi - dmi) * hp + (double)(dpi - sgi) * hm);
+    const double hh = sgi > 0 ? H + t : H - t;
+    const double lin = sgi > 0 ? H + hp : H - hm;
+    return (hm_ < hh && hh < hp_) ? hh : lin;
+}
+__device__ __forceinline__ double p2_height(double hm_, double H, double hp_, int32_t dpi, int32_t dmi, int32_t sgi) {
+    return p2_height_y(hm_, H, hp_, dpi, dmi, sgi, rcp_int((double)dpi), rcp_int((double)dmi),
+                       rcp_int((double)(dpi - dmi)));
+}
+
 struct SigStats {
     double h[5];
     int32_t act[5];
@@ -162,19 +181,7 @@ struct SigStats {
                 const int32_t dmi = act[i - 1] - act[i];
                 if ((d4 >= 4 && dpi > 1) || (d4 <= -4 && dmi < -1)) {
                     const int32_t sgi = d4 > 0 ? 1 : -1;  // d / |d|, exactly +-1
-                    const double dp = (double)dpi, dm = (double)dmi;
-                    const double ydp = rcp_int(dp), ydm = rcp_int(dm), ym = rcp_int((double)(dpi - dmi));
-                    const double hp = div_by(h[i + 1] - h[i], dp, ydp);
-                    const double hm = div_by(h[i - 1] - h[i], dm, ydm);
-                    const double sgd = (double)sgi;
-                    const double so = sgi > 0 ? ym : -ym;  // sign_d / (dp - dm)
-                    const double hh = h[i] + so * ((sgd - dm) * hp + (dp - sgd) * hm);
-                    if (h[i - 1] < hh && hh < h[i + 1]) {
-                        h[i] = hh;
-                    } else {
-                        if (sgi > 0) h[i] += hp;
-                        if (sgi < 0) h[i] -= hm;
-                    }
+                    h[i] = p2_height(h[i - 1], h[i], h[i + 1], dpi, dmi, sgi);
                     act[i] += sgi;
                 }
             }
@@ -697,8 +704,29 @@ __device__ __forceinline__ double readlane_f64(double v, uint32_t l) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-__device__ double chain_long_p2(const uint32_t* __restrict__ x, uint32_t n) {
+// The adjusting markers of one step (mask M, bit i-1 = marker i): their nine reciprocals first
+// (independent of the heights), then the dependent height chain marker 1 -> 2 -> 3, all in one
+// basic block so the in-order issue overlaps the reciprocal latencies.
+template <int M>
+__device__ __forceinline__ void p2_adjust(double& h1, double& h2, double& h3, double h0, double h4,
+                                          const int32_t (&dp)[3], const int32_t (&dm)[3], const int32_t (&sg)[3]) {
+    double yp[3], ym[3], yd[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if ((M >> i) & 1) {
+            yp[i] = rcp_int((double)dp[i]);
+            ym[i] = rcp_int((double)dm[i]);
+            yd[i] = rcp_int((double)(dp[i] - dm[i]));
+        }
+    }
+    if constexpr ((M & 1) != 0) h1 = p2_height_y(h0, h1, h2, dp[0], dm[0], sg[0], yp[0], ym[0], yd[0]);
+    if constexpr ((M & 2) != 0) h2 = p2_height_y(h1, h2, h3, dp[1], dm[1], sg[1], yp[1], ym[1], yd[1]);
+    if constexpr ((M & 4) != 0) h3 = p2_height_y(h2, h3, h4, dp[2], dm[2], sg[2], yp[2], ym[2], yd[2]);
+}
+
+__device__ __forceinline__ double chain_long_p2(const uint32_t* __restrict__ x, uint32_t n_) {
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n_);  // wave-uniform: scalar walk
     SigStats st;
     st.init();
     const uint32_t n0 = min(n, 5u);
@@ -707,7 +735,7 @@ __device__ double chain_long_p2(const uint32_t* __restrict__ x, uint32_t n) {
     double h1 = st.h[1], h2 = st.h[2], h3 = st.h[3];
     uint32_t h0i = (uint32_t)st.h[0], h4i = (uint32_t)st.h[4];  // extremes are always samples
     int32_t a1 = st.act[1], a2 = st.act[2], a3 = st.act[3], a4 = st.act[4];
-    uint32_t cnt = 5;
+    int32_t k4 = 0;  // cnt - 5 after the increment below
     uint32_t xn = 5 + lane < n ? x[5 + lane] : 0u;
     for (uint32_t base = 5; base < n; base += 64) {
         const uint32_t m = min(64u, n - base);
@@ -719,42 +747,56 @@ __device__ double chain_long_p2(const uint32_t* __restrict__ x, uint32_t n) {
         const double xd = (double)xl;
         uint64_t B1 = __ballot(live && h1 <= xd), B2 = __ballot(live && h2 <= xd), B3 = __ballot(live && h3 <= xd);
         for (uint32_t l = 0; l < m; ++l) {
-            const int32_t cell = 1 + (int32_t)((B1 >> l) & 1u) + (int32_t)((B2 >> l) & 1u) + (int32_t)((B3 >> l) & 1u);
-            a1 += cell <= 1;
-            a2 += cell <= 2;
-            a3 += cell <= 3;
+            // integer walk (scalar): cell, positions, the three adjust decisions in marker order
+            a1 += ((B1 >> l) & 1u) ? 0 : 1;
+            a2 += ((B2 >> l) & 1u) ? 0 : 1;
+            a3 += ((B3 >> l) & 1u) ? 0 : 1;
             a4 += 1;
-            ++cnt;
-            const int32_t k4 = (int32_t)(cnt - 5);
-            bool moved = false;
-            // marker i: d4 = 4*(desired - actual), exact; heights only when it adjusts
-#define SKM_P2_MARKER(I, AM, A, AP, HM, H, HP)                                                      \
-            {                                                                                      \
-                const int32_t d4 = 4 * ((I) + 1) + k4 * (I) - 4 * (A);                             \
-                const int32_t dpi = (AP) - (A), dmi = (AM) - (A);                                  \
-                if ((d4 >= 4 && dpi > 1) || (d4 <= -4 && dmi < -1)) {                             \
-                    const int32_t sgi = d4 > 0 ? 1 : -1;                                           \
-                    const double hm_ = (HM), hp_ = (HP);                                           \
-                    const double dp = (double)dpi, dm = (double)dmi;                               \
-                    const double ydp = rcp_int(dp), ydm = rcp_int(dm), ym = rcp_int((double)(dpi - dmi)); \
-                    const double hp = div_by(hp_ - (H), dp, ydp);                                  \
-                    const double hm = div_by(hm_ - (H), dm, ydm);                                  \
-                    const double sgd = (double)sgi;                                                \
-                    const double so = sgi > 0 ? ym : -ym;                                          \
-                    const double hh = (H) + so * ((sgd - dm) * hp + (dp - sgd) * hm);              \
-                    if (hm_ < hh && hh < hp_)                                                      \
-                        (H) = hh;                                                                  \
-                    else                                                                           \
-                        (H) = sgi > 0 ? (H) + hp : (H) - hm;                                       \
-                    (A) += sgi;                                                                    \
-                    moved = true;                                                                  \
-                }                                                                                  \
+            ++k4;
+            int32_t dp[3], dm[3], sg[3];
+            uint32_t mask = 0;
+            {
+                const int32_t d4 = 8 + k4 - 4 * a1;
+                dp[0] = a2 - a1;
+                dm[0] = 1 - a1;
+                sg[0] = d4 > 0 ? 1 : -1;
+                if ((d4 >= 4 && dp[0] > 1) || (d4 <= -4 && dm[0] < -1)) {
+                    mask |= 1u;
+                    a1 += sg[0];
+                }
             }
-            SKM_P2_MARKER(1, 1, a1, a2, (double)(uint32_t)__builtin_amdgcn_readlane((int)imin, (int)l), h1, h2)
-            SKM_P2_MARKER(2, a1, a2, a3, h1, h2, h3)
-            SKM_P2_MARKER(3, a2, a3, a4, h2, h3, (double)(uint32_t)__builtin_amdgcn_readlane((int)imax, (int)l))
-#undef SKM_P2_MARKER
-            if (moved) {
+            {
+                const int32_t d4 = 12 + 2 * k4 - 4 * a2;
+                dp[1] = a3 - a2;
+                dm[1] = a1 - a2;
+                sg[1] = d4 > 0 ? 1 : -1;
+                if ((d4 >= 4 && dp[1] > 1) || (d4 <= -4 && dm[1] < -1)) {
+                    mask |= 2u;
+                    a2 += sg[1];
+                }
+            }
+            {
+                const int32_t d4 = 16 + 3 * k4 - 4 * a3;
+                dp[2] = a4 - a3;
+                dm[2] = a2 - a3;
+                sg[2] = d4 > 0 ? 1 : -1;
+                if ((d4 >= 4 && dp[2] > 1) || (d4 <= -4 && dm[2] < -1)) {
+                    mask |= 4u;
+                    a3 += sg[2];
+                }
+            }
+            if (mask) {
+                const double h0 = (double)(uint32_t)__builtin_amdgcn_readlane((int)imin, (int)l);
+                const double h4 = (double)(uint32_t)__builtin_amdgcn_readlane((int)imax, (int)l);
+                switch (mask) {
+                    case 1: p2_adjust<1>(h1, h2, h3, h0, h4, dp, dm, sg); break;
+                    case 2: p2_adjust<2>(h1, h2, h3, h0, h4, dp, dm, sg); break;
+                    case 3: p2_adjust<3>(h1, h2, h3, h0, h4, dp, dm, sg); break;
+                    case 4: p2_adjust<4>(h1, h2, h3, h0, h4, dp, dm, sg); break;
+                    case 5: p2_adjust<5>(h1, h2, h3, h0, h4, dp, dm, sg); break;
+                    case 6: p2_adjust<6>(h1, h2, h3, h0, h4, dp, dm, sg); break;
+                    default: p2_adjust<7>(h1, h2, h3, h0, h4, dp, dm, sg); break;
+                }
                 B1 = __ballot(live && h1 <= xd);
                 B2 = __ballot(live && h2 <= xd);
                 B3 = __ballot(live && h3 <= xd);
@@ -766,8 +808,9 @@ __device__ double chain_long_p2(const uint32_t* __restrict__ x, uint32_t n) {
     return h2;
 }
 
-__device__ double chain_long_var(const uint32_t* __restrict__ x, uint32_t n) {
+__device__ __forceinline__ double chain_long_var(const uint32_t* __restrict__ x, uint32_t n_) {
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n_);
     double var = 0.0;
     uint32_t sum = 0;  // running u32 sum; only its low 16 bits are the accumulator's sum
     uint32_t xn = lane < n ? x[lane] : 0u;
@@ -839,6 +882,39 @@ __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, ui
         out[jb.out_idx].var = d2u16(st.var);
     else
         out[jb.out_idx].median = d2u16(st.h[2]);
+}
+
+// Diagnostics: one half of the wave-pair chain code alone (which 0: P^2, 1: variance).
+__global__ __launch_bounds__(64) void k_chain_long_half(const Job* __restrict__ jobs, const uint32_t* __restrict__ lens,
+                                                        int which, double* __restrict__ out) {
+    const Job jb = jobs[blockIdx.x];
+    const uint32_t* x = lens + (jb.lens_off & LENS_OFF_MASK);
+    const double r = which == 0 ? chain_long_p2(x, jb.n) : chain_long_var(x, jb.n);
+    if (threadIdx.x == 0) out[blockIdx.x] = r;
+}
+
+// Diagnostics: one chain, raw P^2 median and variance (mode 1: one lane; 2: wave pair).
+__global__ __launch_bounds__(128) void k_chain_eval(const uint32_t* __restrict__ x, uint32_t n, int mode,
+                                                    double* __restrict__ out) {
+    if (mode == 2) {
+        if (threadIdx.x < 64) {
+            const double m = chain_long_p2(x, n);
+            if (threadIdx.x == 0) out[0] = m;
+        } else {
+            const double v = chain_long_var(x, n);
+            if (threadIdx.x == 64) out[1] = v;
+        }
+    } else if ((threadIdx.x & 63u) == 0) {
+        SigStats st;
+        st.init();
+        if (threadIdx.x == 0) {
+            chain_run<false>(st, x, n);
+            out[0] = st.h[2];
+        } else {
+            chain_run<true>(st, x, n);
+            out[1] = st.var;
+        }
+    }
 }
 
 // Diagnostics: rcp_int / div_by against IEEE division.  Thread t checks m = t + 1 (and -m), then
@@ -2983,9 +3059,19 @@ void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, c
     SKM_HIP(hipMemcpyAsync(pin, cs.offs.as<uint64_t>() + (uint64_t)nwg * JOB_CLASSES, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
     const uint64_t nlong = *pin;
-    if (nlong)
-        hipLaunchKernelGGL(k_chain_long, dim3((uint32_t)nlong), dim3(128), 0, st, cs.sorted.as<Job>(), nlong, lens, recs32,
-                           tmp32, big32, out, env_int("SKM_CHAIN_PRIO", 0));
+    if (nlong) {
+        // dynamic LDS reserves most of a CU's LDS for each long chain, so no group-by workgroup
+        // shares its CU (the chain is issue-latency bound: one wave pair, one instruction at a time)
+        static const uint32_t lds = (uint32_t)env_int("SKM_CHAIN_LDS_KB", 0) * 1024u;
+        static bool attr = false;
+        if (lds > 65536 && !attr) {
+            SKM_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_chain_long),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            attr = true;
+        }
+        hipLaunchKernelGGL(k_chain_long, dim3((uint32_t)nlong), dim3(128), lds, st, cs.sorted.as<Job>(), nlong, lens,
+                           recs32, tmp32, big32, out, env_int("SKM_CHAIN_PRIO", 0));
+    }
     if (nj > nlong) {
         const uint64_t threads = ceil_div(nj - nlong, 64) * 128;
         hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, st,
@@ -3389,7 +3475,7 @@ int skm_build_debug_jobs(skm_build* b, uint32_t* out, int cap) {
 }
 
 // Diagnostics: time k_chains on `njobs` synthetic jobs of length n (lengths 300 +- 60).
-int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms) {
+int skm_debug_chain_bench(uint32_t n, uint32_t njobs, int mode, float* ms) {
     SKM_API_BEGIN
     SKM_CHECK(ms && n && njobs, SKM_E_ARG, "bad argument");
     std::vector<uint32_t> lens((size_t)n * njobs);
@@ -3403,7 +3489,7 @@ int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms) {
     DevBuf dl, dj, dout;
     dl.ensure(4 * lens.size());
     dj.ensure(sizeof(Job) * njobs);
-    dout.ensure(sizeof(skm_stored_kmer_data) * njobs);
+    dout.ensure(std::max(sizeof(skm_stored_kmer_data), sizeof(double)) * njobs);
     SKM_HIP(hipMemcpy(dl.p, lens.data(), 4 * lens.size(), hipMemcpyHostToDevice));
     SKM_HIP(hipMemcpy(dj.p, jobs.data(), sizeof(Job) * njobs, hipMemcpyHostToDevice));
     hipEvent_t e0, e1;
@@ -3412,7 +3498,10 @@ int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms) {
     const uint64_t threads = ceil_div(njobs, 64) * 128;
     for (int it = 0; it < 2; ++it) {
         SKM_HIP(hipEventRecord(e0, 0));
-        if (n >= (1u << LONG_CLASS))
+        if (mode == 3 || mode == 4)
+            hipLaunchKernelGGL(k_chain_long_half, dim3(njobs), dim3(64), 0, 0, dj.as<Job>(), dl.as<uint32_t>(),
+                               mode - 3, reinterpret_cast<double*>(dout.p));
+        else if (mode == 2 || (mode == 0 && n >= (1u << LONG_CLASS)))
             hipLaunchKernelGGL(k_chain_long, dim3(njobs), dim3(128), 0, 0, dj.as<Job>(), (uint64_t)njobs,
                                dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(),
                                dout.as<skm_stored_kmer_data>(), 0);
@@ -3426,6 +3515,23 @@ int skm_debug_chain_bench(uint32_t n, uint32_t njobs, float* ms) {
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    SKM_API_END
+}
+
+// Diagnostics: one chain through the per-lane (mode 1) or wave-pair (mode 2) code, raw results.
+int skm_debug_chain_eval(const uint32_t* samples, uint32_t n, int mode, double* median, double* var) {
+    SKM_API_BEGIN
+    SKM_CHECK(samples && n && median && var && (mode == 1 || mode == 2), SKM_E_ARG, "bad argument");
+    DevBuf dx, dout;
+    dx.ensure(4ull * n);
+    dout.ensure(16);
+    SKM_HIP(hipMemcpy(dx.p, samples, 4ull * n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_chain_eval, dim3(1), dim3(128), 0, 0, dx.as<uint32_t>(), n, mode, dout.as<double>());
+    SKM_HIP(hipGetLastError());
+    double r[2];
+    SKM_HIP(hipMemcpy(r, dout.p, 16, hipMemcpyDeviceToHost));
+    *median = r[0];
+    *var = r[1];
     SKM_API_END
 }
 
