@@ -862,26 +862,29 @@ __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, ui
                                                 const uint32_t* __restrict__ lens, const uint32_t* __restrict__ recs32,
                                                 const uint32_t* __restrict__ tmp32, const uint32_t* __restrict__ big32,
                                                 skm_stored_kmer_data* __restrict__ out) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t wave = t >> 6;
-    const uint64_t j = (wave >> 1) * 64 + (t & 63u);
-    const bool var_wave = (wave & 1u) != 0;
-    if (j >= njobs) return;
-    const Job jb = jobs[j];
-    const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
-    const uint32_t* x = (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
-                        (jb.lens_off & LENS_OFF_MASK);
-    const uint32_t n = jb.n;
-    SigStats st;
-    st.init();
-    if (var_wave)
-        chain_run<true>(st, x, n);
-    else
-        chain_run<false>(st, x, n);
-    if (var_wave)
-        out[jb.out_idx].var = d2u16(st.var);
-    else
-        out[jb.out_idx].median = d2u16(st.h[2]);
+    // wave pairs walk blocks of 64 jobs (grid may be smaller than the job count: a capped grid
+    // keeps few waves resident beside a concurrent kernel, longest jobs first)
+    const bool var_wave = ((threadIdx.x >> 6) & 1u) != 0;
+    const uint64_t pairs = (uint64_t)gridDim.x * (blockDim.x >> 7);
+    for (uint64_t pr = (uint64_t)blockIdx.x * (blockDim.x >> 7) + (threadIdx.x >> 7); pr * 64 < njobs; pr += pairs) {
+        const uint64_t j = pr * 64 + (threadIdx.x & 63u);
+        if (j >= njobs) break;
+        const Job jb = jobs[j];
+        const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
+        const uint32_t* x = (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
+                            (jb.lens_off & LENS_OFF_MASK);
+        const uint32_t n = jb.n;
+        SigStats st;
+        st.init();
+        if (var_wave)
+            chain_run<true>(st, x, n);
+        else
+            chain_run<false>(st, x, n);
+        if (var_wave)
+            out[jb.out_idx].var = d2u16(st.var);
+        else
+            out[jb.out_idx].median = d2u16(st.h[2]);
+    }
 }
 
 // Diagnostics: one half of the wave-pair chain code alone (which 0: P^2, 1: variance).
@@ -1350,6 +1353,7 @@ struct BucketArgs {
     unsigned long long* stamps;   // optional [32] per-phase cycle sums (diagnostics)
     uint64_t* big_desc;        // [big_cap][2] groups of > 64 members handed to k_big_groups
     uint32_t big_cap;
+    int prio;                  // wave issue priority of the group-by (above the concurrent chains)
 };
 
 #define SKM_STAMP(i)                                                          \
@@ -1810,6 +1814,9 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     const uint64_t n = r1 - r0;
     if (n == 0) return;
     const uint64_t hprefix = (uint64_t)(A.bucket_base + bucket) << A.rem_bits;
+    if (A.prio == 1) __builtin_amdgcn_s_setprio(1);
+    if (A.prio == 2) __builtin_amdgcn_s_setprio(2);
+    if (A.prio >= 3) __builtin_amdgcn_s_setprio(3);
 
     // a bucket that fits LDS is one batch straight from recs; otherwise the sub-buckets of the
     // partition pass (k_partition) in tmp: consecutive sub-buckets are contiguous and hold
@@ -2161,24 +2168,37 @@ __global__ __launch_bounds__(BP_THREADS, 2) void k_partition(BucketArgs A) {
     __syncthreads();
     // staged scatter: each round sorts PT_ROUND elements by sub-bucket in LDS, then writes each
     // sub-bucket's run contiguously (whole lines instead of scattered 8-byte stores)
+    // the next round's elements are loaded into registers before this round's LDS work, so the
+    // HBM latency overlaps the staging instead of opening every round
     constexpr uint32_t PER = PT_ROUND / BP_THREADS;
     for (uint32_t p = 0; p < nseg; ++p) {
         uint64_t base, len;
         seg(p, base, len);
+        uint64_t nh[PER], nl[PER];
+#pragma unroll
+        for (uint32_t u = 0; u < PER; ++u) {
+            const uint64_t j = threadIdx.x + (uint64_t)u * BP_THREADS;
+            if (j < len) {
+                nh[u] = A.recs_hi[base + j];
+                nl[u] = A.recs_lo[base + j];
+            }
+        }
         for (uint64_t rb = 0; rb < len; rb += PT_ROUND) {
             for (uint32_t d = threadIdx.x; d < nsub; d += blockDim.x) s_rc[d] = 0;
-            __syncthreads();
             uint64_t eh[PER], el[PER];
             uint32_t sb[PER], rk[PER];
 #pragma unroll
             for (uint32_t u = 0; u < PER; ++u) {
-                const uint64_t j = rb + threadIdx.x + (uint64_t)u * BP_THREADS;
+                eh[u] = nh[u];
+                el[u] = nl[u];
                 sb[u] = 0xFFFFFFFFu;
+                const uint64_t j = rb + PT_ROUND + threadIdx.x + (uint64_t)u * BP_THREADS;
                 if (j < len) {
-                    eh[u] = A.recs_hi[base + j];
-                    el[u] = A.recs_lo[base + j];
+                    nh[u] = A.recs_hi[base + j];
+                    nl[u] = A.recs_lo[base + j];
                 }
             }
+            __syncthreads();
 #pragma unroll
             for (uint32_t u = 0; u < PER; ++u) {
                 const uint64_t j = rb + threadIdx.x + (uint64_t)u * BP_THREADS;
@@ -2251,12 +2271,20 @@ struct OvfScratch {
 
 // Overflow sub-buckets (n > CAP): global-memory bitonic sort (LDS for strides < CAP), then the
 // same group processing on the global arrays.
-__global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratch S) {
+// Chains of at least inline_min samples (the heaviest k-mers, the longest serial work of the whole
+// build) run inside k_overflow as soon as their sub-bucket is grouped -- the host orders the
+// overflow sub-buckets largest first -- instead of waiting for the whole overflow pass.
+constexpr uint32_t OVF_INLINE_CAP = 32;   // inline chains per workgroup (more: ordinary jobs)
+
+__global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratch S, uint32_t inline_min, int prio) {
     __shared__ uint64_t s_hi[CAP];
     __shared__ uint64_t s_lo[CAP];
     __shared__ __align__(16) uint32_t s_wave[48];
     __shared__ uint32_t s_nbig;
     __shared__ uint32_t s_big[BP_THREADS];
+    __shared__ uint32_t s_ninl;
+    __shared__ uint64_t s_inl[OVF_INLINE_CAP][2];  // lens offset, n << 32 | output index
+    if (threadIdx.x == 0) s_ninl = 0;
     const OvfEntry e = A.ovf[blockIdx.x];
     const uint64_t* src_hi = (e.src ? A.tmp_hi : A.recs_hi) + e.off;
     const uint64_t* src_lo = (e.src ? A.tmp_lo : A.recs_lo) + e.off;
@@ -2390,9 +2418,13 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
         const bool kept = (H >> 63) != 0;
         const uint64_t jb = kept ? jobinfo[a] : 0ull;
         const uint32_t jn = (uint32_t)(jb & 0xFFFFFFFFu);
+        // an inline chain takes a slot of s_inl now (no job); without a free slot it is a job
+        uint32_t islot = OVF_INLINE_CAP;
+        if (jn >= inline_min) islot = atomicAdd(&s_ninl, 1u);
+        const bool inl = islot < OVF_INLINE_CAP;
         uint32_t K, J, Lt;
         const uint32_t kpos = wg_exclusive_scan(kept ? 1u : 0u, s_wave, K);
-        const uint32_t jpos = wg_exclusive_scan(jn ? 1u : 0u, s_wave, J);
+        const uint32_t jpos = wg_exclusive_scan((jn && !inl) ? 1u : 0u, s_wave, J);
         const uint32_t lpos = wg_exclusive_scan(jn, s_wave, Lt);
         if (K == 0) continue;
         if (tid == 0) {
@@ -2414,7 +2446,12 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
                 jbr.lens_off = s_base[2] + lpos;
                 jbr.n = jn;
                 jbr.out_idx = (uint32_t)o;
-                A.jobs[s_base[1] + jpos] = jbr;
+                if (inl) {
+                    s_inl[islot][0] = jbr.lens_off;
+                    s_inl[islot][1] = ((uint64_t)jn << 32) | (uint32_t)o;
+                } else {
+                    A.jobs[s_base[1] + jpos] = jbr;
+                }
                 if (jn <= 64) {
                     const uint64_t start = jb >> 32;
                     for (uint32_t t = 0; t < jn; ++t)
@@ -2441,6 +2478,27 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
             for (uint32_t t = tid; t < nq; t += nt) A.lens[loff + t] = A.glen[glo[start + nq - 1 - t] >> 36];
         }
         __syncthreads();
+    }
+    // inline chains: a wave pair each (P^2 on the even wave, variance on the odd), raised issue
+    // priority -- they are the critical path of the overflow stream
+    __threadfence_block();
+    __syncthreads();
+    const uint32_t ninl = min(s_ninl, OVF_INLINE_CAP);
+    const uint32_t wave = tid >> 6, pairs = (nt >> 6) / 2;
+    if (ninl && prio == 1) __builtin_amdgcn_s_setprio(1);
+    if (ninl && prio == 2) __builtin_amdgcn_s_setprio(2);
+    if (ninl && prio >= 3) __builtin_amdgcn_s_setprio(3);
+    for (uint32_t q = wave / 2; q < ninl; q += pairs) {
+        const uint64_t off = s_inl[q][0], w = s_inl[q][1];
+        const uint32_t cn = (uint32_t)(w >> 32), o = (uint32_t)w;
+        const uint32_t* x = A.lens + off;
+        if ((wave & 1u) == 0) {
+            const double med = chain_long_p2(x, cn);
+            if ((tid & 63u) == 0) A.out_data[o].median = d2u16(med);
+        } else {
+            const double v = chain_long_var(x, cn);
+            if ((tid & 63u) == 0) A.out_data[o].var = d2u16(v);
+        }
     }
 }
 
@@ -2564,16 +2622,16 @@ struct skm_build {
     std::vector<skm_build*> group;
 
     // second stream: overflow sub-buckets + their chains, concurrent with the group-by
-    hipStream_t stream2 = nullptr;
-    hipEvent_t ev_part = nullptr, ev_o[3] = {};
-    DevBuf d_sub_tab, d_jobs2;
+    hipStream_t stream2 = nullptr, stream3 = nullptr;
+    hipEvent_t ev_part = nullptr, ev_o[3] = {}, ev_o3[3] = {};
+    DevBuf d_sub_tab, d_jobs2, d_jobs3;
 
     // pinned host staging for the pipeline's small readbacks
-    unsigned long long* h_pin = nullptr;   // [32] counters
+    unsigned long long* h_pin = nullptr;   // [64] counters
     OvfEntry* h_ovf = nullptr;
     size_t h_ovf_cap = 0;
     unsigned long long* pinned_ctr() {
-        if (!h_pin) SKM_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_pin), 32 * 8, hipHostMallocDefault));
+        if (!h_pin) SKM_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_pin), 64 * 8, hipHostMallocDefault));
         return h_pin;
     }
     OvfEntry* pinned_ovf(size_t n) {
@@ -2587,7 +2645,8 @@ struct skm_build {
     }
 
     uint64_t jobs2_cap = 0;
-    ChainSet cs_main, cs_ovf;
+    ChainSet cs_main, cs_ovf, cs_ovf3;
+    uint32_t n_ovf_heavy = 0;
 };
 
 namespace {
@@ -2794,7 +2853,7 @@ void prepare_local(skm_build* b) {
     const uint64_t W = b->n_windows;
     b->d_recs_hi.ensure(8 * std::max<uint64_t>(W, 1));
     b->d_recs_lo.ensure(8 * std::max<uint64_t>(W, 1));
-    b->d_ctr.ensure(128);
+    b->d_ctr.ensure(256);
     b->d_dfunc.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
     b->d_swf.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
 }
@@ -3045,7 +3104,8 @@ int env_int(const char* name, int dflt) {
 // job sort by length class (longest first) + the chain kernel, on stream st
 void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, const uint32_t* lens,
                    const uint32_t* recs32, const uint32_t* tmp32, const uint32_t* big32, skm_stored_kmer_data* out,
-                   uint32_t long_class, unsigned long long* pin) {
+                   uint32_t long_class, unsigned long long* pin, hipStream_t st_short = nullptr,
+                   hipEvent_t ev_sorted = nullptr, uint32_t max_wgs = 0) {
     if (!nj) return;
     const uint32_t nwg = (uint32_t)std::min<uint64_t>(1024, ceil_div(nj, 4096));
     const uint64_t chunk = ceil_div(nj, nwg);
@@ -3056,6 +3116,7 @@ void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, c
     hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(64), 0, st, cs.hist.as<uint32_t>(), nwg, cs.offs.as<uint64_t>(), long_class);
     hipLaunchKernelGGL(k_job_scatter, dim3(nwg), dim3(JOB_WG), 0, st, jobs, nj, chunk, cs.offs.as<uint64_t>(),
                        cs.sorted.as<Job>());
+    if (st_short && ev_sorted) SKM_HIP(hipEventRecord(ev_sorted, st));  // sorted jobs ready
     SKM_HIP(hipMemcpyAsync(pin, cs.offs.as<uint64_t>() + (uint64_t)nwg * JOB_CLASSES, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
     const uint64_t nlong = *pin;
@@ -3073,8 +3134,16 @@ void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, c
                            recs32, tmp32, big32, out, env_int("SKM_CHAIN_PRIO", 0));
     }
     if (nj > nlong) {
+        // the per-lane chains on their own stream (when given): they do not wait for the long ones
+        hipStream_t ss = st;
+        if (st_short && ev_sorted) {
+            SKM_HIP(hipStreamWaitEvent(st_short, ev_sorted, 0));
+            ss = st_short;
+        }
         const uint64_t threads = ceil_div(nj - nlong, 64) * 128;
-        hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, st,
+        uint64_t wgs = ceil_div(threads, 256);
+        if (max_wgs) wgs = std::min<uint64_t>(wgs, max_wgs);
+        hipLaunchKernelGGL(k_chains, dim3((uint32_t)wgs), dim3(256), 0, ss,
                            cs.sorted.as<Job>() + nlong, nj - nlong, lens, recs32, tmp32, big32, out);
     }
     SKM_HIP(hipGetLastError());
@@ -3095,7 +3164,7 @@ void phase_group(skm_build* b) {
     const bool multi = b->world > 1;
     const uint32_t NB1 = 1u << b->b1_bits;
     SKM_HIP(hipEventRecord(b->ev[4], st));
-    SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 128, st));
+    SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 256, st));
     SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->n_total ? b->n_total : 1, st));
     unsigned long long* ctr_d = b->d_ctr.as<unsigned long long>();
     BucketArgs A;
@@ -3123,6 +3192,7 @@ void phase_group(skm_build* b) {
     A.lens = b->d_lens.as<uint32_t>();
     A.ovf = b->d_ovf.as<OvfEntry>();
     A.ovf_cap = (uint32_t)b->ovf_cap;
+    A.prio = env_int("SKM_BUCKET_PRIO", 0);
     A.stamps = nullptr;
     if (b->stamps) {
         b->d_stamps.ensure(32 * 8);
@@ -3144,13 +3214,20 @@ void phase_group(skm_build* b) {
     const uint32_t novf = (uint32_t)(ctr[1] & 0xFFFFFFFFull);
     SKM_CHECK(novf <= b->ovf_cap, SKM_E_OOM, "overflow list capacity exceeded");
     b->n_overflow = novf;
-    // ---- 5. overflow sub-buckets on the second stream ----
-    BucketArgs A2 = A;
+    // ---- 5. overflow sub-buckets (> CAP elements), largest first, concurrent with the group-by:
+    //      the heavy ones (>= SKM_OVF_HEAVY elements: they alone can hold the longest P^2 chains)
+    //      on stream 2, whose chains start as soon as they are grouped; the rest on stream 3 ----
+    hipStream_t st3 = b->stream3;
+    BucketArgs A2 = A, A3 = A;
+    OvfScratch S;
     uint64_t ovf_elems = 0;
+    uint32_t nheavy = 0;
     if (novf) {
         OvfEntry* ov = b->pinned_ovf(novf);
         SKM_HIP(hipMemcpyAsync(ov, b->d_ovf.p, sizeof(OvfEntry) * novf, hipMemcpyDeviceToHost, st));
         SKM_HIP(hipStreamSynchronize(st));
+        std::sort(ov, ov + novf, [](const OvfEntry& x, const OvfEntry& y) { return x.n > y.n; });
+        const uint32_t heavy_min = (uint32_t)env_int("SKM_OVF_HEAVY", 8192);
         uint64_t tot = 0;
         for (uint32_t q = 0; q < novf; ++q) {
             OvfEntry& e = ov[q];
@@ -3160,6 +3237,7 @@ void phase_group(skm_build* b) {
             e.scratch = tot;
             tot += np;
             ovf_elems += e.n;
+            if (e.n >= heavy_min) ++nheavy;
         }
         b->d_ovf_hi.ensure(tot * 8);
         b->d_ovf_lo.ensure(tot * 8);
@@ -3172,20 +3250,33 @@ void phase_group(skm_build* b) {
         SKM_HIP(hipMemcpyAsync(b->d_ovf.p, ov, sizeof(OvfEntry) * novf, hipMemcpyHostToDevice, st));
         SKM_HIP(hipEventRecord(b->ev_part, st));
         SKM_HIP(hipStreamWaitEvent(st2, b->ev_part, 0));
-        OvfScratch S;
+        SKM_HIP(hipStreamWaitEvent(st3, b->ev_part, 0));
         S.hi = b->d_ovf_hi.as<uint64_t>();
         S.lo = b->d_ovf_lo.as<uint64_t>();
         S.heads = b->d_ovf_heads.as<uint32_t>();
         S.jobinfo = b->d_ovf_job.as<uint64_t>();
         S.fmean = b->d_ovf_fm.as<uint32_t>();
-        A2.ctr = ctr_d + 8;  // own job / length counters; the kept counter stays shared
+        // both parts append to one job list (own job / length counters of the overflow; the kept
+        // counter stays shared); the chains start when both parts are grouped
+        A2.ctr = ctr_d + 8;
         A2.jobs = b->d_jobs2.as<Job>();
         A2.lens = b->d_lens.as<uint32_t>();
+        A3.ctr = A2.ctr;
+        A3.jobs = A2.jobs;
+        A3.lens = A2.lens;
+        A3.ovf = A2.ovf + nheavy;
+        const uint32_t inline_min = (uint32_t)env_int("SKM_OVF_INLINE_MIN", 0x7FFFFFFF);
+        const int prio = env_int("SKM_INLINE_PRIO", 3);
         SKM_HIP(hipEventRecord(b->ev_o[0], st2));
-        hipLaunchKernelGGL(k_overflow, dim3(novf), dim3(BP_THREADS), 0, st2, A2, S);
-        SKM_HIP(hipGetLastError());
+        if (nheavy)
+            hipLaunchKernelGGL(k_overflow, dim3(nheavy), dim3(BP_THREADS), 0, st2, A2, S, inline_min, prio);
         SKM_HIP(hipEventRecord(b->ev_o[1], st2));
+        SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
+        if (novf > nheavy)
+            hipLaunchKernelGGL(k_overflow, dim3(novf - nheavy), dim3(BP_THREADS), 0, st3, A3, S, inline_min, prio);
+        SKM_HIP(hipGetLastError());
     }
+    b->n_ovf_heavy = nheavy;
     T(2);
     // ---- 4b. group-by of the sub-buckets that fit LDS; groups of > 64 members are handed to
     //      k_big_groups (one wave each) and appended ----
@@ -3213,22 +3304,26 @@ void phase_group(skm_build* b) {
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[12], st));
     T(3);
-    // ---- 6. deferred P^2 / variance chains: the overflow's as soon as it is done ----
+    // ---- 6. deferred P^2 / variance chains: the overflow's as soon as both parts are grouped;
+    //      the long ones (a wave pair each) on stream 2, the per-lane ones on stream 3 ----
     b->n_jobs = b->n_lens = 0;
     b->ovf_kept = 0;
     if (!novf) b->ovf_elems = 0;
     if (novf) {
-        SKM_HIP(hipMemcpyAsync(ctr + 8, ctr_d + 8, 8 * 5, hipMemcpyDeviceToHost, st2));
+        SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
+        SKM_HIP(hipStreamWaitEvent(st2, b->ev_o3[0], 0));
+        SKM_HIP(hipMemcpyAsync(ctr + 32, ctr_d + 8, 8 * 5, hipMemcpyDeviceToHost, st2));
         SKM_HIP(hipStreamSynchronize(st2));
-        SKM_CHECK(ctr[8 + 3] <= b->jobs2_cap && ctr[8 + 4] <= b->lens_cap, SKM_E_OOM, "overflow chain buffers overflowed");
-        // the overflow holds the longest chains: per-lane below 32768 samples (fewer waves beside
-        // the group-by), a wave pair each from there (latency-bound, grows with the world size)
-        launch_chains(st2, A2.jobs, ctr[8 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, nullptr, A.out_data,
-                      (uint32_t)env_int("SKM_OVF_LONG_CLASS", 15), ctr + 21);
+        SKM_CHECK(ctr[32 + 3] <= b->jobs2_cap && ctr[32 + 4] <= b->lens_cap, SKM_E_OOM,
+                  "overflow chain buffers overflowed");
+        launch_chains(st2, A2.jobs, ctr[32 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, nullptr, A.out_data,
+                      (uint32_t)env_int("SKM_OVF_LONG_CLASS", 14), ctr + 21, st3, b->ev_o3[2],
+                      (uint32_t)env_int("SKM_OVF_CHAIN_WGS", 0));
         SKM_HIP(hipEventRecord(b->ev_o[2], st2));
-        b->n_jobs += ctr[8 + 3];
-        b->ovf_kept = ctr[8 + 0];
-        b->n_lens += ctr[8 + 4];
+        SKM_HIP(hipEventRecord(b->ev_o3[1], st3));
+        b->n_jobs += ctr[32 + 3];
+        b->ovf_kept = ctr[32 + 0];
+        b->n_lens += ctr[32 + 4];
     }
     T(4);
     SKM_HIP(hipMemcpyAsync(ctr, ctr_d, 8 * 7, hipMemcpyDeviceToHost, st));
@@ -3240,7 +3335,10 @@ void phase_group(skm_build* b) {
     launch_chains(st, A.jobs, ctr[3], b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
                   reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, LONG_CLASS, ctr + 20);
     b->n_jobs += ctr[3];
-    if (novf) SKM_HIP(hipStreamWaitEvent(st, b->ev_o[2], 0));
+    if (novf) {
+        SKM_HIP(hipStreamWaitEvent(st, b->ev_o[2], 0));
+        SKM_HIP(hipStreamWaitEvent(st, b->ev_o3[1], 0));
+    }
     SKM_HIP(hipEventRecord(b->ev[6], st));
     SKM_HIP(hipEventRecord(b->ev[7], st));
     T(5);
@@ -3278,7 +3376,12 @@ void phase_final(skm_build* b) {
     const int from[7] = {0, 1, 2, 4, 5, 12, 7}, to[7] = {1, 2, 3, 12, 6, 6, 8};
     for (int i = 0; i < 7; ++i) SKM_HIP(hipEventElapsedTime(&b->last_ms[i], b->ev[from[i]], b->ev[to[i]]));
     b->last_ms[4] = 0.f;
-    if (b->n_overflow) SKM_HIP(hipEventElapsedTime(&b->last_ms[4], b->ev_o[0], b->ev_o[1]));
+    if (b->n_overflow) {  // the overflow path end to end (both parts, their chains included)
+        float t2 = 0.f, t3 = 0.f;
+        SKM_HIP(hipEventElapsedTime(&t2, b->ev_o[0], b->ev_o[2]));
+        SKM_HIP(hipEventElapsedTime(&t3, b->ev_o[0], b->ev_o3[1]));
+        b->last_ms[4] = std::max(t2, t3);
+    }
     SKM_HIP(hipEventElapsedTime(&b->last_ms[7], b->ev[0], b->ev[8]));
     SKM_HIP(hipEventElapsedTime(&b->last_ms[8], b->ev[3], b->ev[4]));
     SKM_HIP(hipEventElapsedTime(&b->last_ms[9], b->ev[4], b->ev[10]));   // level-2 partition kernel
@@ -3335,9 +3438,11 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     SKM_HIP(hipSetDevice(b->device));
     SKM_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
     SKM_HIP(hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking));
+    SKM_HIP(hipStreamCreateWithFlags(&b->stream3, hipStreamNonBlocking));
     for (auto& e : b->ev) SKM_HIP(hipEventCreate(&e));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_part, hipEventDisableTiming));
     for (auto& e : b->ev_o) SKM_HIP(hipEventCreate(&e));
+    for (auto& e : b->ev_o3) SKM_HIP(hipEventCreate(&e));
     set_geometry(b);
     *out = b;
     SKM_API_END
@@ -3710,15 +3815,19 @@ void skm_build_destroy(skm_build* b) {
     for (auto* x : b->group)  // leave the other members usable on their own
         if (x != b) x->group.clear();
     if (b->stream2) (void)hipStreamSynchronize(b->stream2);
+    if (b->stream3) (void)hipStreamSynchronize(b->stream3);
     for (auto& e : b->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : b->ev_o)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : b->ev_o3)
         if (e) (void)hipEventDestroy(e);
     if (b->ev_part) (void)hipEventDestroy(b->ev_part);
     if (b->h_pin) (void)hipHostFree(b->h_pin);
     if (b->h_ovf) (void)hipHostFree(b->h_ovf);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     if (b->stream2) (void)hipStreamDestroy(b->stream2);
+    if (b->stream3) (void)hipStreamDestroy(b->stream3);
     delete b;
 }
 

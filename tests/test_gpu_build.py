@@ -71,6 +71,17 @@ def test_level2_partition_and_overflow(skm, gpu):
     assert_same(got, ref)
 
 
+@pytest.mark.parametrize("inline_min", ["16", "1000000000"])
+def test_overflow_inline_chains(skm, gpu, monkeypatch, inline_min):
+    # every overflow chain of >= 16 samples inline in k_overflow (wave-pair chain code, up to
+    # OVF_INLINE_CAP per workgroup, the rest as jobs) -- and none inline
+    monkeypatch.setenv("SKM_OVF_INLINE_MIN", inline_min)
+    p = synth.generate_arrays(60000, 60, per_file=2000, seed=4)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    got, ref = run_both(skm, r, o, l, f, i, len(funcs))
+    assert_same(got, ref)
+
+
 def test_edge_cases(skm, gpu):
     seqs = [
         b"",                       # empty

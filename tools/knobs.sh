@@ -2,7 +2,7 @@
 # run the probe under several knob settings; prints the timings of each
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
-CFGS=${CFGS:-"SKM_OVF_LONG_CLASS=15|SKM_OVF_LONG_CLASS=14|SKM_OVF_LONG_CLASS=13|SKM_OVF_LONG_CLASS=12"}
+CFGS=${CFGS:-"SKM_OVF_HEAVY=8192"}
 IFS='|' read -ra ARR <<< "$CFGS"
 for cfg in "${ARR[@]}"; do
   echo "== $cfg"
