@@ -114,13 +114,15 @@ def main():
     n_kept = ctrs["kept"]                       # kept k-mers this rank owns
     # dominant single kernel: k_bucket_process (group-by + cut + statistics of every sub-bucket
     # that fits LDS).  Its algorithmic bytes: the 16-byte elements it reads once, the 18 bytes per
-    # k-mer it keeps; the overflow sub-buckets belong to k_overflow and are excluded.
+    # k-mer it keeps; the overflow sub-buckets (k_overflow) and the k-mers of groups of > 64
+    # members (kept by k_big_groups) are excluded.
     kernels = {"k_extract<false>": "extract_count", "k_partition": "partition", "k_bucket_process": "bucket_kernel"}
     dom = max(kernels, key=lambda k: phase.get(kernels[k], 0.0))
     alg = {
         "k_extract<false>": res_bytes,
         "k_partition": 32 * grouped,  # 16-byte elements read once and written once
-        "k_bucket_process": 16 * (grouped - ctrs["overflow_elements"]) + 18 * (n_kept - ctrs["overflow_kept"]),
+        "k_bucket_process": 16 * (grouped - ctrs["overflow_elements"])
+        + 18 * (n_kept - ctrs["overflow_kept"] - ctrs["big_kept"]),
     }
     dom_ms = phase[kernels[dom]]
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
