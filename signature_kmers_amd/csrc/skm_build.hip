@@ -1706,7 +1706,8 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     __syncthreads();
     SKM_STAMP(11);
     {   // groups of more than 64 members: members (func << 48 | ordinal) into the group's own
-        // consumed slots, one descriptor each; k_big_groups resolves them register-resident
+        // consumed slots (protein length beside it), one descriptor each; k_big_groups resolves
+        // them register-resident
         const uint32_t nbig = cstart[7] - cstart[6];
         const uint64_t bbase = *reinterpret_cast<const unsigned long long*>(L.wave + 44);
         const uint32_t wave = tid >> 6, nwaves = nt >> 6, lane = tid & 63u;
@@ -1716,9 +1717,12 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
             const uint32_t rep = L.glist[g];
             const uint32_t a = L.goff[rep];
             const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
+            uint64_t* slots_lo = const_cast<uint64_t*>(src_lo);
             for (uint32_t t = lane; t < c; t += 64) {
                 const uint32_t j = L.order[a + t];
-                slots[a + t] = ((L.hi[j] & 0xFFFFull) << 48) | (L.lo[j] >> 16);
+                const uint64_t hj = L.hi[j], lj = L.lo[j];
+                slots[a + t] = ((hj & 0xFFFFull) << 48) | (lj >> 16);
+                slots_lo[a + t] = elem_len(hj, lj, A.glen);  // no per-member gathers downstream
             }
             const uint64_t q = bbase + bi;
             if (lane == 0 && q < A.big_cap) {
@@ -1887,7 +1891,8 @@ struct BigArgs {
     uint32_t cap;
     const uint64_t* recs_hi;
     const uint64_t* tmp_hi;
-    const uint32_t* glen;
+    const uint64_t* recs_lo;   // lo slots: the members' protein lengths
+    const uint64_t* tmp_lo;
     uint8_t* flags;
     BigOut* out;
 };
@@ -1910,11 +1915,11 @@ __device__ __forceinline__ void bitonic_cross(uint64_t (&ky)[E], bool take_min) 
 }
 
 template <int E>
-__device__ __forceinline__ void big_group(const BigArgs& B, uint64_t g, uint64_t* mem, uint32_t c, uint64_t h43,
-                                          uint64_t lens_off) {
+__device__ __forceinline__ void big_group(const BigArgs& B, uint64_t g, uint64_t* mem, const uint64_t* mlen,
+                                          uint32_t c, uint64_t h43, uint64_t lens_off) {
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t fo[E];  // func << 16 | offset (padding: 0xFFFFFFFF)
-    uint64_t ky[E];  // ordinal (s << 20 | i) << 16
+    uint64_t ky[E];  // ordinal (s << 20 | i) << 16 | member index
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t t = lane * E + (uint32_t)e;
@@ -1922,10 +1927,10 @@ __device__ __forceinline__ void big_group(const BigArgs& B, uint64_t g, uint64_t
         ky[e] = ~0ull;
         if (t < c) {
             const uint64_t v = mem[t];
-            const uint32_t s = (uint32_t)(v >> ELEM_I_BITS) & ((1u << ELEM_S_BITS) - 1u);
+            const uint32_t len = (uint32_t)mlen[t];
             const uint32_t i = (uint32_t)v & ((1u << ELEM_I_BITS) - 1u);
-            fo[e] = ((uint32_t)(v >> 48) << 16) | ((B.glen[s] - i) & 0xFFFFu);
-            ky[e] = v << 16;
+            fo[e] = ((uint32_t)(v >> 48) << 16) | ((len - i) & 0xFFFFu);
+            ky[e] = (v << 16) | t;
         }
     }
     // majority candidate (a function with >= 80 % of the members is the strict majority)
@@ -1964,9 +1969,8 @@ __device__ __forceinline__ void big_group(const BigArgs& B, uint64_t g, uint64_t
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         if (fo[e] != 0xFFFFFFFFu) {
-            const uint32_t s = (uint32_t)(ky[e] >> (16 + ELEM_I_BITS));
-            B.flags[s] = 1;
-            if (p[e]) sum += B.glen[s];
+            B.flags[(uint32_t)(ky[e] >> (16 + ELEM_I_BITS))] = 1;
+            if (p[e]) sum += (uint32_t)mlen[ky[e] & 0xFFFFu];  // L2-warm (read above)
         }
         if (!p[e]) ky[e] = ~0ull;  // sort key: best-function members only
     }
@@ -2026,7 +2030,7 @@ __device__ __forceinline__ void big_group(const BigArgs& B, uint64_t g, uint64_t
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const uint32_t t = lane * E + (uint32_t)e;
-        if (t < nb) lens[nb - 1 - t] = B.glen[(uint32_t)(ky[e] >> (16 + ELEM_I_BITS))];
+        if (t < nb) lens[nb - 1 - t] = (uint32_t)mlen[ky[e] & 0xFFFFu];
     }
     o.n = nb;
     o.avg = (uint16_t)pre;
@@ -2050,13 +2054,14 @@ __global__ __launch_bounds__(BIG_WG, LARGE ? 1 : 2) void k_big_groups(BigArgs B)
         const uint64_t h43 = d0 & KEY_MASK;
         const uint64_t sel = d1 >> LENS_SEL_SHIFT, off = d1 & LENS_OFF_MASK;
         uint64_t* mem = const_cast<uint64_t*>(sel == LENS_IN_RECS ? B.recs_hi : B.tmp_hi) + off / 2;
+        const uint64_t* mlen = (sel == LENS_IN_RECS ? B.recs_lo : B.tmp_lo) + off / 2;
         if constexpr (LARGE) {
-            big_group<32>(B, g, mem, c, h43, d1);
+            big_group<32>(B, g, mem, mlen, c, h43, d1);
         } else {
-            if (c <= 128u) big_group<2>(B, g, mem, c, h43, d1);
-            else if (c <= 256u) big_group<4>(B, g, mem, c, h43, d1);
-            else if (c <= 512u) big_group<8>(B, g, mem, c, h43, d1);
-            else big_group<16>(B, g, mem, c, h43, d1);
+            if (c <= 128u) big_group<2>(B, g, mem, mlen, c, h43, d1);
+            else if (c <= 256u) big_group<4>(B, g, mem, mlen, c, h43, d1);
+            else if (c <= 512u) big_group<8>(B, g, mem, mlen, c, h43, d1);
+            else big_group<16>(B, g, mem, mlen, c, h43, d1);
         }
     }
 }
@@ -3291,7 +3296,8 @@ void phase_group(skm_build* b) {
     BA.cap = A.big_cap;
     BA.recs_hi = A.recs_hi;
     BA.tmp_hi = A.tmp_hi;
-    BA.glen = A.glen;
+    BA.recs_lo = A.recs_lo;
+    BA.tmp_lo = A.tmp_lo;
     BA.flags = A.flags;
     BA.out = b->d_big_out.as<BigOut>();
     SKM_HIP(hipEventRecord(b->ev[11], st));
