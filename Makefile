@@ -12,10 +12,12 @@ HIP_SRCS = $(SRC)/skm_build.hip $(SRC)/skm_annotate.hip
 CPP_SRCS = $(SRC)/skm_host.cpp $(SRC)/skm_bdz.cpp
 OBJS     = $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(CPP_SRCS))
 LIB      = signature_kmers_amd/libskm.so
-TOOLS    = bin/kmers-build-signatures bin/kmers-call-functions bin/kmers-annotate-seqs
+TOOLS    = bin/kmers-build-signatures bin/kmers-call-functions bin/kmers-annotate-seqs bin/skm-front-probe
 ORACLE   = oracle/liboracle_skm.so
+FRONT    = $(OBJDIR)/front/skm_front.o $(OBJDIR)/front/skm_caller.o
+FRONTH   = $(wildcard $(SRC)/front/*.h) include/skm.h
 
-all: $(LIB) $(ORACLE)
+all: $(LIB) $(ORACLE) $(TOOLS)
 tools: $(TOOLS)
 
 $(OBJDIR)/%.o: $(SRC)/%.hip $(wildcard $(SRC)/*.h) include/skm.h
@@ -29,9 +31,15 @@ $(OBJDIR)/%.o: $(SRC)/%.cpp $(wildcard $(SRC)/*.h) include/skm.h
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
-bin/%: $(SRC)/tools/%.cpp $(LIB) $(wildcard $(SRC)/*.h)
+# host front end + CLIs: plain C++ over the C-ABI (no HIP in these translation units)
+$(OBJDIR)/front/%.o: $(SRC)/front/%.cpp $(FRONTH)
+	@mkdir -p $(OBJDIR)/front
+	$(CXX) -O2 -std=c++17 -Wall -Iinclude -I$(SRC)/front -c $< -o $@
+
+bin/%: $(SRC)/tools/%.cpp $(FRONT) $(LIB) $(FRONTH)
 	@mkdir -p bin
-	$(HIPCC) -O2 -std=c++17 -Iinclude -I$(SRC) $< -o $@ -L signature_kmers_amd -lskm -Wl,-rpath,'$$ORIGIN/../signature_kmers_amd'
+	$(CXX) -O2 -std=c++17 -Wall -Iinclude -I$(SRC)/front $< $(FRONT) -o $@ -L signature_kmers_amd -lskm -pthread \
+	  -Wl,-rpath,'$$ORIGIN/../signature_kmers_amd' -Wl,-rpath,/opt/rocm/lib
 
 $(ORACLE): oracle/skm_oracle.cpp
 	$(CXX) -O2 -fPIC -shared -std=c++17 -ffp-contract=off $< -o $@

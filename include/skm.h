@@ -166,7 +166,13 @@ typedef struct skm_db skm_db;
 int skm_db_open(skm_db** out, const char* mph_path, const char* dat_path, int device);
 int skm_db_open_mem(skm_db** out, const uint8_t* mph, size_t mph_len, const uint8_t* dat,
                     size_t dat_len, int device);
-/* cmph_size() (cmph_kmer.h:102) */
+/* Exact-key DB over the kept k-mers of a build: KeptKmerDB<K> (kept_kmer_db.h:9-31), used by the
+ * recall pass of kmers-build-signatures (kmers-build-signatures.cc:238-349).  A window hits only
+ * if its k-mer is one of keys (record data[i]); keys must be distinct and non-zero.  Laid out in
+ * HBM as an open-addressing table (load <= 1/2) + the 10-byte records.  skm_db_lookup returns
+ * the record index, or n for a miss.                                                          */
+int skm_db_open_kept(skm_db** out, const uint64_t* keys, const skm_stored_kmer_data* data, size_t n, int device);
+/* cmph_size() (cmph_kmer.h:102); for an exact DB the number of kept k-mers */
 int skm_db_size(skm_db* db, uint32_t* m);
 /* Batched cmph_search(hash, key, 8) (cmph_kmer.h:90-92); idx >= size is a miss. */
 int skm_db_lookup(skm_db* db, const uint64_t* keys, size_t n, uint32_t* idx_out);

@@ -540,8 +540,13 @@ void hitset_process(std::vector<Hit>& hits, double seqlen, uint16_t& current_fI,
 }  // namespace
 
 // One query sequence.  Returns the number of calls written (<= cap) or the needed count.
-int64_t oracle_process_aa_seq(const oracle_bdz* db, const oracle_stored* dat, const uint8_t* seq,
-                              uint32_t len, const oracle_annot_opts* opts, oracle_call* out, uint64_t cap) {
+}  // extern "C"
+
+// fetch(ptr) -> const oracle_stored* or nullptr: CmphKmerDb::fetch (idx >= size -> no callback,
+// cmph_kmer.h:139-147) or KeptKmerDB::fetch (exact key, kept_kmer_db.h:20-27).
+template <class Fetch>
+static int64_t process_aa_seq_impl(Fetch fetch, const uint8_t* seq, uint32_t len, const oracle_annot_opts* opts,
+                                   oracle_call* out, uint64_t cap) {
     const int N = 8;
     std::vector<Hit> hits;
     std::vector<oracle_call> calls;
@@ -564,9 +569,9 @@ int64_t oracle_process_aa_seq(const oracle_bdz* db, const oracle_stored* dat, co
             continue;
         }
         size_t offset = (size_t)(ptr - seq);
-        uint32_t idx = oracle_bdz_search(db, ptr, N);
-        if (idx < db->m) {  // CmphKmerDb::fetch: idx >= hash_size -> ec = 1, no callback
-            const oracle_stored& kdata = dat[idx];
+        const oracle_stored* kp = fetch(ptr);
+        if (kp) {
+            const oracle_stored& kdata = *kp;
             bool skip = opts->ignore_hypo && kdata.function_index == (uint16_t)opts->hypo_index &&
                         opts->hypo_index >= 0;
             if (!skip) {
@@ -590,6 +595,45 @@ int64_t oracle_process_aa_seq(const oracle_bdz* db, const oracle_stored* dat, co
     if ((int)hits.size() >= opts->min_hits) hitset_process(hits, seqlen, current_fI, calls, *opts);
     for (size_t i = 0; i < calls.size() && i < cap; ++i) out[i] = calls[i];
     return (int64_t)calls.size();
+}
+
+extern "C" {
+
+int64_t oracle_process_aa_seq(const oracle_bdz* db, const oracle_stored* dat, const uint8_t* seq,
+                              uint32_t len, const oracle_annot_opts* opts, oracle_call* out, uint64_t cap) {
+    auto fetch = [&](const uint8_t* k) -> const oracle_stored* {
+        uint32_t idx = oracle_bdz_search(db, k, 8);
+        return idx < db->m ? &dat[idx] : nullptr;
+    };
+    return process_aa_seq_impl(fetch, seq, len, opts, out, cap);
+}
+
+// Recall pass against the exact kept-k-mer DB (kmers-build-signatures.cc:238-349): keys sorted
+// ascending (as oracle_build returns them), data[i] the record of keys[i].
+int64_t oracle_annotate_exact(const uint64_t* keys, const oracle_stored* data, uint64_t nkeys, const uint8_t* residues,
+                              const uint64_t* seq_off, const uint32_t* seq_len, uint64_t n_seqs,
+                              const oracle_annot_opts* opts, uint64_t* call_off, oracle_call* calls, uint64_t cap) {
+    auto fetch = [&](const uint8_t* k) -> const oracle_stored* {
+        uint64_t key = load_key(k);
+        const uint64_t* it = std::lower_bound(keys, keys + nkeys, key);
+        return (it != keys + nkeys && *it == key) ? &data[it - keys] : nullptr;
+    };
+    uint64_t total = 0;
+    std::vector<oracle_call> tmp(1024);
+    for (uint64_t s = 0; s < n_seqs; ++s) {
+        call_off[s] = total;
+        int64_t n = process_aa_seq_impl(fetch, residues + seq_off[s], seq_len[s], opts, tmp.data(), tmp.size());
+        if ((uint64_t)n > tmp.size()) {
+            tmp.resize(n);
+            n = process_aa_seq_impl(fetch, residues + seq_off[s], seq_len[s], opts, tmp.data(), tmp.size());
+        }
+        for (int64_t i = 0; i < n; ++i) {
+            if (total < cap) calls[total] = tmp[i];
+            total++;
+        }
+    }
+    call_off[n_seqs] = total;
+    return total <= cap ? (int64_t)total : -1;
 }
 
 // Batch form: CSR output (call_off has n_seqs+1 entries).  Returns total calls or -1 if cap short.

@@ -82,6 +82,7 @@ _SIGS = {
     "skm_debug_div_check": (C.c_int, [C.c_uint64, C.c_uint32, C.POINTER(C.c_uint64)]),
     "skm_db_open": (C.c_int, [C.POINTER(_P), C.c_char_p, C.c_char_p, C.c_int]),
     "skm_db_open_mem": (C.c_int, [C.POINTER(_P), _P, C.c_size_t, _P, C.c_size_t, C.c_int]),
+    "skm_db_open_kept": (C.c_int, [C.POINTER(_P), _P, _P, C.c_size_t, C.c_int]),
     "skm_db_size": (C.c_int, [_P, C.POINTER(C.c_uint32)]),
     "skm_db_lookup": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "skm_db_close": (None, [_P]),
@@ -340,6 +341,19 @@ class CmphKmerDb:
             self.close()
         except Exception:
             pass
+
+
+class KeptKmerDb(CmphKmerDb):
+    """KeptKmerDB<8> (kept_kmer_db.h:9-31): exact-key DB over a build's kept k-mers, resident in HBM
+    (the recall pass's DB, kmers-build-signatures.cc:238).  lookup_keys returns the record index
+    of each key, len(keys) for a miss."""
+
+    def __init__(self, keys: np.ndarray, data: np.ndarray, device: int = 0):
+        self._h = C.c_void_p()
+        self.device = device
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        data = np.ascontiguousarray(data, dtype=STORED_DTYPE)
+        _check(lib().skm_db_open_kept(C.byref(self._h), _ptr(keys), _ptr(data), len(keys), device))
 
 
 def read_function_index(path: str) -> list:

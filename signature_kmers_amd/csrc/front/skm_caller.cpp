@@ -1,0 +1,138 @@
+// skm_caller.cpp -- see skm_caller.h.
+#include "skm_caller.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <fstream>
+#include <thread>
+
+namespace skmf {
+
+bool read_function_index(const std::string& path, std::vector<std::string>& table, std::string& err) {
+    std::ifstream f(path);
+    if (!f) {
+        err = "cannot read " + path;
+        return false;
+    }
+    std::vector<std::pair<int, std::string>> rows;
+    int max_id = 0;
+    std::string line;
+    while (std::getline(f, line, '\n')) {
+        size_t tab = line.find('\t');
+        int id = std::stoi(line.substr(0, tab));
+        std::string name;
+        if (tab != std::string::npos) {
+            size_t t2 = line.find('\t', tab + 1);
+            name = line.substr(tab + 1, t2 == std::string::npos ? std::string::npos : t2 - tab - 1);
+        }
+        max_id = std::max(max_id, id);
+        rows.emplace_back(id, name);
+    }
+    table.assign((size_t)max_id + 1, std::string());
+    for (auto& r : rows) table[(size_t)r.first] = r.second;
+    return true;
+}
+
+int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std::vector<std::string>& function_index,
+               bool ignore_hypo, int n_threads, std::vector<std::vector<SeqCall>>& out, std::string& err,
+               double* device_ms, uint64_t max_batch_residues) {
+    auto hit = std::find(function_index.begin(), function_index.end(), "hypothetical protein");
+    if (hit == function_index.end()) {  // process_aa_seq exits here (call_functions.tcc:269-274)
+        err = "Cannot find hypothetical protein index";
+        return SKM_E_ARG;
+    }
+    skm_annot_opts o{};
+    o.min_hits = 5;
+    o.max_gap = 200;
+    o.ignore_hypo = ignore_hypo ? 1 : 0;
+    o.hypo_index = (int32_t)(hit - function_index.begin());
+    o.mean_mode = 0;
+    o.mad_mode = 0;
+    std::vector<const char*> fidx(function_index.size());
+    for (size_t i = 0; i < function_index.size(); ++i) fidx[i] = function_index[i].c_str();
+
+    out.assign(files.size(), std::vector<SeqCall>());
+    for (size_t f = 0; f < files.size(); ++f) out[f].resize(files[f]->size());
+    if (device_ms) *device_ms = 0;
+
+    size_t f0 = 0;
+    while (f0 < files.size()) {
+        // one device batch: whole files up to max_batch_residues residues
+        size_t f1 = f0;
+        uint64_t nres = 0, nseq = 0;
+        while (f1 < files.size() && (f1 == f0 || nres + files[f1]->residues.size() <= max_batch_residues)) {
+            nres += files[f1]->residues.size();
+            nseq += files[f1]->size();
+            ++f1;
+        }
+        std::vector<uint8_t> res;
+        std::vector<uint64_t> off;
+        std::vector<uint32_t> len;
+        const uint8_t* rp = nullptr;
+        if (f1 == f0 + 1) {  // single file: use its buffer directly
+            rp = files[f0]->residues.data();
+            off = files[f0]->off;
+            len = files[f0]->len;
+        } else {
+            res.reserve(nres);
+            off.reserve(nseq);
+            len.reserve(nseq);
+            for (size_t f = f0; f < f1; ++f) {
+                const FastaFile& F = *files[f];
+                const uint64_t base = res.size();
+                res.insert(res.end(), F.residues.begin(), F.residues.end());
+                for (size_t r = 0; r < F.size(); ++r) {
+                    off.push_back(base + F.off[r]);
+                    len.push_back(F.len[r]);
+                }
+            }
+            rp = res.data();
+        }
+        skm_calls calls{};
+        auto t0 = std::chrono::steady_clock::now();
+        int rc = skm_annotate(db, rp, off.data(), len.data(), off.size(), &o, &calls);
+        if (device_ms)
+            *device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (rc) {
+            err = skm_last_error();
+            return rc;
+        }
+        // host find_best_call per sequence
+        std::vector<std::pair<size_t, size_t>> where;  // (file, record) per batch sequence
+        where.reserve(off.size());
+        for (size_t f = f0; f < f1; ++f)
+            for (size_t r = 0; r < files[f]->size(); ++r) where.emplace_back(f, r);
+        std::atomic<size_t> next{0};
+        std::atomic<int> first_rc{0};
+        auto work = [&]() {
+            std::vector<char> fb(1 << 16);
+            const size_t chunk = 4096;
+            for (size_t s0; (s0 = next.fetch_add(chunk)) < where.size();) {
+                for (size_t s = s0; s < std::min(where.size(), s0 + chunk); ++s) {
+                    SeqCall& c = out[where[s].first][where[s].second];
+                    float offset = 0;
+                    int r = skm_find_best_call(calls.calls + calls.call_off[s], calls.call_off[s + 1] - calls.call_off[s],
+                                               fidx.data(), fidx.size(), &c.fi, &c.score, &offset, fb.data(), fb.size());
+                    if (r) first_rc = r;
+                    c.func = fb.data();
+                }
+            }
+        };
+        int nt = std::max(1, n_threads);
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+        skm_calls_free(&calls);
+        if (first_rc) {
+            err = skm_last_error();
+            return first_rc;
+        }
+        f0 = f1;
+    }
+    return SKM_OK;
+}
+
+}  // namespace skmf

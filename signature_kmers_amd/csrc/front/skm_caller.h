@@ -1,0 +1,30 @@
+// skm_caller.h -- FunctionCaller<KmerDb>::process_fasta_stream for the CLIs
+// (call_functions.tcc:109-257): every record with a non-empty id is one query; the windows are
+// looked up and the HitSet calls made on the GPU (skm_annotate), find_best_call runs on the host.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "skm.h"
+#include "skm_front.h"
+
+namespace skmf {
+
+struct SeqCall {
+    uint16_t fi = 0xFFFF;
+    float score = 0.0f;
+    std::string func;
+};
+
+// FunctionCaller::read_function_index (call_functions.tcc:123-148): column 0 = index, column 1 =
+// name; the table is sized max index + 1.
+bool read_function_index(const std::string& path, std::vector<std::string>& table, std::string& err);
+
+// Query every sequence of every file (in order) against db.  out[f][r] is the call for record r
+// of file f.  Files are batched so one device batch holds <= max_batch_residues residues.
+int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std::vector<std::string>& function_index,
+               bool ignore_hypo, int n_threads, std::vector<std::vector<SeqCall>>& out, std::string& err,
+               double* device_ms = nullptr, uint64_t max_batch_residues = 2000000000ull);
+
+}  // namespace skmf

@@ -1,0 +1,653 @@
+// skm_front.cpp -- host front end (see skm_front.h for the reference mapping).
+#include "skm_front.h"
+
+#include <dirent.h>
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cctype>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <stdexcept>
+#include <thread>
+
+namespace skmf {
+
+namespace {
+
+inline bool is_space(unsigned char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r'; }
+inline bool is_digit(unsigned char c) { return c >= '0' && c <= '9'; }
+
+struct CharClass {
+    bool alpha[256];
+    CharClass() {
+        for (int c = 0; c < 256; ++c) alpha[c] = (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z');
+    }
+};
+const CharClass kCls;
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// FastaParser (fasta_parser.h:38-144).  The callback fires on '>' in s_id_or_data and once more
+// from parse_complete(); callers ignore records with an empty id, so only non-empty ids are kept.
+// ---------------------------------------------------------------------------------------------
+void parse_fasta_buffer(const char* buf, size_t n, FastaFile& out) {
+    enum State { S_START, S_ID, S_DEF, S_DATA, S_ID_OR_DATA } st = S_START;
+    int line = 1;
+    std::string id, def;
+    uint64_t seq_start = out.residues.size();
+    auto emit = [&]() {
+        if (!id.empty()) {
+            out.ids.push_back(id);
+            out.defs.push_back(def);
+            out.off.push_back(seq_start);
+            out.len.push_back((uint32_t)(out.residues.size() - seq_start));
+        } else {
+            out.residues.resize(seq_start);
+        }
+        id.clear();
+        def.clear();
+        seq_start = out.residues.size();
+    };
+    auto error = [&](const std::string& msg) {
+        std::cerr << "Error found: " << msg << " at line " << line << " id='" << id << "'" << std::endl;
+    };
+    const unsigned char* p = reinterpret_cast<const unsigned char*>(buf);
+    const unsigned char* end = p + n;
+    while (p < end) {
+        const unsigned char c = *p++;
+        if (c == '\n') ++line;
+        if (c == '\r') continue;
+        switch (st) {
+            case S_START:
+                if (c != '>')
+                    error("Missing >");
+                else
+                    st = S_ID;
+                break;
+            case S_ID:
+                if (c == ' ' || c == '\t') {
+                    def.push_back((char)c);
+                    st = S_DEF;
+                } else if (c == '\n') {
+                    st = S_DATA;
+                } else {
+                    id.push_back((char)c);
+                }
+                break;
+            case S_DEF:
+                if (c == '\n')
+                    st = S_DATA;
+                else
+                    def.push_back((char)c);
+                break;
+            case S_DATA:
+                if (c == '\n') {
+                    st = S_ID_OR_DATA;
+                } else if (kCls.alpha[c] || c == '*') {
+                    // fast path: the rest of a residue run
+                    const unsigned char* q = p;
+                    while (q < end && (kCls.alpha[*q] || *q == '*')) ++q;
+                    out.residues.push_back(c);
+                    out.residues.insert(out.residues.end(), p, q);
+                    p = q;
+                } else {
+                    error(std::string("Bad data character '") + (char)c + "'");
+                }
+                break;
+            case S_ID_OR_DATA:
+                if (c == '>') {
+                    emit();
+                    st = S_ID;
+                } else if (c == '\n') {
+                } else if (kCls.alpha[c]) {
+                    out.residues.push_back(c);
+                    st = S_DATA;
+                } else {
+                    error(std::string("Bad id or data character '") + (char)c + "'");
+                }
+                break;
+        }
+    }
+    emit();  // parse_complete()
+}
+
+bool parse_fasta_file(const std::string& path, FastaFile& out) {
+    out = FastaFile();
+    out.path = path;
+    out.filename = path_filename(path);
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    f.seekg(0, std::ios::end);
+    std::streamoff n = f.tellg();
+    f.seekg(0);
+    std::string buf((size_t)std::max<std::streamoff>(n, 0), '\0');
+    if (n > 0) f.read(&buf[0], n);
+    out.residues.reserve((size_t)n);
+    parse_fasta_buffer(buf.data(), buf.size(), out);
+    out.residues.shrink_to_fit();
+    return true;
+}
+
+bool parse_fasta_files(const std::vector<std::string>& paths, std::vector<FastaFile>& out, int n_threads,
+                       std::string& err) {
+    out.assign(paths.size(), FastaFile());
+    std::atomic<size_t> next{0};
+    std::atomic<bool> ok{true};
+    std::string bad;
+    auto work = [&]() {
+        for (size_t i; (i = next.fetch_add(1)) < paths.size();) {
+            if (!parse_fasta_file(paths[i], out[i])) {
+                ok = false;
+                bad = paths[i];
+            }
+        }
+    };
+    int nt = std::max(1, std::min<int>(n_threads, (int)paths.size()));
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    if (!ok) err = "cannot read " + bad;
+    return ok;
+}
+
+// ---------------------------------------------------------------------------------------------
+// paths (path_utils.h)
+// ---------------------------------------------------------------------------------------------
+std::string path_join(const std::string& dir, const std::string& name) {
+    if (dir.empty()) return name;
+    if (dir.back() == '/') return dir + name;
+    return dir + "/" + name;
+}
+std::string path_filename(const std::string& p) {
+    size_t s = p.find_last_of('/');
+    return s == std::string::npos ? p : p.substr(s + 1);
+}
+bool path_is_relative(const std::string& p) { return p.empty() || p[0] != '/'; }
+bool ensure_directory(const std::string& dir) {
+    if (dir.empty()) return true;
+    struct stat sb;
+    if (stat(dir.c_str(), &sb) == 0 && S_ISDIR(sb.st_mode)) return true;
+    return mkdir(dir.c_str(), 0777) == 0;
+}
+
+bool list_regular_files(const std::string& dir, std::vector<std::string>& out, std::string& err) {
+    DIR* d = opendir(dir.c_str());
+    if (!d) {
+        err = "cannot open directory " + dir;
+        return false;
+    }
+    while (struct dirent* e = readdir(d)) {
+        if (!std::strcmp(e->d_name, ".") || !std::strcmp(e->d_name, "..")) continue;
+        std::string p = path_join(dir, e->d_name);
+        struct stat sb;
+        if (stat(p.c_str(), &sb) == 0 && S_ISREG(sb.st_mode)) out.push_back(p);
+    }
+    closedir(d);
+    return true;
+}
+
+std::vector<std::string> load_lines(const std::string& path, bool* ok) {
+    std::vector<std::string> v;
+    std::ifstream f(path);
+    if (ok) *ok = (bool)f;
+    std::string line;
+    while (std::getline(f, line, '\n')) v.push_back(line);
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// seed_utils.h regexes as hand-coded matchers (Boost.Regex Perl semantics, leftmost match,
+// \s = [ \t\n\v\f\r]).
+// ---------------------------------------------------------------------------------------------
+
+// regex_match(str, "(.*?)(?:\s+(\#+)\s+(.*))?"): the lazy prefix stops at the first position i
+// where str[i..] = \s+ #+ \s+ .*  (the optional group is tried before the empty tail).
+void split_func_comment(const std::string& s, std::string& func, std::string& sep, std::string& comment) {
+    const size_t n = s.size();
+    for (size_t i = 0; i < n; ++i) {
+        if (!is_space((unsigned char)s[i])) continue;
+        size_t j = i;
+        while (j < n && is_space((unsigned char)s[j])) ++j;
+        if (j < n && s[j] == '#') {
+            size_t k = j;
+            while (k < n && s[k] == '#') ++k;
+            if (k < n && is_space((unsigned char)s[k])) {
+                size_t c = k;
+                while (c < n && is_space((unsigned char)s[c])) ++c;
+                func = s.substr(0, i);
+                sep = s.substr(j, k - j);
+                comment = s.substr(c);
+                return;
+            }
+        }
+        i = j - 1;  // positions inside this blank run give the same outcome
+    }
+    func = s;
+    sep.clear();
+    comment.clear();
+}
+
+// regex_search(str, "^(?:frag|missing|trunc)"); '^' also matches after a newline (Perl mode)
+bool is_truncated_comment(const std::string& s) {
+    auto at = [&](size_t p) {
+        return s.compare(p, 4, "frag") == 0 || s.compare(p, 7, "missing") == 0 || s.compare(p, 5, "trunc") == 0;
+    };
+    if (at(0)) return true;
+    for (size_t p = 0; p + 1 < s.size(); ++p)
+        if (s[p] == '\n' && at(p + 1)) return true;
+    return false;
+}
+
+// regex_replace(str, "(\s*\#.*$)", ""): everything from the blank run before the first '#'.
+std::string strip_func_comment(const std::string& s) {
+    size_t h = s.find('#');
+    if (h == std::string::npos) return s;
+    size_t w = h;
+    while (w > 0 && is_space((unsigned char)s[w - 1])) --w;
+    return s.substr(0, w);
+}
+
+// sregex_token_iterator(stripped, "\s+[/@]\s+|\s*;\s+", -1)
+std::vector<std::string> roles_of_function(const std::string& function) {
+    const std::string s = strip_func_comment(function);
+    const size_t n = s.size();
+    std::vector<std::string> ret;
+    auto match_at = [&](size_t i, size_t& e) -> bool {
+        // alternative 1: \s+[/@]\s+
+        size_t j = i;
+        while (j < n && is_space((unsigned char)s[j])) ++j;
+        if (j > i && j < n && (s[j] == '/' || s[j] == '@')) {
+            size_t k = j + 1, k0 = k;
+            while (k < n && is_space((unsigned char)s[k])) ++k;
+            if (k > k0) {
+                e = k;
+                return true;
+            }
+        }
+        // alternative 2: \s*;\s+
+        if (j < n && s[j] == ';') {
+            size_t k = j + 1, k0 = k;
+            while (k < n && is_space((unsigned char)s[k])) ++k;
+            if (k > k0) {
+                e = k;
+                return true;
+            }
+        }
+        return false;
+    };
+    size_t last = 0;
+    bool any = false;
+    for (size_t i = 0; i < n; ++i) {
+        size_t e;
+        if (match_at(i, e)) {
+            ret.push_back(s.substr(last, i - last));
+            last = e;
+            i = e - 1;
+            any = true;
+        }
+    }
+    if (!any) {
+        if (n) ret.push_back(s);
+    } else if (last != n) {
+        ret.push_back(s.substr(last));
+    }
+    return ret;
+}
+
+// regex_match(def, "\s+(.*)\s+\[([^]]+)\]$"): the greedy (.*) ends at the blank right before the
+// last '[' whose bracket content (no ']') runs to a final ']'.
+bool match_genome_defline(const std::string& def, std::string& func_part, std::string& genome) {
+    const size_t n = def.size();
+    if (n < 4 || def[n - 1] != ']') return false;
+    size_t q = std::string::npos;
+    for (size_t i = n - 1; i-- > 0;) {
+        if (def[i] == ']') break;
+        if (def[i] == '[' && i + 1 < n - 1 && i >= 1 && is_space((unsigned char)def[i - 1])) {
+            q = i;
+            break;
+        }
+    }
+    if (q == std::string::npos) return false;
+    const size_t p = q - 1;  // the blank consumed by the second \s+
+    if (p < 1 || !is_space((unsigned char)def[0])) return false;
+    size_t R = 0;
+    while (R < n && is_space((unsigned char)def[R])) ++R;
+    const size_t start = std::min(R, p);
+    func_part = def.substr(start, p - start);
+    genome = def.substr(q + 1, n - 1 - (q + 1));
+    return true;
+}
+
+bool search_fig_genome(const std::string& id, std::string& genome) {
+    for (size_t pos = id.find("fig|"); pos != std::string::npos; pos = id.find("fig|", pos + 1)) {
+        size_t a = pos + 4, b = a;
+        while (b < id.size() && is_digit((unsigned char)id[b])) ++b;
+        if (b == a || b >= id.size() || id[b] != '.') continue;
+        size_t c = b + 1, d = c;
+        while (d < id.size() && is_digit((unsigned char)id[d])) ++d;
+        if (d == c) continue;
+        genome = id.substr(a, d - a);
+        return true;
+    }
+    return false;
+}
+
+static bool match_genome_id(const std::string& s) {  // regex_match(s, "\d+\.\d+")
+    size_t b = 0;
+    while (b < s.size() && is_digit((unsigned char)s[b])) ++b;
+    if (b == 0 || b >= s.size() || s[b] != '.') return false;
+    size_t d = b + 1;
+    while (d < s.size() && is_digit((unsigned char)s[d])) ++d;
+    return d > b + 1 && d == s.size();
+}
+
+// ---------------------------------------------------------------------------------------------
+// accumulator_set<float, stats<mean, median, variance, count>>: float sum, P^2 (p = 0.5) in
+// float, iterative variance over the lazy mean (features updated count, sum, median, variance).
+// ---------------------------------------------------------------------------------------------
+void FloatStats::add(float x) {
+    ++count;
+    sum += x;
+    if (count <= 5) {
+        heights[count - 1] = x;
+        if (count == 5) std::sort(heights, heights + 5);
+    } else {
+        static const float incr[5] = {0.0f, 0.25f, 0.5f, 0.75f, 1.0f};
+        size_t cell;
+        if (x < heights[0]) {
+            heights[0] = x;
+            cell = 1;
+        } else if (heights[4] <= x) {
+            heights[4] = x;
+            cell = 4;
+        } else {
+            cell = (size_t)(std::upper_bound(heights, heights + 5, x) - heights);
+        }
+        for (size_t i = cell; i < 5; ++i) actual[i] += 1.0f;
+        for (size_t i = 0; i < 5; ++i) desired[i] += incr[i];
+        for (size_t i = 1; i <= 3; ++i) {
+            float d = desired[i] - actual[i];
+            float dp = actual[i + 1] - actual[i];
+            float dm = actual[i - 1] - actual[i];
+            float hp = (heights[i + 1] - heights[i]) / dp;
+            float hm = (heights[i - 1] - heights[i]) / dm;
+            if ((d >= 1. && dp > 1) || (d <= -1. && dm < -1)) {
+                short sign_d = static_cast<short>(d / std::abs(d));
+                float h = heights[i] + sign_d / (dp - dm) * ((sign_d - dm) * hp + (dp - sign_d) * hm);
+                if (heights[i - 1] < h && h < heights[i + 1]) {
+                    heights[i] = h;
+                } else {
+                    if (d > 0) heights[i] += hp;
+                    if (d < 0) heights[i] -= hm;
+                }
+                actual[i] += sign_d;
+            }
+        }
+    }
+    if (count > 1) {
+        float mean = sum / (float)count;
+        float tmp = x - mean;
+        variance = variance * (float)(count - 1) / (float)count + tmp * tmp / (float)(count - 1);
+    }
+}
+
+std::string fmt_g(double v) {
+    char b[64];
+    std::snprintf(b, sizeof b, "%g", v);
+    return b;
+}
+
+// ---------------------------------------------------------------------------------------------
+// FunctionMap
+// ---------------------------------------------------------------------------------------------
+void FunctionMap::load_id_assignments(const std::string& path) {
+    std::ifstream f(path);
+    std::string line;
+    int lineno = 0;
+    while (std::getline(f, line)) {
+        lineno++;
+        size_t s = line.find('\t');
+        if (s == std::string::npos) {
+            std::cerr << "bad line " << lineno << " in file \"" << path << "\"\n";
+            continue;
+        }
+        size_t s2 = line.find('\t', s + 1);
+        std::string id = line.substr(0, s);
+        std::string func = s2 == std::string::npos ? line.substr(s + 1) : line.substr(s + 1, s2 - s - 1);
+        std::string stripped, delim, comment;
+        split_func_comment(func, stripped, delim, comment);
+        original_assignment_stripped_[id] = stripped;
+        original_assignment_[id] = func;
+        if (delim == "#" && is_truncated_comment(comment)) continue;
+        id_function_map_[id] = stripped;
+    }
+}
+
+void FunctionMap::load_fasta_file(const FastaFile& f, const std::set<std::string>& deleted_fids) {
+    std::string genome;
+    for (size_t r = 0; r < f.size(); ++r) {
+        const std::string& id = f.ids[r];
+        const std::string& def = f.defs[r];
+        if (deleted_fids.count(id)) continue;
+        std::string func;
+        if (!def.empty()) {
+            size_t x = def.find_first_not_of(" \t");
+            if (x == std::string::npos)  // def.substr(npos) throws in the reference
+                throw std::out_of_range("blank definition line for " + id + " in " + f.path);
+            func = def.substr(x);
+        }
+        std::string genome_loc, fpart, g;
+        if (match_genome_defline(def, fpart, g)) {
+            std::string delim, comment;
+            split_func_comment(fpart, func, delim, comment);
+            if (delim == "#" && is_truncated_comment(comment)) continue;
+            genome_loc = g;
+        }
+        if (genome.empty()) {
+            if (def.empty())
+                search_fig_genome(id, genome);
+            else if (!genome_loc.empty())
+                genome = genome_loc;
+        }
+        if (genome.empty()) {
+            genome = f.filename;
+            if (!match_genome_id(genome)) std::cerr << "cannot determine genome from file \"" << f.path << "\"\n";
+        }
+        std::string& cur = id_function_map_[id];
+        if (cur.empty()) {
+            if (!func.empty()) cur = func;
+        } else {
+            func = cur;
+        }
+        if (!func.empty()) {
+            function_genome_map_[func].insert(genome);
+            function_accumulators_[func].add((float)f.len[r]);
+        }
+    }
+}
+
+unsigned FunctionMap::process_kept_functions(int min_reps_required, const std::set<std::string>& ignored) {
+    std::set<std::string> kept;
+    for (const auto& e : function_genome_map_) {
+        const std::string& function = e.first;
+        bool ok = (int)e.second.size() >= min_reps_required || good_functions_.count(function);
+        if (!ok) {
+            for (const auto& role : roles_of_function(function))
+                if (good_roles_.count(role)) {
+                    ok = true;
+                    break;
+                }
+        }
+        if (ok) kept.insert(function);
+    }
+    kept.insert("hypothetical protein");
+    for (const auto& fn : ignored) {
+        std::cerr << "Ignore '" << fn << "'\n";
+        kept.erase(fn);
+    }
+    unsigned short next = 0;
+    function_index_map_.clear();
+    index_function_map_.clear();
+    for (const auto& f : kept) {
+        unsigned short id = next++;
+        function_index_map_[f] = id;
+        index_function_map_[id] = f;
+    }
+    return next;
+}
+
+bool FunctionMap::write_function_index(const std::string& dir) const {
+    std::ofstream of(path_join(dir, "function.index"));
+    if (!of) return false;
+    for (const auto& ent : index_function_map_) {
+        FloatStats& a = function_accumulators_[ent.second];
+        const double mean = a.mean(), median = a.median(), var = a.variance;
+        const double dev = std::sqrt(var);
+        of << ent.first << "\t" << ent.second << "\t" << (int)a.count << "\t" << fmt_g(mean) << "\t" << fmt_g(median)
+           << "\t" << fmt_g(var) << "\t" << fmt_g(dev) << "\n";
+    }
+    return (bool)of;
+}
+
+std::string FunctionMap::lookup_function_of_id(const std::string& id) const {
+    auto it = id_function_map_.find(id);
+    return it == id_function_map_.end() ? std::string() : it->second;
+}
+uint16_t FunctionMap::lookup_index(const std::string& func) const {
+    auto it = function_index_map_.find(func);
+    return it == function_index_map_.end() ? (uint16_t)0xFFFF : it->second;
+}
+std::string FunctionMap::lookup_function(uint16_t idx) const {
+    auto it = index_function_map_.find(idx);
+    return it == index_function_map_.end() ? std::string() : it->second;
+}
+void FunctionMap::lookup_original_assignment(const std::string& id, std::string& func, std::string& stripped) const {
+    auto x = original_assignment_.find(id);
+    if (x != original_assignment_.end()) {
+        func = x->second;
+        stripped = original_assignment_stripped_.at(id);
+    }
+}
+std::vector<std::string> FunctionMap::index_table() const {
+    std::vector<std::string> t;
+    for (const auto& e : index_function_map_) {
+        if (t.size() <= e.first) t.resize((size_t)e.first + 1);
+        t[e.first] = e.second;
+    }
+    return t;
+}
+
+void select_build_sequences(const FunctionMap& fm, const FastaFile& f, unsigned file_number,
+                            unsigned max_seqs_per_file, const std::set<std::string>& deleted_fids,
+                            BuildBatch& out) {
+    out = BuildBatch();
+    unsigned next_sequence_id = file_number * max_seqs_per_file;
+    std::unordered_map<std::string, uint16_t> fi_cache;
+    for (size_t r = 0; r < f.size(); ++r) {
+        const std::string& id = f.ids[r];
+        if (!deleted_fids.empty() && deleted_fids.count(id)) continue;
+        std::string func = fm.lookup_function_of_id(id);
+        if (func.empty()) continue;
+        unsigned seq_id = next_sequence_id++;
+        auto it = fi_cache.find(func);
+        uint16_t fi = it != fi_cache.end() ? it->second : (fi_cache[func] = fm.lookup_index(func));
+        if (fi == 0xFFFF) continue;
+        out.off.push_back(f.off[r]);
+        out.len.push_back(f.len[r]);
+        out.func.push_back(fi);
+        out.seq_id.push_back(seq_id);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// command line
+// ---------------------------------------------------------------------------------------------
+bool Options::parse(int argc, char** argv, std::string& err) {
+    auto find_long = [&](const std::string& n) -> const Spec* {
+        for (auto& s : specs)
+            if (s.name == n) return &s;
+        return nullptr;
+    };
+    auto find_short = [&](char c) -> const Spec* {
+        for (auto& s : specs)
+            if (s.short_name && s.short_name == c) return &s;
+        return nullptr;
+    };
+    size_t pos_i = 0;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        const Spec* sp = nullptr;
+        std::string inline_val;
+        bool has_inline = false;
+        if (a.size() > 2 && a[0] == '-' && a[1] == '-') {
+            std::string nm = a.substr(2);
+            size_t eq = nm.find('=');
+            if (eq != std::string::npos) {
+                inline_val = nm.substr(eq + 1);
+                nm = nm.substr(0, eq);
+                has_inline = true;
+            }
+            sp = find_long(nm);
+            if (!sp) {
+                err = "unrecognised option '" + a + "'";
+                return false;
+            }
+        } else if (a.size() >= 2 && a[0] == '-' && a[1] != '-') {
+            sp = find_short(a[1]);
+            if (!sp) {
+                err = "unrecognised option '" + a + "'";
+                return false;
+            }
+            if (a.size() > 2) {
+                inline_val = a.substr(2);
+                has_inline = true;
+            }
+        } else {
+            if (pos_i >= positional.size()) {
+                err = "too many positional options";
+                return false;
+            }
+            const std::string& pn = positional[pos_i];
+            const Spec* ps = find_long(pn);
+            values[pn].push_back(a);
+            if (!(ps && ps->multi)) ++pos_i;
+            continue;
+        }
+        auto& dst = values[sp->name];
+        if (sp->flag) {
+            dst.push_back("1");
+            continue;
+        }
+        if (has_inline) {
+            dst.push_back(inline_val);
+            if (!sp->multi) continue;
+        } else {
+            if (i + 1 >= argc) {
+                err = "option '--" + sp->name + "' requires an argument";
+                return false;
+            }
+            dst.push_back(argv[++i]);
+        }
+        if (sp->multi)
+            while (i + 1 < argc && argv[i + 1][0] != '-') dst.push_back(argv[++i]);
+    }
+    return true;
+}
+
+std::string Options::get(const std::string& n, const std::string& dflt) const {
+    auto it = values.find(n);
+    return it == values.end() || it->second.empty() ? dflt : it->second.back();
+}
+std::vector<std::string> Options::all(const std::string& n) const {
+    auto it = values.find(n);
+    return it == values.end() ? std::vector<std::string>() : it->second;
+}
+
+}  // namespace skmf

@@ -41,7 +41,57 @@ struct DevBdz {
     const uint16_t* dat;        // 5 u16 per record
     uint32_t m, r, b, seed;
     uint64_t r_magic;           // fastmod: ceil(2^64 / r)
+    // exact-key mode (KeptKmerDB, kept_kmer_db.h:20-27): open-addressing table of the kept keys
+    const unsigned long long* xkeys;  // [mask+1], 0 = empty (a k-mer key is never 0)
+    const uint32_t* xidx;             // record index of the key in xkeys[h]
+    uint64_t xmask;
+    uint32_t xshift;
 };
+
+__device__ __forceinline__ uint64_t xmix(uint64_t k) {  // murmur3 fmix64 (bijective)
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+// KeptKmerDB::fetch: a hit iff the key is a kept k-mer; returns D.m on a miss.
+__device__ __forceinline__ uint32_t exact_lookup(const DevBdz& D, uint32_t lo, uint32_t hi) {
+    const uint64_t k = ((uint64_t)hi << 32) | lo;
+    uint64_t h = xmix(k) >> D.xshift;
+    for (;;) {
+        const uint64_t t = D.xkeys[h];
+        if (t == k) return D.xidx[h];
+        if (t == 0) return D.m;
+        h = (h + 1) & D.xmask;
+    }
+}
+
+__global__ void k_exact_insert(const uint64_t* __restrict__ keys, uint64_t n, unsigned long long* __restrict__ tk,
+                               uint32_t* __restrict__ ti, uint64_t mask, uint32_t shift, uint32_t* __restrict__ bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long k = keys[i];
+    if (k == 0) {
+        atomicOr(bad, 1u);
+        return;
+    }
+    uint64_t h = xmix(k) >> shift;
+    for (;;) {
+        const unsigned long long prev = atomicCAS(&tk[h], 0ull, k);
+        if (prev == 0ull) {
+            ti[h] = (uint32_t)i;
+            return;
+        }
+        if (prev == k) {
+            atomicOr(bad, 2u);
+            return;
+        }
+        h = (h + 1) & mask;
+    }
+}
 
 __device__ __forceinline__ uint32_t fastmod(uint32_t a, uint64_t M, uint32_t d) {
     uint64_t low = M * a;
@@ -93,6 +143,7 @@ __device__ __forceinline__ uint32_t bdz_lookup(const DevBdz& D, uint32_t lo, uin
 
 __device__ __forceinline__ bool ambig(uint32_t c) { return c == 'X' || c == '*'; }
 
+template <bool EXACT>
 __global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict__ res, uint64_t rp, DevBdz D,
                                                       uint32_t* __restrict__ hits) {
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x * LK_POS;
@@ -126,7 +177,7 @@ __global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict
                     lo = (w[wi] >> sh) | (w[wi + 1] << (32 - sh));
                     hi = (w[wi + 1] >> sh) | (w[wi + 2] << (32 - sh));
                 }
-                const uint32_t idx = bdz_lookup(D, lo, hi);
+                const uint32_t idx = EXACT ? exact_lookup(D, lo, hi) : bdz_lookup(D, lo, hi);
                 if (idx < D.m) {
                     const uint16_t* rec = D.dat + (uint64_t)idx * 5;
                     o = ((uint32_t)rec[1] << 16) | rec[2];  // function_index, mean
@@ -467,9 +518,11 @@ using namespace skm;
 
 struct skm_db {
     int device = 0;
+    bool exact = false;          // KeptKmerDB semantics (skm_db_open_kept)
+    uint32_t m = 0;              // hash size (BDZ) or number of kept keys (exact)
     Bdz bdz;
     uint64_t dat_records = 0;
-    DevBuf d_g, d_rank, d_dat;
+    DevBuf d_g, d_rank, d_dat, d_xkeys, d_xidx;
     DevBdz dev{};
 };
 
@@ -512,6 +565,45 @@ void db_upload(skm_db* db, const uint8_t* dat, size_t dat_len) {
     D.b = h.b;
     D.seed = h.seed;
     D.r_magic = h.r ? (~0ull / h.r + 1) : 0;
+    db->m = h.m;
+}
+
+void db_upload_kept(skm_db* db, const uint64_t* keys, const skm_stored_kmer_data* data, size_t n) {
+    SKM_HIP(hipSetDevice(db->device));
+    SKM_CHECK(n < 0xFFFFFFFFull, SKM_E_ARG, "too many kept k-mers for a u32 record index");
+    db->exact = true;
+    db->m = (uint32_t)n;
+    db->dat_records = n;
+    int lg = std::max(4, ilog2_ceil(2 * (uint64_t)std::max<size_t>(n, 1)));  // load factor <= 1/2
+    const uint64_t T = 1ull << lg;
+    db->d_xkeys.ensure(8 * T);
+    db->d_xidx.ensure(4 * T);
+    db->d_dat.ensure(std::max<size_t>(10 * n, 16));
+    SKM_HIP(hipMemset(db->d_xkeys.p, 0, 8 * T));
+    if (n) SKM_HIP(hipMemcpy(db->d_dat.p, data, 10 * n, hipMemcpyHostToDevice));
+    DevBdz& D = db->dev;
+    D = DevBdz{};
+    D.dat = db->d_dat.as<uint16_t>();
+    D.m = (uint32_t)n;
+    D.xkeys = db->d_xkeys.as<unsigned long long>();
+    D.xidx = db->d_xidx.as<uint32_t>();
+    D.xmask = T - 1;
+    D.xshift = 64u - (uint32_t)lg;
+    if (n) {
+        DevBuf dk, dbad;
+        dk.ensure(8 * n);
+        dbad.ensure(4);
+        SKM_HIP(hipMemcpy(dk.p, keys, 8 * n, hipMemcpyHostToDevice));
+        SKM_HIP(hipMemset(dbad.p, 0, 4));
+        hipLaunchKernelGGL(k_exact_insert, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, 0, dk.as<uint64_t>(),
+                           (uint64_t)n, db->d_xkeys.as<unsigned long long>(), db->d_xidx.as<uint32_t>(), T - 1,
+                           64u - (uint32_t)lg, dbad.as<uint32_t>());
+        SKM_HIP(hipGetLastError());
+        uint32_t bad = 0;
+        SKM_HIP(hipMemcpy(&bad, dbad.p, 4, hipMemcpyDeviceToHost));
+        SKM_CHECK(!(bad & 1u), SKM_E_ARG, "kept k-mer key 0 is not a valid k-mer");
+        SKM_CHECK(!(bad & 2u), SKM_E_ARG, "duplicate kept k-mer keys");
+    }
 }
 
 bool read_file(const char* path, std::vector<uint8_t>& out) {
@@ -530,11 +622,15 @@ void query_run(skm_query* q, const skm_annot_opts* o) {
     SKM_HIP(hipSetDevice(db->device));
     hipStream_t st = q->stream;
     SKM_HIP(hipEventRecord(q->ev[0], st));
-    if (q->rp && db->bdz.m) {
+    if (q->rp && db->m) {
         uint64_t nthreads = ceil_div(q->rp, LK_POS);
         uint32_t grid = (uint32_t)std::min<uint64_t>(ceil_div(nthreads, LK_THREADS), 256ull * 16);
-        hipLaunchKernelGGL(k_lookup, dim3(grid), dim3(LK_THREADS), 0, st, q->d_res.as<uint8_t>(), q->rp, db->dev,
-                           q->d_hits.as<uint32_t>());
+        if (db->exact)
+            hipLaunchKernelGGL(k_lookup<true>, dim3(grid), dim3(LK_THREADS), 0, st, q->d_res.as<uint8_t>(), q->rp,
+                               db->dev, q->d_hits.as<uint32_t>());
+        else
+            hipLaunchKernelGGL(k_lookup<false>, dim3(grid), dim3(LK_THREADS), 0, st, q->d_res.as<uint8_t>(), q->rp,
+                               db->dev, q->d_hits.as<uint32_t>());
     } else if (q->rp) {
         SKM_HIP(hipMemsetAsync(q->d_hits.p, 0xFF, 4 * q->rp, st));
     }
@@ -623,25 +719,43 @@ int skm_db_open(skm_db** out, const char* mph_path, const char* dat_path, int de
     SKM_API_END
 }
 
+int skm_db_open_kept(skm_db** out, const uint64_t* keys, const skm_stored_kmer_data* data, size_t n, int device) {
+    SKM_API_BEGIN
+    SKM_CHECK(out && (n == 0 || (keys && data)), SKM_E_ARG, "null argument");
+    auto* db = new skm_db();
+    db->device = device;
+    try {
+        db_upload_kept(db, keys, data, n);
+    } catch (...) {
+        delete db;
+        throw;
+    }
+    *out = db;
+    SKM_API_END
+}
+
 int skm_db_size(skm_db* db, uint32_t* m) {
     if (!db || !m) return SKM_E_ARG;
-    *m = db->bdz.m;
+    *m = db->m;
     return SKM_OK;
 }
 
+extern "C++" {
+template <bool EXACT>
 __global__ void k_lookup_keys(const uint64_t* __restrict__ keys, uint64_t n, DevBdz D, uint32_t* __restrict__ out) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t k = keys[i];
-    out[i] = bdz_lookup(D, (uint32_t)k, (uint32_t)(k >> 32));
+    out[i] = EXACT ? exact_lookup(D, (uint32_t)k, (uint32_t)(k >> 32)) : bdz_lookup(D, (uint32_t)k, (uint32_t)(k >> 32));
 }
+}  // extern "C++"
 
 int skm_db_lookup(skm_db* db, const uint64_t* keys, size_t n, uint32_t* idx_out) {
     SKM_API_BEGIN
     SKM_CHECK(db && (n == 0 || (keys && idx_out)), SKM_E_ARG, "null argument");
     if (n == 0) return SKM_OK;
     SKM_HIP(hipSetDevice(db->device));
-    if (db->bdz.m == 0) {
+    if (db->m == 0) {
         for (size_t i = 0; i < n; ++i) idx_out[i] = 0;  // empty hash: every key maps to rank 0 == size (miss)
         return SKM_OK;
     }
@@ -649,8 +763,12 @@ int skm_db_lookup(skm_db* db, const uint64_t* keys, size_t n, uint32_t* idx_out)
     dk.ensure(8 * n);
     dout.ensure(4 * n);
     SKM_HIP(hipMemcpy(dk.p, keys, 8 * n, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_lookup_keys, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, 0, dk.as<uint64_t>(), (uint64_t)n,
-                       db->dev, dout.as<uint32_t>());
+    if (db->exact)
+        hipLaunchKernelGGL(k_lookup_keys<true>, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, 0, dk.as<uint64_t>(),
+                           (uint64_t)n, db->dev, dout.as<uint32_t>());
+    else
+        hipLaunchKernelGGL(k_lookup_keys<false>, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, 0, dk.as<uint64_t>(),
+                           (uint64_t)n, db->dev, dout.as<uint32_t>());
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipMemcpy(idx_out, dout.p, 4 * n, hipMemcpyDeviceToHost));
     SKM_API_END

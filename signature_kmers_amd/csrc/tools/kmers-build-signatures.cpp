@@ -1,0 +1,333 @@
+// kmers-build-signatures -- drop-in for the reference's main (kmers-build-signatures.cc:126-373).
+//
+// Same options, same files in --kmer-data-dir (function.index, otu.index, genomes, final.kmers,
+// distinct_functions, recall.report.d/<fasta>, kmer_data.mph/.dat with --perfect-hash) and the
+// same stdout lines.  The k-mer extraction, group-by, 80 % cut and statistics run on one MI355X
+// through libskm (skm_build_*); the recall pass runs the GPU annotate path against an exact-key
+// DB of the kept k-mers (KeptKmerDB semantics, skm_db_open_kept); the perfect hash is built on a
+// host thread while the recall runs (as the reference does, kmers-build-signatures.cc:268-276).
+//
+// Result order: final.kmers is written in ascending k-mer key order and distinct_functions in
+// ascending function index; the reference writes both in TBB hash-table order, so compare them
+// as sets.  --nudb-file is not supported (NuDB is out of scope).
+// Extra options: --device N (HIP device), --dump-extract FILE (write the build input arrays and
+// stop before touching the GPU; used by the CPU tests), --mph-seed N.
+#include <sys/stat.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <sstream>
+#include <thread>
+
+#include "skm.h"
+#include "skm_caller.h"
+#include "skm_front.h"
+
+using namespace skmf;
+
+namespace {
+
+const int K = 8;
+const unsigned MaxSequencesPerFile = 100000;
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void die(const std::string& m) {
+    std::cerr << m << "\n";
+    std::exit(1);
+}
+
+std::string kmer_str(uint64_t k) {
+    char b[9];
+    std::memcpy(b, &k, 8);
+    b[8] = 0;
+    return std::string(b, 8);
+}
+
+std::string quoted(const std::string& p) { return "\"" + p + "\""; }
+
+// binary dump of the build input (--dump-extract): u64 n_seqs, u64 n_residues, then
+// residues[n_residues], off u64[n], len u32[n], func u16[n], seq_id u32[n]
+void dump_extract(const std::string& path, const std::vector<FastaFile>& files, const std::vector<BuildBatch>& batches) {
+    std::vector<uint8_t> res;
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len, sid;
+    std::vector<uint16_t> fn;
+    for (size_t f = 0; f < files.size(); ++f) {
+        const BuildBatch& b = batches[f];
+        for (size_t s = 0; s < b.off.size(); ++s) {
+            off.push_back(res.size());
+            res.insert(res.end(), files[f].residues.begin() + b.off[s], files[f].residues.begin() + b.off[s] + b.len[s]);
+            len.push_back(b.len[s]);
+            fn.push_back(b.func[s]);
+            sid.push_back(b.seq_id[s]);
+        }
+    }
+    std::ofstream o(path, std::ios::binary);
+    uint64_t n = off.size(), nr = res.size();
+    o.write((const char*)&n, 8);
+    o.write((const char*)&nr, 8);
+    o.write((const char*)res.data(), (std::streamsize)nr);
+    o.write((const char*)off.data(), (std::streamsize)(8 * n));
+    o.write((const char*)len.data(), (std::streamsize)(4 * n));
+    o.write((const char*)fn.data(), (std::streamsize)(2 * n));
+    o.write((const char*)sid.data(), (std::streamsize)(4 * n));
+    if (!o) die("cannot write " + path);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    Options op;
+    op.specs = {{"definition-dir", 'D', false, true},  {"fasta-dir", 'F', false, true},
+                {"fasta-keep-functions-dir", 'K', false, true}, {"good-functions", 0, false, true},
+                {"good-roles", 0, false, true},        {"deleted-features-file", 0, false, false},
+                {"ignored-functions-file", 0, false, false}, {"kmer-data-dir", 0, false, false},
+                {"nudb-file", 0, false, false},        {"min-reps-required", 0, false, false},
+                {"final-kmers", 0, false, false},      {"n-threads", 0, false, false},
+                {"perfect-hash", 0, false, false},     {"perfect-hash-data", 0, false, false},
+                {"help", 'h', true, false},            {"device", 0, false, false},
+                {"dump-extract", 0, false, false},     {"mph-seed", 0, false, false}};
+    std::string err;
+    if (!op.parse(argc, argv, err)) die(err);
+    if (op.has("help")) {
+        std::cout << "Usage: " << argv[0] << " [options]\nAllowed options:\n"
+                  << "  -D [ --definition-dir ] arg          Directory of function definition files\n"
+                  << "  -F [ --fasta-dir ] arg               Directory of fasta files of protein data\n"
+                  << "  -K [ --fasta-keep-functions-dir ] arg Directory of fasta files of protein data (keep functions defined here)\n"
+                  << "  --good-functions arg                 File containing list of functions to be kept\n"
+                  << "  --good-roles arg                     File containing list of roles to be kept\n"
+                  << "  --deleted-features-file arg          File containing list of deleted feature IDs\n"
+                  << "  --ignored-functions-file arg         File containing list of functions for which we do not create signatures\n"
+                  << "  --kmer-data-dir arg                  Write kmer data files to this directory\n"
+                  << "  --min-reps-required arg              Minimum number of genomes a function must be seen in\n"
+                  << "  --final-kmers arg                    Write final.kmers file\n"
+                  << "  --n-threads arg                      Number of host threads (results do not depend on it)\n"
+                  << "  --perfect-hash arg                   Compute perfect hash of signature kmers and store in this file\n"
+                  << "  --perfect-hash-data arg              Kmer data stored by perfect hash\n"
+                  << "  --device arg                         HIP device ordinal (default 0)\n"
+                  << "  -h [ --help ]                        show this help message\n";
+        return 1;
+    }
+    const double t_start = now_s();
+    // host threads for parsing / find_best_call only: results never depend on it
+    int n_threads = std::atoi(op.get("n-threads", "0").c_str());
+    if (n_threads < 2) n_threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const int device = std::atoi(op.get("device", "0").c_str());
+    const int min_reps_required = std::atoi(op.get("min-reps-required", "3").c_str());
+    const std::string kmer_data_dir = op.get("kmer-data-dir");
+    std::string final_kmers = op.get("final-kmers");
+    std::string ph_file = op.get("perfect-hash"), ph_data = op.get("perfect-hash-data");
+
+    std::vector<std::string> definition_files, fasta_files, keep_files;
+    auto populate = [&](const std::vector<std::string>& dirs, std::vector<std::string>& out) {
+        for (const auto& d : dirs)
+            if (!list_regular_files(d, out, err)) die(err);
+    };
+    populate(op.all("definition-dir"), definition_files);
+    populate(op.all("fasta-dir"), fasta_files);
+    populate(op.all("fasta-keep-functions-dir"), keep_files);
+    std::cout << "definitions: ";
+    for (auto& x : op.all("definition-dir")) std::cout << x << " ";
+    std::cout << std::endl << "fasta: ";
+    for (auto& x : op.all("fasta-dir")) std::cout << x << " ";
+    std::cout << std::endl << "keep: ";
+    for (auto& x : op.all("fasta-keep-functions-dir")) std::cout << x << " ";
+    std::cout << std::endl;
+
+    std::vector<std::string> good_functions, good_roles;
+    for (auto& f : op.all("good-functions")) {
+        bool ok;
+        auto v = load_lines(f, &ok);
+        if (!ok) std::cerr << "could not open " << f << "\n";
+        good_functions.insert(good_functions.end(), v.begin(), v.end());
+    }
+    for (auto& f : op.all("good-roles")) {
+        bool ok;
+        auto v = load_lines(f, &ok);
+        if (!ok) std::cerr << "could not open " << f << "\n";
+        good_roles.insert(good_roles.end(), v.begin(), v.end());
+    }
+
+    FunctionMap fm;
+    fm.add_good_roles(good_roles);
+    fm.add_good_functions(good_functions);
+    for (auto& d : definition_files) fm.load_id_assignments(d);
+
+    std::set<std::string> deleted_fids, ignored_functions;
+    if (op.has("deleted-features-file"))
+        for (auto& l : load_lines(op.get("deleted-features-file"))) deleted_fids.insert(l);
+    if (op.has("ignored-functions-file"))
+        for (auto& l : load_lines(op.get("ignored-functions-file"))) ignored_functions.insert(l);
+
+    if (!kmer_data_dir.empty() && !ensure_directory(kmer_data_dir)) die("Error creating " + quoted(kmer_data_dir));
+
+    // all_fasta_data_ = fasta-dir files, then keep-dir files (signature_build.tcc:26-35)
+    std::cerr << "load fasta\n";
+    std::vector<std::string> all_paths = fasta_files;
+    all_paths.insert(all_paths.end(), keep_files.begin(), keep_files.end());
+    std::vector<FastaFile> files;
+    double t0 = now_s();
+    if (!parse_fasta_files(all_paths, files, n_threads, err)) die(err);
+    try {
+        for (auto& f : files) fm.load_fasta_file(f, deleted_fids);
+    } catch (const std::exception& e) {
+        die(std::string("terminate called after throwing an instance of 'std::out_of_range': ") + e.what());
+    }
+    const double t_parse = now_s() - t0;
+
+    unsigned nkept_f = fm.process_kept_functions(min_reps_required, ignored_functions);
+    std::cout << "kept " << nkept_f << " functions\n";
+    if (!kmer_data_dir.empty()) {
+        if (!fm.write_function_index(kmer_data_dir)) die("cannot write function.index");
+        std::ofstream(path_join(kmer_data_dir, "otu.index")).close();
+        std::ofstream g(path_join(kmer_data_dir, "genomes"));
+        g << "empty genomes\n";
+    }
+
+    std::cerr << "extract kmers\n";
+    std::vector<BuildBatch> batches(files.size());
+    for (size_t f = 0; f < files.size(); ++f)
+        select_build_sequences(fm, files[f], (unsigned)f, MaxSequencesPerFile, deleted_fids, batches[f]);
+    if (op.has("dump-extract")) {
+        dump_extract(op.get("dump-extract"), files, batches);
+        std::cerr << "wrote build input to " << op.get("dump-extract") << "\n";
+        return 0;
+    }
+
+    skm_build* b = nullptr;
+    skm_build_opts bo{};
+    bo.k = K;
+    bo.max_seqs_per_file = MaxSequencesPerFile;
+    bo.n_functions = std::max(1u, nkept_f);
+    bo.canonical_order = 1;
+    bo.rank = 0;
+    bo.world_size = 1;
+    auto check = [](int rc, const char* what) {
+        if (rc) die(std::string(what) + ": " + skm_last_error());
+    };
+    check(skm_build_create(&b, &device, 1, &bo), "skm_build_create");
+    for (size_t f = 0; f < files.size(); ++f) {
+        const BuildBatch& bb = batches[f];
+        if (bb.off.empty()) continue;
+        check(skm_build_add_batch(b, files[f].residues.data(), bb.off.data(), bb.len.data(), bb.func.data(),
+                                  bb.seq_id.data(), bb.off.size()),
+              "skm_build_add_batch");
+    }
+    std::cerr << "process kmers\n";
+    t0 = now_s();
+    check(skm_build_prepare(b), "skm_build_prepare");
+    skm_kept kept{};
+    check(skm_build_finish(b, &kept), "skm_build_finish");
+    float ph[12] = {0};
+    int nph = skm_build_last_timings(b, ph, 12);
+    const double t_build = now_s() - t0;
+    skm_build_destroy(b);
+    std::cout << "Kept " << kept.n << " kmers\n";
+    std::cout << "distinct_signatures=" << kept.distinct_signatures << "\n";
+    std::cout << "num_seqs_with_a_signature=" << kept.n_seqs_with_signature << "\n";
+
+    std::thread final_kmers_thread;
+    if (!final_kmers.empty()) {
+        if (path_is_relative(final_kmers)) {
+            final_kmers = path_join(kmer_data_dir, final_kmers);
+            std::cerr << "Updated final_kmers to " << quoted(final_kmers) << "\n";
+        }
+        final_kmers_thread = std::thread([&]() {
+            std::cerr << "writing kmers to " << quoted(final_kmers) << "\n";
+            std::ofstream kf(final_kmers);
+            std::string buf;
+            buf.reserve(1 << 20);
+            char line[64];
+            for (uint64_t i = 0; i < kept.n; ++i) {
+                int l = std::snprintf(line, sizeof line, "%s\t%u\t%u\t\n", kmer_str(kept.keys[i]).c_str(),
+                                      (unsigned)kept.data[i].avg_from_end, (unsigned)kept.data[i].function_index);
+                buf.append(line, (size_t)l);
+                if (buf.size() > (1 << 20) - 64) {
+                    kf.write(buf.data(), (std::streamsize)buf.size());
+                    buf.clear();
+                }
+            }
+            kf.write(buf.data(), (std::streamsize)buf.size());
+            std::cerr << "writing kmers to " << quoted(final_kmers) << " complete\n";
+        });
+    }
+
+    {
+        std::ofstream df(path_join(kmer_data_dir, "distinct_functions"));
+        for (uint32_t f = 0; f < kept.n_functions; ++f)
+            if (kept.distinct_functions[f]) df << f << "\t" << fm.lookup_function((uint16_t)f) << "\t" << kept.distinct_functions[f] << "\n";
+    }
+
+    const std::string report_dir = path_join(kmer_data_dir, "recall.report.d");
+    if (mkdir(report_dir.c_str(), 0777) != 0) std::cerr << "mkdir " << quoted(report_dir) << " failed\n";
+    const std::string fi_file = path_join(kmer_data_dir, "function.index");
+
+    std::thread perfect_hash_thread;
+    int ph_rc = 0;
+    std::string ph_err;
+    if (!ph_file.empty()) {
+        if (path_is_relative(ph_file)) ph_file = path_join(kmer_data_dir, ph_file);
+        if (path_is_relative(ph_data)) ph_data = path_join(kmer_data_dir, ph_data);
+        const uint32_t seed = (uint32_t)std::strtoul(op.get("mph-seed", "1").c_str(), nullptr, 10);
+        perfect_hash_thread = std::thread([&, seed]() {
+            std::cerr << "build perfect hash into " << quoted(ph_file) << " with data in " << quoted(ph_data) << "\n";
+            ph_rc = skm_mph_build(kept.keys, kept.data, kept.n, seed, ph_file.c_str(), ph_data.c_str());
+            if (ph_rc)
+                ph_err = skm_last_error();
+            else
+                std::cerr << "Wrote " << kept.n << " values\n";
+        });
+    }
+
+    // recall of the training sequences with the new k-mers (kmers-build-signatures.cc:238-349)
+    std::vector<std::string> fidx;
+    if (!read_function_index(fi_file, fidx, err)) die(err);
+    std::cerr << "Begin recall\n";
+    t0 = now_s();
+    skm_db* kdb = nullptr;
+    check(skm_db_open_kept(&kdb, kept.keys, kept.data, kept.n, device), "skm_db_open_kept");
+    std::vector<const FastaFile*> fptr;
+    for (auto& f : files) fptr.push_back(&f);
+    std::vector<std::vector<SeqCall>> calls;
+    double recall_dev_ms = 0;
+    if (call_files(kdb, fptr, fidx, false, n_threads, calls, err, &recall_dev_ms)) die(err);
+    skm_db_close(kdb);
+    for (size_t f = 0; f < files.size(); ++f) {
+        std::map<std::string, std::string> data;  // saver::data (first emplace wins), sorted by id
+        for (size_t r = 0; r < files[f].size(); ++r) {
+            const std::string& id = files[f].ids[r];
+            const SeqCall& c = calls[f][r];
+            std::string orig, orig_stripped;
+            fm.lookup_original_assignment(id, orig, orig_stripped);
+            if (orig_stripped != c.func && !data.count(id))
+                data.emplace(id, id + "\t" + orig + "\t" + orig_stripped + "\t" + c.func + "\t" +
+                                     std::to_string((int)c.fi) + "\t" + fmt_g(c.score) + "\n");
+        }
+        std::ofstream of(path_join(report_dir, files[f].filename));
+        for (auto& e : data) of << e.second;
+    }
+    const double t_recall = now_s() - t0;
+
+    if (op.has("nudb-file")) std::cerr << "--nudb-file: NuDB output is not supported by this build; skipped\n";
+    if (perfect_hash_thread.joinable()) {
+        std::cerr << "Awaiting completion of perfect hash creation\n";
+        perfect_hash_thread.join();
+        if (ph_rc) die("perfect hash: " + ph_err);
+    }
+    if (final_kmers_thread.joinable()) {
+        std::cerr << "Awaiting completion of final kmers dump\n";
+        final_kmers_thread.join();
+    }
+    skm_kept_free(&kept);
+    std::cerr << "timing: parse " << t_parse << " s, build " << t_build << " s (device pipeline "
+              << (nph > 7 ? ph[7] : 0.0f) << " ms), recall " << t_recall << " s, total " << now_s() - t_start << " s\n";
+    std::cerr << "all done\n";
+    return 0;
+}

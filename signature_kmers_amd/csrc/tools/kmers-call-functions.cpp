@@ -1,0 +1,165 @@
+// kmers-call-functions -- drop-in for the reference's main (kmers-call-functions.cc:34-197).
+//
+//   kmers-call-functions [options] data-dir input-file [input-file ...]
+// Opens <data-dir>/kmer_data.mph + .dat (CmphKmerDb, cmph_kmer.h) into HBM, reads
+// <data-dir>/function.index, and writes one line per query sequence
+// "id\tfunc\tfunc_index\tscore\n" (kmers-call-functions.cc:178), files in input order, to -o or
+// stdout.  Window lookups and HitSet calls run on the GPU (skm_annotate), find_best_call on host.
+// --debug-hits prints the per-hit lines of the reference's debug hit callback
+// (kmers-call-functions.cc:109-118) before each file's calls.
+// Extra options: --device N.
+#include <sys/stat.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <thread>
+
+#include "skm.h"
+#include "skm_caller.h"
+#include "skm_front.h"
+
+using namespace skmf;
+
+namespace {
+
+void die(const std::string& m) {
+    std::cerr << m << "\n";
+    std::exit(1);
+}
+
+bool file_exists(const std::string& p) {
+    struct stat sb;
+    return stat(p.c_str(), &sb) == 0;
+}
+
+// --debug-hits: hit stream of FunctionCaller::process_aa_seq (for_each_kmer + fetch + the hypo
+// filter), printed as the reference's hit_cb does.
+void debug_hits(skm_db* db, const std::vector<uint8_t>& dat, const FastaFile& f, const std::vector<std::string>& fidx,
+                bool ignore_hypo, int hypo, std::ostream& os) {
+    uint32_t m = 0;
+    skm_db_size(db, &m);
+    for (size_t r = 0; r < f.size(); ++r) {
+        const uint8_t* s = f.residues.data() + f.off[r];
+        const uint32_t len = f.len[r];
+        std::vector<uint64_t> keys;
+        std::vector<uint32_t> pos;
+        // for_each_kmer<8> (kmer_data.h:76-102)
+        auto is_amb = [](uint8_t c) { return c == '*' || c == 'X'; };
+        uint32_t p = 0;
+        uint32_t na = 0;
+        while (na < len && !is_amb(s[na])) ++na;
+        while (len >= 8 && p <= len - 8) {
+            if (na != len && p + 8 >= na) {
+                p = na + 1;
+                na = p;
+                while (na < len && !is_amb(s[na])) ++na;
+                continue;
+            }
+            uint64_t k;
+            std::memcpy(&k, s + p, 8);
+            keys.push_back(k);
+            pos.push_back(p);
+            ++p;
+        }
+        std::vector<uint32_t> idx(keys.size());
+        if (!keys.empty() && skm_db_lookup(db, keys.data(), keys.size(), idx.data())) die(skm_last_error());
+        for (size_t i = 0; i < keys.size(); ++i) {
+            if (idx[i] >= m) continue;
+            skm_stored_kmer_data kd;
+            std::memcpy(&kd, dat.data() + 10ull * idx[i], 10);
+            if (ignore_hypo && kd.function_index == hypo) continue;
+            char kb[9];
+            std::memcpy(kb, &keys[i], 8);
+            kb[8] = 0;
+            const std::string fn = kd.function_index < fidx.size() ? fidx[kd.function_index] : "";
+            os << kb << "\t" << pos[i] << "\t" << fn << "\t" << kd.median << "\t" << kd.mean << "\t" << kd.var << "\t"
+               << fmt_g(std::sqrt((double)kd.var)) << "\t" << "\n";
+        }
+    }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    Options op;
+    op.specs = {{"data-dir", 'd', false, false}, {"input-files", 'i', false, true}, {"output-files", 'o', false, false},
+                {"n-threads", 'j', false, false}, {"ignore-hypo", 0, true, false},  {"debug-hits", 0, true, false},
+                {"help", 'h', true, false},       {"device", 0, false, false}};
+    op.positional = {"data-dir", "input-files"};
+    std::string err;
+    if (!op.parse(argc, argv, err)) die(err);
+    auto usage = [&]() {
+        std::cout << "Usage: " << argv[0] << " data-dir input-file [input-file, ...]\nAllowed options:\n"
+                  << "  -d [ --data-dir ] arg       Data directory\n"
+                  << "  -i [ --input-files ] arg    Input files\n"
+                  << "  -o [ --output-files ] arg   Output file\n"
+                  << "  -j [ --n-threads ] arg      Number of threads\n"
+                  << "  --ignore-hypo               Ignore hypothetical protein kmers when making calls\n"
+                  << "  --debug-hits                Debug kmer hits\n"
+                  << "  --device arg                HIP device ordinal (default 0)\n"
+                  << "  -h [ --help ]               show this help message\n\n";
+    };
+    if (op.has("help")) {
+        usage();
+        return 0;
+    }
+    std::vector<std::string> inputs = op.all("input-files");
+    if (inputs.empty()) {
+        usage();
+        return 1;
+    }
+    std::cerr << "Data size " << sizeof(skm_stored_kmer_data) << "\n";
+    int n_threads = std::atoi(op.get("n-threads", "0").c_str());
+    if (n_threads < 2) n_threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const int device = std::atoi(op.get("device", "0").c_str());
+    const std::string data_dir = op.get("data-dir");
+    const std::string db_base = path_join(data_dir, "kmer_data");
+    const std::string mph = db_base + ".mph", dat = db_base + ".dat";
+    if (!file_exists(mph)) die("Database \"" + db_base + "\" does not exist");
+    skm_db* db = nullptr;
+    if (skm_db_open(&db, mph.c_str(), dat.c_str(), device)) die(skm_last_error());
+    std::vector<std::string> fidx;
+    if (!read_function_index(path_join(data_dir, "function.index"), fidx, err)) die(err);
+    const bool ignore_hypo = op.has("ignore-hypo");
+
+    std::vector<FastaFile> files;
+    if (!parse_fasta_files(inputs, files, n_threads, err)) die(err);
+    std::vector<const FastaFile*> fptr;
+    for (auto& f : files) fptr.push_back(&f);
+    std::vector<std::vector<SeqCall>> calls;
+    if (call_files(db, fptr, fidx, ignore_hypo, n_threads, calls, err)) die(err);
+
+    std::ofstream ofs;
+    std::ostream* out = &std::cout;
+    if (op.has("output-files")) {
+        ofs.open(op.get("output-files"));
+        if (!ofs) die("cannot write " + op.get("output-files"));
+        out = &ofs;
+    }
+    std::vector<uint8_t> datbuf;
+    int hypo = -1;
+    if (op.has("debug-hits")) {
+        std::ifstream df(dat, std::ios::binary);
+        datbuf.assign(std::istreambuf_iterator<char>(df), std::istreambuf_iterator<char>());
+        for (size_t i = 0; i < fidx.size(); ++i)
+            if (fidx[i] == "hypothetical protein") {
+                hypo = (int)i;
+                break;
+            }
+    }
+    for (size_t f = 0; f < files.size(); ++f) {
+        if (op.has("debug-hits")) debug_hits(db, datbuf, files[f], fidx, ignore_hypo, hypo, std::cout);
+        std::string buf;
+        for (size_t r = 0; r < files[f].size(); ++r) {
+            const SeqCall& c = calls[f][r];
+            buf += files[f].ids[r] + "\t" + c.func + "\t" + std::to_string((unsigned)c.fi) + "\t" + fmt_g(c.score) + "\n";
+        }
+        *out << buf;
+    }
+    out->flush();
+    skm_db_close(db);
+    return 0;
+}

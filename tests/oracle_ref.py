@@ -48,6 +48,9 @@ def olib():
         _lib.oracle_jenkins_hash_vector.argtypes = [C.c_uint32, P, C.c_uint32, P]
         _lib.oracle_annotate.restype = C.c_int64
         _lib.oracle_annotate.argtypes = [P, P, P, P, P, C.c_uint64, C.POINTER(AnnotOpts), P, P, C.c_uint64]
+        _lib.oracle_annotate_exact.restype = C.c_int64
+        _lib.oracle_annotate_exact.argtypes = [P, P, C.c_uint64, P, P, P, C.c_uint64, C.POINTER(AnnotOpts), P, P,
+                                               C.c_uint64]
         _lib.oracle_find_best_call.argtypes = [P, C.c_uint64, C.POINTER(C.c_char_p), C.c_uint64, P, P, P,
                                                C.c_char_p, C.c_uint64]
     return _lib
@@ -132,6 +135,25 @@ def annotate(bdz: Bdz, dat: bytes, residues, seq_off, seq_len, min_hits=5, max_g
     opts = AnnotOpts(min_hits, max_gap, ignore_hypo, hypo_index, mean_mode, mad_mode)
     tot = olib().oracle_annotate(bdz.h, _p(datb), _p(residues), _p(seq_off), _p(seq_len), n, C.byref(opts), _p(off),
                                  _p(calls), cap)
+    assert tot >= 0
+    return off, calls[:tot].copy()
+
+
+def annotate_exact(keys, data, residues, seq_off, seq_len, min_hits=5, max_gap=200, ignore_hypo=0,
+                   hypo_index=-1, mean_mode=0, mad_mode=0):
+    """process_aa_seq against KeptKmerDB (exact keys; keys sorted ascending, data[i] for keys[i])."""
+    keys = np.ascontiguousarray(keys, np.uint64)
+    data = np.ascontiguousarray(data, STORED_DTYPE)
+    residues = np.ascontiguousarray(residues, np.uint8)
+    seq_off = np.ascontiguousarray(seq_off, np.uint64)
+    seq_len = np.ascontiguousarray(seq_len, np.uint32)
+    n = len(seq_len)
+    off = np.zeros(n + 1, np.uint64)
+    cap = int(seq_len.astype(np.int64).sum()) + 16
+    calls = np.zeros(cap, CALL_DTYPE)
+    opts = AnnotOpts(min_hits, max_gap, ignore_hypo, hypo_index, mean_mode, mad_mode)
+    tot = olib().oracle_annotate_exact(_p(keys), _p(data), len(keys), _p(residues), _p(seq_off), _p(seq_len), n,
+                                       C.byref(opts), _p(off), _p(calls), cap)
     assert tot >= 0
     return off, calls[:tot].copy()
 

@@ -83,3 +83,27 @@ def test_query_edge_cases(skm, gpu, tmp_path):
                                        hypo_index=funcs.index("hypothetical protein"))
     np.testing.assert_array_equal(goff, ooff)
     np.testing.assert_array_equal(gcalls.view(np.uint8), ocalls.view(np.uint8))
+
+
+def test_kept_db_exact_lookup_and_recall_calls(skm, gpu, tmp_path):
+    """KeptKmerDB (exact keys): members hit their own record, strangers miss; the call path over
+    it equals the oracle's recall-pass restatement (kept_kmer_db.h:20-27)."""
+    ref, funcs, _, _, p = make_db(skm, tmp_path, n_seqs=2000, fam=50, seed=5)
+    db = skm.KeptKmerDb(ref["keys"], ref["data"])
+    n = len(ref["keys"])
+    assert db.hash_size() == n
+    np.testing.assert_array_equal(db.lookup_keys(ref["keys"]), np.arange(n, dtype=np.uint32))
+    rng = np.random.default_rng(11)
+    strangers = rng.integers(1, 2**63, size=100000, dtype=np.uint64)
+    strangers = strangers[~np.isin(strangers, ref["keys"])]
+    assert (db.lookup_keys(strangers) == n).all()
+    hypo = funcs.index("hypothetical protein")
+    caller = skm.FunctionCaller(db, funcs)
+    off, calls = caller.process_seqs(p.residues, p.seq_off, p.seq_len)
+    ooff, ocalls = oracle_ref.annotate_exact(ref["keys"], ref["data"], p.residues, p.seq_off, p.seq_len,
+                                             hypo_index=hypo)
+    assert len(calls) > 100
+    np.testing.assert_array_equal(off, ooff)
+    np.testing.assert_array_equal(calls.view(np.uint8), ocalls.view(np.uint8))
+    empty = skm.KeptKmerDb(np.zeros(0, np.uint64), np.zeros(0, skm.STORED_DTYPE))
+    assert (empty.lookup_keys(ref["keys"][:10]) == 0).all()

@@ -1,0 +1,162 @@
+"""GPU tests of the drop-in CLIs (bin/kmers-build-signatures, kmers-call-functions,
+kmers-annotate-seqs) end to end against the oracle: every output file of the reference mains,
+byte for byte (final.kmers / distinct_functions compared as line sets: the reference writes them
+in hash-table order)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import front_data
+import oracle_ref
+from conftest import ROOT
+
+import oracle.front_ref as fr  # noqa: E402  (test infrastructure)
+
+BIN = os.path.join(ROOT, "bin")
+pytestmark = pytest.mark.gpu
+
+
+def _lines(path):
+    with open(path, "rb") as fh:
+        return fh.read()
+
+
+def _fidx(out):
+    t = []
+    for line in _lines(os.path.join(out, "function.index")).split(b"\n"):
+        if line:
+            c = line.split(b"\t")
+            i = int(c[0])
+            t += [""] * (i + 1 - len(t))
+            t[i] = c[1].decode("latin-1")
+    return t
+
+
+def _check_build(out, stdout, ref):
+    res, off, ln, fn, sid = ref["build"]
+    nf = ref["n_kept_functions"]
+    o = oracle_ref.build(res, off, ln, fn, sid, nf)
+    assert f"kept {nf} functions\n" in stdout
+    assert f"Kept {len(o['keys'])} kmers\n" in stdout
+    assert f"distinct_signatures={o['distinct_signatures']}\n" in stdout
+    assert f"num_seqs_with_a_signature={o['n_seqs_with_signature']}\n" in stdout
+    assert _lines(os.path.join(out, "function.index")) == ref["fm"].function_index_text()
+    exp = set()
+    for k, d in zip(o["keys"], o["data"]):
+        exp.add(b"%s\t%d\t%d\t" % (int(k).to_bytes(8, "little"), d["avg_from_end"], d["function_index"]))
+    got = _lines(os.path.join(out, "final.kmers")).split(b"\n")
+    assert got[-1] == b""
+    assert len(got) - 1 == len(exp) and set(got[:-1]) == exp
+    dfl = set()
+    for f in range(nf):
+        if o["distinct_functions"][f]:
+            dfl.add(b"%d\t%s\t%d" % (f, ref["fm"].idxf[f], o["distinct_functions"][f]))
+    got = _lines(os.path.join(out, "distinct_functions")).split(b"\n")
+    assert set(got[:-1]) == dfl and len(got) - 1 == len(dfl)
+    # kmer_data.mph / .dat: every kept k-mer finds its record through the BDZ hash
+    bdz = oracle_ref.Bdz(_lines(os.path.join(out, "kmer_data.mph")))
+    assert bdz.size() == len(o["keys"])
+    dat = np.frombuffer(_lines(os.path.join(out, "kmer_data.dat")), oracle_ref.STORED_DTYPE)
+    idx = bdz.search(o["keys"])
+    assert np.array_equal(dat[idx].view(np.uint8), o["data"].view(np.uint8))
+    # recall.report.d/<fasta file name>
+    fidx = _fidx(out)
+    for path, recs in ref["files"]:
+        want = fr.recall_report(oracle_ref, ref["fm"], recs, fidx, o["keys"], o["data"])
+        assert _lines(os.path.join(out, "recall.report.d", os.path.basename(path))) == want, path
+    return o
+
+
+def _run(cmd):
+    p = subprocess.run(cmd, capture_output=True, timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    return p.stdout.decode(), p.stderr.decode()
+
+
+@pytest.fixture(scope="module")
+def edge_build(tmp_path_factory, gpu):
+    tmp = tmp_path_factory.mktemp("cli_edge")
+    d = front_data.write_edge_dirs(str(tmp / "in"))
+    out = str(tmp / "kd")
+    stdout, _ = _run([os.path.join(BIN, "kmers-build-signatures")] + front_data.front_args(d) + [
+        "--kmer-data-dir", out, "--final-kmers", "final.kmers", "--perfect-hash", "kmer_data.mph",
+        "--perfect-hash-data", "kmer_data.dat"])
+    ref = fr.front([d["defs"]], [d["seqs"]], [d["keep"]], fr.read_lines(d["good_functions"]),
+                   fr.read_lines(d["good_roles"]), fr.read_lines(d["deleted"]), fr.read_lines(d["ignored"]),
+                   min_reps=2)
+    return d, out, stdout, ref
+
+
+def test_build_signatures_edge_inputs(edge_build):
+    d, out, stdout, ref = edge_build
+    _check_build(out, stdout, ref)
+    assert os.path.getsize(os.path.join(out, "otu.index")) == 0
+
+
+@pytest.fixture(scope="module")
+def c1_build(tmp_path_factory, gpu):
+    from signature_kmers_amd import synth
+    tmp = tmp_path_factory.mktemp("cli_c1")
+    info = synth.write_dirs(str(tmp / "in"), 1000, 40, per_file=100, extras=True)
+    out = str(tmp / "kd")
+    stdout, _ = _run([os.path.join(BIN, "kmers-build-signatures"), "-D", info["ann_dir"], "-F", info["seqs_dir"],
+                      "--kmer-data-dir", out, "--final-kmers", "final.kmers", "--perfect-hash", "kmer_data.mph",
+                      "--perfect-hash-data", "kmer_data.dat"])
+    ref = fr.front([info["ann_dir"]], [info["seqs_dir"]])
+    return info, out, stdout, ref
+
+
+def test_build_signatures_c1(c1_build):
+    info, out, stdout, ref = c1_build
+    o = _check_build(out, stdout, ref)
+    assert len(o["keys"]) > 1000
+    n_rep = sum(1 for f in os.listdir(os.path.join(out, "recall.report.d")))
+    assert n_rep == len(ref["files"])
+
+
+def _query_dir(tmp, seed=5):
+    from signature_kmers_amd import synth
+    q = synth.write_dirs(str(tmp), 400, 40, per_file=100, seed=seed, extras=True, genome_base=200000)
+    return q["seqs_dir"]
+
+
+@pytest.mark.parametrize("ignore_hypo", [False, True])
+def test_call_functions_matches_oracle(c1_build, tmp_path, ignore_hypo):
+    info, out, _, _ = c1_build
+    qdir = _query_dir(tmp_path / "q")
+    inputs = sorted(os.path.join(qdir, f) for f in os.listdir(qdir))
+    cmd = [os.path.join(BIN, "kmers-call-functions"), out] + inputs + ["-o", str(tmp_path / "calls.txt")]
+    if ignore_hypo:
+        cmd.append("--ignore-hypo")
+    _run(cmd)
+    bdz = oracle_ref.Bdz(_lines(os.path.join(out, "kmer_data.mph")))
+    dat = _lines(os.path.join(out, "kmer_data.dat"))
+    fidx = _fidx(out)
+    want = b""
+    for p in inputs:
+        recs = fr.parse_fasta(_lines(p))
+        w, _ = fr.call_lines(oracle_ref, recs, fidx, bdz, dat, ignore_hypo=ignore_hypo)
+        want += w
+    got = _lines(str(tmp_path / "calls.txt"))
+    assert got == want
+    assert got.count(b"\n") == sum(len(fr.parse_fasta(_lines(p))) for p in inputs)
+    assert b"\tfunction " in got  # some sequences are called
+
+
+def test_annotate_seqs_matches_oracle(c1_build, tmp_path):
+    info, out, _, _ = c1_build
+    qdir = _query_dir(tmp_path / "q", seed=9)
+    calls, unc = str(tmp_path / "calls"), str(tmp_path / "uncalled")
+    _run([os.path.join(BIN, "kmers-annotate-seqs"), out, str(tmp_path / "genus"), qdir, calls, unc])
+    bdz = oracle_ref.Bdz(_lines(os.path.join(out, "kmer_data.mph")))
+    dat = _lines(os.path.join(out, "kmer_data.dat"))
+    fidx = _fidx(out)
+    wc, wu = b"", b""
+    for p in fr.list_files(qdir):
+        c, u = fr.call_lines(oracle_ref, fr.parse_fasta(_lines(p)), fidx, bdz, dat, annotate_mode=True)
+        wc += c
+        wu += u
+    assert _lines(calls) == wc
+    assert _lines(unc) == wu
