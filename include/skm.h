@@ -184,6 +184,13 @@ void skm_db_close(skm_db* db);
 int skm_mph_build(const uint64_t* keys, const skm_stored_kmer_data* data, size_t n, uint32_t seed,
                   const char* mph_path, const char* dat_path);
 
+/* skm_mph_build with the construction on a GPU: same parameters and image format, the
+ * 3-hypergraph peeled in parallel rounds and g assigned round by round on `device`, the rank
+ * table and records placed from the device lookup.  Deterministic for a given (keys, seed).
+ * device < 0 (or fewer than 1024 keys) runs the host builder.                                */
+int skm_mph_build_device(const uint64_t* keys, const skm_stored_kmer_data* data, size_t n, uint32_t seed,
+                         const char* mph_path, const char* dat_path, int device);
+
 /* ------------------------------------------------------------------------------------------
  * Function calling.  Replaces FunctionCaller<CmphKmerDb>::process_aa_seq for a batch of query
  * sequences (call_functions.tcc:259-338 + HitSet :6-108, window iterator kmer_data.h:76-102).

@@ -87,6 +87,7 @@ _SIGS = {
     "skm_db_lookup": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "skm_db_close": (None, [_P]),
     "skm_mph_build": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_char_p, C.c_char_p]),
+    "skm_mph_build_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_char_p, C.c_char_p, C.c_int]),
     "skm_query_create": (C.c_int, [C.POINTER(_P), _P, _P, _P, _P, C.c_size_t]),
     "skm_query_run": (C.c_int, [_P, C.POINTER(_AnnotOpts)]),
     "skm_query_last_timings": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int]),
@@ -295,11 +296,17 @@ def group_run(builders) -> None:
     _check(lib().skm_build_group_run(arr, len(builders)))
 
 
-def mph_build(keys: np.ndarray, data: np.ndarray, mph_path: str, dat_path: str, seed: int = 1):
-    """build_perfect_hash (perfect_hash.h:11-69): cmph-compatible BDZ .mph + dense .dat."""
+def mph_build(keys: np.ndarray, data: np.ndarray, mph_path: str, dat_path: str, seed: int = 1,
+              device: int | None = None):
+    """build_perfect_hash (perfect_hash.h:11-69): cmph-compatible BDZ .mph + dense .dat.
+    device=None: host construction; device=d: parallel peeling on GPU d."""
     keys = np.ascontiguousarray(keys, dtype=np.uint64)
     data = np.ascontiguousarray(data, dtype=STORED_DTYPE)
-    _check(lib().skm_mph_build(_ptr(keys), _ptr(data), len(keys), seed, mph_path.encode(), dat_path.encode()))
+    if device is None:
+        _check(lib().skm_mph_build(_ptr(keys), _ptr(data), len(keys), seed, mph_path.encode(), dat_path.encode()))
+    else:
+        _check(lib().skm_mph_build_device(_ptr(keys), _ptr(data), len(keys), seed, mph_path.encode(),
+                                          dat_path.encode(), device))
 
 
 class CmphKmerDb:

@@ -15,7 +15,9 @@
 
 #include <algorithm>
 #include <cstring>
+#include <cmath>
 #include <fstream>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -925,3 +927,284 @@ void skm_calls_free(skm_calls* c) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// BDZ construction on the device (build_perfect_hash, perfect_hash.h:11-69, via cmph_new
+// CMPH_BDZ): same parameters as the host builder (r = ceil(1.23 m / 3) made odd, n = 3r,
+// jenkins seeds from mt19937(seed)), 3-hypergraph peeled in parallel rounds:
+//   k_mph_edges     one thread per key: 3 vertices, degree += 1, incident-edge XOR ^= e
+//   k_mph_frontier  vertices of degree 1
+//   k_mph_peel      a frontier vertex v peels its only edge e iff v is the first degree-1
+//                   vertex of e (deterministic: one peeler per edge, no atomics on e)
+//   k_mph_apply     the peeled edges leave their vertices; vertices that drop to degree 1 form
+//                   the next frontier
+//   k_mph_assign    rounds in reverse: the free vertex gets (position - g[u1] - g[u2]) mod 3
+//                   (unassigned = 3 = 0 mod 3); edges of one round never share a free vertex
+//                   and their other vertices were freed in later rounds, so a round is parallel
+//   rank table on the host from g; records placed by the device lookup.
+// Any acyclic peel order gives a valid minimal perfect hash; this one is deterministic.
+// ------------------------------------------------------------------------------------------
+namespace skm {
+
+struct MphDev {
+    uint32_t r;
+    uint64_t r_magic;
+    uint32_t seed;
+};
+
+__device__ __forceinline__ void mph_verts(const MphDev& P, uint64_t k, uint32_t v[3]) {
+    uint32_t a = 0x9e3779b9u + (uint32_t)k, b = 0x9e3779b9u + (uint32_t)(k >> 32), c = P.seed + 8u;
+    jmix(a, b, c);
+    v[0] = fastmod(a, P.r_magic, P.r);
+    v[1] = fastmod(b, P.r_magic, P.r) + P.r;
+    v[2] = fastmod(c, P.r_magic, P.r) + 2u * P.r;
+}
+
+__global__ void k_mph_edges(const uint64_t* __restrict__ keys, uint32_t m, MphDev P, uint32_t* __restrict__ ev,
+                            uint32_t* __restrict__ deg, uint32_t* __restrict__ xr) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    uint32_t v[3];
+    mph_verts(P, keys[e], v);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        ev[3ull * e + j] = v[j];
+        atomicAdd(&deg[v[j]], 1u);
+        atomicXor(&xr[v[j]], e);
+    }
+}
+
+__global__ void k_mph_frontier(const uint32_t* __restrict__ deg, uint32_t nv, uint32_t* __restrict__ fr,
+                               uint32_t* __restrict__ nfr) {
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool one = v < nv && deg[v] == 1u;
+    const uint64_t bal = __ballot(one);
+    uint32_t base = 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (lane == 0 && bal) base = atomicAdd(nfr, (uint32_t)__popcll(bal));
+    base = __shfl(base, 0);
+    if (one) fr[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = v;
+}
+
+// peeled entry: e << 2 | position of the free vertex in the edge
+__global__ void k_mph_peel(const uint32_t* __restrict__ fr, uint32_t nf, const uint32_t* __restrict__ ev,
+                           const uint32_t* __restrict__ deg, const uint32_t* __restrict__ xr,
+                           uint32_t* __restrict__ peeled, uint32_t* __restrict__ npeeled) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool take = false;
+    uint32_t ent = 0;
+    if (i < nf) {
+        const uint32_t v = fr[i];
+        if (deg[v] == 1u) {
+            const uint32_t e = xr[v];
+            for (uint32_t p = 0; p < 3; ++p) {
+                const uint32_t u = ev[3ull * e + p];
+                if (deg[u] == 1u) {  // first degree-1 vertex of e peels it
+                    take = u == v;
+                    ent = (e << 2) | p;
+                    break;
+                }
+            }
+        }
+    }
+    const uint64_t bal = __ballot(take);
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t base = 0;
+    if (lane == 0 && bal) base = atomicAdd(npeeled, (uint32_t)__popcll(bal));
+    base = __shfl(base, 0);
+    if (take) peeled[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = ent;
+}
+
+__global__ void k_mph_apply(const uint32_t* __restrict__ peeled, uint32_t p0, uint32_t p1,
+                            const uint32_t* __restrict__ ev, uint32_t* __restrict__ deg, uint32_t* __restrict__ xr,
+                            uint32_t* __restrict__ fr, uint32_t* __restrict__ nfr) {
+    const uint32_t i = p0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p1) return;
+    const uint32_t e = peeled[i] >> 2;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const uint32_t u = ev[3ull * e + j];
+        const uint32_t old = atomicSub(&deg[u], 1u);
+        atomicXor(&xr[u], e);
+        if (old == 2u) fr[atomicAdd(nfr, 1u)] = u;
+    }
+}
+
+__device__ __forceinline__ uint32_t gmod3(const uint32_t* g, uint32_t i) {
+    const uint32_t x = (g[i >> 4] >> ((i & 15u) * 2)) & 3u;
+    return x == 3u ? 0u : x;
+}
+
+__global__ void k_mph_assign(const uint32_t* __restrict__ peeled, uint32_t p0, uint32_t p1,
+                             const uint32_t* __restrict__ ev, uint32_t* __restrict__ g) {
+    const uint32_t i = p0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p1) return;
+    const uint32_t ent = peeled[i], e = ent >> 2, p = ent & 3u;
+    uint32_t s = 0, fv = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) {
+        const uint32_t u = ev[3ull * e + j];
+        if (j == p)
+            fv = u;
+        else
+            s += gmod3(g, u);
+    }
+    const uint32_t val = (p + 6u - s) % 3u;
+    // entries start at 3 (0b11): clear the bits that are 0 in val
+    atomicAnd(&g[fv >> 4], ~((3u & ~val) << ((fv & 15u) * 2)));
+}
+
+__global__ void k_mph_place(const uint64_t* __restrict__ keys, uint32_t m, DevBdz D, const uint16_t* __restrict__ data,
+                            uint16_t* __restrict__ dat, uint32_t* __restrict__ bad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint64_t k = keys[i];
+    const uint32_t idx = bdz_lookup(D, (uint32_t)k, (uint32_t)(k >> 32));
+    if (idx >= m) {
+        atomicOr(bad, 1u);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) dat[5ull * idx + j] = data[5ull * i + j];
+}
+
+}  // namespace skm
+
+extern "C" int skm_mph_build_device(const uint64_t* keys, const skm_stored_kmer_data* data, size_t nkeys, uint32_t seed,
+                                    const char* mph_path, const char* dat_path, int device) {
+    SKM_API_BEGIN
+    SKM_CHECK((nkeys == 0 || (keys && data)) && mph_path && dat_path, SKM_E_ARG, "null argument");
+    if (device < 0 || nkeys < 1024) return skm_mph_build(keys, data, nkeys, seed, mph_path, dat_path);
+    SKM_CHECK(nkeys < (1ull << 30), SKM_E_ARG, "too many keys for one BDZ (edge ids are 30 bits)");
+    SKM_HIP(hipSetDevice(device));
+    const uint32_t m = (uint32_t)nkeys;
+    Bdz h;
+    h.m = m;
+    h.r = (uint32_t)std::ceil((1.23 * m) / 3);
+    if (h.r % 2 == 0) h.r += 1;
+    h.b = 7;
+    h.k = 1u << h.b;
+    DevBuf dkeys, ddata, dev_, ddeg, dxr, dfr0, dfr1, dpeel, dcnt, dg;
+    dkeys.ensure(8ull * m);
+    ddata.ensure(10ull * m);
+    SKM_HIP(hipMemcpy(dkeys.p, keys, 8ull * m, hipMemcpyHostToDevice));
+    SKM_HIP(hipMemcpy(ddata.p, data, 10ull * m, hipMemcpyHostToDevice));
+    dev_.ensure(12ull * m);
+    dpeel.ensure(4ull * m);
+    dcnt.ensure(64);
+    uint32_t* cnt = dcnt.as<uint32_t>();  // [0] frontier A, [1] frontier B, [2] peeled, [3] bad
+    std::mt19937 rng(seed);
+    bool ok = false;
+    std::vector<uint32_t> rounds;  // peel-list boundaries
+    for (int attempt = 0; attempt < 1000 && !ok; ++attempt) {
+        if (attempt > 0 && attempt % 20 == 0) h.r += 2;
+        if (attempt == 1) {  // duplicate keys never give an acyclic graph: check once
+            std::vector<uint64_t> sk(keys, keys + nkeys);
+            std::sort(sk.begin(), sk.end());
+            SKM_CHECK(std::adjacent_find(sk.begin(), sk.end()) == sk.end(), SKM_E_ARG,
+                      "BDZ construction failed: duplicate keys");
+        }
+        h.n = 3 * h.r;
+        h.ranktablesize = (uint32_t)std::ceil(h.n / (double)h.k);
+        h.seed = rng();
+        MphDev P{h.r, ~0ull / h.r + 1, h.seed};
+        const uint32_t nv = h.n;
+        ddeg.ensure(4ull * nv);
+        dxr.ensure(4ull * nv);
+        dfr0.ensure(4ull * nv);
+        dfr1.ensure(4ull * nv);
+        SKM_HIP(hipMemset(ddeg.p, 0, 4ull * nv));
+        SKM_HIP(hipMemset(dxr.p, 0, 4ull * nv));
+        SKM_HIP(hipMemset(dcnt.p, 0, 64));
+        hipLaunchKernelGGL(k_mph_edges, dim3(ceil_div(m, 256)), dim3(256), 0, 0, dkeys.as<uint64_t>(), m, P,
+                           dev_.as<uint32_t>(), ddeg.as<uint32_t>(), dxr.as<uint32_t>());
+        hipLaunchKernelGGL(k_mph_frontier, dim3(ceil_div(nv, 256)), dim3(256), 0, 0, ddeg.as<uint32_t>(), nv,
+                           dfr0.as<uint32_t>(), cnt + 0);
+        SKM_HIP(hipGetLastError());
+        uint32_t hc[4] = {0, 0, 0, 0};
+        SKM_HIP(hipMemcpy(hc, cnt, 16, hipMemcpyDeviceToHost));
+        uint32_t nf = hc[0], npeeled = 0;
+        rounds.assign(1, 0);
+        DevBuf* cur = &dfr0;
+        DevBuf* nxt = &dfr1;
+        int fcur = 0;
+        while (nf > 0) {
+            hipLaunchKernelGGL(k_mph_peel, dim3(ceil_div(nf, 256)), dim3(256), 0, 0, cur->as<uint32_t>(), nf,
+                               dev_.as<uint32_t>(), ddeg.as<uint32_t>(), dxr.as<uint32_t>(), dpeel.as<uint32_t>(),
+                               cnt + 2);
+            SKM_HIP(hipMemset(cnt + (1 - fcur), 0, 4));
+            uint32_t np = 0;
+            SKM_HIP(hipMemcpy(&np, cnt + 2, 4, hipMemcpyDeviceToHost));
+            if (np == npeeled) break;
+            hipLaunchKernelGGL(k_mph_apply, dim3(ceil_div(np - npeeled, 256)), dim3(256), 0, 0, dpeel.as<uint32_t>(),
+                               npeeled, np, dev_.as<uint32_t>(), ddeg.as<uint32_t>(), dxr.as<uint32_t>(),
+                               nxt->as<uint32_t>(), cnt + (1 - fcur));
+            SKM_HIP(hipGetLastError());
+            rounds.push_back(np);
+            npeeled = np;
+            SKM_HIP(hipMemcpy(&nf, cnt + (1 - fcur), 4, hipMemcpyDeviceToHost));
+            std::swap(cur, nxt);
+            fcur = 1 - fcur;
+        }
+        ok = npeeled == m;
+    }
+    SKM_CHECK(ok, SKM_E_ARG, "BDZ construction failed: no acyclic 3-graph in 1000 attempts");
+    // assignment, rounds in reverse
+    const uint64_t gwords = ceil_div(h.n, 16) + 1;
+    dg.ensure(4 * gwords);
+    SKM_HIP(hipMemset(dg.p, 0xFF, 4 * gwords));
+    for (size_t ri = rounds.size() - 1; ri >= 1; --ri) {
+        const uint32_t p0 = rounds[ri - 1], p1 = rounds[ri];
+        hipLaunchKernelGGL(k_mph_assign, dim3(ceil_div(p1 - p0, 256)), dim3(256), 0, 0, dpeel.as<uint32_t>(), p0, p1,
+                           dev_.as<uint32_t>(), dg.as<uint32_t>());
+    }
+    SKM_HIP(hipGetLastError());
+    std::vector<uint32_t> gw(gwords);
+    SKM_HIP(hipMemcpy(gw.data(), dg.p, 4 * gwords, hipMemcpyDeviceToHost));
+    h.g.assign((size_t)std::ceil(h.n / 4.0), 0xFF);
+    std::memcpy(h.g.data(), gw.data(), h.g.size());
+    h.ranktable.assign(h.ranktablesize, 0);
+    {
+        uint32_t count = 0;
+        for (uint32_t i = 0; i < h.ranktablesize; ++i) {
+            h.ranktable[i] = count;
+            const uint32_t v0 = i * h.k, v1 = std::min<uint32_t>(h.n, v0 + h.k);
+            for (uint32_t v = v0; v < v1; v += 16) {  // k = 128: whole words; entries past n stay 3
+                const uint32_t w = gw[v >> 4];
+                count += 16u - (uint32_t)__builtin_popcount(w & (w >> 1) & 0x55555555u);
+            }
+        }
+        SKM_CHECK(count == m, SKM_E_ARG, "BDZ construction: assigned vertex count != number of keys");
+    }
+    // place the records: dat[search(key)] = data
+    DevBuf drank, ddat;
+    drank.ensure(4ull * std::max<uint32_t>(h.ranktablesize, 1));
+    SKM_HIP(hipMemcpy(drank.p, h.ranktable.data(), 4ull * h.ranktablesize, hipMemcpyHostToDevice));
+    ddat.ensure(10ull * m);
+    DevBdz D{};
+    D.g = dg.as<uint32_t>();
+    D.ranktable = drank.as<uint32_t>();
+    D.m = m;
+    D.r = h.r;
+    D.b = h.b;
+    D.seed = h.seed;
+    D.r_magic = ~0ull / h.r + 1;
+    SKM_HIP(hipMemset(cnt + 3, 0, 4));
+    hipLaunchKernelGGL(k_mph_place, dim3(ceil_div(m, 256)), dim3(256), 0, 0, dkeys.as<uint64_t>(), m, D,
+                       ddata.as<uint16_t>(), ddat.as<uint16_t>(), cnt + 3);
+    SKM_HIP(hipGetLastError());
+    uint32_t bad = 0;
+    SKM_HIP(hipMemcpy(&bad, cnt + 3, 4, hipMemcpyDeviceToHost));
+    SKM_CHECK(!bad, SKM_E_ARG, "BDZ construction produced an out-of-range slot");
+    std::vector<skm_stored_kmer_data> kd(m);
+    SKM_HIP(hipMemcpy(kd.data(), ddat.p, 10ull * m, hipMemcpyDeviceToHost));
+    std::vector<uint8_t> img = bdz_dump(h);
+    std::ofstream fm(mph_path, std::ios::binary);
+    SKM_CHECK((bool)fm, SKM_E_IO, std::string("cannot write ") + mph_path);
+    fm.write((const char*)img.data(), (std::streamsize)img.size());
+    std::ofstream fd(dat_path, std::ios::binary);
+    SKM_CHECK((bool)fd, SKM_E_IO, std::string("cannot write ") + dat_path);
+    fd.write((const char*)kd.data(), (std::streamsize)(10ull * m));
+    SKM_CHECK((bool)fm && (bool)fd, SKM_E_IO, "write failed");
+    SKM_API_END
+}

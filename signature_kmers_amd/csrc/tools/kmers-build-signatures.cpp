@@ -278,7 +278,7 @@ int main(int argc, char** argv) {
         const uint32_t seed = (uint32_t)std::strtoul(op.get("mph-seed", "1").c_str(), nullptr, 10);
         perfect_hash_thread = std::thread([&, seed]() {
             std::cerr << "build perfect hash into " << quoted(ph_file) << " with data in " << quoted(ph_data) << "\n";
-            ph_rc = skm_mph_build(kept.keys, kept.data, kept.n, seed, ph_file.c_str(), ph_data.c_str());
+            ph_rc = skm_mph_build_device(kept.keys, kept.data, kept.n, seed, ph_file.c_str(), ph_data.c_str(), device);
             if (ph_rc)
                 ph_err = skm_last_error();
             else

@@ -107,3 +107,27 @@ def test_kept_db_exact_lookup_and_recall_calls(skm, gpu, tmp_path):
     np.testing.assert_array_equal(calls.view(np.uint8), ocalls.view(np.uint8))
     empty = skm.KeptKmerDb(np.zeros(0, np.uint64), np.zeros(0, skm.STORED_DTYPE))
     assert (empty.lookup_keys(ref["keys"][:10]) == 0).all()
+
+
+@pytest.mark.parametrize("n", [1500, 300000])
+def test_device_mph_build_is_minimal_perfect(skm, gpu, tmp_path, n):
+    """skm_mph_build_device: the GPU-peeled BDZ image is cmph-readable (oracle reader), minimal
+    perfect over the keys, places every record, and is deterministic for a seed."""
+    rng = np.random.default_rng(n)
+    keys = np.unique(rng.integers(1, 2**63, size=n, dtype=np.uint64))
+    rng.shuffle(keys)
+    data = np.zeros(len(keys), skm.STORED_DTYPE)
+    data["function_index"] = np.arange(len(keys)) % 65000
+    data["avg_from_end"] = np.arange(len(keys)) // 7
+    mph, dat = str(tmp_path / "a.mph"), str(tmp_path / "a.dat")
+    skm.mph_build(keys, data, mph, dat, seed=3, device=0)
+    ob = oracle_ref.Bdz(open(mph, "rb").read())
+    assert ob.size() == len(keys)
+    idx = ob.search(keys)
+    assert np.array_equal(np.sort(idx), np.arange(len(keys), dtype=np.uint32))
+    d = np.frombuffer(open(dat, "rb").read(), skm.STORED_DTYPE)
+    assert np.array_equal(d[idx].view(np.uint8), data.view(np.uint8))
+    skm.mph_build(keys, data, str(tmp_path / "b.mph"), str(tmp_path / "b.dat"), seed=3, device=0)
+    assert open(mph, "rb").read() == open(str(tmp_path / "b.mph"), "rb").read()
+    db = skm.CmphKmerDb(str(tmp_path / "a"))
+    np.testing.assert_array_equal(db.lookup_keys(keys), idx)
