@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--cpu-sample-seqs", type=int, default=200_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--annot-queries", type=int, default=2_000_000,
+                    help="annotate leg (BASELINE configs[3] at reduced query count; 0 = off; N=1 only)")
     return ap.parse_args()
 
 
@@ -158,6 +160,8 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_baseline(r, o, l, f, i, len(funcs), a.cpu_sample_seqs)
+    if world == 1 and a.annot_queries > 0:
+        out["annotate"] = _annotate_leg(skm, synth, b, funcs, a, files_per_rank, local % ndev)
     b.close()
     if rank == 0:
         line = json.dumps(out)
@@ -167,6 +171,57 @@ def main():
                 fh.write(line + "\n")
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _annotate_leg(skm, synth, b, funcs, a, files_train, device):
+    """kmers-call-functions path (BASELINE configs[3]): fresh query proteins of the same families
+    (files after the training set: their own RNG streams) against the CMPH/BDZ DB of this build,
+    resident in HBM.  One step = window lookup (k_lookup) + HitSet calls + compaction over every
+    query; the calls stay on the device.  Roofline: k_lookup, SURVEY 8(d) B_alg = 1 B/residue +
+    18 B/window (g bytes, rank word, record)."""
+    import tempfile
+    kept = b.finish()
+    t0 = time.time()
+    nq = a.annot_queries
+    per_file = 4000
+    p = synth.generate_arrays(a.seqs + nq, a.families, per_file=per_file, first_file=files_train,
+                              n_files=(nq + per_file - 1) // per_file)
+    gen_s = time.time() - t0
+    with tempfile.TemporaryDirectory(dir="/tmp") as d:
+        base = os.path.join(d, "kmer_data")
+        t0 = time.time()
+        skm.mph_build(kept.keys, kept.data, base + ".mph", base + ".dat", seed=1, device=device)
+        mph_s = time.time() - t0
+        db = skm.CmphKmerDb(base, device=device)
+    hypo = funcs.index("hypothetical protein")
+    q = skm.QueryBatch(db, p.residues, p.seq_off, p.seq_len)
+    nwin = int(np.where(p.seq_len >= 8, p.seq_len.astype(np.int64) - 7, 0).sum())
+    for _ in range(max(1, a.warmup)):
+        q.run(hypo)
+    steps = max(3, a.steps)
+    acc = {}
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        q.run(hypo)
+        for k, v in q.timings().items():
+            acc[k] = acc.get(k, 0.0) + v
+    wall = time.perf_counter() - t1
+    acc = {k: v / steps for k, v in acc.items()}
+    off, calls = q.calls()
+    q.close()
+    db.close()
+    alg = int(len(p.residues)) + 18 * nwin
+    gbs = alg / (acc["lookup"] * 1e-3) / 1e9
+    return {"metric": "query k-mers/sec (window lookup + HitSet calls)", "value": nwin * steps / wall,
+            "unit": "k-mers/s", "ms_per_step": 1000.0 * wall / steps,
+            "config": {"workload": f"C4 at {nq} queries (configs[3] names 10M): fresh proteins of the same "
+                                   f"families vs the CMPH DB of this build in HBM", "queries": nq,
+                       "windows": nwin, "db_keys": int(len(kept.keys)), "calls": int(len(calls))},
+            "phase_ms": acc,
+            "roofline": {"bound": "hbm", "kernel": "k_lookup<false>", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
+                         "avg_launch_ms": acc["lookup"], "traffic": None},
+            "mph_build_s": mph_s, "query_gen_s": gen_s}
 
 
 def _valid_windows(r, o, l, f) -> int:

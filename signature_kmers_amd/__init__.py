@@ -379,6 +379,52 @@ def read_function_index(path: str) -> list:
     return out
 
 
+class QueryBatch:
+    """A batch of query sequences resident in HBM (skm_query_*): run() repeats the device pipeline
+    (window lookup + HitSet calls) without re-uploading; timings() = the last run's device ms."""
+
+    def __init__(self, db: CmphKmerDb, residues, seq_off, seq_len):
+        self._h = C.c_void_p()
+        self.db = db
+        residues = np.ascontiguousarray(residues, dtype=np.uint8)
+        seq_off = np.ascontiguousarray(seq_off, dtype=np.uint64)
+        seq_len = np.ascontiguousarray(seq_len, dtype=np.uint32)
+        _check(lib().skm_query_create(C.byref(self._h), db._h, _ptr(residues), _ptr(seq_off), _ptr(seq_len),
+                                      len(seq_len)))
+
+    def run(self, hypo_index: int, ignore_hypo: bool = False, min_hits: int = 5, max_gap: int = 200):
+        opts = _AnnotOpts(min_hits, max_gap, int(ignore_hypo), hypo_index, 0, 0)
+        _check(lib().skm_query_run(self._h, C.byref(opts)))
+
+    def timings(self) -> dict:
+        ms = (C.c_float * 4)()
+        n = lib().skm_query_last_timings(self._h, ms, 4)
+        return dict(zip(["lookup", "hitset", "compact", "total"], list(ms)[:n]))
+
+    def calls(self):
+        out = _Calls()
+        _check(lib().skm_query_calls(self._h, C.byref(out)))
+        try:
+            n, nc = int(out.n_seqs), int(out.n_calls)
+            off = np.ctypeslib.as_array(out.call_off, shape=(n + 1,)).copy()
+            calls = (np.frombuffer(C.string_at(out.calls, CALL_DTYPE.itemsize * nc), dtype=CALL_DTYPE).copy()
+                     if nc else np.zeros(0, CALL_DTYPE))
+            return off, calls
+        finally:
+            lib().skm_calls_free(C.byref(out))
+
+    def close(self):
+        if self._h:
+            lib().skm_query_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class FunctionCaller:
     """FunctionCaller<CmphKmerDb> (call_functions.h:60-136) with the per-window lookup and HitSet
     state machine on the GPU and find_best_call on the host."""

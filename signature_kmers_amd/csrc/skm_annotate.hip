@@ -7,9 +7,10 @@
 //   k_lookup   one thread per 16 windows: window validity (no 'X'/'*' in the window or the byte
 //              after it), jenkins lookup2 -> 3 vertices -> 2-bit g -> rank (popcount over u32
 //              words of g) -> 10-byte record gather; writes func<<16|mean per window position
-//   k_calls    one thread per query sequence: the HitSet state machine over its window hits,
-//              statistics (Boost.Math mean / median / MAD) on a per-sequence scratch, KmerCall
-//              emission into a per-sequence slot range
+//   k_calls_scan   one thread per query sequence: the HitSet state machine over its window hits,
+//              emitting one segment per HitSet::process
+//   k_seg_process  one wave per segment: statistics (Boost.Math mean / median / MAD) in LDS,
+//              the length test, the KmerCall
 //   scan + k_gather   CSR compaction of the calls
 #include <hip/hip_runtime.h>
 
@@ -145,7 +146,28 @@ __device__ __forceinline__ uint32_t bdz_lookup(const DevBdz& D, uint32_t lo, uin
 
 __device__ __forceinline__ bool ambig(uint32_t c) { return c == 'X' || c == '*'; }
 
-template <bool EXACT>
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// key bytes t..t+7 of the 32-byte window w[8]
+__device__ __forceinline__ void key_at(const uint32_t (&w)[8], int t, uint32_t& lo, uint32_t& hi) {
+    const int wi = t >> 2, sh = (t & 3) * 8;
+    if (sh == 0) {
+        lo = w[wi];
+        hi = w[wi + 1];
+    } else {
+        lo = (w[wi] >> sh) | (w[wi + 1] << (32 - sh));
+        hi = (w[wi + 1] >> sh) | (w[wi + 2] << (32 - sh));
+    }
+}
+
+// MODE: LK_BDZ7 = BDZ with rank blocks of 128 (cmph's default b = 7), LK_EXACT = kept-k-mer
+// table, LK_BDZ = BDZ with any b (per-window search)
+enum { LK_BDZ7 = 0, LK_EXACT = 1, LK_BDZ = 2 };
+template <int MODE>
 __global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict__ res, uint64_t rp, DevBdz D,
                                                       uint32_t* __restrict__ hits) {
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x * LK_POS;
@@ -163,29 +185,79 @@ __global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict
             bad |= ((a || c == 0) ? 1u : 0u) << j;
         }
         uint32_t out[LK_POS];
+        if constexpr (MODE != LK_BDZ7) {
 #pragma unroll
-        for (int t = 0; t < LK_POS; ++t) {
-            const uint64_t p = base + t;
-            uint32_t o = NO_HIT;
-            // for_each_kmer: skip when an ambiguous char lies in [p, p+8] (incl. the next byte)
-            if (p < rp && ((bad >> t) & 0xFFu) == 0 && ((amb >> (t + 8)) & 1u) == 0) {
-                // key bytes t..t+7
-                const int wi = t >> 2, sh = (t & 3) * 8;
-                uint32_t lo, hi;
-                if (sh == 0) {
-                    lo = w[wi];
-                    hi = w[wi + 1];
-                } else {
-                    lo = (w[wi] >> sh) | (w[wi + 1] << (32 - sh));
-                    hi = (w[wi + 1] >> sh) | (w[wi + 2] << (32 - sh));
+            for (int t = 0; t < LK_POS; ++t) {
+                const uint64_t p = base + t;
+                uint32_t o = NO_HIT;
+                if (p < rp && ((bad >> t) & 0xFFu) == 0 && ((amb >> (t + 8)) & 1u) == 0) {
+                    uint32_t lo, hi;
+                    key_at(w, t, lo, hi);
+                    const uint32_t idx = MODE == LK_EXACT ? exact_lookup(D, lo, hi) : bdz_lookup(D, lo, hi);
+                    if (idx < D.m) {
+                        const uint16_t* rec = D.dat + (uint64_t)idx * 5;
+                        o = ((uint32_t)rec[1] << 16) | rec[2];  // function_index, mean
+                    }
                 }
-                const uint32_t idx = EXACT ? exact_lookup(D, lo, hi) : bdz_lookup(D, lo, hi);
-                if (idx < D.m) {
-                    const uint16_t* rec = D.dat + (uint64_t)idx * 5;
-                    o = ((uint32_t)rec[1] << 16) | rec[2];  // function_index, mean
+                out[t] = o;
+            }
+        } else {
+            // BDZ search in phases over 8 windows at a time so every dependent level issues 8+
+            // independent loads: (1) jenkins -> 3 g words, (2) select vertex -> rank word + the
+            // vertex's 32-byte g block, (3) branch-free popcount rank -> .dat record
+#pragma unroll
+            for (int half = 0; half < LK_POS / 8; ++half) {
+                uint32_t hv[8][3], gw[8][3];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    uint32_t lo, hi;
+                    key_at(w, half * 8 + u, lo, hi);
+                    uint32_t a = 0x9e3779b9u + lo, b = 0x9e3779b9u + hi, c = D.seed + 8u;
+                    jmix(a, b, c);
+                    hv[u][0] = fastmod(a, D.r_magic, D.r);
+                    hv[u][1] = fastmod(b, D.r_magic, D.r) + D.r;
+                    hv[u][2] = fastmod(c, D.r_magic, D.r) + 2u * D.r;
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) gw[u][j] = D.g[hv[u][j] >> 4];
+                }
+                uint32_t vv[8], rt[8];
+                uint4 b0[8], b1[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    uint32_t sum = 0;
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) sum += (gw[u][j] >> ((hv[u][j] & 15u) * 2)) & 3u;
+                    const uint32_t sel = sum % 3u;
+                    const uint32_t v = sel == 0 ? hv[u][0] : (sel == 1 ? hv[u][1] : hv[u][2]);
+                    vv[u] = v;
+                    const uint32_t blk = v >> 7;  // b = 7 (checked on open)
+                    rt[u] = D.ranktable[blk];
+                    const uint4* gb = reinterpret_cast<const uint4*>(D.g) + 2ull * blk;
+                    b0[u] = gb[0];
+                    b1[u] = gb[1];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int t = half * 8 + u;
+                    const uint32_t off = vv[u] & 127u, fw = off >> 4, pe = off & 15u;
+                    const uint32_t wd[8] = {b0[u].x, b0[u].y, b0[u].z, b0[u].w, b1[u].x, b1[u].y, b1[u].z, b1[u].w};
+                    uint32_t rank = rt[u], wf = wd[0];
+#pragma unroll
+                    for (uint32_t j = 0; j < 8; ++j) {
+                        rank += j < fw ? 16u - unassigned_in(wd[j]) : 0u;
+                        wf = j == fw ? wd[j] : wf;
+                    }
+                    const uint32_t pmask = pe ? (0xFFFFFFFFu >> (32u - 2u * pe)) : 0u;
+                    rank += pe - unassigned_in(wf & pmask);
+                    const uint64_t p = base + t;
+                    uint32_t o = NO_HIT;
+                    if (p < rp && ((bad >> t) & 0xFFu) == 0 && ((amb >> (t + 8)) & 1u) == 0 && rank < D.m) {
+                        const uint16_t* rec = D.dat + (uint64_t)rank * 5;
+                        o = ((uint32_t)rec[1] << 16) | rec[2];  // function_index, mean
+                    }
+                    out[t] = o;
                 }
             }
-            out[t] = o;
         }
         uint4* dst = reinterpret_cast<uint4*>(hits + base);
         dst[0] = make_uint4(out[0], out[1], out[2], out[3]);
@@ -348,58 +420,243 @@ __device__ void hitset_process(const CallArgs& A, const uint32_t* hit, uint16_t*
     }
 }
 
-__global__ void k_calls(CallArgs A) {
+// HitSet state machine (call_functions.tcc:259-338), thread per sequence.  Each HitSet::process
+// event becomes a segment {sequence, first window, last window, current function}; the
+// statistics of a segment never feed back into the state machine, so they run afterwards one
+// wave per segment (k_seg_process) instead of divergently inside this loop.
+__global__ void k_calls_scan(CallArgs A, uint4* __restrict__ segs) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= A.nseq) return;
     const QMeta m = A.meta[s];
     const uint32_t nwin = m.len >= 8 ? m.len - 7 : 0;
     const uint32_t* hit = A.hits + m.pstart;
-    uint16_t* scr = A.scratch + A.scr_off[s];
-    skm_kmer_call* slots = A.slots + A.cap_off[s];
-    const double seqlen = (double)m.len;
-    uint32_t ncalls = 0;
+    uint4* out = segs + A.cap_off[s];
+    uint32_t nseg = 0;
     // HitSet: all usable hits in window range [first, last_pos]; pair = (prev, last)
     uint32_t count = 0, first = 0, last_pos = 0, prev_pos = 0, last_f = 0, prev_f = 0, cur = 0xFFFFu;
-    for (uint32_t i = 0; i < nwin; ++i) {
-        const uint32_t h = hit[i];
-        if (!usable(h, A)) continue;
-        const uint32_t f = h >> 16;
-        if (count > 0 && (uint64_t)last_pos + (uint64_t)A.max_gap < (uint64_t)i) {
-            if ((int)count >= A.min_hits) {
-                hitset_process(A, hit, scr, first, last_pos, cur, seqlen, slots, ncalls);
-                if (prev_f != cur && prev_f == last_f) {
-                    cur = prev_f;
-                    first = prev_pos;
-                    count = 2;
-                } else {
+    auto process = [&]() {
+        out[nseg++] = make_uint4(s, first, last_pos, cur);
+        if (prev_f != cur && prev_f == last_f) {
+            cur = prev_f;
+            first = prev_pos;
+            count = 2;
+        } else {
+            count = 0;
+        }
+    };
+    for (uint32_t i0 = 0; i0 < nwin; i0 += 8) {
+        uint32_t hb[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) hb[k] = i0 + k < nwin ? hit[i0 + k] : NO_HIT;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t h = hb[k], i = i0 + k;
+            if (!usable(h, A)) continue;
+            const uint32_t f = h >> 16;
+            if (count > 0 && (uint64_t)last_pos + (uint64_t)A.max_gap < (uint64_t)i) {
+                if ((int)count >= A.min_hits)
+                    process();
+                else
                     count = 0;
-                }
-            } else {
-                count = 0;
             }
-        }
-        if (count == 0) {
-            cur = f;
-            first = i;
-        }
-        prev_pos = last_pos;
-        prev_f = last_f;
-        last_pos = i;
-        last_f = f;
-        ++count;
-        if (count > 1 && cur != f && prev_f == f) {
-            hitset_process(A, hit, scr, first, last_pos, cur, seqlen, slots, ncalls);
-            if (prev_f != cur && prev_f == last_f) {
-                cur = prev_f;
-                first = prev_pos;
-                count = 2;
-            } else {
-                count = 0;
+            if (count == 0) {
+                cur = f;
+                first = i;
             }
+            prev_pos = last_pos;
+            prev_f = last_f;
+            last_pos = i;
+            last_f = f;
+            ++count;
+            if (count > 1 && cur != f && prev_f == f) process();
         }
     }
-    if ((int)count >= A.min_hits) hitset_process(A, hit, scr, first, last_pos, cur, seqlen, slots, ncalls);
-    A.counts[s] = ncalls;
+    if ((int)count >= A.min_hits) out[nseg++] = make_uint4(s, first, last_pos, cur);
+    A.counts[s] = nseg;
+}
+
+// dense segment list: segments of sequence s at seg_off[s]..
+__global__ void k_gather_segs(const uint4* __restrict__ segs, const uint64_t* __restrict__ cap_off,
+                              const uint64_t* __restrict__ seg_off, uint32_t nseq, uint4* __restrict__ dense) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseq) return;
+    const uint64_t a = seg_off[s], e = seg_off[s + 1], src = cap_off[s];
+    for (uint64_t j = a; j < e; ++j) dense[j] = segs[src + (j - a)];
+}
+
+// k-th smallest (0-based) |2 v_j - C2| over sorted v[0..n): the deviations left and right of
+// C2/2 are two sorted runs; binary search on how many of the k+1 smallest come from the left.
+__device__ uint32_t kth_dev_sorted(const uint32_t* v, uint32_t n, uint32_t C2, uint32_t k) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (2u * v[mid] > C2)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    const uint32_t nL = lo, nR = n - lo, mm = k + 1;
+    auto Ld = [&](uint32_t i) { return C2 - 2u * v[nL - 1 - i]; };
+    auto Rd = [&](uint32_t i) { return 2u * v[nL + i] - C2; };
+    uint32_t a = mm > nR ? mm - nR : 0u, b = mm < nL ? mm : nL;
+    while (a < b) {  // first t where "take more from the left" is false
+        const uint32_t t = (a + b) >> 1, u = mm - t;
+        if (u > 0 && Rd(u - 1) > Ld(t))
+            a = t + 1;
+        else
+            b = t;
+    }
+    const uint32_t t = a, u = mm - t;
+    const uint32_t x = t > 0 ? Ld(t - 1) : 0u, y = u > 0 ? Rd(u - 1) : 0u;
+    return x > y ? x : y;
+}
+
+constexpr int SEG_WAVES = 4;
+constexpr uint32_t SEG_CAP = 2048;
+
+// One wave per HitSet::process segment (call_functions.tcc:35-103): the hits of the current
+// function in window order (ballot compaction into LDS), Boost.Math mean (four-lane Welford on
+// lanes 0-3, or the single running mean), median by an LDS bitonic sort, MAD as the k-th
+// deviation of the sorted run, the length window test, and the KmerCall (count = -1: none).
+// Segments of more than SEG_CAP hits take the sequential path on a private global scratch.
+__global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, const uint4* __restrict__ segs,
+                                                                uint32_t nseg, skm_kmer_call* __restrict__ out,
+                                                                uint16_t* __restrict__ pool,
+                                                                unsigned long long* __restrict__ pool_ctr) {
+    __shared__ uint32_t sv[SEG_WAVES][SEG_CAP];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t j = blockIdx.x * SEG_WAVES + wave;
+    if (j >= nseg) return;  // wave-uniform
+    const uint4 sg = segs[j];
+    const uint32_t first = sg.y, last = sg.z, cur = sg.w;
+    const QMeta m = A.meta[sg.x];
+    const uint32_t* hit = A.hits + m.pstart;
+    const double seqlen = (double)m.len;
+    uint32_t* buf = sv[wave];
+    uint32_t n = 0, last_cur = first;
+    for (uint32_t i0 = first; i0 <= last; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const uint32_t h = i <= last ? hit[i] : NO_HIT;
+        const bool take = usable(h, A) && (h >> 16) == cur;
+        const uint64_t bal = __ballot(take);
+        const uint32_t pos = n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        if (take && pos < SEG_CAP) buf[pos] = h & 0xFFFFu;
+        if (bal) last_cur = i0 + 63u - (uint32_t)__clzll(bal);
+        n += (uint32_t)__popcll(bal);
+    }
+    if (n > SEG_CAP) {  // long run: the sequential restatement on a private scratch
+        if (lane == 0) {
+            uint16_t* scr = pool + atomicAdd(pool_ctr, (unsigned long long)n);
+            uint32_t nc = 0;
+            hitset_process(A, hit, scr, first, last, cur, seqlen, out + j, nc);
+            if (nc == 0) out[j].count = -1;
+        }
+        return;
+    }
+    wave_sync_lds();
+    // Boost.Math mean over float(kdata.mean) in hit order
+    float mean;
+    if (A.mean_mode == 1) {
+        float mu = 0, fi = 1;
+        if (lane == 0)
+            for (uint32_t q = 0; q < n; ++q) {
+                mu = mu + ((float)buf[q] - mu) / fi;
+                fi += 1;
+            }
+        mean = __shfl(mu, 0);
+    } else {
+        const uint32_t end = n - (n % 4);
+        float mu = 0, fi = 1;
+        if (lane < 4) {
+            for (uint32_t q = lane; q < end; q += 4) {
+                const float inv = 1.0f / fi;
+                float t = (float)buf[q] - mu;
+                t *= inv;
+                mu += t;
+                fi += 1;
+            }
+            if (lane == 3)
+                for (uint32_t q = end; q < n; ++q) {
+                    mu += ((float)buf[q] - mu) / fi;
+                    fi += 1;
+                }
+        }
+        const float m0 = __shfl(mu, 0), m1 = __shfl(mu, 1), m2 = __shfl(mu, 2), m3 = __shfl(mu, 3);
+        const float num1 = float(n - (n % 4)) / float(4);
+        const float num2 = num1 + float(n % 4);
+        mean = (num1 * (m0 + m1 + m2) + num2 * m3) / float(n);
+    }
+    // bitonic sort of buf[0..P), P = next power of two >= n, padded with the maximum
+    uint32_t P = 1;
+    while (P < n) P <<= 1;
+    for (uint32_t q = n + lane; q < P; q += 64) buf[q] = 0xFFFFFFFFu;
+    wave_sync_lds();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t idx = lane; idx < (P >> 1); idx += 64) {
+                const uint32_t i = ((idx & ~(jj - 1u)) << 1) | (idx & (jj - 1u));
+                const uint32_t l = i + jj;
+                const uint32_t x = buf[i], y = buf[l];
+                const bool asc = (i & k) == 0;
+                if ((x > y) == asc) {
+                    buf[i] = y;
+                    buf[l] = x;
+                }
+            }
+            wave_sync_lds();
+        }
+    }
+    if (lane != 0) return;
+    float median;
+    uint32_t C2;
+    if (n & 1) {
+        const uint32_t md = buf[(n - 1) / 2];
+        median = (float)md;
+        C2 = 2u * md;
+    } else {
+        const uint32_t a = buf[n / 2 - 1], b = buf[n / 2];
+        median = ((float)a + (float)b) / 2;
+        C2 = a + b;
+    }
+    float mad;
+    if (n & 1) {
+        mad = (float)kth_dev_sorted(buf, n, C2, (n - 1) / 2) * 0.5f;
+    } else {
+        const float d1 = (float)kth_dev_sorted(buf, n, C2, n / 2 - 1) * 0.5f;
+        const float d2 = (float)kth_dev_sorted(buf, n, C2, n / 2) * 0.5f;
+        mad = (d1 + d2) / 2.0f;
+    }
+    if (mad == 0) mad = 30;
+    const double cutoff_b = (double)mean - 2.0 * (double)mad;
+    const double cutoff_t = (double)mean + 2.0 * (double)mad;
+    skm_kmer_call c;
+    c.start = first;
+    c.end = last_cur + 7u;
+    c.count = ((int)n >= A.min_hits && !(seqlen < cutoff_b || seqlen > cutoff_t)) ? (int32_t)n : -1;
+    c.function_index = (uint16_t)cur;
+    c.pad = 0;
+    c.protein_length_median = (uint32_t)median;
+    c.protein_length_med_avg_dev = mad;
+    out[j] = c;
+}
+
+// calls kept per sequence (segment results with count >= 0)
+__global__ void k_count_calls(const skm_kmer_call* __restrict__ res, const uint64_t* __restrict__ seg_off,
+                              uint32_t nseq, uint32_t* __restrict__ counts) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseq) return;
+    uint32_t c = 0;
+    for (uint64_t j = seg_off[s]; j < seg_off[s + 1]; ++j) c += res[j].count >= 0;
+    counts[s] = c;
+}
+
+__global__ void k_gather_valid(const skm_kmer_call* __restrict__ res, const uint64_t* __restrict__ seg_off,
+                               const uint64_t* __restrict__ call_off, uint32_t nseq, skm_kmer_call* __restrict__ out) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseq) return;
+    uint64_t o = call_off[s];
+    for (uint64_t j = seg_off[s]; j < seg_off[s + 1]; ++j)
+        if (res[j].count >= 0) out[o++] = res[j];
 }
 
 // capacity of the call slot range of sequence s
@@ -536,6 +793,7 @@ struct skm_query {
     uint32_t nseq = 0;
     uint64_t rp = 0, n_windows = 0;
     DevBuf d_res, d_meta, d_hits, d_scr, d_scr_off, d_caps, d_cap_off, d_slots, d_counts, d_call_off, d_calls;
+    DevBuf d_seg_off, d_segs, d_segres, d_pool_ctr;
     Scanner scan;
     uint64_t n_calls = 0;
     bool ran = false;
@@ -628,11 +886,14 @@ void query_run(skm_query* q, const skm_annot_opts* o) {
         uint64_t nthreads = ceil_div(q->rp, LK_POS);
         uint32_t grid = (uint32_t)std::min<uint64_t>(ceil_div(nthreads, LK_THREADS), 256ull * 16);
         if (db->exact)
-            hipLaunchKernelGGL(k_lookup<true>, dim3(grid), dim3(LK_THREADS), 0, st, q->d_res.as<uint8_t>(), q->rp,
-                               db->dev, q->d_hits.as<uint32_t>());
+            hipLaunchKernelGGL(k_lookup<LK_EXACT>, dim3(grid), dim3(LK_THREADS), 0, st, q->d_res.as<uint8_t>(),
+                               q->rp, db->dev, q->d_hits.as<uint32_t>());
+        else if (db->dev.b == 7)
+            hipLaunchKernelGGL(k_lookup<LK_BDZ7>, dim3(grid), dim3(LK_THREADS), 0, st, q->d_res.as<uint8_t>(),
+                               q->rp, db->dev, q->d_hits.as<uint32_t>());
         else
-            hipLaunchKernelGGL(k_lookup<false>, dim3(grid), dim3(LK_THREADS), 0, st, q->d_res.as<uint8_t>(), q->rp,
-                               db->dev, q->d_hits.as<uint32_t>());
+            hipLaunchKernelGGL(k_lookup<LK_BDZ>, dim3(grid), dim3(LK_THREADS), 0, st, q->d_res.as<uint8_t>(),
+                               q->rp, db->dev, q->d_hits.as<uint32_t>());
     } else if (q->rp) {
         SKM_HIP(hipMemsetAsync(q->d_hits.p, 0xFF, 4 * q->rp, st));
     }
@@ -662,15 +923,33 @@ void query_run(skm_query* q, const skm_annot_opts* o) {
         A.mean_mode = o->mean_mode;
         A.hypo = o->hypo_index >= 0 ? (uint32_t)o->hypo_index : 0xFFFFFFFFu;
         SKM_HIP(hipEventRecord(q->ev[2], st));
-        hipLaunchKernelGGL(k_calls, dim3(ceil_div(ns, 64)), dim3(64), 0, st, A);
+        hipLaunchKernelGGL(k_calls_scan, dim3(ceil_div(ns, 64)), dim3(64), 0, st, A, q->d_slots.as<uint4>());
+        SKM_HIP(hipGetLastError());
+        q->scan.run(q->d_counts.as<uint32_t>(), ns, q->d_seg_off.as<uint64_t>(), st);
+        uint64_t nseg = 0;
+        SKM_HIP(hipMemcpyAsync(&nseg, q->d_seg_off.as<uint64_t>() + ns, 8, hipMemcpyDeviceToHost, st));
+        SKM_HIP(hipStreamSynchronize(st));
+        q->d_segs.ensure(16 * std::max<uint64_t>(nseg, 1));
+        q->d_segres.ensure(sizeof(skm_kmer_call) * std::max<uint64_t>(nseg, 1));
+        q->d_scr.ensure(2 * (q->n_windows + 2 * nseg + 64));
+        q->d_pool_ctr.ensure(8);
+        SKM_HIP(hipMemsetAsync(q->d_pool_ctr.p, 0, 8, st));
+        hipLaunchKernelGGL(k_gather_segs, dim3(ceil_div(ns, 256)), dim3(256), 0, st, q->d_slots.as<uint4>(),
+                           q->d_cap_off.as<uint64_t>(), q->d_seg_off.as<uint64_t>(), ns, q->d_segs.as<uint4>());
+        if (nseg)
+            hipLaunchKernelGGL(k_seg_process, dim3((uint32_t)ceil_div(nseg, SEG_WAVES)), dim3(64 * SEG_WAVES), 0, st, A,
+                               q->d_segs.as<uint4>(), (uint32_t)nseg, q->d_segres.as<skm_kmer_call>(),
+                               q->d_scr.as<uint16_t>(), q->d_pool_ctr.as<unsigned long long>());
         SKM_HIP(hipGetLastError());
         SKM_HIP(hipEventRecord(q->ev[3], st));
+        hipLaunchKernelGGL(k_count_calls, dim3(ceil_div(ns, 256)), dim3(256), 0, st, q->d_segres.as<skm_kmer_call>(),
+                           q->d_seg_off.as<uint64_t>(), ns, q->d_counts.as<uint32_t>());
         q->scan.run(q->d_counts.as<uint32_t>(), ns, q->d_call_off.as<uint64_t>(), st);
         SKM_HIP(hipMemcpyAsync(&q->n_calls, q->d_call_off.as<uint64_t>() + ns, 8, hipMemcpyDeviceToHost, st));
         SKM_HIP(hipStreamSynchronize(st));
         q->d_calls.ensure(sizeof(skm_kmer_call) * std::max<uint64_t>(q->n_calls, 1));
-        hipLaunchKernelGGL(k_gather_calls, dim3(ceil_div(ns, 256)), dim3(256), 0, st, q->d_slots.as<skm_kmer_call>(),
-                           q->d_cap_off.as<uint64_t>(), q->d_call_off.as<uint64_t>(), ns, q->d_calls.as<skm_kmer_call>());
+        hipLaunchKernelGGL(k_gather_valid, dim3(ceil_div(ns, 256)), dim3(256), 0, st, q->d_segres.as<skm_kmer_call>(),
+                           q->d_seg_off.as<uint64_t>(), q->d_call_off.as<uint64_t>(), ns, q->d_calls.as<skm_kmer_call>());
         SKM_HIP(hipGetLastError());
     } else {
         SKM_HIP(hipEventRecord(q->ev[2], st));
@@ -851,6 +1130,7 @@ int skm_query_create(skm_query** out, skm_db* db, const uint8_t* residues, const
         q->d_cap_off.ensure(8 * (n_seqs + 1));
         q->d_counts.ensure(4 * std::max<size_t>(n_seqs, 1));
         q->d_call_off.ensure(8 * (n_seqs + 1));
+        q->d_seg_off.ensure(8 * (n_seqs + 1));
         SKM_HIP(hipStreamSynchronize(q->stream));
     } catch (...) {
         skm_query_destroy(q);

@@ -72,7 +72,7 @@ def test_query_edge_cases(skm, gpu, tmp_path):
     caller = skm.FunctionCaller(db, funcs)
     src = p.residues[p.seq_off[0]:p.seq_off[0] + p.seq_len[0]].tobytes()
     seqs = [b"", b"ACDEFGH", b"ACDEFGHI", b"ACDEFGHIX", b"XACDEFGHI", src, src[:50] + b"X" + src[50:],
-            src[:40] + b"*" + src[41:], src.lower(), src * 3, b"X" * 20]
+            src[:40] + b"*" + src[41:], src.lower(), src * 3, b"X" * 20, src * 7, src * 12, src * 40]
     lens = np.array([len(s) for s in seqs], np.uint32)
     off = np.zeros(len(seqs), np.uint64)
     off[1:] = np.cumsum(lens[:-1])
