@@ -23,7 +23,7 @@ __all__ = [
 K = 8
 UNDEFINED_FUNCTION = 0xFFFF
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libskm.so")
+LIB_PATH = os.environ.get("SKM_LIB_PATH") or os.path.join(_HERE, "libskm.so")  # override: A/B builds
 
 STORED_DTYPE = np.dtype([("avg_from_end", "<u2"), ("function_index", "<u2"), ("mean", "<u2"),
                          ("median", "<u2"), ("var", "<u2")])  # StoredKmerData, kmer_data.h:114-128

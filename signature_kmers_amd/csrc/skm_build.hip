@@ -1576,12 +1576,27 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
                                             uint32_t n, const BucketArgs& A, uint64_t hprefix, const SubLds& L) {
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t EMPTY = 0xFFFFFFFFu;
-    // 1. load the elements
-    for (uint32_t j = tid; j < n; j += nt) {
-        L.hi[j] = src_hi[j];
-        L.lo[j] = src_lo[j];
+    // 1. load the elements: every load of the batch in flight at once (a rolled loop waits for
+    //    each pair before its LDS store: CAP / BP_THREADS HBM round trips per batch)
+    constexpr uint32_t LPER = CAP / BP_THREADS;
+    uint64_t eh[LPER], el[LPER];
+#pragma unroll
+    for (uint32_t u = 0; u < LPER; ++u) {
+        const uint32_t j = tid + u * BP_THREADS;
+        if (j < n) {
+            eh[u] = __builtin_nontemporal_load(src_hi + j);
+            el[u] = __builtin_nontemporal_load(src_lo + j);
+        }
     }
     for (uint32_t t = tid; t < (uint32_t)TAB; t += nt) L.tab[t] = EMPTY;
+#pragma unroll
+    for (uint32_t u = 0; u < LPER; ++u) {
+        const uint32_t j = tid + u * BP_THREADS;
+        if (j < n) {
+            L.hi[j] = eh[u];
+            L.lo[j] = el[u];
+        }
+    }
     if (tid == 0) *L.nbig = 0;
     __syncthreads();
     SKM_STAMP(2);
