@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--annot-queries", type=int, default=2_000_000,
                     help="annotate leg (BASELINE configs[3] at reduced query count; 0 = off; N=1 only)")
+    ap.add_argument("--matrix-seqs", type=int, default=100_000,
+                    help="matrix-distance leg (BASELINE configs[4]: all-vs-all over this many query "
+                         "sequences of 200 families; 0 = off; N=1 only)")
     return ap.parse_args()
 
 
@@ -163,6 +166,8 @@ def main():
     if world == 1 and a.annot_queries > 0:
         out["annotate"] = _annotate_leg(skm, synth, b, funcs, a, files_per_rank, local % ndev)
     b.close()
+    if world == 1 and a.matrix_seqs > 0:
+        out["matrix"] = _matrix_leg(skm, synth, a, local % ndev)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
@@ -222,6 +227,64 @@ def _annotate_leg(skm, synth, b, funcs, a, files_train, device):
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
                          "avg_launch_ms": acc["lookup"], "traffic": None},
             "mph_build_s": mph_s, "query_gen_s": gen_s}
+
+
+def _matrix_leg(skm, synth, a, device):
+    """kmers-matrix-distance (BASELINE configs[4]): a 200-family signature DB (built on this GPU from
+    200K training proteins, BDZ on the GPU) resident in HBM, a fresh set of query proteins of the
+    same families, all-vs-all shared-signature-k-mer counts into one dense upper-triangle tile (one
+    GPU holds every row).  One step = window lookup + length filter, k-mer grouping (hash + radix
+    sort), pair increments, compaction of the nonzero pairs; the pairs stay on the device.
+    Roofline: k_md_pairs, SURVEY 8(d) 4 B per pair increment."""
+    import tempfile
+    fam, per_file, n_train = 200, 4000, 200_000
+    t0 = time.time()
+    p = synth.generate_arrays(n_train, fam, per_file=per_file)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    b = skm.SignatureBuilder(len(funcs), device=device)
+    b.add_batch(r, o, l, f, i)
+    kept = b.finish()
+    b.close()
+    nq = a.matrix_seqs
+    f0 = n_train // per_file
+    nfq = (nq + per_file - 1) // per_file
+    q = synth.generate_arrays((f0 + nfq) * per_file, fam, per_file=per_file, first_file=f0, n_files=nfq)
+    n = min(nq, len(q.seq_len))
+    end = int(q.seq_off[n - 1]) + int(q.seq_len[n - 1])
+    res, off, ln = q.residues[:end], q.seq_off[:n], q.seq_len[:n]
+    with tempfile.TemporaryDirectory(dir="/tmp") as d:
+        base = os.path.join(d, "kmer_data")
+        skm.mph_build(kept.keys, kept.data, base + ".mph", base + ".dat", seed=1, device=device)
+        db = skm.CmphKmerDb(base, device=device)
+    prep_s = time.time() - t0
+    md = skm.MatrixDistance(db, funcs, res, off, ln)
+    for _ in range(max(1, a.warmup)):
+        md.run()
+    steps = max(3, a.steps)
+    acc = {}
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        md.run()
+        for k, v in md.timings().items():
+            acc[k] = acc.get(k, 0.0) + v
+    wall = time.perf_counter() - t1
+    acc = {k: v / steps for k, v in acc.items()}
+    c = md.counters()
+    md.close()
+    db.close()
+    alg = 4 * c["increments"]
+    gbs = alg / (acc["pairs"] * 1e-3) / 1e9
+    return {"metric": "query k-mers/sec (lookup + all-vs-all shared signature k-mer counts)",
+            "value": c["windows"] * steps / wall, "unit": "k-mers/s", "ms_per_step": 1000.0 * wall / steps,
+            "pair_increments_per_s": c["increments"] / (acc["pairs"] * 1e-3),
+            "config": {"workload": f"C5: {n} query proteins of {fam} families, all-vs-all, 1 GPU (one tile)",
+                       "queries": n, "families": fam, "db_keys": int(len(kept.keys)), "windows": c["windows"],
+                       "hits": c["hits"], "pair_increments": c["increments"], "nonzero_pairs": c["pairs"]},
+            "phase_ms": acc,
+            "roofline": {"bound": "hbm", "kernel": "k_md_pairs", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
+                         "avg_launch_ms": acc["pairs"], "traffic": None},
+            "prep_s": prep_s}
 
 
 def _valid_windows(r, o, l, f) -> int:

@@ -228,6 +228,47 @@ int skm_annotate(skm_db* db, const uint8_t* residues, const uint64_t* seq_off, c
                  size_t n_seqs, const skm_annot_opts* opts, skm_calls* out);
 void skm_calls_free(skm_calls* c);
 
+/* ------------------------------------------------------------------------------------------
+ * All-vs-all shared-signature-k-mer counts.  Replaces MatrixDistance::compute
+ * (matrix_distance.h:45-170) as run by kmers-matrix-distance (kmers-matrix-distance.cc:94-212):
+ * process_aa_seq with ignore_hypothetical(true) feeds hit_cb (:123-152: hits whose seqlen lies
+ * outside mean +/- 2 sd of the record are dropped; sd = sqrt(var), or 0.1 seqlen when var == 0),
+ * kmer_hit_map[kmer] = set of SeqIdMap indices (seq_id_map.h:12-27), seq_dist[id1][id2]++ for
+ * every id1 < id2 of a k-mer's set (:176-196).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct skm_matrix skm_matrix;
+
+typedef struct skm_matrix_opts {
+    int32_t hypo_index;       /* function index of "hypothetical protein" (dropped); -1: none    */
+    uint32_t row_begin;       /* count only pairs with id1 in [row_begin, row_end): this GPU's    */
+    uint32_t row_end;         /* tile of the triangle (skm_matrix_tile_rows); 0, 0 = every row    */
+    uint32_t pad;
+    uint64_t max_tile_bytes;  /* bound on the dense u32 count tile in HBM (0: 60 % of free HBM);
+                                 larger tiles are processed in row bands                          */
+} skm_matrix_opts;
+
+typedef struct skm_pairs {
+    uint32_t* pairs;          /* [n][3] = (id1, id2, count), id1 < id2, sorted by (id1, id2)      */
+    uint64_t n;
+    uint64_t n_hits;          /* (kmer, sequence) hit records that passed the filters            */
+} skm_pairs;
+
+/* seq_idx[s]: SeqIdMap index of sequence s (index of the first sequence with its id, in input
+ * order; < n_idx).  residues / seq_off / seq_len as in skm_build_add_batch. */
+int skm_matrix_create(skm_matrix** out, skm_db* db, const uint8_t* residues, const uint64_t* seq_off,
+                      const uint32_t* seq_len, const uint32_t* seq_idx, size_t n_seqs, uint32_t n_idx);
+/* Device pipeline on the resident queries; the pairs stay on the device. */
+int skm_matrix_run(skm_matrix* m, const skm_matrix_opts* opts);
+/* [0]=hits [1]=group (hash + sort) [2]=pair increments [3]=compaction [4]=total (ms) */
+int skm_matrix_last_timings(skm_matrix* m, float* ms, int cap);
+/* [0]=windows [1]=hit records [2]=pair increments [3]=nonzero pairs */
+int skm_matrix_counters(skm_matrix* m, uint64_t* out, int cap);
+int skm_matrix_pairs(skm_matrix* m, skm_pairs* out);
+void skm_pairs_free(skm_pairs* p);
+void skm_matrix_destroy(skm_matrix* m);
+/* Row band of rank `rank` of `world` GPUs with (nearly) equal triangle area. */
+int skm_matrix_tile_rows(uint32_t n_idx, int rank, int world, uint32_t* row_begin, uint32_t* row_end);
+
 /* find_best_call (call_functions.tcc:347-659) on the host.  function_index: nfunc C strings
  * (function.index column 1).  out_func receives the called function (NUL-terminated).      */
 int skm_find_best_call(const skm_kmer_call* calls, size_t ncalls, const char* const* function_index,

@@ -29,6 +29,7 @@
 //    oracle_process_aa_seq   call_functions.tcc:259-338 + HitSet::process :35-103,
 //                            for_each_kmer kmer_data.h:76-102
 //    oracle_find_best_call   call_functions.tcc:347-659
+//    oracle_matrix_distance  kmers-matrix-distance.cc:94-212, matrix_distance.h:45-170
 // ============================================================================================
 
 #include <algorithm>
@@ -542,16 +543,12 @@ void hitset_process(std::vector<Hit>& hits, double seqlen, uint16_t& current_fI,
 // One query sequence.  Returns the number of calls written (<= cap) or the needed count.
 }  // extern "C"
 
-// fetch(ptr) -> const oracle_stored* or nullptr: CmphKmerDb::fetch (idx >= size -> no callback,
-// cmph_kmer.h:139-147) or KeptKmerDB::fetch (exact key, kept_kmer_db.h:20-27).
-template <class Fetch>
-static int64_t process_aa_seq_impl(Fetch fetch, const uint8_t* seq, uint32_t len, const oracle_annot_opts* opts,
-                                   oracle_call* out, uint64_t cap) {
+// for_each_kmer<8> (kmer_data.h:76-102): only upper-case 'X' and '*' are ambiguous; a window is
+// skipped when the next ambiguous byte lies inside it OR right after it (kend >= next_ambig,
+// :90), then the scan restarts after that byte (:93).  cb(ptr, offset) per yielded window.
+template <class CB>
+static void for_each_kmer8(const uint8_t* seq, uint32_t len, CB cb) {
     const int N = 8;
-    std::vector<Hit> hits;
-    std::vector<oracle_call> calls;
-    uint16_t current_fI = kUndefinedFunction;
-    double seqlen = static_cast<double>(len);
     const uint8_t* ptr = seq;
     const uint8_t* end = seq + len;
     auto is_ambig = [](uint8_t c) { return c == '*' || c == 'X'; };
@@ -560,7 +557,7 @@ static int64_t process_aa_seq_impl(Fetch fetch, const uint8_t* seq, uint32_t len
         return from;
     };
     const uint8_t* next_ambig = find_ambig(ptr);
-    // for_each_kmer: last_kmer = end - N (pointer compare; no windows when len < N)
+    // last_kmer = end - N (pointer compare; no windows when len < N)
     while (len >= (uint32_t)N && ptr <= end - N) {
         const uint8_t* kend = ptr + N;
         if (next_ambig != end && kend >= next_ambig) {
@@ -568,7 +565,21 @@ static int64_t process_aa_seq_impl(Fetch fetch, const uint8_t* seq, uint32_t len
             next_ambig = find_ambig(ptr);
             continue;
         }
-        size_t offset = (size_t)(ptr - seq);
+        cb(ptr, (size_t)(ptr - seq));
+        ptr++;
+    }
+}
+
+// fetch(ptr) -> const oracle_stored* or nullptr: CmphKmerDb::fetch (idx >= size -> no callback,
+// cmph_kmer.h:139-147) or KeptKmerDB::fetch (exact key, kept_kmer_db.h:20-27).
+template <class Fetch>
+static int64_t process_aa_seq_impl(Fetch fetch, const uint8_t* seq, uint32_t len, const oracle_annot_opts* opts,
+                                   oracle_call* out, uint64_t cap) {
+    std::vector<Hit> hits;
+    std::vector<oracle_call> calls;
+    uint16_t current_fI = kUndefinedFunction;
+    double seqlen = static_cast<double>(len);
+    for_each_kmer8(seq, len, [&](const uint8_t* ptr, size_t offset) {
         const oracle_stored* kp = fetch(ptr);
         if (kp) {
             const oracle_stored& kdata = *kp;
@@ -590,8 +601,7 @@ static int64_t process_aa_seq_impl(Fetch fetch, const uint8_t* seq, uint32_t len
                 }
             }
         }
-        ptr++;
-    }
+    });
     if ((int)hits.size() >= opts->min_hits) hitset_process(hits, seqlen, current_fI, calls, *opts);
     for (size_t i = 0; i < calls.size() && i < cap; ++i) out[i] = calls[i];
     return (int64_t)calls.size();
@@ -656,6 +666,58 @@ int64_t oracle_annotate(const oracle_bdz* db, const oracle_stored* dat, const ui
     }
     call_off[n_seqs] = total;
     return total <= cap ? (int64_t)total : -1;
+}
+
+// --------------------------------------------------------------------------------------------
+//  kmers-matrix-distance (kmers-matrix-distance.cc:94-212; MatrixDistance::compute,
+//  matrix_distance.h:45-170).  process_fasta_stream_parallel (call_functions.tcc:157-215) runs
+//  process_aa_seq with ignore_hypothetical(true) (:164), so hit_cb (:123-152) sees every window of
+//  for_each_kmer whose record is not "hypothetical protein" (call_functions.tcc:285-291):
+//     stddev = var == 0 ? seqlen * 0.1 : sqrt(var);  keep iff mean - 2 sd <= seqlen <= mean + 2 sd
+//  and inserts the sequence's SeqIdMap index (seq_id_map.h:12-27) into kmer_hit_map[kmer] (a set:
+//  one entry per (kmer, index)).  Then for every k-mer and every id1 < id2 of its set
+//  seq_dist[id1][id2]++ (:176-196).  The HitSet / find_best_call results do not feed the matrix.
+//  seq_idx[s]: the SeqIdMap index of sequence s (first occurrence of its id).  Output: (id1, id2,
+//  count) triples sorted by (id1, id2) (the reference prints hash order; compare as sets).
+//  Returns the number of pairs (writes at most cap).
+// --------------------------------------------------------------------------------------------
+int64_t oracle_matrix_distance(const oracle_bdz* db, const oracle_stored* dat, const uint8_t* residues,
+                               const uint64_t* seq_off, const uint32_t* seq_len, const uint32_t* seq_idx,
+                               uint64_t n_seqs, int32_t hypo_index, uint32_t* out, uint64_t cap) {
+    std::map<uint64_t, std::vector<uint32_t>> hit_map;  // kmer -> indices (deduplicated below)
+    for (uint64_t s = 0; s < n_seqs; ++s) {
+        const double seqlen = static_cast<double>(seq_len[s]);
+        for_each_kmer8(residues + seq_off[s], seq_len[s], [&](const uint8_t* ptr, size_t) {
+            const uint32_t idx = oracle_bdz_search(db, ptr, 8);
+            if (idx >= db->m) return;  // fetch: no callback on a miss (cmph_kmer.h:143-146)
+            const oracle_stored& kd = dat[idx];
+            if (hypo_index >= 0 && kd.function_index == (uint16_t)hypo_index) return;
+            const double mean = static_cast<double>(kd.mean);
+            const double stddev = kd.var == 0 ? seqlen * 0.1 : std::sqrt(static_cast<double>(kd.var));
+            const double cutoff_b = mean - stddev * 2.0;
+            const double cutoff_t = mean + stddev * 2.0;
+            if (seqlen < cutoff_b || seqlen > cutoff_t) return;
+            hit_map[load_key(ptr)].push_back(seq_idx[s]);
+        });
+    }
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> dist;
+    for (auto& kv : hit_map) {
+        std::vector<uint32_t>& v = kv.second;
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        for (size_t a = 0; a < v.size(); ++a)
+            for (size_t b = a + 1; b < v.size(); ++b) dist[{v[a], v[b]}]++;
+    }
+    uint64_t n = 0;
+    for (auto& kv : dist) {
+        if (n < cap) {
+            out[3 * n] = kv.first.first;
+            out[3 * n + 1] = kv.first.second;
+            out[3 * n + 2] = kv.second;
+        }
+        ++n;
+    }
+    return (int64_t)n;
 }
 
 // --------------------------------------------------------------------------------------------

@@ -17,7 +17,8 @@ import numpy as np
 __all__ = [
     "SkmError", "lib", "K", "UNDEFINED_FUNCTION", "STORED_DTYPE", "CALL_DTYPE",
     "SignatureBuilder", "KeptKmers", "CmphKmerDb", "FunctionCaller", "mph_build",
-    "kmer_to_str", "str_to_kmer", "keys_from_strings", "device_count",
+    "kmer_to_str", "str_to_kmer", "keys_from_strings", "device_count", "MatrixDistance", "SeqIdMap",
+    "matrix_tile_rows",
 ]
 
 K = 8
@@ -58,6 +59,15 @@ class _Calls(C.Structure):
                 ("n_calls", C.c_uint64), ("n_windows", C.c_uint64)]
 
 
+class _MatrixOpts(C.Structure):
+    _fields_ = [("hypo_index", C.c_int32), ("row_begin", C.c_uint32), ("row_end", C.c_uint32), ("pad", C.c_uint32),
+                ("max_tile_bytes", C.c_uint64)]
+
+
+class _Pairs(C.Structure):
+    _fields_ = [("pairs", C.POINTER(C.c_uint32)), ("n", C.c_uint64), ("n_hits", C.c_uint64)]
+
+
 _P = C.c_void_p
 _SIGS = {
     "skm_last_error": (C.c_char_p, []),
@@ -95,6 +105,14 @@ _SIGS = {
     "skm_query_destroy": (None, [_P]),
     "skm_annotate": (C.c_int, [_P, _P, _P, _P, C.c_size_t, C.POINTER(_AnnotOpts), C.POINTER(_Calls)]),
     "skm_calls_free": (None, [C.POINTER(_Calls)]),
+    "skm_matrix_create": (C.c_int, [C.POINTER(_P), _P, _P, _P, _P, _P, C.c_size_t, C.c_uint32]),
+    "skm_matrix_run": (C.c_int, [_P, C.POINTER(_MatrixOpts)]),
+    "skm_matrix_last_timings": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int]),
+    "skm_matrix_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
+    "skm_matrix_pairs": (C.c_int, [_P, C.POINTER(_Pairs)]),
+    "skm_pairs_free": (None, [C.POINTER(_Pairs)]),
+    "skm_matrix_destroy": (None, [_P]),
+    "skm_matrix_tile_rows": (C.c_int, [C.c_uint32, C.c_int, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "skm_find_best_call": (C.c_int, [_P, C.c_size_t, C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(C.c_uint16),
                                      C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_char_p, C.c_size_t]),
 }
@@ -496,3 +514,100 @@ def find_best_call(calls: np.ndarray, function_index):
     """Host find_best_call (call_functions.tcc:347-659) over one sequence's calls, without a DB:
     -> (function_index, function, score, offset)."""
     return _find_best_call(calls, _fi_array(function_index), len(function_index))
+
+
+class SeqIdMap:
+    """SeqIdMap (seq_id_map.h:7-35): id -> index in order of first appearance."""
+
+    def __init__(self):
+        self._index = {}
+        self._ids = []
+
+    def lookup_id(self, id_: str) -> int:
+        i = self._index.get(id_)
+        if i is None:
+            i = len(self._ids)
+            self._index[id_] = i
+            self._ids.append(id_)
+        return i
+
+    def lookup_index(self, i: int) -> str:
+        return self._ids[i]
+
+    def __len__(self):
+        return len(self._ids)
+
+
+def matrix_tile_rows(n_idx: int, rank: int, world: int):
+    """Row band [begin, end) of GPU `rank` of `world` with (nearly) equal upper-triangle area."""
+    a, b = C.c_uint32(), C.c_uint32()
+    _check(lib().skm_matrix_tile_rows(n_idx, rank, world, C.byref(a), C.byref(b)))
+    return a.value, b.value
+
+
+class MatrixDistance:
+    """MatrixDistance<FunctionCaller<CmphKmerDb>> (matrix_distance.h:30-179) / kmers-matrix-distance
+    (kmers-matrix-distance.cc:94-212): shared-signature-k-mer counts over every pair of query
+    sequences, on the GPU (skm_matrix_*).  seq_idx: SeqIdMap index per sequence (default: 0..n-1);
+    rows=(begin, end) restricts the counts to pairs whose first index lies in [begin, end) -- one
+    GPU's tile (matrix_tile_rows)."""
+
+    def __init__(self, db: CmphKmerDb, function_index, residues, seq_off, seq_len, seq_idx=None,
+                 n_idx: int | None = None):
+        self.db = db
+        fi = read_function_index(function_index) if isinstance(function_index, str) else list(function_index)
+        if "hypothetical protein" not in fi:  # call_functions.tcc:269-274 exits the process
+            raise SkmError("Cannot find hypothetical protein index")
+        self.hypo_index = fi.index("hypothetical protein")
+        residues = np.ascontiguousarray(residues, dtype=np.uint8)
+        seq_off = np.ascontiguousarray(seq_off, dtype=np.uint64)
+        seq_len = np.ascontiguousarray(seq_len, dtype=np.uint32)
+        if seq_idx is None:
+            seq_idx = np.arange(len(seq_len), dtype=np.uint32)
+        seq_idx = np.ascontiguousarray(seq_idx, dtype=np.uint32)
+        self.n_idx = int(n_idx if n_idx is not None else (int(seq_idx.max()) + 1 if len(seq_idx) else 0))
+        self._h = C.c_void_p()
+        _check(lib().skm_matrix_create(C.byref(self._h), db._h, _ptr(residues), _ptr(seq_off), _ptr(seq_len),
+                                       _ptr(seq_idx), len(seq_len), self.n_idx))
+
+    def run(self, rows=None, max_tile_bytes: int = 0):
+        a, b = rows if rows is not None else (0, 0)
+        opts = _MatrixOpts(self.hypo_index, a, b, 0, max_tile_bytes)
+        _check(lib().skm_matrix_run(self._h, C.byref(opts)))
+
+    def timings(self) -> dict:
+        ms = (C.c_float * 5)()
+        n = lib().skm_matrix_last_timings(self._h, ms, 5)
+        return dict(zip(["hits", "group", "pairs", "emit", "total"], list(ms)[:n]))
+
+    def counters(self) -> dict:
+        v = (C.c_uint64 * 4)()
+        n = lib().skm_matrix_counters(self._h, v, 4)
+        return dict(zip(["windows", "hits", "increments", "pairs"], [int(x) for x in list(v)[:n]]))
+
+    def pairs(self) -> np.ndarray:
+        """(n, 3) u32 (id1, id2, count), id1 < id2, sorted by (id1, id2)."""
+        out = _Pairs()
+        _check(lib().skm_matrix_pairs(self._h, C.byref(out)))
+        try:
+            n = int(out.n)
+            if n == 0:
+                return np.zeros((0, 3), np.uint32)
+            return np.ctypeslib.as_array(out.pairs, shape=(n * 3,)).reshape(n, 3).copy()
+        finally:
+            lib().skm_pairs_free(C.byref(out))
+
+    def compute(self, rows=None):
+        self.run(rows)
+        return self.pairs()
+
+    def close(self):
+        if self._h:
+            lib().skm_matrix_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

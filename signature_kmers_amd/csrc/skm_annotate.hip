@@ -24,53 +24,10 @@
 
 #include "skm_bdz.h"
 #include "skm_common.h"
+#include "skm_lookup.h"
 #include "skm_util.h"
 
 namespace skm {
-
-constexpr uint32_t NO_HIT = 0xFFFFFFFFu;
-constexpr int LK_THREADS = 256;
-constexpr int LK_POS = 16;
-
-struct QMeta {
-    uint64_t pstart;
-    uint32_t len;
-    uint32_t pad;
-};
-
-struct DevBdz {
-    const uint32_t* g;          // g as little-endian u32 words (16 entries each), padded
-    const uint32_t* ranktable;
-    const uint16_t* dat;        // 5 u16 per record
-    uint32_t m, r, b, seed;
-    uint64_t r_magic;           // fastmod: ceil(2^64 / r)
-    // exact-key mode (KeptKmerDB, kept_kmer_db.h:20-27): open-addressing table of the kept keys
-    const unsigned long long* xkeys;  // [mask+1], 0 = empty (a k-mer key is never 0)
-    const uint32_t* xidx;             // record index of the key in xkeys[h]
-    uint64_t xmask;
-    uint32_t xshift;
-};
-
-__device__ __forceinline__ uint64_t xmix(uint64_t k) {  // murmur3 fmix64 (bijective)
-    k ^= k >> 33;
-    k *= 0xff51afd7ed558ccdull;
-    k ^= k >> 33;
-    k *= 0xc4ceb9fe1a85ec53ull;
-    k ^= k >> 33;
-    return k;
-}
-
-// KeptKmerDB::fetch: a hit iff the key is a kept k-mer; returns D.m on a miss.
-__device__ __forceinline__ uint32_t exact_lookup(const DevBdz& D, uint32_t lo, uint32_t hi) {
-    const uint64_t k = ((uint64_t)hi << 32) | lo;
-    uint64_t h = xmix(k) >> D.xshift;
-    for (;;) {
-        const uint64_t t = D.xkeys[h];
-        if (t == k) return D.xidx[h];
-        if (t == 0) return D.m;
-        h = (h + 1) & D.xmask;
-    }
-}
 
 __global__ void k_exact_insert(const uint64_t* __restrict__ keys, uint64_t n, unsigned long long* __restrict__ tk,
                                uint32_t* __restrict__ ti, uint64_t mask, uint32_t shift, uint32_t* __restrict__ bad) {
@@ -96,73 +53,6 @@ __global__ void k_exact_insert(const uint64_t* __restrict__ keys, uint64_t n, un
     }
 }
 
-__device__ __forceinline__ uint32_t fastmod(uint32_t a, uint64_t M, uint32_t d) {
-    uint64_t low = M * a;
-    return (uint32_t)__umul64hi(low, (uint64_t)d);
-}
-
-__device__ __forceinline__ void jmix(uint32_t& a, uint32_t& b, uint32_t& c) {
-    a -= b; a -= c; a ^= (c >> 13);
-    b -= c; b -= a; b ^= (a << 8);
-    c -= a; c -= b; c ^= (b >> 13);
-    a -= b; a -= c; a ^= (c >> 12);
-    b -= c; b -= a; b ^= (a << 16);
-    c -= a; c -= b; c ^= (b >> 5);
-    a -= b; a -= c; a ^= (c >> 3);
-    b -= c; b -= a; b ^= (a << 10);
-    c -= a; c -= b; c ^= (b >> 15);
-}
-
-__device__ __forceinline__ uint32_t gval(const uint32_t* g, uint32_t i) { return (g[i >> 4] >> ((i & 15u) * 2)) & 3u; }
-
-__device__ __forceinline__ uint32_t unassigned_in(uint32_t w) { return __popc(w & (w >> 1) & 0x55555555u); }
-
-// cmph bdz_search for an 8-byte key given as two little-endian u32 words
-__device__ __forceinline__ uint32_t bdz_lookup(const DevBdz& D, uint32_t lo, uint32_t hi) {
-    uint32_t a = 0x9e3779b9u + lo, b = 0x9e3779b9u + hi, c = D.seed + 8u;
-    jmix(a, b, c);
-    const uint32_t h0 = fastmod(a, D.r_magic, D.r);
-    const uint32_t h1 = fastmod(b, D.r_magic, D.r) + D.r;
-    const uint32_t h2 = fastmod(c, D.r_magic, D.r) + 2u * D.r;
-    const uint32_t sel = (gval(D.g, h0) + gval(D.g, h1) + gval(D.g, h2)) % 3u;
-    const uint32_t v = sel == 0 ? h0 : (sel == 1 ? h1 : h2);
-    // rank(v): ranktable[v >> b] + assigned entries in [ (v>>b)<<b, v )
-    const uint32_t blk = v >> D.b;
-    uint32_t rank = D.ranktable[blk];
-    uint32_t i = blk << D.b;
-    // head: up to the next 16-aligned entry
-    while (i < v && (i & 15u)) {
-        rank += gval(D.g, i) != 3u;
-        ++i;
-    }
-    for (; i + 16 <= v; i += 16) rank += 16u - unassigned_in(D.g[i >> 4]);
-    if (i < v) {
-        const uint32_t nb = (v - i) * 2u;
-        const uint32_t w = D.g[i >> 4] & ((1u << nb) - 1u);
-        rank += (v - i) - unassigned_in(w);
-    }
-    return rank;
-}
-
-__device__ __forceinline__ bool ambig(uint32_t c) { return c == 'X' || c == '*'; }
-
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// key bytes t..t+7 of the 32-byte window w[8]
-__device__ __forceinline__ void key_at(const uint32_t (&w)[8], int t, uint32_t& lo, uint32_t& hi) {
-    const int wi = t >> 2, sh = (t & 3) * 8;
-    if (sh == 0) {
-        lo = w[wi];
-        hi = w[wi + 1];
-    } else {
-        lo = (w[wi] >> sh) | (w[wi + 1] << (32 - sh));
-        hi = (w[wi + 1] >> sh) | (w[wi + 2] << (32 - sh));
-    }
-}
 
 // MODE: LK_BDZ7 = BDZ with rank blocks of 128 (cmph's default b = 7), LK_EXACT = kept-k-mer
 // table, LK_BDZ = BDZ with any b (per-window search)
@@ -756,34 +646,20 @@ __global__ void k_gather_calls(const skm_kmer_call* __restrict__ slots, const ui
     for (uint64_t j = a; j < e; ++j) out[j] = slots[src + (j - a)];
 }
 
-struct Scanner {
-    DevBuf tiles, total;
-    // out: n+1 u64 entries
-    void run(const uint32_t* in, uint64_t n, uint64_t* out, hipStream_t st) {
-        uint64_t nt = std::max<uint64_t>(1, ceil_div(n, SC_TILE));
-        tiles.ensure(8 * nt);
-        total.ensure(8);
-        hipLaunchKernelGGL(k_scan_tiles, dim3((uint32_t)nt), dim3(SC_THREADS), 0, st, in, n, out, tiles.as<uint64_t>());
-        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, st, tiles.as<uint64_t>(), nt, total.as<uint64_t>());
-        hipLaunchKernelGGL(k_scan_add, dim3((uint32_t)ceil_div(n + 1, 256)), dim3(256), 0, st, out, n,
-                           tiles.as<uint64_t>(), total.as<uint64_t>());
-        SKM_HIP(hipGetLastError());
-    }
-};
+void Scanner::run(const uint32_t* in, uint64_t n, uint64_t* out, hipStream_t st) {
+    uint64_t nt = std::max<uint64_t>(1, ceil_div(n, SC_TILE));
+    tiles.ensure(8 * nt);
+    total.ensure(8);
+    hipLaunchKernelGGL(k_scan_tiles, dim3((uint32_t)nt), dim3(SC_THREADS), 0, st, in, n, out, tiles.as<uint64_t>());
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, st, tiles.as<uint64_t>(), nt, total.as<uint64_t>());
+    hipLaunchKernelGGL(k_scan_add, dim3((uint32_t)ceil_div(n + 1, 256)), dim3(256), 0, st, out, n,
+                       tiles.as<uint64_t>(), total.as<uint64_t>());
+    SKM_HIP(hipGetLastError());
+}
 
 }  // namespace skm
 
 using namespace skm;
-
-struct skm_db {
-    int device = 0;
-    bool exact = false;          // KeptKmerDB semantics (skm_db_open_kept)
-    uint32_t m = 0;              // hash size (BDZ) or number of kept keys (exact)
-    Bdz bdz;
-    uint64_t dat_records = 0;
-    DevBuf d_g, d_rank, d_dat, d_xkeys, d_xidx;
-    DevBdz dev{};
-};
 
 struct skm_query {
     skm_db* db = nullptr;

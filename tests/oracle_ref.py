@@ -51,6 +51,8 @@ def olib():
         _lib.oracle_annotate_exact.restype = C.c_int64
         _lib.oracle_annotate_exact.argtypes = [P, P, C.c_uint64, P, P, P, C.c_uint64, C.POINTER(AnnotOpts), P, P,
                                                C.c_uint64]
+        _lib.oracle_matrix_distance.restype = C.c_int64
+        _lib.oracle_matrix_distance.argtypes = [P, P, P, P, P, P, C.c_uint64, C.c_int32, P, C.c_uint64]
         _lib.oracle_find_best_call.argtypes = [P, C.c_uint64, C.POINTER(C.c_char_p), C.c_uint64, P, P, P,
                                                C.c_char_p, C.c_uint64]
     return _lib
@@ -156,6 +158,22 @@ def annotate_exact(keys, data, residues, seq_off, seq_len, min_hits=5, max_gap=2
                                        C.byref(opts), _p(off), _p(calls), cap)
     assert tot >= 0
     return off, calls[:tot].copy()
+
+
+def matrix_distance(bdz: Bdz, dat: bytes, residues, seq_off, seq_len, seq_idx, hypo_index=-1):
+    """kmers-matrix-distance pair counts: (n, 3) u32 array of (id1, id2, count), sorted."""
+    residues = np.ascontiguousarray(residues, np.uint8)
+    seq_off = np.ascontiguousarray(seq_off, np.uint64)
+    seq_len = np.ascontiguousarray(seq_len, np.uint32)
+    seq_idx = np.ascontiguousarray(seq_idx, np.uint32)
+    datb = np.frombuffer(dat, np.uint8).copy() if dat else np.zeros(10, np.uint8)
+    L = olib()
+    n = int(L.oracle_matrix_distance(bdz.h, _p(datb), _p(residues), _p(seq_off), _p(seq_len), _p(seq_idx),
+                                     len(seq_len), hypo_index, None, 0))
+    out = np.zeros((max(n, 1), 3), np.uint32)
+    L.oracle_matrix_distance(bdz.h, _p(datb), _p(residues), _p(seq_off), _p(seq_len), _p(seq_idx), len(seq_len),
+                             hypo_index, _p(out), n)
+    return out[:n].copy()
 
 
 def find_best_call(calls: np.ndarray, function_index: list):

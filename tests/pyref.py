@@ -148,3 +148,31 @@ def call_windows(seq: bytes):
         out.append((p, int.from_bytes(seq[p:p + 8], "little")))
         p += 1
     return out
+
+
+def matrix_distance(seqs, seq_idx, fetch, hypo_index):
+    """kmers-matrix-distance (kmers-matrix-distance.cc:123-196): every window of for_each_kmer whose
+    record (fetch(key) -> (avg, func, mean, median, var) or None) is not hypothetical and whose
+    sequence length lies within mean -/+ 2 sd (sd = sqrt(var), or 0.1 * seqlen when var == 0) adds
+    the sequence's index to the k-mer's set; every pair id1 < id2 of a set counts once.
+    Returns {(id1, id2): count}."""
+    import math
+    sets = {}
+    for s, seq in enumerate(seqs):
+        seqlen = float(len(seq))
+        for _, key in call_windows(seq):
+            kd = fetch(key)
+            if kd is None or kd[1] == hypo_index:
+                continue
+            mean = float(kd[2])
+            sd = seqlen * 0.1 if kd[4] == 0 else math.sqrt(float(kd[4]))
+            if seqlen < mean - sd * 2.0 or seqlen > mean + sd * 2.0:
+                continue
+            sets.setdefault(key, set()).add(int(seq_idx[s]))
+    dist = {}
+    for ids in sets.values():
+        v = sorted(ids)
+        for a in range(len(v)):
+            for b in range(a + 1, len(v)):
+                dist[(v[a], v[b])] = dist.get((v[a], v[b]), 0) + 1
+    return dist
