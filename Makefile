@@ -12,7 +12,7 @@ HIP_SRCS = $(SRC)/skm_build.hip $(SRC)/skm_annotate.hip $(SRC)/skm_matrix.hip
 CPP_SRCS = $(SRC)/skm_host.cpp $(SRC)/skm_bdz.cpp
 OBJS     = $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(CPP_SRCS))
 LIB      = signature_kmers_amd/libskm.so
-TOOLS    = bin/kmers-build-signatures bin/kmers-call-functions bin/kmers-annotate-seqs bin/skm-front-probe
+TOOLS    = bin/kmers-build-signatures bin/kmers-call-functions bin/kmers-annotate-seqs bin/kmers-matrix-distance bin/skm-front-probe
 ORACLE   = oracle/liboracle_skm.so
 FRONT    = $(OBJDIR)/front/skm_front.o $(OBJDIR)/front/skm_caller.o
 FRONTH   = $(wildcard $(SRC)/front/*.h) include/skm.h

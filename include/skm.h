@@ -261,7 +261,8 @@ int skm_matrix_create(skm_matrix** out, skm_db* db, const uint8_t* residues, con
 int skm_matrix_run(skm_matrix* m, const skm_matrix_opts* opts);
 /* [0]=hits [1]=group (hash + sort) [2]=pair increments [3]=compaction [4]=total (ms) */
 int skm_matrix_last_timings(skm_matrix* m, float* ms, int cap);
-/* [0]=windows [1]=hit records [2]=pair increments [3]=nonzero pairs */
+/* [0]=windows [1]=hit records [2]=pair increments [3]=nonzero pairs [4]=distinct hit k-mers
+ * (kmer_hit_map.size(), kmers-matrix-distance.cc:169) */
 int skm_matrix_counters(skm_matrix* m, uint64_t* out, int cap);
 int skm_matrix_pairs(skm_matrix* m, skm_pairs* out);
 void skm_pairs_free(skm_pairs* p);

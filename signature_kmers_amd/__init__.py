@@ -581,9 +581,9 @@ class MatrixDistance:
         return dict(zip(["hits", "group", "pairs", "emit", "total"], list(ms)[:n]))
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 4)()
-        n = lib().skm_matrix_counters(self._h, v, 4)
-        return dict(zip(["windows", "hits", "increments", "pairs"], [int(x) for x in list(v)[:n]]))
+        v = (C.c_uint64 * 5)()
+        n = lib().skm_matrix_counters(self._h, v, 5)
+        return dict(zip(["windows", "hits", "increments", "pairs", "kmers"], [int(x) for x in list(v)[:n]]))
 
     def pairs(self) -> np.ndarray:
         """(n, 3) u32 (id1, id2, count), id1 < id2, sorted by (id1, id2)."""

@@ -387,7 +387,7 @@ struct skm_matrix {
     DevBuf d_res, d_meta, d_idx, d_rkey, d_ridx, d_nrec, d_tab, d_comp, d_comp2, d_hist, d_hoff, d_flag, d_S,
         d_seg, d_tile, d_rcnt, d_roff, d_out, d_out2, d_incs;
     Scanner scan;
-    uint64_t n_hits = 0, n_incs = 0, n_pairs = 0;
+    uint64_t n_hits = 0, n_incs = 0, n_pairs = 0, n_groups = 0;
     bool ran = false;
 };
 
@@ -427,6 +427,7 @@ void matrix_run(skm_matrix* M, const skm_matrix_opts* o) {
     M->n_hits = n;
     M->n_incs = 0;
     M->n_pairs = 0;
+    M->n_groups = 0;
     // 2. group: slot table + radix sort of (slot, index) composites + group boundaries
     const uint32_t idx_bits = (uint32_t)std::max(1, ilog2_ceil(std::max<uint64_t>(M->nidx, 2)));
     const int lg = std::max(4, ilog2_ceil(2 * std::max<uint64_t>(n, 1)));
@@ -469,6 +470,7 @@ void matrix_run(skm_matrix* M, const skm_matrix_opts* o) {
         hipLaunchKernelGGL(k_md_segstart, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, st, M->d_flag.as<uint32_t>(),
                            M->d_S.as<uint64_t>(), n, M->d_seg.as<uint64_t>());
         SKM_HIP(hipGetLastError());
+        SKM_HIP(hipMemcpyAsync(&M->n_groups, M->d_S.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
     }
     SKM_HIP(hipEventRecord(M->ev[2], st));
     // 3. pair counts, tile by tile (rows [r0, r1) cut into sub-tiles that fit the budget)
@@ -667,8 +669,8 @@ int skm_matrix_last_timings(skm_matrix* m, float* ms, int cap) {
 
 int skm_matrix_counters(skm_matrix* m, uint64_t* out, int cap) {
     if (!m || !out) return SKM_E_ARG;
-    const uint64_t v[4] = {m->n_windows, m->n_hits, m->n_incs, m->n_pairs};
-    const int n = std::min(cap, 4);
+    const uint64_t v[5] = {m->n_windows, m->n_hits, m->n_incs, m->n_pairs, m->n_groups};
+    const int n = std::min(cap, 5);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }

@@ -1,0 +1,135 @@
+// kmers-matrix-distance -- drop-in for the reference's main (kmers-matrix-distance.cc:94-212).
+//
+//   kmers-matrix-distance [options] data-dir input-file
+// Opens <data-dir>/kmer_data.mph + .dat (CmphKmerDb) into HBM, reads <data-dir>/function.index,
+// parses the FASTA file (process_fasta_stream_parallel's parse: records with an empty id are
+// dropped, every other id gets its SeqIdMap index in file order, call_functions.tcc:169-181) and
+// prints "seq1\tseq2\tcount\n" for every pair of sequences sharing count signature-k-mer hits
+// (:199-211) to stdout, like the reference (which parses -o but never uses it).  The pair counts
+// run on the GPU (skm_matrix_*): lookups, hit_cb's length filter (:123-152), k-mer grouping, pair
+// increments, compaction.  Order: sorted by (seq1 index, seq2 index) (the reference prints the
+// hash order of its concurrent maps).  --min-hits, --debug-hits, --verbose and -j are accepted
+// and, as in the reference main, have no effect on the output.
+// Extra options: --device N, --max-tile-bytes B (bound on the dense count tile in HBM).
+#include <sys/stat.h>
+
+#include <cstdio>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "skm.h"
+#include "skm_caller.h"
+#include "skm_front.h"
+
+using namespace skmf;
+
+namespace {
+
+void die(const std::string& m) {
+    std::cerr << m << "\n";
+    std::exit(1);
+}
+
+bool file_exists(const std::string& p) {
+    struct stat sb;
+    return stat(p.c_str(), &sb) == 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    Options op;
+    op.specs = {{"data-dir", 'd', false, false},   {"input-file", 'i', false, false}, {"output-file", 'o', false, false},
+                {"min-hits", 0, false, false},    {"n-threads", 'j', false, false},  {"debug-hits", 0, true, false},
+                {"verbose", 0, true, false},      {"help", 'h', true, false},        {"device", 0, false, false},
+                {"max-tile-bytes", 0, false, false}};
+    op.positional = {"data-dir", "input-file"};
+    std::string err;
+    if (!op.parse(argc, argv, err)) die(err);
+    if (op.has("help")) {
+        std::cout << "Usage: " << argv[0] << " data-dir input-file\nAllowed options:\n"
+                  << "  -d [ --data-dir ] arg       Data directory\n"
+                  << "  -i [ --input-file ] arg     Input fasta file\n"
+                  << "  -o [ --output-file ] arg    Output file\n"
+                  << "  --min-hits arg              Minimum shared kmer hits to emit a match\n"
+                  << "  -j [ --n-threads ] arg      Number of threads\n"
+                  << "  --debug-hits                Debug kmer hits\n"
+                  << "  --verbose                   Verbose mode\n"
+                  << "  --device arg                HIP device ordinal (default 0)\n"
+                  << "  --max-tile-bytes arg        HBM bound of the dense pair-count tile (default: 60 % of free)\n"
+                  << "  -h [ --help ]               show this help message\n\n";
+        return 0;
+    }
+    const int device = std::atoi(op.get("device", "0").c_str());
+    const std::string data_dir = op.get("data-dir");
+    const std::string db_base = path_join(data_dir, "kmer_data");
+    const std::string mph = db_base + ".mph", dat = db_base + ".dat";
+    if (!file_exists(mph)) die("Database \"" + db_base + "\" does not exist");
+    skm_db* db = nullptr;
+    if (skm_db_open(&db, mph.c_str(), dat.c_str(), device)) die(skm_last_error());
+    std::vector<std::string> fidx;
+    if (!read_function_index(path_join(data_dir, "function.index"), fidx, err)) die(err);
+
+    FastaFile f;
+    const std::string in = op.get("input-file");
+    if (!in.empty()) parse_fasta_file(in, f);  // an unreadable file parses as empty (fs::ifstream)
+    // SeqIdMap (seq_id_map.h:12-27): index of the first record with each id
+    std::unordered_map<std::string, uint32_t> id_to_index;
+    std::vector<const std::string*> index_to_id;
+    std::vector<uint32_t> seq_idx(f.size());
+    for (size_t r = 0; r < f.size(); ++r) {
+        auto it = id_to_index.find(f.ids[r]);
+        if (it == id_to_index.end()) {
+            it = id_to_index.emplace(f.ids[r], (uint32_t)index_to_id.size()).first;
+            index_to_id.push_back(&f.ids[r]);
+        }
+        seq_idx[r] = it->second;
+    }
+    int hypo = -1;
+    for (size_t i = 0; i < fidx.size(); ++i)
+        if (fidx[i] == "hypothetical protein") {
+            hypo = (int)i;
+            break;
+        }
+    if (hypo < 0 && f.size() > 0) die("Cannot find hypothetical protein index");  // call_functions.tcc:269-274
+
+    skm_matrix* m = nullptr;
+    if (skm_matrix_create(&m, db, f.residues.data(), f.off.data(), f.len.data(), seq_idx.data(), f.size(),
+                          (uint32_t)index_to_id.size()))
+        die(skm_last_error());
+    skm_matrix_opts mo;
+    std::memset(&mo, 0, sizeof(mo));
+    mo.hypo_index = hypo;
+    mo.max_tile_bytes = std::strtoull(op.get("max-tile-bytes", "0").c_str(), nullptr, 10);
+    if (skm_matrix_run(m, &mo)) die(skm_last_error());
+    uint64_t ctr[5] = {0, 0, 0, 0, 0};
+    skm_matrix_counters(m, ctr, 5);
+    std::cerr << "kmer_hit_map size " << ctr[4] << "\n";
+    skm_pairs pairs;
+    if (skm_matrix_pairs(m, &pairs)) die(skm_last_error());
+    std::cerr << "write output\n";
+    std::string buf;
+    buf.reserve(1 << 20);
+    for (uint64_t i = 0; i < pairs.n; ++i) {
+        const uint32_t* p = pairs.pairs + 3 * i;
+        buf += *index_to_id[p[0]];
+        buf += '\t';
+        buf += *index_to_id[p[1]];
+        buf += '\t';
+        buf += std::to_string(p[2]);
+        buf += '\n';
+        if (buf.size() > (1u << 20)) {
+            std::fwrite(buf.data(), 1, buf.size(), stdout);
+            buf.clear();
+        }
+    }
+    std::fwrite(buf.data(), 1, buf.size(), stdout);
+    std::fflush(stdout);
+    skm_pairs_free(&pairs);
+    skm_matrix_destroy(m);
+    skm_db_close(db);
+    return 0;
+}

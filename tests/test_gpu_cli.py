@@ -160,3 +160,30 @@ def test_annotate_seqs_matches_oracle(c1_build, tmp_path):
         wu += u
     assert _lines(calls) == wc
     assert _lines(unc) == wu
+
+
+def test_matrix_distance_matches_oracle(c1_build, tmp_path):
+    """kmers-matrix-distance data-dir input-file: "seq1\\tseq2\\tcount" lines (compared as a set: the
+    reference prints hash order), incl. a repeated id (one SeqIdMap index) and an empty id."""
+    info, out, _, _ = c1_build
+    qdir = _query_dir(tmp_path / "q", seed=11)
+    blob = b"".join(_lines(p) for p in fr.list_files(qdir))
+    first = fr.parse_fasta(blob)[0]
+    blob += b">" + first[0] + b" again\n" + first[2][5:] + b"\n>\nACDEFGHIKLMNPQ\n"
+    fa = str(tmp_path / "all.faa")
+    with open(fa, "wb") as fh:
+        fh.write(blob)
+    stdout, stderr = _run([os.path.join(BIN, "kmers-matrix-distance"), out, fa])
+    recs = fr.parse_fasta(blob)
+    ids = {}
+    idx = np.array([ids.setdefault(r[0], len(ids)) for r in recs], np.uint32)
+    names = list(ids)
+    res, off, ln = fr.records_arrays(recs)
+    bdz = oracle_ref.Bdz(_lines(os.path.join(out, "kmer_data.mph")))
+    pairs = oracle_ref.matrix_distance(bdz, _lines(os.path.join(out, "kmer_data.dat")), res, off, ln, idx,
+                                       _fidx(out).index("hypothetical protein"))
+    want = {"%s\t%s\t%d" % (names[a].decode(), names[b].decode(), c) for a, b, c in pairs}
+    got = stdout.split("\n")
+    assert got[-1] == "" and len(got) - 1 == len(want) and set(got[:-1]) == want
+    assert len(want) > 1000
+    assert "kmer_hit_map size " in stderr and "write output" in stderr
