@@ -42,7 +42,7 @@ bin/%: $(SRC)/tools/%.cpp $(FRONT) $(LIB) $(FRONTH)
 	  -Wl,-rpath,'$$ORIGIN/../signature_kmers_amd' -Wl,-rpath,/opt/rocm/lib
 
 $(ORACLE): oracle/skm_oracle.cpp
-	$(CXX) -O2 -fPIC -shared -std=c++17 -ffp-contract=off $< -o $@
+	$(CXX) -O2 -fPIC -shared -std=c++17 -ffp-contract=off -pthread $< -o $@
 
 clean:
 	rm -rf build bin $(LIB) $(ORACLE)

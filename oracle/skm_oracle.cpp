@@ -33,6 +33,7 @@
 // ============================================================================================
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -42,6 +43,7 @@
 #include <regex>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 extern "C" {
@@ -272,6 +274,154 @@ int oracle_build(const uint8_t* residues, const uint64_t* seq_off, const uint32_
     *n_seqs_with_signature = seqs_with_signature.size();
     *distinct_signatures = n_sig;
     return kept <= out_cap ? 0 : -1;
+}
+
+// --------------------------------------------------------------------------------------------
+//  The same build on n_threads host threads (the CPU baseline of bench.py on all the node's
+//  cores).  Same semantics as oracle_build (the --n-threads 1 results, not the
+//  racy multithreaded reference): sequences are split into contiguous ranges, each thread
+//  extracts its range into per-shard lists (shard = hash of the key), the lists of a shard are
+//  concatenated in range order (so insertion order is kept) and each shard is grouped and cut
+//  by one thread exactly like oracle_build.  Kept k-mers come out in shard order (the
+//  reference's kept_kmers_ is a hash map, unordered); out_keys/out_data must hold every window.
+// --------------------------------------------------------------------------------------------
+int oracle_build_mt(const uint8_t* residues, const uint64_t* seq_off, const uint32_t* seq_len,
+                    const uint16_t* seq_func, const uint32_t* seq_id, uint64_t n_seqs, uint32_t n_functions,
+                    int n_threads, uint64_t* out_keys, oracle_stored* out_data, uint64_t* out_n,
+                    uint32_t* distinct_functions, uint32_t* seqs_with_func, uint64_t* n_seqs_with_signature,
+                    uint64_t* distinct_signatures) {
+    const int K = 8;
+    const int T = std::max(1, n_threads);
+    const int S = 8 * T;  // shards
+    auto shard_of = [S](uint64_t k) {
+        k ^= k >> 33;
+        k *= 0xff51afd7ed558ccdull;
+        k ^= k >> 33;
+        return (int)(k % (uint64_t)S);
+    };
+    // contiguous sequence ranges of ~equal residue count
+    uint64_t total = 0;
+    for (uint64_t s = 0; s < n_seqs; ++s) total += seq_len[s];
+    std::vector<uint64_t> cut(T + 1, n_seqs);
+    cut[0] = 0;
+    {
+        uint64_t acc = 0;
+        int t = 1;
+        for (uint64_t s = 0; s < n_seqs && t < T; ++s) {
+            acc += seq_len[s];
+            while (t < T && acc >= total * (uint64_t)t / (uint64_t)T) cut[t++] = s + 1;
+        }
+    }
+    std::vector<std::vector<std::vector<Occ>>> parts(T, std::vector<std::vector<Occ>>(S));
+    std::vector<std::vector<uint32_t>> swf(T, std::vector<uint32_t>(n_functions, 0));
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t]() {
+            for (uint64_t s = cut[t]; s < cut[t + 1]; ++s) {
+                const uint16_t f = seq_func[s];
+                if (f == kUndefinedFunction) continue;
+                if (f < n_functions) swf[t][f]++;
+                const uint8_t* seq = residues + seq_off[s];
+                const uint32_t len = seq_len[s];
+                if (len < (uint32_t)K) continue;
+                uint32_t run = 0;  // valid residues ending at i
+                for (uint32_t i = 0; i < len; ++i) {
+                    run = ok_prot(seq[i]) ? run + 1 : 0;
+                    if (i + 1 >= (uint32_t)K && run >= (uint32_t)K) {
+                        const uint32_t w = i + 1 - K;
+                        const uint64_t key = load_key(seq + w);
+                        parts[t][shard_of(key)].push_back({key, (uint32_t)s, w});
+                    }
+                }
+            }
+        });
+    for (auto& x : th) x.join();
+    th.clear();
+    struct ShardOut {
+        std::vector<uint64_t> keys;
+        std::vector<oracle_stored> data;
+        std::vector<uint32_t> df;
+        uint64_t n_sig = 0;
+    };
+    std::vector<ShardOut> outs(S);
+    std::vector<uint8_t> flag(n_seqs, 0);  // sequence has a kept k-mer
+    std::atomic<int> next(0);
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&]() {
+            std::vector<uint16_t> offsets;
+            for (int sh; (sh = next.fetch_add(1)) < S;) {
+                std::vector<Occ> occ;
+                size_t n = 0;
+                for (int u = 0; u < T; ++u) n += parts[u][sh].size();
+                occ.reserve(n);
+                for (int u = 0; u < T; ++u) {
+                    occ.insert(occ.end(), parts[u][sh].begin(), parts[u][sh].end());
+                    std::vector<Occ>().swap(parts[u][sh]);
+                }
+                std::stable_sort(occ.begin(), occ.end(), [](const Occ& a, const Occ& b) { return a.key < b.key; });
+                ShardOut& O = outs[sh];
+                O.df.assign(n_functions, 0);
+                size_t a = 0;
+                while (a < occ.size()) {
+                    size_t b = a + 1;
+                    while (b < occ.size() && occ[b].key == occ[a].key) ++b;
+                    std::map<uint16_t, int> func_count;
+                    int count = 0;
+                    for (size_t j = b; j-- > a;) {
+                        func_count[seq_func[occ[j].seq]]++;
+                        count++;
+                    }
+                    uint16_t best_func = kUndefinedFunction;
+                    int best_count = -1;
+                    for (auto& x : func_count)
+                        if (best_func == kUndefinedFunction || x.second > best_count) {
+                            best_func = x.first;
+                            best_count = x.second;
+                        }
+                    if (!((float)best_count < float(count) * 0.8f)) {
+                        SigAcc acc;
+                        offsets.clear();
+                        for (size_t j = b; j-- > a;) {
+                            const Occ& o = occ[j];
+                            const uint32_t len = seq_len[o.seq];
+                            if (seq_func[o.seq] == best_func) acc(len);
+                            offsets.push_back((uint16_t)(len - o.i));
+                            __atomic_store_n(&flag[o.seq], (uint8_t)1, __ATOMIC_RELAXED);
+                        }
+                        std::sort(offsets.begin(), offsets.end());
+                        O.keys.push_back(occ[a].key);
+                        O.data.push_back({offsets[offsets.size() / 2], best_func, d2u16(acc.mean()),
+                                          d2u16(acc.median.result()), d2u16(acc.variance)});
+                        O.n_sig++;
+                        if (best_func < n_functions) O.df[best_func]++;
+                    }
+                    a = b;
+                }
+            }
+        });
+    for (auto& x : th) x.join();
+    uint64_t kept = 0, n_sig = 0;
+    for (uint32_t f = 0; f < n_functions; ++f) {
+        distinct_functions[f] = 0;
+        seqs_with_func[f] = 0;
+        for (int t = 0; t < T; ++t) seqs_with_func[f] += swf[t][f];
+    }
+    for (int sh = 0; sh < S; ++sh) {
+        ShardOut& O = outs[sh];
+        std::copy(O.keys.begin(), O.keys.end(), out_keys + kept);
+        std::copy(O.data.begin(), O.data.end(), out_data + kept);
+        kept += O.keys.size();
+        n_sig += O.n_sig;
+        for (uint32_t f = 0; f < n_functions; ++f) distinct_functions[f] += O.df[f];
+    }
+    std::vector<uint32_t> ids;  // seqs_with_a_signature is a set of seq_ids (colliding ids count once)
+    for (uint64_t s = 0; s < n_seqs; ++s)
+        if (flag[s]) ids.push_back(seq_id[s]);
+    std::sort(ids.begin(), ids.end());
+    *out_n = kept;
+    *n_seqs_with_signature = (uint64_t)(std::unique(ids.begin(), ids.end()) - ids.begin());
+    *distinct_signatures = n_sig;
+    return 0;
 }
 
 // Number of windows the build examines (units of the k-mers/s metric): sum over sequences with

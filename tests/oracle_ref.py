@@ -37,6 +37,8 @@ def olib():
         P = C.c_void_p
         _lib.oracle_build.restype = C.c_int
         _lib.oracle_build.argtypes = [P, P, P, P, P, C.c_uint64, C.c_uint32, P, P, C.c_uint64, P, P, P, P, P]
+        _lib.oracle_build_mt.restype = C.c_int
+        _lib.oracle_build_mt.argtypes = [P, P, P, P, P, C.c_uint64, C.c_uint32, C.c_int, P, P, P, P, P, P, P]
         _lib.oracle_count_windows.restype = C.c_uint64
         _lib.oracle_count_windows.argtypes = [P, P, C.c_uint64]
         _lib.oracle_bdz_load.restype = P
@@ -85,6 +87,36 @@ def build(residues, seq_off, seq_len, seq_func, seq_id, n_functions):
     assert rc == 0
     k = int(out_n[0])
     return dict(keys=keys[:k].copy(), data=data[:k].copy(), distinct_functions=df[:n_functions].copy(),
+                seqs_with_func=sw[:n_functions].copy(), n_seqs_with_signature=int(nsig[0]),
+                distinct_signatures=int(dsig[0]))
+
+
+def build_mt(residues, seq_off, seq_len, seq_func, seq_id, n_functions, n_threads, sort=True):
+    """oracle_build on n_threads host threads (CPU baseline); same results, keys sorted if sort."""
+    L = olib()
+    residues = np.ascontiguousarray(residues, np.uint8)
+    seq_off = np.ascontiguousarray(seq_off, np.uint64)
+    seq_len = np.ascontiguousarray(seq_len, np.uint32)
+    seq_func = np.ascontiguousarray(seq_func, np.uint16)
+    seq_id = np.ascontiguousarray(seq_id, np.uint32)
+    n = len(seq_len)
+    cap = int(L.oracle_count_windows(_p(seq_len), _p(seq_func), n)) + 1
+    keys = np.empty(cap, np.uint64)
+    data = np.empty(cap, STORED_DTYPE)
+    df = np.zeros(max(n_functions, 1), np.uint32)
+    sw = np.zeros(max(n_functions, 1), np.uint32)
+    out_n = np.zeros(1, np.uint64)
+    nsig = np.zeros(1, np.uint64)
+    dsig = np.zeros(1, np.uint64)
+    rc = L.oracle_build_mt(_p(residues), _p(seq_off), _p(seq_len), _p(seq_func), _p(seq_id), n, n_functions,
+                           int(n_threads), _p(keys), _p(data), _p(out_n), _p(df), _p(sw), _p(nsig), _p(dsig))
+    assert rc == 0
+    k = int(out_n[0])
+    keys, data = keys[:k], data[:k]
+    if sort:
+        o = np.argsort(keys, kind="stable")
+        keys, data = keys[o], data[o]
+    return dict(keys=keys.copy(), data=data.copy(), distinct_functions=df[:n_functions].copy(),
                 seqs_with_func=sw[:n_functions].copy(), n_seqs_with_signature=int(nsig[0]),
                 distinct_signatures=int(dsig[0]))
 

@@ -164,3 +164,20 @@ def test_oracle_matches_python_restatement(seed):
     assert ref["n_seqs_with_signature"] == nsig
     assert ref["distinct_signatures"] == len(exp)
     assert np.all(np.diff(ref["keys"].astype(np.uint64)) > 0)  # strictly ascending
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_multithreaded_port_equals_single_thread(threads):
+    """oracle_build_mt (bench.py's all-core CPU baseline) == oracle_build, incl. colliding ids."""
+    from signature_kmers_amd import synth
+    p = synth.generate_arrays(3000, 30, per_file=300, extras=True)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    i = (i % 700).astype(np.uint32)  # colliding seq_ids
+    a = oracle_ref.build(r, o, l, f, i, len(funcs))
+    b = oracle_ref.build_mt(r, o, l, f, i, len(funcs), threads)
+    assert np.array_equal(a["keys"], b["keys"])
+    assert np.array_equal(a["data"].view(np.uint8), b["data"].view(np.uint8))
+    for k in ("distinct_functions", "seqs_with_func"):
+        assert np.array_equal(a[k], b[k])
+    assert a["n_seqs_with_signature"] == b["n_seqs_with_signature"]
+    assert a["distinct_signatures"] == b["distinct_signatures"]
