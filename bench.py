@@ -235,10 +235,10 @@ def _annotate_leg(skm, synth, b, funcs, a, files_train, device):
 def _matrix_leg(skm, synth, a, device):
     """kmers-matrix-distance (BASELINE configs[4]): a 200-family signature DB (built on this GPU from
     200K training proteins, BDZ on the GPU) resident in HBM, a fresh set of query proteins of the
-    same families, all-vs-all shared-signature-k-mer counts into one dense upper-triangle tile (one
-    GPU holds every row).  One step = window lookup + length filter, k-mer grouping (hash + radix
-    sort), pair increments, compaction of the nonzero pairs; the pairs stay on the device.
-    Roofline: k_md_pairs, SURVEY 8(d) 4 B per pair increment."""
+    same families, all-vs-all shared-signature-k-mer counts (one GPU computes every row).  One step =
+    window lookup + length filter, k-mer grouping (hash + radix sort), per-row LDS histograms of the
+    pair increments, compaction of the nonzero pairs in row order; the pairs stay on the device.
+    Roofline: k_md_rows (the pair increments), SURVEY 8(d) 4 B per pair increment."""
     import tempfile
     fam, per_file, n_train = 200, 4000, 200_000
     t0 = time.time()
@@ -284,7 +284,7 @@ def _matrix_leg(skm, synth, a, device):
                        "queries": n, "families": fam, "db_keys": int(len(kept.keys)), "windows": c["windows"],
                        "hits": c["hits"], "pair_increments": c["increments"], "nonzero_pairs": c["pairs"]},
             "phase_ms": acc,
-            "roofline": {"bound": "hbm", "kernel": "k_md_pairs", "achieved": gbs, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": "k_md_rows", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
                          "avg_launch_ms": acc["pairs"], "traffic": None},
             "prep_s": prep_s}

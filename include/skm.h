@@ -243,8 +243,8 @@ typedef struct skm_matrix_opts {
     uint32_t row_begin;       /* count only pairs with id1 in [row_begin, row_end): this GPU's    */
     uint32_t row_end;         /* tile of the triangle (skm_matrix_tile_rows); 0, 0 = every row    */
     uint32_t pad;
-    uint64_t max_tile_bytes;  /* bound on the dense u32 count tile in HBM (0: 60 % of free HBM);
-                                 larger tiles are processed in row bands                          */
+    uint64_t max_tile_bytes;  /* reserved (0): the counts live in per-row LDS histograms, no dense
+                                 tile is allocated in HBM                                        */
 } skm_matrix_opts;
 
 typedef struct skm_pairs {

@@ -9,7 +9,7 @@
 // seq_id_map.h:12-27) and every pair id1 < id2 of a k-mer's set adds one to seq_dist[id1][id2]
 // (:176-196).
 //
-// Device pipeline (one GPU holds the row tile [r0, r1) of the upper-triangle count matrix):
+// Device pipeline (one GPU computes the rows [r0, r1) of the upper-triangle count matrix):
 //   k_md_hits      one thread per 16 window positions of the packed queries: window validity,
 //                  DB lookup, record, filters; surviving (kmer, index) records compacted with one
 //                  atomic per wave
@@ -18,11 +18,13 @@
 //   k_rs_hist / k_rs_scatter   LSD radix sort of the composites, 8-bit digits (stable: per-round
 //                  wave match by ballots + per-wave digit counts in LDS)
 //   k_md_starts / k_md_segstart   k-mer group boundaries (composites with equal slot)
-//   k_md_pairs     one wave per 64 consecutive composites; a lane walks its own short pair row,
-//                  rows of > 16 partners are walked by the whole wave; one atomic add per pair
-//                  increment into the dense tile (u32, row-major triangle)
-//   k_md_rowcount / k_md_emit   stable compaction of the nonzero counts into sorted
-//                  (id1, id2, count) triples; emitted cells are reset to 0 for the next run
+//   k_md_rowstat / k_md_rowfill   row lists: every distinct composite with partners after it in
+//                  its group, bucketed by its index id1 (counting sort)
+//   k_md_rows      one 1024-thread workgroup per row (work queue): the row's pair counts in an
+//                  LDS histogram over its columns (u16 counters: 65536 columns per pass), short
+//                  partner lists walked by a lane, long ones by a wave; nonzero columns compacted
+//                  in column order -- no global atomics on the counts, no dense matrix in HBM
+//   k_md_gather    (id1, id2, count) triples in row order
 // The hit records are identical on every GPU (each recomputes them: ~3 % of the time), so the
 // row tiles need no collective; the host concatenates the tiles in row order.
 #include <hip/hip_runtime.h>
@@ -39,7 +41,6 @@
 namespace skm {
 
 constexpr int MD_THREADS = 256;
-constexpr uint32_t MD_LONG_ROW = 16;   // rows with more partners are walked by the whole wave
 
 struct MdHitArgs {
     const uint8_t* res;        // packed residues, a 0 after each sequence
@@ -255,120 +256,242 @@ __global__ void k_md_segstart(const uint32_t* __restrict__ flag, const uint64_t*
     if (e == n - 1) segstart[S[n]] = n;
 }
 
-struct MdPairArgs {
+__host__ __device__ __forceinline__ uint64_t rowbase(uint64_t i, uint64_t n) { return i * (2 * n - i - 1) / 2; }
+
+// Row lists: element e (a distinct (kmer, index) composite whose group has members after it)
+// belongs to row id1 = index(e); its partners are the distinct composites after it in its group.
+struct MdRowArgs {
     const uint64_t* comp;      // sorted composites
     const uint64_t* S;         // exclusive scan of group-start flags [n+1]
     const uint64_t* segstart;  // [nseg+1]
     uint64_t n;
     uint64_t idx_mask;
-    uint32_t r0, r1;           // row tile
-    uint64_t nidx;             // matrix order
-    uint64_t base0;            // rowbase(r0)
-    uint32_t* tile;            // counts, row-major upper triangle of rows [r0, r1)
+    uint32_t r0, rows;         // row tile [r0, r0 + rows)
+    uint64_t nidx;
+    uint32_t* rowlen;          // [rows] entries per row
+    uint32_t* rowub;           // [rows] partner slots per row (upper bound of its nonzero pairs)
+    uint32_t* cursor;          // [rows]
+    const uint64_t* rowoff;    // [rows+1] scan of rowlen
+    const uint64_t* ubo;       // [rows+1] scan of rowub
+    uint32_t* rowlist;         // entries (element positions) by row
+    uint32_t* rownnz;          // [rows] nonzero pairs per row
+    uint32_t* scratch;         // per row, from ubo[row]: (id2, count) pairs
+    unsigned int* rowctr;      // work queue
     unsigned long long* incs;  // pair increments (diagnostics / roofline)
 };
 
-__host__ __device__ __forceinline__ uint64_t rowbase(uint64_t i, uint64_t n) { return i * (2 * n - i - 1) / 2; }
+__device__ __forceinline__ bool md_entry(const MdRowArgs& R, uint64_t e, uint32_t& row, uint64_t& ge) {
+    const uint64_t c = R.comp[e];
+    if (e > 0 && R.comp[e - 1] == c) return false;  // duplicate (kmer, index)
+    const uint64_t id1 = c & R.idx_mask;
+    if (id1 < R.r0 || id1 >= (uint64_t)R.r0 + R.rows) return false;
+    ge = R.segstart[R.S[e + 1]];  // end of e's group (group id S[e+1] - 1)
+    if (ge <= e + 1) return false;
+    row = (uint32_t)(id1 - R.r0);
+    return true;
+}
 
-__global__ __launch_bounds__(MD_THREADS) void k_md_pairs(MdPairArgs P) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t nw = (uint64_t)gridDim.x * (MD_THREADS / 64);
-    uint64_t incs = 0;
-    for (uint64_t c0 = ((uint64_t)blockIdx.x * (MD_THREADS / 64) + (threadIdx.x >> 6)) * 64; c0 < P.n; c0 += nw * 64) {
-        const uint64_t e = c0 + lane;
-        uint64_t ge = 0, roff = 0;
-        bool act = false;
-        if (e < P.n) {
-            const uint64_t c = P.comp[e];
-            const uint64_t id1 = c & P.idx_mask;
-            if ((e == 0 || P.comp[e - 1] != c) && id1 >= P.r0 && id1 < P.r1) {
-                ge = P.segstart[P.S[e + 1]];  // end of e's group (group id S[e+1] - 1)
-                act = ge > e + 1;
-                roff = rowbase(id1, P.nidx) - P.base0 - id1 - 1;
-            }
-        }
-        const bool is_long = act && ge - e - 1 > MD_LONG_ROW;
-        if (act && !is_long) {
-            for (uint64_t q = e + 1; q < ge; ++q) {
-                const uint64_t cq = P.comp[q];
-                if (cq == P.comp[q - 1]) continue;  // duplicate (kmer, index)
-                atomicAdd(&P.tile[roff + (cq & P.idx_mask)], 1u);
-                ++incs;
-            }
-        }
-        uint64_t lm = __ballot(is_long);
-        while (lm) {
-            const int L = __ffsll((unsigned long long)lm) - 1;
-            lm &= lm - 1;
-            const uint64_t le = __shfl(e, L, 64), lge = __shfl(ge, L, 64), lro = __shfl(roff, L, 64);
-            for (uint64_t q = le + 1 + lane; q < lge; q += 64) {
-                const uint64_t cq = P.comp[q];
-                if (cq == P.comp[q - 1]) continue;
-                atomicAdd(&P.tile[lro + (cq & P.idx_mask)], 1u);
-                ++incs;
-            }
-        }
+__global__ void k_md_rowstat(MdRowArgs R) {
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < R.n; e += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t row;
+        uint64_t ge;
+        if (!md_entry(R, e, row, ge)) continue;
+        atomicAdd(&R.rowlen[row], 1u);
+        atomicAdd(&R.rowub[row], (uint32_t)min<uint64_t>(ge - e - 1, 0xFFFFFFFFull));
     }
-    // one atomic per wave
+}
+
+__global__ void k_md_rowfill(MdRowArgs R) {
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < R.n; e += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t row;
+        uint64_t ge;
+        if (!md_entry(R, e, row, ge)) continue;
+        R.rowlist[R.rowoff[row] + atomicAdd(&R.cursor[row], 1u)] = (uint32_t)e;
+    }
+}
+
+// One workgroup per row at a time (work queue): the row's pair counts accumulate in an LDS
+// histogram over its columns id2 = id1+1 .. nidx-1 (u16 counters, two per word: 65536 columns per
+// pass; u32 counters, 32768 per pass, when the row has > 65535 entries and a u16 could wrap) with
+// a bitmap of the touched words; the touched words are then compacted in column order into the
+// row's scratch range and reset (the histogram is all-zero between rows, nothing is cleared).
+// The walk is flattened over the whole workgroup: the partner ranges of up to 1024 entries are
+// prefix-summed and every thread takes partners by index (4 independent loads in flight).  No
+// global atomics on the counts and no dense matrix in HBM.
+constexpr int MR_THREADS = 1024;
+constexpr uint32_t MR_WORDS = 32768;              // 128 KB of LDS
+constexpr uint32_t MR_BM = MR_WORDS / 32;         // bitmap words (== MR_THREADS)
+constexpr uint32_t MR_UNROLL = 4;
+static_assert(MR_BM == (uint32_t)MR_THREADS, "one bitmap word per thread in the compaction");
+
+__device__ __forceinline__ uint32_t wg_scan_excl(uint32_t v, uint32_t* s_w, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) s_w[wave] = x;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < MR_THREADS / 64; ++w) {
+        const uint32_t t = s_w[w];
+        before += w < wave ? t : 0u;
+        tot += t;
+    }
+    total = tot;
+    return before + x - v;
+}
+
+__global__ __launch_bounds__(MR_THREADS) void k_md_rows(MdRowArgs R) {
+    __shared__ __align__(16) uint32_t h[MR_WORDS];
+    __shared__ uint32_t bm[MR_BM];
+    __shared__ uint32_t sp[MR_THREADS];   // partner prefix of the sweep's entries
+    __shared__ uint64_t sq[MR_THREADS];   // first partner of each entry
+    __shared__ uint32_t s_w[MR_THREADS / 64];
+    __shared__ uint32_t s_row;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    for (uint32_t w = tid * 4; w < MR_WORDS; w += MR_THREADS * 4) *reinterpret_cast<uint4*>(&h[w]) = make_uint4(0, 0, 0, 0);
+    bm[tid] = 0;
+    uint64_t incs = 0;
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) s_row = atomicAdd(R.rowctr, 1u);
+        __syncthreads();
+        const uint32_t row = s_row;
+        if (row >= R.rows) break;
+        const uint64_t l0 = R.rowoff[row], l1 = R.rowoff[row + 1];
+        if (l0 == l1) {
+            if (tid == 0) R.rownnz[row] = 0;
+            continue;
+        }
+        const uint64_t id1 = (uint64_t)R.r0 + row;
+        const uint64_t ncol = R.nidx - id1 - 1;
+        const bool wide = l1 - l0 > 65535u;
+        const uint32_t cpp = wide ? MR_WORDS : 2u * MR_WORDS;
+        const bool multi = ncol > cpp;
+        uint32_t* out = R.scratch + 2 * R.ubo[row];
+        uint32_t nnz = 0;
+        for (uint64_t cb = 0; cb < ncol; cb += cpp) {
+            const uint32_t cc = (uint32_t)min<uint64_t>(cpp, ncol - cb);
+            // this pass: id2 in [clo, chi); a group's composites are sorted by index, so each
+            // entry's partners in the window are one range
+            const uint64_t clo = id1 + 1 + cb, chi = clo + cc;
+            for (uint64_t kb = l0; kb < l1; kb += MR_THREADS) {
+                const uint64_t k = kb + tid;
+                uint64_t qa = 0, qb = 0;
+                if (k < l1) {
+                    const uint64_t e = R.rowlist[k];
+                    qa = e + 1;
+                    qb = R.segstart[R.S[e + 1]];
+                    if (multi) {
+                        uint64_t lo = qa, hi = qb;
+                        while (lo < hi) {
+                            const uint64_t mid = (lo + hi) >> 1;
+                            if ((R.comp[mid] & R.idx_mask) < clo) lo = mid + 1; else hi = mid;
+                        }
+                        const uint64_t qa2 = lo;
+                        hi = qb;
+                        while (lo < hi) {
+                            const uint64_t mid = (lo + hi) >> 1;
+                            if ((R.comp[mid] & R.idx_mask) < chi) lo = mid + 1; else hi = mid;
+                        }
+                        qa = qa2;
+                        qb = lo;
+                    }
+                }
+                const uint32_t pc = (uint32_t)(qb - qa);
+                uint32_t T;
+                const uint32_t pre = wg_scan_excl(pc, s_w, T);
+                sp[tid] = pre;
+                sq[tid] = qa;
+                __syncthreads();
+                const uint32_t ne = (uint32_t)min<uint64_t>(MR_THREADS, l1 - kb);
+                for (uint32_t t0 = 0; t0 < T; t0 += MR_THREADS * MR_UNROLL) {
+                    uint64_t cq[MR_UNROLL], cp[MR_UNROLL];
+#pragma unroll
+                    for (uint32_t u = 0; u < MR_UNROLL; ++u) {
+                        const uint32_t t = t0 + u * MR_THREADS + tid;
+                        cq[u] = 0;
+                        cp[u] = 0;
+                        if (t < T) {
+                            // largest entry i with sp[i] <= t
+                            uint32_t i = 0;
+#pragma unroll
+                            for (uint32_t st = MR_THREADS / 2; st >= 1; st >>= 1)
+                                if (i + st < ne && sp[i + st] <= t) i += st;
+                            const uint64_t q = sq[i] + (t - sp[i]);
+                            cq[u] = R.comp[q];
+                            cp[u] = R.comp[q - 1];
+                        }
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < MR_UNROLL; ++u) {
+                        if (cq[u] != cp[u]) {  // a partner, not a duplicate (kmer, index)
+                            const uint32_t c = (uint32_t)((cq[u] & R.idx_mask) - clo);
+                            const uint32_t w = wide ? c : (c >> 1);
+                            atomicAdd(&h[w], wide ? 1u : (1u << (16 * (c & 1u))));
+                            atomicOr(&bm[w >> 5], 1u << (w & 31u));
+                            ++incs;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+            // compaction: thread tid owns bitmap word tid = histogram words 32 tid .. 32 tid + 31
+            const uint32_t bits = bm[tid];
+            uint32_t cnt = 0;
+            for (uint32_t b = bits; b; b &= b - 1) {
+                const uint32_t v = h[tid * 32 + (uint32_t)__ffs(b) - 1];
+                cnt += wide ? 1u : ((v & 0xFFFFu) != 0) + ((v >> 16) != 0);
+            }
+            uint32_t tot;
+            uint32_t o = nnz + wg_scan_excl(cnt, s_w, tot);
+            for (uint32_t b = bits; b; b &= b - 1) {
+                const uint32_t w = tid * 32 + (uint32_t)__ffs(b) - 1;
+                const uint32_t v = h[w];
+                h[w] = 0;
+                if (wide) {
+                    out[2 * o] = (uint32_t)(clo + w);
+                    out[2 * o + 1] = v;
+                    ++o;
+                } else {
+                    if (v & 0xFFFFu) {
+                        out[2 * o] = (uint32_t)(clo + 2 * w);
+                        out[2 * o + 1] = v & 0xFFFFu;
+                        ++o;
+                    }
+                    if (v >> 16) {
+                        out[2 * o] = (uint32_t)(clo + 2 * w + 1);
+                        out[2 * o + 1] = v >> 16;
+                        ++o;
+                    }
+                }
+            }
+            bm[tid] = 0;
+            nnz += tot;
+            __syncthreads();  // s_w / h / bm reuse by the next pass
+        }
+        if (tid == 0) R.rownnz[row] = nnz;
+    }
     uint64_t x = incs;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-    if (lane == 0 && x) atomicAdd(P.incs, (unsigned long long)x);
+    if (lane == 0 && x) atomicAdd(R.incs, (unsigned long long)x);
 }
 
-// nonzero cells per row of the tile
-__global__ __launch_bounds__(MD_THREADS) void k_md_rowcount(const uint32_t* __restrict__ tile, uint32_t r0, uint32_t r1,
-                                                            uint64_t nidx, uint64_t base0, uint32_t* __restrict__ cnt) {
-    __shared__ uint32_t s_w[MD_THREADS / 64];
-    for (uint32_t r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
-        const uint64_t a = rowbase(r, nidx) - base0, len = nidx - r - 1;
-        uint32_t c = 0;
-        const uint32_t* row = tile + a;
-        for (uint64_t j = threadIdx.x; j < len; j += MD_THREADS) c += row[j] != 0;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
-        if ((threadIdx.x & 63u) == 0) s_w[threadIdx.x >> 6] = c;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t t = 0;
-            for (int w = 0; w < MD_THREADS / 64; ++w) t += s_w[w];
-            cnt[r - r0] = t;
-        }
-        __syncthreads();
-    }
-}
-
-// stable compaction of each row's nonzero cells into (id1, id2, count); cells reset to 0
-__global__ __launch_bounds__(MD_THREADS) void k_md_emit(uint32_t* __restrict__ tile, uint32_t r0, uint32_t r1, uint64_t nidx,
-                                                        uint64_t base0, const uint64_t* __restrict__ roff,
-                                                        uint32_t* __restrict__ out) {
-    __shared__ uint32_t s_w[MD_THREADS / 64 + 1];
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (uint32_t r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
-        const uint64_t a = rowbase(r, nidx) - base0, len = nidx - r - 1;
-        uint32_t* row = tile + a;
-        uint64_t o = roff[r - r0];
-        for (uint64_t j0 = 0; j0 < len; j0 += MD_THREADS) {
-            const uint64_t j = j0 + threadIdx.x;
-            const uint32_t v = j < len ? row[j] : 0u;
-            const uint64_t m = __ballot(v != 0);
-            if (lane == 0) s_w[wave] = (uint32_t)__popcll(m);
-            __syncthreads();
-            uint32_t before = 0, tot = 0;
-            for (uint32_t w = 0; w < MD_THREADS / 64; ++w) {
-                before += w < wave ? s_w[w] : 0u;
-                tot += s_w[w];
-            }
-            if (v) {
-                const uint64_t p = o + before + (uint32_t)__popcll(m & lt);
-                out[3 * p] = r;
-                out[3 * p + 1] = (uint32_t)(r + 1 + j);
-                out[3 * p + 2] = v;
-                row[j] = 0;
-            }
-            o += tot;
-            __syncthreads();
+// rows in order: (id2, count) scratch pairs -> (id1, id2, count) triples at the row's final offset
+__global__ void k_md_gather(const uint32_t* __restrict__ scratch, const uint64_t* __restrict__ ubo,
+                            const uint64_t* __restrict__ fo, uint32_t r0, uint32_t rows, uint32_t* __restrict__ out) {
+    for (uint32_t row = blockIdx.x; row < rows; row += gridDim.x) {
+        const uint64_t a = fo[row], cnt = fo[row + 1] - a;
+        const uint32_t* src = scratch + 2 * ubo[row];
+        for (uint64_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+            out[3 * (a + j)] = r0 + row;
+            out[3 * (a + j) + 1] = src[2 * j];
+            out[3 * (a + j) + 2] = src[2 * j + 1];
         }
     }
 }
@@ -385,7 +508,7 @@ struct skm_matrix {
     uint32_t nseq = 0, nidx = 0;
     uint64_t rp = 0, n_windows = 0;
     DevBuf d_res, d_meta, d_idx, d_rkey, d_ridx, d_nrec, d_tab, d_comp, d_comp2, d_hist, d_hoff, d_flag, d_S,
-        d_seg, d_tile, d_rcnt, d_roff, d_out, d_out2, d_incs;
+        d_seg, d_rlen, d_rub, d_rcur, d_roff, d_ubo, d_rnnz, d_fo, d_rlist, d_scr, d_out, d_incs;
     Scanner scan;
     uint64_t n_hits = 0, n_incs = 0, n_pairs = 0, n_groups = 0;
     bool ran = false;
@@ -473,93 +596,77 @@ void matrix_run(skm_matrix* M, const skm_matrix_opts* o) {
         SKM_HIP(hipMemcpyAsync(&M->n_groups, M->d_S.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
     }
     SKM_HIP(hipEventRecord(M->ev[2], st));
-    // 3. pair counts, tile by tile (rows [r0, r1) cut into sub-tiles that fit the budget)
+    // 3. pair counts: row lists, one LDS histogram per row, compaction in row order
     float pairs_ms = 0, emit_ms = 0;
     uint64_t out_n = 0;
     if (n && r1 > r0) {
-        const uint64_t N = M->nidx;
-        size_t freeb = 0, totb = 0;
-        SKM_HIP(hipMemGetInfo(&freeb, &totb));
-        uint64_t budget = o->max_tile_bytes ? o->max_tile_bytes : (uint64_t)(0.6 * (double)(freeb + M->d_tile.bytes));
-        budget = std::max<uint64_t>(budget, 4 * N + 64);
-        std::vector<std::pair<uint32_t, uint32_t>> subs;
-        for (uint32_t a = r0; a < r1;) {
-            uint32_t b = a + 1;
-            // grow b while the sub-tile fits (rows are contiguous in the triangle)
-            uint32_t lo = a + 1, hi = r1;
-            while (lo < hi) {
-                const uint32_t mid = lo + (hi - lo + 1) / 2;
-                if (4 * (rowbase(mid, N) - rowbase(a, N)) <= budget)
-                    lo = mid;
-                else
-                    hi = mid - 1;
-            }
-            b = lo;
-            subs.push_back({a, b});
-            a = b;
-        }
-        uint64_t max_area = 0;
-        for (auto& s : subs) max_area = std::max(max_area, rowbase(s.second, N) - rowbase(s.first, N));
-        const bool fresh = M->d_tile.bytes < 4 * max_area + 16 || !M->d_tile.p;
-        M->d_tile.ensure(4 * max_area + 16);
-        if (fresh) SKM_HIP(hipMemsetAsync(M->d_tile.p, 0, M->d_tile.bytes, st));
-        M->d_incs.ensure(8);
-        SKM_HIP(hipMemsetAsync(M->d_incs.p, 0, 8, st));
-        uint32_t max_rows = 0;
-        for (auto& s : subs) max_rows = std::max(max_rows, s.second - s.first);
-        M->d_rcnt.ensure(4ull * max_rows);
-        M->d_roff.ensure(8ull * (max_rows + 1));
-        hipEvent_t e0, e1, e2;
+        const uint32_t rows = r1 - r0;
+        M->d_rlen.ensure(4ull * rows);
+        M->d_rub.ensure(4ull * rows);
+        M->d_rcur.ensure(4ull * rows);
+        M->d_roff.ensure(8ull * (rows + 1));
+        M->d_ubo.ensure(8ull * (rows + 1));
+        M->d_rnnz.ensure(4ull * rows);
+        M->d_fo.ensure(8ull * (rows + 1));
+        M->d_incs.ensure(16);
+        SKM_HIP(hipMemsetAsync(M->d_rlen.p, 0, 4ull * rows, st));
+        SKM_HIP(hipMemsetAsync(M->d_rub.p, 0, 4ull * rows, st));
+        SKM_HIP(hipMemsetAsync(M->d_rcur.p, 0, 4ull * rows, st));
+        SKM_HIP(hipMemsetAsync(M->d_incs.p, 0, 16, st));
+        MdRowArgs R;
+        R.comp = M->d_comp.as<uint64_t>();
+        R.S = M->d_S.as<uint64_t>();
+        R.segstart = M->d_seg.as<uint64_t>();
+        R.n = n;
+        R.idx_mask = (1ull << idx_bits) - 1;
+        R.r0 = r0;
+        R.rows = rows;
+        R.nidx = M->nidx;
+        R.rowlen = M->d_rlen.as<uint32_t>();
+        R.rowub = M->d_rub.as<uint32_t>();
+        R.cursor = M->d_rcur.as<uint32_t>();
+        R.rowoff = M->d_roff.as<uint64_t>();
+        R.ubo = M->d_ubo.as<uint64_t>();
+        R.rownnz = M->d_rnnz.as<uint32_t>();
+        R.rowctr = reinterpret_cast<unsigned int*>(M->d_incs.as<unsigned long long>() + 1);
+        R.incs = M->d_incs.as<unsigned long long>();
+        const uint32_t ge = (uint32_t)std::min<uint64_t>(ceil_div(n, 256), 256ull * 32);
+        hipLaunchKernelGGL(k_md_rowstat, dim3(ge), dim3(256), 0, st, R);
+        M->scan.run(R.rowlen, rows, M->d_roff.as<uint64_t>(), st);
+        M->scan.run(R.rowub, rows, M->d_ubo.as<uint64_t>(), st);
+        uint64_t tot[2] = {0, 0};
+        SKM_HIP(hipMemcpyAsync(&tot[0], M->d_roff.as<uint64_t>() + rows, 8, hipMemcpyDeviceToHost, st));
+        SKM_HIP(hipMemcpyAsync(&tot[1], M->d_ubo.as<uint64_t>() + rows, 8, hipMemcpyDeviceToHost, st));
+        SKM_HIP(hipStreamSynchronize(st));
+        M->d_rlist.ensure(4 * std::max<uint64_t>(tot[0], 1));
+        M->d_scr.ensure(8 * std::max<uint64_t>(tot[1], 1));
+        R.rowlist = M->d_rlist.as<uint32_t>();
+        R.scratch = M->d_scr.as<uint32_t>();
+        hipLaunchKernelGGL(k_md_rowfill, dim3(ge), dim3(256), 0, st, R);
+        SKM_HIP(hipGetLastError());
+        hipEvent_t e0, e1;
         SKM_HIP(hipEventCreate(&e0));
         SKM_HIP(hipEventCreate(&e1));
-        SKM_HIP(hipEventCreate(&e2));
-        for (auto& s : subs) {
-            MdPairArgs P;
-            P.comp = M->d_comp.as<uint64_t>();
-            P.S = M->d_S.as<uint64_t>();
-            P.segstart = M->d_seg.as<uint64_t>();
-            P.n = n;
-            P.idx_mask = (1ull << idx_bits) - 1;
-            P.r0 = s.first;
-            P.r1 = s.second;
-            P.nidx = N;
-            P.base0 = rowbase(s.first, N);
-            P.tile = M->d_tile.as<uint32_t>();
-            P.incs = M->d_incs.as<unsigned long long>();
-            SKM_HIP(hipEventRecord(e0, st));
-            const uint32_t gp = (uint32_t)std::min<uint64_t>(ceil_div(ceil_div(n, 64), MD_THREADS / 64), 256ull * 64);
-            hipLaunchKernelGGL(k_md_pairs, dim3(gp), dim3(MD_THREADS), 0, st, P);
-            SKM_HIP(hipGetLastError());
-            SKM_HIP(hipEventRecord(e1, st));
-            const uint32_t rows = s.second - s.first;
-            const uint32_t gr = std::min<uint32_t>(rows, 256u * 16u);
-            hipLaunchKernelGGL(k_md_rowcount, dim3(gr), dim3(MD_THREADS), 0, st, M->d_tile.as<uint32_t>(), s.first,
-                               s.second, N, P.base0, M->d_rcnt.as<uint32_t>());
-            M->scan.run(M->d_rcnt.as<uint32_t>(), rows, M->d_roff.as<uint64_t>(), st);
-            uint64_t cnt = 0;
-            SKM_HIP(hipMemcpyAsync(&cnt, M->d_roff.as<uint64_t>() + rows, 8, hipMemcpyDeviceToHost, st));
-            SKM_HIP(hipStreamSynchronize(st));
-            if (12 * (out_n + cnt) + 16 > M->d_out.bytes) {  // grow, keeping the earlier sub-tiles
-                M->d_out2.ensure(12 * (out_n + cnt) + (12 * (out_n + cnt)) / 4 + 16);
-                if (out_n) SKM_HIP(hipMemcpyAsync(M->d_out2.p, M->d_out.p, 12 * out_n, hipMemcpyDeviceToDevice, st));
-                std::swap(M->d_out.p, M->d_out2.p);
-                std::swap(M->d_out.bytes, M->d_out2.bytes);
-            }
-            hipLaunchKernelGGL(k_md_emit, dim3(gr), dim3(MD_THREADS), 0, st, M->d_tile.as<uint32_t>(), s.first, s.second,
-                               N, P.base0, M->d_roff.as<uint64_t>(), M->d_out.as<uint32_t>() + 3 * out_n);
-            SKM_HIP(hipGetLastError());
-            SKM_HIP(hipEventRecord(e2, st));
-            SKM_HIP(hipEventSynchronize(e2));
-            float t1 = 0, t2 = 0;
-            SKM_HIP(hipEventElapsedTime(&t1, e0, e1));
-            SKM_HIP(hipEventElapsedTime(&t2, e1, e2));
-            pairs_ms += t1;
-            emit_ms += t2;
-            out_n += cnt;
-        }
+        SKM_HIP(hipEventRecord(e0, st));
+        int dev = 0, ncu = 256;
+        SKM_HIP(hipGetDevice(&dev));
+        SKM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        hipLaunchKernelGGL(k_md_rows, dim3((uint32_t)std::max(1, ncu)), dim3(MR_THREADS), 0, st, R);
+        SKM_HIP(hipGetLastError());
+        SKM_HIP(hipEventRecord(e1, st));
+        M->scan.run(R.rownnz, rows, M->d_fo.as<uint64_t>(), st);
+        SKM_HIP(hipMemcpyAsync(&out_n, M->d_fo.as<uint64_t>() + rows, 8, hipMemcpyDeviceToHost, st));
+        SKM_HIP(hipStreamSynchronize(st));
+        M->d_out.ensure(12 * std::max<uint64_t>(out_n, 1));
+        hipLaunchKernelGGL(k_md_gather, dim3(std::min<uint32_t>(rows, 256u * 16u)), dim3(256), 0, st,
+                           M->d_scr.as<uint32_t>(), M->d_ubo.as<uint64_t>(), M->d_fo.as<uint64_t>(), r0, rows,
+                           M->d_out.as<uint32_t>());
+        SKM_HIP(hipGetLastError());
+        SKM_HIP(hipEventRecord(M->ev[3], st));
+        SKM_HIP(hipEventSynchronize(M->ev[3]));
+        SKM_HIP(hipEventElapsedTime(&pairs_ms, e0, e1));
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
-        (void)hipEventDestroy(e2);
         unsigned long long incs = 0;
         SKM_HIP(hipMemcpy(&incs, M->d_incs.p, 8, hipMemcpyDeviceToHost));
         M->n_incs = incs;
@@ -570,7 +677,8 @@ void matrix_run(skm_matrix* M, const skm_matrix_opts* o) {
     SKM_HIP(hipEventElapsedTime(&M->last_ms[0], M->ev[0], M->ev[1]));  // hits
     SKM_HIP(hipEventElapsedTime(&M->last_ms[1], M->ev[1], M->ev[2]));  // group (slot + sort + bounds)
     M->last_ms[2] = pairs_ms;                                          // pair increments
-    M->last_ms[3] = emit_ms;                                           // row counts + compaction
+    SKM_HIP(hipEventElapsedTime(&emit_ms, M->ev[2], M->ev[3]));
+    M->last_ms[3] = emit_ms - pairs_ms;                                // row lists + compaction
     SKM_HIP(hipEventElapsedTime(&M->last_ms[4], M->ev[0], M->ev[3]));  // total
     M->ran = true;
 }
