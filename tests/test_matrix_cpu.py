@@ -102,3 +102,17 @@ def test_random_proteome_matches_pyref(skm, tmp_path):
     hypo = funcs.index("hypothetical protein")
     exp = run_both(bdz, datb, table.get, seqs, list(range(len(seqs))), hypo)
     assert len(exp) > 100
+
+
+def test_tile_rows_cover_and_balance(skm):
+    """skm_matrix_tile_rows: the row bands of 1..8 GPUs cover [0, n) in order with nearly equal
+    upper-triangle area (each GPU's share of the pair matrix)."""
+    for n in (0, 1, 7, 1000, 100000):
+        for world in (1, 2, 3, 4, 8):
+            bands = [skm.matrix_tile_rows(n, r, world) for r in range(world)]
+            assert bands[0][0] == 0 and bands[-1][1] == n
+            for (a, b), (c, d) in zip(bands, bands[1:]):
+                assert b == c and a <= b
+            if n >= 1000:
+                area = [sum(n - i - 1 for i in range(a, b)) for a, b in bands]
+                assert max(area) - min(area) <= 2 * n, (n, world, area)  # one row of slack per band edge
