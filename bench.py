@@ -226,9 +226,9 @@ def _annotate_leg(skm, synth, b, funcs, a, files_train, device):
                                    f"families vs the CMPH DB of this build in HBM", "queries": nq,
                        "windows": nwin, "db_keys": int(len(kept.keys)), "calls": int(len(calls))},
             "phase_ms": acc,
-            "roofline": {"bound": "hbm", "kernel": "k_lookup<false>", "achieved": gbs, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": "k_lookup<0>", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
-                         "avg_launch_ms": acc["lookup"], "traffic": None},
+                         "avg_launch_ms": acc["lookup"], "traffic": _pmc_traffic("k_lookup<0>", a.seqs)},
             "mph_build_s": mph_s, "query_gen_s": gen_s}
 
 
@@ -286,7 +286,7 @@ def _matrix_leg(skm, synth, a, device):
             "phase_ms": acc,
             "roofline": {"bound": "hbm", "kernel": "k_md_rows", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
-                         "avg_launch_ms": acc["pairs"], "traffic": None},
+                         "avg_launch_ms": acc["pairs"], "traffic": _pmc_traffic("k_md_rows", a.seqs)},
             "prep_s": prep_s}
 
 

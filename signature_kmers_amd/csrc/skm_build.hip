@@ -572,6 +572,101 @@ __device__ GRes group_wave(const V& v, uint64_t a, uint32_t c, const uint32_t* _
     return r;
 }
 
+__device__ __forceinline__ uint32_t wg_sum(uint32_t x, uint32_t* s_wave) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    x = wave_sum(x);
+    if (lane == 0) s_wave[wave] = x;
+    __syncthreads();
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < nw; ++w) t += s_wave[w];
+    __syncthreads();
+    return t;
+}
+
+__device__ __forceinline__ uint32_t wg_max(uint32_t x, uint32_t* s_wave) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    x = wave_max(x);
+    if (lane == 0) s_wave[wave] = x;
+    __syncthreads();
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < nw; ++w) t = max(t, s_wave[w]);
+    __syncthreads();
+    return t;
+}
+
+__device__ __forceinline__ uint32_t wg_min(uint32_t x, uint32_t* s_wave) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    x = wave_min(x);
+    if (lane == 0) s_wave[wave] = x;
+    __syncthreads();
+    uint32_t t = 0xFFFFFFFFu;
+    for (uint32_t w = 0; w < nw; ++w) t = min(t, s_wave[w]);
+    __syncthreads();
+    return t;
+}
+
+// group_wave's result for a large group computed by the whole workgroup (every thread calls it
+// with the same a, c; the result is uniform).  Function runs from the run heads (compacted in
+// order into heads[0..hcap)), the longest run with ties to the lowest FunctionIndex, the fp32
+// cut, the upper-median offset by a 16-round radix select, flags, the u16 length sum.  Returns
+// false (nothing written) when the group has more than hcap function runs.
+template <class V>
+__device__ bool group_block(const V& v, uint64_t a, uint32_t c, const uint32_t* __restrict__ glen,
+                            uint8_t* __restrict__ flags, uint32_t* heads, uint32_t hcap, uint32_t* s_wave, GRes& r) {
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    r.kept = false;
+    uint32_t H = 0;
+    for (uint32_t t0 = 0; t0 < c; t0 += nt) {
+        const uint32_t t = t0 + tid;
+        const bool head = t < c && (t == 0 || v.func(a + t) != v.func(a + t - 1));
+        uint32_t tot;
+        const uint32_t pos = wg_exclusive_scan(head ? 1u : 0u, s_wave, tot);
+        if (head && H + pos < hcap) heads[H + pos] = t;
+        H += tot;
+    }
+    if (H > hcap) return false;
+    __syncthreads();
+    uint32_t lmax = 0;
+    for (uint32_t j = tid; j < H; j += nt) lmax = max(lmax, (j + 1 < H ? heads[j + 1] : c) - heads[j]);
+    const uint32_t best_c = wg_max(lmax, s_wave);
+    uint32_t fmin = 0xFFFFFFFFu;  // (function << 16 | run index) of the best runs: lowest function wins
+    for (uint32_t j = tid; j < H; j += nt)
+        if ((j + 1 < H ? heads[j + 1] : c) - heads[j] == best_c) fmin = min(fmin, (v.func(a + heads[j]) << 16) | j);
+    const uint32_t fj = wg_min(fmin, s_wave);
+    if ((float)best_c < float(c) * 0.8f) return true;
+    const uint32_t rb = heads[fj & 0xFFFFu];
+    r.kept = true;
+    r.best_f = fj >> 16;
+    r.cbest = best_c;
+    r.rb = rb;
+    // upper median offset: the (c/2)-th smallest (0-based), radix select bit 15 down to 0
+    uint32_t k = c / 2, pre = 0;
+    for (int b = 15; b >= 0; --b) {
+        uint32_t n0 = 0;
+        for (uint32_t t = tid; t < c; t += nt) {
+            const uint32_t o = (uint32_t)(v.lov(a + t) & 0xFFFFu);
+            n0 += (o >> b) == (pre >> b);  // bits above b match the prefix and bit b is clear
+        }
+        n0 = wg_sum(n0, s_wave);
+        if (k >= n0) {
+            k -= n0;
+            pre |= 1u << b;
+        }
+    }
+    r.avg = pre;
+    uint32_t sum = 0;
+    for (uint32_t t = tid; t < c; t += nt) {
+        const uint32_t s = (uint32_t)(v.lov(a + t) >> 36);
+        flags[s] = 1;
+        if (t >= rb && t < rb + best_c) sum += glen[s];
+    }
+    sum = wg_sum(sum, s_wave);
+    r.mean = d2u16((double)(uint16_t)sum / (double)best_c);
+    r.median = 0;
+    r.var = 0;
+    return true;
+}
+
 // Chains run longest-first: jobs are counting-sorted by length class (floor(log2 n), descending)
 // so a wave's 64 jobs have similar lengths.  Waves 2w and 2w+1 run the P^2 median and the
 // variance recurrence of the same 64 jobs (wave-uniform branch).
@@ -2295,6 +2390,7 @@ struct OvfScratch {
 // build) run inside k_overflow as soon as their sub-bucket is grouped -- the host orders the
 // overflow sub-buckets largest first -- instead of waiting for the whole overflow pass.
 constexpr uint32_t OVF_INLINE_CAP = 32;   // inline chains per workgroup (more: ordinary jobs)
+constexpr uint32_t OVF_BLOCK_GROUP = 1024;  // groups above this size: workgroup-cooperative statistics
 
 __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratch S, uint32_t inline_min, int prio) {
     __shared__ uint64_t s_hi[CAP];
@@ -2423,8 +2519,23 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
             const uint32_t gg = s_big[bi];
             const uint32_t a = heads[gg];
             const uint32_t b = gg + 1 < G ? heads[gg + 1] : n;
+            if (b - a > OVF_BLOCK_GROUP) continue;  // the whole workgroup takes it below
             const GRes r = group_wave(V, a, b - a, A.glen, A.flags);
             if ((tid & 63u) == 0) stage(r, a);
+        }
+        // groups of more than OVF_BLOCK_GROUP members (the heaviest k-mers): one at a time by the
+        // whole workgroup (a single wave would walk them ~20 times serially)
+        for (uint32_t bi = 0; bi < nbig; ++bi) {
+            const uint32_t gg = s_big[bi];
+            const uint32_t a = heads[gg];
+            const uint32_t b = gg + 1 < G ? heads[gg + 1] : n;
+            if (b - a <= OVF_BLOCK_GROUP) continue;
+            GRes r;
+            if (!group_block(V, a, b - a, A.glen, A.flags, reinterpret_cast<uint32_t*>(s_hi), 2 * CAP, s_wave, r)) {
+                if (tid < 64) r = group_wave(V, a, b - a, A.glen, A.flags);  // > 2*CAP function runs
+            }
+            if (tid == 0) stage(r, a);
+            __syncthreads();
         }
         __threadfence_block();
         __syncthreads();
@@ -3287,12 +3398,13 @@ void phase_group(skm_build* b) {
         A3.ovf = A2.ovf + nheavy;
         const uint32_t inline_min = (uint32_t)env_int("SKM_OVF_INLINE_MIN", 0x7FFFFFFF);
         const int prio = env_int("SKM_INLINE_PRIO", 3);
+        static const bool dbg_no_ovf = env_int("SKM_DBG_SKIP_OVERFLOW", 0) != 0;  // timing experiments only
         SKM_HIP(hipEventRecord(b->ev_o[0], st2));
-        if (nheavy)
+        if (nheavy && !dbg_no_ovf)
             hipLaunchKernelGGL(k_overflow, dim3(nheavy), dim3(BP_THREADS), 0, st2, A2, S, inline_min, prio);
         SKM_HIP(hipEventRecord(b->ev_o[1], st2));
         SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
-        if (novf > nheavy)
+        if (novf > nheavy && !dbg_no_ovf)
             hipLaunchKernelGGL(k_overflow, dim3(novf - nheavy), dim3(BP_THREADS), 0, st3, A3, S, inline_min, prio);
         SKM_HIP(hipGetLastError());
     }

@@ -18,14 +18,20 @@ step() {  # name, limit, command...
   echo "[$(date +%T)] $name rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 "$O/$name.log"; exit $rc; fi
 }
+PHASE=${PHASE:-all}   # all | trace (bench + kernel trace) | pmc (FETCH_SIZE, WRITE_SIZE passes)
 cd "$R"
-step bench 500 python3 bench.py --steps "$STEPS" --warmup 2 --json-out "$O/bench.json"
 export TMPDIR=/tmp
-cd /tmp
-step prof_trace 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_trace" -o run -- \
-  python3 "$R/bench.py" --steps "$STEPS" --warmup 2 --no-cpu-baseline --json-out "$O/bench_trace.json"
-step prof_fetch 500 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/prof_fetch" -o run -- \
-  python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
-step prof_write 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/prof_write" -o run -- \
-  python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
+if [ "$PHASE" != pmc ]; then
+  step bench 500 python3 bench.py --steps "$STEPS" --warmup 2 --json-out "$O/bench.json"
+  cd /tmp
+  step prof_trace 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_trace" -o run -- \
+    python3 "$R/bench.py" --steps "$STEPS" --warmup 2 --no-cpu-baseline --json-out "$O/bench_trace.json"
+fi
+if [ "$PHASE" != trace ]; then
+  cd /tmp
+  step prof_fetch 500 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/prof_fetch" -o run -- \
+    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
+  step prof_write 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/prof_write" -o run -- \
+    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
+fi
 echo done
