@@ -84,10 +84,7 @@ __global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict
                     uint32_t lo, hi;
                     key_at(w, t, lo, hi);
                     const uint32_t idx = MODE == LK_EXACT ? exact_lookup(D, lo, hi) : bdz_lookup(D, lo, hi);
-                    if (idx < D.m) {
-                        const uint16_t* rec = D.dat + (uint64_t)idx * 5;
-                        o = ((uint32_t)rec[1] << 16) | rec[2];  // function_index, mean
-                    }
+                    if (idx < D.m) o = D.fm[idx];  // function_index << 16 | mean
                 }
                 out[t] = o;
             }
@@ -108,7 +105,7 @@ __global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict
                     hv[u][1] = fastmod(b, D.r_magic, D.r) + D.r;
                     hv[u][2] = fastmod(c, D.r_magic, D.r) + 2u * D.r;
 #pragma unroll
-                    for (int j = 0; j < 3; ++j) gw[u][j] = D.g[hv[u][j] >> 4];
+                    for (int j = 0; j < 3; ++j) gw[u][j] = D.blk[(hv[u][j] >> 7) * 16u + ((hv[u][j] & 127u) >> 4)];
                 }
                 uint32_t vv[8], rt[8];
                 uint4 b0[8], b1[8];
@@ -120,11 +117,11 @@ __global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict
                     const uint32_t sel = sum % 3u;
                     const uint32_t v = sel == 0 ? hv[u][0] : (sel == 1 ? hv[u][1] : hv[u][2]);
                     vv[u] = v;
-                    const uint32_t blk = v >> 7;  // b = 7 (checked on open)
-                    rt[u] = D.ranktable[blk];
-                    const uint4* gb = reinterpret_cast<const uint4*>(D.g) + 2ull * blk;
+                    const uint32_t blk = v >> 7;  // b = 7 (checked on open): the line of v's own g word
+                    const uint4* gb = reinterpret_cast<const uint4*>(D.blk) + 4ull * blk;
                     b0[u] = gb[0];
                     b1[u] = gb[1];
+                    rt[u] = D.blk[16ull * blk + 8];
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
@@ -141,10 +138,8 @@ __global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict
                     rank += pe - unassigned_in(wf & pmask);
                     const uint64_t p = base + t;
                     uint32_t o = NO_HIT;
-                    if (p < rp && ((bad >> t) & 0xFFu) == 0 && ((amb >> (t + 8)) & 1u) == 0 && rank < D.m) {
-                        const uint16_t* rec = D.dat + (uint64_t)rank * 5;
-                        o = ((uint32_t)rec[1] << 16) | rec[2];  // function_index, mean
-                    }
+                    if (p < rp && ((bad >> t) & 0xFFu) == 0 && ((amb >> (t + 8)) & 1u) == 0 && rank < D.m)
+                        o = D.fm[rank];  // function_index << 16 | mean
                     out[t] = o;
                 }
             }
@@ -677,6 +672,21 @@ struct skm_query {
 
 namespace {
 
+// fm[i] = function_index << 16 | mean of record i: the 4 aligned bytes the call path reads per hit
+// (one gather instead of two 2-byte loads from the 10-byte records)
+void upload_fm(skm_db* db, const uint8_t* dat, uint64_t nrec) {
+    std::vector<uint32_t> fm(std::max<uint64_t>(nrec, 1), 0u);
+    for (uint64_t i = 0; i < nrec; ++i) {
+        uint16_t f, mn;
+        std::memcpy(&f, dat + 10 * i + 2, 2);
+        std::memcpy(&mn, dat + 10 * i + 4, 2);
+        fm[i] = ((uint32_t)f << 16) | (uint32_t)mn;
+    }
+    db->d_fm.ensure(4 * fm.size());
+    SKM_HIP(hipMemcpy(db->d_fm.p, fm.data(), 4 * fm.size(), hipMemcpyHostToDevice));
+    db->dev.fm = db->d_fm.as<uint32_t>();
+}
+
 void db_upload(skm_db* db, const uint8_t* dat, size_t dat_len) {
     SKM_HIP(hipSetDevice(db->device));
     Bdz& h = db->bdz;
@@ -702,6 +712,24 @@ void db_upload(skm_db* db, const uint8_t* dat, size_t dat_len) {
     D.seed = h.seed;
     D.r_magic = h.r ? (~0ull / h.r + 1) : 0;
     db->m = h.m;
+    upload_fm(db, dat, dat_len / 10);
+    // b == 7: g and the rank table interleaved, one 64-byte line per 128 vertices
+    D.blk = nullptr;
+    if (h.b == 7) {
+        const uint64_t nblk = (uint64_t)h.n / 128 + 2;
+        std::vector<uint32_t> blk(16 * nblk, 0);
+        const uint32_t* gw = reinterpret_cast<const uint32_t*>(g.data());  // padded with 0xFF
+        for (uint64_t q = 0; q < nblk; ++q) {
+            for (int w = 0; w < 8; ++w) {
+                const uint64_t gi = 8 * q + (uint64_t)w;
+                blk[16 * q + (uint64_t)w] = 4 * gi + 4 <= g.size() ? gw[gi] : 0xFFFFFFFFu;
+            }
+            blk[16 * q + 8] = q < h.ranktable.size() ? h.ranktable[q] : 0u;
+        }
+        db->d_blk.ensure(4 * blk.size());
+        SKM_HIP(hipMemcpy(db->d_blk.p, blk.data(), 4 * blk.size(), hipMemcpyHostToDevice));
+        D.blk = db->d_blk.as<uint32_t>();
+    }
 }
 
 void db_upload_kept(skm_db* db, const uint64_t* keys, const skm_stored_kmer_data* data, size_t n) {
@@ -740,6 +768,7 @@ void db_upload_kept(skm_db* db, const uint64_t* keys, const skm_stored_kmer_data
         SKM_CHECK(!(bad & 1u), SKM_E_ARG, "kept k-mer key 0 is not a valid k-mer");
         SKM_CHECK(!(bad & 2u), SKM_E_ARG, "duplicate kept k-mer keys");
     }
+    upload_fm(db, reinterpret_cast<const uint8_t*>(data), n);
 }
 
 bool read_file(const char* path, std::vector<uint8_t>& out) {

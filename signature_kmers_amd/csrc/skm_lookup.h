@@ -25,6 +25,11 @@ struct DevBdz {
     const uint32_t* g;          // g as little-endian u32 words (16 entries each), padded
     const uint32_t* ranktable;
     const uint16_t* dat;        // 5 u16 per record
+    const uint32_t* fm;         // per record: function_index | mean << 16 (what the call path reads)
+    // b == 7: 64-byte line per block of 128 vertices: u32 words 0-7 = the block's g, word 8 = its
+    // rank table entry, so the selected vertex's rank word and g block share one line with its
+    // own g word (already fetched for the vertex selection)
+    const uint32_t* blk;
     uint32_t m, r, b, seed;
     uint64_t r_magic;           // fastmod: ceil(2^64 / r)
     // exact-key mode (KeptKmerDB, kept_kmer_db.h:20-27): open-addressing table of the kept keys
@@ -138,6 +143,6 @@ struct skm_db {
     uint32_t m = 0;              // hash size (BDZ) or number of kept keys (exact)
     skm::Bdz bdz;
     uint64_t dat_records = 0;
-    skm::DevBuf d_g, d_rank, d_dat, d_xkeys, d_xidx;
+    skm::DevBuf d_g, d_rank, d_dat, d_xkeys, d_xidx, d_fm, d_blk;
     skm::DevBdz dev{};
 };

@@ -39,8 +39,21 @@ def main():
     shutil.copy(os.path.join(src, "prof_trace", "run_kernel_stats.csv"), os.path.join(dst, f"{rnd}_kernel_stats.csv"))
     bench = json.load(open(os.path.join(src, "bench.json")))
     json.dump(bench, open(os.path.join(dst, f"{rnd}_bench.json"), "w"), indent=1)
+    legs = os.path.join(src, "prof_trace_legs", "run_kernel_stats.csv")
+    if os.path.exists(legs):
+        shutil.copy(legs, os.path.join(dst, f"{rnd}_kernel_stats_legs.csv"))
     fetch = per_kernel(os.path.join(src, "prof_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(src, "prof_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    # kernels of the annotate / matrix legs from their own passes (the build kernels of those
+    # passes also ran the matrix leg's smaller training build, so they are not taken from there)
+    fl = os.path.join(src, "prof_fetch_legs", "run_counter_collection.csv")
+    if os.path.exists(fl):
+        f2 = per_kernel(fl, "FETCH_SIZE")
+        w2 = per_kernel(os.path.join(src, "prof_write_legs", "run_counter_collection.csv"), "WRITE_SIZE")
+        for k in set(f2) | set(w2):
+            if k not in fetch and k not in write:
+                fetch[k] = f2.get(k, 0.0)
+                write[k] = w2.get(k, 0.0)
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
         f, w = fetch.get(k, 0.0), write.get(k, 0.0)
