@@ -201,6 +201,7 @@ def _annotate_leg(skm, synth, b, funcs, a, files_train, device):
         skm.mph_build(kept.keys, kept.data, base + ".mph", base + ".dat", seed=1, device=device)
         mph_s = time.time() - t0
         db = skm.CmphKmerDb(base, device=device)
+        files = None if a.no_cpu_baseline else (open(base + ".mph", "rb").read(), open(base + ".dat", "rb").read())
     hypo = funcs.index("hypothetical protein")
     q = skm.QueryBatch(db, p.residues, p.seq_off, p.seq_len)
     nwin = int(np.where(p.seq_len >= 8, p.seq_len.astype(np.int64) - 7, 0).sum())
@@ -220,6 +221,22 @@ def _annotate_leg(skm, synth, b, funcs, a, files_train, device):
     db.close()
     alg = int(len(p.residues)) + 18 * nwin
     gbs = alg / (acc["lookup"] * 1e-3) / 1e9
+    cpu = None
+    if files is not None:  # the call path of the oracle on the host cores, bounded sample
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_ref
+        threads = _cpu_threads(a.cpu_threads)
+        n = min(len(p.seq_len), 200_000)
+        end = int(p.seq_off[n - 1]) + int(p.seq_len[n - 1])
+        ob = oracle_ref.Bdz(files[0])
+        t = time.perf_counter()
+        oracle_ref.annotate_mt(ob, files[1], p.residues[:end], p.seq_off[:n], p.seq_len[:n], threads, hypo_index=hypo)
+        dt = time.perf_counter() - t
+        w = int(np.where(p.seq_len[:n] >= 8, p.seq_len[:n].astype(np.int64) - 7, 0).sum())
+        cpu = {"value": w / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
+               "sample": f"first {n} query proteins ({w} windows), {dt:.1f} s, oracle/skm_oracle.cpp "
+                         f"oracle_annotate_mt (process_aa_seq per sequence) on {threads} host threads"}
+        del ob, files
     return {"metric": "query k-mers/sec (window lookup + HitSet calls)", "value": nwin * steps / wall,
             "unit": "k-mers/s", "ms_per_step": 1000.0 * wall / steps,
             "config": {"workload": f"C4 at {nq} queries (configs[3] names 10M): fresh proteins of the same "
@@ -229,7 +246,7 @@ def _annotate_leg(skm, synth, b, funcs, a, files_train, device):
             "roofline": {"bound": "hbm", "kernel": "k_lookup<0>", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
                          "avg_launch_ms": acc["lookup"], "traffic": _pmc_traffic("k_lookup<0>", a.seqs)},
-            "mph_build_s": mph_s, "query_gen_s": gen_s}
+            "cpu_baseline": cpu, "mph_build_s": mph_s, "query_gen_s": gen_s}
 
 
 def _matrix_leg(skm, synth, a, device):
@@ -259,6 +276,7 @@ def _matrix_leg(skm, synth, a, device):
         base = os.path.join(d, "kmer_data")
         skm.mph_build(kept.keys, kept.data, base + ".mph", base + ".dat", seed=1, device=device)
         db = skm.CmphKmerDb(base, device=device)
+        files = None if a.no_cpu_baseline else (open(base + ".mph", "rb").read(), open(base + ".dat", "rb").read())
     prep_s = time.time() - t0
     md = skm.MatrixDistance(db, funcs, res, off, ln)
     for _ in range(max(1, a.warmup)):
@@ -277,6 +295,23 @@ def _matrix_leg(skm, synth, a, device):
     db.close()
     alg = 4 * c["increments"]
     gbs = alg / (acc["pairs"] * 1e-3) / 1e9
+    cpu = None
+    if files is not None:  # the oracle's matrix distance (single thread) on a bounded sample
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_ref
+        ns = min(n, 10_000)
+        e2 = int(off[ns - 1]) + int(ln[ns - 1])
+        ob = oracle_ref.Bdz(files[0])
+        t = time.perf_counter()
+        oracle_ref.matrix_distance(ob, files[1], res[:e2], off[:ns], ln[:ns], np.arange(ns, dtype=np.uint32),
+                                   funcs.index("hypothetical protein"))
+        dt = time.perf_counter() - t
+        w = int(np.where(ln[:ns] >= 8, ln[:ns].astype(np.int64) - 7, 0).sum())
+        cpu = {"value": w / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
+               "sample": f"all-vs-all over the first {ns} query proteins ({w} windows; pair work grows with the "
+                         f"square of the sample, so this rate is an upper bound for 100K), {dt:.1f} s, "
+                         f"oracle/skm_oracle.cpp oracle_matrix_distance, one thread"}
+        del ob, files
     return {"metric": "query k-mers/sec (lookup + all-vs-all shared signature k-mer counts)",
             "value": c["windows"] * steps / wall, "unit": "k-mers/s", "ms_per_step": 1000.0 * wall / steps,
             "pair_increments_per_s": c["increments"] / (acc["pairs"] * 1e-3),
@@ -287,7 +322,7 @@ def _matrix_leg(skm, synth, a, device):
             "roofline": {"bound": "hbm", "kernel": "k_md_rows", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
                          "avg_launch_ms": acc["pairs"], "traffic": _pmc_traffic("k_md_rows", a.seqs)},
-            "prep_s": prep_s}
+            "cpu_baseline": cpu, "prep_s": prep_s}
 
 
 def _valid_windows(r, o, l, f) -> int:
@@ -319,14 +354,19 @@ def _pmc_traffic(kernel: str, seqs: int):
         return None
 
 
+def _cpu_threads(threads: int) -> int:
+    if threads <= 0:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    return threads
+
+
 def _cpu_baseline(r, o, l, f, i, nf, n_sample, threads):
     """The CPU port of the build (oracle/skm_oracle.cpp oracle_build_mt: the --n-threads 1 results
     computed on all the host cores this job owns -- extract into key-hash shards, per-shard stable
     sort + group + cut + statistics) on the first n_sample sequences of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref
-    if threads <= 0:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = _cpu_threads(threads)
     n = min(n_sample, len(l))
     end = int(o[n - 1]) + int(l[n - 1])
     t = time.perf_counter()

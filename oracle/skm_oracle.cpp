@@ -818,6 +818,35 @@ int64_t oracle_annotate(const oracle_bdz* db, const oracle_stored* dat, const ui
     return total <= cap ? (int64_t)total : -1;
 }
 
+// The call path on n_threads host threads (bench.py's CPU baseline of the annotate leg): each
+// thread runs process_aa_seq over a contiguous range of sequences (the reference parallelises
+// over files, kmers-call-functions.cc:166-189; here one batch is split).  Returns the number of
+// calls (the calls themselves are computed and dropped).
+int64_t oracle_annotate_mt(const oracle_bdz* db, const oracle_stored* dat, const uint8_t* residues,
+                           const uint64_t* seq_off, const uint32_t* seq_len, uint64_t n_seqs,
+                           const oracle_annot_opts* opts, int n_threads) {
+    const int T = std::max(1, n_threads);
+    std::vector<int64_t> cnt(T, 0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t]() {
+            std::vector<oracle_call> tmp(1024);
+            const uint64_t s0 = n_seqs * (uint64_t)t / (uint64_t)T, s1 = n_seqs * (uint64_t)(t + 1) / (uint64_t)T;
+            for (uint64_t s = s0; s < s1; ++s) {
+                int64_t n = oracle_process_aa_seq(db, dat, residues + seq_off[s], seq_len[s], opts, tmp.data(), tmp.size());
+                if ((uint64_t)n > tmp.size()) {
+                    tmp.resize(n);
+                    n = oracle_process_aa_seq(db, dat, residues + seq_off[s], seq_len[s], opts, tmp.data(), tmp.size());
+                }
+                cnt[t] += n;
+            }
+        });
+    for (auto& x : th) x.join();
+    int64_t total = 0;
+    for (int64_t c : cnt) total += c;
+    return total;
+}
+
 // --------------------------------------------------------------------------------------------
 //  kmers-matrix-distance (kmers-matrix-distance.cc:94-212; MatrixDistance::compute,
 //  matrix_distance.h:45-170).  process_fasta_stream_parallel (call_functions.tcc:157-215) runs

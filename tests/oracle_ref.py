@@ -53,6 +53,8 @@ def olib():
         _lib.oracle_annotate_exact.restype = C.c_int64
         _lib.oracle_annotate_exact.argtypes = [P, P, C.c_uint64, P, P, P, C.c_uint64, C.POINTER(AnnotOpts), P, P,
                                                C.c_uint64]
+        _lib.oracle_annotate_mt.restype = C.c_int64
+        _lib.oracle_annotate_mt.argtypes = [P, P, P, P, P, C.c_uint64, C.POINTER(AnnotOpts), C.c_int]
         _lib.oracle_matrix_distance.restype = C.c_int64
         _lib.oracle_matrix_distance.argtypes = [P, P, P, P, P, P, C.c_uint64, C.c_int32, P, C.c_uint64]
         _lib.oracle_find_best_call.argtypes = [P, C.c_uint64, C.POINTER(C.c_char_p), C.c_uint64, P, P, P,
@@ -171,6 +173,18 @@ def annotate(bdz: Bdz, dat: bytes, residues, seq_off, seq_len, min_hits=5, max_g
                                  _p(calls), cap)
     assert tot >= 0
     return off, calls[:tot].copy()
+
+
+def annotate_mt(bdz: Bdz, dat: bytes, residues, seq_off, seq_len, n_threads, min_hits=5, max_gap=200,
+                ignore_hypo=0, hypo_index=-1, mean_mode=0, mad_mode=0) -> int:
+    """process_aa_seq over every sequence on n_threads host threads; returns the number of calls."""
+    residues = np.ascontiguousarray(residues, np.uint8)
+    seq_off = np.ascontiguousarray(seq_off, np.uint64)
+    seq_len = np.ascontiguousarray(seq_len, np.uint32)
+    datb = np.frombuffer(dat, np.uint8).copy() if dat else np.zeros(10, np.uint8)
+    opts = AnnotOpts(min_hits, max_gap, ignore_hypo, hypo_index, mean_mode, mad_mode)
+    return int(olib().oracle_annotate_mt(bdz.h, _p(datb), _p(residues), _p(seq_off), _p(seq_len), len(seq_len),
+                                         C.byref(opts), int(n_threads)))
 
 
 def annotate_exact(keys, data, residues, seq_off, seq_len, min_hits=5, max_gap=200, ignore_hypo=0,

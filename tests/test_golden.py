@@ -104,3 +104,46 @@ def test_gpu_annotate_reproduces_golden(skm, gpu, annot):
         np.testing.assert_array_equal(off, g[ko])
         np.testing.assert_array_equal(calls.view(np.uint8).reshape(-1, 24), g[kc])
     db.close()
+
+
+@pytest.fixture(scope="module")
+def matrix(annot):
+    import make_golden_matrix
+    g = np.load(os.path.join(GOLD, "matrix_small.npz"), allow_pickle=False)
+    r, o, l, idx, nidx = make_golden_matrix.matrix_inputs()
+    assert make_golden.digest(r, o, l, idx) == str(g["input_sha256"]), "matrix fixture input drifted"
+    assert nidx == int(g["n_idx"])
+    return g, (r, o, l, idx, nidx)
+
+
+def test_oracle_reproduces_matrix(annot, matrix):
+    a, _ = annot
+    g, (r, o, l, idx, nidx) = matrix
+    funcs = list(a["functions"])
+    ob = oracle_ref.Bdz(a["mph"].tobytes())
+    got = oracle_ref.matrix_distance(ob, a["dat"].tobytes(), r, o, l, idx, funcs.index("hypothetical protein"))
+    np.testing.assert_array_equal(got, g["pairs"])
+    assert len(got) > 1000
+
+
+@pytest.mark.gpu
+def test_gpu_matrix_reproduces_golden(skm, gpu, annot, matrix):
+    a, _ = annot
+    g, (r, o, l, idx, nidx) = matrix
+    db = skm.CmphKmerDb(mph=a["mph"].tobytes(), dat=a["dat"].tobytes(), device=gpu)
+    md = skm.MatrixDistance(db, list(a["functions"]), r, o, l, seq_idx=idx, n_idx=nidx)
+    np.testing.assert_array_equal(md.compute(), g["pairs"])
+    md.close()
+    db.close()
+
+
+def test_multithreaded_annotate_port_counts_the_same_calls(annot):
+    """oracle_annotate_mt (bench.py's all-core CPU baseline of the annotate leg) makes the calls
+    of the single-thread restatement."""
+    g, (qr, qo, ql) = annot
+    funcs = list(g["functions"])
+    ob = oracle_ref.Bdz(g["mph"].tobytes())
+    hypo = funcs.index("hypothetical protein")
+    for threads in (1, 3, 8):
+        n = oracle_ref.annotate_mt(ob, g["dat"].tobytes(), qr, qo, ql, threads, hypo_index=hypo)
+        assert n == len(g["calls"])
