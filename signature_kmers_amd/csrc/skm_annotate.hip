@@ -317,16 +317,20 @@ __global__ void k_calls_scan(CallArgs A, uint4* __restrict__ segs) {
     const uint32_t* hit = A.hits + m.pstart;
     uint4* out = segs + A.cap_off[s];
     uint32_t nseg = 0;
-    // HitSet: all usable hits in window range [first, last_pos]; pair = (prev, last)
-    uint32_t count = 0, first = 0, last_pos = 0, prev_pos = 0, last_f = 0, prev_f = 0, cur = 0xFFFFu;
+    // HitSet: all usable hits in window range [first, last_pos]; pair = (prev, last); ncur = the
+    // hits of the current function (HitSet::process's fI_count).  A process() event with
+    // ncur < min_hits emits no call (call_functions.tcc:60), so it yields no segment.
+    uint32_t count = 0, ncur = 0, first = 0, last_pos = 0, prev_pos = 0, last_f = 0, prev_f = 0, cur = 0xFFFFu;
     auto process = [&]() {
-        out[nseg++] = make_uint4(s, first, last_pos, cur);
+        if ((int)ncur >= A.min_hits) out[nseg++] = make_uint4(s, first, last_pos, cur);
         if (prev_f != cur && prev_f == last_f) {
             cur = prev_f;
             first = prev_pos;
             count = 2;
+            ncur = 2;  // the kept pair has the new current function
         } else {
             count = 0;
+            ncur = 0;
         }
     };
     for (uint32_t i0 = 0; i0 < nwin; i0 += 8) {
@@ -339,10 +343,12 @@ __global__ void k_calls_scan(CallArgs A, uint4* __restrict__ segs) {
             if (!usable(h, A)) continue;
             const uint32_t f = h >> 16;
             if (count > 0 && (uint64_t)last_pos + (uint64_t)A.max_gap < (uint64_t)i) {
-                if ((int)count >= A.min_hits)
+                if ((int)count >= A.min_hits) {
                     process();
-                else
+                } else {
                     count = 0;
+                    ncur = 0;
+                }
             }
             if (count == 0) {
                 cur = f;
@@ -353,10 +359,11 @@ __global__ void k_calls_scan(CallArgs A, uint4* __restrict__ segs) {
             last_pos = i;
             last_f = f;
             ++count;
+            ncur += f == cur;
             if (count > 1 && cur != f && prev_f == f) process();
         }
     }
-    if ((int)count >= A.min_hits) out[nseg++] = make_uint4(s, first, last_pos, cur);
+    if ((int)count >= A.min_hits && (int)ncur >= A.min_hits) out[nseg++] = make_uint4(s, first, last_pos, cur);
     A.counts[s] = nseg;
 }
 
