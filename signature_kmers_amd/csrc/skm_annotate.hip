@@ -404,7 +404,7 @@ __device__ uint32_t kth_dev_sorted(const uint32_t* v, uint32_t n, uint32_t C2, u
 }
 
 constexpr int SEG_WAVES = 4;
-constexpr uint32_t SEG_CAP = 2048;
+constexpr uint32_t SEG_CAP = 1024;  // 16 KB of LDS per 4-wave block: 8 blocks per CU (2048: 5)
 
 // One wave per HitSet::process segment (call_functions.tcc:35-103): the hits of the current
 // function in window order (ballot compaction into LDS), Boost.Math mean (four-lane Welford on
