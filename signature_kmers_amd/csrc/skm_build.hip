@@ -2412,8 +2412,17 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
     const uint32_t N = e.npad, n = e.n;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint64_t hprefix = (uint64_t)(A.bucket_base + e.bucket) << A.rem_bits;
-    // phase 0: chunks of CAP sorted in LDS (directions from the global index)
-    for (uint32_t c0 = 0; c0 < N; c0 += CAP) {
+    // phase 0: chunks of CAP sorted in LDS (directions from the global index).  The padding
+    // beyond n holds the maximum key, so a chunk made only of padding is sorted in either
+    // direction: it is written, not sorted (the merges below move data into it, so they run
+    // over all N)
+    const uint32_t nch = (n + CAP - 1) / CAP * CAP;  // first all-padding chunk
+    for (uint32_t c0 = nch; c0 < N; c0 += CAP)
+        for (uint32_t j = tid; j < CAP; j += nt) {
+            ghi[c0 + j] = ~0ull;
+            glo[c0 + j] = ~0ull;
+        }
+    for (uint32_t c0 = 0; c0 < nch; c0 += CAP) {
         for (uint32_t j = tid; j < CAP; j += nt) {
             const uint32_t g = c0 + j;
             if (g < n) {
