@@ -226,19 +226,18 @@ __device__ __forceinline__ bool elem_less(uint64_t ah, uint64_t al, uint64_t bh,
     return ah < bh || (ah == bh && al < bl);
 }
 
-// Bitonic network over hi/lo[0..N) restricted to stages k in [kmin..kmax] (pow2), all strides j
-// of those stages below jlim; gidx0 = global index of element 0 (for chunked global sorts).
-__device__ void bitonic_lds(uint64_t* hi, uint64_t* lo, uint32_t N, uint32_t kmin, uint32_t kmax, uint32_t jtop,
-                            uint64_t gidx0) {
+// Bitonic network over hi/lo[0..N) restricted to stages k in [kmin..kmax] (pow2), strides j of
+// those stages up to jtop.  Ascending-only network: the first step of stage k pairs i with its mirror i ^ (k - 1) in the
+// k-block, the later steps are half-cleaners; every block ends ascending, so maximum-key padding
+// at the top never moves and work on it can be skipped.
+__device__ void bitonic_lds(uint64_t* hi, uint64_t* lo, uint32_t N, uint32_t kmin, uint32_t kmax, uint32_t jtop) {
     for (uint32_t k = kmin; k <= kmax; k <<= 1) {
         for (uint32_t j = min(k >> 1, jtop); j > 0; j >>= 1) {
             for (uint32_t t = threadIdx.x; t < N / 2; t += blockDim.x) {
                 uint32_t i = 2 * t - (t & (j - 1));
-                uint32_t l = i + j;
-                bool asc = (((gidx0 + i) & k) == 0);
+                uint32_t l = j == (k >> 1) ? (i ^ (k - 1)) : i + j;
                 uint64_t ah = hi[i], al = lo[i], bh = hi[l], bl = lo[l];
-                bool gt = elem_less(bh, bl, ah, al);
-                if (gt == asc) {
+                if (elem_less(bh, bl, ah, al)) {
                     hi[i] = bh;
                     lo[i] = bl;
                     hi[l] = ah;
@@ -2412,10 +2411,9 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
     const uint32_t N = e.npad, n = e.n;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint64_t hprefix = (uint64_t)(A.bucket_base + e.bucket) << A.rem_bits;
-    // phase 0: chunks of CAP sorted in LDS (directions from the global index).  The padding
-    // beyond n holds the maximum key, so a chunk made only of padding is sorted in either
-    // direction: it is written, not sorted (the merges below move data into it, so they run
-    // over all N)
+    // phase 0: chunks of CAP sorted ascending in LDS.  The padding beyond n holds the maximum
+    // key and the network is ascending-only, so no element ever moves into a chunk made only of
+    // padding: those chunks are written once and skipped by every later step
     const uint32_t nch = (n + CAP - 1) / CAP * CAP;  // first all-padding chunk
     for (uint32_t c0 = nch; c0 < N; c0 += CAP)
         for (uint32_t j = tid; j < CAP; j += nt) {
@@ -2434,7 +2432,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
             }
         }
         __syncthreads();
-        bitonic_lds(s_hi, s_lo, CAP, 2, CAP, CAP, c0);
+        bitonic_lds(s_hi, s_lo, CAP, 2, CAP, CAP);
         for (uint32_t j = tid; j < CAP; j += nt) {
             ghi[c0 + j] = s_hi[j];
             glo[c0 + j] = s_lo[j];
@@ -2446,10 +2444,10 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
         for (uint32_t j = k >> 1; j >= (uint32_t)CAP; j >>= 1) {
             for (uint32_t t = tid; t < N / 2; t += nt) {
                 const uint32_t i = 2 * t - (t & (j - 1));
-                const uint32_t l = i + j;
-                const bool asc = ((i & k) == 0);
+                if (i >= nch) continue;  // i and its partner above it are both maximum-key padding
+                const uint32_t l = j == (k >> 1) ? (i ^ (k - 1)) : i + j;
                 const uint64_t ah = ghi[i], al = glo[i], bh = ghi[l], bl = glo[l];
-                if (elem_less(bh, bl, ah, al) == asc) {
+                if (elem_less(bh, bl, ah, al)) {
                     ghi[i] = bh;
                     glo[i] = bl;
                     ghi[l] = ah;
@@ -2459,13 +2457,13 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
             __threadfence_block();
             __syncthreads();
         }
-        for (uint32_t c0 = 0; c0 < N; c0 += CAP) {
+        for (uint32_t c0 = 0; c0 < nch; c0 += CAP) {  // chunks above nch stay all padding
             for (uint32_t j = tid; j < CAP; j += nt) {
                 s_hi[j] = ghi[c0 + j];
                 s_lo[j] = glo[c0 + j];
             }
             __syncthreads();
-            bitonic_lds(s_hi, s_lo, CAP, k, k, CAP >> 1, c0);
+            bitonic_lds(s_hi, s_lo, CAP, k, k, CAP >> 1);
             for (uint32_t j = tid; j < CAP; j += nt) {
                 ghi[c0 + j] = s_hi[j];
                 glo[c0 + j] = s_lo[j];
