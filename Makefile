@@ -41,10 +41,16 @@ bin/%: $(SRC)/tools/%.cpp $(FRONT) $(LIB) $(FRONTH)
 	$(CXX) -O2 -std=c++17 -Wall -Iinclude -I$(SRC)/front $< $(FRONT) -o $@ -L signature_kmers_amd -lskm -pthread \
 	  -Wl,-rpath,'$$ORIGIN/../signature_kmers_amd' -Wl,-rpath,/opt/rocm/lib
 
+# random-gather ceiling of the annotate lookup (not part of `all`)
+probe: bin/gather_probe
+bin/gather_probe: tools/gather_probe.cpp
+	@mkdir -p bin
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -x hip $< -o $@
+
 $(ORACLE): oracle/skm_oracle.cpp
 	$(CXX) -O2 -fPIC -shared -std=c++17 -ffp-contract=off -pthread $< -o $@
 
 clean:
 	rm -rf build bin $(LIB) $(ORACLE)
 
-.PHONY: all clean
+.PHONY: all clean probe
