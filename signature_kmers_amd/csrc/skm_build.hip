@@ -2215,14 +2215,14 @@ __global__ __launch_bounds__(BIG_WG) void k_big_append(const BigOut* __restrict_
 // so the overflow path (and its long P^2 chains) can run concurrently with the group-by.
 constexpr uint32_t PT_ROUND = 2048;  // elements staged per round of the level-2 scatter
 
-__global__ __launch_bounds__(BP_THREADS, 2) void k_partition(BucketArgs A) {
-    __shared__ uint32_t s_sub[(1 << MAX_B2) + 1];
-    __shared__ uint32_t s_cur[1 << MAX_B2];
+// LDS ~52 KB: three workgroups per CU (the sub-bucket of a staged element is recomputed from its
+// key instead of staged, and the running write offsets double as the sub-bucket table)
+__global__ __launch_bounds__(BP_THREADS, 3) void k_partition(BucketArgs A) {
+    __shared__ uint32_t s_cur[(1 << MAX_B2) + 1];   // counts, then running write offsets
     __shared__ uint32_t s_rc[1 << MAX_B2];          // this round's count per sub-bucket
-    __shared__ uint32_t s_ro[(1 << MAX_B2) + 1];    // ... and its staging offset
+    __shared__ uint16_t s_ro[(1 << MAX_B2) + 1];    // ... and its staging offset (<= PT_ROUND)
     __shared__ uint64_t s_sh[PT_ROUND];
     __shared__ uint64_t s_sl[PT_ROUND];
-    __shared__ uint16_t s_sd[PT_ROUND];
     __shared__ __align__(16) uint32_t s_wave[48];
     const uint32_t bucket = blockIdx.x;
     if (bucket >= A.nbuckets) return;
@@ -2238,7 +2238,7 @@ __global__ __launch_bounds__(BP_THREADS, 2) void k_partition(BucketArgs A) {
     while (b2 < MAX_B2 && (n >> b2) > (uint64_t)SUB_TARGET) ++b2;
     const uint32_t nsub = 1u << b2;
     const int shift = A.rem_bits - b2;
-    for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_sub[d] = 0;
+    for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_cur[d] = 0;
     __syncthreads();
     // the bucket's elements: one contiguous range, or one piece per source rank after the exchange
     const uint32_t nseg = A.nsrc;
@@ -2256,7 +2256,7 @@ __global__ __launch_bounds__(BP_THREADS, 2) void k_partition(BucketArgs A) {
         seg(p, base, len);
         for (uint64_t j = threadIdx.x; j < len; j += blockDim.x) {
             const uint64_t h = A.recs_hi[base + j];
-            atomicAdd(&s_sub[(uint32_t)(((h >> 16) & rem_mask) >> shift)], 1u);
+            atomicAdd(&s_cur[(uint32_t)(((h >> 16) & rem_mask) >> shift)], 1u);
         }
     }
     __syncthreads();
@@ -2264,21 +2264,20 @@ __global__ __launch_bounds__(BP_THREADS, 2) void k_partition(BucketArgs A) {
         const uint32_t per = (nsub + blockDim.x - 1) / blockDim.x;
         const uint32_t d0 = threadIdx.x * per;
         uint32_t local = 0;
-        for (uint32_t d = d0; d < min(nsub, d0 + per); ++d) local += s_sub[d];
+        for (uint32_t d = d0; d < min(nsub, d0 + per); ++d) local += s_cur[d];
         uint32_t tot;
         uint32_t run = wg_exclusive_scan(local, s_wave, tot);
         for (uint32_t d = d0; d < min(nsub, d0 + per); ++d) {
-            const uint32_t t = s_sub[d];
-            s_sub[d] = run;
+            const uint32_t t = s_cur[d];
+            s_cur[d] = run;
             run += t;
         }
         __syncthreads();
-        if (threadIdx.x == 0) s_sub[nsub] = tot;
+        if (threadIdx.x == 0) s_cur[nsub] = tot;
         __syncthreads();
     }
-    for (uint32_t d = threadIdx.x; d < nsub; d += blockDim.x) s_cur[d] = s_sub[d];
     if (threadIdx.x == 0) tab[0] = nsub;
-    for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) tab[1 + d] = s_sub[d];
+    for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) tab[1 + d] = s_cur[d];
     __syncthreads();
     // staged scatter: each round sorts PT_ROUND elements by sub-bucket in LDS, then writes each
     // sub-bucket's run contiguously (whole lines instead of scattered 8-byte stores)
@@ -2330,10 +2329,10 @@ __global__ __launch_bounds__(BP_THREADS, 2) void k_partition(BucketArgs A) {
                 uint32_t tot;
                 uint32_t run = wg_exclusive_scan(local, s_wave, tot);
                 for (uint32_t d = d0; d < min(nsub, d0 + per); ++d) {
-                    s_ro[d] = run;
+                    s_ro[d] = (uint16_t)run;
                     run += s_rc[d];
                 }
-                if (threadIdx.x == 0) s_ro[nsub] = tot;
+                if (threadIdx.x == 0) s_ro[nsub] = (uint16_t)tot;
                 __syncthreads();
             }
 #pragma unroll
@@ -2342,14 +2341,14 @@ __global__ __launch_bounds__(BP_THREADS, 2) void k_partition(BucketArgs A) {
                     const uint32_t slot = s_ro[sb[u]] + rk[u];
                     s_sh[slot] = eh[u];
                     s_sl[slot] = el[u];
-                    s_sd[slot] = (uint16_t)sb[u];
                 }
             __syncthreads();
             const uint32_t tot = s_ro[nsub];
             for (uint32_t k = threadIdx.x; k < tot; k += blockDim.x) {
-                const uint32_t d = s_sd[k];
+                const uint64_t h = s_sh[k];
+                const uint32_t d = (uint32_t)(((h >> 16) & rem_mask) >> shift);
                 const uint64_t o = r0 + s_cur[d] + (k - s_ro[d]);
-                A.tmp_hi[o] = s_sh[k];
+                A.tmp_hi[o] = h;
                 A.tmp_lo[o] = s_sl[k];
             }
             __syncthreads();
@@ -2357,13 +2356,15 @@ __global__ __launch_bounds__(BP_THREADS, 2) void k_partition(BucketArgs A) {
             __syncthreads();
         }
     }
+    // s_cur[d] now ends sub-bucket d, i.e. starts d + 1
     for (uint32_t d = threadIdx.x; d < nsub; d += blockDim.x) {
-        const uint32_t cnt = s_sub[d + 1] - s_sub[d];
+        const uint32_t beg = d ? s_cur[d - 1] : 0u;
+        const uint32_t cnt = s_cur[d] - beg;
         if (cnt > (uint32_t)CAP) {
             const unsigned int en = atomicAdd(reinterpret_cast<unsigned int*>(&A.ctr[1]), 1u);
             if (en < A.ovf_cap) {
                 OvfEntry o;
-                o.off = r0 + s_sub[d];
+                o.off = r0 + beg;
                 o.n = cnt;
                 o.bucket = bucket;
                 o.scratch = 0;
