@@ -1183,13 +1183,30 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
     const int l0_shift = nbits - SC_L0_BITS;
     const uint64_t begin = (uint64_t)blockIdx.x * X.span;
     const uint64_t end = min(begin + X.span, X.rp);
+    // the next round's residues and sequence record are loaded before this round's LDS work, so
+    // their HBM latency (blk2seq -> meta is a dependent pair) overlaps the staging
+    uint2 nv0 = make_uint2(0u, 0u), nv1 = make_uint2(0u, 0u);
+    uint32_t ns = 0;
+    SeqMeta nm{};
+    auto fetch = [&](uint64_t b) {
+        const uint64_t q = b + (uint64_t)threadIdx.x * SC_POS;
+        nv0 = nv1 = make_uint2(0u, 0u);
+        if (q < end) {  // the residue buffer is padded by 64 bytes past rp, not more
+            nv0 = *reinterpret_cast<const uint2*>(res + q);
+            nv1 = *reinterpret_cast<const uint2*>(res + q + 8);
+            ns = X.blk2seq[q >> 6];
+            nm = X.meta[ns];
+        }
+    };
+    fetch(begin);
     for (uint64_t base = begin; base < end; base += SC_ROUND) {
         if (threadIdx.x < 128) L.cnt[threadIdx.x] = 0;
         __syncthreads();
         const uint64_t p0 = base + (uint64_t)threadIdx.x * SC_POS;
-        const bool live = p0 < end;  // the residue buffer is padded by 64 bytes past rp, not more
-        const uint2 v0 = live ? *reinterpret_cast<const uint2*>(res + p0) : make_uint2(0u, 0u);
-        const uint2 v1 = live ? *reinterpret_cast<const uint2*>(res + p0 + 8) : make_uint2(0u, 0u);
+        const uint2 v0 = nv0, v1 = nv1;
+        uint32_t s = ns;
+        SeqMeta m = nm;
+        if (base + SC_ROUND < end) fetch(base + SC_ROUND);
         const uint32_t w[4] = {v0.x, v0.y, v1.x, v1.y};
         uint32_t code[16];
         uint32_t valid = 0;
@@ -1203,12 +1220,6 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
 #pragma unroll
         for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
         constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
-        uint32_t s = 0;
-        SeqMeta m{};
-        if (valid) {
-            s = X.blk2seq[p0 >> 6];
-            m = X.meta[s];
-        }
         uint64_t eh[SC_POS], el[SC_POS];
         uint32_t rk[SC_POS], l0[SC_POS];
         uint32_t ok = 0;
