@@ -2164,7 +2164,7 @@ constexpr int BIG_WG = 256;
 // LARGE = false: groups of 65..1024 members (E <= 16, 128 VGPRs, 2 waves per SIMD);
 // LARGE = true: 1025..CAP (E = 32), a separate launch so the common case keeps its occupancy.
 template <bool LARGE>
-__global__ __launch_bounds__(BIG_WG, LARGE ? 1 : 2) void k_big_groups(BigArgs B) {
+__global__ __launch_bounds__(BIG_WG, LARGE ? 3 : 4) void k_big_groups(BigArgs B) {
     const uint64_t nd = min((uint64_t)*B.ndesc, (uint64_t)B.cap);
     const uint64_t nw = (uint64_t)gridDim.x * (BIG_WG / 64);
     for (uint64_t g = (uint64_t)blockIdx.x * (BIG_WG / 64) + (threadIdx.x >> 6); g < nd; g += nw) {
