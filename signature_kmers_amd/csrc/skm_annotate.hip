@@ -90,8 +90,8 @@ __global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict
             }
         } else {
             // BDZ search in phases over 8 windows at a time so every dependent level issues 8+
-            // independent loads: (1) jenkins -> 3 g words, (2) select vertex -> rank word + the
-            // vertex's 32-byte g block, (3) branch-free popcount rank -> .dat record
+            // independent loads: (1) jenkins -> 3 g words, (2) select vertex -> the rank word of its
+            // g word (same line), (3) one popcount -> .dat record
 #pragma unroll
             for (int half = 0; half < LK_POS / 8; ++half) {
                 uint32_t hv[8][3], gw[8][3];
@@ -107,8 +107,7 @@ __global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict
 #pragma unroll
                     for (int j = 0; j < 3; ++j) gw[u][j] = D.blk[(hv[u][j] >> 7) * 16u + ((hv[u][j] & 127u) >> 4)];
                 }
-                uint32_t vv[8], rt[8];
-                uint4 b0[8], b1[8];
+                uint32_t vv[8], rw[8], ws[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     uint32_t sum = 0;
@@ -117,25 +116,16 @@ __global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict
                     const uint32_t sel = sum % 3u;
                     const uint32_t v = sel == 0 ? hv[u][0] : (sel == 1 ? hv[u][1] : hv[u][2]);
                     vv[u] = v;
-                    const uint32_t blk = v >> 7;  // b = 7 (checked on open): the line of v's own g word
-                    const uint4* gb = reinterpret_cast<const uint4*>(D.blk) + 4ull * blk;
-                    b0[u] = gb[0];
-                    b1[u] = gb[1];
-                    rt[u] = D.blk[16ull * blk + 8];
+                    ws[u] = sel == 0 ? gw[u][0] : (sel == 1 ? gw[u][1] : gw[u][2]);  // v's own g word
+                    // b = 7 (checked on open): the rank of v's g word, in the line phase 1 touched
+                    rw[u] = D.blk[16ull * (v >> 7) + 8 + ((v & 127u) >> 4)];
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int t = half * 8 + u;
-                    const uint32_t off = vv[u] & 127u, fw = off >> 4, pe = off & 15u;
-                    const uint32_t wd[8] = {b0[u].x, b0[u].y, b0[u].z, b0[u].w, b1[u].x, b1[u].y, b1[u].z, b1[u].w};
-                    uint32_t rank = rt[u], wf = wd[0];
-#pragma unroll
-                    for (uint32_t j = 0; j < 8; ++j) {
-                        rank += j < fw ? 16u - unassigned_in(wd[j]) : 0u;
-                        wf = j == fw ? wd[j] : wf;
-                    }
+                    const uint32_t pe = vv[u] & 15u;
                     const uint32_t pmask = pe ? (0xFFFFFFFFu >> (32u - 2u * pe)) : 0u;
-                    rank += pe - unassigned_in(wf & pmask);
+                    const uint32_t rank = rw[u] + pe - unassigned_in(ws[u] & pmask);
                     const uint64_t p = base + t;
                     uint32_t o = NO_HIT;
                     if (p < rp && ((bad >> t) & 0xFFu) == 0 && ((amb >> (t + 8)) & 1u) == 0 && rank < D.m)
@@ -731,7 +721,14 @@ void db_upload(skm_db* db, const uint8_t* dat, size_t dat_len) {
                 const uint64_t gi = 8 * q + (uint64_t)w;
                 blk[16 * q + (uint64_t)w] = 4 * gi + 4 <= g.size() ? gw[gi] : 0xFFFFFFFFu;
             }
-            blk[16 * q + 8] = q < h.ranktable.size() ? h.ranktable[q] : 0u;
+            // words 8..15: the rank of the first vertex of each g word (rank table entry plus
+            // the assigned vertices of the words before it), so a lookup needs one more word
+            uint32_t r = q < h.ranktable.size() ? h.ranktable[q] : 0u;
+            for (int w = 0; w < 8; ++w) {
+                blk[16 * q + 8 + (uint64_t)w] = r;
+                const uint32_t x = blk[16 * q + (uint64_t)w];
+                r += 16u - (uint32_t)__builtin_popcount(x & (x >> 1) & 0x55555555u);
+            }
         }
         db->d_blk.ensure(4 * blk.size());
         SKM_HIP(hipMemcpy(db->d_blk.p, blk.data(), 4 * blk.size(), hipMemcpyHostToDevice));

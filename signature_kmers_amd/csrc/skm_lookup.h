@@ -26,9 +26,10 @@ struct DevBdz {
     const uint32_t* ranktable;
     const uint16_t* dat;        // 5 u16 per record
     const uint32_t* fm;         // per record: function_index | mean << 16 (what the call path reads)
-    // b == 7: 64-byte line per block of 128 vertices: u32 words 0-7 = the block's g, word 8 = its
-    // rank table entry, so the selected vertex's rank word and g block share one line with its
-    // own g word (already fetched for the vertex selection)
+    // b == 7: 64-byte line per block of 128 vertices: u32 words 0-7 = the block's g, words 8-15 =
+    // the rank of the first vertex of each g word (rank table entry + assigned vertices before
+    // it), so a vertex's rank is one word of the line its g word (fetched for the vertex
+    // selection) already lives in
     const uint32_t* blk;
     uint32_t m, r, b, seed;
     uint64_t r_magic;           // fastmod: ceil(2^64 / r)
