@@ -58,7 +58,7 @@ __global__ void k_exact_insert(const uint64_t* __restrict__ keys, uint64_t n, un
 // table, LK_BDZ = BDZ with any b (per-window search)
 enum { LK_BDZ7 = 0, LK_EXACT = 1, LK_BDZ = 2 };
 template <int MODE>
-__global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict__ res, uint64_t rp, DevBdz D,
+__global__ __launch_bounds__(LK_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_lookup(const uint8_t* __restrict__ res, uint64_t rp, DevBdz D,
                                                       uint32_t* __restrict__ hits) {
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x * LK_POS;
     for (uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * LK_POS; base < rp; base += step) {
@@ -90,46 +90,49 @@ __global__ __launch_bounds__(LK_THREADS) void k_lookup(const uint8_t* __restrict
             }
         } else {
             // BDZ search in phases over 8 windows at a time so every dependent level issues 8+
-            // independent loads: (1) jenkins -> 3 g words, (2) select vertex -> the rank word of its
-            // g word (same line), (3) one popcount -> .dat record
+            // independent loads: (1) jenkins -> 3 (g word, rank word) pairs, one 8-byte load each,
+            // (2) select vertex, one popcount -> .dat record
 #pragma unroll
             for (int half = 0; half < LK_POS / 8; ++half) {
-                uint32_t hv[8][3], gw[8][3];
+                uint32_t hl[8];  // the candidates' in-word positions (v & 15), 4 bits each
+                uint2 gp[8][3];  // (g word, rank of its first vertex) of each candidate
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     uint32_t lo, hi;
                     key_at(w, half * 8 + u, lo, hi);
                     uint32_t a = 0x9e3779b9u + lo, b = 0x9e3779b9u + hi, c = D.seed + 8u;
                     jmix(a, b, c);
-                    hv[u][0] = fastmod(a, D.r_magic, D.r);
-                    hv[u][1] = fastmod(b, D.r_magic, D.r) + D.r;
-                    hv[u][2] = fastmod(c, D.r_magic, D.r) + 2u * D.r;
+                    const uint32_t hv[3] = {fastmod(a, D.r_magic, D.r), fastmod(b, D.r_magic, D.r) + D.r,
+                                            fastmod(c, D.r_magic, D.r) + 2u * D.r};
+                    hl[u] = (hv[0] & 15u) | (hv[1] & 15u) << 4 | (hv[2] & 15u) << 8;
 #pragma unroll
-                    for (int j = 0; j < 3; ++j) gw[u][j] = D.blk[(hv[u][j] >> 7) * 16u + ((hv[u][j] & 127u) >> 4)];
+                    for (int j = 0; j < 3; ++j)
+                        gp[u][j] = *reinterpret_cast<const uint2*>(D.blk + (hv[j] >> 7) * 16u + 2u * ((hv[j] & 127u) >> 4));
                 }
-                uint32_t vv[8], rw[8], ws[8];
+                uint32_t rank[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     uint32_t sum = 0;
 #pragma unroll
-                    for (int j = 0; j < 3; ++j) sum += (gw[u][j] >> ((hv[u][j] & 15u) * 2)) & 3u;
+                    for (int j = 0; j < 3; ++j) sum += (gp[u][j].x >> (((hl[u] >> (4 * j)) & 15u) * 2)) & 3u;
                     const uint32_t sel = sum % 3u;
-                    const uint32_t v = sel == 0 ? hv[u][0] : (sel == 1 ? hv[u][1] : hv[u][2]);
-                    vv[u] = v;
-                    ws[u] = sel == 0 ? gw[u][0] : (sel == 1 ? gw[u][1] : gw[u][2]);  // v's own g word
-                    // b = 7 (checked on open): the rank of v's g word, in the line phase 1 touched
-                    rw[u] = D.blk[16ull * (v >> 7) + 8 + ((v & 127u) >> 4)];
+                    // v's own g word and the rank of its first vertex (b = 7, checked on open)
+                    // (selected per component: a select of whole uint2 values becomes a
+                    // dynamically indexed stack array)
+                    const bool s0 = sel == 0, s1 = sel == 1;
+                    const uint32_t qx = s0 ? gp[u][0].x : (s1 ? gp[u][1].x : gp[u][2].x);
+                    const uint32_t qy = s0 ? gp[u][0].y : (s1 ? gp[u][1].y : gp[u][2].y);
+                    const uint32_t pe = (hl[u] >> (4 * sel)) & 15u;
+                    const uint32_t pmask = pe ? (0xFFFFFFFFu >> (32u - 2u * pe)) : 0u;
+                    rank[u] = qy + pe - unassigned_in(qx & pmask);
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int t = half * 8 + u;
-                    const uint32_t pe = vv[u] & 15u;
-                    const uint32_t pmask = pe ? (0xFFFFFFFFu >> (32u - 2u * pe)) : 0u;
-                    const uint32_t rank = rw[u] + pe - unassigned_in(ws[u] & pmask);
                     const uint64_t p = base + t;
                     uint32_t o = NO_HIT;
-                    if (p < rp && ((bad >> t) & 0xFFu) == 0 && ((amb >> (t + 8)) & 1u) == 0 && rank < D.m)
-                        o = D.fm[rank];  // function_index << 16 | mean
+                    if (p < rp && ((bad >> t) & 0xFFu) == 0 && ((amb >> (t + 8)) & 1u) == 0 && rank[u] < D.m)
+                        o = D.fm[rank[u]];  // function_index << 16 | mean
                     out[t] = o;
                 }
             }
@@ -717,16 +720,14 @@ void db_upload(skm_db* db, const uint8_t* dat, size_t dat_len) {
         std::vector<uint32_t> blk(16 * nblk, 0);
         const uint32_t* gw = reinterpret_cast<const uint32_t*>(g.data());  // padded with 0xFF
         for (uint64_t q = 0; q < nblk; ++q) {
-            for (int w = 0; w < 8; ++w) {
-                const uint64_t gi = 8 * q + (uint64_t)w;
-                blk[16 * q + (uint64_t)w] = 4 * gi + 4 <= g.size() ? gw[gi] : 0xFFFFFFFFu;
-            }
-            // words 8..15: the rank of the first vertex of each g word (rank table entry plus
-            // the assigned vertices of the words before it), so a lookup needs one more word
+            // pairs (g word w, rank of its first vertex = rank table entry plus the assigned
+            // vertices of the words before it): one 8-byte load gives a vertex's g value and rank
             uint32_t r = q < h.ranktable.size() ? h.ranktable[q] : 0u;
             for (int w = 0; w < 8; ++w) {
-                blk[16 * q + 8 + (uint64_t)w] = r;
-                const uint32_t x = blk[16 * q + (uint64_t)w];
+                const uint64_t gi = 8 * q + (uint64_t)w;
+                const uint32_t x = 4 * gi + 4 <= g.size() ? gw[gi] : 0xFFFFFFFFu;
+                blk[16 * q + 2 * (uint64_t)w] = x;
+                blk[16 * q + 2 * (uint64_t)w + 1] = r;
                 r += 16u - (uint32_t)__builtin_popcount(x & (x >> 1) & 0x55555555u);
             }
         }

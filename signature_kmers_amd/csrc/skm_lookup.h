@@ -26,10 +26,9 @@ struct DevBdz {
     const uint32_t* ranktable;
     const uint16_t* dat;        // 5 u16 per record
     const uint32_t* fm;         // per record: function_index | mean << 16 (what the call path reads)
-    // b == 7: 64-byte line per block of 128 vertices: u32 words 0-7 = the block's g, words 8-15 =
-    // the rank of the first vertex of each g word (rank table entry + assigned vertices before
-    // it), so a vertex's rank is one word of the line its g word (fetched for the vertex
-    // selection) already lives in
+    // b == 7: 64-byte line per block of 128 vertices: 8 pairs (g word, rank of its first vertex =
+    // rank table entry + assigned vertices before it), so the 8-byte load that fetches a
+    // candidate vertex's g word for the selection also brings its rank
     const uint32_t* blk;
     uint32_t m, r, b, seed;
     uint64_t r_magic;           // fastmod: ceil(2^64 / r)
