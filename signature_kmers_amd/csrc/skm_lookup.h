@@ -108,6 +108,29 @@ __device__ __forceinline__ uint32_t bdz_lookup(const DevBdz& D, uint32_t lo, uin
     return rank;
 }
 
+// the same search over the b == 7 (g word, rank) pair lines (D.blk): one 8-byte gather per
+// candidate vertex, then the rank from the selected pair
+__device__ __forceinline__ uint32_t bdz7_lookup(const DevBdz& D, uint32_t lo, uint32_t hi) {
+    uint32_t a = 0x9e3779b9u + lo, b = 0x9e3779b9u + hi, c = D.seed + 8u;
+    jmix(a, b, c);
+    const uint32_t hv[3] = {fastmod(a, D.r_magic, D.r), fastmod(b, D.r_magic, D.r) + D.r,
+                            fastmod(c, D.r_magic, D.r) + 2u * D.r};
+    uint2 gp[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+        gp[j] = *reinterpret_cast<const uint2*>(D.blk + (hv[j] >> 7) * 16u + 2u * ((hv[j] & 127u) >> 4));
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) sum += (gp[j].x >> ((hv[j] & 15u) * 2)) & 3u;
+    const uint32_t sel = sum % 3u;
+    const bool s0 = sel == 0, s1 = sel == 1;
+    const uint32_t qx = s0 ? gp[0].x : (s1 ? gp[1].x : gp[2].x);
+    const uint32_t qy = s0 ? gp[0].y : (s1 ? gp[1].y : gp[2].y);
+    const uint32_t pe = (s0 ? hv[0] : (s1 ? hv[1] : hv[2])) & 15u;
+    const uint32_t pmask = pe ? (0xFFFFFFFFu >> (32u - 2u * pe)) : 0u;
+    return qy + pe - unassigned_in(qx & pmask);
+}
+
 __device__ __forceinline__ bool ambig(uint32_t c) { return c == 'X' || c == '*'; }
 
 __device__ __forceinline__ void wave_sync_lds() {

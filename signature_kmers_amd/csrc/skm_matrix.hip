@@ -57,7 +57,7 @@ struct MdHitArgs {
 };
 
 __device__ __forceinline__ uint32_t md_rank(const DevBdz& D, int exact, uint32_t lo, uint32_t hi) {
-    return exact ? exact_lookup(D, lo, hi) : bdz_lookup(D, lo, hi);
+    return exact ? exact_lookup(D, lo, hi) : (D.blk ? bdz7_lookup(D, lo, hi) : bdz_lookup(D, lo, hi));
 }
 
 // largest s with meta[s].pstart <= p
