@@ -120,6 +120,18 @@ int skm_build_last_timings(skm_build* b, float* ms, int cap);
  * [9]=groups of > 64 members handed to k_big_groups [10]=k-mers kept among them;
  * returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
+/* Build options beyond skm_build_opts (take effect at the next prepare/run):
+ *   "key_range_passes"        0 = automatic; else P = 1, 2, 4 .. 64 passes over disjoint k-mer
+ *                             ranges (top bits of the key hash).  The reference holds the whole
+ *                             proteome in one multimap (signature_build.h:61,122); a GPU shard
+ *                             whose occurrences exceed the work buffers is grouped pass by pass,
+ *                             with identical results (each k-mer lives in exactly one pass).
+ *   "device_memory_budget_mb" memory the automatic pass count plans for (0 = free memory).
+ * Diagnostic tunables (defaults are the tuned values): "overflow_heavy_min",
+ *   "overflow_inline_min", "overflow_inline_prio", "overflow_long_class", "overflow_chain_wgs",
+ *   "chain_prio", "bucket_prio", "chain_lds_kb", "host_timing".
+ * Unknown names and out-of-range values return SKM_E_ARG. */
+int skm_build_set_option(skm_build* b, const char* name, int64_t value);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then
  * enable/disable stamping for subsequent runs. */
 int skm_build_debug_stamps(skm_build* b, int enable, uint64_t* out, int cap);
@@ -176,6 +188,9 @@ int skm_db_open_kept(skm_db** out, const uint64_t* keys, const skm_stored_kmer_d
 int skm_db_size(skm_db* db, uint32_t* m);
 /* Batched cmph_search(hash, key, 8) (cmph_kmer.h:90-92); idx >= size is a miss. */
 int skm_db_lookup(skm_db* db, const uint64_t* keys, size_t n, uint32_t* idx_out);
+/* test hook: the same search through the generic bdz_search walk (any b), bypassing the b == 7
+ * (g word, rank) pair lines that skm_db_lookup / the annotate kernels use when present */
+int skm_debug_db_lookup_generic(skm_db* db, const uint64_t* keys, size_t n, uint32_t* idx_out);
 void skm_db_close(skm_db* db);
 
 /* Build a BDZ minimal perfect hash over keys (build_perfect_hash, perfect_hash.h:11-69):

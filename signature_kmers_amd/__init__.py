@@ -79,6 +79,7 @@ _SIGS = {
     "skm_build_run": (C.c_int, [_P]),
     "skm_build_last_timings": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int]),
     "skm_build_finish": (C.c_int, [_P, C.POINTER(_Kept)]),
+    "skm_build_set_option": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "skm_build_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
     "skm_build_debug_jobs": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int]),
     "skm_debug_chain_bench": (C.c_int, [C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_float)]),
@@ -95,6 +96,7 @@ _SIGS = {
     "skm_db_open_kept": (C.c_int, [C.POINTER(_P), _P, _P, C.c_size_t, C.c_int]),
     "skm_db_size": (C.c_int, [_P, C.POINTER(C.c_uint32)]),
     "skm_db_lookup": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "skm_debug_db_lookup_generic": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "skm_db_close": (None, [_P]),
     "skm_mph_build": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_char_p, C.c_char_p]),
     "skm_mph_build_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_char_p, C.c_char_p, C.c_int]),
@@ -255,6 +257,11 @@ class SignatureBuilder:
                  "exchange", "partition", "bucket_kernel", "big_groups"]
         return {names[i]: float(ms[i]) for i in range(n)}
 
+    def set_option(self, name: str, value: int):
+        """skm_build_set_option: "key_range_passes" (0 = automatic), "device_memory_budget_mb",
+        and the diagnostic tunables named in include/skm.h."""
+        _check(lib().skm_build_set_option(self._h, name.encode(), int(value)))
+
     def counters(self) -> dict:
         v = (C.c_uint64 * 11)()
         n = lib().skm_build_counters(self._h, v, 11)
@@ -354,6 +361,15 @@ class CmphKmerDb:
         out = np.zeros(len(keys), dtype=np.uint32)
         if len(keys):
             _check(lib().skm_db_lookup(self._h, _ptr(keys), len(keys), _ptr(out)))
+        return out
+
+    def lookup_keys_generic(self, keys: np.ndarray) -> np.ndarray:
+        """Test hook: the generic bdz_search walk (skm_debug_db_lookup_generic), bypassing the
+        b == 7 (g word, rank) pair lines that lookup_keys and the annotate kernels use."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        out = np.zeros(len(keys), dtype=np.uint32)
+        if len(keys):
+            _check(lib().skm_debug_db_lookup_generic(self._h, _ptr(keys), len(keys), _ptr(out)))
         return out
 
     def close(self):

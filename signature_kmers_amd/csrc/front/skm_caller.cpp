@@ -6,6 +6,7 @@
 #include <chrono>
 #include <cstring>
 #include <fstream>
+#include <mutex>
 #include <thread>
 
 namespace skmf {
@@ -106,6 +107,8 @@ int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std
             for (size_t r = 0; r < files[f]->size(); ++r) where.emplace_back(f, r);
         std::atomic<size_t> next{0};
         std::atomic<int> first_rc{0};
+        std::mutex err_mu;  // skm_last_error() is per thread: the failing worker records its own message
+        std::string worker_err;
         auto work = [&]() {
             std::vector<char> fb(1 << 16);
             const size_t chunk = 4096;
@@ -115,7 +118,13 @@ int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std
                     float offset = 0;
                     int r = skm_find_best_call(calls.calls + calls.call_off[s], calls.call_off[s + 1] - calls.call_off[s],
                                                fidx.data(), fidx.size(), &c.fi, &c.score, &offset, fb.data(), fb.size());
-                    if (r) first_rc = r;
+                    if (r) {
+                        std::lock_guard<std::mutex> lk(err_mu);
+                        if (!first_rc) {
+                            first_rc = r;
+                            worker_err = skm_last_error();
+                        }
+                    }
                     c.func = fb.data();
                 }
             }
@@ -127,7 +136,7 @@ int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std
         for (auto& t : th) t.join();
         skm_calls_free(&calls);
         if (first_rc) {
-            err = skm_last_error();
+            err = worker_err.empty() ? std::string("find_best_call failed") : worker_err;
             return first_rc;
         }
         f0 = f1;

@@ -932,16 +932,18 @@ int skm_db_size(skm_db* db, uint32_t* m) {
 }
 
 extern "C++" {
-template <bool EXACT>
+// mode 0: exact table; 1: generic bdz_search (any b); 2: the (g word, rank) pair lines (b == 7)
+template <int MODE>
 __global__ void k_lookup_keys(const uint64_t* __restrict__ keys, uint64_t n, DevBdz D, uint32_t* __restrict__ out) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t k = keys[i];
-    out[i] = EXACT ? exact_lookup(D, (uint32_t)k, (uint32_t)(k >> 32)) : bdz_lookup(D, (uint32_t)k, (uint32_t)(k >> 32));
+    const uint32_t lo = (uint32_t)k, hi = (uint32_t)(k >> 32);
+    out[i] = MODE == 0 ? exact_lookup(D, lo, hi) : MODE == 1 ? bdz_lookup(D, lo, hi) : bdz7_lookup(D, lo, hi);
 }
 }  // extern "C++"
 
-int skm_db_lookup(skm_db* db, const uint64_t* keys, size_t n, uint32_t* idx_out) {
+static int db_lookup(skm_db* db, const uint64_t* keys, size_t n, uint32_t* idx_out, bool generic) {
     SKM_API_BEGIN
     SKM_CHECK(db && (n == 0 || (keys && idx_out)), SKM_E_ARG, "null argument");
     if (n == 0) return SKM_OK;
@@ -954,15 +956,25 @@ int skm_db_lookup(skm_db* db, const uint64_t* keys, size_t n, uint32_t* idx_out)
     dk.ensure(8 * n);
     dout.ensure(4 * n);
     SKM_HIP(hipMemcpy(dk.p, keys, 8 * n, hipMemcpyHostToDevice));
+    const dim3 grid((uint32_t)ceil_div(n, 256)), blk(256);
+    // the same search the annotate / matrix kernels run: pair lines whenever the DB has them
     if (db->exact)
-        hipLaunchKernelGGL(k_lookup_keys<true>, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, 0, dk.as<uint64_t>(),
-                           (uint64_t)n, db->dev, dout.as<uint32_t>());
+        hipLaunchKernelGGL(k_lookup_keys<0>, grid, blk, 0, 0, dk.as<uint64_t>(), (uint64_t)n, db->dev, dout.as<uint32_t>());
+    else if (db->dev.blk && !generic)
+        hipLaunchKernelGGL(k_lookup_keys<2>, grid, blk, 0, 0, dk.as<uint64_t>(), (uint64_t)n, db->dev, dout.as<uint32_t>());
     else
-        hipLaunchKernelGGL(k_lookup_keys<false>, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, 0, dk.as<uint64_t>(),
-                           (uint64_t)n, db->dev, dout.as<uint32_t>());
+        hipLaunchKernelGGL(k_lookup_keys<1>, grid, blk, 0, 0, dk.as<uint64_t>(), (uint64_t)n, db->dev, dout.as<uint32_t>());
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipMemcpy(idx_out, dout.p, 4 * n, hipMemcpyDeviceToHost));
     SKM_API_END
+}
+
+int skm_db_lookup(skm_db* db, const uint64_t* keys, size_t n, uint32_t* idx_out) {
+    return db_lookup(db, keys, n, idx_out, false);
+}
+
+int skm_debug_db_lookup_generic(skm_db* db, const uint64_t* keys, size_t n, uint32_t* idx_out) {
+    return db_lookup(db, keys, n, idx_out, true);
 }
 
 void skm_db_close(skm_db* db) { delete db; }

@@ -104,8 +104,13 @@ bool bdz_parse(const uint8_t* buf, size_t len, Bdz& h, std::string& err) {
     }
     h.ranktable.resize(h.ranktablesize);
     if (h.ranktablesize) std::memcpy(h.ranktable.data(), buf + p, 4ull * h.ranktablesize);
-    if (h.r == 0 || h.n != 3 * h.r || size != h.m) {
+    // everything the searches index must be in range: g[v] for v < n = 3r, ranktable[v >> b]
+    if (h.r == 0 || 3ull * h.r != (uint64_t)h.n || size != h.m || h.m > h.n) {
         err = "inconsistent BDZ parameters";
+        return false;
+    }
+    if (h.b >= 32 || h.k != (1u << h.b) || (uint64_t)h.ranktablesize < ((uint64_t)h.n + h.k - 1) / h.k) {
+        err = "inconsistent BDZ rank table (k, b, ranktablesize)";
         return false;
     }
     return true;

@@ -1054,6 +1054,9 @@ struct ExtractArgs {
     const uint8_t* res;
     uint64_t rp, span;
     int owner_bits, b1_bits;
+    int pass_bits;                  // key-range passes: windows whose mix43 top pass_bits == pass_id
+    uint32_t pass_id;
+    const uint8_t* ids;             // pass_bits > 0: per-window pass id (0xFF: no valid window)
     uint32_t* hist;                 // count pass: [wg][bucket]
     const uint32_t* offs;           // scatter pass: [wg][bucket] element offsets within the owner
     const uint64_t* owner_start;    // [owners+1]
@@ -1064,23 +1067,93 @@ struct ExtractArgs {
     uint64_t* out_lo;
 };
 
-template <bool SCATTER>
+// bit t set iff byte t of the 16 bytes equals v
+__device__ __forceinline__ uint32_t match16(const uint4 w, uint32_t v) {
+    const uint32_t x[4] = {w.x, w.y, w.z, w.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) m |= (((x[j >> 2] >> (8 * (j & 3))) & 0xFFu) == v ? 1u : 0u) << j;
+    return m;
+}
+
+// ------------------------------------------------------------------------------------------
+// Key-range passes (out-of-core build).  A shard whose occurrence elements do not fit the work
+// buffers is grouped in P = 2^pass_bits passes over disjoint k-mer ranges (the top pass_bits of
+// mix43(key)); every k-mer lives in exactly one pass, so the passes' kept sets are disjoint and
+// their union is the single-pass result.  k_pass_ids computes each window's pass id once per
+// run (one scan of the resident residues); each pass's extract kernels then read the id bytes
+// and hash only their own windows.  With counts != nullptr (prepare), it histograms the valid
+// windows by the top 6 hash bits instead, which sizes the passes.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ res, uint64_t rp, int pass_bits,
+                                                  uint8_t* __restrict__ ids, unsigned long long* __restrict__ counts) {
+    __shared__ uint32_t s_cnt[64];
+    if (counts) {
+        if (threadIdx.x < 64) s_cnt[threadIdx.x] = 0;
+        __syncthreads();
+    }
+    const uint64_t nchunk = (rp + 15) >> 4;
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunk; c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t base = c << 4;
+        const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
+        const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
+        const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        uint32_t code[24];
+        uint32_t valid = 0;
+#pragma unroll
+        for (int j = 0; j < 24; ++j) {
+            const uint32_t cd = residue_code((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+            valid |= (cd < 40u ? 1u : 0u) << j;
+            code[j] = cd < 40u ? cd : 0u;
+        }
+        uint64_t k = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
+        constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
+        uint32_t out[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
+            uint32_t id = 0xFFu;
+            if (((valid >> t) & 0xFFu) == 0xFFu && base + t < rp) {
+                const uint64_t h = mix43(k);
+                if (counts)
+                    atomicAdd(&s_cnt[(uint32_t)(h >> (KEY_BITS - 6))], 1u);
+                else
+                    id = (uint32_t)(h >> (KEY_BITS - pass_bits));
+            }
+            out[t >> 2] |= id << (8 * (t & 3));
+        }
+        if (!counts) *reinterpret_cast<uint4*>(ids + base) = make_uint4(out[0], out[1], out[2], out[3]);
+    }
+    if (counts) {
+        __syncthreads();
+        if (threadIdx.x < 64 && s_cnt[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)s_cnt[threadIdx.x]);
+    }
+}
+
+// Per-workgroup histogram of the level-1 buckets (count pass).  IDS: key-range pass mode, only
+// the windows whose id byte is this pass are hashed and counted.
+template <bool IDS>
 __global__ __launch_bounds__(EX_THREADS) void k_extract(ExtractArgs X) {
     const uint8_t* __restrict__ res = X.res;
     const uint64_t rp = X.rp, span = X.span;
-    const int owner_bits = X.owner_bits, b1_bits = X.b1_bits;
     extern __shared__ uint32_t s_cnt[];  // [NB]
-    const int nbits = owner_bits + b1_bits;
+    const int nbits = X.owner_bits + X.b1_bits;
     const uint32_t NB = 1u << nbits;
-    const int rem_bits = KEY_BITS - nbits;
-    const uint64_t rem_mask = (1ull << rem_bits) - 1;
+    const int rem_bits = KEY_BITS - X.pass_bits - nbits;
     const uint32_t wg = blockIdx.x;
-    for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) s_cnt[b] = SCATTER ? X.offs[(uint64_t)wg * NB + b] : 0u;
+    for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) s_cnt[b] = 0u;
     __syncthreads();
     const uint64_t begin = (uint64_t)wg * span;
     const uint64_t end = min(begin + span, rp);
     for (uint64_t base = begin + (uint64_t)threadIdx.x * EX_POS_PER_THREAD; base < end;
          base += (uint64_t)blockDim.x * EX_POS_PER_THREAD) {
+        uint32_t want = 0xFFFFu;
+        if (IDS) {
+            want = match16(*reinterpret_cast<const uint4*>(X.ids + base), X.pass_id);
+            if (!want) continue;
+        }
         const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
         const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
         const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
@@ -1097,37 +1170,19 @@ __global__ __launch_bounds__(EX_THREADS) void k_extract(ExtractArgs X) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
         constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
-        uint32_t s = 0;
-        SeqMeta m{};
-        if (SCATTER && valid) {
-            s = X.blk2seq[base >> 6];
-            m = X.meta[s];
-        }
 #pragma unroll
         for (int t = 0; t < EX_POS_PER_THREAD; ++t) {
             if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
             const uint64_t p = base + t;
-            if (((valid >> t) & 0xFFu) == 0xFFu && p < end) {
+            const bool ok = IDS ? ((want >> t) & 1u) != 0 : ((valid >> t) & 0xFFu) == 0xFFu;
+            if (ok && p < end) {
                 const uint64_t h = mix43(k);
-                const uint32_t bucket = (uint32_t)(h >> rem_bits);
-                if (SCATTER) {
-                    while (p > m.pstart + m.len) m = X.meta[++s];  // valid windows never span a separator
-                    const uint32_t idx = atomicAdd(&s_cnt[bucket], 1u);
-                    const uint64_t o = X.owner_start[bucket >> b1_bits] + idx;
-                    uint64_t eh, el;
-                    make_elem(h & rem_mask, X.s_base + s, (uint32_t)(p - m.pstart), m, eh, el);
-                    X.out_hi[o] = eh;
-                    X.out_lo[o] = el;
-                } else {
-                    atomicAdd(&s_cnt[bucket], 1u);
-                }
+                atomicAdd(&s_cnt[(uint32_t)(h >> rem_bits) & (NB - 1)], 1u);
             }
         }
     }
-    if (!SCATTER) {
-        __syncthreads();
-        for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) X.hist[(uint64_t)wg * NB + b] = s_cnt[b];
-    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) X.hist[(uint64_t)wg * NB + b] = s_cnt[b];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1172,13 +1227,15 @@ __device__ __forceinline__ uint32_t stage_reserve(StageLds& L, uint32_t nd, unsi
     return tot;
 }
 
+template <bool IDS>
 __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, unsigned long long* __restrict__ cur0,
                                                                  uint64_t* __restrict__ out_hi,
                                                                  uint64_t* __restrict__ out_lo) {
     __shared__ StageLds L;
     const uint8_t* __restrict__ res = X.res;
     const int nbits = X.owner_bits + X.b1_bits;
-    const int rem_bits = KEY_BITS - nbits;
+    const uint32_t NB = 1u << nbits;
+    const int rem_bits = KEY_BITS - X.pass_bits - nbits;
     const uint64_t rem_mask = (1ull << rem_bits) - 1;
     const int l0_shift = nbits - SC_L0_BITS;
     const uint64_t begin = (uint64_t)blockIdx.x * X.span;
@@ -1186,12 +1243,18 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
     // the next round's residues and sequence record are loaded before this round's LDS work, so
     // their HBM latency (blk2seq -> meta is a dependent pair) overlaps the staging
     uint2 nv0 = make_uint2(0u, 0u), nv1 = make_uint2(0u, 0u);
-    uint32_t ns = 0;
+    uint32_t ns = 0, nwant = 0;
     SeqMeta nm{};
     auto fetch = [&](uint64_t b) {
         const uint64_t q = b + (uint64_t)threadIdx.x * SC_POS;
         nv0 = nv1 = make_uint2(0u, 0u);
+        nwant = 0;
         if (q < end) {  // the residue buffer is padded by 64 bytes past rp, not more
+            if (IDS) {
+                const uint2 id = *reinterpret_cast<const uint2*>(X.ids + q);
+                nwant = match16(make_uint4(id.x, id.y, 0xFFFFFFFFu, 0xFFFFFFFFu), X.pass_id) & 0xFFu;
+                if (!nwant) return;
+            }
             nv0 = *reinterpret_cast<const uint2*>(res + q);
             nv1 = *reinterpret_cast<const uint2*>(res + q + 8);
             ns = X.blk2seq[q >> 6];
@@ -1205,6 +1268,7 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
         const uint64_t p0 = base + (uint64_t)threadIdx.x * SC_POS;
         const uint2 v0 = nv0, v1 = nv1;
         uint32_t s = ns;
+        const uint32_t want = nwant;
         SeqMeta m = nm;
         if (base + SC_ROUND < end) fetch(base + SC_ROUND);
         const uint32_t w[4] = {v0.x, v0.y, v1.x, v1.y};
@@ -1229,10 +1293,11 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
             const uint64_t p = p0 + t;
             eh[t] = el[t] = 0;
             rk[t] = l0[t] = 0;
-            if (((valid >> t) & 0xFFu) == 0xFFu && p < end) {
+            const bool okw = IDS ? ((want >> t) & 1u) != 0 : ((valid >> t) & 0xFFu) == 0xFFu;
+            if (okw && p < end) {
                 while (p > m.pstart + m.len) m = X.meta[++s];  // valid windows never span a separator
                 const uint64_t h = mix43(k);
-                const uint32_t bucket = (uint32_t)(h >> rem_bits);
+                const uint32_t bucket = (uint32_t)(h >> rem_bits) & (NB - 1);
                 make_elem(h & rem_mask, X.s_base + s, (uint32_t)(p - m.pstart), m, eh[t], el[t]);
                 el[t] = (el[t] & ~0xFFFFull) | bucket;  // bucket id rides in the offset field until pass 2
                 l0[t] = bucket >> l0_shift;
@@ -2704,6 +2769,22 @@ __global__ void k_count_flags(const uint8_t* __restrict__ flags, uint32_t nseq, 
     if ((threadIdx.x & 63) == 0 && local) atomicAdd(out, (unsigned long long)local);
 }
 
+// Build options beyond skm_build_opts: the key-range pass count and device-memory budget
+// (skm_build_set_option), and diagnostic tunables kept at their tuned defaults in production.
+struct Tune {
+    int passes = 0;                  // key-range passes: 0 = automatic from the memory budget
+    int64_t mem_budget_mb = 0;       // device memory the build may plan for (0 = free memory)
+    int ovf_heavy = 8192;            // overflow sub-buckets >= this many elements go to stream 2
+    int ovf_inline_min = 0x7FFFFFFF; // overflow chains of >= this many samples run inline
+    int inline_prio = 3;
+    int ovf_long_class = 14;
+    int ovf_chain_wgs = 0;
+    int chain_prio = 0;
+    int bucket_prio = 0;
+    int chain_lds_kb = 0;
+    int host_timing = 0;
+};
+
 }  // namespace skm
 
 // ==========================================================================================
@@ -2797,6 +2878,20 @@ struct skm_build {
     uint64_t jobs2_cap = 0;
     ChainSet cs_main, cs_ovf, cs_ovf3;
     uint32_t n_ovf_heavy = 0;
+
+    // key-range passes (out-of-core build): P = 2^pass_bits passes over disjoint k-mer ranges
+    int pass_bits = 0;
+    uint64_t pass_max = 0;              // valid windows of the largest pass (this shard)
+    uint64_t valid_total = 0;           // valid windows of this shard
+    DevBuf d_ids;                       // per-window pass id (pass_bits > 0)
+    uint64_t kept_cap = 0;              // kept k-mer arena (keys + records), shared by all passes
+    hipEvent_t ev_start = nullptr;
+    // run totals over the passes (counters(), timings)
+    struct Acc {
+        uint64_t novf, jobs, lens, ovf_elems, ovf_kept, big, big_kept, grouped;
+    } acc{};
+    float pass_ms[12] = {};
+    skm::Tune tune;
 };
 
 namespace {
@@ -2969,7 +3064,6 @@ void prepare_local(skm_build* b) {
     b->rp = rp;
     b->nseq = (uint32_t)b->h_meta.size();
     SKM_CHECK(b->h_meta.size() < (1ull << ELEM_S_BITS), SKM_E_ARG, "too many sequences in one build shard");
-    SKM_CHECK(b->n_windows < (1ull << 32), SKM_E_ARG, "more than 2^32 windows in one GPU shard");
     // upload
     b->d_res.ensure(rp + 64);
     SKM_HIP(hipMemsetAsync(b->d_res.p, 0, rp + 64, b->stream));
@@ -3000,15 +3094,62 @@ void prepare_local(skm_build* b) {
     b->d_bstart32.ensure(sizeof(uint32_t) * (NB + 1));
     b->d_bstart.ensure(sizeof(uint64_t) * (NB + 1));
     b->d_owner_start.ensure(sizeof(uint64_t) * 80);
-    const uint64_t W = b->n_windows;
-    b->d_recs_hi.ensure(8 * std::max<uint64_t>(W, 1));
-    b->d_recs_lo.ensure(8 * std::max<uint64_t>(W, 1));
     b->d_ctr.ensure(256);
     b->d_dfunc.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
     b->d_swf.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
 }
 
-// buffers sized by the number of elements this rank groups
+// Valid windows of this shard by the top 6 bits of mix43(key) (one scan), then the pass count:
+// the smallest power of two whose largest pass fits the 32-bit element indexing and whose
+// per-pass work buffers (~PASS_BYTES per element) leave room for the kept arena (18 B per kept
+// k-mer, accumulated over all passes).
+constexpr uint64_t PASS_BYTES = 104;   // recs 16 + tmp 16 + received 16 (world > 1) + chain lens/jobs ~10 + overflow scratch ~40
+void size_passes(skm_build* b) {
+    DevBuf d_cnt;
+    d_cnt.ensure(8 * 64);
+    SKM_HIP(hipMemsetAsync(d_cnt.p, 0, 8 * 64, b->stream));
+    if (b->rp)
+        hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 0, b->stream, b->d_res.as<uint8_t>(), b->rp, 0,
+                           nullptr, d_cnt.as<unsigned long long>());
+    SKM_HIP(hipGetLastError());
+    uint64_t cnt[64];
+    SKM_HIP(hipMemcpyAsync(cnt, d_cnt.p, sizeof(cnt), hipMemcpyDeviceToHost, b->stream));
+    SKM_HIP(hipStreamSynchronize(b->stream));
+    b->valid_total = 0;
+    for (int i = 0; i < 64; ++i) b->valid_total += cnt[i];
+    auto pass_max = [&](int pb) {
+        uint64_t m = 0;
+        const int per = 64 >> pb;
+        for (int p = 0; p < (1 << pb); ++p) {
+            uint64_t t = 0;
+            for (int i = 0; i < per; ++i) t += cnt[p * per + i];
+            m = std::max(m, t);
+        }
+        return m;
+    };
+    size_t fr = 0, tot = 0;
+    SKM_HIP(hipMemGetInfo(&fr, &tot));
+    const uint64_t budget = b->tune.mem_budget_mb > 0 ? (uint64_t)b->tune.mem_budget_mb << 20 : (uint64_t)fr;
+    int pb = 0;
+    if (b->tune.passes > 0) {
+        while ((1 << pb) < b->tune.passes) ++pb;
+    } else {
+        // up to a quarter of the elements may sit in one pass's received buffer after the
+        // exchange (skewed owners); 2^32 - 2^28 leaves the same slack for the 32-bit indexing
+        while (pb < 6) {
+            const uint64_t m = pass_max(pb);
+            const uint64_t work = m * PASS_BYTES + (pb ? b->rp : 0);
+            if (m < (1ull << 32) - (1ull << 28) && work <= budget / 2) break;
+            ++pb;
+        }
+    }
+    SKM_CHECK(pb <= 6, SKM_E_ARG, "key_range_passes must be a power of two <= 64");
+    b->pass_bits = pb;
+    b->pass_max = pass_max(pb);
+    SKM_CHECK(b->pass_max < (1ull << 32), SKM_E_ARG, "more than 2^32 occurrences in one pass of one GPU shard");
+}
+
+// buffers sized by the number of elements this rank groups in one pass
 void ensure_local(skm_build* b, uint64_t n) {
     if (n <= b->cap_local && b->cap_local) return;
     const uint64_t c = std::max<uint64_t>(n + n / 16, 1);
@@ -3018,9 +3159,11 @@ void ensure_local(skm_build* b, uint64_t n) {
     }
     b->d_tmp_hi.ensure(8 * c);
     b->d_tmp_lo.ensure(8 * c);
-
-    b->d_keys.ensure(8 * c);
-    b->d_data.ensure(sizeof(skm_stored_kmer_data) * c + 16);
+    if (b->pass_bits == 0) {  // one pass: the kept arena never holds more than its elements
+        b->d_keys.ensure(8 * c);
+        b->d_data.ensure(sizeof(skm_stored_kmer_data) * c + 16);
+        b->kept_cap = c;
+    }
     const uint32_t NB1 = 1u << b->b1_bits;
     b->ovf_cap = c / CAP + NB1 + 16;
     b->jobs_cap = c / 3 + 16;
@@ -3031,11 +3174,59 @@ void ensure_local(skm_build* b, uint64_t n) {
     b->cap_local = c;
 }
 
+// extract buffers (one pass of this shard), the pass-id bytes, and with passes the kept arena
+void size_local(skm_build* b) {
+    const uint64_t W = std::max<uint64_t>(b->pass_max, 1);
+    b->d_recs_hi.ensure(8 * W);
+    b->d_recs_lo.ensure(8 * W);
+    if (b->pass_bits > 0) {
+        b->d_ids.ensure(((b->rp + 15) & ~15ull) + 64);
+        SKM_HIP(hipMemsetAsync(b->d_ids.p, 0xFF, ((b->rp + 15) & ~15ull) + 64, b->stream));
+    }
+}
+
+void size_arena(skm_build* b) {
+    if (b->pass_bits == 0) return;
+    size_t fr = 0, tot = 0;
+    SKM_HIP(hipMemGetInfo(&fr, &tot));
+    // the pass work buffers beyond what is allocated now (tmp, chains, overflow scratch) come out
+    // of the same memory: keep ~PASS_BYTES - 32 per element of the largest pass in reserve
+    const uint64_t reserve = b->pass_max * (PASS_BYTES - 32) + (1ull << 30);
+    const uint64_t avail = fr > reserve ? fr - reserve : 0;
+    uint64_t cap = std::min<uint64_t>(b->valid_total + 16, avail / (8 + sizeof(skm_stored_kmer_data)));
+    if (b->tune.mem_budget_mb > 0) {
+        const uint64_t budget = (uint64_t)b->tune.mem_budget_mb << 20;
+        const uint64_t used = b->pass_max * PASS_BYTES + b->rp;
+        cap = std::min<uint64_t>(cap, budget > used ? (budget - used) / 18 : 0);
+    }
+    cap = std::max<uint64_t>(cap, b->pass_max + 16);
+    b->d_keys.ensure(8 * cap);
+    b->d_data.ensure(sizeof(skm_stored_kmer_data) * cap + 16);
+    b->kept_cap = cap;
+}
+
 void prepare(const Ranks& bs) {
     bool need = false;
     for (auto* b : bs) need |= !b->prepared;
     if (!need) return;
-    for (auto* b : bs) prepare_local(b);
+    for (auto* b : bs) {
+        prepare_local(b);
+        size_passes(b);
+    }
+    {   // every rank runs the same passes
+        std::vector<uint64_t> mine;
+        for (auto* b : bs) mine.push_back((uint64_t)b->pass_bits);
+        const std::vector<uint64_t> all = bs[0]->world > 1 ? allgather_u64(bs, mine) : mine;
+        uint64_t pb = 0;
+        for (auto v : all) pb = std::max(pb, v);
+        for (auto* b : bs) {
+            if ((uint64_t)b->pass_bits != pb) {
+                b->tune.passes = 1 << pb;
+                size_passes(b);
+            }
+            size_local(b);
+        }
+    }
     skm_build* b0 = bs[0];
     if (b0->world == 1) {
         b0->s_base = 0;
@@ -3044,7 +3235,7 @@ void prepare(const Ranks& bs) {
         std::vector<uint32_t> len(b0->nseq);
         for (uint32_t s = 0; s < b0->nseq; ++s) len[s] = b0->h_meta[s].len;
         if (b0->nseq) SKM_HIP(hipMemcpyAsync(b0->d_glen.p, len.data(), 4 * b0->nseq, hipMemcpyHostToDevice, b0->stream));
-        ensure_local(b0, b0->n_windows);
+        ensure_local(b0, b0->pass_max);
     } else {
         // global sequence numbering: ranks hold contiguous file ranges in rank order
         std::vector<uint64_t> mine;
@@ -3092,10 +3283,11 @@ void prepare(const Ranks& bs) {
             b->g_strict = true;
             for (uint64_t s = 1; s < tot; ++s)
                 if (b->g_seqid[s] <= b->g_seqid[s - 1]) b->g_strict = false;
-            ensure_local(b, b->n_windows);  // first guess; grown at run time if the exchange brings more
+            ensure_local(b, b->pass_max);  // first guess; grown at run time if the exchange brings more
         }
     }
     for (auto* b : bs) {
+        size_arena(b);
         b->d_flags.ensure(std::max<uint64_t>(b->n_total, 1));
         SKM_HIP(hipStreamSynchronize(b->stream));
         b->prepared = true;
@@ -3106,7 +3298,7 @@ void prepare(const Ranks& bs) {
 // ------------------------------------------------------------------------------------------
 // run: extract -> [exchange] -> group-by -> chains -> statistics [-> reductions]
 // ------------------------------------------------------------------------------------------
-void phase_extract(skm_build* b) {
+void phase_extract(skm_build* b, uint32_t pass) {
     hipStream_t st = b->stream;
     const int nbits = b->owner_bits + b->b1_bits;
     const uint32_t NB = 1u << nbits;
@@ -3120,6 +3312,9 @@ void phase_extract(skm_build* b) {
     X.span = b->span;
     X.owner_bits = b->owner_bits;
     X.b1_bits = b->b1_bits;
+    X.pass_bits = b->pass_bits;
+    X.pass_id = pass;
+    X.ids = b->pass_bits ? b->d_ids.as<uint8_t>() : nullptr;
     X.hist = b->d_hist.as<uint32_t>();
     X.offs = b->d_offs.as<uint32_t>();
     X.owner_start = b->d_owner_start.as<uint64_t>();
@@ -3128,7 +3323,10 @@ void phase_extract(skm_build* b) {
     X.s_base = b->s_base;
     X.out_hi = b->d_recs_hi.as<uint64_t>();
     X.out_lo = b->d_recs_lo.as<uint64_t>();
-    hipLaunchKernelGGL(k_extract<false>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, X);
+    if (b->pass_bits)
+        hipLaunchKernelGGL(k_extract<true>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, X);
+    else
+        hipLaunchKernelGGL(k_extract<false>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, X);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[1], st));
     // ---- 2. scan ----
@@ -3150,9 +3348,13 @@ void phase_extract(skm_build* b) {
     b->d_slices.ensure(4 * 80);
     hipLaunchKernelGGL(k_stage_init, dim3((NB + 255) / 256), dim3(256), 0, st, b->d_bstart.as<uint64_t>(), NB, l0_shift,
                        b->d_cur0.as<unsigned long long>(), b->d_cur1.as<unsigned long long>(), b->d_slices.as<uint32_t>());
-    hipLaunchKernelGGL(k_extract_stage, dim3(b->nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
-                       b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
-    const uint32_t nsl = (uint32_t)(ceil_div(b->n_windows, SC_SLICE) + (1u << SC_L0_BITS));
+    if (b->pass_bits)
+        hipLaunchKernelGGL(k_extract_stage<true>, dim3(b->nwg), dim3(EX_THREADS), 0, st, X,
+                           b->d_cur0.as<unsigned long long>(), b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
+    else
+        hipLaunchKernelGGL(k_extract_stage<false>, dim3(b->nwg), dim3(EX_THREADS), 0, st, X,
+                           b->d_cur0.as<unsigned long long>(), b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
+    const uint32_t nsl = (uint32_t)(ceil_div(b->pass_max, SC_SLICE) + (1u << SC_L0_BITS));
     hipLaunchKernelGGL(k_split_stage, dim3(nsl), dim3(EX_THREADS), 0, st, b->d_tmp_hi.as<uint64_t>(),
                        b->d_tmp_lo.as<uint64_t>(), b->d_bstart.as<uint64_t>(), nbits, b->d_slices.as<uint32_t>(),
                        b->d_cur1.as<unsigned long long>(), b->d_recs_hi.as<uint64_t>(), b->d_recs_lo.as<uint64_t>());
@@ -3245,14 +3447,8 @@ void exchange(const Ranks& bs) {
     alltoallv(bs, ex_lo);
 }
 
-// tuning knobs for experiments (defaults are the tuned values)
-int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v ? atoi(v) : dflt;
-}
-
 // job sort by length class (longest first) + the chain kernel, on stream st
-void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, const uint32_t* lens,
+void launch_chains(const Tune& tn, hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, const uint32_t* lens,
                    const uint32_t* recs32, const uint32_t* tmp32, const uint32_t* big32, skm_stored_kmer_data* out,
                    uint32_t long_class, unsigned long long* pin, hipStream_t st_short = nullptr,
                    hipEvent_t ev_sorted = nullptr, uint32_t max_wgs = 0) {
@@ -3273,7 +3469,7 @@ void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, c
     if (nlong) {
         // dynamic LDS reserves most of a CU's LDS for each long chain, so no group-by workgroup
         // shares its CU (the chain is issue-latency bound: one wave pair, one instruction at a time)
-        static const uint32_t lds = (uint32_t)env_int("SKM_CHAIN_LDS_KB", 0) * 1024u;
+        const uint32_t lds = (uint32_t)tn.chain_lds_kb * 1024u;
         static bool attr = false;
         if (lds > 65536 && !attr) {
             SKM_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_chain_long),
@@ -3281,7 +3477,7 @@ void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, c
             attr = true;
         }
         hipLaunchKernelGGL(k_chain_long, dim3((uint32_t)nlong), dim3(128), lds, st, cs.sorted.as<Job>(), nlong, lens,
-                           recs32, tmp32, big32, out, env_int("SKM_CHAIN_PRIO", 0));
+                           recs32, tmp32, big32, out, tn.chain_prio);
     }
     if (nj > nlong) {
         // the per-lane chains on their own stream (when given): they do not wait for the long ones
@@ -3302,20 +3498,20 @@ void launch_chains(hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, c
 // Group-by.  k_partition splits the oversized level-1 buckets; the overflow sub-buckets (the
 // heaviest k-mers and their long P^2 chains) then run on a second stream, concurrently with
 // k_bucket_process on the first.
-void phase_group(skm_build* b) {
+void phase_group(skm_build* b, uint32_t pass) {
     // host-side timeline (SKM_HOST_TIMING=1): where the host waits between launches
-    static const bool host_timing = getenv("SKM_HOST_TIMING") != nullptr;
+    const bool host_timing = b->tune.host_timing != 0;
     const auto t0 = std::chrono::steady_clock::now();
     double tm[8] = {0};
 #define T(i) \
     if (host_timing) tm[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count()
     hipStream_t st = b->stream, st2 = b->stream2;
-    const uint32_t F = b->opts.n_functions;
     const bool multi = b->world > 1;
     const uint32_t NB1 = 1u << b->b1_bits;
     SKM_HIP(hipEventRecord(b->ev[4], st));
-    SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 256, st));
-    SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->n_total ? b->n_total : 1, st));
+    // per-pass counters; [0] (kept k-mers: the arena cursor) and the signature flags run over
+    // all passes (begin_run clears them)
+    SKM_HIP(hipMemsetAsync(b->d_ctr.as<unsigned long long>() + 1, 0, 256 - 8, st));
     unsigned long long* ctr_d = b->d_ctr.as<unsigned long long>();
     BucketArgs A;
     A.recs_hi = multi ? b->d_rhi.as<uint64_t>() : b->d_recs_hi.as<uint64_t>();
@@ -3331,8 +3527,8 @@ void phase_group(skm_build* b) {
     A.kept_ctr = ctr_d;
 
     A.nbuckets = NB1;
-    A.bucket_base = (uint32_t)b->rank << b->b1_bits;
-    A.rem_bits = KEY_BITS - b->owner_bits - b->b1_bits;
+    A.bucket_base = (pass << (b->owner_bits + b->b1_bits)) | ((uint32_t)b->rank << b->b1_bits);
+    A.rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
     A.glen = b->d_glen.as<uint32_t>();
     A.flags = b->d_flags.as<uint8_t>();
     A.ctr = ctr_d;
@@ -3342,7 +3538,7 @@ void phase_group(skm_build* b) {
     A.lens = b->d_lens.as<uint32_t>();
     A.ovf = b->d_ovf.as<OvfEntry>();
     A.ovf_cap = (uint32_t)b->ovf_cap;
-    A.prio = env_int("SKM_BUCKET_PRIO", 0);
+    A.prio = b->tune.bucket_prio;
     A.stamps = nullptr;
     if (b->stamps) {
         b->d_stamps.ensure(32 * 8);
@@ -3361,6 +3557,8 @@ void phase_group(skm_build* b) {
     SKM_HIP(hipStreamSynchronize(st));
     T(1);
     if (!multi) b->n_local = ctr[16];
+    SKM_CHECK(ctr[0] + b->n_local <= b->kept_cap, SKM_E_OOM,
+              "kept k-mer arena exhausted (raise the device memory budget or the key-range passes)");
     const uint32_t novf = (uint32_t)(ctr[1] & 0xFFFFFFFFull);
     SKM_CHECK(novf <= b->ovf_cap, SKM_E_OOM, "overflow list capacity exceeded");
     b->n_overflow = novf;
@@ -3377,7 +3575,7 @@ void phase_group(skm_build* b) {
         SKM_HIP(hipMemcpyAsync(ov, b->d_ovf.p, sizeof(OvfEntry) * novf, hipMemcpyDeviceToHost, st));
         SKM_HIP(hipStreamSynchronize(st));
         std::sort(ov, ov + novf, [](const OvfEntry& x, const OvfEntry& y) { return x.n > y.n; });
-        const uint32_t heavy_min = (uint32_t)env_int("SKM_OVF_HEAVY", 8192);
+        const uint32_t heavy_min = (uint32_t)b->tune.ovf_heavy;
         uint64_t tot = 0;
         for (uint32_t q = 0; q < novf; ++q) {
             OvfEntry& e = ov[q];
@@ -3415,15 +3613,14 @@ void phase_group(skm_build* b) {
         A3.jobs = A2.jobs;
         A3.lens = A2.lens;
         A3.ovf = A2.ovf + nheavy;
-        const uint32_t inline_min = (uint32_t)env_int("SKM_OVF_INLINE_MIN", 0x7FFFFFFF);
-        const int prio = env_int("SKM_INLINE_PRIO", 3);
-        static const bool dbg_no_ovf = env_int("SKM_DBG_SKIP_OVERFLOW", 0) != 0;  // timing experiments only
+        const uint32_t inline_min = (uint32_t)b->tune.ovf_inline_min;
+        const int prio = b->tune.inline_prio;
         SKM_HIP(hipEventRecord(b->ev_o[0], st2));
-        if (nheavy && !dbg_no_ovf)
+        if (nheavy)
             hipLaunchKernelGGL(k_overflow, dim3(nheavy), dim3(BP_THREADS), 0, st2, A2, S, inline_min, prio);
         SKM_HIP(hipEventRecord(b->ev_o[1], st2));
         SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
-        if (novf > nheavy && !dbg_no_ovf)
+        if (novf > nheavy)
             hipLaunchKernelGGL(k_overflow, dim3(novf - nheavy), dim3(BP_THREADS), 0, st3, A3, S, inline_min, prio);
         SKM_HIP(hipGetLastError());
     }
@@ -3468,9 +3665,8 @@ void phase_group(skm_build* b) {
         SKM_HIP(hipStreamSynchronize(st2));
         SKM_CHECK(ctr[32 + 3] <= b->jobs2_cap && ctr[32 + 4] <= b->lens_cap, SKM_E_OOM,
                   "overflow chain buffers overflowed");
-        launch_chains(st2, A2.jobs, ctr[32 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, nullptr, A.out_data,
-                      (uint32_t)env_int("SKM_OVF_LONG_CLASS", 14), ctr + 21, st3, b->ev_o3[2],
-                      (uint32_t)env_int("SKM_OVF_CHAIN_WGS", 0));
+        launch_chains(b->tune, st2, A2.jobs, ctr[32 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, nullptr, A.out_data,
+                      (uint32_t)b->tune.ovf_long_class, ctr + 21, st3, b->ev_o3[2], (uint32_t)b->tune.ovf_chain_wgs);
         SKM_HIP(hipEventRecord(b->ev_o[2], st2));
         SKM_HIP(hipEventRecord(b->ev_o3[1], st3));
         b->n_jobs += ctr[32 + 3];
@@ -3484,7 +3680,7 @@ void phase_group(skm_build* b) {
     SKM_CHECK(ctr[5] <= b->big_cap, SKM_E_OOM, "big-group descriptor capacity exceeded");
     b->n_big = ctr[5];
     b->big_kept = ctr[6];
-    launch_chains(st, A.jobs, ctr[3], b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
+    launch_chains(b->tune, st, A.jobs, ctr[3], b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
                   reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, LONG_CLASS, ctr + 20);
     b->n_jobs += ctr[3];
     if (novf) {
@@ -3494,10 +3690,65 @@ void phase_group(skm_build* b) {
     SKM_HIP(hipEventRecord(b->ev[6], st));
     SKM_HIP(hipEventRecord(b->ev[7], st));
     T(5);
-    // ---- 7. per-rank statistics ----
+    // ---- 7. the arena cursor after this pass ----
     SKM_HIP(hipMemcpyAsync(ctr + 17, ctr_d, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
     b->n_kept = ctr[17];
+    T(6);
+    if (host_timing)
+        fprintf(stderr, "host ms: part %.3f ovf-read %.3f launches %.3f ovf-chains %.3f main-chains %.3f stats %.3f end %.3f\n",
+                tm[0], tm[1], tm[2], tm[3], tm[4], tm[5], tm[6]);
+#undef T
+}
+
+// run start: arena cursor, signature flags, accumulators; the pass ids (one residue scan)
+void begin_run(skm_build* b) {
+    hipStream_t st = b->stream;
+    SKM_HIP(hipEventRecord(b->ev_start, st));
+    SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 256, st));
+    SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->n_total ? b->n_total : 1, st));
+    if (b->pass_bits && b->rp)
+        hipLaunchKernelGGL(k_pass_ids, dim3(4096), dim3(256), 0, st, b->d_res.as<uint8_t>(), b->rp, b->pass_bits,
+                           b->d_ids.as<uint8_t>(), nullptr);
+    SKM_HIP(hipGetLastError());
+    b->acc = skm_build::Acc{};
+    std::memset(b->pass_ms, 0, sizeof(b->pass_ms));
+    b->n_kept = 0;
+}
+
+// after a pass's group phase (its events have completed): totals and phase times
+void end_pass(skm_build* b) {
+    auto& a = b->acc;
+    a.novf += b->n_overflow;
+    a.jobs += b->n_jobs;
+    a.lens += b->n_lens;
+    a.ovf_elems += b->ovf_elems;
+    a.ovf_kept += b->ovf_kept;
+    a.big += b->n_big;
+    a.big_kept += b->big_kept;
+    a.grouped += b->n_local;
+    // [0] extract-count [1] scan [2] extract-scatter [3] bucket [5] chains [8] exchange
+    // [9] partition [10] group-by kernel [11] big groups; [4] overflow (own streams)
+    const int idx[9] = {0, 1, 2, 3, 5, 8, 9, 10, 11};
+    const int from[9] = {0, 1, 2, 4, 12, 3, 4, 11, 5}, to[9] = {1, 2, 3, 12, 6, 4, 10, 5, 12};
+    for (int i = 0; i < 9; ++i) {
+        float t = 0.f;
+        SKM_HIP(hipEventElapsedTime(&t, b->ev[from[i]], b->ev[to[i]]));
+        b->pass_ms[idx[i]] += t;
+    }
+    if (b->n_overflow) {  // the overflow path end to end (both parts, their chains included)
+        float t2 = 0.f, t3 = 0.f;
+        SKM_HIP(hipEventElapsedTime(&t2, b->ev_o[0], b->ev_o[2]));
+        SKM_HIP(hipEventElapsedTime(&t3, b->ev_o[0], b->ev_o3[1]));
+        b->pass_ms[4] += std::max(t2, t3);
+    }
+}
+
+// per-rank statistics over the whole arena (distinct_functions) and the shard (seqs_with_func)
+void phase_stats(skm_build* b) {
+    hipStream_t st = b->stream;
+    const uint32_t F = b->opts.n_functions;
+    SKM_HIP(hipEventRecord(b->ev[7], st));
     SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     const size_t lds_f = F <= 16384 ? sizeof(uint32_t) * F : 0;
@@ -3508,11 +3759,6 @@ void phase_group(skm_build* b) {
         hipLaunchKernelGGL(k_func_hist_seqs, dim3(256), dim3(256), lds_f, st, b->d_meta.as<SeqMeta>(), b->nseq, F,
                            b->d_swf.as<uint32_t>());
     SKM_HIP(hipGetLastError());
-    T(6);
-    if (host_timing)
-        fprintf(stderr, "host ms: part %.3f ovf-read %.3f launches %.3f ovf-chains %.3f main-chains %.3f stats %.3f end %.3f\n",
-                tm[0], tm[1], tm[2], tm[3], tm[4], tm[5], tm[6]);
-#undef T
 }
 
 void phase_final(skm_build* b) {
@@ -3522,31 +3768,34 @@ void phase_final(skm_build* b) {
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[8], st));
     SKM_HIP(hipEventSynchronize(b->ev[8]));
-    // [0] extract-count [1] scan [2] extract-scatter [3] bucket [4] overflow [5] chains
-    // [6] stats (+ reductions) [7] total [8] exchange
-    // [4] overflow: its own kernel time on the second stream (it overlaps [3])
-    const int from[7] = {0, 1, 2, 4, 5, 12, 7}, to[7] = {1, 2, 3, 12, 6, 6, 8};
-    for (int i = 0; i < 7; ++i) SKM_HIP(hipEventElapsedTime(&b->last_ms[i], b->ev[from[i]], b->ev[to[i]]));
-    b->last_ms[4] = 0.f;
-    if (b->n_overflow) {  // the overflow path end to end (both parts, their chains included)
-        float t2 = 0.f, t3 = 0.f;
-        SKM_HIP(hipEventElapsedTime(&t2, b->ev_o[0], b->ev_o[2]));
-        SKM_HIP(hipEventElapsedTime(&t3, b->ev_o[0], b->ev_o3[1]));
-        b->last_ms[4] = std::max(t2, t3);
-    }
-    SKM_HIP(hipEventElapsedTime(&b->last_ms[7], b->ev[0], b->ev[8]));
-    SKM_HIP(hipEventElapsedTime(&b->last_ms[8], b->ev[3], b->ev[4]));
-    SKM_HIP(hipEventElapsedTime(&b->last_ms[9], b->ev[4], b->ev[10]));   // level-2 partition kernel
-    SKM_HIP(hipEventElapsedTime(&b->last_ms[10], b->ev[11], b->ev[5]));  // group-by kernel alone
-    SKM_HIP(hipEventElapsedTime(&b->last_ms[11], b->ev[5], b->ev[12]));  // big groups + append
+    for (int i = 0; i < 12; ++i) b->last_ms[i] = b->pass_ms[i];
+    SKM_HIP(hipEventElapsedTime(&b->last_ms[6], b->ev[7], b->ev[8]));      // stats (+ reductions)
+    SKM_HIP(hipEventElapsedTime(&b->last_ms[7], b->ev_start, b->ev[8]));   // whole run
+    // run totals for counters() / finish()
+    b->n_overflow = (uint32_t)b->acc.novf;
+    b->n_jobs = b->acc.jobs;
+    b->n_lens = b->acc.lens;
+    b->ovf_elems = b->acc.ovf_elems;
+    b->ovf_kept = b->acc.ovf_kept;
+    b->n_big = b->acc.big;
+    b->big_kept = b->acc.big_kept;
+    b->n_local = b->acc.grouped;
     b->ran = true;
 }
 
 void run_ranks(const Ranks& bs) {
     prepare(bs);
-    for (auto* b : bs) phase_extract(b);
-    if (bs[0]->world > 1) exchange(bs);
-    for (auto* b : bs) phase_group(b);
+    for (auto* b : bs) begin_run(b);
+    const uint32_t P = 1u << bs[0]->pass_bits;
+    for (uint32_t pass = 0; pass < P; ++pass) {
+        for (auto* b : bs) phase_extract(b, pass);
+        if (bs[0]->world > 1) exchange(bs);
+        for (auto* b : bs) {
+            phase_group(b, pass);
+            end_pass(b);
+        }
+    }
+    for (auto* b : bs) phase_stats(b);
     if (bs[0]->world > 1) {
         std::vector<void*> df, sw, fl;
         for (auto* b : bs) {
@@ -3592,6 +3841,7 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     SKM_HIP(hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking));
     SKM_HIP(hipStreamCreateWithFlags(&b->stream3, hipStreamNonBlocking));
     for (auto& e : b->ev) SKM_HIP(hipEventCreate(&e));
+    SKM_HIP(hipEventCreate(&b->ev_start));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_part, hipEventDisableTiming));
     for (auto& e : b->ev_o) SKM_HIP(hipEventCreate(&e));
     for (auto& e : b->ev_o3) SKM_HIP(hipEventCreate(&e));
@@ -3699,6 +3949,38 @@ int skm_build_set_comm(skm_build* b, const uint8_t id[128]) {
 #else
     throw Error(SKM_E_COMM, "libskm was built without RCCL");
 #endif
+    SKM_API_END
+}
+
+int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
+    SKM_API_BEGIN
+    SKM_CHECK(b && name, SKM_E_ARG, "null argument");
+    const std::string n(name);
+    Tune& t = b->tune;
+    if (n == "key_range_passes") {
+        SKM_CHECK(value >= 0 && value <= 64 && (value & (value - 1)) == 0, SKM_E_ARG,
+                  "key_range_passes must be 0 (automatic) or a power of two <= 64");
+        t.passes = (int)value;
+    } else if (n == "device_memory_budget_mb") {
+        SKM_CHECK(value >= 0, SKM_E_ARG, "device_memory_budget_mb must be >= 0");
+        t.mem_budget_mb = value;
+    } else {
+        int* f = n == "overflow_heavy_min" ? &t.ovf_heavy
+               : n == "overflow_inline_min" ? &t.ovf_inline_min
+               : n == "overflow_inline_prio" ? &t.inline_prio
+               : n == "overflow_long_class" ? &t.ovf_long_class
+               : n == "overflow_chain_wgs" ? &t.ovf_chain_wgs
+               : n == "chain_prio" ? &t.chain_prio
+               : n == "bucket_prio" ? &t.bucket_prio
+               : n == "chain_lds_kb" ? &t.chain_lds_kb
+               : n == "host_timing" ? &t.host_timing : nullptr;
+        SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
+        SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
+        if (n == "overflow_long_class") SKM_CHECK(value >= 1 && value < 32, SKM_E_ARG, "overflow_long_class in [1, 32)");
+        *f = (int)value;
+    }
+    b->prepared = false;  // pass geometry and buffers are re-planned on the next prepare/run
+    b->ran = false;
     SKM_API_END
 }
 
@@ -3975,6 +4257,7 @@ void skm_build_destroy(skm_build* b) {
     for (auto& e : b->ev_o3)
         if (e) (void)hipEventDestroy(e);
     if (b->ev_part) (void)hipEventDestroy(b->ev_part);
+    if (b->ev_start) (void)hipEventDestroy(b->ev_start);
     if (b->h_pin) (void)hipHostFree(b->h_pin);
     if (b->h_ovf) (void)hipHostFree(b->h_ovf);
     if (b->stream) (void)hipStreamDestroy(b->stream);

@@ -56,6 +56,19 @@ def test_oracle_reproduces_annot(annot):
         np.testing.assert_array_equal(calls.view(np.uint8).reshape(-1, 24), g[kc])
 
 
+def test_parallel_oracle_annotate_equals_single_thread(annot):
+    """annotate_par (the C2-scale GPU parity checker) is the single-thread restatement over
+    sequence ranges: the same CSR calls as the golden fixture, for several thread counts."""
+    g, (qr, qo, ql) = annot
+    funcs = list(g["functions"])
+    ob = oracle_ref.Bdz(g["mph"].tobytes())
+    hypo = funcs.index("hypothetical protein")
+    for t in (1, 3, 8):
+        off, calls = oracle_ref.annotate_par(ob, g["dat"].tobytes(), qr, qo, ql, t, hypo_index=hypo)
+        np.testing.assert_array_equal(off, g["call_off"])
+        np.testing.assert_array_equal(calls.view(np.uint8).reshape(-1, 24), g["calls"])
+
+
 def test_host_mph_build_reproduces_golden_image(skm, annot, tmp_path):
     g, _ = annot
     keys = g["db_keys"]

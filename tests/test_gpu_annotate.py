@@ -37,6 +37,30 @@ def test_lookup_members_and_strangers(skm, gpu, tmp_path):
     np.testing.assert_array_equal(d[idx], ref["data"])
 
 
+@pytest.mark.parametrize("n", [1, 2, 41, 42, 43, 127, 128, 129, 1000, 4099, 65537])
+def test_pair_line_lookup_matches_bdz_search(skm, gpu, tmp_path, n):
+    """The b = 7 (g word, rank) pair-line search (bdz7_lookup: skm_db_lookup, k_lookup<0>, the
+    matrix hits) equals cmph bdz_search (oracle) and the generic device walk, per key, for members
+    and strangers.  Key counts put the last vertex block anywhere from one pair to a full line
+    (the padded final block); 400K strangers hit every vertex of these hashes, so every pair,
+    word and 128-vertex line boundary is exercised."""
+    rng = np.random.default_rng(1000 + n)
+    keys = np.unique(rng.integers(1, 2**63, size=n, dtype=np.uint64))
+    data = np.zeros(len(keys), skm.STORED_DTYPE)
+    data["function_index"] = np.arange(len(keys)) % 4000
+    base = str(tmp_path / "kmer_data")
+    skm.mph_build(keys, data, base + ".mph", base + ".dat", seed=7)
+    ob = oracle_ref.Bdz(open(base + ".mph", "rb").read())
+    db = skm.CmphKmerDb(base)
+    strangers = rng.integers(0, 2**64 - 1, size=400000, dtype=np.uint64)
+    for q in (keys, strangers):
+        want = ob.search(q)
+        np.testing.assert_array_equal(db.lookup_keys(q), want)
+        np.testing.assert_array_equal(db.lookup_keys_generic(q), want)
+    assert np.array_equal(np.sort(db.lookup_keys(keys)), np.arange(len(keys), dtype=np.uint32))
+    db.close()
+
+
 @pytest.mark.parametrize("ignore_hypo", [0, 1])
 def test_calls_match_oracle(skm, gpu, tmp_path, ignore_hypo):
     ref, funcs, mph, dat, _ = make_db(skm, tmp_path)

@@ -11,8 +11,10 @@ from signature_kmers_amd import synth
 pytestmark = pytest.mark.gpu
 
 
-def run_both(skm, residues, seq_off, seq_len, seq_func, seq_id, nf):
+def run_both(skm, residues, seq_off, seq_len, seq_func, seq_id, nf, options=None):
     b = skm.SignatureBuilder(nf)
+    for k, v in (options or {}).items():
+        b.set_option(k, v)
     b.add_batch(residues, seq_off, seq_len, seq_func, seq_id)
     got = b.finish()
     b.close()
@@ -71,14 +73,56 @@ def test_level2_partition_and_overflow(skm, gpu):
     assert_same(got, ref)
 
 
-@pytest.mark.parametrize("inline_min", ["16", "1000000000"])
-def test_overflow_inline_chains(skm, gpu, monkeypatch, inline_min):
+@pytest.mark.parametrize("inline_min", [16, 1000000000])
+def test_overflow_inline_chains(skm, gpu, inline_min):
     # every overflow chain of >= 16 samples inline in k_overflow (wave-pair chain code, up to
     # OVF_INLINE_CAP per workgroup, the rest as jobs) -- and none inline
-    monkeypatch.setenv("SKM_OVF_INLINE_MIN", inline_min)
     p = synth.generate_arrays(60000, 60, per_file=2000, seed=4)
     r, o, l, f, i, funcs = synth.build_inputs(p)
-    got, ref = run_both(skm, r, o, l, f, i, len(funcs))
+    got, ref = run_both(skm, r, o, l, f, i, len(funcs), {"overflow_inline_min": inline_min})
+    assert_same(got, ref)
+
+
+@pytest.mark.parametrize("passes", [2, 4, 64])
+def test_key_range_passes(skm, gpu, passes):
+    """Out-of-core build: P passes over disjoint k-mer ranges (each k-mer in exactly one pass)
+    give the single-pass result bit for bit, overflow sub-buckets and chains included, and a
+    second run over the same handle repeats it (arena cursor, flags and counters reset)."""
+    p = synth.generate_arrays(60000, 60, per_file=2000, seed=6)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    ref = oracle_ref.build(r, o, l, f, i, len(funcs))
+    b = skm.SignatureBuilder(len(funcs))
+    b.set_option("key_range_passes", passes)
+    b.add_batch(r, o, l, f, i)
+    b.run()
+    c1 = b.counters()
+    b.run()
+    assert b.counters() == c1
+    got = b.finish()
+    b.close()
+    assert_same(got, ref)
+    assert c1["overflow_subbuckets"] > 0 and c1["grouped"] == oracle_ref.count_windows(l, f) - _invalid(r, o, l, f)
+
+
+def _invalid(r, o, l, f):
+    ok = np.zeros(256, bool)
+    ok[np.frombuffer(b"ACDEFGHIKLMNPQRSTVWYacdefghiklmnpqrstvwy", np.uint8)] = True
+    good = ok[r].astype(np.int64)
+    c = np.concatenate([[0], np.cumsum(good)])
+    bad = 0
+    for s0, ln, fn in zip(o.astype(np.int64), l.astype(np.int64), f):
+        if fn == 0xFFFF or ln < 8:
+            continue
+        bad += int(((c[s0 + 8:s0 + ln + 1] - c[s0:s0 + ln - 7]) != 8).sum())
+    return bad
+
+
+def test_automatic_passes_from_memory_budget(skm, gpu):
+    """A device-memory budget too small for one pass makes the build plan several passes by
+    itself (the 50M-proteome path on one GPU), with the same result."""
+    p = synth.generate_arrays(20000, 40, per_file=1000, seed=7)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    got, ref = run_both(skm, r, o, l, f, i, len(funcs), {"device_memory_budget_mb": 600})
     assert_same(got, ref)
 
 

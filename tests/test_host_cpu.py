@@ -147,3 +147,41 @@ def test_write_dirs_layout(tmp_path):
     txt = (tmp_path / "Seqs" / seqs[0]).read_text()
     assert txt.startswith(">fig|") and all(len(x) <= 60 for x in txt.splitlines() if not x.startswith(">"))
     assert isinstance(info, dict)
+
+
+def _bdz_image(skm, tmp_path, n=1000):
+    rng = np.random.default_rng(5)
+    keys = np.unique(rng.integers(1, 2**63, size=n, dtype=np.uint64))
+    data = np.zeros(len(keys), skm.STORED_DTYPE)
+    base = str(tmp_path / "kmer_data")
+    skm.mph_build(keys, data, base + ".mph", base + ".dat", seed=1)  # host construction
+    return bytearray(open(base + ".mph", "rb").read()), open(base + ".dat", "rb").read()
+
+
+def test_malformed_bdz_images_are_rejected_before_any_device_use(skm, tmp_path):
+    """bdz_parse bounds every index the searches use: n = 3r (64-bit), m <= n, b < 32,
+    k = 2^b, ranktablesize >= ceil(n/k).  A bad image fails with the parse error; a good one
+    gets past parsing (and then fails only for want of a device here)."""
+    import ctypes as C
+    lib = skm.lib()
+    img, dat = _bdz_image(skm, tmp_path)
+    n = int.from_bytes(img[24:28], "little")
+    koff = 36 + (n + 3) // 4
+
+    def open_err(buf):
+        h = C.c_void_p()
+        b = bytes(buf)
+        rc = lib.skm_db_open_mem(C.byref(h), b, len(b), dat, len(dat), 0)
+        return rc, lib.skm_last_error().decode()
+
+    rc, msg = open_err(img)
+    assert "kmer_data.mph" not in msg  # parsed fine; any failure here is the missing device
+    bad = []
+    x = bytearray(img); x[32:36] = (0x55555556).to_bytes(4, "little"); bad.append(x)   # 3r wraps to n in u32
+    x = bytearray(img); x[koff + 4] = 40; bad.append(x)                                # b >= 32
+    x = bytearray(img); x[koff:koff + 4] = (64).to_bytes(4, "little"); bad.append(x)    # k != 2^b
+    x = bytearray(img); x[koff + 5:koff + 9] = (1).to_bytes(4, "little"); bad.append(x[:koff + 13])  # short rank table
+    x = bytearray(img); x[4:8] = (n + 1).to_bytes(4, "little"); x[28:32] = (n + 1).to_bytes(4, "little"); bad.append(x)  # m > n
+    for b in bad:
+        rc, msg = open_err(b)
+        assert rc != 0 and "kmer_data.mph" in msg, msg
