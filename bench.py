@@ -2,15 +2,24 @@
 """bench.py -- signature-k-mer build throughput on MI355X (BASELINE.json metric).
 
 Metric: k-mers/sec (windows examined by extract+hash+count+cut), whole job over N GPUs.
-Workload at N=1: BASELINE configs[1] -- 1M synthetic protein sequences, k=8, signature build on
-one MI355X (SURVEY.md 8(d) generator, seed 20241115).  At N>1 (weak scaling) rank r holds the
-r-th contiguous range of files of an N x 1M proteome and the ranks run ONE build over the union:
-occurrence elements go to the owner GPU of their k-mer with an RCCL all-to-all over xGMI, then
-per-function counts and signature flags are all-reduced.
 
-One step = one full device pass of the build pipeline over the HBM-resident input
-(extract/count, scan, extract/scatter, bucket group-by + cut + statistics, overflow, stats).
-Inputs are uploaded before the timed region; outputs stay on the device.
+Headline workload (north_star / BASELINE configs[2], strong scaling): the 50M-protein synthetic
+proteome (SURVEY.md 8(d) generator, seed 20241115, 4,000 families, 12,500 genome files of 4,000
+proteins) built on N GPUs of one node.  Rank r holds the r-th contiguous range of files; the
+ranks run ONE build over the union: each key-range pass extracts the rank's occurrences of that
+pass's k-mer range, sends them to the k-mer's owner GPU (RCCL all-to-all over xGMI), groups
+and cuts them there; per-function counts and signature flags are all-reduced at the end
+(SURVEY.md 8(e)).  On one GPU the 16.2 G occurrences exceed HBM, so the build runs as key-range
+passes over the resident residues (include/skm.h skm_build_set_option "key_range_passes").
+
+One step = one full device pass of the build over the HBM-resident input (pass ids, per pass:
+extract/count, scan, extract/scatter, [exchange], partition, group-by + cut + statistics,
+overflow, chains; then statistics and reductions).  Inputs are uploaded before the timed region;
+outputs stay on the device.
+
+Secondary lines (same JSON object): "weak" = C2 (1M proteins per GPU; configs[1] at N=1) with its
+own roofline; at N=1 also the annotate leg (configs[3]: 10M queries vs the C2 DB in HBM) and the
+matrix-distance leg (configs[4]).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]   (N>1 under torch.distributed.run)
 """
@@ -28,6 +37,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
+PER_FILE = 4000
+C2_SEQS = 1_000_000
 
 
 def parse():
@@ -35,20 +46,76 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--seqs", type=int, default=1_000_000, help="sequences per GPU")
+    ap.add_argument("--seqs-total", type=int, default=50_000_000,
+                    help="proteins of the headline proteome, split over the GPUs (strong scaling)")
     ap.add_argument("--families", type=int, default=4000)
-    ap.add_argument("--cpu-sample-seqs", type=int, default=1_000_000,
-                    help="sequences of the workload the CPU baseline builds (default: all of C2)")
-    ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="host threads of the CPU baseline (0: OMP_NUM_THREADS, else min(16, cores))")
+    ap.add_argument("--weak-seqs", type=int, default=C2_SEQS,
+                    help="proteins per GPU of the secondary weak-scaling (C2) line; 0 = off")
+    ap.add_argument("--cpu-sample-seqs", type=int, default=C2_SEQS,
+                    help="sequences of the workload the CPU baseline builds (a bounded sample)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="host threads of the CPU baseline (0: all usable)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gen-workers", type=int, default=0, help="generator processes (0: usable cores)")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--annot-queries", type=int, default=2_000_000,
-                    help="annotate leg (BASELINE configs[3] at reduced query count; 0 = off; N=1 only)")
+    ap.add_argument("--annot-queries", type=int, default=10_000_000,
+                    help="annotate leg (BASELINE configs[3]); 0 = off; N=1 only")
     ap.add_argument("--matrix-seqs", type=int, default=100_000,
-                    help="matrix-distance leg (BASELINE configs[4]: all-vs-all over this many query "
-                         "sequences of 200 families; 0 = off; N=1 only)")
+                    help="matrix-distance leg (BASELINE configs[4]); 0 = off; N=1 only")
     return ap.parse_args()
+
+
+def host_cores() -> dict:
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota when one is
+    set (the GPU boxes give each job a 16-CPU quota on a larger machine), plus the CPU model."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) // int(p)
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = min(aff, quota) if quota else aff
+    return {"usable": max(1, usable), "affinity": aff, "cgroup_quota": quota, "model": model}
+
+
+def _windows(lens) -> int:
+    return int(np.where(lens >= 8, lens.astype(np.int64) - 7, 0).sum())
+
+
+class Shard:
+    """Per-file generator output of one rank (SURVEY 8(d) arrays, file order)."""
+
+    def __init__(self, parts):
+        self.parts = parts
+        self.n_seqs = sum(len(p[2]) for p in parts)
+        self.n_windows = sum(_windows(p[2]) for p in parts)
+        self.n_residues = sum(len(p[0]) for p in parts)
+
+    def add_to(self, b):
+        for r, o, l, f, i in self.parts:
+            b.add_batch(r, o, l, f, i)
+
+    def packed(self, first_files=None):
+        ps = self.parts if first_files is None else self.parts[:first_files]
+        r = np.concatenate([p[0] for p in ps])
+        lens = np.concatenate([p[2] for p in ps])
+        off = np.zeros(len(lens), np.uint64)
+        if len(lens):
+            off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        return (r, off, lens, np.concatenate([p[3] for p in ps]), np.concatenate([p[4] for p in ps]))
+
+
+def gen(synth, n_total, families, first_file, n_files, workers):
+    return Shard(list(synth.iter_file_inputs(n_total, families, PER_FILE, first_file, n_files, workers=workers)))
 
 
 def main():
@@ -57,120 +124,122 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    import signature_kmers_amd as skm
-    from signature_kmers_amd import synth
-    uid = None
+    cores = host_cores()
+    workers = a.gen_workers or min(16, cores["usable"])
     if world > 1:
         import torch.distributed as dist  # gloo: rendezvous, barrier, max over ranks (host side)
         dist.init_process_group("gloo")
+        workers = max(1, workers // min(world, 8))
+    from signature_kmers_amd import synth
+
+    # ---- every input this rank needs, generated BEFORE any GPU call (the pool spawns processes) ----
+    t0 = time.time()
+    files_total = (a.seqs_total + PER_FILE - 1) // PER_FILE
+    f0, f1 = rank * files_total // world, (rank + 1) * files_total // world
+    c3 = gen(synth, a.seqs_total, a.families, f0, f1 - f0, workers)
+    c2_files = (a.weak_seqs + PER_FILE - 1) // PER_FILE
+    if a.weak_seqs and f0 == rank * c2_files and f1 - f0 >= c2_files:
+        c2 = Shard(c3.parts[:c2_files])  # files [r*250, r*250+250): the same bytes as the weak shard
+    elif a.weak_seqs:
+        c2 = gen(synth, a.weak_seqs * world, a.families, rank * c2_files, c2_files, workers)
+    else:
+        c2 = None
+    queries = None
+    if world == 1 and a.annot_queries > 0:
+        nqf = (a.annot_queries + PER_FILE - 1) // PER_FILE
+        if c2_files + nqf <= len(c3.parts):  # files after the training set: fresh proteins, own RNG streams
+            queries = Shard(c3.parts[c2_files:c2_files + nqf])
+        else:
+            queries = gen(synth, (c2_files + nqf) * PER_FILE, a.families, c2_files, nqf, workers)
+    matrix_in = None
+    if world == 1 and a.matrix_seqs > 0:
+        fam, n_train = 200, 200_000
+        nfq = (a.matrix_seqs + PER_FILE - 1) // PER_FILE
+        tf = n_train // PER_FILE
+        matrix_in = (gen(synth, n_train, fam, 0, tf, workers), gen(synth, (tf + nfq) * PER_FILE, fam, tf, nfq, workers),
+                     synth.functions(fam))
+    funcs = synth.functions(a.families)
+    gen_s = time.time() - t0
+
+    import signature_kmers_amd as skm
+    ndev = max(1, skm.device_count())
+    device = local % ndev
+
+    def new_uid():
+        if world == 1:
+            return None
         box = [skm.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
-        uid = box[0]
+        return box[0]
 
-    # ---- synthetic shard (one RNG stream per file: shards are rank-independent) ----
-    per_file = 4000
-    files_per_rank = (a.seqs + per_file - 1) // per_file
+    # ---- headline: C3 strong scaling ----
+    uid = new_uid()
     t0 = time.time()
-    p = synth.generate_arrays(a.seqs * world, a.families, per_file=per_file, first_file=rank * files_per_rank,
-                              n_files=files_per_rank)
-    r, o, l, f, i, funcs = synth.build_inputs(p)
-    gen_s = time.time() - t0
-    n_windows = int(np.where((f != 0xFFFF) & (l >= 8), l.astype(np.int64) - 7, 0).sum())
-
-    ndev = max(1, skm.device_count())
-    b = skm.SignatureBuilder(len(funcs), device=local % ndev, rank=rank, world_size=world)
-    b.add_batch(r, o, l, f, i)
+    b = skm.SignatureBuilder(len(funcs), device=device, rank=rank, world_size=world)
+    c3.add_to(b)
     if uid is not None:
-        b.set_comm(uid)  # RCCL communicator over the world (data-path exchange)
+        b.set_comm(uid)
     b.prepare()
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    for _ in range(a.warmup):
-        b.run()
-    phase = {}
-    barrier()
-    t1 = time.perf_counter()
-    for _ in range(a.steps):
-        b.run()
-        for k, v in b.timings().items():
-            phase[k] = phase.get(k, 0.0) + v
-    t_local = time.perf_counter() - t1  # run() returns after its final event has completed
-    barrier()
-    t_max = t_local
-    if dist is not None:
-        import torch
-        tt = torch.tensor([t_local], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
-        nw = torch.tensor([n_windows], dtype=torch.float64)
-        dist.all_reduce(nw, op=dist.ReduceOp.SUM)
-        total_windows = float(nw.item())
-    else:
-        total_windows = float(n_windows)
-    ms_per_step = 1000.0 * t_max / a.steps
-    value = total_windows * a.steps / t_max
-    phase = {k: v / a.steps for k, v in phase.items()}
-
-    # ---- roofline: dominant kernel (bucket group-by) and the whole pipeline ----
-    res_bytes = int(len(r) + len(l))
-    valid = _valid_windows(r, o, l, f)          # occurrence elements this rank extracts
-    ctrs = b.counters()
-    grouped = ctrs["grouped"]                   # elements this rank groups (after the exchange)
-    n_kept = ctrs["kept"]                       # kept k-mers this rank owns
-    # dominant single kernel: k_bucket_process (group-by + cut + statistics of every sub-bucket
-    # that fits LDS).  Its algorithmic bytes: the 16-byte elements it reads once, the 18 bytes per
-    # k-mer it keeps; the overflow sub-buckets (k_overflow) and the k-mers of groups of > 64
-    # members (kept by k_big_groups) are excluded.
-    kernels = {"k_extract<false>": "extract_count", "k_partition": "partition", "k_bucket_process": "bucket_kernel"}
-    dom = max(kernels, key=lambda k: phase.get(kernels[k], 0.0))
-    alg = {
-        "k_extract<false>": res_bytes,
-        "k_partition": 32 * grouped,  # 16-byte elements read once and written once
-        "k_bucket_process": 16 * (grouped - ctrs["overflow_elements"])
-        + 18 * (n_kept - ctrs["overflow_kept"] - ctrs["big_kept"]),
-    }
-    dom_ms = phase[kernels[dom]]
-    achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
-    pipe_alg = res_bytes + 16 * valid + 16 * grouped + 18 * n_kept  # SURVEY 8(d) B_alg
-    pipe_gbs = pipe_alg / (phase["total"] * 1e-3) / 1e9
-    traffic = _pmc_traffic(dom, a.seqs)
-
+    prep_s = time.time() - t0
+    head = _measure(skm, b, a.steps, a.warmup, c3, world, dist)
+    b.close()
+    per_gpu = a.seqs_total // world
     out = {
         "metric": "k-mers/sec (extract+hash+count) at 1/2/4/8 GPUs; achieved HBM GB/s %",
-        "value": value,
+        "value": head["value"],
         "unit": "k-mers/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": ms_per_step,
+        "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (SURVEY 8(d) generator, seed 20241115)",
-        "config": {"workload": "C2: 1M protein seqs/GPU, k=8, signature build (extract+group+cut+stats)",
-                   "seqs_per_gpu": a.seqs, "families": a.families, "windows_per_gpu": n_windows,
-                   "valid_windows_per_gpu": valid, "kept_kmers_rank0": n_kept, "grouped_elements_rank0": grouped,
-                   "parallelism": "single GPU" if world == 1 else
-                   f"{world} GPUs, owner-partitioned RCCL all-to-all + all-reduce"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "alg_bytes_per_launch": alg[dom], "avg_launch_ms": dom_ms},
-        "pipeline": {"alg_bytes": pipe_alg, "ms": phase["total"], "GBs": pipe_gbs, "frac": pipe_gbs / HBM_PEAK_GBS,
-                     "phase_ms": phase},
+        "config": {"workload": f"C3: {a.seqs_total:,}-protein proteome, k=8, signature build "
+                               f"(extract+group+cut+stats), {world} GPU(s), ~{per_gpu:,} proteins per GPU",
+                   "seqs_total": a.seqs_total, "families": a.families, "windows_total": head["windows_total"],
+                   "windows_rank0": c3.n_windows, "key_range_passes": head["passes"],
+                   "kept_kmers_rank0": head["counters"]["kept"], "grouped_elements_rank0": head["counters"]["grouped"],
+                   "parallelism": "single GPU, key-range passes" if world == 1 else
+                   f"{world} GPUs, owner-partitioned RCCL all-to-all + all-reduce, per key-range pass"},
+        "roofline": head["roofline"],
+        "pipeline": head["pipeline"],
         "cpu_baseline": None,
         "gen_seconds": gen_s,
+        "prepare_seconds": prep_s,
     }
+    cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = _cpu_baseline(r, o, l, f, i, len(funcs), a.cpu_sample_seqs, a.cpu_threads)
-    if world == 1 and a.annot_queries > 0:
-        out["annotate"] = _annotate_leg(skm, synth, b, funcs, a, files_per_rank, local % ndev)
-    b.close()
-    if world == 1 and a.matrix_seqs > 0:
-        out["matrix"] = _matrix_leg(skm, synth, a, local % ndev)
+        cpu = _cpu_baseline(c3, len(funcs), a.cpu_sample_seqs, a.cpu_threads or cores["usable"], cores, a.seqs_total)
+        out["cpu_baseline"] = cpu
+
+    # ---- secondary: C2 per GPU (weak scaling; configs[1] at N=1) ----
+    kept = None
+    if c2 is not None:
+        uid = new_uid()
+        b = skm.SignatureBuilder(len(funcs), device=device, rank=rank, world_size=world)
+        c2.add_to(b)
+        if uid is not None:
+            b.set_comm(uid)
+        b.prepare()
+        weak = _measure(skm, b, a.steps, a.warmup, c2, world, dist)
+        out["weak"] = {"value": weak["value"], "unit": "k-mers/s", "ms_per_step": weak["ms_per_step"],
+                       "scaling": "weak",
+                       "config": {"workload": f"C2: {a.weak_seqs:,} proteins per GPU x {world}, k=8, signature build",
+                                  "windows_total": weak["windows_total"], "kept_kmers_rank0": weak["counters"]["kept"],
+                                  "key_range_passes": weak["passes"]},
+                       "roofline": weak["roofline"], "pipeline": weak["pipeline"],
+                       "cpu_baseline": cpu and dict(cpu, note="the same bounded sample: the first 1M proteins "
+                                                               "of the C3 proteome are the C2 workload")}
+        if world == 1 and queries is not None:
+            kept = b.finish()
+        b.close()
+    if world == 1 and queries is not None and kept is not None:
+        out["annotate"] = _annotate_leg(skm, kept, funcs, queries, a, device, cores)
+    if world == 1 and matrix_in is not None:
+        out["matrix"] = _matrix_leg(skm, matrix_in, a, device, cores)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
@@ -181,20 +250,77 @@ def main():
         dist.destroy_process_group()
 
 
-def _annotate_leg(skm, synth, b, funcs, a, files_train, device):
-    """kmers-call-functions path (BASELINE configs[3]): fresh query proteins of the same families
-    (files after the training set: their own RNG streams) against the CMPH/BDZ DB of this build,
-    resident in HBM.  One step = window lookup (k_lookup) + HitSet calls + compaction over every
-    query; the calls stay on the device.  Roofline: k_lookup, SURVEY 8(d) B_alg = 1 B/residue +
-    18 B/window (g bytes, rank word, record)."""
+def _measure(skm, b, steps, warmup, shard, world, dist):
+    """Warmup, then exactly `steps` timed runs bracketed by barriers; max over ranks."""
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(warmup):
+        b.run()
+    phase = {}
+    barrier()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        b.run()  # returns after the run's final event has completed (device synchronised)
+        for k, v in b.timings().items():
+            phase[k] = phase.get(k, 0.0) + v
+    t_local = time.perf_counter() - t1
+    barrier()
+    ctrs = b.counters()
+    t_max, windows_total = t_local, float(shard.n_windows)
+    sums = {"grouped": ctrs["grouped"], "kept": ctrs["kept"], "res": shard.n_residues + shard.n_seqs}
+    if dist is not None:
+        import torch
+        tt = torch.tensor([t_local], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+        v = torch.tensor([float(shard.n_windows), float(sums["grouped"]), float(sums["kept"]), float(sums["res"])],
+                         dtype=torch.float64)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        windows_total = float(v[0])
+        sums = {"grouped": int(v[1]), "kept": int(v[2]), "res": int(v[3])}
+    phase = {k: v / steps for k, v in phase.items()}
+    # dominant single kernel of this rank (summed over the passes of one step): its algorithmic
+    # bytes -- k_bucket_process: the 16-byte elements it groups + 18 B per k-mer it keeps (the
+    # overflow sub-buckets and the > 64-member groups excluded); k_partition: 32 B per element;
+    # k_extract: 1 B per residue
+    kernels = {"k_extract": "extract_count", "k_partition": "partition", "k_bucket_process": "bucket_kernel"}
+    dom = max(kernels, key=lambda k: phase.get(kernels[k], 0.0))
+    alg = {
+        "k_extract": (shard.n_residues + shard.n_seqs) * max(1, b.passes()),
+        "k_partition": 32 * ctrs["grouped"],
+        "k_bucket_process": 16 * (ctrs["grouped"] - ctrs["overflow_elements"])
+        + 18 * (ctrs["kept"] - ctrs["overflow_kept"] - ctrs["big_kept"]),
+    }
+    dom_ms = phase[kernels[dom]]
+    achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
+    # SURVEY 8(d) B_alg over the whole job: 1 B/residue + 32 B/valid window + 18 B/kept k-mer
+    pipe_alg = sums["res"] + 32 * sums["grouped"] + 18 * sums["kept"]
+    pipe_gbs = pipe_alg / (t_max / steps) / 1e9
+    return {
+        "value": windows_total * steps / t_max,
+        "ms_per_step": 1000.0 * t_max / steps,
+        "windows_total": int(windows_total),
+        "passes": b.passes(),
+        "counters": ctrs,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic(dom, shard.n_seqs),
+                     "alg_bytes_per_launch": alg[dom], "avg_launch_ms": dom_ms,
+                     "launches_per_step": b.passes()},
+        "pipeline": {"alg_bytes": pipe_alg, "ms": 1000.0 * t_max / steps, "GBs": pipe_gbs,
+                     "frac": pipe_gbs / HBM_PEAK_GBS / max(1, world), "phase_ms_rank0": phase},
+    }
+
+
+def _annotate_leg(skm, kept, funcs, q, a, device, cores):
+    """kmers-call-functions path (BASELINE configs[3]): 10M fresh query proteins of the same
+    families (genome files after the C2 training set: their own RNG streams) against the CMPH/BDZ
+    DB of the C2 build, resident in HBM.  One step = window lookup (k_lookup) + HitSet calls +
+    compaction over every query; the calls stay on the device.  Roofline: k_lookup<0>, SURVEY
+    8(d) B_alg = 1 B/residue + 18 B/window."""
     import tempfile
-    kept = b.finish()
-    t0 = time.time()
-    nq = a.annot_queries
-    per_file = 4000
-    p = synth.generate_arrays(a.seqs + nq, a.families, per_file=per_file, first_file=files_train,
-                              n_files=(nq + per_file - 1) // per_file)
-    gen_s = time.time() - t0
+    res, off, lens, _, _ = q.packed()
     with tempfile.TemporaryDirectory(dir="/tmp") as d:
         base = os.path.join(d, "kmer_data")
         t0 = time.time()
@@ -203,75 +329,71 @@ def _annotate_leg(skm, synth, b, funcs, a, files_train, device):
         db = skm.CmphKmerDb(base, device=device)
         files = None if a.no_cpu_baseline else (open(base + ".mph", "rb").read(), open(base + ".dat", "rb").read())
     hypo = funcs.index("hypothetical protein")
-    q = skm.QueryBatch(db, p.residues, p.seq_off, p.seq_len)
-    nwin = int(np.where(p.seq_len >= 8, p.seq_len.astype(np.int64) - 7, 0).sum())
+    qb = skm.QueryBatch(db, res, off, lens)
+    nwin = _windows(lens)
     for _ in range(max(1, a.warmup)):
-        q.run(hypo)
-    steps = max(3, a.steps)
+        qb.run(hypo)
+    steps = max(3, min(a.steps, 10))
     acc = {}
     t1 = time.perf_counter()
     for _ in range(steps):
-        q.run(hypo)
-        for k, v in q.timings().items():
+        qb.run(hypo)
+        for k, v in qb.timings().items():
             acc[k] = acc.get(k, 0.0) + v
     wall = time.perf_counter() - t1
     acc = {k: v / steps for k, v in acc.items()}
-    off, calls = q.calls()
-    q.close()
+    _, calls = qb.calls()
+    qb.close()
     db.close()
-    alg = int(len(p.residues)) + 18 * nwin
+    alg = int(len(res)) + 18 * nwin
     gbs = alg / (acc["lookup"] * 1e-3) / 1e9
     cpu = None
     if files is not None:  # the call path of the oracle on the host cores, bounded sample
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ref
-        threads = _cpu_threads(a.cpu_threads)
-        n = min(len(p.seq_len), 200_000)
-        end = int(p.seq_off[n - 1]) + int(p.seq_len[n - 1])
+        threads = a.cpu_threads or cores["usable"]
+        n = min(len(lens), 200_000)
+        end = int(off[n - 1]) + int(lens[n - 1])
         ob = oracle_ref.Bdz(files[0])
         t = time.perf_counter()
-        oracle_ref.annotate_mt(ob, files[1], p.residues[:end], p.seq_off[:n], p.seq_len[:n], threads, hypo_index=hypo)
+        oracle_ref.annotate_mt(ob, files[1], res[:end], off[:n], lens[:n], threads, hypo_index=hypo)
         dt = time.perf_counter() - t
-        w = int(np.where(p.seq_len[:n] >= 8, p.seq_len[:n].astype(np.int64) - 7, 0).sum())
+        w = _windows(lens[:n])
         cpu = {"value": w / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
+               "host": {k: cores[k] for k in ("model", "affinity", "cgroup_quota")},
                "sample": f"first {n} query proteins ({w} windows), {dt:.1f} s, oracle/skm_oracle.cpp "
                          f"oracle_annotate_mt (process_aa_seq per sequence) on {threads} host threads"}
         del ob, files
     return {"metric": "query k-mers/sec (window lookup + HitSet calls)", "value": nwin * steps / wall,
-            "unit": "k-mers/s", "ms_per_step": 1000.0 * wall / steps,
-            "config": {"workload": f"C4 at {nq} queries (configs[3] names 10M): fresh proteins of the same "
-                                   f"families vs the CMPH DB of this build in HBM", "queries": nq,
+            "unit": "k-mers/s", "ms_per_step": 1000.0 * wall / steps, "steps": steps,
+            "config": {"workload": f"C4: {len(lens):,} fresh query proteins of the same families vs the CMPH DB "
+                                   f"of the C2 build in HBM, 1 GPU", "queries": int(len(lens)),
                        "windows": nwin, "db_keys": int(len(kept.keys)), "calls": int(len(calls))},
             "phase_ms": acc,
             "roofline": {"bound": "hbm", "kernel": "k_lookup<0>", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
-                         "avg_launch_ms": acc["lookup"], "traffic": _pmc_traffic("k_lookup<0>", a.seqs)},
-            "cpu_baseline": cpu, "mph_build_s": mph_s, "query_gen_s": gen_s}
+                         "avg_launch_ms": acc["lookup"], "traffic": _pmc_traffic("k_lookup<0>", len(lens))},
+            "cpu_baseline": cpu, "mph_build_s": mph_s}
 
 
-def _matrix_leg(skm, synth, a, device):
+def _matrix_leg(skm, matrix_in, a, device, cores):
     """kmers-matrix-distance (BASELINE configs[4]): a 200-family signature DB (built on this GPU from
-    200K training proteins, BDZ on the GPU) resident in HBM, a fresh set of query proteins of the
-    same families, all-vs-all shared-signature-k-mer counts (one GPU computes every row).  One step =
+    200K training proteins, BDZ on the GPU) resident in HBM, 100K fresh query proteins of the same
+    families, all-vs-all shared-signature-k-mer counts (one GPU computes every row).  One step =
     window lookup + length filter, k-mer grouping (hash + radix sort), per-row LDS histograms of the
     pair increments, compaction of the nonzero pairs in row order; the pairs stay on the device.
     Roofline: k_md_rows (the pair increments), SURVEY 8(d) 4 B per pair increment."""
     import tempfile
-    fam, per_file, n_train = 200, 4000, 200_000
+    train, qs, funcs = matrix_in
     t0 = time.time()
-    p = synth.generate_arrays(n_train, fam, per_file=per_file)
-    r, o, l, f, i, funcs = synth.build_inputs(p)
     b = skm.SignatureBuilder(len(funcs), device=device)
-    b.add_batch(r, o, l, f, i)
+    train.add_to(b)
     kept = b.finish()
     b.close()
-    nq = a.matrix_seqs
-    f0 = n_train // per_file
-    nfq = (nq + per_file - 1) // per_file
-    q = synth.generate_arrays((f0 + nfq) * per_file, fam, per_file=per_file, first_file=f0, n_files=nfq)
-    n = min(nq, len(q.seq_len))
-    end = int(q.seq_off[n - 1]) + int(q.seq_len[n - 1])
-    res, off, ln = q.residues[:end], q.seq_off[:n], q.seq_len[:n]
+    res, off, ln, _, _ = qs.packed()
+    n = min(a.matrix_seqs, len(ln))
+    end = int(off[n - 1]) + int(ln[n - 1])
+    res, off, ln = res[:end], off[:n], ln[:n]
     with tempfile.TemporaryDirectory(dir="/tmp") as d:
         base = os.path.join(d, "kmer_data")
         skm.mph_build(kept.keys, kept.data, base + ".mph", base + ".dat", seed=1, device=device)
@@ -281,7 +403,7 @@ def _matrix_leg(skm, synth, a, device):
     md = skm.MatrixDistance(db, funcs, res, off, ln)
     for _ in range(max(1, a.warmup)):
         md.run()
-    steps = max(3, a.steps)
+    steps = max(3, min(a.steps, 10))
     acc = {}
     t1 = time.perf_counter()
     for _ in range(steps):
@@ -296,48 +418,35 @@ def _matrix_leg(skm, synth, a, device):
     alg = 4 * c["increments"]
     gbs = alg / (acc["pairs"] * 1e-3) / 1e9
     cpu = None
-    if files is not None:  # the oracle's matrix distance (single thread) on a bounded sample
+    if files is not None:  # the oracle's matrix distance on the host cores, bounded sample
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ref
-        ns = min(n, 10_000)
+        threads = a.cpu_threads or cores["usable"]
+        ns = min(n, 20_000)
         e2 = int(off[ns - 1]) + int(ln[ns - 1])
         ob = oracle_ref.Bdz(files[0])
         t = time.perf_counter()
-        oracle_ref.matrix_distance(ob, files[1], res[:e2], off[:ns], ln[:ns], np.arange(ns, dtype=np.uint32),
-                                   funcs.index("hypothetical protein"))
+        oracle_ref.matrix_distance_mt(ob, files[1], res[:e2], off[:ns], ln[:ns], np.arange(ns, dtype=np.uint32),
+                                      funcs.index("hypothetical protein"), n_threads=threads, want_pairs=False)
         dt = time.perf_counter() - t
-        w = int(np.where(ln[:ns] >= 8, ln[:ns].astype(np.int64) - 7, 0).sum())
-        cpu = {"value": w / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
+        w = _windows(ln[:ns])
+        cpu = {"value": w / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
+               "host": {k: cores[k] for k in ("model", "affinity", "cgroup_quota")},
                "sample": f"all-vs-all over the first {ns} query proteins ({w} windows; pair work grows with the "
                          f"square of the sample, so this rate is an upper bound for 100K), {dt:.1f} s, "
-                         f"oracle/skm_oracle.cpp oracle_matrix_distance, one thread"}
+                         f"oracle/skm_oracle.cpp oracle_matrix_distance on {threads} host threads"}
         del ob, files
     return {"metric": "query k-mers/sec (lookup + all-vs-all shared signature k-mer counts)",
             "value": c["windows"] * steps / wall, "unit": "k-mers/s", "ms_per_step": 1000.0 * wall / steps,
-            "pair_increments_per_s": c["increments"] / (acc["pairs"] * 1e-3),
-            "config": {"workload": f"C5: {n} query proteins of {fam} families, all-vs-all, 1 GPU (one tile)",
-                       "queries": n, "families": fam, "db_keys": int(len(kept.keys)), "windows": c["windows"],
+            "steps": steps, "pair_increments_per_s": c["increments"] / (acc["pairs"] * 1e-3),
+            "config": {"workload": f"C5: {n} query proteins of 200 families, all-vs-all, 1 GPU (one tile)",
+                       "queries": n, "families": 200, "db_keys": int(len(kept.keys)), "windows": c["windows"],
                        "hits": c["hits"], "pair_increments": c["increments"], "nonzero_pairs": c["pairs"]},
             "phase_ms": acc,
             "roofline": {"bound": "hbm", "kernel": "k_md_rows", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
-                         "avg_launch_ms": acc["pairs"], "traffic": _pmc_traffic("k_md_rows", a.seqs)},
+                         "avg_launch_ms": acc["pairs"], "traffic": _pmc_traffic("k_md_rows", n)},
             "cpu_baseline": cpu, "prep_s": prep_s}
-
-
-def _valid_windows(r, o, l, f) -> int:
-    """Count of windows whose 8 residues are all in ok_prot_ (records the build materialises)."""
-    ok = np.zeros(256, bool)
-    ok[np.frombuffer(b"ACDEFGHIKLMNPQRSTVWYacdefghiklmnpqrstvwy", np.uint8)] = True
-    good = ok[r].astype(np.int32)
-    c = np.concatenate([[0], np.cumsum(good)])
-    total = 0
-    for s0, ln, fn in zip(o.astype(np.int64), l.astype(np.int64), f):
-        if fn == 0xFFFF or ln < 8:
-            continue
-        w = c[s0 + 8:s0 + ln + 1] - c[s0:s0 + ln - 7]
-        total += int((w == 8).sum())
-    return total
 
 
 def _pmc_traffic(kernel: str, seqs: int):
@@ -347,36 +456,33 @@ def _pmc_traffic(kernel: str, seqs: int):
     try:
         d = json.load(open(path))
         e = d["kernels"][kernel]
-        if int(d.get("seqs_per_gpu", -1)) != seqs:
+        if int(e.get("seqs", d.get("seqs_per_gpu", -1))) != int(seqs):
             return None
         return e["hbm_bytes_per_launch"]
     except Exception:
         return None
 
 
-def _cpu_threads(threads: int) -> int:
-    if threads <= 0:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    return threads
-
-
-def _cpu_baseline(r, o, l, f, i, nf, n_sample, threads):
+def _cpu_baseline(shard, nfun, n_sample, threads, cores, seqs_total):
     """The CPU port of the build (oracle/skm_oracle.cpp oracle_build_mt: the --n-threads 1 results
-    computed on all the host cores this job owns -- extract into key-hash shards, per-shard stable
-    sort + group + cut + statistics) on the first n_sample sequences of the same workload."""
+    computed on every usable host core -- extract into key-hash shards, per-shard stable sort +
+    group + cut + statistics) on the first n_sample sequences of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref
-    threads = _cpu_threads(threads)
+    nf = (n_sample + PER_FILE - 1) // PER_FILE
+    r, o, l, f, i = shard.packed(first_files=nf)
     n = min(n_sample, len(l))
     end = int(o[n - 1]) + int(l[n - 1])
     t = time.perf_counter()
-    oracle_ref.build_mt(r[:end], o[:n], l[:n], f[:n], i[:n], nf, threads, sort=False)
+    oracle_ref.build_mt(r[:end], o[:n], l[:n], f[:n], i[:n], nfun, threads, sort=False)
     dt = time.perf_counter() - t
     w = oracle_ref.count_windows(l[:n], f[:n])
     return {"value": w / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} sequences of the same workload ({w} windows), {dt:.1f} s, "
-                      f"oracle/skm_oracle.cpp oracle_build_mt on {threads} host threads "
-                      f"(--n-threads 1 results; unsorted output like the reference's hash map)"}
+            "host": {k: cores[k] for k in ("model", "affinity", "cgroup_quota")},
+            "sample": f"first {n:,} of the {seqs_total:,} sequences of the same workload ({w:,} windows), "
+                      f"{dt:.1f} s, oracle/skm_oracle.cpp oracle_build_mt on {threads} host threads "
+                      f"(every CPU of this job's cgroup quota; --n-threads 1 results, unsorted output like the "
+                      f"reference's hash map)"}
 
 
 if __name__ == "__main__":

@@ -117,8 +117,9 @@ int skm_build_last_timings(skm_build* b, float* ms, int cap);
 /* Counters of the last run: [0]=windows [1]=kept (owned by this rank) [2]=overflow sub-buckets
  * [3]=chain jobs [4]=chain samples [5]=sequences [6]=occurrences grouped on this rank
  * [7]=occurrences in overflow sub-buckets [8]=k-mers kept by the overflow path
- * [9]=groups of > 64 members handed to k_big_groups [10]=k-mers kept among them;
- * returns entries written. */
+ * [9]=groups of > 64 members handed to k_big_groups [10]=k-mers kept among them
+ * [11]=key-range passes [12]=valid windows (occurrences) this rank extracts; totals over the
+ * passes of the run; returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Build options beyond skm_build_opts (take effect at the next prepare/run):
  *   "key_range_passes"        0 = automatic; else P = 1, 2, 4 .. 64 passes over disjoint k-mer

@@ -899,6 +899,100 @@ int64_t oracle_matrix_distance(const oracle_bdz* db, const oracle_stored* dat, c
     return (int64_t)n;
 }
 
+// The same pair counts on n_threads host threads (bench.py's CPU baseline of the matrix leg; the
+// reference fills kmer_hit_map from process_fasta_stream_parallel's TBB tasks, matrix_distance.h
+// :130-143).  (1) threads over sequence ranges collect (kmer, index) hits; (2) threads over k-mer
+// hash shards dedupe each k-mer's index set and emit its id1 < id2 pair keys; (3) threads over
+// id1 shards sort and run-length count the pair keys.  out != nullptr: the pairs sorted by
+// (id1, id2), as oracle_matrix_distance.  Returns the number of pairs (writes at most cap).
+int64_t oracle_matrix_distance_mt(const oracle_bdz* db, const oracle_stored* dat, const uint8_t* residues,
+                                  const uint64_t* seq_off, const uint32_t* seq_len, const uint32_t* seq_idx,
+                                  uint64_t n_seqs, int32_t hypo_index, uint32_t* out, uint64_t cap, int n_threads) {
+    const int T = std::max(1, n_threads);
+    auto shard_of = [T](uint64_t k) { return (int)(((k * 0x9E3779B97F4A7C15ull) >> 40) % (uint64_t)T); };
+    // (1) hits, bucketed by k-mer shard per producing thread
+    std::vector<std::vector<std::vector<std::pair<uint64_t, uint32_t>>>> hits(T, std::vector<std::vector<std::pair<uint64_t, uint32_t>>>(T));
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t]() {
+                const uint64_t s0 = n_seqs * (uint64_t)t / (uint64_t)T, s1 = n_seqs * (uint64_t)(t + 1) / (uint64_t)T;
+                for (uint64_t s = s0; s < s1; ++s) {
+                    const double seqlen = static_cast<double>(seq_len[s]);
+                    for_each_kmer8(residues + seq_off[s], seq_len[s], [&](const uint8_t* ptr, size_t) {
+                        const uint32_t idx = oracle_bdz_search(db, ptr, 8);
+                        if (idx >= db->m) return;
+                        const oracle_stored& kd = dat[idx];
+                        if (hypo_index >= 0 && kd.function_index == (uint16_t)hypo_index) return;
+                        const double mean = static_cast<double>(kd.mean);
+                        const double stddev = kd.var == 0 ? seqlen * 0.1 : std::sqrt(static_cast<double>(kd.var));
+                        if (seqlen < mean - stddev * 2.0 || seqlen > mean + stddev * 2.0) return;
+                        const uint64_t k = load_key(ptr);
+                        hits[t][shard_of(k)].emplace_back(k, seq_idx[s]);
+                    });
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    // (2) per k-mer shard: group, dedupe, emit pair keys bucketed by id1 shard
+    std::vector<std::vector<std::vector<uint64_t>>> pairs(T, std::vector<std::vector<uint64_t>>(T));
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t]() {
+                std::vector<std::pair<uint64_t, uint32_t>> v;
+                for (int p = 0; p < T; ++p) v.insert(v.end(), hits[p][t].begin(), hits[p][t].end());
+                for (int p = 0; p < T; ++p) std::vector<std::pair<uint64_t, uint32_t>>().swap(hits[p][t]);
+                std::sort(v.begin(), v.end());
+                v.erase(std::unique(v.begin(), v.end()), v.end());
+                for (size_t a = 0; a < v.size();) {
+                    size_t e = a;
+                    while (e < v.size() && v[e].first == v[a].first) ++e;
+                    for (size_t i = a; i < e; ++i)
+                        for (size_t j = i + 1; j < e; ++j)
+                            pairs[t][v[i].second % (uint32_t)T].push_back(((uint64_t)v[i].second << 32) | v[j].second);
+                    a = e;
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    // (3) per id1 shard: count
+    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> cnt(T);
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t]() {
+                std::vector<uint64_t> v;
+                for (int p = 0; p < T; ++p) {
+                    v.insert(v.end(), pairs[p][t].begin(), pairs[p][t].end());
+                    std::vector<uint64_t>().swap(pairs[p][t]);
+                }
+                std::sort(v.begin(), v.end());
+                for (size_t a = 0; a < v.size();) {
+                    size_t e = a;
+                    while (e < v.size() && v[e] == v[a]) ++e;
+                    cnt[t].emplace_back(v[a], (uint32_t)(e - a));
+                    a = e;
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    uint64_t n = 0;
+    for (auto& c : cnt) n += c.size();
+    if (out) {
+        std::vector<std::pair<uint64_t, uint32_t>> all;
+        all.reserve(n);
+        for (auto& c : cnt) all.insert(all.end(), c.begin(), c.end());
+        std::sort(all.begin(), all.end());
+        for (uint64_t i = 0; i < n && i < cap; ++i) {
+            out[3 * i] = (uint32_t)(all[i].first >> 32);
+            out[3 * i + 1] = (uint32_t)all[i].first;
+            out[3 * i + 2] = all[i].second;
+        }
+    }
+    return (int64_t)n;
+}
+
 // --------------------------------------------------------------------------------------------
 //  find_best_call (call_functions.tcc:347-659).  function_index: array of nfunc C strings
 //  (function.index column 1).  Writes the called function string (NUL-terminated) into out_func.

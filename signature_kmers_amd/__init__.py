@@ -262,11 +262,15 @@ class SignatureBuilder:
         and the diagnostic tunables named in include/skm.h."""
         _check(lib().skm_build_set_option(self._h, name.encode(), int(value)))
 
+    def passes(self) -> int:
+        """Key-range passes of the last run (1 when the shard fits the work buffers)."""
+        return self.counters()["passes"]
+
     def counters(self) -> dict:
-        v = (C.c_uint64 * 11)()
-        n = lib().skm_build_counters(self._h, v, 11)
+        v = (C.c_uint64 * 13)()
+        n = lib().skm_build_counters(self._h, v, 13)
         names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped",
-                 "overflow_elements", "overflow_kept", "big_groups", "big_kept"]
+                 "overflow_elements", "overflow_kept", "big_groups", "big_kept", "passes", "valid"]
         return {names[i]: int(v[i]) for i in range(n)}
 
     def debug_jobs(self, k: int = 64) -> list:

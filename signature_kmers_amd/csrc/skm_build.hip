@@ -4090,9 +4090,9 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
-    const uint64_t v[11] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
-                            b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept};
-    int n = std::min(cap, 11);
+    const uint64_t v[13] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+                            b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total};
+    int n = std::min(cap, 13);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }

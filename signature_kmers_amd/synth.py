@@ -213,3 +213,55 @@ def write_dirs(root: str, n_seqs: int, n_families: int, per_file: int, seed: int
                 an.write(f"{pid}\t{p.names[p.labels[s]]}\n")
         files.append(g)
     return {"seqs_dir": seqs_dir, "ann_dir": ann_dir, "files": files, "proteome": p}
+
+
+# ------------------------------------------------------------------------------------------
+# Parallel generation (the 50M-protein C3 proteome): files are independent RNG streams, so a
+# pool of worker processes generates them in any order and the caller consumes them in file
+# order.  Workers are spawned (never forked): the caller may already hold a GPU context.
+# ------------------------------------------------------------------------------------------
+_WORKER_FAM = {}
+
+
+def _file_inputs(args):
+    """build_inputs of one genome file: (residues, seq_off, seq_len, seq_func, seq_id)."""
+    n_seqs, n_families, per_file, f, seed, extras = args
+    key = (n_families, seed)
+    if key not in _WORKER_FAM:
+        fam = make_families(n_families, seed)
+        fi = function_index_of(fam.names)
+        _WORKER_FAM[key] = (fam, np.array([fi[n] for n in fam.names], dtype=np.uint16))
+    fam, func_of_family = _WORKER_FAM[key]
+    n = min(per_file, n_seqs - f * per_file)
+    res, lens, _, labels = _mutate_file(fam, n, f, seed, extras)
+    lens = lens.astype(np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    if n:
+        off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    seq_id = (np.uint32(f) * np.uint32(100000) + np.arange(n, dtype=np.uint32)).astype(np.uint32)
+    return res, off, lens, func_of_family[labels], seq_id
+
+
+def iter_file_inputs(n_seqs: int, n_families: int, per_file: int = 4000, first_file: int = 0,
+                     n_files: int | None = None, seed: int = SEED, extras: bool = False, workers: int = 1):
+    """Yields build_inputs-style arrays per genome file, in file order, for files
+    [first_file, first_file + n_files) of an n_seqs proteome; `workers` > 1 generates them in a
+    spawned process pool (identical bytes: one RNG stream per file)."""
+    total_files = (n_seqs + per_file - 1) // per_file
+    if n_files is None:
+        n_files = total_files - first_file
+    files = range(first_file, min(total_files, first_file + n_files))
+    jobs = [(n_seqs, n_families, per_file, f, seed, extras) for f in files]
+    if workers <= 1 or len(jobs) <= 1:
+        for j in jobs:
+            yield _file_inputs(j)
+        return
+    import multiprocessing as mp
+    with mp.get_context("spawn").Pool(workers) as pool:
+        yield from pool.imap(_file_inputs, jobs, chunksize=4)
+
+
+def functions(n_families: int, seed: int = SEED) -> list:
+    """The function list (FunctionIndex order) of a proteome of n_families families."""
+    fi = function_index_of(make_families(n_families, seed).names)
+    return sorted(fi, key=fi.get)

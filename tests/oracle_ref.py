@@ -57,6 +57,8 @@ def olib():
         _lib.oracle_annotate_mt.argtypes = [P, P, P, P, P, C.c_uint64, C.POINTER(AnnotOpts), C.c_int]
         _lib.oracle_matrix_distance.restype = C.c_int64
         _lib.oracle_matrix_distance.argtypes = [P, P, P, P, P, P, C.c_uint64, C.c_int32, P, C.c_uint64]
+        _lib.oracle_matrix_distance_mt.restype = C.c_int64
+        _lib.oracle_matrix_distance_mt.argtypes = [P, P, P, P, P, P, C.c_uint64, C.c_int32, P, C.c_uint64, C.c_int]
         _lib.oracle_find_best_call.argtypes = [P, C.c_uint64, C.POINTER(C.c_char_p), C.c_uint64, P, P, P,
                                                C.c_char_p, C.c_uint64]
     return _lib
@@ -240,6 +242,27 @@ def annotate_exact(keys, data, residues, seq_off, seq_len, min_hits=5, max_gap=2
                                        C.byref(opts), _p(off), _p(calls), cap)
     assert tot >= 0
     return off, calls[:tot].copy()
+
+
+def matrix_distance_mt(bdz: Bdz, dat: bytes, residues, seq_off, seq_len, seq_idx, hypo_index=-1, n_threads=1,
+                       want_pairs=True):
+    """oracle_matrix_distance_mt: the pair counts on n_threads host threads; (n, 3) sorted pairs,
+    or (want_pairs=False, the CPU baseline) only their number."""
+    residues = np.ascontiguousarray(residues, np.uint8)
+    seq_off = np.ascontiguousarray(seq_off, np.uint64)
+    seq_len = np.ascontiguousarray(seq_len, np.uint32)
+    seq_idx = np.ascontiguousarray(seq_idx, np.uint32)
+    datb = np.frombuffer(dat, np.uint8).copy() if dat else np.zeros(10, np.uint8)
+    L = olib()
+    if not want_pairs:
+        return int(L.oracle_matrix_distance_mt(bdz.h, _p(datb), _p(residues), _p(seq_off), _p(seq_len), _p(seq_idx),
+                                               len(seq_len), hypo_index, None, 0, int(n_threads)))
+    n = int(L.oracle_matrix_distance_mt(bdz.h, _p(datb), _p(residues), _p(seq_off), _p(seq_len), _p(seq_idx),
+                                        len(seq_len), hypo_index, None, 0, int(n_threads)))
+    out = np.zeros((max(n, 1), 3), np.uint32)
+    L.oracle_matrix_distance_mt(bdz.h, _p(datb), _p(residues), _p(seq_off), _p(seq_len), _p(seq_idx), len(seq_len),
+                                hypo_index, _p(out), n, int(n_threads))
+    return out[:n].copy()
 
 
 def matrix_distance(bdz: Bdz, dat: bytes, residues, seq_off, seq_len, seq_idx, hypo_index=-1):

@@ -116,3 +116,29 @@ def test_tile_rows_cover_and_balance(skm):
             if n >= 1000:
                 area = [sum(n - i - 1 for i in range(a, b)) for a, b in bands]
                 assert max(area) - min(area) <= 2 * n, (n, world, area)  # one row of slack per band edge
+
+
+def test_parallel_oracle_matrix_equals_single_thread():
+    """oracle_matrix_distance_mt (bench.py's CPU baseline of the matrix leg) gives the
+    single-thread restatement's pairs for any thread count."""
+    from signature_kmers_amd import synth
+    import tempfile
+    import signature_kmers_amd as skm
+    p = synth.generate_arrays(3000, 30, per_file=500, seed=9)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    ref = oracle_ref.build(r, o, l, f, i, len(funcs))
+    with tempfile.TemporaryDirectory() as d:
+        base = d + "/kmer_data"
+        skm.mph_build(ref["keys"], ref["data"], base + ".mph", base + ".dat", seed=1)
+        ob = oracle_ref.Bdz(open(base + ".mph", "rb").read())
+        dat = open(base + ".dat", "rb").read()
+    q = synth.generate_arrays(5000, 30, per_file=500, first_file=6, n_files=4, seed=9)
+    idx = (np.arange(len(q.seq_len)) % 1500).astype(np.uint32)  # repeated SeqIdMap indices too
+    hypo = funcs.index("hypothetical protein")
+    want = oracle_ref.matrix_distance(ob, dat, q.residues, q.seq_off, q.seq_len, idx, hypo)
+    assert len(want) > 1000
+    for t in (1, 3, 8):
+        got = oracle_ref.matrix_distance_mt(ob, dat, q.residues, q.seq_off, q.seq_len, idx, hypo, n_threads=t)
+        np.testing.assert_array_equal(got, want)
+        assert oracle_ref.matrix_distance_mt(ob, dat, q.residues, q.seq_off, q.seq_len, idx, hypo, n_threads=t,
+                                             want_pairs=False) == len(want)
