@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gen-workers", type=int, default=0, help="generator processes (0: usable cores)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--cache-dir", default=None, help="save / reuse the generated headline shard (profiling)")
+    ap.add_argument("--cache-only", action="store_true", help="generate + cache the headline shard, then exit")
+    ap.add_argument("--option", action="append", default=[],
+                    help="name=value: skm_build_set_option on the headline build (experiments)")
     ap.add_argument("--annot-queries", type=int, default=10_000_000,
                     help="annotate leg (BASELINE configs[3]); 0 = off; N=1 only")
     ap.add_argument("--matrix-seqs", type=int, default=100_000,
@@ -87,6 +91,14 @@ def host_cores() -> dict:
     return {"usable": max(1, usable), "affinity": aff, "cgroup_quota": quota, "model": model}
 
 
+_T0 = time.time()
+
+
+def log(msg: str):
+    """Progress on stderr (the GPU harness takes a silent run for a hung one)."""
+    print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def _windows(lens) -> int:
     return int(np.where(lens >= 8, lens.astype(np.int64) - 7, 0).sum())
 
@@ -114,8 +126,33 @@ class Shard:
         return (r, off, lens, np.concatenate([p[3] for p in ps]), np.concatenate([p[4] for p in ps]))
 
 
-def gen(synth, n_total, families, first_file, n_files, workers):
-    return Shard(list(synth.iter_file_inputs(n_total, families, PER_FILE, first_file, n_files, workers=workers)))
+def gen(synth, n_total, families, first_file, n_files, workers, cache=None):
+    """The rank's files; with cache (a directory) they are saved on first use and memory-mapped
+    afterwards (profiling runs: generator pools do not run under rocprofv3)."""
+    tag = f"{n_total}_{families}_{first_file}_{n_files}"
+    if cache and os.path.exists(os.path.join(cache, tag + ".res.npy")):
+        res = np.load(os.path.join(cache, tag + ".res.npy"), mmap_mode="r")
+        meta = np.load(os.path.join(cache, tag + ".meta.npz"))
+        lens, func, ids, nper = meta["lens"], meta["func"], meta["ids"], meta["nper"]
+        parts, so, ro = [], 0, 0
+        for n in nper:
+            ln = lens[so:so + n]
+            off = np.zeros(n, np.uint64)
+            if n:
+                off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+            tot = int(ln.sum())
+            parts.append((res[ro:ro + tot], off, ln, func[so:so + n], ids[so:so + n]))
+            so += n
+            ro += tot
+        return Shard(parts)
+    sh = Shard(list(synth.iter_file_inputs(n_total, families, PER_FILE, first_file, n_files, workers=workers)))
+    if cache:
+        os.makedirs(cache, exist_ok=True)
+        np.save(os.path.join(cache, tag + ".res.npy"), np.concatenate([p[0] for p in sh.parts]))
+        np.savez(os.path.join(cache, tag + ".meta.npz"), lens=np.concatenate([p[2] for p in sh.parts]),
+                 func=np.concatenate([p[3] for p in sh.parts]), ids=np.concatenate([p[4] for p in sh.parts]),
+                 nper=np.array([len(p[2]) for p in sh.parts], np.int64))
+    return sh
 
 
 def main():
@@ -136,7 +173,12 @@ def main():
     t0 = time.time()
     files_total = (a.seqs_total + PER_FILE - 1) // PER_FILE
     f0, f1 = rank * files_total // world, (rank + 1) * files_total // world
-    c3 = gen(synth, a.seqs_total, a.families, f0, f1 - f0, workers)
+    log(f"rank {rank}/{world}: generating files [{f0}, {f1}) with {workers} workers")
+    c3 = gen(synth, a.seqs_total, a.families, f0, f1 - f0, workers, a.cache_dir)
+    if a.cache_only:
+        log("inputs cached")
+        return
+    log(f"generated {c3.n_seqs:,} proteins, {c3.n_windows:,} windows")
     c2_files = (a.weak_seqs + PER_FILE - 1) // PER_FILE
     if a.weak_seqs and f0 == rank * c2_files and f1 - f0 >= c2_files:
         c2 = Shard(c3.parts[:c2_files])  # files [r*250, r*250+250): the same bytes as the weak shard
@@ -176,11 +218,15 @@ def main():
     uid = new_uid()
     t0 = time.time()
     b = skm.SignatureBuilder(len(funcs), device=device, rank=rank, world_size=world)
+    for kv in a.option:
+        k, v = kv.split("=", 1)
+        b.set_option(k, int(v))
     c3.add_to(b)
     if uid is not None:
         b.set_comm(uid)
     b.prepare()
     prep_s = time.time() - t0
+    log(f"C3 prepared in {prep_s:.1f} s")
     head = _measure(skm, b, a.steps, a.warmup, c3, world, dist)
     b.close()
     per_gpu = a.seqs_total // world
@@ -237,8 +283,10 @@ def main():
             kept = b.finish()
         b.close()
     if world == 1 and queries is not None and kept is not None:
+        log("annotate leg")
         out["annotate"] = _annotate_leg(skm, kept, funcs, queries, a, device, cores)
     if world == 1 and matrix_in is not None:
+        log("matrix leg")
         out["matrix"] = _matrix_leg(skm, matrix_in, a, device, cores)
     if rank == 0:
         line = json.dumps(out)
@@ -256,8 +304,9 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
         if dist is not None:
             dist.barrier()
 
-    for _ in range(warmup):
+    for w in range(warmup):
         b.run()
+        log(f"warmup {w + 1}/{warmup}")
     phase = {}
     barrier()
     t1 = time.perf_counter()
@@ -265,6 +314,7 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
         b.run()  # returns after the run's final event has completed (device synchronised)
         for k, v in b.timings().items():
             phase[k] = phase.get(k, 0.0) + v
+        log(f"step done ({b.timings()['total']:.1f} ms device)")
     t_local = time.perf_counter() - t1
     barrier()
     ctrs = b.counters()
@@ -422,7 +472,7 @@ def _matrix_leg(skm, matrix_in, a, device, cores):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ref
         threads = a.cpu_threads or cores["usable"]
-        ns = min(n, 20_000)
+        ns = n
         e2 = int(off[ns - 1]) + int(ln[ns - 1])
         ob = oracle_ref.Bdz(files[0])
         t = time.perf_counter()

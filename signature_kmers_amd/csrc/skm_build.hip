@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -725,6 +726,48 @@ __global__ __launch_bounds__(JOB_WG) void k_job_scatter(const Job* __restrict__ 
     }
 }
 
+// Long chains leave the pass: their samples (wherever the group-by left them: consumed element
+// slots, the overflow's lengths buffer) are stashed into a run-persistent arena so the chains can
+// run on their own streams while the next passes reuse every work buffer.  k_long_plan: one
+// workgroup, exclusive offsets of the first nlong (class-sorted) jobs' sample counts.
+__global__ __launch_bounds__(1024) void k_long_plan(const Job* __restrict__ jobs, const uint64_t* __restrict__ nlong_p,
+                                                    uint64_t* __restrict__ off) {
+    __shared__ uint32_t s_wave[17];
+    __shared__ unsigned long long s_run;
+    const uint64_t nlong = *nlong_p;
+    if (threadIdx.x == 0) s_run = 0;
+    __syncthreads();
+    for (uint64_t b = 0; b < nlong; b += blockDim.x) {
+        const uint64_t j = b + threadIdx.x;
+        const uint32_t n = j < nlong ? jobs[j].n : 0u;
+        uint32_t tot;
+        const uint32_t ex = wg_exclusive_scan(n, s_wave, tot);
+        const unsigned long long run = s_run;
+        if (j < nlong) off[j] = run + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) s_run = run + tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        off[nlong] = s_run;
+        off[nlong + 1] = nlong;
+    }
+}
+
+// one workgroup per long job: copy its samples into arena + off[j], rewrite the job to point there
+__global__ __launch_bounds__(256) void k_long_stash(const Job* __restrict__ jobs, const uint64_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ lens, const uint32_t* __restrict__ recs32,
+                                                    const uint32_t* __restrict__ tmp32, const uint32_t* __restrict__ big32,
+                                                    uint32_t* __restrict__ arena, Job* __restrict__ out_jobs) {
+    const Job jb = jobs[blockIdx.x];
+    const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
+    const uint32_t* x = (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
+                        (jb.lens_off & LENS_OFF_MASK);
+    const uint64_t o = off[blockIdx.x];
+    for (uint32_t i = threadIdx.x; i < jb.n; i += blockDim.x) arena[o + i] = x[i];
+    if (threadIdx.x == 0) out_jobs[blockIdx.x] = Job{reinterpret_cast<uint64_t>(arena + o), jb.n, jb.out_idx};
+}
+
 // One chain over x[0..n): blocks of 16 samples; the next block's loads (index clamped, so no
 // per-element branch) are in flight while the current block is consumed.
 template <bool VAR>
@@ -941,8 +984,11 @@ __global__ __launch_bounds__(128) void k_chain_long(const Job* __restrict__ jobs
     if (prio >= 3) __builtin_amdgcn_s_setprio(3);
     const Job jb = jobs[blockIdx.x];
     const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
-    const uint32_t* x = (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
-                        (jb.lens_off & LENS_OFF_MASK);
+    // lens == nullptr: stashed jobs, lens_off is the samples' device address
+    const uint32_t* x =
+        !lens && sel == 0 ? reinterpret_cast<const uint32_t*>(jb.lens_off)
+                          : (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
+                                (jb.lens_off & LENS_OFF_MASK);
     if (threadIdx.x < 64) {
         const double med = chain_long_p2(x, jb.n);
         if (threadIdx.x == 0) out[jb.out_idx].median = d2u16(med);
@@ -1132,16 +1178,15 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
     }
 }
 
-// Per-workgroup histogram of the level-1 buckets (count pass).  IDS: key-range pass mode, only
-// the windows whose id byte is this pass are hashed and counted.
-template <bool IDS>
+// Per-workgroup histogram of the level-1 buckets (count pass, one key-range pass = the whole
+// key space).
 __global__ __launch_bounds__(EX_THREADS) void k_extract(ExtractArgs X) {
     const uint8_t* __restrict__ res = X.res;
     const uint64_t rp = X.rp, span = X.span;
     extern __shared__ uint32_t s_cnt[];  // [NB]
     const int nbits = X.owner_bits + X.b1_bits;
     const uint32_t NB = 1u << nbits;
-    const int rem_bits = KEY_BITS - X.pass_bits - nbits;
+    const int rem_bits = KEY_BITS - nbits;
     const uint32_t wg = blockIdx.x;
     for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) s_cnt[b] = 0u;
     __syncthreads();
@@ -1149,11 +1194,6 @@ __global__ __launch_bounds__(EX_THREADS) void k_extract(ExtractArgs X) {
     const uint64_t end = min(begin + span, rp);
     for (uint64_t base = begin + (uint64_t)threadIdx.x * EX_POS_PER_THREAD; base < end;
          base += (uint64_t)blockDim.x * EX_POS_PER_THREAD) {
-        uint32_t want = 0xFFFFu;
-        if (IDS) {
-            want = match16(*reinterpret_cast<const uint4*>(X.ids + base), X.pass_id);
-            if (!want) continue;
-        }
         const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
         const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
         const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
@@ -1174,15 +1214,80 @@ __global__ __launch_bounds__(EX_THREADS) void k_extract(ExtractArgs X) {
         for (int t = 0; t < EX_POS_PER_THREAD; ++t) {
             if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
             const uint64_t p = base + t;
-            const bool ok = IDS ? ((want >> t) & 1u) != 0 : ((valid >> t) & 0xFFu) == 0xFFu;
-            if (ok && p < end) {
+            if (((valid >> t) & 0xFFu) == 0xFFu && p < end) {
                 const uint64_t h = mix43(k);
-                atomicAdd(&s_cnt[(uint32_t)(h >> rem_bits) & (NB - 1)], 1u);
+                atomicAdd(&s_cnt[(uint32_t)(h >> rem_bits)], 1u);
             }
         }
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) X.hist[(uint64_t)wg * NB + b] = s_cnt[b];
+}
+
+// ------------------------------------------------------------------------------------------
+// Key-range pass extraction.  k_pass_compact turns the id bytes into the ascending packed
+// positions of this pass's windows (one workgroup per 32K windows, one cursor reservation per
+// workgroup: the ranges land in any order, which is immaterial, elements carry their ordinal);
+// the count and stage kernels then work on 1/P of the windows at the density of a one-pass build
+// instead of rescanning every residue.
+// ------------------------------------------------------------------------------------------
+constexpr int CP_THREADS = 256, CP_PER_THREAD = 128;  // 32768 windows per workgroup
+__global__ __launch_bounds__(CP_THREADS) void k_pass_compact(const uint8_t* __restrict__ ids, uint64_t rp, uint32_t pass,
+                                                             uint64_t* __restrict__ pos,
+                                                             unsigned long long* __restrict__ cursor) {
+    __shared__ uint32_t s_wave[CP_THREADS / 64 + 1];
+    __shared__ unsigned long long s_base;
+    const uint64_t base = (uint64_t)blockIdx.x * CP_THREADS * CP_PER_THREAD + (uint64_t)threadIdx.x * CP_PER_THREAD;
+    uint32_t m[CP_PER_THREAD / 16];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < CP_PER_THREAD / 16; ++k) {
+        const uint64_t q = base + 16u * k;
+        m[k] = q < rp ? match16(*reinterpret_cast<const uint4*>(ids + q), pass) : 0u;
+        cnt += __popc(m[k]);
+    }
+    uint32_t tot;
+    uint32_t off = wg_exclusive_scan(cnt, s_wave, tot);
+    if (threadIdx.x == 0) s_base = tot ? atomicAdd(cursor, (unsigned long long)tot) : 0ull;
+    __syncthreads();
+    uint64_t* out = pos + s_base + off;
+#pragma unroll
+    for (int k = 0; k < CP_PER_THREAD / 16; ++k)
+        for (uint32_t w = m[k]; w; w &= w - 1) *out++ = base + 16u * k + (uint32_t)__ffs(w) - 1u;
+}
+
+// the 8 residue bytes at packed position p (the buffer is padded past its end)
+__device__ __forceinline__ uint64_t load_window(const uint8_t* __restrict__ res, uint64_t p) {
+    const uint64_t a = p & ~7ull;
+    const uint32_t sh = (uint32_t)(p & 7u) * 8u;
+    const uint64_t w0 = *reinterpret_cast<const uint64_t*>(res + a);
+    const uint64_t w1 = *reinterpret_cast<const uint64_t*>(res + a + 8);
+    return sh ? (w0 >> sh) | (w1 << (64u - sh)) : w0;
+}
+
+// mix43 of the base-40 key of a (valid) window
+__device__ __forceinline__ uint64_t window_hash(uint64_t raw) {
+    uint64_t k = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) k = k * 40u + residue_code((uint32_t)((raw >> (8 * j)) & 0xFFu));
+    return mix43(k);
+}
+
+// count pass over this pass's positions pos[0..n): per-workgroup level-1 bucket histogram
+__global__ __launch_bounds__(EX_THREADS) void k_extract_pos(ExtractArgs X, const uint64_t* __restrict__ pos, uint64_t n) {
+    extern __shared__ uint32_t s_cnt[];  // [NB]
+    const int nbits = X.owner_bits + X.b1_bits;
+    const uint32_t NB = 1u << nbits;
+    const int rem_bits = KEY_BITS - X.pass_bits - nbits;
+    for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) s_cnt[b] = 0u;
+    __syncthreads();
+    const uint64_t begin = (uint64_t)blockIdx.x * X.span, end = min(begin + X.span, n);
+    for (uint64_t j = begin + threadIdx.x; j < end; j += blockDim.x) {
+        const uint64_t h = window_hash(load_window(X.res, pos[j]));
+        atomicAdd(&s_cnt[(uint32_t)(h >> rem_bits) & (NB - 1)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) X.hist[(uint64_t)blockIdx.x * NB + b] = s_cnt[b];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1227,15 +1332,13 @@ __device__ __forceinline__ uint32_t stage_reserve(StageLds& L, uint32_t nd, unsi
     return tot;
 }
 
-template <bool IDS>
 __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, unsigned long long* __restrict__ cur0,
                                                                  uint64_t* __restrict__ out_hi,
                                                                  uint64_t* __restrict__ out_lo) {
     __shared__ StageLds L;
     const uint8_t* __restrict__ res = X.res;
     const int nbits = X.owner_bits + X.b1_bits;
-    const uint32_t NB = 1u << nbits;
-    const int rem_bits = KEY_BITS - X.pass_bits - nbits;
+    const int rem_bits = KEY_BITS - nbits;
     const uint64_t rem_mask = (1ull << rem_bits) - 1;
     const int l0_shift = nbits - SC_L0_BITS;
     const uint64_t begin = (uint64_t)blockIdx.x * X.span;
@@ -1243,18 +1346,12 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
     // the next round's residues and sequence record are loaded before this round's LDS work, so
     // their HBM latency (blk2seq -> meta is a dependent pair) overlaps the staging
     uint2 nv0 = make_uint2(0u, 0u), nv1 = make_uint2(0u, 0u);
-    uint32_t ns = 0, nwant = 0;
+    uint32_t ns = 0;
     SeqMeta nm{};
     auto fetch = [&](uint64_t b) {
         const uint64_t q = b + (uint64_t)threadIdx.x * SC_POS;
         nv0 = nv1 = make_uint2(0u, 0u);
-        nwant = 0;
         if (q < end) {  // the residue buffer is padded by 64 bytes past rp, not more
-            if (IDS) {
-                const uint2 id = *reinterpret_cast<const uint2*>(X.ids + q);
-                nwant = match16(make_uint4(id.x, id.y, 0xFFFFFFFFu, 0xFFFFFFFFu), X.pass_id) & 0xFFu;
-                if (!nwant) return;
-            }
             nv0 = *reinterpret_cast<const uint2*>(res + q);
             nv1 = *reinterpret_cast<const uint2*>(res + q + 8);
             ns = X.blk2seq[q >> 6];
@@ -1268,7 +1365,6 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
         const uint64_t p0 = base + (uint64_t)threadIdx.x * SC_POS;
         const uint2 v0 = nv0, v1 = nv1;
         uint32_t s = ns;
-        const uint32_t want = nwant;
         SeqMeta m = nm;
         if (base + SC_ROUND < end) fetch(base + SC_ROUND);
         const uint32_t w[4] = {v0.x, v0.y, v1.x, v1.y};
@@ -1293,11 +1389,10 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
             const uint64_t p = p0 + t;
             eh[t] = el[t] = 0;
             rk[t] = l0[t] = 0;
-            const bool okw = IDS ? ((want >> t) & 1u) != 0 : ((valid >> t) & 0xFFu) == 0xFFu;
-            if (okw && p < end) {
+            if (((valid >> t) & 0xFFu) == 0xFFu && p < end) {
                 while (p > m.pstart + m.len) m = X.meta[++s];  // valid windows never span a separator
                 const uint64_t h = mix43(k);
-                const uint32_t bucket = (uint32_t)(h >> rem_bits) & (NB - 1);
+                const uint32_t bucket = (uint32_t)(h >> rem_bits);
                 make_elem(h & rem_mask, X.s_base + s, (uint32_t)(p - m.pstart), m, eh[t], el[t]);
                 el[t] = (el[t] & ~0xFFFFull) | bucket;  // bucket id rides in the offset field until pass 2
                 l0[t] = bucket >> l0_shift;
@@ -1310,6 +1405,75 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
 #pragma unroll
         for (int t = 0; t < SC_POS; ++t)
             if ((ok >> t) & 1u) {
+                const uint32_t slot = L.off[l0[t]] + rk[t];
+                L.hi[slot] = eh[t];
+                L.lo[slot] = el[t];
+                L.dst[slot] = (uint8_t)l0[t];
+            }
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < tot; j += blockDim.x) {
+            const uint32_t d = L.dst[j];
+            const uint64_t o = L.base[d] + (j - L.off[d]);
+            out_hi[o] = L.hi[j];
+            out_lo[o] = L.lo[j];
+        }
+        __syncthreads();
+    }
+}
+
+// The staged level-0 scatter over a key-range pass's positions pos[0..n) (same staging rounds
+// as k_extract_stage; each position finds its sequence through blk2seq, reusing the previous
+// one while it still contains the window).
+__global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage_pos(ExtractArgs X, const uint64_t* __restrict__ pos,
+                                                                     uint64_t n, unsigned long long* __restrict__ cur0,
+                                                                     uint64_t* __restrict__ out_hi,
+                                                                     uint64_t* __restrict__ out_lo) {
+    __shared__ StageLds L;
+    const int nbits = X.owner_bits + X.b1_bits;
+    const uint32_t NB = 1u << nbits;
+    const int rem_bits = KEY_BITS - X.pass_bits - nbits;
+    const uint64_t rem_mask = (1ull << rem_bits) - 1;
+    const int l0_shift = nbits - SC_L0_BITS;
+    const uint64_t begin = (uint64_t)blockIdx.x * X.span, end = min(begin + X.span, n);
+    uint32_t s = 0xFFFFFFFFu;
+    SeqMeta m{};
+    for (uint64_t base = begin; base < end; base += SC_ROUND) {
+        if (threadIdx.x < 128) L.cnt[threadIdx.x] = 0;
+        __syncthreads();
+        uint64_t pp[SC_POS], raw[SC_POS];
+#pragma unroll
+        for (int t = 0; t < SC_POS; ++t) {
+            const uint64_t j = base + (uint64_t)threadIdx.x * SC_POS + t;
+            pp[t] = j < end ? pos[j] : ~0ull;
+        }
+#pragma unroll
+        for (int t = 0; t < SC_POS; ++t) raw[t] = pp[t] != ~0ull ? load_window(X.res, pp[t]) : 0ull;
+        uint64_t eh[SC_POS], el[SC_POS];
+        uint32_t rk[SC_POS], l0[SC_POS];
+#pragma unroll
+        for (int t = 0; t < SC_POS; ++t) {
+            eh[t] = el[t] = 0;
+            rk[t] = l0[t] = 0;
+            const uint64_t p = pp[t];
+            if (p != ~0ull) {
+                if (s == 0xFFFFFFFFu || p < m.pstart || p > m.pstart + m.len) {
+                    s = X.blk2seq[p >> 6];
+                    m = X.meta[s];
+                }
+                while (p > m.pstart + m.len) m = X.meta[++s];
+                const uint64_t h = window_hash(raw[t]);
+                const uint32_t bucket = (uint32_t)(h >> rem_bits) & (NB - 1);
+                make_elem(h & rem_mask, X.s_base + s, (uint32_t)(p - m.pstart), m, eh[t], el[t]);
+                el[t] = (el[t] & ~0xFFFFull) | bucket;  // bucket id rides in the offset field until pass 2
+                l0[t] = bucket >> l0_shift;
+                rk[t] = atomicAdd(&L.cnt[l0[t]], 1u);
+            }
+        }
+        __syncthreads();
+        const uint32_t tot = stage_reserve(L, 1u << SC_L0_BITS, cur0, 0);
+#pragma unroll
+        for (int t = 0; t < SC_POS; ++t)
+            if (pp[t] != ~0ull) {
                 const uint32_t slot = L.off[l0[t]] + rk[t];
                 L.hi[slot] = eh[t];
                 L.lo[slot] = el[t];
@@ -2777,7 +2941,8 @@ struct Tune {
     int ovf_heavy = 8192;            // overflow sub-buckets >= this many elements go to stream 2
     int ovf_inline_min = 0x7FFFFFFF; // overflow chains of >= this many samples run inline
     int inline_prio = 3;
-    int ovf_long_class = 14;
+    int ovf_long_class = 14;         // chains of >= 2^class samples leave the pass (chain streams)
+    int main_long_class = 14;
     int ovf_chain_wgs = 0;
     int chain_prio = 0;
     int bucket_prio = 0;
@@ -2793,7 +2958,7 @@ struct Tune {
 using namespace skm;
 
 struct ChainSet {            // job sort scratch + sorted jobs of one chain launch
-    DevBuf hist, offs, sorted;
+    DevBuf hist, offs, sorted, long_off;
 };
 
 struct skm_build {
@@ -2884,6 +3049,7 @@ struct skm_build {
     uint64_t pass_max = 0;              // valid windows of the largest pass (this shard)
     uint64_t valid_total = 0;           // valid windows of this shard
     DevBuf d_ids;                       // per-window pass id (pass_bits > 0)
+    DevBuf d_pos;                       // this pass's window positions (pass_bits > 0)
     uint64_t kept_cap = 0;              // kept k-mer arena (keys + records), shared by all passes
     hipEvent_t ev_start = nullptr;
     // run totals over the passes (counters(), timings)
@@ -2892,6 +3058,13 @@ struct skm_build {
     } acc{};
     float pass_ms[12] = {};
     skm::Tune tune;
+    // key-range passes: the long chains leave their pass (stashed samples, run-level job list) and
+    // run in batches on a fourth stream (mid-run and at the end), overlapping the later passes
+    hipStream_t chain_st = nullptr;
+    hipEvent_t chain_ev[3] = {};
+    std::deque<DevBuf> long_arena;       // stashed samples per (pass, launch site)
+    DevBuf d_long_jobs;                  // run-level list of stashed long jobs (device addresses)
+    uint64_t long_jobs_cap = 0, n_long = 0, long_samples = 0, long_launched = 0;
 };
 
 namespace {
@@ -3180,6 +3353,13 @@ void size_local(skm_build* b) {
     b->d_recs_hi.ensure(8 * W);
     b->d_recs_lo.ensure(8 * W);
     if (b->pass_bits > 0) {
+        b->d_pos.ensure(8 * W);
+        // the histogram matrix of a pass may use every extract workgroup row
+        const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
+        b->d_hist.ensure(sizeof(uint32_t) * (uint64_t)EX_MAX_WG * NB);
+        b->d_offs.ensure(sizeof(uint32_t) * (uint64_t)EX_MAX_WG * NB);
+        b->d_partial.ensure(sizeof(uint32_t) * (uint64_t)ceil_div(EX_MAX_WG, SCAN_ROWS) * NB);
+        b->d_rbbase.ensure(sizeof(uint32_t) * (uint64_t)ceil_div(EX_MAX_WG, SCAN_ROWS) * NB);
         b->d_ids.ensure(((b->rp + 15) & ~15ull) + 64);
         SKM_HIP(hipMemsetAsync(b->d_ids.p, 0xFF, ((b->rp + 15) & ~15ull) + 64, b->stream));
     }
@@ -3323,19 +3503,35 @@ void phase_extract(skm_build* b, uint32_t pass) {
     X.s_base = b->s_base;
     X.out_hi = b->d_recs_hi.as<uint64_t>();
     X.out_lo = b->d_recs_lo.as<uint64_t>();
-    if (b->pass_bits)
-        hipLaunchKernelGGL(k_extract<true>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, X);
-    else
-        hipLaunchKernelGGL(k_extract<false>, dim3(b->nwg), dim3(EX_THREADS), lds_cnt, st, X);
+    uint32_t nwg = b->nwg;
+    uint64_t npos = 0;
+    if (b->pass_bits) {
+        // this pass's window positions (compaction of the id bytes), then the count over them
+        unsigned long long* cur = b->d_ctr.as<unsigned long long>() + 24;
+        SKM_HIP(hipMemsetAsync(cur, 0, 8, st));
+        hipLaunchKernelGGL(k_pass_compact, dim3((uint32_t)ceil_div(b->rp, (uint64_t)CP_THREADS * CP_PER_THREAD)),
+                           dim3(CP_THREADS), 0, st, b->d_ids.as<uint8_t>(), b->rp, pass, b->d_pos.as<uint64_t>(), cur);
+        unsigned long long* pin = b->pinned_ctr();
+        SKM_HIP(hipMemcpyAsync(pin + 40, cur, 8, hipMemcpyDeviceToHost, st));
+        SKM_HIP(hipStreamSynchronize(st));
+        npos = pin[40];
+        SKM_CHECK(npos <= b->pass_max, SKM_E_STATE, "key-range pass larger than planned");
+        nwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(EX_MAX_WG, ceil_div(npos, (uint64_t)SC_ROUND * 4)));
+        X.span = ceil_div(ceil_div(npos ? npos : 1, nwg), (uint64_t)SC_ROUND) * SC_ROUND;
+        nwg = (uint32_t)std::max<uint64_t>(1, ceil_div(npos ? npos : 1, X.span));
+        hipLaunchKernelGGL(k_extract_pos, dim3(nwg), dim3(EX_THREADS), lds_cnt, st, X, b->d_pos.as<uint64_t>(), npos);
+    } else {
+        hipLaunchKernelGGL(k_extract, dim3(nwg), dim3(EX_THREADS), lds_cnt, st, X);
+    }
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[1], st));
     // ---- 2. scan ----
-    const uint32_t nrb = (uint32_t)ceil_div(b->nwg, SCAN_ROWS);
+    const uint32_t nrb = (uint32_t)ceil_div(nwg, SCAN_ROWS);
     dim3 gsc((NB + 255) / 256, nrb);
-    hipLaunchKernelGGL(k_colsum, gsc, dim3(256), 0, st, b->d_hist.as<uint32_t>(), b->nwg, NB, b->d_partial.as<uint32_t>());
+    hipLaunchKernelGGL(k_colsum, gsc, dim3(256), 0, st, b->d_hist.as<uint32_t>(), nwg, NB, b->d_partial.as<uint32_t>());
     hipLaunchKernelGGL(k_bstart, dim3(1), dim3(1024), 0, st, b->d_partial.as<uint32_t>(), nrb, NB, b->b1_bits,
                        b->d_rbbase.as<uint32_t>(), b->d_bstart32.as<uint32_t>(), b->d_owner_start.as<uint64_t>(), nowners);
-    hipLaunchKernelGGL(k_coloffs, gsc, dim3(256), 0, st, b->d_hist.as<uint32_t>(), b->d_rbbase.as<uint32_t>(), b->nwg,
+    hipLaunchKernelGGL(k_coloffs, gsc, dim3(256), 0, st, b->d_hist.as<uint32_t>(), b->d_rbbase.as<uint32_t>(), nwg,
                        NB, b->d_offs.as<uint32_t>());
     hipLaunchKernelGGL(k_abs_starts, dim3((NB + 1 + 255) / 256), dim3(256), 0, st, b->d_bstart32.as<uint32_t>(),
                        b->d_owner_start.as<uint64_t>(), NB, b->b1_bits, nowners, b->d_bstart.as<uint64_t>());
@@ -3349,11 +3545,11 @@ void phase_extract(skm_build* b, uint32_t pass) {
     hipLaunchKernelGGL(k_stage_init, dim3((NB + 255) / 256), dim3(256), 0, st, b->d_bstart.as<uint64_t>(), NB, l0_shift,
                        b->d_cur0.as<unsigned long long>(), b->d_cur1.as<unsigned long long>(), b->d_slices.as<uint32_t>());
     if (b->pass_bits)
-        hipLaunchKernelGGL(k_extract_stage<true>, dim3(b->nwg), dim3(EX_THREADS), 0, st, X,
+        hipLaunchKernelGGL(k_extract_stage_pos, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_pos.as<uint64_t>(), npos,
                            b->d_cur0.as<unsigned long long>(), b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
     else
-        hipLaunchKernelGGL(k_extract_stage<false>, dim3(b->nwg), dim3(EX_THREADS), 0, st, X,
-                           b->d_cur0.as<unsigned long long>(), b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
+        hipLaunchKernelGGL(k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
+                           b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
     const uint32_t nsl = (uint32_t)(ceil_div(b->pass_max, SC_SLICE) + (1u << SC_L0_BITS));
     hipLaunchKernelGGL(k_split_stage, dim3(nsl), dim3(EX_THREADS), 0, st, b->d_tmp_hi.as<uint64_t>(),
                        b->d_tmp_lo.as<uint64_t>(), b->d_bstart.as<uint64_t>(), nbits, b->d_slices.as<uint32_t>(),
@@ -3447,12 +3643,16 @@ void exchange(const Ranks& bs) {
     alltoallv(bs, ex_lo);
 }
 
-// job sort by length class (longest first) + the chain kernel, on stream st
-void launch_chains(const Tune& tn, hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs, const uint32_t* lens,
-                   const uint32_t* recs32, const uint32_t* tmp32, const uint32_t* big32, skm_stored_kmer_data* out,
-                   uint32_t long_class, unsigned long long* pin, hipStream_t st_short = nullptr,
-                   hipEvent_t ev_sorted = nullptr, uint32_t max_wgs = 0) {
+// Job sort by length class (longest first) + the chain kernels.  Chains of >= 2^long_class
+// samples get a wave pair each (k_chain_long): their samples are stashed into the run's long
+// arena and they run on one of the build's chain streams, overlapping the following passes; the
+// per-lane chains run on st (or st_short) within the pass.
+void launch_chains(skm_build* b, uint32_t site, hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs,
+                   const uint32_t* lens, const uint32_t* recs32, const uint32_t* tmp32, const uint32_t* big32,
+                   skm_stored_kmer_data* out, uint32_t long_class, unsigned long long* pin,
+                   hipStream_t st_short = nullptr, hipEvent_t ev_sorted = nullptr, uint32_t max_wgs = 0) {
     if (!nj) return;
+    const Tune& tn = b->tune;
     const uint32_t nwg = (uint32_t)std::min<uint64_t>(1024, ceil_div(nj, 4096));
     const uint64_t chunk = ceil_div(nj, nwg);
     cs.hist.ensure(4ull * nwg * JOB_CLASSES);
@@ -3463,12 +3663,15 @@ void launch_chains(const Tune& tn, hipStream_t st, const Job* jobs, uint64_t nj,
     hipLaunchKernelGGL(k_job_scatter, dim3(nwg), dim3(JOB_WG), 0, st, jobs, nj, chunk, cs.offs.as<uint64_t>(),
                        cs.sorted.as<Job>());
     if (st_short && ev_sorted) SKM_HIP(hipEventRecord(ev_sorted, st));  // sorted jobs ready
+    // long jobs first in the sorted order: their offsets in the arena, count and total samples
+    cs.long_off.ensure(8ull * (nj + 2));
+    hipLaunchKernelGGL(k_long_plan, dim3(1), dim3(1024), 0, st, cs.sorted.as<Job>(),
+                       cs.offs.as<uint64_t>() + (uint64_t)nwg * JOB_CLASSES, cs.long_off.as<uint64_t>());
     SKM_HIP(hipMemcpyAsync(pin, cs.offs.as<uint64_t>() + (uint64_t)nwg * JOB_CLASSES, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
     const uint64_t nlong = *pin;
-    if (nlong) {
-        // dynamic LDS reserves most of a CU's LDS for each long chain, so no group-by workgroup
-        // shares its CU (the chain is issue-latency bound: one wave pair, one instruction at a time)
+    if (nlong && b->pass_bits == 0) {
+        // one pass: the long chains start on st as soon as their jobs are sorted
         const uint32_t lds = (uint32_t)tn.chain_lds_kb * 1024u;
         static bool attr = false;
         if (lds > 65536 && !attr) {
@@ -3478,6 +3681,20 @@ void launch_chains(const Tune& tn, hipStream_t st, const Job* jobs, uint64_t nj,
         }
         hipLaunchKernelGGL(k_chain_long, dim3((uint32_t)nlong), dim3(128), lds, st, cs.sorted.as<Job>(), nlong, lens,
                            recs32, tmp32, big32, out, tn.chain_prio);
+        b->n_long += nlong;
+    } else if (nlong) {
+        SKM_HIP(hipMemcpyAsync(pin, cs.long_off.as<uint64_t>() + nlong, 8, hipMemcpyDeviceToHost, st));
+        SKM_HIP(hipStreamSynchronize(st));
+        const uint64_t total = *pin;
+        if (b->long_arena.size() <= site) b->long_arena.resize(site + 1);
+        b->long_arena[site].ensure(4 * std::max<uint64_t>(total, 1));
+        SKM_CHECK(b->n_long + nlong <= b->long_jobs_cap, SKM_E_STATE, "long chain job list exceeded");
+        hipLaunchKernelGGL(k_long_stash, dim3((uint32_t)nlong), dim3(256), 0, st, cs.sorted.as<Job>(),
+                           cs.long_off.as<uint64_t>(), lens, recs32, tmp32, big32, b->long_arena[site].as<uint32_t>(),
+                           b->d_long_jobs.as<Job>() + b->n_long);
+        SKM_HIP(hipGetLastError());
+        b->n_long += nlong;
+        b->long_samples += total;
     }
     if (nj > nlong) {
         // the per-lane chains on their own stream (when given): they do not wait for the long ones
@@ -3665,8 +3882,9 @@ void phase_group(skm_build* b, uint32_t pass) {
         SKM_HIP(hipStreamSynchronize(st2));
         SKM_CHECK(ctr[32 + 3] <= b->jobs2_cap && ctr[32 + 4] <= b->lens_cap, SKM_E_OOM,
                   "overflow chain buffers overflowed");
-        launch_chains(b->tune, st2, A2.jobs, ctr[32 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, nullptr, A.out_data,
-                      (uint32_t)b->tune.ovf_long_class, ctr + 21, st3, b->ev_o3[2], (uint32_t)b->tune.ovf_chain_wgs);
+        launch_chains(b, 2 * pass + 1, st2, A2.jobs, ctr[32 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, nullptr,
+                      A.out_data, (uint32_t)b->tune.ovf_long_class, ctr + 21, st3, b->ev_o3[2],
+                      (uint32_t)b->tune.ovf_chain_wgs);
         SKM_HIP(hipEventRecord(b->ev_o[2], st2));
         SKM_HIP(hipEventRecord(b->ev_o3[1], st3));
         b->n_jobs += ctr[32 + 3];
@@ -3680,8 +3898,9 @@ void phase_group(skm_build* b, uint32_t pass) {
     SKM_CHECK(ctr[5] <= b->big_cap, SKM_E_OOM, "big-group descriptor capacity exceeded");
     b->n_big = ctr[5];
     b->big_kept = ctr[6];
-    launch_chains(b->tune, st, A.jobs, ctr[3], b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
-                  reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, LONG_CLASS, ctr + 20);
+    launch_chains(b, 2 * pass, st, A.jobs, ctr[3], b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
+                  reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, (uint32_t)b->tune.main_long_class,
+                  ctr + 20);
     b->n_jobs += ctr[3];
     if (novf) {
         SKM_HIP(hipStreamWaitEvent(st, b->ev_o[2], 0));
@@ -3713,6 +3932,15 @@ void begin_run(skm_build* b) {
     SKM_HIP(hipGetLastError());
     b->acc = skm_build::Acc{};
     std::memset(b->pass_ms, 0, sizeof(b->pass_ms));
+    b->n_long = b->long_samples = b->long_launched = 0;
+    if (b->pass_bits) {  // every long job has >= 2^class distinct samples of this shard's elements
+        const int cls = std::min(b->tune.main_long_class, b->tune.ovf_long_class);
+        const uint64_t cap = b->world * (b->valid_total >> cls) + 4096;  // received elements: bounded by the world's
+        if (cap > b->long_jobs_cap) {
+            b->d_long_jobs.ensure(sizeof(Job) * cap);
+            b->long_jobs_cap = cap;
+        }
+    }
     b->n_kept = 0;
 }
 
@@ -3744,10 +3972,30 @@ void end_pass(skm_build* b) {
     }
 }
 
+// key-range passes: run the stashed long chains not yet launched, as one batch on the chain
+// stream, after the stashes on st / stream2 (both already ordered before this host call)
+void flush_long_chains(skm_build* b) {
+    if (b->n_long <= b->long_launched) return;
+    SKM_HIP(hipEventRecord(b->chain_ev[0], b->stream));
+    SKM_HIP(hipEventRecord(b->chain_ev[1], b->stream2));
+    SKM_HIP(hipStreamWaitEvent(b->chain_st, b->chain_ev[0], 0));
+    SKM_HIP(hipStreamWaitEvent(b->chain_st, b->chain_ev[1], 0));
+    const uint64_t n = b->n_long - b->long_launched;
+    hipLaunchKernelGGL(k_chain_long, dim3((uint32_t)n), dim3(128), 0, b->chain_st, b->d_long_jobs.as<Job>() + b->long_launched,
+                       n, nullptr, nullptr, nullptr, nullptr, b->d_data.as<skm_stored_kmer_data>(), b->tune.chain_prio);
+    SKM_HIP(hipGetLastError());
+    b->long_launched = b->n_long;
+}
+
 // per-rank statistics over the whole arena (distinct_functions) and the shard (seqs_with_func)
 void phase_stats(skm_build* b) {
     hipStream_t st = b->stream;
     const uint32_t F = b->opts.n_functions;
+    if (b->pass_bits) {  // the long chains of every pass
+        flush_long_chains(b);
+        SKM_HIP(hipEventRecord(b->chain_ev[2], b->chain_st));
+        SKM_HIP(hipStreamWaitEvent(st, b->chain_ev[2], 0));
+    }
     SKM_HIP(hipEventRecord(b->ev[7], st));
     SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
@@ -3793,6 +4041,7 @@ void run_ranks(const Ranks& bs) {
         for (auto* b : bs) {
             phase_group(b, pass);
             end_pass(b);
+            if (P >= 4 && pass + 1 == P / 2) flush_long_chains(b);  // first half's chains overlap the second half
         }
     }
     for (auto* b : bs) phase_stats(b);
@@ -3842,6 +4091,8 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     SKM_HIP(hipStreamCreateWithFlags(&b->stream3, hipStreamNonBlocking));
     for (auto& e : b->ev) SKM_HIP(hipEventCreate(&e));
     SKM_HIP(hipEventCreate(&b->ev_start));
+    SKM_HIP(hipStreamCreateWithFlags(&b->chain_st, hipStreamNonBlocking));
+    for (auto& e : b->chain_ev) SKM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_part, hipEventDisableTiming));
     for (auto& e : b->ev_o) SKM_HIP(hipEventCreate(&e));
     for (auto& e : b->ev_o3) SKM_HIP(hipEventCreate(&e));
@@ -3969,6 +4220,7 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "overflow_inline_min" ? &t.ovf_inline_min
                : n == "overflow_inline_prio" ? &t.inline_prio
                : n == "overflow_long_class" ? &t.ovf_long_class
+               : n == "main_long_class" ? &t.main_long_class
                : n == "overflow_chain_wgs" ? &t.ovf_chain_wgs
                : n == "chain_prio" ? &t.chain_prio
                : n == "bucket_prio" ? &t.bucket_prio
@@ -3976,7 +4228,8 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "host_timing" ? &t.host_timing : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
-        if (n == "overflow_long_class") SKM_CHECK(value >= 1 && value < 32, SKM_E_ARG, "overflow_long_class in [1, 32)");
+        if (n == "overflow_long_class" || n == "main_long_class")
+            SKM_CHECK(value >= 1 && value < 32, SKM_E_ARG, "long chain classes in [1, 32)");
         *f = (int)value;
     }
     b->prepared = false;  // pass geometry and buffers are re-planned on the next prepare/run
@@ -4258,6 +4511,12 @@ void skm_build_destroy(skm_build* b) {
         if (e) (void)hipEventDestroy(e);
     if (b->ev_part) (void)hipEventDestroy(b->ev_part);
     if (b->ev_start) (void)hipEventDestroy(b->ev_start);
+    if (b->chain_st) {
+        (void)hipStreamSynchronize(b->chain_st);
+        (void)hipStreamDestroy(b->chain_st);
+    }
+    for (auto& e : b->chain_ev)
+        if (e) (void)hipEventDestroy(e);
     if (b->h_pin) (void)hipHostFree(b->h_pin);
     if (b->h_ovf) (void)hipHostFree(b->h_ovf);
     if (b->stream) (void)hipStreamDestroy(b->stream);
