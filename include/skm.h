@@ -121,6 +121,32 @@ int skm_build_last_timings(skm_build* b, float* ms, int cap);
  * [11]=key-range passes [12]=valid windows (occurrences) this rank extracts; totals over the
  * passes of the run; returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
+/* Host transport: the rank collectives of a multi-process build run by the caller on host
+ * buffers, for ranks joined by a channel other than RCCL (the tests drive it with
+ * torch.distributed gloo; production multi-GPU runs use skm_build_set_comm).  The library stages
+ * device data through host memory around each call.  Every callback returns 0 on success. */
+typedef struct skm_transport {
+    void* ctx;
+    /* variable all-to-all (bytes): send + soff[q] (scnt[q] bytes) goes to rank q, which receives
+     * it at recv + roff[p] (rcnt[p] bytes) for source p */
+    int (*alltoallv)(void* ctx, const void* send, const uint64_t* scnt, const uint64_t* soff, void* recv,
+                     const uint64_t* rcnt, const uint64_t* roff);
+    /* in-place element-wise reduction over the ranks: op 0 = u32 sum (mod 2^32), 1 = u8 max */
+    int (*allreduce)(void* ctx, void* data, uint64_t count, int op);
+    /* every rank's bytes_per_rank[r] bytes, concatenated in rank order into recv */
+    int (*allgatherv)(void* ctx, const void* send, void* recv, const uint64_t* bytes_per_rank);
+} skm_transport;
+/* Join the ranks through a host transport instead of RCCL (world_size > 1; copied). */
+int skm_build_set_transport(skm_build* b, const skm_transport* tp);
+/* Test hooks (host only, no device): the exchange planning of one key-range pass as rank `rank`
+ * of `world`: bucket_starts [world*nb1+1] are this rank's owner-major level-1 bucket starts; the
+ * per-bucket counts go through tp->alltoallv; out: recv_off/recv_cnt [world] (elements, source
+ * order) and vstart [nb1+1] (bucket-major starts of the received elements).  And a self-check of
+ * the three callbacks (returns 0 when every collective gave the expected result). */
+int skm_debug_exchange_plan(const skm_transport* tp, int rank, int world, uint32_t nb1, const uint64_t* bucket_starts,
+                            uint64_t* recv_off, uint64_t* recv_cnt, uint64_t* vstart);
+int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
+
 /* Build options beyond skm_build_opts (take effect at the next prepare/run):
  *   "key_range_passes"        0 = automatic; else P = 1, 2, 4 .. 64 passes over disjoint k-mer
  *                             ranges (top bits of the key hash).  The reference holds the whole

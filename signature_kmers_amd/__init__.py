@@ -42,6 +42,16 @@ class _BuildOpts(C.Structure):
                 ("canonical_order", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32)]
 
 
+_A2A_T = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_void_p,
+                     C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
+_RED_T = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int)
+_AGV_T = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64))
+
+
+class _Transport(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("alltoallv", _A2A_T), ("allreduce", _RED_T), ("allgatherv", _AGV_T)]
+
+
 class _Kept(C.Structure):
     _fields_ = [("keys", C.POINTER(C.c_uint64)), ("data", C.c_void_p), ("n", C.c_uint64),
                 ("distinct_functions", C.POINTER(C.c_uint32)), ("seqs_with_func", C.POINTER(C.c_uint32)),
@@ -80,6 +90,9 @@ _SIGS = {
     "skm_build_last_timings": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int]),
     "skm_build_finish": (C.c_int, [_P, C.POINTER(_Kept)]),
     "skm_build_set_option": (C.c_int, [_P, C.c_char_p, C.c_int64]),
+    "skm_build_set_transport": (C.c_int, [_P, C.POINTER(_Transport)]),
+    "skm_debug_exchange_plan": (C.c_int, [C.POINTER(_Transport), C.c_int, C.c_int, C.c_uint32, _P, _P, _P, _P]),
+    "skm_debug_transport_check": (C.c_int, [C.POINTER(_Transport), C.c_int, C.c_int]),
     "skm_build_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
     "skm_build_debug_jobs": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int]),
     "skm_debug_chain_bench": (C.c_int, [C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_float)]),
@@ -239,6 +252,11 @@ class SignatureBuilder:
         _check(lib().skm_build_add_batch(self._h, _ptr(residues), _ptr(seq_off), _ptr(seq_len), _ptr(seq_func),
                                          _ptr(sid) if sid is not None else None, n))
 
+    def set_transport(self, transport: "GlooTransport"):
+        """Join the ranks through a host transport (skm_build_set_transport) instead of RCCL."""
+        self._transport = transport  # the callbacks must outlive the handle's runs
+        _check(lib().skm_build_set_transport(self._h, transport.ptr))
+
     def set_comm(self, unique_id: bytes):
         """Join the RCCL communicator (collective over the world_size ranks)."""
         buf = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
@@ -309,6 +327,94 @@ class SignatureBuilder:
             self.close()
         except Exception:
             pass
+
+
+class GlooTransport:
+    """skm_transport over torch.distributed (the default process group, e.g. gloo on the host):
+    the rank collectives of a multi-process build without RCCL (tests; CPU-side channels).
+    Callbacks run on the calling thread; an exception is reported as a failed collective."""
+
+    def __init__(self):
+        import torch.distributed as dist
+        self.dist = dist
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self._cbs = (_A2A_T(self._a2a), _RED_T(self._red), _AGV_T(self._agv))
+        self.struct = _Transport(None, *self._cbs)
+        self.ptr = C.pointer(self.struct)
+
+    @staticmethod
+    def _buf(addr, n):
+        import torch
+        if n == 0:
+            return torch.zeros(0, dtype=torch.uint8)
+        return torch.frombuffer((C.c_uint8 * n).from_address(addr), dtype=torch.uint8)
+
+    def _a2a(self, ctx, send, scnt, soff, recv, rcnt, roff):
+        try:
+            W, me = self.world, self.rank
+            sc = [int(scnt[i]) for i in range(W)]
+            so = [int(soff[i]) for i in range(W)]
+            rc = [int(rcnt[i]) for i in range(W)]
+            ro = [int(roff[i]) for i in range(W)]
+            if sc[me]:
+                C.memmove(recv + ro[me], send + so[me], sc[me])
+            reqs = []
+            for q in range(W):
+                if q == me:
+                    continue
+                if sc[q]:
+                    reqs.append(self.dist.isend(self._buf(send + so[q], sc[q]).clone(), q))
+                if rc[q]:
+                    reqs.append(self.dist.irecv(self._buf(recv + ro[q], rc[q]), q))
+            for r in reqs:
+                r.wait()
+            return 0
+        except Exception:  # reported to the library as a failed collective
+            import traceback
+            traceback.print_exc()
+            return -1
+
+    def _red(self, ctx, data, count, op):
+        try:
+            import torch
+            n = int(count)
+            if op == 0:
+                a = np.ctypeslib.as_array(C.cast(data, C.POINTER(C.c_uint32)), shape=(n,))
+                t = torch.from_numpy(a.astype(np.int64))
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+                a[:] = (t.numpy() & 0xFFFFFFFF).astype(np.uint32)
+            else:
+                a = np.ctypeslib.as_array(C.cast(data, C.POINTER(C.c_uint8)), shape=(n,))
+                t = torch.from_numpy(a.astype(np.int32))
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+                a[:] = t.numpy().astype(np.uint8)
+            return 0
+        except Exception:
+            import traceback
+            traceback.print_exc()
+            return -1
+
+    def _agv(self, ctx, send, recv, bytes_per_rank):
+        try:
+            import torch
+            W = self.world
+            nb = [int(bytes_per_rank[i]) for i in range(W)]
+            m = max(1, max(nb))
+            mine = torch.zeros(m, dtype=torch.uint8)
+            if nb[self.rank]:
+                mine[:nb[self.rank]] = self._buf(send, nb[self.rank])
+            outs = [torch.zeros(m, dtype=torch.uint8) for _ in range(W)]
+            self.dist.all_gather(outs, mine)
+            o = 0
+            for r in range(W):
+                if nb[r]:
+                    self._buf(recv + o, nb[r])[:] = outs[r][:nb[r]]
+                o += nb[r]
+            return 0
+        except Exception:
+            import traceback
+            traceback.print_exc()
+            return -1
 
 
 def comm_unique_id() -> bytes:

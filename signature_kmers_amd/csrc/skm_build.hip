@@ -3016,6 +3016,7 @@ struct skm_build {
     ncclComm_t comm = nullptr;
 #endif
     std::vector<skm_build*> group;
+    skm_transport tp{};                   // host transport (tp.alltoallv != nullptr)
 
     // second stream: overflow sub-buckets + their chains, concurrent with the group-by
     hipStream_t stream2 = nullptr, stream3 = nullptr;
@@ -3098,6 +3099,74 @@ void sync_all(const Ranks& bs) {
     } while (0)
 #endif
 
+bool has_tp(const Ranks& bs) { return bs.size() == 1 && bs[0]->world > 1 && bs[0]->tp.alltoallv != nullptr; }
+
+void tp_check(int rc, const char* what) {
+    SKM_CHECK(rc == 0, SKM_E_COMM, std::string("host transport ") + what + " failed");
+}
+
+// Exchange planning of one pass (pure host arithmetic).  Send side: from the owner-major bucket
+// starts, per-bucket counts (the all-to-all payload) and each peer's contiguous element range.
+struct SendPlan {
+    std::vector<uint32_t> cnt;        // [W * NB1]
+    std::vector<uint64_t> off, n;     // [W] elements
+};
+SendPlan plan_send(const uint64_t* abs, int W, uint32_t NB1) {
+    SendPlan p;
+    const uint64_t NB = (uint64_t)NB1 * W;
+    p.cnt.resize(NB);
+    for (uint64_t k = 0; k < NB; ++k) p.cnt[k] = (uint32_t)(abs[k + 1] - abs[k]);
+    p.off.assign(W, 0);
+    p.n.assign(W, 0);
+    for (int q = 0; q < W; ++q) {
+        p.off[q] = abs[(uint64_t)q * NB1];
+        p.n[q] = abs[(uint64_t)(q + 1) * NB1] - abs[(uint64_t)q * NB1];
+    }
+    return p;
+}
+// Receive side, from the received counts [source][bucket]: source-major pieces in the receive
+// buffer, and the bucket-major virtual numbering the partition kernel uses for tmp.
+struct RecvPlan {
+    std::vector<uint64_t> off, n;         // [W] elements per source
+    std::vector<uint64_t> seg_start;      // [W * NB1]
+    std::vector<uint32_t> seg_len;        // [W * NB1]
+    std::vector<uint64_t> vstart;         // [NB1 + 1]
+    uint64_t total = 0;
+};
+RecvPlan plan_recv(const uint32_t* rc, int W, uint32_t NB1) {
+    RecvPlan p;
+    const uint64_t NB = (uint64_t)NB1 * W;
+    p.off.assign(W, 0);
+    p.n.assign(W, 0);
+    p.seg_start.resize(NB);
+    p.seg_len.resize(NB);
+    p.vstart.assign(NB1 + 1, 0);
+    std::vector<uint64_t> bucket_tot(NB1, 0);
+    uint64_t run = 0;
+    for (int s = 0; s < W; ++s) {
+        p.off[s] = run;
+        for (uint32_t k = 0; k < NB1; ++k) {
+            const uint32_t c = rc[(uint64_t)s * NB1 + k];
+            p.seg_start[(uint64_t)s * NB1 + k] = run;
+            p.seg_len[(uint64_t)s * NB1 + k] = c;
+            bucket_tot[k] += c;
+            run += c;
+        }
+        p.n[s] = run - p.off[s];
+    }
+    for (uint32_t k = 0; k < NB1; ++k) p.vstart[k + 1] = p.vstart[k] + bucket_tot[k];
+    p.total = run;
+    return p;
+}
+
+// host-transport all-to-all of host buffers with byte offsets/counts per peer (packed staging)
+void tp_alltoallv_host(const skm_transport& tp, int W, const uint8_t* send, const std::vector<uint64_t>& soff,
+                       const std::vector<uint64_t>& scnt, uint8_t* recv, const std::vector<uint64_t>& roff,
+                       const std::vector<uint64_t>& rcnt) {
+    tp_check(tp.alltoallv(tp.ctx, send, scnt.data(), soff.data(), recv, rcnt.data(), roff.data()), "alltoallv");
+    (void)W;
+}
+
 // all-to-all with variable counts: rank p sends send[p] + soff[p][q] (scnt[p][q] bytes) to rank q,
 // which receives it at recv[q] + roff[q][p].
 struct A2A {
@@ -3107,6 +3176,26 @@ struct A2A {
 };
 
 void alltoallv(const Ranks& bs, const A2A& x) {
+    if (has_tp(bs)) {  // device -> packed host staging -> caller's channel -> device
+        skm_build* b = bs[0];
+        const int W = b->world;
+        std::vector<uint64_t> so(W), ro(W);
+        uint64_t st = 0, rt = 0;
+        for (int q = 0; q < W; ++q) {
+            so[q] = st;
+            st += x.scnt[0][q];
+            ro[q] = rt;
+            rt += x.rcnt[0][q];
+        }
+        std::vector<uint8_t> hs(std::max<uint64_t>(st, 1)), hr(std::max<uint64_t>(rt, 1));
+        SKM_HIP(hipStreamSynchronize(b->stream));
+        for (int q = 0; q < W; ++q)
+            if (x.scnt[0][q]) SKM_HIP(hipMemcpy(hs.data() + so[q], x.send[0] + x.soff[0][q], x.scnt[0][q], hipMemcpyDeviceToHost));
+        tp_alltoallv_host(b->tp, W, hs.data(), so, x.scnt[0], hr.data(), ro, x.rcnt[0]);
+        for (int q = 0; q < W; ++q)
+            if (x.rcnt[0][q]) SKM_HIP(hipMemcpy(x.recv[0] + x.roff[0][q], hr.data() + ro[q], x.rcnt[0][q], hipMemcpyHostToDevice));
+        return;
+    }
     if (is_group(bs)) {
         sync_all(bs);
         const size_t W = bs.size();
@@ -3141,6 +3230,16 @@ enum class Red { SumU32, MaxU8 };
 
 void allreduce(const Ranks& bs, const std::vector<void*>& ptr, size_t count, Red op) {
     if (count == 0) return;
+    if (has_tp(bs)) {
+        skm_build* b = bs[0];
+        const size_t es = op == Red::SumU32 ? 4 : 1;
+        std::vector<uint8_t> h(count * es);
+        SKM_HIP(hipStreamSynchronize(b->stream));
+        SKM_HIP(hipMemcpy(h.data(), ptr[0], count * es, hipMemcpyDeviceToHost));
+        tp_check(b->tp.allreduce(b->tp.ctx, h.data(), count, op == Red::SumU32 ? 0 : 1), "allreduce");
+        SKM_HIP(hipMemcpy(ptr[0], h.data(), count * es, hipMemcpyHostToDevice));
+        return;
+    }
     if (is_group(bs)) {
         sync_all(bs);
         const size_t es = op == Red::SumU32 ? 4 : 1;
@@ -3171,6 +3270,12 @@ void allreduce(const Ranks& bs, const std::vector<void*>& ptr, size_t count, Red
 
 // gather one u64 per rank to every rank (host values)
 std::vector<uint64_t> allgather_u64(const Ranks& bs, const std::vector<uint64_t>& mine) {
+    if (has_tp(bs)) {
+        skm_build* b = bs[0];
+        std::vector<uint64_t> out(b->world), bytes(b->world, 8);
+        tp_check(b->tp.allgatherv(b->tp.ctx, &mine[0], out.data(), bytes.data()), "allgatherv");
+        return out;
+    }
     if (is_group(bs)) return mine;  // one value per handle, already in rank order
 #if defined(SKM_WITH_RCCL)
     skm_build* b = bs[0];
@@ -3193,6 +3298,16 @@ void allgatherv(const Ranks& bs, const std::vector<const void*>& src, const std:
     const size_t W = bytes_per_rank.size();
     std::vector<uint64_t> off(W + 1, 0);
     for (size_t r = 0; r < W; ++r) off[r + 1] = off[r] + bytes_per_rank[r];
+    if (has_tp(bs)) {
+        skm_build* b = bs[0];
+        std::vector<uint8_t> hs(std::max<uint64_t>(bytes_per_rank[b->rank], 1)), hr(std::max<uint64_t>(off[W], 1));
+        SKM_HIP(hipStreamSynchronize(b->stream));
+        if (bytes_per_rank[b->rank])
+            SKM_HIP(hipMemcpy(hs.data(), src[0], bytes_per_rank[b->rank], hipMemcpyDeviceToHost));
+        tp_check(b->tp.allgatherv(b->tp.ctx, hs.data(), hr.data(), bytes_per_rank.data()), "allgatherv");
+        if (off[W]) SKM_HIP(hipMemcpy(dst[0], hr.data(), off[W], hipMemcpyHostToDevice));
+        return;
+    }
     if (is_group(bs)) {
         sync_all(bs);
         for (size_t q = 0; q < bs.size(); ++q)
@@ -3569,17 +3684,12 @@ void exchange(const Ranks& bs) {
         std::vector<uint64_t> abs(NB + 1);
         SKM_HIP(hipMemcpyAsync(abs.data(), b->d_bstart.p, 8 * (NB + 1), hipMemcpyDeviceToHost, b->stream));
         SKM_HIP(hipStreamSynchronize(b->stream));
-        std::vector<uint32_t> cnt(NB);
-        for (uint32_t k = 0; k < NB; ++k) cnt[k] = (uint32_t)(abs[k + 1] - abs[k]);
-        b->send_off.assign(W, 0);
-        b->send_cnt.assign(W, 0);
-        for (int q = 0; q < W; ++q) {
-            b->send_off[q] = abs[(uint64_t)q * NB1];
-            b->send_cnt[q] = abs[(uint64_t)(q + 1) * NB1] - abs[(uint64_t)q * NB1];
-        }
+        const SendPlan sp = plan_send(abs.data(), W, NB1);
+        b->send_off = sp.off;
+        b->send_cnt = sp.n;
         b->d_cnt_send.ensure(4ull * NB);
         b->d_cnt_recv.ensure(4ull * NB);
-        SKM_HIP(hipMemcpyAsync(b->d_cnt_send.p, cnt.data(), 4ull * NB, hipMemcpyHostToDevice, b->stream));
+        SKM_HIP(hipMemcpy(b->d_cnt_send.p, sp.cnt.data(), 4ull * NB, hipMemcpyHostToDevice));
         cx.send.push_back(b->d_cnt_send.as<uint8_t>());
         cx.recv.push_back(b->d_cnt_recv.as<uint8_t>());
         std::vector<uint64_t> off(W), c(W, 4ull * NB1);
@@ -3596,31 +3706,17 @@ void exchange(const Ranks& bs) {
         std::vector<uint32_t> rc(NB);  // [source][bucket]
         SKM_HIP(hipMemcpyAsync(rc.data(), b->d_cnt_recv.p, 4ull * NB, hipMemcpyDeviceToHost, b->stream));
         SKM_HIP(hipStreamSynchronize(b->stream));
-        b->recv_off.assign(W, 0);
-        b->recv_cnt.assign(W, 0);
-        std::vector<uint64_t> seg_start(NB), bucket_tot(NB1, 0), vstart(NB1 + 1, 0);
-        std::vector<uint32_t> seg_len(NB);
-        uint64_t run = 0;
-        for (int p = 0; p < W; ++p) {
-            b->recv_off[p] = run;
-            for (uint32_t k = 0; k < NB1; ++k) {
-                const uint32_t c = rc[(uint64_t)p * NB1 + k];
-                seg_start[(uint64_t)p * NB1 + k] = run;
-                seg_len[(uint64_t)p * NB1 + k] = c;
-                bucket_tot[k] += c;
-                run += c;
-            }
-            b->recv_cnt[p] = run - b->recv_off[p];
-        }
-        for (uint32_t k = 0; k < NB1; ++k) vstart[k + 1] = vstart[k] + bucket_tot[k];
-        b->n_local = run;
-        ensure_local(b, run);
+        const RecvPlan rp = plan_recv(rc.data(), W, NB1);
+        b->recv_off = rp.off;
+        b->recv_cnt = rp.n;
+        b->n_local = rp.total;
+        ensure_local(b, rp.total);
         b->d_seg_start.ensure(8ull * NB);
         b->d_seg_len.ensure(4ull * NB);
         b->d_vstart.ensure(8ull * (NB1 + 1));
-        SKM_HIP(hipMemcpyAsync(b->d_seg_start.p, seg_start.data(), 8ull * NB, hipMemcpyHostToDevice, b->stream));
-        SKM_HIP(hipMemcpyAsync(b->d_seg_len.p, seg_len.data(), 4ull * NB, hipMemcpyHostToDevice, b->stream));
-        SKM_HIP(hipMemcpyAsync(b->d_vstart.p, vstart.data(), 8ull * (NB1 + 1), hipMemcpyHostToDevice, b->stream));
+        SKM_HIP(hipMemcpy(b->d_seg_start.p, rp.seg_start.data(), 8ull * NB, hipMemcpyHostToDevice));
+        SKM_HIP(hipMemcpy(b->d_seg_len.p, rp.seg_len.data(), 4ull * NB, hipMemcpyHostToDevice));
+        SKM_HIP(hipMemcpy(b->d_vstart.p, rp.vstart.data(), 8ull * (NB1 + 1), hipMemcpyHostToDevice));
         std::vector<uint64_t> so(W), sc(W), ro(W), rcn(W);
         for (int q = 0; q < W; ++q) {
             so[q] = 8 * b->send_off[q];
@@ -4136,8 +4232,8 @@ static void check_transport(skm_build* b) {
 #else
     const bool comm = false;
 #endif
-    SKM_CHECK(b->world == 1 || comm || !b->group.empty(), SKM_E_STATE,
-              "world_size > 1 needs skm_build_set_comm (or skm_build_group_run) first");
+    SKM_CHECK(b->world == 1 || comm || !b->group.empty() || b->tp.alltoallv, SKM_E_STATE,
+              "world_size > 1 needs skm_build_set_comm, skm_build_set_transport or skm_build_group_run first");
 }
 
 int skm_build_prepare(skm_build* b) {
@@ -4184,6 +4280,87 @@ int skm_comm_unique_id(uint8_t id[128]) {
     std::memset(id, 0, 128);
     throw Error(SKM_E_COMM, "libskm was built without RCCL");
 #endif
+    SKM_API_END
+}
+
+int skm_build_set_transport(skm_build* b, const skm_transport* tp) {
+    SKM_API_BEGIN
+    SKM_CHECK(b && tp && tp->alltoallv && tp->allreduce && tp->allgatherv, SKM_E_ARG, "incomplete transport");
+#if defined(SKM_WITH_RCCL)
+    SKM_CHECK(b->comm == nullptr, SKM_E_STATE, "an RCCL communicator is already set");
+#endif
+    b->tp = *tp;
+    SKM_API_END
+}
+
+int skm_debug_exchange_plan(const skm_transport* tp, int rank, int world, uint32_t nb1, const uint64_t* bucket_starts,
+                            uint64_t* recv_off, uint64_t* recv_cnt, uint64_t* vstart) {
+    SKM_API_BEGIN
+    SKM_CHECK(tp && tp->alltoallv && bucket_starts && recv_off && recv_cnt && vstart && world >= 1 && rank >= 0 &&
+                  rank < world && nb1 >= 1, SKM_E_ARG, "bad argument");
+    const SendPlan sp = plan_send(bucket_starts, world, nb1);
+    std::vector<uint64_t> off(world), c(world, 4ull * nb1);
+    for (int q = 0; q < world; ++q) off[q] = 4ull * nb1 * q;
+    std::vector<uint32_t> rc((uint64_t)world * nb1);
+    tp_alltoallv_host(*tp, world, reinterpret_cast<const uint8_t*>(sp.cnt.data()), off, c,
+                      reinterpret_cast<uint8_t*>(rc.data()), off, c);
+    const RecvPlan rp = plan_recv(rc.data(), world, nb1);
+    for (int q = 0; q < world; ++q) {
+        recv_off[q] = rp.off[q];
+        recv_cnt[q] = rp.n[q];
+    }
+    for (uint32_t k = 0; k <= nb1; ++k) vstart[k] = rp.vstart[k];
+    SKM_API_END
+}
+
+int skm_debug_transport_check(const skm_transport* tp, int rank, int world) {
+    SKM_API_BEGIN
+    SKM_CHECK(tp && tp->alltoallv && tp->allreduce && tp->allgatherv && world >= 1 && rank >= 0 && rank < world,
+              SKM_E_ARG, "bad argument");
+    // allreduce: u32 sums wrap mod 2^32, u8 max
+    std::vector<uint32_t> u(1000);
+    for (uint32_t i = 0; i < u.size(); ++i) u[i] = 0x80000000u + (uint32_t)rank * 7u + i;
+    tp_check(tp->allreduce(tp->ctx, u.data(), u.size(), 0), "allreduce");
+    for (uint32_t i = 0; i < u.size(); ++i) {
+        uint32_t want = 0;
+        for (int r = 0; r < world; ++r) want += 0x80000000u + (uint32_t)r * 7u + i;
+        SKM_CHECK(u[i] == want, SKM_E_COMM, "allreduce(u32 sum) mismatch");
+    }
+    std::vector<uint8_t> m(300);
+    for (uint32_t i = 0; i < m.size(); ++i) m[i] = (uint8_t)((i * 31u + (uint32_t)rank * 101u) & 0xFFu);
+    tp_check(tp->allreduce(tp->ctx, m.data(), m.size(), 1), "allreduce");
+    for (uint32_t i = 0; i < m.size(); ++i) {
+        uint8_t want = 0;
+        for (int r = 0; r < world; ++r) want = std::max<uint8_t>(want, (uint8_t)((i * 31u + (uint32_t)r * 101u) & 0xFFu));
+        SKM_CHECK(m[i] == want, SKM_E_COMM, "allreduce(u8 max) mismatch");
+    }
+    // allgatherv: rank r contributes 3r + 1 bytes of value r + 1
+    std::vector<uint64_t> bytes(world), o(world + 1, 0);
+    for (int r = 0; r < world; ++r) {
+        bytes[r] = 3u * r + 1u;
+        o[r + 1] = o[r] + bytes[r];
+    }
+    std::vector<uint8_t> mine(bytes[rank], (uint8_t)(rank + 1)), all(o[world]);
+    tp_check(tp->allgatherv(tp->ctx, mine.data(), all.data(), bytes.data()), "allgatherv");
+    for (int r = 0; r < world; ++r)
+        for (uint64_t j = o[r]; j < o[r + 1]; ++j) SKM_CHECK(all[j] == (uint8_t)(r + 1), SKM_E_COMM, "allgatherv mismatch");
+    // alltoallv: rank p sends p*16 + q + 1 bytes of value (p * world + q) & 0xFF to rank q
+    std::vector<uint64_t> sc(world), so(world), rcn(world), ro(world);
+    uint64_t st = 0, rt = 0;
+    for (int q = 0; q < world; ++q) {
+        sc[q] = (uint64_t)rank * 16 + q + 1;
+        so[q] = st;
+        st += sc[q];
+        rcn[q] = (uint64_t)q * 16 + rank + 1;
+        ro[q] = rt;
+        rt += rcn[q];
+    }
+    std::vector<uint8_t> sb(st), rb(rt, 0xEE);
+    for (int q = 0; q < world; ++q) std::memset(sb.data() + so[q], (rank * world + q) & 0xFF, sc[q]);
+    tp_check(tp->alltoallv(tp->ctx, sb.data(), sc.data(), so.data(), rb.data(), rcn.data(), ro.data()), "alltoallv");
+    for (int p = 0; p < world; ++p)
+        for (uint64_t j = 0; j < rcn[p]; ++j)
+            SKM_CHECK(rb[ro[p] + j] == (uint8_t)((p * world + rank) & 0xFF), SKM_E_COMM, "alltoallv mismatch");
     SKM_API_END
 }
 

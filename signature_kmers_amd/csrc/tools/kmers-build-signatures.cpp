@@ -12,6 +12,15 @@
 // as sets.  --nudb-file is not supported (NuDB is out of scope).
 // Extra options: --device N (HIP device), --dump-extract FILE (write the build input arrays and
 // stop before touching the GPU; used by the CPU tests), --mph-seed N.
+// Multi-GPU: --n-gpus N forks one process per GPU (rank r on device r) before
+// any GPU or thread use; or, under an external launcher (RANK / WORLD_SIZE / LOCAL_RANK in the
+// environment, e.g. torchrun --no-python), each launched process is one rank and rank 0 hands the
+// RCCL unique id to the others through --comm-file (default <kmer-data-dir>/.skm_comm_id).
+// Every rank parses all inputs (the FunctionMap needs every file), builds the contiguous range of
+// files r*F/N .. (r+1)*F/N, the ranks exchange occurrences by owner GPU (RCCL all-to-all) and
+// rank 0 gathers the kept k-mers and writes every output, exactly as one process would.
+// --comm host joins the forked ranks through socketpairs instead of RCCL (several ranks may then
+// share one GPU: --device is every rank's device; used by the tests).
 #include <sys/stat.h>
 
 #include <chrono>
@@ -26,6 +35,7 @@
 #include "skm.h"
 #include "skm_caller.h"
 #include "skm_front.h"
+#include "skm_mesh.h"
 
 using namespace skmf;
 
@@ -93,7 +103,9 @@ int main(int argc, char** argv) {
                 {"final-kmers", 0, false, false},      {"n-threads", 0, false, false},
                 {"perfect-hash", 0, false, false},     {"perfect-hash-data", 0, false, false},
                 {"help", 'h', true, false},            {"device", 0, false, false},
-                {"dump-extract", 0, false, false},     {"mph-seed", 0, false, false}};
+                {"dump-extract", 0, false, false},     {"mph-seed", 0, false, false},
+                {"n-gpus", 0, false, false},           {"comm", 0, false, false},
+                {"comm-file", 0, false, false}};
     std::string err;
     if (!op.parse(argc, argv, err)) die(err);
     if (op.has("help")) {
@@ -112,14 +124,38 @@ int main(int argc, char** argv) {
                   << "  --perfect-hash arg                   Compute perfect hash of signature kmers and store in this file\n"
                   << "  --perfect-hash-data arg              Kmer data stored by perfect hash\n"
                   << "  --device arg                         HIP device ordinal (default 0)\n"
+                  << "  --n-gpus arg                         ranks (one process and GPU each, power of two)\n"
+                  << "  --comm arg                           rccl (default) or host (socketpairs; ranks may share a GPU)\n"
+                  << "  --comm-file arg                      RCCL id rendezvous file under an external launcher\n"
                   << "  -h [ --help ]                        show this help message\n";
         return 1;
     }
     const double t_start = now_s();
+    // ranks: forked here (before any thread or GPU use), or given by an external launcher
+    Mesh mesh;
+    const std::string comm = op.get("comm", "rccl");
+    if (comm != "rccl" && comm != "host") die("--comm must be rccl or host");
+    const char* env_ws = std::getenv("WORLD_SIZE");
+    const bool launched = env_ws && std::atoi(env_ws) > 1 && !op.has("n-gpus");
+    int local_rank = 0;
+    if (launched) {
+        if (comm == "host") die("--comm host needs --n-gpus (forked ranks)");
+        mesh.world = std::atoi(env_ws);
+        mesh.rank = std::atoi(std::getenv("RANK") ? std::getenv("RANK") : "0");
+        local_rank = std::atoi(std::getenv("LOCAL_RANK") ? std::getenv("LOCAL_RANK") : "0");
+    } else {
+        const int ng = std::atoi(op.get("n-gpus", "1").c_str());
+        if (ng < 1 || ng > 64 || (ng & (ng - 1))) die("--n-gpus must be a power of two in [1, 64]");
+        if (!mesh_fork(ng, mesh, err)) die(err);
+        local_rank = mesh.rank;
+    }
+    const int rank = mesh.rank, world = mesh.world;
+    if (rank != 0 && !std::freopen("/dev/null", "w", stdout)) die("cannot silence rank stdout");
     // host threads for parsing / find_best_call only: results never depend on it
     int n_threads = std::atoi(op.get("n-threads", "0").c_str());
     if (n_threads < 2) n_threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    const int device = std::atoi(op.get("device", "0").c_str());
+    if (world > 1) n_threads = std::max(1, n_threads / std::min(world, 8));
+    const int device = std::atoi(op.get("device", "0").c_str()) + (world > 1 && comm == "rccl" ? local_rank : 0);
     const int min_reps_required = std::atoi(op.get("min-reps-required", "3").c_str());
     const std::string kmer_data_dir = op.get("kmer-data-dir");
     std::string final_kmers = op.get("final-kmers");
@@ -196,8 +232,10 @@ int main(int argc, char** argv) {
     for (size_t f = 0; f < files.size(); ++f)
         select_build_sequences(fm, files[f], (unsigned)f, MaxSequencesPerFile, deleted_fids, batches[f]);
     if (op.has("dump-extract")) {
+        if (rank != 0) return 0;
         dump_extract(op.get("dump-extract"), files, batches);
         std::cerr << "wrote build input to " << op.get("dump-extract") << "\n";
+        if (!mesh.wait_children(err)) die(err);
         return 0;
     }
 
@@ -207,13 +245,29 @@ int main(int argc, char** argv) {
     bo.max_seqs_per_file = MaxSequencesPerFile;
     bo.n_functions = std::max(1u, nkept_f);
     bo.canonical_order = 1;
-    bo.rank = 0;
-    bo.world_size = 1;
+    bo.rank = rank;
+    bo.world_size = world;
     auto check = [](int rc, const char* what) {
         if (rc) die(std::string(what) + ": " + skm_last_error());
     };
     check(skm_build_create(&b, &device, 1, &bo), "skm_build_create");
-    for (size_t f = 0; f < files.size(); ++f) {
+    // this rank's contiguous range of files (global file numbering keeps seq_id = file*100000+k)
+    const size_t f0 = files.size() * (size_t)rank / (size_t)world, f1 = files.size() * (size_t)(rank + 1) / (size_t)world;
+    skm_transport tp = mesh.transport();
+    if (world > 1 && comm == "host") {
+        check(skm_build_set_transport(b, &tp), "skm_build_set_transport");
+    } else if (world > 1) {
+        uint8_t id[128] = {0};
+        if (rank == 0) check(skm_comm_unique_id(id), "skm_comm_unique_id");
+        if (launched) {
+            const std::string cf = op.get("comm-file", path_join(kmer_data_dir.empty() ? "." : kmer_data_dir, ".skm_comm_id"));
+            if (!file_rendezvous(cf, rank, id, 300.0, err)) die(err);
+        } else if (!mesh.share_id(id, err)) {
+            die(err);
+        }
+        check(skm_build_set_comm(b, id), "skm_build_set_comm");
+    }
+    for (size_t f = f0; f < f1; ++f) {
         const BuildBatch& bb = batches[f];
         if (bb.off.empty()) continue;
         check(skm_build_add_batch(b, files[f].residues.data(), bb.off.data(), bb.len.data(), bb.func.data(),
@@ -229,6 +283,10 @@ int main(int argc, char** argv) {
     int nph = skm_build_last_timings(b, ph, 12);
     const double t_build = now_s() - t0;
     skm_build_destroy(b);
+    if (rank != 0) {  // rank 0 holds every kept k-mer and the all-reduced statistics
+        skm_kept_free(&kept);
+        return 0;
+    }
     std::cout << "Kept " << kept.n << " kmers\n";
     std::cout << "distinct_signatures=" << kept.distinct_signatures << "\n";
     std::cout << "num_seqs_with_a_signature=" << kept.n_seqs_with_signature << "\n";
@@ -326,6 +384,7 @@ int main(int argc, char** argv) {
         final_kmers_thread.join();
     }
     skm_kept_free(&kept);
+    if (!mesh.wait_children(err)) die(err);
     std::cerr << "timing: parse " << t_parse << " s, build " << t_build << " s (device pipeline "
               << (nph > 7 ? ph[7] : 0.0f) << " ms), recall " << t_recall << " s, total " << now_s() - t_start << " s\n";
     std::cerr << "all done\n";
