@@ -164,6 +164,9 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value);
 int skm_build_debug_stamps(skm_build* b, int enable, uint64_t* out, int cap);
 /* Diagnostics: lengths of the first cap chain jobs in execution order (longest first). */
 int skm_build_debug_jobs(skm_build* b, uint32_t* out, int cap);
+/* Diagnostics: element counts of the last pass's overflow sub-buckets (largest first); returns
+ * how many there are (at most cap written). */
+int skm_build_debug_overflow(skm_build* b, uint32_t* out, int cap);
 /* Diagnostics: device time of the chain kernel on njobs synthetic jobs of length n
  * (mode 0: the build's choice by length, 1: one lane per chain, 2: one wave pair per chain). */
 int skm_debug_chain_bench(uint32_t n, uint32_t njobs, int mode, float* ms);
@@ -244,7 +247,8 @@ typedef struct skm_annot_opts {
     int32_t ignore_hypo;   /* --ignore-hypo                                                */
     int32_t hypo_index;    /* index of "hypothetical protein" in function.index           */
     int32_t mean_mode;     /* Boost.Math mean: 0 = >=1.76 four-lane (default), 1 = <=1.75  */
-    int32_t mad_mode;      /* 0 = |x(mid)-median| (the only mode on the device)            */
+    int32_t mad_mode;      /* MAD: 0 = |x(mid)-median| (>=1.76), 1 = |x(mid)| (older Boost,  */
+                           /* libstdc++ nth_element order)                      */
 } skm_annot_opts;
 
 typedef struct skm_calls {

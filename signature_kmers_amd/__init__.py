@@ -95,6 +95,7 @@ _SIGS = {
     "skm_debug_transport_check": (C.c_int, [C.POINTER(_Transport), C.c_int, C.c_int]),
     "skm_build_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
     "skm_build_debug_jobs": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int]),
+    "skm_build_debug_overflow": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int]),
     "skm_debug_chain_bench": (C.c_int, [C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_float)]),
     "skm_debug_chain_eval": (C.c_int, [_P, C.c_uint32, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "skm_build_debug_stamps": (C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64), C.c_int]),
@@ -295,6 +296,12 @@ class SignatureBuilder:
         v = (C.c_uint32 * k)()
         _check(lib().skm_build_debug_jobs(self._h, v, k))
         return [int(x) for x in v]
+
+    def debug_overflow(self, k: int = 4096) -> list:
+        """Element counts of the last pass's overflow sub-buckets, largest first."""
+        v = (C.c_uint32 * k)()
+        n = lib().skm_build_debug_overflow(self._h, v, k)
+        return [int(x) for x in v[:min(max(n, 0), k)]]
 
     def debug_stamps(self, enable: bool) -> list:
         v = (C.c_uint64 * 32)()
@@ -574,7 +581,10 @@ class FunctionCaller:
     state machine on the GPU and find_best_call on the host."""
 
     def __init__(self, db: CmphKmerDb, function_index, min_hits: int = 5, max_gap: int = 200,
-                 mean_mode: int = 0):
+                 mean_mode: int = 0, mad_mode: int = 0):
+        """mean_mode / mad_mode: the Boost.Math the reference was compiled against
+        (call_functions.tcc:51-53): 0 / 0 = >= 1.76 (four-lane mean, |x(mid) - median| MAD),
+        1 / 1 = the older single running mean and the MAD that returns |x(mid)|."""
         self.db = db
         self.function_index = read_function_index(function_index) if isinstance(function_index, str) \
             else list(function_index)
@@ -582,6 +592,7 @@ class FunctionCaller:
         self.max_gap = max_gap
         self.ignore_hypothetical_ = False
         self.mean_mode = mean_mode
+        self.mad_mode = mad_mode
         try:
             self.hypo_index = self.function_index.index("hypothetical protein")
         except ValueError:
@@ -593,7 +604,7 @@ class FunctionCaller:
 
     def _opts(self):
         return _AnnotOpts(self.min_hits, self.max_gap, 1 if self.ignore_hypothetical_ else 0, self.hypo_index,
-                          self.mean_mode, 0)
+                          self.mean_mode, self.mad_mode)
 
     def process_seqs(self, residues, seq_off, seq_len):
         """process_aa_seq for a batch: returns (call_off u64[n+1], calls CALL_DTYPE)."""

@@ -36,6 +36,15 @@ bool read_function_index(const std::string& path, std::vector<std::string>& tabl
     return true;
 }
 
+namespace {
+int g_mean_mode = 0, g_mad_mode = 0;
+}
+
+void set_boost_math_modes(int mean_mode, int mad_mode) {
+    g_mean_mode = mean_mode;
+    g_mad_mode = mad_mode;
+}
+
 int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std::vector<std::string>& function_index,
                bool ignore_hypo, int n_threads, std::vector<std::vector<SeqCall>>& out, std::string& err,
                double* device_ms, uint64_t max_batch_residues) {
@@ -49,8 +58,8 @@ int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std
     o.max_gap = 200;
     o.ignore_hypo = ignore_hypo ? 1 : 0;
     o.hypo_index = (int32_t)(hit - function_index.begin());
-    o.mean_mode = 0;
-    o.mad_mode = 0;
+    o.mean_mode = g_mean_mode;
+    o.mad_mode = g_mad_mode;
     std::vector<const char*> fidx(function_index.size());
     for (size_t i = 0; i < function_index.size(); ++i) fidx[i] = function_index[i].c_str();
 

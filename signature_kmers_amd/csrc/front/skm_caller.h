@@ -21,6 +21,12 @@ struct SeqCall {
 // name; the table is sized max index + 1.
 bool read_function_index(const std::string& path, std::vector<std::string>& table, std::string& err);
 
+// Boost.Math statistics the reference was compiled against (call_functions.tcc:51-53; SURVEY
+// A.6): mean_mode 0 = the >= 1.76 four-lane mean, 1 = the single running mean; mad_mode 0 =
+// |x(mid) - median|, 1 = the older median_absolute_deviation that returns |x(mid)|.  Process-wide
+// setting for call_files (the CLIs' --boost-math-stats option); default 0 / 0.
+void set_boost_math_modes(int mean_mode, int mad_mode);
+
 // Query every sequence of every file (in order) against db.  out[f][r] is the call for record r
 // of file f.  Files are batched so one device batch holds <= max_batch_residues residues.
 int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std::vector<std::string>& function_index,

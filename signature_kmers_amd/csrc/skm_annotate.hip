@@ -25,6 +25,7 @@
 #include "skm_bdz.h"
 #include "skm_common.h"
 #include "skm_lookup.h"
+#include "skm_select.h"
 #include "skm_util.h"
 
 namespace skm {
@@ -154,7 +155,7 @@ struct CallArgs {
     skm_kmer_call* slots;
     uint32_t* counts;           // [nseq]
     uint32_t nseq;
-    int min_hits, max_gap, ignore_hypo, mean_mode;
+    int min_hits, max_gap, ignore_hypo, mean_mode, mad_mode;
     uint32_t hypo;
 };
 
@@ -262,25 +263,28 @@ __device__ void hitset_process(const CallArgs& A, const uint32_t* hit, uint16_t*
         }
         mean = (num1 * (mu[0] + mu[1] + mu[2]) + num2 * mu[3]) / float(n);
     }
-    heap_sort_u16(scr, n);
-    float median;
-    uint32_t C2;
-    if (n & 1) {
-        const uint32_t m = scr[(n - 1) / 2];
-        median = (float)m;
-        C2 = 2u * m;
+    float median, mad;
+    if (A.mad_mode == 1) {
+        legacy_median_mad(scr, n, median, mad);
     } else {
-        const uint32_t a = scr[n / 2 - 1], b = scr[n / 2];
-        median = ((float)a + (float)b) / 2;
-        C2 = a + b;
-    }
-    float mad;
-    if (n & 1) {
-        mad = (float)kth_dev(scr, n, C2, (n - 1) / 2) * 0.5f;
-    } else {
-        const float d1 = (float)kth_dev(scr, n, C2, n / 2 - 1) * 0.5f;
-        const float d2 = (float)kth_dev(scr, n, C2, n / 2) * 0.5f;
-        mad = (d1 + d2) / 2.0f;
+        heap_sort_u16(scr, n);
+        uint32_t C2;
+        if (n & 1) {
+            const uint32_t m = scr[(n - 1) / 2];
+            median = (float)m;
+            C2 = 2u * m;
+        } else {
+            const uint32_t a = scr[n / 2 - 1], b = scr[n / 2];
+            median = ((float)a + (float)b) / 2;
+            C2 = a + b;
+        }
+        if (n & 1) {
+            mad = (float)kth_dev(scr, n, C2, (n - 1) / 2) * 0.5f;
+        } else {
+            const float d1 = (float)kth_dev(scr, n, C2, n / 2 - 1) * 0.5f;
+            const float d2 = (float)kth_dev(scr, n, C2, n / 2) * 0.5f;
+            mad = (d1 + d2) / 2.0f;
+        }
     }
     if (mad == 0) mad = 30;
     const double cutoff_b = (double)mean - 2.0 * (double)mad;
@@ -471,6 +475,27 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
         const float num2 = num1 + float(n % 4);
         mean = (num1 * (m0 + m1 + m2) + num2 * m3) / float(n);
     }
+    auto emit = [&](float median, float mad) {
+        if (mad == 0) mad = 30;
+        const double cutoff_b = (double)mean - 2.0 * (double)mad;
+        const double cutoff_t = (double)mean + 2.0 * (double)mad;
+        skm_kmer_call c;
+        c.start = first;
+        c.end = last_cur + 7u;
+        c.count = ((int)n >= A.min_hits && !(seqlen < cutoff_b || seqlen > cutoff_t)) ? (int32_t)n : -1;
+        c.function_index = (uint16_t)cur;
+        c.pad = 0;
+        c.protein_length_median = (uint32_t)median;
+        c.protein_length_med_avg_dev = mad;
+        out[j] = c;
+    };
+    if (A.mad_mode == 1) {  // the <= 1.75 MAD: libstdc++ selection order on the hit-order run
+        if (lane != 0) return;
+        float median, mad;
+        legacy_median_mad(buf, n, median, mad);
+        emit(median, mad);
+        return;
+    }
     // bitonic sort of buf[0..P), P = next power of two >= n, padded with the maximum
     uint32_t P = 1;
     while (P < n) P <<= 1;
@@ -511,18 +536,7 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
         const float d2 = (float)kth_dev_sorted(buf, n, C2, n / 2) * 0.5f;
         mad = (d1 + d2) / 2.0f;
     }
-    if (mad == 0) mad = 30;
-    const double cutoff_b = (double)mean - 2.0 * (double)mad;
-    const double cutoff_t = (double)mean + 2.0 * (double)mad;
-    skm_kmer_call c;
-    c.start = first;
-    c.end = last_cur + 7u;
-    c.count = ((int)n >= A.min_hits && !(seqlen < cutoff_b || seqlen > cutoff_t)) ? (int32_t)n : -1;
-    c.function_index = (uint16_t)cur;
-    c.pad = 0;
-    c.protein_length_median = (uint32_t)median;
-    c.protein_length_med_avg_dev = mad;
-    out[j] = c;
+    emit(median, mad);
 }
 
 // calls kept per sequence (segment results with count >= 0)
@@ -831,6 +845,7 @@ void query_run(skm_query* q, const skm_annot_opts* o) {
         A.max_gap = o->max_gap;
         A.ignore_hypo = o->ignore_hypo && o->hypo_index >= 0;
         A.mean_mode = o->mean_mode;
+        A.mad_mode = o->mad_mode;
         A.hypo = o->hypo_index >= 0 ? (uint32_t)o->hypo_index : 0xFFFFFFFFu;
         SKM_HIP(hipEventRecord(q->ev[2], st));
         hipLaunchKernelGGL(k_calls_scan, dim3(ceil_div(ns, 64)), dim3(64), 0, st, A, q->d_slots.as<uint4>());
@@ -1065,7 +1080,8 @@ int skm_query_create(skm_query** out, skm_db* db, const uint8_t* residues, const
 int skm_query_run(skm_query* q, const skm_annot_opts* opts) {
     SKM_API_BEGIN
     SKM_CHECK(q && opts, SKM_E_ARG, "null argument");
-    SKM_CHECK(opts->mad_mode == 0, SKM_E_ARG, "device path implements mad_mode 0 only");
+    SKM_CHECK(opts->mean_mode == 0 || opts->mean_mode == 1, SKM_E_ARG, "mean_mode must be 0 or 1");
+    SKM_CHECK(opts->mad_mode == 0 || opts->mad_mode == 1, SKM_E_ARG, "mad_mode must be 0 or 1");
     SKM_CHECK(opts->min_hits >= 1 && opts->max_gap >= 0, SKM_E_ARG, "invalid min_hits / max_gap");
     query_run(q, opts);
     SKM_API_END

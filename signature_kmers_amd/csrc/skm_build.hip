@@ -2642,14 +2642,19 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
     __shared__ uint64_t s_inl[OVF_INLINE_CAP][2];  // lens offset, n << 32 | output index
     if (threadIdx.x == 0) s_ninl = 0;
     const OvfEntry e = A.ovf[blockIdx.x];
-    const uint64_t* src_hi = (e.src ? A.tmp_hi : A.recs_hi) + e.off;
-    const uint64_t* src_lo = (e.src ? A.tmp_lo : A.recs_lo) + e.off;
+    if (e.n == 0) return;  // every key of the sub-bucket went to k_heavy
+    // src 2: the light remainder k_ovf_split compacted into this entry's own scratch (sorted in
+    // place: each chunk is loaded whole before it is written back)
+    const uint64_t* src_hi = (e.src == 2 ? S.hi : e.src ? A.tmp_hi : A.recs_hi) + e.off;
+    const uint64_t* src_lo = (e.src == 2 ? S.lo : e.src ? A.tmp_lo : A.recs_lo) + e.off;
     uint64_t* ghi = S.hi + e.scratch;
     uint64_t* glo = S.lo + e.scratch;
     uint32_t* heads = S.heads + e.scratch;
     uint64_t* jobinfo = S.jobinfo + e.scratch;
     uint32_t* fmean = S.fmean + e.scratch;
-    const uint32_t N = e.npad, n = e.n;
+    const uint32_t n = e.n;
+    uint32_t N = CAP;  // the network size: pow2 >= n, at least one chunk (<= the entry's scratch)
+    while (N < n) N <<= 1;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint64_t hprefix = (uint64_t)(A.bucket_base + e.bucket) << A.rem_bits;
     // phase 0: chunks of CAP sorted ascending in LDS.  The padding beyond n holds the maximum
@@ -2881,6 +2886,382 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Heavy keys.  An overflow sub-bucket is oversized because a few k-mers occur thousands of times
+// (at C3, single k-mers reach ~10^6 occurrences); sorting such a sub-bucket by (key, function,
+// ordinal) with a one-workgroup global bitonic network costs O(n log^2 n) passes.  The large
+// sub-buckets are split first (k_ovf_split): an LDS table counts each key's occurrences, keys of
+// >= HEAVY_MIN occurrences are copied out to their own contiguous range (k_heavy), the rest (the
+// "light" keys, ~SUB_TARGET elements) is compacted in place of the sub-bucket's scratch and runs
+// through k_overflow as before, now mostly as a single LDS chunk.
+//
+// A heavy key needs no sort by (function, ordinal) (process_kmer_set, signature_build.tcc:219-293):
+//   - best function: a function with >= 80 % of the occurrences is the strict majority, so the
+//     Boyer-Moore candidate plus an exact count decides the cut (fp32, as everywhere);
+//   - avg_from_end (upper median of the offsets), the u16 length sum, the signature flags: order-free;
+//   - the P^2 median / variance samples are the best-function members' protein lengths in visit
+//     (reverse ordinal) order; the ordinal is (sequence, window) and every member of one sequence
+//     contributes the same length, so the samples are glen[s] over the members' sequence indices
+//     sorted descending -- a u32 radix sort, not a 16-byte sort.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t HEAVY_MIN = 1024;        // occurrences that make a key heavy
+constexpr uint32_t SPLIT_MIN = 4096;        // overflow sub-buckets of at least this size are split
+constexpr uint32_t SPLIT_TAB = 4096;        // LDS key table slots (load <= ~0.5 at SUB_TARGET)
+constexpr uint32_t SPLIT_MAXH = 256;        // heavy keys taken out of one sub-bucket (more stay light)
+constexpr uint32_t HEAVY_WG = 512;
+constexpr uint32_t HEAVY_GRID = 512;        // k_heavy: persistent workgroups looping over the keys
+
+struct HeavyKey {
+    uint64_t off;       // first element in the heavy arrays
+    uint32_t n;         // occurrences
+    uint32_t bucket;    // level-1 bucket of its sub-bucket
+    uint32_t rem;       // the key's low hash bits (group key)
+    uint32_t pad;
+};
+
+struct HeavyArgs {
+    HeavyKey* keys;
+    unsigned long long* nkeys;    // device counters (cleared per pass)
+    unsigned long long* cursor;
+    uint64_t* hi;                 // heavy elements, key-contiguous
+    uint64_t* lo;
+    uint32_t* s0;                 // radix-sort ping-pong of the best members' sequence indices
+    uint32_t* s1;
+};
+
+__device__ __forceinline__ uint32_t split_hash(uint32_t rem) { return (rem * 0x9E3779B1u) >> (32 - 12); }
+
+// One workgroup per overflow entry of >= SPLIT_MIN elements (the first entries of the sorted list).
+__global__ __launch_bounds__(BP_THREADS) void k_ovf_split(BucketArgs A, OvfScratch S, HeavyArgs H) {
+    static_assert(SPLIT_TAB == 4096, "split_hash yields 12 bits");
+    __shared__ uint32_t s_key[SPLIT_TAB];
+    __shared__ uint32_t s_cnt[SPLIT_TAB];
+    __shared__ uint16_t s_hid[SPLIT_TAB];
+    __shared__ uint64_t s_hbase[SPLIT_MAXH];
+    __shared__ uint32_t s_hcur[SPLIT_MAXH];
+    __shared__ uint32_t s_nh, s_fail, s_lcur, s_heavy;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x, lane = tid & 63u;
+    OvfEntry e = A.ovf[blockIdx.x];
+    const uint64_t* src_hi = (e.src ? A.tmp_hi : A.recs_hi) + e.off;
+    const uint64_t* src_lo = (e.src ? A.tmp_lo : A.recs_lo) + e.off;
+    const uint32_t n = e.n;
+    constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+    for (uint32_t q = tid; q < SPLIT_TAB; q += nt) {
+        s_key[q] = EMPTY;
+        s_cnt[q] = 0;
+        s_hid[q] = 0xFFFFu;
+    }
+    if (tid == 0) {
+        s_nh = 0;
+        s_fail = 0;
+        s_lcur = 0;
+        s_heavy = 0;
+    }
+    __syncthreads();
+    // ---- 1. occurrences per key (wave-aggregated for the lanes sharing lane 0's key) ----
+    for (uint32_t j0 = 0; j0 < n; j0 += nt) {
+        const uint32_t j = j0 + tid;
+        const bool v = j < n;
+        const uint32_t rem = v ? (uint32_t)(src_hi[j] >> 16) & REM_MASK : EMPTY;
+        const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)rem);
+        const uint64_t same = __ballot(v && rem == r0);
+        const bool lead = v && rem == r0 && lane == (uint32_t)(__ffsll((long long)same) - 1);
+        if (v && (rem != r0 || lead)) {
+            uint32_t slot = split_hash(rem), probe = 0;
+            for (; probe < SPLIT_TAB; ++probe) {
+                const uint32_t k = s_key[slot];
+                if (k == rem) break;
+                if (k == EMPTY) {
+                    const uint32_t old = atomicCAS(&s_key[slot], EMPTY, rem);
+                    if (old == EMPTY || old == rem) break;
+                }
+                slot = (slot + 1) & (SPLIT_TAB - 1);
+            }
+            if (probe == SPLIT_TAB)
+                s_fail = 1;
+            else
+                atomicAdd(&s_cnt[slot], lead ? (uint32_t)__popcll(same) : 1u);
+        }
+    }
+    __syncthreads();
+    if (s_fail) return;  // more distinct keys than the table holds: the entry keeps the sort path
+    // ---- 2. heavy keys: their own ranges in the heavy arrays ----
+    for (uint32_t q = tid; q < SPLIT_TAB; q += nt)
+        if (s_cnt[q] >= HEAVY_MIN) {
+            const uint32_t h = atomicAdd(&s_nh, 1u);
+            if (h < SPLIT_MAXH) {
+                s_hid[q] = (uint16_t)h;
+                s_hcur[h] = 0;
+                const uint64_t hk = atomicAdd(H.nkeys, 1ull);
+                const uint64_t base = atomicAdd(H.cursor, (unsigned long long)s_cnt[q]);
+                s_hbase[h] = base;
+                HeavyKey K;
+                K.off = base;
+                K.n = s_cnt[q];
+                K.bucket = e.bucket;
+                K.rem = s_key[q];
+                K.pad = 0;
+                H.keys[hk] = K;
+                atomicAdd(&s_heavy, s_cnt[q]);
+            }
+        }
+    __syncthreads();
+    if (s_heavy == 0) return;  // nothing heavy: unchanged
+    // ---- 3. scatter: heavy members to their key's range, the rest compacted into the scratch ----
+    uint64_t* lhi = S.hi + e.scratch;
+    uint64_t* llo = S.lo + e.scratch;
+    for (uint32_t j0 = 0; j0 < n; j0 += nt) {
+        const uint32_t j = j0 + tid;
+        const bool v = j < n;
+        uint64_t eh = 0, el = 0;
+        uint32_t hid = 0xFFFFu;
+        if (v) {
+            eh = src_hi[j];
+            el = src_lo[j];
+            const uint32_t rem = (uint32_t)(eh >> 16) & REM_MASK;
+            uint32_t slot = split_hash(rem);
+            while (s_key[slot] != rem) slot = (slot + 1) & (SPLIT_TAB - 1);
+            hid = s_hid[slot];
+        }
+        // light members: wave-aggregated cursor
+        const uint64_t lm = __ballot(v && hid == 0xFFFFu);
+        uint32_t lbase = 0;
+        if (lm) {
+            const uint32_t leader = (uint32_t)(__ffsll((long long)lm) - 1);
+            if (lane == leader) lbase = atomicAdd(&s_lcur, (uint32_t)__popcll(lm));
+            lbase = (uint32_t)__shfl((int)lbase, (int)leader, 64);
+        }
+        if (v && hid == 0xFFFFu) {
+            const uint32_t pos = lbase + (uint32_t)__popcll(lm & ((1ull << lane) - 1ull));
+            lhi[pos] = eh;
+            llo[pos] = el;
+        }
+        // heavy members: aggregated for the lanes sharing lane 0's key
+        const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(v ? hid : 0xFFFFu));
+        const uint64_t hm = __ballot(v && hid != 0xFFFFu && hid == h0);
+        uint32_t hbase = 0;
+        if (hm) {
+            const uint32_t leader = (uint32_t)(__ffsll((long long)hm) - 1);
+            if (lane == leader) hbase = atomicAdd(&s_hcur[h0], (uint32_t)__popcll(hm));
+            hbase = (uint32_t)__shfl((int)hbase, (int)leader, 64);
+        }
+        if (v && hid != 0xFFFFu) {
+            const uint32_t pos = hid == h0 ? hbase + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))
+                                           : atomicAdd(&s_hcur[hid], 1u);
+            const uint64_t o = s_hbase[hid] + pos;
+            H.hi[o] = eh;
+            H.lo[o] = el;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {  // the entry now names its light remainder (in place in its scratch)
+        e.n = n - s_heavy;
+        e.src = 2;
+        e.off = e.scratch;
+        A.ovf[blockIdx.x] = e;
+    }
+}
+
+// Stable LSD radix sort (ascending) of a[0..n) by one workgroup, 8-bit digits over `bits` bits,
+// ping-ponging with b; returns the buffer holding the result.  Items go in rounds of one per
+// thread; a round's rank among equal digits is the wave ballot match plus the lower waves'
+// counts (tagged with the round number, so the count table is never cleared).
+__device__ uint32_t* wg_radix_sort_u32(uint32_t* a, uint32_t* b, uint32_t n, int bits, uint32_t* s_hist,
+                                       uint32_t (*s_wc)[256], uint32_t* s_run, uint32_t& tag) {
+    const uint32_t tid = threadIdx.x, nt = blockDim.x, lane = tid & 63u, wave = tid >> 6, nw = nt >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int shift = 0; shift < bits; shift += 8) {
+        for (uint32_t d = tid; d < 256; d += nt) s_hist[d] = 0;
+        __syncthreads();
+        for (uint32_t j = tid; j < n; j += nt) atomicAdd(&s_hist[(a[j] >> shift) & 255u], 1u);
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t acc = 0;
+            for (uint32_t d = 0; d < 256; ++d) {
+                s_run[d] = acc;
+                acc += s_hist[d];
+            }
+        }
+        __syncthreads();
+        for (uint32_t j0 = 0; j0 < n; j0 += nt) {
+            ++tag;
+            const uint32_t j = j0 + tid;
+            const bool v = j < n;
+            const uint32_t k = v ? a[j] : 0u;
+            const uint32_t d = (k >> shift) & 255u;
+            uint64_t peers = __ballot(v);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint64_t m = __ballot((d >> q) & 1u);
+                peers &= ((d >> q) & 1u) ? m : ~m;
+            }
+            const uint32_t pre = (uint32_t)__popcll(peers & lt);
+            if (v && pre == 0) s_wc[wave][d] = (tag << 7) | (uint32_t)__popcll(peers);
+            __syncthreads();
+            if (v) {
+                uint32_t o = s_run[d] + pre;
+                for (uint32_t w = 0; w < wave; ++w) {
+                    const uint32_t c = s_wc[w][d];
+                    if ((c >> 7) == (tag & 0x1FFFFFFu)) o += c & 127u;
+                }
+                b[o] = k;
+            }
+            __syncthreads();
+            for (uint32_t dd = tid; dd < 256; dd += nt) {
+                uint32_t add = 0;
+                for (uint32_t w = 0; w < nw; ++w) {
+                    const uint32_t c = s_wc[w][dd];
+                    if ((c >> 7) == (tag & 0x1FFFFFFu)) add += c & 127u;
+                }
+                s_run[dd] += add;
+            }
+            __syncthreads();
+        }
+        uint32_t* t = a;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+// One heavy key per workgroup iteration (persistent grid; the key count is read on the device).
+__global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
+    __shared__ uint32_t s_hist[256], s_run[256];
+    __shared__ uint32_t s_wc[HEAVY_WG / 64][256];
+    __shared__ __align__(16) uint32_t s_wave[48];
+    __shared__ uint32_t s_bm[2 * (HEAVY_WG / 64)];
+    __shared__ uint32_t s_cur;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x, lane = tid & 63u, wave = tid >> 6, nw = nt >> 6;
+    const uint32_t nkeys = (uint32_t)*H.nkeys;
+    uint32_t tag = 0;  // round tags of s_wc: 0 is never a live round
+    for (uint32_t q = tid; q < (HEAVY_WG / 64) * 256; q += nt) (&s_wc[0][0])[q] = 0;
+    __syncthreads();
+    for (uint32_t q = blockIdx.x; q < nkeys; q += gridDim.x) {
+        const HeavyKey K = H.keys[q];
+        const uint64_t* hi = H.hi + K.off;
+        const uint64_t* lo = H.lo + K.off;
+        const uint32_t n = K.n;
+        // ---- Boyer-Moore majority function, then its exact count ----
+        uint32_t cand = 0xFFFFFFFFu, cc = 0;
+        for (uint32_t j = tid; j < n; j += nt) {
+            const uint32_t f = (uint32_t)(hi[j] & 0xFFFFu);
+            if (cc == 0) {
+                cand = f;
+                cc = 1;
+            } else if (f == cand) {
+                ++cc;
+            } else {
+                --cc;
+            }
+        }
+        bm_combine(cand, cc);  // over the wave (lane 0 broadcast)
+        if (lane == 0) {
+            s_bm[2 * wave] = cand;
+            s_bm[2 * wave + 1] = cc;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t c0 = s_bm[0], n0 = s_bm[1];
+            for (uint32_t w = 1; w < nw; ++w) {
+                const uint32_t c1 = s_bm[2 * w], n1 = s_bm[2 * w + 1];
+                if (c1 == c0) {
+                    n0 += n1;
+                } else if (n0 >= n1) {
+                    n0 -= n1;
+                } else {
+                    c0 = c1;
+                    n0 = n1 - n0;
+                }
+            }
+            s_bm[0] = c0;
+        }
+        __syncthreads();
+        const uint32_t best_f = s_bm[0];
+        uint32_t cb = 0;
+        for (uint32_t j = tid; j < n; j += nt) cb += (uint32_t)(hi[j] & 0xFFFFu) == best_f;
+        cb = wg_sum(cb, s_wave);
+        if ((float)cb < float(n) * 0.8f) continue;  // cut (uniform); the best run is the majority
+        // ---- flags, u16 length sum and the best members' sequence indices ----
+        if (tid == 0) s_cur = 0;
+        __syncthreads();
+        uint32_t* sa = H.s0 + K.off;
+        uint32_t* sb = H.s1 + K.off;
+        uint32_t sum = 0, smax = 0;
+        for (uint32_t j0 = 0; j0 < n; j0 += nt) {
+            const uint32_t j = j0 + tid;
+            const bool v = j < n;
+            uint32_t s = 0;
+            bool best = false;
+            if (v) {
+                s = (uint32_t)(lo[j] >> 36);
+                A.flags[s] = 1;
+                best = (uint32_t)(hi[j] & 0xFFFFu) == best_f;
+                if (best) {
+                    sum += A.glen[s];
+                    smax = max(smax, s);
+                }
+            }
+            const uint64_t bm = __ballot(best);
+            uint32_t base = 0;
+            if (bm) {
+                const uint32_t leader = (uint32_t)(__ffsll((long long)bm) - 1);
+                if (lane == leader) base = atomicAdd(&s_cur, (uint32_t)__popcll(bm));
+                base = (uint32_t)__shfl((int)base, (int)leader, 64);
+            }
+            if (best) sa[base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] = s;
+        }
+        sum = wg_sum(sum, s_wave);
+        smax = wg_max(smax, s_wave);
+        const uint16_t mean = d2u16((double)(uint16_t)sum / (double)cb);
+        // ---- avg_from_end: the (n/2)-th smallest offset, radix select over two 8-bit digits ----
+        uint32_t k = n / 2, pre = 0;
+        for (int sh = 8; sh >= 0; sh -= 8) {
+            for (uint32_t d = tid; d < 256; d += nt) s_hist[d] = 0;
+            __syncthreads();
+            for (uint32_t j = tid; j < n; j += nt) {
+                const uint32_t o = (uint32_t)(lo[j] & 0xFFFFu);
+                if (sh == 0 && (o >> 8) != (pre >> 8)) continue;
+                atomicAdd(&s_hist[(o >> sh) & 255u], 1u);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t d = 0;
+                while (k >= s_hist[d]) k -= s_hist[d++];
+                s_run[0] = d;
+                s_run[1] = k;
+            }
+            __syncthreads();
+            pre |= s_run[0] << sh;
+            k = s_run[1];
+            __syncthreads();
+        }
+        // ---- samples in visit order: sequence indices descending ----
+        int bits = 0;
+        while (bits < 32 && (smax >> bits)) bits += 8;
+        const uint32_t* sorted = wg_radix_sort_u32(sa, sb, cb, bits, s_hist, s_wc, s_run, tag);
+        __syncthreads();
+        if (tid == 0) {
+            s_run[0] = (uint32_t)atomicAdd(A.kept_ctr, 1ull);
+            atomicAdd(&A.ctr[0], 1ull);
+            s_run[1] = (uint32_t)atomicAdd(&A.ctr[3], 1ull);
+            s_run[2] = (uint32_t)atomicAdd(&A.ctr[4], (unsigned long long)cb);
+        }
+        __syncthreads();
+        const uint32_t o = s_run[0], jb = s_run[1], loff = s_run[2];
+        for (uint32_t t = tid; t < cb; t += nt) A.lens[(uint64_t)loff + t] = A.glen[sorted[cb - 1 - t]];
+        if (tid == 0) {
+            const uint64_t h43 = ((uint64_t)(A.bucket_base + K.bucket) << A.rem_bits) | K.rem;
+            write_kept(A, o, kept_hi(h43, pre), kept_lo(best_f, mean, 0, 0));
+            Job jbr;
+            jbr.lens_off = loff;
+            jbr.n = cb;
+            jbr.out_idx = o;
+            A.jobs[jb] = jbr;
+        }
+        __syncthreads();
+    }
+}
+
 // distinct_functions[f] += kept k-mers with best function f (LDS privatised when it fits)
 __global__ void k_func_hist_kept(const skm_stored_kmer_data* __restrict__ data, uint64_t n, uint32_t nf,
                                  uint32_t* __restrict__ dfunc) {
@@ -2997,7 +3378,7 @@ struct skm_build {
     uint64_t big_cap = 0, n_big = 0, big_kept = 0;
     bool stamps = false;
     uint64_t jobs_cap = 0, lens_cap = 0, n_jobs = 0, n_lens = 0;
-    uint32_t n_overflow = 0;
+    uint32_t n_overflow = 0, n_overflow_last = 0;
     uint32_t nwg = 0;
     uint64_t span = 0;
     uint64_t n_kept = 0;
@@ -3020,7 +3401,8 @@ struct skm_build {
 
     // second stream: overflow sub-buckets + their chains, concurrent with the group-by
     hipStream_t stream2 = nullptr, stream3 = nullptr;
-    hipEvent_t ev_part = nullptr, ev_o[3] = {}, ev_o3[3] = {};
+    hipEvent_t ev_part = nullptr, ev_split = nullptr, ev_o[3] = {}, ev_o3[3] = {};
+    DevBuf d_hv_keys, d_hv_hi, d_hv_lo, d_hv_s0, d_hv_s1;   // heavy keys of the split overflow
     DevBuf d_sub_tab, d_jobs2, d_jobs3;
 
     // pinned host staging for the pipeline's small readbacks
@@ -3875,6 +4257,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     const uint32_t novf = (uint32_t)(ctr[1] & 0xFFFFFFFFull);
     SKM_CHECK(novf <= b->ovf_cap, SKM_E_OOM, "overflow list capacity exceeded");
     b->n_overflow = novf;
+    b->n_overflow_last = novf;
     // ---- 5. overflow sub-buckets (> CAP elements), largest first, concurrent with the group-by:
     //      the heavy ones (>= SKM_OVF_HEAVY elements: they alone can hold the longest P^2 chains)
     //      on stream 2, whose chains start as soon as they are grouped; the rest on stream 3 ----
@@ -3929,10 +4312,35 @@ void phase_group(skm_build* b, uint32_t pass) {
         const uint32_t inline_min = (uint32_t)b->tune.ovf_inline_min;
         const int prio = b->tune.inline_prio;
         SKM_HIP(hipEventRecord(b->ev_o[0], st2));
+        SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
+        // the largest entries (a prefix of the sorted list) lose their heavy keys to k_heavy first;
+        // both overflow streams then read the rewritten entries
+        uint32_t nsplit = 0;
+        uint64_t split_elems = 0;
+        while (nsplit < novf && ov[nsplit].n >= SPLIT_MIN) split_elems += ov[nsplit++].n;
+        if (nsplit) {
+            b->d_hv_keys.ensure(sizeof(HeavyKey) * (split_elems / HEAVY_MIN + 16));
+            b->d_hv_hi.ensure(8 * split_elems);
+            b->d_hv_lo.ensure(8 * split_elems);
+            b->d_hv_s0.ensure(4 * split_elems);
+            b->d_hv_s1.ensure(4 * split_elems);
+            HeavyArgs H;
+            H.keys = b->d_hv_keys.as<HeavyKey>();
+            H.nkeys = ctr_d + 18;  // cleared with the pass's counters
+            H.cursor = ctr_d + 19;
+            H.hi = b->d_hv_hi.as<uint64_t>();
+            H.lo = b->d_hv_lo.as<uint64_t>();
+            H.s0 = b->d_hv_s0.as<uint32_t>();
+            H.s1 = b->d_hv_s1.as<uint32_t>();
+            hipLaunchKernelGGL(k_ovf_split, dim3(nsplit), dim3(BP_THREADS), 0, st2, A2, S, H);
+            SKM_HIP(hipEventRecord(b->ev_split, st2));
+            SKM_HIP(hipStreamWaitEvent(st3, b->ev_split, 0));
+            hipLaunchKernelGGL(k_heavy, dim3(HEAVY_GRID), dim3(HEAVY_WG), 0, st2, A2, H);
+            SKM_HIP(hipGetLastError());
+        }
         if (nheavy)
             hipLaunchKernelGGL(k_overflow, dim3(nheavy), dim3(BP_THREADS), 0, st2, A2, S, inline_min, prio);
         SKM_HIP(hipEventRecord(b->ev_o[1], st2));
-        SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
         if (novf > nheavy)
             hipLaunchKernelGGL(k_overflow, dim3(novf - nheavy), dim3(BP_THREADS), 0, st3, A3, S, inline_min, prio);
         SKM_HIP(hipGetLastError());
@@ -4190,6 +4598,7 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     SKM_HIP(hipStreamCreateWithFlags(&b->chain_st, hipStreamNonBlocking));
     for (auto& e : b->chain_ev) SKM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_part, hipEventDisableTiming));
+    SKM_HIP(hipEventCreateWithFlags(&b->ev_split, hipEventDisableTiming));
     for (auto& e : b->ev_o) SKM_HIP(hipEventCreate(&e));
     for (auto& e : b->ev_o3) SKM_HIP(hipEventCreate(&e));
     set_geometry(b);
@@ -4443,6 +4852,13 @@ int skm_build_debug_jobs(skm_build* b, uint32_t* out, int cap) {
     SKM_API_END
 }
 
+int skm_build_debug_overflow(skm_build* b, uint32_t* out, int cap) {
+    if (!b || !out) return SKM_E_ARG;
+    const uint32_t n = b->h_ovf ? std::min<uint32_t>(b->n_overflow_last, (uint32_t)b->h_ovf_cap) : 0u;
+    for (int i = 0; i < cap; ++i) out[i] = (uint32_t)i < n ? b->h_ovf[i].n : 0u;
+    return (int)n;
+}
+
 // Diagnostics: time k_chains on `njobs` synthetic jobs of length n (lengths 300 +- 60).
 int skm_debug_chain_bench(uint32_t n, uint32_t njobs, int mode, float* ms) {
     SKM_API_BEGIN
@@ -4687,6 +5103,7 @@ void skm_build_destroy(skm_build* b) {
     for (auto& e : b->ev_o3)
         if (e) (void)hipEventDestroy(e);
     if (b->ev_part) (void)hipEventDestroy(b->ev_part);
+    if (b->ev_split) (void)hipEventDestroy(b->ev_split);
     if (b->ev_start) (void)hipEventDestroy(b->ev_start);
     if (b->chain_st) {
         (void)hipStreamSynchronize(b->chain_st);

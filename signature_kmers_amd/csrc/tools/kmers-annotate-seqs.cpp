@@ -5,7 +5,9 @@
 // (CmphKmerDb in HBM).  Called ids go to calls-file as "id\tfunc\tfunc_index\tscore\n"; ids whose
 // call has no function index (no call, or an "f1 ?? f2" call) go to uncalled-ids-file
 // (kmers-annotate-seqs.cc:136-146,163-167).  genus-data-dir is accepted and unused, as upstream.
-// Extra options: --device N.
+// Extra options: --device N; --boost-math-stats current|legacy (the Boost.Math mean / MAD the
+// reference was compiled against, call_functions.tcc:51-53: current = >= 1.76, legacy = the older
+// single running mean and |x(mid)| MAD).
 #include <sys/stat.h>
 
 #include <cstdio>
@@ -32,7 +34,7 @@ int main(int argc, char** argv) {
                 {"sequences-dir", 0, false, false},   {"calls-file", 0, false, false},
                 {"uncalled-ids-file", 0, false, false}, {"parallel", 'j', false, false},
                 {"ignore-hypo", 0, true, false},      {"help", 'h', true, false},
-                {"device", 0, false, false}};
+                {"device", 0, false, false}, {"boost-math-stats", 0, false, false}};
     op.positional = {"kmer-data-dir", "genus-data-dir", "sequences-dir", "calls-file", "uncalled-ids-file"};
     std::string err;
     if (!op.parse(argc, argv, err)) die(err);
@@ -47,11 +49,17 @@ int main(int argc, char** argv) {
                   << "  -j [ --parallel ] arg         Number of threads\n"
                   << "  --ignore-hypo                 Ignore hypothetical protein kmers when making calls\n"
                   << "  --device arg                  HIP device ordinal (default 0)\n"
+                  << "  --boost-math-stats arg          current (default) | legacy Boost.Math mean/MAD\n"
                   << "  -h [ --help ]                 show this help message\n\n";
         return 0;
     }
     int n_threads = std::atoi(op.get("parallel", "0").c_str());
     if (n_threads < 2) n_threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    {
+        const std::string bm = op.get("boost-math-stats", "current");
+        if (bm != "current" && bm != "legacy") die("--boost-math-stats must be current or legacy");
+        set_boost_math_modes(bm == "legacy", bm == "legacy");
+    }
     const int device = std::atoi(op.get("device", "0").c_str());
     const std::string data_dir = op.get("kmer-data-dir");
     const std::string db_base = path_join(data_dir, "kmer_data");

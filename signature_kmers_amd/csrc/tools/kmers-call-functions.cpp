@@ -7,7 +7,9 @@
 // stdout.  Window lookups and HitSet calls run on the GPU (skm_annotate), find_best_call on host.
 // --debug-hits prints the per-hit lines of the reference's debug hit callback
 // (kmers-call-functions.cc:109-118) before each file's calls.
-// Extra options: --device N.
+// Extra options: --device N; --boost-math-stats current|legacy (the Boost.Math mean / MAD the
+// reference was compiled against, call_functions.tcc:51-53: current = >= 1.76, legacy = the older
+// single running mean and |x(mid)| MAD).
 #include <sys/stat.h>
 
 #include <cmath>
@@ -87,7 +89,7 @@ int main(int argc, char** argv) {
     Options op;
     op.specs = {{"data-dir", 'd', false, false}, {"input-files", 'i', false, true}, {"output-files", 'o', false, false},
                 {"n-threads", 'j', false, false}, {"ignore-hypo", 0, true, false},  {"debug-hits", 0, true, false},
-                {"help", 'h', true, false},       {"device", 0, false, false}};
+                {"help", 'h', true, false},       {"device", 0, false, false}, {"boost-math-stats", 0, false, false}};
     op.positional = {"data-dir", "input-files"};
     std::string err;
     if (!op.parse(argc, argv, err)) die(err);
@@ -100,6 +102,7 @@ int main(int argc, char** argv) {
                   << "  --ignore-hypo               Ignore hypothetical protein kmers when making calls\n"
                   << "  --debug-hits                Debug kmer hits\n"
                   << "  --device arg                HIP device ordinal (default 0)\n"
+                  << "  --boost-math-stats arg        current (default) | legacy Boost.Math mean/MAD\n"
                   << "  -h [ --help ]               show this help message\n\n";
     };
     if (op.has("help")) {
@@ -114,6 +117,11 @@ int main(int argc, char** argv) {
     std::cerr << "Data size " << sizeof(skm_stored_kmer_data) << "\n";
     int n_threads = std::atoi(op.get("n-threads", "0").c_str());
     if (n_threads < 2) n_threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    {
+        const std::string bm = op.get("boost-math-stats", "current");
+        if (bm != "current" && bm != "legacy") die("--boost-math-stats must be current or legacy");
+        set_boost_math_modes(bm == "legacy", bm == "legacy");
+    }
     const int device = std::atoi(op.get("device", "0").c_str());
     const std::string data_dir = op.get("data-dir");
     const std::string db_base = path_join(data_dir, "kmer_data");

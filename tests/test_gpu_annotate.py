@@ -155,3 +155,58 @@ def test_device_mph_build_is_minimal_perfect(skm, gpu, tmp_path, n):
     assert open(mph, "rb").read() == open(str(tmp_path / "b.mph"), "rb").read()
     db = skm.CmphKmerDb(str(tmp_path / "a"))
     np.testing.assert_array_equal(db.lookup_keys(keys), idx)
+
+
+def _long_family(rng, n_copies, length, func, first_id):
+    """n_copies ~1 %-mutated variants of one random protein of `length` residues, one function:
+    their k-mers are kept with a mean length near `length`, so a query of that length makes a
+    call whose segment has > 1024 hits (the sequential HitSet path)."""
+    aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+    base = aa[rng.integers(0, 20, length)]
+    seqs = []
+    for _ in range(n_copies):
+        v = base.copy()
+        m = rng.random(length) < 0.01
+        v[m] = aa[rng.integers(0, 20, int(m.sum()))]
+        seqs.append(v)
+    lens = np.full(n_copies, length, np.uint32)
+    return seqs, lens, np.full(n_copies, func, np.uint16), np.arange(first_id, first_id + n_copies, dtype=np.uint32)
+
+
+@pytest.mark.parametrize("mean_mode,mad_mode", [(1, 0), (0, 1), (1, 1)])
+def test_boost_math_modes_match_oracle(skm, gpu, tmp_path, mean_mode, mad_mode):
+    """The Boost.Math switch (call_functions.tcc:51-53) on the device: the single
+    running mean (mean_mode 1) and the older MAD returning |x(mid)| after libstdc++'s nth_element
+    permutations (mad_mode 1) equal the oracle (std::nth_element itself), on the LDS segment path
+    and on the > 1024-hit sequential path (a long protein family added to the DB)."""
+    rng = np.random.default_rng(77)
+    p = synth.generate_arrays(3000, 60, per_file=500, seed=21)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    lseqs, llens, lf, lid = _long_family(rng, 14, 3000, int(f[f != 0xFFFF][0]), int(i.max()) + 1)
+    r2 = np.concatenate([r] + lseqs)
+    o2 = np.concatenate([o, len(r) + np.arange(len(lseqs), dtype=np.uint64) * 3000])
+    ref = oracle_ref.build(r2, o2, np.concatenate([l, llens]), np.concatenate([f, lf]), np.concatenate([i, lid]),
+                           len(funcs))
+    base = str(tmp_path / "kmer_data")
+    skm.mph_build(ref["keys"], ref["data"], base + ".mph", base + ".dat", seed=7)
+    db = skm.CmphKmerDb(base)
+    q = synth.generate_arrays(60000, 60, per_file=500, first_file=40, n_files=6, seed=21, extras=True)
+    seqs = [q.residues[q.seq_off[k]:q.seq_off[k] + q.seq_len[k]].tobytes() for k in range(len(q.seq_len))]
+    seqs += [v.tobytes() for v in lseqs[:6]]
+    lens = np.array([len(s) for s in seqs], np.uint32)
+    off = np.zeros(len(seqs), np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    res = np.frombuffer(b"".join(seqs), np.uint8)
+    hypo = funcs.index("hypothetical protein")
+    caller = skm.FunctionCaller(db, funcs, mean_mode=mean_mode, mad_mode=mad_mode)
+    goff, gcalls = caller.process_seqs(res, off, lens)
+    ob = oracle_ref.Bdz(open(base + ".mph", "rb").read())
+    dat = open(base + ".dat", "rb").read()
+    ooff, ocalls = oracle_ref.annotate(ob, dat, res, off, lens, hypo_index=hypo, mean_mode=mean_mode,
+                                       mad_mode=mad_mode)
+    assert len(gcalls) > 1000 and (gcalls["count"] > 1024).any()
+    np.testing.assert_array_equal(goff, ooff)
+    np.testing.assert_array_equal(gcalls.view(np.uint8), ocalls.view(np.uint8))
+    if mad_mode:  # the switch changes results on this data (ties in |x - median| are common)
+        _, base_calls = oracle_ref.annotate(ob, dat, res, off, lens, hypo_index=hypo, mean_mode=mean_mode, mad_mode=0)
+        assert len(base_calls) != len(ocalls) or not np.array_equal(base_calls.view(np.uint8), ocalls.view(np.uint8))

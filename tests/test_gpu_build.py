@@ -219,3 +219,50 @@ def test_rerun_is_idempotent(skm, gpu):
 def test_device_exact_division(skm, gpu):
     # reciprocal of every integer up to 2^22 (both signs) and 2^22 * 64 random quotients
     assert skm.debug_div_check(1 << 22, 64) == 0
+
+
+@pytest.mark.parametrize("passes", [0, 2])
+def test_heavy_keys_split_path(skm, gpu, passes):
+    """k_ovf_split / k_heavy: overflow sub-buckets of >= 4096 elements lose their keys of >= 1024
+    occurrences to the heavy path (Boyer-Moore majority + exact count for the fp32 80 % cut, radix
+    select of the upper-median offset, sequence-index radix sort for the visit-order samples).
+    Planted 8-mers: pure (kept, some sequences hold it three times), exactly 80 % (kept),
+    one short of 80 % (cut), a 50/50 tie (cut), and one inside a > 65535-residue protein."""
+    rng = np.random.default_rng(44)
+    aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+
+    def rnd(k):
+        return bytes(rng.choice(aa, k))
+    seqs, funcs = [], []
+    plan = [(rnd(8), [1] * 5000, True), (rnd(8), [2] * 3200 + [3] * 800, False),
+            (rnd(8), [2] * 3199 + [5] * 801, False), (rnd(8), [4] * 2100 + [0] * 2100, False),
+            (rnd(8), [0] * 4100, False)]
+    for pi, (core, fl, rep) in enumerate(plan):
+        rng.shuffle(fl)
+        for j, fn in enumerate(fl):
+            a, b = rnd(int(rng.integers(0, 400))), rnd(int(rng.integers(0, 400)))
+            body = core * 3 if (rep and j % 7 == 0) else core
+            if pi == 4 and j == 17:
+                a = rnd(70000)
+            seqs.append(a + body + b)
+            funcs.append(fn)
+    order = rng.permutation(len(seqs))
+    seqs = [seqs[k] for k in order]
+    res, off, lens = pack(seqs)
+    func = np.array(funcs, np.uint16)[order]
+    sid = np.arange(len(seqs), dtype=np.uint32)
+    ref = oracle_ref.build(res, off, lens, func, sid, 6)
+    b = skm.SignatureBuilder(6)
+    if passes:
+        b.set_option("key_range_passes", passes)
+    b.add_batch(res, off, lens, func, sid)
+    b.run()
+    ovf = b.debug_overflow()
+    got = b.finish()
+    b.close()
+    assert_same(got, ref)
+    keys = {int.from_bytes(c, "little"): fl for c, fl, _ in plan}
+    kept = set(int(k) for k in got.keys)
+    assert [k in kept for k in keys] == [True, True, False, False, True]
+    if not passes:
+        assert max(ovf) >= 4096

@@ -187,3 +187,94 @@ def test_matrix_distance_matches_oracle(c1_build, tmp_path):
     assert got[-1] == "" and len(got) - 1 == len(want) and set(got[:-1]) == want
     assert len(want) > 1000
     assert "kmer_hit_map size " in stderr and "write output" in stderr
+
+
+def _kmer_windows(seq: bytes):
+    """for_each_kmer<8> (kmer_data.h:76-102): 'X' / '*' end a run; a window is skipped when the
+    next ambiguous byte lies inside it or right after it."""
+    L, p, out = len(seq), 0, []
+
+    def nxt(q):
+        while q < L and seq[q] not in b"X*":
+            q += 1
+        return q
+    na = nxt(0)
+    while L >= 8 and p <= L - 8:
+        if na != L and p + 8 >= na:
+            p = na + 1
+            na = nxt(p)
+            continue
+        out.append(p)
+        p += 1
+    return out
+
+
+@pytest.mark.parametrize("ignore_hypo", [False, True])
+def test_call_functions_debug_hits(c1_build, tmp_path, ignore_hypo):
+    """--debug-hits prints the reference's hit_cb line per DB hit (kmers-call-functions.cc:109-118:
+    kmer, offset, function, median, mean, var, sqrt(var)), after the hypothetical filter
+    (call_functions.tcc:284-291), before each file's calls; the calls file is unchanged."""
+    info, out, _, _ = c1_build
+    qdir = _query_dir(tmp_path / "q", seed=13)
+    inputs = sorted(os.path.join(qdir, f) for f in os.listdir(qdir))[:2]
+    cmd = [os.path.join(BIN, "kmers-call-functions"), out] + inputs + ["-o", str(tmp_path / "calls.txt"),
+                                                                        "--debug-hits"]
+    if ignore_hypo:
+        cmd.append("--ignore-hypo")
+    stdout, _ = _run(cmd)
+    bdz = oracle_ref.Bdz(_lines(os.path.join(out, "kmer_data.mph")))
+    dat = np.frombuffer(_lines(os.path.join(out, "kmer_data.dat")), oracle_ref.STORED_DTYPE)
+    fidx = _fidx(out)
+    hypo = fidx.index("hypothetical protein")
+    want, calls_want = [], b""
+    for p in inputs:
+        recs = fr.parse_fasta(_lines(p))
+        for _, _, seq in recs:
+            pos = _kmer_windows(seq)
+            if not pos:
+                continue
+            keys = np.array([int.from_bytes(seq[q:q + 8], "little") for q in pos], np.uint64)
+            idx = bdz.search(keys)
+            for q, k, ix in zip(pos, keys, idx):
+                if ix >= len(dat):
+                    continue
+                d = dat[ix]
+                if ignore_hypo and int(d["function_index"]) == hypo:
+                    continue
+                fn = fidx[d["function_index"]] if d["function_index"] < len(fidx) else ""
+                want.append("%s\t%d\t%s\t%d\t%d\t%d\t%s\t" % (int(k).to_bytes(8, "little").decode("latin-1"), q, fn,
+                                                             d["median"], d["mean"], d["var"],
+                                                             fr.fmt_g(float(np.sqrt(float(d["var"]))))))
+        w, _ = fr.call_lines(oracle_ref, recs, fidx, bdz, _lines(os.path.join(out, "kmer_data.dat")),
+                             ignore_hypo=ignore_hypo)
+        calls_want += w
+    got = stdout.split("\n")
+    assert got[-1] == "" and got[:-1] == want
+    assert len(want) > 1000
+    assert _lines(str(tmp_path / "calls.txt")) == calls_want
+
+
+def test_call_functions_boost_math_legacy(c1_build, tmp_path):
+    """--boost-math-stats legacy: the calls of a reference compiled against the older Boost.Math
+    (single running mean, MAD = |x(mid)|; call_functions.tcc:51-53) -- the oracle's modes 1/1."""
+    info, out, _, _ = c1_build
+    qdir = _query_dir(tmp_path / "q", seed=17)
+    inputs = sorted(os.path.join(qdir, f) for f in os.listdir(qdir))
+    _run([os.path.join(BIN, "kmers-call-functions"), out] + inputs + ["-o", str(tmp_path / "calls.txt"),
+                                                                      "--boost-math-stats", "legacy"])
+    bdz = oracle_ref.Bdz(_lines(os.path.join(out, "kmer_data.mph")))
+    dat = _lines(os.path.join(out, "kmer_data.dat"))
+    fidx = _fidx(out)
+    hypo = fidx.index("hypothetical protein")
+    want = b""
+    for p in inputs:
+        recs = fr.parse_fasta(_lines(p))
+        res, off, ln = fr.records_arrays(recs)
+        coff, calls = oracle_ref.annotate(bdz, dat, res, off, ln, hypo_index=hypo, mean_mode=1, mad_mode=1)
+        for r, (pid, _, _) in enumerate(recs):
+            fi, func, score, _ = oracle_ref.find_best_call(calls[coff[r]:coff[r + 1]], fidx)
+            want += b"%s\t%s\t%d\t%s\n" % (pid, func.encode("latin-1"), fi, fr.fmt_g(score).encode())
+    assert _lines(str(tmp_path / "calls.txt")) == want
+    p = subprocess.run([os.path.join(BIN, "kmers-call-functions"), out, inputs[0], "--boost-math-stats", "old"],
+                       capture_output=True, timeout=120)
+    assert p.returncode != 0 and b"--boost-math-stats" in p.stderr

@@ -1,0 +1,62 @@
+"""C3 (50M-protein) build diagnostics on one GPU: per-phase timings, counters, the last pass's
+overflow sub-bucket sizes, the longest chain jobs, and the chain kernels' per-sample latency.
+Inputs come from bench.py's generator cache (python bench.py --cache-dir D --cache-only first).
+    python tools/c3_diag.py --cache-dir /tmp/c3 [--option name=value ...]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import signature_kmers_amd as skm  # noqa: E402
+from signature_kmers_amd import synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--cache-dir", required=True)
+ap.add_argument("--seqs-total", type=int, default=50_000_000)
+ap.add_argument("--families", type=int, default=4000)
+ap.add_argument("--steps", type=int, default=1)
+ap.add_argument("--option", action="append", default=[])
+ap.add_argument("--chain-bench", action="store_true")
+a = ap.parse_args()
+
+
+def log(m):
+    print(f"[diag] {m}", flush=True)
+
+
+if a.chain_bench:
+    for n in (1 << 16, 1 << 20):
+        for mode, nm in ((2, "wave pair"), (3, "P2 wave"), (4, "var wave")):
+            ms = skm.debug_chain_bench(n, 1, mode)
+            log(f"chain n={n} {nm}: {ms:.2f} ms = {1e6 * ms / n:.1f} ns/sample")
+files = (a.seqs_total + bench.PER_FILE - 1) // bench.PER_FILE
+sh = bench.gen(synth, a.seqs_total, a.families, 0, files, 1, a.cache_dir)
+log(f"{sh.n_seqs:,} proteins, {sh.n_windows:,} windows")
+b = skm.SignatureBuilder(len(synth.functions(a.families)))
+for kv in a.option:
+    k, v = kv.split("=", 1)
+    b.set_option(k, int(v))
+sh.add_to(b)
+t = time.time()
+b.prepare()
+log(f"prepare {time.time() - t:.1f} s")
+for s in range(a.steps + 1):
+    t = time.time()
+    b.run()
+    log(f"run {s}: {1000 * (time.time() - t):.0f} ms wall; " + json.dumps({k: round(v, 1) for k, v in b.timings().items()}))
+c = b.counters()
+log("counters " + json.dumps(c))
+ov = b.debug_overflow(1 << 16)
+if ov:
+    import numpy as np
+    v = np.array(ov, np.int64)
+    log(f"last pass overflow: {len(v)} sub-buckets, {v.sum():,} elements; largest {ov[:16]}")
+    for lim in (1 << 12, 1 << 14, 1 << 16, 1 << 18, 1 << 20):
+        sel = v >= lim
+        log(f"  >= {lim:>8d}: {int(sel.sum()):6d} sub-buckets, {int(v[sel].sum()):>12,} elements")
+log(f"longest jobs (last pass) {b.debug_jobs(32)}")
+b.close()
