@@ -156,7 +156,9 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   "device_memory_budget_mb" memory the automatic pass count plans for (0 = free memory).
  * Diagnostic tunables (defaults are the tuned values): "overflow_heavy_min",
  *   "overflow_inline_min", "overflow_inline_prio", "overflow_long_class", "overflow_chain_wgs",
- *   "chain_prio", "bucket_prio", "chain_lds_kb", "host_timing".
+ *   "chain_prio", "bucket_prio", "chain_lds_kb", "host_timing",
+ *   "heavy_min" (occurrences that send a k-mer to the heavy path), "split_min" (overflow
+ *   sub-buckets at least this large are split into heavy keys + a light remainder).
  * Unknown names and out-of-range values return SKM_E_ARG. */
 int skm_build_set_option(skm_build* b, const char* name, int64_t value);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then

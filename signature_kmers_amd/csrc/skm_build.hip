@@ -2931,8 +2931,10 @@ struct HeavyArgs {
 
 __device__ __forceinline__ uint32_t split_hash(uint32_t rem) { return (rem * 0x9E3779B1u) >> (32 - 12); }
 
+constexpr uint32_t SPLIT_U = 8;   // elements per thread per iteration (loads issued together)
+
 // One workgroup per overflow entry of >= SPLIT_MIN elements (the first entries of the sorted list).
-__global__ __launch_bounds__(BP_THREADS) void k_ovf_split(BucketArgs A, OvfScratch S, HeavyArgs H) {
+__global__ __launch_bounds__(BP_THREADS) void k_ovf_split(BucketArgs A, OvfScratch S, HeavyArgs H, uint32_t heavy_min) {
     static_assert(SPLIT_TAB == 4096, "split_hash yields 12 bits");
     __shared__ uint32_t s_key[SPLIT_TAB];
     __shared__ uint32_t s_cnt[SPLIT_TAB];
@@ -2958,36 +2960,45 @@ __global__ __launch_bounds__(BP_THREADS) void k_ovf_split(BucketArgs A, OvfScrat
         s_heavy = 0;
     }
     __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
     // ---- 1. occurrences per key (wave-aggregated for the lanes sharing lane 0's key) ----
-    for (uint32_t j0 = 0; j0 < n; j0 += nt) {
-        const uint32_t j = j0 + tid;
-        const bool v = j < n;
-        const uint32_t rem = v ? (uint32_t)(src_hi[j] >> 16) & REM_MASK : EMPTY;
-        const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)rem);
-        const uint64_t same = __ballot(v && rem == r0);
-        const bool lead = v && rem == r0 && lane == (uint32_t)(__ffsll((long long)same) - 1);
-        if (v && (rem != r0 || lead)) {
-            uint32_t slot = split_hash(rem), probe = 0;
-            for (; probe < SPLIT_TAB; ++probe) {
-                const uint32_t k = s_key[slot];
-                if (k == rem) break;
-                if (k == EMPTY) {
-                    const uint32_t old = atomicCAS(&s_key[slot], EMPTY, rem);
-                    if (old == EMPTY || old == rem) break;
+    for (uint32_t j0 = 0; j0 < n; j0 += nt * SPLIT_U) {
+        uint32_t rems[SPLIT_U];
+#pragma unroll
+        for (uint32_t u = 0; u < SPLIT_U; ++u) {
+            const uint32_t j = j0 + u * nt + tid;
+            rems[u] = j < n ? (uint32_t)(src_hi[j] >> 16) & REM_MASK : EMPTY;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < SPLIT_U; ++u) {
+            const uint32_t rem = rems[u];
+            const bool v = rem != EMPTY;
+            const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)rem);
+            const uint64_t same = __ballot(v && rem == r0);
+            const bool lead = v && rem == r0 && (same & lt) == 0;
+            if (v && (rem != r0 || lead)) {
+                uint32_t slot = split_hash(rem), probe = 0;
+                for (; probe < SPLIT_TAB; ++probe) {
+                    const uint32_t k = s_key[slot];
+                    if (k == rem) break;
+                    if (k == EMPTY) {
+                        const uint32_t old = atomicCAS(&s_key[slot], EMPTY, rem);
+                        if (old == EMPTY || old == rem) break;
+                    }
+                    slot = (slot + 1) & (SPLIT_TAB - 1);
                 }
-                slot = (slot + 1) & (SPLIT_TAB - 1);
+                if (probe == SPLIT_TAB)
+                    s_fail = 1;
+                else
+                    atomicAdd(&s_cnt[slot], lead ? (uint32_t)__popcll(same) : 1u);
             }
-            if (probe == SPLIT_TAB)
-                s_fail = 1;
-            else
-                atomicAdd(&s_cnt[slot], lead ? (uint32_t)__popcll(same) : 1u);
         }
     }
     __syncthreads();
     if (s_fail) return;  // more distinct keys than the table holds: the entry keeps the sort path
     // ---- 2. heavy keys: their own ranges in the heavy arrays ----
     for (uint32_t q = tid; q < SPLIT_TAB; q += nt)
-        if (s_cnt[q] >= HEAVY_MIN) {
+        if (s_cnt[q] >= heavy_min) {
             const uint32_t h = atomicAdd(&s_nh, 1u);
             if (h < SPLIT_MAXH) {
                 s_hid[q] = (uint16_t)h;
@@ -3010,47 +3021,52 @@ __global__ __launch_bounds__(BP_THREADS) void k_ovf_split(BucketArgs A, OvfScrat
     // ---- 3. scatter: heavy members to their key's range, the rest compacted into the scratch ----
     uint64_t* lhi = S.hi + e.scratch;
     uint64_t* llo = S.lo + e.scratch;
-    for (uint32_t j0 = 0; j0 < n; j0 += nt) {
-        const uint32_t j = j0 + tid;
-        const bool v = j < n;
-        uint64_t eh = 0, el = 0;
-        uint32_t hid = 0xFFFFu;
-        if (v) {
-            eh = src_hi[j];
-            el = src_lo[j];
-            const uint32_t rem = (uint32_t)(eh >> 16) & REM_MASK;
-            uint32_t slot = split_hash(rem);
-            while (s_key[slot] != rem) slot = (slot + 1) & (SPLIT_TAB - 1);
-            hid = s_hid[slot];
+    for (uint32_t j0 = 0; j0 < n; j0 += nt * SPLIT_U) {
+        uint64_t eh[SPLIT_U], el[SPLIT_U];
+#pragma unroll
+        for (uint32_t u = 0; u < SPLIT_U; ++u) {
+            const uint32_t j = j0 + u * nt + tid;
+            eh[u] = j < n ? src_hi[j] : ~0ull;
+            el[u] = j < n ? src_lo[j] : 0ull;
         }
-        // light members: wave-aggregated cursor
-        const uint64_t lm = __ballot(v && hid == 0xFFFFu);
-        uint32_t lbase = 0;
-        if (lm) {
-            const uint32_t leader = (uint32_t)(__ffsll((long long)lm) - 1);
-            if (lane == leader) lbase = atomicAdd(&s_lcur, (uint32_t)__popcll(lm));
-            lbase = (uint32_t)__shfl((int)lbase, (int)leader, 64);
-        }
-        if (v && hid == 0xFFFFu) {
-            const uint32_t pos = lbase + (uint32_t)__popcll(lm & ((1ull << lane) - 1ull));
-            lhi[pos] = eh;
-            llo[pos] = el;
-        }
-        // heavy members: aggregated for the lanes sharing lane 0's key
-        const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(v ? hid : 0xFFFFu));
-        const uint64_t hm = __ballot(v && hid != 0xFFFFu && hid == h0);
-        uint32_t hbase = 0;
-        if (hm) {
-            const uint32_t leader = (uint32_t)(__ffsll((long long)hm) - 1);
-            if (lane == leader) hbase = atomicAdd(&s_hcur[h0], (uint32_t)__popcll(hm));
-            hbase = (uint32_t)__shfl((int)hbase, (int)leader, 64);
-        }
-        if (v && hid != 0xFFFFu) {
-            const uint32_t pos = hid == h0 ? hbase + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))
-                                           : atomicAdd(&s_hcur[hid], 1u);
-            const uint64_t o = s_hbase[hid] + pos;
-            H.hi[o] = eh;
-            H.lo[o] = el;
+#pragma unroll
+        for (uint32_t u = 0; u < SPLIT_U; ++u) {
+            const bool v = eh[u] != ~0ull;
+            uint32_t hid = 0xFFFFu;
+            if (v) {
+                const uint32_t rem = (uint32_t)(eh[u] >> 16) & REM_MASK;
+                uint32_t slot = split_hash(rem);
+                while (s_key[slot] != rem) slot = (slot + 1) & (SPLIT_TAB - 1);
+                hid = s_hid[slot];
+            }
+            // light members: wave-aggregated cursor
+            const uint64_t lm = __ballot(v && hid == 0xFFFFu);
+            uint32_t lbase = 0;
+            if (lm) {
+                const uint32_t leader = (uint32_t)(__ffsll((long long)lm) - 1);
+                if (lane == leader) lbase = atomicAdd(&s_lcur, (uint32_t)__popcll(lm));
+                lbase = (uint32_t)__shfl((int)lbase, (int)leader, 64);
+            }
+            if (v && hid == 0xFFFFu) {
+                const uint32_t pos = lbase + (uint32_t)__popcll(lm & lt);
+                lhi[pos] = eh[u];
+                llo[pos] = el[u];
+            }
+            // heavy members: aggregated for the lanes sharing lane 0's key
+            const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(v ? hid : 0xFFFFu));
+            const uint64_t hm = __ballot(v && hid != 0xFFFFu && hid == h0);
+            uint32_t hbase = 0;
+            if (hm) {
+                const uint32_t leader = (uint32_t)(__ffsll((long long)hm) - 1);
+                if (lane == leader) hbase = atomicAdd(&s_hcur[h0], (uint32_t)__popcll(hm));
+                hbase = (uint32_t)__shfl((int)hbase, (int)leader, 64);
+            }
+            if (v && hid != 0xFFFFu) {
+                const uint32_t pos = hid == h0 ? hbase + (uint32_t)__popcll(hm & lt) : atomicAdd(&s_hcur[hid], 1u);
+                const uint64_t o = s_hbase[hid] + pos;
+                H.hi[o] = eh[u];
+                H.lo[o] = el[u];
+            }
         }
     }
     __syncthreads();
@@ -3062,56 +3078,71 @@ __global__ __launch_bounds__(BP_THREADS) void k_ovf_split(BucketArgs A, OvfScrat
     }
 }
 
-// Stable LSD radix sort (ascending) of a[0..n) by one workgroup, 8-bit digits over `bits` bits,
+// Stable LSD radix sort (ascending) of a[0..n) by one workgroup, RB-bit digits over `bits` bits,
 // ping-ponging with b; returns the buffer holding the result.  Items go in rounds of one per
-// thread; a round's rank among equal digits is the wave ballot match plus the lower waves'
-// counts (tagged with the round number, so the count table is never cleared).
+// thread, the next round's item loaded before the current one is ranked; a round's rank among
+// equal digits is the wave ballot match plus the lower waves' counts (tagged with the round
+// number, so the count table is never cleared: tag 0 is never live).
+constexpr int RB = 9;
+constexpr uint32_t RBINS = 1u << RB;
 __device__ uint32_t* wg_radix_sort_u32(uint32_t* a, uint32_t* b, uint32_t n, int bits, uint32_t* s_hist,
-                                       uint32_t (*s_wc)[256], uint32_t* s_run, uint32_t& tag) {
+                                       uint32_t (*s_wc)[RBINS], uint32_t* s_run, uint32_t& tag) {
     const uint32_t tid = threadIdx.x, nt = blockDim.x, lane = tid & 63u, wave = tid >> 6, nw = nt >> 6;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (int shift = 0; shift < bits; shift += 8) {
-        for (uint32_t d = tid; d < 256; d += nt) s_hist[d] = 0;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int shift = 0; shift < bits; shift += RB) {
+        for (uint32_t d = tid; d < RBINS; d += nt) s_hist[d] = 0;
         __syncthreads();
-        for (uint32_t j = tid; j < n; j += nt) atomicAdd(&s_hist[(a[j] >> shift) & 255u], 1u);
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t acc = 0;
-            for (uint32_t d = 0; d < 256; ++d) {
-                s_run[d] = acc;
-                acc += s_hist[d];
+        for (uint32_t j0 = 0; j0 < n; j0 += nt * SPLIT_U) {
+            uint32_t x[SPLIT_U];
+#pragma unroll
+            for (uint32_t u = 0; u < SPLIT_U; ++u) {
+                const uint32_t j = j0 + u * nt + tid;
+                x[u] = j < n ? a[j] : 0u;
             }
+#pragma unroll
+            for (uint32_t u = 0; u < SPLIT_U; ++u)
+                if (j0 + u * nt + tid < n) atomicAdd(&s_hist[(x[u] >> shift) & (RBINS - 1)], 1u);
         }
         __syncthreads();
+        {   // exclusive scan of the bins (one bin per thread, RBINS <= blockDim)
+            const uint32_t c = tid < RBINS ? s_hist[tid] : 0u;
+            uint32_t tot;
+            const uint32_t ex = wg_exclusive_scan(c, s_run + RBINS, tot);
+            if (tid < RBINS) s_run[tid] = ex;
+            __syncthreads();
+        }
+        uint32_t nk = tid < n ? a[tid] : 0u;
         for (uint32_t j0 = 0; j0 < n; j0 += nt) {
             ++tag;
             const uint32_t j = j0 + tid;
             const bool v = j < n;
-            const uint32_t k = v ? a[j] : 0u;
-            const uint32_t d = (k >> shift) & 255u;
+            const uint32_t k = nk;
+            if (j0 + nt + tid < n) nk = a[j0 + nt + tid];
+            const uint32_t d = (k >> shift) & (RBINS - 1);
             uint64_t peers = __ballot(v);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
+            for (int q = 0; q < RB; ++q) {
                 const uint64_t m = __ballot((d >> q) & 1u);
                 peers &= ((d >> q) & 1u) ? m : ~m;
             }
             const uint32_t pre = (uint32_t)__popcll(peers & lt);
-            if (v && pre == 0) s_wc[wave][d] = (tag << 7) | (uint32_t)__popcll(peers);
+            const uint32_t tg = tag & 0x1FFFFFFu;
+            if (v && pre == 0) s_wc[wave][d] = (tg << 7) | (uint32_t)__popcll(peers);
             __syncthreads();
             if (v) {
                 uint32_t o = s_run[d] + pre;
                 for (uint32_t w = 0; w < wave; ++w) {
                     const uint32_t c = s_wc[w][d];
-                    if ((c >> 7) == (tag & 0x1FFFFFFu)) o += c & 127u;
+                    if ((c >> 7) == tg) o += c & 127u;
                 }
                 b[o] = k;
             }
             __syncthreads();
-            for (uint32_t dd = tid; dd < 256; dd += nt) {
+            for (uint32_t dd = tid; dd < RBINS; dd += nt) {
                 uint32_t add = 0;
                 for (uint32_t w = 0; w < nw; ++w) {
                     const uint32_t c = s_wc[w][dd];
-                    if ((c >> 7) == (tag & 0x1FFFFFFu)) add += c & 127u;
+                    if ((c >> 7) == tg) add += c & 127u;
                 }
                 s_run[dd] += add;
             }
@@ -3126,16 +3157,19 @@ __device__ uint32_t* wg_radix_sort_u32(uint32_t* a, uint32_t* b, uint32_t n, int
 
 // One heavy key per workgroup iteration (persistent grid; the key count is read on the device).
 __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
-    __shared__ uint32_t s_hist[256], s_run[256];
-    __shared__ uint32_t s_wc[HEAVY_WG / 64][256];
+    static_assert(RBINS <= HEAVY_WG, "one radix bin per thread in the scan");
+    __shared__ uint32_t s_hist[RBINS], s_run[RBINS + 48];
+    __shared__ uint32_t s_wc[HEAVY_WG / 64][RBINS];
     __shared__ __align__(16) uint32_t s_wave[48];
     __shared__ uint32_t s_bm[2 * (HEAVY_WG / 64)];
-    __shared__ uint32_t s_cur;
+    __shared__ uint32_t s_cur, s_sel[2];
     const uint32_t tid = threadIdx.x, nt = blockDim.x, lane = tid & 63u, wave = tid >> 6, nw = nt >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
     const uint32_t nkeys = (uint32_t)*H.nkeys;
     uint32_t tag = 0;  // round tags of s_wc: 0 is never a live round
-    for (uint32_t q = tid; q < (HEAVY_WG / 64) * 256; q += nt) (&s_wc[0][0])[q] = 0;
+    for (uint32_t q = tid; q < (HEAVY_WG / 64) * RBINS; q += nt) (&s_wc[0][0])[q] = 0;
     __syncthreads();
+    constexpr uint32_t U = SPLIT_U;
     for (uint32_t q = blockIdx.x; q < nkeys; q += gridDim.x) {
         const HeavyKey K = H.keys[q];
         const uint64_t* hi = H.hi + K.off;
@@ -3143,15 +3177,24 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
         const uint32_t n = K.n;
         // ---- Boyer-Moore majority function, then its exact count ----
         uint32_t cand = 0xFFFFFFFFu, cc = 0;
-        for (uint32_t j = tid; j < n; j += nt) {
-            const uint32_t f = (uint32_t)(hi[j] & 0xFFFFu);
-            if (cc == 0) {
-                cand = f;
-                cc = 1;
-            } else if (f == cand) {
-                ++cc;
-            } else {
-                --cc;
+        for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
+            uint32_t f[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t j = j0 + u * nt + tid;
+                f[u] = j < n ? (uint32_t)(hi[j] & 0xFFFFu) : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                if (f[u] == 0xFFFFFFFFu) continue;
+                if (cc == 0) {
+                    cand = f[u];
+                    cc = 1;
+                } else if (f[u] == cand) {
+                    ++cc;
+                } else {
+                    --cc;
+                }
             }
         }
         bm_combine(cand, cc);  // over the wave (lane 0 broadcast)
@@ -3173,82 +3216,125 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
                     n0 = n1 - n0;
                 }
             }
-            s_bm[0] = c0;
+            s_sel[0] = c0;
         }
         __syncthreads();
-        const uint32_t best_f = s_bm[0];
+        const uint32_t best_f = s_sel[0];
         uint32_t cb = 0;
-        for (uint32_t j = tid; j < n; j += nt) cb += (uint32_t)(hi[j] & 0xFFFFu) == best_f;
+        for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
+            uint32_t f[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t j = j0 + u * nt + tid;
+                f[u] = j < n ? (uint32_t)(hi[j] & 0xFFFFu) : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) cb += f[u] == best_f;
+        }
         cb = wg_sum(cb, s_wave);
         if ((float)cb < float(n) * 0.8f) continue;  // cut (uniform); the best run is the majority
-        // ---- flags, u16 length sum and the best members' sequence indices ----
+        // ---- flags, u16 length sum and the best members' sequence indices; offset histogram
+        //      of the high byte for the upper-median select ----
         if (tid == 0) s_cur = 0;
+        for (uint32_t d = tid; d < 256; d += nt) s_hist[d] = 0;
         __syncthreads();
         uint32_t* sa = H.s0 + K.off;
         uint32_t* sb = H.s1 + K.off;
         uint32_t sum = 0, smax = 0;
-        for (uint32_t j0 = 0; j0 < n; j0 += nt) {
-            const uint32_t j = j0 + tid;
-            const bool v = j < n;
-            uint32_t s = 0;
-            bool best = false;
-            if (v) {
-                s = (uint32_t)(lo[j] >> 36);
-                A.flags[s] = 1;
-                best = (uint32_t)(hi[j] & 0xFFFFu) == best_f;
+        for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
+            uint64_t l[U];
+            uint32_t f[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t j = j0 + u * nt + tid;
+                f[u] = j < n ? (uint32_t)(hi[j] & 0xFFFFu) : 0xFFFFFFFFu;
+                l[u] = j < n ? lo[j] : 0ull;
+            }
+            uint32_t gl[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) gl[u] = f[u] == best_f ? A.glen[(uint32_t)(l[u] >> 36)] : 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const bool v = f[u] != 0xFFFFFFFFu;
+                const uint32_t s = (uint32_t)(l[u] >> 36);
+                const bool best = f[u] == best_f;
+                if (v) {
+                    A.flags[s] = 1;
+                    atomicAdd(&s_hist[(uint32_t)(l[u] >> 8) & 255u], 1u);
+                }
                 if (best) {
-                    sum += A.glen[s];
+                    sum += gl[u];
                     smax = max(smax, s);
                 }
+                const uint64_t bm = __ballot(best);
+                uint32_t base = 0;
+                if (bm) {
+                    const uint32_t leader = (uint32_t)(__ffsll((long long)bm) - 1);
+                    if (lane == leader) base = atomicAdd(&s_cur, (uint32_t)__popcll(bm));
+                    base = (uint32_t)__shfl((int)base, (int)leader, 64);
+                }
+                if (best) sa[base + (uint32_t)__popcll(bm & lt)] = s;
             }
-            const uint64_t bm = __ballot(best);
-            uint32_t base = 0;
-            if (bm) {
-                const uint32_t leader = (uint32_t)(__ffsll((long long)bm) - 1);
-                if (lane == leader) base = atomicAdd(&s_cur, (uint32_t)__popcll(bm));
-                base = (uint32_t)__shfl((int)base, (int)leader, 64);
-            }
-            if (best) sa[base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] = s;
         }
         sum = wg_sum(sum, s_wave);
         smax = wg_max(smax, s_wave);
         const uint16_t mean = d2u16((double)(uint16_t)sum / (double)cb);
-        // ---- avg_from_end: the (n/2)-th smallest offset, radix select over two 8-bit digits ----
+        // ---- avg_from_end: the (n/2)-th smallest offset, high byte then low byte ----
         uint32_t k = n / 2, pre = 0;
         for (int sh = 8; sh >= 0; sh -= 8) {
-            for (uint32_t d = tid; d < 256; d += nt) s_hist[d] = 0;
-            __syncthreads();
-            for (uint32_t j = tid; j < n; j += nt) {
-                const uint32_t o = (uint32_t)(lo[j] & 0xFFFFu);
-                if (sh == 0 && (o >> 8) != (pre >> 8)) continue;
-                atomicAdd(&s_hist[(o >> sh) & 255u], 1u);
+            if (sh == 0) {
+                for (uint32_t d = tid; d < 256; d += nt) s_hist[d] = 0;
+                __syncthreads();
+                for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
+                    uint32_t o[U];
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) {
+                        const uint32_t j = j0 + u * nt + tid;
+                        o[u] = j < n ? (uint32_t)(lo[j] & 0xFFFFu) : 0xFFFFFFFFu;
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u)
+                        if (o[u] != 0xFFFFFFFFu && (o[u] >> 8) == (pre >> 8)) atomicAdd(&s_hist[o[u] & 255u], 1u);
+                }
             }
             __syncthreads();
             if (tid == 0) {
                 uint32_t d = 0;
                 while (k >= s_hist[d]) k -= s_hist[d++];
-                s_run[0] = d;
-                s_run[1] = k;
+                s_sel[0] = d;
+                s_sel[1] = k;
             }
             __syncthreads();
-            pre |= s_run[0] << sh;
-            k = s_run[1];
+            pre |= s_sel[0] << sh;
+            k = s_sel[1];
             __syncthreads();
         }
         // ---- samples in visit order: sequence indices descending ----
         int bits = 0;
-        while (bits < 32 && (smax >> bits)) bits += 8;
+        while (bits < 32 && (smax >> bits)) bits += RB;
         const uint32_t* sorted = wg_radix_sort_u32(sa, sb, cb, bits, s_hist, s_wc, s_run, tag);
         __syncthreads();
         if (tid == 0) {
-            s_run[0] = (uint32_t)atomicAdd(A.kept_ctr, 1ull);
+            s_sel[0] = (uint32_t)atomicAdd(A.kept_ctr, 1ull);
             atomicAdd(&A.ctr[0], 1ull);
-            s_run[1] = (uint32_t)atomicAdd(&A.ctr[3], 1ull);
-            s_run[2] = (uint32_t)atomicAdd(&A.ctr[4], (unsigned long long)cb);
+            s_sel[1] = (uint32_t)atomicAdd(&A.ctr[3], 1ull);
+            s_cur = (uint32_t)atomicAdd(&A.ctr[4], (unsigned long long)cb);
         }
         __syncthreads();
-        const uint32_t o = s_run[0], jb = s_run[1], loff = s_run[2];
-        for (uint32_t t = tid; t < cb; t += nt) A.lens[(uint64_t)loff + t] = A.glen[sorted[cb - 1 - t]];
+        const uint32_t o = s_sel[0], jb = s_sel[1], loff = s_cur;
+        for (uint32_t t0 = 0; t0 < cb; t0 += nt * U) {
+            uint32_t sv[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t t = t0 + u * nt + tid;
+                sv[u] = t < cb ? sorted[cb - 1 - t] : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t t = t0 + u * nt + tid;
+                if (t < cb) A.lens[(uint64_t)loff + t] = A.glen[sv[u]];
+            }
+        }
         if (tid == 0) {
             const uint64_t h43 = ((uint64_t)(A.bucket_base + K.bucket) << A.rem_bits) | K.rem;
             write_kept(A, o, kept_hi(h43, pre), kept_lo(best_f, mean, 0, 0));
@@ -3329,6 +3415,8 @@ struct Tune {
     int bucket_prio = 0;
     int chain_lds_kb = 0;
     int host_timing = 0;
+    int heavy_min = (int)HEAVY_MIN;  // occurrences that make a key heavy (k_ovf_split)
+    int split_min = (int)SPLIT_MIN;  // overflow sub-buckets of at least this size are split
 };
 
 }  // namespace skm
@@ -4317,9 +4405,11 @@ void phase_group(skm_build* b, uint32_t pass) {
         // both overflow streams then read the rewritten entries
         uint32_t nsplit = 0;
         uint64_t split_elems = 0;
-        while (nsplit < novf && ov[nsplit].n >= SPLIT_MIN) split_elems += ov[nsplit++].n;
+        const uint32_t split_min = (uint32_t)std::max(b->tune.split_min, CAP + 1);
+        const uint32_t key_min = (uint32_t)std::max(b->tune.heavy_min, 2);
+        while (nsplit < novf && ov[nsplit].n >= split_min) split_elems += ov[nsplit++].n;
         if (nsplit) {
-            b->d_hv_keys.ensure(sizeof(HeavyKey) * (split_elems / HEAVY_MIN + 16));
+            b->d_hv_keys.ensure(sizeof(HeavyKey) * (split_elems / key_min + 16));
             b->d_hv_hi.ensure(8 * split_elems);
             b->d_hv_lo.ensure(8 * split_elems);
             b->d_hv_s0.ensure(4 * split_elems);
@@ -4332,7 +4422,7 @@ void phase_group(skm_build* b, uint32_t pass) {
             H.lo = b->d_hv_lo.as<uint64_t>();
             H.s0 = b->d_hv_s0.as<uint32_t>();
             H.s1 = b->d_hv_s1.as<uint32_t>();
-            hipLaunchKernelGGL(k_ovf_split, dim3(nsplit), dim3(BP_THREADS), 0, st2, A2, S, H);
+            hipLaunchKernelGGL(k_ovf_split, dim3(nsplit), dim3(BP_THREADS), 0, st2, A2, S, H, key_min);
             SKM_HIP(hipEventRecord(b->ev_split, st2));
             SKM_HIP(hipStreamWaitEvent(st3, b->ev_split, 0));
             hipLaunchKernelGGL(k_heavy, dim3(HEAVY_GRID), dim3(HEAVY_WG), 0, st2, A2, H);
@@ -4811,7 +4901,9 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "chain_prio" ? &t.chain_prio
                : n == "bucket_prio" ? &t.bucket_prio
                : n == "chain_lds_kb" ? &t.chain_lds_kb
-               : n == "host_timing" ? &t.host_timing : nullptr;
+               : n == "host_timing" ? &t.host_timing
+               : n == "heavy_min" ? &t.heavy_min
+               : n == "split_min" ? &t.split_min : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")
