@@ -21,6 +21,8 @@ ap.add_argument("--families", type=int, default=4000)
 ap.add_argument("--steps", type=int, default=1)
 ap.add_argument("--option", action="append", default=[])
 ap.add_argument("--chain-bench", action="store_true")
+ap.add_argument("--files", type=int, default=0, help="only the first N genome files (250 = the C2 workload)")
+ap.add_argument("--runs", type=int, default=0, help="builds to run (default: steps + 1, or 6 with --files)")
 a = ap.parse_args()
 
 
@@ -35,6 +37,8 @@ if a.chain_bench:
             log(f"chain n={n} {nm}: {ms:.2f} ms = {1e6 * ms / n:.1f} ns/sample")
 files = (a.seqs_total + bench.PER_FILE - 1) // bench.PER_FILE
 sh = bench.gen(synth, a.seqs_total, a.families, 0, files, 1, a.cache_dir)
+if a.files:
+    sh = bench.Shard(sh.parts[:a.files])
 log(f"{sh.n_seqs:,} proteins, {sh.n_windows:,} windows")
 b = skm.SignatureBuilder(len(synth.functions(a.families)))
 for kv in a.option:
@@ -44,7 +48,7 @@ sh.add_to(b)
 t = time.time()
 b.prepare()
 log(f"prepare {time.time() - t:.1f} s")
-for s in range(a.steps + 1):
+for s in range(a.runs or (a.steps + (1 if a.files == 0 else 5))):
     t = time.time()
     b.run()
     log(f"run {s}: {1000 * (time.time() - t):.0f} ms wall; " + json.dumps({k: round(v, 1) for k, v in b.timings().items()}))

@@ -9,7 +9,7 @@ eval "set -- $VARIANTS"
 for v in "$@"; do
   opts=""
   for kv in $v; do opts="$opts --option $kv"; done
-  timeout -k 10 300 python3 -u tools/c3_diag.py --cache-dir /tmp/c3 --steps 2 $opts > $O/c3v$i.log 2>&1 || { tail -5 $O/c3v$i.log; exit 1; }
-  echo "variant $i [$v]: $(grep 'run 2' $O/c3v$i.log)"
+  timeout -k 10 300 python3 -u tools/c3_diag.py --cache-dir /tmp/c3 --steps 2 ${DIAG_ARGS:-} $opts > $O/c3v$i.log 2>&1 || { tail -5 $O/c3v$i.log; exit 1; }
+  echo "variant $i [$v]: $(grep 'run ' $O/c3v$i.log | tail -1)"
   i=$((i+1))
 done
