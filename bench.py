@@ -31,6 +31,11 @@ import os
 import sys
 import time
 
+# libskm drives up to 8 streams per build (two overflow streams, stashed and giant chain streams);
+# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4), read at HIP init
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))

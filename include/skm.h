@@ -118,8 +118,9 @@ int skm_build_last_timings(skm_build* b, float* ms, int cap);
  * [3]=chain jobs [4]=chain samples [5]=sequences [6]=occurrences grouped on this rank
  * [7]=occurrences in overflow sub-buckets [8]=k-mers kept by the overflow path
  * [9]=groups of > 64 members handed to k_big_groups [10]=k-mers kept among them
- * [11]=key-range passes [12]=valid windows (occurrences) this rank extracts; totals over the
- * passes of the run; returns entries written. */
+ * [11]=key-range passes [12]=valid windows (occurrences) this rank extracts [13]=giant chains
+ * (heavy k-mers whose P^2 / variance chains start right after k_heavy) [14]=the longest of them;
+ * totals over the passes of the run; returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Host transport: the rank collectives of a multi-process build run by the caller on host
  * buffers, for ranks joined by a channel other than RCCL (the tests drive it with
@@ -158,7 +159,9 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   "overflow_inline_min", "overflow_inline_prio", "overflow_long_class", "overflow_chain_wgs",
  *   "chain_prio", "bucket_prio", "chain_lds_kb", "host_timing",
  *   "heavy_min" (occurrences that send a k-mer to the heavy path), "split_min" (overflow
- *   sub-buckets at least this large are split into heavy keys + a light remainder).
+ *   sub-buckets at least this large are split into heavy keys + a light remainder),
+ *   "giant_class" (heavy chains of >= 2^class samples start right after the heavy kernel on
+ *   their own streams; 0 = off).
  * Unknown names and out-of-range values return SKM_E_ARG. */
 int skm_build_set_option(skm_build* b, const char* name, int64_t value);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then

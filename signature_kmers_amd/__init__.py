@@ -286,10 +286,11 @@ class SignatureBuilder:
         return self.counters()["passes"]
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 13)()
-        n = lib().skm_build_counters(self._h, v, 13)
+        v = (C.c_uint64 * 15)()
+        n = lib().skm_build_counters(self._h, v, 15)
         names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped",
-                 "overflow_elements", "overflow_kept", "big_groups", "big_kept", "passes", "valid"]
+                 "overflow_elements", "overflow_kept", "big_groups", "big_kept", "passes", "valid", "giant_chains",
+                 "giant_max"]
         return {names[i]: int(v[i]) for i in range(n)}
 
     def debug_jobs(self, k: int = 64) -> list:

@@ -998,6 +998,27 @@ __global__ __launch_bounds__(128) void k_chain_long(const Job* __restrict__ jobs
     }
 }
 
+// Giant chains of one pass (k_heavy's slot list): the job count is read on the device, so the
+// launch needs no host round trip; one wave pair per job, idle workgroups exit at once.
+__global__ __launch_bounds__(128) void k_chain_dyn(const Job* __restrict__ jobs, const unsigned long long* __restrict__ njobs,
+                                                   skm_stored_kmer_data* __restrict__ out, int prio) {
+    const uint64_t nj = *njobs;
+    if (prio == 1) __builtin_amdgcn_s_setprio(1);
+    if (prio == 2) __builtin_amdgcn_s_setprio(2);
+    if (prio >= 3) __builtin_amdgcn_s_setprio(3);
+    for (uint64_t q = blockIdx.x; q < nj; q += gridDim.x) {
+        const Job jb = jobs[q];
+        const uint32_t* x = reinterpret_cast<const uint32_t*>(jb.lens_off);
+        if (threadIdx.x < 64) {
+            const double med = chain_long_p2(x, jb.n);
+            if (threadIdx.x == 0) out[jb.out_idx].median = d2u16(med);
+        } else {
+            const double v = chain_long_var(x, jb.n);
+            if (threadIdx.x == 64) out[jb.out_idx].var = d2u16(v);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, uint64_t njobs,
                                                 const uint32_t* __restrict__ lens, const uint32_t* __restrict__ recs32,
                                                 const uint32_t* __restrict__ tmp32, const uint32_t* __restrict__ big32,
@@ -2927,6 +2948,15 @@ struct HeavyArgs {
     uint64_t* lo;
     uint32_t* s0;                 // radix-sort ping-pong of the best members' sequence indices
     uint32_t* s1;
+    // giant chains (>= 2^giant_class samples): samples and jobs in this pass's slot buffers, run
+    // by k_chain_dyn on a chain stream as soon as k_heavy ends (the pass's own lens buffer is
+    // reused by the next pass; the slot's is not until its chains are done)
+    uint32_t giant_min;           // 0: off
+    uint32_t* gsamples;
+    Job* gjobs;
+    unsigned long long* gcount;   // [0] jobs, [1] samples
+    uint64_t gcap;                // sample capacity
+    unsigned long long* gstat;    // run totals: [0] giant chains, [1] longest
 };
 
 __device__ __forceinline__ uint32_t split_hash(uint32_t rem) { return (rem * 0x9E3779B1u) >> (32 - 12); }
@@ -3314,14 +3344,23 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
         while (bits < 32 && (smax >> bits)) bits += RB;
         const uint32_t* sorted = wg_radix_sort_u32(sa, sb, cb, bits, s_hist, s_wc, s_run, tag);
         __syncthreads();
+        const bool giant = H.giant_min && cb >= H.giant_min;
         if (tid == 0) {
             s_sel[0] = (uint32_t)atomicAdd(A.kept_ctr, 1ull);
             atomicAdd(&A.ctr[0], 1ull);
-            s_sel[1] = (uint32_t)atomicAdd(&A.ctr[3], 1ull);
-            s_cur = (uint32_t)atomicAdd(&A.ctr[4], (unsigned long long)cb);
+            if (giant) {
+                s_sel[1] = (uint32_t)atomicAdd(&H.gcount[0], 1ull);
+                s_cur = (uint32_t)atomicAdd(&H.gcount[1], (unsigned long long)cb);
+                atomicAdd(&H.gstat[0], 1ull);
+                atomicMax(&H.gstat[1], (unsigned long long)cb);
+            } else {
+                s_sel[1] = (uint32_t)atomicAdd(&A.ctr[3], 1ull);
+                s_cur = (uint32_t)atomicAdd(&A.ctr[4], (unsigned long long)cb);
+            }
         }
         __syncthreads();
         const uint32_t o = s_sel[0], jb = s_sel[1], loff = s_cur;
+        uint32_t* lens_out = giant ? H.gsamples : A.lens;
         for (uint32_t t0 = 0; t0 < cb; t0 += nt * U) {
             uint32_t sv[U];
 #pragma unroll
@@ -3332,17 +3371,22 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
                 const uint32_t t = t0 + u * nt + tid;
-                if (t < cb) A.lens[(uint64_t)loff + t] = A.glen[sv[u]];
+                if (t < cb) lens_out[(uint64_t)loff + t] = A.glen[sv[u]];
             }
         }
         if (tid == 0) {
             const uint64_t h43 = ((uint64_t)(A.bucket_base + K.bucket) << A.rem_bits) | K.rem;
             write_kept(A, o, kept_hi(h43, pre), kept_lo(best_f, mean, 0, 0));
             Job jbr;
-            jbr.lens_off = loff;
             jbr.n = cb;
             jbr.out_idx = o;
-            A.jobs[jb] = jbr;
+            if (giant) {
+                jbr.lens_off = reinterpret_cast<uint64_t>(H.gsamples + loff);  // device address
+                H.gjobs[jb] = jbr;
+            } else {
+                jbr.lens_off = loff;
+                A.jobs[jb] = jbr;
+            }
         }
         __syncthreads();
     }
@@ -3417,6 +3461,10 @@ struct Tune {
     int host_timing = 0;
     int heavy_min = (int)HEAVY_MIN;  // occurrences that make a key heavy (k_ovf_split)
     int split_min = (int)SPLIT_MIN;  // overflow sub-buckets of at least this size are split
+    // heavy chains of >= 2^class samples start right after k_heavy on rotating chain streams
+    // (0: off, the default: measured at C3, the FP64-bound chains running beside the pass kernels
+    // slow them by more than the ~0.5 s tail they would hide -- DESIGN.md section 4)
+    int giant_class = 0;
 };
 
 }  // namespace skm
@@ -3533,6 +3581,14 @@ struct skm_build {
     // run in batches on a fourth stream (mid-run and at the end), overlapping the later passes
     hipStream_t chain_st = nullptr;
     hipEvent_t chain_ev[3] = {};
+    // giant chains of k_heavy: rotating slots (stream, sample / job buffers, counters, events)
+    static constexpr int GSLOTS = 4;
+    hipStream_t gst[GSLOTS] = {};
+    hipEvent_t gev_ready[GSLOTS] = {}, gev_done[GSLOTS] = {};
+    std::deque<DevBuf> gsamples, gjobs, gcount;   // per key-range pass (reused by the next run)
+    bool gused[GSLOTS] = {};
+    DevBuf d_gstat;                      // run totals: giant chains, longest giant chain
+    uint64_t giant_jobs = 0, giant_max = 0;
     std::deque<DevBuf> long_arena;       // stashed samples per (pass, launch site)
     DevBuf d_long_jobs;                  // run-level list of stashed long jobs (device addresses)
     uint64_t long_jobs_cap = 0, n_long = 0, long_samples = 0, long_launched = 0;
@@ -4422,11 +4478,49 @@ void phase_group(skm_build* b, uint32_t pass) {
             H.lo = b->d_hv_lo.as<uint64_t>();
             H.s0 = b->d_hv_s0.as<uint32_t>();
             H.s1 = b->d_hv_s1.as<uint32_t>();
+            // giant chains: samples and jobs in this pass's own buffers (a giant key's sub-bucket has
+            // at least giant_min elements, which bounds their size), run on a rotating chain stream
+            const int gs = (int)(pass % skm_build::GSLOTS);
+            H.giant_min = b->tune.giant_class > 0 ? 1u << b->tune.giant_class : 0u;
+            H.gsamples = nullptr;
+            H.gjobs = nullptr;
+            H.gcount = nullptr;
+            H.gcap = 0;
+            H.gstat = nullptr;
+            uint64_t gcap = 0;
+            for (uint32_t q = 0; q < nsplit && H.giant_min; ++q)
+                if (ov[q].n >= H.giant_min) gcap += ov[q].n;
+            if (gcap == 0) H.giant_min = 0;
+            if (H.giant_min) {
+                while (b->gsamples.size() <= pass) {
+                    b->gsamples.emplace_back();
+                    b->gjobs.emplace_back();
+                    b->gcount.emplace_back();
+                }
+                b->gsamples[pass].ensure(4 * gcap);
+                b->gjobs[pass].ensure(sizeof(Job) * (gcap / H.giant_min + 16));
+                b->gcount[pass].ensure(16);
+                SKM_HIP(hipMemsetAsync(b->gcount[pass].p, 0, 16, st2));
+                H.gsamples = b->gsamples[pass].as<uint32_t>();
+                H.gjobs = b->gjobs[pass].as<Job>();
+                H.gcount = b->gcount[pass].as<unsigned long long>();
+                H.gcap = gcap;
+                H.gstat = b->d_gstat.as<unsigned long long>();
+            }
             hipLaunchKernelGGL(k_ovf_split, dim3(nsplit), dim3(BP_THREADS), 0, st2, A2, S, H, key_min);
             SKM_HIP(hipEventRecord(b->ev_split, st2));
             SKM_HIP(hipStreamWaitEvent(st3, b->ev_split, 0));
             hipLaunchKernelGGL(k_heavy, dim3(HEAVY_GRID), dim3(HEAVY_WG), 0, st2, A2, H);
             SKM_HIP(hipGetLastError());
+            if (H.giant_min) {
+                SKM_HIP(hipEventRecord(b->gev_ready[gs], st2));
+                SKM_HIP(hipStreamWaitEvent(b->gst[gs], b->gev_ready[gs], 0));
+                hipLaunchKernelGGL(k_chain_dyn, dim3(1024), dim3(128), 0, b->gst[gs], H.gjobs, H.gcount,
+                                   A.out_data, b->tune.chain_prio);
+                SKM_HIP(hipGetLastError());
+                SKM_HIP(hipEventRecord(b->gev_done[gs], b->gst[gs]));
+                b->gused[gs] = true;
+            }
         }
         if (nheavy)
             hipLaunchKernelGGL(k_overflow, dim3(nheavy), dim3(BP_THREADS), 0, st2, A2, S, inline_min, prio);
@@ -4520,6 +4614,8 @@ void begin_run(skm_build* b) {
     SKM_HIP(hipEventRecord(b->ev_start, st));
     SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 256, st));
     SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->n_total ? b->n_total : 1, st));
+    b->d_gstat.ensure(16);
+    SKM_HIP(hipMemsetAsync(b->d_gstat.p, 0, 16, st));
     if (b->pass_bits && b->rp)
         hipLaunchKernelGGL(k_pass_ids, dim3(4096), dim3(256), 0, st, b->d_res.as<uint8_t>(), b->rp, b->pass_bits,
                            b->d_ids.as<uint8_t>(), nullptr);
@@ -4590,6 +4686,8 @@ void phase_stats(skm_build* b) {
         SKM_HIP(hipEventRecord(b->chain_ev[2], b->chain_st));
         SKM_HIP(hipStreamWaitEvent(st, b->chain_ev[2], 0));
     }
+    for (int g = 0; g < skm_build::GSLOTS; ++g)  // the giant chains of every pass
+        if (b->gused[g]) SKM_HIP(hipStreamWaitEvent(st, b->gev_done[g], 0));
     SKM_HIP(hipEventRecord(b->ev[7], st));
     SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
@@ -4608,8 +4706,14 @@ void phase_final(skm_build* b) {
     hipLaunchKernelGGL(k_count_flags, dim3(256), dim3(256), 0, st, b->d_flags.as<uint8_t>(), b->n_total,
                        b->d_ctr.as<unsigned long long>() + 2);
     SKM_HIP(hipGetLastError());
+    {
+        unsigned long long* pin = b->pinned_ctr();
+        SKM_HIP(hipMemcpyAsync(pin + 48, b->d_gstat.p, 16, hipMemcpyDeviceToHost, st));
+    }
     SKM_HIP(hipEventRecord(b->ev[8], st));
     SKM_HIP(hipEventSynchronize(b->ev[8]));
+    b->giant_jobs = b->pinned_ctr()[48];
+    b->giant_max = b->pinned_ctr()[49];
     for (int i = 0; i < 12; ++i) b->last_ms[i] = b->pass_ms[i];
     SKM_HIP(hipEventElapsedTime(&b->last_ms[6], b->ev[7], b->ev[8]));      // stats (+ reductions)
     SKM_HIP(hipEventElapsedTime(&b->last_ms[7], b->ev_start, b->ev[8]));   // whole run
@@ -4661,6 +4765,17 @@ Ranks ranks_of(skm_build* b) {
 
 }  // namespace
 
+// A build drives up to 8 streams at once (group-by, two overflow streams, the stashed-chain
+// stream and four giant-chain slots).  HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues
+// (default 4); streams sharing a queue execute in order, which would serialise a pass behind the
+// previous pass's long chains.  Ask for at least 8 (read at HIP init, so
+// this only takes effect when libskm is loaded before the first HIP call; bench.py, the tests and
+// the CLIs set it themselves).
+__attribute__((constructor)) static void skm_hw_queues() {
+    const char* q = getenv("GPU_MAX_HW_QUEUES");
+    if (!q || atoi(q) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
+}
+
 extern "C" {
 
 int skm_build_create(skm_build** out, const int* devices, int n_devices, const skm_build_opts* opts) {
@@ -4686,6 +4801,11 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     for (auto& e : b->ev) SKM_HIP(hipEventCreate(&e));
     SKM_HIP(hipEventCreate(&b->ev_start));
     SKM_HIP(hipStreamCreateWithFlags(&b->chain_st, hipStreamNonBlocking));
+    for (int g = 0; g < skm_build::GSLOTS; ++g) {
+        SKM_HIP(hipStreamCreateWithFlags(&b->gst[g], hipStreamNonBlocking));
+        SKM_HIP(hipEventCreateWithFlags(&b->gev_ready[g], hipEventDisableTiming));
+        SKM_HIP(hipEventCreateWithFlags(&b->gev_done[g], hipEventDisableTiming));
+    }
     for (auto& e : b->chain_ev) SKM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_part, hipEventDisableTiming));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_split, hipEventDisableTiming));
@@ -4903,11 +5023,13 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "chain_lds_kb" ? &t.chain_lds_kb
                : n == "host_timing" ? &t.host_timing
                : n == "heavy_min" ? &t.heavy_min
-               : n == "split_min" ? &t.split_min : nullptr;
+               : n == "split_min" ? &t.split_min
+               : n == "giant_class" ? &t.giant_class : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")
             SKM_CHECK(value >= 1 && value < 32, SKM_E_ARG, "long chain classes in [1, 32)");
+        if (n == "giant_class") SKM_CHECK(value < 32, SKM_E_ARG, "giant_class in [0, 32)");
         *f = (int)value;
     }
     b->prepared = false;  // pass geometry and buffers are re-planned on the next prepare/run
@@ -5028,9 +5150,10 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
-    const uint64_t v[13] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
-                            b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total};
-    int n = std::min(cap, 13);
+    const uint64_t v[15] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+                            b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total,
+                            b->giant_jobs, b->giant_max};
+    int n = std::min(cap, 15);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }
@@ -5197,6 +5320,14 @@ void skm_build_destroy(skm_build* b) {
     if (b->ev_part) (void)hipEventDestroy(b->ev_part);
     if (b->ev_split) (void)hipEventDestroy(b->ev_split);
     if (b->ev_start) (void)hipEventDestroy(b->ev_start);
+    for (int g = 0; g < skm_build::GSLOTS; ++g) {
+        if (b->gst[g]) {
+            (void)hipStreamSynchronize(b->gst[g]);
+            (void)hipStreamDestroy(b->gst[g]);
+        }
+        if (b->gev_ready[g]) (void)hipEventDestroy(b->gev_ready[g]);
+        if (b->gev_done[g]) (void)hipEventDestroy(b->gev_done[g]);
+    }
     if (b->chain_st) {
         (void)hipStreamSynchronize(b->chain_st);
         (void)hipStreamDestroy(b->chain_st);

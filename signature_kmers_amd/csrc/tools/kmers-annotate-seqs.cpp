@@ -11,6 +11,7 @@
 #include <sys/stat.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <iostream>
 #include <thread>
@@ -29,6 +30,10 @@ void die(const std::string& m) {
 }  // namespace
 
 int main(int argc, char** argv) {
+    {  // libskm runs up to 8 streams at once: at least 8 hardware queues (read at the first HIP call)
+        const char* q = getenv("GPU_MAX_HW_QUEUES");
+        if (!q || atoi(q) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
+    }
     Options op;
     op.specs = {{"kmer-data-dir", 'd', false, false}, {"genus-data-dir", 'g', false, false},
                 {"sequences-dir", 0, false, false},   {"calls-file", 0, false, false},

@@ -25,6 +25,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
@@ -94,6 +95,10 @@ void dump_extract(const std::string& path, const std::vector<FastaFile>& files, 
 }  // namespace
 
 int main(int argc, char** argv) {
+    {  // libskm runs up to 8 streams at once: at least 8 hardware queues (read at the first HIP call)
+        const char* q = getenv("GPU_MAX_HW_QUEUES");
+        if (!q || atoi(q) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
+    }
     Options op;
     op.specs = {{"definition-dir", 'D', false, true},  {"fasta-dir", 'F', false, true},
                 {"fasta-keep-functions-dir", 'K', false, true}, {"good-functions", 0, false, true},

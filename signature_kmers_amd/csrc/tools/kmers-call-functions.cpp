@@ -14,6 +14,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
@@ -86,6 +87,10 @@ void debug_hits(skm_db* db, const std::vector<uint8_t>& dat, const FastaFile& f,
 }  // namespace
 
 int main(int argc, char** argv) {
+    {  // libskm runs up to 8 streams at once: at least 8 hardware queues (read at the first HIP call)
+        const char* q = getenv("GPU_MAX_HW_QUEUES");
+        if (!q || atoi(q) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
+    }
     Options op;
     op.specs = {{"data-dir", 'd', false, false}, {"input-files", 'i', false, true}, {"output-files", 'o', false, false},
                 {"n-threads", 'j', false, false}, {"ignore-hypo", 0, true, false},  {"debug-hits", 0, true, false},

@@ -14,6 +14,7 @@
 #include <sys/stat.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <string>
@@ -41,6 +42,10 @@ bool file_exists(const std::string& p) {
 }  // namespace
 
 int main(int argc, char** argv) {
+    {  // libskm runs up to 8 streams at once: at least 8 hardware queues (read at the first HIP call)
+        const char* q = getenv("GPU_MAX_HW_QUEUES");
+        if (!q || atoi(q) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
+    }
     Options op;
     op.specs = {{"data-dir", 'd', false, false},   {"input-file", 'i', false, false}, {"output-file", 'o', false, false},
                 {"min-hits", 0, false, false},    {"n-threads", 'j', false, false},  {"debug-hits", 0, true, false},

@@ -1,4 +1,7 @@
 import os
+
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:  # libskm runs up to 8 streams (read at HIP init)
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 import sys
 
 import pytest

@@ -221,8 +221,8 @@ def test_device_exact_division(skm, gpu):
     assert skm.debug_div_check(1 << 22, 64) == 0
 
 
-@pytest.mark.parametrize("passes", [0, 2])
-def test_heavy_keys_split_path(skm, gpu, passes):
+@pytest.mark.parametrize("passes,giant_class", [(0, 0), (0, 11), (2, 12), (4, 17)])
+def test_heavy_keys_split_path(skm, gpu, passes, giant_class):
     """k_ovf_split / k_heavy: overflow sub-buckets of >= 4096 elements lose their keys of >= 1024
     occurrences to the heavy path (Boyer-Moore majority + exact count for the fp32 80 % cut, radix
     select of the upper-median offset, sequence-index radix sort for the visit-order samples).
@@ -255,9 +255,12 @@ def test_heavy_keys_split_path(skm, gpu, passes):
     b = skm.SignatureBuilder(6)
     if passes:
         b.set_option("key_range_passes", passes)
+    b.set_option("giant_class", giant_class)  # 0: off; 11/12: the planted keys' chains start after k_heavy
     b.add_batch(res, off, lens, func, sid)
     b.run()
     ovf = b.debug_overflow()
+    if giant_class in (11, 12):
+        assert b.counters()["giant_chains"] >= 2
     got = b.finish()
     b.close()
     assert_same(got, ref)
