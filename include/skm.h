@@ -104,7 +104,15 @@ int skm_build_add_batch(skm_build* b, const uint8_t* residues, const uint64_t* s
                         const uint32_t* seq_len, const uint16_t* seq_func, const uint32_t* seq_id,
                         size_t n_seqs);
 
-/* Upload + pack everything added so far into HBM (idempotent). */
+/* Optional capacity hint: the total residues and sequences that will be added, so the HBM
+ * residue buffer is allocated once instead of grown.  Batches stream to HBM as they are added,
+ * packed into two pinned staging buffers that alternate (the host packs one while the DMA engine
+ * copies the other); the caller may overlap parsing with add_batch (kmers-build-signatures does).
+ * Replaces nothing in the reference (its build reads the FASTA into host memory,
+ * signature_build.tcc:48-70); new in this port. */
+int skm_build_reserve(skm_build* b, uint64_t n_residues, uint64_t n_seqs);
+
+/* Flush the last staging buffer, pack the metadata into HBM (idempotent). */
 int skm_build_prepare(skm_build* b);
 /* Run the device pipeline over the resident input; results stay on the device. */
 int skm_build_run(skm_build* b);

@@ -94,6 +94,7 @@ _SIGS = {
     "skm_debug_exchange_plan": (C.c_int, [C.POINTER(_Transport), C.c_int, C.c_int, C.c_uint32, _P, _P, _P, _P]),
     "skm_debug_transport_check": (C.c_int, [C.POINTER(_Transport), C.c_int, C.c_int]),
     "skm_build_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
+    "skm_build_reserve": (C.c_int, [_P, C.c_uint64, C.c_uint64]),
     "skm_build_debug_jobs": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int]),
     "skm_build_debug_overflow": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int]),
     "skm_debug_chain_bench": (C.c_int, [C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_float)]),
@@ -252,6 +253,11 @@ class SignatureBuilder:
         sid = None if seq_id is None else np.ascontiguousarray(seq_id, dtype=np.uint32)
         _check(lib().skm_build_add_batch(self._h, _ptr(residues), _ptr(seq_off), _ptr(seq_len), _ptr(seq_func),
                                          _ptr(sid) if sid is not None else None, n))
+
+    def reserve(self, n_residues: int, n_seqs: int):
+        """skm_build_reserve: capacity hint so the HBM residue buffer is allocated once (batches
+        stream to HBM through two alternating pinned staging buffers as they are added)."""
+        _check(lib().skm_build_reserve(self._h, int(n_residues), int(n_seqs)))
 
     def set_transport(self, transport: "GlooTransport"):
         """Join the ranks through a host transport (skm_build_set_transport) instead of RCCL."""

@@ -218,6 +218,7 @@ __device__ uint32_t kth_dev(const uint16_t* v, uint32_t n, uint32_t C2, uint32_t
 }
 
 // HitSet::process over window range [first, last] with current function cur.
+template <bool LEGACY_MAD>
 __device__ void hitset_process(const CallArgs& A, const uint32_t* hit, uint16_t* scr, uint32_t first, uint32_t last,
                                uint32_t cur, double seqlen, skm_kmer_call* slots, uint32_t& ncalls) {
     uint32_t n = 0, last_cur = first;
@@ -264,7 +265,7 @@ __device__ void hitset_process(const CallArgs& A, const uint32_t* hit, uint16_t*
         mean = (num1 * (mu[0] + mu[1] + mu[2]) + num2 * mu[3]) / float(n);
     }
     float median, mad;
-    if (A.mad_mode == 1) {
+    if constexpr (LEGACY_MAD) {
         legacy_median_mad(scr, n, median, mad);
     } else {
         heap_sort_u16(scr, n);
@@ -408,6 +409,7 @@ constexpr uint32_t SEG_CAP = 1024;  // 16 KB of LDS per 4-wave block: 8 blocks p
 // lanes 0-3, or the single running mean), median by an LDS bitonic sort, MAD as the k-th
 // deviation of the sorted run, the length window test, and the KmerCall (count = -1: none).
 // Segments of more than SEG_CAP hits take the sequential path on a private global scratch.
+template <bool LEGACY_MAD>  // mad_mode 1 in its own instantiation: no register cost for the default
 __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, const uint4* __restrict__ segs,
                                                                 uint32_t nseg, skm_kmer_call* __restrict__ out,
                                                                 uint16_t* __restrict__ pool,
@@ -437,7 +439,7 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
         if (lane == 0) {
             uint16_t* scr = pool + atomicAdd(pool_ctr, (unsigned long long)n);
             uint32_t nc = 0;
-            hitset_process(A, hit, scr, first, last, cur, seqlen, out + j, nc);
+            hitset_process<LEGACY_MAD>(A, hit, scr, first, last, cur, seqlen, out + j, nc);
             if (nc == 0) out[j].count = -1;
         }
         return;
@@ -489,7 +491,7 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
         c.protein_length_med_avg_dev = mad;
         out[j] = c;
     };
-    if (A.mad_mode == 1) {  // the <= 1.75 MAD: libstdc++ selection order on the hit-order run
+    if constexpr (LEGACY_MAD) {  // the <= 1.75 MAD: libstdc++ selection order on the hit-order run
         if (lane != 0) return;
         float median, mad;
         legacy_median_mad(buf, n, median, mad);
@@ -862,9 +864,12 @@ void query_run(skm_query* q, const skm_annot_opts* o) {
         hipLaunchKernelGGL(k_gather_segs, dim3(ceil_div(ns, 256)), dim3(256), 0, st, q->d_slots.as<uint4>(),
                            q->d_cap_off.as<uint64_t>(), q->d_seg_off.as<uint64_t>(), ns, q->d_segs.as<uint4>());
         if (nseg)
-            hipLaunchKernelGGL(k_seg_process, dim3((uint32_t)ceil_div(nseg, SEG_WAVES)), dim3(64 * SEG_WAVES), 0, st, A,
+        {
+            auto kseg = A.mad_mode == 1 ? k_seg_process<true> : k_seg_process<false>;
+            hipLaunchKernelGGL(kseg, dim3((uint32_t)ceil_div(nseg, SEG_WAVES)), dim3(64 * SEG_WAVES), 0, st, A,
                                q->d_segs.as<uint4>(), (uint32_t)nseg, q->d_segres.as<skm_kmer_call>(),
                                q->d_scr.as<uint16_t>(), q->d_pool_ctr.as<unsigned long long>());
+        }
         SKM_HIP(hipGetLastError());
         SKM_HIP(hipEventRecord(q->ev[3], st));
         hipLaunchKernelGGL(k_count_calls, dim3(ceil_div(ns, 256)), dim3(256), 0, st, q->d_segres.as<skm_kmer_call>(),

@@ -3487,7 +3487,18 @@ struct skm_build {
     uint64_t ovf_elems = 0, ovf_kept = 0;
 
     // host staging (reference emission order, only sequences with a kept function)
-    std::vector<uint8_t> h_res;     // packed residues with one 0 separator after each sequence
+    // residues stream to HBM as batches arrive: packed (one 0 separator after each sequence) into
+    // two pinned staging buffers that alternate -- the host fills one while the DMA engine copies
+    // the other (section 8(f)4); prepare only flushes the last one
+    uint8_t* st_pin[2] = {};
+    size_t st_fill[2] = {};
+    hipEvent_t st_ev[2] = {};
+    bool st_busy[2] = {};
+    int st_cur = 0;
+    uint64_t rp_total = 0;          // residues packed so far (incl. separators)
+    uint64_t rp_dev = 0;            // bytes of them issued to the device
+    uint64_t res_cap = 0;           // d_res capacity
+    double stage_ms = 0;            // host time spent packing + waiting for a free staging buffer
     std::vector<SeqMeta> h_meta;
     std::vector<uint32_t> h_seqid;
     uint64_t n_windows = 0;
@@ -3871,17 +3882,57 @@ void set_geometry(skm_build* b) {
     b->b1_bits = total - ob;
 }
 
+// ------------------------------------------------------------------------------------------
+// Residue staging (pinned, double-buffered host -> HBM)
+// ------------------------------------------------------------------------------------------
+constexpr size_t STAGE_BYTES = 64ull << 20;
+
+// d_res holds at least `need` bytes; growing keeps the bytes already uploaded (device copy)
+void res_reserve(skm_build* b, uint64_t need) {
+    if (need <= b->res_cap && b->d_res.p) return;
+    const uint64_t cap = std::max<uint64_t>({need, b->res_cap + b->res_cap / 2, STAGE_BYTES});
+    void* np = nullptr;
+    SKM_HIP(hipMalloc(&np, cap));
+    if (b->rp_dev) SKM_HIP(hipMemcpyAsync(np, b->d_res.p, b->rp_dev, hipMemcpyDeviceToDevice, b->stream));
+    SKM_HIP(hipStreamSynchronize(b->stream));
+    if (b->d_res.p) SKM_HIP(hipFree(b->d_res.p));
+    b->d_res.p = np;
+    b->d_res.bytes = cap;
+    b->res_cap = cap;
+}
+
+// hand the current staging buffer to the DMA engine and switch to the other one (waiting only if
+// its previous copy is still in flight)
+void stage_flush(skm_build* b) {
+    const int c = b->st_cur;
+    if (b->st_fill[c]) {
+        res_reserve(b, b->rp_dev + b->st_fill[c] + 64);
+        SKM_HIP(hipMemcpyAsync(b->d_res.as<uint8_t>() + b->rp_dev, b->st_pin[c], b->st_fill[c], hipMemcpyHostToDevice,
+                               b->stream));
+        SKM_HIP(hipEventRecord(b->st_ev[c], b->stream));
+        b->st_busy[c] = true;
+        b->rp_dev += b->st_fill[c];
+        b->st_fill[c] = 0;
+    }
+    b->st_cur ^= 1;
+    const int n = b->st_cur;
+    if (b->st_busy[n]) {
+        SKM_HIP(hipEventSynchronize(b->st_ev[n]));
+        b->st_busy[n] = false;
+    }
+    b->st_fill[n] = 0;
+}
+
 void prepare_local(skm_build* b) {
     SKM_HIP(hipSetDevice(b->device));
     set_geometry(b);
-    const uint64_t rp = b->h_res.size();
+    stage_flush(b);  // the last staging buffer; the residues are then resident
+    const uint64_t rp = b->rp_total;
     b->rp = rp;
     b->nseq = (uint32_t)b->h_meta.size();
     SKM_CHECK(b->h_meta.size() < (1ull << ELEM_S_BITS), SKM_E_ARG, "too many sequences in one build shard");
-    // upload
-    b->d_res.ensure(rp + 64);
-    SKM_HIP(hipMemsetAsync(b->d_res.p, 0, rp + 64, b->stream));
-    if (rp) SKM_HIP(hipMemcpyAsync(b->d_res.p, b->h_res.data(), rp, hipMemcpyHostToDevice, b->stream));
+    res_reserve(b, rp + 64);
+    SKM_HIP(hipMemsetAsync(b->d_res.as<uint8_t>() + rp, 0, 64, b->stream));  // window-load padding
     b->d_meta.ensure(sizeof(SeqMeta) * (b->nseq + 1));
     SeqMeta sentinel{rp, 0, 0xFFFF, 0};
     std::vector<SeqMeta> meta = b->h_meta;
@@ -4808,6 +4859,10 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     }
     for (auto& e : b->chain_ev) SKM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_part, hipEventDisableTiming));
+    for (int i = 0; i < 2; ++i) {
+        SKM_HIP(hipHostMalloc(reinterpret_cast<void**>(&b->st_pin[i]), STAGE_BYTES, hipHostMallocDefault));
+        SKM_HIP(hipEventCreateWithFlags(&b->st_ev[i], hipEventDisableTiming));
+    }
     SKM_HIP(hipEventCreateWithFlags(&b->ev_split, hipEventDisableTiming));
     for (auto& e : b->ev_o) SKM_HIP(hipEventCreate(&e));
     for (auto& e : b->ev_o3) SKM_HIP(hipEventCreate(&e));
@@ -4821,6 +4876,7 @@ int skm_build_add_batch(skm_build* b, const uint8_t* residues, const uint64_t* s
     SKM_API_BEGIN
     SKM_CHECK(b, SKM_E_ARG, "null build");
     SKM_CHECK(n_seqs == 0 || (residues && seq_off && seq_len && seq_func), SKM_E_ARG, "null array");
+    SKM_HIP(hipSetDevice(b->device));
     for (size_t s = 0; s < n_seqs; ++s) {
         const uint16_t f = seq_func[s];
         if (f == SKM_UNDEFINED_FUNCTION) continue;  // signature_build.tcc:155-158
@@ -4828,12 +4884,16 @@ int skm_build_add_batch(skm_build* b, const uint8_t* residues, const uint64_t* s
         const uint32_t len = seq_len[s];
         SKM_CHECK(len < (1u << ELEM_I_BITS), SKM_E_ARG, "protein longer than 1,048,575 residues");
         SeqMeta m;
-        m.pstart = b->h_res.size();
+        m.pstart = b->rp_total;
         m.len = len;
         m.func = f;
         m.pad = 0;
-        b->h_res.insert(b->h_res.end(), residues + seq_off[s], residues + seq_off[s] + len);
-        b->h_res.push_back(0);
+        if (b->st_fill[b->st_cur] + len + 1 > STAGE_BYTES) stage_flush(b);
+        uint8_t* dst = b->st_pin[b->st_cur] + b->st_fill[b->st_cur];
+        std::memcpy(dst, residues + seq_off[s], len);
+        dst[len] = 0;
+        b->st_fill[b->st_cur] += len + 1;
+        b->rp_total += len + 1;
         const uint32_t sid = seq_id ? seq_id[s] : (uint32_t)b->h_meta.size();
         if (!b->h_seqid.empty() && sid <= b->h_seqid.back()) b->seqid_strict = false;
         b->h_meta.push_back(m);
@@ -4842,6 +4902,16 @@ int skm_build_add_batch(skm_build* b, const uint8_t* residues, const uint64_t* s
     }
     b->prepared = false;
     b->ran = false;
+    SKM_API_END
+}
+
+int skm_build_reserve(skm_build* b, uint64_t n_residues, uint64_t n_seqs) {
+    SKM_API_BEGIN
+    SKM_CHECK(b, SKM_E_ARG, "null build");
+    SKM_HIP(hipSetDevice(b->device));
+    res_reserve(b, n_residues + n_seqs + 64);
+    b->h_meta.reserve(n_seqs);
+    b->h_seqid.reserve(n_seqs);
     SKM_API_END
 }
 
@@ -5318,6 +5388,11 @@ void skm_build_destroy(skm_build* b) {
     for (auto& e : b->ev_o3)
         if (e) (void)hipEventDestroy(e);
     if (b->ev_part) (void)hipEventDestroy(b->ev_part);
+    for (int i = 0; i < 2; ++i) {
+        if (b->st_busy[i] && b->st_ev[i]) (void)hipEventSynchronize(b->st_ev[i]);
+        if (b->st_pin[i]) (void)hipHostFree(b->st_pin[i]);
+        if (b->st_ev[i]) (void)hipEventDestroy(b->st_ev[i]);
+    }
     if (b->ev_split) (void)hipEventDestroy(b->ev_split);
     if (b->ev_start) (void)hipEventDestroy(b->ev_start);
     for (int g = 0; g < skm_build::GSLOTS; ++g) {

@@ -32,6 +32,9 @@
 #include <map>
 #include <sstream>
 #include <thread>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 
 #include "skm.h"
 #include "skm_caller.h"
@@ -234,9 +237,33 @@ int main(int argc, char** argv) {
 
     std::cerr << "extract kmers\n";
     std::vector<BuildBatch> batches(files.size());
-    for (size_t f = 0; f < files.size(); ++f)
-        select_build_sequences(fm, files[f], (unsigned)f, MaxSequencesPerFile, deleted_fids, batches[f]);
-    if (op.has("dump-extract")) {
+    // this rank's contiguous range of files (global file numbering keeps seq_id = file*100000+k)
+    const size_t f0 = files.size() * (size_t)rank / (size_t)world, f1 = files.size() * (size_t)(rank + 1) / (size_t)world;
+    // Sequence selection runs on a worker pool, file by file, while this thread streams every
+    // finished file (in order) into the build: skm_build_add_batch packs it into a pinned staging
+    // buffer whose DMA to HBM overlaps the next file's packing and the workers' selection.
+    const bool dump = op.has("dump-extract");
+    const size_t s0 = dump ? 0 : f0, s1 = dump ? files.size() : f1;
+    std::mutex sel_mu;
+    std::condition_variable sel_cv;
+    std::vector<char> sel_done(files.size(), 0);
+    std::atomic<size_t> sel_next{s0};
+    auto sel_work = [&]() {
+        for (size_t f; (f = sel_next.fetch_add(1)) < s1;) {
+            select_build_sequences(fm, files[f], (unsigned)f, MaxSequencesPerFile, deleted_fids, batches[f]);
+            std::lock_guard<std::mutex> g(sel_mu);
+            sel_done[f] = 1;
+            sel_cv.notify_all();
+        }
+    };
+    std::vector<std::thread> sel_pool;
+    for (int t = 0; t < std::max(1, n_threads - 1); ++t) sel_pool.emplace_back(sel_work);
+    auto join_selection = [&]() {
+        for (auto& t : sel_pool)
+            if (t.joinable()) t.join();
+    };
+    if (dump) {
+        join_selection();
         if (rank != 0) return 0;
         dump_extract(op.get("dump-extract"), files, batches);
         std::cerr << "wrote build input to " << op.get("dump-extract") << "\n";
@@ -256,8 +283,14 @@ int main(int argc, char** argv) {
         if (rc) die(std::string(what) + ": " + skm_last_error());
     };
     check(skm_build_create(&b, &device, 1, &bo), "skm_build_create");
-    // this rank's contiguous range of files (global file numbering keeps seq_id = file*100000+k)
-    const size_t f0 = files.size() * (size_t)rank / (size_t)world, f1 = files.size() * (size_t)(rank + 1) / (size_t)world;
+    {
+        uint64_t nres = 0, nseq = 0;
+        for (size_t f = f0; f < f1; ++f) {
+            nres += files[f].residues.size();
+            nseq += files[f].size();
+        }
+        check(skm_build_reserve(b, nres, nseq), "skm_build_reserve");
+    }
     skm_transport tp = mesh.transport();
     if (world > 1 && comm == "host") {
         check(skm_build_set_transport(b, &tp), "skm_build_set_transport");
@@ -273,12 +306,17 @@ int main(int argc, char** argv) {
         check(skm_build_set_comm(b, id), "skm_build_set_comm");
     }
     for (size_t f = f0; f < f1; ++f) {
+        {
+            std::unique_lock<std::mutex> g(sel_mu);
+            sel_cv.wait(g, [&] { return sel_done[f] != 0; });
+        }
         const BuildBatch& bb = batches[f];
         if (bb.off.empty()) continue;
         check(skm_build_add_batch(b, files[f].residues.data(), bb.off.data(), bb.len.data(), bb.func.data(),
                                   bb.seq_id.data(), bb.off.size()),
               "skm_build_add_batch");
     }
+    join_selection();
     std::cerr << "process kmers\n";
     t0 = now_s();
     check(skm_build_prepare(b), "skm_build_prepare");
