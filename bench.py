@@ -365,7 +365,9 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
         "passes": b.passes(),
         "counters": ctrs,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic(dom, shard.n_seqs),
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": _pmc_traffic(dom, {50_000_000: "c3", 1_000_000: "c2"}.get(shard.n_seqs, "") if world == 1
+                                             else "", shard.n_seqs),
                      "alg_bytes_per_launch": alg[dom], "avg_launch_ms": dom_ms,
                      "launches_per_step": b.passes()},
         "pipeline": {"alg_bytes": pipe_alg, "ms": 1000.0 * t_max / steps, "GBs": pipe_gbs,
@@ -442,7 +444,7 @@ def _annotate_leg(skm, kept, funcs, q, a, device, cores):
             "phase_ms": acc,
             "roofline": {"bound": "hbm", "kernel": "k_lookup<0>", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
-                         "avg_launch_ms": acc["lookup"], "traffic": _pmc_traffic("k_lookup<0>", len(lens))},
+                         "avg_launch_ms": acc["lookup"], "traffic": _pmc_traffic("k_lookup<0>", "legs", len(lens))},
             "cpu_baseline": cpu, "mph_build_s": mph_s}
 
 
@@ -515,20 +517,23 @@ def _matrix_leg(skm, matrix_in, a, device, cores):
             "phase_ms": acc,
             "roofline": {"bound": "hbm", "kernel": "k_md_rows", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
-                         "avg_launch_ms": acc["pairs"], "traffic": _pmc_traffic("k_md_rows", n)},
+                         "avg_launch_ms": acc["pairs"], "traffic": _pmc_traffic("k_md_rows", "legs", 10_000_000 if n == 100_000 else -1)},
             "cpu_baseline": cpu, "prep_s": prep_s}
 
 
-def _pmc_traffic(kernel: str, seqs: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json),
-    when it was measured on this kernel and workload; else None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def _pmc_traffic(kernel: str, workload: str, seqs: int):
+    """HBM bytes of `kernel` from the committed rocprofv3 PMC summary (profiles/r02_pmc_traffic.json,
+    tools/gpu_profile_r02.sh + tools/pmc_summary_r02.py): per build run (16 launches at C3, one at
+    C2 -- the same span as alg_bytes_per_launch / avg_launch_ms here) or per launch (legs), when it
+    was measured on this kernel and workload size; else None.  Streaming kernels count FETCH_SIZE
+    x2, gather kernels x1 (profiles/r02_fetch_calib.json)."""
+    path = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
     try:
         d = json.load(open(path))
-        e = d["kernels"][kernel]
-        if int(e.get("seqs", d.get("seqs_per_gpu", -1))) != int(seqs):
+        wl = d["workloads"][workload]
+        if int(wl.get("seqs", wl.get("queries", -1))) != int(seqs):
             return None
-        return e["hbm_bytes_per_launch"]
+        return d["kernels"][kernel][workload]["hbm_bytes"]
     except Exception:
         return None
 
