@@ -200,7 +200,7 @@ def main():
         else:
             queries = gen(synth, (c2_files + nqf) * PER_FILE, a.families, c2_files, nqf, workers)
     matrix_in = None
-    if world == 1 and a.matrix_seqs > 0:
+    if a.matrix_seqs > 0:  # every rank: the DB is replicated, the pair triangle tiled by rows
         fam, n_train = 200, 200_000
         nfq = (a.matrix_seqs + PER_FILE - 1) // PER_FILE
         tf = n_train // PER_FILE
@@ -295,9 +295,11 @@ def main():
     if world == 1 and queries is not None and kept is not None:
         log("annotate leg")
         out["annotate"] = _annotate_leg(skm, kept, funcs, queries, a, device, cores)
-    if world == 1 and matrix_in is not None:
+    if matrix_in is not None:
         log("matrix leg")
-        out["matrix"] = _matrix_leg(skm, matrix_in, a, device, cores)
+        mx = _matrix_leg(skm, matrix_in, a, device, cores, rank, world, dist)
+        if rank == 0:
+            out["matrix"] = mx
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
@@ -448,10 +450,12 @@ def _annotate_leg(skm, kept, funcs, q, a, device, cores):
             "cpu_baseline": cpu, "mph_build_s": mph_s}
 
 
-def _matrix_leg(skm, matrix_in, a, device, cores):
+def _matrix_leg(skm, matrix_in, a, device, cores, rank=0, world=1, dist=None):
     """kmers-matrix-distance (BASELINE configs[4]): a 200-family signature DB (built on this GPU from
     200K training proteins, BDZ on the GPU) resident in HBM, 100K fresh query proteins of the same
-    families, all-vs-all shared-signature-k-mer counts (one GPU computes every row).  One step =
+    families, all-vs-all shared-signature-k-mer counts.  With N ranks each GPU computes its band
+    of rows of the pair triangle (skm_matrix_tile_rows, equal triangle area; the hit lists are
+    recomputed on every GPU, no collective) and the step time is the max over ranks.  One step =
     window lookup + length filter, k-mer grouping (hash + radix sort), per-row LDS histograms of the
     pair increments, compaction of the nonzero pairs in row order; the pairs stay on the device.
     Roofline: k_md_rows (the pair increments), SURVEY 8(d) 4 B per pair increment."""
@@ -473,24 +477,36 @@ def _matrix_leg(skm, matrix_in, a, device, cores):
         files = None if a.no_cpu_baseline else (open(base + ".mph", "rb").read(), open(base + ".dat", "rb").read())
     prep_s = time.time() - t0
     md = skm.MatrixDistance(db, funcs, res, off, ln)
+    rows = skm.matrix_tile_rows(n, rank, world) if world > 1 else None
     for _ in range(max(1, a.warmup)):
-        md.run()
+        md.run(rows)
     steps = max(3, min(a.steps, 10))
     acc = {}
+    if dist is not None:
+        dist.barrier()
     t1 = time.perf_counter()
     for _ in range(steps):
-        md.run()
+        md.run(rows)
         for k, v in md.timings().items():
             acc[k] = acc.get(k, 0.0) + v
     wall = time.perf_counter() - t1
     acc = {k: v / steps for k, v in acc.items()}
     c = md.counters()
+    if dist is not None:  # max time over ranks; pair work summed over the bands
+        import torch
+        dist.barrier()
+        tt = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall = float(tt.item())
+        v = torch.tensor([float(c["increments"]), float(c["pairs"])], dtype=torch.float64)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        c = dict(c, increments=int(v[0]), pairs=int(v[1]))
     md.close()
     db.close()
     alg = 4 * c["increments"]
     gbs = alg / (acc["pairs"] * 1e-3) / 1e9
     cpu = None
-    if files is not None:  # the oracle's matrix distance on the host cores, bounded sample
+    if files is not None and world == 1:  # the oracle's matrix distance on the host cores, bounded sample
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ref
         threads = a.cpu_threads or cores["usable"]
@@ -511,7 +527,9 @@ def _matrix_leg(skm, matrix_in, a, device, cores):
     return {"metric": "query k-mers/sec (lookup + all-vs-all shared signature k-mer counts)",
             "value": c["windows"] * steps / wall, "unit": "k-mers/s", "ms_per_step": 1000.0 * wall / steps,
             "steps": steps, "pair_increments_per_s": c["increments"] / (acc["pairs"] * 1e-3),
-            "config": {"workload": f"C5: {n} query proteins of 200 families, all-vs-all, 1 GPU (one tile)",
+            "scaling": "strong", "n_gpus": world,
+            "config": {"workload": f"C5: {n} query proteins of 200 families, all-vs-all, {world} GPU(s) "
+                                   f"({'row bands of the triangle' if world > 1 else 'one tile'})",
                        "queries": n, "families": 200, "db_keys": int(len(kept.keys)), "windows": c["windows"],
                        "hits": c["hits"], "pair_increments": c["increments"], "nonzero_pairs": c["pairs"]},
             "phase_ms": acc,

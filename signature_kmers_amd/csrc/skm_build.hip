@@ -3465,6 +3465,7 @@ struct Tune {
     // (0: off, the default: measured at C3, the FP64-bound chains running beside the pass kernels
     // slow them by more than the ~0.5 s tail they would hide -- DESIGN.md section 4)
     int giant_class = 0;
+    int giant_passes = 0;            // giant chains only in the last N passes (0: all)
 };
 
 }  // namespace skm
@@ -4532,7 +4533,11 @@ void phase_group(skm_build* b, uint32_t pass) {
             // giant chains: samples and jobs in this pass's own buffers (a giant key's sub-bucket has
             // at least giant_min elements, which bounds their size), run on a rotating chain stream
             const int gs = (int)(pass % skm_build::GSLOTS);
-            H.giant_min = b->tune.giant_class > 0 ? 1u << b->tune.giant_class : 0u;
+            // (only in the last giant_passes passes: earlier passes' long chains overlap the
+            // later passes from the stash batches anyway; the last pass's would form the tail)
+            const uint32_t P = 1u << b->pass_bits;
+            const bool late = b->tune.giant_passes <= 0 || pass + (uint32_t)b->tune.giant_passes >= P;
+            H.giant_min = b->tune.giant_class > 0 && late ? 1u << b->tune.giant_class : 0u;
             H.gsamples = nullptr;
             H.gjobs = nullptr;
             H.gcount = nullptr;
@@ -5094,7 +5099,8 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "host_timing" ? &t.host_timing
                : n == "heavy_min" ? &t.heavy_min
                : n == "split_min" ? &t.split_min
-               : n == "giant_class" ? &t.giant_class : nullptr;
+               : n == "giant_class" ? &t.giant_class
+               : n == "giant_passes" ? &t.giant_passes : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")

@@ -11,7 +11,14 @@
 // hash order of its concurrent maps).  --min-hits, --debug-hits, --verbose and -j are accepted
 // and, as in the reference main, have no effect on the output.
 // Extra options: --device N, --max-tile-bytes B (bound on the dense count tile in HBM).
+// Multi-GPU: --n-gpus N forks one process per GPU before any GPU use; rank r
+// computes the rows [r_begin, r_end) of the pair triangle (skm_matrix_tile_rows: bands of equal
+// triangle area) on device --device + r (all on --device with --same-device, as the tests do on
+// one GPU) and streams its band's lines to rank 0 over a socket; rank 0 prints the bands in rank
+// order, i.e. the same lines in the same (seq1, seq2) order as one GPU.  No collective: every
+// rank recomputes the hit lists, the pair increments are split.
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -24,6 +31,7 @@
 #include "skm.h"
 #include "skm_caller.h"
 #include "skm_front.h"
+#include "skm_mesh.h"
 
 using namespace skmf;
 
@@ -50,7 +58,8 @@ int main(int argc, char** argv) {
     op.specs = {{"data-dir", 'd', false, false},   {"input-file", 'i', false, false}, {"output-file", 'o', false, false},
                 {"min-hits", 0, false, false},    {"n-threads", 'j', false, false},  {"debug-hits", 0, true, false},
                 {"verbose", 0, true, false},      {"help", 'h', true, false},        {"device", 0, false, false},
-                {"max-tile-bytes", 0, false, false}};
+                {"max-tile-bytes", 0, false, false}, {"n-gpus", 0, false, false},
+                {"same-device", 0, true, false}};
     op.positional = {"data-dir", "input-file"};
     std::string err;
     if (!op.parse(argc, argv, err)) die(err);
@@ -65,10 +74,16 @@ int main(int argc, char** argv) {
                   << "  --verbose                   Verbose mode\n"
                   << "  --device arg                HIP device ordinal (default 0)\n"
                   << "  --max-tile-bytes arg        HBM bound of the dense pair-count tile (default: 60 % of free)\n"
+                  << "  --n-gpus arg                ranks (one process and GPU each), row bands of the triangle\n"
+                  << "  --same-device               every rank on --device\n"
                   << "  -h [ --help ]               show this help message\n\n";
         return 0;
     }
-    const int device = std::atoi(op.get("device", "0").c_str());
+    const int ng = std::atoi(op.get("n-gpus", "1").c_str());
+    if (ng < 1 || ng > 64) die("--n-gpus must be in [1, 64]");
+    Mesh mesh;
+    if (!mesh_fork(ng, mesh, err)) die(err);  // before any GPU call
+    const int device = std::atoi(op.get("device", "0").c_str()) + (op.has("same-device") ? 0 : mesh.rank);
     const std::string data_dir = op.get("data-dir");
     const std::string db_base = path_join(data_dir, "kmer_data");
     const std::string mph = db_base + ".mph", dat = db_base + ".dat";
@@ -108,14 +123,29 @@ int main(int argc, char** argv) {
     skm_matrix_opts mo;
     std::memset(&mo, 0, sizeof(mo));
     mo.hypo_index = hypo;
+    if (ng > 1 && skm_matrix_tile_rows((uint32_t)index_to_id.size(), (uint32_t)mesh.rank, (uint32_t)ng, &mo.row_begin,
+                                       &mo.row_end))
+        die(skm_last_error());
     mo.max_tile_bytes = std::strtoull(op.get("max-tile-bytes", "0").c_str(), nullptr, 10);
     if (skm_matrix_run(m, &mo)) die(skm_last_error());
     uint64_t ctr[5] = {0, 0, 0, 0, 0};
     skm_matrix_counters(m, ctr, 5);
-    std::cerr << "kmer_hit_map size " << ctr[4] << "\n";
+    if (mesh.rank == 0) std::cerr << "kmer_hit_map size " << ctr[4] << "\n";
     skm_pairs pairs;
     if (skm_matrix_pairs(m, &pairs)) die(skm_last_error());
-    std::cerr << "write output\n";
+    if (mesh.rank == 0) std::cerr << "write output\n";
+    // rank 0 prints to stdout; the other ranks stream their band to rank 0
+    const int out_fd = mesh.rank == 0 ? 1 : mesh.fd[0];
+    auto flush = [&](std::string& b) {
+        size_t o = 0;
+        while (o < b.size()) {
+            const ssize_t w = write(out_fd, b.data() + o, b.size() - o);
+            if (w <= 0) die("write failed");
+            o += (size_t)w;
+        }
+        b.clear();
+    };
+    std::fflush(stdout);
     std::string buf;
     buf.reserve(1 << 20);
     for (uint64_t i = 0; i < pairs.n; ++i) {
@@ -126,15 +156,27 @@ int main(int argc, char** argv) {
         buf += '\t';
         buf += std::to_string(p[2]);
         buf += '\n';
-        if (buf.size() > (1u << 20)) {
-            std::fwrite(buf.data(), 1, buf.size(), stdout);
-            buf.clear();
-        }
+        if (buf.size() > (1u << 20)) flush(buf);
     }
-    std::fwrite(buf.data(), 1, buf.size(), stdout);
-    std::fflush(stdout);
+    flush(buf);
     skm_pairs_free(&pairs);
     skm_matrix_destroy(m);
     skm_db_close(db);
+    if (mesh.rank != 0) {
+        close(mesh.fd[0]);
+        return 0;
+    }
+    // the other bands, in rank (= row) order
+    std::vector<char> chunk(1 << 20);
+    for (int q = 1; q < ng; ++q) {
+        for (;;) {
+            const ssize_t r = read(mesh.fd[q], chunk.data(), chunk.size());
+            if (r < 0) die("read from rank " + std::to_string(q) + " failed");
+            if (r == 0) break;
+            std::string part(chunk.data(), (size_t)r);
+            flush(part);
+        }
+    }
+    if (!mesh.wait_children(err)) die(err);
     return 0;
 }

@@ -278,3 +278,42 @@ def test_call_functions_boost_math_legacy(c1_build, tmp_path):
     p = subprocess.run([os.path.join(BIN, "kmers-call-functions"), out, inputs[0], "--boost-math-stats", "old"],
                        capture_output=True, timeout=120)
     assert p.returncode != 0 and b"--boost-math-stats" in p.stderr
+
+
+def test_matrix_distance_row_bands_multi_rank(c1_build, tmp_path):
+    """kmers-matrix-distance --n-gpus 2/3 (--same-device: every rank on the one GPU): rank r
+    computes its band of rows (skm_matrix_tile_rows) and rank 0 prints the bands in rank order --
+    byte-identical to the one-process output."""
+    info, out, _, _ = c1_build
+    qdir = _query_dir(tmp_path / "q", seed=19)
+    fa = str(tmp_path / "all.faa")
+    with open(fa, "wb") as fh:
+        fh.write(b"".join(_lines(p) for p in fr.list_files(qdir)))
+    one, _ = _run([os.path.join(BIN, "kmers-matrix-distance"), out, fa])
+    assert one.count("\n") > 1000
+    for n in (2, 3):
+        many, err = _run([os.path.join(BIN, "kmers-matrix-distance"), out, fa, "--n-gpus", str(n), "--same-device"])
+        assert many == one, n
+        assert err.count("kmer_hit_map size ") == 1
+
+
+def test_build_signatures_multi_rank_host_comm(tmp_path, gpu):
+    """kmers-build-signatures --n-gpus 2 --comm host: two forked ranks on the one GPU, each
+    building its contiguous range of files and exchanging occurrences by owner through the
+    socketpair host transport; rank 0 writes every output -- the same files and stdout lines
+    as one process."""
+    from signature_kmers_amd import synth
+    info = synth.write_dirs(str(tmp_path / "in"), 1000, 40, per_file=100, extras=True)
+    outs = {}
+    for tag, extra in (("one", []), ("two", ["--n-gpus", "2", "--comm", "host"])):
+        o = str(tmp_path / tag)
+        stdout, _ = _run([os.path.join(BIN, "kmers-build-signatures"), "-D", info["ann_dir"], "-F", info["seqs_dir"],
+                          "--kmer-data-dir", o, "--final-kmers", "final.kmers", "--perfect-hash", "kmer_data.mph",
+                          "--perfect-hash-data", "kmer_data.dat"] + extra)
+        outs[tag] = (o, stdout)
+    (o1, s1), (o2, s2) = outs["one"], outs["two"]
+    assert s1 == s2
+    for name in ("final.kmers", "distinct_functions", "function.index", "kmer_data.dat"):
+        assert sorted(_lines(os.path.join(o1, name)).split(b"\n")) == sorted(_lines(os.path.join(o2, name)).split(b"\n")), name
+    for f in os.listdir(os.path.join(o1, "recall.report.d")):
+        assert _lines(os.path.join(o1, "recall.report.d", f)) == _lines(os.path.join(o2, "recall.report.d", f)), f
