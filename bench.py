@@ -69,7 +69,10 @@ def parse():
     ap.add_argument("--annot-queries", type=int, default=10_000_000,
                     help="annotate leg (BASELINE configs[3]); 0 = off; N=1 only")
     ap.add_argument("--matrix-seqs", type=int, default=100_000,
-                    help="matrix-distance leg (BASELINE configs[4]); 0 = off; N=1 only")
+                    help="matrix-distance leg (BASELINE configs[4]); 0 = off; row bands over the ranks")
+    ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
+                    help="rank exchange of the build: RCCL over xGMI, or the gloo host transport (rehearses the "
+                         "multi-rank path with several ranks on one GPU)")
     return ap.parse_args()
 
 
@@ -214,7 +217,7 @@ def main():
     device = local % ndev
 
     def new_uid():
-        if world == 1:
+        if world == 1 or a.comm == "host":
             return None
         box = [skm.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
@@ -230,6 +233,8 @@ def main():
     c3.add_to(b)
     if uid is not None:
         b.set_comm(uid)
+    elif world > 1:
+        b.set_transport(skm.GlooTransport())
     b.prepare()
     prep_s = time.time() - t0
     log(f"C3 prepared in {prep_s:.1f} s")
@@ -255,7 +260,8 @@ def main():
                    "windows_rank0": c3.n_windows, "key_range_passes": head["passes"],
                    "kept_kmers_rank0": head["counters"]["kept"], "grouped_elements_rank0": head["counters"]["grouped"],
                    "parallelism": "single GPU, key-range passes" if world == 1 else
-                   f"{world} GPUs, owner-partitioned RCCL all-to-all + all-reduce, per key-range pass"},
+                   f"{world} GPUs, owner-partitioned {'RCCL' if a.comm == 'rccl' else 'gloo host-transport'} "
+                   f"all-to-all + all-reduce, per key-range pass"},
         "roofline": head["roofline"],
         "pipeline": head["pipeline"],
         "pcie_inclusive": _pcie_inclusive(head, prep_s),
@@ -277,6 +283,8 @@ def main():
         c2.add_to(b)
         if uid is not None:
             b.set_comm(uid)
+        elif world > 1:
+            b.set_transport(skm.GlooTransport())
         b.prepare()
         prep2 = time.time() - t0
         weak = _measure(skm, b, a.steps, a.warmup, c2, world, dist)

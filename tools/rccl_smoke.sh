@@ -6,8 +6,8 @@ O=$R/gpurun_out/rccl
 mkdir -p "$O"
 cd "$R"
 NCCL_DEBUG=WARN timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-  --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 --seqs-total 400000 --weak-seqs 0 --annot-queries 0 \
-  --matrix-seqs 0 --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench2.log" 2>&1
+  --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 --seqs-total 400000 --weak-seqs 100000 --annot-queries 0 --matrix-seqs 20000 \
+  --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench2.log" 2>&1
 rc=$?
 echo "rc=$rc"
 tail -30 "$O/bench2.log" | cut -c1-400
