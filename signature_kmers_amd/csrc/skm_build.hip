@@ -1746,8 +1746,10 @@ __device__ __forceinline__ uint64_t kept_lo(uint32_t f, uint32_t mean, uint32_t 
     return (uint64_t)f | ((uint64_t)mean << 16) | ((uint64_t)med << 32) | ((uint64_t)var << 48);
 }
 
+// The kept arena holds the k-mer's 43-bit hash until the run's last kernel over the arena
+// (k_kept_finalize) decodes every key in one streaming pass, off the group-by's emit phase.
 __device__ __forceinline__ void write_kept(const BucketArgs& A, uint64_t o, uint64_t H, uint64_t L) {
-    A.out_keys[o] = decode_key(unmix43((H >> 16) & KEY_MASK));
+    A.out_keys[o] = (H >> 16) & KEY_MASK;
     skm_stored_kmer_data d;
     d.avg_from_end = (uint16_t)(H & 0xFFFFu);
     d.function_index = (uint16_t)(L & 0xFFFFu);
@@ -3393,14 +3395,17 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
 }
 
 // distinct_functions[f] += kept k-mers with best function f (LDS privatised when it fits)
-__global__ void k_func_hist_kept(const skm_stored_kmer_data* __restrict__ data, uint64_t n, uint32_t nf,
-                                 uint32_t* __restrict__ dfunc) {
+// Over the whole kept arena after the last pass: decode each key (43-bit hash -> unmix43 ->
+// base-40 -> the 8 residue bytes, Kmer<8> as a little-endian u64) and count distinct_functions.
+__global__ void k_kept_finalize(uint64_t* __restrict__ keys, const skm_stored_kmer_data* __restrict__ data, uint64_t n,
+                                uint32_t nf, uint32_t* __restrict__ dfunc) {
     extern __shared__ uint32_t s_h[];
     const bool lds = nf <= 16384;
     if (lds)
         for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) s_h[f] = 0;
     __syncthreads();
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        keys[i] = decode_key(unmix43(keys[i]));
         uint32_t f = data[i].function_index;
         if (f < nf) {
             if (lds)
@@ -4749,7 +4754,8 @@ void phase_stats(skm_build* b) {
     SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     const size_t lds_f = F <= 16384 ? sizeof(uint32_t) * F : 0;
     if (b->n_kept)
-        hipLaunchKernelGGL(k_func_hist_kept, dim3(1024), dim3(256), lds_f, st, b->d_data.as<skm_stored_kmer_data>(),
+        hipLaunchKernelGGL(k_kept_finalize, dim3(2048), dim3(256), lds_f, st, b->d_keys.as<uint64_t>(),
+                           b->d_data.as<skm_stored_kmer_data>(),
                            b->n_kept, F, b->d_dfunc.as<uint32_t>());
     if (b->nseq)
         hipLaunchKernelGGL(k_func_hist_seqs, dim3(256), dim3(256), lds_f, st, b->d_meta.as<SeqMeta>(), b->nseq, F,
