@@ -1255,7 +1255,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_extract(ExtractArgs X) {
 constexpr int CP_THREADS = 256, CP_PER_THREAD = 128;  // 32768 windows per workgroup
 __global__ __launch_bounds__(CP_THREADS) void k_pass_compact(const uint8_t* __restrict__ ids, uint64_t rp, uint32_t pass,
                                                              uint64_t* __restrict__ pos,
-                                                             unsigned long long* __restrict__ cursor) {
+                                                             unsigned long long* __restrict__ cursor, uint64_t cap) {
     __shared__ uint32_t s_wave[CP_THREADS / 64 + 1];
     __shared__ unsigned long long s_base;
     const uint64_t base = (uint64_t)blockIdx.x * CP_THREADS * CP_PER_THREAD + (uint64_t)threadIdx.x * CP_PER_THREAD;
@@ -1271,10 +1271,11 @@ __global__ __launch_bounds__(CP_THREADS) void k_pass_compact(const uint8_t* __re
     uint32_t off = wg_exclusive_scan(cnt, s_wave, tot);
     if (threadIdx.x == 0) s_base = tot ? atomicAdd(cursor, (unsigned long long)tot) : 0ull;
     __syncthreads();
-    uint64_t* out = pos + s_base + off;
+    uint64_t o = s_base + off;  // the pass sizes were counted at prepare with the same hash: o < cap
 #pragma unroll
     for (int k = 0; k < CP_PER_THREAD / 16; ++k)
-        for (uint32_t w = m[k]; w; w &= w - 1) *out++ = base + 16u * k + (uint32_t)__ffs(w) - 1u;
+        for (uint32_t w = m[k]; w; w &= w - 1, ++o)
+            if (o < cap) pos[o] = base + 16u * k + (uint32_t)__ffs(w) - 1u;
 }
 
 // the 8 residue bytes at packed position p (the buffer is padded past its end)
@@ -1295,7 +1296,9 @@ __device__ __forceinline__ uint64_t window_hash(uint64_t raw) {
 }
 
 // count pass over this pass's positions pos[0..n): per-workgroup level-1 bucket histogram
-__global__ __launch_bounds__(EX_THREADS) void k_extract_pos(ExtractArgs X, const uint64_t* __restrict__ pos, uint64_t n) {
+__global__ __launch_bounds__(EX_THREADS) void k_extract_pos(ExtractArgs X, const uint64_t* __restrict__ pos,
+                                                             const unsigned long long* __restrict__ np) {
+    const uint64_t n = *np;  // this pass's window count (k_pass_compact's cursor): no host round trip
     extern __shared__ uint32_t s_cnt[];  // [NB]
     const int nbits = X.owner_bits + X.b1_bits;
     const uint32_t NB = 1u << nbits;
@@ -1446,9 +1449,11 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
 // as k_extract_stage; each position finds its sequence through blk2seq, reusing the previous
 // one while it still contains the window).
 __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage_pos(ExtractArgs X, const uint64_t* __restrict__ pos,
-                                                                     uint64_t n, unsigned long long* __restrict__ cur0,
+                                                                     const unsigned long long* __restrict__ np,
+                                                                     unsigned long long* __restrict__ cur0,
                                                                      uint64_t* __restrict__ out_hi,
                                                                      uint64_t* __restrict__ out_lo) {
+    const uint64_t n = *np;
     __shared__ StageLds L;
     const int nbits = X.owner_bits + X.b1_bits;
     const uint32_t NB = 1u << nbits;
@@ -3471,6 +3476,7 @@ struct Tune {
     // slow them by more than the ~0.5 s tail they would hide -- DESIGN.md section 4)
     int giant_class = 0;
     int giant_passes = 0;            // giant chains only in the last N passes (0: all)
+    int prefetch = 1;                // next pass's compaction + count during this pass's group-by
 };
 
 }  // namespace skm
@@ -3585,7 +3591,14 @@ struct skm_build {
     uint64_t pass_max = 0;              // valid windows of the largest pass (this shard)
     uint64_t valid_total = 0;           // valid windows of this shard
     DevBuf d_ids;                       // per-window pass id (pass_bits > 0)
-    DevBuf d_pos;                       // this pass's window positions (pass_bits > 0)
+    // a pass's window positions, level-1 histogram matrix and window count, double-buffered: the
+    // next pass's compaction + count run on stx during this pass's group-by (prefetch_pass)
+    DevBuf d_pos2[2], d_hist2[2], d_npos;
+    hipStream_t stx = nullptr;
+    hipEvent_t ev_pf_ready = nullptr, ev_pf_done[2] = {};
+    int64_t pf_pass = -1;               // the pass whose compaction + count are already queued
+    uint32_t pf_nwg = 1;                // count-kernel rows of the histogram matrix (pass mode)
+    uint64_t pf_span = 0;
     uint64_t kept_cap = 0;              // kept k-mer arena (keys + records), shared by all passes
     hipEvent_t ev_start = nullptr;
     // run totals over the passes (counters(), timings)
@@ -3599,7 +3612,7 @@ struct skm_build {
     hipStream_t chain_st = nullptr;
     hipEvent_t chain_ev[3] = {};
     // giant chains of k_heavy: rotating slots (stream, sample / job buffers, counters, events)
-    static constexpr int GSLOTS = 4;
+    static constexpr int GSLOTS = 3;  // + st, st2, st3, chain_st, stx: 8 streams
     hipStream_t gst[GSLOTS] = {};
     hipEvent_t gev_ready[GSLOTS] = {}, gev_done[GSLOTS] = {};
     std::deque<DevBuf> gsamples, gjobs, gcount;   // per key-range pass (reused by the next run)
@@ -4051,9 +4064,17 @@ void size_local(skm_build* b) {
     b->d_recs_hi.ensure(8 * W);
     b->d_recs_lo.ensure(8 * W);
     if (b->pass_bits > 0) {
-        b->d_pos.ensure(8 * W);
-        // the histogram matrix of a pass may use every extract workgroup row
         const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
+        for (int k = 0; k < (b->pass_bits ? 2 : 1); ++k) {
+            b->d_pos2[k].ensure(8 * W);
+            b->d_hist2[k].ensure(sizeof(uint32_t) * (uint64_t)EX_MAX_WG * NB);
+        }
+        b->d_npos.ensure(16);
+        // count-kernel geometry from the largest pass (the kernels read the pass's own count)
+        uint32_t nwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(EX_MAX_WG, ceil_div(W, (uint64_t)SC_ROUND * 4)));
+        b->pf_span = ceil_div(ceil_div(W, nwg), (uint64_t)SC_ROUND) * SC_ROUND;
+        b->pf_nwg = (uint32_t)std::max<uint64_t>(1, ceil_div(W, b->pf_span));
+        // the histogram matrix of a pass may use every extract workgroup row
         b->d_hist.ensure(sizeof(uint32_t) * (uint64_t)EX_MAX_WG * NB);
         b->d_offs.ensure(sizeof(uint32_t) * (uint64_t)EX_MAX_WG * NB);
         b->d_partial.ensure(sizeof(uint32_t) * (uint64_t)ceil_div(EX_MAX_WG, SCAN_ROWS) * NB);
@@ -4176,6 +4197,33 @@ void prepare(const Ranks& bs) {
 // ------------------------------------------------------------------------------------------
 // run: extract -> [exchange] -> group-by -> chains -> statistics [-> reductions]
 // ------------------------------------------------------------------------------------------
+// Key-range pass `pass`: its window positions (compaction of the id bytes) and the per-workgroup
+// level-1 histogram over them, into buffer set pass & 1, on stream `st` (no host round trip: the
+// kernels read the pass's window count on the device).
+void prefetch_pass(skm_build* b, uint32_t pass, hipStream_t st) {
+    const int k = pass & 1;
+    const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
+    unsigned long long* np = b->d_npos.as<unsigned long long>() + k;
+    SKM_HIP(hipMemsetAsync(np, 0, 8, st));
+    hipLaunchKernelGGL(k_pass_compact, dim3((uint32_t)ceil_div(b->rp, (uint64_t)CP_THREADS * CP_PER_THREAD)),
+                       dim3(CP_THREADS), 0, st, b->d_ids.as<uint8_t>(), b->rp, pass, b->d_pos2[k].as<uint64_t>(), np,
+                       b->pass_max);
+    ExtractArgs X{};
+    X.res = b->d_res.as<uint8_t>();
+    X.rp = b->rp;
+    X.span = b->pf_span;
+    X.owner_bits = b->owner_bits;
+    X.b1_bits = b->b1_bits;
+    X.pass_bits = b->pass_bits;
+    X.pass_id = pass;
+    X.hist = b->d_hist2[k].as<uint32_t>();
+    hipLaunchKernelGGL(k_extract_pos, dim3(b->pf_nwg), dim3(EX_THREADS), sizeof(uint32_t) * NB, st, X,
+                       b->d_pos2[k].as<uint64_t>(), np);
+    SKM_HIP(hipGetLastError());
+    if (st != b->stream) SKM_HIP(hipEventRecord(b->ev_pf_done[k], st));
+    b->pf_pass = pass;
+}
+
 void phase_extract(skm_build* b, uint32_t pass) {
     hipStream_t st = b->stream;
     const int nbits = b->owner_bits + b->b1_bits;
@@ -4202,22 +4250,19 @@ void phase_extract(skm_build* b, uint32_t pass) {
     X.out_hi = b->d_recs_hi.as<uint64_t>();
     X.out_lo = b->d_recs_lo.as<uint64_t>();
     uint32_t nwg = b->nwg;
-    uint64_t npos = 0;
     if (b->pass_bits) {
-        // this pass's window positions (compaction of the id bytes), then the count over them
-        unsigned long long* cur = b->d_ctr.as<unsigned long long>() + 24;
-        SKM_HIP(hipMemsetAsync(cur, 0, 8, st));
-        hipLaunchKernelGGL(k_pass_compact, dim3((uint32_t)ceil_div(b->rp, (uint64_t)CP_THREADS * CP_PER_THREAD)),
-                           dim3(CP_THREADS), 0, st, b->d_ids.as<uint8_t>(), b->rp, pass, b->d_pos.as<uint64_t>(), cur);
-        unsigned long long* pin = b->pinned_ctr();
-        SKM_HIP(hipMemcpyAsync(pin + 40, cur, 8, hipMemcpyDeviceToHost, st));
-        SKM_HIP(hipStreamSynchronize(st));
-        npos = pin[40];
-        SKM_CHECK(npos <= b->pass_max, SKM_E_STATE, "key-range pass larger than planned");
-        nwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(EX_MAX_WG, ceil_div(npos, (uint64_t)SC_ROUND * 4)));
-        X.span = ceil_div(ceil_div(npos ? npos : 1, nwg), (uint64_t)SC_ROUND) * SC_ROUND;
-        nwg = (uint32_t)std::max<uint64_t>(1, ceil_div(npos ? npos : 1, X.span));
-        hipLaunchKernelGGL(k_extract_pos, dim3(nwg), dim3(EX_THREADS), lds_cnt, st, X, b->d_pos.as<uint64_t>(), npos);
+        // this pass's window positions and count: queued on stx during the previous pass's
+        // group-by (prefetch_pass), or now for the run's first pass
+        const int k = pass & 1;
+        if (b->pf_pass == (int64_t)pass && pass > 0)
+            SKM_HIP(hipStreamWaitEvent(st, b->ev_pf_done[k], 0));
+        else
+            prefetch_pass(b, pass, st);
+        b->pf_pass = -1;
+        X.hist = b->d_hist2[k].as<uint32_t>();
+        X.span = b->pf_span;
+        nwg = b->pf_nwg;
+        (void)lds_cnt;
     } else {
         hipLaunchKernelGGL(k_extract, dim3(nwg), dim3(EX_THREADS), lds_cnt, st, X);
     }
@@ -4226,10 +4271,10 @@ void phase_extract(skm_build* b, uint32_t pass) {
     // ---- 2. scan ----
     const uint32_t nrb = (uint32_t)ceil_div(nwg, SCAN_ROWS);
     dim3 gsc((NB + 255) / 256, nrb);
-    hipLaunchKernelGGL(k_colsum, gsc, dim3(256), 0, st, b->d_hist.as<uint32_t>(), nwg, NB, b->d_partial.as<uint32_t>());
+    hipLaunchKernelGGL(k_colsum, gsc, dim3(256), 0, st, X.hist, nwg, NB, b->d_partial.as<uint32_t>());
     hipLaunchKernelGGL(k_bstart, dim3(1), dim3(1024), 0, st, b->d_partial.as<uint32_t>(), nrb, NB, b->b1_bits,
                        b->d_rbbase.as<uint32_t>(), b->d_bstart32.as<uint32_t>(), b->d_owner_start.as<uint64_t>(), nowners);
-    hipLaunchKernelGGL(k_coloffs, gsc, dim3(256), 0, st, b->d_hist.as<uint32_t>(), b->d_rbbase.as<uint32_t>(), nwg,
+    hipLaunchKernelGGL(k_coloffs, gsc, dim3(256), 0, st, X.hist, b->d_rbbase.as<uint32_t>(), nwg,
                        NB, b->d_offs.as<uint32_t>());
     hipLaunchKernelGGL(k_abs_starts, dim3((NB + 1 + 255) / 256), dim3(256), 0, st, b->d_bstart32.as<uint32_t>(),
                        b->d_owner_start.as<uint64_t>(), NB, b->b1_bits, nowners, b->d_bstart.as<uint64_t>());
@@ -4243,8 +4288,9 @@ void phase_extract(skm_build* b, uint32_t pass) {
     hipLaunchKernelGGL(k_stage_init, dim3((NB + 255) / 256), dim3(256), 0, st, b->d_bstart.as<uint64_t>(), NB, l0_shift,
                        b->d_cur0.as<unsigned long long>(), b->d_cur1.as<unsigned long long>(), b->d_slices.as<uint32_t>());
     if (b->pass_bits)
-        hipLaunchKernelGGL(k_extract_stage_pos, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_pos.as<uint64_t>(), npos,
-                           b->d_cur0.as<unsigned long long>(), b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
+        hipLaunchKernelGGL(k_extract_stage_pos, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_pos2[pass & 1].as<uint64_t>(),
+                           b->d_npos.as<unsigned long long>() + (pass & 1), b->d_cur0.as<unsigned long long>(),
+                           b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
     else
         hipLaunchKernelGGL(k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
                            b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
@@ -4446,6 +4492,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     hipLaunchKernelGGL(k_partition, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[10], st));
+    SKM_HIP(hipEventRecord(b->ev_pf_ready, st));
     // readbacks go through pinned host memory (no staging copies, no pageable-copy stalls)
     unsigned long long* ctr = b->pinned_ctr();
     SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, 8 * 5, hipMemcpyDeviceToHost, st));
@@ -4613,6 +4660,12 @@ void phase_group(skm_build* b, uint32_t pass) {
     hipLaunchKernelGGL(k_bucket_process, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[5], st));
+    // the next pass's compaction + count overlap this pass's group-by on stx: its buffer set was
+    // last read by this pass's predecessor's extract, complete once this pass's partition is
+    if (b->pass_bits && pass + 1 < (1u << b->pass_bits) && b->tune.prefetch) {
+        SKM_HIP(hipStreamWaitEvent(b->stx, b->ev_pf_ready, 0));
+        prefetch_pass(b, pass + 1, b->stx);
+    }
     hipLaunchKernelGGL(k_big_groups<false>, dim3(2048), dim3(BIG_WG), 0, st, BA);
     hipLaunchKernelGGL(k_big_groups<true>, dim3(512), dim3(BIG_WG), 0, st, BA);
     hipLaunchKernelGGL(k_big_append, dim3(256), dim3(BIG_WG), 0, st, BA.out, BA, A);
@@ -4863,6 +4916,9 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     for (auto& e : b->ev) SKM_HIP(hipEventCreate(&e));
     SKM_HIP(hipEventCreate(&b->ev_start));
     SKM_HIP(hipStreamCreateWithFlags(&b->chain_st, hipStreamNonBlocking));
+    SKM_HIP(hipStreamCreateWithFlags(&b->stx, hipStreamNonBlocking));
+    SKM_HIP(hipEventCreateWithFlags(&b->ev_pf_ready, hipEventDisableTiming));
+    for (auto& e : b->ev_pf_done) SKM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (int g = 0; g < skm_build::GSLOTS; ++g) {
         SKM_HIP(hipStreamCreateWithFlags(&b->gst[g], hipStreamNonBlocking));
         SKM_HIP(hipEventCreateWithFlags(&b->gev_ready[g], hipEventDisableTiming));
@@ -5106,7 +5162,8 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "heavy_min" ? &t.heavy_min
                : n == "split_min" ? &t.split_min
                : n == "giant_class" ? &t.giant_class
-               : n == "giant_passes" ? &t.giant_passes : nullptr;
+               : n == "giant_passes" ? &t.giant_passes
+               : n == "prefetch" ? &t.prefetch : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")
@@ -5415,6 +5472,13 @@ void skm_build_destroy(skm_build* b) {
         if (b->gev_ready[g]) (void)hipEventDestroy(b->gev_ready[g]);
         if (b->gev_done[g]) (void)hipEventDestroy(b->gev_done[g]);
     }
+    if (b->stx) {
+        (void)hipStreamSynchronize(b->stx);
+        (void)hipStreamDestroy(b->stx);
+    }
+    if (b->ev_pf_ready) (void)hipEventDestroy(b->ev_pf_ready);
+    for (auto& e : b->ev_pf_done)
+        if (e) (void)hipEventDestroy(e);
     if (b->chain_st) {
         (void)hipStreamSynchronize(b->chain_st);
         (void)hipStreamDestroy(b->chain_st);
