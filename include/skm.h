@@ -127,7 +127,12 @@ int skm_build_last_timings(skm_build* b, float* ms, int cap);
  * [7]=occurrences in overflow sub-buckets [8]=k-mers kept by the overflow path
  * [9]=groups of > 64 members handed to k_big_groups [10]=k-mers kept among them
  * [11]=key-range passes [12]=valid windows (occurrences) this rank extracts [13]=giant chains
- * (heavy k-mers whose P^2 / variance chains start right after k_heavy) [14]=the longest of them;
+ * (heavy k-mers whose P^2 / variance chains start right after k_heavy) [14]=the longest of them
+ * [15]=redone steps since create (a run that outgrew a data-sized work buffer -- the overflow
+ * scratch, the split path, the stashed long chains -- records its demand and is redone once with
+ * the buffers grown; the capacities persist, so later runs on the same input are not)
+ * [16..19]=capacities of those buffers (overflow scratch elements, split-path elements, stashed
+ * long-chain samples, stashed long jobs) [20..23]=the last run's demands on them;
  * totals over the passes of the run; returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Host transport: the rank collectives of a multi-process build run by the caller on host

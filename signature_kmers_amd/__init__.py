@@ -292,11 +292,12 @@ class SignatureBuilder:
         return self.counters()["passes"]
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 15)()
-        n = lib().skm_build_counters(self._h, v, 15)
+        v = (C.c_uint64 * 24)()
+        n = lib().skm_build_counters(self._h, v, 24)
         names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped",
                  "overflow_elements", "overflow_kept", "big_groups", "big_kept", "passes", "valid", "giant_chains",
-                 "giant_max"]
+                 "giant_max", "redone", "cap_overflow_scratch", "cap_split", "cap_long_samples", "cap_long_jobs",
+                 "demand_overflow_scratch", "demand_split", "demand_long_samples", "demand_long_jobs"]
         return {names[i]: int(v[i]) for i in range(n)}
 
     def debug_jobs(self, k: int = 64) -> list:

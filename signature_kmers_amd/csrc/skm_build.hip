@@ -670,17 +670,68 @@ __device__ bool group_block(const V& v, uint64_t a, uint32_t c, const uint32_t* 
 // Chains run longest-first: jobs are counting-sorted by length class (floor(log2 n), descending)
 // so a wave's 64 jobs have similar lengths.  Waves 2w and 2w+1 run the P^2 median and the
 // variance recurrence of the same 64 jobs (wave-uniform branch).
+// Run-level device slots (skm_build::d_run, cleared by begin_run): what the passes need to know
+// about each other, kept on the device so a step issues every launch without a host round trip
+enum : uint32_t {
+    RUN_FLAGS = 0,          // RUN_F_* bits
+    RUN_LONG_CUR = 1,       // stashed long-chain samples (run arena cursor)
+    RUN_LONG_N = 2,         // stashed long jobs
+    RUN_LONG_FLUSHED = 3,   // long jobs already handed to k_chain_long
+    RUN_SNAP = 4,           // [4..7] two k_long_snap ranges
+    RUN_DEM_TOT = 8,        // demands (max over passes): overflow scratch elements,
+    RUN_DEM_SPLIT = 9,      //   split-path elements,
+    RUN_DEM_LONG = 10,      //   stashed samples,
+    RUN_DEM_LJOBS = 11,     //   stashed jobs
+    RUN_ACC_NOVF = 16,      // run totals
+    RUN_ACC_JOBS = 17,
+    RUN_ACC_LENS = 18,
+    RUN_ACC_OVF_ELEMS = 19,
+    RUN_ACC_OVF_KEPT = 20,
+    RUN_ACC_BIG = 21,
+    RUN_ACC_BIG_KEPT = 22,
+    RUN_ACC_GROUPED = 23,
+    RUN_LAST_NOVF = 24,     // the last pass's overflow entries and chain jobs (diagnostics)
+    RUN_LAST_JOBS = 25,
+    RUN_NLOC = 26,          // world > 1: the pass's received element count (host-written)
+    RUN_SLOTS = 32
+};
+constexpr unsigned long long RUN_F_ARENA = 1;  // the kept arena cannot take a pass: SKM_E_OOM
+constexpr unsigned long long RUN_F_RERUN = 2;  // a work buffer was too small: grown to the demand, step redone
+constexpr unsigned long long RUN_F_CAP = 4;    // a proven bound was exceeded: SKM_E_STATE
+// k_ovf_plan's per-pass plan (skm_build::d_plan): list sizes and the work-queue counters of the
+// persistent overflow kernels
+enum : uint32_t {
+    PLAN_NOVF = 0,      // overflow entries (0 when the pass is skipped)
+    PLAN_NSPLIT = 1,    // the first NSPLIT entries (>= split_min elements) go through k_ovf_split
+    PLAN_NHEAVY = 2,    // the first NHEAVY (>= ovf_heavy elements) run on stream 2, the rest on stream 3
+    PLAN_SKIP = 3,      // nonzero: the run is abandoned (error or redo), the pass's group-by is skipped
+    PLAN_Q_SPLIT = 4,   // queue counters
+    PLAN_Q_HEAVY = 5,
+    PLAN_Q_REST = 6,
+    PLAN_SLOTS = 8
+};
+
 constexpr int JOB_CLASSES = 32;
 constexpr int JOB_WG = 256;
 
 __device__ __forceinline__ uint32_t job_class(uint32_t n) { return 31u - (uint32_t)__clz(n | 1u); }
 
-__global__ __launch_bounds__(JOB_WG) void k_job_count(const Job* __restrict__ jobs, uint64_t njobs, uint64_t chunk,
-                                                      uint32_t* __restrict__ hist) {
+// The job count is read on the device (capped at the list's capacity); each of the fixed
+// gridDim.x workgroups takes one contiguous chunk of it.
+__device__ __forceinline__ void job_chunk(const unsigned long long* nj_p, uint64_t cap, uint64_t& a, uint64_t& e) {
+    const uint64_t nj = min((uint64_t)*nj_p, cap);
+    const uint64_t chunk = (nj + gridDim.x - 1) / gridDim.x;
+    a = min(nj, (uint64_t)blockIdx.x * chunk);
+    e = min(nj, a + chunk);
+}
+
+__global__ __launch_bounds__(JOB_WG) void k_job_count(const Job* __restrict__ jobs, const unsigned long long* nj_p,
+                                                      uint64_t cap, uint32_t* __restrict__ hist) {
     __shared__ uint32_t h[JOB_CLASSES];
     if (threadIdx.x < JOB_CLASSES) h[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t a = (uint64_t)blockIdx.x * chunk, e = min(njobs, a + chunk);
+    uint64_t a, e;
+    job_chunk(nj_p, cap, a, e);
     for (uint64_t j = a + threadIdx.x; j < e; j += blockDim.x) atomicAdd(&h[job_class(jobs[j].n)], 1u);
     __syncthreads();
     if (threadIdx.x < JOB_CLASSES) hist[blockIdx.x * JOB_CLASSES + threadIdx.x] = h[threadIdx.x];
@@ -714,12 +765,14 @@ __global__ void k_job_scan(const uint32_t* __restrict__ hist, uint32_t nwg, uint
     }
 }
 
-__global__ __launch_bounds__(JOB_WG) void k_job_scatter(const Job* __restrict__ jobs, uint64_t njobs, uint64_t chunk,
-                                                        const uint64_t* __restrict__ offs, Job* __restrict__ sorted) {
+__global__ __launch_bounds__(JOB_WG) void k_job_scatter(const Job* __restrict__ jobs, const unsigned long long* nj_p,
+                                                        uint64_t cap, const uint64_t* __restrict__ offs,
+                                                        Job* __restrict__ sorted) {
     __shared__ unsigned long long cur[JOB_CLASSES];
     if (threadIdx.x < JOB_CLASSES) cur[threadIdx.x] = offs[blockIdx.x * JOB_CLASSES + threadIdx.x];
     __syncthreads();
-    const uint64_t a = (uint64_t)blockIdx.x * chunk, e = min(njobs, a + chunk);
+    uint64_t a, e;
+    job_chunk(nj_p, cap, a, e);
     for (uint64_t j = a + threadIdx.x; j < e; j += blockDim.x) {
         const Job jb = jobs[j];
         sorted[atomicAdd(&cur[job_class(jb.n)], 1ull)] = jb;
@@ -729,9 +782,13 @@ __global__ __launch_bounds__(JOB_WG) void k_job_scatter(const Job* __restrict__ 
 // Long chains leave the pass: their samples (wherever the group-by left them: consumed element
 // slots, the overflow's lengths buffer) are stashed into a run-persistent arena so the chains can
 // run on their own streams while the next passes reuse every work buffer.  k_long_plan: one
-// workgroup, exclusive offsets of the first nlong (class-sorted) jobs' sample counts.
+// workgroup, exclusive offsets of the first nlong (class-sorted) jobs' sample counts; with `run`
+// (key-range passes) it also reserves the samples' range of the run's arena and the jobs' slots of
+// the run's long-job list:  off[nlong] = samples, [nlong+1] = nlong, [nlong+2] = arena base,
+// [nlong+3] = job base, [nlong+4] = 1 if both fit (else the demand is recorded and the run redone).
 __global__ __launch_bounds__(1024) void k_long_plan(const Job* __restrict__ jobs, const uint64_t* __restrict__ nlong_p,
-                                                    uint64_t* __restrict__ off) {
+                                                    uint64_t* __restrict__ off, unsigned long long* __restrict__ run,
+                                                    uint64_t arena_cap, uint64_t jobs_cap) {
     __shared__ uint32_t s_wave[17];
     __shared__ unsigned long long s_run;
     const uint64_t nlong = *nlong_p;
@@ -742,30 +799,63 @@ __global__ __launch_bounds__(1024) void k_long_plan(const Job* __restrict__ jobs
         const uint32_t n = j < nlong ? jobs[j].n : 0u;
         uint32_t tot;
         const uint32_t ex = wg_exclusive_scan(n, s_wave, tot);
-        const unsigned long long run = s_run;
-        if (j < nlong) off[j] = run + ex;
+        const unsigned long long run_ = s_run;
+        if (j < nlong) off[j] = run_ + ex;
         __syncthreads();
-        if (threadIdx.x == 0) s_run = run + tot;
+        if (threadIdx.x == 0) s_run = run_ + tot;
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        off[nlong] = s_run;
+        const uint64_t total = s_run;
+        off[nlong] = total;
         off[nlong + 1] = nlong;
+        if (run) {
+            uint64_t base = 0, jbase = 0;
+            bool ok = true;
+            if (nlong) {
+                base = atomicAdd(&run[RUN_LONG_CUR], (unsigned long long)total);
+                jbase = atomicAdd(&run[RUN_LONG_N], (unsigned long long)nlong);
+                ok = base + total <= arena_cap && jbase + nlong <= jobs_cap;
+                if (!ok) {
+                    atomicMax(&run[RUN_DEM_LONG], (unsigned long long)(base + total));
+                    atomicMax(&run[RUN_DEM_LJOBS], (unsigned long long)(jbase + nlong));
+                    atomicOr(&run[RUN_FLAGS], (unsigned long long)RUN_F_RERUN);
+                }
+            }
+            off[nlong + 2] = base;
+            off[nlong + 3] = jbase;
+            off[nlong + 4] = ok ? 1u : 0u;
+        }
     }
 }
 
-// one workgroup per long job: copy its samples into arena + off[j], rewrite the job to point there
-__global__ __launch_bounds__(256) void k_long_stash(const Job* __restrict__ jobs, const uint64_t* __restrict__ off,
+// persistent grid over the long jobs (count on the device): copy each one's samples into the
+// run's arena, append the rewritten job to the run's long-job list
+__global__ __launch_bounds__(256) void k_long_stash(const Job* __restrict__ jobs, const uint64_t* __restrict__ nlong_p,
+                                                    const uint64_t* __restrict__ off,
                                                     const uint32_t* __restrict__ lens, const uint32_t* __restrict__ recs32,
                                                     const uint32_t* __restrict__ tmp32, const uint32_t* __restrict__ big32,
                                                     uint32_t* __restrict__ arena, Job* __restrict__ out_jobs) {
-    const Job jb = jobs[blockIdx.x];
-    const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
-    const uint32_t* x = (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
-                        (jb.lens_off & LENS_OFF_MASK);
-    const uint64_t o = off[blockIdx.x];
-    for (uint32_t i = threadIdx.x; i < jb.n; i += blockDim.x) arena[o + i] = x[i];
-    if (threadIdx.x == 0) out_jobs[blockIdx.x] = Job{reinterpret_cast<uint64_t>(arena + o), jb.n, jb.out_idx};
+    const uint64_t nlong = *nlong_p;
+    if (nlong == 0 || off[nlong + 4] == 0) return;
+    const uint64_t base = off[nlong + 2], jbase = off[nlong + 3];
+    for (uint64_t q = blockIdx.x; q < nlong; q += gridDim.x) {
+        const Job jb = jobs[q];
+        const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
+        const uint32_t* x = (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
+                            (jb.lens_off & LENS_OFF_MASK);
+        const uint64_t o = base + off[q];
+        for (uint32_t i = threadIdx.x; i < jb.n; i += blockDim.x) arena[o + i] = x[i];
+        if (threadIdx.x == 0) out_jobs[jbase + q] = Job{reinterpret_cast<uint64_t>(arena + o), jb.n, jb.out_idx};
+    }
+}
+
+// k_chain_long's job range of a stashed batch: [run's flushed mark, run's job count), then the mark
+// moves (one thread, on the group-by stream after the passes' stashes)
+__global__ void k_long_snap(unsigned long long* __restrict__ run, unsigned long long* __restrict__ range) {
+    range[0] = run[RUN_LONG_FLUSHED];
+    range[1] = run[RUN_LONG_N];
+    run[RUN_LONG_FLUSHED] = range[1];
 }
 
 // One chain over x[0..n): blocks of 16 samples; the next block's loads (index clamped, so no
@@ -972,29 +1062,34 @@ __device__ __forceinline__ double chain_long_var(const uint32_t* __restrict__ x,
     return var;
 }
 
-__global__ __launch_bounds__(128) void k_chain_long(const Job* __restrict__ jobs, uint64_t njobs,
+// jobs [*lo_p (0 when null), *hi_p): a wave pair each, persistent grid
+__global__ __launch_bounds__(128) void k_chain_long(const Job* __restrict__ jobs, const unsigned long long* lo_p,
+                                                    const unsigned long long* hi_p,
                                                     const uint32_t* __restrict__ lens,
                                                     const uint32_t* __restrict__ recs32,
                                                     const uint32_t* __restrict__ tmp32,
                                                     const uint32_t* __restrict__ big32,
                                                     skm_stored_kmer_data* __restrict__ out, int prio) {
-    if (blockIdx.x >= njobs) return;
+    const uint64_t lo = lo_p ? (uint64_t)*lo_p : 0ull, hi = *hi_p;
+    if (lo + blockIdx.x >= hi) return;
     if (prio == 1) __builtin_amdgcn_s_setprio(1);
     if (prio == 2) __builtin_amdgcn_s_setprio(2);
     if (prio >= 3) __builtin_amdgcn_s_setprio(3);
-    const Job jb = jobs[blockIdx.x];
-    const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
-    // lens == nullptr: stashed jobs, lens_off is the samples' device address
-    const uint32_t* x =
-        !lens && sel == 0 ? reinterpret_cast<const uint32_t*>(jb.lens_off)
-                          : (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
-                                (jb.lens_off & LENS_OFF_MASK);
-    if (threadIdx.x < 64) {
-        const double med = chain_long_p2(x, jb.n);
-        if (threadIdx.x == 0) out[jb.out_idx].median = d2u16(med);
-    } else {
-        const double v = chain_long_var(x, jb.n);
-        if (threadIdx.x == 64) out[jb.out_idx].var = d2u16(v);
+    for (uint64_t q = lo + blockIdx.x; q < hi; q += gridDim.x) {
+        const Job jb = jobs[q];
+        const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
+        // lens == nullptr: stashed jobs, lens_off is the samples' device address
+        const uint32_t* x =
+            !lens && sel == 0 ? reinterpret_cast<const uint32_t*>(jb.lens_off)
+                              : (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
+                                    (jb.lens_off & LENS_OFF_MASK);
+        if (threadIdx.x < 64) {
+            const double med = chain_long_p2(x, jb.n);
+            if (threadIdx.x == 0) out[jb.out_idx].median = d2u16(med);
+        } else {
+            const double v = chain_long_var(x, jb.n);
+            if (threadIdx.x == 64) out[jb.out_idx].var = d2u16(v);
+        }
     }
 }
 
@@ -1019,12 +1114,19 @@ __global__ __launch_bounds__(128) void k_chain_dyn(const Job* __restrict__ jobs,
     }
 }
 
-__global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, uint64_t njobs,
+// jobs [*lo_p, min(*hi_p, cap)) (the per-lane chains after the long ones of the class-sorted list)
+__global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, const unsigned long long* lo_p,
+                                                const unsigned long long* hi_p, uint64_t cap,
                                                 const uint32_t* __restrict__ lens, const uint32_t* __restrict__ recs32,
                                                 const uint32_t* __restrict__ tmp32, const uint32_t* __restrict__ big32,
                                                 skm_stored_kmer_data* __restrict__ out) {
     // wave pairs walk blocks of 64 jobs (grid may be smaller than the job count: a capped grid
     // keeps few waves resident beside a concurrent kernel, longest jobs first)
+    const uint64_t lo = lo_p ? (uint64_t)*lo_p : 0ull;
+    const uint64_t hi = min((uint64_t)*hi_p, cap);
+    if (hi <= lo) return;
+    jobs += lo;
+    const uint64_t njobs = hi - lo;
     const bool var_wave = ((threadIdx.x >> 6) & 1u) != 0;
     const uint64_t pairs = (uint64_t)gridDim.x * (blockDim.x >> 7);
     for (uint64_t pr = (uint64_t)blockIdx.x * (blockDim.x >> 7) + (threadIdx.x >> 7); pr * 64 < njobs; pr += pairs) {
@@ -1714,6 +1816,7 @@ struct BucketArgs {
     uint64_t* big_desc;        // [big_cap][2] groups of > 64 members handed to k_big_groups
     uint32_t big_cap;
     int prio;                  // wave issue priority of the group-by (above the concurrent chains)
+    const uint32_t* skip;      // k_ovf_plan's verdict for the pass (nonzero: the run is being abandoned)
 };
 
 #define SKM_STAMP(i)                                                          \
@@ -2173,6 +2276,7 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
     __shared__ uint32_t s_nbig;
     __shared__ uint64_t s_tlast;
     __shared__ uint32_t s_ccnt[24];
+    if (A.skip && *A.skip) return;
     SubLds L;
     L.ccnt = s_ccnt;
     L.tlast = &s_tlast;
@@ -2660,7 +2764,8 @@ struct OvfScratch {
 constexpr uint32_t OVF_INLINE_CAP = 32;   // inline chains per workgroup (more: ordinary jobs)
 constexpr uint32_t OVF_BLOCK_GROUP = 1024;  // groups above this size: workgroup-cooperative statistics
 
-__global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratch S, uint32_t inline_min, int prio) {
+__global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratch S, uint32_t* plan, int lo_slot,
+                                                          int hi_slot, int q_slot, uint32_t inline_min, int prio) {
     __shared__ uint64_t s_hi[CAP];
     __shared__ uint64_t s_lo[CAP];
     __shared__ __align__(16) uint32_t s_wave[48];
@@ -2668,76 +2773,48 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
     __shared__ uint32_t s_big[BP_THREADS];
     __shared__ uint32_t s_ninl;
     __shared__ uint64_t s_inl[OVF_INLINE_CAP][2];  // lens offset, n << 32 | output index
-    if (threadIdx.x == 0) s_ninl = 0;
-    const OvfEntry e = A.ovf[blockIdx.x];
-    if (e.n == 0) return;  // every key of the sub-bucket went to k_heavy
-    // src 2: the light remainder k_ovf_split compacted into this entry's own scratch (sorted in
-    // place: each chunk is loaded whole before it is written back)
-    const uint64_t* src_hi = (e.src == 2 ? S.hi : e.src ? A.tmp_hi : A.recs_hi) + e.off;
-    const uint64_t* src_lo = (e.src == 2 ? S.lo : e.src ? A.tmp_lo : A.recs_lo) + e.off;
-    uint64_t* ghi = S.hi + e.scratch;
-    uint64_t* glo = S.lo + e.scratch;
-    uint32_t* heads = S.heads + e.scratch;
-    uint64_t* jobinfo = S.jobinfo + e.scratch;
-    uint32_t* fmean = S.fmean + e.scratch;
-    const uint32_t n = e.n;
-    uint32_t N = CAP;  // the network size: pow2 >= n, at least one chunk (<= the entry's scratch)
-    while (N < n) N <<= 1;
-    const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    const uint64_t hprefix = (uint64_t)(A.bucket_base + e.bucket) << A.rem_bits;
-    // phase 0: chunks of CAP sorted ascending in LDS.  The padding beyond n holds the maximum
-    // key and the network is ascending-only, so no element ever moves into a chunk made only of
-    // padding: those chunks are written once and skipped by every later step
-    const uint32_t nch = (n + CAP - 1) / CAP * CAP;  // first all-padding chunk
-    for (uint32_t c0 = nch; c0 < N; c0 += CAP)
-        for (uint32_t j = tid; j < CAP; j += nt) {
-            ghi[c0 + j] = ~0ull;
-            glo[c0 + j] = ~0ull;
-        }
-    for (uint32_t c0 = 0; c0 < nch; c0 += CAP) {
-        for (uint32_t j = tid; j < CAP; j += nt) {
-            const uint32_t g = c0 + j;
-            if (g < n) {
-                s_hi[j] = src_hi[g] & 0x00007FFFFFFFFFFFull;  // group key = rem | func (length bits dropped)
-                s_lo[j] = src_lo[g];
-            } else {
-                s_hi[j] = ~0ull;
-                s_lo[j] = ~0ull;
+    __shared__ uint32_t s_q;
+    // entries [plan[lo_slot] (0 when < 0), plan[hi_slot]) of k_ovf_plan's list, taken one at a time
+    // from the queue counter plan[q_slot] (largest first: the list is sorted by size class)
+    const uint32_t q_lo = lo_slot < 0 ? 0u : plan[lo_slot], q_hi = plan[hi_slot];
+    auto entry = [&](const OvfEntry e) {
+        if (e.n == 0) return;  // every key of the sub-bucket went to k_heavy
+        // src 2: the light remainder k_ovf_split compacted into this entry's own scratch (sorted in
+        // place: each chunk is loaded whole before it is written back)
+        const uint64_t* src_hi = (e.src == 2 ? S.hi : e.src ? A.tmp_hi : A.recs_hi) + e.off;
+        const uint64_t* src_lo = (e.src == 2 ? S.lo : e.src ? A.tmp_lo : A.recs_lo) + e.off;
+        uint64_t* ghi = S.hi + e.scratch;
+        uint64_t* glo = S.lo + e.scratch;
+        uint32_t* heads = S.heads + e.scratch;
+        uint64_t* jobinfo = S.jobinfo + e.scratch;
+        uint32_t* fmean = S.fmean + e.scratch;
+        const uint32_t n = e.n;
+        uint32_t N = CAP;  // the network size: pow2 >= n, at least one chunk (<= the entry's scratch)
+        while (N < n) N <<= 1;
+        const uint32_t tid = threadIdx.x, nt = blockDim.x;
+        const uint64_t hprefix = (uint64_t)(A.bucket_base + e.bucket) << A.rem_bits;
+        // phase 0: chunks of CAP sorted ascending in LDS.  The padding beyond n holds the maximum
+        // key and the network is ascending-only, so no element ever moves into a chunk made only of
+        // padding: those chunks are written once and skipped by every later step
+        const uint32_t nch = (n + CAP - 1) / CAP * CAP;  // first all-padding chunk
+        for (uint32_t c0 = nch; c0 < N; c0 += CAP)
+            for (uint32_t j = tid; j < CAP; j += nt) {
+                ghi[c0 + j] = ~0ull;
+                glo[c0 + j] = ~0ull;
             }
-        }
-        __syncthreads();
-        bitonic_lds(s_hi, s_lo, CAP, 2, CAP, CAP);
-        for (uint32_t j = tid; j < CAP; j += nt) {
-            ghi[c0 + j] = s_hi[j];
-            glo[c0 + j] = s_lo[j];
-        }
-        __threadfence_block();
-        __syncthreads();
-    }
-    for (uint32_t k = 2 * CAP; k <= N; k <<= 1) {
-        for (uint32_t j = k >> 1; j >= (uint32_t)CAP; j >>= 1) {
-            for (uint32_t t = tid; t < N / 2; t += nt) {
-                const uint32_t i = 2 * t - (t & (j - 1));
-                if (i >= nch) continue;  // i and its partner above it are both maximum-key padding
-                const uint32_t l = j == (k >> 1) ? (i ^ (k - 1)) : i + j;
-                const uint64_t ah = ghi[i], al = glo[i], bh = ghi[l], bl = glo[l];
-                if (elem_less(bh, bl, ah, al)) {
-                    ghi[i] = bh;
-                    glo[i] = bl;
-                    ghi[l] = ah;
-                    glo[l] = al;
+        for (uint32_t c0 = 0; c0 < nch; c0 += CAP) {
+            for (uint32_t j = tid; j < CAP; j += nt) {
+                const uint32_t g = c0 + j;
+                if (g < n) {
+                    s_hi[j] = src_hi[g] & 0x00007FFFFFFFFFFFull;  // group key = rem | func (length bits dropped)
+                    s_lo[j] = src_lo[g];
+                } else {
+                    s_hi[j] = ~0ull;
+                    s_lo[j] = ~0ull;
                 }
             }
-            __threadfence_block();
             __syncthreads();
-        }
-        for (uint32_t c0 = 0; c0 < nch; c0 += CAP) {  // chunks above nch stay all padding
-            for (uint32_t j = tid; j < CAP; j += nt) {
-                s_hi[j] = ghi[c0 + j];
-                s_lo[j] = glo[c0 + j];
-            }
-            __syncthreads();
-            bitonic_lds(s_hi, s_lo, CAP, k, k, CAP >> 1);
+            bitonic_lds(s_hi, s_lo, CAP, 2, CAP, CAP);
             for (uint32_t j = tid; j < CAP; j += nt) {
                 ghi[c0 + j] = s_hi[j];
                 glo[c0 + j] = s_lo[j];
@@ -2745,172 +2822,215 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
             __threadfence_block();
             __syncthreads();
         }
-    }
-    // group heads
-    uint32_t G = 0;
-    for (uint32_t c0 = 0; c0 < n; c0 += nt) {
-        const uint32_t t = c0 + tid;
-        const bool head = t < n && (t == 0 || (ghi[t] >> 16) != (ghi[t - 1] >> 16));
-        uint32_t tot;
-        const uint32_t pos = wg_exclusive_scan(head ? 1u : 0u, s_wave, tot);
-        if (head) {
-            heads[G + pos] = t;
-            jobinfo[t] = 0;
-        }
-        G += tot;
-    }
-    __threadfence_block();
-    __syncthreads();
-    const GlbView V{ghi, glo};
-    auto stage = [&](const GRes& r, uint32_t a) {
-        if (!r.kept) return;
-        const uint64_t h43 = hprefix | (ghi[a] >> 16);
-        if (r.cbest >= 3) {
-            jobinfo[a] = ((uint64_t)(a + r.rb) << 32) | r.cbest;
-            fmean[a] = r.best_f | ((uint32_t)r.mean << 16);
-        } else {
-            glo[a] = kept_lo(r.best_f, r.mean, r.median, r.var);
-        }
-        ghi[a] = kept_hi(h43, r.avg);
-    };
-    for (uint32_t g0 = 0; g0 < G; g0 += nt) {
-        if (tid == 0) s_nbig = 0;
-        __syncthreads();
-        const uint32_t g = g0 + tid;
-        if (g < G) {
-            const uint32_t a = heads[g];
-            const uint32_t b = g + 1 < G ? heads[g + 1] : n;
-            const uint32_t c = b - a;
-            if (c > (uint32_t)SMALLC) {
-                s_big[atomicAdd(&s_nbig, 1u)] = g;
-            } else {
-                GRes r;
-                if (c <= 4)
-                    r = group_thread<4>(V, a, c, A.glen, A.flags);
-                else if (c <= 8)
-                    r = group_thread<8>(V, a, c, A.glen, A.flags);
-                else
-                    r = group_thread<16>(V, a, c, A.glen, A.flags);
-                stage(r, a);
+        for (uint32_t k = 2 * CAP; k <= N; k <<= 1) {
+            for (uint32_t j = k >> 1; j >= (uint32_t)CAP; j >>= 1) {
+                for (uint32_t t = tid; t < N / 2; t += nt) {
+                    const uint32_t i = 2 * t - (t & (j - 1));
+                    if (i >= nch) continue;  // i and its partner above it are both maximum-key padding
+                    const uint32_t l = j == (k >> 1) ? (i ^ (k - 1)) : i + j;
+                    const uint64_t ah = ghi[i], al = glo[i], bh = ghi[l], bl = glo[l];
+                    if (elem_less(bh, bl, ah, al)) {
+                        ghi[i] = bh;
+                        glo[i] = bl;
+                        ghi[l] = ah;
+                        glo[l] = al;
+                    }
+                }
+                __threadfence_block();
+                __syncthreads();
+            }
+            for (uint32_t c0 = 0; c0 < nch; c0 += CAP) {  // chunks above nch stay all padding
+                for (uint32_t j = tid; j < CAP; j += nt) {
+                    s_hi[j] = ghi[c0 + j];
+                    s_lo[j] = glo[c0 + j];
+                }
+                __syncthreads();
+                bitonic_lds(s_hi, s_lo, CAP, k, k, CAP >> 1);
+                for (uint32_t j = tid; j < CAP; j += nt) {
+                    ghi[c0 + j] = s_hi[j];
+                    glo[c0 + j] = s_lo[j];
+                }
+                __threadfence_block();
+                __syncthreads();
             }
         }
-        __syncthreads();
-        const uint32_t nbig = s_nbig;
-        for (uint32_t bi = tid >> 6; bi < nbig; bi += nt >> 6) {
-            const uint32_t gg = s_big[bi];
-            const uint32_t a = heads[gg];
-            const uint32_t b = gg + 1 < G ? heads[gg + 1] : n;
-            if (b - a > OVF_BLOCK_GROUP) continue;  // the whole workgroup takes it below
-            const GRes r = group_wave(V, a, b - a, A.glen, A.flags);
-            if ((tid & 63u) == 0) stage(r, a);
-        }
-        // groups of more than OVF_BLOCK_GROUP members (the heaviest k-mers): one at a time by the
-        // whole workgroup (a single wave would walk them ~20 times serially)
-        for (uint32_t bi = 0; bi < nbig; ++bi) {
-            const uint32_t gg = s_big[bi];
-            const uint32_t a = heads[gg];
-            const uint32_t b = gg + 1 < G ? heads[gg + 1] : n;
-            if (b - a <= OVF_BLOCK_GROUP) continue;
-            GRes r;
-            if (!group_block(V, a, b - a, A.glen, A.flags, reinterpret_cast<uint32_t*>(s_hi), 2 * CAP, s_wave, r)) {
-                if (tid < 64) r = group_wave(V, a, b - a, A.glen, A.flags);  // > 2*CAP function runs
+        // group heads
+        uint32_t G = 0;
+        for (uint32_t c0 = 0; c0 < n; c0 += nt) {
+            const uint32_t t = c0 + tid;
+            const bool head = t < n && (t == 0 || (ghi[t] >> 16) != (ghi[t - 1] >> 16));
+            uint32_t tot;
+            const uint32_t pos = wg_exclusive_scan(head ? 1u : 0u, s_wave, tot);
+            if (head) {
+                heads[G + pos] = t;
+                jobinfo[t] = 0;
             }
-            if (tid == 0) stage(r, a);
-            __syncthreads();
+            G += tot;
         }
         __threadfence_block();
         __syncthreads();
-    }
-    // emit over groups
-    unsigned long long* s_base = reinterpret_cast<unsigned long long*>(s_wave + 36);
-    for (uint32_t g0 = 0; g0 < G; g0 += nt) {
-        const uint32_t g = g0 + tid;
-        const uint32_t a = g < G ? heads[g] : 0u;
-        const uint64_t H = g < G ? ghi[a] : 0ull;
-        const bool kept = (H >> 63) != 0;
-        const uint64_t jb = kept ? jobinfo[a] : 0ull;
-        const uint32_t jn = (uint32_t)(jb & 0xFFFFFFFFu);
-        // an inline chain takes a slot of s_inl now (no job); without a free slot it is a job
-        uint32_t islot = OVF_INLINE_CAP;
-        if (jn >= inline_min) islot = atomicAdd(&s_ninl, 1u);
-        const bool inl = islot < OVF_INLINE_CAP;
-        uint32_t K, J, Lt;
-        const uint32_t kpos = wg_exclusive_scan(kept ? 1u : 0u, s_wave, K);
-        const uint32_t jpos = wg_exclusive_scan((jn && !inl) ? 1u : 0u, s_wave, J);
-        const uint32_t lpos = wg_exclusive_scan(jn, s_wave, Lt);
-        if (K == 0) continue;
-        if (tid == 0) {
-            s_base[0] = atomicAdd(A.kept_ctr, (unsigned long long)K);
-            atomicAdd(&A.ctr[0], (unsigned long long)K);  // the overflow's own kept count
-            if (J) {
-                s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)J);
-                s_base[2] = atomicAdd(&A.ctr[4], (unsigned long long)Lt);
-            }
-            s_nbig = 0;
-        }
-        __syncthreads();
-        if (kept) {
-            const uint64_t o = s_base[0] + kpos;
-            if (jn) {
-                const uint32_t fm = fmean[a];
-                write_kept(A, o, H, kept_lo(fm & 0xFFFFu, fm >> 16, 0, 0));
-                Job jbr;
-                jbr.lens_off = s_base[2] + lpos;
-                jbr.n = jn;
-                jbr.out_idx = (uint32_t)o;
-                if (inl) {
-                    s_inl[islot][0] = jbr.lens_off;
-                    s_inl[islot][1] = ((uint64_t)jn << 32) | (uint32_t)o;
-                } else {
-                    A.jobs[s_base[1] + jpos] = jbr;
-                }
-                if (jn <= 64) {
-                    const uint64_t start = jb >> 32;
-                    for (uint32_t t = 0; t < jn; ++t)
-                        A.lens[jbr.lens_off + t] = A.glen[glo[start + jn - 1 - t] >> 36];
-                } else {
-                    const uint32_t bi = atomicAdd(&s_nbig, 1u);
-                    s_big[bi] = g;
-                    s_lo[bi] = jbr.lens_off;
-                }
+        const GlbView V{ghi, glo};
+        auto stage = [&](const GRes& r, uint32_t a) {
+            if (!r.kept) return;
+            const uint64_t h43 = hprefix | (ghi[a] >> 16);
+            if (r.cbest >= 3) {
+                jobinfo[a] = ((uint64_t)(a + r.rb) << 32) | r.cbest;
+                fmean[a] = r.best_f | ((uint32_t)r.mean << 16);
             } else {
-                write_kept(A, o, H, glo[a]);
+                glo[a] = kept_lo(r.best_f, r.mean, r.median, r.var);
+            }
+            ghi[a] = kept_hi(h43, r.avg);
+        };
+        for (uint32_t g0 = 0; g0 < G; g0 += nt) {
+            if (tid == 0) s_nbig = 0;
+            __syncthreads();
+            const uint32_t g = g0 + tid;
+            if (g < G) {
+                const uint32_t a = heads[g];
+                const uint32_t b = g + 1 < G ? heads[g + 1] : n;
+                const uint32_t c = b - a;
+                if (c > (uint32_t)SMALLC) {
+                    s_big[atomicAdd(&s_nbig, 1u)] = g;
+                } else {
+                    GRes r;
+                    if (c <= 4)
+                        r = group_thread<4>(V, a, c, A.glen, A.flags);
+                    else if (c <= 8)
+                        r = group_thread<8>(V, a, c, A.glen, A.flags);
+                    else
+                        r = group_thread<16>(V, a, c, A.glen, A.flags);
+                    stage(r, a);
+                }
+            }
+            __syncthreads();
+            const uint32_t nbig = s_nbig;
+            for (uint32_t bi = tid >> 6; bi < nbig; bi += nt >> 6) {
+                const uint32_t gg = s_big[bi];
+                const uint32_t a = heads[gg];
+                const uint32_t b = gg + 1 < G ? heads[gg + 1] : n;
+                if (b - a > OVF_BLOCK_GROUP) continue;  // the whole workgroup takes it below
+                const GRes r = group_wave(V, a, b - a, A.glen, A.flags);
+                if ((tid & 63u) == 0) stage(r, a);
+            }
+            // groups of more than OVF_BLOCK_GROUP members (the heaviest k-mers): one at a time by the
+            // whole workgroup (a single wave would walk them ~20 times serially)
+            for (uint32_t bi = 0; bi < nbig; ++bi) {
+                const uint32_t gg = s_big[bi];
+                const uint32_t a = heads[gg];
+                const uint32_t b = gg + 1 < G ? heads[gg + 1] : n;
+                if (b - a <= OVF_BLOCK_GROUP) continue;
+                GRes r;
+                if (!group_block(V, a, b - a, A.glen, A.flags, reinterpret_cast<uint32_t*>(s_hi), 2 * CAP, s_wave, r)) {
+                    if (tid < 64) r = group_wave(V, a, b - a, A.glen, A.flags);  // > 2*CAP function runs
+                }
+                if (tid == 0) stage(r, a);
+                __syncthreads();
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+        // emit over groups
+        unsigned long long* s_base = reinterpret_cast<unsigned long long*>(s_wave + 36);
+        for (uint32_t g0 = 0; g0 < G; g0 += nt) {
+            const uint32_t g = g0 + tid;
+            const uint32_t a = g < G ? heads[g] : 0u;
+            const uint64_t H = g < G ? ghi[a] : 0ull;
+            const bool kept = (H >> 63) != 0;
+            const uint64_t jb = kept ? jobinfo[a] : 0ull;
+            const uint32_t jn = (uint32_t)(jb & 0xFFFFFFFFu);
+            // an inline chain takes a slot of s_inl now (no job); without a free slot it is a job
+            uint32_t islot = OVF_INLINE_CAP;
+            if (jn >= inline_min) islot = atomicAdd(&s_ninl, 1u);
+            const bool inl = islot < OVF_INLINE_CAP;
+            uint32_t K, J, Lt;
+            const uint32_t kpos = wg_exclusive_scan(kept ? 1u : 0u, s_wave, K);
+            const uint32_t jpos = wg_exclusive_scan((jn && !inl) ? 1u : 0u, s_wave, J);
+            const uint32_t lpos = wg_exclusive_scan(jn, s_wave, Lt);
+            if (K == 0) continue;
+            if (tid == 0) {
+                s_base[0] = atomicAdd(A.kept_ctr, (unsigned long long)K);
+                atomicAdd(&A.ctr[0], (unsigned long long)K);  // the overflow's own kept count
+                if (J) {
+                    s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)J);
+                    s_base[2] = atomicAdd(&A.ctr[4], (unsigned long long)Lt);
+                }
+                s_nbig = 0;
+            }
+            __syncthreads();
+            if (kept) {
+                const uint64_t o = s_base[0] + kpos;
+                if (jn) {
+                    const uint32_t fm = fmean[a];
+                    write_kept(A, o, H, kept_lo(fm & 0xFFFFu, fm >> 16, 0, 0));
+                    Job jbr;
+                    jbr.lens_off = s_base[2] + lpos;
+                    jbr.n = jn;
+                    jbr.out_idx = (uint32_t)o;
+                    if (inl) {
+                        s_inl[islot][0] = jbr.lens_off;
+                        s_inl[islot][1] = ((uint64_t)jn << 32) | (uint32_t)o;
+                    } else {
+                        A.jobs[s_base[1] + jpos] = jbr;
+                    }
+                    if (jn <= 64) {
+                        const uint64_t start = jb >> 32;
+                        for (uint32_t t = 0; t < jn; ++t)
+                            A.lens[jbr.lens_off + t] = A.glen[glo[start + jn - 1 - t] >> 36];
+                    } else {
+                        const uint32_t bi = atomicAdd(&s_nbig, 1u);
+                        s_big[bi] = g;
+                        s_lo[bi] = jbr.lens_off;
+                    }
+                } else {
+                    write_kept(A, o, H, glo[a]);
+                }
+            }
+            __syncthreads();
+            // long chains: the whole workgroup writes their lengths
+            const uint32_t nb = s_nbig;
+            for (uint32_t q = 0; q < nb; ++q) {
+                const uint32_t gg = s_big[q];
+                const uint32_t aa = heads[gg];
+                const uint64_t jbq = jobinfo[aa];
+                const uint32_t nq = (uint32_t)(jbq & 0xFFFFFFFFu);
+                const uint64_t start = jbq >> 32;
+                const uint64_t loff = s_lo[q];
+                for (uint32_t t = tid; t < nq; t += nt) A.lens[loff + t] = A.glen[glo[start + nq - 1 - t] >> 36];
+            }
+            __syncthreads();
+        }
+        // inline chains: a wave pair each (P^2 on the even wave, variance on the odd), raised issue
+        // priority -- they are the critical path of the overflow stream
+        __threadfence_block();
+        __syncthreads();
+        const uint32_t ninl = min(s_ninl, OVF_INLINE_CAP);
+        const uint32_t wave = tid >> 6, pairs = (nt >> 6) / 2;
+        if (ninl && prio == 1) __builtin_amdgcn_s_setprio(1);
+        if (ninl && prio == 2) __builtin_amdgcn_s_setprio(2);
+        if (ninl && prio >= 3) __builtin_amdgcn_s_setprio(3);
+        for (uint32_t q = wave / 2; q < ninl; q += pairs) {
+            const uint64_t off = s_inl[q][0], w = s_inl[q][1];
+            const uint32_t cn = (uint32_t)(w >> 32), o = (uint32_t)w;
+            const uint32_t* x = A.lens + off;
+            if ((wave & 1u) == 0) {
+                const double med = chain_long_p2(x, cn);
+                if ((tid & 63u) == 0) A.out_data[o].median = d2u16(med);
+            } else {
+                const double v = chain_long_var(x, cn);
+                if ((tid & 63u) == 0) A.out_data[o].var = d2u16(v);
             }
         }
-        __syncthreads();
-        // long chains: the whole workgroup writes their lengths
-        const uint32_t nb = s_nbig;
-        for (uint32_t q = 0; q < nb; ++q) {
-            const uint32_t gg = s_big[q];
-            const uint32_t aa = heads[gg];
-            const uint64_t jbq = jobinfo[aa];
-            const uint32_t nq = (uint32_t)(jbq & 0xFFFFFFFFu);
-            const uint64_t start = jbq >> 32;
-            const uint64_t loff = s_lo[q];
-            for (uint32_t t = tid; t < nq; t += nt) A.lens[loff + t] = A.glen[glo[start + nq - 1 - t] >> 36];
+    };
+    for (;;) {
+        if (threadIdx.x == 0) {
+            s_q = q_lo + atomicAdd(&plan[q_slot], 1u);
+            s_ninl = 0;
         }
         __syncthreads();
-    }
-    // inline chains: a wave pair each (P^2 on the even wave, variance on the odd), raised issue
-    // priority -- they are the critical path of the overflow stream
-    __threadfence_block();
-    __syncthreads();
-    const uint32_t ninl = min(s_ninl, OVF_INLINE_CAP);
-    const uint32_t wave = tid >> 6, pairs = (nt >> 6) / 2;
-    if (ninl && prio == 1) __builtin_amdgcn_s_setprio(1);
-    if (ninl && prio == 2) __builtin_amdgcn_s_setprio(2);
-    if (ninl && prio >= 3) __builtin_amdgcn_s_setprio(3);
-    for (uint32_t q = wave / 2; q < ninl; q += pairs) {
-        const uint64_t off = s_inl[q][0], w = s_inl[q][1];
-        const uint32_t cn = (uint32_t)(w >> 32), o = (uint32_t)w;
-        const uint32_t* x = A.lens + off;
-        if ((wave & 1u) == 0) {
-            const double med = chain_long_p2(x, cn);
-            if ((tid & 63u) == 0) A.out_data[o].median = d2u16(med);
-        } else {
-            const double v = chain_long_var(x, cn);
-            if ((tid & 63u) == 0) A.out_data[o].var = d2u16(v);
-        }
+        const uint32_t q = s_q;
+        if (q >= q_hi) break;
+        entry(A.ovf[q]);
+        __syncthreads();
     }
 }
 
@@ -2971,7 +3091,8 @@ __device__ __forceinline__ uint32_t split_hash(uint32_t rem) { return (rem * 0x9
 constexpr uint32_t SPLIT_U = 8;   // elements per thread per iteration (loads issued together)
 
 // One workgroup per overflow entry of >= SPLIT_MIN elements (the first entries of the sorted list).
-__global__ __launch_bounds__(BP_THREADS) void k_ovf_split(BucketArgs A, OvfScratch S, HeavyArgs H, uint32_t heavy_min) {
+__global__ __launch_bounds__(BP_THREADS) void k_ovf_split(BucketArgs A, OvfScratch S, HeavyArgs H, uint32_t heavy_min,
+                                                           uint32_t* plan) {
     static_assert(SPLIT_TAB == 4096, "split_hash yields 12 bits");
     __shared__ uint32_t s_key[SPLIT_TAB];
     __shared__ uint32_t s_cnt[SPLIT_TAB];
@@ -2980,138 +3101,151 @@ __global__ __launch_bounds__(BP_THREADS) void k_ovf_split(BucketArgs A, OvfScrat
     __shared__ uint32_t s_hcur[SPLIT_MAXH];
     __shared__ uint32_t s_nh, s_fail, s_lcur, s_heavy;
     const uint32_t tid = threadIdx.x, nt = blockDim.x, lane = tid & 63u;
-    OvfEntry e = A.ovf[blockIdx.x];
-    const uint64_t* src_hi = (e.src ? A.tmp_hi : A.recs_hi) + e.off;
-    const uint64_t* src_lo = (e.src ? A.tmp_lo : A.recs_lo) + e.off;
-    const uint32_t n = e.n;
-    constexpr uint32_t EMPTY = 0xFFFFFFFFu;
-    for (uint32_t q = tid; q < SPLIT_TAB; q += nt) {
-        s_key[q] = EMPTY;
-        s_cnt[q] = 0;
-        s_hid[q] = 0xFFFFu;
-    }
-    if (tid == 0) {
-        s_nh = 0;
-        s_fail = 0;
-        s_lcur = 0;
-        s_heavy = 0;
-    }
-    __syncthreads();
-    const uint64_t lt = (1ull << lane) - 1ull;
-    // ---- 1. occurrences per key (wave-aggregated for the lanes sharing lane 0's key) ----
-    for (uint32_t j0 = 0; j0 < n; j0 += nt * SPLIT_U) {
-        uint32_t rems[SPLIT_U];
-#pragma unroll
-        for (uint32_t u = 0; u < SPLIT_U; ++u) {
-            const uint32_t j = j0 + u * nt + tid;
-            rems[u] = j < n ? (uint32_t)(src_hi[j] >> 16) & REM_MASK : EMPTY;
+    __shared__ uint32_t s_q;
+    // entries [0, plan[PLAN_NSPLIT]) of k_ovf_plan's list (the largest), from queue plan[PLAN_Q_SPLIT]
+    const uint32_t q_hi = plan[PLAN_NSPLIT];
+    auto entry = [&](const uint32_t qe) {
+        OvfEntry e = A.ovf[qe];
+        const uint64_t* src_hi = (e.src ? A.tmp_hi : A.recs_hi) + e.off;
+        const uint64_t* src_lo = (e.src ? A.tmp_lo : A.recs_lo) + e.off;
+        const uint32_t n = e.n;
+        constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+        for (uint32_t q = tid; q < SPLIT_TAB; q += nt) {
+            s_key[q] = EMPTY;
+            s_cnt[q] = 0;
+            s_hid[q] = 0xFFFFu;
         }
-#pragma unroll
-        for (uint32_t u = 0; u < SPLIT_U; ++u) {
-            const uint32_t rem = rems[u];
-            const bool v = rem != EMPTY;
-            const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)rem);
-            const uint64_t same = __ballot(v && rem == r0);
-            const bool lead = v && rem == r0 && (same & lt) == 0;
-            if (v && (rem != r0 || lead)) {
-                uint32_t slot = split_hash(rem), probe = 0;
-                for (; probe < SPLIT_TAB; ++probe) {
-                    const uint32_t k = s_key[slot];
-                    if (k == rem) break;
-                    if (k == EMPTY) {
-                        const uint32_t old = atomicCAS(&s_key[slot], EMPTY, rem);
-                        if (old == EMPTY || old == rem) break;
+        if (tid == 0) {
+            s_nh = 0;
+            s_fail = 0;
+            s_lcur = 0;
+            s_heavy = 0;
+        }
+        __syncthreads();
+        const uint64_t lt = (1ull << lane) - 1ull;
+        // ---- 1. occurrences per key (wave-aggregated for the lanes sharing lane 0's key) ----
+        for (uint32_t j0 = 0; j0 < n; j0 += nt * SPLIT_U) {
+            uint32_t rems[SPLIT_U];
+    #pragma unroll
+            for (uint32_t u = 0; u < SPLIT_U; ++u) {
+                const uint32_t j = j0 + u * nt + tid;
+                rems[u] = j < n ? (uint32_t)(src_hi[j] >> 16) & REM_MASK : EMPTY;
+            }
+    #pragma unroll
+            for (uint32_t u = 0; u < SPLIT_U; ++u) {
+                const uint32_t rem = rems[u];
+                const bool v = rem != EMPTY;
+                const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)rem);
+                const uint64_t same = __ballot(v && rem == r0);
+                const bool lead = v && rem == r0 && (same & lt) == 0;
+                if (v && (rem != r0 || lead)) {
+                    uint32_t slot = split_hash(rem), probe = 0;
+                    for (; probe < SPLIT_TAB; ++probe) {
+                        const uint32_t k = s_key[slot];
+                        if (k == rem) break;
+                        if (k == EMPTY) {
+                            const uint32_t old = atomicCAS(&s_key[slot], EMPTY, rem);
+                            if (old == EMPTY || old == rem) break;
+                        }
+                        slot = (slot + 1) & (SPLIT_TAB - 1);
                     }
-                    slot = (slot + 1) & (SPLIT_TAB - 1);
+                    if (probe == SPLIT_TAB)
+                        s_fail = 1;
+                    else
+                        atomicAdd(&s_cnt[slot], lead ? (uint32_t)__popcll(same) : 1u);
                 }
-                if (probe == SPLIT_TAB)
-                    s_fail = 1;
-                else
-                    atomicAdd(&s_cnt[slot], lead ? (uint32_t)__popcll(same) : 1u);
             }
         }
-    }
-    __syncthreads();
-    if (s_fail) return;  // more distinct keys than the table holds: the entry keeps the sort path
-    // ---- 2. heavy keys: their own ranges in the heavy arrays ----
-    for (uint32_t q = tid; q < SPLIT_TAB; q += nt)
-        if (s_cnt[q] >= heavy_min) {
-            const uint32_t h = atomicAdd(&s_nh, 1u);
-            if (h < SPLIT_MAXH) {
-                s_hid[q] = (uint16_t)h;
-                s_hcur[h] = 0;
-                const uint64_t hk = atomicAdd(H.nkeys, 1ull);
-                const uint64_t base = atomicAdd(H.cursor, (unsigned long long)s_cnt[q]);
-                s_hbase[h] = base;
-                HeavyKey K;
-                K.off = base;
-                K.n = s_cnt[q];
-                K.bucket = e.bucket;
-                K.rem = s_key[q];
-                K.pad = 0;
-                H.keys[hk] = K;
-                atomicAdd(&s_heavy, s_cnt[q]);
+        __syncthreads();
+        if (s_fail) return;  // more distinct keys than the table holds: the entry keeps the sort path
+        // ---- 2. heavy keys: their own ranges in the heavy arrays ----
+        for (uint32_t q = tid; q < SPLIT_TAB; q += nt)
+            if (s_cnt[q] >= heavy_min) {
+                const uint32_t h = atomicAdd(&s_nh, 1u);
+                if (h < SPLIT_MAXH) {
+                    s_hid[q] = (uint16_t)h;
+                    s_hcur[h] = 0;
+                    const uint64_t hk = atomicAdd(H.nkeys, 1ull);
+                    const uint64_t base = atomicAdd(H.cursor, (unsigned long long)s_cnt[q]);
+                    s_hbase[h] = base;
+                    HeavyKey K;
+                    K.off = base;
+                    K.n = s_cnt[q];
+                    K.bucket = e.bucket;
+                    K.rem = s_key[q];
+                    K.pad = 0;
+                    H.keys[hk] = K;
+                    atomicAdd(&s_heavy, s_cnt[q]);
+                }
+            }
+        __syncthreads();
+        if (s_heavy == 0) return;  // nothing heavy: unchanged
+        // ---- 3. scatter: heavy members to their key's range, the rest compacted into the scratch ----
+        uint64_t* lhi = S.hi + e.scratch;
+        uint64_t* llo = S.lo + e.scratch;
+        for (uint32_t j0 = 0; j0 < n; j0 += nt * SPLIT_U) {
+            uint64_t eh[SPLIT_U], el[SPLIT_U];
+    #pragma unroll
+            for (uint32_t u = 0; u < SPLIT_U; ++u) {
+                const uint32_t j = j0 + u * nt + tid;
+                eh[u] = j < n ? src_hi[j] : ~0ull;
+                el[u] = j < n ? src_lo[j] : 0ull;
+            }
+    #pragma unroll
+            for (uint32_t u = 0; u < SPLIT_U; ++u) {
+                const bool v = eh[u] != ~0ull;
+                uint32_t hid = 0xFFFFu;
+                if (v) {
+                    const uint32_t rem = (uint32_t)(eh[u] >> 16) & REM_MASK;
+                    uint32_t slot = split_hash(rem);
+                    while (s_key[slot] != rem) slot = (slot + 1) & (SPLIT_TAB - 1);
+                    hid = s_hid[slot];
+                }
+                // light members: wave-aggregated cursor
+                const uint64_t lm = __ballot(v && hid == 0xFFFFu);
+                uint32_t lbase = 0;
+                if (lm) {
+                    const uint32_t leader = (uint32_t)(__ffsll((long long)lm) - 1);
+                    if (lane == leader) lbase = atomicAdd(&s_lcur, (uint32_t)__popcll(lm));
+                    lbase = (uint32_t)__shfl((int)lbase, (int)leader, 64);
+                }
+                if (v && hid == 0xFFFFu) {
+                    const uint32_t pos = lbase + (uint32_t)__popcll(lm & lt);
+                    lhi[pos] = eh[u];
+                    llo[pos] = el[u];
+                }
+                // heavy members: aggregated for the lanes sharing lane 0's key
+                const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(v ? hid : 0xFFFFu));
+                const uint64_t hm = __ballot(v && hid != 0xFFFFu && hid == h0);
+                uint32_t hbase = 0;
+                if (hm) {
+                    const uint32_t leader = (uint32_t)(__ffsll((long long)hm) - 1);
+                    if (lane == leader) hbase = atomicAdd(&s_hcur[h0], (uint32_t)__popcll(hm));
+                    hbase = (uint32_t)__shfl((int)hbase, (int)leader, 64);
+                }
+                if (v && hid != 0xFFFFu) {
+                    const uint32_t pos = hid == h0 ? hbase + (uint32_t)__popcll(hm & lt) : atomicAdd(&s_hcur[hid], 1u);
+                    const uint64_t o = s_hbase[hid] + pos;
+                    H.hi[o] = eh[u];
+                    H.lo[o] = el[u];
+                }
             }
         }
-    __syncthreads();
-    if (s_heavy == 0) return;  // nothing heavy: unchanged
-    // ---- 3. scatter: heavy members to their key's range, the rest compacted into the scratch ----
-    uint64_t* lhi = S.hi + e.scratch;
-    uint64_t* llo = S.lo + e.scratch;
-    for (uint32_t j0 = 0; j0 < n; j0 += nt * SPLIT_U) {
-        uint64_t eh[SPLIT_U], el[SPLIT_U];
-#pragma unroll
-        for (uint32_t u = 0; u < SPLIT_U; ++u) {
-            const uint32_t j = j0 + u * nt + tid;
-            eh[u] = j < n ? src_hi[j] : ~0ull;
-            el[u] = j < n ? src_lo[j] : 0ull;
+        __syncthreads();
+        if (tid == 0) {  // the entry now names its light remainder (in place in its scratch)
+            e.n = n - s_heavy;
+            e.src = 2;
+            e.off = e.scratch;
+            A.ovf[qe] = e;
         }
-#pragma unroll
-        for (uint32_t u = 0; u < SPLIT_U; ++u) {
-            const bool v = eh[u] != ~0ull;
-            uint32_t hid = 0xFFFFu;
-            if (v) {
-                const uint32_t rem = (uint32_t)(eh[u] >> 16) & REM_MASK;
-                uint32_t slot = split_hash(rem);
-                while (s_key[slot] != rem) slot = (slot + 1) & (SPLIT_TAB - 1);
-                hid = s_hid[slot];
-            }
-            // light members: wave-aggregated cursor
-            const uint64_t lm = __ballot(v && hid == 0xFFFFu);
-            uint32_t lbase = 0;
-            if (lm) {
-                const uint32_t leader = (uint32_t)(__ffsll((long long)lm) - 1);
-                if (lane == leader) lbase = atomicAdd(&s_lcur, (uint32_t)__popcll(lm));
-                lbase = (uint32_t)__shfl((int)lbase, (int)leader, 64);
-            }
-            if (v && hid == 0xFFFFu) {
-                const uint32_t pos = lbase + (uint32_t)__popcll(lm & lt);
-                lhi[pos] = eh[u];
-                llo[pos] = el[u];
-            }
-            // heavy members: aggregated for the lanes sharing lane 0's key
-            const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(v ? hid : 0xFFFFu));
-            const uint64_t hm = __ballot(v && hid != 0xFFFFu && hid == h0);
-            uint32_t hbase = 0;
-            if (hm) {
-                const uint32_t leader = (uint32_t)(__ffsll((long long)hm) - 1);
-                if (lane == leader) hbase = atomicAdd(&s_hcur[h0], (uint32_t)__popcll(hm));
-                hbase = (uint32_t)__shfl((int)hbase, (int)leader, 64);
-            }
-            if (v && hid != 0xFFFFu) {
-                const uint32_t pos = hid == h0 ? hbase + (uint32_t)__popcll(hm & lt) : atomicAdd(&s_hcur[hid], 1u);
-                const uint64_t o = s_hbase[hid] + pos;
-                H.hi[o] = eh[u];
-                H.lo[o] = el[u];
-            }
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {  // the entry now names its light remainder (in place in its scratch)
-        e.n = n - s_heavy;
-        e.src = 2;
-        e.off = e.scratch;
-        A.ovf[blockIdx.x] = e;
+    };
+    for (;;) {
+        if (tid == 0) s_q = atomicAdd(&plan[PLAN_Q_SPLIT], 1u);
+        __syncthreads();
+        const uint32_t q = s_q;
+        if (q >= q_hi) break;
+        entry(q);
+        __syncthreads();
     }
 }
 
@@ -3199,7 +3333,7 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
     __shared__ uint32_t s_wc[HEAVY_WG / 64][RBINS];
     __shared__ __align__(16) uint32_t s_wave[48];
     __shared__ uint32_t s_bm[2 * (HEAVY_WG / 64)];
-    __shared__ uint32_t s_cur, s_sel[2];
+    __shared__ uint32_t s_cur, s_sel[3];
     const uint32_t tid = threadIdx.x, nt = blockDim.x, lane = tid & 63u, wave = tid >> 6, nw = nt >> 6;
     const uint64_t lt = (1ull << lane) - 1ull;
     const uint32_t nkeys = (uint32_t)*H.nkeys;
@@ -3351,22 +3485,31 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
         while (bits < 32 && (smax >> bits)) bits += RB;
         const uint32_t* sorted = wg_radix_sort_u32(sa, sb, cb, bits, s_hist, s_wc, s_run, tag);
         __syncthreads();
-        const bool giant = H.giant_min && cb >= H.giant_min;
         if (tid == 0) {
             s_sel[0] = (uint32_t)atomicAdd(A.kept_ctr, 1ull);
             atomicAdd(&A.ctr[0], 1ull);
-            if (giant) {
-                s_sel[1] = (uint32_t)atomicAdd(&H.gcount[0], 1ull);
-                s_cur = (uint32_t)atomicAdd(&H.gcount[1], (unsigned long long)cb);
-                atomicAdd(&H.gstat[0], 1ull);
-                atomicMax(&H.gstat[1], (unsigned long long)cb);
-            } else {
+            // a giant chain's samples go to the pass's giant buffer while it has room (sized
+            // before the run: a key that does not fit takes the ordinary job path)
+            bool g = false;
+            if (H.giant_min && cb >= H.giant_min) {
+                const uint64_t c = atomicAdd(&H.gcount[1], (unsigned long long)cb);
+                if (c + cb <= H.gcap) {
+                    g = true;
+                    s_cur = (uint32_t)c;
+                    s_sel[1] = (uint32_t)atomicAdd(&H.gcount[0], 1ull);
+                    atomicAdd(&H.gstat[0], 1ull);
+                    atomicMax(&H.gstat[1], (unsigned long long)cb);
+                }
+            }
+            if (!g) {
                 s_sel[1] = (uint32_t)atomicAdd(&A.ctr[3], 1ull);
                 s_cur = (uint32_t)atomicAdd(&A.ctr[4], (unsigned long long)cb);
             }
+            s_sel[2] = g ? 1u : 0u;
         }
         __syncthreads();
         const uint32_t o = s_sel[0], jb = s_sel[1], loff = s_cur;
+        const bool giant = s_sel[2] != 0;
         uint32_t* lens_out = giant ? H.gsamples : A.lens;
         for (uint32_t t0 = 0; t0 < cb; t0 += nt * U) {
             uint32_t sv[U];
@@ -3399,12 +3542,152 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Overflow plan, on the device (one workgroup, right after k_partition): the host used to read the
+// overflow list back, sort it by size and size the scratch.  The entries are counting-sorted into
+// descending size classes (tier by the split / heavy thresholds, then floor(log2 n)), so the split
+// and heavy entries are prefixes and the persistent kernels take the largest first; each entry gets
+// its scratch range (pow2 >= n elements); the totals are checked against the work buffers sized
+// before the run (too small: the demand is recorded and the step redone with grown buffers) and the
+// kept arena against the pass's element count (full: SKM_E_OOM at the step's end).
+// ------------------------------------------------------------------------------------------
+struct PlanArgs {
+    const OvfEntry* in;                 // k_partition's list
+    OvfEntry* out;                      // sorted by size class, descending, scratch assigned
+    const unsigned long long* ctr;      // the pass's counters: [0] arena cursor, [1] entries (low 32 bits)
+    const unsigned long long* nloc;     // elements the pass groups
+    unsigned long long* run;
+    uint32_t* plan;
+    uint32_t ovf_cap, split_min, heavy_min;
+    uint64_t kept_cap, tot_cap, split_cap;
+};
+
+constexpr uint32_t PLAN_BINS = 3 * 32;
+
+__device__ __forceinline__ uint32_t plan_bin(uint32_t n, uint32_t split_min, uint32_t heavy_min) {
+    const uint32_t tier = (n >= split_min ? 1u : 0u) + (n >= heavy_min ? 1u : 0u);
+    return PLAN_BINS - 1u - (tier * 32u + (31u - (uint32_t)__clz(n | 1u)));  // 0: the largest
+}
+
+__global__ __launch_bounds__(1024) void k_ovf_plan(PlanArgs P) {
+    __shared__ uint32_t s_cnt[PLAN_BINS];
+    __shared__ unsigned long long s_part[1024];
+    __shared__ unsigned long long s_tot, s_elems, s_split;
+    __shared__ uint32_t s_nsplit, s_nheavy;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const uint64_t raw = P.ctr[1] & 0xFFFFFFFFull;
+    const uint32_t n = (uint32_t)min<uint64_t>(raw, P.ovf_cap);
+    for (uint32_t i = tid; i < PLAN_BINS; i += nt) s_cnt[i] = 0;
+    if (tid == 0) {
+        s_tot = s_elems = s_split = 0;
+        s_nsplit = s_nheavy = 0;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += nt) atomicAdd(&s_cnt[plan_bin(P.in[i].n, P.split_min, P.heavy_min)], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t r = 0;
+        for (uint32_t b = 0; b < PLAN_BINS; ++b) {
+            const uint32_t c = s_cnt[b];
+            s_cnt[b] = r;
+            r += c;
+        }
+    }
+    __syncthreads();
+    unsigned long long lt = 0, le = 0, ls = 0;
+    uint32_t lns = 0, lnh = 0;
+    for (uint32_t i = tid; i < n; i += nt) {
+        OvfEntry e = P.in[i];
+        const uint32_t pos = atomicAdd(&s_cnt[plan_bin(e.n, P.split_min, P.heavy_min)], 1u);
+        uint64_t np = 1;
+        while (np < e.n) np <<= 1;
+        e.npad = (uint32_t)np;
+        P.out[pos] = e;
+        lt += np;
+        le += e.n;
+        if (e.n >= P.split_min) {
+            ls += e.n;
+            ++lns;
+        }
+        if (e.n >= P.heavy_min) ++lnh;
+    }
+    atomicAdd(&s_tot, lt);
+    atomicAdd(&s_elems, le);
+    atomicAdd(&s_split, ls);
+    atomicAdd(&s_nsplit, lns);
+    atomicAdd(&s_nheavy, lnh);
+    __threadfence_block();
+    __syncthreads();
+    // scratch offsets in list order: a contiguous run of entries per thread
+    const uint32_t per = (n + nt - 1) / nt;
+    const uint32_t a = min(n, tid * per), e_ = min(n, a + per);
+    unsigned long long sum = 0;
+    for (uint32_t i = a; i < e_; ++i) sum += P.out[i].npad;
+    s_part[tid] = sum;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long r = 0;
+        for (uint32_t t = 0; t < nt; ++t) {
+            const unsigned long long v = s_part[t];
+            s_part[t] = r;
+            r += v;
+        }
+    }
+    __syncthreads();
+    unsigned long long o = s_part[tid];
+    for (uint32_t i = a; i < e_; ++i) {
+        P.out[i].scratch = o;
+        o += P.out[i].npad;
+    }
+    if (tid == 0) {
+        unsigned long long* R = P.run;
+        const uint64_t tot = s_tot, split = s_split, nl = *P.nloc;
+        // demands are recorded for every pass, so one redo takes the whole run
+        atomicMax(&R[RUN_DEM_TOT], (unsigned long long)tot);
+        atomicMax(&R[RUN_DEM_SPLIT], (unsigned long long)split);
+        if (raw > P.ovf_cap) atomicOr(&R[RUN_FLAGS], RUN_F_CAP);
+        const bool over = tot > P.tot_cap || split > P.split_cap;
+        if (over) atomicOr(&R[RUN_FLAGS], RUN_F_RERUN);
+        if (P.ctr[0] + nl > P.kept_cap) atomicOr(&R[RUN_FLAGS], RUN_F_ARENA);
+        // a pass that does not fit is skipped (the step is redone); after an error every pass is.
+        // The passes after a mere overrun still run, so their demands are known for the redo
+        const bool skip = over || (atomicAdd(&R[RUN_FLAGS], 0ull) & (RUN_F_ARENA | RUN_F_CAP)) != 0;
+        P.plan[PLAN_NOVF] = skip ? 0u : n;
+        P.plan[PLAN_NSPLIT] = skip ? 0u : s_nsplit;
+        P.plan[PLAN_NHEAVY] = skip ? 0u : s_nheavy;
+        P.plan[PLAN_SKIP] = skip ? 1u : 0u;
+        P.plan[PLAN_Q_SPLIT] = 0;
+        P.plan[PLAN_Q_HEAVY] = 0;
+        P.plan[PLAN_Q_REST] = 0;
+        R[RUN_ACC_NOVF] += n;
+        R[RUN_ACC_OVF_ELEMS] += s_elems;
+        R[RUN_ACC_GROUPED] += nl;
+        R[RUN_LAST_NOVF] = n;
+    }
+}
+
+// end of a pass (one thread, after both overflow streams joined): run totals and the bounds the
+// chain lists rely on
+__global__ void k_pass_account(const unsigned long long* __restrict__ ctr, unsigned long long* __restrict__ run,
+                               uint64_t jobs_cap, uint64_t jobs2_cap, uint64_t big_cap, uint64_t lens_cap) {
+    const unsigned long long j = ctr[3] + ctr[8 + 3];
+    run[RUN_ACC_JOBS] += j;
+    run[RUN_ACC_LENS] += ctr[8 + 4];
+    run[RUN_ACC_OVF_KEPT] += ctr[8];
+    run[RUN_ACC_BIG] += ctr[5];
+    run[RUN_ACC_BIG_KEPT] += ctr[6];
+    run[RUN_LAST_JOBS] = j;
+    if (ctr[3] > jobs_cap || ctr[8 + 3] > jobs2_cap || ctr[5] > big_cap || ctr[8 + 4] > lens_cap)
+        atomicOr(&run[RUN_FLAGS], RUN_F_CAP);
+}
+
 // distinct_functions[f] += kept k-mers with best function f (LDS privatised when it fits)
 // Over the whole kept arena after the last pass: decode each key (43-bit hash -> unmix43 ->
 // base-40 -> the 8 residue bytes, Kmer<8> as a little-endian u64) and count distinct_functions.
-__global__ void k_kept_finalize(uint64_t* __restrict__ keys, const skm_stored_kmer_data* __restrict__ data, uint64_t n,
-                                uint32_t nf, uint32_t* __restrict__ dfunc) {
+__global__ void k_kept_finalize(uint64_t* __restrict__ keys, const skm_stored_kmer_data* __restrict__ data,
+                                const unsigned long long* __restrict__ n_p, uint32_t nf, uint32_t* __restrict__ dfunc) {
     extern __shared__ uint32_t s_h[];
+    const uint64_t n = *n_p;  // the arena cursor after the last pass
     const bool lds = nf <= 16384;
     if (lds)
         for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) s_h[f] = 0;
@@ -3494,7 +3777,14 @@ struct skm_build {
     skm_build_opts opts{};
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[13] = {};
+    // timing events, one set per key-range pass (read after the step's single host sync)
+    struct EvSet {
+        hipEvent_t ev[13] = {}, o[3] = {}, o3[3] = {};
+    };
+    std::deque<EvSet> evsets;
+    hipEvent_t* ev = nullptr;           // the current pass's set
+    hipEvent_t* ev_o = nullptr;
+    hipEvent_t* ev_o3 = nullptr;
     float last_ms[12] = {};
     uint64_t ovf_elems = 0, ovf_kept = 0;
 
@@ -3560,16 +3850,16 @@ struct skm_build {
 
     // second stream: overflow sub-buckets + their chains, concurrent with the group-by
     hipStream_t stream2 = nullptr, stream3 = nullptr;
-    hipEvent_t ev_part = nullptr, ev_split = nullptr, ev_o[3] = {}, ev_o3[3] = {};
+    hipEvent_t ev_part = nullptr, ev_split = nullptr;
     DevBuf d_hv_keys, d_hv_hi, d_hv_lo, d_hv_s0, d_hv_s1;   // heavy keys of the split overflow
     DevBuf d_sub_tab, d_jobs2, d_jobs3;
 
     // pinned host staging for the pipeline's small readbacks
-    unsigned long long* h_pin = nullptr;   // [64] counters
+    unsigned long long* h_pin = nullptr;   // [128] counters and run slots
     OvfEntry* h_ovf = nullptr;
     size_t h_ovf_cap = 0;
     unsigned long long* pinned_ctr() {
-        if (!h_pin) SKM_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_pin), 64 * 8, hipHostMallocDefault));
+        if (!h_pin) SKM_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_pin), 128 * 8, hipHostMallocDefault));
         return h_pin;
     }
     OvfEntry* pinned_ovf(size_t n) {
@@ -3619,9 +3909,14 @@ struct skm_build {
     bool gused[GSLOTS] = {};
     DevBuf d_gstat;                      // run totals: giant chains, longest giant chain
     uint64_t giant_jobs = 0, giant_max = 0;
-    std::deque<DevBuf> long_arena;       // stashed samples per (pass, launch site)
+    DevBuf d_long_arena;                 // stashed samples of the run's long chains
     DevBuf d_long_jobs;                  // run-level list of stashed long jobs (device addresses)
-    uint64_t long_jobs_cap = 0, n_long = 0, long_samples = 0, long_launched = 0;
+    uint64_t long_jobs_cap = 0;
+    // device-side pass control: the overflow plan (sorted list, per-pass plan) and the run slots
+    DevBuf d_ovf2, d_plan, d_run;
+    // capacities of the data-dependent work buffers (alloc_caps), grown to a run's demand
+    uint64_t tot_cap = 0, split_cap = 0, long_cap = 0;
+    uint64_t run_flags = 0, demand[4] = {}, n_jobs_last = 0, n_redo = 0;
 };
 
 namespace {
@@ -4055,6 +4350,9 @@ void ensure_local(skm_build* b, uint64_t n) {
     b->d_jobs.ensure(sizeof(Job) * b->jobs_cap);
     b->d_lens.ensure(sizeof(uint32_t) * b->lens_cap);
     b->d_ovf.ensure(sizeof(OvfEntry) * b->ovf_cap);
+    b->big_cap = c / 65 + 64;  // groups of > 64 members
+    b->d_big_desc.ensure(16 * b->big_cap);
+    b->d_big_out.ensure(sizeof(BigOut) * b->big_cap);
     b->cap_local = c;
 }
 
@@ -4088,9 +4386,9 @@ void size_arena(skm_build* b) {
     if (b->pass_bits == 0) return;
     size_t fr = 0, tot = 0;
     SKM_HIP(hipMemGetInfo(&fr, &tot));
-    // the pass work buffers beyond what is allocated now (tmp, chains, overflow scratch) come out
-    // of the same memory: keep ~PASS_BYTES - 32 per element of the largest pass in reserve
-    const uint64_t reserve = b->pass_max * (PASS_BYTES - 32) + (1ull << 30);
+    // the work buffers are allocated by now (alloc_caps); keep 32 B per element of the largest pass
+    // in reserve for a redo that grows them (and for the received buffers at world > 1)
+    const uint64_t reserve = b->pass_max * 32 + (1ull << 30);
     const uint64_t avail = fr > reserve ? fr - reserve : 0;
     uint64_t cap = std::min<uint64_t>(b->valid_total + 16, avail / (8 + sizeof(skm_stored_kmer_data)));
     if (b->tune.mem_budget_mb > 0) {
@@ -4103,6 +4401,8 @@ void size_arena(skm_build* b) {
     b->d_data.ensure(sizeof(skm_stored_kmer_data) * cap + 16);
     b->kept_cap = cap;
 }
+
+void alloc_caps(skm_build* b);
 
 void prepare(const Ranks& bs) {
     bool need = false;
@@ -4186,6 +4486,12 @@ void prepare(const Ranks& bs) {
         }
     }
     for (auto* b : bs) {
+        if (!b->tot_cap) {  // first guesses; a run that needs more grows them (run_ranks)
+            b->tot_cap = b->cap_local / 8 * 5 + (1u << 16);
+            b->split_cap = b->tot_cap / 2;
+            b->long_cap = b->pass_bits ? b->valid_total / 8 + (1u << 16) : 0;
+        }
+        alloc_caps(b);
         size_arena(b);
         b->d_flags.ensure(std::max<uint64_t>(b->n_total, 1));
         SKM_HIP(hipStreamSynchronize(b->stream));
@@ -4339,7 +4645,11 @@ void exchange(const Ranks& bs) {
         b->recv_off = rp.off;
         b->recv_cnt = rp.n;
         b->n_local = rp.total;
-        ensure_local(b, rp.total);
+        if (rp.total > b->cap_local) {
+            ensure_local(b, rp.total);
+            SKM_HIP(hipDeviceSynchronize());  // the chain lists follow the grown element capacity
+            alloc_caps(b);
+        }
         b->d_seg_start.ensure(8ull * NB);
         b->d_seg_len.ensure(4ull * NB);
         b->d_vstart.ensure(8ull * (NB1 + 1));
@@ -4368,34 +4678,33 @@ void exchange(const Ranks& bs) {
     alltoallv(bs, ex_lo);
 }
 
-// Job sort by length class (longest first) + the chain kernels.  Chains of >= 2^long_class
-// samples get a wave pair each (k_chain_long): their samples are stashed into the run's long
-// arena and they run on one of the build's chain streams, overlapping the following passes; the
-// per-lane chains run on st (or st_short) within the pass.
-void launch_chains(skm_build* b, uint32_t site, hipStream_t st, const Job* jobs, uint64_t nj, ChainSet& cs,
-                   const uint32_t* lens, const uint32_t* recs32, const uint32_t* tmp32, const uint32_t* big32,
-                   skm_stored_kmer_data* out, uint32_t long_class, unsigned long long* pin,
+// Job sort by length class (longest first) + the chain kernels, for a job list whose length is on
+// the device (nj_d, at most cap).  Chains of >= 2^long_class samples get a wave pair each
+// (k_chain_long): in situ with one pass; with key-range passes their samples are stashed into the
+// run's long arena and they run on the chain stream, overlapping the following passes.  The
+// per-lane chains run on st (or st_short) within the pass.  Fixed grids that read the counts on
+// the device: no host round trip.
+constexpr uint32_t JOB_NWG = 256;      // k_job_count / k_job_scatter workgroups (one chunk each)
+constexpr uint32_t CHAIN_GRID = 4096;  // k_chains workgroups (two wave pairs each, grid-stride)
+constexpr uint32_t LONG_GRID = 2048;   // k_chain_long / k_long_stash workgroups (one job at a time)
+constexpr uint32_t SPLIT_GRID = 512;   // k_ovf_split workgroups (work queue)
+constexpr uint32_t OVF_GRID = 1024;    // k_overflow workgroups per stream (work queue)
+
+void launch_chains(skm_build* b, hipStream_t st, const Job* jobs, const unsigned long long* nj_d, uint64_t cap,
+                   ChainSet& cs, const uint32_t* lens, const uint32_t* recs32, const uint32_t* tmp32,
+                   const uint32_t* big32, skm_stored_kmer_data* out, uint32_t long_class,
                    hipStream_t st_short = nullptr, hipEvent_t ev_sorted = nullptr, uint32_t max_wgs = 0) {
-    if (!nj) return;
     const Tune& tn = b->tune;
-    const uint32_t nwg = (uint32_t)std::min<uint64_t>(1024, ceil_div(nj, 4096));
-    const uint64_t chunk = ceil_div(nj, nwg);
-    cs.hist.ensure(4ull * nwg * JOB_CLASSES);
-    cs.offs.ensure(8ull * nwg * JOB_CLASSES + 8);
-    cs.sorted.ensure(sizeof(Job) * nj);
-    hipLaunchKernelGGL(k_job_count, dim3(nwg), dim3(JOB_WG), 0, st, jobs, nj, chunk, cs.hist.as<uint32_t>());
-    hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(64), 0, st, cs.hist.as<uint32_t>(), nwg, cs.offs.as<uint64_t>(), long_class);
-    hipLaunchKernelGGL(k_job_scatter, dim3(nwg), dim3(JOB_WG), 0, st, jobs, nj, chunk, cs.offs.as<uint64_t>(),
+    hipLaunchKernelGGL(k_job_count, dim3(JOB_NWG), dim3(JOB_WG), 0, st, jobs, nj_d, cap, cs.hist.as<uint32_t>());
+    hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(64), 0, st, cs.hist.as<uint32_t>(), JOB_NWG, cs.offs.as<uint64_t>(),
+                       long_class);
+    hipLaunchKernelGGL(k_job_scatter, dim3(JOB_NWG), dim3(JOB_WG), 0, st, jobs, nj_d, cap, cs.offs.as<uint64_t>(),
                        cs.sorted.as<Job>());
     if (st_short && ev_sorted) SKM_HIP(hipEventRecord(ev_sorted, st));  // sorted jobs ready
-    // long jobs first in the sorted order: their offsets in the arena, count and total samples
-    cs.long_off.ensure(8ull * (nj + 2));
-    hipLaunchKernelGGL(k_long_plan, dim3(1), dim3(1024), 0, st, cs.sorted.as<Job>(),
-                       cs.offs.as<uint64_t>() + (uint64_t)nwg * JOB_CLASSES, cs.long_off.as<uint64_t>());
-    SKM_HIP(hipMemcpyAsync(pin, cs.offs.as<uint64_t>() + (uint64_t)nwg * JOB_CLASSES, 8, hipMemcpyDeviceToHost, st));
-    SKM_HIP(hipStreamSynchronize(st));
-    const uint64_t nlong = *pin;
-    if (nlong && b->pass_bits == 0) {
+    // k_job_scan leaves the long jobs' count after the offsets; they lead the sorted order
+    const uint64_t* nlong_d = cs.offs.as<uint64_t>() + (uint64_t)JOB_NWG * JOB_CLASSES;
+    const auto* nlong_u = reinterpret_cast<const unsigned long long*>(nlong_d);
+    if (b->pass_bits == 0) {
         // one pass: the long chains start on st as soon as their jobs are sorted
         const uint32_t lds = (uint32_t)tn.chain_lds_kb * 1024u;
         static bool attr = false;
@@ -4404,50 +4713,33 @@ void launch_chains(skm_build* b, uint32_t site, hipStream_t st, const Job* jobs,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             attr = true;
         }
-        hipLaunchKernelGGL(k_chain_long, dim3((uint32_t)nlong), dim3(128), lds, st, cs.sorted.as<Job>(), nlong, lens,
-                           recs32, tmp32, big32, out, tn.chain_prio);
-        b->n_long += nlong;
-    } else if (nlong) {
-        SKM_HIP(hipMemcpyAsync(pin, cs.long_off.as<uint64_t>() + nlong, 8, hipMemcpyDeviceToHost, st));
-        SKM_HIP(hipStreamSynchronize(st));
-        const uint64_t total = *pin;
-        if (b->long_arena.size() <= site) b->long_arena.resize(site + 1);
-        b->long_arena[site].ensure(4 * std::max<uint64_t>(total, 1));
-        SKM_CHECK(b->n_long + nlong <= b->long_jobs_cap, SKM_E_STATE, "long chain job list exceeded");
-        hipLaunchKernelGGL(k_long_stash, dim3((uint32_t)nlong), dim3(256), 0, st, cs.sorted.as<Job>(),
-                           cs.long_off.as<uint64_t>(), lens, recs32, tmp32, big32, b->long_arena[site].as<uint32_t>(),
-                           b->d_long_jobs.as<Job>() + b->n_long);
-        SKM_HIP(hipGetLastError());
-        b->n_long += nlong;
-        b->long_samples += total;
+        hipLaunchKernelGGL(k_chain_long, dim3(LONG_GRID), dim3(128), lds, st, cs.sorted.as<Job>(), nullptr, nlong_u,
+                           lens, recs32, tmp32, big32, out, tn.chain_prio);
+    } else {
+        hipLaunchKernelGGL(k_long_plan, dim3(1), dim3(1024), 0, st, cs.sorted.as<Job>(), nlong_d,
+                           cs.long_off.as<uint64_t>(), b->d_run.as<unsigned long long>(), b->long_cap,
+                           b->long_jobs_cap);
+        hipLaunchKernelGGL(k_long_stash, dim3(LONG_GRID), dim3(256), 0, st, cs.sorted.as<Job>(), nlong_d,
+                           cs.long_off.as<uint64_t>(), lens, recs32, tmp32, big32, b->d_long_arena.as<uint32_t>(),
+                           b->d_long_jobs.as<Job>());
     }
-    if (nj > nlong) {
-        // the per-lane chains on their own stream (when given): they do not wait for the long ones
-        hipStream_t ss = st;
-        if (st_short && ev_sorted) {
-            SKM_HIP(hipStreamWaitEvent(st_short, ev_sorted, 0));
-            ss = st_short;
-        }
-        const uint64_t threads = ceil_div(nj - nlong, 64) * 128;
-        uint64_t wgs = ceil_div(threads, 256);
-        if (max_wgs) wgs = std::min<uint64_t>(wgs, max_wgs);
-        hipLaunchKernelGGL(k_chains, dim3((uint32_t)wgs), dim3(256), 0, ss,
-                           cs.sorted.as<Job>() + nlong, nj - nlong, lens, recs32, tmp32, big32, out);
+    // the per-lane chains on their own stream (when given): they do not wait for the long ones
+    hipStream_t ss = st;
+    if (st_short && ev_sorted) {
+        SKM_HIP(hipStreamWaitEvent(st_short, ev_sorted, 0));
+        ss = st_short;
     }
+    hipLaunchKernelGGL(k_chains, dim3(max_wgs ? max_wgs : CHAIN_GRID), dim3(256), 0, ss, cs.sorted.as<Job>(), nlong_u,
+                       nj_d, cap, lens, recs32, tmp32, big32, out);
     SKM_HIP(hipGetLastError());
 }
 
-// Group-by.  k_partition splits the oversized level-1 buckets; the overflow sub-buckets (the
-// heaviest k-mers and their long P^2 chains) then run on a second stream, concurrently with
-// k_bucket_process on the first.
+// Group-by.  k_partition splits the oversized level-1 buckets and k_ovf_plan orders and sizes the
+// overflow sub-buckets on the device; the overflow (the heaviest k-mers and their long P^2 chains)
+// then runs on streams 2 and 3, concurrently with k_bucket_process on the first.  No host round
+// trip: every launch is issued up front, the grids that depend on counts are persistent.
 void phase_group(skm_build* b, uint32_t pass) {
-    // host-side timeline (SKM_HOST_TIMING=1): where the host waits between launches
-    const bool host_timing = b->tune.host_timing != 0;
-    const auto t0 = std::chrono::steady_clock::now();
-    double tm[8] = {0};
-#define T(i) \
-    if (host_timing) tm[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count()
-    hipStream_t st = b->stream, st2 = b->stream2;
+    hipStream_t st = b->stream, st2 = b->stream2, st3 = b->stream3;
     const bool multi = b->world > 1;
     const uint32_t NB1 = 1u << b->b1_bits;
     SKM_HIP(hipEventRecord(b->ev[4], st));
@@ -4455,6 +4747,8 @@ void phase_group(skm_build* b, uint32_t pass) {
     // all passes (begin_run clears them)
     SKM_HIP(hipMemsetAsync(b->d_ctr.as<unsigned long long>() + 1, 0, 256 - 8, st));
     unsigned long long* ctr_d = b->d_ctr.as<unsigned long long>();
+    unsigned long long* run_d = b->d_run.as<unsigned long long>();
+    uint32_t* plan_d = b->d_plan.as<uint32_t>();
     BucketArgs A;
     A.recs_hi = multi ? b->d_rhi.as<uint64_t>() : b->d_recs_hi.as<uint64_t>();
     A.recs_lo = multi ? b->d_rlo.as<uint64_t>() : b->d_recs_lo.as<uint64_t>();
@@ -4464,10 +4758,8 @@ void phase_group(skm_build* b, uint32_t pass) {
     A.seg_start = multi ? b->d_seg_start.as<uint64_t>() : nullptr;
     A.seg_len = multi ? b->d_seg_len.as<uint32_t>() : nullptr;
     A.nsrc = multi ? (uint32_t)b->world : 1u;
-    b->d_sub_tab.ensure(4ull * NB1 * SUB_TAB);
     A.sub_tab = b->d_sub_tab.as<uint32_t>();
     A.kept_ctr = ctr_d;
-
     A.nbuckets = NB1;
     A.bucket_base = (pass << (b->owner_bits + b->b1_bits)) | ((uint32_t)b->rank << b->b1_bits);
     A.rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
@@ -4482,170 +4774,123 @@ void phase_group(skm_build* b, uint32_t pass) {
     A.ovf_cap = (uint32_t)b->ovf_cap;
     A.prio = b->tune.bucket_prio;
     A.stamps = nullptr;
+    A.big_desc = b->d_big_desc.as<uint64_t>();
+    A.big_cap = (uint32_t)std::min<uint64_t>(b->big_cap, 0xFFFFFFFFull);
+    A.skip = nullptr;
     if (b->stamps) {
-        b->d_stamps.ensure(32 * 8);
         SKM_HIP(hipMemsetAsync(b->d_stamps.p, 0, 32 * 8, st));
         A.stamps = b->d_stamps.as<unsigned long long>();
     }
-    T(0);
     // ---- 4a. level-2 partition ----
     hipLaunchKernelGGL(k_partition, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[10], st));
     SKM_HIP(hipEventRecord(b->ev_pf_ready, st));
-    // readbacks go through pinned host memory (no staging copies, no pageable-copy stalls)
-    unsigned long long* ctr = b->pinned_ctr();
-    SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, 8 * 5, hipMemcpyDeviceToHost, st));
-    if (!multi) SKM_HIP(hipMemcpyAsync(ctr + 16, b->d_bstart.as<uint64_t>() + NB1, 8, hipMemcpyDeviceToHost, st));
-    SKM_HIP(hipStreamSynchronize(st));
-    T(1);
-    if (!multi) b->n_local = ctr[16];
-    SKM_CHECK(ctr[0] + b->n_local <= b->kept_cap, SKM_E_OOM,
-              "kept k-mer arena exhausted (raise the device memory budget or the key-range passes)");
-    const uint32_t novf = (uint32_t)(ctr[1] & 0xFFFFFFFFull);
-    SKM_CHECK(novf <= b->ovf_cap, SKM_E_OOM, "overflow list capacity exceeded");
-    b->n_overflow = novf;
-    b->n_overflow_last = novf;
+    // ---- the overflow plan (the pass's element count: the last bucket start, or the exchange's) ----
+    const unsigned long long* nloc_d;
+    if (multi) {  // the exchange already synchronised this pass: the count is a host value
+        unsigned long long* pin = b->pinned_ctr();
+        pin[40] = b->n_local;
+        SKM_HIP(hipMemcpyAsync(run_d + RUN_NLOC, pin + 40, 8, hipMemcpyHostToDevice, st));
+        nloc_d = run_d + RUN_NLOC;
+    } else {
+        nloc_d = reinterpret_cast<const unsigned long long*>(b->d_bstart.as<uint64_t>() + NB1);
+    }
+    const uint32_t split_min = (uint32_t)std::max(b->tune.split_min, CAP + 1);
+    const uint32_t key_min = (uint32_t)std::max(b->tune.heavy_min, 2);
+    PlanArgs P;
+    P.in = b->d_ovf.as<OvfEntry>();
+    P.out = b->d_ovf2.as<OvfEntry>();
+    P.ctr = ctr_d;
+    P.nloc = nloc_d;
+    P.run = run_d;
+    P.plan = plan_d;
+    P.ovf_cap = (uint32_t)b->ovf_cap;
+    P.split_min = split_min;
+    P.heavy_min = (uint32_t)b->tune.ovf_heavy;
+    P.kept_cap = b->kept_cap;
+    P.tot_cap = b->tot_cap;
+    P.split_cap = b->split_cap;
+    hipLaunchKernelGGL(k_ovf_plan, dim3(1), dim3(1024), 0, st, P);
+    SKM_HIP(hipGetLastError());
+    A.skip = plan_d + PLAN_SKIP;
+    SKM_HIP(hipEventRecord(b->ev_part, st));
+    SKM_HIP(hipStreamWaitEvent(st2, b->ev_part, 0));
+    SKM_HIP(hipStreamWaitEvent(st3, b->ev_part, 0));
     // ---- 5. overflow sub-buckets (> CAP elements), largest first, concurrent with the group-by:
-    //      the heavy ones (>= SKM_OVF_HEAVY elements: they alone can hold the longest P^2 chains)
-    //      on stream 2, whose chains start as soon as they are grouped; the rest on stream 3 ----
-    hipStream_t st3 = b->stream3;
+    //      the split (heavy keys out to k_heavy) and the heavy entries on stream 2, whose chains
+    //      start as soon as they are grouped; the rest on stream 3 ----
     BucketArgs A2 = A, A3 = A;
     OvfScratch S;
-    uint64_t ovf_elems = 0;
-    uint32_t nheavy = 0;
-    if (novf) {
-        OvfEntry* ov = b->pinned_ovf(novf);
-        SKM_HIP(hipMemcpyAsync(ov, b->d_ovf.p, sizeof(OvfEntry) * novf, hipMemcpyDeviceToHost, st));
-        SKM_HIP(hipStreamSynchronize(st));
-        std::sort(ov, ov + novf, [](const OvfEntry& x, const OvfEntry& y) { return x.n > y.n; });
-        const uint32_t heavy_min = (uint32_t)b->tune.ovf_heavy;
-        uint64_t tot = 0;
-        for (uint32_t q = 0; q < novf; ++q) {
-            OvfEntry& e = ov[q];
-            uint32_t np = 1;
-            while (np < e.n) np <<= 1;
-            e.npad = np;
-            e.scratch = tot;
-            tot += np;
-            ovf_elems += e.n;
-            if (e.n >= heavy_min) ++nheavy;
-        }
-        b->d_ovf_hi.ensure(tot * 8);
-        b->d_ovf_lo.ensure(tot * 8);
-        b->d_ovf_heads.ensure(tot * 4);
-        b->d_ovf_job.ensure(tot * 8);
-        b->d_ovf_fm.ensure(tot * 4);
-        b->jobs2_cap = ovf_elems / 3 + 16;
-        b->ovf_elems = ovf_elems;
-        b->d_jobs2.ensure(sizeof(Job) * b->jobs2_cap);
-        SKM_HIP(hipMemcpyAsync(b->d_ovf.p, ov, sizeof(OvfEntry) * novf, hipMemcpyHostToDevice, st));
-        SKM_HIP(hipEventRecord(b->ev_part, st));
-        SKM_HIP(hipStreamWaitEvent(st2, b->ev_part, 0));
-        SKM_HIP(hipStreamWaitEvent(st3, b->ev_part, 0));
-        S.hi = b->d_ovf_hi.as<uint64_t>();
-        S.lo = b->d_ovf_lo.as<uint64_t>();
-        S.heads = b->d_ovf_heads.as<uint32_t>();
-        S.jobinfo = b->d_ovf_job.as<uint64_t>();
-        S.fmean = b->d_ovf_fm.as<uint32_t>();
-        // both parts append to one job list (own job / length counters of the overflow; the kept
-        // counter stays shared); the chains start when both parts are grouped
-        A2.ctr = ctr_d + 8;
-        A2.jobs = b->d_jobs2.as<Job>();
-        A2.lens = b->d_lens.as<uint32_t>();
-        A3.ctr = A2.ctr;
-        A3.jobs = A2.jobs;
-        A3.lens = A2.lens;
-        A3.ovf = A2.ovf + nheavy;
-        const uint32_t inline_min = (uint32_t)b->tune.ovf_inline_min;
-        const int prio = b->tune.inline_prio;
-        SKM_HIP(hipEventRecord(b->ev_o[0], st2));
-        SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
-        // the largest entries (a prefix of the sorted list) lose their heavy keys to k_heavy first;
-        // both overflow streams then read the rewritten entries
-        uint32_t nsplit = 0;
-        uint64_t split_elems = 0;
-        const uint32_t split_min = (uint32_t)std::max(b->tune.split_min, CAP + 1);
-        const uint32_t key_min = (uint32_t)std::max(b->tune.heavy_min, 2);
-        while (nsplit < novf && ov[nsplit].n >= split_min) split_elems += ov[nsplit++].n;
-        if (nsplit) {
-            b->d_hv_keys.ensure(sizeof(HeavyKey) * (split_elems / key_min + 16));
-            b->d_hv_hi.ensure(8 * split_elems);
-            b->d_hv_lo.ensure(8 * split_elems);
-            b->d_hv_s0.ensure(4 * split_elems);
-            b->d_hv_s1.ensure(4 * split_elems);
-            HeavyArgs H;
-            H.keys = b->d_hv_keys.as<HeavyKey>();
-            H.nkeys = ctr_d + 18;  // cleared with the pass's counters
-            H.cursor = ctr_d + 19;
-            H.hi = b->d_hv_hi.as<uint64_t>();
-            H.lo = b->d_hv_lo.as<uint64_t>();
-            H.s0 = b->d_hv_s0.as<uint32_t>();
-            H.s1 = b->d_hv_s1.as<uint32_t>();
-            // giant chains: samples and jobs in this pass's own buffers (a giant key's sub-bucket has
-            // at least giant_min elements, which bounds their size), run on a rotating chain stream
-            const int gs = (int)(pass % skm_build::GSLOTS);
-            // (only in the last giant_passes passes: earlier passes' long chains overlap the
-            // later passes from the stash batches anyway; the last pass's would form the tail)
-            const uint32_t P = 1u << b->pass_bits;
-            const bool late = b->tune.giant_passes <= 0 || pass + (uint32_t)b->tune.giant_passes >= P;
-            H.giant_min = b->tune.giant_class > 0 && late ? 1u << b->tune.giant_class : 0u;
-            H.gsamples = nullptr;
-            H.gjobs = nullptr;
-            H.gcount = nullptr;
-            H.gcap = 0;
-            H.gstat = nullptr;
-            uint64_t gcap = 0;
-            for (uint32_t q = 0; q < nsplit && H.giant_min; ++q)
-                if (ov[q].n >= H.giant_min) gcap += ov[q].n;
-            if (gcap == 0) H.giant_min = 0;
-            if (H.giant_min) {
-                while (b->gsamples.size() <= pass) {
-                    b->gsamples.emplace_back();
-                    b->gjobs.emplace_back();
-                    b->gcount.emplace_back();
-                }
-                b->gsamples[pass].ensure(4 * gcap);
-                b->gjobs[pass].ensure(sizeof(Job) * (gcap / H.giant_min + 16));
-                b->gcount[pass].ensure(16);
-                SKM_HIP(hipMemsetAsync(b->gcount[pass].p, 0, 16, st2));
-                H.gsamples = b->gsamples[pass].as<uint32_t>();
-                H.gjobs = b->gjobs[pass].as<Job>();
-                H.gcount = b->gcount[pass].as<unsigned long long>();
-                H.gcap = gcap;
-                H.gstat = b->d_gstat.as<unsigned long long>();
-            }
-            hipLaunchKernelGGL(k_ovf_split, dim3(nsplit), dim3(BP_THREADS), 0, st2, A2, S, H, key_min);
-            SKM_HIP(hipEventRecord(b->ev_split, st2));
-            SKM_HIP(hipStreamWaitEvent(st3, b->ev_split, 0));
-            hipLaunchKernelGGL(k_heavy, dim3(HEAVY_GRID), dim3(HEAVY_WG), 0, st2, A2, H);
-            SKM_HIP(hipGetLastError());
-            if (H.giant_min) {
-                SKM_HIP(hipEventRecord(b->gev_ready[gs], st2));
-                SKM_HIP(hipStreamWaitEvent(b->gst[gs], b->gev_ready[gs], 0));
-                hipLaunchKernelGGL(k_chain_dyn, dim3(1024), dim3(128), 0, b->gst[gs], H.gjobs, H.gcount,
-                                   A.out_data, b->tune.chain_prio);
-                SKM_HIP(hipGetLastError());
-                SKM_HIP(hipEventRecord(b->gev_done[gs], b->gst[gs]));
-                b->gused[gs] = true;
-            }
-        }
-        if (nheavy)
-            hipLaunchKernelGGL(k_overflow, dim3(nheavy), dim3(BP_THREADS), 0, st2, A2, S, inline_min, prio);
-        SKM_HIP(hipEventRecord(b->ev_o[1], st2));
-        if (novf > nheavy)
-            hipLaunchKernelGGL(k_overflow, dim3(novf - nheavy), dim3(BP_THREADS), 0, st3, A3, S, inline_min, prio);
-        SKM_HIP(hipGetLastError());
+    S.hi = b->d_ovf_hi.as<uint64_t>();
+    S.lo = b->d_ovf_lo.as<uint64_t>();
+    S.heads = b->d_ovf_heads.as<uint32_t>();
+    S.jobinfo = b->d_ovf_job.as<uint64_t>();
+    S.fmean = b->d_ovf_fm.as<uint32_t>();
+    // both parts append to one job list (own job / length counters of the overflow; the kept
+    // counter stays shared); the chains start when both parts are grouped
+    A2.ovf = b->d_ovf2.as<OvfEntry>();
+    A2.ctr = ctr_d + 8;
+    A2.jobs = b->d_jobs2.as<Job>();
+    A2.lens = b->d_lens.as<uint32_t>();
+    A3.ovf = A2.ovf;
+    A3.ctr = A2.ctr;
+    A3.jobs = A2.jobs;
+    A3.lens = A2.lens;
+    const uint32_t inline_min = (uint32_t)b->tune.ovf_inline_min;
+    const int prio = b->tune.inline_prio;
+    SKM_HIP(hipEventRecord(b->ev_o[0], st2));
+    SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
+    HeavyArgs H;
+    H.keys = b->d_hv_keys.as<HeavyKey>();
+    H.nkeys = ctr_d + 18;  // cleared with the pass's counters
+    H.cursor = ctr_d + 19;
+    H.hi = b->d_hv_hi.as<uint64_t>();
+    H.lo = b->d_hv_lo.as<uint64_t>();
+    H.s0 = b->d_hv_s0.as<uint32_t>();
+    H.s1 = b->d_hv_s1.as<uint32_t>();
+    // giant chains: samples and jobs in this pass's own buffers, run on a rotating chain stream
+    // (only in the last giant_passes passes: earlier passes' long chains overlap the later passes
+    // from the stash batches anyway; the last pass's would form the tail)
+    const int gs = (int)(pass % skm_build::GSLOTS);
+    const uint32_t NP = 1u << b->pass_bits;
+    const bool late = b->tune.giant_passes <= 0 || pass + (uint32_t)b->tune.giant_passes >= NP;
+    H.giant_min = b->tune.giant_class > 0 && late && pass < b->gsamples.size() ? 1u << b->tune.giant_class : 0u;
+    H.gsamples = nullptr;
+    H.gjobs = nullptr;
+    H.gcount = nullptr;
+    H.gcap = 0;
+    H.gstat = nullptr;
+    if (H.giant_min) {
+        SKM_HIP(hipMemsetAsync(b->gcount[pass].p, 0, 16, st2));
+        H.gsamples = b->gsamples[pass].as<uint32_t>();
+        H.gjobs = b->gjobs[pass].as<Job>();
+        H.gcount = b->gcount[pass].as<unsigned long long>();
+        H.gcap = b->split_cap;
+        H.gstat = b->d_gstat.as<unsigned long long>();
     }
-    b->n_ovf_heavy = nheavy;
-    T(2);
+    hipLaunchKernelGGL(k_ovf_split, dim3(SPLIT_GRID), dim3(BP_THREADS), 0, st2, A2, S, H, key_min, plan_d);
+    SKM_HIP(hipEventRecord(b->ev_split, st2));
+    SKM_HIP(hipStreamWaitEvent(st3, b->ev_split, 0));
+    hipLaunchKernelGGL(k_heavy, dim3(HEAVY_GRID), dim3(HEAVY_WG), 0, st2, A2, H);
+    SKM_HIP(hipGetLastError());
+    if (H.giant_min) {
+        SKM_HIP(hipEventRecord(b->gev_ready[gs], st2));
+        SKM_HIP(hipStreamWaitEvent(b->gst[gs], b->gev_ready[gs], 0));
+        hipLaunchKernelGGL(k_chain_dyn, dim3(1024), dim3(128), 0, b->gst[gs], H.gjobs, H.gcount, A.out_data,
+                           b->tune.chain_prio);
+        SKM_HIP(hipGetLastError());
+        SKM_HIP(hipEventRecord(b->gev_done[gs], b->gst[gs]));
+        b->gused[gs] = true;
+    }
+    hipLaunchKernelGGL(k_overflow, dim3(OVF_GRID), dim3(BP_THREADS), 0, st2, A2, S, plan_d, -1, (int)PLAN_NHEAVY,
+                       (int)PLAN_Q_HEAVY, inline_min, prio);
+    SKM_HIP(hipEventRecord(b->ev_o[1], st2));
+    hipLaunchKernelGGL(k_overflow, dim3(OVF_GRID), dim3(BP_THREADS), 0, st3, A3, S, plan_d, (int)PLAN_NHEAVY,
+                       (int)PLAN_NOVF, (int)PLAN_Q_REST, inline_min, prio);
+    SKM_HIP(hipGetLastError());
     // ---- 4b. group-by of the sub-buckets that fit LDS; groups of > 64 members are handed to
     //      k_big_groups (one wave each) and appended ----
-    b->big_cap = b->n_local / 65 + 64;
-    b->d_big_desc.ensure(16 * b->big_cap);
-    b->d_big_out.ensure(sizeof(BigOut) * b->big_cap);
-    A.big_desc = b->d_big_desc.as<uint64_t>();
-    A.big_cap = (uint32_t)std::min<uint64_t>(b->big_cap, 0xFFFFFFFFull);
     BigArgs BA;
     BA.desc = A.big_desc;
     BA.ndesc = ctr_d + 5;
@@ -4662,7 +4907,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     SKM_HIP(hipEventRecord(b->ev[5], st));
     // the next pass's compaction + count overlap this pass's group-by on stx: its buffer set was
     // last read by this pass's predecessor's extract, complete once this pass's partition is
-    if (b->pass_bits && pass + 1 < (1u << b->pass_bits) && b->tune.prefetch) {
+    if (b->pass_bits && pass + 1 < NP && b->tune.prefetch) {
         SKM_HIP(hipStreamWaitEvent(b->stx, b->ev_pf_ready, 0));
         prefetch_pass(b, pass + 1, b->stx);
     }
@@ -4671,62 +4916,91 @@ void phase_group(skm_build* b, uint32_t pass) {
     hipLaunchKernelGGL(k_big_append, dim3(256), dim3(BIG_WG), 0, st, BA.out, BA, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[12], st));
-    T(3);
-    // ---- 6. deferred P^2 / variance chains: the overflow's as soon as both parts are grouped;
-    //      the long ones (a wave pair each) on stream 2, the per-lane ones on stream 3 ----
-    b->n_jobs = b->n_lens = 0;
-    b->ovf_kept = 0;
-    if (!novf) b->ovf_elems = 0;
-    if (novf) {
-        SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
-        SKM_HIP(hipStreamWaitEvent(st2, b->ev_o3[0], 0));
-        SKM_HIP(hipMemcpyAsync(ctr + 32, ctr_d + 8, 8 * 5, hipMemcpyDeviceToHost, st2));
-        SKM_HIP(hipStreamSynchronize(st2));
-        SKM_CHECK(ctr[32 + 3] <= b->jobs2_cap && ctr[32 + 4] <= b->lens_cap, SKM_E_OOM,
-                  "overflow chain buffers overflowed");
-        launch_chains(b, 2 * pass + 1, st2, A2.jobs, ctr[32 + 3], b->cs_ovf, A2.lens, nullptr, nullptr, nullptr,
-                      A.out_data, (uint32_t)b->tune.ovf_long_class, ctr + 21, st3, b->ev_o3[2],
-                      (uint32_t)b->tune.ovf_chain_wgs);
-        SKM_HIP(hipEventRecord(b->ev_o[2], st2));
-        SKM_HIP(hipEventRecord(b->ev_o3[1], st3));
-        b->n_jobs += ctr[32 + 3];
-        b->ovf_kept = ctr[32 + 0];
-        b->n_lens += ctr[32 + 4];
-    }
-    T(4);
-    SKM_HIP(hipMemcpyAsync(ctr, ctr_d, 8 * 7, hipMemcpyDeviceToHost, st));
-    SKM_HIP(hipStreamSynchronize(st));
-    SKM_CHECK(ctr[3] <= b->jobs_cap, SKM_E_OOM, "chain buffers overflowed");
-    SKM_CHECK(ctr[5] <= b->big_cap, SKM_E_OOM, "big-group descriptor capacity exceeded");
-    b->n_big = ctr[5];
-    b->big_kept = ctr[6];
-    launch_chains(b, 2 * pass, st, A.jobs, ctr[3], b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
-                  reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, (uint32_t)b->tune.main_long_class,
-                  ctr + 20);
-    b->n_jobs += ctr[3];
-    if (novf) {
-        SKM_HIP(hipStreamWaitEvent(st, b->ev_o[2], 0));
-        SKM_HIP(hipStreamWaitEvent(st, b->ev_o3[1], 0));
-    }
+    // ---- 6. deferred P^2 / variance chains: the overflow's as soon as both parts are grouped
+    //      (the long ones on stream 2, the per-lane ones on stream 3), the group-by's on st ----
+    SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
+    SKM_HIP(hipStreamWaitEvent(st2, b->ev_o3[0], 0));
+    launch_chains(b, st2, A2.jobs, ctr_d + 8 + 3, b->jobs2_cap, b->cs_ovf, A2.lens, nullptr, nullptr, nullptr,
+                  A.out_data, (uint32_t)b->tune.ovf_long_class, st3, b->ev_o3[2], (uint32_t)b->tune.ovf_chain_wgs);
+    SKM_HIP(hipEventRecord(b->ev_o[2], st2));
+    SKM_HIP(hipEventRecord(b->ev_o3[1], st3));
+    launch_chains(b, st, A.jobs, ctr_d + 3, b->jobs_cap, b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
+                  reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, (uint32_t)b->tune.main_long_class);
+    SKM_HIP(hipStreamWaitEvent(st, b->ev_o[2], 0));
+    SKM_HIP(hipStreamWaitEvent(st, b->ev_o3[1], 0));
     SKM_HIP(hipEventRecord(b->ev[6], st));
+    // ---- 7. run totals and the chain lists' bounds ----
+    hipLaunchKernelGGL(k_pass_account, dim3(1), dim3(1), 0, st, ctr_d, run_d, b->jobs_cap, b->jobs2_cap, b->big_cap,
+                       b->lens_cap);
+    SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[7], st));
-    T(5);
-    // ---- 7. the arena cursor after this pass ----
-    SKM_HIP(hipMemcpyAsync(ctr + 17, ctr_d, 8, hipMemcpyDeviceToHost, st));
-    SKM_HIP(hipStreamSynchronize(st));
-    b->n_kept = ctr[17];
-    T(6);
-    if (host_timing)
-        fprintf(stderr, "host ms: part %.3f ovf-read %.3f launches %.3f ovf-chains %.3f main-chains %.3f stats %.3f end %.3f\n",
-                tm[0], tm[1], tm[2], tm[3], tm[4], tm[5], tm[6]);
-#undef T
 }
 
-// run start: arena cursor, signature flags, accumulators; the pass ids (one residue scan)
+// Work buffers whose size depends on the data (the overflow scratch, the split path, the chain
+// lists, the stashed long chains, the giant slots): sized from the capacities before the run, so
+// the passes need no host decisions.  A run that outgrows one records its demand; run_ranks grows
+// the capacities and redoes the step (the first run on a new input at most).
+void alloc_caps(skm_build* b) {
+    const uint64_t T = std::max<uint64_t>(b->tot_cap, 1), Sp = std::max<uint64_t>(b->split_cap, 1);
+    b->d_ovf_hi.ensure(8 * T);
+    b->d_ovf_lo.ensure(8 * T);
+    b->d_ovf_heads.ensure(4 * T);
+    b->d_ovf_job.ensure(8 * T);
+    b->d_ovf_fm.ensure(4 * T);
+    b->jobs2_cap = T / 3 + 16;  // a job has >= 3 members
+    b->d_jobs2.ensure(sizeof(Job) * b->jobs2_cap);
+    const uint32_t key_min = (uint32_t)std::max(b->tune.heavy_min, 2);
+    b->d_hv_keys.ensure(sizeof(HeavyKey) * (Sp / key_min + 16));
+    b->d_hv_hi.ensure(8 * Sp);
+    b->d_hv_lo.ensure(8 * Sp);
+    b->d_hv_s0.ensure(4 * Sp);
+    b->d_hv_s1.ensure(4 * Sp);
+    b->d_ovf2.ensure(sizeof(OvfEntry) * std::max<uint64_t>(b->ovf_cap, 1));
+    b->d_plan.ensure(4 * PLAN_SLOTS);
+    b->d_run.ensure(8 * RUN_SLOTS);
+    b->d_sub_tab.ensure(4ull * (1u << b->b1_bits) * SUB_TAB);
+    b->d_stamps.ensure(32 * 8);
+    // job sort scratch; the long jobs (>= 2^class samples each) bound the plan offsets
+    const int cls = std::max(1, std::min(b->tune.main_long_class, b->tune.ovf_long_class));
+    struct {
+        ChainSet* cs;
+        uint64_t cap, elems;
+    } sets[2] = {{&b->cs_main, b->jobs_cap, b->cap_local}, {&b->cs_ovf, b->jobs2_cap, T}};
+    for (auto& c : sets) {
+        c.cs->hist.ensure(4ull * JOB_NWG * JOB_CLASSES);
+        c.cs->offs.ensure(8ull * JOB_NWG * JOB_CLASSES + 16);
+        c.cs->sorted.ensure(sizeof(Job) * c.cap);
+        c.cs->long_off.ensure(8ull * (std::min(c.cap, (c.elems >> cls) + 16) + 8));
+    }
+    if (b->pass_bits) {
+        // every long job has >= 2^class distinct samples of this shard's elements (received ones:
+        // bounded by the world's)
+        b->long_jobs_cap = std::max<uint64_t>(b->long_jobs_cap, b->world * (b->valid_total >> cls) + 4096);
+        b->d_long_jobs.ensure(sizeof(Job) * b->long_jobs_cap);
+        b->d_long_arena.ensure(4 * std::max<uint64_t>(b->long_cap, 1));
+    }
+    const uint32_t NP = 1u << b->pass_bits;
+    if (b->tune.giant_class > 0) {
+        while (b->gsamples.size() < NP) {
+            b->gsamples.emplace_back();
+            b->gjobs.emplace_back();
+            b->gcount.emplace_back();
+        }
+        for (uint32_t p = 0; p < NP; ++p) {
+            b->gsamples[p].ensure(4 * Sp);
+            b->gjobs[p].ensure(sizeof(Job) * (Sp / (1u << b->tune.giant_class) + 16));
+            b->gcount[p].ensure(16);
+        }
+    }
+}
+
+// run start: arena cursor, signature flags, run slots; the pass ids (one residue scan)
 void begin_run(skm_build* b) {
     hipStream_t st = b->stream;
+    alloc_caps(b);
     SKM_HIP(hipEventRecord(b->ev_start, st));
     SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 256, st));
+    SKM_HIP(hipMemsetAsync(b->d_run.p, 0, 8 * RUN_SLOTS, st));
     SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->n_total ? b->n_total : 1, st));
     b->d_gstat.ensure(16);
     SKM_HIP(hipMemsetAsync(b->d_gstat.p, 0, 16, st));
@@ -4736,59 +5010,56 @@ void begin_run(skm_build* b) {
     SKM_HIP(hipGetLastError());
     b->acc = skm_build::Acc{};
     std::memset(b->pass_ms, 0, sizeof(b->pass_ms));
-    b->n_long = b->long_samples = b->long_launched = 0;
-    if (b->pass_bits) {  // every long job has >= 2^class distinct samples of this shard's elements
-        const int cls = std::min(b->tune.main_long_class, b->tune.ovf_long_class);
-        const uint64_t cap = b->world * (b->valid_total >> cls) + 4096;  // received elements: bounded by the world's
-        if (cap > b->long_jobs_cap) {
-            b->d_long_jobs.ensure(sizeof(Job) * cap);
-            b->long_jobs_cap = cap;
-        }
-    }
+    for (bool& g : b->gused) g = false;
     b->n_kept = 0;
 }
 
-// after a pass's group phase (its events have completed): totals and phase times
-void end_pass(skm_build* b) {
-    auto& a = b->acc;
-    a.novf += b->n_overflow;
-    a.jobs += b->n_jobs;
-    a.lens += b->n_lens;
-    a.ovf_elems += b->ovf_elems;
-    a.ovf_kept += b->ovf_kept;
-    a.big += b->n_big;
-    a.big_kept += b->big_kept;
-    a.grouped += b->n_local;
+// the pass's timing events (one set per pass: read once, after the step's single host sync)
+void use_evset(skm_build* b, uint32_t pass) {
+    while (b->evsets.size() <= pass) {
+        b->evsets.emplace_back();
+        skm_build::EvSet& e = b->evsets.back();
+        for (auto& x : e.ev) SKM_HIP(hipEventCreate(&x));
+        for (auto& x : e.o) SKM_HIP(hipEventCreate(&x));
+        for (auto& x : e.o3) SKM_HIP(hipEventCreate(&x));
+    }
+    b->ev = b->evsets[pass].ev;
+    b->ev_o = b->evsets[pass].o;
+    b->ev_o3 = b->evsets[pass].o3;
+}
+
+// after the step's sync: phase times of every pass
+void pass_times(skm_build* b, uint32_t npass) {
     // [0] extract-count [1] scan [2] extract-scatter [3] bucket [5] chains [8] exchange
     // [9] partition [10] group-by kernel [11] big groups; [4] overflow (own streams)
     const int idx[9] = {0, 1, 2, 3, 5, 8, 9, 10, 11};
     const int from[9] = {0, 1, 2, 4, 12, 3, 4, 11, 5}, to[9] = {1, 2, 3, 12, 6, 4, 10, 5, 12};
-    for (int i = 0; i < 9; ++i) {
-        float t = 0.f;
-        SKM_HIP(hipEventElapsedTime(&t, b->ev[from[i]], b->ev[to[i]]));
-        b->pass_ms[idx[i]] += t;
-    }
-    if (b->n_overflow) {  // the overflow path end to end (both parts, their chains included)
-        float t2 = 0.f, t3 = 0.f;
-        SKM_HIP(hipEventElapsedTime(&t2, b->ev_o[0], b->ev_o[2]));
-        SKM_HIP(hipEventElapsedTime(&t3, b->ev_o[0], b->ev_o3[1]));
+    for (uint32_t p = 0; p < npass && p < b->evsets.size(); ++p) {
+        const skm_build::EvSet& e = b->evsets[p];
+        for (int i = 0; i < 9; ++i) {
+            float t = 0.f;
+            SKM_HIP(hipEventElapsedTime(&t, e.ev[from[i]], e.ev[to[i]]));
+            b->pass_ms[idx[i]] += t;
+        }
+        float t2 = 0.f, t3 = 0.f;  // the overflow path end to end (both parts, their chains included)
+        SKM_HIP(hipEventElapsedTime(&t2, e.o[0], e.o[2]));
+        SKM_HIP(hipEventElapsedTime(&t3, e.o[0], e.o3[1]));
         b->pass_ms[4] += std::max(t2, t3);
     }
 }
 
 // key-range passes: run the stashed long chains not yet launched, as one batch on the chain
-// stream, after the stashes on st / stream2 (both already ordered before this host call)
-void flush_long_chains(skm_build* b) {
-    if (b->n_long <= b->long_launched) return;
+// stream.  The batch's job range is taken on st (k_long_snap), in stream order after the passes so
+// far -- whose overflow stashes st already waited for -- and before the next pass reserves more.
+void flush_long_chains(skm_build* b, int slot) {
+    unsigned long long* run_d = b->d_run.as<unsigned long long>();
+    unsigned long long* rng = run_d + RUN_SNAP + 2 * slot;
+    hipLaunchKernelGGL(k_long_snap, dim3(1), dim3(1), 0, b->stream, run_d, rng);
     SKM_HIP(hipEventRecord(b->chain_ev[0], b->stream));
-    SKM_HIP(hipEventRecord(b->chain_ev[1], b->stream2));
     SKM_HIP(hipStreamWaitEvent(b->chain_st, b->chain_ev[0], 0));
-    SKM_HIP(hipStreamWaitEvent(b->chain_st, b->chain_ev[1], 0));
-    const uint64_t n = b->n_long - b->long_launched;
-    hipLaunchKernelGGL(k_chain_long, dim3((uint32_t)n), dim3(128), 0, b->chain_st, b->d_long_jobs.as<Job>() + b->long_launched,
-                       n, nullptr, nullptr, nullptr, nullptr, b->d_data.as<skm_stored_kmer_data>(), b->tune.chain_prio);
+    hipLaunchKernelGGL(k_chain_long, dim3(LONG_GRID), dim3(128), 0, b->chain_st, b->d_long_jobs.as<Job>(), rng, rng + 1,
+                       nullptr, nullptr, nullptr, nullptr, b->d_data.as<skm_stored_kmer_data>(), b->tune.chain_prio);
     SKM_HIP(hipGetLastError());
-    b->long_launched = b->n_long;
 }
 
 // per-rank statistics over the whole arena (distinct_functions) and the shard (seqs_with_func)
@@ -4796,7 +5067,7 @@ void phase_stats(skm_build* b) {
     hipStream_t st = b->stream;
     const uint32_t F = b->opts.n_functions;
     if (b->pass_bits) {  // the long chains of every pass
-        flush_long_chains(b);
+        flush_long_chains(b, 1);
         SKM_HIP(hipEventRecord(b->chain_ev[2], b->chain_st));
         SKM_HIP(hipStreamWaitEvent(st, b->chain_ev[2], 0));
     }
@@ -4806,55 +5077,79 @@ void phase_stats(skm_build* b) {
     SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     const size_t lds_f = F <= 16384 ? sizeof(uint32_t) * F : 0;
-    if (b->n_kept)
-        hipLaunchKernelGGL(k_kept_finalize, dim3(2048), dim3(256), lds_f, st, b->d_keys.as<uint64_t>(),
-                           b->d_data.as<skm_stored_kmer_data>(),
-                           b->n_kept, F, b->d_dfunc.as<uint32_t>());
+    hipLaunchKernelGGL(k_kept_finalize, dim3(2048), dim3(256), lds_f, st, b->d_keys.as<uint64_t>(),
+                       b->d_data.as<skm_stored_kmer_data>(), b->d_ctr.as<unsigned long long>(), F,
+                       b->d_dfunc.as<uint32_t>());
     if (b->nseq)
         hipLaunchKernelGGL(k_func_hist_seqs, dim3(256), dim3(256), lds_f, st, b->d_meta.as<SeqMeta>(), b->nseq, F,
                            b->d_swf.as<uint32_t>());
     SKM_HIP(hipGetLastError());
 }
 
+// the step's one host synchronisation: counters, run slots and timings come back together
 void phase_final(skm_build* b) {
     hipStream_t st = b->stream;
     hipLaunchKernelGGL(k_count_flags, dim3(256), dim3(256), 0, st, b->d_flags.as<uint8_t>(), b->n_total,
                        b->d_ctr.as<unsigned long long>() + 2);
     SKM_HIP(hipGetLastError());
-    {
-        unsigned long long* pin = b->pinned_ctr();
-        SKM_HIP(hipMemcpyAsync(pin + 48, b->d_gstat.p, 16, hipMemcpyDeviceToHost, st));
-    }
+    unsigned long long* pin = b->pinned_ctr();
+    SKM_HIP(hipMemcpyAsync(pin + 48, b->d_gstat.p, 16, hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipMemcpyAsync(pin + 56, b->d_ctr.p, 8, hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipMemcpyAsync(pin + 64, b->d_run.p, 8 * RUN_SLOTS, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipEventRecord(b->ev[8], st));
     SKM_HIP(hipEventSynchronize(b->ev[8]));
-    b->giant_jobs = b->pinned_ctr()[48];
-    b->giant_max = b->pinned_ctr()[49];
+    const unsigned long long* R = pin + 64;
+    b->giant_jobs = pin[48];
+    b->giant_max = pin[49];
+    b->n_kept = pin[56];
+    b->run_flags = R[RUN_FLAGS];
+    for (int i = 0; i < 4; ++i) b->demand[i] = R[RUN_DEM_TOT + i];
+    // the long arena's cursors count every reservation, the ones that did not fit included
+    b->demand[2] = std::max<uint64_t>(b->demand[2], R[RUN_LONG_CUR]);
+    b->demand[3] = std::max<uint64_t>(b->demand[3], R[RUN_LONG_N]);
+    pass_times(b, 1u << b->pass_bits);
     for (int i = 0; i < 12; ++i) b->last_ms[i] = b->pass_ms[i];
     SKM_HIP(hipEventElapsedTime(&b->last_ms[6], b->ev[7], b->ev[8]));      // stats (+ reductions)
     SKM_HIP(hipEventElapsedTime(&b->last_ms[7], b->ev_start, b->ev[8]));   // whole run
     // run totals for counters() / finish()
-    b->n_overflow = (uint32_t)b->acc.novf;
-    b->n_jobs = b->acc.jobs;
-    b->n_lens = b->acc.lens;
-    b->ovf_elems = b->acc.ovf_elems;
-    b->ovf_kept = b->acc.ovf_kept;
-    b->n_big = b->acc.big;
-    b->big_kept = b->acc.big_kept;
-    b->n_local = b->acc.grouped;
+    b->n_overflow = (uint32_t)R[RUN_ACC_NOVF];
+    b->n_overflow_last = (uint32_t)R[RUN_LAST_NOVF];
+    b->n_jobs = R[RUN_ACC_JOBS];
+    b->n_jobs_last = R[RUN_LAST_JOBS];
+    b->n_lens = R[RUN_ACC_LENS];
+    b->ovf_elems = R[RUN_ACC_OVF_ELEMS];
+    b->ovf_kept = R[RUN_ACC_OVF_KEPT];
+    b->n_big = R[RUN_ACC_BIG];
+    b->big_kept = R[RUN_ACC_BIG_KEPT];
+    b->n_local = R[RUN_ACC_GROUPED];
     b->ran = true;
 }
 
-void run_ranks(const Ranks& bs) {
-    prepare(bs);
+// a redo: capacities grown to the recorded demands (with slack), buffers reallocated
+void grow_caps(skm_build* b) {
+    auto grow = [](uint64_t& cap, uint64_t dem) {
+        if (dem > cap) cap = dem + dem / 8 + 1024;
+    };
+    grow(b->tot_cap, b->demand[0]);
+    grow(b->split_cap, b->demand[1]);
+    grow(b->long_cap, b->demand[2]);
+    grow(b->long_jobs_cap, b->demand[3]);
+    SKM_HIP(hipDeviceSynchronize());
+    alloc_caps(b);
+}
+
+void run_once(const Ranks& bs) {
     for (auto* b : bs) begin_run(b);
     const uint32_t P = 1u << bs[0]->pass_bits;
     for (uint32_t pass = 0; pass < P; ++pass) {
-        for (auto* b : bs) phase_extract(b, pass);
+        for (auto* b : bs) {
+            use_evset(b, pass);
+            phase_extract(b, pass);
+        }
         if (bs[0]->world > 1) exchange(bs);
         for (auto* b : bs) {
             phase_group(b, pass);
-            end_pass(b);
-            if (P >= 4 && pass + 1 == P / 2) flush_long_chains(b);  // first half's chains overlap the second half
+            if (P >= 4 && pass + 1 == P / 2) flush_long_chains(b, 0);  // first half's chains overlap the second half
         }
     }
     for (auto* b : bs) phase_stats(b);
@@ -4871,6 +5166,29 @@ void run_ranks(const Ranks& bs) {
         allreduce(bs, fl, bs[0]->n_total, Red::MaxU8);
     }
     for (auto* b : bs) phase_final(b);
+}
+
+void run_ranks(const Ranks& bs) {
+    prepare(bs);
+    for (int attempt = 0;; ++attempt) {
+        run_once(bs);
+        std::vector<uint64_t> mine;
+        for (auto* b : bs) mine.push_back((b->run_flags & RUN_F_RERUN) ? 1u : 0u);
+        const std::vector<uint64_t> all = bs[0]->world > 1 ? allgather_u64(bs, mine) : mine;
+        bool redo = false;
+        for (auto v : all) redo |= v != 0;
+        if (!redo) break;
+        SKM_CHECK(attempt < 3, SKM_E_STATE, "build work buffers did not converge");
+        for (auto* b : bs) {
+            grow_caps(b);
+            ++b->n_redo;
+        }
+    }
+    for (auto* b : bs) {
+        SKM_CHECK(!(b->run_flags & RUN_F_ARENA), SKM_E_OOM,
+                  "kept k-mer arena exhausted (raise the device memory budget or the key-range passes)");
+        SKM_CHECK(!(b->run_flags & RUN_F_CAP), SKM_E_STATE, "build work list capacity exceeded");
+    }
 }
 
 Ranks ranks_of(skm_build* b) {
@@ -4913,7 +5231,7 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     SKM_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
     SKM_HIP(hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking));
     SKM_HIP(hipStreamCreateWithFlags(&b->stream3, hipStreamNonBlocking));
-    for (auto& e : b->ev) SKM_HIP(hipEventCreate(&e));
+    use_evset(b, 0);
     SKM_HIP(hipEventCreate(&b->ev_start));
     SKM_HIP(hipStreamCreateWithFlags(&b->chain_st, hipStreamNonBlocking));
     SKM_HIP(hipStreamCreateWithFlags(&b->stx, hipStreamNonBlocking));
@@ -4931,8 +5249,6 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
         SKM_HIP(hipEventCreateWithFlags(&b->st_ev[i], hipEventDisableTiming));
     }
     SKM_HIP(hipEventCreateWithFlags(&b->ev_split, hipEventDisableTiming));
-    for (auto& e : b->ev_o) SKM_HIP(hipEventCreate(&e));
-    for (auto& e : b->ev_o3) SKM_HIP(hipEventCreate(&e));
     set_geometry(b);
     *out = b;
     SKM_API_END
@@ -5189,26 +5505,31 @@ int skm_build_debug_stamps(skm_build* b, int enable, uint64_t* out, int cap) {
     SKM_API_END
 }
 
-// Diagnostics: lengths of the first `cap` chain jobs in execution order (longest class first).
+// Diagnostics: lengths of the first `cap` chain jobs of the last pass in execution order (longest
+// class first; the overflow's, the longest, when the pass had an overflow).
 int skm_build_debug_jobs(skm_build* b, uint32_t* out, int cap) {
     SKM_API_BEGIN
     SKM_CHECK(b && out, SKM_E_ARG, "null argument");
-    const uint64_t n = std::min<uint64_t>((uint64_t)cap, b->n_jobs);
+    SKM_HIP(hipDeviceSynchronize());
+    const uint64_t n = std::min<uint64_t>((uint64_t)cap, b->n_jobs_last);
     std::vector<Job> j(n);
-    const uint64_t n2 = std::min<uint64_t>(n, b->cs_ovf.sorted.bytes / sizeof(Job));
-    if (b->n_overflow && n2) {  // the overflow's chains (the longest) first
-        SKM_HIP(hipMemcpy(j.data(), b->cs_ovf.sorted.p, sizeof(Job) * n2, hipMemcpyDeviceToHost));
-    } else if (n) {
-        SKM_HIP(hipMemcpy(j.data(), b->cs_main.sorted.p, sizeof(Job) * n, hipMemcpyDeviceToHost));
-    }
-    for (uint64_t i = 0; i < (uint64_t)cap; ++i) out[i] = i < n ? j[i].n : 0u;
+    const bool ovf = b->n_overflow_last && b->cs_ovf.sorted.p;
+    const DevBuf& src = ovf ? b->cs_ovf.sorted : b->cs_main.sorted;
+    const uint64_t m = std::min<uint64_t>(n, src.bytes / sizeof(Job));
+    if (m) SKM_HIP(hipMemcpy(j.data(), src.p, sizeof(Job) * m, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < (uint64_t)cap; ++i) out[i] = i < m ? j[i].n : 0u;
     SKM_API_END
 }
 
+// Diagnostics: element counts of the last pass's overflow sub-buckets as k_partition listed them
+// (before k_ovf_split takes the heavy keys out); returns how many there were.
 int skm_build_debug_overflow(skm_build* b, uint32_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
-    const uint32_t n = b->h_ovf ? std::min<uint32_t>(b->n_overflow_last, (uint32_t)b->h_ovf_cap) : 0u;
-    for (int i = 0; i < cap; ++i) out[i] = (uint32_t)i < n ? b->h_ovf[i].n : 0u;
+    if (hipSetDevice(b->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return SKM_E_HIP;
+    const uint32_t n = b->d_ovf.p ? (uint32_t)std::min<uint64_t>(b->n_overflow_last, b->d_ovf.bytes / sizeof(OvfEntry)) : 0u;
+    std::vector<OvfEntry> e(n);
+    if (n && hipMemcpy(e.data(), b->d_ovf.p, sizeof(OvfEntry) * n, hipMemcpyDeviceToHost) != hipSuccess) return SKM_E_HIP;
+    for (int i = 0; i < cap; ++i) out[i] = (uint32_t)i < n ? e[i].n : 0u;
     return (int)n;
 }
 
@@ -5230,6 +5551,10 @@ int skm_debug_chain_bench(uint32_t n, uint32_t njobs, int mode, float* ms) {
     dout.ensure(std::max(sizeof(skm_stored_kmer_data), sizeof(double)) * njobs);
     SKM_HIP(hipMemcpy(dl.p, lens.data(), 4 * lens.size(), hipMemcpyHostToDevice));
     SKM_HIP(hipMemcpy(dj.p, jobs.data(), sizeof(Job) * njobs, hipMemcpyHostToDevice));
+    DevBuf dn;  // the job count, as the chain kernels read it
+    dn.ensure(8);
+    const unsigned long long nj64 = njobs;
+    SKM_HIP(hipMemcpy(dn.p, &nj64, 8, hipMemcpyHostToDevice));
     hipEvent_t e0, e1;
     SKM_HIP(hipEventCreate(&e0));
     SKM_HIP(hipEventCreate(&e1));
@@ -5240,13 +5565,13 @@ int skm_debug_chain_bench(uint32_t n, uint32_t njobs, int mode, float* ms) {
             hipLaunchKernelGGL(k_chain_long_half, dim3(njobs), dim3(64), 0, 0, dj.as<Job>(), dl.as<uint32_t>(),
                                mode - 3, reinterpret_cast<double*>(dout.p));
         else if (mode == 2 || (mode == 0 && n >= (1u << LONG_CLASS)))
-            hipLaunchKernelGGL(k_chain_long, dim3(njobs), dim3(128), 0, 0, dj.as<Job>(), (uint64_t)njobs,
+            hipLaunchKernelGGL(k_chain_long, dim3(njobs), dim3(128), 0, 0, dj.as<Job>(), nullptr, dn.as<unsigned long long>(),
                                dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(),
                                dout.as<skm_stored_kmer_data>(), 0);
         else
-        hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, 0, dj.as<Job>(),
-                           (uint64_t)njobs, dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(), dl.as<uint32_t>(),
-                           dout.as<skm_stored_kmer_data>());
+            hipLaunchKernelGGL(k_chains, dim3((uint32_t)ceil_div(threads, 256)), dim3(256), 0, 0, dj.as<Job>(), nullptr,
+                               dn.as<unsigned long long>(), (uint64_t)njobs, dl.as<uint32_t>(), dl.as<uint32_t>(),
+                               dl.as<uint32_t>(), dl.as<uint32_t>(), dout.as<skm_stored_kmer_data>());
         SKM_HIP(hipEventRecord(e1, 0));
         SKM_HIP(hipEventSynchronize(e1));
         SKM_HIP(hipEventElapsedTime(ms, e0, e1));
@@ -5289,10 +5614,11 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
-    const uint64_t v[15] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+    const uint64_t v[24] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
                             b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total,
-                            b->giant_jobs, b->giant_max};
-    int n = std::min(cap, 15);
+                            b->giant_jobs, b->giant_max, b->n_redo, b->tot_cap, b->split_cap, b->long_cap,
+                            b->long_jobs_cap, b->demand[0], b->demand[1], b->demand[2], b->demand[3]};
+    int n = std::min(cap, 24);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }
@@ -5450,12 +5776,15 @@ void skm_build_destroy(skm_build* b) {
         if (x != b) x->group.clear();
     if (b->stream2) (void)hipStreamSynchronize(b->stream2);
     if (b->stream3) (void)hipStreamSynchronize(b->stream3);
-    for (auto& e : b->ev)
-        if (e) (void)hipEventDestroy(e);
-    for (auto& e : b->ev_o)
-        if (e) (void)hipEventDestroy(e);
-    for (auto& e : b->ev_o3)
-        if (e) (void)hipEventDestroy(e);
+    if (b->chain_st) (void)hipStreamSynchronize(b->chain_st);
+    for (auto& set : b->evsets) {
+        for (auto& e : set.ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& e : set.o)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& e : set.o3)
+            if (e) (void)hipEventDestroy(e);
+    }
     if (b->ev_part) (void)hipEventDestroy(b->ev_part);
     for (int i = 0; i < 2; ++i) {
         if (b->st_busy[i] && b->st_ev[i]) (void)hipEventSynchronize(b->st_ev[i]);
