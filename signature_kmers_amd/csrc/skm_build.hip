@@ -3760,6 +3760,9 @@ struct Tune {
     int giant_class = 0;
     int giant_passes = 0;            // giant chains only in the last N passes (0: all)
     int prefetch = 1;                // next pass's compaction + count during this pass's group-by
+    int ovf_grid = 1024;             // persistent grids: k_overflow (per stream),
+    int split_grid = 512;            //   k_ovf_split,
+    int chain_grid = 4096;           //   k_chains
 };
 
 }  // namespace skm
@@ -4685,10 +4688,7 @@ void exchange(const Ranks& bs) {
 // per-lane chains run on st (or st_short) within the pass.  Fixed grids that read the counts on
 // the device: no host round trip.
 constexpr uint32_t JOB_NWG = 256;      // k_job_count / k_job_scatter workgroups (one chunk each)
-constexpr uint32_t CHAIN_GRID = 4096;  // k_chains workgroups (two wave pairs each, grid-stride)
 constexpr uint32_t LONG_GRID = 2048;   // k_chain_long / k_long_stash workgroups (one job at a time)
-constexpr uint32_t SPLIT_GRID = 512;   // k_ovf_split workgroups (work queue)
-constexpr uint32_t OVF_GRID = 1024;    // k_overflow workgroups per stream (work queue)
 
 void launch_chains(skm_build* b, hipStream_t st, const Job* jobs, const unsigned long long* nj_d, uint64_t cap,
                    ChainSet& cs, const uint32_t* lens, const uint32_t* recs32, const uint32_t* tmp32,
@@ -4729,7 +4729,7 @@ void launch_chains(skm_build* b, hipStream_t st, const Job* jobs, const unsigned
         SKM_HIP(hipStreamWaitEvent(st_short, ev_sorted, 0));
         ss = st_short;
     }
-    hipLaunchKernelGGL(k_chains, dim3(max_wgs ? max_wgs : CHAIN_GRID), dim3(256), 0, ss, cs.sorted.as<Job>(), nlong_u,
+    hipLaunchKernelGGL(k_chains, dim3(max_wgs ? max_wgs : (uint32_t)std::max(1, tn.chain_grid)), dim3(256), 0, ss, cs.sorted.as<Job>(), nlong_u,
                        nj_d, cap, lens, recs32, tmp32, big32, out);
     SKM_HIP(hipGetLastError());
 }
@@ -4869,7 +4869,7 @@ void phase_group(skm_build* b, uint32_t pass) {
         H.gcap = b->split_cap;
         H.gstat = b->d_gstat.as<unsigned long long>();
     }
-    hipLaunchKernelGGL(k_ovf_split, dim3(SPLIT_GRID), dim3(BP_THREADS), 0, st2, A2, S, H, key_min, plan_d);
+    hipLaunchKernelGGL(k_ovf_split, dim3((uint32_t)std::max(1, b->tune.split_grid)), dim3(BP_THREADS), 0, st2, A2, S, H, key_min, plan_d);
     SKM_HIP(hipEventRecord(b->ev_split, st2));
     SKM_HIP(hipStreamWaitEvent(st3, b->ev_split, 0));
     hipLaunchKernelGGL(k_heavy, dim3(HEAVY_GRID), dim3(HEAVY_WG), 0, st2, A2, H);
@@ -4883,10 +4883,10 @@ void phase_group(skm_build* b, uint32_t pass) {
         SKM_HIP(hipEventRecord(b->gev_done[gs], b->gst[gs]));
         b->gused[gs] = true;
     }
-    hipLaunchKernelGGL(k_overflow, dim3(OVF_GRID), dim3(BP_THREADS), 0, st2, A2, S, plan_d, -1, (int)PLAN_NHEAVY,
+    hipLaunchKernelGGL(k_overflow, dim3((uint32_t)std::max(1, b->tune.ovf_grid)), dim3(BP_THREADS), 0, st2, A2, S, plan_d, -1, (int)PLAN_NHEAVY,
                        (int)PLAN_Q_HEAVY, inline_min, prio);
     SKM_HIP(hipEventRecord(b->ev_o[1], st2));
-    hipLaunchKernelGGL(k_overflow, dim3(OVF_GRID), dim3(BP_THREADS), 0, st3, A3, S, plan_d, (int)PLAN_NHEAVY,
+    hipLaunchKernelGGL(k_overflow, dim3((uint32_t)std::max(1, b->tune.ovf_grid)), dim3(BP_THREADS), 0, st3, A3, S, plan_d, (int)PLAN_NHEAVY,
                        (int)PLAN_NOVF, (int)PLAN_Q_REST, inline_min, prio);
     SKM_HIP(hipGetLastError());
     // ---- 4b. group-by of the sub-buckets that fit LDS; groups of > 64 members are handed to
@@ -5461,6 +5461,12 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
         SKM_CHECK(value >= 0 && value <= 64 && (value & (value - 1)) == 0, SKM_E_ARG,
                   "key_range_passes must be 0 (automatic) or a power of two <= 64");
         t.passes = (int)value;
+    } else if (n == "work_buffer_elements") {
+        // capacities of the data-sized work buffers (tests: force the grow-and-redo path); 0 = the
+        // automatic first guess
+        SKM_CHECK(value >= 0, SKM_E_ARG, "work_buffer_elements must be >= 0");
+        b->tot_cap = b->split_cap = b->long_cap = (uint64_t)value;
+        b->long_jobs_cap = value ? 1 : 0;
     } else if (n == "device_memory_budget_mb") {
         SKM_CHECK(value >= 0, SKM_E_ARG, "device_memory_budget_mb must be >= 0");
         t.mem_budget_mb = value;
@@ -5479,7 +5485,10 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "split_min" ? &t.split_min
                : n == "giant_class" ? &t.giant_class
                : n == "giant_passes" ? &t.giant_passes
-               : n == "prefetch" ? &t.prefetch : nullptr;
+               : n == "prefetch" ? &t.prefetch
+               : n == "overflow_grid" ? &t.ovf_grid
+               : n == "split_grid" ? &t.split_grid
+               : n == "chain_grid" ? &t.chain_grid : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")

@@ -107,6 +107,36 @@ def test_key_range_passes(skm, gpu, passes, long_class):
     assert c1["overflow_subbuckets"] > 0 and c1["grouped"] == oracle_ref.count_windows(l, f) - _invalid(r, o, l, f)
 
 
+@pytest.mark.parametrize("passes", [0, 4])
+def test_work_buffers_grow_and_redo(skm, gpu, passes):
+    """The data-sized work buffers (overflow scratch, split path, stashed long chains) start far
+    too small: the step runs without a host round trip, records its demands on the device, and is
+    redone with the buffers grown; the result is the oracle's bit for bit, and the next run on the
+    same handle needs no redo."""
+    p = synth.generate_arrays(60000, 60, per_file=2000, seed=6)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    ref = oracle_ref.build(r, o, l, f, i, len(funcs))
+    b = skm.SignatureBuilder(len(funcs))
+    if passes:
+        b.set_option("key_range_passes", passes)
+    b.set_option("main_long_class", 8)
+    b.set_option("overflow_long_class", 8)
+    b.set_option("work_buffer_elements", 64)
+    b.add_batch(r, o, l, f, i)
+    b.run()
+    c1 = b.counters()
+    assert c1["redone"] >= 1, c1
+    assert c1["demand_overflow_scratch"] <= c1["cap_overflow_scratch"]
+    assert c1["demand_split"] <= c1["cap_split"]
+    if passes:
+        assert 0 < c1["demand_long_samples"] <= c1["cap_long_samples"]
+    b.run()
+    assert b.counters()["redone"] == c1["redone"]
+    got = b.finish()
+    b.close()
+    assert_same(got, ref)
+
+
 def _invalid(r, o, l, f):
     ok = np.zeros(256, bool)
     ok[np.frombuffer(b"ACDEFGHIKLMNPQRSTVWYacdefghiklmnpqrstvwy", np.uint8)] = True
