@@ -677,7 +677,7 @@ enum : uint32_t {
     RUN_LONG_CUR = 1,       // stashed long-chain samples (run arena cursor)
     RUN_LONG_N = 2,         // stashed long jobs
     RUN_LONG_FLUSHED = 3,   // long jobs already handed to k_chain_long
-    RUN_SNAP = 4,           // [4..7] two k_long_snap ranges
+    RUN_SNAP = 28,          // [28..61] k_long_snap ranges, one per stashed-chain batch (<= 17)
     RUN_DEM_TOT = 8,        // demands (max over passes): overflow scratch elements,
     RUN_DEM_SPLIT = 9,      //   split-path elements,
     RUN_DEM_LONG = 10,      //   stashed samples,
@@ -693,7 +693,7 @@ enum : uint32_t {
     RUN_LAST_NOVF = 24,     // the last pass's overflow entries and chain jobs (diagnostics)
     RUN_LAST_JOBS = 25,
     RUN_NLOC = 26,          // world > 1: the pass's received element count (host-written)
-    RUN_SLOTS = 32
+    RUN_SLOTS = 64
 };
 constexpr unsigned long long RUN_F_ARENA = 1;  // the kept arena cannot take a pass: SKM_E_OOM
 constexpr unsigned long long RUN_F_RERUN = 2;  // a work buffer was too small: grown to the demand, step redone
@@ -3763,6 +3763,9 @@ struct Tune {
     int ovf_grid = 1024;             // persistent grids: k_overflow (per stream),
     int split_grid = 512;            //   k_ovf_split,
     int chain_grid = 4096;           //   k_chains
+    int stream_prio = 0;             // 1: the group-by stream at the highest priority
+    int chain_batches = 4;           // key-range passes: stashed long chains leave in this many batches
+    int chain_streams = 1;           //   over this many streams (1..4)
 };
 
 }  // namespace skm
@@ -3910,6 +3913,7 @@ struct skm_build {
     hipEvent_t gev_ready[GSLOTS] = {}, gev_done[GSLOTS] = {};
     std::deque<DevBuf> gsamples, gjobs, gcount;   // per key-range pass (reused by the next run)
     bool gused[GSLOTS] = {};
+    bool chain_used[GSLOTS + 1] = {};   // long-chain batches issued on chain_stream(k) this run
     DevBuf d_gstat;                      // run totals: giant chains, longest giant chain
     uint64_t giant_jobs = 0, giant_max = 0;
     DevBuf d_long_arena;                 // stashed samples of the run's long chains
@@ -5011,6 +5015,7 @@ void begin_run(skm_build* b) {
     b->acc = skm_build::Acc{};
     std::memset(b->pass_ms, 0, sizeof(b->pass_ms));
     for (bool& g : b->gused) g = false;
+    for (bool& g : b->chain_used) g = false;
     b->n_kept = 0;
 }
 
@@ -5051,13 +5056,24 @@ void pass_times(skm_build* b, uint32_t npass) {
 // key-range passes: run the stashed long chains not yet launched, as one batch on the chain
 // stream.  The batch's job range is taken on st (k_long_snap), in stream order after the passes so
 // far -- whose overflow stashes st already waited for -- and before the next pass reserves more.
+// Batches go to the chain stream, or rotate over it and the giant-chain streams (chain_streams
+// option).  A batch lasts as long as its longest chain, so on one stream the batches queue behind
+// each other -- which measured better at C3 (four batches: 2.46 s vs 2.50 s rotating over four
+// streams): fewer FP64 chain waves compete with the pass kernels.
+hipStream_t chain_stream(skm_build* b, int slot) {
+    const int k = slot % std::max(1, std::min(b->tune.chain_streams, 1 + skm_build::GSLOTS));
+    return k == 0 ? b->chain_st : b->gst[k - 1];
+}
+
 void flush_long_chains(skm_build* b, int slot) {
     unsigned long long* run_d = b->d_run.as<unsigned long long>();
     unsigned long long* rng = run_d + RUN_SNAP + 2 * slot;
     hipLaunchKernelGGL(k_long_snap, dim3(1), dim3(1), 0, b->stream, run_d, rng);
     SKM_HIP(hipEventRecord(b->chain_ev[0], b->stream));
-    SKM_HIP(hipStreamWaitEvent(b->chain_st, b->chain_ev[0], 0));
-    hipLaunchKernelGGL(k_chain_long, dim3(LONG_GRID), dim3(128), 0, b->chain_st, b->d_long_jobs.as<Job>(), rng, rng + 1,
+    hipStream_t cs = chain_stream(b, slot);
+    SKM_HIP(hipStreamWaitEvent(cs, b->chain_ev[0], 0));
+    b->chain_used[slot % std::max(1, std::min(b->tune.chain_streams, 1 + skm_build::GSLOTS))] = true;
+    hipLaunchKernelGGL(k_chain_long, dim3(LONG_GRID), dim3(128), 0, cs, b->d_long_jobs.as<Job>(), rng, rng + 1,
                        nullptr, nullptr, nullptr, nullptr, b->d_data.as<skm_stored_kmer_data>(), b->tune.chain_prio);
     SKM_HIP(hipGetLastError());
 }
@@ -5066,10 +5082,15 @@ void flush_long_chains(skm_build* b, int slot) {
 void phase_stats(skm_build* b) {
     hipStream_t st = b->stream;
     const uint32_t F = b->opts.n_functions;
-    if (b->pass_bits) {  // the long chains of every pass
-        flush_long_chains(b, 1);
-        SKM_HIP(hipEventRecord(b->chain_ev[2], b->chain_st));
-        SKM_HIP(hipStreamWaitEvent(st, b->chain_ev[2], 0));
+    if (b->pass_bits) {  // the long chains of every pass (the last batch on the chain stream)
+        flush_long_chains(b, 16);
+        for (int k = 0; k <= skm_build::GSLOTS; ++k) {
+            if (!b->chain_used[k]) continue;
+            const hipStream_t cs = chain_stream(b, k);
+            hipEvent_t e = k == 0 ? b->chain_ev[2] : b->gev_done[k - 1];
+            SKM_HIP(hipEventRecord(e, cs));
+            SKM_HIP(hipStreamWaitEvent(st, e, 0));
+        }
     }
     for (int g = 0; g < skm_build::GSLOTS; ++g)  // the giant chains of every pass
         if (b->gused[g]) SKM_HIP(hipStreamWaitEvent(st, b->gev_done[g], 0));
@@ -5149,7 +5170,11 @@ void run_once(const Ranks& bs) {
         if (bs[0]->world > 1) exchange(bs);
         for (auto* b : bs) {
             phase_group(b, pass);
-            if (P >= 4 && pass + 1 == P / 2) flush_long_chains(b, 0);  // first half's chains overlap the second half
+            // the stashed long chains leave in batches (default two: the first half's chains
+            // overlap the second half); the last batch runs after the last pass (phase_stats)
+            const uint32_t nb = std::min<uint32_t>(P >= 4 ? (uint32_t)std::max(1, b->tune.chain_batches) : 1u, 16u);
+            const uint32_t per = std::max<uint32_t>(1u, P / nb);
+            if (nb > 1 && (pass + 1) % per == 0 && pass + 1 < P) flush_long_chains(b, (int)((pass + 1) / per - 1));
         }
     }
     for (auto* b : bs) phase_stats(b);
@@ -5461,6 +5486,17 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
         SKM_CHECK(value >= 0 && value <= 64 && (value & (value - 1)) == 0, SKM_E_ARG,
                   "key_range_passes must be 0 (automatic) or a power of two <= 64");
         t.passes = (int)value;
+    } else if (n == "stream_priority") {
+        // 1: the group-by stream (the step's critical path) at the device's highest priority, so
+        // its workgroups are dispatched ahead of the overflow / chain / prefetch streams' work
+        SKM_CHECK(value == 0 || value == 1, SKM_E_ARG, "stream_priority must be 0 or 1");
+        SKM_HIP(hipSetDevice(b->device));
+        SKM_HIP(hipStreamSynchronize(b->stream));
+        SKM_HIP(hipStreamDestroy(b->stream));
+        int least = 0, greatest = 0;
+        SKM_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        SKM_HIP(hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, value ? greatest : least));
+        t.stream_prio = (int)value;
     } else if (n == "work_buffer_elements") {
         // capacities of the data-sized work buffers (tests: force the grow-and-redo path); 0 = the
         // automatic first guess
@@ -5488,7 +5524,9 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "prefetch" ? &t.prefetch
                : n == "overflow_grid" ? &t.ovf_grid
                : n == "split_grid" ? &t.split_grid
-               : n == "chain_grid" ? &t.chain_grid : nullptr;
+               : n == "chain_grid" ? &t.chain_grid
+               : n == "chain_batches" ? &t.chain_batches
+               : n == "chain_streams" ? &t.chain_streams : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")
