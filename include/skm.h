@@ -174,16 +174,23 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   "heavy_min" (occurrences that send a k-mer to the heavy path), "split_min" (overflow
  *   sub-buckets at least this large are split into heavy keys + a light remainder),
  *   "giant_class" (heavy chains of >= 2^class samples start right after the heavy kernel on
- *   their own streams; 0 = off).
+ *   their own streams; 0 = off; default: 14 with one pass, off with key-range passes),
+ *   "giant_passes", "prefetch" (the next pass's compaction during this pass's group-by, 1),
+ *   "overflow_grid" / "split_grid" / "chain_grid" (persistent-grid sizes), "stream_priority"
+ *   (1: the group-by stream at the highest priority), "chain_batches" (key-range passes: the
+ *   stashed long chains leave in this many batches, 4) / "chain_streams" (over 1..4 streams, 1),
+ *   "work_buffer_elements" (capacity of the data-sized work buffers; tests force the
+ *   grow-and-redo path with a small value; 0 = automatic).
  * Unknown names and out-of-range values return SKM_E_ARG. */
 int skm_build_set_option(skm_build* b, const char* name, int64_t value);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then
  * enable/disable stamping for subsequent runs. */
 int skm_build_debug_stamps(skm_build* b, int enable, uint64_t* out, int cap);
-/* Diagnostics: lengths of the first cap chain jobs in execution order (longest first). */
+/* Diagnostics: lengths of the first cap chain jobs of the last pass in execution order (longest
+ * first; the overflow's list when the pass had overflow sub-buckets). */
 int skm_build_debug_jobs(skm_build* b, uint32_t* out, int cap);
-/* Diagnostics: element counts of the last pass's overflow sub-buckets (largest first); returns
- * how many there are (at most cap written). */
+/* Diagnostics: element counts of the last pass's overflow sub-buckets as the partition listed
+ * them; returns how many there are (at most cap written). */
 int skm_build_debug_overflow(skm_build* b, uint32_t* out, int cap);
 /* Diagnostics: device time of the chain kernel on njobs synthetic jobs of length n
  * (mode 0: the build's choice by length, 1: one lane per chain, 2: one wave pair per chain). */

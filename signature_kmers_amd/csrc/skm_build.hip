@@ -3755,9 +3755,10 @@ struct Tune {
     int heavy_min = (int)HEAVY_MIN;  // occurrences that make a key heavy (k_ovf_split)
     int split_min = (int)SPLIT_MIN;  // overflow sub-buckets of at least this size are split
     // heavy chains of >= 2^class samples start right after k_heavy on rotating chain streams
-    // (0: off, the default: measured at C3, the FP64-bound chains running beside the pass kernels
-    // slow them by more than the ~0.5 s tail they would hide -- DESIGN.md section 4)
-    int giant_class = 0;
+    // (0: off; -1, the default: 14 with one pass, off with key-range passes -- measured at C3, the
+    // FP64-bound chains running beside the pass kernels slow them by more than the tail they
+    // would hide; giant_class())
+    int giant_class = -1;
     int giant_passes = 0;            // giant chains only in the last N passes (0: all)
     int prefetch = 1;                // next pass's compaction + count during this pass's group-by
     int ovf_grid = 1024;             // persistent grids: k_overflow (per stream),
@@ -4691,6 +4692,13 @@ void exchange(const Ranks& bs) {
 // run's long arena and they run on the chain stream, overlapping the following passes.  The
 // per-lane chains run on st (or st_short) within the pass.  Fixed grids that read the counts on
 // the device: no host round trip.
+// Giant chains (k_heavy's chains of >= 2^class samples start on a chain stream right after it):
+// the option, or by default 14 with one pass (C2: -0.5 ms, the longest P^2 chain is that path's
+// end) and off with key-range passes (C3: +60..80 ms, the FP64 chain waves slow the passes).
+int giant_class(const skm_build* b) {
+    return b->tune.giant_class >= 0 ? b->tune.giant_class : (b->pass_bits == 0 ? 14 : 0);
+}
+
 constexpr uint32_t JOB_NWG = 256;      // k_job_count / k_job_scatter workgroups (one chunk each)
 constexpr uint32_t LONG_GRID = 2048;   // k_chain_long / k_long_stash workgroups (one job at a time)
 
@@ -4859,7 +4867,8 @@ void phase_group(skm_build* b, uint32_t pass) {
     const int gs = (int)(pass % skm_build::GSLOTS);
     const uint32_t NP = 1u << b->pass_bits;
     const bool late = b->tune.giant_passes <= 0 || pass + (uint32_t)b->tune.giant_passes >= NP;
-    H.giant_min = b->tune.giant_class > 0 && late && pass < b->gsamples.size() ? 1u << b->tune.giant_class : 0u;
+    const int gcls = giant_class(b);
+    H.giant_min = gcls > 0 && late && pass < b->gsamples.size() ? 1u << gcls : 0u;
     H.gsamples = nullptr;
     H.gjobs = nullptr;
     H.gcount = nullptr;
@@ -4984,7 +4993,7 @@ void alloc_caps(skm_build* b) {
         b->d_long_arena.ensure(4 * std::max<uint64_t>(b->long_cap, 1));
     }
     const uint32_t NP = 1u << b->pass_bits;
-    if (b->tune.giant_class > 0) {
+    if (giant_class(b) > 0) {
         while (b->gsamples.size() < NP) {
             b->gsamples.emplace_back();
             b->gjobs.emplace_back();
@@ -4992,7 +5001,7 @@ void alloc_caps(skm_build* b) {
         }
         for (uint32_t p = 0; p < NP; ++p) {
             b->gsamples[p].ensure(4 * Sp);
-            b->gjobs[p].ensure(sizeof(Job) * (Sp / (1u << b->tune.giant_class) + 16));
+            b->gjobs[p].ensure(sizeof(Job) * (Sp / (1u << giant_class(b)) + 16));
             b->gcount[p].ensure(16);
         }
     }
