@@ -376,10 +376,14 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
         "counters": ctrs,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": _pmc_traffic(dom, {50_000_000: "c3", 1_000_000: "c2"}.get(shard.n_seqs, "") if world == 1
-                                             else "", shard.n_seqs),
-                     "alg_bytes_per_launch": alg[dom], "avg_launch_ms": dom_ms,
-                     "launches_per_step": b.passes()},
+                     "traffic": _per_launch(_pmc_traffic(dom, {50_000_000: "c3", 1_000_000: "c2"}.get(shard.n_seqs, "")
+                                                         if world == 1 else "", shard.n_seqs), b.passes()),
+                     # one launch per key-range pass: per-launch figures are the step's / passes
+                     # (the ratio -- achieved -- is the same either way)
+                     "alg_bytes_per_launch": alg[dom] / max(1, b.passes()),
+                     "avg_launch_ms": dom_ms / max(1, b.passes()),
+                     "alg_bytes_per_step": alg[dom], "kernel_ms_per_step": dom_ms,
+                     "launches_per_step": max(1, b.passes())},
         "pipeline": {"alg_bytes": pipe_alg, "ms": 1000.0 * t_max / steps, "GBs": pipe_gbs,
                      "frac": pipe_gbs / HBM_PEAK_GBS / max(1, world), "phase_ms_rank0": phase},
     }
@@ -547,10 +551,14 @@ def _matrix_leg(skm, matrix_in, a, device, cores, rank=0, world=1, dist=None):
             "cpu_baseline": cpu, "prep_s": prep_s}
 
 
+def _per_launch(traffic, passes):
+    return None if traffic is None else traffic / max(1, passes)
+
+
 def _pmc_traffic(kernel: str, workload: str, seqs: int):
     """HBM bytes of `kernel` from the committed rocprofv3 PMC summary (profiles/r02_pmc_traffic.json,
     tools/gpu_profile_r02.sh + tools/pmc_summary_r02.py): per build run (16 launches at C3, one at
-    C2 -- the same span as alg_bytes_per_launch / avg_launch_ms here) or per launch (legs), when it
+    C2 -- divided by the passes for the per-launch roofline) or per launch (legs), when it
     was measured on this kernel and workload size; else None.  Streaming kernels count FETCH_SIZE
     x2, gather kernels x1 (profiles/r02_fetch_calib.json)."""
     path = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
