@@ -193,7 +193,8 @@ int skm_build_debug_jobs(skm_build* b, uint32_t* out, int cap);
  * them; returns how many there are (at most cap written). */
 int skm_build_debug_overflow(skm_build* b, uint32_t* out, int cap);
 /* Diagnostics: device time of the chain kernel on njobs synthetic jobs of length n
- * (mode 0: the build's choice by length, 1: one lane per chain, 2: one wave pair per chain). */
+ * (mode 0: the build's choice by length, 1: one lane per chain, 2: one wave pair per chain;
+ *  3 / 5: the P^2 wave alone, previous / current walk; 4: the variance wave alone). */
 int skm_debug_chain_bench(uint32_t n, uint32_t njobs, int mode, float* ms);
 /* Diagnostics: the P^2 median and the variance (raw doubles) of one chain of n samples in visit
  * order, by the per-lane (mode 1) or the wave-pair (mode 2) chain code. */

@@ -1035,6 +1035,125 @@ __device__ __forceinline__ double chain_long_p2(const uint32_t* __restrict__ x, 
     return h2;
 }
 
+// The same walk with the adjust decisions branch-free (s_cselect instead of short-circuit
+// branches) and the reciprocals of one step computed lane-parallel: lane 3(i-1) + {0, 1, 2} holds
+// marker i's divisors dp, dm, dp - dm, one vector rcp + Newton sequence gives all nine RN(1/m),
+// and each adjusting marker reads its three back with v_readlane (the same values as rcp_int).
+// v_writelane_b32 (no clang builtin for it): lane L of v takes the wave-uniform x
+template <int L>
+__device__ __forceinline__ int32_t writelane_i32_(int32_t v, int32_t x) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(L));
+    return v;
+}
+#define writelane_i32(v, x, L) writelane_i32_<L>((v), (x))
+
+template <int L>
+__device__ __forceinline__ double p2_height_lanes(double hm_, double H, double hp_, int32_t dpi, int32_t dmi,
+                                                  int32_t sgi, double y) {
+    return p2_height_y(hm_, H, hp_, dpi, dmi, sgi, readlane_f64(y, L), readlane_f64(y, L + 1), readlane_f64(y, L + 2));
+}
+template <int M>
+__device__ __forceinline__ void p2_adjust_lanes(double& h1, double& h2, double& h3, double h0, double h4,
+                                                const int32_t (&dp)[3], const int32_t (&dm)[3], const int32_t (&sg)[3],
+                                                double y) {
+    if constexpr ((M & 1) != 0) h1 = p2_height_lanes<0>(h0, h1, h2, dp[0], dm[0], sg[0], y);
+    if constexpr ((M & 2) != 0) h2 = p2_height_lanes<3>(h1, h2, h3, dp[1], dm[1], sg[1], y);
+    if constexpr ((M & 4) != 0) h3 = p2_height_lanes<6>(h2, h3, h4, dp[2], dm[2], sg[2], y);
+}
+
+__device__ __forceinline__ double chain_long_p2v(const uint32_t* __restrict__ x, uint32_t n_) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n_);
+    SigStats st;
+    st.init();
+    const uint32_t n0 = min(n, 5u);
+    for (uint32_t i = 0; i < n0; ++i) st.add_p2(x[i]);
+    if (n <= 5) return st.h[2];
+    double h1 = st.h[1], h2 = st.h[2], h3 = st.h[3];
+    uint32_t h0i = (uint32_t)st.h[0], h4i = (uint32_t)st.h[4];
+    int32_t a1 = st.act[1], a2 = st.act[2], a3 = st.act[3], a4 = st.act[4];
+    int32_t k4 = 0;
+    uint32_t xn = 5 + lane < n ? x[5 + lane] : 0u;
+    for (uint32_t base = 5; base < n; base += 64) {
+        const uint32_t m = min(64u, n - base);
+        const uint32_t xl = xn;
+        const bool live = lane < m;
+        xn = base + 64 + lane < n ? x[base + 64 + lane] : 0u;
+        const uint32_t imin = min(h0i, incl_scan_min(live ? xl : 0xFFFFFFFFu));
+        const uint32_t imax = max(h4i, incl_scan_max(live ? xl : 0u));
+        const double xd = (double)xl;
+        uint64_t B1 = __ballot(live && h1 <= xd), B2 = __ballot(live && h2 <= xd), B3 = __ballot(live && h3 <= xd);
+        for (uint32_t l = 0; l < m; ++l) {
+            a1 += 1 - (int32_t)((B1 >> l) & 1u);
+            a2 += 1 - (int32_t)((B2 >> l) & 1u);
+            a3 += 1 - (int32_t)((B3 >> l) & 1u);
+            a4 += 1;
+            ++k4;
+            int32_t dp[3], dm[3], sg[3];
+            int32_t adj;
+            uint32_t mask;
+            {
+                const int32_t d4 = 8 + k4 - 4 * a1;
+                dp[0] = a2 - a1;
+                dm[0] = 1 - a1;
+                sg[0] = d4 > 0 ? 1 : -1;
+                adj = ((int32_t)(d4 >= 4) & (int32_t)(dp[0] > 1)) | ((int32_t)(d4 <= -4) & (int32_t)(dm[0] < -1));
+                a1 += adj ? sg[0] : 0;
+                mask = adj ? 1u : 0u;
+            }
+            {
+                const int32_t d4 = 12 + 2 * k4 - 4 * a2;
+                dp[1] = a3 - a2;
+                dm[1] = a1 - a2;
+                sg[1] = d4 > 0 ? 1 : -1;
+                adj = ((int32_t)(d4 >= 4) & (int32_t)(dp[1] > 1)) | ((int32_t)(d4 <= -4) & (int32_t)(dm[1] < -1));
+                a2 += adj ? sg[1] : 0;
+                mask |= adj ? 2u : 0u;
+            }
+            {
+                const int32_t d4 = 16 + 3 * k4 - 4 * a3;
+                dp[2] = a4 - a3;
+                dm[2] = a2 - a3;
+                sg[2] = d4 > 0 ? 1 : -1;
+                adj = ((int32_t)(d4 >= 4) & (int32_t)(dp[2] > 1)) | ((int32_t)(d4 <= -4) & (int32_t)(dm[2] < -1));
+                a3 += adj ? sg[2] : 0;
+                mask |= adj ? 4u : 0u;
+            }
+            if (mask) {
+                // lanes 0..8: marker i's dp, dm, dp - dm (unused lanes keep 1)
+                int32_t dv = 1;
+                dv = writelane_i32(dv, dp[0], 0);
+                dv = writelane_i32(dv, dm[0], 1);
+                dv = writelane_i32(dv, dp[0] - dm[0], 2);
+                dv = writelane_i32(dv, dp[1], 3);
+                dv = writelane_i32(dv, dm[1], 4);
+                dv = writelane_i32(dv, dp[1] - dm[1], 5);
+                dv = writelane_i32(dv, dp[2], 6);
+                dv = writelane_i32(dv, dm[2], 7);
+                dv = writelane_i32(dv, dp[2] - dm[2], 8);
+                const double y = rcp_int((double)dv);
+                const double h0 = (double)(uint32_t)__builtin_amdgcn_readlane((int)imin, (int)l);
+                const double h4 = (double)(uint32_t)__builtin_amdgcn_readlane((int)imax, (int)l);
+                switch (mask) {
+                    case 1: p2_adjust_lanes<1>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
+                    case 2: p2_adjust_lanes<2>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
+                    case 3: p2_adjust_lanes<3>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
+                    case 4: p2_adjust_lanes<4>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
+                    case 5: p2_adjust_lanes<5>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
+                    case 6: p2_adjust_lanes<6>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
+                    default: p2_adjust_lanes<7>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
+                }
+                B1 = __ballot(live && h1 <= xd);
+                B2 = __ballot(live && h2 <= xd);
+                B3 = __ballot(live && h3 <= xd);
+            }
+        }
+        h0i = (uint32_t)__builtin_amdgcn_readlane((int)imin, (int)(m - 1));
+        h4i = (uint32_t)__builtin_amdgcn_readlane((int)imax, (int)(m - 1));
+    }
+    return h2;
+}
+
 __device__ __forceinline__ double chain_long_var(const uint32_t* __restrict__ x, uint32_t n_) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n_);
@@ -1084,7 +1203,7 @@ __global__ __launch_bounds__(128) void k_chain_long(const Job* __restrict__ jobs
                               : (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
                                     (jb.lens_off & LENS_OFF_MASK);
         if (threadIdx.x < 64) {
-            const double med = chain_long_p2(x, jb.n);
+            const double med = chain_long_p2v(x, jb.n);
             if (threadIdx.x == 0) out[jb.out_idx].median = d2u16(med);
         } else {
             const double v = chain_long_var(x, jb.n);
@@ -1105,7 +1224,7 @@ __global__ __launch_bounds__(128) void k_chain_dyn(const Job* __restrict__ jobs,
         const Job jb = jobs[q];
         const uint32_t* x = reinterpret_cast<const uint32_t*>(jb.lens_off);
         if (threadIdx.x < 64) {
-            const double med = chain_long_p2(x, jb.n);
+            const double med = chain_long_p2v(x, jb.n);
             if (threadIdx.x == 0) out[jb.out_idx].median = d2u16(med);
         } else {
             const double v = chain_long_var(x, jb.n);
@@ -1155,7 +1274,7 @@ __global__ __launch_bounds__(64) void k_chain_long_half(const Job* __restrict__ 
                                                         int which, double* __restrict__ out) {
     const Job jb = jobs[blockIdx.x];
     const uint32_t* x = lens + (jb.lens_off & LENS_OFF_MASK);
-    const double r = which == 0 ? chain_long_p2(x, jb.n) : chain_long_var(x, jb.n);
+    const double r = which == 0 ? chain_long_p2(x, jb.n) : which == 2 ? chain_long_p2v(x, jb.n) : chain_long_var(x, jb.n);
     if (threadIdx.x == 0) out[blockIdx.x] = r;
 }
 
@@ -1164,7 +1283,7 @@ __global__ __launch_bounds__(128) void k_chain_eval(const uint32_t* __restrict__
                                                     double* __restrict__ out) {
     if (mode == 2) {
         if (threadIdx.x < 64) {
-            const double m = chain_long_p2(x, n);
+            const double m = chain_long_p2v(x, n);
             if (threadIdx.x == 0) out[0] = m;
         } else {
             const double v = chain_long_var(x, n);
@@ -5617,7 +5736,7 @@ int skm_debug_chain_bench(uint32_t n, uint32_t njobs, int mode, float* ms) {
     const uint64_t threads = ceil_div(njobs, 64) * 128;
     for (int it = 0; it < 2; ++it) {
         SKM_HIP(hipEventRecord(e0, 0));
-        if (mode == 3 || mode == 4)
+        if (mode == 3 || mode == 4 || mode == 5)
             hipLaunchKernelGGL(k_chain_long_half, dim3(njobs), dim3(64), 0, 0, dj.as<Job>(), dl.as<uint32_t>(),
                                mode - 3, reinterpret_cast<double*>(dout.p));
         else if (mode == 2 || (mode == 0 && n >= (1u << LONG_CLASS)))
