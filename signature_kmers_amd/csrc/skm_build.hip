@@ -1047,18 +1047,41 @@ __device__ __forceinline__ int32_t writelane_i32_(int32_t v, int32_t x) {
 }
 #define writelane_i32(v, x, L) writelane_i32_<L>((v), (x))
 
+// p2_height_y split at the dependence on the lower neighbour: the upper quotient (hp_ - H) / dp
+// uses only heights no earlier marker of this step changes, so every adjusting marker's upper
+// half is issued first and only the lower half stays on the marker 1 -> 2 -> 3 chain.
+struct P2Up {
+    double hp, a, ym;
+};
 template <int L>
-__device__ __forceinline__ double p2_height_lanes(double hm_, double H, double hp_, int32_t dpi, int32_t dmi,
-                                                  int32_t sgi, double y) {
-    return p2_height_y(hm_, H, hp_, dpi, dmi, sgi, readlane_f64(y, L), readlane_f64(y, L + 1), readlane_f64(y, L + 2));
+__device__ __forceinline__ P2Up p2_upper(double H, double hp_, int32_t dpi, int32_t dmi, int32_t sgi, double y) {
+    P2Up u;
+    u.hp = div_by(hp_ - H, (double)dpi, readlane_f64(y, L));
+    u.a = (double)(sgi - dmi) * u.hp;
+    u.ym = readlane_f64(y, L + 2);
+    return u;
+}
+template <int L>
+__device__ __forceinline__ double p2_lower(double hm_, double H, double hp_, int32_t dpi, int32_t dmi, int32_t sgi,
+                                           const P2Up& u, double y) {
+    const double hm = div_by(hm_ - H, (double)dmi, readlane_f64(y, L + 1));
+    const double t = u.ym * (u.a + (double)(dpi - sgi) * hm);
+    const double hh = sgi > 0 ? H + t : H - t;
+    const double lin = sgi > 0 ? H + u.hp : H - hm;
+    return (hm_ < hh && hh < hp_) ? hh : lin;
 }
 template <int M>
 __device__ __forceinline__ void p2_adjust_lanes(double& h1, double& h2, double& h3, double h0, double h4,
                                                 const int32_t (&dp)[3], const int32_t (&dm)[3], const int32_t (&sg)[3],
                                                 double y) {
-    if constexpr ((M & 1) != 0) h1 = p2_height_lanes<0>(h0, h1, h2, dp[0], dm[0], sg[0], y);
-    if constexpr ((M & 2) != 0) h2 = p2_height_lanes<3>(h1, h2, h3, dp[1], dm[1], sg[1], y);
-    if constexpr ((M & 4) != 0) h3 = p2_height_lanes<6>(h2, h3, h4, dp[2], dm[2], sg[2], y);
+    const double o2 = h2, o3 = h3;  // upper neighbours as the step found them
+    P2Up u1, u2, u3;
+    if constexpr ((M & 1) != 0) u1 = p2_upper<0>(h1, o2, dp[0], dm[0], sg[0], y);
+    if constexpr ((M & 2) != 0) u2 = p2_upper<3>(o2, o3, dp[1], dm[1], sg[1], y);
+    if constexpr ((M & 4) != 0) u3 = p2_upper<6>(o3, h4, dp[2], dm[2], sg[2], y);
+    if constexpr ((M & 1) != 0) h1 = p2_lower<0>(h0, h1, o2, dp[0], dm[0], sg[0], u1, y);
+    if constexpr ((M & 2) != 0) h2 = p2_lower<3>(h1, o2, o3, dp[1], dm[1], sg[1], u2, y);
+    if constexpr ((M & 4) != 0) h3 = p2_lower<6>(h2, o3, h4, dp[2], dm[2], sg[2], u3, y);
 }
 
 __device__ __forceinline__ double chain_long_p2v(const uint32_t* __restrict__ x, uint32_t n_) {
@@ -1072,7 +1095,7 @@ __device__ __forceinline__ double chain_long_p2v(const uint32_t* __restrict__ x,
     double h1 = st.h[1], h2 = st.h[2], h3 = st.h[3];
     uint32_t h0i = (uint32_t)st.h[0], h4i = (uint32_t)st.h[4];
     int32_t a1 = st.act[1], a2 = st.act[2], a3 = st.act[3], a4 = st.act[4];
-    int32_t k4 = 0;
+    int32_t K1 = 8, K2 = 12, K3 = 16;  // 4 * desired positions: 4(i+1) + i*(cnt-5)
     uint32_t xn = 5 + lane < n ? x[5 + lane] : 0u;
     for (uint32_t base = 5; base < n; base += 64) {
         const uint32_t m = min(64u, n - base);
@@ -1084,40 +1107,48 @@ __device__ __forceinline__ double chain_long_p2v(const uint32_t* __restrict__ x,
         const double xd = (double)xl;
         uint64_t B1 = __ballot(live && h1 <= xd), B2 = __ballot(live && h2 <= xd), B3 = __ballot(live && h3 <= xd);
         for (uint32_t l = 0; l < m; ++l) {
+            // positions: +1 below the sample's cell (B bit clear), a4 always
             a1 += 1 - (int32_t)((B1 >> l) & 1u);
             a2 += 1 - (int32_t)((B2 >> l) & 1u);
             a3 += 1 - (int32_t)((B3 >> l) & 1u);
             a4 += 1;
-            ++k4;
+            K1 += 1;  // 4 * desired position of marker i = K_i
+            K2 += 2;
+            K3 += 3;
+            // adjust decisions as sign bits, no compares: up = (d4 >= 4 && dp > 1) is the sign of
+            // (3 - d4) & (1 - dp); down = (d4 <= -4 && dm < -1) the sign of (d4 + 3) & (dm + 1);
+            // the two exclude each other and the step is up - down (sg = +1 up, -1 down)
             int32_t dp[3], dm[3], sg[3];
-            int32_t adj;
             uint32_t mask;
             {
-                const int32_t d4 = 8 + k4 - 4 * a1;
+                const int32_t d4 = K1 - 4 * a1;
                 dp[0] = a2 - a1;
                 dm[0] = 1 - a1;
-                sg[0] = d4 > 0 ? 1 : -1;
-                adj = ((int32_t)(d4 >= 4) & (int32_t)(dp[0] > 1)) | ((int32_t)(d4 <= -4) & (int32_t)(dm[0] < -1));
-                a1 += adj ? sg[0] : 0;
-                mask = adj ? 1u : 0u;
+                const uint32_t up = ((uint32_t)(3 - d4) & (uint32_t)(1 - dp[0])) >> 31;
+                const uint32_t dn = ((uint32_t)(d4 + 3) & (uint32_t)(dm[0] + 1)) >> 31;
+                a1 += (int32_t)up - (int32_t)dn;
+                sg[0] = 1 - 2 * (int32_t)dn;
+                mask = up | dn;
             }
             {
-                const int32_t d4 = 12 + 2 * k4 - 4 * a2;
+                const int32_t d4 = K2 - 4 * a2;
                 dp[1] = a3 - a2;
                 dm[1] = a1 - a2;
-                sg[1] = d4 > 0 ? 1 : -1;
-                adj = ((int32_t)(d4 >= 4) & (int32_t)(dp[1] > 1)) | ((int32_t)(d4 <= -4) & (int32_t)(dm[1] < -1));
-                a2 += adj ? sg[1] : 0;
-                mask |= adj ? 2u : 0u;
+                const uint32_t up = ((uint32_t)(3 - d4) & (uint32_t)(1 - dp[1])) >> 31;
+                const uint32_t dn = ((uint32_t)(d4 + 3) & (uint32_t)(dm[1] + 1)) >> 31;
+                a2 += (int32_t)up - (int32_t)dn;
+                sg[1] = 1 - 2 * (int32_t)dn;
+                mask |= (up | dn) << 1;
             }
             {
-                const int32_t d4 = 16 + 3 * k4 - 4 * a3;
+                const int32_t d4 = K3 - 4 * a3;
                 dp[2] = a4 - a3;
                 dm[2] = a2 - a3;
-                sg[2] = d4 > 0 ? 1 : -1;
-                adj = ((int32_t)(d4 >= 4) & (int32_t)(dp[2] > 1)) | ((int32_t)(d4 <= -4) & (int32_t)(dm[2] < -1));
-                a3 += adj ? sg[2] : 0;
-                mask |= adj ? 4u : 0u;
+                const uint32_t up = ((uint32_t)(3 - d4) & (uint32_t)(1 - dp[2])) >> 31;
+                const uint32_t dn = ((uint32_t)(d4 + 3) & (uint32_t)(dm[2] + 1)) >> 31;
+                a3 += (int32_t)up - (int32_t)dn;
+                sg[2] = 1 - 2 * (int32_t)dn;
+                mask |= (up | dn) << 2;
             }
             if (mask) {
                 // lanes 0..8: marker i's dp, dm, dp - dm (unused lanes keep 1)
