@@ -1065,15 +1065,20 @@ template <int L>
 __device__ __forceinline__ double p2_lower(double hm_, double H, double hp_, int32_t dpi, int32_t dmi, int32_t sgi,
                                            const P2Up& u, double y) {
     const double hm = div_by(hm_ - H, (double)dmi, readlane_f64(y, L + 1));
-    const double t = u.ym * (u.a + (double)(dpi - sgi) * hm);
-    const double hh = sgi > 0 ? H + t : H - t;
+    // H -+ RN(ym * S) == H + RN(+-ym * S): RN is odd, and x - y is x + (-y)
+    const double ysg = sgi > 0 ? u.ym : -u.ym;
+    const double hh = H + ysg * (u.a + (double)(dpi - sgi) * hm);
     const double lin = sgi > 0 ? H + u.hp : H - hm;
     return (hm_ < hh && hh < hp_) ? hh : lin;
 }
 template <int M>
-__device__ __forceinline__ void p2_adjust_lanes(double& h1, double& h2, double& h3, double h0, double h4,
-                                                const int32_t (&dp)[3], const int32_t (&dm)[3], const int32_t (&sg)[3],
-                                                double y) {
+__device__ __forceinline__ void p2_adjust_lanes(double& h1, double& h2, double& h3, uint32_t imin, uint32_t imax,
+                                                uint32_t l, const int32_t (&dp)[3], const int32_t (&dm)[3],
+                                                const int32_t (&sg)[3], double y) {
+    // the extremes after sample l (lane-prefix min / max), read only by the markers next to them
+    double h0 = 0.0, h4 = 0.0;
+    if constexpr ((M & 1) != 0) h0 = (double)(uint32_t)__builtin_amdgcn_readlane((int)imin, (int)l);
+    if constexpr ((M & 4) != 0) h4 = (double)(uint32_t)__builtin_amdgcn_readlane((int)imax, (int)l);
     const double o2 = h2, o3 = h3;  // upper neighbours as the step found them
     P2Up u1, u2, u3;
     if constexpr ((M & 1) != 0) u1 = p2_upper<0>(h1, o2, dp[0], dm[0], sg[0], y);
@@ -1105,7 +1110,8 @@ __device__ __forceinline__ double chain_long_p2v(const uint32_t* __restrict__ x,
         const uint32_t imin = min(h0i, incl_scan_min(live ? xl : 0xFFFFFFFFu));
         const uint32_t imax = max(h4i, incl_scan_max(live ? xl : 0u));
         const double xd = (double)xl;
-        uint64_t B1 = __ballot(live && h1 <= xd), B2 = __ballot(live && h2 <= xd), B3 = __ballot(live && h3 <= xd);
+        // bits of lanes >= m are never read: no live mask on the ballots
+        uint64_t B1 = __ballot(h1 <= xd), B2 = __ballot(h2 <= xd), B3 = __ballot(h3 <= xd);
         for (uint32_t l = 0; l < m; ++l) {
             // positions: +1 below the sample's cell (B bit clear), a4 always
             a1 += 1 - (int32_t)((B1 >> l) & 1u);
@@ -1151,10 +1157,9 @@ __device__ __forceinline__ double chain_long_p2v(const uint32_t* __restrict__ x,
                 mask |= (up | dn) << 2;
             }
             if (mask) {
-                // lanes 0..8: marker i's dp, dm, dp - dm (unused lanes keep 1)
-                int32_t dv = 1;
+                // lanes 0..8: marker i's dp, dm, dp - dm (the other lanes hold dm[0] = 1 - a1 < 0)
+                int32_t dv = dm[0];
                 dv = writelane_i32(dv, dp[0], 0);
-                dv = writelane_i32(dv, dm[0], 1);
                 dv = writelane_i32(dv, dp[0] - dm[0], 2);
                 dv = writelane_i32(dv, dp[1], 3);
                 dv = writelane_i32(dv, dm[1], 4);
@@ -1163,20 +1168,18 @@ __device__ __forceinline__ double chain_long_p2v(const uint32_t* __restrict__ x,
                 dv = writelane_i32(dv, dm[2], 7);
                 dv = writelane_i32(dv, dp[2] - dm[2], 8);
                 const double y = rcp_int((double)dv);
-                const double h0 = (double)(uint32_t)__builtin_amdgcn_readlane((int)imin, (int)l);
-                const double h4 = (double)(uint32_t)__builtin_amdgcn_readlane((int)imax, (int)l);
                 switch (mask) {
-                    case 1: p2_adjust_lanes<1>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
-                    case 2: p2_adjust_lanes<2>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
-                    case 3: p2_adjust_lanes<3>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
-                    case 4: p2_adjust_lanes<4>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
-                    case 5: p2_adjust_lanes<5>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
-                    case 6: p2_adjust_lanes<6>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
-                    default: p2_adjust_lanes<7>(h1, h2, h3, h0, h4, dp, dm, sg, y); break;
+                    case 1: p2_adjust_lanes<1>(h1, h2, h3, imin, imax, l, dp, dm, sg, y); break;
+                    case 2: p2_adjust_lanes<2>(h1, h2, h3, imin, imax, l, dp, dm, sg, y); break;
+                    case 3: p2_adjust_lanes<3>(h1, h2, h3, imin, imax, l, dp, dm, sg, y); break;
+                    case 4: p2_adjust_lanes<4>(h1, h2, h3, imin, imax, l, dp, dm, sg, y); break;
+                    case 5: p2_adjust_lanes<5>(h1, h2, h3, imin, imax, l, dp, dm, sg, y); break;
+                    case 6: p2_adjust_lanes<6>(h1, h2, h3, imin, imax, l, dp, dm, sg, y); break;
+                    default: p2_adjust_lanes<7>(h1, h2, h3, imin, imax, l, dp, dm, sg, y); break;
                 }
-                B1 = __ballot(live && h1 <= xd);
-                B2 = __ballot(live && h2 <= xd);
-                B3 = __ballot(live && h3 <= xd);
+                B1 = __ballot(h1 <= xd);
+                B2 = __ballot(h2 <= xd);
+                B3 = __ballot(h3 <= xd);
             }
         }
         h0i = (uint32_t)__builtin_amdgcn_readlane((int)imin, (int)(m - 1));
