@@ -180,6 +180,8 @@ struct SigStats {
                 const int32_t d4 = 4 * (i + 1) + k4 * i - 4 * act[i];  // 4*d
                 const int32_t dpi = act[i + 1] - act[i];
                 const int32_t dmi = act[i - 1] - act[i];
+                // (a branch-free form -- the height computed for every lane and selected -- measured
+                // slower: 744 vs 514 ns/sample with 16 chains per wave, markers often adjust in no lane)
                 if ((d4 >= 4 && dpi > 1) || (d4 <= -4 && dmi < -1)) {
                     const int32_t sgi = d4 > 0 ? 1 : -1;  // d / |d|, exactly +-1
                     h[i] = p2_height(h[i - 1], h[i], h[i + 1], dpi, dmi, sgi);
