@@ -3569,16 +3569,19 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
         uint32_t sum = 0, smax = 0;
         for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
             uint64_t l[U];
-            uint32_t f[U];
+            uint32_t f[U], gl[U];
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
                 const uint32_t j = j0 + u * nt + tid;
-                f[u] = j < n ? (uint32_t)(hi[j] & 0xFFFFu) : 0xFFFFFFFFu;
+                const uint64_t h = j < n ? hi[j] : ~0ull;
+                f[u] = j < n ? (uint32_t)(h & 0xFFFFu) : 0xFFFFFFFFu;
+                // the mean's accumulator is a u16: the element's length mod 2^16 (bits 48..63 of
+                // the heavy copy, which keeps the length bits) is all it needs -- no glen gather
+                gl[u] = (uint32_t)(h >> 48);
                 l[u] = j < n ? lo[j] : 0ull;
             }
-            uint32_t gl[U];
 #pragma unroll
-            for (uint32_t u = 0; u < U; ++u) gl[u] = f[u] == best_f ? A.glen[(uint32_t)(l[u] >> 36)] : 0u;
+            for (uint32_t u = 0; u < U; ++u) gl[u] = f[u] == best_f ? gl[u] : 0u;
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
                 const bool v = f[u] != 0xFFFFFFFFu;
