@@ -1513,39 +1513,26 @@ constexpr int CP_THREADS = 256, CP_PER_THREAD = 128;  // 32768 windows per workg
 __global__ __launch_bounds__(CP_THREADS) void k_pass_compact(const uint8_t* __restrict__ ids, uint64_t rp, uint32_t pass,
                                                              uint64_t* __restrict__ pos,
                                                              unsigned long long* __restrict__ cursor, uint64_t cap) {
-    // Wave w of the workgroup covers 64 * CP_PER_THREAD consecutive windows; its k-th load takes
-    // the k-th 1 KB of them, 16 ids per lane, so every load instruction reads whole lines.  The
-    // positions keep ascending order: per chunk a wave prefix over the lanes, chunks in order,
-    // waves in order.
-    constexpr int K = CP_PER_THREAD / 16;
     __shared__ uint32_t s_wave[CP_THREADS / 64 + 1];
     __shared__ unsigned long long s_base;
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint64_t wbase = (uint64_t)blockIdx.x * CP_THREADS * CP_PER_THREAD + (uint64_t)wave * 64u * CP_PER_THREAD;
-    uint32_t m[K], pre[K];
-    uint32_t wcnt = 0;  // the wave's matches so far (uniform)
+    const uint64_t base = (uint64_t)blockIdx.x * CP_THREADS * CP_PER_THREAD + (uint64_t)threadIdx.x * CP_PER_THREAD;
+    uint32_t m[CP_PER_THREAD / 16];
+    uint32_t cnt = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint64_t q = wbase + 16u * (64u * (uint32_t)k + lane);
+    for (int k = 0; k < CP_PER_THREAD / 16; ++k) {
+        const uint64_t q = base + 16u * k;
         m[k] = q < rp ? match16(*reinterpret_cast<const uint4*>(ids + q), pass) : 0u;
-        const uint32_t c = (uint32_t)__popc(m[k]);
-        const uint32_t incl = wave_incl_scan(c);
-        pre[k] = wcnt + incl - c;
-        wcnt += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        cnt += __popc(m[k]);
     }
     uint32_t tot;
-    const uint32_t woff = wg_exclusive_scan(lane == 0 ? wcnt : 0u, s_wave, tot);
-    const uint32_t wb = (uint32_t)__builtin_amdgcn_readfirstlane((int)woff);  // lane 0: waves before this one
+    uint32_t off = wg_exclusive_scan(cnt, s_wave, tot);
     if (threadIdx.x == 0) s_base = tot ? atomicAdd(cursor, (unsigned long long)tot) : 0ull;
     __syncthreads();
-    const uint64_t o0 = s_base + wb;  // the pass sizes were counted at prepare with the same hash: o < cap
+    uint64_t o = s_base + off;  // the pass sizes were counted at prepare with the same hash: o < cap
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint64_t q = wbase + 16u * (64u * (uint32_t)k + lane);
-        uint64_t o = o0 + pre[k];
+    for (int k = 0; k < CP_PER_THREAD / 16; ++k)
         for (uint32_t w = m[k]; w; w &= w - 1, ++o)
-            if (o < cap) pos[o] = q + (uint32_t)__ffs(w) - 1u;
-    }
+            if (o < cap) pos[o] = base + 16u * k + (uint32_t)__ffs(w) - 1u;
 }
 
 // the 8 residue bytes at packed position p (the buffer is padded past its end)
