@@ -1,3 +1,6 @@
+# A/B of two libskm builds on the C3 step (record of the k_pass_compact experiment):
+# 'new' = signature_kmers_amd/libskm.so, 'old' = ab/libskm_oldcompact.so (build it from the variant
+# source with the Makefile's hipcc flags first); plus a rocprof kernel-stats run of 'old'.
 set -u
 O=gpurun_out; mkdir -p $O; R=$(pwd); export TMPDIR=/tmp
 timeout -k 10 300 python3 bench.py --cache-dir /tmp/c3 --cache-only > $O/abc_cache.log 2>&1 || { tail -5 $O/abc_cache.log; exit 1; }
