@@ -56,8 +56,8 @@ def parse():
     ap.add_argument("--families", type=int, default=4000)
     ap.add_argument("--weak-seqs", type=int, default=C2_SEQS,
                     help="proteins per GPU of the secondary weak-scaling (C2) line; 0 = off")
-    ap.add_argument("--cpu-sample-seqs", type=int, default=C2_SEQS,
-                    help="sequences of the workload the CPU baseline builds (a bounded sample)")
+    ap.add_argument("--cpu-shard-div", type=int, default=8,
+                    help="the C3 CPU baseline builds the first 1/N shard of the proteome (SURVEY 8(d): 1/8)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="host threads of the CPU baseline (0: all usable)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gen-workers", type=int, default=0, help="generator processes (0: usable cores)")
@@ -269,10 +269,17 @@ def main():
         "gen_seconds": gen_s,
         "prepare_seconds": prep_s,
     }
-    cpu = None
+    out["chain_tail_ms"] = head["chain_tail_ms"]
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = _cpu_baseline(c3, len(funcs), a.cpu_sample_seqs, a.cpu_threads or cores["usable"], cores, a.seqs_total)
-        out["cpu_baseline"] = cpu
+        n = a.seqs_total // max(1, a.cpu_shard_div)
+        log(f"CPU baseline: first {n:,} proteins (1/{a.cpu_shard_div} shard of C3)")
+        out["cpu_baseline"] = _cpu_baseline(
+            c3, len(funcs), n, a.cpu_threads or cores["usable"], cores,
+            f"the first {n:,} of the {a.seqs_total:,} proteins = one 1/{a.cpu_shard_div} shard "
+            f"(genome files 0..{(n + PER_FILE - 1) // PER_FILE - 1}) of the C3 proteome; value is that shard's "
+            f"build rate, taken as the extrapolated C3 rate (EXTRAPOLATION, SURVEY 8(d): a shard's k-mer groups are "
+            f"~1/{a.cpu_shard_div} the size of the whole proteome's, and the full 15 G-occurrence build does not fit "
+            f"the reference's host-memory design)")
 
     # ---- secondary: C2 per GPU (weak scaling; configs[1] at N=1) ----
     kept = None
@@ -293,10 +300,12 @@ def main():
                        "config": {"workload": f"C2: {a.weak_seqs:,} proteins per GPU x {world}, k=8, signature build",
                                   "windows_total": weak["windows_total"], "kept_kmers_rank0": weak["counters"]["kept"],
                                   "key_range_passes": weak["passes"]},
-                       "roofline": weak["roofline"], "pipeline": weak["pipeline"],
-                       "pcie_inclusive": _pcie_inclusive(weak, prep2),
-                       "cpu_baseline": cpu and dict(cpu, note="the same bounded sample: the first 1M proteins "
-                                                               "of the C3 proteome are the C2 workload")}
+                       "roofline": weak["roofline"], "pipeline": weak["pipeline"], "chain_tail_ms": weak["chain_tail_ms"],
+                       "pcie_inclusive": _pcie_inclusive(weak, prep2), "cpu_baseline": None}
+        if rank == 0 and world == 1 and not a.no_cpu_baseline:
+            out["weak"]["cpu_baseline"] = _cpu_baseline(
+                c2, len(funcs), a.weak_seqs, a.cpu_threads or cores["usable"], cores,
+                f"the whole C2 workload ({a.weak_seqs:,} proteins, measured, not extrapolated)")
         if world == 1 and queries is not None:
             kept = b.finish()
         b.close()
@@ -318,8 +327,38 @@ def main():
         dist.destroy_process_group()
 
 
+def _alg_bytes(kernel, c, res_bytes):
+    """SURVEY 8(d) algorithmic bytes of one build kernel over one step (all its launches), from the
+    run's counters; None for a kernel without a stated figure.  c = b.counters()."""
+    valid, grouped = c["valid"], c["grouped"]
+    table = {
+        # the group-by: the 16-byte elements it groups + 18 B per k-mer it keeps (the overflow
+        # sub-buckets and the > 64-member groups are other kernels')
+        "k_bucket_process": 16 * (grouped - c["overflow_elements"])
+        + 18 * (c["kept"] - c["overflow_kept"] - c["big_kept"]),
+        "k_partition": 32 * grouped,                       # read + write of each element
+        "k_split_stage": 32 * valid,
+        "k_extract_stage_pos": res_bytes + 16 * valid,     # residues once + the element written
+        "k_extract_stage": res_bytes + 16 * valid,
+        "k_extract_pos": 16 * valid,                       # position + window
+        "k_extract": res_bytes,
+        "k_pass_compact": res_bytes * max(1, c["passes"]) + 8 * valid,  # pass-id bytes + positions
+        "k_pass_ids": 2 * res_bytes,                       # residues read, one id byte written
+        "k_overflow": 16 * c["overflow_elements"],
+        "k_ovf_split": 32 * c["overflow_elements"],
+        "k_heavy": 16 * c["overflow_elements"],
+        "k_chain_long": 4 * c["long_samples"],             # SURVEY 8(d): 4 B per chain sample
+        "k_chains": 4 * c["chain_samples"],
+        "k_kept_finalize": 36 * c["kept"],                 # 18 B per kept k-mer read + written
+    }
+    v = table.get(kernel)
+    return None if v is None or v <= 0 else float(v)
+
+
 def _measure(skm, b, steps, warmup, shard, world, dist):
-    """Warmup, then exactly `steps` timed runs bracketed by barriers; max over ranks."""
+    """Warmup, then one untimed diagnostic run with every kernel launch bracketed by events (the
+    per-kernel GPU time that picks the dominant kernel), then exactly `steps` timed runs bracketed
+    by barriers, events around the dominant kernel's launches only; max over ranks."""
     def barrier():
         if dist is not None:
             dist.barrier()
@@ -327,16 +366,27 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
     for w in range(warmup):
         b.run()
         log(f"warmup {w + 1}/{warmup}")
+    b.set_kernel_timing(True)
+    b.run()
+    ktab = b.kernel_timings()
+    dom = max(ktab, key=lambda k: ktab[k][0]) if ktab else "k_bucket_process"
+    b.set_kernel_timing(True, dom)
+    log(f"dominant kernel by GPU time: {dom} ({ktab.get(dom, (0, 0))[0]:.1f} ms in {ktab.get(dom, (0, 0))[1]} launches)")
     phase = {}
+    dom_ms, dom_n = 0.0, 0
     barrier()
     t1 = time.perf_counter()
     for _ in range(steps):
         b.run()  # returns after the run's final event has completed (device synchronised)
         for k, v in b.timings().items():
             phase[k] = phase.get(k, 0.0) + v
+        kt = b.kernel_timings().get(dom, (0.0, 0))
+        dom_ms += kt[0]
+        dom_n += kt[1]
         log(f"step done ({b.timings()['total']:.1f} ms device)")
     t_local = time.perf_counter() - t1
     barrier()
+    b.set_kernel_timing(False)
     ctrs = b.counters()
     t_max, windows_total = t_local, float(shard.n_windows)
     sums = {"grouped": ctrs["grouped"], "kept": ctrs["kept"], "res": shard.n_residues + shard.n_seqs}
@@ -351,23 +401,18 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
         windows_total = float(v[0])
         sums = {"grouped": int(v[1]), "kept": int(v[2]), "res": int(v[3])}
     phase = {k: v / steps for k, v in phase.items()}
-    # dominant single kernel of this rank (summed over the passes of one step): its algorithmic
-    # bytes -- k_bucket_process: the 16-byte elements it groups + 18 B per k-mer it keeps (the
-    # overflow sub-buckets and the > 64-member groups excluded); k_partition: 32 B per element;
-    # k_extract: 1 B per residue
-    kernels = {"k_extract": "extract_count", "k_partition": "partition", "k_bucket_process": "bucket_kernel"}
-    dom = max(kernels, key=lambda k: phase.get(kernels[k], 0.0))
-    alg = {
-        "k_extract": (shard.n_residues + shard.n_seqs) * max(1, b.passes()),
-        "k_partition": 32 * ctrs["grouped"],
-        "k_bucket_process": 16 * (ctrs["grouped"] - ctrs["overflow_elements"])
-        + 18 * (ctrs["kept"] - ctrs["overflow_kept"] - ctrs["big_kept"]),
-    }
-    dom_ms = phase[kernels[dom]]
-    achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
+    # the dominant kernel (largest GPU time per step over every kernel of the run, measured by the
+    # diagnostic run's events): its algorithmic bytes over its launch time in the timed steps
+    dom_ms_step = dom_ms / steps
+    launches = max(1, dom_n // steps)
+    alg = _alg_bytes(dom, ctrs, shard.n_residues + shard.n_seqs)
+    achieved = alg / (dom_ms_step * 1e-3) / 1e9 if alg and dom_ms_step > 0 else None
+    wl = {50_000_000: "c3", 1_000_000: "c2"}.get(shard.n_seqs, "") if world == 1 else ""
+    traffic = _pmc_traffic(dom, wl, shard.n_seqs)
     # SURVEY 8(d) B_alg over the whole job: 1 B/residue + 32 B/valid window + 18 B/kept k-mer
     pipe_alg = sums["res"] + 32 * sums["grouped"] + 18 * sums["kept"]
     pipe_gbs = pipe_alg / (t_max / steps) / 1e9
+    top = sorted(ktab.items(), key=lambda kv: -kv[1][0])[:14]
     return {
         "value": windows_total * steps / t_max,
         "ms_per_step": 1000.0 * t_max / steps,
@@ -375,15 +420,18 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
         "passes": b.passes(),
         "counters": ctrs,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": _per_launch(_pmc_traffic(dom, {50_000_000: "c3", 1_000_000: "c2"}.get(shard.n_seqs, "")
-                                                         if world == 1 else "", shard.n_seqs), b.passes()),
-                     # one launch per key-range pass: per-launch figures are the step's / passes
-                     # (the ratio -- achieved -- is the same either way)
-                     "alg_bytes_per_launch": alg[dom] / max(1, b.passes()),
-                     "avg_launch_ms": dom_ms / max(1, b.passes()),
-                     "alg_bytes_per_step": alg[dom], "kernel_ms_per_step": dom_ms,
-                     "launches_per_step": max(1, b.passes())},
+                     "frac": achieved / HBM_PEAK_GBS if achieved is not None else None,
+                     "traffic": None if traffic is None else traffic / launches,
+                     "traffic_source": None if traffic is None else f"profiles/{_PMC_FILE} (same libskm sources)",
+                     "alg_bytes_per_launch": None if alg is None else alg / launches,
+                     "avg_launch_ms": dom_ms_step / launches,
+                     "alg_bytes_per_step": alg, "kernel_ms_per_step": dom_ms_step,
+                     "launches_per_step": launches,
+                     "selection": "largest GPU time per step over every kernel launch of the run (event pairs "
+                                  "around each launch in one untimed run); timed: events around this kernel's "
+                                  "launches in the timed steps",
+                     "kernels_ms_per_step": {k: round(v[0], 2) for k, v in top}},
+        "chain_tail_ms": phase.get("chain_tail"),
         "pipeline": {"alg_bytes": pipe_alg, "ms": 1000.0 * t_max / steps, "GBs": pipe_gbs,
                      "frac": pipe_gbs / HBM_PEAK_GBS / max(1, world), "phase_ms_rank0": phase},
     }
@@ -532,8 +580,8 @@ def _matrix_leg(skm, matrix_in, a, device, cores, rank=0, world=1, dist=None):
         w = _windows(ln[:ns])
         cpu = {"value": w / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
                "host": {k: cores[k] for k in ("model", "affinity", "cgroup_quota")},
-               "sample": f"all-vs-all over the first {ns} query proteins ({w} windows; pair work grows with the "
-                         f"square of the sample, so this rate is an upper bound for 100K), {dt:.1f} s, "
+               "sample": f"all-vs-all over the {ns} query proteins ({w} windows, "
+                         f"{dt:.1f} s: the whole C5 workload, measured, not extrapolated), "
                          f"oracle/skm_oracle.cpp oracle_matrix_distance on {threads} host threads"}
         del ob, files
     return {"metric": "query k-mers/sec (lookup + all-vs-all shared signature k-mer counts)",
@@ -555,15 +603,33 @@ def _per_launch(traffic, passes):
     return None if traffic is None else traffic / max(1, passes)
 
 
+_PMC_FILE = "r03_pmc_traffic.json"
+
+
+def src_sha16() -> str:
+    """Hash of libskm's device sources (signature_kmers_amd/csrc/*.hip, *.h): a PMC profile counts
+    for the benched code only if it was taken on the same sources."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    d = os.path.join(ROOT, "signature_kmers_amd", "csrc")
+    for f in sorted(glob.glob(os.path.join(d, "*.hip")) + glob.glob(os.path.join(d, "*.h"))):
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def _pmc_traffic(kernel: str, workload: str, seqs: int):
-    """HBM bytes of `kernel` from the committed rocprofv3 PMC summary (profiles/r02_pmc_traffic.json,
-    tools/gpu_profile_r02.sh + tools/pmc_summary_r02.py): per build run (16 launches at C3, one at
-    C2 -- divided by the passes for the per-launch roofline) or per launch (legs), when it
-    was measured on this kernel and workload size; else None.  Streaming kernels count FETCH_SIZE
-    x2, gather kernels x1 (profiles/r02_fetch_calib.json)."""
-    path = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+    """HBM bytes of `kernel` from the committed rocprofv3 PMC summary (profiles/r03_pmc_traffic.json,
+    tools/gpu_profile_r03.sh + tools/pmc_summary_r03.py): per build run (all launches of a step)
+    or per launch (legs), when it was measured on this kernel and workload size AND on the same
+    device sources as this run (src_sha16); else None.  Streaming kernels count FETCH_SIZE x2,
+    gather kernels x1 (profiles/r02_fetch_calib.json)."""
+    path = os.path.join(ROOT, "profiles", _PMC_FILE)
     try:
         d = json.load(open(path))
+        if d.get("src_sha16") != src_sha16():
+            return None
         wl = d["workloads"][workload]
         if int(wl.get("seqs", wl.get("queries", -1))) != int(seqs):
             return None
@@ -572,10 +638,10 @@ def _pmc_traffic(kernel: str, workload: str, seqs: int):
         return None
 
 
-def _cpu_baseline(shard, nfun, n_sample, threads, cores, seqs_total):
+def _cpu_baseline(shard, nfun, n_sample, threads, cores, what):
     """The CPU port of the build (oracle/skm_oracle.cpp oracle_build_mt: the --n-threads 1 results
     computed on every usable host core -- extract into key-hash shards, per-shard stable sort +
-    group + cut + statistics) on the first n_sample sequences of the same workload."""
+    group + cut + statistics) on the first n_sample sequences of the workload (`what` says which)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref
     nf = (n_sample + PER_FILE - 1) // PER_FILE
@@ -588,10 +654,9 @@ def _cpu_baseline(shard, nfun, n_sample, threads, cores, seqs_total):
     w = oracle_ref.count_windows(l[:n], f[:n])
     return {"value": w / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
             "host": {k: cores[k] for k in ("model", "affinity", "cgroup_quota")},
-            "sample": f"first {n:,} of the {seqs_total:,} sequences of the same workload ({w:,} windows), "
-                      f"{dt:.1f} s, oracle/skm_oracle.cpp oracle_build_mt on {threads} host threads "
-                      f"(every CPU of this job's cgroup quota; --n-threads 1 results, unsorted output like the "
-                      f"reference's hash map)"}
+            "sample": f"{what}: {w:,} windows in {dt:.1f} s, oracle/skm_oracle.cpp oracle_build_mt on {threads} "
+                      f"host threads (every CPU of this job's cgroup quota; --n-threads 1 results, unsorted output "
+                      f"like the reference's hash map)"}
 
 
 if __name__ == "__main__":

@@ -122,6 +122,17 @@ int skm_build_run(skm_build* b);
  * [10]=group-by kernel alone [11]=groups of > 64 members (k_big_groups + append);
  * returns entries written. */
 int skm_build_last_timings(skm_build* b, float* ms, int cap);
+/* [12] of skm_build_last_timings: the long-chain tail -- device time from the end of the last
+ * key-range pass on the group-by stream until the last stashed P^2 / variance chain is done. */
+/* Per-kernel device time (diagnostics and the bench's roofline): with enable != 0 every kernel
+ * launch of a run -- or only the launches of the kernel named `only` (e.g. "k_bucket_process";
+ * NULL = all) -- is bracketed by an event pair on its stream, and after the run's host
+ * synchronisation the durations are summed by kernel name.  skm_build_kernel_timings returns the
+ * number of kernels of the last run and writes, for the first `cap`, the total ms and launch count
+ * and (names != NULL) their names, one per line.  New in this port (the reference has no device
+ * code; its only timing is the stderr phase banners, kmers-build-signatures.cc:178-325). */
+int skm_build_set_kernel_timing(skm_build* b, int enable, const char* only);
+int skm_build_kernel_timings(skm_build* b, char* names, size_t names_cap, float* ms, uint64_t* launches, int cap);
 /* Counters of the last run: [0]=windows [1]=kept (owned by this rank) [2]=overflow sub-buckets
  * [3]=chain jobs [4]=chain samples [5]=sequences [6]=occurrences grouped on this rank
  * [7]=occurrences in overflow sub-buckets [8]=k-mers kept by the overflow path
@@ -132,7 +143,8 @@ int skm_build_last_timings(skm_build* b, float* ms, int cap);
  * scratch, the split path, the stashed long chains -- records its demand and is redone once with
  * the buffers grown; the capacities persist, so later runs on the same input are not)
  * [16..19]=capacities of those buffers (overflow scratch elements, split-path elements, stashed
- * long-chain samples, stashed long jobs) [20..23]=the last run's demands on them;
+ * long-chain samples, stashed long jobs) [20..23]=the last run's demands on them [24]=samples of
+ * the stashed long chains (chains of >= 2^14 samples with key-range passes);
  * totals over the passes of the run; returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Host transport: the rank collectives of a multi-process build run by the caller on host
@@ -206,6 +218,20 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches);
  * this is collective: rank 0 receives every rank's kept k-mers (keys sorted), the other ranks
  * the k-mers they own; the statistics are global on every rank. */
 int skm_build_finish(skm_build* b, skm_kept* out);
+/* The kept k-mers of one output slice: those whose slice hash -- MurmurHash3's fmix64 of the
+ * little-endian key, top slice_bits bits -- equals `slice` (0 <= slice < 2^slice_bits, slice_bits
+ * <= 16; slice_bits 0 = every kept k-mer), keys sorted, with the build's global statistics.  The
+ * 2^slice_bits slices partition the kept set, so a caller streams an output too large for one
+ * host copy slice by slice (the 50M-protein build keeps ~2.9G k-mers).  The reference writes
+ * final.kmers / the .dat from one in-memory KeptKmers map (kmers-build-signatures.cc:198-264);
+ * its order is hash order, so slices written one after another are a valid final.kmers.
+ * n_seqs_with_signature counts sequences (not distinct seq ids).  With world_size > 1: this
+ * rank's own k-mers of the slice (not collective for the keys; distinct_signatures is global). */
+int skm_build_finish_slice(skm_build* b, int slice_bits, uint32_t slice, skm_kept* out);
+/* The last run's per-sequence signature flags (KmerStatistics::seqs_with_a_signature, signature_
+ * build.tcc:275, as a bitmap over the sequences with a kept function in add order; world_size > 1:
+ * every rank's sequences in rank order): min(cap, sequences) bytes of 0/1. */
+int skm_build_signature_flags(skm_build* b, uint8_t* out, uint64_t cap);
 void skm_kept_free(skm_kept* k);
 void skm_build_destroy(skm_build* b);
 

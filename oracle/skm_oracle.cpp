@@ -74,11 +74,16 @@ namespace {
 
 const uint16_t kUndefinedFunction = 0xFFFF;  // kmer_data.h:23
 
-// ok_prot_ (signature_build.h:102-103): 20 amino acids, both cases.
-bool ok_prot(unsigned char c) {
-    static const char* s = "ACDEFGHIKLMNPQRSTVWYacdefghiklmnpqrstvwy";
-    return c != 0 && std::strchr(s, c) != nullptr;
-}
+// ok_prot_ (signature_build.h:102-103): 20 amino acids, both cases.  std::set<unsigned char>::find
+// of the reference as a 256-entry membership table (same answer for every byte).
+struct OkProt {
+    bool t[256] = {};
+    OkProt() {
+        for (const char* s = "ACDEFGHIKLMNPQRSTVWYacdefghiklmnpqrstvwy"; *s; ++s) t[(unsigned char)*s] = true;
+    }
+};
+const OkProt kOkProt;
+inline bool ok_prot(unsigned char c) { return kOkProt.t[c]; }
 
 // double -> unsigned short as gcc/x86-64 emits it (cvttsd2si to a 32-bit int, keep 16 bits);
 // out-of-range doubles give the integer-indefinite value 0x80000000 -> 0.  
@@ -285,12 +290,52 @@ int oracle_build(const uint8_t* residues, const uint64_t* seq_off, const uint32_
 //  by one thread exactly like oracle_build.  Kept k-mers come out in shard order (the
 //  reference's kept_kmers_ is a hash map, unordered); out_keys/out_data must hold every window.
 // --------------------------------------------------------------------------------------------
+// The build restricted to one slice of the key space (checks at sizes the whole build cannot be
+// held in host memory, e.g. the 50M-protein proteome): only windows whose key passes
+// slice_hash(key) >> (64 - sel_bits) == sel are grouped (sel_bits 0 = every window).  Every key's
+// occurrences are all in or all out, so each selected group is exactly the reference's group.
+// Besides the kept k-mers of the slice (at most out_cap; *out_n is the full count) it returns the
+// valid windows of the WHOLE input (*valid_windows, all keys), the largest selected group
+// (*max_group) and, if seq_flags != nullptr, the per-sequence flags of the slice's kept k-mers.
+// slice_hash is MurmurHash3's 64-bit finalizer of the little-endian key (a public function; the
+// product's skm_build_finish_slice selects with the same one).
+static inline uint64_t slice_hash(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+int oracle_build_sel_mt(const uint8_t* residues, const uint64_t* seq_off, const uint32_t* seq_len,
+                        const uint16_t* seq_func, const uint32_t* seq_id, uint64_t n_seqs, uint32_t n_functions,
+                        int n_threads, int sel_bits, uint64_t sel, uint64_t* out_keys, oracle_stored* out_data,
+                        uint64_t out_cap, uint64_t* out_n, uint32_t* distinct_functions, uint32_t* seqs_with_func,
+                        uint64_t* n_seqs_with_signature, uint64_t* distinct_signatures, uint64_t* valid_windows,
+                        uint64_t* max_group, uint8_t* seq_flags);
+
 int oracle_build_mt(const uint8_t* residues, const uint64_t* seq_off, const uint32_t* seq_len,
                     const uint16_t* seq_func, const uint32_t* seq_id, uint64_t n_seqs, uint32_t n_functions,
                     int n_threads, uint64_t* out_keys, oracle_stored* out_data, uint64_t* out_n,
                     uint32_t* distinct_functions, uint32_t* seqs_with_func, uint64_t* n_seqs_with_signature,
                     uint64_t* distinct_signatures) {
+    uint64_t valid = 0, mg = 0;
+    return oracle_build_sel_mt(residues, seq_off, seq_len, seq_func, seq_id, n_seqs, n_functions, n_threads, 0, 0,
+                               out_keys, out_data, ~0ull, out_n, distinct_functions, seqs_with_func,
+                               n_seqs_with_signature, distinct_signatures, &valid, &mg, nullptr);
+}
+
+int oracle_build_sel_mt(const uint8_t* residues, const uint64_t* seq_off, const uint32_t* seq_len,
+                        const uint16_t* seq_func, const uint32_t* seq_id, uint64_t n_seqs, uint32_t n_functions,
+                        int n_threads, int sel_bits, uint64_t sel, uint64_t* out_keys, oracle_stored* out_data,
+                        uint64_t out_cap, uint64_t* out_n, uint32_t* distinct_functions, uint32_t* seqs_with_func,
+                        uint64_t* n_seqs_with_signature, uint64_t* distinct_signatures, uint64_t* valid_windows,
+                        uint64_t* max_group, uint8_t* seq_flags) {
     const int K = 8;
+    auto selected = [sel_bits, sel](uint64_t key) {
+        return sel_bits == 0 || (slice_hash(key) >> (64 - sel_bits)) == sel;
+    };
     const int T = std::max(1, n_threads);
     const int S = 8 * T;  // shards
     auto shard_of = [S](uint64_t k) {
@@ -314,9 +359,11 @@ int oracle_build_mt(const uint8_t* residues, const uint64_t* seq_off, const uint
     }
     std::vector<std::vector<std::vector<Occ>>> parts(T, std::vector<std::vector<Occ>>(S));
     std::vector<std::vector<uint32_t>> swf(T, std::vector<uint32_t>(n_functions, 0));
+    std::vector<uint64_t> nvalid(T, 0);
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t)
         th.emplace_back([&, t]() {
+            uint64_t nv = 0;
             for (uint64_t s = cut[t]; s < cut[t + 1]; ++s) {
                 const uint16_t f = seq_func[s];
                 if (f == kUndefinedFunction) continue;
@@ -330,10 +377,12 @@ int oracle_build_mt(const uint8_t* residues, const uint64_t* seq_off, const uint
                     if (i + 1 >= (uint32_t)K && run >= (uint32_t)K) {
                         const uint32_t w = i + 1 - K;
                         const uint64_t key = load_key(seq + w);
-                        parts[t][shard_of(key)].push_back({key, (uint32_t)s, w});
+                        ++nv;
+                        if (selected(key)) parts[t][shard_of(key)].push_back({key, (uint32_t)s, w});
                     }
                 }
             }
+            nvalid[t] = nv;
         });
     for (auto& x : th) x.join();
     th.clear();
@@ -341,7 +390,7 @@ int oracle_build_mt(const uint8_t* residues, const uint64_t* seq_off, const uint
         std::vector<uint64_t> keys;
         std::vector<oracle_stored> data;
         std::vector<uint32_t> df;
-        uint64_t n_sig = 0;
+        uint64_t n_sig = 0, max_group = 0;
     };
     std::vector<ShardOut> outs(S);
     std::vector<uint8_t> flag(n_seqs, 0);  // sequence has a kept k-mer
@@ -365,6 +414,7 @@ int oracle_build_mt(const uint8_t* residues, const uint64_t* seq_off, const uint
                 while (a < occ.size()) {
                     size_t b = a + 1;
                     while (b < occ.size() && occ[b].key == occ[a].key) ++b;
+                    O.max_group = std::max<uint64_t>(O.max_group, b - a);
                     std::map<uint16_t, int> func_count;
                     int count = 0;
                     for (size_t j = b; j-- > a;) {
@@ -406,14 +456,23 @@ int oracle_build_mt(const uint8_t* residues, const uint64_t* seq_off, const uint
         seqs_with_func[f] = 0;
         for (int t = 0; t < T; ++t) seqs_with_func[f] += swf[t][f];
     }
+    uint64_t mg = 0;
     for (int sh = 0; sh < S; ++sh) {
         ShardOut& O = outs[sh];
-        std::copy(O.keys.begin(), O.keys.end(), out_keys + kept);
-        std::copy(O.data.begin(), O.data.end(), out_data + kept);
+        const uint64_t room = kept < out_cap ? out_cap - kept : 0;
+        const uint64_t c = std::min<uint64_t>(room, O.keys.size());
+        std::copy(O.keys.begin(), O.keys.begin() + c, out_keys + kept);
+        std::copy(O.data.begin(), O.data.begin() + c, out_data + kept);
         kept += O.keys.size();
         n_sig += O.n_sig;
+        mg = std::max(mg, O.max_group);
         for (uint32_t f = 0; f < n_functions; ++f) distinct_functions[f] += O.df[f];
     }
+    uint64_t nv = 0;
+    for (int t = 0; t < T; ++t) nv += nvalid[t];
+    *valid_windows = nv;
+    *max_group = mg;
+    if (seq_flags) std::copy(flag.begin(), flag.end(), seq_flags);
     std::vector<uint32_t> ids;  // seqs_with_a_signature is a set of seq_ids (colliding ids count once)
     for (uint64_t s = 0; s < n_seqs; ++s)
         if (flag[s]) ids.push_back(seq_id[s]);
@@ -421,7 +480,7 @@ int oracle_build_mt(const uint8_t* residues, const uint64_t* seq_off, const uint
     *out_n = kept;
     *n_seqs_with_signature = (uint64_t)(std::unique(ids.begin(), ids.end()) - ids.begin());
     *distinct_signatures = n_sig;
-    return 0;
+    return kept <= out_cap ? 0 : -1;
 }
 
 // Number of windows the build examines (units of the k-mers/s metric): sum over sequences with

@@ -88,7 +88,12 @@ _SIGS = {
     "skm_build_prepare": (C.c_int, [_P]),
     "skm_build_run": (C.c_int, [_P]),
     "skm_build_last_timings": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int]),
+    "skm_build_set_kernel_timing": (C.c_int, [_P, C.c_int, C.c_char_p]),
+    "skm_build_kernel_timings": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.POINTER(C.c_float), C.POINTER(C.c_uint64),
+                                           C.c_int]),
     "skm_build_finish": (C.c_int, [_P, C.POINTER(_Kept)]),
+    "skm_build_finish_slice": (C.c_int, [_P, C.c_int, C.c_uint32, C.POINTER(_Kept)]),
+    "skm_build_signature_flags": (C.c_int, [_P, _P, C.c_uint64]),
     "skm_build_set_option": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "skm_build_set_transport": (C.c_int, [_P, C.POINTER(_Transport)]),
     "skm_debug_exchange_plan": (C.c_int, [C.POINTER(_Transport), C.c_int, C.c_int, C.c_uint32, _P, _P, _P, _P]),
@@ -276,11 +281,27 @@ class SignatureBuilder:
         _check(lib().skm_build_run(self._h))
 
     def timings(self) -> dict:
-        ms = (C.c_float * 12)()
-        n = lib().skm_build_last_timings(self._h, ms, 12)
+        ms = (C.c_float * 13)()
+        n = lib().skm_build_last_timings(self._h, ms, 13)
         names = ["extract_count", "scan", "extract_scatter", "bucket_process", "overflow", "chains", "stats", "total",
-                 "exchange", "partition", "bucket_kernel", "big_groups"]
+                 "exchange", "partition", "bucket_kernel", "big_groups", "chain_tail"]
         return {names[i]: float(ms[i]) for i in range(n)}
+
+    def set_kernel_timing(self, enable: bool, only: str | None = None):
+        """Event pairs around every kernel launch of the next runs (or only kernel `only`)."""
+        _check(lib().skm_build_set_kernel_timing(self._h, 1 if enable else 0, only.encode() if only else None))
+
+    def kernel_timings(self) -> dict:
+        """{kernel name: (total device ms, launches)} of the last run (set_kernel_timing)."""
+        n = lib().skm_build_kernel_timings(self._h, None, 0, None, None, 0)
+        if n <= 0:
+            return {}
+        ms = (C.c_float * n)()
+        cnt = (C.c_uint64 * n)()
+        buf = C.create_string_buffer(64 * n + 64)
+        lib().skm_build_kernel_timings(self._h, buf, len(buf), ms, cnt, n)
+        names = buf.value.decode().split("\n")[:n]
+        return {names[i]: (float(ms[i]), int(cnt[i])) for i in range(n)}
 
     def set_option(self, name: str, value: int):
         """skm_build_set_option: "key_range_passes" (0 = automatic), "device_memory_budget_mb",
@@ -292,12 +313,13 @@ class SignatureBuilder:
         return self.counters()["passes"]
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 24)()
-        n = lib().skm_build_counters(self._h, v, 24)
+        v = (C.c_uint64 * 25)()
+        n = lib().skm_build_counters(self._h, v, 25)
         names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped",
                  "overflow_elements", "overflow_kept", "big_groups", "big_kept", "passes", "valid", "giant_chains",
                  "giant_max", "redone", "cap_overflow_scratch", "cap_split", "cap_long_samples", "cap_long_jobs",
-                 "demand_overflow_scratch", "demand_split", "demand_long_samples", "demand_long_jobs"]
+                 "demand_overflow_scratch", "demand_split", "demand_long_samples", "demand_long_jobs",
+                 "long_samples"]
         return {names[i]: int(v[i]) for i in range(n)}
 
     def debug_jobs(self, k: int = 64) -> list:
@@ -319,6 +341,24 @@ class SignatureBuilder:
     def finish(self) -> KeptKmers:
         k = _Kept()
         _check(lib().skm_build_finish(self._h, C.byref(k)))
+        return self._kept(k)
+
+    def finish_slice(self, slice_bits: int, slice_: int) -> KeptKmers:
+        """skm_build_finish_slice: the kept k-mers whose slice hash (fmix64 of the key, top
+        slice_bits bits) is slice_, keys sorted; statistics are the whole build's."""
+        k = _Kept()
+        _check(lib().skm_build_finish_slice(self._h, int(slice_bits), int(slice_), C.byref(k)))
+        return self._kept(k)
+
+    def signature_flags(self) -> np.ndarray:
+        """Per-sequence signature flags of the last run (sequences with a kept function, add order)."""
+        n = self.counters()["sequences"]
+        out = np.zeros(max(n, 1), np.uint8)
+        _check(lib().skm_build_signature_flags(self._h, _ptr(out), n))
+        return out[:n]
+
+    @staticmethod
+    def _kept(k) -> KeptKmers:
         try:
             n = int(k.n)
             keys = np.ctypeslib.as_array(k.keys, shape=(max(n, 1),))[:n].copy() if n else np.zeros(0, np.uint64)

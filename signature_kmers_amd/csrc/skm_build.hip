@@ -31,6 +31,7 @@
 #include <deque>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "skm_common.h"
@@ -207,6 +208,16 @@ struct SigStats {
 };
 
 constexpr uint32_t REM_MASK = 0x7FFFFFFFu;   // rem <= 31 bits; bit 47 of hi is the big-length flag
+
+// The 43-bit hashed key of an element from its level-1 bucket prefix and its 31-bit rem field.
+// With key-range passes, a heavy k-mer may be grouped in an earlier pass than its hash names
+// (k_pass_ids routes it; pass = top pass_bits of the hash): its rem field then carries (natural
+// pass ^ this pass) above the rem bits, which restores the natural pass bits (pshift = 43 - pass
+// bits); the bits are 0 for every other element.  Grouping compares the whole rem field, so keys
+// routed in from different passes never merge.
+__device__ __forceinline__ uint64_t key_h43(uint64_t hprefix, uint64_t remf, int rem_bits, int pshift) {
+    return (hprefix ^ ((remf >> rem_bits) << pshift)) | (remf & ((1ull << rem_bits) - 1ull));
+}
 
 // protein length of an element: carried mod 2^16 unless the big-length flag is set
 __device__ __forceinline__ uint32_t elem_len(uint64_t hi, uint64_t lo, const uint32_t* __restrict__ glen) {
@@ -684,6 +695,8 @@ enum : uint32_t {
     RUN_DEM_SPLIT = 9,      //   split-path elements,
     RUN_DEM_LONG = 10,      //   stashed samples,
     RUN_DEM_LJOBS = 11,     //   stashed jobs
+    RUN_LONG_WANT = 12,     // stashed samples / jobs asked for by every pass (the fitted ones and
+    RUN_LONG_WANTJ = 13,    //   the ones that did not fit: the demand of a redo)
     RUN_ACC_NOVF = 16,      // run totals
     RUN_ACC_JOBS = 17,
     RUN_ACC_LENS = 18,
@@ -815,12 +828,29 @@ __global__ __launch_bounds__(1024) void k_long_plan(const Job* __restrict__ jobs
             uint64_t base = 0, jbase = 0;
             bool ok = true;
             if (nlong) {
-                base = atomicAdd(&run[RUN_LONG_CUR], (unsigned long long)total);
-                jbase = atomicAdd(&run[RUN_LONG_N], (unsigned long long)nlong);
-                ok = base + total <= arena_cap && jbase + nlong <= jobs_cap;
+                // the run's cursors advance only by reservations that fit (compare-and-swap), so
+                // the long-job list [flushed, RUN_LONG_N) never names a slot k_long_stash skipped;
+                // what every pass asked for accumulates separately as the redo's demand
+                const unsigned long long want = atomicAdd(&run[RUN_LONG_WANT], (unsigned long long)total) + total;
+                const unsigned long long wantj = atomicAdd(&run[RUN_LONG_WANTJ], (unsigned long long)nlong) + nlong;
+                auto reserve = [&](unsigned long long* c, uint64_t n, uint64_t cap, uint64_t& at) {
+                    unsigned long long cur = *(volatile unsigned long long*)c;
+                    while (true) {
+                        if (cur + n > cap) return false;
+                        const unsigned long long seen = atomicCAS(c, cur, cur + n);
+                        if (seen == cur) {
+                            at = cur;
+                            return true;
+                        }
+                        cur = seen;
+                    }
+                };
+                ok = reserve(&run[RUN_LONG_CUR], total, arena_cap, base);
+                // a job-slot failure after the samples fit leaves those samples unused (the run is redone)
+                ok = ok && reserve(&run[RUN_LONG_N], nlong, jobs_cap, jbase);
                 if (!ok) {
-                    atomicMax(&run[RUN_DEM_LONG], (unsigned long long)(base + total));
-                    atomicMax(&run[RUN_DEM_LJOBS], (unsigned long long)(jbase + nlong));
+                    atomicMax(&run[RUN_DEM_LONG], want);
+                    atomicMax(&run[RUN_DEM_LJOBS], wantj);
                     atomicOr(&run[RUN_FLAGS], (unsigned long long)RUN_F_RERUN);
                 }
             }
@@ -854,10 +884,14 @@ __global__ __launch_bounds__(256) void k_long_stash(const Job* __restrict__ jobs
 
 // k_chain_long's job range of a stashed batch: [run's flushed mark, run's job count), then the mark
 // moves (one thread, on the group-by stream after the passes' stashes)
-__global__ void k_long_snap(unsigned long long* __restrict__ run, unsigned long long* __restrict__ range) {
-    range[0] = run[RUN_LONG_FLUSHED];
-    range[1] = run[RUN_LONG_N];
-    run[RUN_LONG_FLUSHED] = range[1];
+__global__ void k_long_snap(unsigned long long* __restrict__ run, unsigned long long* __restrict__ range,
+                            uint64_t jobs_cap) {
+    // RUN_LONG_N only counts stashed jobs (k_long_plan reserves by compare-and-swap); the clamp to
+    // the list's capacity is a second line of defence for k_chain_long, which has no bound check
+    const unsigned long long hi = min(run[RUN_LONG_N], (unsigned long long)jobs_cap);
+    range[0] = min(run[RUN_LONG_FLUSHED], hi);
+    range[1] = hi;
+    run[RUN_LONG_FLUSHED] = hi;
 }
 
 // One chain over x[0..n): blocks of 16 samples; the next block's loads (index clamped, so no
@@ -1387,6 +1421,7 @@ struct ExtractArgs {
     const uint32_t* blk2seq;        // sequence containing packed position 64*b
     const SeqMeta* meta;
     uint32_t s_base;                // global index of this shard's first sequence
+    uint64_t pos_cap;               // key-range passes: capacity of the position list (pass_max)
     uint64_t* out_hi;
     uint64_t* out_lo;
 };
@@ -1407,15 +1442,84 @@ __device__ __forceinline__ uint32_t match16(const uint4 w, uint32_t v) {
 // their union is the single-pass result.  k_pass_ids computes each window's pass id once per
 // run (one scan of the resident residues); each pass's extract kernels then read the id bytes
 // and hash only their own windows.  With counts != nullptr (prepare), it histograms the valid
-// windows by the top 6 hash bits instead, which sizes the passes.
+// windows by pass id -- or, with pass_bits == 0, by the top 6 hash bits, which sizes the passes.
+//
+// Heavy-key routing.  The longest serial work of the build is the P^2 / variance chain of the
+// heaviest k-mers (~10^6 samples at C3: ~0.3 s each); a pass that ends the run with such a chain
+// leaves it as a tail after the last pass.  A Bloom filter of the keys with >= route_heavy_min
+// occurrences (from a sampled count-min sketch at prepare) routes those keys of the second half of
+// the passes into the first half (pass id - P/2), so their chains are stashed early and run beside
+// the remaining passes.  Routing is a function of the key alone, so every occurrence of a k-mer is
+// still in exactly one pass; the element keeps (natural ^ routed pass) above its rem bits
+// (key_h43).  False positives of the filter only move a few light keys too.
 // ------------------------------------------------------------------------------------------
+constexpr int CMS_BITS = 22;        // count-min sketch of sampled windows: 2 rows of 2^22 u32 (32 MB)
+constexpr int BLOOM_BITS = 19;      // Bloom filter of the heavy keys: 2^19 bits (64 KB), two probes
+constexpr int ROUTE_SAMPLE = 6;     // 1 in 2^6 window positions are sampled
+
+__device__ __forceinline__ uint32_t cms_slot(uint64_t h, int row) {
+    return row == 0 ? (uint32_t)(h & ((1u << CMS_BITS) - 1u)) : (uint32_t)((h >> 21) & ((1u << CMS_BITS) - 1u));
+}
+__device__ __forceinline__ bool bloom_has(const uint32_t* bloom, uint64_t h) {
+    const uint32_t b1 = (uint32_t)(h & ((1u << BLOOM_BITS) - 1u));
+    const uint32_t b2 = (uint32_t)((h >> 24) & ((1u << BLOOM_BITS) - 1u));
+    return ((bloom[b1 >> 5] >> (b1 & 31u)) & (bloom[b2 >> 5] >> (b2 & 31u)) & 1u) != 0;
+}
+
+// mix43 of the (valid) window at packed position p, or ~0 when the window is not valid
+__device__ __forceinline__ uint64_t sampled_hash(const uint8_t* __restrict__ res, uint64_t p, uint64_t rp) {
+    if (p >= rp) return ~0ull;
+    const uint64_t a = p & ~7ull;  // the buffer is padded past rp
+    const uint32_t sh = (uint32_t)(p & 7u) * 8u;
+    const uint64_t w0 = *reinterpret_cast<const uint64_t*>(res + a);
+    const uint64_t w1 = *reinterpret_cast<const uint64_t*>(res + a + 8);
+    const uint64_t raw = sh ? (w0 >> sh) | (w1 << (64u - sh)) : w0;
+    uint64_t k = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t cd = residue_code((uint32_t)((raw >> (8 * j)) & 0xFFu));
+        if (cd >= 40u) return ~0ull;
+        k = k * 40u + cd;
+    }
+    return mix43(k);
+}
+
+// sketch (bloom == nullptr): count the sampled windows of every key into both rows;
+// bloom pass: keys whose estimate (the smaller row) reaches `thresh` set their two filter bits
+__global__ __launch_bounds__(256) void k_route_sketch(const uint8_t* __restrict__ res, uint64_t rp,
+                                                      uint32_t* __restrict__ cms, uint32_t thresh,
+                                                      uint32_t* __restrict__ bloom) {
+    const uint64_t ns = (rp + (1u << ROUTE_SAMPLE) - 1) >> ROUTE_SAMPLE;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t h = sampled_hash(res, i << ROUTE_SAMPLE, rp);
+        if (h == ~0ull) continue;
+        uint32_t* r0 = cms + cms_slot(h, 0);
+        uint32_t* r1 = cms + (1u << CMS_BITS) + cms_slot(h, 1);
+        if (!bloom) {
+            atomicAdd(r0, 1u);
+            atomicAdd(r1, 1u);
+        } else if (min(*r0, *r1) >= thresh) {
+            const uint32_t b1 = (uint32_t)(h & ((1u << BLOOM_BITS) - 1u));
+            const uint32_t b2 = (uint32_t)((h >> 24) & ((1u << BLOOM_BITS) - 1u));
+            atomicOr(&bloom[b1 >> 5], 1u << (b1 & 31u));
+            atomicOr(&bloom[b2 >> 5], 1u << (b2 & 31u));
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ res, uint64_t rp, int pass_bits,
-                                                  uint8_t* __restrict__ ids, unsigned long long* __restrict__ counts) {
+                                                  uint8_t* __restrict__ ids, unsigned long long* __restrict__ counts,
+                                                  const uint32_t* __restrict__ bloom) {
     __shared__ uint32_t s_cnt[64];
+    extern __shared__ uint32_t s_bloom[];  // (1 << BLOOM_BITS) / 32 words when routing
     if (counts) {
         if (threadIdx.x < 64) s_cnt[threadIdx.x] = 0;
-        __syncthreads();
     }
+    const bool route = bloom != nullptr && pass_bits >= 1;
+    if (route)
+        for (uint32_t w = threadIdx.x; w < (1u << BLOOM_BITS) / 32u; w += blockDim.x) s_bloom[w] = bloom[w];
+    __syncthreads();
+    const uint32_t half = pass_bits >= 1 ? 1u << (pass_bits - 1) : 0u;
     const uint64_t nchunk = (rp + 15) >> 4;
     for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunk; c += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t base = c << 4;
@@ -1441,10 +1545,13 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
             uint32_t id = 0xFFu;
             if (((valid >> t) & 0xFFu) == 0xFFu && base + t < rp) {
                 const uint64_t h = mix43(k);
-                if (counts)
-                    atomicAdd(&s_cnt[(uint32_t)(h >> (KEY_BITS - 6))], 1u);
-                else
+                if (pass_bits == 0) {
+                    if (counts) atomicAdd(&s_cnt[(uint32_t)(h >> (KEY_BITS - 6))], 1u);
+                } else {
                     id = (uint32_t)(h >> (KEY_BITS - pass_bits));
+                    if (route && id >= half && bloom_has(s_bloom, h)) id -= half;
+                    if (counts) atomicAdd(&s_cnt[id], 1u);
+                }
             }
             out[t >> 2] |= id << (8 * (t & 3));
         }
@@ -1512,7 +1619,8 @@ __global__ __launch_bounds__(EX_THREADS) void k_extract(ExtractArgs X) {
 constexpr int CP_THREADS = 256, CP_PER_THREAD = 128;  // 32768 windows per workgroup
 __global__ __launch_bounds__(CP_THREADS) void k_pass_compact(const uint8_t* __restrict__ ids, uint64_t rp, uint32_t pass,
                                                              uint64_t* __restrict__ pos,
-                                                             unsigned long long* __restrict__ cursor, uint64_t cap) {
+                                                             unsigned long long* __restrict__ cursor, uint64_t cap,
+                                                             unsigned long long* __restrict__ run) {
     __shared__ uint32_t s_wave[CP_THREADS / 64 + 1];
     __shared__ unsigned long long s_base;
     const uint64_t base = (uint64_t)blockIdx.x * CP_THREADS * CP_PER_THREAD + (uint64_t)threadIdx.x * CP_PER_THREAD;
@@ -1526,9 +1634,14 @@ __global__ __launch_bounds__(CP_THREADS) void k_pass_compact(const uint8_t* __re
     }
     uint32_t tot;
     uint32_t off = wg_exclusive_scan(cnt, s_wave, tot);
-    if (threadIdx.x == 0) s_base = tot ? atomicAdd(cursor, (unsigned long long)tot) : 0ull;
+    if (threadIdx.x == 0) {
+        s_base = tot ? atomicAdd(cursor, (unsigned long long)tot) : 0ull;
+        // the pass sizes were counted at prepare with the same hash, so the cursor stays below cap;
+        // if it ever does not, the run fails (SKM_E_STATE) instead of losing occurrences
+        if (s_base + tot > cap) atomicOr(&run[RUN_FLAGS], (unsigned long long)RUN_F_CAP);
+    }
     __syncthreads();
-    uint64_t o = s_base + off;  // the pass sizes were counted at prepare with the same hash: o < cap
+    uint64_t o = s_base + off;
 #pragma unroll
     for (int k = 0; k < CP_PER_THREAD / 16; ++k)
         for (uint32_t w = m[k]; w; w &= w - 1, ++o)
@@ -1555,7 +1668,9 @@ __device__ __forceinline__ uint64_t window_hash(uint64_t raw) {
 // count pass over this pass's positions pos[0..n): per-workgroup level-1 bucket histogram
 __global__ __launch_bounds__(EX_THREADS) void k_extract_pos(ExtractArgs X, const uint64_t* __restrict__ pos,
                                                              const unsigned long long* __restrict__ np) {
-    const uint64_t n = *np;  // this pass's window count (k_pass_compact's cursor): no host round trip
+    // this pass's window count (k_pass_compact's cursor; no host round trip), clamped to the list's
+    // capacity (a larger cursor already failed the run with RUN_F_CAP)
+    const uint64_t n = min((uint64_t)*np, X.pos_cap);
     extern __shared__ uint32_t s_cnt[];  // [NB]
     const int nbits = X.owner_bits + X.b1_bits;
     const uint32_t NB = 1u << nbits;
@@ -1710,7 +1825,7 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage_pos(ExtractArgs
                                                                      unsigned long long* __restrict__ cur0,
                                                                      uint64_t* __restrict__ out_hi,
                                                                      uint64_t* __restrict__ out_lo) {
-    const uint64_t n = *np;
+    const uint64_t n = min((uint64_t)*np, X.pos_cap);
     __shared__ StageLds L;
     const int nbits = X.owner_bits + X.b1_bits;
     const uint32_t NB = 1u << nbits;
@@ -1746,7 +1861,9 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage_pos(ExtractArgs
                 while (p > m.pstart + m.len) m = X.meta[++s];
                 const uint64_t h = window_hash(raw[t]);
                 const uint32_t bucket = (uint32_t)(h >> rem_bits) & (NB - 1);
-                make_elem(h & rem_mask, X.s_base + s, (uint32_t)(p - m.pstart), m, eh[t], el[t]);
+                // a heavy key routed in from a later pass keeps (natural ^ this pass) above its rem
+                const uint64_t route = (uint64_t)((uint32_t)(h >> (KEY_BITS - X.pass_bits)) ^ X.pass_id) << rem_bits;
+                make_elem((h & rem_mask) | route, X.s_base + s, (uint32_t)(p - m.pstart), m, eh[t], el[t]);
                 el[t] = (el[t] & ~0xFFFFull) | bucket;  // bucket id rides in the offset field until pass 2
                 l0[t] = bucket >> l0_shift;
                 rk[t] = atomicAdd(&L.cnt[l0[t]], 1u);
@@ -1971,6 +2088,7 @@ struct BucketArgs {
     uint64_t* big_desc;        // [big_cap][2] groups of > 64 members handed to k_big_groups
     uint32_t big_cap;
     int prio;                  // wave issue priority of the group-by (above the concurrent chains)
+    int pshift;                // KEY_BITS - pass bits (key_h43)
     const uint32_t* skip;      // k_ovf_plan's verdict for the pass (nonzero: the run is being abandoned)
 };
 
@@ -2177,7 +2295,7 @@ __device__ __forceinline__ void seg_groups(const SubLds& L, uint32_t q0, uint32_
         r.avg = avg;
         r.mean = d2u16((double)(uint16_t)sum / (double)cbest);
         stats_small(r, x0, cbest == 2 ? x1 : 0u, cbest);
-        const uint64_t h43 = hprefix | ((L.hi[rep] >> 16) & REM_MASK);
+        const uint64_t h43 = key_h43(hprefix, (L.hi[rep] >> 16) & REM_MASK, A.rem_bits, A.pshift);
         L.hi[rep] = kept_hi(h43, r.avg);
         if (cbest >= 3) {
             jobinfo[rep] = (a << 16) | JOB_KEPT | cbest;  // chain lengths at lens32[2a..2a+cbest)
@@ -2255,7 +2373,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         } else if (in && cnt == 1) {  // group of one: always kept (1 >= 0.8), median 0, var 0
             const uint64_t H = L.hi[j], Lo = L.lo[j];
             A.flags[Lo >> 36] = 1;
-            L.hi[j] = kept_hi(hprefix | ((H >> 16) & REM_MASK), (uint32_t)(Lo & 0xFFFFu));
+            L.hi[j] = kept_hi(key_h43(hprefix, (H >> 16) & REM_MASK, A.rem_bits, A.pshift), (uint32_t)(Lo & 0xFFFFu));
             L.lo[j] = kept_lo((uint32_t)(H & 0xFFFFu), d2u16((double)(uint16_t)(H >> 48) / 1.0), 0, 0);
             L.rank[j] = 0xFFFFu;  // singleton marker
         }
@@ -2361,7 +2479,8 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
             }
             const uint64_t q = bbase + bi;
             if (lane == 0 && q < A.big_cap) {
-                A.big_desc[2 * q] = (hprefix | ((L.hi[rep] >> 16) & REM_MASK)) | ((uint64_t)c << KEY_BITS);
+                A.big_desc[2 * q] = key_h43(hprefix, (L.hi[rep] >> 16) & REM_MASK, A.rem_bits, A.pshift) |
+                                    ((uint64_t)c << KEY_BITS);
                 A.big_desc[2 * q + 1] = L.lens_sel + 2 * a;
             }
         }
@@ -3027,7 +3146,7 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
         const GlbView V{ghi, glo};
         auto stage = [&](const GRes& r, uint32_t a) {
             if (!r.kept) return;
-            const uint64_t h43 = hprefix | (ghi[a] >> 16);
+            const uint64_t h43 = key_h43(hprefix, ghi[a] >> 16, A.rem_bits, A.pshift);
             if (r.cbest >= 3) {
                 jobinfo[a] = ((uint64_t)(a + r.rb) << 32) | r.cbest;
                 fmean[a] = r.best_f | ((uint32_t)r.mean << 16);
@@ -3688,7 +3807,7 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
             }
         }
         if (tid == 0) {
-            const uint64_t h43 = ((uint64_t)(A.bucket_base + K.bucket) << A.rem_bits) | K.rem;
+            const uint64_t h43 = key_h43((uint64_t)(A.bucket_base + K.bucket) << A.rem_bits, K.rem, A.rem_bits, A.pshift);
             write_kept(A, o, kept_hi(h43, pre), kept_lo(best_f, mean, 0, 0));
             Job jbr;
             jbr.n = cb;
@@ -3831,6 +3950,16 @@ __global__ __launch_bounds__(1024) void k_ovf_plan(PlanArgs P) {
 
 // end of a pass (one thread, after both overflow streams joined): run totals and the bounds the
 // chain lists rely on
+// tests (poison_jobs): every slot of the stashed long-job list holds a canary job whose output
+// record is the arena's spare slot at index `idx` (past the kept capacity); k_chain_long reaching a
+// slot k_long_stash did not write would overwrite the canary record, which phase_final checks
+__global__ void k_poison_jobs(Job* __restrict__ jobs, uint64_t n, uint64_t samples, uint32_t idx,
+                             skm_stored_kmer_data* __restrict__ out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t j = t; j < n; j += (uint64_t)gridDim.x * blockDim.x) jobs[j] = Job{samples, 8u, idx};
+    if (t == 0) out[idx] = skm_stored_kmer_data{0xC0DE, 0xC0DE, 0xC0DE, 0xC0DE, 0xC0DE};
+}
+
 __global__ void k_pass_account(const unsigned long long* __restrict__ ctr, unsigned long long* __restrict__ run,
                                uint64_t jobs_cap, uint64_t jobs2_cap, uint64_t big_cap, uint64_t lens_cap) {
     const unsigned long long j = ctr[3] + ctr[8 + 3];
@@ -3900,6 +4029,32 @@ __global__ void k_count_flags(const uint8_t* __restrict__ flags, uint32_t nseq, 
     if ((threadIdx.x & 63) == 0 && local) atomicAdd(out, (unsigned long long)local);
 }
 
+// skm_build_finish_slice: kept k-mers of one output slice (top bits of slice_hash(key)), compacted
+// in any order (the host sorts them); count first, then the copy into the slice's own buffers
+__global__ __launch_bounds__(256) void k_slice_select(const uint64_t* __restrict__ keys,
+                                                      const skm_stored_kmer_data* __restrict__ data, uint64_t n,
+                                                      int bits, uint64_t slice, unsigned long long* __restrict__ cursor,
+                                                      uint64_t* __restrict__ out_keys,
+                                                      skm_stored_kmer_data* __restrict__ out_data) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < n; b0 += stride) {
+        const uint64_t j = b0 + threadIdx.x;
+        const uint64_t k = j < n ? keys[j] : 0ull;
+        const bool in = j < n && (bits == 0 || (slice_hash(k) >> (64 - bits)) == slice);
+        const uint64_t m = __ballot(in);
+        if (!m) continue;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(cursor, (unsigned long long)__popcll(m));
+        base = __shfl(base, 0, 64);
+        if (in && out_keys) {
+            const uint64_t o = base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+            out_keys[o] = k;
+            out_data[o] = data[j];
+        }
+    }
+}
+
 // Build options beyond skm_build_opts: the key-range pass count and device-memory budget
 // (skm_build_set_option), and diagnostic tunables kept at their tuned defaults in production.
 struct Tune {
@@ -3930,6 +4085,9 @@ struct Tune {
     int stream_prio = 0;             // 1: the group-by stream at the highest priority
     int chain_batches = 4;           // key-range passes: stashed long chains leave in this many batches
     int chain_streams = 1;           //   over this many streams (1..4)
+    int poison_jobs = 0;             // tests: every slot of the run's long-job list starts as a canary job
+    int route_heavy_min = 1 << 16;   // key-range passes: k-mers of >= this many occurrences are routed into
+                                     //   the first half of the passes (0: off; k_pass_ids)
 };
 
 }  // namespace skm
@@ -3955,7 +4113,7 @@ struct skm_build {
     hipEvent_t* ev = nullptr;           // the current pass's set
     hipEvent_t* ev_o = nullptr;
     hipEvent_t* ev_o3 = nullptr;
-    float last_ms[12] = {};
+    float last_ms[13] = {};
     uint64_t ovf_elems = 0, ovf_kept = 0;
 
     // host staging (reference emission order, only sequences with a kept function)
@@ -4051,6 +4209,8 @@ struct skm_build {
     uint64_t pass_max = 0;              // valid windows of the largest pass (this shard)
     uint64_t valid_total = 0;           // valid windows of this shard
     DevBuf d_ids;                       // per-window pass id (pass_bits > 0)
+    DevBuf d_bloom;                     // heavy-key routing filter (route)
+    bool route = false;
     // a pass's window positions, level-1 histogram matrix and window count, double-buffered: the
     // next pass's compaction + count run on stx during this pass's group-by (prefetch_pass)
     DevBuf d_pos2[2], d_hist2[2], d_npos;
@@ -4088,9 +4248,71 @@ struct skm_build {
     // capacities of the data-dependent work buffers (alloc_caps), grown to a run's demand
     uint64_t tot_cap = 0, split_cap = 0, long_cap = 0;
     uint64_t run_flags = 0, demand[4] = {}, n_jobs_last = 0, n_redo = 0;
+    uint64_t long_samples = 0;          // samples of the stashed long chains (last run)
+    // per-kernel device time (skm_build_set_kernel_timing): an event pair around every launch of
+    // the run (or of one kernel), summed by kernel name after the step's host synchronisation
+    int kt_mode = 0;
+    std::string kt_only;
+    std::vector<hipEvent_t> kt_pool;
+    size_t kt_used = 0;
+    struct KtRec {
+        const char* name;
+        size_t e0;
+    };
+    std::vector<KtRec> kt_recs;
+    std::vector<std::string> kt_names;  // last run: kernel names, total ms, launches
+    std::vector<double> kt_ms;
+    std::vector<uint64_t> kt_n;
+    // the long-chain tail: from the end of the last pass on the group-by stream to the last chain
+    hipEvent_t ev_tail[2] = {};
 };
 
 namespace {
+
+// SKM_LAUNCH: hipLaunchKernelGGL with the launch bracketed by an event pair when kernel timing is
+// on for this kernel (skm_build_set_kernel_timing); otherwise exactly the launch
+int kt_begin(skm_build* b, const char* name, hipStream_t st) {
+    if (!b->kt_mode || (!b->kt_only.empty() && b->kt_only != name)) return -1;
+    while (b->kt_pool.size() < b->kt_used + 2) {
+        hipEvent_t e;
+        SKM_HIP(hipEventCreate(&e));
+        b->kt_pool.push_back(e);
+    }
+    const size_t e0 = b->kt_used;
+    b->kt_used += 2;
+    SKM_HIP(hipEventRecord(b->kt_pool[e0], st));
+    b->kt_recs.push_back({name, e0});
+    return (int)e0;
+}
+void kt_end(skm_build* b, int e0, hipStream_t st) {
+    if (e0 >= 0) SKM_HIP(hipEventRecord(b->kt_pool[(size_t)e0 + 1], st));
+}
+#define SKM_LAUNCH(B, K, G, BL, LDS, ST, ...)                   \
+    do {                                                        \
+        const int _kt = kt_begin((B), #K, (ST));                \
+        hipLaunchKernelGGL(K, G, BL, LDS, ST, __VA_ARGS__);     \
+        kt_end((B), _kt, (ST));                                 \
+    } while (0)
+
+// after the step's synchronisation: per-kernel totals of the run
+void kt_collect(skm_build* b) {
+    b->kt_names.clear();
+    b->kt_ms.clear();
+    b->kt_n.clear();
+    for (const auto& r : b->kt_recs) {
+        float t = 0.f;
+        SKM_HIP(hipEventElapsedTime(&t, b->kt_pool[r.e0], b->kt_pool[r.e0 + 1]));
+        size_t k = 0;
+        while (k < b->kt_names.size() && b->kt_names[k] != r.name) ++k;
+        if (k == b->kt_names.size()) {
+            b->kt_names.emplace_back(r.name);
+            b->kt_ms.push_back(0.0);
+            b->kt_n.push_back(0);
+        }
+        b->kt_ms[k] += t;
+        b->kt_n[k] += 1;
+    }
+}
 
 __global__ void k_abs_starts(const uint32_t* rel, const uint64_t* ost, uint32_t NB, int b1_bits, uint32_t nowners,
                              uint64_t* out) {
@@ -4454,13 +4676,15 @@ void prepare_local(skm_build* b) {
 // per-pass work buffers (~PASS_BYTES per element) leave room for the kept arena (18 B per kept
 // k-mer, accumulated over all passes).
 constexpr uint64_t PASS_BYTES = 104;   // recs 16 + tmp 16 + received 16 (world > 1) + chain lens/jobs ~10 + overflow scratch ~40
-void size_passes(skm_build* b) {
+// forced_pb >= 0: the pass count the ranks agreed on (prepare), which leaves the caller's
+// key_range_passes option as it was set
+void size_passes(skm_build* b, int forced_pb = -1) {
     DevBuf d_cnt;
     d_cnt.ensure(8 * 64);
     SKM_HIP(hipMemsetAsync(d_cnt.p, 0, 8 * 64, b->stream));
     if (b->rp)
         hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 0, b->stream, b->d_res.as<uint8_t>(), b->rp, 0,
-                           nullptr, d_cnt.as<unsigned long long>());
+                           nullptr, d_cnt.as<unsigned long long>(), nullptr);
     SKM_HIP(hipGetLastError());
     uint64_t cnt[64];
     SKM_HIP(hipMemcpyAsync(cnt, d_cnt.p, sizeof(cnt), hipMemcpyDeviceToHost, b->stream));
@@ -4481,7 +4705,9 @@ void size_passes(skm_build* b) {
     SKM_HIP(hipMemGetInfo(&fr, &tot));
     const uint64_t budget = b->tune.mem_budget_mb > 0 ? (uint64_t)b->tune.mem_budget_mb << 20 : (uint64_t)fr;
     int pb = 0;
-    if (b->tune.passes > 0) {
+    if (forced_pb >= 0) {
+        pb = forced_pb;
+    } else if (b->tune.passes > 0) {
         while ((1 << pb) < b->tune.passes) ++pb;
     } else {
         // up to a quarter of the elements may sit in one pass's received buffer after the
@@ -4496,6 +4722,32 @@ void size_passes(skm_build* b) {
     SKM_CHECK(pb <= 6, SKM_E_ARG, "key_range_passes must be a power of two <= 64");
     b->pass_bits = pb;
     b->pass_max = pass_max(pb);
+    // heavy-key routing (one GPU, at least 4 passes): the count-min sketch of 1/64 of the windows,
+    // the Bloom filter of the keys whose estimate reaches route_heavy_min / 64 (with 15 % slack),
+    // then the pass sizes once more, by routed pass id
+    b->route = false;
+    if (pb >= 2 && b->world == 1 && b->tune.route_heavy_min > 0 && b->rp) {
+        DevBuf cms;
+        cms.ensure(4ull << (CMS_BITS + 1));
+        b->d_bloom.ensure((1u << BLOOM_BITS) / 8);
+        SKM_HIP(hipMemsetAsync(cms.p, 0, 4ull << (CMS_BITS + 1), b->stream));
+        SKM_HIP(hipMemsetAsync(b->d_bloom.p, 0, (1u << BLOOM_BITS) / 8, b->stream));
+        const uint32_t thresh = std::max<uint32_t>(8, (uint32_t)(((uint64_t)b->tune.route_heavy_min >> ROUTE_SAMPLE) * 85 / 100));
+        hipLaunchKernelGGL(k_route_sketch, dim3(2048), dim3(256), 0, b->stream, b->d_res.as<uint8_t>(), b->rp,
+                           cms.as<uint32_t>(), 0u, nullptr);
+        hipLaunchKernelGGL(k_route_sketch, dim3(2048), dim3(256), 0, b->stream, b->d_res.as<uint8_t>(), b->rp,
+                           cms.as<uint32_t>(), thresh, b->d_bloom.as<uint32_t>());
+        SKM_HIP(hipMemsetAsync(d_cnt.p, 0, 8 * 64, b->stream));
+        hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), (1u << BLOOM_BITS) / 8, b->stream, b->d_res.as<uint8_t>(),
+                           b->rp, pb, nullptr, d_cnt.as<unsigned long long>(), b->d_bloom.as<uint32_t>());
+        SKM_HIP(hipGetLastError());
+        SKM_HIP(hipMemcpyAsync(cnt, d_cnt.p, sizeof(cnt), hipMemcpyDeviceToHost, b->stream));
+        SKM_HIP(hipStreamSynchronize(b->stream));
+        uint64_t m = 0;
+        for (int p = 0; p < (1 << pb); ++p) m = std::max<uint64_t>(m, cnt[p]);
+        b->pass_max = m;
+        b->route = true;
+    }
     SKM_CHECK(b->pass_max < (1ull << 32), SKM_E_ARG, "more than 2^32 occurrences in one pass of one GPU shard");
 }
 
@@ -4590,10 +4842,7 @@ void prepare(const Ranks& bs) {
         uint64_t pb = 0;
         for (auto v : all) pb = std::max(pb, v);
         for (auto* b : bs) {
-            if ((uint64_t)b->pass_bits != pb) {
-                b->tune.passes = 1 << pb;
-                size_passes(b);
-            }
+            if ((uint64_t)b->pass_bits != pb) size_passes(b, (int)pb);
             size_local(b);
         }
     }
@@ -4682,9 +4931,9 @@ void prefetch_pass(skm_build* b, uint32_t pass, hipStream_t st) {
     const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
     unsigned long long* np = b->d_npos.as<unsigned long long>() + k;
     SKM_HIP(hipMemsetAsync(np, 0, 8, st));
-    hipLaunchKernelGGL(k_pass_compact, dim3((uint32_t)ceil_div(b->rp, (uint64_t)CP_THREADS * CP_PER_THREAD)),
+    SKM_LAUNCH(b, k_pass_compact, dim3((uint32_t)ceil_div(b->rp, (uint64_t)CP_THREADS * CP_PER_THREAD)),
                        dim3(CP_THREADS), 0, st, b->d_ids.as<uint8_t>(), b->rp, pass, b->d_pos2[k].as<uint64_t>(), np,
-                       b->pass_max);
+                       b->pass_max, b->d_run.as<unsigned long long>());
     ExtractArgs X{};
     X.res = b->d_res.as<uint8_t>();
     X.rp = b->rp;
@@ -4693,8 +4942,9 @@ void prefetch_pass(skm_build* b, uint32_t pass, hipStream_t st) {
     X.b1_bits = b->b1_bits;
     X.pass_bits = b->pass_bits;
     X.pass_id = pass;
+    X.pos_cap = b->pass_max;
     X.hist = b->d_hist2[k].as<uint32_t>();
-    hipLaunchKernelGGL(k_extract_pos, dim3(b->pf_nwg), dim3(EX_THREADS), sizeof(uint32_t) * NB, st, X,
+    SKM_LAUNCH(b, k_extract_pos, dim3(b->pf_nwg), dim3(EX_THREADS), sizeof(uint32_t) * NB, st, X,
                        b->d_pos2[k].as<uint64_t>(), np);
     SKM_HIP(hipGetLastError());
     if (st != b->stream) SKM_HIP(hipEventRecord(b->ev_pf_done[k], st));
@@ -4717,6 +4967,7 @@ void phase_extract(skm_build* b, uint32_t pass) {
     X.b1_bits = b->b1_bits;
     X.pass_bits = b->pass_bits;
     X.pass_id = pass;
+    X.pos_cap = b->pass_max;
     X.ids = b->pass_bits ? b->d_ids.as<uint8_t>() : nullptr;
     X.hist = b->d_hist.as<uint32_t>();
     X.offs = b->d_offs.as<uint32_t>();
@@ -4741,19 +4992,19 @@ void phase_extract(skm_build* b, uint32_t pass) {
         nwg = b->pf_nwg;
         (void)lds_cnt;
     } else {
-        hipLaunchKernelGGL(k_extract, dim3(nwg), dim3(EX_THREADS), lds_cnt, st, X);
+        SKM_LAUNCH(b, k_extract, dim3(nwg), dim3(EX_THREADS), lds_cnt, st, X);
     }
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[1], st));
     // ---- 2. scan ----
     const uint32_t nrb = (uint32_t)ceil_div(nwg, SCAN_ROWS);
     dim3 gsc((NB + 255) / 256, nrb);
-    hipLaunchKernelGGL(k_colsum, gsc, dim3(256), 0, st, X.hist, nwg, NB, b->d_partial.as<uint32_t>());
-    hipLaunchKernelGGL(k_bstart, dim3(1), dim3(1024), 0, st, b->d_partial.as<uint32_t>(), nrb, NB, b->b1_bits,
+    SKM_LAUNCH(b, k_colsum, gsc, dim3(256), 0, st, X.hist, nwg, NB, b->d_partial.as<uint32_t>());
+    SKM_LAUNCH(b, k_bstart, dim3(1), dim3(1024), 0, st, b->d_partial.as<uint32_t>(), nrb, NB, b->b1_bits,
                        b->d_rbbase.as<uint32_t>(), b->d_bstart32.as<uint32_t>(), b->d_owner_start.as<uint64_t>(), nowners);
-    hipLaunchKernelGGL(k_coloffs, gsc, dim3(256), 0, st, X.hist, b->d_rbbase.as<uint32_t>(), nwg,
+    SKM_LAUNCH(b, k_coloffs, gsc, dim3(256), 0, st, X.hist, b->d_rbbase.as<uint32_t>(), nwg,
                        NB, b->d_offs.as<uint32_t>());
-    hipLaunchKernelGGL(k_abs_starts, dim3((NB + 1 + 255) / 256), dim3(256), 0, st, b->d_bstart32.as<uint32_t>(),
+    SKM_LAUNCH(b, k_abs_starts, dim3((NB + 1 + 255) / 256), dim3(256), 0, st, b->d_bstart32.as<uint32_t>(),
                        b->d_owner_start.as<uint64_t>(), NB, b->b1_bits, nowners, b->d_bstart.as<uint64_t>());
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[2], st));
@@ -4762,17 +5013,17 @@ void phase_extract(skm_build* b, uint32_t pass) {
     b->d_cur0.ensure(8 * 64);
     b->d_cur1.ensure(8ull * NB);
     b->d_slices.ensure(4 * 80);
-    hipLaunchKernelGGL(k_stage_init, dim3((NB + 255) / 256), dim3(256), 0, st, b->d_bstart.as<uint64_t>(), NB, l0_shift,
+    SKM_LAUNCH(b, k_stage_init, dim3((NB + 255) / 256), dim3(256), 0, st, b->d_bstart.as<uint64_t>(), NB, l0_shift,
                        b->d_cur0.as<unsigned long long>(), b->d_cur1.as<unsigned long long>(), b->d_slices.as<uint32_t>());
     if (b->pass_bits)
-        hipLaunchKernelGGL(k_extract_stage_pos, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_pos2[pass & 1].as<uint64_t>(),
+        SKM_LAUNCH(b, k_extract_stage_pos, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_pos2[pass & 1].as<uint64_t>(),
                            b->d_npos.as<unsigned long long>() + (pass & 1), b->d_cur0.as<unsigned long long>(),
                            b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
     else
-        hipLaunchKernelGGL(k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
+        SKM_LAUNCH(b, k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
                            b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
     const uint32_t nsl = (uint32_t)(ceil_div(b->pass_max, SC_SLICE) + (1u << SC_L0_BITS));
-    hipLaunchKernelGGL(k_split_stage, dim3(nsl), dim3(EX_THREADS), 0, st, b->d_tmp_hi.as<uint64_t>(),
+    SKM_LAUNCH(b, k_split_stage, dim3(nsl), dim3(EX_THREADS), 0, st, b->d_tmp_hi.as<uint64_t>(),
                        b->d_tmp_lo.as<uint64_t>(), b->d_bstart.as<uint64_t>(), nbits, b->d_slices.as<uint32_t>(),
                        b->d_cur1.as<unsigned long long>(), b->d_recs_hi.as<uint64_t>(), b->d_recs_lo.as<uint64_t>());
     SKM_HIP(hipGetLastError());
@@ -4870,10 +5121,10 @@ void launch_chains(skm_build* b, hipStream_t st, const Job* jobs, const unsigned
                    const uint32_t* big32, skm_stored_kmer_data* out, uint32_t long_class,
                    hipStream_t st_short = nullptr, hipEvent_t ev_sorted = nullptr, uint32_t max_wgs = 0) {
     const Tune& tn = b->tune;
-    hipLaunchKernelGGL(k_job_count, dim3(JOB_NWG), dim3(JOB_WG), 0, st, jobs, nj_d, cap, cs.hist.as<uint32_t>());
-    hipLaunchKernelGGL(k_job_scan, dim3(1), dim3(64), 0, st, cs.hist.as<uint32_t>(), JOB_NWG, cs.offs.as<uint64_t>(),
+    SKM_LAUNCH(b, k_job_count, dim3(JOB_NWG), dim3(JOB_WG), 0, st, jobs, nj_d, cap, cs.hist.as<uint32_t>());
+    SKM_LAUNCH(b, k_job_scan, dim3(1), dim3(64), 0, st, cs.hist.as<uint32_t>(), JOB_NWG, cs.offs.as<uint64_t>(),
                        long_class);
-    hipLaunchKernelGGL(k_job_scatter, dim3(JOB_NWG), dim3(JOB_WG), 0, st, jobs, nj_d, cap, cs.offs.as<uint64_t>(),
+    SKM_LAUNCH(b, k_job_scatter, dim3(JOB_NWG), dim3(JOB_WG), 0, st, jobs, nj_d, cap, cs.offs.as<uint64_t>(),
                        cs.sorted.as<Job>());
     if (st_short && ev_sorted) SKM_HIP(hipEventRecord(ev_sorted, st));  // sorted jobs ready
     // k_job_scan leaves the long jobs' count after the offsets; they lead the sorted order
@@ -4888,13 +5139,13 @@ void launch_chains(skm_build* b, hipStream_t st, const Job* jobs, const unsigned
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             attr = true;
         }
-        hipLaunchKernelGGL(k_chain_long, dim3(LONG_GRID), dim3(128), lds, st, cs.sorted.as<Job>(), nullptr, nlong_u,
+        SKM_LAUNCH(b, k_chain_long, dim3(LONG_GRID), dim3(128), lds, st, cs.sorted.as<Job>(), nullptr, nlong_u,
                            lens, recs32, tmp32, big32, out, tn.chain_prio);
     } else {
-        hipLaunchKernelGGL(k_long_plan, dim3(1), dim3(1024), 0, st, cs.sorted.as<Job>(), nlong_d,
+        SKM_LAUNCH(b, k_long_plan, dim3(1), dim3(1024), 0, st, cs.sorted.as<Job>(), nlong_d,
                            cs.long_off.as<uint64_t>(), b->d_run.as<unsigned long long>(), b->long_cap,
                            b->long_jobs_cap);
-        hipLaunchKernelGGL(k_long_stash, dim3(LONG_GRID), dim3(256), 0, st, cs.sorted.as<Job>(), nlong_d,
+        SKM_LAUNCH(b, k_long_stash, dim3(LONG_GRID), dim3(256), 0, st, cs.sorted.as<Job>(), nlong_d,
                            cs.long_off.as<uint64_t>(), lens, recs32, tmp32, big32, b->d_long_arena.as<uint32_t>(),
                            b->d_long_jobs.as<Job>());
     }
@@ -4904,7 +5155,7 @@ void launch_chains(skm_build* b, hipStream_t st, const Job* jobs, const unsigned
         SKM_HIP(hipStreamWaitEvent(st_short, ev_sorted, 0));
         ss = st_short;
     }
-    hipLaunchKernelGGL(k_chains, dim3(max_wgs ? max_wgs : (uint32_t)std::max(1, tn.chain_grid)), dim3(256), 0, ss, cs.sorted.as<Job>(), nlong_u,
+    SKM_LAUNCH(b, k_chains, dim3(max_wgs ? max_wgs : (uint32_t)std::max(1, tn.chain_grid)), dim3(256), 0, ss, cs.sorted.as<Job>(), nlong_u,
                        nj_d, cap, lens, recs32, tmp32, big32, out);
     SKM_HIP(hipGetLastError());
 }
@@ -4938,6 +5189,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     A.nbuckets = NB1;
     A.bucket_base = (pass << (b->owner_bits + b->b1_bits)) | ((uint32_t)b->rank << b->b1_bits);
     A.rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
+    A.pshift = KEY_BITS - b->pass_bits;
     A.glen = b->d_glen.as<uint32_t>();
     A.flags = b->d_flags.as<uint8_t>();
     A.ctr = ctr_d;
@@ -4957,7 +5209,7 @@ void phase_group(skm_build* b, uint32_t pass) {
         A.stamps = b->d_stamps.as<unsigned long long>();
     }
     // ---- 4a. level-2 partition ----
-    hipLaunchKernelGGL(k_partition, dim3(NB1), dim3(BP_THREADS), 0, st, A);
+    SKM_LAUNCH(b, k_partition, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[10], st));
     SKM_HIP(hipEventRecord(b->ev_pf_ready, st));
@@ -4986,7 +5238,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     P.kept_cap = b->kept_cap;
     P.tot_cap = b->tot_cap;
     P.split_cap = b->split_cap;
-    hipLaunchKernelGGL(k_ovf_plan, dim3(1), dim3(1024), 0, st, P);
+    SKM_LAUNCH(b, k_ovf_plan, dim3(1), dim3(1024), 0, st, P);
     SKM_HIP(hipGetLastError());
     A.skip = plan_d + PLAN_SKIP;
     SKM_HIP(hipEventRecord(b->ev_part, st));
@@ -5045,24 +5297,24 @@ void phase_group(skm_build* b, uint32_t pass) {
         H.gcap = b->split_cap;
         H.gstat = b->d_gstat.as<unsigned long long>();
     }
-    hipLaunchKernelGGL(k_ovf_split, dim3((uint32_t)std::max(1, b->tune.split_grid)), dim3(BP_THREADS), 0, st2, A2, S, H, key_min, plan_d);
+    SKM_LAUNCH(b, k_ovf_split, dim3((uint32_t)std::max(1, b->tune.split_grid)), dim3(BP_THREADS), 0, st2, A2, S, H, key_min, plan_d);
     SKM_HIP(hipEventRecord(b->ev_split, st2));
     SKM_HIP(hipStreamWaitEvent(st3, b->ev_split, 0));
-    hipLaunchKernelGGL(k_heavy, dim3(HEAVY_GRID), dim3(HEAVY_WG), 0, st2, A2, H);
+    SKM_LAUNCH(b, k_heavy, dim3(HEAVY_GRID), dim3(HEAVY_WG), 0, st2, A2, H);
     SKM_HIP(hipGetLastError());
     if (H.giant_min) {
         SKM_HIP(hipEventRecord(b->gev_ready[gs], st2));
         SKM_HIP(hipStreamWaitEvent(b->gst[gs], b->gev_ready[gs], 0));
-        hipLaunchKernelGGL(k_chain_dyn, dim3(1024), dim3(128), 0, b->gst[gs], H.gjobs, H.gcount, A.out_data,
+        SKM_LAUNCH(b, k_chain_dyn, dim3(1024), dim3(128), 0, b->gst[gs], H.gjobs, H.gcount, A.out_data,
                            b->tune.chain_prio);
         SKM_HIP(hipGetLastError());
         SKM_HIP(hipEventRecord(b->gev_done[gs], b->gst[gs]));
         b->gused[gs] = true;
     }
-    hipLaunchKernelGGL(k_overflow, dim3((uint32_t)std::max(1, b->tune.ovf_grid)), dim3(BP_THREADS), 0, st2, A2, S, plan_d, -1, (int)PLAN_NHEAVY,
+    SKM_LAUNCH(b, k_overflow, dim3((uint32_t)std::max(1, b->tune.ovf_grid)), dim3(BP_THREADS), 0, st2, A2, S, plan_d, -1, (int)PLAN_NHEAVY,
                        (int)PLAN_Q_HEAVY, inline_min, prio);
     SKM_HIP(hipEventRecord(b->ev_o[1], st2));
-    hipLaunchKernelGGL(k_overflow, dim3((uint32_t)std::max(1, b->tune.ovf_grid)), dim3(BP_THREADS), 0, st3, A3, S, plan_d, (int)PLAN_NHEAVY,
+    SKM_LAUNCH(b, k_overflow, dim3((uint32_t)std::max(1, b->tune.ovf_grid)), dim3(BP_THREADS), 0, st3, A3, S, plan_d, (int)PLAN_NHEAVY,
                        (int)PLAN_NOVF, (int)PLAN_Q_REST, inline_min, prio);
     SKM_HIP(hipGetLastError());
     // ---- 4b. group-by of the sub-buckets that fit LDS; groups of > 64 members are handed to
@@ -5078,7 +5330,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     BA.flags = A.flags;
     BA.out = b->d_big_out.as<BigOut>();
     SKM_HIP(hipEventRecord(b->ev[11], st));
-    hipLaunchKernelGGL(k_bucket_process, dim3(NB1), dim3(BP_THREADS), 0, st, A);
+    SKM_LAUNCH(b, k_bucket_process, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[5], st));
     // the next pass's compaction + count overlap this pass's group-by on stx: its buffer set was
@@ -5087,9 +5339,9 @@ void phase_group(skm_build* b, uint32_t pass) {
         SKM_HIP(hipStreamWaitEvent(b->stx, b->ev_pf_ready, 0));
         prefetch_pass(b, pass + 1, b->stx);
     }
-    hipLaunchKernelGGL(k_big_groups<false>, dim3(2048), dim3(BIG_WG), 0, st, BA);
-    hipLaunchKernelGGL(k_big_groups<true>, dim3(512), dim3(BIG_WG), 0, st, BA);
-    hipLaunchKernelGGL(k_big_append, dim3(256), dim3(BIG_WG), 0, st, BA.out, BA, A);
+    SKM_LAUNCH(b, k_big_groups<false>, dim3(2048), dim3(BIG_WG), 0, st, BA);
+    SKM_LAUNCH(b, k_big_groups<true>, dim3(512), dim3(BIG_WG), 0, st, BA);
+    SKM_LAUNCH(b, k_big_append, dim3(256), dim3(BIG_WG), 0, st, BA.out, BA, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[12], st));
     // ---- 6. deferred P^2 / variance chains: the overflow's as soon as both parts are grouped
@@ -5106,7 +5358,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     SKM_HIP(hipStreamWaitEvent(st, b->ev_o3[1], 0));
     SKM_HIP(hipEventRecord(b->ev[6], st));
     // ---- 7. run totals and the chain lists' bounds ----
-    hipLaunchKernelGGL(k_pass_account, dim3(1), dim3(1), 0, st, ctr_d, run_d, b->jobs_cap, b->jobs2_cap, b->big_cap,
+    SKM_LAUNCH(b, k_pass_account, dim3(1), dim3(1), 0, st, ctr_d, run_d, b->jobs_cap, b->jobs2_cap, b->big_cap,
                        b->lens_cap);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[7], st));
@@ -5180,11 +5432,18 @@ void begin_run(skm_build* b) {
     SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->n_total ? b->n_total : 1, st));
     b->d_gstat.ensure(16);
     SKM_HIP(hipMemsetAsync(b->d_gstat.p, 0, 16, st));
+    if (b->tune.poison_jobs && b->pass_bits && b->long_jobs_cap)
+        hipLaunchKernelGGL(k_poison_jobs, dim3(256), dim3(256), 0, st, b->d_long_jobs.as<Job>(), b->long_jobs_cap,
+                           reinterpret_cast<uint64_t>(b->d_long_arena.p), (uint32_t)b->kept_cap,
+                           b->d_data.as<skm_stored_kmer_data>());
     if (b->pass_bits && b->rp)
-        hipLaunchKernelGGL(k_pass_ids, dim3(4096), dim3(256), 0, st, b->d_res.as<uint8_t>(), b->rp, b->pass_bits,
-                           b->d_ids.as<uint8_t>(), nullptr);
+        SKM_LAUNCH(b, k_pass_ids, dim3(4096), dim3(256), b->route ? (1u << BLOOM_BITS) / 8 : 0u, st,
+                   b->d_res.as<uint8_t>(), b->rp, b->pass_bits, b->d_ids.as<uint8_t>(), nullptr,
+                   b->route ? b->d_bloom.as<uint32_t>() : nullptr);
     SKM_HIP(hipGetLastError());
     b->acc = skm_build::Acc{};
+    b->kt_used = 0;
+    b->kt_recs.clear();
     std::memset(b->pass_ms, 0, sizeof(b->pass_ms));
     for (bool& g : b->gused) g = false;
     for (bool& g : b->chain_used) g = false;
@@ -5240,12 +5499,12 @@ hipStream_t chain_stream(skm_build* b, int slot) {
 void flush_long_chains(skm_build* b, int slot) {
     unsigned long long* run_d = b->d_run.as<unsigned long long>();
     unsigned long long* rng = run_d + RUN_SNAP + 2 * slot;
-    hipLaunchKernelGGL(k_long_snap, dim3(1), dim3(1), 0, b->stream, run_d, rng);
+    SKM_LAUNCH(b, k_long_snap, dim3(1), dim3(1), 0, b->stream, run_d, rng, b->long_jobs_cap);
     SKM_HIP(hipEventRecord(b->chain_ev[0], b->stream));
     hipStream_t cs = chain_stream(b, slot);
     SKM_HIP(hipStreamWaitEvent(cs, b->chain_ev[0], 0));
     b->chain_used[slot % std::max(1, std::min(b->tune.chain_streams, 1 + skm_build::GSLOTS))] = true;
-    hipLaunchKernelGGL(k_chain_long, dim3(LONG_GRID), dim3(128), 0, cs, b->d_long_jobs.as<Job>(), rng, rng + 1,
+    SKM_LAUNCH(b, k_chain_long, dim3(LONG_GRID), dim3(128), 0, cs, b->d_long_jobs.as<Job>(), rng, rng + 1,
                        nullptr, nullptr, nullptr, nullptr, b->d_data.as<skm_stored_kmer_data>(), b->tune.chain_prio);
     SKM_HIP(hipGetLastError());
 }
@@ -5254,6 +5513,7 @@ void flush_long_chains(skm_build* b, int slot) {
 void phase_stats(skm_build* b) {
     hipStream_t st = b->stream;
     const uint32_t F = b->opts.n_functions;
+    SKM_HIP(hipEventRecord(b->ev_tail[0], st));  // the last pass is issued: the tail starts here
     if (b->pass_bits) {  // the long chains of every pass (the last batch on the chain stream)
         flush_long_chains(b, 16);
         for (int k = 0; k <= skm_build::GSLOTS; ++k) {
@@ -5266,15 +5526,16 @@ void phase_stats(skm_build* b) {
     }
     for (int g = 0; g < skm_build::GSLOTS; ++g)  // the giant chains of every pass
         if (b->gused[g]) SKM_HIP(hipStreamWaitEvent(st, b->gev_done[g], 0));
+    SKM_HIP(hipEventRecord(b->ev_tail[1], st));
     SKM_HIP(hipEventRecord(b->ev[7], st));
     SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
     const size_t lds_f = F <= 16384 ? sizeof(uint32_t) * F : 0;
-    hipLaunchKernelGGL(k_kept_finalize, dim3(2048), dim3(256), lds_f, st, b->d_keys.as<uint64_t>(),
+    SKM_LAUNCH(b, k_kept_finalize, dim3(2048), dim3(256), lds_f, st, b->d_keys.as<uint64_t>(),
                        b->d_data.as<skm_stored_kmer_data>(), b->d_ctr.as<unsigned long long>(), F,
                        b->d_dfunc.as<uint32_t>());
     if (b->nseq)
-        hipLaunchKernelGGL(k_func_hist_seqs, dim3(256), dim3(256), lds_f, st, b->d_meta.as<SeqMeta>(), b->nseq, F,
+        SKM_LAUNCH(b, k_func_hist_seqs, dim3(256), dim3(256), lds_f, st, b->d_meta.as<SeqMeta>(), b->nseq, F,
                            b->d_swf.as<uint32_t>());
     SKM_HIP(hipGetLastError());
 }
@@ -5282,13 +5543,17 @@ void phase_stats(skm_build* b) {
 // the step's one host synchronisation: counters, run slots and timings come back together
 void phase_final(skm_build* b) {
     hipStream_t st = b->stream;
-    hipLaunchKernelGGL(k_count_flags, dim3(256), dim3(256), 0, st, b->d_flags.as<uint8_t>(), b->n_total,
+    SKM_LAUNCH(b, k_count_flags, dim3(256), dim3(256), 0, st, b->d_flags.as<uint8_t>(), b->n_total,
                        b->d_ctr.as<unsigned long long>() + 2);
     SKM_HIP(hipGetLastError());
     unsigned long long* pin = b->pinned_ctr();
     SKM_HIP(hipMemcpyAsync(pin + 48, b->d_gstat.p, 16, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipMemcpyAsync(pin + 56, b->d_ctr.p, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipMemcpyAsync(pin + 64, b->d_run.p, 8 * RUN_SLOTS, hipMemcpyDeviceToHost, st));
+    const bool canary = b->tune.poison_jobs && b->pass_bits && b->long_jobs_cap;
+    if (canary)
+        SKM_HIP(hipMemcpyAsync(pin + 42, b->d_data.as<skm_stored_kmer_data>() + b->kept_cap,
+                               sizeof(skm_stored_kmer_data), hipMemcpyDeviceToHost, st));
     SKM_HIP(hipEventRecord(b->ev[8], st));
     SKM_HIP(hipEventSynchronize(b->ev[8]));
     const unsigned long long* R = pin + 64;
@@ -5296,14 +5561,21 @@ void phase_final(skm_build* b) {
     b->giant_max = pin[49];
     b->n_kept = pin[56];
     b->run_flags = R[RUN_FLAGS];
+    if (canary) {  // a chain ran on a long-job slot that no stash wrote
+        const auto* c = reinterpret_cast<const skm_stored_kmer_data*>(pin + 42);
+        if (c->median != 0xC0DE || c->var != 0xC0DE) b->run_flags |= RUN_F_CAP;
+    }
     for (int i = 0; i < 4; ++i) b->demand[i] = R[RUN_DEM_TOT + i];
-    // the long arena's cursors count every reservation, the ones that did not fit included
-    b->demand[2] = std::max<uint64_t>(b->demand[2], R[RUN_LONG_CUR]);
-    b->demand[3] = std::max<uint64_t>(b->demand[3], R[RUN_LONG_N]);
+    // what the passes asked of the long arena and job list (the reservations that did not fit included)
+    b->demand[2] = std::max<uint64_t>(b->demand[2], R[RUN_LONG_WANT]);
+    b->demand[3] = std::max<uint64_t>(b->demand[3], R[RUN_LONG_WANTJ]);
     pass_times(b, 1u << b->pass_bits);
     for (int i = 0; i < 12; ++i) b->last_ms[i] = b->pass_ms[i];
     SKM_HIP(hipEventElapsedTime(&b->last_ms[6], b->ev[7], b->ev[8]));      // stats (+ reductions)
     SKM_HIP(hipEventElapsedTime(&b->last_ms[7], b->ev_start, b->ev[8]));   // whole run
+    SKM_HIP(hipEventElapsedTime(&b->last_ms[12], b->ev_tail[0], b->ev_tail[1]));  // long-chain tail
+    b->long_samples = R[RUN_LONG_CUR];
+    kt_collect(b);
     // run totals for counters() / finish()
     b->n_overflow = (uint32_t)R[RUN_ACC_NOVF];
     b->n_overflow_last = (uint32_t)R[RUN_LAST_NOVF];
@@ -5441,6 +5713,7 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     }
     for (auto& e : b->chain_ev) SKM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_part, hipEventDisableTiming));
+    for (auto& e : b->ev_tail) SKM_HIP(hipEventCreate(&e));
     for (int i = 0; i < 2; ++i) {
         SKM_HIP(hipHostMalloc(reinterpret_cast<void**>(&b->st_pin[i]), STAGE_BYTES, hipHostMallocDefault));
         SKM_HIP(hipEventCreateWithFlags(&b->st_ev[i], hipEventDisableTiming));
@@ -5698,7 +5971,9 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "split_grid" ? &t.split_grid
                : n == "chain_grid" ? &t.chain_grid
                : n == "chain_batches" ? &t.chain_batches
-               : n == "chain_streams" ? &t.chain_streams : nullptr;
+               : n == "chain_streams" ? &t.chain_streams
+               : n == "poison_jobs" ? &t.poison_jobs
+               : n == "route_heavy_min" ? &t.route_heavy_min : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")
@@ -5833,18 +6108,47 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
-    const uint64_t v[24] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+    const uint64_t v[25] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
                             b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total,
                             b->giant_jobs, b->giant_max, b->n_redo, b->tot_cap, b->split_cap, b->long_cap,
-                            b->long_jobs_cap, b->demand[0], b->demand[1], b->demand[2], b->demand[3]};
-    int n = std::min(cap, 24);
+                            b->long_jobs_cap, b->demand[0], b->demand[1], b->demand[2], b->demand[3],
+                            b->long_samples};
+    int n = std::min(cap, 25);
     for (int i = 0; i < n; ++i) out[i] = v[i];
+    return n;
+}
+
+int skm_build_set_kernel_timing(skm_build* b, int enable, const char* only) {
+    SKM_API_BEGIN
+    SKM_CHECK(b, SKM_E_ARG, "null build");
+    b->kt_mode = enable ? 1 : 0;
+    b->kt_only = only ? std::string(only) : std::string();
+    SKM_API_END
+}
+
+int skm_build_kernel_timings(skm_build* b, char* names, size_t names_cap, float* ms, uint64_t* launches, int cap) {
+    if (!b) return SKM_E_ARG;
+    const int n = (int)b->kt_names.size();
+    std::string all;
+    for (int k = 0; k < n; ++k) {
+        if (k < cap) {
+            if (ms) ms[k] = (float)b->kt_ms[k];
+            if (launches) launches[k] = b->kt_n[k];
+        }
+        all += b->kt_names[k];
+        all += '\n';
+    }
+    if (names && names_cap) {
+        const size_t c = std::min(names_cap - 1, all.size());
+        std::memcpy(names, all.data(), c);
+        names[c] = 0;
+    }
     return n;
 }
 
 int skm_build_last_timings(skm_build* b, float* ms, int cap) {
     if (!b || !ms) return SKM_E_ARG;
-    int n = std::min(cap, 12);
+    int n = std::min(cap, 13);
     for (int i = 0; i < n; ++i) ms[i] = b->last_ms[i];
     return n;
 }
@@ -5975,6 +6279,107 @@ int skm_build_finish(skm_build* b, skm_kept* out) {
     SKM_API_END
 }
 
+int skm_build_finish_slice(skm_build* b, int slice_bits, uint32_t slice, skm_kept* out) {
+    SKM_API_BEGIN
+    SKM_CHECK(b && out, SKM_E_ARG, "null argument");
+    SKM_CHECK(slice_bits >= 0 && slice_bits <= 16 && slice < (1u << slice_bits), SKM_E_ARG, "bad slice");
+    check_transport(b);
+    SKM_HIP(hipSetDevice(b->device));
+    const Ranks bs = ranks_of(b);
+    bool need = false;
+    for (auto* x : bs) need |= !x->prepared || !x->ran;
+    if (need) run_ranks(bs);
+    std::memset(out, 0, sizeof(*out));
+    hipStream_t st = b->stream;
+    const uint32_t F = b->opts.n_functions;
+    DevBuf cur, dk, dd;
+    cur.ensure(8);
+    SKM_HIP(hipMemsetAsync(cur.p, 0, 8, st));
+    const uint64_t nk = b->n_kept;
+    if (nk)
+        hipLaunchKernelGGL(k_slice_select, dim3(2048), dim3(256), 0, st, b->d_keys.as<uint64_t>(),
+                           b->d_data.as<skm_stored_kmer_data>(), nk, slice_bits, (uint64_t)slice,
+                           cur.as<unsigned long long>(), nullptr, nullptr);
+    SKM_HIP(hipGetLastError());
+    uint64_t n = 0;
+    SKM_HIP(hipMemcpyAsync(&n, cur.p, 8, hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipStreamSynchronize(st));
+    std::vector<uint64_t> keys(n);
+    std::vector<skm_stored_kmer_data> data(n);
+    if (n) {
+        dk.ensure(8 * n);
+        dd.ensure(sizeof(skm_stored_kmer_data) * n + 16);
+        SKM_HIP(hipMemsetAsync(cur.p, 0, 8, st));
+        hipLaunchKernelGGL(k_slice_select, dim3(2048), dim3(256), 0, st, b->d_keys.as<uint64_t>(),
+                           b->d_data.as<skm_stored_kmer_data>(), nk, slice_bits, (uint64_t)slice,
+                           cur.as<unsigned long long>(), dk.as<uint64_t>(), dd.as<skm_stored_kmer_data>());
+        SKM_HIP(hipGetLastError());
+        SKM_HIP(hipMemcpyAsync(keys.data(), dk.p, 8 * n, hipMemcpyDeviceToHost, st));
+        SKM_HIP(hipMemcpyAsync(data.data(), dd.p, sizeof(skm_stored_kmer_data) * n, hipMemcpyDeviceToHost, st));
+    }
+    out->distinct_functions = (uint32_t*)std::malloc(sizeof(uint32_t) * std::max<uint32_t>(F, 1));
+    out->seqs_with_func = (uint32_t*)std::malloc(sizeof(uint32_t) * std::max<uint32_t>(F, 1));
+    out->keys = (uint64_t*)std::malloc(8 * std::max<uint64_t>(n, 1));
+    out->data = (skm_stored_kmer_data*)std::malloc(sizeof(skm_stored_kmer_data) * std::max<uint64_t>(n, 1));
+    SKM_CHECK(out->distinct_functions && out->seqs_with_func && out->keys && out->data, SKM_E_OOM,
+              "host allocation failed");
+    if (F) {
+        SKM_HIP(hipMemcpyAsync(out->distinct_functions, b->d_dfunc.p, sizeof(uint32_t) * F, hipMemcpyDeviceToHost, st));
+        SKM_HIP(hipMemcpyAsync(out->seqs_with_func, b->d_swf.p, sizeof(uint32_t) * F, hipMemcpyDeviceToHost, st));
+    }
+    unsigned long long ctr[3];
+    SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, sizeof(ctr), hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipStreamSynchronize(st));
+    // keys ascending: chunks sorted on the host threads, then merged pairwise
+    std::vector<std::pair<uint64_t, uint32_t>> kv(n);
+    for (uint64_t i = 0; i < n; ++i) kv[i] = {keys[i], (uint32_t)i};
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>(16, n / 65536 + 1));
+    std::vector<uint64_t> cut(T + 1);
+    for (int t = 0; t <= T; ++t) cut[t] = n * (uint64_t)t / (uint64_t)T;
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t]() { std::sort(kv.begin() + cut[t], kv.begin() + cut[t + 1]); });
+        for (auto& x : th) x.join();
+    }
+    for (int w = 1; w < T; w <<= 1) {
+        std::vector<std::thread> th;
+        for (int t = 0; t + w < T; t += 2 * w)
+            th.emplace_back([&, t, w]() {
+                std::inplace_merge(kv.begin() + cut[t], kv.begin() + cut[t + w], kv.begin() + cut[std::min(T, t + 2 * w)]);
+            });
+        for (auto& x : th) x.join();
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+        out->keys[i] = kv[i].first;
+        out->data[i] = data[kv[i].second];
+    }
+    out->n = n;
+    out->n_functions = F;
+    uint64_t total = b->n_kept;
+    if (b->world > 1) {
+        std::vector<uint64_t> mine;
+        for (auto* x : bs) mine.push_back(x->n_kept);
+        total = 0;
+        for (auto v : allgather_u64(bs, mine)) total += v;
+    }
+    out->distinct_signatures = total;
+    out->n_seqs_with_signature = ctr[2];  // per sequence (colliding seq ids counted per sequence)
+    out->n_windows = b->n_windows;
+    out->n_records = b->n_local;
+    SKM_API_END
+}
+
+int skm_build_signature_flags(skm_build* b, uint8_t* out, uint64_t cap) {
+    SKM_API_BEGIN
+    SKM_CHECK(b && out, SKM_E_ARG, "null argument");
+    SKM_CHECK(b->ran, SKM_E_STATE, "no completed run");
+    SKM_HIP(hipSetDevice(b->device));
+    const uint64_t n = std::min<uint64_t>(cap, b->n_total);
+    if (n) SKM_HIP(hipMemcpy(out, b->d_flags.p, n, hipMemcpyDeviceToHost));
+    SKM_API_END
+}
+
 void skm_kept_free(skm_kept* k) {
     if (!k) return;
     std::free(k->keys);
@@ -6005,6 +6410,9 @@ void skm_build_destroy(skm_build* b) {
             if (e) (void)hipEventDestroy(e);
     }
     if (b->ev_part) (void)hipEventDestroy(b->ev_part);
+    for (auto& e : b->ev_tail)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : b->kt_pool) (void)hipEventDestroy(e);
     for (int i = 0; i < 2; ++i) {
         if (b->st_busy[i] && b->st_ev[i]) (void)hipEventSynchronize(b->st_ev[i]);
         if (b->st_pin[i]) (void)hipHostFree(b->st_pin[i]);

@@ -107,6 +107,18 @@ SKM_HD uint64_t encode_key(uint64_t raw) {
     return k;
 }
 
+// Output slices (skm_build_finish_slice): the kept k-mers whose slice_hash has top bits == slice.
+// MurmurHash3's 64-bit finalizer of the little-endian key, independent of the build's own mix43
+// so a checker can select the same slice from the raw keys alone.
+SKM_HD uint64_t slice_hash(uint64_t key) {
+    key ^= key >> 33;
+    key *= 0xff51afd7ed558ccdull;
+    key ^= key >> 33;
+    key *= 0xc4ceb9fe1a85ec53ull;
+    key ^= key >> 33;
+    return key;
+}
+
 // Occurrence record geometry.
 struct RecGeom {
     int owner_bits;  // log2(world size)

@@ -39,6 +39,9 @@ def olib():
         _lib.oracle_build.argtypes = [P, P, P, P, P, C.c_uint64, C.c_uint32, P, P, C.c_uint64, P, P, P, P, P]
         _lib.oracle_build_mt.restype = C.c_int
         _lib.oracle_build_mt.argtypes = [P, P, P, P, P, C.c_uint64, C.c_uint32, C.c_int, P, P, P, P, P, P, P]
+        _lib.oracle_build_sel_mt.restype = C.c_int
+        _lib.oracle_build_sel_mt.argtypes = [P, P, P, P, P, C.c_uint64, C.c_uint32, C.c_int, C.c_int, C.c_uint64, P, P,
+                                             C.c_uint64, P, P, P, P, P, P, P, P]
         _lib.oracle_count_windows.restype = C.c_uint64
         _lib.oracle_count_windows.argtypes = [P, P, C.c_uint64]
         _lib.oracle_bdz_load.restype = P
@@ -123,6 +126,55 @@ def build_mt(residues, seq_off, seq_len, seq_func, seq_id, n_functions, n_thread
     return dict(keys=keys.copy(), data=data.copy(), distinct_functions=df[:n_functions].copy(),
                 seqs_with_func=sw[:n_functions].copy(), n_seqs_with_signature=int(nsig[0]),
                 distinct_signatures=int(dsig[0]))
+
+
+def slice_hash(keys: np.ndarray) -> np.ndarray:
+    """MurmurHash3 fmix64 of little-endian keys (the output-slice hash, numpy)."""
+    k = np.ascontiguousarray(keys, np.uint64).copy()
+    with np.errstate(over="ignore"):
+        k ^= k >> np.uint64(33)
+        k *= np.uint64(0xff51afd7ed558ccd)
+        k ^= k >> np.uint64(33)
+        k *= np.uint64(0xc4ceb9fe1a85ec53)
+        k ^= k >> np.uint64(33)
+    return k
+
+
+def build_slice_mt(residues, seq_off, seq_len, seq_func, seq_id, n_functions, n_threads, sel_bits, sel,
+                   want_flags=False):
+    """oracle_build_sel_mt: the build restricted to the keys of one output slice (fmix64 top
+    sel_bits == sel) on n_threads host threads.  Returns the slice's kept k-mers (sorted), its
+    distinct_functions / distinct_signatures / n_seqs_with_signature, the input's valid windows
+    (all keys), the largest selected group and optionally per-sequence flags of the slice."""
+    L = olib()
+    residues = np.ascontiguousarray(residues, np.uint8)
+    seq_off = np.ascontiguousarray(seq_off, np.uint64)
+    seq_len = np.ascontiguousarray(seq_len, np.uint32)
+    seq_func = np.ascontiguousarray(seq_func, np.uint16)
+    seq_id = np.ascontiguousarray(seq_id, np.uint32)
+    n = len(seq_len)
+    w = int(L.oracle_count_windows(_p(seq_len), _p(seq_func), n))
+    cap = 2 * (w >> sel_bits) + (1 << 20)  # kept <= selected windows (~ w / 2^sel_bits); retried if short
+    while True:
+        keys = np.empty(cap, np.uint64)
+        data = np.empty(cap, STORED_DTYPE)
+        df = np.zeros(max(n_functions, 1), np.uint32)
+        sw = np.zeros(max(n_functions, 1), np.uint32)
+        out_n, nsig, dsig, valid, mg = (np.zeros(1, np.uint64) for _ in range(5))
+        flags = np.zeros(max(n, 1), np.uint8) if want_flags else None
+        rc = L.oracle_build_sel_mt(_p(residues), _p(seq_off), _p(seq_len), _p(seq_func), _p(seq_id), n, n_functions,
+                                   int(n_threads), int(sel_bits), int(sel), _p(keys), _p(data), cap, _p(out_n),
+                                   _p(df), _p(sw), _p(nsig), _p(dsig), _p(valid), _p(mg),
+                                   _p(flags) if flags is not None else None)
+        k = int(out_n[0])
+        if rc == 0:
+            break
+        cap = k + 1
+    o = np.argsort(keys[:k], kind="stable")
+    return dict(keys=keys[:k][o].copy(), data=data[:k][o].copy(), distinct_functions=df[:n_functions].copy(),
+                seqs_with_func=sw[:n_functions].copy(), n_seqs_with_signature=int(nsig[0]),
+                distinct_signatures=int(dsig[0]), valid_windows=int(valid[0]), max_group=int(mg[0]),
+                flags=None if flags is None else flags[:n])
 
 
 def count_windows(seq_len, seq_func) -> int:

@@ -112,13 +112,16 @@ def test_work_buffers_grow_and_redo(skm, gpu, passes):
     """The data-sized work buffers (overflow scratch, split path, stashed long chains) start far
     too small: the step runs without a host round trip, records its demands on the device, and is
     redone with the buffers grown; the result is the oracle's bit for bit, and the next run on the
-    same handle needs no redo."""
+    same handle needs no redo.  With passes, every slot of the stashed long-job list starts as a
+    canary job (poison_jobs): a long chain launched on a slot that no stash wrote -- the first,
+    too-small attempt reserves none -- would overwrite the canary record and fail the run."""
     p = synth.generate_arrays(60000, 60, per_file=2000, seed=6)
     r, o, l, f, i, funcs = synth.build_inputs(p)
     ref = oracle_ref.build(r, o, l, f, i, len(funcs))
     b = skm.SignatureBuilder(len(funcs))
     if passes:
         b.set_option("key_range_passes", passes)
+        b.set_option("poison_jobs", 1)
     b.set_option("main_long_class", 8)
     b.set_option("overflow_long_class", 8)
     b.set_option("work_buffer_elements", 64)

@@ -120,3 +120,51 @@ def test_matrix_exact_db(skm, gpu, tmp_path):
     assert len(exp) > 1000
     md.close()
     db.close()
+
+
+def test_c5_full_100k_bit_exact(skm, gpu, tmp_path):
+    """BASELINE configs[4] at full size, the bench's matrix leg: a 200-family signature DB built on
+    the GPU from 200K training proteins (genome files 0..49, device-peeled BDZ), all-vs-all over
+    the 100K fresh query proteins of files 50..74 (~73M nonzero pairs, ~293M pair increments) vs
+    oracle_matrix_distance on every host core (kmers-matrix-distance.cc:123-211), bit-exact as
+    sorted (id1, id2, count)."""
+    import os
+    fam, per = 200, 4000
+    th = len(os.sched_getaffinity(0))
+    try:
+        qq, pp = open("/sys/fs/cgroup/cpu.max").read().split()
+        if qq != "max":
+            th = max(1, min(th, int(qq) // int(pp)))
+    except (OSError, ValueError):
+        pass
+
+    def packed(n_total, f0, nf):
+        parts = list(synth.iter_file_inputs(n_total, fam, per, f0, nf, workers=min(16, th)))
+        cat = [np.concatenate([p[k] for p in parts]) for k in range(5)]
+        off = np.zeros(len(cat[2]), np.uint64)
+        off[1:] = np.cumsum(cat[2][:-1], dtype=np.uint64)
+        return cat[0], off, cat[2], cat[3], cat[4]
+
+    funcs = synth.functions(fam)
+    r, o, l, f, i = packed(200_000, 0, 50)
+    b = skm.SignatureBuilder(len(funcs))
+    b.add_batch(r, o, l, f, i)
+    kept = b.finish()
+    b.close()
+    base = str(tmp_path / "kmer_data")
+    skm.mph_build(kept.keys, kept.data, base + ".mph", base + ".dat", seed=1, device=0)
+    qr, qo, ql, _, _ = packed(300_000, 50, 25)
+    assert len(ql) == 100_000
+    db = skm.CmphKmerDb(base, device=0)
+    md = skm.MatrixDistance(db, funcs, qr, qo, ql)
+    got = md.compute()
+    c = md.counters()
+    md.close()
+    db.close()
+    ob = oracle_ref.Bdz(open(base + ".mph", "rb").read())
+    exp = oracle_ref.matrix_distance_mt(ob, open(base + ".dat", "rb").read(), qr, qo, ql,
+                                        np.arange(len(ql), dtype=np.uint32), funcs.index("hypothetical protein"),
+                                        n_threads=th)
+    assert len(exp) > 50_000_000, len(exp)
+    assert c["pairs"] == len(exp) and c["increments"] == int(exp[:, 2].astype(np.int64).sum())
+    assert np.array_equal(got, exp)

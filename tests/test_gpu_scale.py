@@ -1,5 +1,5 @@
 """Parity at BASELINE configs[1] size (C2: 1M synthetic proteins, 4,000 families) and against the
-C2-built signature DB (C4's database, 1M fresh queries).
+C2-built signature DB (C4's database, all 10M fresh queries of configs[3]).
 
 At this size the heaviest k-mers have ~2*10^4 occurrences: the build reaches the overflow path
 (sub-buckets beyond LDS, global bitonic sort), the in-situ wave-pair P^2 chains of >= 16,384
@@ -70,9 +70,22 @@ def test_c2_build_bit_exact(skm, c2, passes):
     c2.setdefault("kept", got)
 
 
+def _pooled(n_total, first_file, n_files):
+    """Files [first_file, first_file + n_files) of an n_total proteome from the bench's worker
+    pool, packed (residues, seq_off, seq_len)."""
+    parts = list(synth.iter_file_inputs(n_total, FAM, 4000, first_file, n_files, workers=min(16, _threads())))
+    lens = np.concatenate([p[2] for p in parts])
+    res = np.concatenate([p[0] for p in parts])
+    off = np.zeros(len(lens), np.uint64)
+    off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    return res, off, lens
+
+
 def test_c4_db_calls_bit_exact(skm, c2, tmp_path):
-    """Calls of 1M fresh queries against the C2-built CMPH/BDZ DB (168.7M keys, device-peeled
-    MPH, resident in HBM) vs process_aa_seq of the oracle on the same .mph/.dat image."""
+    """BASELINE configs[3] at full size: the calls of all 10M fresh queries (3.03 G windows, the
+    bench's C4 leg: genome files 250..2749 of the C3 proteome) against the C2-built CMPH/BDZ DB
+    (168.7M keys, device-peeled MPH, resident in HBM) vs process_aa_seq of the oracle on the
+    same .mph/.dat image, on every host core (call_functions.tcc:259-338)."""
     kept = c2.get("kept")
     if kept is None:
         r, o, l, f, i = c2["inputs"]
@@ -83,18 +96,18 @@ def test_c4_db_calls_bit_exact(skm, c2, tmp_path):
     funcs = c2["funcs"]
     base = str(tmp_path / "kmer_data")
     skm.mph_build(kept.keys, kept.data, base + ".mph", base + ".dat", seed=1, device=0)
-    nq = 1_000_000
-    q = synth.generate_arrays(N_C2 + nq, FAM, per_file=4000, first_file=N_C2 // 4000, n_files=nq // 4000)
-    assert len(q.seq_len) == nq
+    nq = 10_000_000
+    qr, qo, ql = _pooled(50_000_000, N_C2 // 4000, nq // 4000)
+    assert len(ql) == nq
     db = skm.CmphKmerDb(base, device=0)
     assert db.hash_size() == len(kept.keys)
     hypo = funcs.index("hypothetical protein")
     caller = skm.FunctionCaller(db, funcs)
-    off, calls = caller.process_seqs(q.residues, q.seq_off, q.seq_len)
+    off, calls = caller.process_seqs(qr, qo, ql)
     db.close()
     ob = oracle_ref.Bdz(open(base + ".mph", "rb").read())
-    ooff, ocalls = oracle_ref.annotate_par(ob, open(base + ".dat", "rb").read(), q.residues, q.seq_off, q.seq_len,
-                                           _threads(), hypo_index=hypo)
-    assert len(calls) > 500_000
+    ooff, ocalls = oracle_ref.annotate_par(ob, open(base + ".dat", "rb").read(), qr, qo, ql, _threads(), hypo_index=hypo)
+    assert int(np.where(ql >= 8, ql.astype(np.int64) - 7, 0).sum()) > 3_000_000_000
+    assert len(calls) > 5_000_000
     assert np.array_equal(off, ooff)
     assert np.array_equal(calls.view(np.uint8), ocalls.view(np.uint8))
