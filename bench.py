@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--annot-queries", type=int, default=10_000_000,
                     help="annotate leg (BASELINE configs[3]); 0 = off; N=1 only")
     ap.add_argument("--matrix-seqs", type=int, default=100_000,
-                    help="matrix-distance leg (BASELINE configs[4]); 0 = off; row bands over the ranks")
+                    help="matrix-distance leg (BASELINE configs[4]); 0 = off; owner-partitioned over the ranks")
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
                     help="rank exchange of the build: RCCL over xGMI, or the gloo host transport (rehearses the "
                          "multi-rank path with several ranks on one GPU)")
@@ -536,8 +536,20 @@ def _matrix_leg(skm, matrix_in, a, device, cores, rank=0, world=1, dist=None):
         db = skm.CmphKmerDb(base, device=device)
         files = None if a.no_cpu_baseline else (open(base + ".mph", "rb").read(), open(base + ".dat", "rb").read())
     prep_s = time.time() - t0
-    md = skm.MatrixDistance(db, funcs, res, off, ln)
-    rows = skm.matrix_tile_rows(n, rank, world) if world > 1 else None
+    if world > 1:  # rank r: its contiguous range of the queries; hits to k-mer owners, groups to row bands
+        part = np.array_split(np.arange(n), world)[rank]
+        qa, qb = (int(part[0]), int(part[-1]) + 1) if len(part) else (0, 0)
+        md = skm.MatrixDistance(db, funcs, res, off[qa:qb], ln[qa:qb], seq_idx=np.arange(qa, qb, dtype=np.uint32),
+                                n_idx=n)
+        if a.comm == "host":
+            md.set_transport(skm.GlooTransport())
+        else:
+            box = [skm.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            md.set_comm(box[0], rank, world)
+    else:
+        md = skm.MatrixDistance(db, funcs, res, off, ln)
+    rows = None
     for _ in range(max(1, a.warmup)):
         md.run(rows)
     steps = max(3, min(a.steps, 10))
@@ -558,13 +570,16 @@ def _matrix_leg(skm, matrix_in, a, device, cores, rank=0, world=1, dist=None):
         tt = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall = float(tt.item())
-        v = torch.tensor([float(c["increments"]), float(c["pairs"])], dtype=torch.float64)
+        v = torch.tensor([float(c["increments"]), float(c["pairs"]), float(c["windows"]), float(c["local_hits"])],
+                         dtype=torch.float64)
         dist.all_reduce(v, op=dist.ReduceOp.SUM)
-        c = dict(c, increments=int(v[0]), pairs=int(v[1]))
+        c = dict(c, increments=int(v[0]), pairs=int(v[1]), windows=int(v[2]), hits=int(v[3]))
     md.close()
     db.close()
     alg = 4 * c["increments"]
     gbs = alg / (acc["pairs"] * 1e-3) / 1e9
+    split = ("query ranges per GPU, hits owner-partitioned by k-mer, k-mer groups routed to the row bands of the "
+             "triangle" if world > 1 else "one tile")
     cpu = None
     if files is not None and world == 1:  # the oracle's matrix distance on the host cores, bounded sample
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -588,8 +603,7 @@ def _matrix_leg(skm, matrix_in, a, device, cores, rank=0, world=1, dist=None):
             "value": c["windows"] * steps / wall, "unit": "k-mers/s", "ms_per_step": 1000.0 * wall / steps,
             "steps": steps, "pair_increments_per_s": c["increments"] / (acc["pairs"] * 1e-3),
             "scaling": "strong", "n_gpus": world,
-            "config": {"workload": f"C5: {n} query proteins of 200 families, all-vs-all, {world} GPU(s) "
-                                   f"({'row bands of the triangle' if world > 1 else 'one tile'})",
+            "config": {"workload": f"C5: {n} query proteins of 200 families, all-vs-all, {world} GPU(s) ({split})",
                        "queries": n, "families": 200, "db_keys": int(len(kept.keys)), "windows": c["windows"],
                        "hits": c["hits"], "pair_increments": c["increments"], "nonzero_pairs": c["pairs"]},
             "phase_ms": acc,

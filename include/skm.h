@@ -144,7 +144,8 @@ int skm_build_kernel_timings(skm_build* b, char* names, size_t names_cap, float*
  * the buffers grown; the capacities persist, so later runs on the same input are not)
  * [16..19]=capacities of those buffers (overflow scratch elements, split-path elements, stashed
  * long-chain samples, stashed long jobs) [20..23]=the last run's demands on them [24]=samples of
- * the stashed long chains (chains of >= 2^14 samples with key-range passes);
+ * the stashed long chains (chains of >= 2^14 samples with key-range passes) [25]=occurrences of
+ * heavy k-mers routed into the first half of the key-range passes ("route_heavy_min");
  * totals over the passes of the run; returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Host transport: the rank collectives of a multi-process build run by the caller on host
@@ -192,7 +193,11 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   (1: the group-by stream at the highest priority), "chain_batches" (key-range passes: the
  *   stashed long chains leave in this many batches, 4) / "chain_streams" (over 1..4 streams, 1),
  *   "work_buffer_elements" (capacity of the data-sized work buffers; tests force the
- *   grow-and-redo path with a small value; 0 = automatic).
+ *   grow-and-redo path with a small value; 0 = automatic), "poison_jobs" (tests: canary jobs in
+ *   the stashed long-job list), "route_heavy_min" (one GPU, >= 4 key-range passes: k-mers with at
+ *   least this many occurrences -- estimated at prepare from a count-min sketch of 1/64 of the
+ *   windows -- are grouped in the first half of the passes, so their long P^2 chains run beside
+ *   the later passes instead of after the last one; 65536; 0 = off).
  * Unknown names and out-of-range values return SKM_E_ARG. */
 int skm_build_set_option(skm_build* b, const char* name, int64_t value);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then
@@ -357,10 +362,22 @@ int skm_matrix_create(skm_matrix** out, skm_db* db, const uint8_t* residues, con
                       const uint32_t* seq_len, const uint32_t* seq_idx, size_t n_seqs, uint32_t n_idx);
 /* Device pipeline on the resident queries; the pairs stay on the device. */
 int skm_matrix_run(skm_matrix* m, const skm_matrix_opts* opts);
+/* Multi-GPU matrix distance: rank `rank` of `world` created its handle over its
+ * own contiguous range of the query sequences, with the global SeqIdMap indices and n_idx (every
+ * rank's the same).  After joining the ranks -- a host transport (copied) or an RCCL communicator
+ * (rank 0's skm_comm_unique_id, collective) -- skm_matrix_run is collective: each rank looks up
+ * only its own queries (kmers-matrix-distance.cc:123-152 hit_cb), every (k-mer, index) hit goes
+ * to the k-mer's owner GPU (all-to-all), the owner builds its k-mers' kmer_hit_map entries and
+ * sends each one's index set to the GPUs whose row band (skm_matrix_tile_rows) it has pairs in
+ * (all-to-all), and each GPU counts the pairs of its band (:176-196); opts row_begin / row_end are
+ * ignored, and skm_matrix_pairs returns the band's pairs (concatenate the ranks' in rank order). */
+int skm_matrix_set_transport(skm_matrix* m, int rank, int world, const skm_transport* tp);
+int skm_matrix_set_comm(skm_matrix* m, int rank, int world, const uint8_t id[128]);
 /* [0]=hits [1]=group (hash + sort) [2]=pair increments [3]=compaction [4]=total (ms) */
 int skm_matrix_last_timings(skm_matrix* m, float* ms, int cap);
 /* [0]=windows [1]=hit records [2]=pair increments [3]=nonzero pairs [4]=distinct hit k-mers
- * (kmer_hit_map.size(), kmers-matrix-distance.cc:169) */
+ * (kmer_hit_map.size(), kmers-matrix-distance.cc:169; with ranks: the k-mers this rank owns)
+ * [5]=hits of this handle's queries [6]=with ranks: index entries routed to this rank's band */
 int skm_matrix_counters(skm_matrix* m, uint64_t* out, int cap);
 int skm_matrix_pairs(skm_matrix* m, skm_pairs* out);
 void skm_pairs_free(skm_pairs* p);

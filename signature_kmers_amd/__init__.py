@@ -129,6 +129,8 @@ _SIGS = {
     "skm_calls_free": (None, [C.POINTER(_Calls)]),
     "skm_matrix_create": (C.c_int, [C.POINTER(_P), _P, _P, _P, _P, _P, C.c_size_t, C.c_uint32]),
     "skm_matrix_run": (C.c_int, [_P, C.POINTER(_MatrixOpts)]),
+    "skm_matrix_set_transport": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(_Transport)]),
+    "skm_matrix_set_comm": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "skm_matrix_last_timings": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int]),
     "skm_matrix_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int]),
     "skm_matrix_pairs": (C.c_int, [_P, C.POINTER(_Pairs)]),
@@ -313,13 +315,13 @@ class SignatureBuilder:
         return self.counters()["passes"]
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 25)()
-        n = lib().skm_build_counters(self._h, v, 25)
+        v = (C.c_uint64 * 26)()
+        n = lib().skm_build_counters(self._h, v, 26)
         names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped",
                  "overflow_elements", "overflow_kept", "big_groups", "big_kept", "passes", "valid", "giant_chains",
                  "giant_max", "redone", "cap_overflow_scratch", "cap_split", "cap_long_samples", "cap_long_jobs",
                  "demand_overflow_scratch", "demand_split", "demand_long_samples", "demand_long_jobs",
-                 "long_samples"]
+                 "long_samples", "routed"]
         return {names[i]: int(v[i]) for i in range(n)}
 
     def debug_jobs(self, k: int = 64) -> list:
@@ -755,6 +757,18 @@ class MatrixDistance:
         _check(lib().skm_matrix_create(C.byref(self._h), db._h, _ptr(residues), _ptr(seq_off), _ptr(seq_len),
                                        _ptr(seq_idx), len(seq_len), self.n_idx))
 
+    def set_transport(self, transport: "GlooTransport"):
+        """Join the ranks of a multi-GPU matrix distance through a host transport: this handle's
+        queries are rank transport.rank's range; run() becomes collective and pairs() returns the
+        rank's row band (skm_matrix_tile_rows)."""
+        self._transport = transport
+        _check(lib().skm_matrix_set_transport(self._h, transport.rank, transport.world, transport.ptr))
+
+    def set_comm(self, unique_id: bytes, rank: int, world: int):
+        """Join the ranks over RCCL (collective; rank 0's comm_unique_id broadcast to every rank)."""
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
+        _check(lib().skm_matrix_set_comm(self._h, rank, world, buf))
+
     def run(self, rows=None, max_tile_bytes: int = 0):
         a, b = rows if rows is not None else (0, 0)
         opts = _MatrixOpts(self.hypo_index, a, b, 0, max_tile_bytes)
@@ -766,9 +780,10 @@ class MatrixDistance:
         return dict(zip(["hits", "group", "pairs", "emit", "total"], list(ms)[:n]))
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 5)()
-        n = lib().skm_matrix_counters(self._h, v, 5)
-        return dict(zip(["windows", "hits", "increments", "pairs", "kmers"], [int(x) for x in list(v)[:n]]))
+        v = (C.c_uint64 * 7)()
+        n = lib().skm_matrix_counters(self._h, v, 7)
+        return dict(zip(["windows", "hits", "increments", "pairs", "kmers", "local_hits", "routed"],
+                        [int(x) for x in list(v)[:n]]))
 
     def pairs(self) -> np.ndarray:
         """(n, 3) u32 (id1, id2, count), id1 < id2, sorted by (id1, id2)."""

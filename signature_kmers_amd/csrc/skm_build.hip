@@ -1507,14 +1507,19 @@ __global__ __launch_bounds__(256) void k_route_sketch(const uint8_t* __restrict_
     }
 }
 
+// counts mode: pass_bits == owner_bits == 0 -> by the top 6 hash bits; else by (pass id <<
+// owner_bits | owner),
+// ncnt = 2^(pass_bits + owner_bits) counters (<= 4096).  Dynamic LDS: ncnt counters, then the Bloom
+// filter when routing.
 __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ res, uint64_t rp, int pass_bits,
-                                                  uint8_t* __restrict__ ids, unsigned long long* __restrict__ counts,
-                                                  const uint32_t* __restrict__ bloom) {
-    __shared__ uint32_t s_cnt[64];
-    extern __shared__ uint32_t s_bloom[];  // (1 << BLOOM_BITS) / 32 words when routing
-    if (counts) {
-        if (threadIdx.x < 64) s_cnt[threadIdx.x] = 0;
-    }
+                                                  int owner_bits, uint8_t* __restrict__ ids,
+                                                  unsigned long long* __restrict__ counts,
+                                                  const uint32_t* __restrict__ bloom, uint32_t ncnt) {
+    extern __shared__ uint32_t s_dyn[];
+    uint32_t* s_cnt = s_dyn;
+    uint32_t* s_bloom = s_dyn + ncnt;  // (1 << BLOOM_BITS) / 32 words when routing
+    if (counts)
+        for (uint32_t c = threadIdx.x; c < ncnt; c += blockDim.x) s_cnt[c] = 0;
     const bool route = bloom != nullptr && pass_bits >= 1;
     if (route)
         for (uint32_t w = threadIdx.x; w < (1u << BLOOM_BITS) / 32u; w += blockDim.x) s_bloom[w] = bloom[w];
@@ -1545,12 +1550,15 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
             uint32_t id = 0xFFu;
             if (((valid >> t) & 0xFFu) == 0xFFu && base + t < rp) {
                 const uint64_t h = mix43(k);
-                if (pass_bits == 0) {
+                if (pass_bits == 0 && owner_bits == 0) {
                     if (counts) atomicAdd(&s_cnt[(uint32_t)(h >> (KEY_BITS - 6))], 1u);
                 } else {
-                    id = (uint32_t)(h >> (KEY_BITS - pass_bits));
+                    id = pass_bits ? (uint32_t)(h >> (KEY_BITS - pass_bits)) : 0u;
                     if (route && id >= half && bloom_has(s_bloom, h)) id -= half;
-                    if (counts) atomicAdd(&s_cnt[id], 1u);
+                    if (counts) {
+                        const uint32_t own = (uint32_t)(h >> (KEY_BITS - pass_bits - owner_bits)) & ((1u << owner_bits) - 1u);
+                        atomicAdd(&s_cnt[(id << owner_bits) | own], 1u);
+                    }
                 }
             }
             out[t >> 2] |= id << (8 * (t & 3));
@@ -1559,7 +1567,8 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
     }
     if (counts) {
         __syncthreads();
-        if (threadIdx.x < 64 && s_cnt[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)s_cnt[threadIdx.x]);
+        for (uint32_t c = threadIdx.x; c < ncnt; c += blockDim.x)
+            if (s_cnt[c]) atomicAdd(&counts[c], (unsigned long long)s_cnt[c]);
     }
 }
 
@@ -4029,6 +4038,63 @@ __global__ void k_count_flags(const uint8_t* __restrict__ flags, uint32_t nseq, 
     if ((threadIdx.x & 63) == 0 && local) atomicAdd(out, (unsigned long long)local);
 }
 
+// world > 1 exchange of one pass (exchange()): per-bucket element counts from the owner-major
+// bucket starts; each peer's total is checked against the prepare-time count the transfer sizes
+// were planned with (a mismatch fails the run with SKM_E_STATE instead of mis-sized transfers)
+__global__ void k_send_counts(const uint64_t* __restrict__ bstart, uint32_t NB, uint32_t NB1, uint32_t W,
+                              const unsigned long long* __restrict__ expect, unsigned long long* __restrict__ run,
+                              uint32_t* __restrict__ out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < NB) out[t] = (uint32_t)(bstart[t + 1] - bstart[t]);
+    if (t < W && bstart[(uint64_t)(t + 1) * NB1] - bstart[(uint64_t)t * NB1] != expect[t])
+        atomicOr(&run[RUN_FLAGS], (unsigned long long)RUN_F_CAP);
+}
+
+// the receive layout from the received counts cnt[source][bucket] (one workgroup): source-major
+// pieces (seg_start = exclusive scan of the flattened counts, seg_len = counts) and the bucket-major
+// virtual numbering the partition kernel uses (vstart[k] = elements of buckets < k over all
+// sources; vstart[NB1] = the pass's element count, read by the overflow plan)
+__global__ __launch_bounds__(1024) void k_recv_plan(const uint32_t* __restrict__ cnt, uint32_t W, uint32_t NB1,
+                                                    const unsigned long long* __restrict__ expect,
+                                                    unsigned long long* __restrict__ run,
+                                                    uint64_t* __restrict__ seg_start, uint32_t* __restrict__ seg_len,
+                                                    uint64_t* __restrict__ vstart) {
+    __shared__ uint32_t s_wave[17];
+    __shared__ unsigned long long s_tot[64];
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t N = W * NB1;
+    {   // flat exclusive scan (consecutive chunks per thread)
+        const uint32_t per = (N + nt - 1) / nt, a = min(N, tid * per), e = min(N, a + per);
+        uint32_t loc = 0;
+        for (uint32_t i = a; i < e; ++i) loc += cnt[i];
+        uint32_t tot;
+        uint64_t run_ = wg_exclusive_scan(loc, s_wave, tot);
+        for (uint32_t i = a; i < e; ++i) {
+            seg_start[i] = run_;
+            seg_len[i] = cnt[i];
+            run_ += cnt[i];
+        }
+    }
+    if (tid < 64) s_tot[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < N; i += nt) atomicAdd(&s_tot[i / NB1], (unsigned long long)cnt[i]);
+    __syncthreads();
+    if (tid < W && s_tot[tid] != expect[tid]) atomicOr(&run[RUN_FLAGS], (unsigned long long)RUN_F_CAP);
+    {   // per-bucket sums over the sources, exclusive scan over the buckets
+        const uint32_t per = (NB1 + nt - 1) / nt, a = min(NB1, tid * per), e = min(NB1, a + per);
+        uint32_t loc = 0;
+        for (uint32_t k = a; k < e; ++k)
+            for (uint32_t p = 0; p < W; ++p) loc += cnt[(uint64_t)p * NB1 + k];
+        uint32_t tot;
+        uint64_t run_ = wg_exclusive_scan(loc, s_wave, tot);
+        for (uint32_t k = a; k < e; ++k) {
+            vstart[k] = run_;
+            for (uint32_t p = 0; p < W; ++p) run_ += cnt[(uint64_t)p * NB1 + k];
+        }
+        if (tid == 0) vstart[NB1] = tot;
+    }
+}
+
 // skm_build_finish_slice: kept k-mers of one output slice (top bits of slice_hash(key)), compacted
 // in any order (the host sorts them); count first, then the copy into the slice's own buffers
 __global__ __launch_bounds__(256) void k_slice_select(const uint64_t* __restrict__ keys,
@@ -4165,7 +4231,11 @@ struct skm_build {
     DevBuf d_rhi, d_rlo;                 // received elements, [source rank][level-1 bucket]
     DevBuf d_cnt_send, d_cnt_recv;       // [world][NB1] element counts
     DevBuf d_seg_start, d_seg_len, d_vstart;
-    std::vector<uint64_t> send_off, send_cnt, recv_off, recv_cnt;
+    // elements this rank sends to / receives from each peer in each pass ([pass][peer], exchanged
+    // at prepare: pass_peer_counts), their device copy (sends, then receives) for the checks
+    std::vector<uint64_t> xs_send, xs_recv;
+    DevBuf d_xs;
+    uint64_t n_local_max = 0;            // the largest pass's received elements
     uint64_t n_local = 0;                // elements this rank groups (received, or extracted at world 1)
     uint64_t cap_local = 0;
 
@@ -4211,6 +4281,7 @@ struct skm_build {
     DevBuf d_ids;                       // per-window pass id (pass_bits > 0)
     DevBuf d_bloom;                     // heavy-key routing filter (route)
     bool route = false;
+    uint64_t routed = 0;                // occurrences routed into the first half of the passes
     // a pass's window positions, level-1 histogram matrix and window count, double-buffered: the
     // next pass's compaction + count run on stx during this pass's group-by (prefetch_pass)
     DevBuf d_pos2[2], d_hist2[2], d_npos;
@@ -4683,8 +4754,8 @@ void size_passes(skm_build* b, int forced_pb = -1) {
     d_cnt.ensure(8 * 64);
     SKM_HIP(hipMemsetAsync(d_cnt.p, 0, 8 * 64, b->stream));
     if (b->rp)
-        hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 0, b->stream, b->d_res.as<uint8_t>(), b->rp, 0,
-                           nullptr, d_cnt.as<unsigned long long>(), nullptr);
+        hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 4u * 64, b->stream, b->d_res.as<uint8_t>(), b->rp, 0, 0,
+                           nullptr, d_cnt.as<unsigned long long>(), nullptr, 64u);
     SKM_HIP(hipGetLastError());
     uint64_t cnt[64];
     SKM_HIP(hipMemcpyAsync(cnt, d_cnt.p, sizeof(cnt), hipMemcpyDeviceToHost, b->stream));
@@ -4726,6 +4797,7 @@ void size_passes(skm_build* b, int forced_pb = -1) {
     // the Bloom filter of the keys whose estimate reaches route_heavy_min / 64 (with 15 % slack),
     // then the pass sizes once more, by routed pass id
     b->route = false;
+    b->routed = 0;
     if (pb >= 2 && b->world == 1 && b->tune.route_heavy_min > 0 && b->rp) {
         DevBuf cms;
         cms.ensure(4ull << (CMS_BITS + 1));
@@ -4737,15 +4809,21 @@ void size_passes(skm_build* b, int forced_pb = -1) {
                            cms.as<uint32_t>(), 0u, nullptr);
         hipLaunchKernelGGL(k_route_sketch, dim3(2048), dim3(256), 0, b->stream, b->d_res.as<uint8_t>(), b->rp,
                            cms.as<uint32_t>(), thresh, b->d_bloom.as<uint32_t>());
+        uint64_t natural_late = 0;  // occurrences of the second half before routing
+        for (int p = 1 << (pb - 1); p < (1 << pb); ++p)
+            for (int i = 0; i < (64 >> pb); ++i) natural_late += cnt[p * (64 >> pb) + i];
         SKM_HIP(hipMemsetAsync(d_cnt.p, 0, 8 * 64, b->stream));
-        hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), (1u << BLOOM_BITS) / 8, b->stream, b->d_res.as<uint8_t>(),
-                           b->rp, pb, nullptr, d_cnt.as<unsigned long long>(), b->d_bloom.as<uint32_t>());
+        hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 4u * 64 + (1u << BLOOM_BITS) / 8, b->stream,
+                           b->d_res.as<uint8_t>(), b->rp, pb, 0, nullptr, d_cnt.as<unsigned long long>(),
+                           b->d_bloom.as<uint32_t>(), 64u);
         SKM_HIP(hipGetLastError());
         SKM_HIP(hipMemcpyAsync(cnt, d_cnt.p, sizeof(cnt), hipMemcpyDeviceToHost, b->stream));
         SKM_HIP(hipStreamSynchronize(b->stream));
-        uint64_t m = 0;
+        uint64_t m = 0, late = 0;
         for (int p = 0; p < (1 << pb); ++p) m = std::max<uint64_t>(m, cnt[p]);
+        for (int p = 1 << (pb - 1); p < (1 << pb); ++p) late += cnt[p];
         b->pass_max = m;
+        b->routed = natural_late - late;
         b->route = true;
     }
     SKM_CHECK(b->pass_max < (1ull << 32), SKM_E_ARG, "more than 2^32 occurrences in one pass of one GPU shard");
@@ -4826,6 +4904,7 @@ void size_arena(skm_build* b) {
 }
 
 void alloc_caps(skm_build* b);
+void pass_peer_counts(const Ranks& bs);
 
 void prepare(const Ranks& bs) {
     bool need = false;
@@ -4895,6 +4974,7 @@ void prepare(const Ranks& bs) {
             allgatherv(bs, {src_i[0]}, {dst_i[0]}, bytes);
         }
         sync_all(bs);
+        pass_peer_counts(bs);  // every pass's send / receive sizes, known to the host from here on
         for (size_t k = 0; k < bs.size(); ++k) {
             skm_build* b = bs[k];
             b->g_seqid.resize(tot);
@@ -4902,7 +4982,7 @@ void prepare(const Ranks& bs) {
             b->g_strict = true;
             for (uint64_t s = 1; s < tot; ++s)
                 if (b->g_seqid[s] <= b->g_seqid[s - 1]) b->g_strict = false;
-            ensure_local(b, b->pass_max);  // first guess; grown at run time if the exchange brings more
+            ensure_local(b, std::max(b->pass_max, b->n_local_max));  // the largest pass's received elements
         }
     }
     for (auto* b : bs) {
@@ -5030,23 +5110,22 @@ void phase_extract(skm_build* b, uint32_t pass) {
     SKM_HIP(hipEventRecord(b->ev[3], st));
 }
 
-// world > 1: send layout from the local bucket starts, counts all-to-all, receive layout
-void exchange(const Ranks& bs) {
+// world > 1, one key-range pass: the element counts of every (pass, peer) pair were exchanged at
+// prepare (pass_peer_counts), so every size of the pass's all-to-alls is a host value already and
+// the exchange issues without a host round trip: per-bucket counts (fixed size) and the elements
+// (RCCL: stream-ordered grouped send/recv; the in-process group and the host transport stage and
+// synchronise inside alltoallv), then the receive layout is planned on the device (k_recv_plan).
+void exchange(const Ranks& bs, uint32_t pass) {
     const int W = bs[0]->world;
     const uint32_t NB1 = 1u << bs[0]->b1_bits;
     const uint32_t NB = NB1 * (uint32_t)W;
-    // 1. per-peer counts of its buckets
-    A2A cx;
+    A2A cx, ex_hi, ex_lo;
     for (auto* b : bs) {
-        std::vector<uint64_t> abs(NB + 1);
-        SKM_HIP(hipMemcpyAsync(abs.data(), b->d_bstart.p, 8 * (NB + 1), hipMemcpyDeviceToHost, b->stream));
-        SKM_HIP(hipStreamSynchronize(b->stream));
-        const SendPlan sp = plan_send(abs.data(), W, NB1);
-        b->send_off = sp.off;
-        b->send_cnt = sp.n;
         b->d_cnt_send.ensure(4ull * NB);
         b->d_cnt_recv.ensure(4ull * NB);
-        SKM_HIP(hipMemcpy(b->d_cnt_send.p, sp.cnt.data(), 4ull * NB, hipMemcpyHostToDevice));
+        SKM_LAUNCH(b, k_send_counts, dim3((NB + 255) / 256), dim3(256), 0, b->stream, b->d_bstart.as<uint64_t>(), NB, NB1,
+                   (uint32_t)W, b->d_xs.as<unsigned long long>() + (uint64_t)pass * W, b->d_run.as<unsigned long long>(),
+                   b->d_cnt_send.as<uint32_t>());
         cx.send.push_back(b->d_cnt_send.as<uint8_t>());
         cx.recv.push_back(b->d_cnt_recv.as<uint8_t>());
         std::vector<uint64_t> off(W), c(W, 4ull * NB1);
@@ -5055,35 +5134,16 @@ void exchange(const Ranks& bs) {
         cx.scnt.push_back(c);
         cx.roff.push_back(off);
         cx.rcnt.push_back(c);
-    }
-    alltoallv(bs, cx);
-    // 2. receive layout: source-major pieces, bucket-major virtual numbering for tmp
-    A2A ex_hi, ex_lo;
-    for (auto* b : bs) {
-        std::vector<uint32_t> rc(NB);  // [source][bucket]
-        SKM_HIP(hipMemcpyAsync(rc.data(), b->d_cnt_recv.p, 4ull * NB, hipMemcpyDeviceToHost, b->stream));
-        SKM_HIP(hipStreamSynchronize(b->stream));
-        const RecvPlan rp = plan_recv(rc.data(), W, NB1);
-        b->recv_off = rp.off;
-        b->recv_cnt = rp.n;
-        b->n_local = rp.total;
-        if (rp.total > b->cap_local) {
-            ensure_local(b, rp.total);
-            SKM_HIP(hipDeviceSynchronize());  // the chain lists follow the grown element capacity
-            alloc_caps(b);
-        }
-        b->d_seg_start.ensure(8ull * NB);
-        b->d_seg_len.ensure(4ull * NB);
-        b->d_vstart.ensure(8ull * (NB1 + 1));
-        SKM_HIP(hipMemcpy(b->d_seg_start.p, rp.seg_start.data(), 8ull * NB, hipMemcpyHostToDevice));
-        SKM_HIP(hipMemcpy(b->d_seg_len.p, rp.seg_len.data(), 4ull * NB, hipMemcpyHostToDevice));
-        SKM_HIP(hipMemcpy(b->d_vstart.p, rp.vstart.data(), 8ull * (NB1 + 1), hipMemcpyHostToDevice));
         std::vector<uint64_t> so(W), sc(W), ro(W), rcn(W);
+        uint64_t s0 = 0, r0 = 0;
         for (int q = 0; q < W; ++q) {
-            so[q] = 8 * b->send_off[q];
-            sc[q] = 8 * b->send_cnt[q];
-            ro[q] = 8 * b->recv_off[q];
-            rcn[q] = 8 * b->recv_cnt[q];
+            const uint64_t ns = b->xs_send[(uint64_t)pass * W + q], nr = b->xs_recv[(uint64_t)pass * W + q];
+            so[q] = 8 * s0;
+            sc[q] = 8 * ns;
+            ro[q] = 8 * r0;
+            rcn[q] = 8 * nr;
+            s0 += ns;
+            r0 += nr;
         }
         ex_hi.send.push_back(b->d_recs_hi.as<uint8_t>());
         ex_hi.recv.push_back(b->d_rhi.as<uint8_t>());
@@ -5096,8 +5156,79 @@ void exchange(const Ranks& bs) {
             e->rcnt.push_back(rcn);
         }
     }
+    alltoallv(bs, cx);
     alltoallv(bs, ex_hi);
     alltoallv(bs, ex_lo);
+    for (auto* b : bs) {
+        b->d_seg_start.ensure(8ull * NB);
+        b->d_seg_len.ensure(4ull * NB);
+        b->d_vstart.ensure(8ull * (NB1 + 1));
+        SKM_LAUNCH(b, k_recv_plan, dim3(1), dim3(1024), 0, b->stream, b->d_cnt_recv.as<uint32_t>(), (uint32_t)W, NB1,
+                   b->d_xs.as<unsigned long long>() + (uint64_t)(b->xs_recv.size() / W + pass) * W,
+                   b->d_run.as<unsigned long long>(), b->d_seg_start.as<uint64_t>(), b->d_seg_len.as<uint32_t>(),
+                   b->d_vstart.as<uint64_t>());
+        SKM_HIP(hipGetLastError());
+    }
+}
+
+// world > 1, at prepare: every rank's valid windows by (pass, owner) -- one counting scan -- and
+// one all-to-all of those counts, so each pass's send and receive sizes are known to the host up
+// front; the received elements of the largest pass size this rank's work buffers
+void pass_peer_counts(const Ranks& bs) {
+    const int W = bs[0]->world;
+    const uint32_t P = 1u << bs[0]->pass_bits;
+    A2A x;
+    std::vector<DevBuf> snd(bs.size()), rcv(bs.size());
+    for (size_t k = 0; k < bs.size(); ++k) {
+        skm_build* b = bs[k];
+        DevBuf cnt;
+        cnt.ensure(8ull * P * W);
+        SKM_HIP(hipMemsetAsync(cnt.p, 0, 8ull * P * W, b->stream));
+        if (b->rp)
+            hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 4u * P * W, b->stream, b->d_res.as<uint8_t>(), b->rp,
+                               b->pass_bits, b->owner_bits, nullptr, cnt.as<unsigned long long>(), nullptr, P * W);
+        SKM_HIP(hipGetLastError());
+        std::vector<uint64_t> c(P * W), t(P * W);
+        SKM_HIP(hipMemcpyAsync(c.data(), cnt.p, 8ull * P * W, hipMemcpyDeviceToHost, b->stream));
+        SKM_HIP(hipStreamSynchronize(b->stream));
+        b->xs_send = c;  // [pass][peer]
+        for (uint32_t p = 0; p < P; ++p)
+            for (int q = 0; q < W; ++q) t[(uint64_t)q * P + p] = c[(uint64_t)p * W + q];  // [peer][pass]
+        snd[k].ensure(8ull * P * W);
+        rcv[k].ensure(8ull * P * W);
+        SKM_HIP(hipMemcpy(snd[k].p, t.data(), 8ull * P * W, hipMemcpyHostToDevice));
+        x.send.push_back(snd[k].as<uint8_t>());
+        x.recv.push_back(rcv[k].as<uint8_t>());
+        std::vector<uint64_t> off(W), n(W, 8ull * P);
+        for (int q = 0; q < W; ++q) off[q] = 8ull * P * q;
+        x.soff.push_back(off);
+        x.scnt.push_back(n);
+        x.roff.push_back(off);
+        x.rcnt.push_back(n);
+    }
+    alltoallv(bs, x);
+    sync_all(bs);
+    for (size_t k = 0; k < bs.size(); ++k) {
+        skm_build* b = bs[k];
+        std::vector<uint64_t> t(P * W);
+        SKM_HIP(hipMemcpy(t.data(), rcv[k].p, 8ull * P * W, hipMemcpyDeviceToHost));
+        b->xs_recv.assign((uint64_t)P * W, 0);
+        uint64_t most = 0;
+        for (uint32_t p = 0; p < P; ++p) {
+            uint64_t tot = 0;
+            for (int q = 0; q < W; ++q) {
+                b->xs_recv[(uint64_t)p * W + q] = t[(uint64_t)q * P + p];  // [pass][source]
+                tot += t[(uint64_t)q * P + p];
+            }
+            most = std::max(most, tot);
+        }
+        SKM_CHECK(most < (1ull << 32) - (1ull << 28), SKM_E_ARG, "more than 2^32 occurrences in one pass of one GPU");
+        b->n_local_max = most;
+        // device copy for the exchange's checks: [pass][peer] sends, then [pass][source] receives
+        b->d_xs.ensure(16ull * P * W);
+        SKM_HIP(hipMemcpy(b->d_xs.p, b->xs_send.data(), 8ull * P * W, hipMemcpyHostToDevice));
+        SKM_HIP(hipMemcpy(b->d_xs.as<uint64_t>() + (uint64_t)P * W, b->xs_recv.data(), 8ull * P * W, hipMemcpyHostToDevice));
+    }
 }
 
 // Job sort by length class (longest first) + the chain kernels, for a job list whose length is on
@@ -5215,11 +5346,8 @@ void phase_group(skm_build* b, uint32_t pass) {
     SKM_HIP(hipEventRecord(b->ev_pf_ready, st));
     // ---- the overflow plan (the pass's element count: the last bucket start, or the exchange's) ----
     const unsigned long long* nloc_d;
-    if (multi) {  // the exchange already synchronised this pass: the count is a host value
-        unsigned long long* pin = b->pinned_ctr();
-        pin[40] = b->n_local;
-        SKM_HIP(hipMemcpyAsync(run_d + RUN_NLOC, pin + 40, 8, hipMemcpyHostToDevice, st));
-        nloc_d = run_d + RUN_NLOC;
+    if (multi) {  // the received element count: k_recv_plan's vstart[NB1]
+        nloc_d = reinterpret_cast<const unsigned long long*>(b->d_vstart.as<uint64_t>() + NB1);
     } else {
         nloc_d = reinterpret_cast<const unsigned long long*>(b->d_bstart.as<uint64_t>() + NB1);
     }
@@ -5438,8 +5566,8 @@ void begin_run(skm_build* b) {
                            b->d_data.as<skm_stored_kmer_data>());
     if (b->pass_bits && b->rp)
         SKM_LAUNCH(b, k_pass_ids, dim3(4096), dim3(256), b->route ? (1u << BLOOM_BITS) / 8 : 0u, st,
-                   b->d_res.as<uint8_t>(), b->rp, b->pass_bits, b->d_ids.as<uint8_t>(), nullptr,
-                   b->route ? b->d_bloom.as<uint32_t>() : nullptr);
+                   b->d_res.as<uint8_t>(), b->rp, b->pass_bits, 0, b->d_ids.as<uint8_t>(), nullptr,
+                   b->route ? b->d_bloom.as<uint32_t>() : nullptr, 0u);
     SKM_HIP(hipGetLastError());
     b->acc = skm_build::Acc{};
     b->kt_used = 0;
@@ -5611,7 +5739,7 @@ void run_once(const Ranks& bs) {
             use_evset(b, pass);
             phase_extract(b, pass);
         }
-        if (bs[0]->world > 1) exchange(bs);
+        if (bs[0]->world > 1) exchange(bs, pass);
         for (auto* b : bs) {
             phase_group(b, pass);
             // the stashed long chains leave in batches (default two: the first half's chains
@@ -6108,12 +6236,12 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
-    const uint64_t v[25] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+    const uint64_t v[26] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
                             b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total,
                             b->giant_jobs, b->giant_max, b->n_redo, b->tot_cap, b->split_cap, b->long_cap,
                             b->long_jobs_cap, b->demand[0], b->demand[1], b->demand[2], b->demand[3],
-                            b->long_samples};
-    int n = std::min(cap, 25);
+                            b->long_samples, b->routed};
+    int n = std::min(cap, 26);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }

@@ -25,8 +25,13 @@
 //                  partner lists walked by a lane, long ones by a wave; nonzero columns compacted
 //                  in column order -- no global atomics on the counts, no dense matrix in HBM
 //   k_md_gather    (id1, id2, count) triples in row order
-// The hit records are identical on every GPU (each recomputes them: ~3 % of the time), so the
-// row tiles need no collective; the host concatenates the tiles in row order.
+// Multi-GPU (skm_matrix_set_transport / skm_matrix_set_comm): rank r of W holds a
+// contiguous range of the query sequences.  It looks up only those (k_md_hits), sends each hit to
+// the k-mer's owner GPU (k_md_owner_*, one all-to-all), the owner groups its k-mers (slot table +
+// radix sort) and sends every group's members to the GPUs whose row band (skm_matrix_tile_rows)
+// the group has pairs in -- the suffix of members from the band's first row on (k_md_route_*,
+// one all-to-all) -- and each GPU counts the pairs of its band from the groups it received.  The
+// host concatenates the bands in row order.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -37,6 +42,10 @@
 #include "skm_common.h"
 #include "skm_lookup.h"
 #include "skm_util.h"
+
+#if defined(SKM_WITH_RCCL)
+#include <rccl/rccl.h>
+#endif
 
 namespace skm {
 
@@ -496,6 +505,102 @@ __global__ void k_md_gather(const uint32_t* __restrict__ scratch, const uint64_t
     }
 }
 
+// ---- multi-GPU: hits to the k-mer's owner, groups to the row bands they touch ----
+__device__ __forceinline__ uint32_t md_owner(uint64_t k, uint32_t W) {
+    return (uint32_t)(((xmix(k) >> 32) * (uint64_t)W) >> 32);
+}
+
+constexpr int OW_TILE = 4096;
+
+// cnt[W]: hits per owner (LDS counts per tile, one global add per owner per tile)
+__global__ __launch_bounds__(256) void k_md_owner_count(const unsigned long long* __restrict__ keys,
+                                                        const unsigned long long* __restrict__ nrec, uint32_t W,
+                                                        unsigned long long* __restrict__ cnt) {
+    __shared__ uint32_t c[64];
+    const uint64_t n = *nrec;
+    if (threadIdx.x < 64) c[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        atomicAdd(&c[md_owner(keys[i], W)], 1u);
+    __syncthreads();
+    if (threadIdx.x < W && c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], (unsigned long long)c[threadIdx.x]);
+}
+
+// owner-major send buffers: each tile reserves its owners' ranges once (cur[o] starts at the
+// owner's offset), then places its hits (order within an owner is immaterial: the owner sorts)
+__global__ __launch_bounds__(256) void k_md_owner_scatter(const unsigned long long* __restrict__ keys,
+                                                          const uint32_t* __restrict__ idx,
+                                                          const unsigned long long* __restrict__ nrec, uint32_t W,
+                                                          unsigned long long* __restrict__ cur,
+                                                          unsigned long long* __restrict__ skey,
+                                                          uint32_t* __restrict__ sidx) {
+    __shared__ uint32_t c[64];
+    __shared__ unsigned long long base[64];
+    const uint64_t n = *nrec;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * OW_TILE; t0 < n; t0 += (uint64_t)gridDim.x * OW_TILE) {
+        if (threadIdx.x < 64) c[threadIdx.x] = 0;
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < OW_TILE && t0 + j < n; j += blockDim.x) atomicAdd(&c[md_owner(keys[t0 + j], W)], 1u);
+        __syncthreads();
+        if (threadIdx.x < W) {
+            base[threadIdx.x] = c[threadIdx.x] ? atomicAdd(&cur[threadIdx.x], (unsigned long long)c[threadIdx.x]) : 0ull;
+            c[threadIdx.x] = 0;
+        }
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < OW_TILE && t0 + j < n; j += blockDim.x) {
+            const unsigned long long k = keys[t0 + j];
+            const uint32_t o = md_owner(k, W);
+            const uint64_t at = base[o] + atomicAdd(&c[o], 1u);
+            skey[at] = k;
+            sidx[at] = idx[t0 + j];
+        }
+        __syncthreads();
+    }
+}
+
+// first composite of the group [a, e) whose index is >= lo (the group is sorted by index)
+__device__ __forceinline__ uint64_t md_first_ge(const uint64_t* __restrict__ comp, uint64_t a, uint64_t e,
+                                                uint64_t idx_mask, uint64_t lo) {
+    while (a < e) {
+        const uint64_t mid = (a + e) >> 1;
+        if ((comp[mid] & idx_mask) < lo) a = mid + 1; else e = mid;
+    }
+    return a;
+}
+
+// cnt[b * G + g]: members group g sends to band b -- its suffix from band b's first row, when a
+// member of the band has a partner after it; 0 otherwise
+__global__ void k_md_route_count(const uint64_t* __restrict__ comp, const uint64_t* __restrict__ segstart,
+                                 uint64_t G, uint64_t idx_mask, const uint32_t* __restrict__ band, uint32_t W,
+                                 uint32_t* __restrict__ cnt) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t a = segstart[g], e = segstart[g + 1];
+        for (uint32_t b = 0; b < W; ++b) {
+            const uint64_t f = md_first_ge(comp, a, e, idx_mask, band[b]);
+            const bool send = f + 1 < e && (comp[f] & idx_mask) < band[b + 1];
+            cnt[(uint64_t)b * G + g] = send ? (uint32_t)(e - f) : 0u;
+        }
+    }
+}
+
+// the members of each group for each band, as (gid << idx_bits | index) with gid = gbase + g
+// (globally increasing in source-rank order: the receiver's composites are already sorted)
+__global__ void k_md_route_fill(const uint64_t* __restrict__ comp, const uint64_t* __restrict__ segstart, uint64_t G,
+                                uint64_t idx_mask, uint32_t idx_bits, const uint32_t* __restrict__ band, uint32_t W,
+                                const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ off,
+                                const uint64_t* __restrict__ sbase, uint64_t gbase, uint64_t* __restrict__ out) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e = segstart[g + 1];
+        for (uint32_t b = 0; b < W; ++b) {
+            const uint32_t c = cnt[(uint64_t)b * G + g];
+            if (!c) continue;
+            uint64_t* dst = out + sbase[b] + off[(uint64_t)b * (G + 1) + g];
+            const uint64_t f = e - c;
+            for (uint32_t j = 0; j < c; ++j) dst[j] = ((gbase + g) << idx_bits) | (comp[f + j] & idx_mask);
+        }
+    }
+}
+
 }  // namespace skm
 
 using namespace skm;
@@ -512,16 +617,260 @@ struct skm_matrix {
     Scanner scan;
     uint64_t n_hits = 0, n_incs = 0, n_pairs = 0, n_groups = 0;
     bool ran = false;
+    // ranks: this handle's queries are rank `rank` of `world`; joined by a host transport or RCCL
+    int rank = 0, world = 1;
+    skm_transport tp{};
+#if defined(SKM_WITH_RCCL)
+    ncclComm_t comm = nullptr;
+#endif
+    DevBuf d_ocnt, d_skey, d_sidx, d_band, d_rtc, d_rto, d_sbase, d_send, d_xbuf;
+    uint64_t n_local_hits = 0, n_routed = 0;
+    uint32_t band_lo = 0, band_hi = 0;
 };
 
 namespace {
+
+// ---- rank collectives of the multi-GPU matrix (host transport or RCCL) ----
+#if defined(SKM_WITH_RCCL)
+#define MX_NCCL(x)                                                                                          \
+    do {                                                                                                    \
+        ncclResult_t _r = (x);                                                                              \
+        if (_r != ncclSuccess) throw skm::Error(SKM_E_COMM, std::string("RCCL: ") + ncclGetErrorString(_r)); \
+    } while (0)
+#endif
+
+void mx_tp_check(int rc, const char* what) {
+    SKM_CHECK(rc == 0, SKM_E_COMM, std::string("host transport ") + what + " failed");
+}
+
+// device all-to-all of bytes: send + soff[q] (scnt[q]) to rank q, received at recv + roff[p]
+void mx_alltoallv(skm_matrix* M, const uint8_t* send, const std::vector<uint64_t>& soff,
+                  const std::vector<uint64_t>& scnt, uint8_t* recv, const std::vector<uint64_t>& roff,
+                  const std::vector<uint64_t>& rcnt) {
+    const int W = M->world, me = M->rank;
+    if (M->tp.alltoallv) {
+        std::vector<uint64_t> so(W), ro(W);
+        uint64_t st = 0, rt = 0;
+        for (int q = 0; q < W; ++q) {
+            so[q] = st;
+            st += scnt[q];
+            ro[q] = rt;
+            rt += rcnt[q];
+        }
+        std::vector<uint8_t> hs(std::max<uint64_t>(st, 1)), hr(std::max<uint64_t>(rt, 1));
+        SKM_HIP(hipStreamSynchronize(M->stream));
+        for (int q = 0; q < W; ++q)
+            if (scnt[q]) SKM_HIP(hipMemcpy(hs.data() + so[q], send + soff[q], scnt[q], hipMemcpyDeviceToHost));
+        mx_tp_check(M->tp.alltoallv(M->tp.ctx, hs.data(), scnt.data(), so.data(), hr.data(), rcnt.data(), ro.data()),
+                    "alltoallv");
+        for (int q = 0; q < W; ++q)
+            if (rcnt[q]) SKM_HIP(hipMemcpy(recv + roff[q], hr.data() + ro[q], rcnt[q], hipMemcpyHostToDevice));
+        return;
+    }
+#if defined(SKM_WITH_RCCL)
+    SKM_CHECK(M->comm, SKM_E_STATE, "matrix ranks joined by neither a transport nor a communicator");
+    if (scnt[me]) SKM_HIP(hipMemcpyAsync(recv + roff[me], send + soff[me], scnt[me], hipMemcpyDeviceToDevice, M->stream));
+    MX_NCCL(ncclGroupStart());
+    for (int q = 0; q < W; ++q) {
+        if (q == me) continue;
+        if (scnt[q]) MX_NCCL(ncclSend(send + soff[q], scnt[q], ncclUint8, q, M->comm, M->stream));
+        if (rcnt[q]) MX_NCCL(ncclRecv(recv + roff[q], rcnt[q], ncclUint8, q, M->comm, M->stream));
+    }
+    MX_NCCL(ncclGroupEnd());
+#else
+    (void)me;
+    throw Error(SKM_E_COMM, "libskm was built without RCCL");
+#endif
+}
+
+// every rank sends one u64 to every rank: out[p] = what rank p sent to this rank
+std::vector<uint64_t> mx_exchange_u64(skm_matrix* M, const std::vector<uint64_t>& mine) {
+    const int W = M->world;
+    std::vector<uint64_t> out(W, 0);
+    if (M->tp.alltoallv) {
+        std::vector<uint64_t> c(W, 8), o(W);
+        for (int q = 0; q < W; ++q) o[q] = 8ull * q;
+        mx_tp_check(M->tp.alltoallv(M->tp.ctx, mine.data(), c.data(), o.data(), out.data(), c.data(), o.data()),
+                    "alltoallv");
+        return out;
+    }
+    M->d_xbuf.ensure(16ull * W);
+    uint8_t* d = M->d_xbuf.as<uint8_t>();
+    SKM_HIP(hipMemcpyAsync(d, mine.data(), 8ull * W, hipMemcpyHostToDevice, M->stream));
+    std::vector<uint64_t> c(W, 8), o(W);
+    for (int q = 0; q < W; ++q) o[q] = 8ull * q;
+    mx_alltoallv(M, d, o, c, d + 8ull * W, o, c);
+    SKM_HIP(hipMemcpyAsync(out.data(), d + 8ull * W, 8ull * W, hipMemcpyDeviceToHost, M->stream));
+    SKM_HIP(hipStreamSynchronize(M->stream));
+    return out;
+}
+
+// the composite group-by of n (kmer, index) hits (slot table + LSD radix sort): d_comp sorted,
+// d_S / d_seg the group boundaries; returns the number of groups
+uint64_t md_group(skm_matrix* M, const unsigned long long* keys, const uint32_t* idx, const unsigned long long* nrec,
+                  uint64_t n, uint32_t idx_bits, hipStream_t st) {
+    const int lg = std::max(4, ilog2_ceil(2 * std::max<uint64_t>(n, 1)));
+    const uint32_t key_bits = (uint32_t)lg + idx_bits;
+    SKM_CHECK(key_bits <= 64, SKM_E_ARG, "matrix distance: too many hits / sequences for 64-bit composites");
+    if (!n) return 0;
+    const uint64_t T = 1ull << lg;
+    M->d_tab.ensure(8 * T);
+    SKM_HIP(hipMemsetAsync(M->d_tab.p, 0, 8 * T, st));
+    M->d_comp.ensure(8 * n);
+    M->d_comp2.ensure(8 * n);
+    const uint32_t g = (uint32_t)std::min<uint64_t>(ceil_div(n, 256), 256ull * 32);
+    hipLaunchKernelGGL(k_md_slot, dim3(g), dim3(256), 0, st, keys, idx, nrec, M->d_tab.as<unsigned long long>(), T - 1,
+                       64u - (uint32_t)lg, idx_bits, M->d_comp.as<uint64_t>());
+    SKM_HIP(hipGetLastError());
+    const uint32_t nb = (uint32_t)ceil_div(n, RS_TILE);
+    M->d_hist.ensure(4ull * 256 * nb);
+    M->d_hoff.ensure(8ull * (256 * (uint64_t)nb + 1));
+    uint64_t* a = M->d_comp.as<uint64_t>();
+    uint64_t* b = M->d_comp2.as<uint64_t>();
+    for (uint32_t sh = 0; sh < key_bits; sh += 8) {
+        hipLaunchKernelGGL(k_rs_hist, dim3(nb), dim3(RS_THREADS), 0, st, a, n, (int)sh, nb, M->d_hist.as<uint32_t>());
+        M->scan.run(M->d_hist.as<uint32_t>(), 256ull * nb, M->d_hoff.as<uint64_t>(), st);
+        hipLaunchKernelGGL(k_rs_scatter, dim3(nb), dim3(RS_THREADS), 0, st, a, n, (int)sh, nb, M->d_hoff.as<uint64_t>(), b);
+        SKM_HIP(hipGetLastError());
+        std::swap(a, b);
+    }
+    if (a != M->d_comp.as<uint64_t>()) {
+        std::swap(M->d_comp.p, M->d_comp2.p);
+        std::swap(M->d_comp.bytes, M->d_comp2.bytes);
+    }
+    return 1;  // groups: md_bounds
+}
+
+// group boundaries of the sorted composites d_comp[0..n): S (scan of group starts), segstart
+uint64_t md_bounds(skm_matrix* M, uint64_t n, uint32_t idx_bits, hipStream_t st) {
+    if (!n) return 0;
+    M->d_flag.ensure(4 * n);
+    M->d_S.ensure(8 * (n + 1));
+    hipLaunchKernelGGL(k_md_starts, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, st, M->d_comp.as<uint64_t>(), n,
+                       idx_bits, M->d_flag.as<uint32_t>());
+    M->scan.run(M->d_flag.as<uint32_t>(), n, M->d_S.as<uint64_t>(), st);
+    M->d_seg.ensure(8 * (n + 1));
+    hipLaunchKernelGGL(k_md_segstart, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, st, M->d_flag.as<uint32_t>(),
+                       M->d_S.as<uint64_t>(), n, M->d_seg.as<uint64_t>());
+    SKM_HIP(hipGetLastError());
+    uint64_t G = 0;
+    SKM_HIP(hipMemcpyAsync(&G, M->d_S.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipStreamSynchronize(st));
+    return G;
+}
+
+// world > 1: hits -> owners -> groups -> bands; leaves this band's received groups in d_comp /
+// d_S / d_seg and returns their composite count
+uint64_t md_exchange(skm_matrix* M, uint64_t n_local, uint32_t idx_bits, hipStream_t st) {
+    const int W = M->world;
+    // 1. hits to the k-mer owners
+    M->d_ocnt.ensure(8ull * (2 * W));
+    unsigned long long* ocnt = M->d_ocnt.as<unsigned long long>();
+    SKM_HIP(hipMemsetAsync(ocnt, 0, 8ull * W, st));
+    const uint32_t ge = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(n_local, 256), 256ull * 32));
+    hipLaunchKernelGGL(k_md_owner_count, dim3(ge), dim3(256), 0, st, M->d_rkey.as<unsigned long long>(),
+                       M->d_nrec.as<unsigned long long>(), (uint32_t)W, ocnt);
+    SKM_HIP(hipGetLastError());
+    std::vector<uint64_t> sc(W), so(W, 0);
+    SKM_HIP(hipMemcpyAsync(sc.data(), ocnt, 8ull * W, hipMemcpyDeviceToHost, st));
+    SKM_HIP(hipStreamSynchronize(st));
+    for (int q = 1; q < W; ++q) so[q] = so[q - 1] + sc[q - 1];
+    M->d_skey.ensure(8 * std::max<uint64_t>(n_local, 1));
+    M->d_sidx.ensure(4 * std::max<uint64_t>(n_local, 1));
+    SKM_HIP(hipMemcpyAsync(ocnt + W, so.data(), 8ull * W, hipMemcpyHostToDevice, st));
+    const uint32_t gs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(n_local, OW_TILE), 4096));
+    hipLaunchKernelGGL(k_md_owner_scatter, dim3(gs), dim3(256), 0, st, M->d_rkey.as<unsigned long long>(),
+                       M->d_ridx.as<uint32_t>(), M->d_nrec.as<unsigned long long>(), (uint32_t)W, ocnt + W,
+                       M->d_skey.as<unsigned long long>(), M->d_sidx.as<uint32_t>());
+    SKM_HIP(hipGetLastError());
+    SKM_HIP(hipStreamSynchronize(st));  // the local hits are copied out before d_rkey / d_ridx are reused
+    const std::vector<uint64_t> rc = mx_exchange_u64(M, sc);
+    std::vector<uint64_t> ro(W, 0);
+    for (int q = 1; q < W; ++q) ro[q] = ro[q - 1] + rc[q - 1];
+    const uint64_t n_own = ro[W - 1] + rc[W - 1];
+    M->d_rkey.ensure(8 * std::max<uint64_t>(n_own, 1));  // the local hits were copied out already
+    M->d_ridx.ensure(4 * std::max<uint64_t>(n_own, 1));
+    auto scaled = [](const std::vector<uint64_t>& v, uint64_t k) {
+        std::vector<uint64_t> r(v.size());
+        for (size_t i = 0; i < v.size(); ++i) r[i] = v[i] * k;
+        return r;
+    };
+    SKM_HIP(hipStreamSynchronize(st));
+    mx_alltoallv(M, M->d_skey.as<uint8_t>(), scaled(so, 8), scaled(sc, 8), M->d_rkey.as<uint8_t>(), scaled(ro, 8),
+                 scaled(rc, 8));
+    mx_alltoallv(M, M->d_sidx.as<uint8_t>(), scaled(so, 4), scaled(sc, 4), M->d_ridx.as<uint8_t>(), scaled(ro, 4),
+                 scaled(rc, 4));
+    SKM_HIP(hipMemcpyAsync(M->d_nrec.p, &n_own, 8, hipMemcpyHostToDevice, st));
+    SKM_HIP(hipStreamSynchronize(st));
+    // 2. the owned k-mers' groups
+    md_group(M, M->d_rkey.as<unsigned long long>(), M->d_ridx.as<uint32_t>(), M->d_nrec.as<unsigned long long>(), n_own,
+             idx_bits, st);
+    const uint64_t G = md_bounds(M, n_own, idx_bits, st);
+    // 3. group suffixes to the row bands (band b = skm_matrix_tile_rows(n_idx, b, W))
+    std::vector<uint32_t> band(W + 1);
+    for (int q = 0; q < W; ++q) skm_matrix_tile_rows(M->nidx, q, W, &band[q], &band[q + 1]);
+    M->d_band.ensure(4ull * (W + 1));
+    SKM_HIP(hipMemcpyAsync(M->d_band.p, band.data(), 4ull * (W + 1), hipMemcpyHostToDevice, st));
+    SKM_HIP(hipStreamSynchronize(st));
+    std::vector<uint64_t> mine(W, G);
+    const std::vector<uint64_t> gall = mx_exchange_u64(M, mine);
+    uint64_t gbase = 0, gtot = 0;
+    for (int q = 0; q < W; ++q) {
+        if (q < M->rank) gbase += gall[q];
+        gtot += gall[q];
+    }
+    SKM_CHECK(gtot < (1ull << (64 - idx_bits)), SKM_E_ARG, "matrix distance: too many k-mer groups for 64-bit composites");
+    const uint64_t idx_mask = (1ull << idx_bits) - 1;
+    std::vector<uint64_t> bc(W, 0), bo(W, 0);
+    if (G) {
+        M->d_rtc.ensure(4ull * W * G);
+        M->d_rto.ensure(8ull * W * (G + 1));
+        const uint32_t gg = (uint32_t)std::min<uint64_t>(ceil_div(G, 256), 256ull * 32);
+        hipLaunchKernelGGL(k_md_route_count, dim3(gg), dim3(256), 0, st, M->d_comp.as<uint64_t>(), M->d_seg.as<uint64_t>(),
+                           G, idx_mask, M->d_band.as<uint32_t>(), (uint32_t)W, M->d_rtc.as<uint32_t>());
+        SKM_HIP(hipGetLastError());
+        for (int q = 0; q < W; ++q)
+            M->scan.run(M->d_rtc.as<uint32_t>() + (uint64_t)q * G, G, M->d_rto.as<uint64_t>() + (uint64_t)q * (G + 1), st);
+        for (int q = 0; q < W; ++q)
+            SKM_HIP(hipMemcpyAsync(&bc[q], M->d_rto.as<uint64_t>() + (uint64_t)q * (G + 1) + G, 8, hipMemcpyDeviceToHost, st));
+        SKM_HIP(hipStreamSynchronize(st));
+        for (int q = 1; q < W; ++q) bo[q] = bo[q - 1] + bc[q - 1];
+        const uint64_t tot = bo[W - 1] + bc[W - 1];
+        M->d_send.ensure(8 * std::max<uint64_t>(tot, 1));
+        M->d_sbase.ensure(8ull * W);
+        SKM_HIP(hipMemcpyAsync(M->d_sbase.p, bo.data(), 8ull * W, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_md_route_fill, dim3(gg), dim3(256), 0, st, M->d_comp.as<uint64_t>(), M->d_seg.as<uint64_t>(),
+                           G, idx_mask, idx_bits, M->d_band.as<uint32_t>(), (uint32_t)W, M->d_rtc.as<uint32_t>(),
+                           M->d_rto.as<uint64_t>(), M->d_sbase.as<uint64_t>(), gbase, M->d_send.as<uint64_t>());
+        SKM_HIP(hipGetLastError());
+        SKM_HIP(hipStreamSynchronize(st));
+    } else {
+        M->d_send.ensure(8);
+    }
+    const std::vector<uint64_t> rbc = mx_exchange_u64(M, bc);
+    std::vector<uint64_t> rbo(W, 0);
+    for (int q = 1; q < W; ++q) rbo[q] = rbo[q - 1] + rbc[q - 1];
+    const uint64_t n_band = rbo[W - 1] + rbc[W - 1];
+    M->d_comp2.ensure(8 * std::max<uint64_t>(n_band, 1));
+    mx_alltoallv(M, M->d_send.as<uint8_t>(), scaled(bo, 8), scaled(bc, 8), M->d_comp2.as<uint8_t>(), scaled(rbo, 8),
+                 scaled(rbc, 8));
+    SKM_HIP(hipStreamSynchronize(st));
+    std::swap(M->d_comp.p, M->d_comp2.p);
+    std::swap(M->d_comp.bytes, M->d_comp2.bytes);
+    M->n_routed = n_band;
+    M->band_lo = band[M->rank];
+    M->band_hi = band[M->rank + 1];
+    M->n_groups = G;
+    md_bounds(M, n_band, idx_bits, st);
+    return n_band;
+}
 
 void matrix_run(skm_matrix* M, const skm_matrix_opts* o) {
     skm_db* db = M->db;
     SKM_HIP(hipSetDevice(db->device));
     hipStream_t st = M->stream;
-    const uint32_t r0 = (o->row_begin == 0 && o->row_end == 0) ? 0u : o->row_begin;
-    const uint32_t r1 = (o->row_begin == 0 && o->row_end == 0) ? M->nidx : std::min(o->row_end, M->nidx);
+    const uint32_t r0_in = (o->row_begin == 0 && o->row_end == 0) ? 0u : o->row_begin;
+    const uint32_t r1_in = (o->row_begin == 0 && o->row_end == 0) ? M->nidx : std::min(o->row_end, M->nidx);
     SKM_HIP(hipEventRecord(M->ev[0], st));
     // 1. hits
     SKM_HIP(hipMemsetAsync(M->d_nrec.p, 0, 16, st));
@@ -548,52 +897,23 @@ void matrix_run(skm_matrix* M, const skm_matrix_opts* o) {
     SKM_HIP(hipMemcpyAsync(&n, M->d_nrec.p, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
     M->n_hits = n;
+    M->n_local_hits = n;
     M->n_incs = 0;
     M->n_pairs = 0;
     M->n_groups = 0;
     // 2. group: slot table + radix sort of (slot, index) composites + group boundaries
     const uint32_t idx_bits = (uint32_t)std::max(1, ilog2_ceil(std::max<uint64_t>(M->nidx, 2)));
-    const int lg = std::max(4, ilog2_ceil(2 * std::max<uint64_t>(n, 1)));
-    const uint32_t key_bits = (uint32_t)lg + idx_bits;
-    SKM_CHECK(key_bits <= 64, SKM_E_ARG, "matrix distance: too many hits / sequences for 64-bit composites");
-    if (n) {
-        const uint64_t T = 1ull << lg;
-        M->d_tab.ensure(8 * T);
-        SKM_HIP(hipMemsetAsync(M->d_tab.p, 0, 8 * T, st));
-        M->d_comp.ensure(8 * n);
-        M->d_comp2.ensure(8 * n);
-        const uint32_t g = (uint32_t)std::min<uint64_t>(ceil_div(n, 256), 256ull * 32);
-        hipLaunchKernelGGL(k_md_slot, dim3(g), dim3(256), 0, st, M->d_rkey.as<unsigned long long>(),
-                           M->d_ridx.as<uint32_t>(), M->d_nrec.as<unsigned long long>(),
-                           M->d_tab.as<unsigned long long>(), T - 1, 64u - (uint32_t)lg, idx_bits, M->d_comp.as<uint64_t>());
-        SKM_HIP(hipGetLastError());
-        const uint32_t nb = (uint32_t)ceil_div(n, RS_TILE);
-        M->d_hist.ensure(4ull * 256 * nb);
-        M->d_hoff.ensure(8ull * (256 * (uint64_t)nb + 1));
-        uint64_t* a = M->d_comp.as<uint64_t>();
-        uint64_t* b = M->d_comp2.as<uint64_t>();
-        for (uint32_t sh = 0; sh < key_bits; sh += 8) {
-            hipLaunchKernelGGL(k_rs_hist, dim3(nb), dim3(RS_THREADS), 0, st, a, n, (int)sh, nb, M->d_hist.as<uint32_t>());
-            M->scan.run(M->d_hist.as<uint32_t>(), 256ull * nb, M->d_hoff.as<uint64_t>(), st);
-            hipLaunchKernelGGL(k_rs_scatter, dim3(nb), dim3(RS_THREADS), 0, st, a, n, (int)sh, nb,
-                               M->d_hoff.as<uint64_t>(), b);
-            SKM_HIP(hipGetLastError());
-            std::swap(a, b);
-        }
-        if (a != M->d_comp.as<uint64_t>()) {
-            std::swap(M->d_comp.p, M->d_comp2.p);
-            std::swap(M->d_comp.bytes, M->d_comp2.bytes);
-        }
-        M->d_flag.ensure(4 * n);
-        M->d_S.ensure(8 * (n + 1));
-        hipLaunchKernelGGL(k_md_starts, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, st, M->d_comp.as<uint64_t>(), n,
-                           idx_bits, M->d_flag.as<uint32_t>());
-        M->scan.run(M->d_flag.as<uint32_t>(), n, M->d_S.as<uint64_t>(), st);
-        M->d_seg.ensure(8 * (n + 1));
-        hipLaunchKernelGGL(k_md_segstart, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, st, M->d_flag.as<uint32_t>(),
-                           M->d_S.as<uint64_t>(), n, M->d_seg.as<uint64_t>());
-        SKM_HIP(hipGetLastError());
-        SKM_HIP(hipMemcpyAsync(&M->n_groups, M->d_S.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+    const bool multi = M->world > 1;
+    uint32_t r0 = r0_in, r1 = r1_in;
+    if (multi) {  // owner-partitioned hits, band-routed groups: this rank's band of rows
+        n = md_exchange(M, n, idx_bits, st);
+        r0 = M->band_lo;
+        r1 = M->band_hi;
+    }
+    if (n && !multi) {
+        md_group(M, M->d_rkey.as<unsigned long long>(), M->d_ridx.as<uint32_t>(), M->d_nrec.as<unsigned long long>(), n,
+                 idx_bits, st);
+        M->n_groups = md_bounds(M, n, idx_bits, st);
     }
     SKM_HIP(hipEventRecord(M->ev[2], st));
     // 3. pair counts: row lists, one LDS histogram per row, compaction in row order
@@ -760,6 +1080,36 @@ int skm_matrix_create(skm_matrix** out, skm_db* db, const uint8_t* residues, con
     SKM_API_END
 }
 
+int skm_matrix_set_transport(skm_matrix* m, int rank, int world, const skm_transport* tp) {
+    SKM_API_BEGIN
+    SKM_CHECK(m && tp && tp->alltoallv, SKM_E_ARG, "incomplete transport");
+    SKM_CHECK(world >= 1 && world <= 64 && rank >= 0 && rank < world, SKM_E_ARG, "rank / world out of range");
+    m->rank = rank;
+    m->world = world;
+    m->tp = *tp;
+    SKM_API_END
+}
+
+int skm_matrix_set_comm(skm_matrix* m, int rank, int world, const uint8_t id[128]) {
+    SKM_API_BEGIN
+    SKM_CHECK(m && id, SKM_E_ARG, "null argument");
+    SKM_CHECK(world >= 1 && world <= 64 && rank >= 0 && rank < world, SKM_E_ARG, "rank / world out of range");
+#if defined(SKM_WITH_RCCL)
+    SKM_CHECK(m->comm == nullptr, SKM_E_STATE, "communicator already set");
+    SKM_HIP(hipSetDevice(m->db->device));
+    m->rank = rank;
+    m->world = world;
+    if (world > 1) {
+        ncclUniqueId u;
+        std::memcpy(&u, id, 128);
+        MX_NCCL(ncclCommInitRank(&m->comm, world, u, rank));
+    }
+#else
+    throw Error(SKM_E_COMM, "libskm was built without RCCL");
+#endif
+    SKM_API_END
+}
+
 int skm_matrix_run(skm_matrix* m, const skm_matrix_opts* opts) {
     SKM_API_BEGIN
     SKM_CHECK(m && opts, SKM_E_ARG, "null argument");
@@ -777,8 +1127,8 @@ int skm_matrix_last_timings(skm_matrix* m, float* ms, int cap) {
 
 int skm_matrix_counters(skm_matrix* m, uint64_t* out, int cap) {
     if (!m || !out) return SKM_E_ARG;
-    const uint64_t v[5] = {m->n_windows, m->n_hits, m->n_incs, m->n_pairs, m->n_groups};
-    const int n = std::min(cap, 5);
+    const uint64_t v[7] = {m->n_windows, m->n_hits, m->n_incs, m->n_pairs, m->n_groups, m->n_local_hits, m->n_routed};
+    const int n = std::min(cap, 7);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }
@@ -807,6 +1157,9 @@ void skm_matrix_destroy(skm_matrix* m) {
     if (!m) return;
     (void)hipSetDevice(m->db->device);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
+#if defined(SKM_WITH_RCCL)
+    if (m->comm) (void)ncclCommDestroy(m->comm);
+#endif
     for (auto& e : m->ev)
         if (e) (void)hipEventDestroy(e);
     if (m->stream) (void)hipStreamDestroy(m->stream);

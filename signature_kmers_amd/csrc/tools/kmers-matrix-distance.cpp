@@ -11,12 +11,15 @@
 // hash order of its concurrent maps).  --min-hits, --debug-hits, --verbose and -j are accepted
 // and, as in the reference main, have no effect on the output.
 // Extra options: --device N, --max-tile-bytes B (bound on the dense count tile in HBM).
-// Multi-GPU: --n-gpus N forks one process per GPU before any GPU use; rank r
-// computes the rows [r_begin, r_end) of the pair triangle (skm_matrix_tile_rows: bands of equal
-// triangle area) on device --device + r (all on --device with --same-device, as the tests do on
-// one GPU) and streams its band's lines to rank 0 over a socket; rank 0 prints the bands in rank
-// order, i.e. the same lines in the same (seq1, seq2) order as one GPU.  No collective: every
-// rank recomputes the hit lists, the pair increments are split.
+// Multi-GPU: --n-gpus N forks one process per GPU before any GPU use, on
+// device --device + r (all on --device with --same-device, as the tests do on one GPU).  Every rank
+// parses the input (the SeqIdMap indices are global) and looks up only its contiguous range of the
+// records; the (k-mer, index) hits go to the k-mer's owner GPU and each k-mer's index set to the
+// GPUs whose row band of the pair triangle (skm_matrix_tile_rows: bands of equal area) it has pairs
+// in -- two all-to-alls, over RCCL (--comm rccl, default) or the forked ranks' socketpairs
+// (--comm host) -- and rank r counts the pairs of its band.  Each rank streams its band's lines to
+// rank 0, which prints the bands in rank order: the same lines in the same (seq1, seq2) order as
+// one GPU.
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -59,7 +62,7 @@ int main(int argc, char** argv) {
                 {"min-hits", 0, false, false},    {"n-threads", 'j', false, false},  {"debug-hits", 0, true, false},
                 {"verbose", 0, true, false},      {"help", 'h', true, false},        {"device", 0, false, false},
                 {"max-tile-bytes", 0, false, false}, {"n-gpus", 0, false, false},
-                {"same-device", 0, true, false}};
+                {"same-device", 0, true, false},  {"comm", 0, false, false}};
     op.positional = {"data-dir", "input-file"};
     std::string err;
     if (!op.parse(argc, argv, err)) die(err);
@@ -74,7 +77,9 @@ int main(int argc, char** argv) {
                   << "  --verbose                   Verbose mode\n"
                   << "  --device arg                HIP device ordinal (default 0)\n"
                   << "  --max-tile-bytes arg        HBM bound of the dense pair-count tile (default: 60 % of free)\n"
-                  << "  --n-gpus arg                ranks (one process and GPU each), row bands of the triangle\n"
+                  << "  --n-gpus arg                ranks (one process and GPU each): query ranges, k-mer owners,\n"
+                  << "                              row bands of the triangle\n"
+                  << "  --comm arg                  rccl (default) or host (socketpairs; ranks may share a GPU)\n"
                   << "  --same-device               every rank on --device\n"
                   << "  -h [ --help ]               show this help message\n\n";
         return 0;
@@ -116,16 +121,31 @@ int main(int argc, char** argv) {
         }
     if (hypo < 0 && f.size() > 0) die("Cannot find hypothetical protein index");  // call_functions.tcc:269-274
 
+    // this rank's records: the r-th of ng contiguous ranges
+    const size_t ra = f.size() * (size_t)mesh.rank / (size_t)ng, rb = f.size() * (size_t)(mesh.rank + 1) / (size_t)ng;
+    const size_t nmine = rb - ra;
     skm_matrix* m = nullptr;
-    if (skm_matrix_create(&m, db, f.residues.data(), f.off.data(), f.len.data(), seq_idx.data(), f.size(),
+    if (skm_matrix_create(&m, db, f.residues.data(), nmine ? f.off.data() + ra : nullptr,
+                          nmine ? f.len.data() + ra : nullptr, nmine ? seq_idx.data() + ra : nullptr, nmine,
                           (uint32_t)index_to_id.size()))
         die(skm_last_error());
+    skm_transport tp = mesh.transport();
+    if (ng > 1) {
+        const std::string comm = op.get("comm", "rccl");
+        if (comm == "host") {
+            if (skm_matrix_set_transport(m, mesh.rank, ng, &tp)) die(skm_last_error());
+        } else if (comm == "rccl") {
+            uint8_t id[128];
+            if (mesh.rank == 0 && skm_comm_unique_id(id)) die(skm_last_error());
+            if (!mesh.share_id(id, err)) die(err);
+            if (skm_matrix_set_comm(m, mesh.rank, ng, id)) die(skm_last_error());
+        } else {
+            die("--comm must be rccl or host");
+        }
+    }
     skm_matrix_opts mo;
     std::memset(&mo, 0, sizeof(mo));
     mo.hypo_index = hypo;
-    if (ng > 1 && skm_matrix_tile_rows((uint32_t)index_to_id.size(), (uint32_t)mesh.rank, (uint32_t)ng, &mo.row_begin,
-                                       &mo.row_end))
-        die(skm_last_error());
     mo.max_tile_bytes = std::strtoull(op.get("max-tile-bytes", "0").c_str(), nullptr, 10);
     if (skm_matrix_run(m, &mo)) die(skm_last_error());
     uint64_t ctr[5] = {0, 0, 0, 0, 0};

@@ -4,7 +4,10 @@ torch.distributed.run.  Modes:
          host transport, checked against numpy on the gathered inputs of every rank;
   build  rank r builds the r-th contiguous file range on cuda:0 (every rank shares the one GPU),
          exchanging through the gloo host transport; rank 0's kept set and statistics must equal
-         the oracle on the union (one pass and two key-range passes).
+         the oracle on the union (one pass and two key-range passes);
+  matrix rank r looks up its range of the queries for kmers-matrix-distance, hits go to their
+         k-mer's owner and groups to the row bands they touch over the gloo transport; the bands
+         concatenated equal the oracle's pairs.
 Writes <out>/ok.<rank> on success."""
 import os
 import sys
@@ -72,13 +75,61 @@ def build(skm, dist, rank, world):
             assert got.distinct_signatures == len(ref["keys"]) if ref else True
 
 
+def matrix(skm, dist, rank, world):
+    """Multi-GPU kmers-matrix-distance over the gloo host transport: rank r looks up its contiguous
+    range of the queries, hits go to their k-mer's owner, groups to the row bands they touch; the
+    bands concatenated in rank order equal the oracle's pairs over all queries (SeqIdMap indices
+    global, some shared across the rank boundary)."""
+    import oracle_ref
+    from signature_kmers_amd import synth
+    p = synth.generate_arrays(3000, 30, per_file=500, seed=41)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    ref = oracle_ref.build(r, o, l, f, i, len(funcs))
+    out = sys.argv[2]
+    base = os.path.join(out, f"kmer_data.{rank}")
+    skm.mph_build(ref["keys"], ref["data"], base + ".mph", base + ".dat", seed=7)  # host builder: same bytes
+    q = synth.generate_arrays(40 * 500, 30, per_file=500, first_file=20, n_files=20, seed=41, extras=True)
+    n = len(q.seq_len)
+    idx = np.arange(n, dtype=np.uint32)
+    for s in range(7, n, 7):  # SeqIdMap: repeated ids share an index (across rank boundaries too)
+        idx[s] = idx[s - 3]
+    _, idx = np.unique(idx, return_inverse=True)  # first-appearance order == sorted order here
+    idx = idx.astype(np.uint32)
+    nidx = int(idx.max()) + 1
+    part = np.array_split(np.arange(n), world)[rank]
+    a, b = int(part[0]), int(part[-1]) + 1
+    db = skm.CmphKmerDb(base, device=0)
+    md = skm.MatrixDistance(db, funcs, q.residues, q.seq_off[a:b], q.seq_len[a:b], seq_idx=idx[a:b], n_idx=nidx)
+    md.set_transport(skm.GlooTransport())
+    got = md.compute()
+    c = md.counters()
+    lo, hi = skm.matrix_tile_rows(nidx, rank, world)
+    assert len(got) == 0 or (got[:, 0].min() >= lo and got[:, 0].max() < hi)
+    md.run()  # collective again on the same handle: the same band
+    assert np.array_equal(md.pairs(), got)
+    md.close()
+    db.close()
+    parts = [None] * world
+    dist.all_gather_object(parts, got)
+    ctrs = [None] * world
+    dist.all_gather_object(ctrs, c)
+    if rank == 0:
+        allp = np.concatenate(parts)
+        ob = oracle_ref.Bdz(open(base + ".mph", "rb").read())
+        exp = oracle_ref.matrix_distance(ob, open(base + ".dat", "rb").read(), q.residues, q.seq_off, q.seq_len, idx,
+                                         funcs.index("hypothetical protein"))
+        assert len(exp) > 10000
+        assert np.array_equal(allp, exp), (len(allp), len(exp))
+        assert sum(x["increments"] for x in ctrs) == int(exp[:, 2].astype(np.int64).sum())
+
+
 def main():
     mode, out = sys.argv[1], sys.argv[2]
     import torch.distributed as dist
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     import signature_kmers_amd as skm
-    {"plan": plan, "build": build}[mode](skm, dist, rank, world)
+    {"plan": plan, "build": build, "matrix": matrix}[mode](skm, dist, rank, world)
     dist.barrier()
     open(os.path.join(out, f"ok.{rank}"), "w").write("ok\n")
     dist.destroy_process_group()

@@ -107,6 +107,30 @@ def test_key_range_passes(skm, gpu, passes, long_class):
     assert c1["overflow_subbuckets"] > 0 and c1["grouped"] == oracle_ref.count_windows(l, f) - _invalid(r, o, l, f)
 
 
+@pytest.mark.parametrize("passes,route_min", [(4, 256), (16, 64), (64, 1024)])
+def test_heavy_key_routing(skm, gpu, passes, route_min):
+    """Heavy-key routing (route_heavy_min): the k-mers whose sampled occurrence estimate reaches the
+    threshold are grouped in the first half of the key-range passes, their elements carrying
+    (natural pass ^ routed pass) above the rem bits so the key decodes back -- the kept set is the
+    oracle's bit for bit, and many occurrences were actually routed."""
+    p = synth.generate_arrays(60000, 60, per_file=2000, seed=6)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    ref = oracle_ref.build(r, o, l, f, i, len(funcs))
+    b = skm.SignatureBuilder(len(funcs))
+    b.set_option("key_range_passes", passes)
+    b.set_option("route_heavy_min", route_min)
+    b.set_option("main_long_class", 8)
+    b.set_option("overflow_long_class", 8)
+    b.add_batch(r, o, l, f, i)
+    b.run()
+    c = b.counters()
+    got = b.finish()
+    b.close()
+    assert c["routed"] > 100_000, c
+    assert c["grouped"] == c["valid"]
+    assert_same(got, ref)
+
+
 @pytest.mark.parametrize("passes", [0, 4])
 def test_work_buffers_grow_and_redo(skm, gpu, passes):
     """The data-sized work buffers (overflow scratch, split path, stashed long chains) start far

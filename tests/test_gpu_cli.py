@@ -281,9 +281,10 @@ def test_call_functions_boost_math_legacy(c1_build, tmp_path):
 
 
 def test_matrix_distance_row_bands_multi_rank(c1_build, tmp_path):
-    """kmers-matrix-distance --n-gpus 2/3 (--same-device: every rank on the one GPU): rank r
-    computes its band of rows (skm_matrix_tile_rows) and rank 0 prints the bands in rank order --
-    byte-identical to the one-process output."""
+    """kmers-matrix-distance --n-gpus 2/3 --comm host (--same-device: every rank on the one GPU):
+    rank r looks up its range of the records, hits go to their k-mer's owner and k-mer groups to
+    the row bands (skm_matrix_tile_rows) over the ranks' socketpairs, rank r counts its band and
+    rank 0 prints the bands in rank order -- byte-identical to the one-process output."""
     info, out, _, _ = c1_build
     qdir = _query_dir(tmp_path / "q", seed=19)
     fa = str(tmp_path / "all.faa")
@@ -292,7 +293,8 @@ def test_matrix_distance_row_bands_multi_rank(c1_build, tmp_path):
     one, _ = _run([os.path.join(BIN, "kmers-matrix-distance"), out, fa])
     assert one.count("\n") > 1000
     for n in (2, 3):
-        many, err = _run([os.path.join(BIN, "kmers-matrix-distance"), out, fa, "--n-gpus", str(n), "--same-device"])
+        many, err = _run([os.path.join(BIN, "kmers-matrix-distance"), out, fa, "--n-gpus", str(n), "--same-device",
+                          "--comm", "host"])
         assert many == one, n
         assert err.count("kmer_hit_map size ") == 1
 

@@ -49,13 +49,15 @@ def _same(got, ref):
     assert got.distinct_signatures == ref["distinct_signatures"]
 
 
-@pytest.mark.parametrize("passes", [0, 4])
-def test_c2_build_bit_exact(skm, c2, passes):
-    """The whole C2 build vs the oracle, bit for bit (one pass, and four key-range passes)."""
+@pytest.mark.parametrize("passes,route_min", [(0, 0), (4, 0), (8, 2048)])
+def test_c2_build_bit_exact(skm, c2, passes, route_min):
+    """The whole C2 build vs the oracle, bit for bit (one pass; four key-range passes; eight with the
+    k-mers of >= 2048 occurrences routed into the first four)."""
     r, o, l, f, i = c2["inputs"]
     b = skm.SignatureBuilder(len(c2["funcs"]))
     if passes:
         b.set_option("key_range_passes", passes)
+        b.set_option("route_heavy_min", route_min)
     b.add_batch(r, o, l, f, i)
     b.run()
     c = b.counters()
@@ -65,7 +67,11 @@ def test_c2_build_bit_exact(skm, c2, passes):
     # the paths this size exists to reach
     assert c["overflow_subbuckets"] > 100 and c["overflow_elements"] > 10_000_000
     assert c["big_groups"] > 10_000
-    assert max(max(jobs), c["giant_max"]) >= 16384, (jobs, c)  # wave-pair chains (in situ or giant)
+    # wave-pair chains of >= 2^14 samples (in situ or giant with one pass; stashed with passes --
+    # with routing the last pass, whose jobs debug_jobs lists, holds no heavy k-mer)
+    assert max(max(jobs), c["giant_max"]) >= 16384 or c["long_samples"] >= 16384, (jobs, c)
+    if route_min:
+        assert c["routed"] > 1_000_000, c
     _same(got, c2["ref"])
     c2.setdefault("kept", got)
 

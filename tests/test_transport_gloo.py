@@ -37,3 +37,11 @@ def test_gloo_transport_and_exchange_plan(skm, tmp_path, world):
 @pytest.mark.gpu
 def test_gloo_two_process_build_matches_oracle(skm, gpu, tmp_path):
     run_ranks("build", 2, tmp_path, timeout=400)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_multi_process_matrix_matches_oracle(skm, gpu, tmp_path, world):
+    """kmers-matrix-distance over `world` processes on one GPU: owner-partitioned hits and
+    band-routed k-mer groups through the host transport, pairs bit-exact."""
+    run_ranks("matrix", world, tmp_path, timeout=400)
