@@ -36,23 +36,29 @@ const CharClass kCls;
 // FastaParser (fasta_parser.h:38-144).  The callback fires on '>' in s_id_or_data and once more
 // from parse_complete(); callers ignore records with an empty id, so only non-empty ids are kept.
 // ---------------------------------------------------------------------------------------------
-void parse_fasta_buffer(const char* buf, size_t n, FastaFile& out) {
+// Keep = false is the headers-only form (ids, definitions, offsets and lengths, no residue
+// bytes): what a rank needs of the files another rank builds.
+namespace {
+template <bool Keep>
+void parse_fasta_impl(const char* buf, size_t n, FastaFile& out) {
     enum State { S_START, S_ID, S_DEF, S_DATA, S_ID_OR_DATA } st = S_START;
     int line = 1;
     std::string id, def;
-    uint64_t seq_start = out.residues.size();
+    uint64_t nres = Keep ? out.residues.size() : out.n_residues;
+    uint64_t seq_start = nres;
     auto emit = [&]() {
         if (!id.empty()) {
             out.ids.push_back(id);
             out.defs.push_back(def);
             out.off.push_back(seq_start);
-            out.len.push_back((uint32_t)(out.residues.size() - seq_start));
+            out.len.push_back((uint32_t)(nres - seq_start));
         } else {
-            out.residues.resize(seq_start);
+            nres = seq_start;
+            if (Keep) out.residues.resize(seq_start);
         }
         id.clear();
         def.clear();
-        seq_start = out.residues.size();
+        seq_start = nres;
     };
     auto error = [&](const std::string& msg) {
         std::cerr << "Error found: " << msg << " at line " << line << " id='" << id << "'" << std::endl;
@@ -93,8 +99,11 @@ void parse_fasta_buffer(const char* buf, size_t n, FastaFile& out) {
                     // fast path: the rest of a residue run
                     const unsigned char* q = p;
                     while (q < end && (kCls.alpha[*q] || *q == '*')) ++q;
-                    out.residues.push_back(c);
-                    out.residues.insert(out.residues.end(), p, q);
+                    if (Keep) {
+                        out.residues.push_back(c);
+                        out.residues.insert(out.residues.end(), p, q);
+                    }
+                    nres += (uint64_t)(q - p) + 1;
                     p = q;
                 } else {
                     error(std::string("Bad data character '") + (char)c + "'");
@@ -106,7 +115,8 @@ void parse_fasta_buffer(const char* buf, size_t n, FastaFile& out) {
                     st = S_ID;
                 } else if (c == '\n') {
                 } else if (kCls.alpha[c]) {
-                    out.residues.push_back(c);
+                    if (Keep) out.residues.push_back(c);
+                    ++nres;
                     st = S_DATA;
                 } else {
                     error(std::string("Bad id or data character '") + (char)c + "'");
@@ -115,9 +125,18 @@ void parse_fasta_buffer(const char* buf, size_t n, FastaFile& out) {
         }
     }
     emit();  // parse_complete()
+    out.n_residues = nres;
+}
+}  // namespace
+
+void parse_fasta_buffer(const char* buf, size_t n, FastaFile& out, bool keep_residues) {
+    if (keep_residues)
+        parse_fasta_impl<true>(buf, n, out);
+    else
+        parse_fasta_impl<false>(buf, n, out);
 }
 
-bool parse_fasta_file(const std::string& path, FastaFile& out) {
+bool parse_fasta_file(const std::string& path, FastaFile& out, bool keep_residues) {
     out = FastaFile();
     out.path = path;
     out.filename = path_filename(path);
@@ -128,21 +147,21 @@ bool parse_fasta_file(const std::string& path, FastaFile& out) {
     f.seekg(0);
     std::string buf((size_t)std::max<std::streamoff>(n, 0), '\0');
     if (n > 0) f.read(&buf[0], n);
-    out.residues.reserve((size_t)n);
-    parse_fasta_buffer(buf.data(), buf.size(), out);
+    if (keep_residues) out.residues.reserve((size_t)n);
+    parse_fasta_buffer(buf.data(), buf.size(), out, keep_residues);
     out.residues.shrink_to_fit();
     return true;
 }
 
 bool parse_fasta_files(const std::vector<std::string>& paths, std::vector<FastaFile>& out, int n_threads,
-                       std::string& err) {
+                       std::string& err, const std::vector<char>* keep_residues) {
     out.assign(paths.size(), FastaFile());
     std::atomic<size_t> next{0};
     std::atomic<bool> ok{true};
     std::string bad;
     auto work = [&]() {
         for (size_t i; (i = next.fetch_add(1)) < paths.size();) {
-            if (!parse_fasta_file(paths[i], out[i])) {
+            if (!parse_fasta_file(paths[i], out[i], !keep_residues || (*keep_residues)[i])) {
                 ok = false;
                 bad = paths[i];
             }

@@ -28,18 +28,22 @@ struct FastaFile {
     std::vector<std::string> defs;  // definition line incl. its leading blank (fasta_parser.h:65-68)
     std::vector<uint64_t> off;      // into residues
     std::vector<uint32_t> len;
-    std::vector<uint8_t> residues;
+    std::vector<uint8_t> residues;  // empty when parsed headers-only
+    uint64_t n_residues = 0;        // residue count (also when headers-only)
     size_t size() const { return ids.size(); }
 };
 
 // FastaParser state machine over a whole file.  Parse errors are reported on stderr exactly as
 // the reference prints them and the offending character is dropped.  Returns false if the file
 // cannot be read.
-bool parse_fasta_file(const std::string& path, FastaFile& out);
-void parse_fasta_buffer(const char* buf, size_t n, FastaFile& out);
-// Parse several files on up to n_threads threads; result order = input order.
+// keep_residues = false: headers-only (ids, definitions, offsets and lengths as if the residues
+// were kept, no residue bytes; same parse errors).
+bool parse_fasta_file(const std::string& path, FastaFile& out, bool keep_residues = true);
+void parse_fasta_buffer(const char* buf, size_t n, FastaFile& out, bool keep_residues = true);
+// Parse several files on up to n_threads threads; result order = input order.  keep_residues
+// (optional, one flag per path) selects the headers-only form for the files whose flag is 0.
 bool parse_fasta_files(const std::vector<std::string>& paths, std::vector<FastaFile>& out, int n_threads,
-                       std::string& err);
+                       std::string& err, const std::vector<char>* keep_residues = nullptr);
 
 // path_utils.h: regular files of each directory in directory_iterator (readdir) order.
 bool list_regular_files(const std::string& dir, std::vector<std::string>& out, std::string& err);

@@ -16,8 +16,9 @@
 // any GPU or thread use; or, under an external launcher (RANK / WORLD_SIZE / LOCAL_RANK in the
 // environment, e.g. torchrun --no-python), each launched process is one rank and rank 0 hands the
 // RCCL unique id to the others through --comm-file (default <kmer-data-dir>/.skm_comm_id).
-// Every rank parses all inputs (the FunctionMap needs every file), builds the contiguous range of
-// files r*F/N .. (r+1)*F/N, the ranks exchange occurrences by owner GPU (RCCL all-to-all) and
+// Every rank parses every file's headers (the FunctionMap needs them all) but keeps residues only
+// for the files it builds (rank 0, which runs the recall pass, keeps all); rank r builds the
+// contiguous range of files r*F/N .. (r+1)*F/N, the ranks exchange occurrences by owner GPU (RCCL all-to-all) and
 // rank 0 gathers the kept k-mers and writes every output, exactly as one process would.
 // --comm host joins the forked ranks through socketpairs instead of RCCL (several ranks may then
 // share one GPU: --device is every rank's device; used by the tests).
@@ -217,8 +218,16 @@ int main(int argc, char** argv) {
     std::vector<std::string> all_paths = fasta_files;
     all_paths.insert(all_paths.end(), keep_files.begin(), keep_files.end());
     std::vector<FastaFile> files;
+    // this rank's contiguous range of files (global file numbering keeps seq_id = file*100000+k)
+    const size_t f0 = all_paths.size() * (size_t)rank / (size_t)world,
+                 f1 = all_paths.size() * (size_t)(rank + 1) / (size_t)world;
+    const bool dump = op.has("dump-extract");
+    // The FunctionMap needs every file's headers; residues are kept only for the files this rank
+    // builds -- and on rank 0, whose recall pass reads every sequence, for all of them.
+    std::vector<char> keep_res(all_paths.size(), 0);
+    for (size_t f = 0; f < all_paths.size(); ++f) keep_res[f] = rank == 0 || dump || (f >= f0 && f < f1);
     double t0 = now_s();
-    if (!parse_fasta_files(all_paths, files, n_threads, err)) die(err);
+    if (!parse_fasta_files(all_paths, files, n_threads, err, &keep_res)) die(err);
     try {
         for (auto& f : files) fm.load_fasta_file(f, deleted_fids);
     } catch (const std::exception& e) {
@@ -237,12 +246,9 @@ int main(int argc, char** argv) {
 
     std::cerr << "extract kmers\n";
     std::vector<BuildBatch> batches(files.size());
-    // this rank's contiguous range of files (global file numbering keeps seq_id = file*100000+k)
-    const size_t f0 = files.size() * (size_t)rank / (size_t)world, f1 = files.size() * (size_t)(rank + 1) / (size_t)world;
     // Sequence selection runs on a worker pool, file by file, while this thread streams every
     // finished file (in order) into the build: skm_build_add_batch packs it into a pinned staging
     // buffer whose DMA to HBM overlaps the next file's packing and the workers' selection.
-    const bool dump = op.has("dump-extract");
     const size_t s0 = dump ? 0 : f0, s1 = dump ? files.size() : f1;
     std::mutex sel_mu;
     std::condition_variable sel_cv;

@@ -3,6 +3,8 @@
 // hex-encoded results, tab separated:
 //   split_func_comment: func sep comment | is_truncated_comment(s) | strip_func_comment(s) |
 //   roles_of_function(s) joined by 0x01 | genome defline match (0/1) func genome | fig genome (0/1) genome
+// skm-front-probe --fasta FILE KEEP: parse FILE (KEEP 1 = with residues, 0 = headers-only) and print
+// one line per record (hex id, hex definition, offset, length), then "n_residues N residues R".
 #include <cstdio>
 #include <iostream>
 #include <string>
@@ -26,7 +28,15 @@ static std::string hex(const std::string& s) {
     return h.empty() ? "-" : h;
 }
 
-int main() {
+int main(int argc, char** argv) {
+    if (argc == 4 && std::string(argv[1]) == "--fasta") {
+        FastaFile f;
+        if (!parse_fasta_file(argv[2], f, std::string(argv[3]) == "1")) return 1;
+        for (size_t r = 0; r < f.size(); ++r)
+            std::cout << hex(f.ids[r]) << "\t" << hex(f.defs[r]) << "\t" << f.off[r] << "\t" << f.len[r] << "\n";
+        std::cout << "n_residues " << f.n_residues << " residues " << f.residues.size() << "\n";
+        return 0;
+    }
     std::string line;
     while (std::getline(std::cin, line)) {
         std::string s = line == "-" ? std::string() : unhex(line);

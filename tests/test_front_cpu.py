@@ -74,6 +74,23 @@ def test_fasta_parser_edge_cases():
     assert recs == [(b"id1", b" def one", b"ACGTMKmk*"), (b"id2", b"\tx", b"idQQ")]
 
 
+def test_fasta_headers_only_parse_matches_full(tools, tmp_path):
+    # the headers-only parse (other ranks' files in the multi-rank CLI) yields the same records,
+    # offsets and lengths as the full parse, and parses the same (bad) characters the same way
+    data = (b"junk\n>id1 def one\r\nACGT\n*MK\nmk1-*\n\n>\nAAAA\n>id2\tx\n>id3\nQQ\n"
+            + b"".join(b">s%d fn %d\n%s\n" % (i, i, b"ACDEFGHIKLMNPQRSTVWY"[: 1 + i % 20] * (1 + i % 7)) for i in range(300)))
+    f = tmp_path / "x.faa"
+    f.write_bytes(data)
+    probe = os.path.join(tools, "skm-front-probe")
+    full = subprocess.run([probe, "--fasta", str(f), "1"], capture_output=True, check=True)
+    light = subprocess.run([probe, "--fasta", str(f), "0"], capture_output=True, check=True)
+    fl, ll = full.stdout.decode().splitlines(), light.stdout.decode().splitlines()
+    assert fl[:-1] == ll[:-1] and len(fl) == 303
+    nf, nl = fl[-1].split(), ll[-1].split()
+    assert nf[1] == nl[1] == nf[3] and nl[3] == "0"
+    assert full.stderr == light.stderr and b"Bad data character" in full.stderr
+
+
 def _run_front(tools, d, out, extra=()):
     cmd = [os.path.join(tools, "kmers-build-signatures")] + front_data.front_args(d) + [
         "--kmer-data-dir", out, "--dump-extract", os.path.join(out, "extract.bin")] + list(extra)
