@@ -1,12 +1,15 @@
 // skm_mesh.cpp -- see skm_mesh.h.
 #include "skm_mesh.h"
 
+#include <signal.h>
+#include <sys/prctl.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -170,6 +173,9 @@ bool mesh_fork(int world, Mesh& m, std::string& err) {
         }
         if (pid == 0) {
             me = q;
+            // a child blocked in a collective must not outlive rank 0 (which exits on any failure)
+            prctl(PR_SET_PDEATHSIG, SIGTERM);
+            if (getppid() == 1) _exit(1);
             break;
         }
         m.children.push_back(pid);
@@ -228,7 +234,29 @@ bool Mesh::share_id(uint8_t id[128], std::string& err) {
     return true;
 }
 
+void Mesh::watch_children() {
+    if (rank != 0 || children.empty() || watching) return;
+    watching = std::make_shared<std::atomic<bool>>(true);
+    std::thread([kids = children, on = watching]() {
+        while (on->load()) {
+            for (size_t i = 0; i < kids.size(); ++i) {
+                siginfo_t si{};
+                // WNOWAIT: the child stays waitable for wait_children
+                if (waitid(P_PID, (id_t)kids[i], &si, WEXITED | WNOHANG | WNOWAIT) != 0 || si.si_pid == 0) continue;
+                if (si.si_code == CLD_EXITED && si.si_status == 0) continue;
+                if (!on->load()) return;
+                std::fprintf(stderr, "rank %zu failed; stopping the other ranks\n", i + 1);
+                for (pid_t k : kids) kill(k, SIGTERM);
+                std::fflush(nullptr);
+                _exit(1);
+            }
+            std::this_thread::sleep_for(std::chrono::milliseconds(100));
+        }
+    }).detach();
+}
+
 bool Mesh::wait_children(std::string& err) {
+    if (watching) watching->store(false);
     bool ok = true;
     for (size_t i = 0; i < children.size(); ++i) {
         int st = 0;

@@ -8,7 +8,9 @@
 
 #include <sys/types.h>
 
+#include <atomic>
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -27,6 +29,11 @@ struct Mesh {
     bool share_id(uint8_t id[128], std::string& err);
     // rank 0: wait for every child; false (with err) if any failed
     bool wait_children(std::string& err);
+    // rank 0: until wait_children, a thread polls the children; one that fails makes rank 0
+    // terminate the others and exit 1 (a rank blocked in an RCCL collective would wait forever).
+    // Children die with rank 0 (PR_SET_PDEATHSIG).
+    void watch_children();
+    std::shared_ptr<std::atomic<bool>> watching;
 };
 
 // fork world-1 children; returns false on failure (err set).  In each process m.rank is its rank.

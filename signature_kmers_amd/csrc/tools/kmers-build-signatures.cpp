@@ -156,6 +156,7 @@ int main(int argc, char** argv) {
         const int ng = std::atoi(op.get("n-gpus", "1").c_str());
         if (ng < 1 || ng > 64 || (ng & (ng - 1))) die("--n-gpus must be a power of two in [1, 64]");
         if (!mesh_fork(ng, mesh, err)) die(err);
+        mesh.watch_children();
         local_rank = mesh.rank;
     }
     const int rank = mesh.rank, world = mesh.world;
@@ -297,6 +298,9 @@ int main(int argc, char** argv) {
         }
         check(skm_build_reserve(b, nres, nseq), "skm_build_reserve");
     }
+    // test hook (tests/test_gpu_cli.py): this rank fails before joining the communicator
+    if (const char* fail = std::getenv("SKM_CLI_FAIL_RANK"))
+        if (world > 1 && std::atoi(fail) == rank) die("injected failure (SKM_CLI_FAIL_RANK)");
     skm_transport tp = mesh.transport();
     if (world > 1 && comm == "host") {
         check(skm_build_set_transport(b, &tp), "skm_build_set_transport");

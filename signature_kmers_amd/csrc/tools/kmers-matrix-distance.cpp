@@ -88,6 +88,7 @@ int main(int argc, char** argv) {
     if (ng < 1 || ng > 64) die("--n-gpus must be in [1, 64]");
     Mesh mesh;
     if (!mesh_fork(ng, mesh, err)) die(err);  // before any GPU call
+    mesh.watch_children();
     const int device = std::atoi(op.get("device", "0").c_str()) + (op.has("same-device") ? 0 : mesh.rank);
     const std::string data_dir = op.get("data-dir");
     const std::string db_base = path_join(data_dir, "kmer_data");

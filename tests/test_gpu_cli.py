@@ -319,3 +319,18 @@ def test_build_signatures_multi_rank_host_comm(tmp_path, gpu):
         assert sorted(_lines(os.path.join(o1, name)).split(b"\n")) == sorted(_lines(os.path.join(o2, name)).split(b"\n")), name
     for f in os.listdir(os.path.join(o1, "recall.report.d")):
         assert _lines(os.path.join(o1, "recall.report.d", f)) == _lines(os.path.join(o2, "recall.report.d", f)), f
+
+
+def test_build_signatures_rank_failure_stops_the_job(tmp_path, gpu):
+    """--n-gpus 2 --comm rccl with rank 1 failing before it joins the communicator: rank 0 would
+    block in the RCCL init forever; its child watcher terminates the job with exit status 1
+    (on a one-GPU box rank 1 also fails earlier, on device 1 -- the same path)."""
+    from signature_kmers_amd import synth
+    info = synth.write_dirs(str(tmp_path / "in"), 200, 10, per_file=100, extras=False)
+    env = dict(os.environ, SKM_CLI_FAIL_RANK="1")
+    p = subprocess.run([os.path.join(BIN, "kmers-build-signatures"), "-D", info["ann_dir"], "-F", info["seqs_dir"],
+                        "--kmer-data-dir", str(tmp_path / "o"), "--n-gpus", "2", "--comm", "rccl"],
+                       capture_output=True, timeout=120, env=env)
+    err = p.stderr.decode()
+    assert p.returncode == 1, err[-2000:]
+    assert "rank 1 failed" in err, err[-2000:]
