@@ -340,9 +340,9 @@ def _alg_bytes(kernel, c, res_bytes):
         "k_split_stage": 32 * valid,
         "k_extract_stage_pos": res_bytes + 16 * valid,     # residues once + the element written
         "k_extract_stage": res_bytes + 16 * valid,
-        "k_extract_pos": 16 * valid,                       # position + window
         "k_extract": res_bytes,
-        "k_pass_compact": res_bytes * max(1, c["passes"]) + 8 * valid,  # pass-id bytes + positions
+        # per pass: the pass-id bytes of every window + the pass's positions written
+        "k_pass_select": res_bytes * max(1, c["passes"]) + 8 * valid,
         "k_pass_ids": 2 * res_bytes,                       # residues read, one id byte written
         "k_overflow": 16 * c["overflow_elements"],
         "k_ovf_split": 32 * c["overflow_elements"],

@@ -197,7 +197,9 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   the stashed long-job list), "route_heavy_min" (one GPU, >= 4 key-range passes: k-mers with at
  *   least this many occurrences -- estimated at prepare from a count-min sketch of 1/64 of the
  *   windows -- are grouped in the first half of the passes, so their long P^2 chains run beside
- *   the later passes instead of after the last one; 65536; 0 = off).
+ *   the later passes instead of after the last one; 65536; 0 = off), "stage_round" (key-range
+ *   passes: 1 = the staged position scatter in half rounds of 2048 elements, four workgroups
+ *   per CU, the default; 0 = rounds of 4096).
  * Unknown names and out-of-range values return SKM_E_ARG. */
 int skm_build_set_option(skm_build* b, const char* name, int64_t value);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then

@@ -1484,6 +1484,23 @@ __device__ __forceinline__ uint64_t sampled_hash(const uint8_t* __restrict__ res
     return mix43(k);
 }
 
+// the 8 residue bytes at packed position p (the buffer is padded past its end)
+__device__ __forceinline__ uint64_t load_window(const uint8_t* __restrict__ res, uint64_t p) {
+    const uint64_t a = p & ~7ull;
+    const uint32_t sh = (uint32_t)(p & 7u) * 8u;
+    const uint64_t w0 = *reinterpret_cast<const uint64_t*>(res + a);
+    const uint64_t w1 = *reinterpret_cast<const uint64_t*>(res + a + 8);
+    return sh ? (w0 >> sh) | (w1 << (64u - sh)) : w0;
+}
+
+// mix43 of the base-40 key of a (valid) window
+__device__ __forceinline__ uint64_t window_hash(uint64_t raw) {
+    uint64_t k = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) k = k * 40u + residue_code((uint32_t)((raw >> (8 * j)) & 0xFFu));
+    return mix43(k);
+}
+
 // sketch (bloom == nullptr): count the sampled windows of every key into both rows;
 // bloom pass: keys whose estimate (the smaller row) reaches `thresh` set their two filter bits
 __global__ __launch_bounds__(256) void k_route_sketch(const uint8_t* __restrict__ res, uint64_t rp,
@@ -1511,14 +1528,20 @@ __global__ __launch_bounds__(256) void k_route_sketch(const uint8_t* __restrict_
 // owner_bits | owner),
 // ncnt = 2^(pass_bits + owner_bits) counters (<= 4096).  Dynamic LDS: ncnt counters, then the Bloom
 // filter when routing.
+// rows != nullptr (the run's ids, with pass_bits > 0): workgroup w takes the contiguous windows
+// [w * span, (w + 1) * span) (span a multiple of 16) and writes its windows per pass to
+// rows[w * ncnt + pass] -- k_sel_scan turns them into each workgroup's output offsets in every
+// pass's position list, so k_pass_select writes the positions in order without atomics.
 __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ res, uint64_t rp, int pass_bits,
                                                   int owner_bits, uint8_t* __restrict__ ids,
                                                   unsigned long long* __restrict__ counts,
-                                                  const uint32_t* __restrict__ bloom, uint32_t ncnt) {
+                                                  const uint32_t* __restrict__ bloom, uint32_t ncnt,
+                                                  uint32_t* __restrict__ rows = nullptr, uint64_t span = 0) {
     extern __shared__ uint32_t s_dyn[];
     uint32_t* s_cnt = s_dyn;
     uint32_t* s_bloom = s_dyn + ncnt;  // (1 << BLOOM_BITS) / 32 words when routing
-    if (counts)
+    const bool tally = counts != nullptr || rows != nullptr;
+    if (tally)
         for (uint32_t c = threadIdx.x; c < ncnt; c += blockDim.x) s_cnt[c] = 0;
     const bool route = bloom != nullptr && pass_bits >= 1;
     if (route)
@@ -1526,7 +1549,10 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
     __syncthreads();
     const uint32_t half = pass_bits >= 1 ? 1u << (pass_bits - 1) : 0u;
     const uint64_t nchunk = (rp + 15) >> 4;
-    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunk; c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t c0 = rows ? ((uint64_t)blockIdx.x * span >> 4) + threadIdx.x : (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t cend = rows ? min(nchunk, ((uint64_t)blockIdx.x + 1) * span >> 4) : nchunk;
+    const uint64_t cstep = rows ? (uint64_t)blockDim.x : (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t c = c0; c < cend; c += cstep) {
         const uint64_t base = c << 4;
         const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
         const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
@@ -1555,7 +1581,7 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
                 } else {
                     id = pass_bits ? (uint32_t)(h >> (KEY_BITS - pass_bits)) : 0u;
                     if (route && id >= half && bloom_has(s_bloom, h)) id -= half;
-                    if (counts) {
+                    if (tally) {
                         const uint32_t own = (uint32_t)(h >> (KEY_BITS - pass_bits - owner_bits)) & ((1u << owner_bits) - 1u);
                         atomicAdd(&s_cnt[(id << owner_bits) | own], 1u);
                     }
@@ -1570,6 +1596,81 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
         for (uint32_t c = threadIdx.x; c < ncnt; c += blockDim.x)
             if (s_cnt[c]) atomicAdd(&counts[c], (unsigned long long)s_cnt[c]);
     }
+    if (rows) {
+        __syncthreads();
+        for (uint32_t c = threadIdx.x; c < ncnt; c += blockDim.x) rows[(uint64_t)blockIdx.x * ncnt + c] = s_cnt[c];
+    }
+}
+
+// Every pass's position list: workgroup w of k_pass_ids / k_pass_select writes its windows of
+// pass p at off[p * (nwg + 1) + w] (exclusive scan over w), npos[p] = the pass's window count
+// (checked against the list's capacity: a larger pass fails the run, SKM_E_STATE).  One workgroup
+// per pass.
+constexpr uint32_t SEL_WG = 2048;
+__global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ rows, uint32_t nwg, uint32_t P,
+                                                   uint64_t* __restrict__ off, unsigned long long* __restrict__ npos,
+                                                   uint64_t cap, unsigned long long* __restrict__ run) {
+    __shared__ uint32_t s_wave[17];
+    const uint32_t p = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t per = (nwg + nt - 1) / nt, a = min(nwg, tid * per), e = min(nwg, a + per);
+    uint64_t loc = 0;
+    for (uint32_t w = a; w < e; ++w) loc += rows[(uint64_t)w * P + p];
+    uint32_t tot32;
+    // windows per pass fit 32 bits (prepare checks the largest pass against 2^32)
+    uint64_t r = wg_exclusive_scan((uint32_t)loc, s_wave, tot32);
+    for (uint32_t w = a; w < e; ++w) {
+        off[(uint64_t)p * (nwg + 1) + w] = r;
+        r += rows[(uint64_t)w * P + p];
+    }
+    if (tid == 0) {
+        off[(uint64_t)p * (nwg + 1) + nwg] = tot32;
+        npos[p] = tot32;
+        if (tot32 > cap) atomicOr(&run[RUN_FLAGS], (unsigned long long)RUN_F_CAP);
+    }
+}
+
+// One pass's window positions, in position order, and the level-1 bucket histogram over them
+// (replaces a compaction + a separate count kernel): workgroup w reads the id bytes of its
+// windows tile by tile (coalesced 16-byte loads, 4096 windows per tile), stages the tile's
+// matches in LDS, writes them contiguously at its precomputed offset, and hashes each matched
+// window into an LDS histogram, merged into the pass's global histogram once per workgroup.
+constexpr uint32_t SEL_THREADS = 256, SEL_TILE = SEL_THREADS * 16;
+__global__ __launch_bounds__(SEL_THREADS) void k_pass_select(const uint8_t* __restrict__ ids,
+                                                            const uint8_t* __restrict__ res, uint64_t rp,
+                                                            uint64_t span, uint32_t pass,
+                                                            const uint64_t* __restrict__ off, uint64_t cap,
+                                                            uint64_t* __restrict__ pos, int rem_bits, uint32_t NB,
+                                                            uint32_t* __restrict__ hist) {
+    __shared__ uint32_t s_pos[SEL_TILE];   // tile-relative positions of the tile's matches
+    __shared__ uint32_t s_wave[17];
+    extern __shared__ uint32_t s_h[];      // [NB]
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < NB; k += SEL_THREADS) s_h[k] = 0;
+    const uint64_t a = (uint64_t)blockIdx.x * span, e = min(rp, a + span);
+    uint64_t o = off[blockIdx.x];
+    __syncthreads();
+    for (uint64_t t0 = a; t0 < e; t0 += SEL_TILE) {
+        const uint64_t q = t0 + 16u * tid;
+        uint32_t m = 0;
+        if (q < e) {
+            m = match16(*reinterpret_cast<const uint4*>(ids + q), pass);
+            if (e - q < 16) m &= (1u << (uint32_t)(e - q)) - 1u;
+        }
+        uint32_t tot;
+        uint32_t x = wg_exclusive_scan((uint32_t)__popc(m), s_wave, tot);
+        for (uint32_t w = m; w; w &= w - 1) s_pos[x++] = 16u * tid + (uint32_t)__ffs(w) - 1u;
+        __syncthreads();
+        for (uint32_t j = tid; j < tot; j += SEL_THREADS) {
+            const uint64_t p = t0 + s_pos[j];
+            if (o + j < cap) pos[o + j] = p;
+            const uint64_t h = window_hash(load_window(res, p));
+            atomicAdd(&s_h[(uint32_t)(h >> rem_bits) & (NB - 1)], 1u);
+        }
+        o += tot;
+        __syncthreads();
+    }
+    for (uint32_t k = tid; k < NB; k += SEL_THREADS)
+        if (s_h[k]) atomicAdd(&hist[k], s_h[k]);
 }
 
 // Per-workgroup histogram of the level-1 buckets (count pass, one key-range pass = the whole
@@ -1619,83 +1720,6 @@ __global__ __launch_bounds__(EX_THREADS) void k_extract(ExtractArgs X) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Key-range pass extraction.  k_pass_compact turns the id bytes into the ascending packed
-// positions of this pass's windows (one workgroup per 32K windows, one cursor reservation per
-// workgroup: the ranges land in any order, which is immaterial, elements carry their ordinal);
-// the count and stage kernels then work on 1/P of the windows at the density of a one-pass build
-// instead of rescanning every residue.
-// ------------------------------------------------------------------------------------------
-constexpr int CP_THREADS = 256, CP_PER_THREAD = 128;  // 32768 windows per workgroup
-__global__ __launch_bounds__(CP_THREADS) void k_pass_compact(const uint8_t* __restrict__ ids, uint64_t rp, uint32_t pass,
-                                                             uint64_t* __restrict__ pos,
-                                                             unsigned long long* __restrict__ cursor, uint64_t cap,
-                                                             unsigned long long* __restrict__ run) {
-    __shared__ uint32_t s_wave[CP_THREADS / 64 + 1];
-    __shared__ unsigned long long s_base;
-    const uint64_t base = (uint64_t)blockIdx.x * CP_THREADS * CP_PER_THREAD + (uint64_t)threadIdx.x * CP_PER_THREAD;
-    uint32_t m[CP_PER_THREAD / 16];
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int k = 0; k < CP_PER_THREAD / 16; ++k) {
-        const uint64_t q = base + 16u * k;
-        m[k] = q < rp ? match16(*reinterpret_cast<const uint4*>(ids + q), pass) : 0u;
-        cnt += __popc(m[k]);
-    }
-    uint32_t tot;
-    uint32_t off = wg_exclusive_scan(cnt, s_wave, tot);
-    if (threadIdx.x == 0) {
-        s_base = tot ? atomicAdd(cursor, (unsigned long long)tot) : 0ull;
-        // the pass sizes were counted at prepare with the same hash, so the cursor stays below cap;
-        // if it ever does not, the run fails (SKM_E_STATE) instead of losing occurrences
-        if (s_base + tot > cap) atomicOr(&run[RUN_FLAGS], (unsigned long long)RUN_F_CAP);
-    }
-    __syncthreads();
-    uint64_t o = s_base + off;
-#pragma unroll
-    for (int k = 0; k < CP_PER_THREAD / 16; ++k)
-        for (uint32_t w = m[k]; w; w &= w - 1, ++o)
-            if (o < cap) pos[o] = base + 16u * k + (uint32_t)__ffs(w) - 1u;
-}
-
-// the 8 residue bytes at packed position p (the buffer is padded past its end)
-__device__ __forceinline__ uint64_t load_window(const uint8_t* __restrict__ res, uint64_t p) {
-    const uint64_t a = p & ~7ull;
-    const uint32_t sh = (uint32_t)(p & 7u) * 8u;
-    const uint64_t w0 = *reinterpret_cast<const uint64_t*>(res + a);
-    const uint64_t w1 = *reinterpret_cast<const uint64_t*>(res + a + 8);
-    return sh ? (w0 >> sh) | (w1 << (64u - sh)) : w0;
-}
-
-// mix43 of the base-40 key of a (valid) window
-__device__ __forceinline__ uint64_t window_hash(uint64_t raw) {
-    uint64_t k = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) k = k * 40u + residue_code((uint32_t)((raw >> (8 * j)) & 0xFFu));
-    return mix43(k);
-}
-
-// count pass over this pass's positions pos[0..n): per-workgroup level-1 bucket histogram
-__global__ __launch_bounds__(EX_THREADS) void k_extract_pos(ExtractArgs X, const uint64_t* __restrict__ pos,
-                                                             const unsigned long long* __restrict__ np) {
-    // this pass's window count (k_pass_compact's cursor; no host round trip), clamped to the list's
-    // capacity (a larger cursor already failed the run with RUN_F_CAP)
-    const uint64_t n = min((uint64_t)*np, X.pos_cap);
-    extern __shared__ uint32_t s_cnt[];  // [NB]
-    const int nbits = X.owner_bits + X.b1_bits;
-    const uint32_t NB = 1u << nbits;
-    const int rem_bits = KEY_BITS - X.pass_bits - nbits;
-    for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) s_cnt[b] = 0u;
-    __syncthreads();
-    const uint64_t begin = (uint64_t)blockIdx.x * X.span, end = min(begin + X.span, n);
-    for (uint64_t j = begin + threadIdx.x; j < end; j += blockDim.x) {
-        const uint64_t h = window_hash(load_window(X.res, pos[j]));
-        atomicAdd(&s_cnt[(uint32_t)(h >> rem_bits) & (NB - 1)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) X.hist[(uint64_t)blockIdx.x * NB + b] = s_cnt[b];
-}
-
-// ------------------------------------------------------------------------------------------
 // Two-pass LDS-staged scatter of the occurrence elements (replaces a direct 4096-way scatter,
 // whose 16-byte stores from every workgroup into every bucket left partial lines in L2:
 // ~4x write amplification measured).  Pass 1 partitions by the top 6 bucket bits (64-way) as
@@ -1711,18 +1735,29 @@ constexpr int SC_L0_BITS = 6;         // pass-1 fan-out
 constexpr int SC_POS = SC_ROUND / EX_THREADS;  // windows per thread per round (8)
 constexpr uint64_t SC_SLICE = 65536;  // pass-2 elements per workgroup
 
-struct StageLds {
-    uint64_t hi[SC_ROUND];
-    uint64_t lo[SC_ROUND];
-    uint8_t dst[SC_ROUND];
+// Staged-scatter cursors, one per 128-byte line: every workgroup of a launch reserves from the
+// same 64 level-0 cursors each round, and atomics on one line serialise.
+constexpr uint32_t CUR_STRIDE = 16;
+
+template <int R>
+struct StageLdsT {
+    uint64_t hi[R];
+    uint64_t lo[R];
+    uint8_t dst[R];
     uint32_t cnt[128];
     uint32_t off[129];
     unsigned long long base[128];
     uint32_t wave[48];
 };
+using StageLds = StageLdsT<SC_ROUND>;
+// k_extract_stage_pos's half round (option stage_round = 1, the default): 2048 elements, ~37 KB
+// of LDS, four workgroups per CU instead of two to hide the position -> sequence -> window gather
+// chain (C3 step 2046 -> 1950 ms, the kernel 435 -> 320 ms per step)
+constexpr int SC_ROUND_HALF = SC_ROUND / 2;
 
 // counts already in L.cnt[0..nd): exclusive offsets, then one global reservation per destination
-__device__ __forceinline__ uint32_t stage_reserve(StageLds& L, uint32_t nd, unsigned long long* __restrict__ cur,
+template <class Lds>
+__device__ __forceinline__ uint32_t stage_reserve(Lds& L, uint32_t nd, unsigned long long* __restrict__ cur,
                                                   uint32_t cur_base) {
     const uint32_t t = threadIdx.x;
     uint32_t tot;
@@ -1730,7 +1765,7 @@ __device__ __forceinline__ uint32_t stage_reserve(StageLds& L, uint32_t nd, unsi
     const uint32_t ex = wg_exclusive_scan(c, L.wave, tot);
     if (t < nd) {
         L.off[t] = ex;
-        L.base[t] = c ? atomicAdd(&cur[cur_base + t], (unsigned long long)c) : 0ull;
+        L.base[t] = c ? atomicAdd(&cur[(uint64_t)(cur_base + t) * CUR_STRIDE], (unsigned long long)c) : 0ull;
     }
     if (t == 0) L.off[nd] = tot;
     __syncthreads();
@@ -1829,13 +1864,15 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
 // The staged level-0 scatter over a key-range pass's positions pos[0..n) (same staging rounds
 // as k_extract_stage; each position finds its sequence through blk2seq, reusing the previous
 // one while it still contains the window).
-__global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage_pos(ExtractArgs X, const uint64_t* __restrict__ pos,
-                                                                     const unsigned long long* __restrict__ np,
-                                                                     unsigned long long* __restrict__ cur0,
-                                                                     uint64_t* __restrict__ out_hi,
-                                                                     uint64_t* __restrict__ out_lo) {
+template <int R, int MINB>
+__global__ __launch_bounds__(EX_THREADS, MINB) void k_extract_stage_pos(ExtractArgs X, const uint64_t* __restrict__ pos,
+                                                                        const unsigned long long* __restrict__ np,
+                                                                        unsigned long long* __restrict__ cur0,
+                                                                        uint64_t* __restrict__ out_hi,
+                                                                        uint64_t* __restrict__ out_lo) {
+    constexpr int SC_POS = R / EX_THREADS;
     const uint64_t n = min((uint64_t)*np, X.pos_cap);
-    __shared__ StageLds L;
+    __shared__ StageLdsT<R> L;
     const int nbits = X.owner_bits + X.b1_bits;
     const uint32_t NB = 1u << nbits;
     const int rem_bits = KEY_BITS - X.pass_bits - nbits;
@@ -1844,7 +1881,7 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage_pos(ExtractArgs
     const uint64_t begin = (uint64_t)blockIdx.x * X.span, end = min(begin + X.span, n);
     uint32_t s = 0xFFFFFFFFu;
     SeqMeta m{};
-    for (uint64_t base = begin; base < end; base += SC_ROUND) {
+    for (uint64_t base = begin; base < end; base += R) {
         if (threadIdx.x < 128) L.cnt[threadIdx.x] = 0;
         __syncthreads();
         uint64_t pp[SC_POS], raw[SC_POS];
@@ -1904,14 +1941,14 @@ __global__ void k_stage_init(const uint64_t* __restrict__ bstart, uint32_t NB, i
                              unsigned long long* __restrict__ cur0, unsigned long long* __restrict__ cur1,
                              uint32_t* __restrict__ slice_base) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < NB) cur1[t] = bstart[t];
+    if (t < NB) cur1[(uint64_t)t * CUR_STRIDE] = bstart[t];
     if (blockIdx.x == 0) {
         __shared__ uint32_t s_n[(1 << SC_L0_BITS) + 1];
         const uint32_t n0 = 1u << SC_L0_BITS;
         if (threadIdx.x < n0) {
             const uint64_t a = bstart[(uint64_t)threadIdx.x << l0_shift];
             const uint64_t e = bstart[(uint64_t)(threadIdx.x + 1) << l0_shift];
-            cur0[threadIdx.x] = a;
+            cur0[threadIdx.x * CUR_STRIDE] = a;
             s_n[threadIdx.x] = (uint32_t)((e - a + SC_SLICE - 1) / SC_SLICE);
         }
         __syncthreads();
@@ -2319,22 +2356,32 @@ __device__ __forceinline__ void seg_groups(const SubLds& L, uint32_t q0, uint32_
 // One sub-bucket of n <= CAP records: LDS hash grouping (ranks from the insert atomics give a
 // counting sort by group), singletons resolved immediately, multi-occurrence groups by threads
 // (small) or waves (large); no workgroup-wide sort.
-__device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi, const uint64_t* __restrict__ src_lo,
-                                            uint32_t n, const BucketArgs& A, uint64_t hprefix, const SubLds& L) {
-    const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    const uint32_t EMPTY = 0xFFFFFFFFu;
-    // 1. load the elements: every load of the batch in flight at once (a rolled loop waits for
-    //    each pair before its LDS store: CAP / BP_THREADS HBM round trips per batch)
-    constexpr uint32_t LPER = CAP / BP_THREADS;
-    uint64_t eh[LPER], el[LPER];
+constexpr uint32_t LPER = CAP / BP_THREADS;  // elements per thread of one batch
+
+// the batch's elements into registers, every load in flight at once (a rolled loop would wait for
+// each pair before its LDS store)
+__device__ __forceinline__ void load_batch(const uint64_t* __restrict__ src_hi, const uint64_t* __restrict__ src_lo,
+                                           uint32_t n, uint64_t (&eh)[LPER], uint64_t (&el)[LPER]) {
 #pragma unroll
     for (uint32_t u = 0; u < LPER; ++u) {
-        const uint32_t j = tid + u * BP_THREADS;
+        const uint32_t j = threadIdx.x + u * BP_THREADS;
         if (j < n) {
             eh[u] = __builtin_nontemporal_load(src_hi + j);
             el[u] = __builtin_nontemporal_load(src_lo + j);
         }
     }
+}
+
+// One batch of n <= CAP elements.  (Measured: issuing the next batch's loads here, to overlap their
+// latency with this batch's work, gained nothing -- the other workgroup of the CU already hides
+// it -- and cost register spills.)
+__device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi, const uint64_t* __restrict__ src_lo,
+                                            uint32_t n, const BucketArgs& A, uint64_t hprefix, const SubLds& L) {
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t EMPTY = 0xFFFFFFFFu;
+    // 1. the elements into LDS
+    uint64_t eh[LPER], el[LPER];
+    load_batch(src_hi, src_lo, n, eh, el);
     for (uint32_t t = tid; t < (uint32_t)TAB; t += nt) L.tab[t] = EMPTY;
 #pragma unroll
     for (uint32_t u = 0; u < LPER; ++u) {
@@ -2366,28 +2413,39 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     }
     __syncthreads();
     SKM_STAMP(3);
-    // 3. singletons resolved in place; multi-occurrence groups get a slice of `order`
+    // 3. singletons resolved in place; multi-occurrence groups get a slice of `order` (each thread
+    //    owns LPER consecutive elements: one workgroup scan for the whole batch)
     uint32_t M = 0, G = 0;
-    for (uint32_t c0 = 0; c0 < n; c0 += nt) {
-        const uint32_t j = c0 + tid;
-        const bool in = j < n;
-        const uint32_t e = in ? L.tab[L.slot[j]] : 0u;
-        const uint32_t cnt = e & 0xFFFFu;
-        const bool grp = in && cnt > 1 && (e >> 16) == j;
-        uint32_t tot;
-        const uint32_t v = wg_exclusive_scan(grp ? ((cnt << 13) | 1u) : 0u, L.wave, tot);
-        if (grp) {
-            L.goff[j] = (uint16_t)(M + (v >> 13));
-            L.glist[G + (v & 0x1FFFu)] = (uint16_t)j;
-        } else if (in && cnt == 1) {  // group of one: always kept (1 >= 0.8), median 0, var 0
-            const uint64_t H = L.hi[j], Lo = L.lo[j];
-            A.flags[Lo >> 36] = 1;
-            L.hi[j] = kept_hi(key_h43(hprefix, (H >> 16) & REM_MASK, A.rem_bits, A.pshift), (uint32_t)(Lo & 0xFFFFu));
-            L.lo[j] = kept_lo((uint32_t)(H & 0xFFFFu), d2u16((double)(uint16_t)(H >> 48) / 1.0), 0, 0);
-            L.rank[j] = 0xFFFFu;  // singleton marker
+    {
+        const uint32_t j0 = tid * LPER;
+        uint32_t ev[LPER], loc = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < LPER; ++u) {
+            const uint32_t j = j0 + u;
+            ev[u] = j < n ? L.tab[L.slot[j]] : 0u;
+            const uint32_t cnt = ev[u] & 0xFFFFu;
+            loc += (cnt > 1 && (ev[u] >> 16) == j) ? ((cnt << 13) | 1u) : 0u;
         }
-        M += tot >> 13;
-        G += tot & 0x1FFFu;
+        uint32_t tot;
+        uint32_t v = wg_exclusive_scan(loc, L.wave, tot);
+#pragma unroll
+        for (uint32_t u = 0; u < LPER; ++u) {
+            const uint32_t j = j0 + u;
+            const uint32_t cnt = ev[u] & 0xFFFFu;
+            if (j < n && cnt > 1 && (ev[u] >> 16) == j) {
+                L.goff[j] = (uint16_t)(v >> 13);
+                L.glist[v & 0x1FFFu] = (uint16_t)j;
+                v += (cnt << 13) | 1u;
+            } else if (j < n && cnt == 1) {  // group of one: always kept (1 >= 0.8), median 0, var 0
+                const uint64_t H = L.hi[j], Lo = L.lo[j];
+                A.flags[Lo >> 36] = 1;
+                L.hi[j] = kept_hi(key_h43(hprefix, (H >> 16) & REM_MASK, A.rem_bits, A.pshift), (uint32_t)(Lo & 0xFFFFu));
+                L.lo[j] = kept_lo((uint32_t)(H & 0xFFFFu), d2u16((double)(uint16_t)(H >> 48) / 1.0), 0, 0);
+                L.rank[j] = 0xFFFFu;  // singleton marker
+            }
+        }
+        M = tot >> 13;
+        G = tot & 0x1FFFu;
     }
     __syncthreads();
     SKM_STAMP(4);
@@ -2413,7 +2471,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     for (uint32_t g = tid; g < G; g += nt) {
         const uint32_t a = L.goff[L.glist[g]];
         const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
-        atomicAdd(&ccnt[cls_of(c)], 1u);
+        atomicAdd(&ccnt[cls_of(c)], 1u);  // (a per-wave ballot version measured slower)
     }
     __syncthreads();
     // ccnt[0..7]: cursors, [8..15]: class starts in big[], [16..23]: first wave task of each class
@@ -2496,8 +2554,9 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     }
     __syncthreads();
     SKM_STAMP(7);
-    // 6. emit kept k-mers and chain jobs: one scan and one reservation per sub-bucket; each
-    //    thread owns EMIT_PER consecutive elements so its outputs are consecutive
+    // 6. emit kept k-mers and chain jobs: one scan and one reservation per batch; the kept
+    //    elements are first compacted in LDS (slot[] = kept list, order[] = job list, rank[] =
+    //    a job's kept position) so consecutive lanes write consecutive records
     constexpr uint32_t EMIT_PER = CAP / BP_THREADS;
     unsigned long long* s_base = reinterpret_cast<unsigned long long*>(L.wave + 36);
     const uint32_t j0 = tid * EMIT_PER;
@@ -2514,29 +2573,47 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         s_base[0] = atomicAdd(A.kept_ctr, (unsigned long long)(tot & 0xFFFFu));
         if (tot >> 16) s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)(tot >> 16));
     }
-    __syncthreads();
-    if (tot & 0xFFFFu) {
-        uint64_t o = s_base[0] + (pos & 0xFFFFu);
-        uint64_t oj = s_base[1] + (pos >> 16);
+    {
+        uint32_t pk = pos & 0xFFFFu, pj = pos >> 16;
 #pragma unroll
         for (uint32_t u = 0; u < EMIT_PER; ++u) {
-            const uint32_t j = j0 + u;
-            const uint32_t jb = j < n ? jobinfo[j] : 0u;
+            const uint32_t jb = j0 + u < n ? jobinfo[j0 + u] : 0u;
             if (!(jb & JOB_KEPT)) continue;
-            const uint64_t H = L.hi[j];
-            const uint32_t jn = jb & JOB_COUNT_MASK;
-            if (jn) {
-                const uint32_t fm = fmean[j];
-                write_kept(A, o, H, kept_lo(fm & 0xFFFFu, fm >> 16, 0, 0));
-                Job jbr;
-                jbr.lens_off = L.lens_sel + 2 * (jb >> 16);
-                jbr.n = jn;
-                jbr.out_idx = (uint32_t)o;
-                A.jobs[oj++] = jbr;
-            } else {
-                write_kept(A, o, H, L.lo[j]);
+            L.slot[pk] = (uint16_t)(j0 + u);
+            if (jb & JOB_COUNT_MASK) {
+                L.order[pj++] = (uint16_t)(j0 + u);
+                L.rank[j0 + u] = (uint16_t)pk;
             }
-            ++o;
+            ++pk;
+        }
+    }
+    __syncthreads();
+    const uint32_t nkept = tot & 0xFFFFu, njob = tot >> 16;
+    if (nkept) {
+        const uint64_t ob = s_base[0];
+#pragma unroll 1
+        for (uint32_t t = tid; t < nkept; t += nt) {
+            const uint32_t j = L.slot[t];
+            const uint32_t jb = jobinfo[j];
+            uint64_t lo;
+            if (jb & JOB_COUNT_MASK) {
+                const uint32_t fm = fmean[j];
+                lo = kept_lo(fm & 0xFFFFu, fm >> 16, 0, 0);
+            } else {
+                lo = L.lo[j];
+            }
+            write_kept(A, ob + t, L.hi[j], lo);
+        }
+        const uint64_t jbase = njob ? s_base[1] : 0;
+#pragma unroll 1
+        for (uint32_t t = tid; t < njob; t += nt) {
+            const uint32_t j = L.order[t];
+            const uint32_t jb = jobinfo[j];
+            Job jbr;
+            jbr.lens_off = L.lens_sel + 2 * (jb >> 16);
+            jbr.n = jb & JOB_COUNT_MASK;
+            jbr.out_idx = (uint32_t)(ob + L.rank[j]);
+            A.jobs[jbase + t] = jbr;
         }
     }
     __syncthreads();
@@ -2600,17 +2677,18 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
         __syncthreads();
         SKM_STAMP(9);
     }
-    for (uint32_t d = 0; d < nsub;) {
-        const uint64_t* src_hi;
-        const uint64_t* src_lo;
-        uint32_t cnt;
+    // batches: the whole bucket (fits LDS), or runs of consecutive sub-buckets of <= CAP elements
+    // in total (sub-buckets beyond CAP are k_overflow's)
+    struct Batch {
+        uint32_t a, cnt;  // first element (bucket-relative), elements; cnt == 0: none left
+    };
+    auto next_batch = [&](uint32_t& d) -> Batch {
         if (direct) {
-            src_hi = A.recs_hi + r0;
-            src_lo = A.recs_lo + r0;
-            cnt = (uint32_t)n;
-            L.lens_sel = (LENS_IN_RECS << LENS_SEL_SHIFT) | (2 * r0);
+            if (d >= 1) return Batch{0, 0};
             d = 1;
-        } else {
+            return Batch{0, (uint32_t)n};
+        }
+        while (d < nsub) {
             const uint32_t a = s_sub[d];
             if (s_sub[d + 1] - a == 0 || s_sub[d + 1] - a > (uint32_t)CAP) {  // empty, or k_overflow's
                 ++d;
@@ -2618,14 +2696,19 @@ __global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) 
             }
             uint32_t d2 = d + 1;
             while (d2 < nsub && s_sub[d2 + 1] - a <= (uint32_t)CAP) ++d2;
-            cnt = s_sub[d2] - a;
-            src_hi = A.tmp_hi + r0 + a;
-            src_lo = A.tmp_lo + r0 + a;
-            L.lens_sel = (LENS_IN_TMP << LENS_SEL_SHIFT) | (2 * (r0 + a));
             d = d2;
+            return Batch{a, s_sub[d2] - a};
         }
-        L.lens32 = reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(src_hi));
-        process_sub(src_hi, src_lo, cnt, A, hprefix, L);
+        return Batch{0, 0};
+    };
+    const uint64_t* base_hi = direct ? A.recs_hi + r0 : A.tmp_hi + r0;
+    const uint64_t* base_lo = direct ? A.recs_lo + r0 : A.tmp_lo + r0;
+    const uint64_t sel = direct ? LENS_IN_RECS : LENS_IN_TMP;
+    uint32_t d = 0;
+    for (Batch cur = next_batch(d); cur.cnt; cur = next_batch(d)) {
+        L.lens_sel = (sel << LENS_SEL_SHIFT) | (2 * (r0 + cur.a));
+        L.lens32 = reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(base_hi + cur.a));
+        process_sub(base_hi + cur.a, base_lo + cur.a, cur.cnt, A, hprefix, L);
         __syncthreads();
         SKM_STAMP(10);
     }
@@ -4154,6 +4237,8 @@ struct Tune {
     int poison_jobs = 0;             // tests: every slot of the run's long-job list starts as a canary job
     int route_heavy_min = 1 << 16;   // key-range passes: k-mers of >= this many occurrences are routed into
                                      //   the first half of the passes (0: off; k_pass_ids)
+    int stage_round = 1;             // key-range passes: 1 = the staged position scatter in half rounds
+                                     //   (2048 elements, four workgroups per CU); 0 = full rounds
 };
 
 }  // namespace skm
@@ -4284,7 +4369,9 @@ struct skm_build {
     uint64_t routed = 0;                // occurrences routed into the first half of the passes
     // a pass's window positions, level-1 histogram matrix and window count, double-buffered: the
     // next pass's compaction + count run on stx during this pass's group-by (prefetch_pass)
-    DevBuf d_pos2[2], d_hist2[2], d_npos;
+    DevBuf d_pos2[2], d_hist2[2], d_npos;  // d_npos: every pass's window count (k_sel_scan)
+    DevBuf d_selrows, d_seloff;          // per-workgroup windows of each pass, their scanned offsets
+    uint64_t sel_span = 0;               // windows per k_pass_ids / k_pass_select workgroup
     hipStream_t stx = nullptr;
     hipEvent_t ev_pf_ready = nullptr, ev_pf_done[2] = {};
     int64_t pf_pass = -1;               // the pass whose compaction + count are already queued
@@ -4361,6 +4448,13 @@ void kt_end(skm_build* b, int e0, hipStream_t st) {
 #define SKM_LAUNCH(B, K, G, BL, LDS, ST, ...)                   \
     do {                                                        \
         const int _kt = kt_begin((B), #K, (ST));                \
+        hipLaunchKernelGGL(K, G, BL, LDS, ST, __VA_ARGS__);     \
+        kt_end((B), _kt, (ST));                                 \
+    } while (0)
+// the same, timed under an explicit name (template instantiations sharing one table row)
+#define SKM_LAUNCH_AS(B, NAME, K, G, BL, LDS, ST, ...)          \
+    do {                                                        \
+        const int _kt = kt_begin((B), NAME, (ST));              \
         hipLaunchKernelGGL(K, G, BL, LDS, ST, __VA_ARGS__);     \
         kt_end((B), _kt, (ST));                                 \
     } while (0)
@@ -4866,11 +4960,18 @@ void size_local(skm_build* b) {
         const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
         for (int k = 0; k < (b->pass_bits ? 2 : 1); ++k) {
             b->d_pos2[k].ensure(8 * W);
-            b->d_hist2[k].ensure(sizeof(uint32_t) * (uint64_t)EX_MAX_WG * NB);
+            b->d_hist2[k].ensure(sizeof(uint32_t) * (uint64_t)NB);
         }
-        b->d_npos.ensure(16);
+        const uint32_t P = 1u << b->pass_bits;
+        b->d_npos.ensure(8ull * P);
+        b->d_selrows.ensure(4ull * SEL_WG * P);
+        b->d_seloff.ensure(8ull * P * (SEL_WG + 1));
+        b->sel_span = ceil_div(ceil_div(std::max<uint64_t>(b->rp, 1), SEL_WG), 16) * 16;
         // count-kernel geometry from the largest pass (the kernels read the pass's own count)
-        uint32_t nwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(EX_MAX_WG, ceil_div(W, (uint64_t)SC_ROUND * 4)));
+        // (the pass's histogram comes from k_pass_select: this grid is the staged scatter's alone;
+        // the half-round variant runs four workgroups per CU)
+        const uint64_t stage_wg = b->tune.stage_round == 1 ? 4ull * EX_MAX_WG : EX_MAX_WG;
+        uint32_t nwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(stage_wg, ceil_div(W, (uint64_t)SC_ROUND * 4)));
         b->pf_span = ceil_div(ceil_div(W, nwg), (uint64_t)SC_ROUND) * SC_ROUND;
         b->pf_nwg = (uint32_t)std::max<uint64_t>(1, ceil_div(W, b->pf_span));
         // the histogram matrix of a pass may use every extract workgroup row
@@ -5009,23 +5110,11 @@ void prepare(const Ranks& bs) {
 void prefetch_pass(skm_build* b, uint32_t pass, hipStream_t st) {
     const int k = pass & 1;
     const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
-    unsigned long long* np = b->d_npos.as<unsigned long long>() + k;
-    SKM_HIP(hipMemsetAsync(np, 0, 8, st));
-    SKM_LAUNCH(b, k_pass_compact, dim3((uint32_t)ceil_div(b->rp, (uint64_t)CP_THREADS * CP_PER_THREAD)),
-                       dim3(CP_THREADS), 0, st, b->d_ids.as<uint8_t>(), b->rp, pass, b->d_pos2[k].as<uint64_t>(), np,
-                       b->pass_max, b->d_run.as<unsigned long long>());
-    ExtractArgs X{};
-    X.res = b->d_res.as<uint8_t>();
-    X.rp = b->rp;
-    X.span = b->pf_span;
-    X.owner_bits = b->owner_bits;
-    X.b1_bits = b->b1_bits;
-    X.pass_bits = b->pass_bits;
-    X.pass_id = pass;
-    X.pos_cap = b->pass_max;
-    X.hist = b->d_hist2[k].as<uint32_t>();
-    SKM_LAUNCH(b, k_extract_pos, dim3(b->pf_nwg), dim3(EX_THREADS), sizeof(uint32_t) * NB, st, X,
-                       b->d_pos2[k].as<uint64_t>(), np);
+    SKM_HIP(hipMemsetAsync(b->d_hist2[k].p, 0, sizeof(uint32_t) * NB, st));
+    const int rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
+    SKM_LAUNCH(b, k_pass_select, dim3(SEL_WG), dim3(SEL_THREADS), sizeof(uint32_t) * NB, st, b->d_ids.as<uint8_t>(),
+               b->d_res.as<uint8_t>(), b->rp, b->sel_span, pass, b->d_seloff.as<uint64_t>() + (uint64_t)pass * (SEL_WG + 1),
+               b->pass_max, b->d_pos2[k].as<uint64_t>(), rem_bits, NB, b->d_hist2[k].as<uint32_t>());
     SKM_HIP(hipGetLastError());
     if (st != b->stream) SKM_HIP(hipEventRecord(b->ev_pf_done[k], st));
     b->pf_pass = pass;
@@ -5057,7 +5146,7 @@ void phase_extract(skm_build* b, uint32_t pass) {
     X.s_base = b->s_base;
     X.out_hi = b->d_recs_hi.as<uint64_t>();
     X.out_lo = b->d_recs_lo.as<uint64_t>();
-    uint32_t nwg = b->nwg;
+    uint32_t nwg = b->nwg, hist_rows = b->nwg;
     if (b->pass_bits) {
         // this pass's window positions and count: queued on stx during the previous pass's
         // group-by (prefetch_pass), or now for the run's first pass
@@ -5067,9 +5156,10 @@ void phase_extract(skm_build* b, uint32_t pass) {
         else
             prefetch_pass(b, pass, st);
         b->pf_pass = -1;
-        X.hist = b->d_hist2[k].as<uint32_t>();
+        X.hist = b->d_hist2[k].as<uint32_t>();  // one row: k_pass_select's histogram of the pass
         X.span = b->pf_span;
         nwg = b->pf_nwg;
+        hist_rows = 1;
         (void)lds_cnt;
     } else {
         SKM_LAUNCH(b, k_extract, dim3(nwg), dim3(EX_THREADS), lds_cnt, st, X);
@@ -5077,12 +5167,12 @@ void phase_extract(skm_build* b, uint32_t pass) {
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[1], st));
     // ---- 2. scan ----
-    const uint32_t nrb = (uint32_t)ceil_div(nwg, SCAN_ROWS);
+    const uint32_t nrb = (uint32_t)ceil_div(hist_rows, SCAN_ROWS);
     dim3 gsc((NB + 255) / 256, nrb);
-    SKM_LAUNCH(b, k_colsum, gsc, dim3(256), 0, st, X.hist, nwg, NB, b->d_partial.as<uint32_t>());
+    SKM_LAUNCH(b, k_colsum, gsc, dim3(256), 0, st, X.hist, hist_rows, NB, b->d_partial.as<uint32_t>());
     SKM_LAUNCH(b, k_bstart, dim3(1), dim3(1024), 0, st, b->d_partial.as<uint32_t>(), nrb, NB, b->b1_bits,
                        b->d_rbbase.as<uint32_t>(), b->d_bstart32.as<uint32_t>(), b->d_owner_start.as<uint64_t>(), nowners);
-    SKM_LAUNCH(b, k_coloffs, gsc, dim3(256), 0, st, X.hist, b->d_rbbase.as<uint32_t>(), nwg,
+    SKM_LAUNCH(b, k_coloffs, gsc, dim3(256), 0, st, X.hist, b->d_rbbase.as<uint32_t>(), hist_rows,
                        NB, b->d_offs.as<uint32_t>());
     SKM_LAUNCH(b, k_abs_starts, dim3((NB + 1 + 255) / 256), dim3(256), 0, st, b->d_bstart32.as<uint32_t>(),
                        b->d_owner_start.as<uint64_t>(), NB, b->b1_bits, nowners, b->d_bstart.as<uint64_t>());
@@ -5090,15 +5180,19 @@ void phase_extract(skm_build* b, uint32_t pass) {
     SKM_HIP(hipEventRecord(b->ev[2], st));
     // ---- 3. scatter: 64-way staged pass into tmp, then the split into the final buckets ----
     const int l0_shift = nbits - SC_L0_BITS;
-    b->d_cur0.ensure(8 * 64);
-    b->d_cur1.ensure(8ull * NB);
+    b->d_cur0.ensure(8ull * 64 * CUR_STRIDE);
+    b->d_cur1.ensure(8ull * NB * CUR_STRIDE);
     b->d_slices.ensure(4 * 80);
     SKM_LAUNCH(b, k_stage_init, dim3((NB + 255) / 256), dim3(256), 0, st, b->d_bstart.as<uint64_t>(), NB, l0_shift,
                        b->d_cur0.as<unsigned long long>(), b->d_cur1.as<unsigned long long>(), b->d_slices.as<uint32_t>());
-    if (b->pass_bits)
-        SKM_LAUNCH(b, k_extract_stage_pos, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_pos2[pass & 1].as<uint64_t>(),
-                           b->d_npos.as<unsigned long long>() + (pass & 1), b->d_cur0.as<unsigned long long>(),
-                           b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
+    if (b->pass_bits && b->tune.stage_round == 1)
+        SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND_HALF, 4>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
+                   b->d_pos2[pass & 1].as<uint64_t>(), b->d_npos.as<unsigned long long>() + pass,
+                   b->d_cur0.as<unsigned long long>(), b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
+    else if (b->pass_bits)
+        SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND, 2>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
+                   b->d_pos2[pass & 1].as<uint64_t>(), b->d_npos.as<unsigned long long>() + pass,
+                   b->d_cur0.as<unsigned long long>(), b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
     else
         SKM_LAUNCH(b, k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
                            b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
@@ -5564,10 +5658,15 @@ void begin_run(skm_build* b) {
         hipLaunchKernelGGL(k_poison_jobs, dim3(256), dim3(256), 0, st, b->d_long_jobs.as<Job>(), b->long_jobs_cap,
                            reinterpret_cast<uint64_t>(b->d_long_arena.p), (uint32_t)b->kept_cap,
                            b->d_data.as<skm_stored_kmer_data>());
-    if (b->pass_bits && b->rp)
-        SKM_LAUNCH(b, k_pass_ids, dim3(4096), dim3(256), b->route ? (1u << BLOOM_BITS) / 8 : 0u, st,
+    if (b->pass_bits) {
+        const uint32_t P = 1u << b->pass_bits;
+        SKM_LAUNCH(b, k_pass_ids, dim3(SEL_WG), dim3(256), 4u * P + (b->route ? (1u << BLOOM_BITS) / 8 : 0u), st,
                    b->d_res.as<uint8_t>(), b->rp, b->pass_bits, 0, b->d_ids.as<uint8_t>(), nullptr,
-                   b->route ? b->d_bloom.as<uint32_t>() : nullptr, 0u);
+                   b->route ? b->d_bloom.as<uint32_t>() : nullptr, P, b->d_selrows.as<uint32_t>(), b->sel_span);
+        SKM_LAUNCH(b, k_sel_scan, dim3(P), dim3(1024), 0, st, b->d_selrows.as<uint32_t>(), SEL_WG, P,
+                   b->d_seloff.as<uint64_t>(), b->d_npos.as<unsigned long long>(), b->pass_max,
+                   b->d_run.as<unsigned long long>());
+    }
     SKM_HIP(hipGetLastError());
     b->acc = skm_build::Acc{};
     b->kt_used = 0;
@@ -6101,7 +6200,8 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "chain_batches" ? &t.chain_batches
                : n == "chain_streams" ? &t.chain_streams
                : n == "poison_jobs" ? &t.poison_jobs
-               : n == "route_heavy_min" ? &t.route_heavy_min : nullptr;
+               : n == "route_heavy_min" ? &t.route_heavy_min
+               : n == "stage_round" ? &t.stage_round : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")

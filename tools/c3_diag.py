@@ -23,6 +23,7 @@ ap.add_argument("--option", action="append", default=[])
 ap.add_argument("--chain-bench", action="store_true")
 ap.add_argument("--files", type=int, default=0, help="only the first N genome files (250 = the C2 workload)")
 ap.add_argument("--runs", type=int, default=0, help="builds to run (default: steps + 1, or 6 with --files)")
+ap.add_argument("--stamps", action="store_true", help="one more run with k_bucket_process phase stamps")
 a = ap.parse_args()
 
 
@@ -52,6 +53,18 @@ for s in range(a.runs or (a.steps + (1 if a.files == 0 else 5))):
     t = time.time()
     b.run()
     log(f"run {s}: {1000 * (time.time() - t):.0f} ms wall; " + json.dumps({k: round(v, 1) for k, v in b.timings().items()}))
+if a.stamps:
+    b.debug_stamps(True)
+    b.run()
+    st = b.debug_stamps(False)
+    tot = sum(st[:16])
+    names = {0: "l2_count", 1: "l2_scatter", 9: "l2_setup", 2: "sub_load", 3: "sub_hash", 4: "sub_classify",
+             5: "sub_scatter", 6: "sub_class_sort", 11: "sub_seg_groups", 7: "sub_big_groups", 8: "sub_emit",
+             10: "sub_loop_tail"}
+    log("stamps (cycles summed over workgroups):")
+    for k in sorted(names):
+        log(f"  {names[k]:>20s} {st[k]:>16d} {100.0 * st[k] / max(tot, 1):6.1f}%")
+    log("timings(stamped) " + json.dumps({k: round(v, 1) for k, v in b.timings().items()}))
 c = b.counters()
 log("counters " + json.dumps(c))
 ov = b.debug_overflow(1 << 16)

@@ -13,6 +13,8 @@ for set in "$@"; do
   timeout -k 10 300 python3 bench.py --cache-dir /tmp/c3 --steps 5 --warmup 1 --weak-seqs 0 --annot-queries 0 \
     --matrix-seqs 0 --no-cpu-baseline $args --json-out $O/c3_opts_$i.json > $O/c3_opts_$i.log 2>&1 \
     || { tail -5 $O/c3_opts_$i.log; exit 1; }
-  python3 -c "import json,sys; d=json.load(open('$O/c3_opts_$i.json')); print(sys.argv[1] or 'defaults', round(d['ms_per_step'],1))" "$set"
+  python3 -c "
+import json,sys; d=json.load(open('$O/c3_opts_$i.json')); r=d['roofline']; k=r.get('kernels_ms_per_step') or {}
+print(sys.argv[1] or 'defaults', round(d['ms_per_step'],1), 'tail', d.get('chain_tail_ms'), {n: round(v) for n, v in sorted(k.items(), key=lambda x: -x[1])[:8]})" "$set"
   i=$((i+1))
 done
