@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round-3 profile set (run via gpurun from the repo root; inputs cached under /tmp/c3):
+#   c3_stamps.log  k_bucket_process phase stamps of one C3 build (tools/c3_diag.py --stamps)
 #   prof_c3/  rocprofv3 kernel trace + stats, C3 headline build (bench.py, 1 warmup + 2 steps)
 #   prof_c2/  the same for the C2 workload (first 250 files; tools/c3_diag.py, 3 runs)
 #   prof_legs/  annotate (10M queries) + matrix (100K) legs (bench.py on the C2 proteome)
@@ -28,6 +29,7 @@ C3="python3 $R/bench.py --cache-dir /tmp/c3 --weak-seqs 0 --annot-queries 0 --ma
 C2="python3 $R/tools/c3_diag.py --cache-dir /tmp/c3 --files 250"
 LEGS="python3 $R/bench.py --seqs-total 1000000 --no-cpu-baseline"
 if [ "${PHASE:-all}" != pmc ]; then
+  step c3_stamps 300 python3 $R/tools/c3_diag.py --cache-dir /tmp/c3 --runs 1 --stamps
   step prof_c3 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_c3" -o run -- $C3 --steps 2 --warmup 1 --json-out "$O/bench_c3_trace.json"
   step prof_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_c2" -o run -- $C2 --runs 3
   step prof_legs 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_legs" -o run -- $LEGS --steps 3 --warmup 1 --json-out "$O/bench_legs_trace.json"

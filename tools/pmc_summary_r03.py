@@ -29,8 +29,9 @@ def per_kernel(path, counter):
         if row["Counter_Name"] != counter:
             continue
         name = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("skm::", "")
-        if name.startswith("k_extract_stage_pos<"):  # the round-size variants share one row (bench.py)
-            name = "k_extract_stage_pos"
+        for base in ("k_extract_stage_pos", "k_pass_select"):  # variants share one row (bench.py)
+            if name.startswith(base + "<"):
+                name = base
         acc[name].append(float(row["Counter_Value"]))
     return acc
 
