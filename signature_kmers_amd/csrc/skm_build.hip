@@ -1631,34 +1631,55 @@ __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ 
 
 // One pass's window positions, in position order, and the level-1 bucket histogram over them
 // (replaces a compaction + a separate count kernel): workgroup w reads the id bytes of its
-// windows tile by tile (coalesced 16-byte loads, 4096 windows per tile), stages the tile's
-// matches in LDS, writes them contiguously at its precomputed offset, and hashes each matched
-// window into an LDS histogram, merged into the pass's global histogram once per workgroup.
-constexpr uint32_t SEL_THREADS = 256, SEL_TILE = SEL_THREADS * 16;
+// windows tile by tile (each thread U consecutive 16-byte loads, the next tile's issued before
+// this tile's matches are processed), stages the tile's matches in LDS, writes them contiguously
+// at its precomputed offset, and hashes each matched window into an LDS histogram, merged into
+// the pass's global histogram once per workgroup.
+constexpr uint32_t SEL_THREADS = 256;
+template <uint32_t U>
 __global__ __launch_bounds__(SEL_THREADS) void k_pass_select(const uint8_t* __restrict__ ids,
                                                             const uint8_t* __restrict__ res, uint64_t rp,
                                                             uint64_t span, uint32_t pass,
                                                             const uint64_t* __restrict__ off, uint64_t cap,
                                                             uint64_t* __restrict__ pos, int rem_bits, uint32_t NB,
                                                             uint32_t* __restrict__ hist) {
-    __shared__ uint32_t s_pos[SEL_TILE];   // tile-relative positions of the tile's matches
+    constexpr uint32_t TILE = SEL_THREADS * 16 * U;
+    static_assert(TILE <= 65536, "tile-relative positions are u16");
+    __shared__ uint16_t s_pos[TILE];       // tile-relative positions of the tile's matches
     __shared__ uint32_t s_wave[17];
     extern __shared__ uint32_t s_h[];      // [NB]
     const uint32_t tid = threadIdx.x;
     for (uint32_t k = tid; k < NB; k += SEL_THREADS) s_h[k] = 0;
     const uint64_t a = (uint64_t)blockIdx.x * span, e = min(rp, a + span);
     uint64_t o = off[blockIdx.x];
-    __syncthreads();
-    for (uint64_t t0 = a; t0 < e; t0 += SEL_TILE) {
-        const uint64_t q = t0 + 16u * tid;
-        uint32_t m = 0;
-        if (q < e) {
-            m = match16(*reinterpret_cast<const uint4*>(ids + q), pass);
-            if (e - q < 16) m &= (1u << (uint32_t)(e - q)) - 1u;
+    uint4 nxt[U];
+    auto fetch = [&](uint64_t t0) {
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint64_t q = t0 + 16u * (U * tid + u);
+            nxt[u] = q < e ? *reinterpret_cast<const uint4*>(ids + q) : make_uint4(0u, 0u, 0u, 0u);
         }
+    };
+    if (a < e) fetch(a);
+    __syncthreads();
+    for (uint64_t t0 = a; t0 < e; t0 += TILE) {
+        uint32_t m[U], c = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint64_t q = t0 + 16u * (U * tid + u);
+            m[u] = 0;
+            if (q < e) {
+                m[u] = match16(nxt[u], pass);
+                if (e - q < 16) m[u] &= (1u << (uint32_t)(e - q)) - 1u;
+            }
+            c += (uint32_t)__popc(m[u]);
+        }
+        if (t0 + TILE < e) fetch(t0 + TILE);
         uint32_t tot;
-        uint32_t x = wg_exclusive_scan((uint32_t)__popc(m), s_wave, tot);
-        for (uint32_t w = m; w; w &= w - 1) s_pos[x++] = 16u * tid + (uint32_t)__ffs(w) - 1u;
+        uint32_t x = wg_exclusive_scan(c, s_wave, tot);
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u)
+            for (uint32_t w = m[u]; w; w &= w - 1) s_pos[x++] = (uint16_t)(16u * (U * tid + u) + (uint32_t)__ffs(w) - 1u);
         __syncthreads();
         for (uint32_t j = tid; j < tot; j += SEL_THREADS) {
             const uint64_t p = t0 + s_pos[j];
@@ -2569,10 +2590,10 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     }
     uint32_t tot;
     const uint32_t pos = wg_exclusive_scan(cnt, L.wave, tot);
-    if (tid == 0 && (tot & 0xFFFFu)) {
-        s_base[0] = atomicAdd(A.kept_ctr, (unsigned long long)(tot & 0xFFFFu));
-        if (tot >> 16) s_base[1] = atomicAdd(&A.ctr[3], (unsigned long long)(tot >> 16));
-    }
+    // the two reservations from two waves at once, their latency behind the LDS compaction
+    unsigned long long rsv = 0;
+    if (tid == 0 && (tot & 0xFFFFu)) rsv = atomicAdd(A.kept_ctr, (unsigned long long)(tot & 0xFFFFu));
+    if (tid == 64 && (tot >> 16)) rsv = atomicAdd(&A.ctr[3], (unsigned long long)(tot >> 16));
     {
         uint32_t pk = pos & 0xFFFFu, pj = pos >> 16;
 #pragma unroll
@@ -2587,6 +2608,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
             ++pk;
         }
     }
+    if (tid == 0 || tid == 64) s_base[tid >> 6] = rsv;
     __syncthreads();
     const uint32_t nkept = tot & 0xFFFFu, njob = tot >> 16;
     if (nkept) {
@@ -4237,6 +4259,8 @@ struct Tune {
     int poison_jobs = 0;             // tests: every slot of the run's long-job list starts as a canary job
     int route_heavy_min = 1 << 16;   // key-range passes: k-mers of >= this many occurrences are routed into
                                      //   the first half of the passes (0: off; k_pass_ids)
+    int select_tile = 1;             // key-range passes: k_pass_select tiles of 2 (1) or 1 (0) 16-byte id
+                                     //   loads per thread, the next tile's loads ahead of this tile's work
     int stage_round = 1;             // key-range passes: 1 = the staged position scatter in half rounds
                                      //   (2048 elements, four workgroups per CU); 0 = full rounds
 };
@@ -5112,9 +5136,16 @@ void prefetch_pass(skm_build* b, uint32_t pass, hipStream_t st) {
     const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
     SKM_HIP(hipMemsetAsync(b->d_hist2[k].p, 0, sizeof(uint32_t) * NB, st));
     const int rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
-    SKM_LAUNCH(b, k_pass_select, dim3(SEL_WG), dim3(SEL_THREADS), sizeof(uint32_t) * NB, st, b->d_ids.as<uint8_t>(),
-               b->d_res.as<uint8_t>(), b->rp, b->sel_span, pass, b->d_seloff.as<uint64_t>() + (uint64_t)pass * (SEL_WG + 1),
-               b->pass_max, b->d_pos2[k].as<uint64_t>(), rem_bits, NB, b->d_hist2[k].as<uint32_t>());
+    if (b->tune.select_tile == 0)
+        SKM_LAUNCH_AS(b, "k_pass_select", k_pass_select<1>, dim3(SEL_WG), dim3(SEL_THREADS), sizeof(uint32_t) * NB, st,
+                      b->d_ids.as<uint8_t>(), b->d_res.as<uint8_t>(), b->rp, b->sel_span, pass,
+                      b->d_seloff.as<uint64_t>() + (uint64_t)pass * (SEL_WG + 1), b->pass_max,
+                      b->d_pos2[k].as<uint64_t>(), rem_bits, NB, b->d_hist2[k].as<uint32_t>());
+    else
+        SKM_LAUNCH_AS(b, "k_pass_select", k_pass_select<2>, dim3(SEL_WG), dim3(SEL_THREADS), sizeof(uint32_t) * NB, st,
+                      b->d_ids.as<uint8_t>(), b->d_res.as<uint8_t>(), b->rp, b->sel_span, pass,
+                      b->d_seloff.as<uint64_t>() + (uint64_t)pass * (SEL_WG + 1), b->pass_max,
+                      b->d_pos2[k].as<uint64_t>(), rem_bits, NB, b->d_hist2[k].as<uint32_t>());
     SKM_HIP(hipGetLastError());
     if (st != b->stream) SKM_HIP(hipEventRecord(b->ev_pf_done[k], st));
     b->pf_pass = pass;
@@ -6201,7 +6232,8 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "chain_streams" ? &t.chain_streams
                : n == "poison_jobs" ? &t.poison_jobs
                : n == "route_heavy_min" ? &t.route_heavy_min
-               : n == "stage_round" ? &t.stage_round : nullptr;
+               : n == "stage_round" ? &t.stage_round
+               : n == "select_tile" ? &t.select_tile : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")
