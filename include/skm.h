@@ -199,7 +199,8 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   windows -- are grouped in the first half of the passes, so their long P^2 chains run beside
  *   the later passes instead of after the last one; 65536; 0 = off), "stage_round" (key-range
  *   passes: 1 = the staged position scatter in half rounds of 2048 elements, four workgroups
- *   per CU, the default; 0 = rounds of 4096).
+ *   per CU, the default; 0 = rounds of 4096), "select_tile" (key-range passes: the pass
+ *   selection's id loads per thread per tile, 1 = two (default), 0 = one).
  * Unknown names and out-of-range values return SKM_E_ARG. */
 int skm_build_set_option(skm_build* b, const char* name, int64_t value);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then
