@@ -200,7 +200,10 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   the later passes instead of after the last one; 65536; 0 = off), "stage_round" (key-range
  *   passes: 1 = the staged position scatter in half rounds of 2048 elements, four workgroups
  *   per CU, the default; 0 = rounds of 4096), "select_tile" (key-range passes: the pass
- *   selection's id loads per thread per tile, 1 = two (default), 0 = one).
+ *   selection's id loads per thread per tile, 1 = two (default), 0 = one), "partition_round"
+ *   (k_partition staging rounds: 0 = 2048 elements, three 512-thread workgroups per CU (default);
+ *   1 = 4096, one per CU; 2 = 4096, one 1024-thread workgroup per CU), "flag_check" (1: the
+ *   group-by reads a sequence's signature flag before storing it; 0).
  * Unknown names and out-of-range values return SKM_E_ARG. */
 int skm_build_set_option(skm_build* b, const char* name, int64_t value);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then

@@ -2156,6 +2156,7 @@ struct BucketArgs {
     uint32_t big_cap;
     int prio;                  // wave issue priority of the group-by (above the concurrent chains)
     int pshift;                // KEY_BITS - pass bits (key_h43)
+    int flag_check;            // 1: a signature flag is stored only when it reads 0 (option flag_check)
     const uint32_t* skip;      // k_ovf_plan's verdict for the pass (nonzero: the run is being abandoned)
 };
 
@@ -2349,8 +2350,9 @@ __device__ __forceinline__ void seg_groups(const SubLds& L, uint32_t q0, uint32_
     const uint64_t Rs = R & segmask;
     const uint32_t rs = Rs ? (uint32_t)__ffsll((long long)Rs) - 1u : sbase;
     const uint32_t s = (uint32_t)(key >> ELEM_I_BITS) & ((1u << ELEM_S_BITS) - 1u);
+    const uint32_t fl = (A.flag_check && real) ? A.flags[s] : 0u;
     const uint32_t len = (pay & 1u) ? A.glen[s] : len16;
-    if (kept && real) A.flags[s] = 1;
+    if (kept && real && fl == 0) A.flags[s] = 1;
     const uint32_t x0 = (uint32_t)__shfl((int)len, (int)(rs + cbest - 1), 64);  // first visited
     const uint32_t x1 = (uint32_t)__shfl((int)len, (int)rs, 64);                // second when cbest == 2
     if (kept && inrun && cbest >= 3) L.lens32[2 * a + (rs + cbest - 1 - lane)] = len;  // visit order
@@ -2459,7 +2461,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
                 v += (cnt << 13) | 1u;
             } else if (j < n && cnt == 1) {  // group of one: always kept (1 >= 0.8), median 0, var 0
                 const uint64_t H = L.hi[j], Lo = L.lo[j];
-                A.flags[Lo >> 36] = 1;
+                if (!A.flag_check || A.flags[Lo >> 36] == 0) A.flags[Lo >> 36] = 1;
                 L.hi[j] = kept_hi(key_h43(hprefix, (H >> 16) & REM_MASK, A.rem_bits, A.pshift), (uint32_t)(Lo & 0xFFFFu));
                 L.lo[j] = kept_lo((uint32_t)(H & 0xFFFFu), d2u16((double)(uint16_t)(H >> 48) / 1.0), 0, 0);
                 L.rank[j] = 0xFFFFu;  // singleton marker
@@ -2973,11 +2975,13 @@ __global__ __launch_bounds__(BIG_WG) void k_big_append(const BigOut* __restrict_
 // several ranks): count by the next b2 bits of rem, exclusive scan, scatter into tmp.  Writes the
 // sub-bucket table for k_bucket_process and queues sub-buckets larger than CAP for k_overflow,
 // so the overflow path (and its long P^2 chains) can run concurrently with the group-by.
-constexpr uint32_t PT_ROUND = 2048;  // elements staged per round of the level-2 scatter
-
-// LDS ~52 KB: three workgroups per CU (the sub-bucket of a staged element is recomputed from its
-// key instead of staged, and the running write offsets double as the sub-bucket table)
-__global__ __launch_bounds__(BP_THREADS, 3) void k_partition(BucketArgs A) {
+// PT_ROUND elements staged per round of the level-2 scatter.  LDS ~52 KB at 2048: three
+// workgroups per CU (the sub-bucket of a staged element is recomputed from its key instead of
+// staged, and the running write offsets double as the sub-bucket table); 4096 (option
+// partition_round = 1, 2): one per CU, but each round's run per sub-bucket is twice as long, so
+// fewer 128-byte lines leave L2 partly written.
+template <uint32_t PT_ROUND, uint32_t PT_THREADS, int MINB>
+__global__ __launch_bounds__(PT_THREADS, MINB) void k_partition(BucketArgs A) {
     __shared__ uint32_t s_cur[(1 << MAX_B2) + 1];   // counts, then running write offsets
     __shared__ uint32_t s_rc[1 << MAX_B2];          // this round's count per sub-bucket
     __shared__ uint16_t s_ro[(1 << MAX_B2) + 1];    // ... and its staging offset (<= PT_ROUND)
@@ -3043,17 +3047,22 @@ __global__ __launch_bounds__(BP_THREADS, 3) void k_partition(BucketArgs A) {
     // sub-bucket's run contiguously (whole lines instead of scattered 8-byte stores)
     // the next round's elements are loaded into registers before this round's LDS work, so the
     // HBM latency overlaps the staging instead of opening every round
-    constexpr uint32_t PER = PT_ROUND / BP_THREADS;
+    // (the register prefetch only in the 2048 form: the 4096 form would spill)
+    constexpr uint32_t PER = PT_ROUND / PT_THREADS;
+    constexpr bool PF = PER <= 4;
+    constexpr uint32_t NPF = PF ? PER : 1;
     for (uint32_t p = 0; p < nseg; ++p) {
         uint64_t base, len;
         seg(p, base, len);
-        uint64_t nh[PER], nl[PER];
+        uint64_t nh[NPF], nl[NPF];
+        if constexpr (PF) {
 #pragma unroll
-        for (uint32_t u = 0; u < PER; ++u) {
-            const uint64_t j = threadIdx.x + (uint64_t)u * BP_THREADS;
-            if (j < len) {
-                nh[u] = A.recs_hi[base + j];
-                nl[u] = A.recs_lo[base + j];
+            for (uint32_t u = 0; u < PER; ++u) {
+                const uint64_t j = threadIdx.x + (uint64_t)u * PT_THREADS;
+                if (j < len) {
+                    nh[u] = A.recs_hi[base + j];
+                    nl[u] = A.recs_lo[base + j];
+                }
             }
         }
         for (uint64_t rb = 0; rb < len; rb += PT_ROUND) {
@@ -3062,19 +3071,27 @@ __global__ __launch_bounds__(BP_THREADS, 3) void k_partition(BucketArgs A) {
             uint32_t sb[PER], rk[PER];
 #pragma unroll
             for (uint32_t u = 0; u < PER; ++u) {
-                eh[u] = nh[u];
-                el[u] = nl[u];
                 sb[u] = 0xFFFFFFFFu;
-                const uint64_t j = rb + PT_ROUND + threadIdx.x + (uint64_t)u * BP_THREADS;
-                if (j < len) {
-                    nh[u] = A.recs_hi[base + j];
-                    nl[u] = A.recs_lo[base + j];
+                if constexpr (PF) {
+                    eh[u] = nh[u];
+                    el[u] = nl[u];
+                    const uint64_t j = rb + PT_ROUND + threadIdx.x + (uint64_t)u * PT_THREADS;
+                    if (j < len) {
+                        nh[u] = A.recs_hi[base + j];
+                        nl[u] = A.recs_lo[base + j];
+                    }
+                } else {
+                    const uint64_t j = rb + threadIdx.x + (uint64_t)u * PT_THREADS;
+                    if (j < len) {
+                        eh[u] = A.recs_hi[base + j];
+                        el[u] = A.recs_lo[base + j];
+                    }
                 }
             }
             __syncthreads();
 #pragma unroll
             for (uint32_t u = 0; u < PER; ++u) {
-                const uint64_t j = rb + threadIdx.x + (uint64_t)u * BP_THREADS;
+                const uint64_t j = rb + threadIdx.x + (uint64_t)u * PT_THREADS;
                 if (j < len) {
                     sb[u] = (uint32_t)(((eh[u] >> 16) & rem_mask) >> shift);
                     rk[u] = atomicAdd(&s_rc[sb[u]], 1u);
@@ -4259,6 +4276,9 @@ struct Tune {
     int poison_jobs = 0;             // tests: every slot of the run's long-job list starts as a canary job
     int route_heavy_min = 1 << 16;   // key-range passes: k-mers of >= this many occurrences are routed into
                                      //   the first half of the passes (0: off; k_pass_ids)
+    int flag_check = 0;              // 1: k_bucket_process reads a signature flag before storing it
+    int partition_round = 0;         // k_partition staging rounds: 0 = 2048 elements (three 512-thread
+                                     //   workgroups per CU), 1 = 4096 (one), 2 = 4096 (one of 1024 threads)
     int select_tile = 1;             // key-range passes: k_pass_select tiles of 2 (1) or 1 (0) 16-byte id
                                      //   loads per thread, the next tile's loads ahead of this tile's work
     int stage_round = 1;             // key-range passes: 1 = the staged position scatter in half rounds
@@ -5448,6 +5468,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     A.pshift = KEY_BITS - b->pass_bits;
     A.glen = b->d_glen.as<uint32_t>();
     A.flags = b->d_flags.as<uint8_t>();
+    A.flag_check = b->tune.flag_check;
     A.ctr = ctr_d;
     A.out_keys = b->d_keys.as<uint64_t>();
     A.out_data = b->d_data.as<skm_stored_kmer_data>();
@@ -5465,7 +5486,12 @@ void phase_group(skm_build* b, uint32_t pass) {
         A.stamps = b->d_stamps.as<unsigned long long>();
     }
     // ---- 4a. level-2 partition ----
-    SKM_LAUNCH(b, k_partition, dim3(NB1), dim3(BP_THREADS), 0, st, A);
+    if (b->tune.partition_round == 1)
+        SKM_LAUNCH_AS(b, "k_partition", (k_partition<4096, 512, 1>), dim3(NB1), dim3(512), 0, st, A);
+    else if (b->tune.partition_round == 2)
+        SKM_LAUNCH_AS(b, "k_partition", (k_partition<4096, 1024, 1>), dim3(NB1), dim3(1024), 0, st, A);
+    else
+        SKM_LAUNCH_AS(b, "k_partition", (k_partition<2048, BP_THREADS, 3>), dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[10], st));
     SKM_HIP(hipEventRecord(b->ev_pf_ready, st));
@@ -6233,7 +6259,9 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "poison_jobs" ? &t.poison_jobs
                : n == "route_heavy_min" ? &t.route_heavy_min
                : n == "stage_round" ? &t.stage_round
-               : n == "select_tile" ? &t.select_tile : nullptr;
+               : n == "select_tile" ? &t.select_tile
+               : n == "partition_round" ? &t.partition_round
+               : n == "flag_check" ? &t.flag_check : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")

@@ -83,19 +83,23 @@ def test_overflow_inline_chains(skm, gpu, inline_min):
     assert_same(got, ref)
 
 
-@pytest.mark.parametrize("passes,long_class,stage_round", [(1, 6, 1), (2, 14, 1), (4, 8, 1), (64, 14, 1), (4, 8, 0)])
-def test_key_range_passes(skm, gpu, passes, long_class, stage_round):
+@pytest.mark.parametrize("passes,long_class,opts", [(1, 6, {}), (2, 14, {}), (4, 8, {}), (64, 14, {}),
+                                                   (4, 8, {"stage_round": 0}), (4, 8, {"partition_round": 1}),
+                                                   (4, 8, {"partition_round": 2})])
+def test_key_range_passes(skm, gpu, passes, long_class, opts):
     """Out-of-core build: P passes over disjoint k-mer ranges (each k-mer in exactly one pass)
     give the single-pass result bit for bit, overflow sub-buckets and chains included, and a
     second run over the same handle repeats it (arena cursor, flags and counters reset).  Low
     long-chain classes send most chains through the stash + chain streams that outlive a pass.
-    stage_round = 0: the staged position scatter in full rounds (1, half rounds, is the default)."""
+    opts: the staging / partition round-size variants (stage_round 0: full rounds;
+    partition_round 1, 2: rounds of 4096 with 512 / 1024 threads)."""
     p = synth.generate_arrays(60000, 60, per_file=2000, seed=6)
     r, o, l, f, i, funcs = synth.build_inputs(p)
     ref = oracle_ref.build(r, o, l, f, i, len(funcs))
     b = skm.SignatureBuilder(len(funcs))
     b.set_option("key_range_passes", passes)
-    b.set_option("stage_round", stage_round)
+    for k, v in opts.items():
+        b.set_option(k, v)
     b.set_option("main_long_class", long_class)
     b.set_option("overflow_long_class", long_class)
     b.add_batch(r, o, l, f, i)
