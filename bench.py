@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--gen-workers", type=int, default=0, help="generator processes (0: usable cores)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--cache-dir", default=None, help="save / reuse the generated headline shard (profiling)")
-    ap.add_argument("--cache-only", action="store_true", help="generate + cache the headline shard, then exit")
+    ap.add_argument("--cache-only", action="store_true", help="generate + cache every input of this run (headline shard, queries, matrix sets), then exit")
     ap.add_argument("--option", action="append", default=[],
                     help="name=value: skm_build_set_option on the headline build (experiments)")
     ap.add_argument("--annot-queries", type=int, default=10_000_000,
@@ -184,9 +184,6 @@ def main():
     f0, f1 = rank * files_total // world, (rank + 1) * files_total // world
     log(f"rank {rank}/{world}: generating files [{f0}, {f1}) with {workers} workers")
     c3 = gen(synth, a.seqs_total, a.families, f0, f1 - f0, workers, a.cache_dir)
-    if a.cache_only:
-        log("inputs cached")
-        return
     log(f"generated {c3.n_seqs:,} proteins, {c3.n_windows:,} windows")
     c2_files = (a.weak_seqs + PER_FILE - 1) // PER_FILE
     if a.weak_seqs and f0 == rank * c2_files and f1 - f0 >= c2_files:
@@ -201,14 +198,17 @@ def main():
         if c2_files + nqf <= len(c3.parts):  # files after the training set: fresh proteins, own RNG streams
             queries = Shard(c3.parts[c2_files:c2_files + nqf])
         else:
-            queries = gen(synth, (c2_files + nqf) * PER_FILE, a.families, c2_files, nqf, workers)
+            queries = gen(synth, (c2_files + nqf) * PER_FILE, a.families, c2_files, nqf, workers, a.cache_dir)
     matrix_in = None
     if a.matrix_seqs > 0:  # every rank: the DB is replicated, the pair triangle tiled by rows
         fam, n_train = 200, 200_000
         nfq = (a.matrix_seqs + PER_FILE - 1) // PER_FILE
         tf = n_train // PER_FILE
-        matrix_in = (gen(synth, n_train, fam, 0, tf, workers), gen(synth, (tf + nfq) * PER_FILE, fam, tf, nfq, workers),
-                     synth.functions(fam))
+        matrix_in = (gen(synth, n_train, fam, 0, tf, workers, a.cache_dir),
+                     gen(synth, (tf + nfq) * PER_FILE, fam, tf, nfq, workers, a.cache_dir), synth.functions(fam))
+    if a.cache_only:
+        log("inputs cached")
+        return
     funcs = synth.functions(a.families)
     gen_s = time.time() - t0
 

@@ -203,7 +203,10 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   selection's id loads per thread per tile, 1 = two (default), 0 = one), "partition_round"
  *   (k_partition staging rounds: 0 = 2048 elements, three 512-thread workgroups per CU (default);
  *   1 = 4096, one per CU; 2 = 4096, one 1024-thread workgroup per CU), "flag_check" (1: the
- *   group-by reads a sequence's signature flag before storing it; 0).
+ *   group-by reads a sequence's signature flag before storing it; 0), "serial_overflow"
+ *   (diagnostics: 1 = a pass's overflow path starts after its group-by kernel; 0), "chain_cus"
+ *   (the stashed long chains' stream confined to this many CUs, a multiple of 8; 0 = all),
+ *   "side_cus" (the same for the overflow streams and the next pass's selection).
  * Unknown names and out-of-range values return SKM_E_ARG. */
 int skm_build_set_option(skm_build* b, const char* name, int64_t value);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then

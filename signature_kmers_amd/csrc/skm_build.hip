@@ -373,6 +373,23 @@ __device__ uint32_t wg_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t& to
     return r;
 }
 
+// The same scan with one barrier: every thread sums the wave totals itself.  The caller must
+// pass a barrier before s_wave is written again (the next scan on it).
+__device__ __forceinline__ uint32_t wg_exclusive_scan1(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint32_t x = wave_incl_scan(v);
+    if (lane == 63) s_wave[wave] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t w = 0; w < nw; ++w) {
+        const uint32_t t = s_wave[w];
+        pre += w < wave ? t : 0u;
+        tot += t;
+    }
+    total = tot;
+    return pre + x - v;
+}
+
 // ------------------------------------------------------------------------------------------
 // Group processing (process_kmer_set, signature_build.tcc:219-293).
 //
@@ -2415,6 +2432,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         }
     }
     if (tid == 0) *L.nbig = 0;
+    if (tid < 8) L.ccnt[tid] = 0;  // the size-class counters (last read before this batch's emit)
     __syncthreads();
     SKM_STAMP(2);
     // 2. hash insert: slot = representative << 16 | count; the pre-increment count is the rank
@@ -2450,7 +2468,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
             loc += (cnt > 1 && (ev[u] >> 16) == j) ? ((cnt << 13) | 1u) : 0u;
         }
         uint32_t tot;
-        uint32_t v = wg_exclusive_scan(loc, L.wave, tot);
+        uint32_t v = wg_exclusive_scan1(loc, L.wave, tot);  // L.wave next written by the emit scan
 #pragma unroll
         for (uint32_t u = 0; u < LPER; ++u) {
             const uint32_t j = j0 + u;
@@ -2472,22 +2490,14 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     }
     __syncthreads();
     SKM_STAMP(4);
-    // 4. counting-sort scatter of the multi-occurrence elements
+    // 4. counting-sort scatter of the multi-occurrence elements, and the groups' size classes:
+    //    classes 0..5 = segment size 2,4,..,64 (packed 64/S per wave), class 6 = more than 64
+    //    members (one wave per group).  `big` will hold the class-ordered list.
     for (uint32_t j = tid; j < n; j += nt) {
         const uint32_t e = L.tab[L.slot[j]];
         if ((e & 0xFFFFu) > 1) L.order[L.goff[e >> 16] + L.rank[j]] = (uint16_t)j;
     }
-    __syncthreads();
-    uint32_t* jobinfo = L.tab;        // per representative: best-run start << 16 | KEPT | best count
-    uint32_t* fmean = L.tab + CAP;    // per representative: func | mean << 16
-    for (uint32_t j = tid; j < n; j += nt) jobinfo[j] = L.rank[j] == 0xFFFFu ? JOB_KEPT : 0u;
-    __syncthreads();
-    SKM_STAMP(5);
-    // 5. groups by size class: classes 0..5 = segment size 2,4,..,64 (packed 64/S per wave),
-    //    class 6 = more than 64 members (one wave per group).  `big` holds the class-ordered list.
     uint32_t* ccnt = L.ccnt;
-    if (tid < 8) ccnt[tid] = 0;
-    __syncthreads();
     auto cls_of = [](uint32_t c) -> uint32_t {
         return c > 64u ? 6u : 31u - (uint32_t)__clz(c - 1u) - 0u;  // c in [2,64]: ceil(log2 c) - 1
     };
@@ -2497,6 +2507,11 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         atomicAdd(&ccnt[cls_of(c)], 1u);  // (a per-wave ballot version measured slower)
     }
     __syncthreads();
+    SKM_STAMP(5);
+    // 5. the job info (over the hash table, read for the last time above), the class offsets
+    uint32_t* jobinfo = L.tab;        // per representative: best-run start << 16 | KEPT | best count
+    uint32_t* fmean = L.tab + CAP;    // per representative: func | mean << 16
+    for (uint32_t j = tid; j < n; j += nt) jobinfo[j] = L.rank[j] == 0xFFFFu ? JOB_KEPT : 0u;
     // ccnt[0..7]: cursors, [8..15]: class starts in big[], [16..23]: first wave task of each class
     uint32_t* cstart = ccnt + 8;
     uint32_t* tstart = ccnt + 16;
@@ -2515,7 +2530,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         tstart[7] = acc;
     }
     // groups of more than 64 members go to k_big_groups: reserve their descriptors now, the
-    // atomic's latency hides behind the packed-group phase
+    // atomic's latency behind the class scatter
     unsigned long long big_base = 0;
     if (tid == 0 && cstart[7] > cstart[6]) big_base = atomicAdd(&A.ctr[5], (unsigned long long)(cstart[7] - cstart[6]));
     __syncthreads();
@@ -2524,17 +2539,53 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
         L.big[atomicAdd(&ccnt[cls_of(c)], 1u)] = (uint16_t)g;
     }
+    if (tid == 0) *reinterpret_cast<unsigned long long*>(L.wave + 44) = big_base;
     __syncthreads();
     SKM_STAMP(6);
     {
-        // wave tasks: class k packs 64 >> (k + 1) groups per task
+        // one list of wave tasks: first the hand-off of each group of more than 64 members (its
+        // members (func << 48 | ordinal) into the group's own consumed slots, protein length
+        // beside it, one descriptor each; k_big_groups resolves them register-resident), then the
+        // packed groups -- class k packs 64 >> (k + 1) groups per task
         const uint32_t ntask = tstart[6];
-        const uint32_t wave = tid >> 6, nwaves = nt >> 6;
-        for (uint32_t t = wave; t < ntask; t += nwaves) {
+        const uint32_t nbig = cstart[7] - cstart[6];
+        const uint64_t bbase = *reinterpret_cast<const unsigned long long*>(L.wave + 44);
+        const uint32_t wave = tid >> 6, nwaves = nt >> 6, lane = tid & 63u;
+        uint64_t* slots = reinterpret_cast<uint64_t*>(L.lens32);
+        uint64_t* slots_lo = const_cast<uint64_t*>(src_lo);
+        // tasks taken from an LDS counter (ccnt[7], zeroed with the class counters), longest first:
+        // the hand-offs, then the packed classes from 64-lane segments down to pairs
+        (void)wave;
+        (void)nwaves;
+        for (;;) {
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(&ccnt[7], 1u);
+            t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+            if (t >= nbig + ntask) break;
+            if (t < nbig) {
+                const uint32_t g = L.big[cstart[6] + t];
+                const uint32_t rep = L.glist[g];
+                const uint32_t a = L.goff[rep];
+                const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
+                for (uint32_t u = lane; u < c; u += 64) {
+                    const uint32_t j = L.order[a + u];
+                    const uint64_t hj = L.hi[j], lj = L.lo[j];
+                    slots[a + u] = ((hj & 0xFFFFull) << 48) | (lj >> 16);
+                    slots_lo[a + u] = elem_len(hj, lj, A.glen);  // no per-member gathers downstream
+                }
+                const uint64_t q = bbase + t;
+                if (lane == 0 && q < A.big_cap) {
+                    A.big_desc[2 * q] = key_h43(hprefix, (L.hi[rep] >> 16) & REM_MASK, A.rem_bits, A.pshift) |
+                                        ((uint64_t)c << KEY_BITS);
+                    A.big_desc[2 * q + 1] = L.lens_sel + 2 * a;
+                }
+                continue;
+            }
+            const uint32_t ts = ntask - 1u - (t - nbig);
             uint32_t k = 0;
-            while (k < 5 && t >= tstart[k + 1]) ++k;
+            while (k < 5 && ts >= tstart[k + 1]) ++k;
             const uint32_t per = 64u >> (k + 1);
-            const uint32_t q0 = cstart[k] + (t - tstart[k]) * per, qe = cstart[k + 1];
+            const uint32_t q0 = cstart[k] + (ts - tstart[k]) * per, qe = cstart[k + 1];
             switch (k) {
                 case 0: seg_groups<2>(L, q0, qe, G, M, A, hprefix, jobinfo, fmean); break;
                 case 1: seg_groups<4>(L, q0, qe, G, M, A, hprefix, jobinfo, fmean); break;
@@ -2545,37 +2596,8 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
             }
         }
     }
-    if (tid == 0) *reinterpret_cast<unsigned long long*>(L.wave + 44) = big_base;
     __syncthreads();
     SKM_STAMP(11);
-    {   // groups of more than 64 members: members (func << 48 | ordinal) into the group's own
-        // consumed slots (protein length beside it), one descriptor each; k_big_groups resolves
-        // them register-resident
-        const uint32_t nbig = cstart[7] - cstart[6];
-        const uint64_t bbase = *reinterpret_cast<const unsigned long long*>(L.wave + 44);
-        const uint32_t wave = tid >> 6, nwaves = nt >> 6, lane = tid & 63u;
-        uint64_t* slots = reinterpret_cast<uint64_t*>(L.lens32);
-        for (uint32_t bi = wave; bi < nbig; bi += nwaves) {
-            const uint32_t g = L.big[cstart[6] + bi];
-            const uint32_t rep = L.glist[g];
-            const uint32_t a = L.goff[rep];
-            const uint32_t c = g + 1 < G ? L.goff[L.glist[g + 1]] - a : M - a;
-            uint64_t* slots_lo = const_cast<uint64_t*>(src_lo);
-            for (uint32_t t = lane; t < c; t += 64) {
-                const uint32_t j = L.order[a + t];
-                const uint64_t hj = L.hi[j], lj = L.lo[j];
-                slots[a + t] = ((hj & 0xFFFFull) << 48) | (lj >> 16);
-                slots_lo[a + t] = elem_len(hj, lj, A.glen);  // no per-member gathers downstream
-            }
-            const uint64_t q = bbase + bi;
-            if (lane == 0 && q < A.big_cap) {
-                A.big_desc[2 * q] = key_h43(hprefix, (L.hi[rep] >> 16) & REM_MASK, A.rem_bits, A.pshift) |
-                                    ((uint64_t)c << KEY_BITS);
-                A.big_desc[2 * q + 1] = L.lens_sel + 2 * a;
-            }
-        }
-    }
-    __syncthreads();
     SKM_STAMP(7);
     // 6. emit kept k-mers and chain jobs: one scan and one reservation per batch; the kept
     //    elements are first compacted in LDS (slot[] = kept list, order[] = job list, rank[] =
@@ -2591,7 +2613,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         cnt += ((jb & JOB_KEPT) ? 1u : 0u) | ((jb & JOB_COUNT_MASK) ? 0x10000u : 0u);
     }
     uint32_t tot;
-    const uint32_t pos = wg_exclusive_scan(cnt, L.wave, tot);
+    const uint32_t pos = wg_exclusive_scan1(cnt, L.wave, tot);  // next written by the next batch's classify
     // the two reservations from two waves at once, their latency behind the LDS compaction
     unsigned long long rsv = 0;
     if (tid == 0 && (tot & 0xFFFFu)) rsv = atomicAdd(A.kept_ctr, (unsigned long long)(tot & 0xFFFFu));
@@ -4276,6 +4298,9 @@ struct Tune {
     int poison_jobs = 0;             // tests: every slot of the run's long-job list starts as a canary job
     int route_heavy_min = 1 << 16;   // key-range passes: k-mers of >= this many occurrences are routed into
                                      //   the first half of the passes (0: off; k_pass_ids)
+    int chain_cus = 0;               // CUs of the long-chain stream (0: all; set_option recreates it)
+    int side_cus = 0;                // CUs of the overflow and selection streams (0: all)
+    int serial_overflow = 0;         // diagnostics: 1 = the overflow path starts after the group-by kernel
     int flag_check = 0;              // 1: k_bucket_process reads a signature flag before storing it
     int partition_round = 0;         // k_partition staging rounds: 0 = 2048 elements (three 512-thread
                                      //   workgroups per CU), 1 = 4096 (one), 2 = 4096 (one of 1024 threads)
@@ -5520,9 +5545,6 @@ void phase_group(skm_build* b, uint32_t pass) {
     SKM_LAUNCH(b, k_ovf_plan, dim3(1), dim3(1024), 0, st, P);
     SKM_HIP(hipGetLastError());
     A.skip = plan_d + PLAN_SKIP;
-    SKM_HIP(hipEventRecord(b->ev_part, st));
-    SKM_HIP(hipStreamWaitEvent(st2, b->ev_part, 0));
-    SKM_HIP(hipStreamWaitEvent(st3, b->ev_part, 0));
     // ---- 5. overflow sub-buckets (> CAP elements), largest first, concurrent with the group-by:
     //      the split (heavy keys out to k_heavy) and the heavy entries on stream 2, whose chains
     //      start as soon as they are grouped; the rest on stream 3 ----
@@ -5545,8 +5567,6 @@ void phase_group(skm_build* b, uint32_t pass) {
     A3.lens = A2.lens;
     const uint32_t inline_min = (uint32_t)b->tune.ovf_inline_min;
     const int prio = b->tune.inline_prio;
-    SKM_HIP(hipEventRecord(b->ev_o[0], st2));
-    SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
     HeavyArgs H;
     H.keys = b->d_hv_keys.as<HeavyKey>();
     H.nkeys = ctr_d + 18;  // cleared with the pass's counters
@@ -5569,13 +5589,21 @@ void phase_group(skm_build* b, uint32_t pass) {
     H.gcap = 0;
     H.gstat = nullptr;
     if (H.giant_min) {
-        SKM_HIP(hipMemsetAsync(b->gcount[pass].p, 0, 16, st2));
         H.gsamples = b->gsamples[pass].as<uint32_t>();
         H.gjobs = b->gjobs[pass].as<Job>();
         H.gcount = b->gcount[pass].as<unsigned long long>();
         H.gcap = b->split_cap;
         H.gstat = b->d_gstat.as<unsigned long long>();
     }
+    // issued before the group-by (concurrent with it), or after it (option serial_overflow: the
+    // group-by's time alone)
+    auto launch_overflow = [&]() {
+    SKM_HIP(hipEventRecord(b->ev_part, st));
+    SKM_HIP(hipStreamWaitEvent(st2, b->ev_part, 0));
+    SKM_HIP(hipStreamWaitEvent(st3, b->ev_part, 0));
+    SKM_HIP(hipEventRecord(b->ev_o[0], st2));
+    SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
+    if (H.giant_min) SKM_HIP(hipMemsetAsync(b->gcount[pass].p, 0, 16, st2));
     SKM_LAUNCH(b, k_ovf_split, dim3((uint32_t)std::max(1, b->tune.split_grid)), dim3(BP_THREADS), 0, st2, A2, S, H, key_min, plan_d);
     SKM_HIP(hipEventRecord(b->ev_split, st2));
     SKM_HIP(hipStreamWaitEvent(st3, b->ev_split, 0));
@@ -5596,6 +5624,8 @@ void phase_group(skm_build* b, uint32_t pass) {
     SKM_LAUNCH(b, k_overflow, dim3((uint32_t)std::max(1, b->tune.ovf_grid)), dim3(BP_THREADS), 0, st3, A3, S, plan_d, (int)PLAN_NHEAVY,
                        (int)PLAN_NOVF, (int)PLAN_Q_REST, inline_min, prio);
     SKM_HIP(hipGetLastError());
+    };
+    if (!b->tune.serial_overflow) launch_overflow();
     // ---- 4b. group-by of the sub-buckets that fit LDS; groups of > 64 members are handed to
     //      k_big_groups (one wave each) and appended ----
     BigArgs BA;
@@ -5612,6 +5642,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     SKM_LAUNCH(b, k_bucket_process, dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[5], st));
+    if (b->tune.serial_overflow) launch_overflow();
     // the next pass's compaction + count overlap this pass's group-by on stx: its buffer set was
     // last read by this pass's predecessor's extract, complete once this pass's partition is
     if (b->pass_bits && pass + 1 < NP && b->tune.prefetch) {
@@ -6226,6 +6257,43 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
         SKM_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
         SKM_HIP(hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, value ? greatest : least));
         t.stream_prio = (int)value;
+    } else if (n == "chain_cus" || n == "side_cus") {
+        // chain_cus: the long-chain stream confined to this many CUs (0: all) -- a batch of
+        // stashed long chains is thousands of two-wave workgroups whose registers would otherwise
+        // keep one of the two group-by workgroups off every CU while it runs; side_cus: the same
+        // for the overflow streams and the next pass's selection.  The CUs taken are the last
+        // value/8 of every 32 (spread over the XCDs).
+        SKM_CHECK(value >= 0 && value <= 256 && value % 8 == 0, SKM_E_ARG, (n + " must be a multiple of 8 in [0, 256]").c_str());
+        SKM_HIP(hipSetDevice(b->device));
+        hipDeviceProp_t prop;
+        SKM_HIP(hipGetDeviceProperties(&prop, b->device));
+        const uint32_t ncu = (uint32_t)prop.multiProcessorCount;
+        auto remake = [&](hipStream_t& x) {
+            SKM_HIP(hipStreamSynchronize(x));
+            SKM_HIP(hipStreamDestroy(x));
+            if (value == 0 || (uint32_t)value >= ncu) {
+                SKM_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+                return;
+            }
+            std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+            const uint32_t per = (uint32_t)value / 8;  // per block of 32 CUs
+            uint32_t taken = 0;
+            for (uint32_t c = 0; c < ncu && taken < (uint32_t)value; ++c)
+                if (c % 32 >= 32 - per) {
+                    mask[c / 32] |= 1u << (c % 32);
+                    ++taken;
+                }
+            SKM_HIP(hipExtStreamCreateWithCUMask(&x, (uint32_t)mask.size(), mask.data()));
+        };
+        if (n == "chain_cus") {
+            remake(b->chain_st);
+            t.chain_cus = (int)value;
+        } else {
+            remake(b->stream2);
+            remake(b->stream3);
+            remake(b->stx);
+            t.side_cus = (int)value;
+        }
     } else if (n == "work_buffer_elements") {
         // capacities of the data-sized work buffers (tests: force the grow-and-redo path); 0 = the
         // automatic first guess
@@ -6261,7 +6329,8 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "stage_round" ? &t.stage_round
                : n == "select_tile" ? &t.select_tile
                : n == "partition_round" ? &t.partition_round
-               : n == "flag_check" ? &t.flag_check : nullptr;
+               : n == "flag_check" ? &t.flag_check
+               : n == "serial_overflow" ? &t.serial_overflow : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")

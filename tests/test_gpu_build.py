@@ -85,14 +85,17 @@ def test_overflow_inline_chains(skm, gpu, inline_min):
 
 @pytest.mark.parametrize("passes,long_class,opts", [(1, 6, {}), (2, 14, {}), (4, 8, {}), (64, 14, {}),
                                                    (4, 8, {"stage_round": 0}), (4, 8, {"partition_round": 1}),
-                                                   (4, 8, {"partition_round": 2})])
+                                                   (4, 8, {"partition_round": 2}), (1, 6, {"flag_check": 1}),
+                                                   (4, 8, {"serial_overflow": 1}), (4, 8, {"chain_cus": 32}),
+                                                   (4, 8, {"side_cus": 64})])
 def test_key_range_passes(skm, gpu, passes, long_class, opts):
     """Out-of-core build: P passes over disjoint k-mer ranges (each k-mer in exactly one pass)
     give the single-pass result bit for bit, overflow sub-buckets and chains included, and a
     second run over the same handle repeats it (arena cursor, flags and counters reset).  Low
     long-chain classes send most chains through the stash + chain streams that outlive a pass.
     opts: the staging / partition round-size variants (stage_round 0: full rounds;
-    partition_round 1, 2: rounds of 4096 with 512 / 1024 threads)."""
+    partition_round 1, 2: rounds of 4096 with 512 / 1024 threads), flag_check, serial_overflow, chain_cus / side_cus (the long-chain / overflow
+    and selection streams on a subset of the CUs)."""
     p = synth.generate_arrays(60000, 60, per_file=2000, seed=6)
     r, o, l, f, i, funcs = synth.build_inputs(p)
     ref = oracle_ref.build(r, o, l, f, i, len(funcs))

@@ -27,7 +27,7 @@ step cache 300 python3 bench.py --cache-dir /tmp/c3 --cache-only
 cd /tmp
 C3="python3 -u $R/bench.py --cache-dir /tmp/c3 --weak-seqs 0 --annot-queries 0 --matrix-seqs 0 --no-cpu-baseline"
 C2="python3 -u $R/tools/c3_diag.py --cache-dir /tmp/c3 --files 250"
-LEGS="python3 -u $R/bench.py --seqs-total 1000000 --no-cpu-baseline"
+LEGS="python3 -u $R/bench.py --seqs-total 1000000 --cache-dir /tmp/legs --no-cpu-baseline"
 # PHASE: all | trace (stamps + C3/C2 traces) | pmc (C3/C2 counters) | legs (legs trace + counters)
 P=${PHASE:-all}
 if [ "$P" = all ] || [ "$P" = trace ]; then
@@ -43,6 +43,7 @@ if [ "$P" = all ] || [ "$P" = pmc ]; then
   done
 fi
 if [ "$P" = all ] || [ "$P" = legs ]; then
+  step legs_cache 400 python3 -u $R/bench.py --seqs-total 1000000 --cache-dir /tmp/legs --cache-only
   step prof_legs 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_legs" -o run -- $LEGS --steps 3 --warmup 1 --json-out "$O/bench_legs_trace.json"
   for c in FETCH_SIZE WRITE_SIZE; do
     lc=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
