@@ -206,7 +206,10 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   group-by reads a sequence's signature flag before storing it; 0), "serial_overflow"
  *   (diagnostics: 1 = a pass's overflow path starts after its group-by kernel; 0), "chain_cus"
  *   (the stashed long chains' stream confined to this many CUs, a multiple of 8; 0 = all),
- *   "side_cus" (the same for the overflow streams and the next pass's selection).
+ *   "side_cus" (the same for the overflow streams and the next pass's selection), "overlap"
+ *   (key-range passes on one GPU: 1 = pipelined passes -- a second element buffer set when it
+ *   fits, so a pass's overflow path runs beside the next pass's extract and partition; 0 = each
+ *   pass waits for its overflow path, the default), "heavy_grid" (k_heavy's persistent grid, 512).
  * Unknown names and out-of-range values return SKM_E_ARG. */
 int skm_build_set_option(skm_build* b, const char* name, int64_t value);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then

@@ -3989,7 +3989,8 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
 struct PlanArgs {
     const OvfEntry* in;                 // k_partition's list
     OvfEntry* out;                      // sorted by size class, descending, scratch assigned
-    const unsigned long long* ctr;      // the pass's counters: [0] arena cursor, [1] entries (low 32 bits)
+    const unsigned long long* ctr;      // the pass's counters: [1] entries (low 32 bits)
+    const unsigned long long* kept;     // [0]: the kept arena cursor
     const unsigned long long* nloc;     // elements the pass groups
     unsigned long long* run;
     uint32_t* plan;
@@ -4083,7 +4084,7 @@ __global__ __launch_bounds__(1024) void k_ovf_plan(PlanArgs P) {
         if (raw > P.ovf_cap) atomicOr(&R[RUN_FLAGS], RUN_F_CAP);
         const bool over = tot > P.tot_cap || split > P.split_cap;
         if (over) atomicOr(&R[RUN_FLAGS], RUN_F_RERUN);
-        if (P.ctr[0] + nl > P.kept_cap) atomicOr(&R[RUN_FLAGS], RUN_F_ARENA);
+        if (P.kept[0] + nl > P.kept_cap) atomicOr(&R[RUN_FLAGS], RUN_F_ARENA);
         // a pass that does not fit is skipped (the step is redone); after an error every pass is.
         // The passes after a mere overrun still run, so their demands are known for the redo
         const bool skip = over || (atomicAdd(&R[RUN_FLAGS], 0ull) & (RUN_F_ARENA | RUN_F_CAP)) != 0;
@@ -4289,7 +4290,8 @@ struct Tune {
     int giant_class = -1;
     int giant_passes = 0;            // giant chains only in the last N passes (0: all)
     int prefetch = 1;                // next pass's compaction + count during this pass's group-by
-    int ovf_grid = 1024;             // persistent grids: k_overflow (per stream),
+    int heavy_grid = (int)HEAVY_GRID; // persistent grids: k_heavy,
+    int ovf_grid = 1024;             //   k_overflow (per stream),
     int split_grid = 512;            //   k_ovf_split,
     int chain_grid = 4096;           //   k_chains
     int stream_prio = 0;             // 1: the group-by stream at the highest priority
@@ -4298,6 +4300,7 @@ struct Tune {
     int poison_jobs = 0;             // tests: every slot of the run's long-job list starts as a canary job
     int route_heavy_min = 1 << 16;   // key-range passes: k-mers of >= this many occurrences are routed into
                                      //   the first half of the passes (0: off; k_pass_ids)
+    int overlap = 0;                 // key-range passes, one GPU: pipelined passes (a second element set)
     int chain_cus = 0;               // CUs of the long-chain stream (0: all; set_option recreates it)
     int side_cus = 0;                // CUs of the overflow and selection streams (0: all)
     int serial_overflow = 0;         // diagnostics: 1 = the overflow path starts after the group-by kernel
@@ -4443,6 +4446,15 @@ struct skm_build {
     uint64_t sel_span = 0;               // windows per k_pass_ids / k_pass_select workgroup
     hipStream_t stx = nullptr;
     hipEvent_t ev_pf_ready = nullptr, ev_pf_done[2] = {};
+    // pipelined passes (option overlap, one GPU, key-range passes): a second element buffer set,
+    // so that a pass's overflow path (streams 2/3, reading its buffers) overlaps the next pass's
+    // extract / split / partition instead of closing the pass; per-set counter blocks, plans and
+    // overflow lists; ev_ovf_done[k] = the overflow path (and the pass accounting) of the last
+    // pass that used set k is complete, ev_main_done[k] = its main-stream work is
+    bool overlap = false;
+    DevBuf d_recs_hi2, d_recs_lo2, d_tmp_hi2, d_tmp_lo2, d_ovf2b;
+    hipEvent_t ev_ovf_done[2] = {}, ev_main_done[2] = {};
+    bool ovf_pending[2] = {false, false};
     int64_t pf_pass = -1;               // the pass whose compaction + count are already queued
     uint32_t pf_nwg = 1;                // count-kernel rows of the histogram matrix (pass mode)
     uint64_t pf_span = 0;
@@ -4900,7 +4912,7 @@ void prepare_local(skm_build* b) {
     b->d_bstart32.ensure(sizeof(uint32_t) * (NB + 1));
     b->d_bstart.ensure(sizeof(uint64_t) * (NB + 1));
     b->d_owner_start.ensure(sizeof(uint64_t) * 80);
-    b->d_ctr.ensure(256);
+    b->d_ctr.ensure(3 * 256);
     b->d_dfunc.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
     b->d_swf.ensure(sizeof(uint32_t) * std::max<uint32_t>(b->opts.n_functions, 1));
 }
@@ -5164,6 +5176,24 @@ void prepare(const Ranks& bs) {
         alloc_caps(b);
         size_arena(b);
         b->d_flags.ensure(std::max<uint64_t>(b->n_total, 1));
+        // pipelined passes when the second element buffer set fits beside everything else with a
+        // tenth of the memory to spare (the data-sized buffers may still grow on a redo)
+        b->overlap = false;
+        if (b->tune.overlap && b->world == 1 && b->pass_bits > 0) {
+            size_t fr = 0, tot = 0;
+            SKM_HIP(hipMemGetInfo(&fr, &tot));
+            const uint64_t need = 16 * std::max<uint64_t>(b->pass_max, 1) + 16 * b->cap_local;
+            if (b->d_recs_hi2.bytes >= 8 * std::max<uint64_t>(b->pass_max, 1) && b->d_tmp_hi2.bytes >= 8 * b->cap_local) {
+                b->overlap = true;
+            } else if ((uint64_t)fr > need + tot / 10) {
+                b->d_recs_hi2.ensure(8 * std::max<uint64_t>(b->pass_max, 1));
+                b->d_recs_lo2.ensure(8 * std::max<uint64_t>(b->pass_max, 1));
+                b->d_tmp_hi2.ensure(8 * b->cap_local);
+                b->d_tmp_lo2.ensure(8 * b->cap_local);
+                b->overlap = true;
+            }
+            if (b->overlap) b->d_ovf2b.ensure(sizeof(OvfEntry) * std::max<uint64_t>(b->ovf_cap, 1));
+        }
         SKM_HIP(hipStreamSynchronize(b->stream));
         b->prepared = true;
         b->ran = false;
@@ -5196,6 +5226,17 @@ void prefetch_pass(skm_build* b, uint32_t pass, hipStream_t st) {
     b->pf_pass = pass;
 }
 
+// the element buffer set, counter block, plan and overflow list of a pass (set 0 unless overlap)
+inline int pset(const skm_build* b, uint32_t pass) { return b->overlap ? (int)(pass & 1u) : 0; }
+inline uint64_t* recs_hi(skm_build* b, uint32_t pass) { return (pset(b, pass) ? b->d_recs_hi2 : b->d_recs_hi).as<uint64_t>(); }
+inline uint64_t* recs_lo(skm_build* b, uint32_t pass) { return (pset(b, pass) ? b->d_recs_lo2 : b->d_recs_lo).as<uint64_t>(); }
+inline uint64_t* tmp_hi(skm_build* b, uint32_t pass) { return (pset(b, pass) ? b->d_tmp_hi2 : b->d_tmp_hi).as<uint64_t>(); }
+inline uint64_t* tmp_lo(skm_build* b, uint32_t pass) { return (pset(b, pass) ? b->d_tmp_lo2 : b->d_tmp_lo).as<uint64_t>(); }
+// d_ctr: [0] the kept arena cursor, [2] the flag count (run-level); per-set pass counters at 32, 64
+inline unsigned long long* pass_ctr(skm_build* b, uint32_t pass) {
+    return b->d_ctr.as<unsigned long long>() + 32 * (1 + pset(b, pass));
+}
+
 void phase_extract(skm_build* b, uint32_t pass) {
     hipStream_t st = b->stream;
     const int nbits = b->owner_bits + b->b1_bits;
@@ -5220,8 +5261,8 @@ void phase_extract(skm_build* b, uint32_t pass) {
     X.blk2seq = b->d_blk2seq.as<uint32_t>();
     X.meta = b->d_meta.as<SeqMeta>();
     X.s_base = b->s_base;
-    X.out_hi = b->d_recs_hi.as<uint64_t>();
-    X.out_lo = b->d_recs_lo.as<uint64_t>();
+    X.out_hi = recs_hi(b, pass);
+    X.out_lo = recs_lo(b, pass);
     uint32_t nwg = b->nwg, hist_rows = b->nwg;
     if (b->pass_bits) {
         // this pass's window positions and count: queued on stx during the previous pass's
@@ -5255,6 +5296,10 @@ void phase_extract(skm_build* b, uint32_t pass) {
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[2], st));
     // ---- 3. scatter: 64-way staged pass into tmp, then the split into the final buckets ----
+    if (b->overlap && b->ovf_pending[pset(b, pass)]) {  // the set's previous pass still read it
+        SKM_HIP(hipStreamWaitEvent(st, b->ev_ovf_done[pset(b, pass)], 0));
+        b->ovf_pending[pset(b, pass)] = false;
+    }
     const int l0_shift = nbits - SC_L0_BITS;
     b->d_cur0.ensure(8ull * 64 * CUR_STRIDE);
     b->d_cur1.ensure(8ull * NB * CUR_STRIDE);
@@ -5264,18 +5309,18 @@ void phase_extract(skm_build* b, uint32_t pass) {
     if (b->pass_bits && b->tune.stage_round == 1)
         SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND_HALF, 4>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
                    b->d_pos2[pass & 1].as<uint64_t>(), b->d_npos.as<unsigned long long>() + pass,
-                   b->d_cur0.as<unsigned long long>(), b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
+                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass));
     else if (b->pass_bits)
         SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND, 2>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
                    b->d_pos2[pass & 1].as<uint64_t>(), b->d_npos.as<unsigned long long>() + pass,
-                   b->d_cur0.as<unsigned long long>(), b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
+                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass));
     else
         SKM_LAUNCH(b, k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
-                           b->d_tmp_hi.as<uint64_t>(), b->d_tmp_lo.as<uint64_t>());
+                           tmp_hi(b, pass), tmp_lo(b, pass));
     const uint32_t nsl = (uint32_t)(ceil_div(b->pass_max, SC_SLICE) + (1u << SC_L0_BITS));
-    SKM_LAUNCH(b, k_split_stage, dim3(nsl), dim3(EX_THREADS), 0, st, b->d_tmp_hi.as<uint64_t>(),
-                       b->d_tmp_lo.as<uint64_t>(), b->d_bstart.as<uint64_t>(), nbits, b->d_slices.as<uint32_t>(),
-                       b->d_cur1.as<unsigned long long>(), b->d_recs_hi.as<uint64_t>(), b->d_recs_lo.as<uint64_t>());
+    SKM_LAUNCH(b, k_split_stage, dim3(nsl), dim3(EX_THREADS), 0, st, tmp_hi(b, pass),
+                       tmp_lo(b, pass), b->d_bstart.as<uint64_t>(), nbits, b->d_slices.as<uint32_t>(),
+                       b->d_cur1.as<unsigned long long>(), recs_hi(b, pass), recs_lo(b, pass));
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[3], st));
 }
@@ -5472,21 +5517,23 @@ void phase_group(skm_build* b, uint32_t pass) {
     SKM_HIP(hipEventRecord(b->ev[4], st));
     // per-pass counters; [0] (kept k-mers: the arena cursor) and the signature flags run over
     // all passes (begin_run clears them)
-    SKM_HIP(hipMemsetAsync(b->d_ctr.as<unsigned long long>() + 1, 0, 256 - 8, st));
-    unsigned long long* ctr_d = b->d_ctr.as<unsigned long long>();
+    unsigned long long* ctr_d = pass_ctr(b, pass);
+    SKM_HIP(hipMemsetAsync(ctr_d, 0, 256, st));
     unsigned long long* run_d = b->d_run.as<unsigned long long>();
-    uint32_t* plan_d = b->d_plan.as<uint32_t>();
+    const int ks = pset(b, pass);
+    uint32_t* plan_d = b->d_plan.as<uint32_t>() + PLAN_SLOTS * ks;
+    OvfEntry* ovf2_d = (ks ? b->d_ovf2b : b->d_ovf2).as<OvfEntry>();
     BucketArgs A;
-    A.recs_hi = multi ? b->d_rhi.as<uint64_t>() : b->d_recs_hi.as<uint64_t>();
-    A.recs_lo = multi ? b->d_rlo.as<uint64_t>() : b->d_recs_lo.as<uint64_t>();
-    A.tmp_hi = b->d_tmp_hi.as<uint64_t>();
-    A.tmp_lo = b->d_tmp_lo.as<uint64_t>();
+    A.recs_hi = multi ? b->d_rhi.as<uint64_t>() : recs_hi(b, pass);
+    A.recs_lo = multi ? b->d_rlo.as<uint64_t>() : recs_lo(b, pass);
+    A.tmp_hi = tmp_hi(b, pass);
+    A.tmp_lo = tmp_lo(b, pass);
     A.bstart = multi ? b->d_vstart.as<uint64_t>() : b->d_bstart.as<uint64_t>();
     A.seg_start = multi ? b->d_seg_start.as<uint64_t>() : nullptr;
     A.seg_len = multi ? b->d_seg_len.as<uint32_t>() : nullptr;
     A.nsrc = multi ? (uint32_t)b->world : 1u;
     A.sub_tab = b->d_sub_tab.as<uint32_t>();
-    A.kept_ctr = ctr_d;
+    A.kept_ctr = b->d_ctr.as<unsigned long long>();
     A.nbuckets = NB1;
     A.bucket_base = (pass << (b->owner_bits + b->b1_bits)) | ((uint32_t)b->rank << b->b1_bits);
     A.rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
@@ -5531,8 +5578,9 @@ void phase_group(skm_build* b, uint32_t pass) {
     const uint32_t key_min = (uint32_t)std::max(b->tune.heavy_min, 2);
     PlanArgs P;
     P.in = b->d_ovf.as<OvfEntry>();
-    P.out = b->d_ovf2.as<OvfEntry>();
+    P.out = ovf2_d;
     P.ctr = ctr_d;
+    P.kept = b->d_ctr.as<unsigned long long>();
     P.nloc = nloc_d;
     P.run = run_d;
     P.plan = plan_d;
@@ -5557,7 +5605,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     S.fmean = b->d_ovf_fm.as<uint32_t>();
     // both parts append to one job list (own job / length counters of the overflow; the kept
     // counter stays shared); the chains start when both parts are grouped
-    A2.ovf = b->d_ovf2.as<OvfEntry>();
+    A2.ovf = ovf2_d;
     A2.ctr = ctr_d + 8;
     A2.jobs = b->d_jobs2.as<Job>();
     A2.lens = b->d_lens.as<uint32_t>();
@@ -5607,7 +5655,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     SKM_LAUNCH(b, k_ovf_split, dim3((uint32_t)std::max(1, b->tune.split_grid)), dim3(BP_THREADS), 0, st2, A2, S, H, key_min, plan_d);
     SKM_HIP(hipEventRecord(b->ev_split, st2));
     SKM_HIP(hipStreamWaitEvent(st3, b->ev_split, 0));
-    SKM_LAUNCH(b, k_heavy, dim3(HEAVY_GRID), dim3(HEAVY_WG), 0, st2, A2, H);
+    SKM_LAUNCH(b, k_heavy, dim3((uint32_t)std::max(1, b->tune.heavy_grid)), dim3(HEAVY_WG), 0, st2, A2, H);
     SKM_HIP(hipGetLastError());
     if (H.giant_min) {
         SKM_HIP(hipEventRecord(b->gev_ready[gs], st2));
@@ -5664,6 +5712,21 @@ void phase_group(skm_build* b, uint32_t pass) {
     SKM_HIP(hipEventRecord(b->ev_o3[1], st3));
     launch_chains(b, st, A.jobs, ctr_d + 3, b->jobs_cap, b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
                   reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, (uint32_t)b->tune.main_long_class);
+    if (b->overlap) {
+        // the pass ends on the main stream here; its overflow path and accounting finish on
+        // stream 2 beside the next pass, whose staging into this set waits for ev_ovf_done
+        SKM_HIP(hipEventRecord(b->ev_main_done[ks], st));
+        SKM_HIP(hipEventRecord(b->ev[6], st));
+        SKM_HIP(hipStreamWaitEvent(st2, b->ev_o3[1], 0));
+        SKM_HIP(hipStreamWaitEvent(st2, b->ev_main_done[ks], 0));
+        SKM_LAUNCH(b, k_pass_account, dim3(1), dim3(1), 0, st2, ctr_d, run_d, b->jobs_cap, b->jobs2_cap, b->big_cap,
+                   b->lens_cap);
+        SKM_HIP(hipGetLastError());
+        SKM_HIP(hipEventRecord(b->ev_ovf_done[ks], st2));
+        b->ovf_pending[ks] = true;
+        SKM_HIP(hipEventRecord(b->ev[7], st));
+        return;
+    }
     SKM_HIP(hipStreamWaitEvent(st, b->ev_o[2], 0));
     SKM_HIP(hipStreamWaitEvent(st, b->ev_o3[1], 0));
     SKM_HIP(hipEventRecord(b->ev[6], st));
@@ -5672,6 +5735,15 @@ void phase_group(skm_build* b, uint32_t pass) {
                        b->lens_cap);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[7], st));
+}
+
+// overlap: the main stream waits for every pass's overflow path still in flight
+void drain_overflow(skm_build* b) {
+    for (int k = 0; k < 2; ++k)
+        if (b->ovf_pending[k]) {
+            SKM_HIP(hipStreamWaitEvent(b->stream, b->ev_ovf_done[k], 0));
+            b->ovf_pending[k] = false;
+        }
 }
 
 // Work buffers whose size depends on the data (the overflow scratch, the split path, the chain
@@ -5694,7 +5766,8 @@ void alloc_caps(skm_build* b) {
     b->d_hv_s0.ensure(4 * Sp);
     b->d_hv_s1.ensure(4 * Sp);
     b->d_ovf2.ensure(sizeof(OvfEntry) * std::max<uint64_t>(b->ovf_cap, 1));
-    b->d_plan.ensure(4 * PLAN_SLOTS);
+    if (b->overlap) b->d_ovf2b.ensure(sizeof(OvfEntry) * std::max<uint64_t>(b->ovf_cap, 1));
+    b->d_plan.ensure(4 * PLAN_SLOTS * 2);
     b->d_run.ensure(8 * RUN_SLOTS);
     b->d_sub_tab.ensure(4ull * (1u << b->b1_bits) * SUB_TAB);
     b->d_stamps.ensure(32 * 8);
@@ -5737,7 +5810,8 @@ void begin_run(skm_build* b) {
     hipStream_t st = b->stream;
     alloc_caps(b);
     SKM_HIP(hipEventRecord(b->ev_start, st));
-    SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 256, st));
+    SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 3 * 256, st));
+    b->ovf_pending[0] = b->ovf_pending[1] = false;
     SKM_HIP(hipMemsetAsync(b->d_run.p, 0, 8 * RUN_SLOTS, st));
     SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->n_total ? b->n_total : 1, st));
     b->d_gstat.ensure(16);
@@ -5829,6 +5903,7 @@ void phase_stats(skm_build* b) {
     hipStream_t st = b->stream;
     const uint32_t F = b->opts.n_functions;
     SKM_HIP(hipEventRecord(b->ev_tail[0], st));  // the last pass is issued: the tail starts here
+    drain_overflow(b);
     if (b->pass_bits) {  // the long chains of every pass (the last batch on the chain stream)
         flush_long_chains(b, 16);
         for (int k = 0; k <= skm_build::GSLOTS; ++k) {
@@ -5933,7 +6008,10 @@ void run_once(const Ranks& bs) {
             // overlap the second half); the last batch runs after the last pass (phase_stats)
             const uint32_t nb = std::min<uint32_t>(P >= 4 ? (uint32_t)std::max(1, b->tune.chain_batches) : 1u, 16u);
             const uint32_t per = std::max<uint32_t>(1u, P / nb);
-            if (nb > 1 && (pass + 1) % per == 0 && pass + 1 < P) flush_long_chains(b, (int)((pass + 1) / per - 1));
+            if (nb > 1 && (pass + 1) % per == 0 && pass + 1 < P) {
+                drain_overflow(b);  // the snapshot takes every stash issued so far, complete
+                flush_long_chains(b, (int)((pass + 1) / per - 1));
+            }
         }
     }
     for (auto* b : bs) phase_stats(b);
@@ -6028,6 +6106,10 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     }
     for (auto& e : b->chain_ev) SKM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_part, hipEventDisableTiming));
+    for (int k = 0; k < 2; ++k) {
+        SKM_HIP(hipEventCreateWithFlags(&b->ev_ovf_done[k], hipEventDisableTiming));
+        SKM_HIP(hipEventCreateWithFlags(&b->ev_main_done[k], hipEventDisableTiming));
+    }
     for (auto& e : b->ev_tail) SKM_HIP(hipEventCreate(&e));
     for (int i = 0; i < 2; ++i) {
         SKM_HIP(hipHostMalloc(reinterpret_cast<void**>(&b->st_pin[i]), STAGE_BYTES, hipHostMallocDefault));
@@ -6330,7 +6412,9 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "select_tile" ? &t.select_tile
                : n == "partition_round" ? &t.partition_round
                : n == "flag_check" ? &t.flag_check
-               : n == "serial_overflow" ? &t.serial_overflow : nullptr;
+               : n == "serial_overflow" ? &t.serial_overflow
+               : n == "overlap" ? &t.overlap
+               : n == "heavy_grid" ? &t.heavy_grid : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")
@@ -6767,6 +6851,10 @@ void skm_build_destroy(skm_build* b) {
             if (e) (void)hipEventDestroy(e);
     }
     if (b->ev_part) (void)hipEventDestroy(b->ev_part);
+    for (int k = 0; k < 2; ++k) {
+        if (b->ev_ovf_done[k]) (void)hipEventDestroy(b->ev_ovf_done[k]);
+        if (b->ev_main_done[k]) (void)hipEventDestroy(b->ev_main_done[k]);
+    }
     for (auto& e : b->ev_tail)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : b->kt_pool) (void)hipEventDestroy(e);
