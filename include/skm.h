@@ -197,7 +197,9 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   the stashed long-job list), "route_heavy_min" (one GPU, >= 4 key-range passes: k-mers with at
  *   least this many occurrences -- estimated at prepare from a count-min sketch of 1/64 of the
  *   windows -- are grouped in the first half of the passes, so their long P^2 chains run beside
- *   the later passes instead of after the last one; 65536; 0 = off), "stage_round" (key-range
+ *   the later passes instead of after the last one; 65536; 0 = off), "route_vacate" (the last
+ *   this many passes hold no routed heavy key, whose keys are spread over the others by hash;
+ *   0 = the second half, mapped to pass - P/2), "stage_round" (key-range
  *   passes: 1 = the staged position scatter in half rounds of 2048 elements, four workgroups
  *   per CU, the default; 0 = rounds of 4096), "select_tile" (key-range passes: the pass
  *   selection's id loads per thread per tile, 1 = two (default), 0 = one), "partition_round"

@@ -1553,7 +1553,8 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
                                                   int owner_bits, uint8_t* __restrict__ ids,
                                                   unsigned long long* __restrict__ counts,
                                                   const uint32_t* __restrict__ bloom, uint32_t ncnt,
-                                                  uint32_t* __restrict__ rows = nullptr, uint64_t span = 0) {
+                                                  uint32_t* __restrict__ rows = nullptr, uint64_t span = 0,
+                                                  uint32_t vac = 0) {
     extern __shared__ uint32_t s_dyn[];
     uint32_t* s_cnt = s_dyn;
     uint32_t* s_bloom = s_dyn + ncnt;  // (1 << BLOOM_BITS) / 32 words when routing
@@ -1565,6 +1566,9 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
         for (uint32_t w = threadIdx.x; w < (1u << BLOOM_BITS) / 32u; w += blockDim.x) s_bloom[w] = bloom[w];
     __syncthreads();
     const uint32_t half = pass_bits >= 1 ? 1u << (pass_bits - 1) : 0u;
+    // routing vacates the last R passes: R = half (vac 0) maps pass p to p - P/2; any other R
+    // spreads the heavy keys of the last R passes over the first P - R by 16 hash bits
+    const uint32_t R = vac ? min(vac, (1u << pass_bits) - 1u) : half, keep = (1u << pass_bits) - R;
     const uint64_t nchunk = (rp + 15) >> 4;
     const uint64_t c0 = rows ? ((uint64_t)blockIdx.x * span >> 4) + threadIdx.x : (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t cend = rows ? min(nchunk, ((uint64_t)blockIdx.x + 1) * span >> 4) : nchunk;
@@ -1597,7 +1601,8 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
                     if (counts) atomicAdd(&s_cnt[(uint32_t)(h >> (KEY_BITS - 6))], 1u);
                 } else {
                     id = pass_bits ? (uint32_t)(h >> (KEY_BITS - pass_bits)) : 0u;
-                    if (route && id >= half && bloom_has(s_bloom, h)) id -= half;
+                    if (route && id >= keep && bloom_has(s_bloom, h))
+                        id = R == half ? id - half : (uint32_t)(((uint32_t)(h & 0xFFFFu) * keep) >> 16);
                     if (tally) {
                         const uint32_t own = (uint32_t)(h >> (KEY_BITS - pass_bits - owner_bits)) & ((1u << owner_bits) - 1u);
                         atomicAdd(&s_cnt[(id << owner_bits) | own], 1u);
@@ -4298,6 +4303,7 @@ struct Tune {
     int chain_batches = 4;           // key-range passes: stashed long chains leave in this many batches
     int chain_streams = 1;           //   over this many streams (1..4)
     int poison_jobs = 0;             // tests: every slot of the run's long-job list starts as a canary job
+    int route_vacate = 0;            // routing: the last this many passes hold no heavy key (0: half)
     int route_heavy_min = 1 << 16;   // key-range passes: k-mers of >= this many occurrences are routed into
                                      //   the first half of the passes (0: off; k_pass_ids)
     int overlap = 0;                 // key-range passes, one GPU: pipelined passes (a second element set)
@@ -4984,19 +4990,21 @@ void size_passes(skm_build* b, int forced_pb = -1) {
                            cms.as<uint32_t>(), 0u, nullptr);
         hipLaunchKernelGGL(k_route_sketch, dim3(2048), dim3(256), 0, b->stream, b->d_res.as<uint8_t>(), b->rp,
                            cms.as<uint32_t>(), thresh, b->d_bloom.as<uint32_t>());
-        uint64_t natural_late = 0;  // occurrences of the second half before routing
-        for (int p = 1 << (pb - 1); p < (1 << pb); ++p)
+        // the vacated passes: the second half, or the last route_vacate
+        const int R = b->tune.route_vacate > 0 ? std::min(b->tune.route_vacate, (1 << pb) - 1) : 1 << (pb - 1);
+        uint64_t natural_late = 0;  // occurrences of the vacated passes before routing
+        for (int p = (1 << pb) - R; p < (1 << pb); ++p)
             for (int i = 0; i < (64 >> pb); ++i) natural_late += cnt[p * (64 >> pb) + i];
         SKM_HIP(hipMemsetAsync(d_cnt.p, 0, 8 * 64, b->stream));
         hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 4u * 64 + (1u << BLOOM_BITS) / 8, b->stream,
                            b->d_res.as<uint8_t>(), b->rp, pb, 0, nullptr, d_cnt.as<unsigned long long>(),
-                           b->d_bloom.as<uint32_t>(), 64u);
+                           b->d_bloom.as<uint32_t>(), 64u, nullptr, 0, (uint32_t)std::max(0, b->tune.route_vacate));
         SKM_HIP(hipGetLastError());
         SKM_HIP(hipMemcpyAsync(cnt, d_cnt.p, sizeof(cnt), hipMemcpyDeviceToHost, b->stream));
         SKM_HIP(hipStreamSynchronize(b->stream));
         uint64_t m = 0, late = 0;
         for (int p = 0; p < (1 << pb); ++p) m = std::max<uint64_t>(m, cnt[p]);
-        for (int p = 1 << (pb - 1); p < (1 << pb); ++p) late += cnt[p];
+        for (int p = (1 << pb) - R; p < (1 << pb); ++p) late += cnt[p];
         b->pass_max = m;
         b->routed = natural_late - late;
         b->route = true;
@@ -5824,7 +5832,8 @@ void begin_run(skm_build* b) {
         const uint32_t P = 1u << b->pass_bits;
         SKM_LAUNCH(b, k_pass_ids, dim3(SEL_WG), dim3(256), 4u * P + (b->route ? (1u << BLOOM_BITS) / 8 : 0u), st,
                    b->d_res.as<uint8_t>(), b->rp, b->pass_bits, 0, b->d_ids.as<uint8_t>(), nullptr,
-                   b->route ? b->d_bloom.as<uint32_t>() : nullptr, P, b->d_selrows.as<uint32_t>(), b->sel_span);
+                   b->route ? b->d_bloom.as<uint32_t>() : nullptr, P, b->d_selrows.as<uint32_t>(), b->sel_span,
+                   (uint32_t)std::max(0, b->tune.route_vacate));
         SKM_LAUNCH(b, k_sel_scan, dim3(P), dim3(1024), 0, st, b->d_selrows.as<uint32_t>(), SEL_WG, P,
                    b->d_seloff.as<uint64_t>(), b->d_npos.as<unsigned long long>(), b->pass_max,
                    b->d_run.as<unsigned long long>());
@@ -6414,7 +6423,8 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "flag_check" ? &t.flag_check
                : n == "serial_overflow" ? &t.serial_overflow
                : n == "overlap" ? &t.overlap
-               : n == "heavy_grid" ? &t.heavy_grid : nullptr;
+               : n == "heavy_grid" ? &t.heavy_grid
+               : n == "route_vacate" ? &t.route_vacate : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")

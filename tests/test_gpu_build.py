@@ -119,8 +119,8 @@ def test_key_range_passes(skm, gpu, passes, long_class, opts):
     assert c1["overflow_subbuckets"] > 0 and c1["grouped"] == oracle_ref.count_windows(l, f) - _invalid(r, o, l, f)
 
 
-@pytest.mark.parametrize("passes,route_min", [(4, 256), (16, 64), (64, 1024)])
-def test_heavy_key_routing(skm, gpu, passes, route_min):
+@pytest.mark.parametrize("passes,route_min,vacate", [(4, 256, 0), (16, 64, 0), (64, 1024, 0), (16, 64, 4), (16, 64, 1)])
+def test_heavy_key_routing(skm, gpu, passes, route_min, vacate):
     """Heavy-key routing (route_heavy_min): the k-mers whose sampled occurrence estimate reaches the
     threshold are grouped in the first half of the key-range passes, their elements carrying
     (natural pass ^ routed pass) above the rem bits so the key decodes back -- the kept set is the
@@ -131,6 +131,7 @@ def test_heavy_key_routing(skm, gpu, passes, route_min):
     b = skm.SignatureBuilder(len(funcs))
     b.set_option("key_range_passes", passes)
     b.set_option("route_heavy_min", route_min)
+    b.set_option("route_vacate", vacate)  # 0: the second half; else the last `vacate` passes, spread
     b.set_option("main_long_class", 8)
     b.set_option("overflow_long_class", 8)
     b.add_batch(r, o, l, f, i)
