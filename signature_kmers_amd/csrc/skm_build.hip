@@ -460,6 +460,22 @@ __device__ __forceinline__ void stats_small(GRes& r, uint32_t x0, uint32_t x1, u
 }
 
 // Thread-level group of c <= N members starting at a.
+// A sequence's signature flag (process_kmer_set's seqs_with_a_signature.insert,
+// signature_build.tcc:269).  Bit 0 of the pointer selects the form (option flag_bits): a byte per
+// sequence, stored; or a bit per sequence, read first and set by a device-scope atomicOr only while
+// it reads clear (most sequences are flagged by their first kept k-mer, later marks only read; a
+// stale read costs one redundant atomic, never a lost flag).  k_flags_from_bits expands the bits.
+__device__ __forceinline__ void mark_seq(uint8_t* f, uint32_t s) {
+    const uintptr_t p = reinterpret_cast<uintptr_t>(f);
+    if (p & 1u) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(p & ~(uintptr_t)1) + (s >> 5);
+        const uint32_t m = 1u << (s & 31u);
+        if (!(*w & m)) atomicOr(w, m);
+    } else {
+        f[s] = 1;
+    }
+}
+
 template <int N, class V>
 __device__ GRes group_thread(const V& v, uint64_t a, uint32_t c, const uint32_t* __restrict__ glen,
                              uint8_t* __restrict__ flags) {
@@ -509,7 +525,7 @@ __device__ GRes group_thread(const V& v, uint64_t a, uint32_t c, const uint32_t*
     for (uint32_t t = 0; t < c; ++t) {
         const uint64_t lo = v.lov(a + t);
         const uint32_t s = (uint32_t)(lo >> 36);
-        flags[s] = 1;
+        if (flags) mark_seq(flags, s);
         if (t >= rb && t < rb + best_c) {
             const uint32_t len = glen[s];
             sum += len;
@@ -592,7 +608,7 @@ __device__ GRes group_wave(const V& v, uint64_t a, uint32_t c, const uint32_t* _
     uint32_t sum = 0;
     for (uint32_t t = lane; t < c; t += 64) {
         const uint32_t s = (uint32_t)(v.lov(a + t) >> 36);
-        flags[s] = 1;
+        if (flags) mark_seq(flags, s);
         if (t >= rb && t < rb + best_c) sum += glen[s];
     }
     sum = wave_sum(sum);
@@ -687,7 +703,7 @@ __device__ bool group_block(const V& v, uint64_t a, uint32_t c, const uint32_t* 
     uint32_t sum = 0;
     for (uint32_t t = tid; t < c; t += nt) {
         const uint32_t s = (uint32_t)(v.lov(a + t) >> 36);
-        flags[s] = 1;
+        if (flags) mark_seq(flags, s);
         if (t >= rb && t < rb + best_c) sum += glen[s];
     }
     sum = wg_sum(sum, s_wave);
@@ -1275,7 +1291,8 @@ __global__ __launch_bounds__(128) void k_chain_long(const Job* __restrict__ jobs
                                                     const uint32_t* __restrict__ recs32,
                                                     const uint32_t* __restrict__ tmp32,
                                                     const uint32_t* __restrict__ big32,
-                                                    skm_stored_kmer_data* __restrict__ out, int prio) {
+                                                    skm_stored_kmer_data* __restrict__ out, int prio,
+                                                    uint32_t min_n = 0) {
     const uint64_t lo = lo_p ? (uint64_t)*lo_p : 0ull, hi = *hi_p;
     if (lo + blockIdx.x >= hi) return;
     if (prio == 1) __builtin_amdgcn_s_setprio(1);
@@ -1283,6 +1300,7 @@ __global__ __launch_bounds__(128) void k_chain_long(const Job* __restrict__ jobs
     if (prio >= 3) __builtin_amdgcn_s_setprio(3);
     for (uint64_t q = lo + blockIdx.x; q < hi; q += gridDim.x) {
         const Job jb = jobs[q];
+        if (jb.n < min_n) continue;  // k_chains' (one lane each)
         const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
         // lens == nullptr: stashed jobs, lens_off is the samples' device address
         const uint32_t* x =
@@ -1325,7 +1343,7 @@ __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, co
                                                 const unsigned long long* hi_p, uint64_t cap,
                                                 const uint32_t* __restrict__ lens, const uint32_t* __restrict__ recs32,
                                                 const uint32_t* __restrict__ tmp32, const uint32_t* __restrict__ big32,
-                                                skm_stored_kmer_data* __restrict__ out) {
+                                                skm_stored_kmer_data* __restrict__ out, uint32_t max_n = 0) {
     // wave pairs walk blocks of 64 jobs (grid may be smaller than the job count: a capped grid
     // keeps few waves resident beside a concurrent kernel, longest jobs first)
     const uint64_t lo = lo_p ? (uint64_t)*lo_p : 0ull;
@@ -1340,9 +1358,13 @@ __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, co
         if (j >= njobs) break;
         const Job jb = jobs[j];
         const uint64_t sel = jb.lens_off >> LENS_SEL_SHIFT;
-        const uint32_t* x = (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
-                            (jb.lens_off & LENS_OFF_MASK);
+        // lens == nullptr: stashed long jobs, lens_off is the samples' device address
+        const uint32_t* x =
+            !lens && sel == 0 ? reinterpret_cast<const uint32_t*>(jb.lens_off)
+                              : (sel == LENS_IN_RECS ? recs32 : sel == LENS_IN_TMP ? tmp32 : sel == LENS_IN_BIG ? big32 : lens) +
+                                    (jb.lens_off & LENS_OFF_MASK);
         const uint32_t n = jb.n;
+        if (max_n && n >= max_n) continue;  // k_chain_long's (a wave pair each)
         SigStats st;
         st.init();
         if (var_wave)
@@ -2374,7 +2396,7 @@ __device__ __forceinline__ void seg_groups(const SubLds& L, uint32_t q0, uint32_
     const uint32_t s = (uint32_t)(key >> ELEM_I_BITS) & ((1u << ELEM_S_BITS) - 1u);
     const uint32_t fl = (A.flag_check && real) ? A.flags[s] : 0u;
     const uint32_t len = (pay & 1u) ? A.glen[s] : len16;
-    if (kept && real && fl == 0) A.flags[s] = 1;
+    if (kept && real && fl == 0 && A.flags) mark_seq(A.flags, s);
     const uint32_t x0 = (uint32_t)__shfl((int)len, (int)(rs + cbest - 1), 64);  // first visited
     const uint32_t x1 = (uint32_t)__shfl((int)len, (int)rs, 64);                // second when cbest == 2
     if (kept && inrun && cbest >= 3) L.lens32[2 * a + (rs + cbest - 1 - lane)] = len;  // visit order
@@ -2484,7 +2506,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
                 v += (cnt << 13) | 1u;
             } else if (j < n && cnt == 1) {  // group of one: always kept (1 >= 0.8), median 0, var 0
                 const uint64_t H = L.hi[j], Lo = L.lo[j];
-                if (!A.flag_check || A.flags[Lo >> 36] == 0) A.flags[Lo >> 36] = 1;
+                if (A.flags && (!A.flag_check || A.flags[Lo >> 36] == 0)) mark_seq(A.flags, (uint32_t)(Lo >> 36));
                 L.hi[j] = kept_hi(key_h43(hprefix, (H >> 16) & REM_MASK, A.rem_bits, A.pshift), (uint32_t)(Lo & 0xFFFFu));
                 L.lo[j] = kept_lo((uint32_t)(H & 0xFFFFu), d2u16((double)(uint16_t)(H >> 48) / 1.0), 0, 0);
                 L.rank[j] = 0xFFFFu;  // singleton marker
@@ -2867,7 +2889,7 @@ __device__ __forceinline__ void big_group(const BigArgs& B, uint64_t g, uint64_t
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         if (fo[e] != 0xFFFFFFFFu) {
-            B.flags[(uint32_t)(ky[e] >> (16 + ELEM_I_BITS))] = 1;
+            if (B.flags) mark_seq(B.flags, (uint32_t)(ky[e] >> (16 + ELEM_I_BITS)));
             if (p[e]) sum += (uint32_t)mlen[ky[e] & 0xFFFFu];  // L2-warm (read above)
         }
         if (!p[e]) ky[e] = ~0ull;  // sort key: best-function members only
@@ -3510,6 +3532,7 @@ struct HeavyArgs {
     // giant chains (>= 2^giant_class samples): samples and jobs in this pass's slot buffers, run
     // by k_chain_dyn on a chain stream as soon as k_heavy ends (the pass's own lens buffer is
     // reused by the next pass; the slot's is not until its chains are done)
+    uint32_t nosort;              // diagnostics (option diag & 2): the samples in member order
     uint32_t giant_min;           // 0: off
     uint32_t* gsamples;
     Job* gjobs;
@@ -3865,7 +3888,7 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
                 const uint32_t s = (uint32_t)(l[u] >> 36);
                 const bool best = f[u] == best_f;
                 if (v) {
-                    if (!best) A.flags[s] = 1;  // the best members' flags go out in sorted order below
+                    if (!best && A.flags) mark_seq(A.flags, s);  // the best members' flags go out in sorted order below
                     atomicAdd(&s_hist[(uint32_t)(l[u] >> 8) & 255u], 1u);
                 }
                 if (best) {
@@ -3918,7 +3941,7 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
         // ---- samples in visit order: sequence indices descending ----
         int bits = 0;
         while (bits < 32 && (smax >> bits)) bits += RB;
-        const uint32_t* sorted = wg_radix_sort_u32(sa, sb, cb, bits, s_hist, s_wc, s_run, tag);
+        const uint32_t* sorted = H.nosort ? sa : wg_radix_sort_u32(sa, sb, cb, bits, s_hist, s_wc, s_run, tag);
         __syncthreads();
         if (tid == 0) {
             s_sel[0] = (uint32_t)atomicAdd(A.kept_ctr, 1ull);
@@ -3960,7 +3983,7 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
                     // monotone sequence indices: the length gathers and the signature flags of the
                     // best members touch neighbouring lines instead of random ones
                     lens_out[(uint64_t)loff + t] = A.glen[sv[u]];
-                    A.flags[sv[u]] = 1;
+                    if (A.flags) mark_seq(A.flags, sv[u]);
                 }
             }
         }
@@ -4180,6 +4203,16 @@ __global__ void k_func_hist_seqs(const SeqMeta* __restrict__ meta, uint32_t nseq
             if (s_h[f]) atomicAdd(&swf[f], s_h[f]);
 }
 
+// option flag_bits: the per-sequence bytes from the run's flag bits (one word of 32 flags per thread)
+__global__ void k_flags_from_bits(const uint32_t* __restrict__ bits, uint32_t nseq, uint8_t* __restrict__ flags) {
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < (nseq + 31) / 32; w += gridDim.x * blockDim.x) {
+        const uint32_t v = bits[w];
+        const uint32_t n = min(32u, nseq - 32 * w);
+        uint8_t* o = flags + 32 * (uint64_t)w;
+        for (uint32_t t = 0; t < n; ++t) o[t] = (uint8_t)((v >> t) & 1u);
+    }
+}
+
 __global__ void k_count_flags(const uint8_t* __restrict__ flags, uint32_t nseq, unsigned long long* __restrict__ out) {
     uint32_t local = 0;
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseq; s += gridDim.x * blockDim.x) local += flags[s] ? 1u : 0u;
@@ -4317,6 +4350,16 @@ struct Tune {
                                      //   loads per thread, the next tile's loads ahead of this tile's work
     int stage_round = 1;             // key-range passes: 1 = the staged position scatter in half rounds
                                      //   (2048 elements, four workgroups per CU); 0 = full rounds
+    // key-range passes: stashed long chains below this many samples run one lane each (k_chains,
+    // 64 chains per wave) instead of on a wave pair, except the batch after the last pass (0: off).
+    // Measured at C3: 1.91 -> 1.70-1.73 s/step -- the wave pairs held ~4 k waves resident for the
+    // whole batch, and a k_bucket_process workgroup needs half of a CU's registers and LDS
+    int lane_long = 1 << 20;
+    int lane_grid = 256;             //   their k_chains grid
+    int flag_bits = 0;               // signature flags as bits, read before an atomic set (mark_seq)
+    int diag = 0;                    // diagnostics only (wrong results): 1 = no signature flag stores,
+                                     //   2 = k_heavy without its sequence-index sort, 4 = no chain kernels,
+                                     //   8 = no stashed long chains, 16 = no per-pass k_chains
 };
 
 }  // namespace skm
@@ -4379,6 +4422,7 @@ struct skm_build {
     DevBuf d_hist, d_offs, d_partial, d_rbbase, d_bstart32, d_bstart, d_owner_start;
     DevBuf d_recs_hi, d_recs_lo, d_tmp_hi, d_tmp_lo;
     DevBuf d_cur0, d_cur1, d_slices;   // staged scatter cursors
+    DevBuf d_flagbits;
     DevBuf d_keys, d_data, d_ctr, d_flags, d_dfunc, d_swf, d_ovf, d_ovf_hi, d_ovf_lo, d_ovf_heads, d_ovf_job, d_ovf_fm;
     DevBuf d_jobs, d_lens, d_stamps, d_big_desc, d_big_out;
     uint64_t big_cap = 0, n_big = 0, big_kept = 0;
@@ -4476,6 +4520,10 @@ struct skm_build {
     // run in batches on a fourth stream (mid-run and at the end), overlapping the later passes
     hipStream_t chain_st = nullptr;
     hipEvent_t chain_ev[3] = {};
+    // stashed long chains below tune.lane_long samples: one lane each (k_chains) on their own stream
+    hipStream_t lane_st = nullptr;
+    hipEvent_t lane_ev = nullptr;
+    bool lane_used = false;
     // giant chains of k_heavy: rotating slots (stream, sample / job buffers, counters, events)
     static constexpr int GSLOTS = 3;  // + st, st2, st3, chain_st, stx: 8 streams
     hipStream_t gst[GSLOTS] = {};
@@ -5184,6 +5232,7 @@ void prepare(const Ranks& bs) {
         alloc_caps(b);
         size_arena(b);
         b->d_flags.ensure(std::max<uint64_t>(b->n_total, 1));
+        b->d_flagbits.ensure(4 * ((b->n_total + 31) / 32 + 1));
         // pipelined passes when the second element buffer set fits beside everything else with a
         // tenth of the memory to spare (the data-sized buffers may still grow on a redo)
         b->overlap = false;
@@ -5484,6 +5533,7 @@ void launch_chains(skm_build* b, hipStream_t st, const Job* jobs, const unsigned
     // k_job_scan leaves the long jobs' count after the offsets; they lead the sorted order
     const uint64_t* nlong_d = cs.offs.as<uint64_t>() + (uint64_t)JOB_NWG * JOB_CLASSES;
     const auto* nlong_u = reinterpret_cast<const unsigned long long*>(nlong_d);
+    const bool run_chains = !(tn.diag & 4) && !(tn.diag & 16);
     if (b->pass_bits == 0) {
         // one pass: the long chains start on st as soon as their jobs are sorted
         const uint32_t lds = (uint32_t)tn.chain_lds_kb * 1024u;
@@ -5493,8 +5543,9 @@ void launch_chains(skm_build* b, hipStream_t st, const Job* jobs, const unsigned
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             attr = true;
         }
-        SKM_LAUNCH(b, k_chain_long, dim3(LONG_GRID), dim3(128), lds, st, cs.sorted.as<Job>(), nullptr, nlong_u,
-                           lens, recs32, tmp32, big32, out, tn.chain_prio);
+        if (run_chains)
+            SKM_LAUNCH(b, k_chain_long, dim3(LONG_GRID), dim3(128), lds, st, cs.sorted.as<Job>(), nullptr, nlong_u,
+                       lens, recs32, tmp32, big32, out, tn.chain_prio);
     } else {
         SKM_LAUNCH(b, k_long_plan, dim3(1), dim3(1024), 0, st, cs.sorted.as<Job>(), nlong_d,
                            cs.long_off.as<uint64_t>(), b->d_run.as<unsigned long long>(), b->long_cap,
@@ -5509,8 +5560,9 @@ void launch_chains(skm_build* b, hipStream_t st, const Job* jobs, const unsigned
         SKM_HIP(hipStreamWaitEvent(st_short, ev_sorted, 0));
         ss = st_short;
     }
-    SKM_LAUNCH(b, k_chains, dim3(max_wgs ? max_wgs : (uint32_t)std::max(1, tn.chain_grid)), dim3(256), 0, ss, cs.sorted.as<Job>(), nlong_u,
-                       nj_d, cap, lens, recs32, tmp32, big32, out);
+    if (run_chains)
+        SKM_LAUNCH(b, k_chains, dim3(max_wgs ? max_wgs : (uint32_t)std::max(1, tn.chain_grid)), dim3(256), 0, ss,
+                   cs.sorted.as<Job>(), nlong_u, nj_d, cap, lens, recs32, tmp32, big32, out);
     SKM_HIP(hipGetLastError());
 }
 
@@ -5547,8 +5599,10 @@ void phase_group(skm_build* b, uint32_t pass) {
     A.rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
     A.pshift = KEY_BITS - b->pass_bits;
     A.glen = b->d_glen.as<uint32_t>();
-    A.flags = b->d_flags.as<uint8_t>();
-    A.flag_check = b->tune.flag_check;
+    A.flags = (b->tune.diag & 1) ? nullptr
+              : b->tune.flag_bits ? reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(b->d_flagbits.p) | 1u)
+                                  : b->d_flags.as<uint8_t>();
+    A.flag_check = b->tune.flag_bits ? 0 : b->tune.flag_check;  // reads the byte form only
     A.ctr = ctr_d;
     A.out_keys = b->d_keys.as<uint64_t>();
     A.out_data = b->d_data.as<skm_stored_kmer_data>();
@@ -5631,6 +5685,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     H.lo = b->d_hv_lo.as<uint64_t>();
     H.s0 = b->d_hv_s0.as<uint32_t>();
     H.s1 = b->d_hv_s1.as<uint32_t>();
+    H.nosort = (b->tune.diag & 2) ? 1u : 0u;
     // giant chains: samples and jobs in this pass's own buffers, run on a rotating chain stream
     // (only in the last giant_passes passes: earlier passes' long chains overlap the later passes
     // from the stash batches anyway; the last pass's would form the tail)
@@ -5822,6 +5877,7 @@ void begin_run(skm_build* b) {
     b->ovf_pending[0] = b->ovf_pending[1] = false;
     SKM_HIP(hipMemsetAsync(b->d_run.p, 0, 8 * RUN_SLOTS, st));
     SKM_HIP(hipMemsetAsync(b->d_flags.p, 0, b->n_total ? b->n_total : 1, st));
+    if (b->tune.flag_bits) SKM_HIP(hipMemsetAsync(b->d_flagbits.p, 0, 4 * ((b->n_total + 31) / 32 + 1), st));
     b->d_gstat.ensure(16);
     SKM_HIP(hipMemsetAsync(b->d_gstat.p, 0, 16, st));
     if (b->tune.poison_jobs && b->pass_bits && b->long_jobs_cap)
@@ -5902,8 +5958,21 @@ void flush_long_chains(skm_build* b, int slot) {
     hipStream_t cs = chain_stream(b, slot);
     SKM_HIP(hipStreamWaitEvent(cs, b->chain_ev[0], 0));
     b->chain_used[slot % std::max(1, std::min(b->tune.chain_streams, 1 + skm_build::GSLOTS))] = true;
-    SKM_LAUNCH(b, k_chain_long, dim3(LONG_GRID), dim3(128), 0, cs, b->d_long_jobs.as<Job>(), rng, rng + 1,
-                       nullptr, nullptr, nullptr, nullptr, b->d_data.as<skm_stored_kmer_data>(), b->tune.chain_prio);
+    // the batch's chains below lane_long samples one lane each (k_chains: 64 chains per wave, ~50x
+    // less wave time per sample than a wave pair, ~2.5x the latency), the rest on wave pairs; the
+    // last batch (slot 16, the tail after the last pass) all on wave pairs
+    const uint32_t lane_max = slot < 16 && b->tune.lane_long > 0 ? (uint32_t)b->tune.lane_long : 0u;
+    if (!(b->tune.diag & 4) && !(b->tune.diag & 8))
+        SKM_LAUNCH(b, k_chain_long, dim3(LONG_GRID), dim3(128), 0, cs, b->d_long_jobs.as<Job>(), rng, rng + 1,
+                   nullptr, nullptr, nullptr, nullptr, b->d_data.as<skm_stored_kmer_data>(), b->tune.chain_prio,
+                   lane_max);
+    if (lane_max && !(b->tune.diag & 4) && !(b->tune.diag & 8)) {
+        SKM_HIP(hipStreamWaitEvent(b->lane_st, b->chain_ev[0], 0));
+        SKM_LAUNCH(b, k_chains, dim3((uint32_t)std::max(1, b->tune.lane_grid)), dim3(256), 0, b->lane_st,
+                   b->d_long_jobs.as<Job>(), rng, rng + 1, b->long_jobs_cap, nullptr, nullptr, nullptr, nullptr,
+                   b->d_data.as<skm_stored_kmer_data>(), lane_max);
+        b->lane_used = true;
+    }
     SKM_HIP(hipGetLastError());
 }
 
@@ -5913,8 +5982,16 @@ void phase_stats(skm_build* b) {
     const uint32_t F = b->opts.n_functions;
     SKM_HIP(hipEventRecord(b->ev_tail[0], st));  // the last pass is issued: the tail starts here
     drain_overflow(b);
+    if (b->tune.flag_bits && b->n_total)
+        SKM_LAUNCH(b, k_flags_from_bits, dim3(1024), dim3(256), 0, st, b->d_flagbits.as<uint32_t>(),
+                   (uint32_t)b->n_total, b->d_flags.as<uint8_t>());
     if (b->pass_bits) {  // the long chains of every pass (the last batch on the chain stream)
         flush_long_chains(b, 16);
+        if (b->lane_used) {
+            SKM_HIP(hipEventRecord(b->lane_ev, b->lane_st));
+            SKM_HIP(hipStreamWaitEvent(st, b->lane_ev, 0));
+            b->lane_used = false;
+        }
         for (int k = 0; k <= skm_build::GSLOTS; ++k) {
             if (!b->chain_used[k]) continue;
             const hipStream_t cs = chain_stream(b, k);
@@ -6105,6 +6182,8 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     use_evset(b, 0);
     SKM_HIP(hipEventCreate(&b->ev_start));
     SKM_HIP(hipStreamCreateWithFlags(&b->chain_st, hipStreamNonBlocking));
+    SKM_HIP(hipStreamCreateWithFlags(&b->lane_st, hipStreamNonBlocking));
+    SKM_HIP(hipEventCreateWithFlags(&b->lane_ev, hipEventDisableTiming));
     SKM_HIP(hipStreamCreateWithFlags(&b->stx, hipStreamNonBlocking));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_pf_ready, hipEventDisableTiming));
     for (auto& e : b->ev_pf_done) SKM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -6421,6 +6500,10 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "select_tile" ? &t.select_tile
                : n == "partition_round" ? &t.partition_round
                : n == "flag_check" ? &t.flag_check
+               : n == "diag" ? &t.diag
+               : n == "flag_bits" ? &t.flag_bits
+               : n == "lane_long" ? &t.lane_long
+               : n == "lane_grid" ? &t.lane_grid
                : n == "serial_overflow" ? &t.serial_overflow
                : n == "overlap" ? &t.overlap
                : n == "heavy_grid" ? &t.heavy_grid
@@ -6894,6 +6977,11 @@ void skm_build_destroy(skm_build* b) {
         (void)hipStreamSynchronize(b->chain_st);
         (void)hipStreamDestroy(b->chain_st);
     }
+    if (b->lane_st) {
+        (void)hipStreamSynchronize(b->lane_st);
+        (void)hipStreamDestroy(b->lane_st);
+    }
+    if (b->lane_ev) (void)hipEventDestroy(b->lane_ev);
     for (auto& e : b->chain_ev)
         if (e) (void)hipEventDestroy(e);
     if (b->h_pin) (void)hipHostFree(b->h_pin);
