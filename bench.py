@@ -351,8 +351,11 @@ def _alg_bytes(kernel, c, res_bytes):
         "k_overflow": 16 * c["overflow_elements"],
         "k_ovf_split": 32 * c["overflow_elements"],
         "k_heavy": 16 * c["overflow_elements"],
-        "k_chain_long": 4 * c["long_samples"],             # 4 B per chain sample
-        "k_chains": 4 * c["chain_samples"],
+        # 4 B per chain sample.  The stashed long chains (key-range passes) run as
+        # k_chains_stash (one lane each) or k_chain_long (a wave pair each; the tail batch's longest)
+        "k_chain_long": 4 * c["long_samples"],
+        "k_chains_stash": 4 * c["long_samples"],
+        "k_chains": 4 * (c["chain_samples"] - (c["long_samples"] if c["passes"] > 1 else 0)),
         "k_kept_finalize": 36 * c["kept"],                 # 18 B per kept k-mer read + written
     }
     v = table.get(kernel)
@@ -417,6 +420,17 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
     pipe_alg = sums["res"] + 32 * sums["grouped"] + 18 * sums["kept"]
     pipe_gbs = pipe_alg / (t_max / steps) / 1e9
     top = sorted(ktab.items(), key=lambda kv: -kv[1][0])[:14]
+    # the main stream's dominant kernel beside it (the group-by; a background chain kernel can hold
+    # the most GPU time while its FP64 recurrences are latency-, not byte-bound)
+    mk = "k_bucket_process"
+    m_ms, m_n = ktab.get(mk, (0.0, 0))
+    m_alg = _alg_bytes(mk, ctrs, shard.n_residues + shard.n_seqs)
+    m_ach = m_alg / (m_ms * 1e-3) / 1e9 if m_alg and m_ms > 0 else None
+    main_stream = {"kernel": mk, "achieved": m_ach, "frac": m_ach / HBM_PEAK_GBS if m_ach else None,
+                   "alg_bytes_per_launch": None if m_alg is None else m_alg / max(1, m_n),
+                   "avg_launch_ms": m_ms / max(1, m_n), "launches_per_step": m_n,
+                   "traffic": (lambda t: None if t is None else t / max(1, m_n))(_pmc_traffic(mk, wl, shard.n_seqs)),
+                   "timing": "events around each launch in the untimed diagnostic run"}
     return {
         "value": windows_total * steps / t_max,
         "ms_per_step": 1000.0 * t_max / steps,
@@ -434,7 +448,8 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
                      "selection": "largest GPU time per step over every kernel launch of the run (event pairs "
                                   "around each launch in one untimed run); timed: events around this kernel's "
                                   "launches in the timed steps",
-                     "kernels_ms_per_step": {k: round(v[0], 2) for k, v in top}},
+                     "kernels_ms_per_step": {k: round(v[0], 2) for k, v in top},
+                     "main_stream": main_stream},
         "chain_tail_ms": phase.get("chain_tail"),
         "pipeline": {"alg_bytes": pipe_alg, "ms": 1000.0 * t_max / steps, "GBs": pipe_gbs,
                      "frac": pipe_gbs / HBM_PEAK_GBS / max(1, world), "phase_ms_rank0": phase},

@@ -4356,7 +4356,9 @@ struct Tune {
     // whole batch, and a k_bucket_process workgroup needs half of a CU's registers and LDS
     int lane_long = 1 << 20;
     int lane_grid = 256;             //   their k_chains grid
-    int flag_bits = 0;               // signature flags as bits, read before an atomic set (mark_seq)
+    int lane_tail = 1 << 12;         //   the last batch's threshold (its wave pairs are the tail's latency)
+    int flag_bits = 1;               // signature flags as bits, read before an atomic set (mark_seq);
+                                     //   0: a byte store per kept occurrence (C3: +58 ms/step)
     int diag = 0;                    // diagnostics only (wrong results): 1 = no signature flag stores,
                                      //   2 = k_heavy without its sequence-index sort, 4 = no chain kernels,
                                      //   8 = no stashed long chains, 16 = no per-pass k_chains
@@ -5959,16 +5961,17 @@ void flush_long_chains(skm_build* b, int slot) {
     SKM_HIP(hipStreamWaitEvent(cs, b->chain_ev[0], 0));
     b->chain_used[slot % std::max(1, std::min(b->tune.chain_streams, 1 + skm_build::GSLOTS))] = true;
     // the batch's chains below lane_long samples one lane each (k_chains: 64 chains per wave, ~50x
-    // less wave time per sample than a wave pair, ~2.5x the latency), the rest on wave pairs; the
-    // last batch (slot 16, the tail after the last pass) all on wave pairs
-    const uint32_t lane_max = slot < 16 && b->tune.lane_long > 0 ? (uint32_t)b->tune.lane_long : 0u;
+    // less wave time per sample than a wave pair, ~2.5x the latency), the rest on wave pairs; in
+    // the last batch (slot 16, the tail after the last pass) only those below lane_tail
+    const int lmax = slot < 16 ? b->tune.lane_long : std::min(b->tune.lane_long, b->tune.lane_tail);
+    const uint32_t lane_max = lmax > 0 ? (uint32_t)lmax : 0u;
     if (!(b->tune.diag & 4) && !(b->tune.diag & 8))
         SKM_LAUNCH(b, k_chain_long, dim3(LONG_GRID), dim3(128), 0, cs, b->d_long_jobs.as<Job>(), rng, rng + 1,
                    nullptr, nullptr, nullptr, nullptr, b->d_data.as<skm_stored_kmer_data>(), b->tune.chain_prio,
                    lane_max);
     if (lane_max && !(b->tune.diag & 4) && !(b->tune.diag & 8)) {
         SKM_HIP(hipStreamWaitEvent(b->lane_st, b->chain_ev[0], 0));
-        SKM_LAUNCH(b, k_chains, dim3((uint32_t)std::max(1, b->tune.lane_grid)), dim3(256), 0, b->lane_st,
+        SKM_LAUNCH_AS(b, "k_chains_stash", k_chains, dim3((uint32_t)std::max(1, b->tune.lane_grid)), dim3(256), 0, b->lane_st,
                    b->d_long_jobs.as<Job>(), rng, rng + 1, b->long_jobs_cap, nullptr, nullptr, nullptr, nullptr,
                    b->d_data.as<skm_stored_kmer_data>(), lane_max);
         b->lane_used = true;
@@ -6504,6 +6507,7 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "flag_bits" ? &t.flag_bits
                : n == "lane_long" ? &t.lane_long
                : n == "lane_grid" ? &t.lane_grid
+               : n == "lane_tail" ? &t.lane_tail
                : n == "serial_overflow" ? &t.serial_overflow
                : n == "overlap" ? &t.overlap
                : n == "heavy_grid" ? &t.heavy_grid

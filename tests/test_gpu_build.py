@@ -85,7 +85,7 @@ def test_overflow_inline_chains(skm, gpu, inline_min):
 
 @pytest.mark.parametrize("passes,long_class,opts", [(1, 6, {}), (2, 14, {}), (4, 8, {}), (64, 14, {}),
                                                    (4, 8, {"stage_round": 0}), (4, 8, {"partition_round": 1}),
-                                                   (4, 8, {"partition_round": 2}), (1, 6, {"flag_check": 1}),
+                                                   (4, 8, {"partition_round": 2}), (1, 6, {"flag_check": 1, "flag_bits": 0}), (4, 8, {"flag_bits": 0}),
                                                    (4, 8, {"serial_overflow": 1}), (4, 8, {"chain_cus": 32}),
                                                    (4, 8, {"side_cus": 64}),
                                                    (4, 8, {"overlap": 1}), (16, 8, {"overlap": 1}),
