@@ -4356,7 +4356,7 @@ struct Tune {
     // whole batch, and a k_bucket_process workgroup needs half of a CU's registers and LDS
     int lane_long = 1 << 20;
     int lane_grid = 256;             //   their k_chains grid
-    int lane_tail = 1 << 12;         //   the last batch's threshold (its wave pairs are the tail's latency)
+    int lane_tail = 1 << 16;         //   the last batch's threshold (its wave pairs are the tail's latency)
     int flag_bits = 1;               // signature flags as bits, read before an atomic set (mark_seq);
                                      //   0: a byte store per kept occurrence (C3: +58 ms/step)
     int diag = 0;                    // diagnostics only (wrong results): 1 = no signature flag stores,
