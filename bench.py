@@ -331,6 +331,16 @@ def main():
         dist.destroy_process_group()
 
 
+_ROOF_NOTES = {
+    "k_chains_stash": "background stream: the stashed long P^2 / variance chains, one lane each -- serial "
+                      "FP64 recurrences in the reference's reverse visit order (SURVEY A.4), so each launch "
+                      "lasts as long as its longest chain (~10^6 samples at ~0.6 us) at a few waves per CU; "
+                      "latency-bound, not byte-bound: main_stream is the step's byte-moving critical path",
+    "k_chains": "P^2 / variance chains (serial FP64 recurrences, one lane each): latency-bound",
+    "k_chain_long": "P^2 / variance chains on wave pairs (serial FP64 recurrences): latency-bound",
+}
+
+
 def _alg_bytes(kernel, c, res_bytes):
     """SURVEY 8(d) algorithmic bytes of one build kernel over one step (all its launches), from the
     run's counters; None for a kernel without a stated figure.  c = b.counters()."""
@@ -449,6 +459,7 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
                                   "around each launch in one untimed run); timed: events around this kernel's "
                                   "launches in the timed steps",
                      "kernels_ms_per_step": {k: round(v[0], 2) for k, v in top},
+                     "note": _ROOF_NOTES.get(dom),
                      "main_stream": main_stream},
         "chain_tail_ms": phase.get("chain_tail"),
         "pipeline": {"alg_bytes": pipe_alg, "ms": 1000.0 * t_max / steps, "GBs": pipe_gbs,
