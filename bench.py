@@ -31,14 +31,14 @@ import os
 import sys
 import time
 
-# libskm drives up to 9 streams per build (two overflow streams, stashed, per-lane and giant chain
+# libskm drives up to 12 streams per build (two overflow streams, stashed, per-lane and giant chain
 # streams);
 # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4), read at HIP init
 # (SKM_HW_QUEUES: an explicit count for A/B runs)
 if os.environ.get("SKM_HW_QUEUES"):
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ["SKM_HW_QUEUES"]
-elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 12:
-    os.environ["GPU_MAX_HW_QUEUES"] = "12"
+elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 import numpy as np
 

@@ -2202,6 +2202,7 @@ struct BucketArgs {
     int pshift;                // KEY_BITS - pass bits (key_h43)
     int flag_check;            // 1: a signature flag is stored only when it reads 0 (option flag_check)
     const uint32_t* skip;      // k_ovf_plan's verdict for the pass (nonzero: the run is being abandoned)
+    uint32_t sub_target;       // k_partition: target elements per level-2 sub-bucket (0: SUB_TARGET)
 };
 
 #define SKM_STAMP(i)                                                          \
@@ -3048,7 +3049,8 @@ __global__ __launch_bounds__(PT_THREADS, MINB) void k_partition(BucketArgs A) {
     }
     const uint64_t rem_mask = (1ull << A.rem_bits) - 1;
     int b2 = 0;
-    while (b2 < MAX_B2 && (n >> b2) > (uint64_t)SUB_TARGET) ++b2;
+    const uint64_t target = A.sub_target ? A.sub_target : (uint32_t)SUB_TARGET;
+    while (b2 < MAX_B2 && (n >> b2) > target) ++b2;
     const uint32_t nsub = 1u << b2;
     const int shift = A.rem_bits - b2;
     for (uint32_t d = threadIdx.x; d <= nsub; d += blockDim.x) s_cur[d] = 0;
@@ -4356,7 +4358,9 @@ struct Tune {
     // whole batch, and a k_bucket_process workgroup needs half of a CU's registers and LDS
     int lane_long = 1 << 20;
     int lane_grid = 256;             //   their k_chains grid
+    int lane_streams = 1;            //   the streams their batches rotate over (1..4)
     int lane_tail = 1 << 16;         //   the last batch's threshold (its wave pairs are the tail's latency)
+    int sub_target = 0;              // k_partition's target elements per level-2 sub-bucket (0: SUB_TARGET)
     int flag_bits = 1;               // signature flags as bits, read before an atomic set (mark_seq);
                                      //   0: a byte store per kept occurrence (C3: +58 ms/step)
     int diag = 0;                    // diagnostics only (wrong results): 1 = no signature flag stores,
@@ -4523,9 +4527,10 @@ struct skm_build {
     hipStream_t chain_st = nullptr;
     hipEvent_t chain_ev[3] = {};
     // stashed long chains below tune.lane_long samples: one lane each (k_chains) on their own stream
-    hipStream_t lane_st = nullptr;
-    hipEvent_t lane_ev = nullptr;
-    bool lane_used = false;
+    static constexpr int LANE_ST = 4;  // batches rotate over tune.lane_streams of them
+    hipStream_t lane_st[LANE_ST] = {};
+    hipEvent_t lane_ev[LANE_ST] = {};
+    bool lane_used[LANE_ST] = {};
     // giant chains of k_heavy: rotating slots (stream, sample / job buffers, counters, events)
     static constexpr int GSLOTS = 3;  // + st, st2, st3, chain_st, stx: 8 streams
     hipStream_t gst[GSLOTS] = {};
@@ -5617,6 +5622,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     A.big_desc = b->d_big_desc.as<uint64_t>();
     A.big_cap = (uint32_t)std::min<uint64_t>(b->big_cap, 0xFFFFFFFFull);
     A.skip = nullptr;
+    A.sub_target = (uint32_t)std::max(0, b->tune.sub_target);
     if (b->stamps) {
         SKM_HIP(hipMemsetAsync(b->d_stamps.p, 0, 32 * 8, st));
         A.stamps = b->d_stamps.as<unsigned long long>();
@@ -5970,11 +5976,15 @@ void flush_long_chains(skm_build* b, int slot) {
                    nullptr, nullptr, nullptr, nullptr, b->d_data.as<skm_stored_kmer_data>(), b->tune.chain_prio,
                    lane_max);
     if (lane_max && !(b->tune.diag & 4) && !(b->tune.diag & 8)) {
-        SKM_HIP(hipStreamWaitEvent(b->lane_st, b->chain_ev[0], 0));
-        SKM_LAUNCH_AS(b, "k_chains_stash", k_chains, dim3((uint32_t)std::max(1, b->tune.lane_grid)), dim3(256), 0, b->lane_st,
+        // a batch lasts as long as its longest chain: batches rotate over lane_streams streams so a
+        // batch of giant chains does not hold back the next one
+        const int ls = slot % std::max(1, std::min(b->tune.lane_streams, (int)skm_build::LANE_ST));
+        hipStream_t lst = b->lane_st[ls];
+        SKM_HIP(hipStreamWaitEvent(lst, b->chain_ev[0], 0));
+        SKM_LAUNCH_AS(b, "k_chains_stash", k_chains, dim3((uint32_t)std::max(1, b->tune.lane_grid)), dim3(256), 0, lst,
                    b->d_long_jobs.as<Job>(), rng, rng + 1, b->long_jobs_cap, nullptr, nullptr, nullptr, nullptr,
                    b->d_data.as<skm_stored_kmer_data>(), lane_max);
-        b->lane_used = true;
+        b->lane_used[ls] = true;
     }
     SKM_HIP(hipGetLastError());
 }
@@ -5990,10 +6000,11 @@ void phase_stats(skm_build* b) {
                    (uint32_t)b->n_total, b->d_flags.as<uint8_t>());
     if (b->pass_bits) {  // the long chains of every pass (the last batch on the chain stream)
         flush_long_chains(b, 16);
-        if (b->lane_used) {
-            SKM_HIP(hipEventRecord(b->lane_ev, b->lane_st));
-            SKM_HIP(hipStreamWaitEvent(st, b->lane_ev, 0));
-            b->lane_used = false;
+        for (int k = 0; k < skm_build::LANE_ST; ++k) {
+            if (!b->lane_used[k]) continue;
+            SKM_HIP(hipEventRecord(b->lane_ev[k], b->lane_st[k]));
+            SKM_HIP(hipStreamWaitEvent(st, b->lane_ev[k], 0));
+            b->lane_used[k] = false;
         }
         for (int k = 0; k <= skm_build::GSLOTS; ++k) {
             if (!b->chain_used[k]) continue;
@@ -6185,8 +6196,10 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     use_evset(b, 0);
     SKM_HIP(hipEventCreate(&b->ev_start));
     SKM_HIP(hipStreamCreateWithFlags(&b->chain_st, hipStreamNonBlocking));
-    SKM_HIP(hipStreamCreateWithFlags(&b->lane_st, hipStreamNonBlocking));
-    SKM_HIP(hipEventCreateWithFlags(&b->lane_ev, hipEventDisableTiming));
+    for (int k = 0; k < skm_build::LANE_ST; ++k) {
+        SKM_HIP(hipStreamCreateWithFlags(&b->lane_st[k], hipStreamNonBlocking));
+        SKM_HIP(hipEventCreateWithFlags(&b->lane_ev[k], hipEventDisableTiming));
+    }
     SKM_HIP(hipStreamCreateWithFlags(&b->stx, hipStreamNonBlocking));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_pf_ready, hipEventDisableTiming));
     for (auto& e : b->ev_pf_done) SKM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -6505,9 +6518,11 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "flag_check" ? &t.flag_check
                : n == "diag" ? &t.diag
                : n == "flag_bits" ? &t.flag_bits
+               : n == "sub_target" ? &t.sub_target
                : n == "lane_long" ? &t.lane_long
                : n == "lane_grid" ? &t.lane_grid
                : n == "lane_tail" ? &t.lane_tail
+               : n == "lane_streams" ? &t.lane_streams
                : n == "serial_overflow" ? &t.serial_overflow
                : n == "overlap" ? &t.overlap
                : n == "heavy_grid" ? &t.heavy_grid
@@ -6981,11 +6996,13 @@ void skm_build_destroy(skm_build* b) {
         (void)hipStreamSynchronize(b->chain_st);
         (void)hipStreamDestroy(b->chain_st);
     }
-    if (b->lane_st) {
-        (void)hipStreamSynchronize(b->lane_st);
-        (void)hipStreamDestroy(b->lane_st);
+    for (int k = 0; k < skm_build::LANE_ST; ++k) {
+        if (b->lane_st[k]) {
+            (void)hipStreamSynchronize(b->lane_st[k]);
+            (void)hipStreamDestroy(b->lane_st[k]);
+        }
+        if (b->lane_ev[k]) (void)hipEventDestroy(b->lane_ev[k]);
     }
-    if (b->lane_ev) (void)hipEventDestroy(b->lane_ev);
     for (auto& e : b->chain_ev)
         if (e) (void)hipEventDestroy(e);
     if (b->h_pin) (void)hipHostFree(b->h_pin);

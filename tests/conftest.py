@@ -1,7 +1,7 @@
 import os
 
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 12:  # libskm runs up to 9 streams (read at HIP init)
-    os.environ["GPU_MAX_HW_QUEUES"] = "12"
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:  # libskm runs up to 12 streams (read at HIP init)
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import sys
 
 import pytest

@@ -12,7 +12,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p "$O"
 export TMPDIR=/tmp
-export GPU_MAX_HW_QUEUES=12
+export GPU_MAX_HW_QUEUES=16
 step() {  # name, limit, command...
   local name=$1 lim=$2; shift 2
   echo "[$(date +%T)] $name"
