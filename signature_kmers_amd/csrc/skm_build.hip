@@ -3527,6 +3527,8 @@ struct HeavyArgs {
     HeavyKey* keys;
     unsigned long long* nkeys;    // device counters (cleared per pass)
     unsigned long long* cursor;
+    unsigned long long* queue;    // k_heavy's work queue (cleared per pass): keys are taken in list
+                                  //   order, largest sub-buckets first (k_ovf_plan / k_ovf_split)
     uint64_t* hi;                 // heavy elements, key-contiguous
     uint64_t* lo;
     uint32_t* s0;                 // radix-sort ping-pong of the best members' sequence indices
@@ -3790,7 +3792,7 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
     __shared__ uint32_t s_wc[HEAVY_WG / 64][RBINS];
     __shared__ __align__(16) uint32_t s_wave[48];
     __shared__ uint32_t s_bm[2 * (HEAVY_WG / 64)];
-    __shared__ uint32_t s_cur, s_sel[3];
+    __shared__ uint32_t s_cur, s_sel[3], s_key;
     const uint32_t tid = threadIdx.x, nt = blockDim.x, lane = tid & 63u, wave = tid >> 6, nw = nt >> 6;
     const uint64_t lt = (1ull << lane) - 1ull;
     const uint32_t nkeys = (uint32_t)*H.nkeys;
@@ -3798,7 +3800,13 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
     for (uint32_t q = tid; q < (HEAVY_WG / 64) * RBINS; q += nt) (&s_wc[0][0])[q] = 0;
     __syncthreads();
     constexpr uint32_t U = SPLIT_U;
-    for (uint32_t q = blockIdx.x; q < nkeys; q += gridDim.x) {
+    for (;;) {
+        // dynamic queue: a workgroup that drew a giant key does not also own every 512th key after it
+        __syncthreads();
+        if (tid == 0) s_key = (uint32_t)min((unsigned long long)nkeys, atomicAdd(H.queue, 1ull));
+        __syncthreads();
+        const uint32_t q = s_key;
+        if (q >= nkeys) break;
         const HeavyKey K = H.keys[q];
         const uint64_t* hi = H.hi + K.off;
         const uint64_t* lo = H.lo + K.off;
@@ -4339,7 +4347,7 @@ struct Tune {
     int chain_streams = 1;           //   over this many streams (1..4)
     int poison_jobs = 0;             // tests: every slot of the run's long-job list starts as a canary job
     int route_vacate = 0;            // routing: the last this many passes hold no heavy key (0: half)
-    int route_heavy_min = 1 << 16;   // key-range passes: k-mers of >= this many occurrences are routed into
+    int route_heavy_min = 1 << 14;   // key-range passes: k-mers of >= this many occurrences are routed into
                                      //   the first half of the passes (0: off; k_pass_ids)
     int overlap = 0;                 // key-range passes, one GPU: pipelined passes (a second element set)
     int chain_cus = 0;               // CUs of the long-chain stream (0: all; set_option recreates it)
@@ -5689,6 +5697,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     H.keys = b->d_hv_keys.as<HeavyKey>();
     H.nkeys = ctr_d + 18;  // cleared with the pass's counters
     H.cursor = ctr_d + 19;
+    H.queue = ctr_d + 20;
     H.hi = b->d_hv_hi.as<uint64_t>();
     H.lo = b->d_hv_lo.as<uint64_t>();
     H.s0 = b->d_hv_s0.as<uint32_t>();
