@@ -2203,6 +2203,7 @@ struct BucketArgs {
     int flag_check;            // 1: a signature flag is stored only when it reads 0 (option flag_check)
     const uint32_t* skip;      // k_ovf_plan's verdict for the pass (nonzero: the run is being abandoned)
     uint32_t sub_target;       // k_partition: target elements per level-2 sub-bucket (0: SUB_TARGET)
+    int diag;                  // option diag (diagnostics only)
 };
 
 #define SKM_STAMP(i)                                                          \
@@ -3235,6 +3236,8 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
     const uint32_t q_lo = lo_slot < 0 ? 0u : plan[lo_slot], q_hi = plan[hi_slot];
     auto entry = [&](const OvfEntry e) {
         if (e.n == 0) return;  // every key of the sub-bucket went to k_heavy
+        if ((A.diag & 32) && e.n <= (uint32_t)CAP) return;  // diagnostics: the entries of one LDS chunk
+        if ((A.diag & 64) && e.n > (uint32_t)CAP) return;   //   / of the global network, skipped
         // src 2: the light remainder k_ovf_split compacted into this entry's own scratch (sorted in
         // place: each chunk is loaded whole before it is written back)
         const uint64_t* src_hi = (e.src == 2 ? S.hi : e.src ? A.tmp_hi : A.recs_hi) + e.off;
@@ -4373,7 +4376,8 @@ struct Tune {
                                      //   0: a byte store per kept occurrence (C3: +58 ms/step)
     int diag = 0;                    // diagnostics only (wrong results): 1 = no signature flag stores,
                                      //   2 = k_heavy without its sequence-index sort, 4 = no chain kernels,
-                                     //   8 = no stashed long chains, 16 = no per-pass k_chains
+                                     //   8 = no stashed long chains, 16 = no per-pass k_chains,
+                                     //   32 / 64 = k_overflow skips its entries of <= / > CAP elements
 };
 
 }  // namespace skm
@@ -5631,6 +5635,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     A.big_cap = (uint32_t)std::min<uint64_t>(b->big_cap, 0xFFFFFFFFull);
     A.skip = nullptr;
     A.sub_target = (uint32_t)std::max(0, b->tune.sub_target);
+    A.diag = b->tune.diag;
     if (b->stamps) {
         SKM_HIP(hipMemsetAsync(b->d_stamps.p, 0, 32 * 8, st));
         A.stamps = b->d_stamps.as<unsigned long long>();
