@@ -197,7 +197,7 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   the stashed long-job list), "route_heavy_min" (one GPU, >= 4 key-range passes: k-mers with at
  *   least this many occurrences -- estimated at prepare from a count-min sketch of 1/64 of the
  *   windows -- are grouped in the first half of the passes, so their long P^2 chains run beside
- *   the later passes instead of after the last one; 65536; 0 = off), "route_vacate" (the last
+ *   the later passes instead of after the last one; 16384; 0 = off), "route_vacate" (the last
  *   this many passes hold no routed heavy key, whose keys are spread over the others by hash;
  *   0 = the second half, mapped to pass - P/2), "stage_round" (key-range
  *   passes: 1 = the staged position scatter in half rounds of 2048 elements, four workgroups
@@ -211,7 +211,16 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   "side_cus" (the same for the overflow streams and the next pass's selection), "overlap"
  *   (key-range passes on one GPU: 1 = pipelined passes -- a second element buffer set when it
  *   fits, so a pass's overflow path runs beside the next pass's extract and partition; 0 = each
- *   pass waits for its overflow path, the default), "heavy_grid" (k_heavy's persistent grid, 512).
+ *   pass waits for its overflow path, the default), "heavy_grid" (k_heavy's persistent grid, 512),
+ *   "lane_long" (key-range passes: stashed long chains below this many samples run one lane each,
+ *   64 chains per wave, instead of on a wave pair; 2^20; 0 = all on wave pairs), "lane_grid"
+ *   (their grid, 256), "lane_tail" (the threshold for the batch after the last pass, 2^16),
+ *   "lane_streams" (their batches rotate over 1..4 streams, 1), "chain_queue" (1: chain waves take
+ *   64-job blocks from a work queue instead of a fixed stride), "flag_bits" (1: signature flags
+ *   kept as bits during the run, read before an atomic set; 0: a byte store per kept
+ *   occurrence), "sub_target" (k_partition's target elements per level-2 sub-bucket; 0 = 1024),
+ *   "diag" (diagnostics only, wrong results: skips of flag stores / the heavy sort / chain
+ *   kernels / overflow entry classes).
  * Unknown names and out-of-range values return SKM_E_ARG. */
 int skm_build_set_option(skm_build* b, const char* name, int64_t value);
 /* Diagnostics: copy the per-phase cycle sums of the last run (if enabled) into out, then
