@@ -1343,9 +1343,13 @@ __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, co
                                                 const unsigned long long* hi_p, uint64_t cap,
                                                 const uint32_t* __restrict__ lens, const uint32_t* __restrict__ recs32,
                                                 const uint32_t* __restrict__ tmp32, const uint32_t* __restrict__ big32,
-                                                skm_stored_kmer_data* __restrict__ out, uint32_t max_n = 0) {
-    // wave pairs walk blocks of 64 jobs (grid may be smaller than the job count: a capped grid
-    // keeps few waves resident beside a concurrent kernel, longest jobs first)
+                                                skm_stored_kmer_data* __restrict__ out, uint32_t max_n = 0,
+                                                unsigned long long* queue = nullptr) {
+    // blocks of 64 jobs, one job per lane: the P^2 of a block on an even wave, its variance on an odd
+    // one (grid may be smaller than the job count: a capped grid keeps few waves resident beside a
+    // concurrent kernel, longest jobs first).  With `queue` (two zeroed counters) every wave takes
+    // its next block from its half's counter, so a wave held by a block of long chains does not
+    // also own a fixed share of the later blocks; without it, wave pairs stride over the blocks.
     const uint64_t lo = lo_p ? (uint64_t)*lo_p : 0ull;
     const uint64_t hi = min((uint64_t)*hi_p, cap);
     if (hi <= lo) return;
@@ -1353,7 +1357,13 @@ __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, co
     const uint64_t njobs = hi - lo;
     const bool var_wave = ((threadIdx.x >> 6) & 1u) != 0;
     const uint64_t pairs = (uint64_t)gridDim.x * (blockDim.x >> 7);
-    for (uint64_t pr = (uint64_t)blockIdx.x * (blockDim.x >> 7) + (threadIdx.x >> 7); pr * 64 < njobs; pr += pairs) {
+    auto take = [&]() -> uint64_t {
+        uint32_t v = 0;
+        if ((threadIdx.x & 63u) == 0) v = (uint32_t)atomicAdd(queue + (var_wave ? 1 : 0), 1ull);
+        return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    };
+    for (uint64_t pr = queue ? take() : (uint64_t)blockIdx.x * (blockDim.x >> 7) + (threadIdx.x >> 7); pr * 64 < njobs;
+         pr = queue ? take() : pr + pairs) {
         const uint64_t j = pr * 64 + (threadIdx.x & 63u);
         if (j >= njobs) break;
         const Job jb = jobs[j];
@@ -4369,6 +4379,7 @@ struct Tune {
     // whole batch, and a k_bucket_process workgroup needs half of a CU's registers and LDS
     int lane_long = 1 << 20;
     int lane_grid = 256;             //   their k_chains grid
+    int chain_queue = 0;             // k_chains: waves take 64-job blocks from a queue (0: strided)
     int lane_streams = 1;            //   the streams their batches rotate over (1..4)
     int lane_tail = 1 << 16;         //   the last batch's threshold (its wave pairs are the tail's latency)
     int sub_target = 0;              // k_partition's target elements per level-2 sub-bucket (0: SUB_TARGET)
@@ -4441,6 +4452,8 @@ struct skm_build {
     DevBuf d_recs_hi, d_recs_lo, d_tmp_hi, d_tmp_lo;
     DevBuf d_cur0, d_cur1, d_slices;   // staged scatter cursors
     DevBuf d_flagbits;
+    DevBuf d_chainq;              // k_chains work queues: two counters per launch of a run
+    uint32_t chainq_next = 0;
     DevBuf d_keys, d_data, d_ctr, d_flags, d_dfunc, d_swf, d_ovf, d_ovf_hi, d_ovf_lo, d_ovf_heads, d_ovf_job, d_ovf_fm;
     DevBuf d_jobs, d_lens, d_stamps, d_big_desc, d_big_out;
     uint64_t big_cap = 0, n_big = 0, big_kept = 0;
@@ -5538,6 +5551,17 @@ int giant_class(const skm_build* b) {
 constexpr uint32_t JOB_NWG = 256;      // k_job_count / k_job_scatter workgroups (one chunk each)
 constexpr uint32_t LONG_GRID = 2048;   // k_chain_long / k_long_stash workgroups (one job at a time)
 
+constexpr uint32_t CHAINQ_SLOTS = 256;  // k_chains launches per run (2 per pass + the stash batches)
+
+// a zeroed pair of k_chains queue counters on stream st (distinct per launch of the run)
+unsigned long long* chain_queue(skm_build* b, hipStream_t st) {
+    if (!b->tune.chain_queue) return nullptr;
+    b->d_chainq.ensure(16ull * CHAINQ_SLOTS);
+    unsigned long long* q = b->d_chainq.as<unsigned long long>() + 2 * (b->chainq_next++ % CHAINQ_SLOTS);
+    SKM_HIP(hipMemsetAsync(q, 0, 16, st));
+    return q;
+}
+
 void launch_chains(skm_build* b, hipStream_t st, const Job* jobs, const unsigned long long* nj_d, uint64_t cap,
                    ChainSet& cs, const uint32_t* lens, const uint32_t* recs32, const uint32_t* tmp32,
                    const uint32_t* big32, skm_stored_kmer_data* out, uint32_t long_class,
@@ -5579,9 +5603,11 @@ void launch_chains(skm_build* b, hipStream_t st, const Job* jobs, const unsigned
         SKM_HIP(hipStreamWaitEvent(st_short, ev_sorted, 0));
         ss = st_short;
     }
-    if (run_chains)
+    if (run_chains) {
+        unsigned long long* q = chain_queue(b, ss);
         SKM_LAUNCH(b, k_chains, dim3(max_wgs ? max_wgs : (uint32_t)std::max(1, tn.chain_grid)), dim3(256), 0, ss,
-                   cs.sorted.as<Job>(), nlong_u, nj_d, cap, lens, recs32, tmp32, big32, out);
+                   cs.sorted.as<Job>(), nlong_u, nj_d, cap, lens, recs32, tmp32, big32, out, 0u, q);
+    }
     SKM_HIP(hipGetLastError());
 }
 
@@ -5894,6 +5920,7 @@ void alloc_caps(skm_build* b) {
 void begin_run(skm_build* b) {
     hipStream_t st = b->stream;
     alloc_caps(b);
+    b->chainq_next = 0;
     SKM_HIP(hipEventRecord(b->ev_start, st));
     SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 3 * 256, st));
     b->ovf_pending[0] = b->ovf_pending[1] = false;
@@ -5995,9 +6022,10 @@ void flush_long_chains(skm_build* b, int slot) {
         const int ls = slot % std::max(1, std::min(b->tune.lane_streams, (int)skm_build::LANE_ST));
         hipStream_t lst = b->lane_st[ls];
         SKM_HIP(hipStreamWaitEvent(lst, b->chain_ev[0], 0));
+        unsigned long long* q = chain_queue(b, lst);
         SKM_LAUNCH_AS(b, "k_chains_stash", k_chains, dim3((uint32_t)std::max(1, b->tune.lane_grid)), dim3(256), 0, lst,
                    b->d_long_jobs.as<Job>(), rng, rng + 1, b->long_jobs_cap, nullptr, nullptr, nullptr, nullptr,
-                   b->d_data.as<skm_stored_kmer_data>(), lane_max);
+                   b->d_data.as<skm_stored_kmer_data>(), lane_max, q);
         b->lane_used[ls] = true;
     }
     SKM_HIP(hipGetLastError());
@@ -6537,6 +6565,7 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "lane_grid" ? &t.lane_grid
                : n == "lane_tail" ? &t.lane_tail
                : n == "lane_streams" ? &t.lane_streams
+               : n == "chain_queue" ? &t.chain_queue
                : n == "serial_overflow" ? &t.serial_overflow
                : n == "overlap" ? &t.overlap
                : n == "heavy_grid" ? &t.heavy_grid
