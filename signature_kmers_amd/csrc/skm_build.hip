@@ -3522,11 +3522,13 @@ __global__ __launch_bounds__(BP_THREADS) void k_overflow(BucketArgs A, OvfScratc
 //     sorted descending -- a u32 radix sort, not a 16-byte sort.
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t HEAVY_MIN = 1024;        // occurrences that make a key heavy
-constexpr uint32_t SPLIT_MIN = 4096;        // overflow sub-buckets of at least this size are split
+// overflow sub-buckets of at least this size are split: every one beyond LDS (C3 A/B: 4096 ->
+// 2049 takes k_overflow's global-network entries down, 1655 -> 1623 ms/step over two boxes)
+constexpr uint32_t SPLIT_MIN = CAP + 1;
 constexpr uint32_t SPLIT_TAB = 4096;        // LDS key table slots (load <= ~0.5 at SUB_TARGET)
 constexpr uint32_t SPLIT_MAXH = 256;        // heavy keys taken out of one sub-bucket (more stay light)
 constexpr uint32_t HEAVY_WG = 512;
-constexpr uint32_t HEAVY_GRID = 512;        // k_heavy: persistent workgroups looping over the keys
+constexpr uint32_t HEAVY_GRID = 1024;       // k_heavy: persistent workgroups taking keys from a queue
 
 struct HeavyKey {
     uint64_t off;       // first element in the heavy arrays
