@@ -229,8 +229,10 @@ def main():
 
     # ---- headline: C3 strong scaling ----
     uid = new_uid()
+    skm.warm_device(device)  # the process's HIP runtime up before the one-shot clock starts
     t0 = time.time()
     b = skm.SignatureBuilder(len(funcs), device=device, rank=rank, world_size=world)
+    create_s = time.time() - t0
     for kv in a.option:
         k, v = kv.split("=", 1)
         b.set_option(k, int(v))
@@ -268,7 +270,7 @@ def main():
                    f"all-to-all + all-reduce, per key-range pass"},
         "roofline": head["roofline"],
         "pipeline": head["pipeline"],
-        "pcie_inclusive": _pcie_inclusive(head, prep_s),
+        "pcie_inclusive": _pcie_inclusive(head, prep_s, create_s),
         "cpu_baseline": None,
         "gen_seconds": gen_s,
         "prepare_seconds": prep_s,
@@ -335,7 +337,7 @@ _ROOF_NOTES = {
     "k_chains_stash": "background stream: the stashed long P^2 / variance chains, one lane each -- serial "
                       "FP64 recurrences in the reference's reverse visit order (SURVEY A.4), so each launch "
                       "lasts as long as its longest chain (~10^6 samples at ~0.6 us) at a few waves per CU; "
-                      "latency-bound, not byte-bound: main_stream is the step's byte-moving critical path",
+                      "latency-bound, not byte-bound: the roofline kernel (the group-by) is the step's byte-moving critical path",
     "k_chains": "P^2 / variance chains (serial FP64 recurrences, one lane each): latency-bound",
     "k_chain_long": "P^2 / variance chains on wave pairs (serial FP64 recurrences): latency-bound",
 }
@@ -361,8 +363,9 @@ def _alg_bytes(kernel, c, res_bytes):
         "k_overflow": 16 * c["overflow_elements"],
         "k_ovf_split": 32 * c["overflow_elements"],
         "k_heavy": 16 * c["overflow_elements"],
-        # 4 B per chain sample.  The stashed long chains (key-range passes) run as
-        # k_chains_stash (one lane each) or k_chain_long (a wave pair each; the tail batch's longest)
+        # the builder's figure (SURVEY 8(d) states none for the chains): one u32 sample read per
+        # recurrence step.  The stashed long chains (key-range passes) run as k_chains_stash (one
+        # lane each) or k_chain_long (a wave pair each; the tail batch's longest)
         "k_chain_long": 4 * c["long_samples"],
         "k_chains_stash": 4 * c["long_samples"],
         "k_chains": 4 * (c["chain_samples"] - (c["long_samples"] if c["passes"] > 1 else 0)),
@@ -386,9 +389,15 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
     b.set_kernel_timing(True)
     b.run()
     ktab = b.kernel_timings()
-    dom = max(ktab, key=lambda k: ktab[k][0]) if ktab else "k_bucket_process"
+    # the roofline's kernel: the group-by (k_bucket_process), the dominant byte-moving kernel of the
+    # main stream that carries the step's critical path; the kernel with the largest GPU time (the
+    # background long-chain batches: latency-bound FP64 recurrences at a few waves per CU) is
+    # reported beside it (roofline.largest_gpu_time)
+    big = max(ktab, key=lambda k: ktab[k][0]) if ktab else None
+    dom = "k_bucket_process"
     b.set_kernel_timing(True, dom)
-    log(f"dominant kernel by GPU time: {dom} ({ktab.get(dom, (0, 0))[0]:.1f} ms in {ktab.get(dom, (0, 0))[1]} launches)")
+    log(f"roofline kernel: {dom} ({ktab.get(dom, (0, 0))[0]:.1f} ms in {ktab.get(dom, (0, 0))[1]} launches); "
+        f"largest GPU time: {big}")
     phase = {}
     dom_ms, dom_n = 0.0, 0
     barrier()
@@ -430,16 +439,16 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
     pipe_alg = sums["res"] + 32 * sums["grouped"] + 18 * sums["kept"]
     pipe_gbs = pipe_alg / (t_max / steps) / 1e9
     top = sorted(ktab.items(), key=lambda kv: -kv[1][0])[:14]
-    # the main stream's dominant kernel beside it (the group-by; a background chain kernel can hold
-    # the most GPU time while its FP64 recurrences are latency-, not byte-bound)
-    mk = "k_bucket_process"
-    m_ms, m_n = ktab.get(mk, (0.0, 0))
-    m_alg = _alg_bytes(mk, ctrs, shard.n_residues + shard.n_seqs)
-    m_ach = m_alg / (m_ms * 1e-3) / 1e9 if m_alg and m_ms > 0 else None
-    main_stream = {"kernel": mk, "achieved": m_ach, "frac": m_ach / HBM_PEAK_GBS if m_ach else None,
-                   "alg_bytes_per_launch": None if m_alg is None else m_alg / max(1, m_n),
-                   "avg_launch_ms": m_ms / max(1, m_n), "launches_per_step": m_n,
-                   "traffic": (lambda t: None if t is None else t / max(1, m_n))(_pmc_traffic(mk, wl, shard.n_seqs)),
+    largest = None
+    if big is not None:
+        g_ms, g_n = ktab[big]
+        g_alg = _alg_bytes(big, ctrs, shard.n_residues + shard.n_seqs)
+        g_ach = g_alg / (g_ms * 1e-3) / 1e9 if g_alg and g_ms > 0 else None
+        largest = {"kernel": big, "achieved": g_ach, "frac": g_ach / HBM_PEAK_GBS if g_ach else None,
+                   "alg_bytes_per_launch": None if g_alg is None else g_alg / max(1, g_n),
+                   "avg_launch_ms": g_ms / max(1, g_n), "launches_per_step": g_n,
+                   "traffic": (lambda t: None if t is None else t / max(1, g_n))(_pmc_traffic(big, wl, shard.n_seqs)),
+                   "note": _ROOF_NOTES.get(big),
                    "timing": "events around each launch in the untimed diagnostic run"}
     return {
         "value": windows_total * steps / t_max,
@@ -455,26 +464,32 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
                      "avg_launch_ms": dom_ms_step / launches,
                      "alg_bytes_per_step": alg, "kernel_ms_per_step": dom_ms_step,
                      "launches_per_step": launches,
-                     "selection": "largest GPU time per step over every kernel launch of the run (event pairs "
-                                  "around each launch in one untimed run); timed: events around this kernel's "
-                                  "launches in the timed steps",
+                     "selection": "the main stream's group-by (the byte-moving kernel on the step's critical "
+                                  "path); timed: events around this kernel's launches in the timed steps",
                      "kernels_ms_per_step": {k: round(v[0], 2) for k, v in top},
-                     "note": _ROOF_NOTES.get(dom),
-                     "main_stream": main_stream},
+                     "largest_gpu_time": largest},
         "chain_tail_ms": phase.get("chain_tail"),
         "pipeline": {"alg_bytes": pipe_alg, "ms": 1000.0 * t_max / steps, "GBs": pipe_gbs,
                      "frac": pipe_gbs / HBM_PEAK_GBS / max(1, world), "phase_ms_rank0": phase},
     }
 
 
-def _pcie_inclusive(m, prep_s):
+def _pcie_inclusive(m, prep_s, create_s=None):
     """The rate from host arrays: add_batch (packing into the pinned double-buffered staging whose
     DMA to HBM overlaps the packing) + prepare + one build step.  Reported beside `value`, which
-    starts with the inputs resident in HBM."""
+    starts with the inputs resident in HBM.  `phases` splits the host time: the handle's creation
+    (streams, pinned staging; the process's HIP runtime is initialised before), add_batch, and
+    prepare's residue / metadata upload, pass plan (device tallies + routing sketch) and the rest."""
     t = prep_s + m["ms_per_step"] / 1000.0
+    c = m["counters"]
+    phases = {"create_s": create_s, "add_batch_s": c.get("add_batch_us", 0) / 1e6,
+              "prepare_upload_s": c.get("prepare_upload_us", 0) / 1e6,
+              "prepare_plan_device_s": c.get("prepare_plan_us", 0) / 1e6,
+              "prepare_rest_s": c.get("prepare_rest_us", 0) / 1e6}
     return {"value": m["windows_total"] / t, "unit": "k-mers/s", "upload_prepare_s": prep_s,
-            "step_s": m["ms_per_step"] / 1000.0,
-            "note": "host arrays -> HBM (skm_build_add_batch: pinned double-buffered staging) + prepare + one step"}
+            "step_s": m["ms_per_step"] / 1000.0, "phases": phases,
+            "note": "host arrays -> HBM (skm_build_add_batch: pinned double-buffered staging, packed on the "
+                    "host pool) + prepare + one step"}
 
 
 def _annotate_leg(skm, kept, funcs, q, a, device, cores):
@@ -543,9 +558,11 @@ def _annotate_leg(skm, kept, funcs, q, a, device, cores):
 def _matrix_leg(skm, matrix_in, a, device, cores, rank=0, world=1, dist=None):
     """kmers-matrix-distance (BASELINE configs[4]): a 200-family signature DB (built on this GPU from
     200K training proteins, BDZ on the GPU) resident in HBM, 100K fresh query proteins of the same
-    families, all-vs-all shared-signature-k-mer counts.  With N ranks each GPU computes its band
-    of rows of the pair triangle (skm_matrix_tile_rows, equal triangle area; the hit lists are
-    recomputed on every GPU, no collective) and the step time is the max over ranks.  One step =
+    families, all-vs-all shared-signature-k-mer counts.  With N ranks each GPU looks up its own
+    range of the queries, the hits go to their k-mer's owner (all-to-all), each owner groups its
+    k-mers and routes every group's member suffix to the row bands it touches (skm_matrix_tile_rows,
+    equal triangle area; all-to-all), each rank counts its band, and the step time is the max over
+    ranks.  One step =
     window lookup + length filter, k-mer grouping (hash + radix sort), per-row LDS histograms of the
     pair increments, compaction of the nonzero pairs in row order; the pairs stay on the device.
     Roofline: k_md_rows (the pair increments), SURVEY 8(d) 4 B per pair increment."""
@@ -647,7 +664,7 @@ def _per_launch(traffic, passes):
     return None if traffic is None else traffic / max(1, passes)
 
 
-_PMC_FILE = "r03_pmc_traffic.json"
+_PMC_FILE = "r04_pmc_traffic.json"
 
 
 def src_sha16() -> str:
@@ -664,8 +681,8 @@ def src_sha16() -> str:
 
 
 def _pmc_traffic(kernel: str, workload: str, seqs: int):
-    """HBM bytes of `kernel` from the committed rocprofv3 PMC summary (profiles/r03_pmc_traffic.json,
-    tools/gpu_profile_r03.sh + tools/pmc_summary_r03.py): per build run (all launches of a step)
+    """HBM bytes of `kernel` from the committed rocprofv3 PMC summary (profiles/r04_pmc_traffic.json,
+    tools/gpu_profile_r04.sh + tools/pmc_summary_r03.py): per build run (all launches of a step)
     or per launch (legs), when it was measured on this kernel and workload size AND on the same
     device sources as this run (src_sha16); else None.  Streaming kernels count FETCH_SIZE x2,
     gather kernels x1 (profiles/r02_fetch_calib.json)."""

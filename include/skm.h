@@ -146,6 +146,10 @@ int skm_build_kernel_timings(skm_build* b, char* names, size_t names_cap, float*
  * long-chain samples, stashed long jobs) [20..23]=the last run's demands on them [24]=samples of
  * the stashed long chains (chains of >= 2^14 samples with key-range passes) [25]=occurrences of
  * heavy k-mers routed into the first half of the key-range passes ("route_heavy_min");
+ * [26]=host microseconds in skm_build_add_batch (all calls; the residues are packed by a pool of
+ * host threads, SKM_HOST_THREADS or min(16, hardware threads)), and prepare's phases in
+ * microseconds: [27] the residue / metadata upload, [28] the pass plan (device tallies of the pass
+ * sizes, heavy-key routing sketch and filter), [29] allocations and the rest;
  * totals over the passes of the run; returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Host transport: the rank collectives of a multi-process build run by the caller on host

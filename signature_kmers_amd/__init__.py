@@ -195,6 +195,12 @@ def device_count() -> int:
     return n.value
 
 
+def warm_device(device: int = 0) -> None:
+    """Bring up the process's HIP runtime and the device context (one throwaway build handle), so
+    that a timed one-shot build does not include the runtime's start-up."""
+    SignatureBuilder(1, device=device).close()
+
+
 def kmer_to_str(key: int) -> str:
     return int(key).to_bytes(8, "little").decode("latin-1")
 
@@ -315,13 +321,13 @@ class SignatureBuilder:
         return self.counters()["passes"]
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 26)()
-        n = lib().skm_build_counters(self._h, v, 26)
+        v = (C.c_uint64 * 30)()
+        n = lib().skm_build_counters(self._h, v, 30)
         names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped",
                  "overflow_elements", "overflow_kept", "big_groups", "big_kept", "passes", "valid", "giant_chains",
                  "giant_max", "redone", "cap_overflow_scratch", "cap_split", "cap_long_samples", "cap_long_jobs",
                  "demand_overflow_scratch", "demand_split", "demand_long_samples", "demand_long_jobs",
-                 "long_samples", "routed"]
+                 "long_samples", "routed", "add_batch_us", "prepare_upload_us", "prepare_plan_us", "prepare_rest_us"]
         return {names[i]: int(v[i]) for i in range(n)}
 
     def debug_jobs(self, k: int = 64) -> list:

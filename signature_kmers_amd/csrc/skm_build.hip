@@ -29,12 +29,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <numeric>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "skm_common.h"
+#include "skm_pool.h"
 #include "skm_util.h"
 
 #if defined(SKM_WITH_RCCL)
@@ -1339,12 +1341,12 @@ __global__ __launch_bounds__(128) void k_chain_dyn(const Job* __restrict__ jobs,
 }
 
 // jobs [*lo_p, min(*hi_p, cap)) (the per-lane chains after the long ones of the class-sorted list)
-__global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, const unsigned long long* lo_p,
-                                                const unsigned long long* hi_p, uint64_t cap,
-                                                const uint32_t* __restrict__ lens, const uint32_t* __restrict__ recs32,
-                                                const uint32_t* __restrict__ tmp32, const uint32_t* __restrict__ big32,
-                                                skm_stored_kmer_data* __restrict__ out, uint32_t max_n = 0,
-                                                unsigned long long* queue = nullptr) {
+__device__ __forceinline__ void chains_body(const Job* __restrict__ jobs, const unsigned long long* lo_p,
+                                            const unsigned long long* hi_p, uint64_t cap,
+                                            const uint32_t* __restrict__ lens, const uint32_t* __restrict__ recs32,
+                                            const uint32_t* __restrict__ tmp32, const uint32_t* __restrict__ big32,
+                                            skm_stored_kmer_data* __restrict__ out, uint32_t max_n,
+                                            unsigned long long* queue) {
     // blocks of 64 jobs, one job per lane: the P^2 of a block on an even wave, its variance on an odd
     // one (grid may be smaller than the job count: a capped grid keeps few waves resident beside a
     // concurrent kernel, longest jobs first).  With `queue` (two zeroed counters) every wave takes
@@ -1386,6 +1388,23 @@ __global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, co
         else
             out[jb.out_idx].median = d2u16(st.h[2]);
     }
+}
+
+// the per-pass chains, and the stashed long chains of key-range passes (the same recurrences; a
+// kernel symbol of their own so that profiles and counter passes tell the background batches apart)
+__global__ __launch_bounds__(256) void k_chains(const Job* __restrict__ jobs, const unsigned long long* lo_p,
+                                                const unsigned long long* hi_p, uint64_t cap,
+                                                const uint32_t* __restrict__ lens, const uint32_t* __restrict__ recs32,
+                                                const uint32_t* __restrict__ tmp32, const uint32_t* __restrict__ big32,
+                                                skm_stored_kmer_data* __restrict__ out, uint32_t max_n = 0,
+                                                unsigned long long* queue = nullptr) {
+    chains_body(jobs, lo_p, hi_p, cap, lens, recs32, tmp32, big32, out, max_n, queue);
+}
+__global__ __launch_bounds__(256) void k_chains_stash(const Job* __restrict__ jobs, const unsigned long long* lo_p,
+                                                      const unsigned long long* hi_p, uint64_t cap,
+                                                      skm_stored_kmer_data* __restrict__ out, uint32_t max_n,
+                                                      unsigned long long* queue) {
+    chains_body(jobs, lo_p, hi_p, cap, nullptr, nullptr, nullptr, nullptr, out, max_n, queue);
 }
 
 // Diagnostics: one half of the wave-pair chain code alone (which 0: P^2, 1: variance).
@@ -1551,10 +1570,12 @@ __device__ __forceinline__ uint64_t window_hash(uint64_t raw) {
 }
 
 // sketch (bloom == nullptr): count the sampled windows of every key into both rows;
-// bloom pass: keys whose estimate (the smaller row) reaches `thresh` set their two filter bits
+// bloom pass: keys whose estimate (the smaller row) reaches `thresh` set their two filter bits,
+// one byte per bit (bloom8[2^BLOOM_BITS]): at world > 1 the ranks' byte filters are combined by
+// an element-wise max (= OR) over the ranks before k_bloom_pack, so every rank routes the same keys
 __global__ __launch_bounds__(256) void k_route_sketch(const uint8_t* __restrict__ res, uint64_t rp,
                                                       uint32_t* __restrict__ cms, uint32_t thresh,
-                                                      uint32_t* __restrict__ bloom) {
+                                                      uint8_t* __restrict__ bloom) {
     const uint64_t ns = (rp + (1u << ROUTE_SAMPLE) - 1) >> ROUTE_SAMPLE;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t h = sampled_hash(res, i << ROUTE_SAMPLE, rp);
@@ -1565,12 +1586,23 @@ __global__ __launch_bounds__(256) void k_route_sketch(const uint8_t* __restrict_
             atomicAdd(r0, 1u);
             atomicAdd(r1, 1u);
         } else if (min(*r0, *r1) >= thresh) {
-            const uint32_t b1 = (uint32_t)(h & ((1u << BLOOM_BITS) - 1u));
-            const uint32_t b2 = (uint32_t)((h >> 24) & ((1u << BLOOM_BITS) - 1u));
-            atomicOr(&bloom[b1 >> 5], 1u << (b1 & 31u));
-            atomicOr(&bloom[b2 >> 5], 1u << (b2 & 31u));
+            bloom[h & ((1u << BLOOM_BITS) - 1u)] = 1u;
+            bloom[(h >> 24) & ((1u << BLOOM_BITS) - 1u)] = 1u;
         }
     }
+}
+
+// the byte filter -> the bit filter k_pass_ids keeps in LDS (one word per thread)
+__global__ void k_bloom_pack(const uint8_t* __restrict__ bloom8, uint32_t* __restrict__ bloom) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= (1u << BLOOM_BITS) / 32u) return;
+    const uint4* src = reinterpret_cast<const uint4*>(bloom8 + 32ull * w);
+    const uint4 a = src[0], c = src[1];
+    const uint32_t x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v |= (((x[j >> 2] >> (8 * (j & 3))) & 0xFFu) != 0u ? 1u : 0u) << j;
+    bloom[w] = v;
 }
 
 // counts mode: pass_bits == owner_bits == 0 -> by the top 6 hash bits; else by (pass id <<
@@ -2406,7 +2438,7 @@ __device__ __forceinline__ void seg_groups(const SubLds& L, uint32_t q0, uint32_
     const uint64_t Rs = R & segmask;
     const uint32_t rs = Rs ? (uint32_t)__ffsll((long long)Rs) - 1u : sbase;
     const uint32_t s = (uint32_t)(key >> ELEM_I_BITS) & ((1u << ELEM_S_BITS) - 1u);
-    const uint32_t fl = (A.flag_check && real) ? A.flags[s] : 0u;
+    const uint32_t fl = (A.flag_check && real && A.flags) ? A.flags[s] : 0u;  // diag 1: no flags
     const uint32_t len = (pay & 1u) ? A.glen[s] : len16;
     if (kept && real && fl == 0 && A.flags) mark_seq(A.flags, s);
     const uint32_t x0 = (uint32_t)__shfl((int)len, (int)(rs + cbest - 1), 64);  // first visited
@@ -4431,9 +4463,14 @@ struct skm_build {
     uint64_t rp_total = 0;          // residues packed so far (incl. separators)
     uint64_t rp_dev = 0;            // bytes of them issued to the device
     uint64_t res_cap = 0;           // d_res capacity
-    double stage_ms = 0;            // host time spent packing + waiting for a free staging buffer
     std::vector<SeqMeta> h_meta;
     std::vector<uint32_t> h_seqid;
+    std::unique_ptr<HostPool> pool;     // host threads of the packing (add_batch)
+    std::vector<uint32_t> h_keep;       // add_batch scratch: the batch's kept sequences, their offsets
+    std::vector<uint64_t> h_cum;
+    // host seconds in add_batch (all calls), and prepare's phases: the residue / metadata upload, the
+    // pass plan (the pass tallies and the routing sketch: device work), the allocations and the rest
+    double add_s = 0, prep_upload_s = 0, prep_plan_s = 0, prep_rest_s = 0;
     uint64_t n_windows = 0;
     bool seqid_strict = true;
     bool prepared = false, ran = false;
@@ -4520,6 +4557,7 @@ struct skm_build {
     uint64_t valid_total = 0;           // valid windows of this shard
     DevBuf d_ids;                       // per-window pass id (pass_bits > 0)
     DevBuf d_bloom;                     // heavy-key routing filter (route)
+    std::vector<uint64_t> cnt64;        // valid windows by the top 6 hash bits (size_passes)
     bool route = false;
     uint64_t routed = 0;                // occurrences routed into the first half of the passes
     // a pass's window positions, level-1 histogram matrix and window count, double-buffered: the
@@ -5056,41 +5094,9 @@ void size_passes(skm_build* b, int forced_pb = -1) {
     SKM_CHECK(pb <= 6, SKM_E_ARG, "key_range_passes must be a power of two <= 64");
     b->pass_bits = pb;
     b->pass_max = pass_max(pb);
-    // heavy-key routing (one GPU, at least 4 passes): the count-min sketch of 1/64 of the windows,
-    // the Bloom filter of the keys whose estimate reaches route_heavy_min / 64 (with 15 % slack),
-    // then the pass sizes once more, by routed pass id
     b->route = false;
     b->routed = 0;
-    if (pb >= 2 && b->world == 1 && b->tune.route_heavy_min > 0 && b->rp) {
-        DevBuf cms;
-        cms.ensure(4ull << (CMS_BITS + 1));
-        b->d_bloom.ensure((1u << BLOOM_BITS) / 8);
-        SKM_HIP(hipMemsetAsync(cms.p, 0, 4ull << (CMS_BITS + 1), b->stream));
-        SKM_HIP(hipMemsetAsync(b->d_bloom.p, 0, (1u << BLOOM_BITS) / 8, b->stream));
-        const uint32_t thresh = std::max<uint32_t>(8, (uint32_t)(((uint64_t)b->tune.route_heavy_min >> ROUTE_SAMPLE) * 85 / 100));
-        hipLaunchKernelGGL(k_route_sketch, dim3(2048), dim3(256), 0, b->stream, b->d_res.as<uint8_t>(), b->rp,
-                           cms.as<uint32_t>(), 0u, nullptr);
-        hipLaunchKernelGGL(k_route_sketch, dim3(2048), dim3(256), 0, b->stream, b->d_res.as<uint8_t>(), b->rp,
-                           cms.as<uint32_t>(), thresh, b->d_bloom.as<uint32_t>());
-        // the vacated passes: the second half, or the last route_vacate
-        const int R = b->tune.route_vacate > 0 ? std::min(b->tune.route_vacate, (1 << pb) - 1) : 1 << (pb - 1);
-        uint64_t natural_late = 0;  // occurrences of the vacated passes before routing
-        for (int p = (1 << pb) - R; p < (1 << pb); ++p)
-            for (int i = 0; i < (64 >> pb); ++i) natural_late += cnt[p * (64 >> pb) + i];
-        SKM_HIP(hipMemsetAsync(d_cnt.p, 0, 8 * 64, b->stream));
-        hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 4u * 64 + (1u << BLOOM_BITS) / 8, b->stream,
-                           b->d_res.as<uint8_t>(), b->rp, pb, 0, nullptr, d_cnt.as<unsigned long long>(),
-                           b->d_bloom.as<uint32_t>(), 64u, nullptr, 0, (uint32_t)std::max(0, b->tune.route_vacate));
-        SKM_HIP(hipGetLastError());
-        SKM_HIP(hipMemcpyAsync(cnt, d_cnt.p, sizeof(cnt), hipMemcpyDeviceToHost, b->stream));
-        SKM_HIP(hipStreamSynchronize(b->stream));
-        uint64_t m = 0, late = 0;
-        for (int p = 0; p < (1 << pb); ++p) m = std::max<uint64_t>(m, cnt[p]);
-        for (int p = (1 << pb) - R; p < (1 << pb); ++p) late += cnt[p];
-        b->pass_max = m;
-        b->routed = natural_late - late;
-        b->route = true;
-    }
+    b->cnt64.assign(cnt, cnt + 64);
     SKM_CHECK(b->pass_max < (1ull << 32), SKM_E_ARG, "more than 2^32 occurrences in one pass of one GPU shard");
 }
 
@@ -5178,25 +5184,131 @@ void size_arena(skm_build* b) {
 void alloc_caps(skm_build* b);
 void pass_peer_counts(const Ranks& bs);
 
+// Heavy-key routing plan, after the ranks agreed on the pass count (one GPU: at least 4 passes;
+// world > 1: at least 2).  Every rank sketches 1/64 of its windows into a count-min sketch; at
+// world > 1 the sketches are summed over the ranks (all-reduce, 32 MB), so a key's estimate is
+// its global occurrence count and every owner's first passes receive the same heavy keys.  The
+// keys whose estimate reaches route_heavy_min / 64 (15 % slack) set their two filter bits; the
+// ranks' filters are OR-ed (all-reduce max over bytes) and packed into the 64 KB bit filter
+// k_pass_ids consults.  The routed pass sizes are then re-checked against the memory budget and
+// the 32-bit slack the pass count was chosen for: a shard whose routed largest pass
+// no longer fits turns routing off on every rank (the ranks must route alike).
+void route_plan(const Ranks& bs) {
+    skm_build* b0 = bs[0];
+    const int pb = b0->pass_bits, W = b0->world;
+    for (auto* b : bs) {
+        b->route = false;
+        b->routed = 0;
+    }
+    uint64_t want = (pb >= (W > 1 ? 1 : 2) && b0->tune.route_heavy_min > 0) ? 1u : 0u;
+    {   // the option is per handle: route only if every rank asks for it
+        std::vector<uint64_t> mine(bs.size(), want);
+        for (size_t k = 0; k < bs.size(); ++k) mine[k] = (pb >= (W > 1 ? 1 : 2) && bs[k]->tune.route_heavy_min > 0) ? 1u : 0u;
+        const std::vector<uint64_t> all = W > 1 ? allgather_u64(bs, mine) : mine;
+        for (auto v : all) want &= v;
+    }
+    if (!want) return;
+    const size_t ncms = 2ull << CMS_BITS, nbl = 1ull << BLOOM_BITS;
+    std::vector<DevBuf> cms(bs.size()), bl8(bs.size());
+    std::vector<void*> pc, pb8;
+    for (size_t k = 0; k < bs.size(); ++k) {
+        skm_build* b = bs[k];
+        cms[k].ensure(4 * ncms);
+        bl8[k].ensure(nbl);
+        SKM_HIP(hipMemsetAsync(cms[k].p, 0, 4 * ncms, b->stream));
+        SKM_HIP(hipMemsetAsync(bl8[k].p, 0, nbl, b->stream));
+        if (b->rp)
+            hipLaunchKernelGGL(k_route_sketch, dim3(2048), dim3(256), 0, b->stream, b->d_res.as<uint8_t>(), b->rp,
+                               cms[k].as<uint32_t>(), 0u, nullptr);
+        SKM_HIP(hipGetLastError());
+        pc.push_back(cms[k].p);
+        pb8.push_back(bl8[k].p);
+    }
+    if (W > 1) allreduce(bs, pc, ncms, Red::SumU32);
+    for (size_t k = 0; k < bs.size(); ++k) {
+        skm_build* b = bs[k];
+        const uint32_t thresh =
+            std::max<uint32_t>(8, (uint32_t)(((uint64_t)b->tune.route_heavy_min >> ROUTE_SAMPLE) * 85 / 100));
+        if (b->rp)
+            hipLaunchKernelGGL(k_route_sketch, dim3(2048), dim3(256), 0, b->stream, b->d_res.as<uint8_t>(), b->rp,
+                               cms[k].as<uint32_t>(), thresh, bl8[k].as<uint8_t>());
+        SKM_HIP(hipGetLastError());
+    }
+    if (W > 1) allreduce(bs, pb8, nbl, Red::MaxU8);
+    std::vector<uint64_t> ok(bs.size(), 1);
+    std::vector<uint64_t> routed_m(bs.size()), routed_n(bs.size());
+    for (size_t k = 0; k < bs.size(); ++k) {
+        skm_build* b = bs[k];
+        b->d_bloom.ensure(nbl / 8);
+        hipLaunchKernelGGL(k_bloom_pack, dim3((uint32_t)(nbl / 32 + 255) / 256), dim3(256), 0, b->stream,
+                           bl8[k].as<uint8_t>(), b->d_bloom.as<uint32_t>());
+        // the routed pass sizes of this shard
+        const uint32_t P = 1u << pb;
+        DevBuf d_cnt;
+        d_cnt.ensure(8 * 64);
+        SKM_HIP(hipMemsetAsync(d_cnt.p, 0, 8 * 64, b->stream));
+        if (b->rp)
+            hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 4u * 64 + (uint32_t)(nbl / 8), b->stream,
+                               b->d_res.as<uint8_t>(), b->rp, pb, 0, nullptr, d_cnt.as<unsigned long long>(),
+                               b->d_bloom.as<uint32_t>(), 64u, nullptr, 0, (uint32_t)std::max(0, b->tune.route_vacate));
+        SKM_HIP(hipGetLastError());
+        uint64_t cnt[64];
+        SKM_HIP(hipMemcpyAsync(cnt, d_cnt.p, sizeof(cnt), hipMemcpyDeviceToHost, b->stream));
+        SKM_HIP(hipStreamSynchronize(b->stream));
+        const int R = b->tune.route_vacate > 0 ? std::min(b->tune.route_vacate, (int)P - 1) : (int)(P >> 1);
+        uint64_t natural_late = 0, late = 0, m = 0;  // occurrences of the vacated passes before / after routing
+        for (int p = (int)P - R; p < (int)P; ++p) {
+            for (int i = 0; i < (64 >> pb); ++i) natural_late += b->cnt64[p * (64 >> pb) + i];
+            late += cnt[p];
+        }
+        for (uint32_t p = 0; p < P; ++p) m = std::max<uint64_t>(m, cnt[p]);
+        size_t fr = 0, tot = 0;
+        SKM_HIP(hipMemGetInfo(&fr, &tot));
+        const uint64_t budget = b->tune.mem_budget_mb > 0 ? (uint64_t)b->tune.mem_budget_mb << 20 : (uint64_t)fr;
+        const bool forced = b->tune.passes > 0;
+        ok[k] = m < (1ull << 32) - (1ull << 28) && (forced || m <= b->pass_max || m * PASS_BYTES + b->rp <= budget / 2);
+        routed_m[k] = m;
+        routed_n[k] = natural_late - late;
+    }
+    {
+        const std::vector<uint64_t> all = W > 1 ? allgather_u64(bs, ok) : ok;
+        for (auto v : all)
+            if (!v) return;  // routing off on every rank: the unrouted pass sizes stand
+    }
+    for (size_t k = 0; k < bs.size(); ++k) {
+        bs[k]->pass_max = routed_m[k];
+        bs[k]->routed = routed_n[k];
+        bs[k]->route = true;
+    }
+}
+
 void prepare(const Ranks& bs) {
     bool need = false;
     for (auto* b : bs) need |= !b->prepared;
     if (!need) return;
-    for (auto* b : bs) {
-        prepare_local(b);
-        size_passes(b);
-    }
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (auto* b : bs) prepare_local(b);
+    for (auto* b : bs) SKM_HIP(hipStreamSynchronize(b->stream));
+    const auto t1 = clk::now();
+    for (auto* b : bs) size_passes(b);
     {   // every rank runs the same passes
         std::vector<uint64_t> mine;
         for (auto* b : bs) mine.push_back((uint64_t)b->pass_bits);
         const std::vector<uint64_t> all = bs[0]->world > 1 ? allgather_u64(bs, mine) : mine;
         uint64_t pb = 0;
         for (auto v : all) pb = std::max(pb, v);
-        for (auto* b : bs) {
+        for (auto* b : bs)
             if ((uint64_t)b->pass_bits != pb) size_passes(b, (int)pb);
-            size_local(b);
-        }
+        route_plan(bs);
+        for (auto* b : bs) SKM_HIP(hipStreamSynchronize(b->stream));
     }
+    const auto t2 = clk::now();
+    for (auto* b : bs) {
+        b->prep_upload_s = std::chrono::duration<double>(t1 - t0).count();
+        b->prep_plan_s = std::chrono::duration<double>(t2 - t1).count();
+    }
+    for (auto* b : bs) size_local(b);
     skm_build* b0 = bs[0];
     if (b0->world == 1) {
         b0->s_base = 0;
@@ -5289,6 +5401,7 @@ void prepare(const Ranks& bs) {
         b->prepared = true;
         b->ran = false;
     }
+    for (auto* b : bs) b->prep_rest_s = std::chrono::duration<double>(clk::now() - t2).count();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -5490,9 +5603,11 @@ void pass_peer_counts(const Ranks& bs) {
         DevBuf cnt;
         cnt.ensure(8ull * P * W);
         SKM_HIP(hipMemsetAsync(cnt.p, 0, 8ull * P * W, b->stream));
-        if (b->rp)
-            hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 4u * P * W, b->stream, b->d_res.as<uint8_t>(), b->rp,
-                               b->pass_bits, b->owner_bits, nullptr, cnt.as<unsigned long long>(), nullptr, P * W);
+        if (b->rp)  // by routed pass id when routing (route_plan)
+            hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 4u * P * W + (b->route ? (1u << BLOOM_BITS) / 8 : 0u),
+                               b->stream, b->d_res.as<uint8_t>(), b->rp, b->pass_bits, b->owner_bits, nullptr,
+                               cnt.as<unsigned long long>(), b->route ? b->d_bloom.as<uint32_t>() : nullptr, P * W,
+                               nullptr, 0, (uint32_t)std::max(0, b->tune.route_vacate));
         SKM_HIP(hipGetLastError());
         std::vector<uint64_t> c(P * W), t(P * W);
         SKM_HIP(hipMemcpyAsync(c.data(), cnt.p, 8ull * P * W, hipMemcpyDeviceToHost, b->stream));
@@ -6025,9 +6140,9 @@ void flush_long_chains(skm_build* b, int slot) {
         hipStream_t lst = b->lane_st[ls];
         SKM_HIP(hipStreamWaitEvent(lst, b->chain_ev[0], 0));
         unsigned long long* q = chain_queue(b, lst);
-        SKM_LAUNCH_AS(b, "k_chains_stash", k_chains, dim3((uint32_t)std::max(1, b->tune.lane_grid)), dim3(256), 0, lst,
-                   b->d_long_jobs.as<Job>(), rng, rng + 1, b->long_jobs_cap, nullptr, nullptr, nullptr, nullptr,
-                   b->d_data.as<skm_stored_kmer_data>(), lane_max, q);
+        SKM_LAUNCH(b, k_chains_stash, dim3((uint32_t)std::max(1, b->tune.lane_grid)), dim3(256), 0, lst,
+                   b->d_long_jobs.as<Job>(), rng, rng + 1, b->long_jobs_cap, b->d_data.as<skm_stored_kmer_data>(),
+                   lane_max, q);
         b->lane_used[ls] = true;
     }
     SKM_HIP(hipGetLastError());
@@ -6150,7 +6265,9 @@ void run_once(const Ranks& bs) {
             phase_group(b, pass);
             // the stashed long chains leave in batches (default two: the first half's chains
             // overlap the second half); the last batch runs after the last pass (phase_stats)
-            const uint32_t nb = std::min<uint32_t>(P >= 4 ? (uint32_t)std::max(1, b->tune.chain_batches) : 1u, 16u);
+            // (two passes -- the world > 1 shape with routing -- flush after the first: the routed
+            // heavy keys' chains then run beside the second pass instead of after it)
+            const uint32_t nb = std::min<uint32_t>(P >= 2 ? std::min<uint32_t>(P, (uint32_t)std::max(1, b->tune.chain_batches)) : 1u, 16u);
             const uint32_t per = std::max<uint32_t>(1u, P / nb);
             if (nb > 1 && (pass + 1) % per == 0 && pass + 1 < P) {
                 drain_overflow(b);  // the snapshot takes every stash issued so far, complete
@@ -6275,31 +6392,75 @@ int skm_build_add_batch(skm_build* b, const uint8_t* residues, const uint64_t* s
     SKM_CHECK(b, SKM_E_ARG, "null build");
     SKM_CHECK(n_seqs == 0 || (residues && seq_off && seq_len && seq_func), SKM_E_ARG, "null array");
     SKM_HIP(hipSetDevice(b->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    // the batch's kept sequences (signature_build.tcc:155-158 skips the others), validated
+    std::vector<uint32_t>& ks = b->h_keep;
+    ks.clear();
     for (size_t s = 0; s < n_seqs; ++s) {
         const uint16_t f = seq_func[s];
-        if (f == SKM_UNDEFINED_FUNCTION) continue;  // signature_build.tcc:155-158
+        if (f == SKM_UNDEFINED_FUNCTION) continue;
         SKM_CHECK(f < b->opts.n_functions, SKM_E_ARG, "seq_func out of range");
-        const uint32_t len = seq_len[s];
-        SKM_CHECK(len < (1u << ELEM_I_BITS), SKM_E_ARG, "protein longer than 1,048,575 residues");
-        SeqMeta m;
-        m.pstart = b->rp_total;
-        m.len = len;
-        m.func = f;
-        m.pad = 0;
-        if (b->st_fill[b->st_cur] + len + 1 > STAGE_BYTES) stage_flush(b);
-        uint8_t* dst = b->st_pin[b->st_cur] + b->st_fill[b->st_cur];
-        std::memcpy(dst, residues + seq_off[s], len);
-        dst[len] = 0;
-        b->st_fill[b->st_cur] += len + 1;
-        b->rp_total += len + 1;
-        const uint32_t sid = seq_id ? seq_id[s] : (uint32_t)b->h_meta.size();
-        if (!b->h_seqid.empty() && sid <= b->h_seqid.back()) b->seqid_strict = false;
-        b->h_meta.push_back(m);
-        b->h_seqid.push_back(sid);
-        if (len >= 8) b->n_windows += len - 7;
+        SKM_CHECK(seq_len[s] < (1u << ELEM_I_BITS), SKM_E_ARG, "protein longer than 1,048,575 residues");
+        ks.push_back((uint32_t)s);
+    }
+    b->h_meta.reserve(b->h_meta.size() + ks.size());
+    b->h_seqid.reserve(b->h_seqid.size() + ks.size());
+    // Segments that fit the current pinned staging buffer: their metadata in order (one thread),
+    // their residues copied by the host pool in byte-balanced parts (the packing used to be one
+    // memcpy per sequence on one thread, ~2 GB/s: 8 s of a C3 one-shot build); the DMA of the
+    // other staging buffer overlaps.
+    if (!b->pool) b->pool.reset(new HostPool(HostPool::default_threads()));
+    std::vector<uint64_t>& cum = b->h_cum;
+    size_t i = 0;
+    while (i < ks.size()) {
+        const size_t room = STAGE_BYTES - b->st_fill[b->st_cur];
+        size_t j = i;
+        uint64_t bytes = 0;
+        cum.clear();
+        while (j < ks.size() && bytes + seq_len[ks[j]] + 1 <= room) {
+            cum.push_back(bytes);
+            bytes += seq_len[ks[j]] + 1;
+            ++j;
+        }
+        if (j == i) {  // the buffer is full: hand it to the DMA engine
+            stage_flush(b);
+            continue;
+        }
+        cum.push_back(bytes);
+        for (size_t k = i; k < j; ++k) {
+            const uint32_t s = ks[k];
+            SeqMeta m;
+            m.pstart = b->rp_total + cum[k - i];
+            m.len = seq_len[s];
+            m.func = seq_func[s];
+            m.pad = 0;
+            const uint32_t sid = seq_id ? seq_id[s] : (uint32_t)b->h_meta.size();
+            if (!b->h_seqid.empty() && sid <= b->h_seqid.back()) b->seqid_strict = false;
+            b->h_meta.push_back(m);
+            b->h_seqid.push_back(sid);
+            if (m.len >= 8) b->n_windows += m.len - 7;
+        }
+        uint8_t* base = b->st_pin[b->st_cur] + b->st_fill[b->st_cur];
+        const int parts = bytes >= (1u << 20) ? std::min<int>(4 * b->pool->threads(), (int)(bytes >> 18)) : 1;
+        const size_t nseg = j - i;
+        b->pool->run(parts, [&](int p) {
+            const uint64_t lo = bytes * (uint64_t)p / (uint64_t)parts, hi = bytes * (uint64_t)(p + 1) / (uint64_t)parts;
+            const size_t a = (size_t)(std::lower_bound(cum.begin(), cum.begin() + nseg, lo) - cum.begin());
+            const size_t e = (size_t)(std::lower_bound(cum.begin(), cum.begin() + nseg, hi) - cum.begin());
+            for (size_t k = a; k < e; ++k) {
+                const uint32_t s = ks[i + k];
+                uint8_t* dst = base + cum[k];
+                std::memcpy(dst, residues + seq_off[s], seq_len[s]);
+                dst[seq_len[s]] = 0;
+            }
+        });
+        b->st_fill[b->st_cur] += bytes;
+        b->rp_total += bytes;
+        i = j;
     }
     b->prepared = false;
     b->ran = false;
+    b->add_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     SKM_API_END
 }
 
@@ -6706,12 +6867,14 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
-    const uint64_t v[26] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+    auto us = [](double sec) { return (uint64_t)(sec * 1e6); };
+    const uint64_t v[30] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
                             b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total,
                             b->giant_jobs, b->giant_max, b->n_redo, b->tot_cap, b->split_cap, b->long_cap,
                             b->long_jobs_cap, b->demand[0], b->demand[1], b->demand[2], b->demand[3],
-                            b->long_samples, b->routed};
-    int n = std::min(cap, 26);
+                            b->long_samples, b->routed, us(b->add_s), us(b->prep_upload_s), us(b->prep_plan_s),
+                            us(b->prep_rest_s)};
+    int n = std::min(cap, 30);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }

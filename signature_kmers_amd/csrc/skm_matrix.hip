@@ -568,36 +568,31 @@ __device__ __forceinline__ uint64_t md_first_ge(const uint64_t* __restrict__ com
     return a;
 }
 
-// cnt[b * G + g]: members group g sends to band b -- its suffix from band b's first row, when a
+// cnt[g]: members group g sends to band b -- its suffix from band b's first row, when a
 // member of the band has a partner after it; 0 otherwise
 __global__ void k_md_route_count(const uint64_t* __restrict__ comp, const uint64_t* __restrict__ segstart,
-                                 uint64_t G, uint64_t idx_mask, const uint32_t* __restrict__ band, uint32_t W,
+                                 uint64_t G, uint64_t idx_mask, const uint32_t* __restrict__ band, uint32_t b,
                                  uint32_t* __restrict__ cnt) {
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t a = segstart[g], e = segstart[g + 1];
-        for (uint32_t b = 0; b < W; ++b) {
-            const uint64_t f = md_first_ge(comp, a, e, idx_mask, band[b]);
-            const bool send = f + 1 < e && (comp[f] & idx_mask) < band[b + 1];
-            cnt[(uint64_t)b * G + g] = send ? (uint32_t)(e - f) : 0u;
-        }
+        const uint64_t f = md_first_ge(comp, a, e, idx_mask, band[b]);
+        const bool send = f + 1 < e && (comp[f] & idx_mask) < band[b + 1];
+        cnt[g] = send ? (uint32_t)(e - f) : 0u;
     }
 }
 
-// the members of each group for each band, as (gid << idx_bits | index) with gid = gbase + g
+// the members of each group for band b, as (gid << idx_bits | index) with gid = gbase + g
 // (globally increasing in source-rank order: the receiver's composites are already sorted)
 __global__ void k_md_route_fill(const uint64_t* __restrict__ comp, const uint64_t* __restrict__ segstart, uint64_t G,
-                                uint64_t idx_mask, uint32_t idx_bits, const uint32_t* __restrict__ band, uint32_t W,
-                                const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ off,
-                                const uint64_t* __restrict__ sbase, uint64_t gbase, uint64_t* __restrict__ out) {
+                                uint64_t idx_mask, uint32_t idx_bits, const uint32_t* __restrict__ cnt,
+                                const uint64_t* __restrict__ off, uint64_t gbase, uint64_t* __restrict__ out) {
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = cnt[g];
+        if (!c) continue;
         const uint64_t e = segstart[g + 1];
-        for (uint32_t b = 0; b < W; ++b) {
-            const uint32_t c = cnt[(uint64_t)b * G + g];
-            if (!c) continue;
-            uint64_t* dst = out + sbase[b] + off[(uint64_t)b * (G + 1) + g];
-            const uint64_t f = e - c;
-            for (uint32_t j = 0; j < c; ++j) dst[j] = ((gbase + g) << idx_bits) | (comp[f + j] & idx_mask);
-        }
+        uint64_t* dst = out + off[g];
+        const uint64_t f = e - c;
+        for (uint32_t j = 0; j < c; ++j) dst[j] = ((gbase + g) << idx_bits) | (comp[f + j] & idx_mask);
     }
 }
 
@@ -623,7 +618,7 @@ struct skm_matrix {
 #if defined(SKM_WITH_RCCL)
     ncclComm_t comm = nullptr;
 #endif
-    DevBuf d_ocnt, d_skey, d_sidx, d_band, d_rtc, d_rto, d_sbase, d_send, d_xbuf;
+    DevBuf d_ocnt, d_skey, d_sidx, d_band, d_rtc, d_rto, d_send, d_xbuf;
     uint64_t n_local_hits = 0, n_routed = 0;
     uint32_t band_lo = 0, band_hi = 0;
 };
@@ -823,26 +818,34 @@ uint64_t md_exchange(skm_matrix* M, uint64_t n_local, uint32_t idx_bits, hipStre
     const uint64_t idx_mask = (1ull << idx_bits) - 1;
     std::vector<uint64_t> bc(W, 0), bo(W, 0);
     if (G) {
-        M->d_rtc.ensure(4ull * W * G);
-        M->d_rto.ensure(8ull * W * (G + 1));
+        // one band at a time over G-sized count / offset buffers (a dense W x G table grew with the
+        // world size times the owned groups -- ADVICE r03): the bands' totals first, then the fill
+        M->d_rtc.ensure(4ull * G);
+        M->d_rto.ensure(8ull * (G + 1));
         const uint32_t gg = (uint32_t)std::min<uint64_t>(ceil_div(G, 256), 256ull * 32);
-        hipLaunchKernelGGL(k_md_route_count, dim3(gg), dim3(256), 0, st, M->d_comp.as<uint64_t>(), M->d_seg.as<uint64_t>(),
-                           G, idx_mask, M->d_band.as<uint32_t>(), (uint32_t)W, M->d_rtc.as<uint32_t>());
-        SKM_HIP(hipGetLastError());
-        for (int q = 0; q < W; ++q)
-            M->scan.run(M->d_rtc.as<uint32_t>() + (uint64_t)q * G, G, M->d_rto.as<uint64_t>() + (uint64_t)q * (G + 1), st);
-        for (int q = 0; q < W; ++q)
-            SKM_HIP(hipMemcpyAsync(&bc[q], M->d_rto.as<uint64_t>() + (uint64_t)q * (G + 1) + G, 8, hipMemcpyDeviceToHost, st));
-        SKM_HIP(hipStreamSynchronize(st));
+        auto count_band = [&](int q) {
+            hipLaunchKernelGGL(k_md_route_count, dim3(gg), dim3(256), 0, st, M->d_comp.as<uint64_t>(),
+                               M->d_seg.as<uint64_t>(), G, idx_mask, M->d_band.as<uint32_t>(), (uint32_t)q,
+                               M->d_rtc.as<uint32_t>());
+            SKM_HIP(hipGetLastError());
+            M->scan.run(M->d_rtc.as<uint32_t>(), G, M->d_rto.as<uint64_t>(), st);
+        };
+        for (int q = 0; q < W; ++q) {
+            count_band(q);
+            SKM_HIP(hipMemcpyAsync(&bc[q], M->d_rto.as<uint64_t>() + G, 8, hipMemcpyDeviceToHost, st));
+            SKM_HIP(hipStreamSynchronize(st));
+        }
         for (int q = 1; q < W; ++q) bo[q] = bo[q - 1] + bc[q - 1];
         const uint64_t tot = bo[W - 1] + bc[W - 1];
         M->d_send.ensure(8 * std::max<uint64_t>(tot, 1));
-        M->d_sbase.ensure(8ull * W);
-        SKM_HIP(hipMemcpyAsync(M->d_sbase.p, bo.data(), 8ull * W, hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_md_route_fill, dim3(gg), dim3(256), 0, st, M->d_comp.as<uint64_t>(), M->d_seg.as<uint64_t>(),
-                           G, idx_mask, idx_bits, M->d_band.as<uint32_t>(), (uint32_t)W, M->d_rtc.as<uint32_t>(),
-                           M->d_rto.as<uint64_t>(), M->d_sbase.as<uint64_t>(), gbase, M->d_send.as<uint64_t>());
-        SKM_HIP(hipGetLastError());
+        for (int q = 0; q < W; ++q) {
+            if (!bc[q]) continue;
+            count_band(q);
+            hipLaunchKernelGGL(k_md_route_fill, dim3(gg), dim3(256), 0, st, M->d_comp.as<uint64_t>(),
+                               M->d_seg.as<uint64_t>(), G, idx_mask, idx_bits, M->d_rtc.as<uint32_t>(),
+                               M->d_rto.as<uint64_t>(), gbase, M->d_send.as<uint64_t>() + bo[q]);
+            SKM_HIP(hipGetLastError());
+        }
         SKM_HIP(hipStreamSynchronize(st));
     } else {
         M->d_send.ensure(8);

@@ -1,0 +1,92 @@
+// skm_pool.h -- a fixed pool of host threads (the host side of a one-shot build
+// must not be one thread).  run(n, f) calls f(0..n-1) on the pool's threads and the caller's,
+// parts taken from an atomic counter, and returns when every part is done.  One run at a time
+// (one build handle is driven from one host thread, include/skm.h).
+#pragma once
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace skm {
+
+class HostPool {
+public:
+    // threads including the caller: SKM_HOST_THREADS, else min(16, hardware threads) -- the GPU
+    // box's cgroup quota is 16 CPUs while nproc shows the whole machine
+    static int default_threads() {
+        if (const char* e = std::getenv("SKM_HOST_THREADS")) {
+            const int v = std::atoi(e);
+            if (v > 0) return std::min(v, 256);
+        }
+        const unsigned hw = std::thread::hardware_concurrency();
+        return (int)std::max(1u, std::min(16u, hw ? hw : 1u));
+    }
+    explicit HostPool(int threads) {
+        for (int i = 1; i < threads; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    HostPool(const HostPool&) = delete;
+    HostPool& operator=(const HostPool&) = delete;
+    int threads() const { return (int)th_.size() + 1; }
+
+    void run(int n, std::function<void(int)> f) {
+        if (th_.empty() || n <= 1) {
+            for (int p = 0; p < n; ++p) f(p);
+            return;
+        }
+        {
+            std::unique_lock<std::mutex> l(m_);
+            done_.wait(l, [&] { return active_ == 0; });  // a late waker of the last run has left
+            job_ = std::move(f);
+            parts_ = n;
+            next_.store(0);
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> l(m_);
+        done_.wait(l, [&] { return active_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    void work() {
+        for (int p; (p = next_.fetch_add(1)) < parts_;) job_(p);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> l(m_);
+        for (;;) {
+            cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            ++active_;
+            l.unlock();
+            work();
+            l.lock();
+            if (--active_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    std::function<void(int)> job_;
+    std::atomic<int> next_{0};
+    int parts_ = 0, active_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+}  // namespace skm

@@ -132,7 +132,9 @@ int main(int argc, char** argv) {
         die(skm_last_error());
     skm_transport tp = mesh.transport();
     if (ng > 1) {
-        const std::string comm = op.get("comm", "rccl");
+        // RCCL cannot put several ranks on one GPU: --same-device defaults to the host transport
+        const std::string comm = op.get("comm", op.has("same-device") ? "host" : "rccl");
+        if (comm == "rccl" && op.has("same-device")) die("--comm rccl needs one GPU per rank (drop --same-device)");
         if (comm == "host") {
             if (skm_matrix_set_transport(m, mesh.rank, ng, &tp)) die(skm_last_error());
         } else if (comm == "rccl") {
@@ -151,7 +153,25 @@ int main(int argc, char** argv) {
     if (skm_matrix_run(m, &mo)) die(skm_last_error());
     uint64_t ctr[5] = {0, 0, 0, 0, 0};
     skm_matrix_counters(m, ctr, 5);
-    if (mesh.rank == 0) std::cerr << "kmer_hit_map size " << ctr[4] << "\n";
+    // ctr[4] counts the k-mers this rank owns (each k-mer has one owner): the ranks send theirs to
+    // rank 0 ahead of their pair bands, so the line prints the whole map's size as one process does
+    // (kmers-matrix-distance.cc:169)
+    uint64_t hit_map = ctr[4];
+    if (mesh.rank != 0) {
+        if (write(mesh.fd[0], &hit_map, 8) != 8) die("write to rank 0 failed");
+    } else {
+        for (int q = 1; q < ng; ++q) {
+            uint64_t v = 0;
+            size_t got = 0;
+            while (got < 8) {
+                const ssize_t r = read(mesh.fd[q], reinterpret_cast<char*>(&v) + got, 8 - got);
+                if (r <= 0) die("read from rank " + std::to_string(q) + " failed");
+                got += (size_t)r;
+            }
+            hit_map += v;
+        }
+        std::cerr << "kmer_hit_map size " << hit_map << "\n";
+    }
     skm_pairs pairs;
     if (skm_matrix_pairs(m, &pairs)) die(skm_last_error());
     if (mesh.rank == 0) std::cerr << "write output\n";

@@ -4,7 +4,8 @@ torch.distributed.run.  Modes:
          host transport, checked against numpy on the gathered inputs of every rank;
   build  rank r builds the r-th contiguous file range on cuda:0 (every rank shares the one GPU),
          exchanging through the gloo host transport; rank 0's kept set and statistics must equal
-         the oracle on the union (one pass and two key-range passes);
+         the oracle on the union (one pass, two key-range passes, and two / four with heavy-key
+         routing);
   matrix rank r looks up its range of the queries for kmers-matrix-distance, hits go to their
          k-mer's owner and groups to the row bands they touch over the gloo transport; the bands
          concatenated equal the oracle's pairs.
@@ -53,9 +54,11 @@ def build(skm, dist, rank, world):
     idx = np.nonzero(np.isin(p.file_of, files))[0]
     ref = oracle_ref.build(r, o, l, f, i, len(funcs)) if rank == 0 else None
     T = skm.GlooTransport()
-    for passes in (1, 2):
+    for passes, route in ((1, 0), (2, 0), (2, 64), (4, 64)):
+        # route > 0: heavy-key routing over the transport (summed sketches, OR-ed filters)
         b = skm.SignatureBuilder(len(funcs), device=0, rank=rank, world_size=world)
         b.set_option("key_range_passes", passes)
+        b.set_option("route_heavy_min", route)
         if len(idx):
             b.add_batch(r, o[idx], l[idx], f[idx], i[idx])
         b.set_transport(T)
