@@ -357,9 +357,9 @@ def _alg_bytes(kernel, c, res_bytes):
         "k_extract_stage_pos": res_bytes + 16 * valid,     # residues once + the element written
         "k_extract_stage": res_bytes + 16 * valid,
         "k_extract": res_bytes,
-        # per pass: the pass-id bytes of every window + the pass's positions written
-        "k_pass_select": res_bytes * max(1, c["passes"]) + 8 * valid,
-        "k_pass_ids": 2 * res_bytes,                       # residues read, one id byte written
+        # per group of passes: the residues once + the group's window positions written
+        "k_pass_emit": res_bytes * max(1, c.get("pass_groups", 1)) + 8 * valid,
+        "k_pass_ids": res_bytes,                           # the per-workgroup pass tally: residues read
         "k_overflow": 16 * c["overflow_elements"],
         "k_ovf_split": 32 * c["overflow_elements"],
         "k_heavy": 16 * c["overflow_elements"],

@@ -149,7 +149,9 @@ int skm_build_kernel_timings(skm_build* b, char* names, size_t names_cap, float*
  * [26]=host microseconds in skm_build_add_batch (all calls; the residues are packed by a pool of
  * host threads, SKM_HOST_THREADS or min(16, hardware threads)), and prepare's phases in
  * microseconds: [27] the residue / metadata upload, [28] the pass plan (device tallies of the pass
- * sizes, heavy-key routing sketch and filter), [29] allocations and the rest;
+ * sizes, heavy-key routing sketch and filter), [29] allocations and the rest; [30] residue scans
+ * per run that emit the key-range passes' window positions (k_pass_emit, one per group of up to
+ * four passes; 0 without key-range passes);
  * totals over the passes of the run; returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Host transport: the rank collectives of a multi-process build run by the caller on host
@@ -192,7 +194,8 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   sub-buckets at least this large are split into heavy keys + a light remainder),
  *   "giant_class" (heavy chains of >= 2^class samples start right after the heavy kernel on
  *   their own streams; 0 = off; default: 14 with one pass, off with key-range passes),
- *   "giant_passes", "prefetch" (the next pass's compaction during this pass's group-by, 1),
+ *   "giant_passes", "prefetch" (the next pass group's positions, k_pass_emit, during the group-by of the group's
+ *   last pass, 1),
  *   "overflow_grid" / "split_grid" / "chain_grid" (persistent-grid sizes), "stream_priority"
  *   (1: the group-by stream at the highest priority), "chain_batches" (key-range passes: the
  *   stashed long chains leave in this many batches, 4) / "chain_streams" (over 1..4 streams, 1),
@@ -205,8 +208,7 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   this many passes hold no routed heavy key, whose keys are spread over the others by hash;
  *   0 = the second half, mapped to pass - P/2), "stage_round" (key-range
  *   passes: 1 = the staged position scatter in half rounds of 2048 elements, four workgroups
- *   per CU, the default; 0 = rounds of 4096), "select_tile" (key-range passes: the pass
- *   selection's id loads per thread per tile, 1 = two (default), 0 = one), "partition_round"
+ *   per CU, the default; 0 = rounds of 4096), "partition_round"
  *   (k_partition staging rounds: 0 = 2048 elements, three 512-thread workgroups per CU (default);
  *   1 = 4096, one per CU; 2 = 4096, one 1024-thread workgroup per CU), "flag_check" (1: the
  *   group-by reads a sequence's signature flag before storing it; 0), "serial_overflow"

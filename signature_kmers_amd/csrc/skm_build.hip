@@ -1612,7 +1612,7 @@ __global__ void k_bloom_pack(const uint8_t* __restrict__ bloom8, uint32_t* __res
 // rows != nullptr (the run's ids, with pass_bits > 0): workgroup w takes the contiguous windows
 // [w * span, (w + 1) * span) (span a multiple of 16) and writes its windows per pass to
 // rows[w * ncnt + pass] -- k_sel_scan turns them into each workgroup's output offsets in every
-// pass's position list, so k_pass_select writes the positions in order without atomics.
+// pass's position list, so k_pass_emit writes the positions in order without atomics.
 __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ res, uint64_t rp, int pass_bits,
                                                   int owner_bits, uint8_t* __restrict__ ids,
                                                   unsigned long long* __restrict__ counts,
@@ -1675,7 +1675,7 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
             }
             out[t >> 2] |= id << (8 * (t & 3));
         }
-        if (!counts) *reinterpret_cast<uint4*>(ids + base) = make_uint4(out[0], out[1], out[2], out[3]);
+        if (!counts && ids) *reinterpret_cast<uint4*>(ids + base) = make_uint4(out[0], out[1], out[2], out[3]);
     }
     if (counts) {
         __syncthreads();
@@ -1688,7 +1688,7 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
     }
 }
 
-// Every pass's position list: workgroup w of k_pass_ids / k_pass_select writes its windows of
+// Every pass's position list: workgroup w of k_pass_ids / k_pass_emit writes its windows of
 // pass p at off[p * (nwg + 1) + w] (exclusive scan over w), npos[p] = the pass's window count
 // (checked against the list's capacity: a larger pass fails the run, SKM_E_STATE).  One workgroup
 // per pass.
@@ -1715,68 +1715,120 @@ __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ 
     }
 }
 
-// One pass's window positions, in position order, and the level-1 bucket histogram over them
-// (replaces a compaction + a separate count kernel): workgroup w reads the id bytes of its
-// windows tile by tile (each thread U consecutive 16-byte loads, the next tile's issued before
-// this tile's matches are processed), stages the tile's matches in LDS, writes them contiguously
-// at its precomputed offset, and hashes each matched window into an LDS histogram, merged into
-// the pass's global histogram once per workgroup.
-constexpr uint32_t SEL_THREADS = 256;
-template <uint32_t U>
-__global__ __launch_bounds__(SEL_THREADS) void k_pass_select(const uint8_t* __restrict__ ids,
-                                                            const uint8_t* __restrict__ res, uint64_t rp,
-                                                            uint64_t span, uint32_t pass,
-                                                            const uint64_t* __restrict__ off, uint64_t cap,
-                                                            uint64_t* __restrict__ pos, int rem_bits, uint32_t NB,
-                                                            uint32_t* __restrict__ hist) {
-    constexpr uint32_t TILE = SEL_THREADS * 16 * U;
-    static_assert(TILE <= 65536, "tile-relative positions are u16");
-    __shared__ uint16_t s_pos[TILE];       // tile-relative positions of the tile's matches
+// The window positions of a GROUP of G consecutive key-range passes, each pass's list in position
+// order, and each pass's level-1 bucket histogram (replaces round 3's per-pass k_pass_select,
+// which re-read every pass-id byte and every matched window's residues on each of the P passes:
+// 33 GB per pass at C3).  One residue scan per group: each workgroup takes the same contiguous
+// windows as k_pass_ids' tally (span, SEL_WG workgroups), hashes every window (heavy-key routing
+// as k_pass_ids), and per tile of 16 x EMIT_THREADS windows ranks the group's windows pass-major
+// by one flattened workgroup scan of the per-thread counts, so each pass's positions go out in
+// order at the workgroup's k_sel_scan offset; the G x NB histogram lives in LDS and is merged
+// once per workgroup.  Reads 1 B/residue per group, writes 8 B per window of the group.
+constexpr uint32_t EMIT_THREADS = 1024;
+constexpr uint32_t EMIT_LDS_WORDS = 16384;   // G x NB histogram words (64 KB): G = 16384 / NB, <= 4
+template <uint32_t G>
+__global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __restrict__ res, uint64_t rp, int pass_bits,
+                                                           uint32_t pass0, const uint32_t* __restrict__ bloom,
+                                                           uint32_t vac, uint64_t span,
+                                                           const uint64_t* __restrict__ seloff,
+                                                           uint64_t* __restrict__ pos, uint64_t cap, int rem_bits,
+                                                           uint32_t NB, uint32_t* __restrict__ hist) {
+    extern __shared__ uint32_t s_dyn[];
+    uint32_t* s_h = s_dyn;                 // [G][NB]
+    uint32_t* s_bloom = s_dyn + G * NB;    // (1 << BLOOM_BITS) / 32 words when routing
+    __shared__ uint32_t s_tab[G * EMIT_THREADS + 1];
     __shared__ uint32_t s_wave[17];
-    extern __shared__ uint32_t s_h[];      // [NB]
     const uint32_t tid = threadIdx.x;
-    for (uint32_t k = tid; k < NB; k += SEL_THREADS) s_h[k] = 0;
-    const uint64_t a = (uint64_t)blockIdx.x * span, e = min(rp, a + span);
-    uint64_t o = off[blockIdx.x];
-    uint4 nxt[U];
-    auto fetch = [&](uint64_t t0) {
+    for (uint32_t k = tid; k < G * NB; k += EMIT_THREADS) s_h[k] = 0;
+    const bool route = bloom != nullptr && pass_bits >= 1;
+    if (route)
+        for (uint32_t w = tid; w < (1u << BLOOM_BITS) / 32u; w += EMIT_THREADS) s_bloom[w] = bloom[w];
+    const uint32_t P = 1u << pass_bits, half = P >> 1;
+    const uint32_t R = vac ? min(vac, P - 1u) : half, keep = P - R;
+    uint64_t run[G];
 #pragma unroll
-        for (uint32_t u = 0; u < U; ++u) {
-            const uint64_t q = t0 + 16u * (U * tid + u);
-            nxt[u] = q < e ? *reinterpret_cast<const uint4*>(ids + q) : make_uint4(0u, 0u, 0u, 0u);
-        }
-    };
-    if (a < e) fetch(a);
+    for (uint32_t q = 0; q < G; ++q) run[q] = seloff[(uint64_t)(pass0 + q) * (SEL_WG + 1) + blockIdx.x];
     __syncthreads();
-    for (uint64_t t0 = a; t0 < e; t0 += TILE) {
-        uint32_t m[U], c = 0;
+    const uint64_t a = (uint64_t)blockIdx.x * span, e = min(rp, a + span);
+    for (uint64_t t0 = a; t0 < e; t0 += 16ull * EMIT_THREADS) {
+        const uint64_t base = t0 + 16ull * tid;
+        uint32_t qs[4] = {~0u, ~0u, ~0u, ~0u};  // byte t: the window's pass within the group (0xFF: none)
+        uint32_t cnt[G];
 #pragma unroll
-        for (uint32_t u = 0; u < U; ++u) {
-            const uint64_t q = t0 + 16u * (U * tid + u);
-            m[u] = 0;
-            if (q < e) {
-                m[u] = match16(nxt[u], pass);
-                if (e - q < 16) m[u] &= (1u << (uint32_t)(e - q)) - 1u;
+        for (uint32_t q = 0; q < G; ++q) cnt[q] = 0;
+        if (base < e) {
+            const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
+            const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
+            const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+            uint32_t code[24];
+            uint32_t valid = 0;
+#pragma unroll
+            for (int j = 0; j < 24; ++j) {
+                const uint32_t cd = residue_code((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+                valid |= (cd < 40u ? 1u : 0u) << j;
+                code[j] = cd < 40u ? cd : 0u;
             }
-            c += (uint32_t)__popc(m[u]);
-        }
-        if (t0 + TILE < e) fetch(t0 + TILE);
-        uint32_t tot;
-        uint32_t x = wg_exclusive_scan(c, s_wave, tot);
+            uint64_t k = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < U; ++u)
-            for (uint32_t w = m[u]; w; w &= w - 1) s_pos[x++] = (uint16_t)(16u * (U * tid + u) + (uint32_t)__ffs(w) - 1u);
-        __syncthreads();
-        for (uint32_t j = tid; j < tot; j += SEL_THREADS) {
-            const uint64_t p = t0 + s_pos[j];
-            if (o + j < cap) pos[o + j] = p;
-            const uint64_t h = window_hash(load_window(res, p));
-            atomicAdd(&s_h[(uint32_t)(h >> rem_bits) & (NB - 1)], 1u);
+            for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
+            constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
+                if (((valid >> t) & 0xFFu) == 0xFFu && base + t < e) {
+                    const uint64_t h = mix43(k);
+                    uint32_t id = (uint32_t)(h >> (KEY_BITS - pass_bits));
+                    if (route && id >= keep && bloom_has(s_bloom, h))
+                        id = R == half ? id - half : (uint32_t)(((uint32_t)(h & 0xFFFFu) * keep) >> 16);
+                    const uint32_t q = id - pass0;
+                    if (q < G) {
+                        atomicAdd(&s_h[q * NB + ((uint32_t)(h >> rem_bits) & (NB - 1))], 1u);
+#pragma unroll
+                        for (uint32_t j = 0; j < G; ++j) cnt[j] += q == j ? 1u : 0u;
+                        qs[t >> 2] &= ~(0xFFu << (8 * (t & 3)));
+                        qs[t >> 2] |= q << (8 * (t & 3));
+                    }
+                }
+            }
         }
-        o += tot;
+#pragma unroll
+        for (uint32_t q = 0; q < G; ++q) s_tab[q * EMIT_THREADS + tid] = cnt[q];
         __syncthreads();
+        {   // exclusive scan of s_tab in pass-major order; thread tid owns entries [G tid, G tid + G)
+            uint32_t loc[G], sum = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < G; ++j) {
+                loc[j] = s_tab[G * tid + j];
+                sum += loc[j];
+            }
+            uint32_t tot;
+            uint32_t ex = wg_exclusive_scan(sum, s_wave, tot);  // its barriers order the reads above
+#pragma unroll
+            for (uint32_t j = 0; j < G; ++j) {
+                s_tab[G * tid + j] = ex;
+                ex += loc[j];
+            }
+            if (tid == 0) s_tab[G * EMIT_THREADS] = tot;
+        }
+        __syncthreads();
+        uint32_t nxt[G];
+#pragma unroll
+        for (uint32_t q = 0; q < G; ++q) nxt[q] = s_tab[q * EMIT_THREADS + tid] - s_tab[q * EMIT_THREADS];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const uint32_t q = (qs[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+            if (q >= G) continue;
+            uint64_t o = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < G; ++j)
+                if (q == j) o = run[j] + nxt[j]++;
+            if (o < cap) pos[(uint64_t)q * cap + o] = base + (uint64_t)t;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < G; ++q) run[q] += s_tab[(q + 1) * EMIT_THREADS] - s_tab[q * EMIT_THREADS];
+        __syncthreads();  // s_tab is rewritten by the next tile
     }
-    for (uint32_t k = tid; k < NB; k += SEL_THREADS)
+    for (uint32_t k = tid; k < G * NB; k += EMIT_THREADS)
         if (s_h[k]) atomicAdd(&hist[k], s_h[k]);
 }
 
@@ -4384,7 +4436,7 @@ struct Tune {
     // would hide; giant_class())
     int giant_class = -1;
     int giant_passes = 0;            // giant chains only in the last N passes (0: all)
-    int prefetch = 1;                // next pass's compaction + count during this pass's group-by
+    int prefetch = 1;                // next pass group's positions (k_pass_emit) during this group-by
     int heavy_grid = (int)HEAVY_GRID; // persistent grids: k_heavy,
     int ovf_grid = 1024;             //   k_overflow (per stream),
     int split_grid = 512;            //   k_ovf_split,
@@ -4403,8 +4455,6 @@ struct Tune {
     int flag_check = 0;              // 1: k_bucket_process reads a signature flag before storing it
     int partition_round = 0;         // k_partition staging rounds: 0 = 2048 elements (three 512-thread
                                      //   workgroups per CU), 1 = 4096 (one), 2 = 4096 (one of 1024 threads)
-    int select_tile = 1;             // key-range passes: k_pass_select tiles of 2 (1) or 1 (0) 16-byte id
-                                     //   loads per thread, the next tile's loads ahead of this tile's work
     int stage_round = 1;             // key-range passes: 1 = the staged position scatter in half rounds
                                      //   (2048 elements, four workgroups per CU); 0 = full rounds
     // key-range passes: stashed long chains below this many samples run one lane each (k_chains,
@@ -4555,18 +4605,19 @@ struct skm_build {
     int pass_bits = 0;
     uint64_t pass_max = 0;              // valid windows of the largest pass (this shard)
     uint64_t valid_total = 0;           // valid windows of this shard
-    DevBuf d_ids;                       // per-window pass id (pass_bits > 0)
     DevBuf d_bloom;                     // heavy-key routing filter (route)
     std::vector<uint64_t> cnt64;        // valid windows by the top 6 hash bits (size_passes)
     bool route = false;
     uint64_t routed = 0;                // occurrences routed into the first half of the passes
-    // a pass's window positions, level-1 histogram matrix and window count, double-buffered: the
-    // next pass's compaction + count run on stx during this pass's group-by (prefetch_pass)
-    DevBuf d_pos2[2], d_hist2[2], d_npos;  // d_npos: every pass's window count (k_sel_scan)
+    // the window positions and level-1 histograms of a group of emit_g passes (k_pass_emit: one
+    // residue scan per group), in emit_g slots; the next group's scan runs on stx once the group's
+    // last pass has staged its elements (ev_staged), beside that pass's group-by
+    DevBuf d_posg, d_histg, d_npos;      // d_npos: every pass's window count (k_sel_scan)
+    uint32_t emit_g = 1;
     DevBuf d_selrows, d_seloff;          // per-workgroup windows of each pass, their scanned offsets
-    uint64_t sel_span = 0;               // windows per k_pass_ids / k_pass_select workgroup
+    uint64_t sel_span = 0;               // windows per k_pass_ids / k_pass_emit workgroup
     hipStream_t stx = nullptr;
-    hipEvent_t ev_pf_ready = nullptr, ev_pf_done[2] = {};
+    hipEvent_t ev_staged = nullptr, ev_emit = nullptr;
     // pipelined passes (option overlap, one GPU, key-range passes): a second element buffer set,
     // so that a pass's overflow path (streams 2/3, reading its buffers) overlaps the next pass's
     // extract / split / partition instead of closing the pass; per-set counter blocks, plans and
@@ -4576,7 +4627,7 @@ struct skm_build {
     DevBuf d_recs_hi2, d_recs_lo2, d_tmp_hi2, d_tmp_lo2, d_ovf2b;
     hipEvent_t ev_ovf_done[2] = {}, ev_main_done[2] = {};
     bool ovf_pending[2] = {false, false};
-    int64_t pf_pass = -1;               // the pass whose compaction + count are already queued
+    int64_t emit_q = -1;                // the group whose scan is queued on stx
     uint32_t pf_nwg = 1;                // count-kernel rows of the histogram matrix (pass mode)
     uint64_t pf_span = 0;
     uint64_t kept_cap = 0;              // kept k-mer arena (keys + records), shared by all passes
@@ -5135,17 +5186,16 @@ void size_local(skm_build* b) {
     b->d_recs_lo.ensure(8 * W);
     if (b->pass_bits > 0) {
         const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
-        for (int k = 0; k < (b->pass_bits ? 2 : 1); ++k) {
-            b->d_pos2[k].ensure(8 * W);
-            b->d_hist2[k].ensure(sizeof(uint32_t) * (uint64_t)NB);
-        }
         const uint32_t P = 1u << b->pass_bits;
+        b->emit_g = std::max<uint32_t>(1, std::min<uint32_t>({P, EMIT_LDS_WORDS / NB, 4u}));
+        b->d_posg.ensure(8 * W * b->emit_g);
+        b->d_histg.ensure(sizeof(uint32_t) * (uint64_t)NB * b->emit_g);
         b->d_npos.ensure(8ull * P);
         b->d_selrows.ensure(4ull * SEL_WG * P);
         b->d_seloff.ensure(8ull * P * (SEL_WG + 1));
         b->sel_span = ceil_div(ceil_div(std::max<uint64_t>(b->rp, 1), SEL_WG), 16) * 16;
         // count-kernel geometry from the largest pass (the kernels read the pass's own count)
-        // (the pass's histogram comes from k_pass_select: this grid is the staged scatter's alone;
+        // (the pass's histogram comes from k_pass_emit: this grid is the staged scatter's alone;
         // the half-round variant runs four workgroups per CU)
         const uint64_t stage_wg = b->tune.stage_round == 1 ? 4ull * EX_MAX_WG : EX_MAX_WG;
         uint32_t nwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(stage_wg, ceil_div(W, (uint64_t)SC_ROUND * 4)));
@@ -5156,8 +5206,6 @@ void size_local(skm_build* b) {
         b->d_offs.ensure(sizeof(uint32_t) * (uint64_t)EX_MAX_WG * NB);
         b->d_partial.ensure(sizeof(uint32_t) * (uint64_t)ceil_div(EX_MAX_WG, SCAN_ROWS) * NB);
         b->d_rbbase.ensure(sizeof(uint32_t) * (uint64_t)ceil_div(EX_MAX_WG, SCAN_ROWS) * NB);
-        b->d_ids.ensure(((b->rp + 15) & ~15ull) + 64);
-        SKM_HIP(hipMemsetAsync(b->d_ids.p, 0xFF, ((b->rp + 15) & ~15ull) + 64, b->stream));
     }
 }
 
@@ -5407,27 +5455,40 @@ void prepare(const Ranks& bs) {
 // ------------------------------------------------------------------------------------------
 // run: extract -> [exchange] -> group-by -> chains -> statistics [-> reductions]
 // ------------------------------------------------------------------------------------------
-// Key-range pass `pass`: its window positions (compaction of the id bytes) and the per-workgroup
-// level-1 histogram over them, into buffer set pass & 1, on stream `st` (no host round trip: the
-// kernels read the pass's window count on the device).
-void prefetch_pass(skm_build* b, uint32_t pass, hipStream_t st) {
-    const int k = pass & 1;
+// Key-range pass group g (passes g*G .. g*G+G-1): every pass's window positions and level-1
+// histogram into the G slots (k_pass_emit), on stream `st` (no host round trip: the offsets and
+// counts come from begin_run's tally and k_sel_scan on the device).
+void emit_group(skm_build* b, uint32_t g, hipStream_t st) {
+    const uint32_t G = b->emit_g;
     const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
-    SKM_HIP(hipMemsetAsync(b->d_hist2[k].p, 0, sizeof(uint32_t) * NB, st));
+    SKM_HIP(hipMemsetAsync(b->d_histg.p, 0, sizeof(uint32_t) * NB * G, st));
     const int rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
-    if (b->tune.select_tile == 0)
-        SKM_LAUNCH_AS(b, "k_pass_select", k_pass_select<1>, dim3(SEL_WG), dim3(SEL_THREADS), sizeof(uint32_t) * NB, st,
-                      b->d_ids.as<uint8_t>(), b->d_res.as<uint8_t>(), b->rp, b->sel_span, pass,
-                      b->d_seloff.as<uint64_t>() + (uint64_t)pass * (SEL_WG + 1), b->pass_max,
-                      b->d_pos2[k].as<uint64_t>(), rem_bits, NB, b->d_hist2[k].as<uint32_t>());
+    const uint32_t lds = 4u * G * NB + (b->route ? (1u << BLOOM_BITS) / 8 : 0u);
+    const uint32_t* bloom = b->route ? b->d_bloom.as<uint32_t>() : nullptr;
+    const uint32_t vac = (uint32_t)std::max(0, b->tune.route_vacate);
+    const uint64_t cap = std::max<uint64_t>(b->pass_max, 1);
+    // the histogram + Bloom filter can pass the 64 KB default dynamic-LDS limit (G = 4 with routing)
+    static bool lds_attr[3] = {false, false, false};
+    const int gi = G == 4 ? 2 : G == 2 ? 1 : 0;
+    if (lds > 65536 && !lds_attr[gi]) {
+        const void* fn = G == 4 ? reinterpret_cast<const void*>(k_pass_emit<4>)
+                         : G == 2 ? reinterpret_cast<const void*>(k_pass_emit<2>) : reinterpret_cast<const void*>(k_pass_emit<1>);
+        SKM_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u * EMIT_LDS_WORDS + (1u << BLOOM_BITS) / 8)));
+        lds_attr[gi] = true;
+    }
+#define SKM_EMIT(GG)                                                                                                    \
+    SKM_LAUNCH_AS(b, "k_pass_emit", k_pass_emit<GG>, dim3(SEL_WG), dim3(EMIT_THREADS), lds, st, b->d_res.as<uint8_t>(), \
+                  b->rp, b->pass_bits, g * G, bloom, vac, b->sel_span, b->d_seloff.as<uint64_t>(), b->d_posg.as<uint64_t>(), \
+                  cap, rem_bits, NB, b->d_histg.as<uint32_t>())
+    if (G == 4)
+        SKM_EMIT(4);
+    else if (G == 2)
+        SKM_EMIT(2);
     else
-        SKM_LAUNCH_AS(b, "k_pass_select", k_pass_select<2>, dim3(SEL_WG), dim3(SEL_THREADS), sizeof(uint32_t) * NB, st,
-                      b->d_ids.as<uint8_t>(), b->d_res.as<uint8_t>(), b->rp, b->sel_span, pass,
-                      b->d_seloff.as<uint64_t>() + (uint64_t)pass * (SEL_WG + 1), b->pass_max,
-                      b->d_pos2[k].as<uint64_t>(), rem_bits, NB, b->d_hist2[k].as<uint32_t>());
+        SKM_EMIT(1);
+#undef SKM_EMIT
     SKM_HIP(hipGetLastError());
-    if (st != b->stream) SKM_HIP(hipEventRecord(b->ev_pf_done[k], st));
-    b->pf_pass = pass;
+    if (st != b->stream) SKM_HIP(hipEventRecord(b->ev_emit, st));
 }
 
 // the element buffer set, counter block, plan and overflow list of a pass (set 0 unless overlap)
@@ -5458,7 +5519,7 @@ void phase_extract(skm_build* b, uint32_t pass) {
     X.pass_bits = b->pass_bits;
     X.pass_id = pass;
     X.pos_cap = b->pass_max;
-    X.ids = b->pass_bits ? b->d_ids.as<uint8_t>() : nullptr;
+    X.ids = nullptr;
     X.hist = b->d_hist.as<uint32_t>();
     X.offs = b->d_offs.as<uint32_t>();
     X.owner_start = b->d_owner_start.as<uint64_t>();
@@ -5469,15 +5530,17 @@ void phase_extract(skm_build* b, uint32_t pass) {
     X.out_lo = recs_lo(b, pass);
     uint32_t nwg = b->nwg, hist_rows = b->nwg;
     if (b->pass_bits) {
-        // this pass's window positions and count: queued on stx during the previous pass's
-        // group-by (prefetch_pass), or now for the run's first pass
-        const int k = pass & 1;
-        if (b->pf_pass == (int64_t)pass && pass > 0)
-            SKM_HIP(hipStreamWaitEvent(st, b->ev_pf_done[k], 0));
-        else
-            prefetch_pass(b, pass, st);
-        b->pf_pass = -1;
-        X.hist = b->d_hist2[k].as<uint32_t>();  // one row: k_pass_select's histogram of the pass
+        // this pass's window positions and histogram: its group's scan, queued on stx during the
+        // previous group's last group-by, or issued now (the run's first group)
+        const uint32_t G = b->emit_g, q = pass % G;
+        if (q == 0) {
+            if (b->emit_q == (int64_t)(pass / G))
+                SKM_HIP(hipStreamWaitEvent(st, b->ev_emit, 0));
+            else
+                emit_group(b, pass / G, st);
+            b->emit_q = -1;
+        }
+        X.hist = b->d_histg.as<uint32_t>() + (uint64_t)q * NB;  // one row: the pass's histogram
         X.span = b->pf_span;
         nwg = b->pf_nwg;
         hist_rows = 1;
@@ -5512,15 +5575,19 @@ void phase_extract(skm_build* b, uint32_t pass) {
                        b->d_cur0.as<unsigned long long>(), b->d_cur1.as<unsigned long long>(), b->d_slices.as<uint32_t>());
     if (b->pass_bits && b->tune.stage_round == 1)
         SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND_HALF, 4>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
-                   b->d_pos2[pass & 1].as<uint64_t>(), b->d_npos.as<unsigned long long>() + pass,
+                   b->d_posg.as<uint64_t>() + (uint64_t)(pass % b->emit_g) * std::max<uint64_t>(b->pass_max, 1),
+                   b->d_npos.as<unsigned long long>() + pass,
                    b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass));
     else if (b->pass_bits)
         SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND, 2>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
-                   b->d_pos2[pass & 1].as<uint64_t>(), b->d_npos.as<unsigned long long>() + pass,
+                   b->d_posg.as<uint64_t>() + (uint64_t)(pass % b->emit_g) * std::max<uint64_t>(b->pass_max, 1),
+                   b->d_npos.as<unsigned long long>() + pass,
                    b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass));
     else
         SKM_LAUNCH(b, k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
                            tmp_hi(b, pass), tmp_lo(b, pass));
+    // the group's slots are free once its last pass has staged its elements
+    if (b->pass_bits && pass % b->emit_g == b->emit_g - 1) SKM_HIP(hipEventRecord(b->ev_staged, st));
     const uint32_t nsl = (uint32_t)(ceil_div(b->pass_max, SC_SLICE) + (1u << SC_L0_BITS));
     SKM_LAUNCH(b, k_split_stage, dim3(nsl), dim3(EX_THREADS), 0, st, tmp_hi(b, pass),
                        tmp_lo(b, pass), b->d_bstart.as<uint64_t>(), nbits, b->d_slices.as<uint32_t>(),
@@ -5792,7 +5859,6 @@ void phase_group(skm_build* b, uint32_t pass) {
         SKM_LAUNCH_AS(b, "k_partition", (k_partition<2048, BP_THREADS, 3>), dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[10], st));
-    SKM_HIP(hipEventRecord(b->ev_pf_ready, st));
     // ---- the overflow plan (the pass's element count: the last bucket start, or the exchange's) ----
     const unsigned long long* nloc_d;
     if (multi) {  // the received element count: k_recv_plan's vstart[NB1]
@@ -5919,11 +5985,12 @@ void phase_group(skm_build* b, uint32_t pass) {
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[5], st));
     if (b->tune.serial_overflow) launch_overflow();
-    // the next pass's compaction + count overlap this pass's group-by on stx: its buffer set was
-    // last read by this pass's predecessor's extract, complete once this pass's partition is
-    if (b->pass_bits && pass + 1 < NP && b->tune.prefetch) {
-        SKM_HIP(hipStreamWaitEvent(b->stx, b->ev_pf_ready, 0));
-        prefetch_pass(b, pass + 1, b->stx);
+    // the next group's positions overlap this pass's group-by on stx (the group's slots were
+    // last read by this pass's staging)
+    if (b->pass_bits && pass + 1 < NP && (pass + 1) % b->emit_g == 0 && b->tune.prefetch) {
+        SKM_HIP(hipStreamWaitEvent(b->stx, b->ev_staged, 0));
+        emit_group(b, (pass + 1) / b->emit_g, b->stx);
+        b->emit_q = (pass + 1) / b->emit_g;
     }
     SKM_LAUNCH(b, k_big_groups<false>, dim3(2048), dim3(BIG_WG), 0, st, BA);
     SKM_LAUNCH(b, k_big_groups<true>, dim3(512), dim3(BIG_WG), 0, st, BA);
@@ -6052,8 +6119,9 @@ void begin_run(skm_build* b) {
                            b->d_data.as<skm_stored_kmer_data>());
     if (b->pass_bits) {
         const uint32_t P = 1u << b->pass_bits;
+        // every workgroup's windows per pass (the tally k_pass_emit's offsets come from)
         SKM_LAUNCH(b, k_pass_ids, dim3(SEL_WG), dim3(256), 4u * P + (b->route ? (1u << BLOOM_BITS) / 8 : 0u), st,
-                   b->d_res.as<uint8_t>(), b->rp, b->pass_bits, 0, b->d_ids.as<uint8_t>(), nullptr,
+                   b->d_res.as<uint8_t>(), b->rp, b->pass_bits, 0, nullptr, nullptr,
                    b->route ? b->d_bloom.as<uint32_t>() : nullptr, P, b->d_selrows.as<uint32_t>(), b->sel_span,
                    (uint32_t)std::max(0, b->tune.route_vacate));
         SKM_LAUNCH(b, k_sel_scan, dim3(P), dim3(1024), 0, st, b->d_selrows.as<uint32_t>(), SEL_WG, P,
@@ -6362,8 +6430,8 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
         SKM_HIP(hipEventCreateWithFlags(&b->lane_ev[k], hipEventDisableTiming));
     }
     SKM_HIP(hipStreamCreateWithFlags(&b->stx, hipStreamNonBlocking));
-    SKM_HIP(hipEventCreateWithFlags(&b->ev_pf_ready, hipEventDisableTiming));
-    for (auto& e : b->ev_pf_done) SKM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    SKM_HIP(hipEventCreateWithFlags(&b->ev_staged, hipEventDisableTiming));
+    SKM_HIP(hipEventCreateWithFlags(&b->ev_emit, hipEventDisableTiming));
     for (int g = 0; g < skm_build::GSLOTS; ++g) {
         SKM_HIP(hipStreamCreateWithFlags(&b->gst[g], hipStreamNonBlocking));
         SKM_HIP(hipEventCreateWithFlags(&b->gev_ready[g], hipEventDisableTiming));
@@ -6718,7 +6786,6 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "poison_jobs" ? &t.poison_jobs
                : n == "route_heavy_min" ? &t.route_heavy_min
                : n == "stage_round" ? &t.stage_round
-               : n == "select_tile" ? &t.select_tile
                : n == "partition_round" ? &t.partition_round
                : n == "flag_check" ? &t.flag_check
                : n == "diag" ? &t.diag
@@ -6868,13 +6935,13 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
     auto us = [](double sec) { return (uint64_t)(sec * 1e6); };
-    const uint64_t v[30] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+    const uint64_t v[31] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
                             b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total,
                             b->giant_jobs, b->giant_max, b->n_redo, b->tot_cap, b->split_cap, b->long_cap,
                             b->long_jobs_cap, b->demand[0], b->demand[1], b->demand[2], b->demand[3],
                             b->long_samples, b->routed, us(b->add_s), us(b->prep_upload_s), us(b->prep_plan_s),
-                            us(b->prep_rest_s)};
-    int n = std::min(cap, 30);
+                            us(b->prep_rest_s), b->pass_bits ? (1ull << b->pass_bits) / b->emit_g : 0ull};
+    int n = std::min(cap, 31);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }
@@ -7197,9 +7264,8 @@ void skm_build_destroy(skm_build* b) {
         (void)hipStreamSynchronize(b->stx);
         (void)hipStreamDestroy(b->stx);
     }
-    if (b->ev_pf_ready) (void)hipEventDestroy(b->ev_pf_ready);
-    for (auto& e : b->ev_pf_done)
-        if (e) (void)hipEventDestroy(e);
+    if (b->ev_staged) (void)hipEventDestroy(b->ev_staged);
+    if (b->ev_emit) (void)hipEventDestroy(b->ev_emit);
     if (b->chain_st) {
         (void)hipStreamSynchronize(b->chain_st);
         (void)hipStreamDestroy(b->chain_st);

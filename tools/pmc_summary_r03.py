@@ -29,7 +29,7 @@ def per_kernel(path, counter):
         if row["Counter_Name"] != counter:
             continue
         name = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("skm::", "")
-        for base in ("k_extract_stage_pos", "k_pass_select", "k_partition"):  # variants share one row (bench.py)
+        for base in ("k_extract_stage_pos", "k_pass_emit", "k_partition"):  # variants share one row (bench.py)
             if name.startswith(base + "<"):
                 name = base
         acc[name].append(float(row["Counter_Value"]))
