@@ -192,6 +192,8 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   "chain_prio", "bucket_prio", "chain_lds_kb", "host_timing",
  *   "heavy_min" (occurrences that send a k-mer to the heavy path), "split_min" (overflow
  *   sub-buckets at least this large are split into heavy keys + a light remainder),
+ *   "heavy_lsd" (1: every heavy k-mer through round 3's Boyer-Moore + LSD-sort path instead of
+ *   the one-read bucketed path; it is the fallback for > 4096 functions or crowded buckets),
  *   "giant_class" (heavy chains of >= 2^class samples start right after the heavy kernel on
  *   their own streams; 0 = off; default: 14 with one pass, off with key-range passes),
  *   "giant_passes", "prefetch" (the next pass group's positions, k_pass_emit, during the group-by of the group's

@@ -3636,6 +3636,8 @@ struct HeavyArgs {
     // by k_chain_dyn on a chain stream as soon as k_heavy ends (the pass's own lens buffer is
     // reused by the next pass; the slot's is not until its chains are done)
     uint32_t nosort;              // diagnostics (option diag & 2): the samples in member order
+    uint32_t fast;                // n_functions <= HV_FT: function counts in LDS, bucketed sample order
+    uint32_t n_total;             // sequences of the build (the bucket range of the sequence indices)
     uint32_t giant_min;           // 0: off
     uint32_t* gsamples;
     Job* gjobs;
@@ -3884,6 +3886,74 @@ __device__ uint32_t* wg_radix_sort_u32(uint32_t* a, uint32_t* b, uint32_t n, int
     return a;
 }
 
+// k_heavy's one-read statistics and bucketed sample order (round 4): the per-function counts of a
+// heavy key in an LDS table (exact best function, no Boyer-Moore + recount), and the best members'
+// (sequence index, length) items scattered into HV_NBK-way sequence-index buckets of <= HV_BCAP
+// items, each bucket sorted by one wave in registers -- instead of compacting sequence indices,
+// LSD-sorting them in three barrier-bound passes and gathering each member's length at random.
+constexpr uint32_t HV_FT = 4096;     // function table (n_functions <= HV_FT; else the Boyer-Moore path)
+constexpr uint32_t HV_NBK = 4096;    // sequence-index buckets per key (power of two <= HV_NBK)
+constexpr uint32_t HV_BCAP = 512;    // items one wave sorts (8 per lane); a larger bucket: the LSD path
+
+// Bitonic sort, descending, of 64 E items held E per lane (item i = e * 64 + lane).
+template <int E>
+__device__ __forceinline__ void wave_sort_desc(uint64_t (&v)[E]) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int k = 2; k <= 64 * E; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int pe = e ^ (j >> 6);
+                    if (pe > e) {
+                        const bool up = (((uint32_t)e * 64u + lane) & (uint32_t)k) == 0;
+                        const uint64_t a = v[e], b = v[pe];
+                        if (up ? a < b : a > b) {
+                            v[e] = b;
+                            v[pe] = a;
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const uint32_t i = (uint32_t)e * 64u + lane;
+                    const uint64_t o = xs64(v[e], j);
+                    const bool keep_max = ((i & (uint32_t)j) == 0) == ((i & (uint32_t)k) == 0);
+                    v[e] = keep_max ? (v[e] > o ? v[e] : o) : (v[e] < o ? v[e] : o);
+                }
+            }
+        }
+    }
+}
+
+// one bucket [a, a + c) of (s + 1, length) items (0: not a best member): sorted descending by one
+// wave, the first nb lengths out in visit order (sequence index descending) at out, the best
+// members' signature flags set in that order
+template <int E>
+__device__ __forceinline__ void heavy_bucket_out(const uint32_t* __restrict__ ks, const uint32_t* __restrict__ ls,
+                                                 uint32_t a, uint32_t c, uint32_t nb, uint32_t* __restrict__ out,
+                                                 uint8_t* flags) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t i = (uint32_t)e * 64u + lane;
+        v[e] = i < c ? ((uint64_t)ks[a + i] << 32) | ls[a + i] : 0ull;
+    }
+    wave_sort_desc<E>(v);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t i = (uint32_t)e * 64u + lane;
+        if (i < nb) {
+            out[i] = (uint32_t)v[e];
+            if (flags) mark_seq(flags, (uint32_t)(v[e] >> 32) - 1u);
+        }
+    }
+}
+
 // One heavy key per workgroup iteration (persistent grid; the key count is read on the device).
 __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
     static_assert(RBINS <= HEAVY_WG, "one radix bin per thread in the scan");
@@ -3892,6 +3962,10 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
     __shared__ __align__(16) uint32_t s_wave[48];
     __shared__ uint32_t s_bm[2 * (HEAVY_WG / 64)];
     __shared__ uint32_t s_cur, s_sel[3], s_key;
+    __shared__ uint32_t s_fb[HV_FT];    // function counts (pass 1), then best members per bucket
+    __shared__ uint32_t s_bk[HV_NBK];   // members per bucket -> bucket cursors -> bucket ends
+    __shared__ uint32_t s_oh[256], s_ol[256];  // offset histograms: high byte, low byte
+    static_assert(HV_FT == HV_NBK, "s_fb doubles as the per-bucket best counts");
     const uint32_t tid = threadIdx.x, nt = blockDim.x, lane = tid & 63u, wave = tid >> 6, nw = nt >> 6;
     const uint64_t lt = (1ull << lane) - 1ull;
     const uint32_t nkeys = (uint32_t)*H.nkeys;
@@ -3910,148 +3984,285 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
         const uint64_t* hi = H.hi + K.off;
         const uint64_t* lo = H.lo + K.off;
         const uint32_t n = K.n;
-        // ---- Boyer-Moore majority function, then its exact count ----
-        uint32_t cand = 0xFFFFFFFFu, cc = 0;
-        for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
-            uint32_t f[U];
+        uint32_t best_f = 0, cb = 0, NBK = 0;
+        bool bucketed = false;
+        if (H.fast) {
+            // ---- one read: function counts, offset high byte, members per sequence bucket ----
+            NBK = 1;
+            while (NBK < HV_NBK && NBK * 256u < n) NBK <<= 1;
+            for (uint32_t d = tid; d < HV_FT; d += nt) s_fb[d] = 0;
+            for (uint32_t d = tid; d < NBK; d += nt) s_bk[d] = 0;
+            for (uint32_t d = tid; d < 256; d += nt) s_oh[d] = 0;
+            __syncthreads();
+            for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
+                uint64_t h[U], l[U];
 #pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint32_t j = j0 + u * nt + tid;
-                f[u] = j < n ? (uint32_t)(hi[j] & 0xFFFFu) : 0xFFFFFFFFu;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                if (f[u] == 0xFFFFFFFFu) continue;
-                if (cc == 0) {
-                    cand = f[u];
-                    cc = 1;
-                } else if (f[u] == cand) {
-                    ++cc;
-                } else {
-                    --cc;
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t j = j0 + u * nt + tid;
+                    h[u] = j < n ? hi[j] : ~0ull;
+                    l[u] = j < n ? lo[j] : 0ull;
                 }
-            }
-        }
-        bm_combine(cand, cc);  // over the wave (lane 0 broadcast)
-        if (lane == 0) {
-            s_bm[2 * wave] = cand;
-            s_bm[2 * wave + 1] = cc;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t c0 = s_bm[0], n0 = s_bm[1];
-            for (uint32_t w = 1; w < nw; ++w) {
-                const uint32_t c1 = s_bm[2 * w], n1 = s_bm[2 * w + 1];
-                if (c1 == c0) {
-                    n0 += n1;
-                } else if (n0 >= n1) {
-                    n0 -= n1;
-                } else {
-                    c0 = c1;
-                    n0 = n1 - n0;
-                }
-            }
-            s_sel[0] = c0;
-        }
-        __syncthreads();
-        const uint32_t best_f = s_sel[0];
-        uint32_t cb = 0;
-        for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
-            uint32_t f[U];
 #pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint32_t j = j0 + u * nt + tid;
-                f[u] = j < n ? (uint32_t)(hi[j] & 0xFFFFu) : 0xFFFFFFFFu;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) cb += f[u] == best_f;
-        }
-        cb = wg_sum(cb, s_wave);
-        if ((float)cb < float(n) * 0.8f) continue;  // cut (uniform); the best run is the majority
-        // ---- flags, u16 length sum and the best members' sequence indices; offset histogram
-        //      of the high byte for the upper-median select ----
-        if (tid == 0) s_cur = 0;
-        for (uint32_t d = tid; d < 256; d += nt) s_hist[d] = 0;
-        __syncthreads();
-        uint32_t* sa = H.s0 + K.off;
-        uint32_t* sb = H.s1 + K.off;
-        uint32_t sum = 0, smax = 0;
-        for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
-            uint64_t l[U];
-            uint32_t f[U], gl[U];
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint32_t j = j0 + u * nt + tid;
-                const uint64_t h = j < n ? hi[j] : ~0ull;
-                f[u] = j < n ? (uint32_t)(h & 0xFFFFu) : 0xFFFFFFFFu;
-                // the mean's accumulator is a u16: the element's length mod 2^16 (bits 48..63 of
-                // the heavy copy, which keeps the length bits) is all it needs -- no glen gather
-                gl[u] = (uint32_t)(h >> 48);
-                l[u] = j < n ? lo[j] : 0ull;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) gl[u] = f[u] == best_f ? gl[u] : 0u;
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const bool v = f[u] != 0xFFFFFFFFu;
-                const uint32_t s = (uint32_t)(l[u] >> 36);
-                const bool best = f[u] == best_f;
-                if (v) {
-                    if (!best && A.flags) mark_seq(A.flags, s);  // the best members' flags go out in sorted order below
-                    atomicAdd(&s_hist[(uint32_t)(l[u] >> 8) & 255u], 1u);
-                }
-                if (best) {
-                    sum += gl[u];
-                    smax = max(smax, s);
-                }
-                const uint64_t bm = __ballot(best);
-                uint32_t base = 0;
-                if (bm) {
-                    const uint32_t leader = (uint32_t)(__ffsll((long long)bm) - 1);
-                    if (lane == leader) base = atomicAdd(&s_cur, (uint32_t)__popcll(bm));
-                    base = (uint32_t)__shfl((int)base, (int)leader, 64);
-                }
-                if (best) sa[base + (uint32_t)__popcll(bm & lt)] = s;
-            }
-        }
-        sum = wg_sum(sum, s_wave);
-        smax = wg_max(smax, s_wave);
-        const uint16_t mean = d2u16((double)(uint16_t)sum / (double)cb);
-        // ---- avg_from_end: the (n/2)-th smallest offset, high byte then low byte ----
-        uint32_t k = n / 2, pre = 0;
-        for (int sh = 8; sh >= 0; sh -= 8) {
-            if (sh == 0) {
-                for (uint32_t d = tid; d < 256; d += nt) s_hist[d] = 0;
-                __syncthreads();
-                for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
-                    uint32_t o[U];
-#pragma unroll
-                    for (uint32_t u = 0; u < U; ++u) {
-                        const uint32_t j = j0 + u * nt + tid;
-                        o[u] = j < n ? (uint32_t)(lo[j] & 0xFFFFu) : 0xFFFFFFFFu;
+                for (uint32_t u = 0; u < U; ++u) {
+                    const bool v = h[u] != ~0ull;
+                    const uint32_t f = v ? (uint32_t)(h[u] & 0xFFFFu) : 0xFFFFFFFFu;
+                    // the lanes sharing lane 0's function add once (a heavy key is mostly one function)
+                    const uint32_t f0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)f);
+                    const uint64_t same = __ballot(v && f == f0);
+                    if (v && f != f0) atomicAdd(&s_fb[f], 1u);
+                    if (v && f == f0 && (same & lt) == 0) atomicAdd(&s_fb[f], (uint32_t)__popcll(same));
+                    if (v) {
+                        atomicAdd(&s_oh[(uint32_t)(l[u] >> 8) & 255u], 1u);
+                        atomicAdd(&s_bk[(uint32_t)(((l[u] >> 36) * NBK) / H.n_total)], 1u);
                     }
-#pragma unroll
-                    for (uint32_t u = 0; u < U; ++u)
-                        if (o[u] != 0xFFFFFFFFu && (o[u] >> 8) == (pre >> 8)) atomicAdd(&s_hist[o[u] & 255u], 1u);
                 }
+            }
+            __syncthreads();
+            // the best function: the largest count, ties to the lowest FunctionIndex (the first
+            // std::map entry wins and only a strictly greater count replaces it)
+            uint32_t cm = 0;
+            for (uint32_t d = tid; d < HV_FT; d += nt) cm = max(cm, s_fb[d]);
+            cm = wg_max(cm, s_wave);
+            uint32_t fm = 0;
+            for (uint32_t d = tid; d < HV_FT; d += nt)
+                if (s_fb[d] == cm) fm = max(fm, HV_FT - 1u - d);
+            fm = wg_max(fm, s_wave);
+            best_f = HV_FT - 1u - fm;
+            cb = cm;
+            uint32_t bm = 0;
+            for (uint32_t d = tid; d < NBK; d += nt) bm = max(bm, s_bk[d]);
+            bm = wg_max(bm, s_wave);
+            bucketed = bm <= HV_BCAP && !H.nosort;
+        } else {
+            // ---- Boyer-Moore majority function, then its exact count ----
+            uint32_t cand = 0xFFFFFFFFu, cc = 0;
+            for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
+                uint32_t f[U];
+    #pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t j = j0 + u * nt + tid;
+                    f[u] = j < n ? (uint32_t)(hi[j] & 0xFFFFu) : 0xFFFFFFFFu;
+                }
+    #pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    if (f[u] == 0xFFFFFFFFu) continue;
+                    if (cc == 0) {
+                        cand = f[u];
+                        cc = 1;
+                    } else if (f[u] == cand) {
+                        ++cc;
+                    } else {
+                        --cc;
+                    }
+                }
+            }
+            bm_combine(cand, cc);  // over the wave (lane 0 broadcast)
+            if (lane == 0) {
+                s_bm[2 * wave] = cand;
+                s_bm[2 * wave + 1] = cc;
             }
             __syncthreads();
             if (tid == 0) {
-                uint32_t d = 0;
-                while (k >= s_hist[d]) k -= s_hist[d++];
-                s_sel[0] = d;
-                s_sel[1] = k;
+                uint32_t c0 = s_bm[0], n0 = s_bm[1];
+                for (uint32_t w = 1; w < nw; ++w) {
+                    const uint32_t c1 = s_bm[2 * w], n1 = s_bm[2 * w + 1];
+                    if (c1 == c0) {
+                        n0 += n1;
+                    } else if (n0 >= n1) {
+                        n0 -= n1;
+                    } else {
+                        c0 = c1;
+                        n0 = n1 - n0;
+                    }
+                }
+                s_sel[0] = c0;
             }
             __syncthreads();
-            pre |= s_sel[0] << sh;
-            k = s_sel[1];
+            const uint32_t best_f = s_sel[0];
+            uint32_t cb = 0;
+            for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
+                uint32_t f[U];
+    #pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t j = j0 + u * nt + tid;
+                    f[u] = j < n ? (uint32_t)(hi[j] & 0xFFFFu) : 0xFFFFFFFFu;
+                }
+    #pragma unroll
+                for (uint32_t u = 0; u < U; ++u) cb += f[u] == best_f;
+            }
+            cb = wg_sum(cb, s_wave);
+        }
+        if ((float)cb < float(n) * 0.8f) continue;  // cut (uniform); the best run is the majority
+        uint32_t pre = 0;         // avg_from_end: the (n/2)-th smallest offset
+        uint16_t mean = 0;
+        const uint32_t* sorted = nullptr;  // the LSD path: the best members' sequence indices, ascending
+        if (bucketed) {
+            // ---- bucket starts; the offset's high byte ----
+            {
+                const uint32_t per = (NBK + nt - 1) / nt, b0 = min(NBK, tid * per), b1 = min(NBK, b0 + per);
+                uint32_t loc = 0;
+                for (uint32_t d = b0; d < b1; ++d) loc += s_bk[d];
+                uint32_t tot;
+                uint32_t x = wg_exclusive_scan(loc, s_wave, tot);
+                for (uint32_t d = b0; d < b1; ++d) {
+                    const uint32_t c = s_bk[d];
+                    s_bk[d] = x;  // cursor = start
+                    x += c;
+                }
+            }
+            for (uint32_t d = tid; d < NBK; d += nt) s_fb[d] = 0;  // best members per bucket
+            for (uint32_t d = tid; d < 256; d += nt) s_ol[d] = 0;
+            if (tid == 0) {
+                uint32_t kk = n / 2, d = 0;
+                while (kk >= s_oh[d]) kk -= s_oh[d++];
+                s_sel[0] = d;
+                s_sel[1] = kk;
+            }
+            __syncthreads();
+            const uint32_t hb = s_sel[0], krem = s_sel[1];
+            // ---- second read: flags of the other members, u16 length sum, the offset's low byte,
+            //      every member's item into its bucket ((s + 1, length) for the best, 0 otherwise) ----
+            uint32_t* ks = H.s0 + K.off;
+            uint32_t* ls = H.s1 + K.off;
+            uint32_t sum = 0;
+            for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
+                uint64_t h[U], l[U];
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t j = j0 + u * nt + tid;
+                    h[u] = j < n ? hi[j] : ~0ull;
+                    l[u] = j < n ? lo[j] : 0ull;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    if (h[u] == ~0ull) continue;
+                    const uint32_t sq = (uint32_t)(l[u] >> 36);
+                    const uint32_t bk = (uint32_t)(((uint64_t)sq * NBK) / H.n_total);
+                    const uint32_t off = (uint32_t)(l[u] & 0xFFFFu);
+                    if ((off >> 8) == hb) atomicAdd(&s_ol[off & 255u], 1u);
+                    const bool best = (uint32_t)(h[u] & 0xFFFFu) == best_f;
+                    const uint32_t slot = atomicAdd(&s_bk[bk], 1u);
+                    if (best) {
+                        sum += (uint32_t)(h[u] >> 48);  // the u16 accumulator needs len mod 2^16 only
+                        atomicAdd(&s_fb[bk], 1u);
+                        ks[slot] = sq + 1u;
+                        ls[slot] = elem_len(h[u], l[u], A.glen);
+                    } else {
+                        ks[slot] = 0u;
+                        ls[slot] = 0u;
+                        if (A.flags) mark_seq(A.flags, sq);
+                    }
+                }
+            }
+            sum = wg_sum(sum, s_wave);  // its barriers also close the scatter
+            mean = d2u16((double)(uint16_t)sum / (double)cb);
+            if (tid == 0) {
+                uint32_t kk = krem, d = 0;
+                while (kk >= s_ol[d]) kk -= s_ol[d++];
+                s_sel[0] = (hb << 8) | d;
+            }
+            // the buckets' output offsets in visit order (sequence index descending: the last
+            // bucket first), in place of their best counts: s_fb[k] = best members of buckets > k
+            {
+                const uint32_t per = (NBK + nt - 1) / nt, r0 = min(NBK, tid * per), r1 = min(NBK, r0 + per);
+                uint32_t loc = 0;
+                for (uint32_t r = r0; r < r1; ++r) loc += s_fb[NBK - 1 - r];
+                uint32_t tot;
+                uint32_t x = wg_exclusive_scan(loc, s_wave, tot);
+                for (uint32_t r = r0; r < r1; ++r) {
+                    const uint32_t c = s_fb[NBK - 1 - r];
+                    s_fb[NBK - 1 - r] = x;
+                    x += c;
+                }
+            }
+            __syncthreads();
+            pre = s_sel[0];
+        } else {
+            // ---- flags, u16 length sum and the best members' sequence indices; offset histogram
+            //      of the high byte for the upper-median select ----
+            if (tid == 0) s_cur = 0;
+            for (uint32_t d = tid; d < 256; d += nt) s_hist[d] = 0;
+            __syncthreads();
+            uint32_t* sa = H.s0 + K.off;
+            uint32_t* sb = H.s1 + K.off;
+            uint32_t sum = 0, smax = 0;
+            for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
+                uint64_t l[U];
+                uint32_t f[U], gl[U];
+    #pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t j = j0 + u * nt + tid;
+                    const uint64_t h = j < n ? hi[j] : ~0ull;
+                    f[u] = j < n ? (uint32_t)(h & 0xFFFFu) : 0xFFFFFFFFu;
+                    // the mean's accumulator is a u16: the element's length mod 2^16 (bits 48..63 of
+                    // the heavy copy, which keeps the length bits) is all it needs -- no glen gather
+                    gl[u] = (uint32_t)(h >> 48);
+                    l[u] = j < n ? lo[j] : 0ull;
+                }
+    #pragma unroll
+                for (uint32_t u = 0; u < U; ++u) gl[u] = f[u] == best_f ? gl[u] : 0u;
+    #pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const bool v = f[u] != 0xFFFFFFFFu;
+                    const uint32_t s = (uint32_t)(l[u] >> 36);
+                    const bool best = f[u] == best_f;
+                    if (v) {
+                        if (!best && A.flags) mark_seq(A.flags, s);  // the best members' flags go out in sorted order below
+                        atomicAdd(&s_hist[(uint32_t)(l[u] >> 8) & 255u], 1u);
+                    }
+                    if (best) {
+                        sum += gl[u];
+                        smax = max(smax, s);
+                    }
+                    const uint64_t bm = __ballot(best);
+                    uint32_t base = 0;
+                    if (bm) {
+                        const uint32_t leader = (uint32_t)(__ffsll((long long)bm) - 1);
+                        if (lane == leader) base = atomicAdd(&s_cur, (uint32_t)__popcll(bm));
+                        base = (uint32_t)__shfl((int)base, (int)leader, 64);
+                    }
+                    if (best) sa[base + (uint32_t)__popcll(bm & lt)] = s;
+                }
+            }
+            sum = wg_sum(sum, s_wave);
+            smax = wg_max(smax, s_wave);
+            mean = d2u16((double)(uint16_t)sum / (double)cb);
+            // ---- avg_from_end: the (n/2)-th smallest offset, high byte then low byte ----
+            uint32_t k = n / 2;
+            for (int sh = 8; sh >= 0; sh -= 8) {
+                if (sh == 0) {
+                    for (uint32_t d = tid; d < 256; d += nt) s_hist[d] = 0;
+                    __syncthreads();
+                    for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
+                        uint32_t o[U];
+    #pragma unroll
+                        for (uint32_t u = 0; u < U; ++u) {
+                            const uint32_t j = j0 + u * nt + tid;
+                            o[u] = j < n ? (uint32_t)(lo[j] & 0xFFFFu) : 0xFFFFFFFFu;
+                        }
+    #pragma unroll
+                        for (uint32_t u = 0; u < U; ++u)
+                            if (o[u] != 0xFFFFFFFFu && (o[u] >> 8) == (pre >> 8)) atomicAdd(&s_hist[o[u] & 255u], 1u);
+                    }
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    uint32_t d = 0;
+                    while (k >= s_hist[d]) k -= s_hist[d++];
+                    s_sel[0] = d;
+                    s_sel[1] = k;
+                }
+                __syncthreads();
+                pre |= s_sel[0] << sh;
+                k = s_sel[1];
+                __syncthreads();
+            }
+            // ---- samples in visit order: sequence indices descending ----
+            int bits = 0;
+            while (bits < 32 && (smax >> bits)) bits += RB;
+            sorted = H.nosort ? sa : wg_radix_sort_u32(sa, sb, cb, bits, s_hist, s_wc, s_run, tag);
             __syncthreads();
         }
-        // ---- samples in visit order: sequence indices descending ----
-        int bits = 0;
-        while (bits < 32 && (smax >> bits)) bits += RB;
-        const uint32_t* sorted = H.nosort ? sa : wg_radix_sort_u32(sa, sb, cb, bits, s_hist, s_wc, s_run, tag);
-        __syncthreads();
         if (tid == 0) {
             s_sel[0] = (uint32_t)atomicAdd(A.kept_ctr, 1ull);
             atomicAdd(&A.ctr[0], 1ull);
@@ -4078,21 +4289,41 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
         const uint32_t o = s_sel[0], jb = s_sel[1], loff = s_cur;
         const bool giant = s_sel[2] != 0;
         uint32_t* lens_out = giant ? H.gsamples : A.lens;
-        for (uint32_t t0 = 0; t0 < cb; t0 += nt * U) {
-            uint32_t sv[U];
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint32_t t = t0 + u * nt + tid;
-                sv[u] = t < cb ? sorted[cb - 1 - t] : 0u;
+        if (bucketed) {
+            // ---- each bucket sorted by one wave; its best members' lengths out in visit order ----
+            const uint32_t* ks = H.s0 + K.off;
+            const uint32_t* ls = H.s1 + K.off;
+            for (uint32_t bk = wave; bk < NBK; bk += nw) {
+                const uint32_t a = bk ? s_bk[bk - 1] : 0u, c = s_bk[bk] - a;
+                const uint32_t nb = (bk ? s_fb[bk - 1] : cb) - s_fb[bk];
+                if (nb == 0) continue;
+                uint32_t* out = lens_out + (uint64_t)loff + s_fb[bk];
+                if (c <= 64)
+                    heavy_bucket_out<1>(ks, ls, a, c, nb, out, A.flags);
+                else if (c <= 128)
+                    heavy_bucket_out<2>(ks, ls, a, c, nb, out, A.flags);
+                else if (c <= 256)
+                    heavy_bucket_out<4>(ks, ls, a, c, nb, out, A.flags);
+                else
+                    heavy_bucket_out<8>(ks, ls, a, c, nb, out, A.flags);
             }
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint32_t t = t0 + u * nt + tid;
-                if (t < cb) {
-                    // monotone sequence indices: the length gathers and the signature flags of the
-                    // best members touch neighbouring lines instead of random ones
-                    lens_out[(uint64_t)loff + t] = A.glen[sv[u]];
-                    if (A.flags) mark_seq(A.flags, sv[u]);
+        } else {
+            for (uint32_t t0 = 0; t0 < cb; t0 += nt * U) {
+                uint32_t sv[U];
+    #pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t t = t0 + u * nt + tid;
+                    sv[u] = t < cb ? sorted[cb - 1 - t] : 0u;
+                }
+    #pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t t = t0 + u * nt + tid;
+                    if (t < cb) {
+                        // monotone sequence indices: the length gathers and the signature flags of the
+                        // best members touch neighbouring lines instead of random ones
+                        lens_out[(uint64_t)loff + t] = A.glen[sv[u]];
+                        if (A.flags) mark_seq(A.flags, sv[u]);
+                    }
                 }
             }
         }
@@ -4467,6 +4698,8 @@ struct Tune {
     int lane_streams = 1;            //   the streams their batches rotate over (1..4)
     int lane_tail = 1 << 16;         //   the last batch's threshold (its wave pairs are the tail's latency)
     int sub_target = 0;              // k_partition's target elements per level-2 sub-bucket (0: SUB_TARGET)
+    int heavy_lsd = 0;               // 1: k_heavy's round-3 path (Boyer-Moore + recount, LSD sort, length
+                                     //   gathers) for every key instead of the one-read bucketed path
     int flag_bits = 1;               // signature flags as bits, read before an atomic set (mark_seq);
                                      //   0: a byte store per kept occurrence (C3: +58 ms/step)
     int diag = 0;                    // diagnostics only (wrong results): 1 = no signature flag stores,
@@ -5917,6 +6150,8 @@ void phase_group(skm_build* b, uint32_t pass) {
     H.s0 = b->d_hv_s0.as<uint32_t>();
     H.s1 = b->d_hv_s1.as<uint32_t>();
     H.nosort = (b->tune.diag & 2) ? 1u : 0u;
+    H.fast = b->opts.n_functions <= HV_FT && !b->tune.heavy_lsd ? 1u : 0u;
+    H.n_total = std::max<uint32_t>(b->n_total, 1);
     // giant chains: samples and jobs in this pass's own buffers, run on a rotating chain stream
     // (only in the last giant_passes passes: earlier passes' long chains overlap the later passes
     // from the stash batches anyway; the last pass's would form the tail)
@@ -6777,6 +7012,7 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "split_min" ? &t.split_min
                : n == "giant_class" ? &t.giant_class
                : n == "giant_passes" ? &t.giant_passes
+               : n == "heavy_lsd" ? &t.heavy_lsd
                : n == "prefetch" ? &t.prefetch
                : n == "overflow_grid" ? &t.ovf_grid
                : n == "split_grid" ? &t.split_grid

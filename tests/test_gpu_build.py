@@ -293,11 +293,18 @@ def test_device_exact_division(skm, gpu):
     assert skm.debug_div_check(1 << 22, 64) == 0
 
 
-@pytest.mark.parametrize("passes,giant_class", [(0, 0), (0, 11), (2, 12), (4, 17)])
-def test_heavy_keys_split_path(skm, gpu, passes, giant_class):
+@pytest.mark.parametrize("passes,giant_class,clustered,lsd", [(0, 0, False, 0), (0, 11, False, 0), (2, 12, False, 0),
+                                                           (4, 17, False, 0), (0, 0, True, 0), (4, 17, True, 0),
+                                                           (0, 0, False, 1), (2, 12, True, 1)])
+def test_heavy_keys_split_path(skm, gpu, passes, giant_class, clustered, lsd):
     """k_ovf_split / k_heavy: overflow sub-buckets of >= 4096 elements lose their keys of >= 1024
-    occurrences to the heavy path (Boyer-Moore majority + exact count for the fp32 80 % cut, radix
-    select of the upper-median offset, sequence-index radix sort for the visit-order samples).
+    occurrences to the heavy path: one read for the per-function counts (LDS table: the exact best
+    function for the fp32 80 % cut), the offset's high byte and the members per sequence-index
+    bucket; a second for the flags, the u16 length sum, the offset's low byte and each member's
+    (sequence, length) item into its bucket; each bucket sorted by one wave for the visit-order
+    samples.  A key whose members crowd one bucket (clustered: each planted key's sequences
+    consecutive) takes the round-3 path -- compaction, LSD radix sort of the sequence indices,
+    length gathers -- as every key does with heavy_lsd = 1 (Boyer-Moore + recount for the best).
     Planted 8-mers: pure (kept, some sequences hold it three times), exactly 80 % (kept),
     one short of 80 % (cut), a 50/50 tie (cut), and one inside a > 65535-residue protein."""
     rng = np.random.default_rng(44)
@@ -318,7 +325,7 @@ def test_heavy_keys_split_path(skm, gpu, passes, giant_class):
                 a = rnd(70000)
             seqs.append(a + body + b)
             funcs.append(fn)
-    order = rng.permutation(len(seqs))
+    order = np.arange(len(seqs)) if clustered else rng.permutation(len(seqs))
     seqs = [seqs[k] for k in order]
     res, off, lens = pack(seqs)
     func = np.array(funcs, np.uint16)[order]
@@ -328,6 +335,7 @@ def test_heavy_keys_split_path(skm, gpu, passes, giant_class):
     if passes:
         b.set_option("key_range_passes", passes)
     b.set_option("giant_class", giant_class)  # 0: off; 11/12: the planted keys' chains start after k_heavy
+    b.set_option("heavy_lsd", lsd)
     b.add_batch(res, off, lens, func, sid)
     b.run()
     ovf = b.debug_overflow()
