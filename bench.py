@@ -72,6 +72,8 @@ def parse():
                     help="name=value: skm_build_set_option on the headline build (experiments)")
     ap.add_argument("--annot-queries", type=int, default=10_000_000,
                     help="annotate leg (BASELINE configs[3]); 0 = off; N=1 only")
+    ap.add_argument("--recall", type=int, default=1,
+                    help="recall leg (SURVEY 8(f)2: the C2 training set vs its exact kept-k-mer DB); 0 = off; N=1 only")
     ap.add_argument("--matrix-seqs", type=int, default=100_000,
                     help="matrix-distance leg (BASELINE configs[4]); 0 = off; owner-partitioned over the ranks")
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
@@ -312,9 +314,12 @@ def main():
             out["weak"]["cpu_baseline"] = _cpu_baseline(
                 c2, len(funcs), a.weak_seqs, a.cpu_threads or cores["usable"], cores,
                 f"the whole C2 workload ({a.weak_seqs:,} proteins, measured, not extrapolated)")
-        if world == 1 and queries is not None:
+        if world == 1 and (queries is not None or a.recall):
             kept = b.finish()
         b.close()
+    if world == 1 and a.recall and kept is not None and c2 is not None:
+        log("recall leg")
+        out["recall"] = _recall_leg(skm, kept, funcs, c2, a, device, cores)
     if world == 1 and queries is not None and kept is not None:
         log("annotate leg")
         out["annotate"] = _annotate_leg(skm, kept, funcs, queries, a, device, cores)
@@ -553,6 +558,66 @@ def _annotate_leg(skm, kept, funcs, q, a, device, cores):
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
                          "avg_launch_ms": acc["lookup"], "traffic": _pmc_traffic("k_lookup<0>", "legs", len(lens))},
             "cpu_baseline": cpu, "mph_build_s": mph_s}
+
+
+def _recall_leg(skm, kept, funcs, train, a, device, cores):
+    """The recall pass (kmers-build-signatures.cc:238-349): the C2 training proteins
+    called against the exact kept-k-mer DB of their own build (KeptKmerDB, kept_kmer_db.h:20-27;
+    the device open-addressing key table), resident in HBM.  One step = window lookup in the exact
+    table + HitSet calls over every training protein; the calls stay on the device.  Roofline:
+    k_lookup<LK_EXACT>, B_alg = 1 B/residue + 18 B/window (the 8-byte key compared + the 10-byte
+    record, as SURVEY 8(d) prices a lookup).  CPU baseline: the oracle's process_aa_seq against the
+    sorted kept set (oracle_annotate_exact) on the host cores, bounded sample."""
+    res, off, lens, _, _ = train.packed()
+    t0 = time.time()
+    db = skm.KeptKmerDb(kept.keys, kept.data, device=device)
+    open_s = time.time() - t0
+    hypo = funcs.index("hypothetical protein")
+    qb = skm.QueryBatch(db, res, off, lens)
+    nwin = _windows(lens)
+    for _ in range(max(1, a.warmup)):
+        qb.run(hypo)
+    steps = max(3, min(a.steps, 10))
+    acc = {}
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        qb.run(hypo)
+        for k, v in qb.timings().items():
+            acc[k] = acc.get(k, 0.0) + v
+    wall = time.perf_counter() - t1
+    acc = {k: v / steps for k, v in acc.items()}
+    _, calls = qb.calls()
+    qb.close()
+    db.close()
+    alg = int(len(res)) + 18 * nwin
+    gbs = alg / (acc["lookup"] * 1e-3) / 1e9
+    cpu = None
+    if not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_ref
+        threads = a.cpu_threads or cores["usable"]
+        n = min(len(lens), 200_000)
+        end = int(off[n - 1]) + int(lens[n - 1])
+        t = time.perf_counter()
+        _, oc = oracle_ref.annotate_exact_par(kept.keys, kept.data, res[:end], off[:n], lens[:n], threads,
+                                              hypo_index=hypo)
+        dt = time.perf_counter() - t
+        w = _windows(lens[:n])
+        cpu = {"value": w / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
+               "host": {k: cores[k] for k in ("model", "affinity", "cgroup_quota")},
+               "sample": f"first {n} training proteins ({w} windows), {dt:.1f} s, oracle/skm_oracle.cpp "
+                         f"oracle_annotate_exact (process_aa_seq vs the sorted kept set) on {threads} host threads"}
+    return {"metric": "training k-mers/sec (recall: exact-DB window lookup + HitSet calls)",
+            "value": nwin * steps / wall, "unit": "k-mers/s", "ms_per_step": 1000.0 * wall / steps, "steps": steps,
+            "config": {"workload": f"recall: the {len(lens):,} C2 training proteins vs the exact DB of their own "
+                                   f"build ({len(kept.keys):,} kept k-mers) in HBM, 1 GPU",
+                       "proteins": int(len(lens)), "windows": nwin, "db_keys": int(len(kept.keys)),
+                       "calls": int(len(calls))},
+            "phase_ms": acc,
+            "roofline": {"bound": "hbm", "kernel": "k_lookup<LK_EXACT>", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
+                         "avg_launch_ms": acc["lookup"], "traffic": _pmc_traffic("k_lookup<1>", "recall", len(lens))},
+            "cpu_baseline": cpu, "db_open_s": open_s}
 
 
 def _matrix_leg(skm, matrix_in, a, device, cores, rank=0, world=1, dist=None):

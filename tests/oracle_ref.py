@@ -296,6 +296,44 @@ def annotate_exact(keys, data, residues, seq_off, seq_len, min_hits=5, max_gap=2
     return off, calls[:tot].copy()
 
 
+def annotate_exact_par(keys, data, residues, seq_off, seq_len, n_threads, min_hits=5, max_gap=200, ignore_hypo=0,
+                       hypo_index=-1, mean_mode=0, mad_mode=0):
+    """annotate_exact() (the recall pass against KeptKmerDB, calls in CSR form) over contiguous
+    sequence ranges on n_threads host threads: oracle_annotate_exact releases the GIL, every range
+    is the single-thread restatement."""
+    from concurrent.futures import ThreadPoolExecutor
+    keys = np.ascontiguousarray(keys, np.uint64)
+    data = np.ascontiguousarray(data, STORED_DTYPE)
+    residues = np.ascontiguousarray(residues, np.uint8)
+    seq_off = np.ascontiguousarray(seq_off, np.uint64)
+    seq_len = np.ascontiguousarray(seq_len, np.uint32)
+    n = len(seq_len)
+    opts = AnnotOpts(min_hits, max_gap, ignore_hypo, hypo_index, mean_mode, mad_mode)
+    T = max(1, int(n_threads))
+    bounds = [n * t // (T * 4) for t in range(T * 4 + 1)]
+
+    def one(t):
+        a, b = bounds[t], bounds[t + 1]
+        cap = 8 * (b - a) + 1024
+        while True:
+            off = np.zeros(b - a + 1, np.uint64)
+            calls = np.zeros(cap, CALL_DTYPE)
+            tot = olib().oracle_annotate_exact(_p(keys), _p(data), len(keys), _p(residues), _p(seq_off[a:b].copy()),
+                                               _p(seq_len[a:b].copy()), b - a, C.byref(opts), _p(off), _p(calls), cap)
+            if tot >= 0:
+                return off, calls[:tot]
+            cap *= 4
+
+    with ThreadPoolExecutor(T) as ex:
+        parts = list(ex.map(one, range(T * 4)))
+    offs = [np.zeros(1, np.uint64)]
+    base = 0
+    for off, calls in parts:
+        offs.append(off[1:] + np.uint64(base))
+        base += len(calls)
+    return np.concatenate(offs), (np.concatenate([c for _, c in parts]) if parts else np.zeros(0, CALL_DTYPE))
+
+
 def matrix_distance_mt(bdz: Bdz, dat: bytes, residues, seq_off, seq_len, seq_idx, hypo_index=-1, n_threads=1,
                        want_pairs=True):
     """oracle_matrix_distance_mt: the pair counts on n_threads host threads; (n, 3) sorted pairs,

@@ -117,3 +117,28 @@ def test_c4_db_calls_bit_exact(skm, c2, tmp_path):
     assert len(calls) > 5_000_000
     assert np.array_equal(off, ooff)
     assert np.array_equal(calls.view(np.uint8), ocalls.view(np.uint8))
+
+
+def test_c2_recall_bit_exact(skm, c2):
+    """The recall pass at C2 size (kmers-build-signatures.cc:238-349): every one of the 1M training
+    proteins (303M windows) called against the exact kept-k-mer DB of its own build (KeptKmerDB,
+    kept_kmer_db.h:20-27: 168.7M keys, the device exact-key table) -- the calls equal process_aa_seq
+    of the oracle against the sorted kept set, on every host core."""
+    kept = c2.get("kept")
+    if kept is None:
+        r, o, l, f, i = c2["inputs"]
+        b = skm.SignatureBuilder(len(c2["funcs"]))
+        b.add_batch(r, o, l, f, i)
+        kept = b.finish()
+        b.close()
+    r, o, l, _, _ = c2["inputs"]
+    funcs = c2["funcs"]
+    hypo = funcs.index("hypothetical protein")
+    db = skm.KeptKmerDb(kept.keys, kept.data, device=0)
+    caller = skm.FunctionCaller(db, funcs)
+    off, calls = caller.process_seqs(r, o, l)
+    db.close()
+    ooff, ocalls = oracle_ref.annotate_exact_par(kept.keys, kept.data, r, o, l, _threads(), hypo_index=hypo)
+    assert len(calls) > 500_000
+    assert np.array_equal(off, ooff)
+    assert np.array_equal(calls.view(np.uint8), ocalls.view(np.uint8))
