@@ -4,12 +4,17 @@ headline workload) built on ONE GPU with its key-range passes, checked against t
 The whole C3 build (15.2 G windows, ~2.9 G kept k-mers) cannot be restated on the host in the
 reference's way (~780 GB for the multimap), so the check is split:
 
-* bit-exact on one output slice: the kept k-mers whose fmix64(key) has top 6 bits == SLICE
-  (skm_build_finish_slice) against oracle_build_sel_mt, which groups only the windows of those
-  keys -- every key's occurrences are all in or all out, so each selected group is exactly the
-  reference's group (signature_build.tcc:184-293).  The slice is 1/64 of the key space and holds
-  k-mers with >= 2^14 occurrences (asserted), i.e. the heavy-key split, the overflow path and the
-  stashed long P^2 chains at their C3 depths;
+* bit-exact on one output slice: the kept k-mers whose fmix64(key) has top 6 bits == the slice
+  of the proteome's heaviest k-mer (skm_build_finish_slice) against oracle_build_sel_mt, which
+  groups only the windows of those keys -- every key's occurrences are all in or all out, so each
+  selected group is exactly the reference's group (signature_build.tcc:184-293).  The slice is
+  1/64 of the key space; choosing it by the heaviest k-mer (counted on a 200K-protein sample of
+  the input) puts the deepest group of the build in it (>= 2^19 occurrences, asserted: the heavy-
+  key split, the overflow path and the longest stashed P^2 / variance chain at C3 depth).  The
+  heaviest chain at C3 is ~9*10^5 samples, below lane_long = 2^20, so with the defaults every
+  stashed chain runs one lane each; a second build of the same input with lane_long = 2^18 and
+  lane_tail = 2^14 runs the deepest chains on wave pairs (k_chain_long, the tail batch included)
+  and must give the same slice;
 * size-independent properties over the whole build: the occurrences grouped equal the oracle's
   count of valid windows of the whole input (every window extracted once, none lost by the
   key-range passes or the per-pass compaction), seqs_with_func equals the per-function sequence
@@ -27,7 +32,32 @@ from signature_kmers_amd import synth
 pytestmark = pytest.mark.gpu
 
 N_C3, FAM, PER_FILE = 50_000_000, 4000, 4000
-SLICE_BITS, SLICE = 6, 0
+SLICE_BITS = 6
+OK_PROT = np.zeros(256, bool)
+OK_PROT[np.frombuffer(b"ACDEFGHIKLMNPQRSTVWYacdefghiklmnpqrstvwy", np.uint8)] = True  # signature_build.h:102-103
+
+
+def _heaviest_key(parts):
+    """The most frequent valid 8-mer (little-endian u64, as skm keys) of the first 50 files'
+    sequences with a kept function: the Zipf-heaviest family's conserved k-mers dominate it."""
+    keys = []
+    for r, o, l, f, _ in parts[:50]:
+        r = np.asarray(r, np.uint8)
+        n = len(r)
+        if n < 8:
+            continue
+        k = np.zeros(n - 7, np.uint64)
+        ok = np.ones(n - 7, bool)
+        for j in range(8):
+            k |= r[j:n - 7 + j].astype(np.uint64) << np.uint64(8 * j)
+            ok &= OK_PROT[r[j:n - 7 + j]]
+        start = np.zeros(n - 7, bool)  # windows inside one sequence with a kept function
+        for a, ln, fn in zip(o.astype(np.int64), l.astype(np.int64), f):
+            if fn != 0xFFFF and ln >= 8:
+                start[a:a + ln - 7] = True
+        keys.append(k[ok & start])
+    u, c = np.unique(np.concatenate(keys), return_counts=True)
+    return int(u[np.argmax(c)])
 
 
 def _threads():
@@ -45,15 +75,25 @@ def test_c3_slice_bit_exact_and_whole_build_properties(skm, gpu):
     parts = list(synth.iter_file_inputs(N_C3, FAM, PER_FILE, workers=min(16, T)))
     funcs = synth.functions(FAM)
     nf = len(funcs)
-    b = skm.SignatureBuilder(nf)
-    b.reserve(sum(len(p[0]) for p in parts), sum(len(p[2]) for p in parts))
-    for r, o, l, f, i in parts:
-        b.add_batch(r, o, l, f, i)
-    b.run()
-    c = b.counters()
-    got = b.finish_slice(SLICE_BITS, SLICE)
-    flags = b.signature_flags()
-    b.close()
+    heavy = _heaviest_key(parts)
+    SLICE = int(oracle_ref.slice_hash(np.array([heavy], np.uint64))[0] >> np.uint64(64 - SLICE_BITS))
+
+    def build(opts):
+        b = skm.SignatureBuilder(nf)
+        for k, v in opts.items():
+            b.set_option(k, v)
+        b.reserve(sum(len(p[0]) for p in parts), sum(len(p[2]) for p in parts))
+        for r, o, l, f, i in parts:
+            b.add_batch(r, o, l, f, i)
+        b.run()
+        c = b.counters()
+        got = b.finish_slice(SLICE_BITS, SLICE)
+        flags = b.signature_flags()
+        b.close()
+        return c, got, flags
+
+    c, got, flags = build({})
+    c2, got2, _ = build({"lane_long": 1 << 18, "lane_tail": 1 << 14})  # the deepest chains on wave pairs
     assert c["passes"] >= 8, c  # the headline's out-of-core path (16 passes at 288 GB)
     # pack the input for the oracle (16.5 GB of residues)
     lens = np.concatenate([p[2] for p in parts])
@@ -65,12 +105,15 @@ def test_c3_slice_bit_exact_and_whole_build_properties(skm, gpu):
     off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
     ref = oracle_ref.build_slice_mt(res, off, lens, func, ids, nf, T, SLICE_BITS, SLICE, want_flags=True)
     # ---- the slice, bit for bit ----
-    assert ref["max_group"] >= 1 << 14, ref["max_group"]  # heavy keys / long chains are in the slice
-    assert len(got.keys) == len(ref["keys"]) > 10_000_000, (len(got.keys), len(ref["keys"]))
-    assert np.array_equal(got.keys, ref["keys"])
-    for fld in ("avg_from_end", "function_index", "mean", "median", "var"):
-        bad = np.nonzero(got.data[fld] != ref["data"][fld])[0]
-        assert len(bad) == 0, (fld, len(bad), got.keys[bad[:5]], got.data[bad[:5]], ref["data"][bad[:5]])
+    assert ref["max_group"] >= 1 << 19, ref["max_group"]  # the heaviest k-mer's group is in the slice
+    assert bool(np.isin(np.uint64(heavy), got.keys)), "the heaviest k-mer is kept, in the checked slice"
+    for g in (got, got2):
+        assert len(g.keys) == len(ref["keys"]) > 10_000_000, (len(g.keys), len(ref["keys"]))
+        assert np.array_equal(g.keys, ref["keys"])
+        for fld in ("avg_from_end", "function_index", "mean", "median", "var"):
+            bad = np.nonzero(g.data[fld] != ref["data"][fld])[0]
+            assert len(bad) == 0, (fld, len(bad), g.keys[bad[:5]], g.data[bad[:5]], ref["data"][bad[:5]])
+    assert c2["long_samples"] == c["long_samples"] > 0
     assert np.array_equal(np.bincount(got.data["function_index"], minlength=nf)[:nf], ref["distinct_functions"])
     # ---- the whole build ----
     kept_fn = func != 0xFFFF

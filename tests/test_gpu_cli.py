@@ -34,10 +34,13 @@ def _fidx(out):
     return t
 
 
-def _check_build(out, stdout, ref):
+def _check_build(out, stdout, ref, threads=0):
+    """Every output of kmers-build-signatures vs the oracle; threads > 0: the oracle build on that
+    many host threads (oracle_build_mt) and the recall reports' files in parallel."""
     res, off, ln, fn, sid = ref["build"]
     nf = ref["n_kept_functions"]
-    o = oracle_ref.build(res, off, ln, fn, sid, nf)
+    o = oracle_ref.build_mt(res, off, ln, fn, sid, nf, threads, sort=True) if threads else \
+        oracle_ref.build(res, off, ln, fn, sid, nf)
     assert f"kept {nf} functions\n" in stdout
     assert f"Kept {len(o['keys'])} kmers\n" in stdout
     assert f"distinct_signatures={o['distinct_signatures']}\n" in stdout
@@ -63,8 +66,17 @@ def _check_build(out, stdout, ref):
     assert np.array_equal(dat[idx].view(np.uint8), o["data"].view(np.uint8))
     # recall.report.d/<fasta file name>
     fidx = _fidx(out)
-    for path, recs in ref["files"]:
-        want = fr.recall_report(oracle_ref, ref["fm"], recs, fidx, o["keys"], o["data"])
+
+    def one(item):
+        path, recs = item
+        return path, fr.recall_report(oracle_ref, ref["fm"], recs, fidx, o["keys"], o["data"])
+    if threads:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(threads) as ex:
+            reports = list(ex.map(one, ref["files"]))
+    else:
+        reports = [one(x) for x in ref["files"]]
+    for path, want in reports:
         assert _lines(os.path.join(out, "recall.report.d", os.path.basename(path))) == want, path
     return o
 
@@ -114,6 +126,28 @@ def test_build_signatures_c1(c1_build):
     assert len(o["keys"]) > 1000
     n_rep = sum(1 for f in os.listdir(os.path.join(out, "recall.report.d")))
     assert n_rep == len(ref["files"])
+
+
+def test_build_signatures_250k(tmp_path, gpu):
+    """kmers-build-signatures end to end at 250,000 proteins (63 genome files of 4,000, 4,000
+    families; VERDICT r03: the drop-in CLI beyond C1 size): FASTA dirs -> function.index,
+    final.kmers, distinct_functions, kmer_data.mph / .dat, recall.report.d/<file> and the stdout
+    statistics, every output against the reference restatement (oracle/front_ref.py + the oracle
+    build and recall on all host cores).  The run's wall time is printed (-s) for DESIGN."""
+    import time
+    from signature_kmers_amd import synth
+    from test_gpu_scale import _threads
+    info = synth.write_dirs(str(tmp_path / "in"), 250_000, 4000, per_file=4000)
+    out = str(tmp_path / "kd")
+    t = time.time()
+    stdout, stderr = _run([os.path.join(BIN, "kmers-build-signatures"), "-D", info["ann_dir"], "-F", info["seqs_dir"],
+                           "--kmer-data-dir", out, "--final-kmers", "final.kmers", "--perfect-hash", "kmer_data.mph",
+                           "--perfect-hash-data", "kmer_data.dat"])
+    wall = time.time() - t
+    print(f"\nkmers-build-signatures 250K proteins: {wall:.1f} s wall\n{stderr[-600:]}")
+    ref = fr.front([info["ann_dir"]], [info["seqs_dir"]])
+    o = _check_build(out, stdout, ref, threads=_threads())
+    assert len(o["keys"]) > 10_000_000 and len(ref["files"]) == 63
 
 
 def _query_dir(tmp, seed=5):
