@@ -331,12 +331,21 @@ __global__ void k_calls_scan(CallArgs A, uint4* __restrict__ segs) {
             ncur = 0;
         }
     };
-    for (uint32_t i0 = 0; i0 < nwin; i0 += 8) {
-        uint32_t hb[8];
+    // the next 16 hits are loaded while these 16 are walked (the walk is a per-thread chain;
+    // the loads of one thread are 64 contiguous bytes)
+    uint32_t nb[16];
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) hb[k] = i0 + k < nwin ? hit[i0 + k] : NO_HIT;
+    for (uint32_t k = 0; k < 16; ++k) nb[k] = k < nwin ? hit[k] : NO_HIT;
+    for (uint32_t i0 = 0; i0 < nwin; i0 += 16) {
+        uint32_t hb[16];
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
+        for (uint32_t k = 0; k < 16; ++k) hb[k] = nb[k];
+        if (i0 + 16 < nwin) {
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) nb[k] = i0 + 16 + k < nwin ? hit[i0 + 16 + k] : NO_HIT;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
             const uint32_t h = hb[k], i = i0 + k;
             if (!usable(h, A)) continue;
             const uint32_t f = h >> 16;
@@ -402,6 +411,28 @@ __device__ uint32_t kth_dev_sorted(const uint32_t* v, uint32_t n, uint32_t C2, u
 }
 
 constexpr int SEG_WAVES = 4;
+
+// k-th smallest (0-based) of a wave's n items x[e] (item e * 64 + lane; values < 2^bits): MSD
+// radix select, one bit per step, counted on ballots (wave-uniform result)
+template <int E>
+__device__ __forceinline__ uint32_t wave_select(const uint32_t (&x)[E], uint32_t n, uint32_t k, int bits) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t pre = 0;
+    for (int b = bits - 1; b >= 0; --b) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if ((uint32_t)e * 64u >= n) break;  // wave-uniform
+            const bool v = (uint32_t)e * 64u + lane < n;
+            c += (uint32_t)__popcll(__ballot(v && ((x[e] ^ pre) >> (b + 1)) == 0 && ((x[e] >> b) & 1u) == 0));
+        }
+        if (k >= c) {
+            k -= c;
+            pre |= 1u << b;
+        }
+    }
+    return pre;
+}
 constexpr uint32_t SEG_CAP = 1024;  // 16 KB of LDS per 4-wave block: 8 blocks per CU (2048: 5)
 
 // One wave per HitSet::process segment (call_functions.tcc:35-103): the hits of the current
@@ -498,47 +529,39 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
         emit(median, mad);
         return;
     }
-    // bitonic sort of buf[0..P), P = next power of two >= n, padded with the maximum
-    uint32_t P = 1;
-    while (P < n) P <<= 1;
-    for (uint32_t q = n + lane; q < P; q += 64) buf[q] = 0xFFFFFFFFu;
-    wave_sync_lds();
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            for (uint32_t idx = lane; idx < (P >> 1); idx += 64) {
-                const uint32_t i = ((idx & ~(jj - 1u)) << 1) | (idx & (jj - 1u));
-                const uint32_t l = i + jj;
-                const uint32_t x = buf[i], y = buf[l];
-                const bool asc = (i & k) == 0;
-                if ((x > y) == asc) {
-                    buf[i] = y;
-                    buf[l] = x;
-                }
-            }
-            wave_sync_lds();
-        }
+    // median and MAD by wave radix selects over the run held in registers (E <= 16 items per lane,
+    // item e * 64 + lane): the (n-1)/2-th (odd n) or the n/2-1-th and n/2-th smallest (even) of the
+    // u16 lengths, then the k-th smallest |2 v - C2| (17 bits) -- the same order statistics the
+    // sorted run gives (call_functions.tcc:51-53), without an LDS sort (round 3: a 512-element
+    // bitonic network per segment, most of the kernel's time)
+    uint32_t x[SEG_CAP / 64];
+#pragma unroll
+    for (int e = 0; e < (int)(SEG_CAP / 64); ++e) {
+        const uint32_t i = (uint32_t)e * 64u + lane;
+        x[e] = i < n ? buf[i] : 0u;
     }
-    if (lane != 0) return;
     float median;
     uint32_t C2;
     if (n & 1) {
-        const uint32_t md = buf[(n - 1) / 2];
+        const uint32_t md = wave_select(x, n, (n - 1) / 2, 16);
         median = (float)md;
         C2 = 2u * md;
     } else {
-        const uint32_t a = buf[n / 2 - 1], b = buf[n / 2];
+        const uint32_t a = wave_select(x, n, n / 2 - 1, 16), b = wave_select(x, n, n / 2, 16);
         median = ((float)a + (float)b) / 2;
         C2 = a + b;
     }
+#pragma unroll
+    for (int e = 0; e < (int)(SEG_CAP / 64); ++e) x[e] = 2u * x[e] > C2 ? 2u * x[e] - C2 : C2 - 2u * x[e];
     float mad;
     if (n & 1) {
-        mad = (float)kth_dev_sorted(buf, n, C2, (n - 1) / 2) * 0.5f;
+        mad = (float)wave_select(x, n, (n - 1) / 2, 17) * 0.5f;
     } else {
-        const float d1 = (float)kth_dev_sorted(buf, n, C2, n / 2 - 1) * 0.5f;
-        const float d2 = (float)kth_dev_sorted(buf, n, C2, n / 2) * 0.5f;
+        const float d1 = (float)wave_select(x, n, n / 2 - 1, 17) * 0.5f;
+        const float d2 = (float)wave_select(x, n, n / 2, 17) * 0.5f;
         mad = (d1 + d2) / 2.0f;
     }
-    emit(median, mad);
+    if (lane == 0) emit(median, mad);
 }
 
 // calls kept per sequence (segment results with count >= 0)
