@@ -6429,8 +6429,11 @@ void flush_long_chains(skm_build* b, int slot) {
     b->chain_used[slot % std::max(1, std::min(b->tune.chain_streams, 1 + skm_build::GSLOTS))] = true;
     // the batch's chains below lane_long samples one lane each (k_chains: 64 chains per wave, ~50x
     // less wave time per sample than a wave pair, ~2.5x the latency), the rest on wave pairs; in
-    // the last batch (slot 16, the tail after the last pass) only those below lane_tail
-    const int lmax = slot < 16 ? b->tune.lane_long : std::min(b->tune.lane_long, b->tune.lane_tail);
+    // the last batch (slot 16, the tail after the last pass) only those below lane_tail -- and with
+    // fewer than 8 passes in every batch (a batch then has at most a few passes to hide a lane
+    // chain's latency behind: the multi-GPU shapes, 1-4 passes per rank)
+    const bool few = (1 << b->pass_bits) < 8;
+    const int lmax = slot < 16 && !few ? b->tune.lane_long : std::min(b->tune.lane_long, b->tune.lane_tail);
     const uint32_t lane_max = lmax > 0 ? (uint32_t)lmax : 0u;
     if (!(b->tune.diag & 4) && !(b->tune.diag & 8))
         SKM_LAUNCH(b, k_chain_long, dim3(LONG_GRID), dim3(128), 0, cs, b->d_long_jobs.as<Job>(), rng, rng + 1,
