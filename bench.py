@@ -616,7 +616,7 @@ def _recall_leg(skm, kept, funcs, train, a, device, cores):
             "phase_ms": acc,
             "roofline": {"bound": "hbm", "kernel": "k_lookup<LK_EXACT>", "achieved": gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
-                         "avg_launch_ms": acc["lookup"], "traffic": _pmc_traffic("k_lookup<1>", "recall", len(lens))},
+                         "avg_launch_ms": acc["lookup"], "traffic": _pmc_traffic("k_lookup<1>", "legs", 10_000_000 if len(lens) == 1_000_000 else -1)},
             "cpu_baseline": cpu, "db_open_s": open_s}
 
 
@@ -747,7 +747,7 @@ def src_sha16() -> str:
 
 def _pmc_traffic(kernel: str, workload: str, seqs: int):
     """HBM bytes of `kernel` from the committed rocprofv3 PMC summary (profiles/r04_pmc_traffic.json,
-    tools/gpu_profile_r04.sh + tools/pmc_summary_r03.py): per build run (all launches of a step)
+    tools/gpu_profile.sh + tools/pmc_summary.py): per build run (all launches of a step)
     or per launch (legs), when it was measured on this kernel and workload size AND on the same
     device sources as this run (src_sha16); else None.  Streaming kernels count FETCH_SIZE x2,
     gather kernels x1 (profiles/r02_fetch_calib.json)."""

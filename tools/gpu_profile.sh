@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 profile set (run via gpurun from the repo root; inputs cached under /tmp/c3):
+# Profile set (run via gpurun from the repo root; inputs cached under /tmp/c3; tools/pmc_summary.py folds it):
 #   c3_stamps.log  k_bucket_process phase stamps of one C3 build (tools/c3_diag.py --stamps)
 #   prof_c3/  rocprofv3 kernel trace + stats, C3 headline build (bench.py, 1 warmup + 2 steps)
 #   prof_c2/  the same for the C2 workload (first 250 files; tools/c3_diag.py, 3 runs)

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Fold a tools/gpu_profile_r03.sh run (gpurun_out/) into profiles/:
+"""Fold a tools/gpu_profile.sh run (gpurun_out/) into profiles/ (round tag R, default r04):
 
-profiles/r03_kernel_stats_{c3,c2,legs}.csv   rocprofv3 --kernel-trace --stats summaries
-profiles/r03_pmc_traffic.json                per kernel and workload: counter KiB per build run (c3,
+profiles/R_kernel_stats_{c3,c2,legs}.csv     rocprofv3 --kernel-trace --stats summaries
+profiles/R_pmc_traffic.json                  per kernel and workload: counter KiB per build run (c3,
                                              c2: one run each) or per launch (legs), and HBM bytes
                                              corrected by the calibrated factor of the kernel's access
                                              shape (profiles/r02_fetch_calib.json: coalesced streaming
@@ -10,7 +10,7 @@ profiles/r03_pmc_traffic.json                per kernel and workload: counter Ki
                                              64-byte request each (x1)); stamped with src_sha16, the
                                              hash of the device sources it was taken on -- bench.py
                                              uses a kernel's traffic only for the same sources
-usage: python tools/pmc_summary_r03.py [gpurun_out]
+usage: python tools/pmc_summary.py [gpurun_out] [round]
 """
 import collections
 import csv
@@ -38,19 +38,21 @@ def per_kernel(path, counter):
 
 def main():
     src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out")
+    rnd = sys.argv[2] if len(sys.argv) > 2 else "r04"
     dst = os.path.join(ROOT, "profiles")
     for w in ("c3", "c2", "legs"):
         p = os.path.join(src, f"prof_{w}", "run_kernel_stats.csv")
         if os.path.exists(p):
-            shutil.copy(p, os.path.join(dst, f"r03_kernel_stats_{w}.csv"))
+            shutil.copy(p, os.path.join(dst, f"{rnd}_kernel_stats_{w}.csv"))
     sha = open(os.path.join(src, "src_sha16.txt")).read().strip()
-    out = {"round": "r03", "src_sha16": sha,
+    out = {"round": rnd, "src_sha16": sha,
            "formula": "(f * FETCH_SIZE + WRITE_SIZE) * 1024; f = 2 for streaming kernels, 1 for gather kernels "
                       "(profiles/r02_fetch_calib.json)",
            "gather_kernels": sorted(GATHER_KERNELS),
            "workloads": {"c3": {"seqs": 50000000, "unit": "per build run (16 key-range passes)"},
                          "c2": {"seqs": 1000000, "unit": "per build run"},
-                         "legs": {"queries": 10000000, "matrix_seqs": 100000, "unit": "per launch"}},
+                         "legs": {"queries": 10000000, "matrix_seqs": 100000, "recall_proteins": 1000000,
+                                  "unit": "per launch"}},
            "kernels": {}}
     for w in ("c3", "c2", "legs"):
         fp = os.path.join(src, f"pmc_{w}_fetch", "run_counter_collection.csv")
@@ -67,7 +69,7 @@ def main():
             fac = 1.0 if k in GATHER_KERNELS else 2.0
             out["kernels"].setdefault(k, {})[w] = {"FETCH_SIZE_KiB": fk, "WRITE_SIZE_KiB": wk, "launches": len(fv),
                                                    "fetch_factor": fac, "hbm_bytes": (fac * fk + wk) * 1024}
-    json.dump(out, open(os.path.join(dst, "r03_pmc_traffic.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(dst, f"{rnd}_pmc_traffic.json"), "w"), indent=1)
     tot = collections.Counter()
     for k, v in out["kernels"].items():
         for w, x in v.items():
