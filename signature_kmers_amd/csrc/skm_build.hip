@@ -4078,8 +4078,8 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
                 s_sel[0] = c0;
             }
             __syncthreads();
-            const uint32_t best_f = s_sel[0];
-            uint32_t cb = 0;
+            best_f = s_sel[0];
+            cb = 0;
             for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
                 uint32_t f[U];
     #pragma unroll
