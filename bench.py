@@ -364,6 +364,7 @@ def _alg_bytes(kernel, c, res_bytes):
         "k_extract": res_bytes,
         # per group of passes: the residues once + the group's window positions written
         "k_pass_emit": res_bytes * max(1, c.get("pass_groups", 1)) + 8 * valid,
+        "k_pass_hist": 8 * valid,                          # each pass's entries read once
         "k_pass_ids": res_bytes,                           # the per-workgroup pass tally: residues read
         "k_overflow": 16 * c["overflow_elements"],
         "k_ovf_split": 32 * c["overflow_elements"],

@@ -1522,7 +1522,9 @@ __device__ __forceinline__ uint32_t match16(const uint4 w, uint32_t v) {
 // (key_h43).  False positives of the filter only move a few light keys too.
 // ------------------------------------------------------------------------------------------
 constexpr int CMS_BITS = 22;        // count-min sketch of sampled windows: 2 rows of 2^22 u32 (32 MB)
-constexpr int BLOOM_BITS = 19;      // Bloom filter of the heavy keys: 2^19 bits (64 KB), two probes
+constexpr int BLOOM_BITS = 18;      // Bloom filter of the heavy keys: 2^18 bits (32 KB of LDS), two probes
+                                    // (C3: ~2*10^4 routed keys -> ~2 % false positives, harmless light
+                                    // keys routed too)
 constexpr int ROUTE_SAMPLE = 6;     // 1 in 2^6 window positions are sampled
 
 __device__ __forceinline__ uint32_t cms_slot(uint64_t h, int row) {
@@ -1716,30 +1718,30 @@ __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ 
 }
 
 // The window positions of a GROUP of G consecutive key-range passes, each pass's list in position
-// order, and each pass's level-1 bucket histogram (replaces round 3's per-pass k_pass_select,
-// which re-read every pass-id byte and every matched window's residues on each of the P passes:
-// 33 GB per pass at C3).  One residue scan per group: each workgroup takes the same contiguous
-// windows as k_pass_ids' tally (span, SEL_WG workgroups), hashes every window (heavy-key routing
-// as k_pass_ids), and per tile of 16 x EMIT_THREADS windows ranks the group's windows pass-major
-// by one flattened workgroup scan of the per-thread counts, so each pass's positions go out in
-// order at the workgroup's k_sel_scan offset; the G x NB histogram lives in LDS and is merged
-// once per workgroup.  Reads 1 B/residue per group, writes 8 B per window of the group.
-constexpr uint32_t EMIT_THREADS = 1024;
-constexpr uint32_t EMIT_LDS_WORDS = 16384;   // G x NB histogram words (64 KB): G = 16384 / NB, <= 4
+// order (replaces round 3's per-pass k_pass_select, which re-read every pass-id byte and every
+// matched window's residues on each of the P passes: 33 GB per pass at C3).  One residue scan per
+// group: each workgroup takes the same contiguous windows as k_pass_ids' tally (span, SEL_WG
+// workgroups), hashes every window (heavy-key routing as k_pass_ids), and per tile of
+// 16 x EMIT_THREADS windows ranks the group's windows pass-major by one flattened workgroup scan of
+// the per-thread counts, so each pass's entries go out in order at the workgroup's k_sel_scan
+// offset.  An entry is the window's position with its level-1 bucket above POS_BITS, so the
+// pass's histogram (k_pass_hist) needs no second look at the residues; 256-thread workgroups with
+// ~36 KB of LDS (the filter) keep four per CU beside the group-by.  Reads 1 B/residue per group,
+// writes 8 B per window of the group.
+constexpr uint32_t EMIT_THREADS = 256;
+constexpr int POS_BITS = 36;                 // pass entry: position | level-1 bucket << POS_BITS
+constexpr uint64_t POS_MASK = (1ull << POS_BITS) - 1ull;
 template <uint32_t G>
 __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __restrict__ res, uint64_t rp, int pass_bits,
                                                            uint32_t pass0, const uint32_t* __restrict__ bloom,
                                                            uint32_t vac, uint64_t span,
                                                            const uint64_t* __restrict__ seloff,
                                                            uint64_t* __restrict__ pos, uint64_t cap, int rem_bits,
-                                                           uint32_t NB, uint32_t* __restrict__ hist) {
-    extern __shared__ uint32_t s_dyn[];
-    uint32_t* s_h = s_dyn;                 // [G][NB]
-    uint32_t* s_bloom = s_dyn + G * NB;    // (1 << BLOOM_BITS) / 32 words when routing
+                                                           uint32_t NB) {
+    extern __shared__ uint32_t s_bloom[];  // (1 << BLOOM_BITS) / 32 words when routing
     __shared__ uint32_t s_tab[G * EMIT_THREADS + 1];
     __shared__ uint32_t s_wave[17];
     const uint32_t tid = threadIdx.x;
-    for (uint32_t k = tid; k < G * NB; k += EMIT_THREADS) s_h[k] = 0;
     const bool route = bloom != nullptr && pass_bits >= 1;
     if (route)
         for (uint32_t w = tid; w < (1u << BLOOM_BITS) / 32u; w += EMIT_THREADS) s_bloom[w] = bloom[w];
@@ -1753,6 +1755,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
     for (uint64_t t0 = a; t0 < e; t0 += 16ull * EMIT_THREADS) {
         const uint64_t base = t0 + 16ull * tid;
         uint32_t qs[4] = {~0u, ~0u, ~0u, ~0u};  // byte t: the window's pass within the group (0xFF: none)
+        uint32_t bks[16];                       // the window's level-1 bucket
         uint32_t cnt[G];
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) cnt[q] = 0;
@@ -1775,6 +1778,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
                 if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
+                bks[t] = 0;
                 if (((valid >> t) & 0xFFu) == 0xFFu && base + t < e) {
                     const uint64_t h = mix43(k);
                     uint32_t id = (uint32_t)(h >> (KEY_BITS - pass_bits));
@@ -1782,7 +1786,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                         id = R == half ? id - half : (uint32_t)(((uint32_t)(h & 0xFFFFu) * keep) >> 16);
                     const uint32_t q = id - pass0;
                     if (q < G) {
-                        atomicAdd(&s_h[q * NB + ((uint32_t)(h >> rem_bits) & (NB - 1))], 1u);
+                        bks[t] = (uint32_t)(h >> rem_bits) & (NB - 1);
 #pragma unroll
                         for (uint32_t j = 0; j < G; ++j) cnt[j] += q == j ? 1u : 0u;
                         qs[t >> 2] &= ~(0xFFu << (8 * (t & 3)));
@@ -1822,14 +1826,42 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 #pragma unroll
             for (uint32_t j = 0; j < G; ++j)
                 if (q == j) o = run[j] + nxt[j]++;
-            if (o < cap) pos[(uint64_t)q * cap + o] = base + (uint64_t)t;
+            if (o < cap) pos[(uint64_t)q * cap + o] = (base + (uint64_t)t) | ((uint64_t)bks[t] << POS_BITS);
         }
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) run[q] += s_tab[(q + 1) * EMIT_THREADS] - s_tab[q * EMIT_THREADS];
         __syncthreads();  // s_tab is rewritten by the next tile
     }
-    for (uint32_t k = tid; k < G * NB; k += EMIT_THREADS)
-        if (s_h[k]) atomicAdd(&hist[k], s_h[k]);
+}
+
+// The level-1 histogram of each pass of a group from its entries' bucket bits: blockIdx.y = the
+// pass within the group, blockIdx.x strides over its list; NB counters in LDS, merged once.
+constexpr uint32_t PH_THREADS = 512;
+__global__ __launch_bounds__(PH_THREADS) void k_pass_hist(const uint64_t* __restrict__ pos, uint64_t cap,
+                                                          const unsigned long long* __restrict__ npos, uint32_t NB,
+                                                          uint32_t* __restrict__ hist) {
+    extern __shared__ uint32_t s_h[];  // [NB]
+    const uint32_t q = blockIdx.y;
+    for (uint32_t k = threadIdx.x; k < NB; k += PH_THREADS) s_h[k] = 0;
+    __syncthreads();
+    const uint64_t n = min((uint64_t)npos[q], cap);
+    const uint64_t* p = pos + (uint64_t)q * cap;
+    constexpr uint32_t U = 4;
+    for (uint64_t j0 = (uint64_t)blockIdx.x * PH_THREADS * U; j0 < n; j0 += (uint64_t)gridDim.x * PH_THREADS * U) {
+        uint64_t v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint64_t j = j0 + u * PH_THREADS + threadIdx.x;
+            v[u] = j < n ? p[j] : ~0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u)
+            if (v[u] != ~0ull) atomicAdd(&s_h[(uint32_t)(v[u] >> POS_BITS)], 1u);
+    }
+    __syncthreads();
+    uint32_t* hq = hist + (uint64_t)q * NB;
+    for (uint32_t k = threadIdx.x; k < NB; k += PH_THREADS)
+        if (s_h[k]) atomicAdd(&hq[k], s_h[k]);
 }
 
 // Per-workgroup histogram of the level-1 buckets (count pass, one key-range pass = the whole
@@ -2047,7 +2079,7 @@ __global__ __launch_bounds__(EX_THREADS, MINB) void k_extract_stage_pos(ExtractA
 #pragma unroll
         for (int t = 0; t < SC_POS; ++t) {
             const uint64_t j = base + (uint64_t)threadIdx.x * SC_POS + t;
-            pp[t] = j < end ? pos[j] : ~0ull;
+            pp[t] = j < end ? pos[j] & POS_MASK : ~0ull;  // k_pass_emit's entry: position | bucket << POS_BITS
         }
 #pragma unroll
         for (int t = 0; t < SC_POS; ++t) raw[t] = pp[t] != ~0ull ? load_window(X.res, pp[t]) : 0ull;
@@ -3895,6 +3927,21 @@ constexpr uint32_t HV_FT = 4096;     // function table (n_functions <= HV_FT; el
 constexpr uint32_t HV_NBK = 4096;    // sequence-index buckets per key (power of two <= HV_NBK)
 constexpr uint32_t HV_BCAP = 512;    // items one wave sorts (8 per lane); a larger bucket: the LSD path
 
+// LDS histogram add of one value per lane into bins that few values share (the offset's high byte:
+// (len - i) mod 2^16 of a family's members lands in a handful of bins, so per-lane atomics would
+// serialise 64-deep on one address): one atomic per distinct bin per wave.
+__device__ __forceinline__ void wave_hist_add(uint32_t* h, uint32_t bin, bool v) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t act = __ballot(v);
+    while (act) {
+        const uint32_t l0 = (uint32_t)__ffsll((long long)act) - 1u;
+        const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)l0);
+        const uint64_t m = __ballot(v && bin == b0) & act;
+        if (lane == l0) atomicAdd(&h[b0], (uint32_t)__popcll(m));
+        act &= ~m;
+    }
+}
+
 // Bitonic sort, descending, of 64 E items held E per lane (item i = e * 64 + lane).
 template <int E>
 __device__ __forceinline__ void wave_sort_desc(uint64_t (&v)[E]) {
@@ -4011,10 +4058,8 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
                     const uint64_t same = __ballot(v && f == f0);
                     if (v && f != f0) atomicAdd(&s_fb[f], 1u);
                     if (v && f == f0 && (same & lt) == 0) atomicAdd(&s_fb[f], (uint32_t)__popcll(same));
-                    if (v) {
-                        atomicAdd(&s_oh[(uint32_t)(l[u] >> 8) & 255u], 1u);
-                        atomicAdd(&s_bk[(uint32_t)(((l[u] >> 36) * NBK) / H.n_total)], 1u);
-                    }
+                    wave_hist_add(s_oh, (uint32_t)(l[u] >> 8) & 255u, v);
+                    if (v) atomicAdd(&s_bk[(uint32_t)(((l[u] >> 36) * NBK) / H.n_total)], 1u);
                 }
             }
             __syncthreads();
@@ -4206,10 +4251,8 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
                     const bool v = f[u] != 0xFFFFFFFFu;
                     const uint32_t s = (uint32_t)(l[u] >> 36);
                     const bool best = f[u] == best_f;
-                    if (v) {
-                        if (!best && A.flags) mark_seq(A.flags, s);  // the best members' flags go out in sorted order below
-                        atomicAdd(&s_hist[(uint32_t)(l[u] >> 8) & 255u], 1u);
-                    }
+                    if (v && !best && A.flags) mark_seq(A.flags, s);  // the best members' flags go out in sorted order below
+                    wave_hist_add(s_hist, (uint32_t)(l[u] >> 8) & 255u, v);
                     if (best) {
                         sum += gl[u];
                         smax = max(smax, s);
@@ -5420,7 +5463,7 @@ void size_local(skm_build* b) {
     if (b->pass_bits > 0) {
         const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
         const uint32_t P = 1u << b->pass_bits;
-        b->emit_g = std::max<uint32_t>(1, std::min<uint32_t>({P, EMIT_LDS_WORDS / NB, 4u}));
+        b->emit_g = std::max<uint32_t>(1, std::min<uint32_t>(P, 4u));
         b->d_posg.ensure(8 * W * b->emit_g);
         b->d_histg.ensure(sizeof(uint32_t) * (uint64_t)NB * b->emit_g);
         b->d_npos.ensure(8ull * P);
@@ -5694,25 +5737,15 @@ void prepare(const Ranks& bs) {
 void emit_group(skm_build* b, uint32_t g, hipStream_t st) {
     const uint32_t G = b->emit_g;
     const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
-    SKM_HIP(hipMemsetAsync(b->d_histg.p, 0, sizeof(uint32_t) * NB * G, st));
     const int rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
-    const uint32_t lds = 4u * G * NB + (b->route ? (1u << BLOOM_BITS) / 8 : 0u);
+    const uint32_t lds = b->route ? (1u << BLOOM_BITS) / 8 : 0u;
     const uint32_t* bloom = b->route ? b->d_bloom.as<uint32_t>() : nullptr;
     const uint32_t vac = (uint32_t)std::max(0, b->tune.route_vacate);
     const uint64_t cap = std::max<uint64_t>(b->pass_max, 1);
-    // the histogram + Bloom filter can pass the 64 KB default dynamic-LDS limit (G = 4 with routing)
-    static bool lds_attr[3] = {false, false, false};
-    const int gi = G == 4 ? 2 : G == 2 ? 1 : 0;
-    if (lds > 65536 && !lds_attr[gi]) {
-        const void* fn = G == 4 ? reinterpret_cast<const void*>(k_pass_emit<4>)
-                         : G == 2 ? reinterpret_cast<const void*>(k_pass_emit<2>) : reinterpret_cast<const void*>(k_pass_emit<1>);
-        SKM_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u * EMIT_LDS_WORDS + (1u << BLOOM_BITS) / 8)));
-        lds_attr[gi] = true;
-    }
 #define SKM_EMIT(GG)                                                                                                    \
     SKM_LAUNCH_AS(b, "k_pass_emit", k_pass_emit<GG>, dim3(SEL_WG), dim3(EMIT_THREADS), lds, st, b->d_res.as<uint8_t>(), \
                   b->rp, b->pass_bits, g * G, bloom, vac, b->sel_span, b->d_seloff.as<uint64_t>(), b->d_posg.as<uint64_t>(), \
-                  cap, rem_bits, NB, b->d_histg.as<uint32_t>())
+                  cap, rem_bits, NB)
     if (G == 4)
         SKM_EMIT(4);
     else if (G == 2)
@@ -5720,6 +5753,10 @@ void emit_group(skm_build* b, uint32_t g, hipStream_t st) {
     else
         SKM_EMIT(1);
 #undef SKM_EMIT
+    // the group's histograms from the entries' bucket bits (8 B per window read, no residues)
+    SKM_HIP(hipMemsetAsync(b->d_histg.p, 0, sizeof(uint32_t) * NB * G, st));
+    SKM_LAUNCH(b, k_pass_hist, dim3(256, G), dim3(PH_THREADS), 4u * NB, st, b->d_posg.as<uint64_t>(), cap,
+               b->d_npos.as<unsigned long long>() + (uint64_t)g * G, NB, b->d_histg.as<uint32_t>());
     SKM_HIP(hipGetLastError());
     if (st != b->stream) SKM_HIP(hipEventRecord(b->ev_emit, st));
 }
