@@ -5,6 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/pmc_sq
 mkdir -p "$O"
 export TMPDIR=/tmp
+export SKM_PROBE_ANNOT=${SKM_PROBE_ANNOT:-1}
 cd /tmp
 timeout -k 10 300 rocprofv3 -L > "$O/counters_list.txt" 2>&1 || true
 i=0
