@@ -1740,7 +1740,9 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                                                            uint32_t NB) {
     extern __shared__ uint32_t s_bloom[];  // (1 << BLOOM_BITS) / 32 words when routing
     __shared__ uint32_t s_tab[G * EMIT_THREADS + 1];
+    __shared__ uint32_t s_out[16 * EMIT_THREADS];  // the tile's entries, pass-major: window | bucket << 12
     __shared__ uint32_t s_wave[17];
+    static_assert(16 * EMIT_THREADS <= 4096, "tile-relative windows fit 12 bits");
     const uint32_t tid = threadIdx.x;
     const bool route = bloom != nullptr && pass_bits >= 1;
     if (route)
@@ -1815,22 +1817,38 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
             if (tid == 0) s_tab[G * EMIT_THREADS] = tot;
         }
         __syncthreads();
+        // the tile's entries staged pass-major in LDS, then written as one contiguous run per pass
         uint32_t nxt[G];
 #pragma unroll
-        for (uint32_t q = 0; q < G; ++q) nxt[q] = s_tab[q * EMIT_THREADS + tid] - s_tab[q * EMIT_THREADS];
+        for (uint32_t q = 0; q < G; ++q) nxt[q] = s_tab[q * EMIT_THREADS + tid];
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             const uint32_t q = (qs[t >> 2] >> (8 * (t & 3))) & 0xFFu;
             if (q >= G) continue;
-            uint64_t o = 0;
+            uint32_t f = 0;
 #pragma unroll
             for (uint32_t j = 0; j < G; ++j)
-                if (q == j) o = run[j] + nxt[j]++;
-            if (o < cap) pos[(uint64_t)q * cap + o] = (base + (uint64_t)t) | ((uint64_t)bks[t] << POS_BITS);
+                if (q == j) f = nxt[j]++;
+            s_out[f] = (16u * tid + (uint32_t)t) | (bks[t] << 12);
+        }
+        __syncthreads();
+        uint32_t qa[G + 1];
+#pragma unroll
+        for (uint32_t q = 0; q <= G; ++q) qa[q] = s_tab[q * EMIT_THREADS];
+        for (uint32_t j = tid; j < qa[G]; j += EMIT_THREADS) {
+            uint32_t q = 0;
+#pragma unroll
+            for (uint32_t k = 1; k < G; ++k) q += j >= qa[k] ? 1u : 0u;
+            uint64_t o = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < G; ++k)
+                if (q == k) o = run[k] + (j - qa[k]);
+            const uint32_t v = s_out[j];
+            if (o < cap) pos[(uint64_t)q * cap + o] = (t0 + (v & 4095u)) | ((uint64_t)(v >> 12) << POS_BITS);
         }
 #pragma unroll
-        for (uint32_t q = 0; q < G; ++q) run[q] += s_tab[(q + 1) * EMIT_THREADS] - s_tab[q * EMIT_THREADS];
-        __syncthreads();  // s_tab is rewritten by the next tile
+        for (uint32_t q = 0; q < G; ++q) run[q] += qa[q + 1] - qa[q];
+        __syncthreads();  // s_tab and s_out are rewritten by the next tile
     }
 }
 
