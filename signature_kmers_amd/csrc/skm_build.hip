@@ -1719,82 +1719,57 @@ __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ 
 
 // The window positions of a GROUP of G consecutive key-range passes, each pass's list in position
 // order (replaces round 3's per-pass k_pass_select, which re-read every pass-id byte and every
-// matched window's residues on each of the P passes: 33 GB per pass at C3).  One residue scan per
-// group: each workgroup takes the same contiguous windows as k_pass_ids' tally (span, SEL_WG
-// workgroups), hashes every window (heavy-key routing as k_pass_ids), and per tile of
-// 16 x EMIT_THREADS windows ranks the group's windows pass-major by one flattened workgroup scan of
-// the per-thread counts, so each pass's entries go out in order at the workgroup's k_sel_scan
-// offset.  An entry is the window's position with its level-1 bucket above POS_BITS, so the
-// pass's histogram (k_pass_hist) needs no second look at the residues; 256-thread workgroups with
-// ~36 KB of LDS (the filter) keep four per CU beside the group-by.  Reads 1 B/residue per group,
-// writes 8 B per window of the group.
+// matched window's residues on each of the P passes: 33 GB per pass at C3).  One scan of the pass
+// ids (k_pass_ids, once per run) per group: each workgroup takes the same contiguous windows as
+// k_pass_ids' tally (span, SEL_WG workgroups), re-hashes only the group's windows for their
+// level-1 bucket, and per tile of 16 x EMIT_THREADS windows ranks them pass-major by one flattened
+// workgroup scan of the per-thread counts; the tile's entries are staged in LDS and go out as one
+// contiguous run per pass at the workgroup's k_sel_scan offset.  An entry is the window's position
+// with its level-1 bucket above POS_BITS, so the pass's histogram (k_pass_hist) needs no second
+// look at the residues.  (Hashing every window in every group instead measured ~50 ms per group at
+// C3: ALU-bound.)  Reads 1 B/residue of ids + the group's windows per group, writes 8 B per window.
 constexpr uint32_t EMIT_THREADS = 256;
 constexpr int POS_BITS = 36;                 // pass entry: position | level-1 bucket << POS_BITS
 constexpr uint64_t POS_MASK = (1ull << POS_BITS) - 1ull;
 template <uint32_t G>
-__global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __restrict__ res, uint64_t rp, int pass_bits,
-                                                           uint32_t pass0, const uint32_t* __restrict__ bloom,
-                                                           uint32_t vac, uint64_t span,
+__global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __restrict__ res, const uint8_t* __restrict__ ids,
+                                                           uint64_t rp, uint32_t pass0, uint64_t span,
                                                            const uint64_t* __restrict__ seloff,
                                                            uint64_t* __restrict__ pos, uint64_t cap, int rem_bits,
                                                            uint32_t NB) {
-    extern __shared__ uint32_t s_bloom[];  // (1 << BLOOM_BITS) / 32 words when routing
     __shared__ uint32_t s_tab[G * EMIT_THREADS + 1];
     __shared__ uint32_t s_out[16 * EMIT_THREADS];  // the tile's entries, pass-major: window | bucket << 12
     __shared__ uint32_t s_wave[17];
     static_assert(16 * EMIT_THREADS <= 4096, "tile-relative windows fit 12 bits");
     const uint32_t tid = threadIdx.x;
-    const bool route = bloom != nullptr && pass_bits >= 1;
-    if (route)
-        for (uint32_t w = tid; w < (1u << BLOOM_BITS) / 32u; w += EMIT_THREADS) s_bloom[w] = bloom[w];
-    const uint32_t P = 1u << pass_bits, half = P >> 1;
-    const uint32_t R = vac ? min(vac, P - 1u) : half, keep = P - R;
     uint64_t run[G];
 #pragma unroll
     for (uint32_t q = 0; q < G; ++q) run[q] = seloff[(uint64_t)(pass0 + q) * (SEL_WG + 1) + blockIdx.x];
-    __syncthreads();
     const uint64_t a = (uint64_t)blockIdx.x * span, e = min(rp, a + span);
+    // the next tile's 16 pass ids per thread are loaded while this tile is ranked and written
+    uint4 nid = make_uint4(~0u, ~0u, ~0u, ~0u);
+    if (a + 16ull * tid < e) nid = *reinterpret_cast<const uint4*>(ids + a + 16ull * tid);
     for (uint64_t t0 = a; t0 < e; t0 += 16ull * EMIT_THREADS) {
         const uint64_t base = t0 + 16ull * tid;
+        const uint4 id4 = nid;
+        if (base + 16ull * EMIT_THREADS < e) nid = *reinterpret_cast<const uint4*>(ids + base + 16ull * EMIT_THREADS);
+        const uint32_t idw[4] = {id4.x, id4.y, id4.z, id4.w};
         uint32_t qs[4] = {~0u, ~0u, ~0u, ~0u};  // byte t: the window's pass within the group (0xFF: none)
         uint32_t bks[16];                       // the window's level-1 bucket
         uint32_t cnt[G];
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) cnt[q] = 0;
-        if (base < e) {
-            const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
-            const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
-            const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-            uint32_t code[24];
-            uint32_t valid = 0;
 #pragma unroll
-            for (int j = 0; j < 24; ++j) {
-                const uint32_t cd = residue_code((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
-                valid |= (cd < 40u ? 1u : 0u) << j;
-                code[j] = cd < 40u ? cd : 0u;
-            }
-            uint64_t k = 0;
+        for (int t = 0; t < 16; ++t) {
+            bks[t] = 0;
+            const uint32_t q = ((idw[t >> 2] >> (8 * (t & 3))) & 0xFFu) - pass0;  // 0xFF (no window): >= G
+            if (q < G && base + t < e) {
+                // the group's windows only (1/P of them per pass): re-hash for the bucket
+                bks[t] = (uint32_t)(window_hash(load_window(res, base + t)) >> rem_bits) & (NB - 1);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
-            constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
-#pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
-                bks[t] = 0;
-                if (((valid >> t) & 0xFFu) == 0xFFu && base + t < e) {
-                    const uint64_t h = mix43(k);
-                    uint32_t id = (uint32_t)(h >> (KEY_BITS - pass_bits));
-                    if (route && id >= keep && bloom_has(s_bloom, h))
-                        id = R == half ? id - half : (uint32_t)(((uint32_t)(h & 0xFFFFu) * keep) >> 16);
-                    const uint32_t q = id - pass0;
-                    if (q < G) {
-                        bks[t] = (uint32_t)(h >> rem_bits) & (NB - 1);
-#pragma unroll
-                        for (uint32_t j = 0; j < G; ++j) cnt[j] += q == j ? 1u : 0u;
-                        qs[t >> 2] &= ~(0xFFu << (8 * (t & 3)));
-                        qs[t >> 2] |= q << (8 * (t & 3));
-                    }
-                }
+                for (uint32_t j = 0; j < G; ++j) cnt[j] += q == j ? 1u : 0u;
+                qs[t >> 2] &= ~(0xFFu << (8 * (t & 3)));
+                qs[t >> 2] |= q << (8 * (t & 3));
             }
         }
 #pragma unroll
@@ -4899,6 +4874,7 @@ struct skm_build {
     int pass_bits = 0;
     uint64_t pass_max = 0;              // valid windows of the largest pass (this shard)
     uint64_t valid_total = 0;           // valid windows of this shard
+    DevBuf d_ids;                       // per-window pass id (pass_bits > 0; k_pass_ids, once per run)
     DevBuf d_bloom;                     // heavy-key routing filter (route)
     std::vector<uint64_t> cnt64;        // valid windows by the top 6 hash bits (size_passes)
     bool route = false;
@@ -5483,6 +5459,8 @@ void size_local(skm_build* b) {
         const uint32_t P = 1u << b->pass_bits;
         b->emit_g = std::max<uint32_t>(1, std::min<uint32_t>(P, 4u));
         b->d_posg.ensure(8 * W * b->emit_g);
+        b->d_ids.ensure(((b->rp + 15) & ~15ull) + 64);
+        SKM_HIP(hipMemsetAsync(b->d_ids.p, 0xFF, ((b->rp + 15) & ~15ull) + 64, b->stream));  // padding: no window
         b->d_histg.ensure(sizeof(uint32_t) * (uint64_t)NB * b->emit_g);
         b->d_npos.ensure(8ull * P);
         b->d_selrows.ensure(4ull * SEL_WG * P);
@@ -5756,13 +5734,10 @@ void emit_group(skm_build* b, uint32_t g, hipStream_t st) {
     const uint32_t G = b->emit_g;
     const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
     const int rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
-    const uint32_t lds = b->route ? (1u << BLOOM_BITS) / 8 : 0u;
-    const uint32_t* bloom = b->route ? b->d_bloom.as<uint32_t>() : nullptr;
-    const uint32_t vac = (uint32_t)std::max(0, b->tune.route_vacate);
     const uint64_t cap = std::max<uint64_t>(b->pass_max, 1);
 #define SKM_EMIT(GG)                                                                                                    \
-    SKM_LAUNCH_AS(b, "k_pass_emit", k_pass_emit<GG>, dim3(SEL_WG), dim3(EMIT_THREADS), lds, st, b->d_res.as<uint8_t>(), \
-                  b->rp, b->pass_bits, g * G, bloom, vac, b->sel_span, b->d_seloff.as<uint64_t>(), b->d_posg.as<uint64_t>(), \
+    SKM_LAUNCH_AS(b, "k_pass_emit", k_pass_emit<GG>, dim3(SEL_WG), dim3(EMIT_THREADS), 0, st, b->d_res.as<uint8_t>(), \
+                  b->d_ids.as<uint8_t>(), b->rp, g * G, b->sel_span, b->d_seloff.as<uint64_t>(), b->d_posg.as<uint64_t>(), \
                   cap, rem_bits, NB)
     if (G == 4)
         SKM_EMIT(4);
@@ -6409,9 +6384,9 @@ void begin_run(skm_build* b) {
                            b->d_data.as<skm_stored_kmer_data>());
     if (b->pass_bits) {
         const uint32_t P = 1u << b->pass_bits;
-        // every workgroup's windows per pass (the tally k_pass_emit's offsets come from)
+        // every window's pass id and every workgroup's windows per pass (k_pass_emit's input and offsets)
         SKM_LAUNCH(b, k_pass_ids, dim3(SEL_WG), dim3(256), 4u * P + (b->route ? (1u << BLOOM_BITS) / 8 : 0u), st,
-                   b->d_res.as<uint8_t>(), b->rp, b->pass_bits, 0, nullptr, nullptr,
+                   b->d_res.as<uint8_t>(), b->rp, b->pass_bits, 0, b->d_ids.as<uint8_t>(), nullptr,
                    b->route ? b->d_bloom.as<uint32_t>() : nullptr, P, b->d_selrows.as<uint32_t>(), b->sel_span,
                    (uint32_t)std::max(0, b->tune.route_vacate));
         SKM_LAUNCH(b, k_sel_scan, dim3(P), dim3(1024), 0, st, b->d_selrows.as<uint32_t>(), SEL_WG, P,
