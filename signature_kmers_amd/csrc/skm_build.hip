@@ -315,6 +315,13 @@ __device__ __forceinline__ uint64_t xs64(uint64_t v, int d) {
 }
 
 // Inclusive wave scan on DPP: row_shr 1/2/4/8 within rows of 16, then row_bcast 15 / 31.
+// LDS written by some lanes of a wave, read by others: a wave-scope fence pair around the barrier
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
@@ -1694,7 +1701,7 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
 // pass p at off[p * (nwg + 1) + w] (exclusive scan over w), npos[p] = the pass's window count
 // (checked against the list's capacity: a larger pass fails the run, SKM_E_STATE).  One workgroup
 // per pass.
-constexpr uint32_t SEL_WG = 2048;
+constexpr uint32_t SEL_WG = 8192;   // tally rows: k_pass_ids workgroups = k_pass_emit waves
 __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ rows, uint32_t nwg, uint32_t P,
                                                    uint64_t* __restrict__ off, unsigned long long* __restrict__ npos,
                                                    uint64_t cap, unsigned long long* __restrict__ run) {
@@ -1719,16 +1726,17 @@ __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ 
 
 // The window positions of a GROUP of G consecutive key-range passes, each pass's list in position
 // order (replaces round 3's per-pass k_pass_select, which re-read every pass-id byte and every
-// matched window's residues on each of the P passes: 33 GB per pass at C3).  One scan of the pass
-// ids (k_pass_ids, once per run) per group: each workgroup takes the same contiguous windows as
-// k_pass_ids' tally (span, SEL_WG workgroups), re-hashes only the group's windows for their
-// level-1 bucket, and per tile of 16 x EMIT_THREADS windows ranks them pass-major by one flattened
-// workgroup scan of the per-thread counts; the tile's entries are staged in LDS and go out as one
-// contiguous run per pass at the workgroup's k_sel_scan offset.  An entry is the window's position
-// with its level-1 bucket above POS_BITS, so the pass's histogram (k_pass_hist) needs no second
-// look at the residues.  (Hashing every window in every group instead measured ~50 ms per group at
-// C3: ALU-bound.)  Reads 1 B/residue of ids + the group's windows per group, writes 8 B per window.
-constexpr uint32_t EMIT_THREADS = 256;
+// matched window's residues on each of the P passes: 33 GB per pass at C3).  One wave per tally
+// row (k_pass_ids' workgroup span, SEL_WG of them): per tile of 64 x 16 windows each lane loads its
+// 16 pass ids and its 32 residue bytes (both coalesced), rolls the 16 keys in registers and mixes
+// only the group's windows for their level-1 bucket; the wave ranks them pass-major with DPP
+// scans, stages the tile's entries in its own 4 KB of LDS and writes one contiguous run per pass
+// at its k_sel_scan offset -- no workgroup barrier anywhere (round-4 first form: 1024-thread
+// workgroups hashing every window of every group, ~50 ms per group at C3).  An entry is the
+// window's position with its level-1 bucket above POS_BITS, so the pass's histogram (k_pass_hist)
+// needs no second look at the residues.  Reads 1 B of id + 1 B of residue per window per group,
+// writes 8 B per window of the group.
+constexpr uint32_t EMIT_THREADS = 64;
 constexpr int POS_BITS = 36;                 // pass entry: position | level-1 bucket << POS_BITS
 constexpr uint64_t POS_MASK = (1ull << POS_BITS) - 1ull;
 template <uint32_t G>
@@ -1737,65 +1745,65 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                                                            const uint64_t* __restrict__ seloff,
                                                            uint64_t* __restrict__ pos, uint64_t cap, int rem_bits,
                                                            uint32_t NB) {
-    __shared__ uint32_t s_tab[G * EMIT_THREADS + 1];
-    __shared__ uint32_t s_out[16 * EMIT_THREADS];  // the tile's entries, pass-major: window | bucket << 12
-    __shared__ uint32_t s_wave[17];
-    static_assert(16 * EMIT_THREADS <= 4096, "tile-relative windows fit 12 bits");
-    const uint32_t tid = threadIdx.x;
+    __shared__ uint32_t s_out[16 * 64];  // the tile's entries, pass-major: window (10 bits) | bucket << 10
+    const uint32_t lane = threadIdx.x;
     uint64_t run[G];
 #pragma unroll
     for (uint32_t q = 0; q < G; ++q) run[q] = seloff[(uint64_t)(pass0 + q) * (SEL_WG + 1) + blockIdx.x];
     const uint64_t a = (uint64_t)blockIdx.x * span, e = min(rp, a + span);
-    // the next tile's 16 pass ids per thread are loaded while this tile is ranked and written
-    uint4 nid = make_uint4(~0u, ~0u, ~0u, ~0u);
-    if (a + 16ull * tid < e) nid = *reinterpret_cast<const uint4*>(ids + a + 16ull * tid);
-    for (uint64_t t0 = a; t0 < e; t0 += 16ull * EMIT_THREADS) {
-        const uint64_t base = t0 + 16ull * tid;
-        const uint4 id4 = nid;
-        if (base + 16ull * EMIT_THREADS < e) nid = *reinterpret_cast<const uint4*>(ids + base + 16ull * EMIT_THREADS);
-        const uint32_t idw[4] = {id4.x, id4.y, id4.z, id4.w};
+    for (uint64_t t0 = a; t0 < e; t0 += 16ull * 64) {
+        const uint64_t base = t0 + 16ull * lane;
         uint32_t qs[4] = {~0u, ~0u, ~0u, ~0u};  // byte t: the window's pass within the group (0xFF: none)
         uint32_t bks[16];                       // the window's level-1 bucket
         uint32_t cnt[G];
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) cnt[q] = 0;
+        if (base < e) {
+            const uint4 id4 = *reinterpret_cast<const uint4*>(ids + base);
+            const uint32_t idw[4] = {id4.x, id4.y, id4.z, id4.w};
+            uint32_t any = 0;
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            bks[t] = 0;
-            const uint32_t q = ((idw[t >> 2] >> (8 * (t & 3))) & 0xFFu) - pass0;  // 0xFF (no window): >= G
-            if (q < G && base + t < e) {
-                // the group's windows only (1/P of them per pass): re-hash for the bucket
-                bks[t] = (uint32_t)(window_hash(load_window(res, base + t)) >> rem_bits) & (NB - 1);
+            for (int t = 0; t < 16; ++t) {
+                const uint32_t q = ((idw[t >> 2] >> (8 * (t & 3))) & 0xFFu) - pass0;  // 0xFF (no window): >= G
+                if (q < G && base + t < e) {
+                    any |= 1u << t;
+                    qs[t >> 2] &= ~(0xFFu << (8 * (t & 3)));
+                    qs[t >> 2] |= q << (8 * (t & 3));
 #pragma unroll
-                for (uint32_t j = 0; j < G; ++j) cnt[j] += q == j ? 1u : 0u;
-                qs[t >> 2] &= ~(0xFFu << (8 * (t & 3)));
-                qs[t >> 2] |= q << (8 * (t & 3));
+                    for (uint32_t j = 0; j < G; ++j) cnt[j] += q == j ? 1u : 0u;
+                }
+            }
+            if (any) {  // the 16 keys rolled from the lane's 24 residues, mixed for the group's windows
+                const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
+                const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
+                const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+                uint32_t code[24];
+#pragma unroll
+                for (int j = 0; j < 24; ++j) {
+                    const uint32_t cd = residue_code((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+                    code[j] = cd < 40u ? cd : 0u;
+                }
+                uint64_t k = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
+                constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
+                    bks[t] = ((any >> t) & 1u) ? (uint32_t)(mix43(k) >> rem_bits) & (NB - 1) : 0u;
+                }
             }
         }
+        // pass-major ranks of the wave's tile: one DPP scan per pass of the group
+        uint32_t off[G], qa[G + 1];
+        qa[0] = 0;
 #pragma unroll
-        for (uint32_t q = 0; q < G; ++q) s_tab[q * EMIT_THREADS + tid] = cnt[q];
-        __syncthreads();
-        {   // exclusive scan of s_tab in pass-major order; thread tid owns entries [G tid, G tid + G)
-            uint32_t loc[G], sum = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < G; ++j) {
-                loc[j] = s_tab[G * tid + j];
-                sum += loc[j];
-            }
-            uint32_t tot;
-            uint32_t ex = wg_exclusive_scan(sum, s_wave, tot);  // its barriers order the reads above
-#pragma unroll
-            for (uint32_t j = 0; j < G; ++j) {
-                s_tab[G * tid + j] = ex;
-                ex += loc[j];
-            }
-            if (tid == 0) s_tab[G * EMIT_THREADS] = tot;
+        for (uint32_t q = 0; q < G; ++q) {
+            const uint32_t inc = wave_incl_scan(cnt[q]);
+            const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            off[q] = qa[q] + inc - cnt[q];
+            qa[q + 1] = qa[q] + tot;
         }
-        __syncthreads();
-        // the tile's entries staged pass-major in LDS, then written as one contiguous run per pass
-        uint32_t nxt[G];
-#pragma unroll
-        for (uint32_t q = 0; q < G; ++q) nxt[q] = s_tab[q * EMIT_THREADS + tid];
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             const uint32_t q = (qs[t >> 2] >> (8 * (t & 3))) & 0xFFu;
@@ -1803,14 +1811,11 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
             uint32_t f = 0;
 #pragma unroll
             for (uint32_t j = 0; j < G; ++j)
-                if (q == j) f = nxt[j]++;
-            s_out[f] = (16u * tid + (uint32_t)t) | (bks[t] << 12);
+                if (q == j) f = off[j]++;
+            s_out[f] = (16u * lane + (uint32_t)t) | (bks[t] << 10);
         }
-        __syncthreads();
-        uint32_t qa[G + 1];
-#pragma unroll
-        for (uint32_t q = 0; q <= G; ++q) qa[q] = s_tab[q * EMIT_THREADS];
-        for (uint32_t j = tid; j < qa[G]; j += EMIT_THREADS) {
+        wave_sync();
+        for (uint32_t j = lane; j < qa[G]; j += 64) {
             uint32_t q = 0;
 #pragma unroll
             for (uint32_t k = 1; k < G; ++k) q += j >= qa[k] ? 1u : 0u;
@@ -1819,11 +1824,11 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
             for (uint32_t k = 0; k < G; ++k)
                 if (q == k) o = run[k] + (j - qa[k]);
             const uint32_t v = s_out[j];
-            if (o < cap) pos[(uint64_t)q * cap + o] = (t0 + (v & 4095u)) | ((uint64_t)(v >> 12) << POS_BITS);
+            if (o < cap) pos[(uint64_t)q * cap + o] = (t0 + (v & 1023u)) | ((uint64_t)(v >> 10) << POS_BITS);
         }
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) run[q] += qa[q + 1] - qa[q];
-        __syncthreads();  // s_tab and s_out are rewritten by the next tile
+        wave_sync();  // s_out is rewritten by the next tile
     }
 }
 
@@ -2402,11 +2407,6 @@ __device__ __forceinline__ void bm_combine(uint32_t& cand, uint32_t& cc) {
     cand = (uint32_t)__shfl((int)cand, 0, 64);
 }
 
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // ------------------------------------------------------------------------------------------
 // Groups of 2..64 members, packed 64/S to a wave in aligned segments of S lanes (S = 2..64, the
