@@ -5849,8 +5849,6 @@ void phase_extract(skm_build* b, uint32_t pass) {
     else
         SKM_LAUNCH(b, k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
                            tmp_hi(b, pass), tmp_lo(b, pass));
-    // the group's slots are free once its last pass has staged its elements
-    if (b->pass_bits && pass % b->emit_g == b->emit_g - 1) SKM_HIP(hipEventRecord(b->ev_staged, st));
     const uint32_t nsl = (uint32_t)(ceil_div(b->pass_max, SC_SLICE) + (1u << SC_L0_BITS));
     SKM_LAUNCH(b, k_split_stage, dim3(nsl), dim3(EX_THREADS), 0, st, tmp_hi(b, pass),
                        tmp_lo(b, pass), b->d_bstart.as<uint64_t>(), nbits, b->d_slices.as<uint32_t>(),
@@ -6122,6 +6120,10 @@ void phase_group(skm_build* b, uint32_t pass) {
         SKM_LAUNCH_AS(b, "k_partition", (k_partition<2048, BP_THREADS, 3>), dim3(NB1), dim3(BP_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[10], st));
+    // the group's position slots are free once its last pass has staged its elements; the next
+    // group's scan waits until this pass's partition is done too, so that it overlaps the group-by
+    // rather than the scatters on the step's critical path
+    if (b->pass_bits && pass % b->emit_g == b->emit_g - 1) SKM_HIP(hipEventRecord(b->ev_staged, st));
     // ---- the overflow plan (the pass's element count: the last bucket start, or the exchange's) ----
     const unsigned long long* nloc_d;
     if (multi) {  // the received element count: k_recv_plan's vstart[NB1]
@@ -6251,7 +6253,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     SKM_HIP(hipEventRecord(b->ev[5], st));
     if (b->tune.serial_overflow) launch_overflow();
     // the next group's positions overlap this pass's group-by on stx (the group's slots were
-    // last read by this pass's staging)
+    // last read by this pass's staging; ev_staged is recorded after the partition)
     if (b->pass_bits && pass + 1 < NP && (pass + 1) % b->emit_g == 0 && b->tune.prefetch) {
         SKM_HIP(hipStreamWaitEvent(b->stx, b->ev_staged, 0));
         emit_group(b, (pass + 1) / b->emit_g, b->stx);
