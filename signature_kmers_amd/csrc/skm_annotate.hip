@@ -412,6 +412,24 @@ __device__ uint32_t kth_dev_sorted(const uint32_t* v, uint32_t n, uint32_t C2, u
 
 constexpr int SEG_WAVES = 4;
 
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d, 64));
+    return v;
+}
+
+// rcp[k] = RN(1 / (k + 1)) in float, by the same correctly rounded division the four-lane mean
+// used inline (-fhip-fp32-correctly-rounded-divide-sqrt): k_seg_process reads it as a table
+__global__ void k_rcp_init(float* __restrict__ rcp, uint32_t n) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) rcp[k] = 1.0f / (float)(k + 1);
+}
+
 // k-th smallest (0-based) of a wave's n items x[e] (item e * 64 + lane; values < 2^bits): MSD
 // radix select, one bit per step, counted on ballots (wave-uniform result)
 template <int E>
@@ -444,7 +462,8 @@ template <bool LEGACY_MAD>  // mad_mode 1 in its own instantiation: no register 
 __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, const uint4* __restrict__ segs,
                                                                 uint32_t nseg, skm_kmer_call* __restrict__ out,
                                                                 uint16_t* __restrict__ pool,
-                                                                unsigned long long* __restrict__ pool_ctr) {
+                                                                unsigned long long* __restrict__ pool_ctr,
+                                                                const float* __restrict__ rcp) {
     __shared__ uint32_t sv[SEG_WAVES][SEG_CAP];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t j = blockIdx.x * SEG_WAVES + wave;
@@ -490,8 +509,10 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
         const uint32_t end = n - (n % 4);
         float mu = 0, fi = 1;
         if (lane < 4) {
+            // inv = RN(1 / fi) from the table (k_rcp_init: the same correctly rounded division),
+            // a uniform load off the recurrence's chain
             for (uint32_t q = lane; q < end; q += 4) {
-                const float inv = 1.0f / fi;
+                const float inv = rcp[q >> 2];
                 float t = (float)buf[q] - mu;
                 t *= inv;
                 mu += t;
@@ -534,31 +555,44 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
     // u16 lengths, then the k-th smallest |2 v - C2| (17 bits) -- the same order statistics the
     // sorted run gives (call_functions.tcc:51-53), without an LDS sort (round 3: a 512-element
     // bitonic network per segment, most of the kernel's time)
+    // the selects run over x - min (a segment's lengths span a few hundred, not 2^16: ~9 radix
+    // steps instead of 16 / 17)
     uint32_t x[SEG_CAP / 64];
+    uint32_t vmin = 0xFFFFu, vmax = 0u;
 #pragma unroll
     for (int e = 0; e < (int)(SEG_CAP / 64); ++e) {
         const uint32_t i = (uint32_t)e * 64u + lane;
         x[e] = i < n ? buf[i] : 0u;
+        if (i < n) {
+            vmin = min(vmin, x[e]);
+            vmax = max(vmax, x[e]);
+        }
     }
+    vmin = wave_min_u32(vmin);
+    vmax = wave_max_u32(vmax);
+    const int vbits = 32 - __clz(vmax - vmin);  // bits of the largest x - vmin (0: all equal)
+#pragma unroll
+    for (int e = 0; e < (int)(SEG_CAP / 64); ++e) x[e] -= vmin;
     float median;
-    uint32_t C2;
+    uint32_t C2;  // 2 * (median - vmin): the deviations |2 v - C2| are shift-invariant
     if (n & 1) {
-        const uint32_t md = wave_select(x, n, (n - 1) / 2, 16);
-        median = (float)md;
+        const uint32_t md = wave_select(x, n, (n - 1) / 2, vbits);
+        median = (float)(md + vmin);
         C2 = 2u * md;
     } else {
-        const uint32_t a = wave_select(x, n, n / 2 - 1, 16), b = wave_select(x, n, n / 2, 16);
-        median = ((float)a + (float)b) / 2;
+        const uint32_t a = wave_select(x, n, n / 2 - 1, vbits), b = wave_select(x, n, n / 2, vbits);
+        median = ((float)(a + vmin) + (float)(b + vmin)) / 2;
         C2 = a + b;
     }
 #pragma unroll
     for (int e = 0; e < (int)(SEG_CAP / 64); ++e) x[e] = 2u * x[e] > C2 ? 2u * x[e] - C2 : C2 - 2u * x[e];
+    const int dbits = vbits + 1;  // |2 v - C2| <= 2 (vmax - vmin)
     float mad;
     if (n & 1) {
-        mad = (float)wave_select(x, n, (n - 1) / 2, 17) * 0.5f;
+        mad = (float)wave_select(x, n, (n - 1) / 2, dbits) * 0.5f;
     } else {
-        const float d1 = (float)wave_select(x, n, n / 2 - 1, 17) * 0.5f;
-        const float d2 = (float)wave_select(x, n, n / 2, 17) * 0.5f;
+        const float d1 = (float)wave_select(x, n, n / 2 - 1, dbits) * 0.5f;
+        const float d2 = (float)wave_select(x, n, n / 2, dbits) * 0.5f;
         mad = (d1 + d2) / 2.0f;
     }
     if (lane == 0) emit(median, mad);
@@ -704,6 +738,7 @@ struct skm_query {
     uint64_t rp = 0, n_windows = 0;
     DevBuf d_res, d_meta, d_hits, d_scr, d_scr_off, d_caps, d_cap_off, d_slots, d_counts, d_call_off, d_calls;
     DevBuf d_seg_off, d_segs, d_segres, d_pool_ctr;
+    DevBuf d_rcp;                   // RN(1/k), k = 1 .. SEG_CAP/4 + 1 (k_seg_process's mean)
     Scanner scan;
     uint64_t n_calls = 0;
     bool ran = false;
@@ -888,10 +923,15 @@ void query_run(skm_query* q, const skm_annot_opts* o) {
                            q->d_cap_off.as<uint64_t>(), q->d_seg_off.as<uint64_t>(), ns, q->d_segs.as<uint4>());
         if (nseg)
         {
+            constexpr uint32_t NRCP = SEG_CAP / 4 + 1;
+            if (!q->d_rcp.p) {
+                q->d_rcp.ensure(4 * NRCP);
+                hipLaunchKernelGGL(k_rcp_init, dim3(ceil_div(NRCP, 256)), dim3(256), 0, st, q->d_rcp.as<float>(), NRCP);
+            }
             auto kseg = A.mad_mode == 1 ? k_seg_process<true> : k_seg_process<false>;
             hipLaunchKernelGGL(kseg, dim3((uint32_t)ceil_div(nseg, SEG_WAVES)), dim3(64 * SEG_WAVES), 0, st, A,
                                q->d_segs.as<uint4>(), (uint32_t)nseg, q->d_segres.as<skm_kmer_call>(),
-                               q->d_scr.as<uint16_t>(), q->d_pool_ctr.as<unsigned long long>());
+                               q->d_scr.as<uint16_t>(), q->d_pool_ctr.as<unsigned long long>(), q->d_rcp.as<float>());
         }
         SKM_HIP(hipGetLastError());
         SKM_HIP(hipEventRecord(q->ev[3], st));
