@@ -93,7 +93,9 @@ def test_c3_slice_bit_exact_and_whole_build_properties(skm, gpu):
         return c, got, flags
 
     c, got, flags = build({})
+    print(f"\nC3 build: {c['passes']} passes, {c['kept']:,} kept", flush=True)
     c2, got2, _ = build({"lane_long": 1 << 18, "lane_tail": 1 << 14})  # the deepest chains on wave pairs
+    print("C3 build (wave-pair chains) done", flush=True)
     assert c["passes"] >= 8, c  # the headline's out-of-core path (16 passes at 288 GB)
     # pack the input for the oracle (16.5 GB of residues)
     lens = np.concatenate([p[2] for p in parts])
@@ -104,6 +106,7 @@ def test_c3_slice_bit_exact_and_whole_build_properties(skm, gpu):
     off = np.zeros(len(lens), np.uint64)
     off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
     ref = oracle_ref.build_slice_mt(res, off, lens, func, ids, nf, T, SLICE_BITS, SLICE, want_flags=True)
+    print(f"oracle slice {SLICE}: {len(ref['keys']):,} kept, deepest group {ref['max_group']:,}", flush=True)
     # ---- the slice, bit for bit ----
     assert ref["max_group"] >= 1 << 19, ref["max_group"]  # the heaviest k-mer's group is in the slice
     assert bool(np.isin(np.uint64(heavy), got.keys)), "the heaviest k-mer is kept, in the checked slice"

@@ -34,6 +34,38 @@ def _fidx(out):
     return t
 
 
+def _parse_final_kmers(buf: bytes):
+    """final.kmers (kmers-build-signatures.cc:212-216: KMER \t avg_from_end \t function_index \t \n,
+    the key as its 8 raw residue bytes) -> (u64 little-endian keys, avg, fi), in file order; every
+    line must have exactly that shape."""
+    b = np.frombuffer(buf, np.uint8)
+    if len(b) == 0:
+        return np.zeros(0, np.uint64), np.zeros(0, np.uint16), np.zeros(0, np.uint16)
+    assert b[-1] == 10
+    nl = np.flatnonzero(b == 10)
+    starts = np.concatenate([[0], nl[:-1] + 1])
+    keys = np.zeros(len(starts), np.uint64)
+    for j in range(8):
+        keys |= b[starts + j].astype(np.uint64) << np.uint64(8 * j)
+    tabs = np.flatnonzero(b == 9)
+    assert len(tabs) == 3 * len(starts)
+    tabs = tabs.reshape(-1, 3)
+    assert np.array_equal(tabs[:, 0], starts + 8) and np.array_equal(tabs[:, 2], nl - 1)
+
+    def field(lo, hi):  # decimal digits in (lo, hi)
+        w = hi - lo - 1
+        assert w.min() >= 1 and w.max() <= 5
+        v = np.zeros(len(lo), np.int64)
+        for d in range(5):
+            i = hi - 1 - d
+            ok = i > lo
+            dig = b[np.where(ok, i, lo)].astype(np.int64) - 48
+            assert np.all((dig[ok] >= 0) & (dig[ok] <= 9))
+            v += np.where(ok, dig * 10 ** d, 0)
+        return v.astype(np.uint16)
+    return keys, field(tabs[:, 0], tabs[:, 1]), field(tabs[:, 1], tabs[:, 2])
+
+
 def _check_build(out, stdout, ref, threads=0):
     """Every output of kmers-build-signatures vs the oracle; threads > 0: the oracle build on that
     many host threads (oracle_build_mt) and the recall reports' files in parallel."""
@@ -46,12 +78,11 @@ def _check_build(out, stdout, ref, threads=0):
     assert f"distinct_signatures={o['distinct_signatures']}\n" in stdout
     assert f"num_seqs_with_a_signature={o['n_seqs_with_signature']}\n" in stdout
     assert _lines(os.path.join(out, "function.index")) == ref["fm"].function_index_text()
-    exp = set()
-    for k, d in zip(o["keys"], o["data"]):
-        exp.add(b"%s\t%d\t%d\t" % (int(k).to_bytes(8, "little"), d["avg_from_end"], d["function_index"]))
-    got = _lines(os.path.join(out, "final.kmers")).split(b"\n")
-    assert got[-1] == b""
-    assert len(got) - 1 == len(exp) and set(got[:-1]) == exp
+    keys, avg, fi = _parse_final_kmers(_lines(os.path.join(out, "final.kmers")))
+    order = np.argsort(keys, kind="stable")
+    assert np.array_equal(keys[order], o["keys"])  # every kept k-mer once (the oracle's are sorted)
+    assert np.array_equal(avg[order], o["data"]["avg_from_end"])
+    assert np.array_equal(fi[order], o["data"]["function_index"])
     dfl = set()
     for f in range(nf):
         if o["distinct_functions"][f]:
@@ -72,6 +103,7 @@ def _check_build(out, stdout, ref, threads=0):
         return path, fr.recall_report(oracle_ref, ref["fm"], recs, fidx, o["keys"], o["data"])
     if threads:
         from concurrent.futures import ThreadPoolExecutor
+        print("outputs checked; recall reports", flush=True)
         with ThreadPoolExecutor(threads) as ex:
             reports = list(ex.map(one, ref["files"]))
     else:
@@ -144,8 +176,9 @@ def test_build_signatures_250k(tmp_path, gpu):
                            "--kmer-data-dir", out, "--final-kmers", "final.kmers", "--perfect-hash", "kmer_data.mph",
                            "--perfect-hash-data", "kmer_data.dat"])
     wall = time.time() - t
-    print(f"\nkmers-build-signatures 250K proteins: {wall:.1f} s wall\n{stderr[-600:]}")
+    print(f"\nkmers-build-signatures 250K proteins: {wall:.1f} s wall\n{stderr[-600:]}", flush=True)
     ref = fr.front([info["ann_dir"]], [info["seqs_dir"]])
+    print("reference front end done", flush=True)
     o = _check_build(out, stdout, ref, threads=_threads())
     assert len(o["keys"]) > 10_000_000 and len(ref["files"]) == 63
 
