@@ -1,6 +1,7 @@
 // skm_front.cpp -- host front end (see skm_front.h for the reference mapping).
 #include "skm_front.h"
 
+#include <cerrno>
 #include <dirent.h>
 #include <sys/stat.h>
 
@@ -193,7 +194,9 @@ bool ensure_directory(const std::string& dir) {
     if (dir.empty()) return true;
     struct stat sb;
     if (stat(dir.c_str(), &sb) == 0 && S_ISDIR(sb.st_mode)) return true;
-    return mkdir(dir.c_str(), 0777) == 0;
+    if (mkdir(dir.c_str(), 0777) == 0) return true;
+    // forked ranks create the output directory concurrently: losing the race is success
+    return errno == EEXIST && stat(dir.c_str(), &sb) == 0 && S_ISDIR(sb.st_mode);
 }
 
 bool list_regular_files(const std::string& dir, std::vector<std::string>& out, std::string& err) {

@@ -3,7 +3,8 @@
 set -u
 O=gpurun_out; mkdir -p $O
 start=$(date +%s)
-timeout -k 10 1050 python3 -u -m pytest tests -m gpu -x -v -s --durations=20 --timeout 420 --timeout-method thread \
+SEL=${SEL:-tests}
+timeout -k 10 1050 python3 -u -m pytest $SEL -m gpu -x -v -s --durations=20 --timeout 420 --timeout-method thread \
   > $O/r04_gputests.log 2>&1; rc=$?
 echo "suite $(( $(date +%s) - start )) s rc=$rc"; tail -28 $O/r04_gputests.log
 exit $rc
