@@ -423,13 +423,6 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
-// rcp[k] = RN(1 / (k + 1)) in float, by the same correctly rounded division the four-lane mean
-// used inline (-fhip-fp32-correctly-rounded-divide-sqrt): k_seg_process reads it as a table
-__global__ void k_rcp_init(float* __restrict__ rcp, uint32_t n) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) rcp[k] = 1.0f / (float)(k + 1);
-}
-
 // k-th smallest (0-based) of a wave's n items x[e] (item e * 64 + lane; values < 2^bits): MSD
 // radix select, one bit per step, counted on ballots (wave-uniform result)
 template <int E>
@@ -462,8 +455,7 @@ template <bool LEGACY_MAD>  // mad_mode 1 in its own instantiation: no register 
 __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, const uint4* __restrict__ segs,
                                                                 uint32_t nseg, skm_kmer_call* __restrict__ out,
                                                                 uint16_t* __restrict__ pool,
-                                                                unsigned long long* __restrict__ pool_ctr,
-                                                                const float* __restrict__ rcp) {
+                                                                unsigned long long* __restrict__ pool_ctr) {
     __shared__ uint32_t sv[SEG_WAVES][SEG_CAP];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t j = blockIdx.x * SEG_WAVES + wave;
@@ -475,9 +467,10 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
     const double seqlen = (double)m.len;
     uint32_t* buf = sv[wave];
     uint32_t n = 0, last_cur = first;
+    uint32_t hn = first + lane <= last ? hit[first + lane] : NO_HIT;  // the next 64 hits in flight
     for (uint32_t i0 = first; i0 <= last; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        const uint32_t h = i <= last ? hit[i] : NO_HIT;
+        const uint32_t h = hn, i1 = i0 + 64u + lane;
+        hn = i1 <= last ? hit[i1] : NO_HIT;
         const bool take = usable(h, A) && (h >> 16) == cur;
         const uint64_t bal = __ballot(take);
         const uint32_t pos = n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
@@ -508,22 +501,35 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
     } else {
         const uint32_t end = n - (n % 4);
         float mu = 0, fi = 1;
-        if (lane < 4) {
-            // inv = RN(1 / fi) from the table (k_rcp_init: the same correctly rounded division),
-            // a uniform load off the recurrence's chain
-            for (uint32_t q = lane; q < end; q += 4) {
-                const float inv = rcp[q >> 2];
-                float t = (float)buf[q] - mu;
-                t *= inv;
-                mu += t;
+        // step i of the four running means (items 4 i .. 4 i + 3, one per lane 0-3) multiplies by
+        // RN(1 / (i + 1)): the same correctly rounded division, done for 64 steps at once (one per
+        // lane) and broadcast by readlane; the items of 8 steps are read from LDS ahead of their
+        // chain (round 3's loop waited on one LDS read and one division per step, round 4's
+        // first version on a global table load per step)
+        const uint32_t nq = end >> 2;
+        for (uint32_t i0 = 0; i0 < nq; i0 += 64) {
+            const float r = 1.0f / (float)(i0 + lane + 1u);
+            const uint32_t cnt = min(64u, nq - i0);
+            for (uint32_t t0 = 0; t0 < cnt; t0 += 8) {
+                float xv[8];  // 4 (i0 + t0 + u) + 3 <= 4 * 255 + 3 < SEG_CAP: in the wave's buffer
+#pragma unroll
+                for (int u = 0; u < 8; ++u) xv[u] = (float)buf[4u * (i0 + t0 + (uint32_t)u) + (lane & 3u)];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (t0 + (uint32_t)u < cnt) {
+                        const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), (int)(t0 + (uint32_t)u)));
+                        float t = xv[u] - mu;
+                        t *= inv;
+                        mu += t;
+                    }
+            }
+        }
+        fi += (float)nq;  // the tail's running count (exact: nq <= 256)
+        if (lane == 3)
+            for (uint32_t q = end; q < n; ++q) {
+                mu += ((float)buf[q] - mu) / fi;
                 fi += 1;
             }
-            if (lane == 3)
-                for (uint32_t q = end; q < n; ++q) {
-                    mu += ((float)buf[q] - mu) / fi;
-                    fi += 1;
-                }
-        }
         const float m0 = __shfl(mu, 0), m1 = __shfl(mu, 1), m2 = __shfl(mu, 2), m3 = __shfl(mu, 3);
         const float num1 = float(n - (n % 4)) / float(4);
         const float num2 = num1 + float(n % 4);
@@ -738,7 +744,6 @@ struct skm_query {
     uint64_t rp = 0, n_windows = 0;
     DevBuf d_res, d_meta, d_hits, d_scr, d_scr_off, d_caps, d_cap_off, d_slots, d_counts, d_call_off, d_calls;
     DevBuf d_seg_off, d_segs, d_segres, d_pool_ctr;
-    DevBuf d_rcp;                   // RN(1/k), k = 1 .. SEG_CAP/4 + 1 (k_seg_process's mean)
     Scanner scan;
     uint64_t n_calls = 0;
     bool ran = false;
@@ -921,17 +926,11 @@ void query_run(skm_query* q, const skm_annot_opts* o) {
         SKM_HIP(hipMemsetAsync(q->d_pool_ctr.p, 0, 8, st));
         hipLaunchKernelGGL(k_gather_segs, dim3(ceil_div(ns, 256)), dim3(256), 0, st, q->d_slots.as<uint4>(),
                            q->d_cap_off.as<uint64_t>(), q->d_seg_off.as<uint64_t>(), ns, q->d_segs.as<uint4>());
-        if (nseg)
-        {
-            constexpr uint32_t NRCP = SEG_CAP / 4 + 1;
-            if (!q->d_rcp.p) {
-                q->d_rcp.ensure(4 * NRCP);
-                hipLaunchKernelGGL(k_rcp_init, dim3(ceil_div(NRCP, 256)), dim3(256), 0, st, q->d_rcp.as<float>(), NRCP);
-            }
+        if (nseg) {
             auto kseg = A.mad_mode == 1 ? k_seg_process<true> : k_seg_process<false>;
             hipLaunchKernelGGL(kseg, dim3((uint32_t)ceil_div(nseg, SEG_WAVES)), dim3(64 * SEG_WAVES), 0, st, A,
                                q->d_segs.as<uint4>(), (uint32_t)nseg, q->d_segres.as<skm_kmer_call>(),
-                               q->d_scr.as<uint16_t>(), q->d_pool_ctr.as<unsigned long long>(), q->d_rcp.as<float>());
+                               q->d_scr.as<uint16_t>(), q->d_pool_ctr.as<unsigned long long>());
         }
         SKM_HIP(hipGetLastError());
         SKM_HIP(hipEventRecord(q->ev[3], st));

@@ -54,6 +54,11 @@ constexpr int EX_MAX_WG = 512;         // rows of the histogram matrix
 constexpr int SCAN_ROWS = 32;          // rows per column-scan block
 constexpr int BP_THREADS = 512;        // bucket-process workgroup: two per CU (LDS ~72 KB each)
 constexpr int CAP = 2048;              // LDS sub-bucket capacity (records)
+#ifndef SKM_BPK_THREADS                // k_bucket_process workgroup (A/B builds: -DSKM_BPK_THREADS=256)
+#define SKM_BPK_THREADS 512
+#endif
+constexpr int BPK_THREADS = SKM_BPK_THREADS;
+constexpr int BPK_WAVES_EU = BPK_THREADS == 512 ? 4 : 2;  // two workgroups per CU (LDS ~78 KB each)
 constexpr int TAB_BITS = 12;
 constexpr int TAB = 1 << TAB_BITS;     // LDS hash slots per sub-bucket (load <= 0.5)
 constexpr int SUB_TARGET = 1024;       // target records per level-2 sub-bucket
@@ -2544,7 +2549,7 @@ __device__ __forceinline__ void seg_groups(const SubLds& L, uint32_t q0, uint32_
 // One sub-bucket of n <= CAP records: LDS hash grouping (ranks from the insert atomics give a
 // counting sort by group), singletons resolved immediately, multi-occurrence groups by threads
 // (small) or waves (large); no workgroup-wide sort.
-constexpr uint32_t LPER = CAP / BP_THREADS;  // elements per thread of one batch
+constexpr uint32_t LPER = CAP / BPK_THREADS;  // elements per thread of one batch
 
 // the batch's elements into registers, every load in flight at once (a rolled loop would wait for
 // each pair before its LDS store)
@@ -2552,7 +2557,7 @@ __device__ __forceinline__ void load_batch(const uint64_t* __restrict__ src_hi, 
                                            uint32_t n, uint64_t (&eh)[LPER], uint64_t (&el)[LPER]) {
 #pragma unroll
     for (uint32_t u = 0; u < LPER; ++u) {
-        const uint32_t j = threadIdx.x + u * BP_THREADS;
+        const uint32_t j = threadIdx.x + u * BPK_THREADS;
         if (j < n) {
             eh[u] = __builtin_nontemporal_load(src_hi + j);
             el[u] = __builtin_nontemporal_load(src_lo + j);
@@ -2573,7 +2578,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     for (uint32_t t = tid; t < (uint32_t)TAB; t += nt) L.tab[t] = EMPTY;
 #pragma unroll
     for (uint32_t u = 0; u < LPER; ++u) {
-        const uint32_t j = tid + u * BP_THREADS;
+        const uint32_t j = tid + u * BPK_THREADS;
         if (j < n) {
             L.hi[j] = eh[u];
             L.lo[j] = el[u];
@@ -2750,7 +2755,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     // 6. emit kept k-mers and chain jobs: one scan and one reservation per batch; the kept
     //    elements are first compacted in LDS (slot[] = kept list, order[] = job list, rank[] =
     //    a job's kept position) so consecutive lanes write consecutive records
-    constexpr uint32_t EMIT_PER = CAP / BP_THREADS;
+    constexpr uint32_t EMIT_PER = CAP / BPK_THREADS;
     unsigned long long* s_base = reinterpret_cast<unsigned long long*>(L.wave + 36);
     const uint32_t j0 = tid * EMIT_PER;
     uint32_t cnt = 0;
@@ -2814,8 +2819,8 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     SKM_STAMP(8);
 }
 
-__global__ __launch_bounds__(BP_THREADS, 4) void k_bucket_process(BucketArgs A) {
-    static_assert(CAP % BP_THREADS == 0, "emit assigns CAP / BP_THREADS elements per thread");
+__global__ __launch_bounds__(BPK_THREADS, BPK_WAVES_EU) void k_bucket_process(BucketArgs A) {
+    static_assert(CAP % BPK_THREADS == 0, "emit assigns CAP / BPK_THREADS elements per thread");
     __shared__ uint64_t s_hi[CAP];
     __shared__ uint64_t s_lo[CAP];
     __shared__ uint32_t s_tab[TAB];
@@ -6248,7 +6253,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     BA.flags = A.flags;
     BA.out = b->d_big_out.as<BigOut>();
     SKM_HIP(hipEventRecord(b->ev[11], st));
-    SKM_LAUNCH(b, k_bucket_process, dim3(NB1), dim3(BP_THREADS), 0, st, A);
+    SKM_LAUNCH(b, k_bucket_process, dim3(NB1), dim3(BPK_THREADS), 0, st, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[5], st));
     if (b->tune.serial_overflow) launch_overflow();
