@@ -446,6 +446,55 @@ __device__ __forceinline__ uint32_t wave_select(const uint32_t (&x)[E], uint32_t
 }
 constexpr uint32_t SEG_CAP = 1024;  // 16 KB of LDS per 4-wave block: 8 blocks per CU (2048: 5)
 
+// a wave's histogram h[0..R) of its n items x[e] (item e * 64 + lane, values < R) in its LDS
+template <int E>
+__device__ __forceinline__ void wave_hist(uint32_t* h, const uint32_t (&x)[E], uint32_t n, uint32_t R) {
+    const uint32_t lane = threadIdx.x & 63u;
+    wave_sync_lds();  // the previous reads of h are done
+    for (uint32_t t = lane; t < R; t += 64) h[t] = 0u;
+    wave_sync_lds();
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if ((uint32_t)e * 64u >= n) break;  // wave-uniform
+        if ((uint32_t)e * 64u + lane < n) atomicAdd(&h[x[e]], 1u);
+    }
+    wave_sync_lds();
+}
+
+// the k1-th and k2-th smallest (0-based) values of a wave histogram h[0..R), R <= SEG_CAP: lane l
+// owns bins [l B, l B + B), one wave scan of the lanes' counts, the owner of rank k walks its bins
+__device__ __forceinline__ void wave_hist_kth2(const uint32_t* h, uint32_t R, uint32_t k1, uint32_t k2,
+                                               uint32_t& v1, uint32_t& v2) {
+    constexpr uint32_t BMAX = SEG_CAP / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t B = (R + 63u) >> 6, b0 = lane * B;
+    uint32_t c[BMAX], sum = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < BMAX; ++b) {
+        if (b >= B) break;  // wave-uniform
+        c[b] = b0 + b < R ? h[b0 + b] : 0u;
+        sum += c[b];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+        if ((int)lane >= d) inc += t;
+    }
+    uint32_t acc = inc - sum, r1 = 0, r2 = 0;
+    const uint64_t o1 = __ballot(acc <= k1 && k1 < inc), o2 = __ballot(acc <= k2 && k2 < inc);
+#pragma unroll
+    for (uint32_t b = 0; b < BMAX; ++b) {
+        if (b >= B) break;
+        const uint32_t a2 = acc + c[b];
+        if (acc <= k1 && k1 < a2) r1 = b0 + b;
+        if (acc <= k2 && k2 < a2) r2 = b0 + b;
+        acc = a2;
+    }
+    v1 = (uint32_t)__builtin_amdgcn_readlane((int)r1, __ffsll((long long)o1) - 1);
+    v2 = (uint32_t)__builtin_amdgcn_readlane((int)r2, __ffsll((long long)o2) - 1);
+}
+
 // One wave per HitSet::process segment (call_functions.tcc:35-103): the hits of the current
 // function in window order (ballot compaction into LDS), Boost.Math mean (four-lane Welford on
 // lanes 0-3, or the single running mean), median by an LDS bitonic sort, MAD as the k-th
@@ -556,13 +605,13 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
         emit(median, mad);
         return;
     }
-    // median and MAD by wave radix selects over the run held in registers (E <= 16 items per lane,
-    // item e * 64 + lane): the (n-1)/2-th (odd n) or the n/2-1-th and n/2-th smallest (even) of the
-    // u16 lengths, then the k-th smallest |2 v - C2| (17 bits) -- the same order statistics the
-    // sorted run gives (call_functions.tcc:51-53), without an LDS sort (round 3: a 512-element
-    // bitonic network per segment, most of the kernel's time)
-    // the selects run over x - min (a segment's lengths span a few hundred, not 2^16: ~9 radix
-    // steps instead of 16 / 17)
+    // median and MAD from the run held in registers (E <= 16 items per lane, item e * 64 + lane):
+    // the (n-1)/2-th (odd n) or the n/2-1-th and n/2-th smallest (even) of the u16 lengths, then
+    // the same ranks of |2 v - C2| -- the order statistics the sorted run gives
+    // (call_functions.tcc:51-53), without an LDS sort (round 3: a 512-element bitonic network per
+    // segment).  A segment's lengths span a few hundred values, so both selects read a histogram of
+    // x - min in the wave's LDS buffer (two per segment); a wider span takes MSD radix selects on
+    // ballots.
     uint32_t x[SEG_CAP / 64];
     uint32_t vmin = 0xFFFFu, vmax = 0u;
 #pragma unroll
@@ -576,10 +625,32 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
     }
     vmin = wave_min_u32(vmin);
     vmax = wave_max_u32(vmax);
-    const int vbits = 32 - __clz(vmax - vmin);  // bits of the largest x - vmin (0: all equal)
 #pragma unroll
     for (int e = 0; e < (int)(SEG_CAP / 64); ++e) x[e] -= vmin;
-    float median;
+    const uint32_t R = vmax - vmin + 1u;  // n == 0: wraps above SEG_CAP (the radix path)
+    float median, mad;
+    if (R <= SEG_CAP) {
+        // the order statistics from histograms in the wave's (now free) LDS buffer: of x - min, then
+        // of the deviations |2 x - C2| = 2 i + (C2 & 1), all of one parity, binned by i < R
+        const uint32_t k1 = (n - 1) / 2, k2 = n / 2;  // odd n: the same rank twice
+        uint32_t a, b;
+        wave_hist(buf, x, n, R);
+        wave_hist_kth2(buf, R, k1, k2, a, b);
+        const uint32_t C2 = a + b;
+        median = (n & 1) ? (float)(a + vmin) : ((float)(a + vmin) + (float)(b + vmin)) / 2;
+#pragma unroll
+        for (int e = 0; e < (int)(SEG_CAP / 64); ++e) x[e] = (2u * x[e] > C2 ? 2u * x[e] - C2 : C2 - 2u * x[e]) >> 1;
+        wave_hist(buf, x, n, R);
+        wave_hist_kth2(buf, R, k1, k2, a, b);
+        const uint32_t p = C2 & 1u;
+        if (n & 1)
+            mad = (float)(2u * a + p) * 0.5f;
+        else
+            mad = ((float)(2u * a + p) * 0.5f + (float)(2u * b + p) * 0.5f) / 2.0f;
+        if (lane == 0) emit(median, mad);
+        return;
+    }
+    const int vbits = 32 - __clz(vmax - vmin);  // bits of the largest x - vmin
     uint32_t C2;  // 2 * (median - vmin): the deviations |2 v - C2| are shift-invariant
     if (n & 1) {
         const uint32_t md = wave_select(x, n, (n - 1) / 2, vbits);
@@ -593,7 +664,6 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
 #pragma unroll
     for (int e = 0; e < (int)(SEG_CAP / 64); ++e) x[e] = 2u * x[e] > C2 ? 2u * x[e] - C2 : C2 - 2u * x[e];
     const int dbits = vbits + 1;  // |2 v - C2| <= 2 (vmax - vmin)
-    float mad;
     if (n & 1) {
         mad = (float)wave_select(x, n, (n - 1) / 2, dbits) * 0.5f;
     } else {
