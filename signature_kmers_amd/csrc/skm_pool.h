@@ -5,6 +5,7 @@
 #pragma once
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <functional>
@@ -33,6 +34,7 @@ public:
         {
             std::lock_guard<std::mutex> g(m_);
             stop_ = true;
+            stop_flag_.store(true);
         }
         cv_.notify_all();
         for (auto& t : th_) t.join();
@@ -52,7 +54,7 @@ public:
             job_ = std::move(f);
             parts_ = n;
             next_.store(0);
-            ++gen_;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         work();
@@ -67,11 +69,17 @@ private:
     }
     void loop() {
         uint64_t seen = 0;
-        std::unique_lock<std::mutex> l(m_);
         for (;;) {
-            cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+            // a caller adding many small batches back to back (one per genome file) would pay a
+            // futex wake-up per batch: spin a little for the next run before sleeping
+            const auto t0 = std::chrono::steady_clock::now();
+            while (gen_.load(std::memory_order_acquire) == seen && !stop_flag_.load(std::memory_order_relaxed) &&
+                   std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(SPIN_US))
+                __builtin_ia32_pause();
+            std::unique_lock<std::mutex> l(m_);
+            cv_.wait(l, [&] { return stop_ || gen_.load() != seen; });
             if (stop_) return;
-            seen = gen_;
+            seen = gen_.load();
             ++active_;
             l.unlock();
             work();
@@ -79,14 +87,16 @@ private:
             if (--active_ == 0) done_.notify_all();
         }
     }
+    static constexpr int SPIN_US = 200;
     std::vector<std::thread> th_;
     std::mutex m_;
     std::condition_variable cv_, done_;
     std::function<void(int)> job_;
     std::atomic<int> next_{0};
     int parts_ = 0, active_ = 0;
-    uint64_t gen_ = 0;
+    std::atomic<uint64_t> gen_{0};
     bool stop_ = false;
+    std::atomic<bool> stop_flag_{false};  // stop_ for the spinning workers
 };
 
 }  // namespace skm
