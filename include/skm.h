@@ -151,7 +151,8 @@ int skm_build_kernel_timings(skm_build* b, char* names, size_t names_cap, float*
  * microseconds: [27] the residue / metadata upload, [28] the pass plan (device tallies of the pass
  * sizes, heavy-key routing sketch and filter), [29] allocations and the rest; [30] residue scans
  * per run that emit the key-range passes' window positions (k_pass_emit, one per group of up to
- * four passes; 0 without key-range passes);
+ * four passes; 0 without key-range passes); [31] of [26]: microseconds packing residues into the
+ * pinned staging buffers, [32] of [26]: microseconds waiting for a staging buffer's DMA to end;
  * totals over the passes of the run; returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Host transport: the rank collectives of a multi-process build run by the caller on host

@@ -4794,7 +4794,7 @@ struct skm_build {
     std::vector<uint64_t> h_cum;
     // host seconds in add_batch (all calls), and prepare's phases: the residue / metadata upload, the
     // pass plan (the pass tallies and the routing sketch: device work), the allocations and the rest
-    double add_s = 0, prep_upload_s = 0, prep_plan_s = 0, prep_rest_s = 0;
+    double add_s = 0, add_pack_s = 0, add_wait_s = 0, prep_upload_s = 0, prep_plan_s = 0, prep_rest_s = 0;
     uint64_t n_windows = 0;
     bool seqid_strict = true;
     bool prepared = false, ran = false;
@@ -5322,7 +5322,9 @@ void stage_flush(skm_build* b) {
     b->st_cur ^= 1;
     const int n = b->st_cur;
     if (b->st_busy[n]) {
+        const auto t0 = std::chrono::steady_clock::now();
         SKM_HIP(hipEventSynchronize(b->st_ev[n]));
+        b->add_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         b->st_busy[n] = false;
     }
     b->st_fill[n] = 0;
@@ -5339,10 +5341,9 @@ void prepare_local(skm_build* b) {
     res_reserve(b, rp + 64);
     SKM_HIP(hipMemsetAsync(b->d_res.as<uint8_t>() + rp, 0, 64, b->stream));  // window-load padding
     b->d_meta.ensure(sizeof(SeqMeta) * (b->nseq + 1));
-    SeqMeta sentinel{rp, 0, 0xFFFF, 0};
-    std::vector<SeqMeta> meta = b->h_meta;
-    meta.push_back(sentinel);
-    SKM_HIP(hipMemcpyAsync(b->d_meta.p, meta.data(), sizeof(SeqMeta) * meta.size(), hipMemcpyHostToDevice, b->stream));
+    const SeqMeta sentinel{rp, 0, 0xFFFF, 0};  // the table, then its sentinel (no host copy of the table)
+    if (b->nseq) SKM_HIP(hipMemcpy(b->d_meta.p, b->h_meta.data(), sizeof(SeqMeta) * b->nseq, hipMemcpyHostToDevice));
+    SKM_HIP(hipMemcpy(b->d_meta.as<SeqMeta>() + b->nseq, &sentinel, sizeof(SeqMeta), hipMemcpyHostToDevice));
     const uint64_t nblk = (rp >> 6) + 1;
     b->d_blk2seq.ensure(sizeof(uint32_t) * nblk);
     SKM_HIP(hipMemsetAsync(b->d_blk2seq.p, 0, sizeof(uint32_t) * nblk, b->stream));
@@ -6746,8 +6747,10 @@ int skm_build_add_batch(skm_build* b, const uint8_t* residues, const uint64_t* s
         SKM_CHECK(seq_len[s] < (1u << ELEM_I_BITS), SKM_E_ARG, "protein longer than 1,048,575 residues");
         ks.push_back((uint32_t)s);
     }
-    b->h_meta.reserve(b->h_meta.size() + ks.size());
-    b->h_seqid.reserve(b->h_seqid.size() + ks.size());
+    if (b->h_meta.capacity() < b->h_meta.size() + ks.size()) {  // geometric growth without skm_build_reserve
+        b->h_meta.reserve(std::max(b->h_meta.size() + ks.size(), 2 * b->h_meta.capacity()));
+        b->h_seqid.reserve(std::max(b->h_seqid.size() + ks.size(), 2 * b->h_seqid.capacity()));
+    }
     // Segments that fit the current pinned staging buffer: their metadata in order (one thread),
     // their residues copied by the host pool in byte-balanced parts (the packing used to be one
     // memcpy per sequence on one thread, ~2 GB/s: 8 s of a C3 one-shot build); the DMA of the
@@ -6786,6 +6789,7 @@ int skm_build_add_batch(skm_build* b, const uint8_t* residues, const uint64_t* s
         uint8_t* base = b->st_pin[b->st_cur] + b->st_fill[b->st_cur];
         const int parts = bytes >= (1u << 20) ? std::min<int>(4 * b->pool->threads(), (int)(bytes >> 18)) : 1;
         const size_t nseg = j - i;
+        const auto tp = std::chrono::steady_clock::now();
         b->pool->run(parts, [&](int p) {
             const uint64_t lo = bytes * (uint64_t)p / (uint64_t)parts, hi = bytes * (uint64_t)(p + 1) / (uint64_t)parts;
             const size_t a = (size_t)(std::lower_bound(cum.begin(), cum.begin() + nseg, lo) - cum.begin());
@@ -6797,6 +6801,7 @@ int skm_build_add_batch(skm_build* b, const uint8_t* residues, const uint64_t* s
                 dst[seq_len[s]] = 0;
             }
         });
+        b->add_pack_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp).count();
         b->st_fill[b->st_cur] += bytes;
         b->rp_total += bytes;
         i = j;
@@ -7211,13 +7216,14 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
     auto us = [](double sec) { return (uint64_t)(sec * 1e6); };
-    const uint64_t v[31] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+    const uint64_t v[33] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
                             b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total,
                             b->giant_jobs, b->giant_max, b->n_redo, b->tot_cap, b->split_cap, b->long_cap,
                             b->long_jobs_cap, b->demand[0], b->demand[1], b->demand[2], b->demand[3],
                             b->long_samples, b->routed, us(b->add_s), us(b->prep_upload_s), us(b->prep_plan_s),
-                            us(b->prep_rest_s), b->pass_bits ? (1ull << b->pass_bits) / b->emit_g : 0ull};
-    int n = std::min(cap, 31);
+                            us(b->prep_rest_s), b->pass_bits ? (1ull << b->pass_bits) / b->emit_g : 0ull, us(b->add_pack_s),
+                            us(b->add_wait_s)};
+    int n = std::min(cap, 33);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }
