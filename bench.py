@@ -484,11 +484,13 @@ def _pcie_inclusive(m, prep_s, create_s=None):
     """The rate from host arrays: add_batch (packing into the pinned double-buffered staging whose
     DMA to HBM overlaps the packing) + prepare + one build step.  Reported beside `value`, which
     starts with the inputs resident in HBM.  `phases` splits the host time: the handle's creation
-    (streams, pinned staging; the process's HIP runtime is initialised before), add_batch, and
+    (streams, pinned staging; the process's HIP runtime is initialised before), add_batch (of it:
+    packing on the host pool, waiting for a staging buffer's DMA), and
     prepare's residue / metadata upload, pass plan (device tallies + routing sketch) and the rest."""
     t = prep_s + m["ms_per_step"] / 1000.0
     c = m["counters"]
     phases = {"create_s": create_s, "add_batch_s": c.get("add_batch_us", 0) / 1e6,
+              "add_pack_s": c.get("add_pack_us", 0) / 1e6, "add_dma_wait_s": c.get("add_dma_wait_us", 0) / 1e6,
               "prepare_upload_s": c.get("prepare_upload_us", 0) / 1e6,
               "prepare_plan_device_s": c.get("prepare_plan_us", 0) / 1e6,
               "prepare_rest_s": c.get("prepare_rest_us", 0) / 1e6}

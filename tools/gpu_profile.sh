@@ -23,13 +23,14 @@ step() {  # name, limit, command...
 }
 cd "$R"
 python3 -c "import bench; print(bench.src_sha16())" > "$O/src_sha16.txt"
-step cache 300 python3 bench.py --cache-dir /tmp/c3 --cache-only
+P=${PHASE:-all}
+case "$P" in legs*) ;; *) step cache 300 python3 bench.py --cache-dir /tmp/c3 --cache-only ;; esac
 cd /tmp
 C3="python3 -u $R/bench.py --cache-dir /tmp/c3 --weak-seqs 0 --annot-queries 0 --matrix-seqs 0 --no-cpu-baseline"
 C2="python3 -u $R/tools/c3_diag.py --cache-dir /tmp/c3 --files 250"
 LEGS="python3 -u $R/bench.py --seqs-total 1000000 --cache-dir /tmp/legs --no-cpu-baseline"
 # PHASE: all | trace (stamps + C3/C2 traces) | pmc (C3/C2 counters) | legs (legs trace + counters)
-P=${PHASE:-all}
+#        | legs_trace (the legs' kernel trace only)
 if [ "$P" = all ] || [ "$P" = trace ]; then
   step c3_stamps 300 python3 -u $R/tools/c3_diag.py --cache-dir /tmp/c3 --runs 1 --stamps
   step prof_c3 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_c3" -o run -- $C3 --steps 2 --warmup 1 --json-out "$O/bench_c3_trace.json"
@@ -42,9 +43,12 @@ if [ "$P" = all ] || [ "$P" = pmc ]; then
     step pmc_c2_$lc 300 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_c2_$lc" -o run -- $C2 --runs 1
   done
 fi
-if [ "$P" = all ] || [ "$P" = legs ]; then
+if [ "$P" = all ] || [ "$P" = legs ] || [ "$P" = legs_trace ]; then
+  cd "$R"
   step legs_cache 400 python3 -u $R/bench.py --seqs-total 1000000 --cache-dir /tmp/legs --cache-only
+  cd /tmp
   step prof_legs 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_legs" -o run -- $LEGS --steps 3 --warmup 1 --json-out "$O/bench_legs_trace.json"
+  [ "$P" = legs_trace ] && { echo done; exit 0; }
   for c in FETCH_SIZE WRITE_SIZE; do
     lc=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
     step pmc_legs_$lc 500 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_legs_$lc" -o run -- $LEGS --steps 1 --warmup 1
