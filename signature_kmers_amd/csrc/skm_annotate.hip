@@ -415,15 +415,28 @@ __device__ uint32_t kth_dev_sorted(const uint32_t* v, uint32_t n, uint32_t C2, u
 #endif
 constexpr int SEG_WAVES = 4;
 
+// wave-wide min / max / inclusive sum on DPP (row_shr 1/2/4/8 within rows of 16, then row_bcast
+// 15 / 31; lanes without a source keep the identity): no LDS round trips, unlike __shfl
+template <int OP>  // 0: min, 1: max, 2: inclusive prefix sum
+__device__ __forceinline__ uint32_t dpp_step(uint32_t x, uint32_t y) {
+    return OP == 0 ? min(x, y) : OP == 1 ? max(x, y) : x + y;
+}
+template <int OP>
+__device__ __forceinline__ uint32_t wave_dpp_scan(uint32_t x) {
+    constexpr int id = OP == 0 ? -1 : 0;
+    x = dpp_step<OP>(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x111, 0xF, 0xF, false));
+    x = dpp_step<OP>(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x112, 0xF, 0xF, false));
+    x = dpp_step<OP>(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x114, 0xF, 0xF, false));
+    x = dpp_step<OP>(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x118, 0xF, 0xF, false));
+    x = dpp_step<OP>(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x142, 0xA, 0xF, false));
+    x = dpp_step<OP>(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x143, 0xC, 0xF, false));
+    return x;
+}
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d, 64));
-    return v;
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_dpp_scan<0>(v), 63);
 }
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d, 64));
-    return v;
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_dpp_scan<1>(v), 63);
 }
 
 // k-th smallest (0-based) of a wave's n items x[e] (item e * 64 + lane; values < 2^bits): MSD
@@ -464,30 +477,24 @@ __device__ __forceinline__ void wave_hist(uint32_t* h, const uint32_t (&x)[E], u
     wave_sync_lds();
 }
 
-// the k1-th and k2-th smallest (0-based) values of a wave histogram h[0..R), R <= SEG_CAP: lane l
-// owns bins [l B, l B + B), one wave scan of the lanes' counts, the owner of rank k walks its bins
-__device__ __forceinline__ void wave_hist_kth2(const uint32_t* h, uint32_t R, uint32_t k1, uint32_t k2,
-                                               uint32_t& v1, uint32_t& v2) {
-    constexpr uint32_t BMAX = SEG_CAP / 64;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t B = (R + 63u) >> 6, b0 = lane * B;
-    uint32_t c[BMAX], sum = 0;
+// the k1-th and k2-th smallest (0-based) values of a wave histogram over [0, R), R <= SEG_CAP,
+// whose bins [b0, b0 + B) lane l holds in c[] (b0 = l B): one DPP scan of the lanes' counts, the
+// owner of rank k walks its bins
+constexpr uint32_t HBMAX = SEG_CAP / 64;
+__device__ __forceinline__ void hist_kth2(const uint32_t (&c)[HBMAX], uint32_t B, uint32_t k1, uint32_t k2,
+                                          uint32_t& v1, uint32_t& v2) {
+    const uint32_t b0 = (threadIdx.x & 63u) * B;
+    uint32_t sum = 0;
 #pragma unroll
-    for (uint32_t b = 0; b < BMAX; ++b) {
+    for (uint32_t b = 0; b < HBMAX; ++b) {
         if (b >= B) break;  // wave-uniform
-        c[b] = b0 + b < R ? h[b0 + b] : 0u;
         sum += c[b];
     }
-    uint32_t inc = sum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
-        if ((int)lane >= d) inc += t;
-    }
+    const uint32_t inc = wave_dpp_scan<2>(sum);
     uint32_t acc = inc - sum, r1 = 0, r2 = 0;
     const uint64_t o1 = __ballot(acc <= k1 && k1 < inc), o2 = __ballot(acc <= k2 && k2 < inc);
 #pragma unroll
-    for (uint32_t b = 0; b < BMAX; ++b) {
+    for (uint32_t b = 0; b < HBMAX; ++b) {
         if (b >= B) break;
         const uint32_t a2 = acc + c[b];
         if (acc <= k1 && k1 < a2) r1 = b0 + b;
@@ -645,16 +652,29 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
         // the order statistics from histograms in the wave's (now free) LDS buffer: of x - min, then
         // of the deviations |2 x - C2| = 2 i + (C2 & 1), all of one parity, binned by i < R
         const uint32_t k1 = (n - 1) / 2, k2 = n / 2;  // odd n: the same rank twice
-        uint32_t a, b;
+        const uint32_t B = (R + 63u) >> 6, b0 = lane * B;
+        uint32_t a, b, c[HBMAX];
         wave_hist(buf, x, n, R);
-        wave_hist_kth2(buf, R, k1, k2, a, b);
+#pragma unroll
+        for (uint32_t t = 0; t < HBMAX; ++t) {
+            if (t >= B) break;  // wave-uniform
+            c[t] = b0 + t < R ? buf[b0 + t] : 0u;
+        }
+        hist_kth2(c, B, k1, k2, a, b);
         const uint32_t C2 = a + b;
         median = (n & 1) ? (float)(a + vmin) : ((float)(a + vmin) + (float)(b + vmin)) / 2;
+        // the deviation histogram folded from the same one: bin i counts the values at
+        // |2 v - C2| = 2 i + p, i.e. v = up + i and v = lo - i (lo = up once when p = 0)
+        const uint32_t p = C2 & 1u, up = (C2 + p) >> 1, lo = (C2 - p) >> 1;
 #pragma unroll
-        for (int e = 0; e < (int)(SEG_CAP / 64); ++e) x[e] = (2u * x[e] > C2 ? 2u * x[e] - C2 : C2 - 2u * x[e]) >> 1;
-        wave_hist(buf, x, n, R);
-        wave_hist_kth2(buf, R, k1, k2, a, b);
-        const uint32_t p = C2 & 1u;
+        for (uint32_t t = 0; t < HBMAX; ++t) {
+            if (t >= B) break;
+            const uint32_t i = b0 + t;
+            uint32_t d = up + i < R ? buf[up + i] : 0u;
+            if ((i > 0 || p) && i <= lo) d += buf[lo - i];
+            c[t] = i < R ? d : 0u;
+        }
+        hist_kth2(c, B, k1, k2, a, b);
         if (n & 1)
             mad = (float)(2u * a + p) * 0.5f;
         else
