@@ -154,7 +154,6 @@ struct CallArgs {
     const uint64_t* cap_off;    // [nseq+1] call slot offsets
     skm_kmer_call* slots;
     uint32_t* counts;           // [nseq]
-    const uint32_t* order;      // [nseq] k_calls_scan's sequence per thread (longest first)
     uint32_t nseq;
     int min_hits, max_gap, ignore_hypo, mean_mode, mad_mode;
     uint32_t hypo;
@@ -309,9 +308,8 @@ __device__ void hitset_process(const CallArgs& A, const uint32_t* hit, uint16_t*
 // statistics of a segment never feed back into the state machine, so they run afterwards one
 // wave per segment (k_seg_process) instead of divergently inside this loop.
 __global__ void k_calls_scan(CallArgs A, uint4* __restrict__ segs) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= A.nseq) return;
-    const uint32_t s = A.order[t];  // the wave's sequences have similar lengths (k_len_order)
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= A.nseq) return;
     const QMeta m = A.meta[s];
     const uint32_t nwin = m.len >= 8 ? m.len - 7 : 0;
     const uint32_t* hit = A.hits + m.pstart;
@@ -736,59 +734,6 @@ __global__ void k_caps(const QMeta* __restrict__ meta, uint32_t nseq, int min_hi
     cap[s] = min_hits > 2 ? nwin / (uint32_t)(min_hits - 2) + 2u : 2u * nwin + 2u;
 }
 
-// k_calls_scan's thread order: the sequences by window count, longest first, binned by 32
-// windows (LB_BINS bins), so a wave's 64 state machines end together instead of waiting for the
-// longest of 64 random lengths.  Histogram (LDS, one global add per bin and workgroup), exclusive
-// scan, scatter (a workgroup's ranks from LDS atomics, one global reservation per bin).
-constexpr uint32_t LB_BINS = 1024, LB_THREADS = 1024, LB_PER = 4;
-__device__ __forceinline__ uint32_t len_bin(const QMeta& m) {
-    const uint32_t w = m.len >= 8 ? m.len - 7 : 0u;
-    return LB_BINS - 1u - min(w >> 5, LB_BINS - 1u);  // descending length
-}
-__global__ __launch_bounds__(LB_THREADS) void k_len_hist(const QMeta* __restrict__ meta, uint32_t nseq,
-                                                         uint32_t* __restrict__ hist) {
-    __shared__ uint32_t h[LB_BINS];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t s0 = blockIdx.x * (LB_THREADS * LB_PER);
-    for (uint32_t u = 0; u < LB_PER; ++u) {
-        const uint32_t s = s0 + u * LB_THREADS + threadIdx.x;
-        if (s < nseq) atomicAdd(&h[len_bin(meta[s])], 1u);
-    }
-    __syncthreads();
-    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
-}
-__global__ __launch_bounds__(LB_BINS) void k_len_scan(uint32_t* __restrict__ hist) {  // in place, exclusive
-    __shared__ uint32_t w[LB_BINS / 64];
-    const uint32_t t = threadIdx.x, v = hist[t];
-    const uint32_t inc = wave_dpp_scan<2>(v);
-    if ((t & 63u) == 63u) w[t >> 6] = inc;
-    __syncthreads();
-    uint32_t base = 0;
-    for (uint32_t k = 0; k < (t >> 6); ++k) base += w[k];
-    hist[t] = base + inc - v;
-}
-__global__ __launch_bounds__(LB_THREADS) void k_len_scatter(const QMeta* __restrict__ meta, uint32_t nseq,
-                                                            uint32_t* __restrict__ cursor, uint32_t* __restrict__ order) {
-    __shared__ uint32_t h[LB_BINS];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t s0 = blockIdx.x * (LB_THREADS * LB_PER);
-    uint32_t bin[LB_PER], rk[LB_PER];
-    for (uint32_t u = 0; u < LB_PER; ++u) {
-        const uint32_t s = s0 + u * LB_THREADS + threadIdx.x;
-        bin[u] = s < nseq ? len_bin(meta[s]) : LB_BINS;
-        rk[u] = bin[u] < LB_BINS ? atomicAdd(&h[bin[u]], 1u) : 0u;
-    }
-    __syncthreads();
-    const uint32_t c = h[threadIdx.x];
-    __syncthreads();
-    if (c) h[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], c);
-    __syncthreads();
-    for (uint32_t u = 0; u < LB_PER; ++u)
-        if (bin[u] < LB_BINS) order[h[bin[u]] + rk[u]] = s0 + u * LB_THREADS + threadIdx.x;
-}
-
 // ---- exclusive scan u32 -> u64 (out has n+1 entries) ----
 constexpr int SC_THREADS = 256, SC_ITEMS = 8, SC_TILE = SC_THREADS * SC_ITEMS;
 
@@ -900,7 +845,7 @@ struct skm_query {
     uint32_t nseq = 0;
     uint64_t rp = 0, n_windows = 0;
     DevBuf d_res, d_meta, d_hits, d_scr, d_scr_off, d_caps, d_cap_off, d_slots, d_counts, d_call_off, d_calls;
-    DevBuf d_seg_off, d_segs, d_segres, d_pool_ctr, d_order, d_lbins;
+    DevBuf d_seg_off, d_segs, d_segres, d_pool_ctr;
     Scanner scan;
     uint64_t n_calls = 0;
     bool ran = false;
@@ -1062,18 +1007,6 @@ void query_run(skm_query* q, const skm_annot_opts* o) {
         A.cap_off = q->d_cap_off.as<uint64_t>();
         A.slots = q->d_slots.as<skm_kmer_call>();
         A.counts = q->d_counts.as<uint32_t>();
-        {   // the state machines' thread order, longest sequences first
-            q->d_order.ensure(4ull * ns);
-            q->d_lbins.ensure(4ull * LB_BINS);
-            SKM_HIP(hipMemsetAsync(q->d_lbins.p, 0, 4ull * LB_BINS, st));
-            const uint32_t g = (uint32_t)ceil_div(ns, LB_THREADS * LB_PER);
-            hipLaunchKernelGGL(k_len_hist, dim3(g), dim3(LB_THREADS), 0, st, q->d_meta.as<QMeta>(), ns,
-                               q->d_lbins.as<uint32_t>());
-            hipLaunchKernelGGL(k_len_scan, dim3(1), dim3(LB_BINS), 0, st, q->d_lbins.as<uint32_t>());
-            hipLaunchKernelGGL(k_len_scatter, dim3(g), dim3(LB_THREADS), 0, st, q->d_meta.as<QMeta>(), ns,
-                               q->d_lbins.as<uint32_t>(), q->d_order.as<uint32_t>());
-        }
-        A.order = q->d_order.as<uint32_t>();
         A.nseq = ns;
         A.min_hits = o->min_hits;
         A.max_gap = o->max_gap;
