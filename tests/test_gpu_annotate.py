@@ -210,3 +210,28 @@ def test_boost_math_modes_match_oracle(skm, gpu, tmp_path, mean_mode, mad_mode):
     if mad_mode:  # the switch changes results on this data (ties in |x - median| are common)
         _, base_calls = oracle_ref.annotate(ob, dat, res, off, lens, hypo_index=hypo, mean_mode=mean_mode, mad_mode=0)
         assert len(base_calls) != len(ocalls) or not np.array_equal(base_calls.view(np.uint8), ocalls.view(np.uint8))
+
+
+@pytest.mark.parametrize("span", [1024, 1025, 65536])
+def test_calls_wide_length_spans(skm, gpu, tmp_path, span):
+    """The HitSet median / MAD over segments whose k-mer mean lengths span up to `span` values
+    (call_functions.tcc:35-103): k_seg_process takes its LDS histograms when a segment's values
+    span <= 1024 and the wave radix selects above; the .dat means are rewritten with random values
+    in [300, 300 + span) so both paths and the boundary between them run, compared with the
+    oracle bit for bit."""
+    ref, funcs, mph, dat, _ = make_db(skm, tmp_path, n_seqs=2000, fam=40, seed=9)
+    d = np.frombuffer(open(dat, "rb").read(), dtype=skm.STORED_DTYPE).copy()
+    rng = np.random.default_rng(span)
+    d["mean"] = (300 + rng.integers(0, span, size=len(d))).clip(0, 65535).astype(np.uint16)
+    open(dat, "wb").write(d.tobytes())
+    db = skm.CmphKmerDb(str(tmp_path / "kmer_data"))
+    caller = skm.FunctionCaller(db, funcs)
+    q = synth.generate_arrays(20000, 40, per_file=500, first_file=40, n_files=4, seed=23, extras=True)
+    goff, gcalls = caller.process_seqs(q.residues, q.seq_off, q.seq_len)
+    ob = oracle_ref.Bdz(open(mph, "rb").read())
+    ooff, ocalls = oracle_ref.annotate(ob, open(dat, "rb").read(), q.residues, q.seq_off, q.seq_len,
+                                       hypo_index=funcs.index("hypothetical protein"))
+    np.testing.assert_array_equal(goff, ooff)
+    assert len(gcalls) == len(ocalls)
+    np.testing.assert_array_equal(gcalls.view(np.uint8), ocalls.view(np.uint8))
+    db.close()
