@@ -490,6 +490,32 @@ __device__ __forceinline__ void mark_seq(uint8_t* f, uint32_t s) {
     }
 }
 
+// mark_seq for up to N sequences of one thread (0xFFFFFFFF: none): every flag read issued before
+// the first atomic, so the reads overlap instead of waiting one after another behind the
+// previous mark's atomic (a stale read costs one redundant atomic, never a lost flag)
+template <int N>
+__device__ __forceinline__ void mark_seqs(uint8_t* f, int flag_check, const uint32_t (&s)[N]) {
+    const uintptr_t p = reinterpret_cast<uintptr_t>(f);
+    if (p & 1u) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(p & ~(uintptr_t)1);
+        uint32_t cur[N];
+#pragma unroll
+        for (int u = 0; u < N; ++u) cur[u] = s[u] != 0xFFFFFFFFu ? w[s[u] >> 5] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int u = 0; u < N; ++u) {
+            const uint32_t m = 1u << (s[u] & 31u);
+            if (!(cur[u] & m)) atomicOr(w + (s[u] >> 5), m);
+        }
+    } else {
+        uint8_t cur[N];
+#pragma unroll
+        for (int u = 0; u < N; ++u) cur[u] = s[u] != 0xFFFFFFFFu && flag_check ? f[s[u]] : (uint8_t)(s[u] == 0xFFFFFFFFu);
+#pragma unroll
+        for (int u = 0; u < N; ++u)
+            if (cur[u] == 0) f[s[u]] = 1;
+    }
+}
+
 template <int N, class V>
 __device__ GRes group_thread(const V& v, uint64_t a, uint32_t c, const uint32_t* __restrict__ glen,
                              uint8_t* __restrict__ flags) {
@@ -2622,22 +2648,25 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         }
         uint32_t tot;
         uint32_t v = wg_exclusive_scan1(loc, L.wave, tot);  // L.wave next written by the emit scan
+        uint32_t ms[LPER];  // the singletons' sequences, flagged after the loop
 #pragma unroll
         for (uint32_t u = 0; u < LPER; ++u) {
             const uint32_t j = j0 + u;
             const uint32_t cnt = ev[u] & 0xFFFFu;
+            ms[u] = 0xFFFFFFFFu;
             if (j < n && cnt > 1 && (ev[u] >> 16) == j) {
                 L.goff[j] = (uint16_t)(v >> 13);
                 L.glist[v & 0x1FFFu] = (uint16_t)j;
                 v += (cnt << 13) | 1u;
             } else if (j < n && cnt == 1) {  // group of one: always kept (1 >= 0.8), median 0, var 0
                 const uint64_t H = L.hi[j], Lo = L.lo[j];
-                if (A.flags && (!A.flag_check || A.flags[Lo >> 36] == 0)) mark_seq(A.flags, (uint32_t)(Lo >> 36));
+                ms[u] = (uint32_t)(Lo >> 36);
                 L.hi[j] = kept_hi(key_h43(hprefix, (H >> 16) & REM_MASK, A.rem_bits, A.pshift), (uint32_t)(Lo & 0xFFFFu));
                 L.lo[j] = kept_lo((uint32_t)(H & 0xFFFFu), d2u16((double)(uint16_t)(H >> 48) / 1.0), 0, 0);
                 L.rank[j] = 0xFFFFu;  // singleton marker
             }
         }
+        if (A.flags) mark_seqs<LPER>(A.flags, A.flag_check, ms);
         M = tot >> 13;
         G = tot & 0x1FFFu;
     }
