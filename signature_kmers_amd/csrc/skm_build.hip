@@ -490,23 +490,6 @@ __device__ __forceinline__ void mark_seq(uint8_t* f, uint32_t s) {
     }
 }
 
-// a sequence's flag read ahead of its mark (bits: the word; bytes: the byte when flag_check, else
-// 0 = "not yet set"), and the mark given that read (a stale read costs one redundant atomic)
-__device__ __forceinline__ uint32_t flag_peek(const uint8_t* f, int flag_check, uint32_t s) {
-    const uintptr_t p = reinterpret_cast<uintptr_t>(f);
-    if (p & 1u) return reinterpret_cast<const uint32_t*>(p & ~(uintptr_t)1)[s >> 5];
-    return flag_check ? f[s] : 0u;
-}
-__device__ __forceinline__ void flag_mark(uint8_t* f, uint32_t s, uint32_t cur) {
-    const uintptr_t p = reinterpret_cast<uintptr_t>(f);
-    if (p & 1u) {
-        const uint32_t m = 1u << (s & 31u);
-        if (!(cur & m)) atomicOr(reinterpret_cast<uint32_t*>(p & ~(uintptr_t)1) + (s >> 5), m);
-    } else if (cur == 0) {
-        f[s] = 1;
-    }
-}
-
 // mark_seq for up to N sequences of one thread (0xFFFFFFFF: none): every flag read issued before
 // the first atomic, so the reads overlap instead of waiting one after another behind the
 // previous mark's atomic (a stale read costs one redundant atomic, never a lost flag)
@@ -2529,16 +2512,12 @@ __device__ __forceinline__ void seg_groups(const SubLds& L, uint32_t q0, uint32_
     }
     const bool real = gv && m < c;
     uint64_t key = ~0ull;
-    uint32_t pay = 0, s_in = 0, fw = 0;
+    uint32_t pay = 0;
     if (real) {
         const uint32_t j = L.order[a + m];
         const uint64_t hj = L.hi[j], lj = L.lo[j];
         key = ((hj & 0xFFFFull) << 48) | (lj >> 16);  // function, then ordinal (s << 20 | i)
         pay = (uint32_t)(hj >> 47);                    // len mod 2^16 << 1 | big-length flag
-        s_in = (uint32_t)(lj >> 36);
-        // the member's flag, read now and marked at the end by this lane (keeping is a property
-        // of the group): the read's latency hides behind the sorts and reductions
-        if (A.flags) fw = flag_peek(A.flags, A.flag_check, s_in);
     }
     key = seg_bitonic64<S>(key, pay, m);
     // function runs (padding lanes are heads of empty runs)
@@ -2567,8 +2546,9 @@ __device__ __forceinline__ void seg_groups(const SubLds& L, uint32_t q0, uint32_
     const uint64_t Rs = R & segmask;
     const uint32_t rs = Rs ? (uint32_t)__ffsll((long long)Rs) - 1u : sbase;
     const uint32_t s = (uint32_t)(key >> ELEM_I_BITS) & ((1u << ELEM_S_BITS) - 1u);
+    const uint32_t fl = (A.flag_check && real && A.flags) ? A.flags[s] : 0u;  // diag 1: no flags
     const uint32_t len = (pay & 1u) ? A.glen[s] : len16;
-    if (kept && real && A.flags) flag_mark(A.flags, s_in, fw);  // diag 1: no flags
+    if (kept && real && fl == 0 && A.flags) mark_seq(A.flags, s);
     const uint32_t x0 = (uint32_t)__shfl((int)len, (int)(rs + cbest - 1), 64);  // first visited
     const uint32_t x1 = (uint32_t)__shfl((int)len, (int)rs, 64);                // second when cbest == 2
     if (kept && inrun && cbest >= 3) L.lens32[2 * a + (rs + cbest - 1 - lane)] = len;  // visit order
