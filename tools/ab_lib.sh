@@ -1,3 +1,6 @@
+#!/bin/bash
+# C3 A/B of two libraries on one box: signature_kmers_amd/libskm_base.so (a saved build of the
+# previous sources) against the current libskm.so, three alternating pairs, C3 cached under /tmp/c3.
 set -u
 O=gpurun_out; mkdir -p $O
 timeout -k 10 300 python3 bench.py --cache-dir /tmp/c3 --cache-only > $O/ab_cache.log 2>&1 || exit 1
