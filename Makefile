@@ -8,7 +8,7 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -DSKM_W
            -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -Wall -Wno-unused-function
 OBJDIR   = build/obj
 SRC      = signature_kmers_amd/csrc
-HIP_SRCS = $(SRC)/skm_build.hip $(SRC)/skm_annotate.hip $(SRC)/skm_matrix.hip
+HIP_SRCS = $(SRC)/skm_build.hip $(SRC)/skm_annotate.hip $(SRC)/skm_matrix.hip $(SRC)/skm_output.hip
 CPP_SRCS = $(SRC)/skm_host.cpp $(SRC)/skm_bdz.cpp
 OBJS     = $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(CPP_SRCS))
 LIB      = signature_kmers_amd/libskm.so

@@ -153,7 +153,10 @@ int skm_build_kernel_timings(skm_build* b, char* names, size_t names_cap, float*
  * per run that emit the key-range passes' window positions (k_pass_emit, one per group of up to
  * four passes; 0 without key-range passes); [31] of [26]: microseconds packing residues into the
  * pinned staging buffers, [32] of [26]: microseconds waiting for a staging buffer's DMA to end;
- * totals over the passes of the run; returns entries written. */
+ * totals over the passes of the run; the last skm_build_finish / _finish_slice's kept-set
+ * hand-off (device radix sort in key-range chunks, streamed through pinned staging): [33] its
+ * host microseconds, [34] of them waiting for the device / PCIe, [35] copying pieces out on the
+ * host pool, [36] chunks; returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Host transport: the rank collectives of a multi-process build run by the caller on host
  * buffers, for ranks joined by a channel other than RCCL (the tests drive it with
@@ -251,9 +254,12 @@ int skm_debug_chain_eval(const uint32_t* samples, uint32_t n, int mode, double* 
 /* Diagnostics: device exact-division helpers (reciprocal + corrected quotient used by the
  * statistics recurrences) against IEEE division: m = 1..nm, then nm*per random pairs. */
 int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches);
-/* Run (if not yet run since the last prepare) and download the result.  With world_size > 1
- * this is collective: rank 0 receives every rank's kept k-mers (keys sorted), the other ranks
- * the k-mers they own; the statistics are global on every rank. */
+/* Run (if not yet run since the last prepare) and download the result, keys ascending (sorted
+ * on the device in key-range chunks and streamed to the host arrays; the reference's KeptKmers is
+ * a hash map, kmers-build-signatures.cc:206-221, so any order is valid).  At most 2^32 - 1 kept
+ * k-mers per call (use skm_build_finish_slice beyond).  With world_size > 1 this is collective:
+ * rank 0 receives every rank's kept k-mers, the other ranks the k-mers they own; the statistics
+ * are global on every rank. */
 int skm_build_finish(skm_build* b, skm_kept* out);
 /* The kept k-mers of one output slice: those whose slice hash -- MurmurHash3's fmix64 of the
  * little-endian key, top slice_bits bits -- equals `slice` (0 <= slice < 2^slice_bits, slice_bits
@@ -357,6 +363,13 @@ int skm_query_run(skm_query* q, const skm_annot_opts* opts);
 int skm_query_last_timings(skm_query* q, float* ms, int cap);
 /* Download the calls of the last run. */
 int skm_query_calls(skm_query* q, skm_calls* out);
+/* The last run's per-window hits as the device lookup produced them (diagnostics and parity tests
+ * of the device window iterator, kmer_data.h:76-102, and fetch, cmph_kmer.h:139-147; the CLI's
+ * --debug-hits prints them as the reference's hit_cb does, kmers-call-functions.cc:109-118):
+ * hit_off [n_seqs+1] CSR offsets; for the first `cap` hits pos = the window's offset in its
+ * sequence and fm = function_index << 16 | mean of its record (either array may be NULL).
+ * *n_out = the total number of hits. */
+int skm_query_window_hits(skm_query* q, uint64_t* hit_off, uint32_t* pos, uint32_t* fm, uint64_t cap, uint64_t* n_out);
 void skm_query_destroy(skm_query* q);
 /* Convenience: create + run + calls + destroy. */
 int skm_annotate(skm_db* db, const uint8_t* residues, const uint64_t* seq_off, const uint32_t* seq_len,

@@ -818,6 +818,14 @@ static int64_t process_aa_seq_impl(Fetch fetch, const uint8_t* seq, uint32_t len
 
 extern "C" {
 
+// The offsets for_each_kmer8 yields over one sequence (out: room for len entries); returns the
+// count.  Pinned against the reference's own for_each_kmer<8> (tests/golden/ref_windows.npz).
+uint32_t oracle_kmer_windows(const uint8_t* seq, uint32_t len, uint32_t* out) {
+    uint32_t n = 0;
+    for_each_kmer8(seq, len, [&](const uint8_t*, size_t off) { out[n++] = (uint32_t)off; });
+    return n;
+}
+
 int64_t oracle_process_aa_seq(const oracle_bdz* db, const oracle_stored* dat, const uint8_t* seq,
                               uint32_t len, const oracle_annot_opts* opts, oracle_call* out, uint64_t cap) {
     auto fetch = [&](const uint8_t* k) -> const oracle_stored* {

@@ -124,6 +124,7 @@ _SIGS = {
     "skm_query_run": (C.c_int, [_P, C.POINTER(_AnnotOpts)]),
     "skm_query_last_timings": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int]),
     "skm_query_calls": (C.c_int, [_P, C.POINTER(_Calls)]),
+    "skm_query_window_hits": (C.c_int, [_P, _P, _P, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "skm_query_destroy": (None, [_P]),
     "skm_annotate": (C.c_int, [_P, _P, _P, _P, C.c_size_t, C.POINTER(_AnnotOpts), C.POINTER(_Calls)]),
     "skm_calls_free": (None, [C.POINTER(_Calls)]),
@@ -237,6 +238,19 @@ class KeptKmers:
             yield f"{kmer_to_str(k)}\t{int(d['avg_from_end'])}\t{int(d['function_index'])}\t\n"
 
 
+class _KeptOwner:
+    """Owns one skm_kept's library arrays; frees them when the last numpy view is gone."""
+
+    def __init__(self, k):
+        self.k = k
+
+    def __del__(self):
+        try:
+            lib().skm_kept_free(C.byref(self.k))
+        except Exception:
+            pass
+
+
 class SignatureBuilder:
     """Device signature build (SignatureBuilder<8>::extract_kmers + process_kmers).
 
@@ -321,14 +335,15 @@ class SignatureBuilder:
         return self.counters()["passes"]
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 33)()
-        n = lib().skm_build_counters(self._h, v, 33)
+        v = (C.c_uint64 * 37)()
+        n = lib().skm_build_counters(self._h, v, 37)
         names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped",
                  "overflow_elements", "overflow_kept", "big_groups", "big_kept", "passes", "valid", "giant_chains",
                  "giant_max", "redone", "cap_overflow_scratch", "cap_split", "cap_long_samples", "cap_long_jobs",
                  "demand_overflow_scratch", "demand_split", "demand_long_samples", "demand_long_jobs",
                  "long_samples", "routed", "add_batch_us", "prepare_upload_us", "prepare_plan_us", "prepare_rest_us",
-                 "pass_groups", "add_pack_us", "add_dma_wait_us"]
+                 "pass_groups", "add_pack_us", "add_dma_wait_us", "finish_us", "finish_wait_us", "finish_copy_us",
+                 "finish_chunks"]
         return {names[i]: int(v[i]) for i in range(n)}
 
     def debug_jobs(self, k: int = 64) -> list:
@@ -368,18 +383,23 @@ class SignatureBuilder:
 
     @staticmethod
     def _kept(k) -> KeptKmers:
-        try:
-            n = int(k.n)
-            keys = np.ctypeslib.as_array(k.keys, shape=(max(n, 1),))[:n].copy() if n else np.zeros(0, np.uint64)
-            data = (np.frombuffer(C.string_at(k.data, 10 * n), dtype=STORED_DTYPE).copy() if n
-                    else np.zeros(0, STORED_DTYPE))
-            nf = int(k.n_functions)
-            df = np.ctypeslib.as_array(k.distinct_functions, shape=(max(nf, 1),))[:nf].copy()
-            sw = np.ctypeslib.as_array(k.seqs_with_func, shape=(max(nf, 1),))[:nf].copy()
-            return KeptKmers(keys, data, df, sw, int(k.n_seqs_with_signature), int(k.distinct_signatures),
-                             int(k.n_windows))
-        finally:
-            lib().skm_kept_free(C.byref(k))
+        """The library's arrays without a copy: keys / data view the hand-off's host arrays, which
+        skm_kept_free releases when the last view is gone."""
+        owner = _KeptOwner(k)
+        n = int(k.n)
+        if n:
+            kb = (C.c_char * (8 * n)).from_address(C.cast(k.keys, C.c_void_p).value)
+            db = (C.c_char * (10 * n)).from_address(C.cast(k.data, C.c_void_p).value)
+            kb._owner = db._owner = owner
+            keys = np.frombuffer(kb, np.uint64)
+            data = np.frombuffer(db, STORED_DTYPE)
+        else:
+            keys, data = np.zeros(0, np.uint64), np.zeros(0, STORED_DTYPE)
+        nf = int(k.n_functions)
+        df = np.ctypeslib.as_array(k.distinct_functions, shape=(max(nf, 1),))[:nf].copy()
+        sw = np.ctypeslib.as_array(k.seqs_with_func, shape=(max(nf, 1),))[:nf].copy()
+        return KeptKmers(keys, data, df, sw, int(k.n_seqs_with_signature), int(k.distinct_signatures),
+                         int(k.n_windows))
 
     def close(self):
         if self._h:
@@ -597,6 +617,7 @@ class QueryBatch:
         residues = np.ascontiguousarray(residues, dtype=np.uint8)
         seq_off = np.ascontiguousarray(seq_off, dtype=np.uint64)
         seq_len = np.ascontiguousarray(seq_len, dtype=np.uint32)
+        self._n_seqs = len(seq_len)
         _check(lib().skm_query_create(C.byref(self._h), db._h, _ptr(residues), _ptr(seq_off), _ptr(seq_len),
                                       len(seq_len)))
 
@@ -620,6 +641,18 @@ class QueryBatch:
             return off, calls
         finally:
             lib().skm_calls_free(C.byref(out))
+
+    def window_hits(self):
+        """skm_query_window_hits: (hit_off [n+1], pos, fm) of the last run -- every window the
+        device lookup found in the DB, as (offset in its sequence, function_index << 16 | mean)."""
+        n_seqs = self._n_seqs
+        off = np.zeros(n_seqs + 1, np.uint64)
+        n = C.c_uint64(0)
+        _check(lib().skm_query_window_hits(self._h, _ptr(off), None, None, 0, C.byref(n)))
+        pos = np.zeros(max(int(n.value), 1), np.uint32)
+        fm = np.zeros(max(int(n.value), 1), np.uint32)
+        _check(lib().skm_query_window_hits(self._h, _ptr(off), _ptr(pos), _ptr(fm), len(pos), C.byref(n)))
+        return off, pos[:n.value], fm[:n.value]
 
     def close(self):
         if self._h:

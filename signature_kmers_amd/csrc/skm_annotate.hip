@@ -1285,6 +1285,38 @@ int skm_query_calls(skm_query* q, skm_calls* out) {
     SKM_API_END
 }
 
+int skm_query_window_hits(skm_query* q, uint64_t* hit_off, uint32_t* pos, uint32_t* fm, uint64_t cap, uint64_t* n_out) {
+    SKM_API_BEGIN
+    SKM_CHECK(q && hit_off && n_out, SKM_E_ARG, "null argument");
+    SKM_CHECK(q->ran, SKM_E_STATE, "skm_query_run has not been called");
+    SKM_HIP(hipSetDevice(q->db->device));
+    // the device hit words, one per packed residue position (sequence s starts at pstart(s) =
+    // sum over t < s of len_t + 1): a window's word is its record's function_index << 16 | mean,
+    // NO_HIT where k_lookup found no usable window or no record
+    std::vector<uint32_t> h(q->rp);
+    if (q->rp) SKM_HIP(hipMemcpyAsync(h.data(), q->d_hits.p, 4 * q->rp, hipMemcpyDeviceToHost, q->stream));
+    std::vector<QMeta> meta(q->nseq);
+    if (q->nseq) SKM_HIP(hipMemcpyAsync(meta.data(), q->d_meta.p, sizeof(QMeta) * q->nseq, hipMemcpyDeviceToHost, q->stream));
+    SKM_HIP(hipStreamSynchronize(q->stream));
+    uint64_t n = 0;
+    for (uint32_t s = 0; s < q->nseq; ++s) {
+        hit_off[s] = n;
+        const uint64_t a = meta[s].pstart;
+        for (uint32_t i = 0; i < meta[s].len; ++i) {
+            const uint32_t w = h[a + i];
+            if (w == NO_HIT) continue;
+            if (n < cap) {
+                if (pos) pos[n] = i;
+                if (fm) fm[n] = w;
+            }
+            ++n;
+        }
+    }
+    hit_off[q->nseq] = n;
+    *n_out = n;
+    SKM_API_END
+}
+
 void skm_query_destroy(skm_query* q) {
     if (!q) return;
     (void)hipSetDevice(q->db->device);

@@ -37,6 +37,7 @@
 
 #include "skm_common.h"
 #include "skm_pool.h"
+#include "skm_output.h"
 #include "skm_util.h"
 
 #if defined(SKM_WITH_RCCL)
@@ -4828,7 +4829,8 @@ struct skm_build {
     uint64_t res_cap = 0;           // d_res capacity
     std::vector<SeqMeta> h_meta;
     std::vector<uint32_t> h_seqid;
-    std::unique_ptr<HostPool> pool;     // host threads of the packing (add_batch)
+    std::unique_ptr<HostPool> pool;     // host threads of the packing (add_batch) and the hand-off copies
+    HandoffStats handoff;               // the last finish's kept-set hand-off (skm_output.hip)
     std::vector<uint32_t> h_keep;       // add_batch scratch: the batch's kept sequences, their offsets
     std::vector<uint64_t> h_cum;
     // host seconds in add_batch (all calls), and prepare's phases: the residue / metadata upload, the
@@ -5414,6 +5416,16 @@ void prepare_local(skm_build* b) {
 // per-pass work buffers (~PASS_BYTES per element) leave room for the kept arena (18 B per kept
 // k-mer, accumulated over all passes).
 constexpr uint64_t PASS_BYTES = 104;   // recs 16 + tmp 16 + received 16 (world > 1) + chain lens/jobs ~10 + overflow scratch ~40
+// HBM a shard's work buffers take for passes of at most m elements: PASS_BYTES per element, with
+// key-range passes also the window-position slots of a pass group (8 B per element and slot,
+// G = min(P, 4) slots, size_local) and the pass-id byte per residue.
+inline uint64_t pass_work(uint64_t m, int pb, uint64_t rp) {
+    const uint64_t G = pb ? std::min<uint64_t>(1ull << pb, 4) : 0;
+    return m * (PASS_BYTES + 8 * G) + (pb ? rp : 0);
+}
+// the work buffers may take 5/8 of the budget; the kept arena (18 B per kept k-mer) and the
+// grow-and-redo reserve share the rest
+inline bool work_fits(uint64_t work, uint64_t budget) { return work <= budget / 8 * 5; }
 // forced_pb >= 0: the pass count the ranks agreed on (prepare), which leaves the caller's
 // key_range_passes option as it was set
 void size_passes(skm_build* b, int forced_pb = -1) {
@@ -5452,8 +5464,7 @@ void size_passes(skm_build* b, int forced_pb = -1) {
         // exchange (skewed owners); 2^32 - 2^28 leaves the same slack for the 32-bit indexing
         while (pb < 6) {
             const uint64_t m = pass_max(pb);
-            const uint64_t work = m * PASS_BYTES + (pb ? b->rp : 0);
-            if (m < (1ull << 32) - (1ull << 28) && work <= budget / 2) break;
+            if (m < (1ull << 32) - (1ull << 28) && work_fits(pass_work(m, pb, b->rp), budget)) break;
             ++pb;
         }
     }
@@ -5537,7 +5548,7 @@ void size_arena(skm_build* b) {
     uint64_t cap = std::min<uint64_t>(b->valid_total + 16, avail / (8 + sizeof(skm_stored_kmer_data)));
     if (b->tune.mem_budget_mb > 0) {
         const uint64_t budget = (uint64_t)b->tune.mem_budget_mb << 20;
-        const uint64_t used = b->pass_max * PASS_BYTES + b->rp;
+        const uint64_t used = pass_work(b->pass_max, b->pass_bits, b->rp);
         cap = std::min<uint64_t>(cap, budget > used ? (budget - used) / 18 : 0);
     }
     cap = std::max<uint64_t>(cap, b->pass_max + 16);
@@ -5631,7 +5642,7 @@ void route_plan(const Ranks& bs) {
         SKM_HIP(hipMemGetInfo(&fr, &tot));
         const uint64_t budget = b->tune.mem_budget_mb > 0 ? (uint64_t)b->tune.mem_budget_mb << 20 : (uint64_t)fr;
         const bool forced = b->tune.passes > 0;
-        ok[k] = m < (1ull << 32) - (1ull << 28) && (forced || m <= b->pass_max || m * PASS_BYTES + b->rp <= budget / 2);
+        ok[k] = m < (1ull << 32) - (1ull << 28) && (forced || m <= b->pass_max || work_fits(pass_work(m, pb, b->rp), budget));
         routed_m[k] = m;
         routed_n[k] = natural_late - late;
     }
@@ -6417,6 +6428,7 @@ void begin_run(skm_build* b) {
     hipStream_t st = b->stream;
     alloc_caps(b);
     b->chainq_next = 0;
+    b->emit_q = -1;  // no pass group's positions are queued from an earlier (possibly aborted) run
     SKM_HIP(hipEventRecord(b->ev_start, st));
     SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 3 * 256, st));
     b->ovf_pending[0] = b->ovf_pending[1] = false;
@@ -7263,14 +7275,15 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
     auto us = [](double sec) { return (uint64_t)(sec * 1e6); };
-    const uint64_t v[33] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+    const uint64_t v[37] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
                             b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total,
                             b->giant_jobs, b->giant_max, b->n_redo, b->tot_cap, b->split_cap, b->long_cap,
                             b->long_jobs_cap, b->demand[0], b->demand[1], b->demand[2], b->demand[3],
                             b->long_samples, b->routed, us(b->add_s), us(b->prep_upload_s), us(b->prep_plan_s),
                             us(b->prep_rest_s), b->pass_bits ? (1ull << b->pass_bits) / b->emit_g : 0ull, us(b->add_pack_s),
-                            us(b->add_wait_s)};
-    int n = std::min(cap, 33);
+                            us(b->add_wait_s), us(b->handoff.total_s), us(b->handoff.wait_s),
+                            us(b->handoff.copy_s), b->handoff.chunks};
+    int n = std::min(cap, 37);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }
@@ -7329,26 +7342,29 @@ int skm_build_finish(skm_build* b, skm_kept* out) {
     for (auto v : nk) total += v;
     const bool gather = b->world > 1 && b->rank == 0;
     const uint64_t n = gather ? total : b->n_kept;
-    std::vector<uint64_t> keys(n);
-    std::vector<skm_stored_kmer_data> data(n);
-    if (b->world > 1 && !bs.empty() && bs.size() > 1) {  // in-process group: plain copies
+    // the arena the hand-off reads: this rank's own, or (rank 0 at world > 1) every rank's in rank
+    // order on this device
+    DevBuf gk, gd;
+    const uint64_t* src_k = b->d_keys.as<uint64_t>();
+    const skm_stored_kmer_data* src_d = b->d_data.as<skm_stored_kmer_data>();
+    if (b->world > 1 && bs.size() > 1) {  // in-process group: device-to-device copies
         if (gather) {
+            gk.ensure(8 * (total + 1));
+            gd.ensure(sizeof(skm_stored_kmer_data) * (total + 1));
             uint64_t o = 0;
             for (auto* x : bs) {
                 if (x->n_kept) {
-                    SKM_HIP(hipMemcpy(keys.data() + o, x->d_keys.p, 8 * x->n_kept, hipMemcpyDeviceToHost));
-                    SKM_HIP(hipMemcpy(data.data() + o, x->d_data.p, sizeof(skm_stored_kmer_data) * x->n_kept,
-                                      hipMemcpyDeviceToHost));
+                    SKM_HIP(hipMemcpy(gk.as<uint64_t>() + o, x->d_keys.p, 8 * x->n_kept, hipMemcpyDeviceToDevice));
+                    SKM_HIP(hipMemcpy(gd.as<skm_stored_kmer_data>() + o, x->d_data.p,
+                                      sizeof(skm_stored_kmer_data) * x->n_kept, hipMemcpyDeviceToDevice));
                 }
                 o += x->n_kept;
             }
-        } else if (n) {
-            SKM_HIP(hipMemcpy(keys.data(), b->d_keys.p, 8 * n, hipMemcpyDeviceToHost));
-            SKM_HIP(hipMemcpy(data.data(), b->d_data.p, sizeof(skm_stored_kmer_data) * n, hipMemcpyDeviceToHost));
+            src_k = gk.as<uint64_t>();
+            src_d = gd.as<skm_stored_kmer_data>();
         }
-    } else if (b->world > 1) {  // RCCL: every rank sends its k-mers to rank 0
+    } else if (b->world > 1) {  // RCCL / host transport: every rank sends its k-mers to rank 0
         const int W = b->world;
-        DevBuf gk, gd;
         A2A xk, xd;
         std::vector<uint64_t> so(W, 0), sck(W, 0), scd(W, 0), rok(W, 0), rod(W, 0), rck(W, 0), rcd(W, 0);
         sck[0] = 8 * b->n_kept;
@@ -7380,16 +7396,10 @@ int skm_build_finish(skm_build* b, skm_kept* out) {
         alltoallv(bs, xk);
         alltoallv(bs, xd);
         SKM_HIP(hipStreamSynchronize(b->stream));
-        const void* sk = gather ? gk.p : b->d_keys.p;
-        const void* sd = gather ? gd.p : b->d_data.p;
-        if (n) {
-            SKM_HIP(hipMemcpy(keys.data(), sk, 8 * n, hipMemcpyDeviceToHost));
-            SKM_HIP(hipMemcpy(data.data(), sd, sizeof(skm_stored_kmer_data) * n, hipMemcpyDeviceToHost));
+        if (gather) {
+            src_k = gk.as<uint64_t>();
+            src_d = gd.as<skm_stored_kmer_data>();
         }
-    } else if (n) {
-        SKM_HIP(hipMemcpyAsync(keys.data(), b->d_keys.p, 8 * n, hipMemcpyDeviceToHost, b->stream));
-        SKM_HIP(hipMemcpyAsync(data.data(), b->d_data.p, sizeof(skm_stored_kmer_data) * n, hipMemcpyDeviceToHost,
-                               b->stream));
     }
     out->distinct_functions = (uint32_t*)std::malloc(sizeof(uint32_t) * std::max<uint32_t>(F, 1));
     out->seqs_with_func = (uint32_t*)std::malloc(sizeof(uint32_t) * std::max<uint32_t>(F, 1));
@@ -7407,17 +7417,9 @@ int skm_build_finish(skm_build* b, skm_kept* out) {
         if (b->n_total) SKM_HIP(hipMemcpyAsync(flags.data(), b->d_flags.p, b->n_total, hipMemcpyDeviceToHost, b->stream));
     }
     SKM_HIP(hipStreamSynchronize(b->stream));
-    // deterministic output order: sort by key
-    std::vector<uint64_t> perm(n);
-    std::iota(perm.begin(), perm.end(), 0);
-    std::sort(perm.begin(), perm.end(), [&](uint64_t x, uint64_t y) { return keys[x] < keys[y]; });
-    out->keys = (uint64_t*)std::malloc(8 * std::max<uint64_t>(n, 1));
-    out->data = (skm_stored_kmer_data*)std::malloc(sizeof(skm_stored_kmer_data) * std::max<uint64_t>(n, 1));
-    SKM_CHECK(out->keys && out->data, SKM_E_OOM, "host allocation failed");
-    for (uint64_t i = 0; i < n; ++i) {
-        out->keys[i] = keys[perm[i]];
-        out->data[i] = data[perm[i]];
-    }
+    // keys ascending: device radix sort in chunks, streamed to the host arrays (skm_output.hip)
+    if (!b->pool) b->pool.reset(new HostPool(HostPool::default_threads()));
+    kept_handoff(src_k, src_d, n, b->stream, b->pool.get(), &out->keys, &out->data, &b->handoff);
     out->n = n;
     out->n_functions = F;
     out->distinct_signatures = total;
@@ -7461,8 +7463,6 @@ int skm_build_finish_slice(skm_build* b, int slice_bits, uint32_t slice, skm_kep
     uint64_t n = 0;
     SKM_HIP(hipMemcpyAsync(&n, cur.p, 8, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
-    std::vector<uint64_t> keys(n);
-    std::vector<skm_stored_kmer_data> data(n);
     if (n) {
         dk.ensure(8 * n);
         dd.ensure(sizeof(skm_stored_kmer_data) * n + 16);
@@ -7471,15 +7471,10 @@ int skm_build_finish_slice(skm_build* b, int slice_bits, uint32_t slice, skm_kep
                            b->d_data.as<skm_stored_kmer_data>(), nk, slice_bits, (uint64_t)slice,
                            cur.as<unsigned long long>(), dk.as<uint64_t>(), dd.as<skm_stored_kmer_data>());
         SKM_HIP(hipGetLastError());
-        SKM_HIP(hipMemcpyAsync(keys.data(), dk.p, 8 * n, hipMemcpyDeviceToHost, st));
-        SKM_HIP(hipMemcpyAsync(data.data(), dd.p, sizeof(skm_stored_kmer_data) * n, hipMemcpyDeviceToHost, st));
     }
     out->distinct_functions = (uint32_t*)std::malloc(sizeof(uint32_t) * std::max<uint32_t>(F, 1));
     out->seqs_with_func = (uint32_t*)std::malloc(sizeof(uint32_t) * std::max<uint32_t>(F, 1));
-    out->keys = (uint64_t*)std::malloc(8 * std::max<uint64_t>(n, 1));
-    out->data = (skm_stored_kmer_data*)std::malloc(sizeof(skm_stored_kmer_data) * std::max<uint64_t>(n, 1));
-    SKM_CHECK(out->distinct_functions && out->seqs_with_func && out->keys && out->data, SKM_E_OOM,
-              "host allocation failed");
+    SKM_CHECK(out->distinct_functions && out->seqs_with_func, SKM_E_OOM, "host allocation failed");
     if (F) {
         SKM_HIP(hipMemcpyAsync(out->distinct_functions, b->d_dfunc.p, sizeof(uint32_t) * F, hipMemcpyDeviceToHost, st));
         SKM_HIP(hipMemcpyAsync(out->seqs_with_func, b->d_swf.p, sizeof(uint32_t) * F, hipMemcpyDeviceToHost, st));
@@ -7487,30 +7482,10 @@ int skm_build_finish_slice(skm_build* b, int slice_bits, uint32_t slice, skm_kep
     unsigned long long ctr[3];
     SKM_HIP(hipMemcpyAsync(ctr, b->d_ctr.p, sizeof(ctr), hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
-    // keys ascending: chunks sorted on the host threads, then merged pairwise
-    std::vector<std::pair<uint64_t, uint32_t>> kv(n);
-    for (uint64_t i = 0; i < n; ++i) kv[i] = {keys[i], (uint32_t)i};
-    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>(16, n / 65536 + 1));
-    std::vector<uint64_t> cut(T + 1);
-    for (int t = 0; t <= T; ++t) cut[t] = n * (uint64_t)t / (uint64_t)T;
-    {
-        std::vector<std::thread> th;
-        for (int t = 0; t < T; ++t)
-            th.emplace_back([&, t]() { std::sort(kv.begin() + cut[t], kv.begin() + cut[t + 1]); });
-        for (auto& x : th) x.join();
-    }
-    for (int w = 1; w < T; w <<= 1) {
-        std::vector<std::thread> th;
-        for (int t = 0; t + w < T; t += 2 * w)
-            th.emplace_back([&, t, w]() {
-                std::inplace_merge(kv.begin() + cut[t], kv.begin() + cut[t + w], kv.begin() + cut[std::min(T, t + 2 * w)]);
-            });
-        for (auto& x : th) x.join();
-    }
-    for (uint64_t i = 0; i < n; ++i) {
-        out->keys[i] = kv[i].first;
-        out->data[i] = data[kv[i].second];
-    }
+    // keys ascending: the slice sorted on the device and streamed out (skm_output.hip)
+    if (!b->pool) b->pool.reset(new HostPool(HostPool::default_threads()));
+    kept_handoff(dk.as<uint64_t>(), dd.as<skm_stored_kmer_data>(), n, st, b->pool.get(), &out->keys, &out->data,
+                 &b->handoff);
     out->n = n;
     out->n_functions = F;
     uint64_t total = b->n_kept;

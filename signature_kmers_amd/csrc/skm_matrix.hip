@@ -830,11 +830,13 @@ uint64_t md_exchange(skm_matrix* M, uint64_t n_local, uint32_t idx_bits, hipStre
             SKM_HIP(hipGetLastError());
             M->scan.run(M->d_rtc.as<uint32_t>(), G, M->d_rto.as<uint64_t>(), st);
         };
+        // every band's count, scan and total copy queued back to back (stream order keeps band q's
+        // total copy ahead of band q+1's scan); one host synchronisation for all W totals
         for (int q = 0; q < W; ++q) {
             count_band(q);
             SKM_HIP(hipMemcpyAsync(&bc[q], M->d_rto.as<uint64_t>() + G, 8, hipMemcpyDeviceToHost, st));
-            SKM_HIP(hipStreamSynchronize(st));
         }
+        SKM_HIP(hipStreamSynchronize(st));
         for (int q = 1; q < W; ++q) bo[q] = bo[q - 1] + bc[q - 1];
         const uint64_t tot = bo[W - 1] + bc[W - 1];
         M->d_send.ensure(8 * std::max<uint64_t>(tot, 1));

@@ -1,0 +1,27 @@
+// skm_output.h -- the kept-set hand-off from HBM to host arrays in key order (skm_output.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdint>
+
+#include "skm.h"
+#include "skm_pool.h"
+
+namespace skm {
+
+struct HandoffStats {
+    uint64_t n = 0, chunks = 0, bytes = 0;
+    double setup_s = 0;  // pinned staging + stream + events
+    double wait_s = 0;   // host waiting for a piece's D2H (device sort + PCIe not yet done)
+    double copy_s = 0;   // host pool copying pieces from pinned staging into the output arrays
+    double total_s = 0;
+};
+
+// The n kept k-mers of a device arena (raw little-endian keys, 10-byte records; keys distinct) into
+// newly allocated host arrays (*keys_out, *data_out; release with std::free), ascending by key.
+// Device work runs on st; pool (may be null) copies the pinned pieces out.
+void kept_handoff(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint64_t n, hipStream_t st,
+                  HostPool* pool, uint64_t** keys_out, skm_stored_kmer_data** data_out, HandoffStats* stats);
+
+}  // namespace skm

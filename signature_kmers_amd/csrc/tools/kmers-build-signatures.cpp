@@ -33,6 +33,7 @@
 #include <map>
 #include <sstream>
 #include <thread>
+#include <vector>
 #include <atomic>
 #include <condition_variable>
 #include <mutex>
@@ -58,14 +59,53 @@ void die(const std::string& m) {
     std::exit(1);
 }
 
-std::string kmer_str(uint64_t k) {
-    char b[9];
-    std::memcpy(b, &k, 8);
-    b[8] = 0;
-    return std::string(b, 8);
-}
-
 std::string quoted(const std::string& p) { return "\"" + p + "\""; }
+
+// final.kmers (kmers-build-signatures.cc:212-216): "KMER\tavg_from_end\tfunction_index\t\n" per
+// kept k-mer.  Blocks of lines are formatted on `threads` threads and written in order.
+void write_final_kmers(const std::string& path, const skm_kept& kept, int threads) {
+    std::ofstream kf(path, std::ios::binary);
+    const uint64_t B = 1u << 20;  // lines per block
+    const uint64_t nb = (kept.n + B - 1) / B;
+    const int T = std::max(1, threads);
+    std::vector<std::string> buf(T);
+    auto fmt_u = [](char* p, unsigned v) {  // decimal, returns the digits written
+        char t[8];
+        int n = 0;
+        do {
+            t[n++] = (char)('0' + v % 10);
+            v /= 10;
+        } while (v);
+        for (int i = 0; i < n; ++i) p[i] = t[n - 1 - i];
+        return n;
+    };
+    for (uint64_t g = 0; g < nb; g += (uint64_t)T) {
+        const int m = (int)std::min<uint64_t>((uint64_t)T, nb - g);
+        auto work = [&](int t) {
+            const uint64_t a = (g + (uint64_t)t) * B, e = std::min<uint64_t>(kept.n, a + B);
+            std::string& o = buf[t];
+            o.resize((e - a) * 24);
+            char* p = &o[0];
+            for (uint64_t i = a; i < e; ++i) {
+                std::memcpy(p, &kept.keys[i], 8);
+                p[8] = '\t';
+                p += 9;
+                p += fmt_u(p, kept.data[i].avg_from_end);
+                *p++ = '\t';
+                p += fmt_u(p, kept.data[i].function_index);
+                *p++ = '\t';
+                *p++ = '\n';
+            }
+            o.resize((size_t)(p - &o[0]));
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < m; ++t) th.emplace_back(work, t);
+        work(0);
+        for (auto& x : th) x.join();
+        for (int t = 0; t < m; ++t) kf.write(buf[t].data(), (std::streamsize)buf[t].size());
+    }
+    if (!kf) die("cannot write " + path);
+}
 
 // binary dump of the build input (--dump-extract): u64 n_seqs, u64 n_residues, then
 // residues[n_residues], off u64[n], len u32[n], func u16[n], seq_id u32[n]
@@ -315,6 +355,7 @@ int main(int argc, char** argv) {
         }
         check(skm_build_set_comm(b, id), "skm_build_set_comm");
     }
+    const double t_add0 = now_s();
     for (size_t f = f0; f < f1; ++f) {
         {
             std::unique_lock<std::mutex> g(sel_mu);
@@ -327,14 +368,21 @@ int main(int argc, char** argv) {
               "skm_build_add_batch");
     }
     join_selection();
+    const double t_add = now_s() - t_add0;
     std::cerr << "process kmers\n";
     t0 = now_s();
     check(skm_build_prepare(b), "skm_build_prepare");
+    const double t_prepare = now_s() - t0;
+    t0 = now_s();
+    check(skm_build_run(b), "skm_build_run");
+    const double t_run = now_s() - t0;
+    t0 = now_s();
     skm_kept kept{};
     check(skm_build_finish(b, &kept), "skm_build_finish");
+    const double t_finish = now_s() - t0;
     float ph[12] = {0};
     int nph = skm_build_last_timings(b, ph, 12);
-    const double t_build = now_s() - t0;
+    const double t_build = t_prepare + t_run + t_finish;
     skm_build_destroy(b);
     if (rank != 0) {  // rank 0 holds every kept k-mer and the all-reduced statistics
         skm_kept_free(&kept);
@@ -345,27 +393,17 @@ int main(int argc, char** argv) {
     std::cout << "num_seqs_with_a_signature=" << kept.n_seqs_with_signature << "\n";
 
     std::thread final_kmers_thread;
+    double t_final_kmers = 0, t_mph = 0;
     if (!final_kmers.empty()) {
         if (path_is_relative(final_kmers)) {
             final_kmers = path_join(kmer_data_dir, final_kmers);
             std::cerr << "Updated final_kmers to " << quoted(final_kmers) << "\n";
         }
         final_kmers_thread = std::thread([&]() {
+            const double tk = now_s();
             std::cerr << "writing kmers to " << quoted(final_kmers) << "\n";
-            std::ofstream kf(final_kmers);
-            std::string buf;
-            buf.reserve(1 << 20);
-            char line[64];
-            for (uint64_t i = 0; i < kept.n; ++i) {
-                int l = std::snprintf(line, sizeof line, "%s\t%u\t%u\t\n", kmer_str(kept.keys[i]).c_str(),
-                                      (unsigned)kept.data[i].avg_from_end, (unsigned)kept.data[i].function_index);
-                buf.append(line, (size_t)l);
-                if (buf.size() > (1 << 20) - 64) {
-                    kf.write(buf.data(), (std::streamsize)buf.size());
-                    buf.clear();
-                }
-            }
-            kf.write(buf.data(), (std::streamsize)buf.size());
+            write_final_kmers(final_kmers, kept, std::max(1, n_threads / 2));
+            t_final_kmers = now_s() - tk;
             std::cerr << "writing kmers to " << quoted(final_kmers) << " complete\n";
         });
     }
@@ -388,8 +426,10 @@ int main(int argc, char** argv) {
         if (path_is_relative(ph_data)) ph_data = path_join(kmer_data_dir, ph_data);
         const uint32_t seed = (uint32_t)std::strtoul(op.get("mph-seed", "1").c_str(), nullptr, 10);
         perfect_hash_thread = std::thread([&, seed]() {
+            const double tm = now_s();
             std::cerr << "build perfect hash into " << quoted(ph_file) << " with data in " << quoted(ph_data) << "\n";
             ph_rc = skm_mph_build_device(kept.keys, kept.data, kept.n, seed, ph_file.c_str(), ph_data.c_str(), device);
+            t_mph = now_s() - tm;
             if (ph_rc)
                 ph_err = skm_last_error();
             else
@@ -425,6 +465,7 @@ int main(int argc, char** argv) {
         for (auto& e : data) of << e.second;
     }
     const double t_recall = now_s() - t0;
+    const double t_recall_dev = recall_dev_ms / 1000.0;
 
     if (op.has("nudb-file")) std::cerr << "--nudb-file: NuDB output is not supported by this build; skipped\n";
     if (perfect_hash_thread.joinable()) {
@@ -440,6 +481,10 @@ int main(int argc, char** argv) {
     if (!mesh.wait_children(err)) die(err);
     std::cerr << "timing: parse " << t_parse << " s, build " << t_build << " s (device pipeline "
               << (nph > 7 ? ph[7] : 0.0f) << " ms), recall " << t_recall << " s, total " << now_s() - t_start << " s\n";
+    // one machine-readable line of the phases (bench.py's cli_build leg)
+    std::cerr << "phases: parse " << t_parse << " add " << t_add << " prepare " << t_prepare << " run " << t_run
+              << " finish " << t_finish << " final_kmers " << t_final_kmers << " mph " << t_mph << " recall "
+              << t_recall << " recall_device " << t_recall_dev << " total " << now_s() - t_start << "\n";
     std::cerr << "all done\n";
     return 0;
 }

@@ -39,48 +39,38 @@ bool file_exists(const std::string& p) {
 }
 
 // --debug-hits: hit stream of FunctionCaller::process_aa_seq (for_each_kmer + fetch + the hypo
-// filter), printed as the reference's hit_cb does.
+// filter), printed as the reference's hit_cb does.  The windows and their DB hits are the device's
+// (k_lookup's window iterator, skm_query_window_hits); the printed record fields come from the
+// .dat slot of each hit window's key.
 void debug_hits(skm_db* db, const std::vector<uint8_t>& dat, const FastaFile& f, const std::vector<std::string>& fidx,
                 bool ignore_hypo, int hypo, std::ostream& os) {
-    uint32_t m = 0;
-    skm_db_size(db, &m);
-    for (size_t r = 0; r < f.size(); ++r) {
-        const uint8_t* s = f.residues.data() + f.off[r];
-        const uint32_t len = f.len[r];
-        std::vector<uint64_t> keys;
-        std::vector<uint32_t> pos;
-        // for_each_kmer<8> (kmer_data.h:76-102)
-        auto is_amb = [](uint8_t c) { return c == '*' || c == 'X'; };
-        uint32_t p = 0;
-        uint32_t na = 0;
-        while (na < len && !is_amb(s[na])) ++na;
-        while (len >= 8 && p <= len - 8) {
-            if (na != len && p + 8 >= na) {
-                p = na + 1;
-                na = p;
-                while (na < len && !is_amb(s[na])) ++na;
-                continue;
-            }
-            uint64_t k;
-            std::memcpy(&k, s + p, 8);
-            keys.push_back(k);
-            pos.push_back(p);
-            ++p;
-        }
-        std::vector<uint32_t> idx(keys.size());
-        if (!keys.empty() && skm_db_lookup(db, keys.data(), keys.size(), idx.data())) die(skm_last_error());
-        for (size_t i = 0; i < keys.size(); ++i) {
-            if (idx[i] >= m) continue;
-            skm_stored_kmer_data kd;
-            std::memcpy(&kd, dat.data() + 10ull * idx[i], 10);
-            if (ignore_hypo && kd.function_index == hypo) continue;
-            char kb[9];
-            std::memcpy(kb, &keys[i], 8);
-            kb[8] = 0;
-            const std::string fn = kd.function_index < fidx.size() ? fidx[kd.function_index] : "";
-            os << kb << "\t" << pos[i] << "\t" << fn << "\t" << kd.median << "\t" << kd.mean << "\t" << kd.var << "\t"
-               << fmt_g(std::sqrt((double)kd.var)) << "\t" << "\n";
-        }
+    const size_t n = f.size();
+    if (n == 0) return;
+    std::vector<uint64_t> off(f.off.begin(), f.off.end());
+    skm_query* q = nullptr;
+    if (skm_query_create(&q, db, f.residues.data(), off.data(), f.len.data(), n)) die(skm_last_error());
+    skm_annot_opts o{5, 200, 0, -1, 0, 0};
+    std::vector<uint64_t> hoff(n + 1);
+    uint64_t nh = 0;
+    if (skm_query_run(q, &o) || skm_query_window_hits(q, hoff.data(), nullptr, nullptr, 0, &nh)) die(skm_last_error());
+    std::vector<uint32_t> pos(std::max<uint64_t>(nh, 1));
+    if (skm_query_window_hits(q, hoff.data(), pos.data(), nullptr, nh, &nh)) die(skm_last_error());
+    skm_query_destroy(q);
+    std::vector<uint64_t> keys(nh);
+    for (size_t r = 0; r < n; ++r)
+        for (uint64_t h = hoff[r]; h < hoff[r + 1]; ++h) std::memcpy(&keys[h], f.residues.data() + f.off[r] + pos[h], 8);
+    std::vector<uint32_t> idx(nh);
+    if (nh && skm_db_lookup(db, keys.data(), nh, idx.data())) die(skm_last_error());
+    for (uint64_t i = 0; i < nh; ++i) {
+        skm_stored_kmer_data kd;
+        std::memcpy(&kd, dat.data() + 10ull * idx[i], 10);
+        if (ignore_hypo && kd.function_index == hypo) continue;
+        char kb[9];
+        std::memcpy(kb, &keys[i], 8);
+        kb[8] = 0;
+        const std::string fn = kd.function_index < fidx.size() ? fidx[kd.function_index] : "";
+        os << kb << "\t" << pos[i] << "\t" << fn << "\t" << kd.median << "\t" << kd.mean << "\t" << kd.var << "\t"
+           << fmt_g(std::sqrt((double)kd.var)) << "\t" << "\n";
     }
 }
 

@@ -5,8 +5,13 @@
 //   roles_of_function(s) joined by 0x01 | genome defline match (0/1) func genome | fig genome (0/1) genome
 // skm-front-probe --fasta FILE KEEP: parse FILE (KEEP 1 = with residues, 0 = headers-only) and print
 // one line per record (hex id, hex definition, offset, length), then "n_residues N residues R".
+// skm-front-probe --fasta-hex: one hex-encoded FASTA file image per stdin line ("-" = empty); per
+// image, one line per record "R <hex id> <hex def> <hex residues>" and one per parse error the
+// parser reported "E <line> <hex message> <hex id>", in the order the parser produced them, then
+// "END" (the shape of oracle/ref_pin's output, so tests compare with the reference's FastaParser).
 #include <cstdio>
 #include <iostream>
+#include <sstream>
 #include <string>
 
 #include "skm_front.h"
@@ -38,6 +43,40 @@ int main(int argc, char** argv) {
         return 0;
     }
     std::string line;
+    if (argc == 2 && std::string(argv[1]) == "--fasta-hex") {
+        while (std::getline(std::cin, line)) {
+            const std::string img = line == "-" ? std::string() : unhex(line);
+            std::ostringstream errs;
+            std::streambuf* old = std::cerr.rdbuf(errs.rdbuf());
+            FastaFile f;
+            parse_fasta_buffer(img.data(), img.size(), f, true);
+            std::cerr.rdbuf(old);
+            // records and errors interleave in parse order: a record is emitted when the next
+            // '>' (or the end) is read, so each error line precedes the records emitted after it;
+            // the probe reports errors with the record they were found in (by the id shown)
+            std::istringstream es(errs.str());
+            std::string el;
+            while (std::getline(es, el)) {
+                // "Error found: <msg> at line <n> id='<id>'"
+                const std::string pre = "Error found: ";
+                const size_t at = el.rfind(" at line "), idq = el.rfind(" id='");
+                if (el.compare(0, pre.size(), pre) != 0 || at == std::string::npos || idq == std::string::npos) {
+                    std::cout << "X " << hex(el) << "\n";
+                    continue;
+                }
+                const std::string msg = el.substr(pre.size(), at - pre.size());
+                const std::string ln = el.substr(at + 9, idq - at - 9);
+                const std::string id = el.substr(idq + 5, el.size() - idq - 6);
+                std::cout << "E " << ln << " " << hex(msg) << " " << hex(id) << "\n";
+            }
+            for (size_t r = 0; r < f.size(); ++r)
+                std::cout << "R " << hex(f.ids[r]) << " " << hex(f.defs[r]) << " "
+                          << hex(std::string(f.residues.begin() + f.off[r], f.residues.begin() + f.off[r] + f.len[r]))
+                          << "\n";
+            std::cout << "END\n";
+        }
+        return 0;
+    }
     while (std::getline(std::cin, line)) {
         std::string s = line == "-" ? std::string() : unhex(line);
         std::string f, sep, c;

@@ -62,6 +62,8 @@ def olib():
         _lib.oracle_matrix_distance.argtypes = [P, P, P, P, P, P, C.c_uint64, C.c_int32, P, C.c_uint64]
         _lib.oracle_matrix_distance_mt.restype = C.c_int64
         _lib.oracle_matrix_distance_mt.argtypes = [P, P, P, P, P, P, C.c_uint64, C.c_int32, P, C.c_uint64, C.c_int]
+        _lib.oracle_kmer_windows.restype = C.c_uint32
+        _lib.oracle_kmer_windows.argtypes = [C.c_char_p, C.c_uint32, P]
         _lib.oracle_find_best_call.argtypes = [P, C.c_uint64, C.POINTER(C.c_char_p), C.c_uint64, P, P, P,
                                                C.c_char_p, C.c_uint64]
     return _lib
@@ -69,6 +71,13 @@ def olib():
 
 def _p(a):
     return a.ctypes.data_as(C.c_void_p)
+
+
+def kmer_windows(seq: bytes) -> np.ndarray:
+    """The window offsets the oracle's for_each_kmer<8> restatement yields over one sequence."""
+    out = np.zeros(max(len(seq), 1), np.uint32)
+    n = olib().oracle_kmer_windows(seq, len(seq), _p(out))
+    return out[:n]
 
 
 def build(residues, seq_off, seq_len, seq_func, seq_id, n_functions):

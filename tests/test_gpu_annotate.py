@@ -109,6 +109,49 @@ def test_query_edge_cases(skm, gpu, tmp_path):
     np.testing.assert_array_equal(gcalls.view(np.uint8), ocalls.view(np.uint8))
 
 
+@pytest.mark.parametrize("kind", ["exact", "bdz"])
+def test_device_windows_match_reference(skm, gpu, tmp_path, kind):
+    """The device window iterator (k_lookup's validity test: no 'X' / '*' in the window or the byte
+    right after it) against the REFERENCE's own for_each_kmer<8> (kmer_data.h:76-102, compiled
+    from the reference: tests/golden/ref_windows.npz).  The DB holds every k-mer of every valid
+    window, so the device's hit windows (skm_query_window_hits) are exactly its windows."""
+    from test_ref_pin_cpu import ref_windows
+    seqs, wins = ref_windows()
+    keys = [int.from_bytes(s[q:q + 8], "little") for s, w in zip(seqs, wins) for q in w]
+    keys = np.unique(np.array(keys, np.uint64))
+    data = np.zeros(len(keys), skm.STORED_DTYPE)
+    data["function_index"] = 1 + np.arange(len(keys)) % 7
+    data["mean"] = np.arange(len(keys)) % 60000
+    if kind == "exact":
+        db = skm.KeptKmerDb(keys, data)
+    else:
+        base = str(tmp_path / "kmer_data")
+        skm.mph_build(keys, data, base + ".mph", base + ".dat", seed=3)
+        db = skm.CmphKmerDb(base)
+    lens = np.array([len(s) for s in seqs], np.uint32)
+    off = np.zeros(len(seqs), np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    qb = skm.QueryBatch(db, np.frombuffer(b"".join(seqs), np.uint8), off, lens)
+    qb.run(hypo_index=-1)
+    hoff, pos, fm = qb.window_hits()
+    for i, w in enumerate(wins):
+        np.testing.assert_array_equal(pos[hoff[i]:hoff[i + 1]], w.astype(np.uint32), err_msg=repr(seqs[i]))
+    # each hit carries its own record's function_index << 16 | mean
+    got = np.array([int.from_bytes(seqs[i][q:q + 8], "little") for i in range(len(seqs))
+                    for q in pos[hoff[i]:hoff[i + 1]]], np.uint64)
+    j = np.searchsorted(keys, got)
+    want = (data["function_index"][j].astype(np.uint32) << 16) | data["mean"][j]
+    if kind == "exact":
+        np.testing.assert_array_equal(fm, want)
+    else:
+        slot = db.lookup_keys(got)
+        d = np.frombuffer(open(str(tmp_path / "kmer_data.dat"), "rb").read(), skm.STORED_DTYPE)
+        np.testing.assert_array_equal(fm, (d["function_index"][slot].astype(np.uint32) << 16) | d["mean"][slot])
+        np.testing.assert_array_equal(fm, want)
+    qb.close()
+    db.close()
+
+
 def test_kept_db_exact_lookup_and_recall_calls(skm, gpu, tmp_path):
     """KeptKmerDB (exact keys): members hit their own record, strangers miss; the call path over
     it equals the oracle's recall-pass restatement (kept_kmer_db.h:20-27)."""
