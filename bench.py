@@ -76,6 +76,11 @@ def parse():
                     help="recall leg (SURVEY 8(f)2: the C2 training set vs its exact kept-k-mer DB); 0 = off; N=1 only")
     ap.add_argument("--matrix-seqs", type=int, default=100_000,
                     help="matrix-distance leg (BASELINE configs[4]); 0 = off; owner-partitioned over the ranks")
+    ap.add_argument("--cli-seqs", type=int, default=1_000_000,
+                    help="cli_build leg: bin/kmers-build-signatures end to end on FASTA directories of this many "
+                         "proteins (BASELINE configs[1]); 0 = off; N=1 only")
+    ap.add_argument("--finish", type=int, default=1,
+                    help="time skm_build_finish (the kept-set hand-off to host arrays) on the headline build; N=1")
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
                     help="rank exchange of the build: RCCL over xGMI, or the gloo host transport (rehearses the "
                          "multi-rank path with several ranks on one GPU)")
@@ -212,6 +217,14 @@ def main():
         tf = n_train // PER_FILE
         matrix_in = (gen(synth, n_train, fam, 0, tf, workers, a.cache_dir),
                      gen(synth, (tf + nfq) * PER_FILE, fam, tf, nfq, workers, a.cache_dir), synth.functions(fam))
+    cli_dir = None
+    if world == 1 and a.cli_seqs > 0:  # FASTA directories for the cli_build leg (spawned writers)
+        import tempfile
+        cli_dir = tempfile.mkdtemp(prefix="skm_cli_", dir="/tmp")
+        t = time.time()
+        synth.write_dirs_parallel(os.path.join(cli_dir, "in"), a.cli_seqs, a.families, per_file=PER_FILE,
+                                  workers=workers)
+        log(f"cli_build input: {a.cli_seqs:,} proteins as FASTA in {time.time() - t:.1f} s")
     if a.cache_only:
         log("inputs cached")
         return
@@ -247,6 +260,20 @@ def main():
     prep_s = time.time() - t0
     log(f"C3 prepared in {prep_s:.1f} s")
     head = _measure(skm, b, a.steps, a.warmup, c3, world, dist)
+    finish = None
+    if world == 1 and a.finish:  # the kept-set hand-off of the headline build (skm_build_finish)
+        t = time.perf_counter()
+        k = b.finish()
+        dt = time.perf_counter() - t
+        c = b.counters()
+        ok = len(k.keys) == c["kept"] and bool(np.all(k.keys[1:] > k.keys[:-1]))
+        finish = {"seconds": dt, "kept": int(len(k.keys)), "bytes": 18 * int(len(k.keys)), "GBs": 18 * len(k.keys) / dt / 1e9,
+                  "sorted_and_complete": ok, "chunks": c["finish_chunks"], "host_wait_s": c["finish_wait_us"] / 1e6,
+                  "host_copy_s": c["finish_copy_us"] / 1e6,
+                  "note": "skm_build_finish: device radix sort in key-range chunks, D2H through pinned staging, "
+                          "copied out by the host pool; keys ascending in malloc'd host arrays"}
+        del k
+        log(f"finish (hand-off of {finish['kept']:,} kept k-mers): {dt:.2f} s")
     b.close()
     per_gpu = a.seqs_total // world
     out = {
@@ -272,7 +299,9 @@ def main():
                    f"all-to-all + all-reduce, per key-range pass"},
         "roofline": head["roofline"],
         "pipeline": head["pipeline"],
+        "value_with_plan": _with_plan(head),
         "pcie_inclusive": _pcie_inclusive(head, prep_s, create_s),
+        "finish": finish,
         "cpu_baseline": None,
         "gen_seconds": gen_s,
         "prepare_seconds": prep_s,
@@ -323,6 +352,9 @@ def main():
     if world == 1 and queries is not None and kept is not None:
         log("annotate leg")
         out["annotate"] = _annotate_leg(skm, kept, funcs, queries, a, device, cores)
+    if cli_dir is not None:
+        log("cli_build leg")
+        out["cli_build"] = _cli_build_leg(cli_dir, a)
     if matrix_in is not None:
         log("matrix leg")
         mx = _matrix_leg(skm, matrix_in, a, device, cores, rank, world, dist)
@@ -462,7 +494,10 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
         "windows_total": int(windows_total),
         "passes": b.passes(),
         "counters": ctrs,
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": "hbm", "kernel": dom, "role": "critical-path kernel (the main stream's group-by)",
+                     "largest_gpu_time_kernel": big,
+                     "largest_gpu_time_frac": None if largest is None else largest["frac"],
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS if achieved is not None else None,
                      "traffic": None if traffic is None else traffic / launches,
                      "traffic_source": None if traffic is None else f"profiles/{_PMC_FILE} (same libskm sources)",
@@ -478,6 +513,52 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
         "pipeline": {"alg_bytes": pipe_alg, "ms": 1000.0 * t_max / steps, "GBs": pipe_gbs,
                      "frac": pipe_gbs / HBM_PEAK_GBS / max(1, world), "phase_ms_rank0": phase},
     }
+
+
+def _with_plan(m):
+    """The headline rate with prepare's device pass plan (route sketch, Bloom pack, pass tallies:
+    work every build pays once per input) added to the step: reported beside `value`, whose timed
+    step reuses the plan."""
+    plan = m["counters"].get("prepare_plan_us", 0) / 1e6
+    t = m["ms_per_step"] / 1000.0 + plan
+    return {"value": m["windows_total"] / t, "unit": "k-mers/s", "plan_s": plan, "step_s": m["ms_per_step"] / 1000.0}
+
+
+def _cli_build_leg(cli_dir, a):
+    """bin/kmers-build-signatures end to end (kmers-build-signatures.cc:126-373) on FASTA directories of
+    a.cli_seqs proteins (BASELINE configs[1] at the default): parse + FunctionMap, sequence selection
+    and add_batch, prepare, the device build, the kept-set hand-off, final.kmers, the BDZ perfect
+    hash + .dat and the recall pass with its reports -- every output file written.  Phases from the
+    CLI's own "phases:" stderr line; value = windows built / wall time of the whole process."""
+    import shutil
+    import subprocess
+    exe = os.path.join(ROOT, "bin", "kmers-build-signatures")
+    d = os.path.join(cli_dir, "in")
+    outd = os.path.join(cli_dir, "kd")
+    cmd = [exe, "-D", os.path.join(d, "Annotations"), "-F", os.path.join(d, "Seqs"), "--kmer-data-dir", outd,
+           "--final-kmers", "final.kmers", "--perfect-hash", "kmer_data.mph", "--perfect-hash-data", "kmer_data.dat"]
+    t = time.perf_counter()
+    p = subprocess.run(cmd, capture_output=True, timeout=600)
+    wall = time.perf_counter() - t
+    res = {"metric": "kmers-build-signatures wall time, FASTA directories -> every output file", "seconds": wall,
+           "rc": p.returncode, "config": {"workload": f"C2 CLI: {a.cli_seqs:,} proteins in "
+                                                      f"{(a.cli_seqs + PER_FILE - 1) // PER_FILE} FASTA files, 1 GPU"}}
+    err = p.stderr.decode(errors="replace")
+    if p.returncode != 0:
+        res["stderr_tail"] = err[-2000:]
+        return res
+    ph = [ln for ln in err.splitlines() if ln.startswith("phases: ")]
+    if ph:
+        f = ph[0].split()[1:]
+        res["phases_s"] = {f[i]: float(f[i + 1]) for i in range(0, len(f) - 1, 2)}
+    out = p.stdout.decode()
+    kept = [ln for ln in out.splitlines() if ln.startswith("Kept ")]
+    res["kept"] = int(kept[0].split()[1]) if kept else None
+    res["output_bytes"] = {f: os.path.getsize(os.path.join(outd, f)) for f in ("final.kmers", "kmer_data.mph",
+                                                                                "kmer_data.dat", "function.index")
+                           if os.path.exists(os.path.join(outd, f))}
+    shutil.rmtree(cli_dir, ignore_errors=True)
+    return res
 
 
 def _pcie_inclusive(m, prep_s, create_s=None):

@@ -318,9 +318,10 @@ def read_lines(path):
 
 
 def front(definition_dirs, fasta_dirs, keep_dirs=(), good_functions=(), good_roles=(), deleted=(), ignored=(),
-          min_reps=3):
+          min_reps=3, records=None):
     """Run the reference front end.  Returns dict(fm, files=[(path, records)], build=(residues, off, len,
-    func, seq_id), n_kept_functions)."""
+    func, seq_id), n_kept_functions).  records: {path: [(id, def, seq)]} to use instead of parsing
+    those files (callers that know what FastaParser yields for them, e.g. generated files)."""
     fm = FunctionMapRef(good_functions, good_roles)
     for d in definition_dirs:
         for p in list_files(d):
@@ -329,8 +330,11 @@ def front(definition_dirs, fasta_dirs, keep_dirs=(), good_functions=(), good_rol
     paths = [p for d in fasta_dirs for p in list_files(d)] + [p for d in keep_dirs for p in list_files(d)]
     files = []
     for p in paths:
-        with open(p, "rb") as fh:
-            recs = parse_fasta(fh.read())
+        if records is not None and p in records:
+            recs = records[p]
+        else:
+            with open(p, "rb") as fh:
+                recs = parse_fasta(fh.read())
         files.append((p, recs))
         fm.load_fasta_records(os.path.basename(p).encode(), recs, deleted)
     nk = fm.process_kept_functions(min_reps, set(ignored))

@@ -265,3 +265,67 @@ def functions(n_families: int, seed: int = SEED) -> list:
     """The function list (FunctionIndex order) of a proteome of n_families families."""
     fi = function_index_of(make_families(n_families, seed).names)
     return sorted(fi, key=fi.get)
+
+
+def fasta_bytes(ids, residues: np.ndarray, lens: np.ndarray, width: int = 60) -> bytes:
+    """FASTA text of records (id, residues[off:off+len]) wrapped at `width` columns, as
+    write_dirs writes it, built without a per-line Python loop."""
+    out = []
+    off = 0
+    for pid, n in zip(ids, lens.tolist()):
+        seq = residues[off:off + n]
+        off += n
+        out.append(b">" + pid + b"\n")
+        if n:
+            rows = (n + width - 1) // width
+            pad = np.full(rows * (width + 1), 10, np.uint8)
+            view = pad.reshape(rows, width + 1)
+            full = n // width
+            if full:
+                view[:full, :width] = seq[:full * width].reshape(full, width)
+            rem = n - full * width
+            if rem:
+                view[full, :rem] = seq[full * width:]
+                out.append(pad[:full * (width + 1) + rem + 1].tobytes())
+            else:
+                out.append(pad.tobytes())
+    return b"".join(out)
+
+
+def _write_file(args):
+    """One genome file of write_dirs: Seqs/<g>.1 and Annotations/<g>.1 (identical bytes)."""
+    root, n_seqs, n_families, per_file, f, seed, extras, genome_base = args
+    key = (n_families, seed)
+    if key not in _WORKER_FAM:
+        fam = make_families(n_families, seed)
+        fi = function_index_of(fam.names)
+        _WORKER_FAM[key] = (fam, np.array([fi[n] for n in fam.names], dtype=np.uint16))
+    fam, _ = _WORKER_FAM[key]
+    n = min(per_file, n_seqs - f * per_file)
+    res, lens, _, labels = _mutate_file(fam, n, f, seed, extras)
+    g = f"{genome_base + f}.1"
+    ids = [f"fig|{g}.peg.{k + 1}".encode() for k in range(n)]
+    with open(os.path.join(root, "Seqs", g), "wb") as fa:
+        fa.write(fasta_bytes(ids, res, lens.astype(np.int64)))
+    with open(os.path.join(root, "Annotations", g), "wb") as an:
+        an.write(b"".join(b"%s\t%s\n" % (pid, fam.names[lab].encode()) for pid, lab in zip(ids, labels)))
+    return g
+
+
+def write_dirs_parallel(root: str, n_seqs: int, n_families: int, per_file: int, seed: int = SEED,
+                        extras: bool = False, genome_base: int = 100000, workers: int = 8) -> dict:
+    """write_dirs with the files generated and written by a spawned process pool (the same bytes);
+    no in-memory proteome is returned (iter_file_inputs regenerates the build arrays)."""
+    seqs_dir = os.path.join(root, "Seqs")
+    ann_dir = os.path.join(root, "Annotations")
+    os.makedirs(seqs_dir, exist_ok=True)
+    os.makedirs(ann_dir, exist_ok=True)
+    n_files = (n_seqs + per_file - 1) // per_file
+    jobs = [(root, n_seqs, n_families, per_file, f, seed, extras, genome_base) for f in range(n_files)]
+    if workers <= 1:
+        files = [_write_file(j) for j in jobs]
+    else:
+        import multiprocessing as mp
+        with mp.get_context("spawn").Pool(workers) as pool:
+            files = list(pool.imap(_write_file, jobs, chunksize=2))
+    return {"seqs_dir": seqs_dir, "ann_dir": ann_dir, "files": files}

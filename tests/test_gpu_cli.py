@@ -161,29 +161,52 @@ def test_build_signatures_c1(c1_build):
     assert n_rep == len(ref["files"])
 
 
-def test_build_signatures_250k(tmp_path, gpu):
-    """kmers-build-signatures end to end at 250,000 proteins (63 genome files of 4,000, 4,000
-    families; VERDICT r03: the drop-in CLI beyond C1 size): FASTA dirs -> function.index,
-    final.kmers, distinct_functions, kmer_data.mph / .dat, recall.report.d/<file> (every 7th file's
-    report byte-compared: the restatement is per-record Python) and the stdout statistics, against
-    the reference restatement (oracle/front_ref.py + the oracle build and recall on all host cores).
-    The run's wall time is printed (-s) for DESIGN."""
+def _generated_records(info, n_seqs, n_families, per_file, threads):
+    """{path: [(id, b"", seq)]}: what FastaParser yields for write_dirs' files, from the generator's
+    arrays (the parser itself is pinned against the reference by tests/golden/ref_fasta.npz): a
+    trailing '*' alone in column 1 of a new 60-column line is dropped (fasta_parser.h:122, a bad
+    id-or-data character)."""
+    from signature_kmers_amd import synth
+    recs = {}
+    for f, (res, off, ln, _, _) in enumerate(synth.iter_file_inputs(n_seqs, n_families, per_file, workers=threads)):
+        g = info["files"][f]
+        rows = []
+        for k in range(len(ln)):
+            a, n = int(off[k]), int(ln[k])
+            seq = res[a:a + n].tobytes()
+            if n % 60 == 1 and seq.endswith(b"*"):
+                seq = seq[:-1]
+            rows.append((b"fig|%s.peg.%d" % (g.encode(), k + 1), b"", seq))
+        recs[os.path.join(info["seqs_dir"], g)] = rows
+    return recs
+
+
+def test_build_signatures_c2(tmp_path, gpu):
+    """kmers-build-signatures end to end at BASELINE configs[1] size -- 1,000,000 proteins in 250
+    genome files of 4,000, 4,000 families: FASTA dirs -> function.index, final.kmers,
+    distinct_functions, kmer_data.mph / .dat, recall.report.d/<file> (every 25th file's report
+    byte-compared: the restatement is per-record Python) and the stdout statistics, against the
+    reference restatement (oracle/front_ref.py + the oracle build and recall on all host cores).
+    The run's phases (the CLI's "phases:" line) are printed (-s) for DESIGN."""
     import time
     from signature_kmers_amd import synth
     from test_gpu_scale import _threads
-    info = synth.write_dirs(str(tmp_path / "in"), 250_000, 4000, per_file=4000)
+    n, fam = 1_000_000, 4000
+    info = synth.write_dirs_parallel(str(tmp_path / "in"), n, fam, per_file=4000, workers=_threads())
     out = str(tmp_path / "kd")
     t = time.time()
     stdout, stderr = _run([os.path.join(BIN, "kmers-build-signatures"), "-D", info["ann_dir"], "-F", info["seqs_dir"],
                            "--kmer-data-dir", out, "--final-kmers", "final.kmers", "--perfect-hash", "kmer_data.mph",
                            "--perfect-hash-data", "kmer_data.dat"])
     wall = time.time() - t
-    print(f"\nkmers-build-signatures 250K proteins: {wall:.1f} s wall\n{stderr[-600:]}", flush=True)
-    ref = fr.front([info["ann_dir"]], [info["seqs_dir"]])
+    phases = [ln for ln in stderr.splitlines() if ln.startswith("phases: ")]
+    print(f"\nkmers-build-signatures C2 (1M proteins): {wall:.1f} s wall\n{phases}", flush=True)
+    assert len(phases) == 1
+    ref = fr.front([info["ann_dir"]], [info["seqs_dir"]], records=_generated_records(info, n, fam, 4000, _threads()))
     print("reference front end done", flush=True)
-    o = _check_build(out, stdout, ref, threads=_threads(), report_stride=7)  # 9 of the 63 reports
-    assert len(o["keys"]) > 10_000_000 and len(ref["files"]) == 63
-    assert len(os.listdir(os.path.join(out, "recall.report.d"))) == 63
+    o = _check_build(out, stdout, ref, threads=_threads(), report_stride=25)  # 10 of the 250 reports
+    assert len(o["keys"]) > 100_000_000 and len(ref["files"]) == 250
+    assert len(os.listdir(os.path.join(out, "recall.report.d"))) == 250
 
 
 def _query_dir(tmp, seed=5):
