@@ -79,6 +79,9 @@ def parse():
     ap.add_argument("--cli-seqs", type=int, default=1_000_000,
                     help="cli_build leg: bin/kmers-build-signatures end to end on FASTA directories of this many "
                          "proteins (BASELINE configs[1]); 0 = off; N=1 only")
+    ap.add_argument("--cli-queries", type=int, default=10_000_000,
+                    help="cli_call leg: bin/kmers-call-functions end to end on this many query proteins (FASTA) "
+                         "against the cli_build leg's DB (BASELINE configs[3]); 0 = off")
     ap.add_argument("--finish", type=int, default=1,
                     help="time skm_build_finish (the kept-set hand-off to host arrays) on the headline build; N=1")
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
@@ -225,6 +228,13 @@ def main():
         synth.write_dirs_parallel(os.path.join(cli_dir, "in"), a.cli_seqs, a.families, per_file=PER_FILE,
                                   workers=workers)
         log(f"cli_build input: {a.cli_seqs:,} proteins as FASTA in {time.time() - t:.1f} s")
+        if a.cli_queries > 0:  # the query genome files after the training set (the annotate leg's proteins)
+            t = time.time()
+            qf0 = (a.cli_seqs + PER_FILE - 1) // PER_FILE
+            nqf = (a.cli_queries + PER_FILE - 1) // PER_FILE
+            synth.write_dirs_parallel(os.path.join(cli_dir, "q"), (qf0 + nqf) * PER_FILE, a.families, per_file=PER_FILE,
+                                      workers=workers, first_file=qf0, n_files=nqf)
+            log(f"cli_call input: {a.cli_queries:,} query proteins as FASTA in {time.time() - t:.1f} s")
     if a.cache_only:
         log("inputs cached")
         return
@@ -355,6 +365,11 @@ def main():
     if cli_dir is not None:
         log("cli_build leg")
         out["cli_build"] = _cli_build_leg(cli_dir, a)
+        if a.cli_queries > 0 and out["cli_build"].get("rc") == 0:
+            log("cli_call leg")
+            out["cli_call"] = _cli_call_leg(cli_dir, a)
+        import shutil
+        shutil.rmtree(cli_dir, ignore_errors=True)
     if matrix_in is not None:
         log("matrix leg")
         mx = _matrix_leg(skm, matrix_in, a, device, cores, rank, world, dist)
@@ -557,7 +572,37 @@ def _cli_build_leg(cli_dir, a):
     res["output_bytes"] = {f: os.path.getsize(os.path.join(outd, f)) for f in ("final.kmers", "kmer_data.mph",
                                                                                 "kmer_data.dat", "function.index")
                            if os.path.exists(os.path.join(outd, f))}
-    shutil.rmtree(cli_dir, ignore_errors=True)
+    shutil.rmtree(os.path.join(cli_dir, "in"), ignore_errors=True)
+    return res
+
+
+def _cli_call_leg(cli_dir, a):
+    """bin/kmers-call-functions end to end (kmers-call-functions.cc:84-196) over a.cli_queries query
+    proteins in FASTA files against the cli_build leg's kmer_data.mph / .dat (BASELINE configs[3]
+    at the default 10M): parse, the device lookup + HitSet calls (skm_annotate, incl. packing,
+    upload and the calls' download), host find_best_call on the host pool, the calls file written.
+    Phases from the CLI's "phases:" stderr line."""
+    import glob
+    import subprocess
+    exe = os.path.join(ROOT, "bin", "kmers-call-functions")
+    files = sorted(glob.glob(os.path.join(cli_dir, "q", "Seqs", "*")))
+    outf = os.path.join(cli_dir, "calls.txt")
+    cmd = [exe, os.path.join(cli_dir, "kd")] + files + ["-o", outf]
+    t = time.perf_counter()
+    p = subprocess.run(cmd, capture_output=True, timeout=900)
+    wall = time.perf_counter() - t
+    res = {"metric": "kmers-call-functions wall time, FASTA files -> calls file", "seconds": wall,
+           "rc": p.returncode, "config": {"workload": f"C4 CLI: {a.cli_queries:,} query proteins in {len(files)} "
+                                                      f"FASTA files vs the C2 CLI's DB, 1 GPU"}}
+    err = p.stderr.decode(errors="replace")
+    if p.returncode != 0:
+        res["stderr_tail"] = err[-2000:]
+        return res
+    ph = [ln for ln in err.splitlines() if ln.startswith("phases: ")]
+    if ph:
+        f = ph[0].split()[1:]
+        res["phases_s"] = {f[i]: float(f[i + 1]) for i in range(0, len(f) - 1, 2)}
+    res["calls_bytes"] = os.path.getsize(outf) if os.path.exists(outf) else None
     return res
 
 

@@ -156,7 +156,8 @@ int skm_build_kernel_timings(skm_build* b, char* names, size_t names_cap, float*
  * totals over the passes of the run; the last skm_build_finish / _finish_slice's kept-set
  * hand-off (device radix sort in key-range chunks, streamed through pinned staging): [33] its
  * host microseconds, [34] of them waiting for the device / PCIe, [35] copying pieces out on the
- * host pool, [36] chunks; returns entries written. */
+ * host pool, [36] chunks, and its device microseconds summed over the chunks: [37] selection,
+ * [38] radix sort, [39] gather, [40] the D2H pieces; returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Host transport: the rank collectives of a multi-process build run by the caller on host
  * buffers, for ranks joined by a channel other than RCCL (the tests drive it with

@@ -47,7 +47,9 @@ void set_boost_math_modes(int mean_mode, int mad_mode) {
 
 int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std::vector<std::string>& function_index,
                bool ignore_hypo, int n_threads, std::vector<std::vector<SeqCall>>& out, std::string& err,
-               double* device_ms, uint64_t max_batch_residues) {
+               double* device_ms, uint64_t max_batch_residues, double* host_ms) {
+    const auto t_begin = std::chrono::steady_clock::now();
+    double dev_ms = 0;
     auto hit = std::find(function_index.begin(), function_index.end(), "hypothetical protein");
     if (hit == function_index.end()) {  // process_aa_seq exits here (call_functions.tcc:269-274)
         err = "Cannot find hypothetical protein index";
@@ -65,7 +67,6 @@ int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std
 
     out.assign(files.size(), std::vector<SeqCall>());
     for (size_t f = 0; f < files.size(); ++f) out[f].resize(files[f]->size());
-    if (device_ms) *device_ms = 0;
 
     size_t f0 = 0;
     while (f0 < files.size()) {
@@ -103,8 +104,7 @@ int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std
         skm_calls calls{};
         auto t0 = std::chrono::steady_clock::now();
         int rc = skm_annotate(db, rp, off.data(), len.data(), off.size(), &o, &calls);
-        if (device_ms)
-            *device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        dev_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (rc) {
             err = skm_last_error();
             return rc;
@@ -150,6 +150,9 @@ int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std
         }
         f0 = f1;
     }
+    if (device_ms) *device_ms = dev_ms;
+    if (host_ms)
+        *host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count() - dev_ms;
     return SKM_OK;
 }
 

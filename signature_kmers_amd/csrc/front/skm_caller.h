@@ -29,8 +29,10 @@ void set_boost_math_modes(int mean_mode, int mad_mode);
 
 // Query every sequence of every file (in order) against db.  out[f][r] is the call for record r
 // of file f.  Files are batched so one device batch holds <= max_batch_residues residues.
+// device_ms: wall ms in skm_annotate (packing, upload, device pipeline, calls download);
+// host_ms: wall ms of the rest (batch assembly, find_best_call on n_threads host threads).
 int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std::vector<std::string>& function_index,
                bool ignore_hypo, int n_threads, std::vector<std::vector<SeqCall>>& out, std::string& err,
-               double* device_ms = nullptr, uint64_t max_batch_residues = 2000000000ull);
+               double* device_ms = nullptr, uint64_t max_batch_residues = 2000000000ull, double* host_ms = nullptr);
 
 }  // namespace skmf

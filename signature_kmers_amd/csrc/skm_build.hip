@@ -7275,15 +7275,17 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
     auto us = [](double sec) { return (uint64_t)(sec * 1e6); };
-    const uint64_t v[37] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+    const uint64_t v[41] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
                             b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total,
                             b->giant_jobs, b->giant_max, b->n_redo, b->tot_cap, b->split_cap, b->long_cap,
                             b->long_jobs_cap, b->demand[0], b->demand[1], b->demand[2], b->demand[3],
                             b->long_samples, b->routed, us(b->add_s), us(b->prep_upload_s), us(b->prep_plan_s),
                             us(b->prep_rest_s), b->pass_bits ? (1ull << b->pass_bits) / b->emit_g : 0ull, us(b->add_pack_s),
                             us(b->add_wait_s), us(b->handoff.total_s), us(b->handoff.wait_s),
-                            us(b->handoff.copy_s), b->handoff.chunks};
-    int n = std::min(cap, 37);
+                            us(b->handoff.copy_s), b->handoff.chunks, (uint64_t)(1e3 * b->handoff.select_ms),
+                            (uint64_t)(1e3 * b->handoff.sort_ms), (uint64_t)(1e3 * b->handoff.gather_ms),
+                            (uint64_t)(1e3 * b->handoff.d2h_ms)};
+    int n = std::min(cap, 41);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }

@@ -16,6 +16,8 @@ struct HandoffStats {
     double wait_s = 0;   // host waiting for a piece's D2H (device sort + PCIe not yet done)
     double copy_s = 0;   // host pool copying pieces from pinned staging into the output arrays
     double total_s = 0;
+    // device time (ms) summed over the chunks: selection, radix sort, gather; and the D2H pieces
+    float select_ms = 0, sort_ms = 0, gather_ms = 0, d2h_ms = 0;
 };
 
 // The n kept k-mers of a device arena (raw little-endian keys, 10-byte records; keys distinct) into

@@ -60,31 +60,56 @@ __global__ __launch_bounds__(OUT_THREADS) void k_out_hist(const uint64_t* __rest
         if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
-// the (sort code, arena index) pairs of the keys whose bin lies in [lo, hi); one atomic per wave
+// the (sort code, arena index) pairs of the keys whose bin lies in [lo, hi).  Tiles of 16
+// elements per thread (coalesced, strided by the block); the block's selected count is scanned
+// over its waves and reserved with ONE atomic per tile -- a chunk selects ~1/22 of the arena's
+// keys, spread over it in hash order, so a per-wave reservation put ~40 M atomics on one address
+// per chunk at C3 (0.5 s per chunk)
+constexpr int SEL_ITEMS = 16;
 __global__ __launch_bounds__(OUT_THREADS) void k_out_select(const uint64_t* __restrict__ keys, uint64_t n, uint32_t lo,
                                                             uint32_t hi, unsigned long long* __restrict__ cur,
                                                             uint64_t* __restrict__ code, uint32_t* __restrict__ idx) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t stride = (uint64_t)gridDim.x * OUT_THREADS;
-    for (uint64_t base = (uint64_t)blockIdx.x * OUT_THREADS; base < n; base += stride) {
-        const uint64_t i = base + threadIdx.x;
-        uint64_t c = 0;
-        bool sel = false;
-        if (i < n) {
-            c = sort_code(keys[i]);
-            const uint32_t bin = (uint32_t)(c >> OUT_BIN_SHIFT);
-            sel = bin >= lo && bin < hi;
+    constexpr int NW = OUT_THREADS / 64;
+    __shared__ uint32_t wsum[NW];
+    __shared__ unsigned long long base_s;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint64_t TILE = (uint64_t)OUT_THREADS * SEL_ITEMS;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * TILE; t0 < n; t0 += (uint64_t)gridDim.x * TILE) {
+        uint64_t c[SEL_ITEMS];
+        uint32_t mask = 0;
+#pragma unroll
+        for (int j = 0; j < SEL_ITEMS; ++j) {
+            const uint64_t i = t0 + (uint64_t)j * OUT_THREADS + tid;
+            c[j] = i < n ? sort_code(keys[i]) : 0;
+            const uint32_t bin = (uint32_t)(c[j] >> OUT_BIN_SHIFT);
+            mask |= (i < n && bin >= lo && bin < hi) ? (1u << j) : 0u;
         }
-        const uint64_t m = __ballot(sel);
-        if (!m) continue;
-        uint64_t at = 0;
-        if (lane == 0) at = atomicAdd(cur, (unsigned long long)__popcll(m));
-        at = __shfl(at, 0);
-        if (sel) {
-            const uint64_t o = at + (uint64_t)__popcll(m & (lane ? (~0ull >> (64 - lane)) : 0ull));
-            code[o] = c;
-            idx[o] = (uint32_t)i;
+        // exclusive prefix of the per-thread counts within the wave (shuffle scan), then over waves
+        const uint32_t cnt = (uint32_t)__popc(mask);
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t v = __shfl_up(incl, d);
+            if (lane >= (uint32_t)d) incl += v;
         }
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t tot = 0;
+            for (int w = 0; w < NW; ++w) tot += wsum[w];
+            base_s = tot ? atomicAdd(cur, (unsigned long long)tot) : 0ull;
+        }
+        __syncthreads();
+        uint64_t o = base_s + (incl - cnt);
+        for (uint32_t w = 0; w < wave; ++w) o += wsum[w];
+#pragma unroll
+        for (int j = 0; j < SEL_ITEMS; ++j)
+            if ((mask >> j) & 1u) {
+                code[o] = c[j];
+                idx[o] = (uint32_t)(t0 + (uint64_t)j * OUT_THREADS + tid);
+                ++o;
+            }
+        __syncthreads();  // wsum / base_s are rewritten by the next tile
     }
 }
 
@@ -181,6 +206,16 @@ void kept_handoff(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint
     uint8_t* pin[2] = {nullptr, nullptr};
     hipStream_t cs = nullptr;
     hipEvent_t ev_g[2] = {}, ev_d[2] = {}, ev_p[2] = {};
+    // timing: per chunk (start, selected, sorted, gathered) on st; per piece (start, end) on cs
+    std::vector<hipEvent_t> tev;
+    auto tmark = [&](hipStream_t s_) -> size_t {
+        hipEvent_t e;
+        SKM_HIP(hipEventCreate(&e));
+        tev.push_back(e);
+        SKM_HIP(hipEventRecord(e, s_));
+        return tev.size() - 1;
+    };
+    std::vector<size_t> cmark, pmark;
     auto cleanup = [&]() {
         if (cs) (void)hipStreamSynchronize(cs);
         (void)hipStreamSynchronize(st);
@@ -189,6 +224,7 @@ void kept_handoff(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint
         for (auto* set : {ev_g, ev_d, ev_p})
             for (int k = 0; k < 2; ++k)
                 if (set[k]) (void)hipEventDestroy(set[k]);
+        for (auto e : tev) (void)hipEventDestroy(e);
         if (cs) (void)hipStreamDestroy(cs);
     };
     try {
@@ -205,17 +241,21 @@ void kept_handoff(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint
             const Chunk& C = chunks[c];
             const int k = (int)(c & 1);
             if (c >= 2) SKM_HIP(hipStreamWaitEvent(st, ev_d[k], 0));  // chunk c-2 has left gk/gd[k]
+            cmark.push_back(tmark(st));
             SKM_HIP(hipMemsetAsync(d_cur.p, 0, 8, st));
             hipLaunchKernelGGL(k_out_select, dim3(grid), dim3(OUT_THREADS), 0, st, dkeys, n, C.lo, C.hi,
                                d_cur.as<unsigned long long>(), kin.as<uint64_t>(), vin.as<uint32_t>());
             SKM_HIP(hipGetLastError());
+            tmark(st);
             size_t tb = tmp.bytes;
             SKM_HIP(rocprim::radix_sort_pairs(tmp.p, tb, kin.as<uint64_t>(), kout.as<uint64_t>(), vin.as<uint32_t>(),
                                               vout.as<uint32_t>(), (size_t)C.n, 0, KEY_BITS, st));
+            tmark(st);
             const uint32_t gg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(C.n, OUT_THREADS), 4096));
             hipLaunchKernelGGL(k_out_gather, dim3(gg), dim3(OUT_THREADS), 0, st, dkeys, ddata, vout.as<uint32_t>(), C.n,
                                gk[k].as<uint64_t>(), gd[k].as<skm_stored_kmer_data>());
             SKM_HIP(hipGetLastError());
+            tmark(st);
             SKM_HIP(hipEventRecord(ev_g[k], st));
         };
         // the pieces: each chunk's keys, then its records, in 64 MB pieces
@@ -247,7 +287,9 @@ void kept_handoff(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint
                 while (enq <= P.chunk + 1 && enq < chunks.size()) enqueue_chunk(enq++);  // keep the sorter one ahead
                 SKM_HIP(hipStreamWaitEvent(cs, ev_g[P.chunk & 1], 0));
             }
+            pmark.push_back(tmark(cs));
             SKM_HIP(hipMemcpyAsync(pin[p & 1], P.src, P.bytes, hipMemcpyDeviceToHost, cs));
+            tmark(cs);
             SKM_HIP(hipEventRecord(ev_p[p & 1], cs));
             if (P.last) SKM_HIP(hipEventRecord(ev_d[P.chunk & 1], cs));
         };
@@ -272,6 +314,21 @@ void kept_handoff(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint
                 for (int q = 0; q < parts; ++q) cp(q);
             S.copy_s += std::chrono::duration<double>(now() - tc).count();
             S.bytes += P.bytes;
+        }
+        SKM_HIP(hipStreamSynchronize(cs));
+        SKM_HIP(hipStreamSynchronize(st));
+        float ms = 0;
+        for (size_t m : cmark) {
+            SKM_HIP(hipEventElapsedTime(&ms, tev[m], tev[m + 1]));
+            S.select_ms += ms;
+            SKM_HIP(hipEventElapsedTime(&ms, tev[m + 1], tev[m + 2]));
+            S.sort_ms += ms;
+            SKM_HIP(hipEventElapsedTime(&ms, tev[m + 2], tev[m + 3]));
+            S.gather_ms += ms;
+        }
+        for (size_t m : pmark) {
+            SKM_HIP(hipEventElapsedTime(&ms, tev[m], tev[m + 1]));
+            S.d2h_ms += ms;
         }
     } catch (...) {
         cleanup();

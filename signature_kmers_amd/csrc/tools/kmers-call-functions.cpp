@@ -18,6 +18,7 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <chrono>
 #include <thread>
 
 #include "skm.h"
@@ -123,17 +124,24 @@ int main(int argc, char** argv) {
     const std::string mph = db_base + ".mph", dat = db_base + ".dat";
     if (!file_exists(mph)) die("Database \"" + db_base + "\" does not exist");
     skm_db* db = nullptr;
+    const auto t_open0 = std::chrono::steady_clock::now();
     if (skm_db_open(&db, mph.c_str(), dat.c_str(), device)) die(skm_last_error());
+    const double t_open = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_open0).count();
     std::vector<std::string> fidx;
     if (!read_function_index(path_join(data_dir, "function.index"), fidx, err)) die(err);
     const bool ignore_hypo = op.has("ignore-hypo");
 
+    auto now_s = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double t0 = now_s();
     std::vector<FastaFile> files;
     if (!parse_fasta_files(inputs, files, n_threads, err)) die(err);
+    const double t_parse = now_s() - t0;
     std::vector<const FastaFile*> fptr;
     for (auto& f : files) fptr.push_back(&f);
     std::vector<std::vector<SeqCall>> calls;
-    if (call_files(db, fptr, fidx, ignore_hypo, n_threads, calls, err)) die(err);
+    double dev_ms = 0, host_ms = 0;
+    if (call_files(db, fptr, fidx, ignore_hypo, n_threads, calls, err, &dev_ms, 2000000000ull, &host_ms)) die(err);
+    t0 = now_s();
 
     std::ofstream ofs;
     std::ostream* out = &std::cout;
@@ -163,6 +171,12 @@ int main(int argc, char** argv) {
         *out << buf;
     }
     out->flush();
+    const double t_write = now_s() - t0;
     skm_db_close(db);
+    uint64_t nrec = 0;
+    for (auto& f : files) nrec += f.size();
+    // one machine-readable line of the phases (bench.py's cli_call leg)
+    std::cerr << "phases: sequences " << nrec << " db_open " << t_open << " parse " << t_parse << " device " << dev_ms / 1e3 << " best_call "
+              << host_ms / 1e3 << " write " << t_write << "\n";
     return 0;
 }

@@ -313,15 +313,18 @@ def _write_file(args):
 
 
 def write_dirs_parallel(root: str, n_seqs: int, n_families: int, per_file: int, seed: int = SEED,
-                        extras: bool = False, genome_base: int = 100000, workers: int = 8) -> dict:
+                        extras: bool = False, genome_base: int = 100000, workers: int = 8, first_file: int = 0,
+                        n_files: int | None = None) -> dict:
     """write_dirs with the files generated and written by a spawned process pool (the same bytes);
-    no in-memory proteome is returned (iter_file_inputs regenerates the build arrays)."""
+    files [first_file, first_file + n_files) of an n_seqs proteome; no in-memory proteome is
+    returned (iter_file_inputs regenerates the build arrays)."""
     seqs_dir = os.path.join(root, "Seqs")
     ann_dir = os.path.join(root, "Annotations")
     os.makedirs(seqs_dir, exist_ok=True)
     os.makedirs(ann_dir, exist_ok=True)
-    n_files = (n_seqs + per_file - 1) // per_file
-    jobs = [(root, n_seqs, n_families, per_file, f, seed, extras, genome_base) for f in range(n_files)]
+    total = (n_seqs + per_file - 1) // per_file
+    last = total if n_files is None else min(total, first_file + n_files)
+    jobs = [(root, n_seqs, n_families, per_file, f, seed, extras, genome_base) for f in range(first_file, last)]
     if workers <= 1:
         files = [_write_file(j) for j in jobs]
     else:

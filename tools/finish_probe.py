@@ -40,7 +40,9 @@ def main():
         c = b.counters()
         ok = len(k.keys) == c["kept"] and bool(np.all(k.keys[1:] > k.keys[:-1]))
         res[f"finish_s_{rep}"] = dt
-        res[f"handoff_{rep}"] = {x: c[x] for x in ("finish_us", "finish_wait_us", "finish_copy_us", "finish_chunks")}
+        res[f"handoff_{rep}"] = {x: c[x] for x in ("finish_us", "finish_wait_us", "finish_copy_us", "finish_chunks",
+                                                    "finish_select_dev_us", "finish_sort_dev_us", "finish_gather_dev_us",
+                                                    "finish_d2h_dev_us")}
         bench.log(f"finish {dt:.3f} s ({res[f'handoff_{rep}']}), sorted+complete: {ok}")
         assert ok
         del k
