@@ -200,7 +200,8 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   "heavy_lsd" (1: every heavy k-mer through round 3's Boyer-Moore + LSD-sort path instead of
  *   the one-read bucketed path; it is the fallback for > 4096 functions or crowded buckets),
  *   "giant_class" (heavy chains of >= 2^class samples start right after the heavy kernel on
- *   their own streams; 0 = off; default: 14 with one pass, off with key-range passes),
+ *   their own streams; 0 = off; default: 14 with one pass or world_size > 1, off with key-range
+ *   passes on one GPU),
  *   "giant_passes", "prefetch" (the next pass group's positions, k_pass_emit, during the group-by of the group's
  *   last pass, 1),
  *   "overflow_grid" / "split_grid" / "chain_grid" (persistent-grid sizes), "stream_priority"

@@ -6045,8 +6045,14 @@ void pass_peer_counts(const Ranks& bs) {
 // Giant chains (k_heavy's chains of >= 2^class samples start on a chain stream right after it):
 // the option, or by default 14 with one pass (C2: -0.5 ms, the longest P^2 chain is that path's
 // end) and off with key-range passes (C3: +60..80 ms, the FP64 chain waves slow the passes).
+// Giant chains (>= 2^class samples) start on their own streams right after k_heavy instead of
+// waiting for the stash batches.  Default on with one pass, and at world > 1 (verdict r04 #4): the
+// owner split leaves each rank few passes (two at 8 GPUs), routing puts the heaviest k-mers into
+// the first, and their stashed chains would only start after that pass's group-by (~0.08 s of a
+// ~0.2 s step) -- the multi-GPU step's floor.  Off on one GPU with key-range passes, where the
+// stash batches overlap the later passes (measured round 3).
 int giant_class(const skm_build* b) {
-    return b->tune.giant_class >= 0 ? b->tune.giant_class : (b->pass_bits == 0 ? 14 : 0);
+    return b->tune.giant_class >= 0 ? b->tune.giant_class : (b->pass_bits == 0 || b->world > 1 ? 14 : 0);
 }
 
 constexpr uint32_t JOB_NWG = 256;      // k_job_count / k_job_scatter workgroups (one chunk each)
