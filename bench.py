@@ -221,7 +221,7 @@ def main():
         matrix_in = (gen(synth, n_train, fam, 0, tf, workers, a.cache_dir),
                      gen(synth, (tf + nfq) * PER_FILE, fam, tf, nfq, workers, a.cache_dir), synth.functions(fam))
     cli_dir = None
-    if world == 1 and a.cli_seqs > 0:  # FASTA directories for the cli_build leg (spawned writers)
+    if world == 1 and a.cli_seqs > 0 and not a.cache_only:  # FASTA directories for the CLI legs (spawned writers)
         import tempfile
         cli_dir = tempfile.mkdtemp(prefix="skm_cli_", dir="/tmp")
         t = time.time()

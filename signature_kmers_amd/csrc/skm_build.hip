@@ -2635,14 +2635,15 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     __syncthreads();
     SKM_STAMP(3);
     // 3. singletons resolved in place; multi-occurrence groups get a slice of `order` (each thread
-    //    owns LPER consecutive elements: one workgroup scan for the whole batch)
+    //    owns LPER elements strided by the workgroup -- consecutive lanes touch consecutive LDS
+    //    words; a thread's LPER consecutive elements put lanes 8 apart on one bank -- and one
+    //    workgroup scan orders the groups by (thread, element): any fixed order will do)
     uint32_t M = 0, G = 0;
     {
-        const uint32_t j0 = tid * LPER;
         uint32_t ev[LPER], loc = 0;
 #pragma unroll
         for (uint32_t u = 0; u < LPER; ++u) {
-            const uint32_t j = j0 + u;
+            const uint32_t j = tid + u * BPK_THREADS;
             ev[u] = j < n ? L.tab[L.slot[j]] : 0u;
             const uint32_t cnt = ev[u] & 0xFFFFu;
             loc += (cnt > 1 && (ev[u] >> 16) == j) ? ((cnt << 13) | 1u) : 0u;
@@ -2652,7 +2653,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         uint32_t ms[LPER];  // the singletons' sequences, flagged after the loop
 #pragma unroll
         for (uint32_t u = 0; u < LPER; ++u) {
-            const uint32_t j = j0 + u;
+            const uint32_t j = tid + u * BPK_THREADS;
             const uint32_t cnt = ev[u] & 0xFFFFu;
             ms[u] = 0xFFFFFFFFu;
             if (j < n && cnt > 1 && (ev[u] >> 16) == j) {
@@ -2787,11 +2788,10 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     //    a job's kept position) so consecutive lanes write consecutive records
     constexpr uint32_t EMIT_PER = CAP / BPK_THREADS;
     unsigned long long* s_base = reinterpret_cast<unsigned long long*>(L.wave + 36);
-    const uint32_t j0 = tid * EMIT_PER;
-    uint32_t cnt = 0;
+    uint32_t cnt = 0;  // (elements strided by the workgroup, as in the classify phase)
 #pragma unroll
     for (uint32_t u = 0; u < EMIT_PER; ++u) {
-        const uint32_t j = j0 + u;
+        const uint32_t j = tid + u * BPK_THREADS;
         const uint32_t jb = j < n ? jobinfo[j] : 0u;
         cnt += ((jb & JOB_KEPT) ? 1u : 0u) | ((jb & JOB_COUNT_MASK) ? 0x10000u : 0u);
     }
@@ -2805,12 +2805,13 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         uint32_t pk = pos & 0xFFFFu, pj = pos >> 16;
 #pragma unroll
         for (uint32_t u = 0; u < EMIT_PER; ++u) {
-            const uint32_t jb = j0 + u < n ? jobinfo[j0 + u] : 0u;
+            const uint32_t j = tid + u * BPK_THREADS;
+            const uint32_t jb = j < n ? jobinfo[j] : 0u;
             if (!(jb & JOB_KEPT)) continue;
-            L.slot[pk] = (uint16_t)(j0 + u);
+            L.slot[pk] = (uint16_t)j;
             if (jb & JOB_COUNT_MASK) {
-                L.order[pj++] = (uint16_t)(j0 + u);
-                L.rank[j0 + u] = (uint16_t)pk;
+                L.order[pj++] = (uint16_t)j;
+                L.rank[j] = (uint16_t)pk;
             }
             ++pk;
         }

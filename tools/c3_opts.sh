@@ -11,7 +11,7 @@ for set in "$@"; do
   args=""
   for kv in $set; do args="$args --option $kv"; done
   timeout -k 10 300 python3 bench.py --cache-dir /tmp/c3 --steps 5 --warmup 1 --weak-seqs 0 --annot-queries 0 \
-    --matrix-seqs 0 --no-cpu-baseline $args --json-out $O/c3_opts_$i.json > $O/c3_opts_$i.log 2>&1 \
+    --matrix-seqs 0 --cli-seqs 0 --finish 0 --no-cpu-baseline $args --json-out $O/c3_opts_$i.json > $O/c3_opts_$i.log 2>&1 \
     || { tail -5 $O/c3_opts_$i.log; exit 1; }
   python3 -c "
 import json,sys; d=json.load(open('$O/c3_opts_$i.json')); r=d['roofline']; k=r.get('kernels_ms_per_step') or {}
