@@ -529,9 +529,6 @@ __device__ uint32_t kth_dev_sorted(const uint32_t* v, uint32_t n, uint32_t C2, u
     return x > y ? x : y;
 }
 
-#ifndef SKM_SEG_DIAG  // A/B builds only (tools/build_ab.sh): 1 = no mean, 2 = no median / MAD
-#define SKM_SEG_DIAG 0
-#endif
 constexpr int SEG_WAVES = 4;
 
 // wave-wide min / max / inclusive sum on DPP (row_shr 1/2/4/8 within rows of 16, then row_bcast
@@ -668,11 +665,6 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
     wave_sync_lds();
     // Boost.Math mean over float(kdata.mean) in hit order
     float mean;
-#if SKM_SEG_DIAG & 1  // diagnostics only (wrong results): no mean
-    if (true) {
-        mean = 0;
-    } else
-#endif
     if (A.mean_mode == 1) {
         float mu = 0, fi = 1;
         if (lane == 0)
@@ -763,10 +755,6 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
     for (int e = 0; e < (int)(SEG_CAP / 64); ++e) x[e] -= vmin;
     const uint32_t R = vmax - vmin + 1u;  // n == 0: wraps above SEG_CAP (the radix path)
     float median, mad;
-#if SKM_SEG_DIAG & 2  // diagnostics only (wrong results): no selects
-    if (lane == 0) emit((float)vmin, (float)R);
-    return;
-#endif
     if (R <= SEG_CAP) {
         // the order statistics from histograms in the wave's (now free) LDS buffer: of x - min, then
         // of the deviations |2 x - C2| = 2 i + (C2 & 1), all of one parity, binned by i < R
