@@ -86,19 +86,30 @@ int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std
             rp = files[f0]->residues.data();
             off = files[f0]->off;
             len = files[f0]->len;
-        } else {
-            res.reserve(nres);
-            off.reserve(nseq);
-            len.reserve(nseq);
+        } else {  // the batch's files side by side, copied by the host threads
+            std::vector<uint64_t> rbase(f1 - f0 + 1, 0), sbase(f1 - f0 + 1, 0);
             for (size_t f = f0; f < f1; ++f) {
-                const FastaFile& F = *files[f];
-                const uint64_t base = res.size();
-                res.insert(res.end(), F.residues.begin(), F.residues.end());
-                for (size_t r = 0; r < F.size(); ++r) {
-                    off.push_back(base + F.off[r]);
-                    len.push_back(F.len[r]);
-                }
+                rbase[f - f0 + 1] = rbase[f - f0] + files[f]->residues.size();
+                sbase[f - f0 + 1] = sbase[f - f0] + files[f]->size();
             }
+            res.resize(nres);
+            off.resize(nseq);
+            len.resize(nseq);
+            std::atomic<size_t> nextf{f0};
+            auto cp = [&]() {
+                for (size_t f; (f = nextf.fetch_add(1)) < f1;) {
+                    const FastaFile& F = *files[f];
+                    std::memcpy(res.data() + rbase[f - f0], F.residues.data(), F.residues.size());
+                    for (size_t r = 0; r < F.size(); ++r) {
+                        off[sbase[f - f0] + r] = rbase[f - f0] + F.off[r];
+                        len[sbase[f - f0] + r] = F.len[r];
+                    }
+                }
+            };
+            std::vector<std::thread> th;
+            for (int t = 1; t < std::max(1, std::min<int>(n_threads, (int)(f1 - f0))); ++t) th.emplace_back(cp);
+            cp();
+            for (auto& t : th) t.join();
             rp = res.data();
         }
         skm_calls calls{};

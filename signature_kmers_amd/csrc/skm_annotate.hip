@@ -25,6 +25,7 @@
 #include "skm_bdz.h"
 #include "skm_common.h"
 #include "skm_lookup.h"
+#include "skm_pool.h"
 #include "skm_select.h"
 #include "skm_util.h"
 
@@ -1310,20 +1311,38 @@ int skm_query_create(skm_query** out, skm_db* db, const uint8_t* residues, const
     try {
         SKM_HIP(hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking));
         for (auto& e : q->ev) SKM_HIP(hipEventCreate(&e));
-        std::vector<uint8_t> res;
         std::vector<QMeta> meta(n_seqs);
         std::vector<uint64_t> scr_off(n_seqs);
         uint64_t total = 0, nwin_tot = 0;
-        for (size_t s = 0; s < n_seqs; ++s) total += (uint64_t)seq_len[s] + 1;
-        res.reserve(total);
         for (size_t s = 0; s < n_seqs; ++s) {
-            meta[s].pstart = res.size();
+            meta[s].pstart = total;
             meta[s].len = seq_len[s];
             meta[s].pad = 0;
-            res.insert(res.end(), residues + seq_off[s], residues + seq_off[s] + seq_len[s]);
-            res.push_back(0);
+            total += (uint64_t)seq_len[s] + 1;
             scr_off[s] = nwin_tot;
             nwin_tot += seq_len[s] >= 8 ? seq_len[s] - 7 : 0;
+        }
+        // the packed residues (one 0 after each sequence), copied by the host pool in
+        // byte-balanced sequence ranges (10 M queries are ~3 GB)
+        std::vector<uint8_t> res(total);
+        {
+            HostPool pool(n_seqs > 4096 ? HostPool::default_threads() : 1);
+            const int parts = std::max(1, std::min<int>(4 * pool.threads(), (int)(total >> 20)));
+            pool.run(parts, [&](int p) {
+                const uint64_t lo = total * (uint64_t)p / (uint64_t)parts, hi = total * (uint64_t)(p + 1) / (uint64_t)parts;
+                auto first_at = [&](uint64_t x) {  // first sequence starting at or after byte x
+                    size_t a = 0, e = n_seqs;
+                    while (a < e) {
+                        const size_t mid = (a + e) / 2;
+                        if (meta[mid].pstart < x) a = mid + 1; else e = mid;
+                    }
+                    return a;
+                };
+                for (size_t s = first_at(lo), e = first_at(hi); s < e; ++s) {
+                    std::memcpy(res.data() + meta[s].pstart, residues + seq_off[s], seq_len[s]);
+                    res[meta[s].pstart + seq_len[s]] = 0;
+                }
+            });
         }
         q->nseq = (uint32_t)n_seqs;
         q->rp = res.size();

@@ -2102,14 +2102,25 @@ __global__ __launch_bounds__(EX_THREADS, MINB) void k_extract_stage_pos(ExtractA
     const uint64_t begin = (uint64_t)blockIdx.x * X.span, end = min(begin + X.span, n);
     uint32_t s = 0xFFFFFFFFu;
     SeqMeta m{};
+    // the next round's entries are loaded before this round's gathers and LDS work (one level
+    // less of the entry -> window / sequence -> record chain in each round's latency)
+    uint64_t nxt[SC_POS];
+#pragma unroll
+    for (int t = 0; t < SC_POS; ++t) {
+        const uint64_t j = begin + (uint64_t)threadIdx.x * SC_POS + t;
+        nxt[t] = j < end ? pos[j] : ~0ull;
+    }
     for (uint64_t base = begin; base < end; base += R) {
         if (threadIdx.x < 128) L.cnt[threadIdx.x] = 0;
         __syncthreads();
         uint64_t pp[SC_POS], raw[SC_POS];
 #pragma unroll
+        for (int t = 0; t < SC_POS; ++t)
+            pp[t] = nxt[t] != ~0ull ? nxt[t] & POS_MASK : ~0ull;  // k_pass_emit's entry: position | bucket << POS_BITS
+#pragma unroll
         for (int t = 0; t < SC_POS; ++t) {
-            const uint64_t j = base + (uint64_t)threadIdx.x * SC_POS + t;
-            pp[t] = j < end ? pos[j] & POS_MASK : ~0ull;  // k_pass_emit's entry: position | bucket << POS_BITS
+            const uint64_t j = base + R + (uint64_t)threadIdx.x * SC_POS + t;
+            nxt[t] = j < end ? pos[j] : ~0ull;
         }
 #pragma unroll
         for (int t = 0; t < SC_POS; ++t) raw[t] = pp[t] != ~0ull ? load_window(X.res, pp[t]) : 0ull;

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <atomic>
 #include <chrono>
 #include <thread>
 
@@ -161,14 +162,35 @@ int main(int argc, char** argv) {
                 break;
             }
     }
+    // each file's lines formatted on the host threads, written in file order
+    std::vector<std::string> text(files.size());
+    {
+        std::atomic<size_t> next{0};
+        auto fmt = [&]() {
+            for (size_t f; (f = next.fetch_add(1)) < files.size();) {
+                std::string& buf = text[f];
+                for (size_t r = 0; r < files[f].size(); ++r) {
+                    const SeqCall& c = calls[f][r];
+                    buf += files[f].ids[r];
+                    buf += '\t';
+                    buf += c.func;
+                    buf += '\t';
+                    buf += std::to_string((unsigned)c.fi);
+                    buf += '\t';
+                    buf += fmt_g(c.score);
+                    buf += '\n';
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < std::min<int>(n_threads, (int)files.size()); ++t) th.emplace_back(fmt);
+        fmt();
+        for (auto& t : th) t.join();
+    }
     for (size_t f = 0; f < files.size(); ++f) {
         if (op.has("debug-hits")) debug_hits(db, datbuf, files[f], fidx, ignore_hypo, hypo, std::cout);
-        std::string buf;
-        for (size_t r = 0; r < files[f].size(); ++r) {
-            const SeqCall& c = calls[f][r];
-            buf += files[f].ids[r] + "\t" + c.func + "\t" + std::to_string((unsigned)c.fi) + "\t" + fmt_g(c.score) + "\n";
-        }
-        *out << buf;
+        out->write(text[f].data(), (std::streamsize)text[f].size());
+        std::string().swap(text[f]);
     }
     out->flush();
     const double t_write = now_s() - t0;
