@@ -858,7 +858,7 @@ def _per_launch(traffic, passes):
     return None if traffic is None else traffic / max(1, passes)
 
 
-_PMC_FILE = "r04_pmc_traffic.json"
+_PMC_FILE = "r05_pmc_traffic.json"
 
 
 def src_sha16() -> str:

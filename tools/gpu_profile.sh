@@ -26,9 +26,9 @@ python3 -c "import bench; print(bench.src_sha16())" > "$O/src_sha16.txt"
 P=${PHASE:-all}
 case "$P" in legs*) ;; *) step cache 300 python3 bench.py --cache-dir /tmp/c3 --cache-only ;; esac
 cd /tmp
-C3="python3 -u $R/bench.py --cache-dir /tmp/c3 --weak-seqs 0 --annot-queries 0 --matrix-seqs 0 --no-cpu-baseline"
+C3="python3 -u $R/bench.py --cache-dir /tmp/c3 --weak-seqs 0 --annot-queries 0 --matrix-seqs 0 --cli-seqs 0 --finish 0 --no-cpu-baseline"
 C2="python3 -u $R/tools/c3_diag.py --cache-dir /tmp/c3 --files 250"
-LEGS="python3 -u $R/bench.py --seqs-total 1000000 --cache-dir /tmp/legs --no-cpu-baseline"
+LEGS="python3 -u $R/bench.py --seqs-total 1000000 --cache-dir /tmp/legs --cli-seqs 0 --finish 0 --no-cpu-baseline"
 # PHASE: all | trace (stamps + C3/C2 traces) | pmc (C3/C2 counters) | legs (legs trace + counters)
 #        | legs_trace (the legs' kernel trace only)
 if [ "$P" = all ] || [ "$P" = trace ]; then

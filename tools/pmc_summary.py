@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Fold a tools/gpu_profile.sh run (gpurun_out/) into profiles/ (round tag R, default r04):
+"""Fold a tools/gpu_profile.sh run (gpurun_out/) into profiles/ (round tag R, default r05):
 
 profiles/R_kernel_stats_{c3,c2,legs}.csv     rocprofv3 --kernel-trace --stats summaries
 profiles/R_pmc_traffic.json                  per kernel and workload: counter KiB per build run (c3,
@@ -38,7 +38,7 @@ def per_kernel(path, counter):
 
 def main():
     src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out")
-    rnd = sys.argv[2] if len(sys.argv) > 2 else "r04"
+    rnd = sys.argv[2] if len(sys.argv) > 2 else "r05"
     dst = os.path.join(ROOT, "profiles")
     for w in ("c3", "c2", "legs"):
         p = os.path.join(src, f"prof_{w}", "run_kernel_stats.csv")
