@@ -1771,14 +1771,30 @@ __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ 
 constexpr uint32_t EMIT_THREADS = 64;
 constexpr int POS_BITS = 36;                 // pass entry: position | level-1 bucket << POS_BITS
 constexpr uint64_t POS_MASK = (1ull << POS_BITS) - 1ull;
-template <uint32_t G>
+// ELEM (option emit_elems, the default where the bucket id fits 16 bits): the entries are the
+// pass's finished 16-byte occurrence elements (hi in pos, lo in pos_lo; the level-1 bucket rides
+// in lo's low 16 bits as in k_extract_stage_pos), built here where the window's residues are
+// already in registers -- the wave walks its span in order, so each lane finds its windows'
+// sequence with one blk2seq / meta lookup per tile.  The staged scatter that follows then streams
+// elements instead of gathering 8 residue bytes, a blk2seq word and a SeqMeta per window.
+struct EmitElemArgs {
+    uint64_t* pos_lo;
+    const uint32_t* blk2seq;
+    const SeqMeta* meta;
+    uint32_t s_base;
+    int pass_bits;
+};
+template <uint32_t G, bool ELEM>
 __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __restrict__ res, const uint8_t* __restrict__ ids,
                                                            uint64_t rp, uint32_t pass0, uint64_t span,
                                                            const uint64_t* __restrict__ seloff,
                                                            uint64_t* __restrict__ pos, uint64_t cap, int rem_bits,
-                                                           uint32_t NB) {
-    __shared__ uint32_t s_out[16 * 64];  // the tile's entries, pass-major: window (10 bits) | bucket << 10
+                                                           uint32_t NB, EmitElemArgs EA) {
+    __shared__ uint32_t s_out[ELEM ? 1 : 16 * 64];  // the tile's entries, pass-major: window (10 bits) | bucket << 10
+    __shared__ uint64_t s_eh[ELEM ? 16 * 64 : 1];   // ELEM: the tile's elements, pass-major
+    __shared__ uint64_t s_el[ELEM ? 16 * 64 : 1];
     const uint32_t lane = threadIdx.x;
+    const uint64_t rem_mask = (1ull << rem_bits) - 1ull;
     uint64_t run[G];
 #pragma unroll
     for (uint32_t q = 0; q < G; ++q) run[q] = seloff[(uint64_t)(pass0 + q) * (SEL_WG + 1) + blockIdx.x];
@@ -1787,7 +1803,11 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
         const uint64_t base = t0 + 16ull * lane;
         uint32_t qs[4] = {~0u, ~0u, ~0u, ~0u};  // byte t: the window's pass within the group (0xFF: none)
         uint32_t bks[16];                       // the window's level-1 bucket
+        uint64_t hs[ELEM ? 16 : 1];             // ELEM: the window's mix43
         uint32_t cnt[G];
+        uint32_t s_blk = 0;                     // ELEM: the sequence holding the lane's first window
+        if constexpr (ELEM)
+            if (base < e) s_blk = EA.blk2seq[base >> 6];  // issued early: the meta lookup depends on it
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) cnt[q] = 0;
         if (base < e) {
@@ -1822,7 +1842,9 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
                     if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
-                    bks[t] = ((any >> t) & 1u) ? (uint32_t)(mix43(k) >> rem_bits) & (NB - 1) : 0u;
+                    const uint64_t h = mix43(k);
+                    bks[t] = ((any >> t) & 1u) ? (uint32_t)(h >> rem_bits) & (NB - 1) : 0u;
+                    if constexpr (ELEM) hs[t] = h;
                 }
             }
         }
@@ -1836,6 +1858,8 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
             off[q] = qa[q] + inc - cnt[q];
             qa[q + 1] = qa[q] + tot;
         }
+        uint32_t ms = 0xFFFFFFFFu;  // ELEM: the lane's current sequence (its meta in mm)
+        SeqMeta mm{};
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             const uint32_t q = (qs[t >> 2] >> (8 * (t & 3))) & 0xFFu;
@@ -1844,7 +1868,23 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 #pragma unroll
             for (uint32_t j = 0; j < G; ++j)
                 if (q == j) f = off[j]++;
-            s_out[f] = (16u * lane + (uint32_t)t) | (bks[t] << 10);
+            if constexpr (ELEM) {
+                const uint64_t p = base + (uint64_t)t;
+                if (ms == 0xFFFFFFFFu) {
+                    ms = s_blk;
+                    mm = EA.meta[ms];
+                }
+                while (p > mm.pstart + mm.len) mm = EA.meta[++ms];  // valid windows never span a separator
+                const uint64_t h = hs[t];
+                // a heavy key routed in from a later pass keeps (natural ^ this pass) above its rem
+                const uint64_t route = (uint64_t)((uint32_t)(h >> (KEY_BITS - EA.pass_bits)) ^ (pass0 + q)) << rem_bits;
+                uint64_t eh, el;
+                make_elem((h & rem_mask) | route, EA.s_base + ms, (uint32_t)(p - mm.pstart), mm, eh, el);
+                s_eh[f] = eh;
+                s_el[f] = (el & ~0xFFFFull) | bks[t];  // the bucket id rides in the offset field until the split
+            } else {
+                s_out[f] = (16u * lane + (uint32_t)t) | (bks[t] << 10);
+            }
         }
         wave_sync();
         for (uint32_t j = lane; j < qa[G]; j += 64) {
@@ -1855,8 +1895,14 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 #pragma unroll
             for (uint32_t k = 0; k < G; ++k)
                 if (q == k) o = run[k] + (j - qa[k]);
-            const uint32_t v = s_out[j];
-            if (o < cap) pos[(uint64_t)q * cap + o] = (t0 + (v & 1023u)) | ((uint64_t)(v >> 10) << POS_BITS);
+            if (o >= cap) continue;
+            if constexpr (ELEM) {
+                pos[(uint64_t)q * cap + o] = s_eh[j];
+                EA.pos_lo[(uint64_t)q * cap + o] = s_el[j];
+            } else {
+                const uint32_t v = s_out[j];
+                pos[(uint64_t)q * cap + o] = (t0 + (v & 1023u)) | ((uint64_t)(v >> 10) << POS_BITS);
+            }
         }
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) run[q] += qa[q + 1] - qa[q];
@@ -1867,6 +1913,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 // The level-1 histogram of each pass of a group from its entries' bucket bits: blockIdx.y = the
 // pass within the group, blockIdx.x strides over its list; NB counters in LDS, merged once.
 constexpr uint32_t PH_THREADS = 512;
+template <bool ELEM>  // ELEM: the entries are elements, the bucket in the low 16 bits of lo (pos = the lo array)
 __global__ __launch_bounds__(PH_THREADS) void k_pass_hist(const uint64_t* __restrict__ pos, uint64_t cap,
                                                           const unsigned long long* __restrict__ npos, uint32_t NB,
                                                           uint32_t* __restrict__ hist) {
@@ -1886,7 +1933,7 @@ __global__ __launch_bounds__(PH_THREADS) void k_pass_hist(const uint64_t* __rest
         }
 #pragma unroll
         for (uint32_t u = 0; u < U; ++u)
-            if (v[u] != ~0ull) atomicAdd(&s_h[(uint32_t)(v[u] >> POS_BITS)], 1u);
+            if (v[u] != ~0ull) atomicAdd(&s_h[ELEM ? (uint32_t)(v[u] & 0xFFFFu) : (uint32_t)(v[u] >> POS_BITS)], 1u);
     }
     __syncthreads();
     uint32_t* hq = hist + (uint64_t)q * NB;
@@ -2085,12 +2132,15 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
 // The staged level-0 scatter over a key-range pass's positions pos[0..n) (same staging rounds
 // as k_extract_stage; each position finds its sequence through blk2seq, reusing the previous
 // one while it still contains the window).
-template <int R, int MINB>
+// With ELEM (k_pass_emit wrote finished elements: pos = hi, pos_lo = lo with the bucket in the
+// low 16 bits) it only stages and scatters them.
+template <int R, int MINB, bool ELEM>
 __global__ __launch_bounds__(EX_THREADS, MINB) void k_extract_stage_pos(ExtractArgs X, const uint64_t* __restrict__ pos,
                                                                         const unsigned long long* __restrict__ np,
                                                                         unsigned long long* __restrict__ cur0,
                                                                         uint64_t* __restrict__ out_hi,
-                                                                        uint64_t* __restrict__ out_lo) {
+                                                                        uint64_t* __restrict__ out_lo,
+                                                                        const uint64_t* __restrict__ pos_lo) {
     constexpr int SC_POS = R / EX_THREADS;
     const uint64_t n = min((uint64_t)*np, X.pos_cap);
     __shared__ StageLdsT<R> L;
@@ -2100,6 +2150,45 @@ __global__ __launch_bounds__(EX_THREADS, MINB) void k_extract_stage_pos(ExtractA
     const uint64_t rem_mask = (1ull << rem_bits) - 1;
     const int l0_shift = nbits - SC_L0_BITS;
     const uint64_t begin = (uint64_t)blockIdx.x * X.span, end = min(begin + X.span, n);
+    if constexpr (ELEM) {
+        for (uint64_t base = begin; base < end; base += R) {
+            if (threadIdx.x < 128) L.cnt[threadIdx.x] = 0;
+            __syncthreads();
+            uint64_t eh[SC_POS], el[SC_POS];
+            uint32_t rk[SC_POS], l0[SC_POS];
+#pragma unroll
+            for (int t = 0; t < SC_POS; ++t) {
+                const uint64_t j = base + (uint64_t)t * EX_THREADS + threadIdx.x;  // coalesced
+                eh[t] = j < end ? __builtin_nontemporal_load(pos + j) : 0ull;
+                el[t] = j < end ? __builtin_nontemporal_load(pos_lo + j) : 0ull;
+            }
+#pragma unroll
+            for (int t = 0; t < SC_POS; ++t) {
+                const uint64_t j = base + (uint64_t)t * EX_THREADS + threadIdx.x;
+                l0[t] = (uint32_t)(el[t] & 0xFFFFu) >> l0_shift;
+                rk[t] = j < end ? atomicAdd(&L.cnt[l0[t]], 1u) : 0u;
+            }
+            __syncthreads();
+            const uint32_t tot = stage_reserve(L, 1u << SC_L0_BITS, cur0, 0);
+#pragma unroll
+            for (int t = 0; t < SC_POS; ++t)
+                if (base + (uint64_t)t * EX_THREADS + threadIdx.x < end) {
+                    const uint32_t slot = L.off[l0[t]] + rk[t];
+                    L.hi[slot] = eh[t];
+                    L.lo[slot] = el[t];
+                    L.dst[slot] = (uint8_t)l0[t];
+                }
+            __syncthreads();
+            for (uint32_t j = threadIdx.x; j < tot; j += blockDim.x) {
+                const uint32_t d = L.dst[j];
+                const uint64_t o = L.base[d] + (j - L.off[d]);
+                out_hi[o] = L.hi[j];
+                out_lo[o] = L.lo[j];
+            }
+            __syncthreads();
+        }
+        return;
+    }
     uint32_t s = 0xFFFFFFFFu;
     SeqMeta m{};
     // the next round's entries are loaded before this round's gathers and LDS work (one level
@@ -4761,6 +4850,8 @@ struct Tune {
     int giant_class = -1;
     int giant_passes = 0;            // giant chains only in the last N passes (0: all)
     int prefetch = 1;                // next pass group's positions (k_pass_emit) during this group-by
+    int emit_elems = 1;              // k_pass_emit writes finished 16-byte elements (1; where the bucket id
+                                     //   fits 16 bits) instead of window positions (0)
     int heavy_grid = (int)HEAVY_GRID; // persistent grids: k_heavy,
     int ovf_grid = 1024;             //   k_overflow (per stream),
     int split_grid = 512;            //   k_ovf_split,
@@ -4941,6 +5032,8 @@ struct skm_build {
     // residue scan per group), in emit_g slots; the next group's scan runs on stx once the group's
     // last pass has staged its elements (ev_staged), beside that pass's group-by
     DevBuf d_posg, d_histg, d_npos;      // d_npos: every pass's window count (k_sel_scan)
+    DevBuf d_posg_lo;                    // emit_elems: the elements' lo words (d_posg holds hi)
+    bool elems = false;                  // this run's k_pass_emit writes elements (emit_elems)
     uint32_t emit_g = 1;
     DevBuf d_selrows, d_seloff;          // per-workgroup windows of each pass, their scanned offsets
     uint64_t sel_span = 0;               // windows per k_pass_ids / k_pass_emit workgroup
@@ -5427,13 +5520,17 @@ void prepare_local(skm_build* b) {
 // the smallest power of two whose largest pass fits the 32-bit element indexing and whose
 // per-pass work buffers (~PASS_BYTES per element) leave room for the kept arena (18 B per kept
 // k-mer, accumulated over all passes).
-constexpr uint64_t PASS_BYTES = 104;   // recs 16 + tmp 16 + received 16 (world > 1) + chain lens/jobs ~10 + overflow scratch ~40
-// HBM a shard's work buffers take for passes of at most m elements: PASS_BYTES per element, with
-// key-range passes also the window-position slots of a pass group (8 B per element and slot,
-// G = min(P, 4) slots, size_local) and the pass-id byte per residue.
-inline uint64_t pass_work(uint64_t m, int pb, uint64_t rp) {
+constexpr uint64_t PASS_BYTES = 88;    // recs 16 + tmp 16 + chain lens/jobs ~10 + overflow scratch ~40 (+ received 16 at world > 1)
+// emit_elems applies to this shard: the level-1 bucket id (owner and bucket bits) fits the 16 bits
+// the element's offset field carries it in until the split
+inline bool elems_on(const skm_build* b) { return b->tune.emit_elems && b->owner_bits + b->b1_bits <= 16; }
+// HBM a shard's work buffers take for passes of at most m elements: PASS_BYTES per element (+16
+// for the received buffer at world > 1), with key-range passes also the entries of a pass group
+// (G = min(P, 4) slots of 8 B per element -- 16 B when k_pass_emit writes elements, size_local)
+// and the pass-id byte per residue.
+inline uint64_t pass_work(uint64_t m, int pb, uint64_t rp, int world, bool elems) {
     const uint64_t G = pb ? std::min<uint64_t>(1ull << pb, 4) : 0;
-    return m * (PASS_BYTES + 8 * G) + (pb ? rp : 0);
+    return m * (PASS_BYTES + (world > 1 ? 16 : 0) + (elems ? 16 : 8) * G) + (pb ? rp : 0);
 }
 // the work buffers may take 5/8 of the budget; the kept arena (18 B per kept k-mer) and the
 // grow-and-redo reserve share the rest
@@ -5476,7 +5573,7 @@ void size_passes(skm_build* b, int forced_pb = -1) {
         // exchange (skewed owners); 2^32 - 2^28 leaves the same slack for the 32-bit indexing
         while (pb < 6) {
             const uint64_t m = pass_max(pb);
-            if (m < (1ull << 32) - (1ull << 28) && work_fits(pass_work(m, pb, b->rp), budget)) break;
+            if (m < (1ull << 32) - (1ull << 28) && work_fits(pass_work(m, pb, b->rp, b->world, elems_on(b)), budget)) break;
             ++pb;
         }
     }
@@ -5526,7 +5623,9 @@ void size_local(skm_build* b) {
         const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
         const uint32_t P = 1u << b->pass_bits;
         b->emit_g = std::max<uint32_t>(1, std::min<uint32_t>(P, 4u));
+        b->elems = elems_on(b);
         b->d_posg.ensure(8 * W * b->emit_g);
+        if (b->elems) b->d_posg_lo.ensure(8 * W * b->emit_g);
         b->d_ids.ensure(((b->rp + 15) & ~15ull) + 64);
         SKM_HIP(hipMemsetAsync(b->d_ids.p, 0xFF, ((b->rp + 15) & ~15ull) + 64, b->stream));  // padding: no window
         b->d_histg.ensure(sizeof(uint32_t) * (uint64_t)NB * b->emit_g);
@@ -5560,7 +5659,7 @@ void size_arena(skm_build* b) {
     uint64_t cap = std::min<uint64_t>(b->valid_total + 16, avail / (8 + sizeof(skm_stored_kmer_data)));
     if (b->tune.mem_budget_mb > 0) {
         const uint64_t budget = (uint64_t)b->tune.mem_budget_mb << 20;
-        const uint64_t used = pass_work(b->pass_max, b->pass_bits, b->rp);
+        const uint64_t used = pass_work(b->pass_max, b->pass_bits, b->rp, b->world, elems_on(b));
         cap = std::min<uint64_t>(cap, budget > used ? (budget - used) / 18 : 0);
     }
     cap = std::max<uint64_t>(cap, b->pass_max + 16);
@@ -5654,7 +5753,7 @@ void route_plan(const Ranks& bs) {
         SKM_HIP(hipMemGetInfo(&fr, &tot));
         const uint64_t budget = b->tune.mem_budget_mb > 0 ? (uint64_t)b->tune.mem_budget_mb << 20 : (uint64_t)fr;
         const bool forced = b->tune.passes > 0;
-        ok[k] = m < (1ull << 32) - (1ull << 28) && (forced || m <= b->pass_max || work_fits(pass_work(m, pb, b->rp), budget));
+        ok[k] = m < (1ull << 32) - (1ull << 28) && (forced || m <= b->pass_max || work_fits(pass_work(m, pb, b->rp, b->world, elems_on(b)), budget));
         routed_m[k] = m;
         routed_n[k] = natural_late - late;
     }
@@ -5803,21 +5902,42 @@ void emit_group(skm_build* b, uint32_t g, hipStream_t st) {
     const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
     const int rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
     const uint64_t cap = std::max<uint64_t>(b->pass_max, 1);
-#define SKM_EMIT(GG)                                                                                                    \
-    SKM_LAUNCH_AS(b, "k_pass_emit", k_pass_emit<GG>, dim3(SEL_WG), dim3(EMIT_THREADS), 0, st, b->d_res.as<uint8_t>(), \
+    EmitElemArgs EA;
+    EA.pos_lo = b->elems ? b->d_posg_lo.as<uint64_t>() : nullptr;
+    EA.blk2seq = b->d_blk2seq.as<uint32_t>();
+    EA.meta = b->d_meta.as<SeqMeta>();
+    EA.s_base = b->s_base;
+    EA.pass_bits = b->pass_bits;
+#define SKM_EMIT(GG, EL)                                                                                                \
+    SKM_LAUNCH_AS(b, "k_pass_emit", (k_pass_emit<GG, EL>), dim3(SEL_WG), dim3(EMIT_THREADS), 0, st, b->d_res.as<uint8_t>(), \
                   b->d_ids.as<uint8_t>(), b->rp, g * G, b->sel_span, b->d_seloff.as<uint64_t>(), b->d_posg.as<uint64_t>(), \
-                  cap, rem_bits, NB)
-    if (G == 4)
-        SKM_EMIT(4);
-    else if (G == 2)
-        SKM_EMIT(2);
-    else
-        SKM_EMIT(1);
+                  cap, rem_bits, NB, EA)
+    if (b->elems) {
+        if (G == 4)
+            SKM_EMIT(4, true);
+        else if (G == 2)
+            SKM_EMIT(2, true);
+        else
+            SKM_EMIT(1, true);
+    } else {
+        if (G == 4)
+            SKM_EMIT(4, false);
+        else if (G == 2)
+            SKM_EMIT(2, false);
+        else
+            SKM_EMIT(1, false);
+    }
 #undef SKM_EMIT
     // the group's histograms from the entries' bucket bits (8 B per window read, no residues)
     SKM_HIP(hipMemsetAsync(b->d_histg.p, 0, sizeof(uint32_t) * NB * G, st));
-    SKM_LAUNCH(b, k_pass_hist, dim3(256, G), dim3(PH_THREADS), 4u * NB, st, b->d_posg.as<uint64_t>(), cap,
-               b->d_npos.as<unsigned long long>() + (uint64_t)g * G, NB, b->d_histg.as<uint32_t>());
+    if (b->elems)
+        SKM_LAUNCH_AS(b, "k_pass_hist", k_pass_hist<true>, dim3(256, G), dim3(PH_THREADS), 4u * NB, st,
+                      b->d_posg_lo.as<uint64_t>(), cap, b->d_npos.as<unsigned long long>() + (uint64_t)g * G, NB,
+                      b->d_histg.as<uint32_t>());
+    else
+        SKM_LAUNCH_AS(b, "k_pass_hist", k_pass_hist<false>, dim3(256, G), dim3(PH_THREADS), 4u * NB, st,
+                      b->d_posg.as<uint64_t>(), cap, b->d_npos.as<unsigned long long>() + (uint64_t)g * G, NB,
+                      b->d_histg.as<uint32_t>());
     SKM_HIP(hipGetLastError());
     if (st != b->stream) SKM_HIP(hipEventRecord(b->ev_emit, st));
 }
@@ -5904,16 +6024,20 @@ void phase_extract(skm_build* b, uint32_t pass) {
     b->d_slices.ensure(4 * 80);
     SKM_LAUNCH(b, k_stage_init, dim3((NB + 255) / 256), dim3(256), 0, st, b->d_bstart.as<uint64_t>(), NB, l0_shift,
                        b->d_cur0.as<unsigned long long>(), b->d_cur1.as<unsigned long long>(), b->d_slices.as<uint32_t>());
-    if (b->pass_bits && b->tune.stage_round == 1)
-        SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND_HALF, 4>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
-                   b->d_posg.as<uint64_t>() + (uint64_t)(pass % b->emit_g) * std::max<uint64_t>(b->pass_max, 1),
-                   b->d_npos.as<unsigned long long>() + pass,
-                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass));
+    const uint64_t slot_off = (uint64_t)(pass % b->emit_g) * std::max<uint64_t>(b->pass_max, 1);
+    const uint64_t* slot_lo = b->elems ? b->d_posg_lo.as<uint64_t>() + slot_off : nullptr;
+    if (b->pass_bits && b->elems)
+        SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND, 2, true>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
+                   b->d_posg.as<uint64_t>() + slot_off, b->d_npos.as<unsigned long long>() + pass,
+                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass), slot_lo);
+    else if (b->pass_bits && b->tune.stage_round == 1)
+        SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND_HALF, 4, false>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
+                   b->d_posg.as<uint64_t>() + slot_off, b->d_npos.as<unsigned long long>() + pass,
+                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass), slot_lo);
     else if (b->pass_bits)
-        SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND, 2>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
-                   b->d_posg.as<uint64_t>() + (uint64_t)(pass % b->emit_g) * std::max<uint64_t>(b->pass_max, 1),
-                   b->d_npos.as<unsigned long long>() + pass,
-                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass));
+        SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND, 2, false>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
+                   b->d_posg.as<uint64_t>() + slot_off, b->d_npos.as<unsigned long long>() + pass,
+                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass), slot_lo);
     else
         SKM_LAUNCH(b, k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
                            tmp_hi(b, pass), tmp_lo(b, pass));
@@ -7136,6 +7260,7 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "giant_passes" ? &t.giant_passes
                : n == "heavy_lsd" ? &t.heavy_lsd
                : n == "prefetch" ? &t.prefetch
+               : n == "emit_elems" ? &t.emit_elems
                : n == "overflow_grid" ? &t.ovf_grid
                : n == "split_grid" ? &t.split_grid
                : n == "chain_grid" ? &t.chain_grid
