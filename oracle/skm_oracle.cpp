@@ -7,10 +7,15 @@
 //  `cpu_baseline` leg of bench.py may load this library.  The product (signature_kmers_amd/,
 //  libskm.so, the CLIs) never links or calls it.
 //
-//  PARITY STATUS: **parity unpinned**.  The reference cannot be compiled here (Boost, TBB<=2020
+//  PARITY STATUS: **partly pinned**.  The window iterator for_each_kmer<8> (kmer_data.h:76-102)
+//  is pinned against the reference's own code: oracle/Makefile.ref compiles kmer_data.h and
+//  fasta_parser.{h,cc} unchanged from /root/reference (std-only headers) into oracle/_ref/ref_pin,
+//  whose outputs over adversarial inputs are tests/golden/ref_windows.npz / ref_fasta.npz
+//  (tests/test_ref_pin_cpu.py checks oracle_kmer_windows against them).  Everything else is
+//  **parity unpinned**: the rest of the reference cannot be compiled here (Boost, TBB<=2020
 //  headers, CMPH and NuDB are absent; NuDB is git-cloned from the network by its Makefile) and
-//  it ships no tests, fixtures or golden vectors.  This restatement is
-//  therefore pinned only by (a) known-answer tests derived from the reference source semantics
+//  it ships no tests, fixtures or golden vectors.  That part is pinned
+//  only by (a) known-answer tests derived from the reference source semantics
 //  (tests/test_oracle_kat.py) and (b) the restated third-party algorithms below, whose versions
 //  are unpinned by the reference Makefile:
 //     * CMPH 2.0.x BDZ  (jenkins lookup2 hash, 2-bit g array, rank table)   -- cmph_kmer.h:85-147
