@@ -12,9 +12,11 @@ reference's way (~780 GB for the multimap), so the check is split:
   the input) puts the deepest group of the build in it (>= 2^19 occurrences, asserted: the heavy-
   key split, the overflow path and the longest stashed P^2 / variance chain at C3 depth).  The
   heaviest chain at C3 is ~9*10^5 samples, below lane_long = 2^20, so with the defaults every
-  stashed chain runs one lane each; a second build of the same input with lane_long = 2^18 and
+  stashed chain runs one lane each; a second run of the same build with lane_long = 2^18 and
   lane_tail = 2^14 runs the deepest chains on wave pairs (k_chain_long, the tail batch included)
   and must give the same slice;
+* the whole kept set through skm_build_finish (2.9 G k-mers, the device-sorted hand-off): keys
+  strictly ascending, as many as the run kept, and its slice equal to finish_slice's;
 * size-independent properties over the whole build: the occurrences grouped equal the oracle's
   count of valid windows of the whole input (every window extracted once, none lost by the
   key-range passes or the per-pass compaction), seqs_with_func equals the per-function sequence
@@ -78,23 +80,38 @@ def test_c3_slice_bit_exact_and_whole_build_properties(skm, gpu):
     heavy = _heaviest_key(parts)
     SLICE = int(oracle_ref.slice_hash(np.array([heavy], np.uint64))[0] >> np.uint64(64 - SLICE_BITS))
 
-    def build(opts):
-        b = skm.SignatureBuilder(nf)
-        for k, v in opts.items():
-            b.set_option(k, v)
-        b.reserve(sum(len(p[0]) for p in parts), sum(len(p[2]) for p in parts))
-        for r, o, l, f, i in parts:
-            b.add_batch(r, o, l, f, i)
-        b.run()
-        c = b.counters()
-        got = b.finish_slice(SLICE_BITS, SLICE)
-        flags = b.signature_flags()
-        b.close()
-        return c, got, flags
-
-    c, got, flags = build({})
+    b = skm.SignatureBuilder(nf)
+    b.reserve(sum(len(p[0]) for p in parts), sum(len(p[2]) for p in parts))
+    for r, o, l, f, i in parts:
+        b.add_batch(r, o, l, f, i)
+    b.run()
+    c = b.counters()
+    got = b.finish_slice(SLICE_BITS, SLICE)
+    flags = b.signature_flags()
     print(f"\nC3 build: {c['passes']} passes, {c['kept']:,} kept", flush=True)
-    c2, got2, _ = build({"lane_long": 1 << 18, "lane_tail": 1 << 14})  # the deepest chains on wave pairs
+    # the whole kept set through skm_build_finish (the device-sorted, streamed hand-off of 2.9 G
+    # k-mers): every kept k-mer once, keys strictly ascending, and its slice is finish_slice's
+    k = b.finish()
+    assert len(k.keys) == c["kept"] == k.distinct_signatures
+    sel_k, sel_d, prev = [], [], None
+    for a in range(0, len(k.keys), 1 << 27):
+        kk = k.keys[a:a + (1 << 27)]
+        assert bool(np.all(kk[1:] > kk[:-1])) and (prev is None or kk[0] > prev)
+        prev = kk[-1]
+        m = (oracle_ref.slice_hash(kk) >> np.uint64(64 - SLICE_BITS)) == np.uint64(SLICE)
+        sel_k.append(kk[m])
+        sel_d.append(k.data[a:a + (1 << 27)][m])
+    assert np.array_equal(np.concatenate(sel_k), got.keys)
+    assert np.array_equal(np.concatenate(sel_d).view(np.uint8), got.data.view(np.uint8))
+    del k, sel_k, sel_d
+    print("C3 finish: sorted, complete, slice consistent", flush=True)
+    # the same build with the deepest chains on wave pairs (k_chain_long, the tail batch included)
+    b.set_option("lane_long", 1 << 18)
+    b.set_option("lane_tail", 1 << 14)
+    b.run()
+    c2 = b.counters()
+    got2 = b.finish_slice(SLICE_BITS, SLICE)
+    b.close()
     print("C3 build (wave-pair chains) done", flush=True)
     assert c["passes"] >= 8, c  # the headline's out-of-core path (16 passes at 288 GB)
     # pack the input for the oracle (16.5 GB of residues)
