@@ -466,6 +466,7 @@ __global__ __launch_bounds__(256) void k_calls_scan_wave(CallArgs A, uint4* __re
         const uint64_t PL = U & ~SP;  // plain hits: the third and later of their run
         uint32_t from = 0;            // lanes below `from` are applied
         auto apply_plain = [&](uint32_t to) {  // the plain hits of lanes [from, to)
+            if (from >= 64) return;  // (a shift by 64 is undefined)
             const uint64_t span = (to >= 64 ? ~0ull : ((1ull << to) - 1ull)) & ~((1ull << from) - 1ull);
             const uint64_t M = PL & span;
             if (!M) return;

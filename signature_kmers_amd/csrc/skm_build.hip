@@ -3335,7 +3335,17 @@ __global__ __launch_bounds__(PT_THREADS, MINB) void k_partition(BucketArgs A) {
     for (uint32_t p = 0; p < nseg; ++p) {
         uint64_t base, len;
         seg(p, base, len);
-        for (uint64_t j = threadIdx.x; j < len; j += blockDim.x) {
+        // eight loads in flight per thread before their LDS atomics (a rolled loop waited for each)
+        constexpr uint32_t CU = 8;
+        uint64_t j0 = threadIdx.x;
+        for (; j0 + (uint64_t)(CU - 1) * PT_THREADS < len; j0 += (uint64_t)CU * PT_THREADS) {
+            uint64_t h[CU];
+#pragma unroll
+            for (uint32_t u = 0; u < CU; ++u) h[u] = A.recs_hi[base + j0 + (uint64_t)u * PT_THREADS];
+#pragma unroll
+            for (uint32_t u = 0; u < CU; ++u) atomicAdd(&s_cur[(uint32_t)(((h[u] >> 16) & rem_mask) >> shift)], 1u);
+        }
+        for (uint64_t j = j0; j < len; j += PT_THREADS) {
             const uint64_t h = A.recs_hi[base + j];
             atomicAdd(&s_cur[(uint32_t)(((h >> 16) & rem_mask) >> shift)], 1u);
         }
