@@ -1790,20 +1790,26 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                                                            const uint64_t* __restrict__ seloff,
                                                            uint64_t* __restrict__ pos, uint64_t cap, int rem_bits,
                                                            uint32_t NB, EmitElemArgs EA) {
-    __shared__ uint32_t s_out[ELEM ? 1 : 16 * 64];  // the tile's entries, pass-major: window (10 bits) | bucket << 10
-    __shared__ uint64_t s_eh[ELEM ? 16 * 64 : 1];   // ELEM: the tile's elements, pass-major
-    __shared__ uint64_t s_el[ELEM ? 16 * 64 : 1];
+    // W windows per lane per tile: 16 for positions (4 KB of staging per wave); 8 for elements, whose
+    // 16-byte staging would otherwise take 16 KB per wave and cap the kernel at 10 waves per CU
+    constexpr uint32_t W = ELEM ? 8 : 16;
+    constexpr uint32_t TILE = W * 64;
+    __shared__ uint32_t s_out[ELEM ? 1 : TILE];  // the tile's entries, pass-major: window (10 bits) | bucket << 10
+    __shared__ uint64_t s_eh[ELEM ? TILE : 1];   // ELEM: the tile's elements, pass-major
+    __shared__ uint64_t s_el[ELEM ? TILE : 1];
     const uint32_t lane = threadIdx.x;
     const uint64_t rem_mask = (1ull << rem_bits) - 1ull;
     uint64_t run[G];
 #pragma unroll
     for (uint32_t q = 0; q < G; ++q) run[q] = seloff[(uint64_t)(pass0 + q) * (SEL_WG + 1) + blockIdx.x];
     const uint64_t a = (uint64_t)blockIdx.x * span, e = min(rp, a + span);
-    for (uint64_t t0 = a; t0 < e; t0 += 16ull * 64) {
-        const uint64_t base = t0 + 16ull * lane;
-        uint32_t qs[4] = {~0u, ~0u, ~0u, ~0u};  // byte t: the window's pass within the group (0xFF: none)
-        uint32_t bks[16];                       // the window's level-1 bucket
-        uint64_t hs[ELEM ? 16 : 1];             // ELEM: the window's mix43
+    for (uint64_t t0 = a; t0 < e; t0 += TILE) {
+        const uint64_t base = t0 + (uint64_t)W * lane;
+        uint32_t qs[W / 4];                     // byte t: the window's pass within the group (0xFF: none)
+#pragma unroll
+        for (uint32_t i = 0; i < W / 4; ++i) qs[i] = ~0u;
+        uint32_t bks[W];                        // the window's level-1 bucket
+        uint64_t hs[ELEM ? W : 1];              // ELEM: the window's mix43
         uint32_t cnt[G];
         uint32_t s_blk = 0;                     // ELEM: the sequence holding the lane's first window
         if constexpr (ELEM)
@@ -1811,11 +1817,17 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) cnt[q] = 0;
         if (base < e) {
-            const uint4 id4 = *reinterpret_cast<const uint4*>(ids + base);
-            const uint32_t idw[4] = {id4.x, id4.y, id4.z, id4.w};
+            uint32_t idw[W / 4];
+            if constexpr (W == 16) {
+                const uint4 id4 = *reinterpret_cast<const uint4*>(ids + base);
+                idw[0] = id4.x; idw[1] = id4.y; idw[2] = id4.z; idw[3] = id4.w;
+            } else {
+                const uint2 id2 = *reinterpret_cast<const uint2*>(ids + base);
+                idw[0] = id2.x; idw[1] = id2.y;
+            }
             uint32_t any = 0;
 #pragma unroll
-            for (int t = 0; t < 16; ++t) {
+            for (uint32_t t = 0; t < W; ++t) {
                 const uint32_t q = ((idw[t >> 2] >> (8 * (t & 3))) & 0xFFu) - pass0;  // 0xFF (no window): >= G
                 if (q < G && base + t < e) {
                     any |= 1u << t;
@@ -1825,13 +1837,18 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                     for (uint32_t j = 0; j < G; ++j) cnt[j] += q == j ? 1u : 0u;
                 }
             }
-            if (any) {  // the 16 keys rolled from the lane's 24 residues, mixed for the group's windows
-                const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
-                const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
-                const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-                uint32_t code[24];
+            if (any) {  // the W keys rolled from the lane's W + 7 residues, mixed for the group's windows
+                constexpr uint32_t NW = W == 16 ? 8 : 4;  // residue words loaded (32 / 16 bytes)
+                uint32_t w[NW];
 #pragma unroll
-                for (int j = 0; j < 24; ++j) {
+                for (uint32_t i = 0; i < NW / 2; ++i) {  // 8-byte loads (base is a multiple of 8)
+                    const uint2 v = *reinterpret_cast<const uint2*>(res + base + 8 * i);
+                    w[2 * i] = v.x;
+                    w[2 * i + 1] = v.y;
+                }
+                uint32_t code[4 * NW];
+#pragma unroll
+                for (uint32_t j = 0; j < 4 * NW; ++j) {
                     const uint32_t cd = residue_code((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
                     code[j] = cd < 40u ? cd : 0u;
                 }
@@ -1840,7 +1857,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                 for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
                 constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
 #pragma unroll
-                for (int t = 0; t < 16; ++t) {
+                for (uint32_t t = 0; t < W; ++t) {
                     if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
                     const uint64_t h = mix43(k);
                     bks[t] = ((any >> t) & 1u) ? (uint32_t)(h >> rem_bits) & (NB - 1) : 0u;
@@ -1861,7 +1878,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
         uint32_t ms = 0xFFFFFFFFu;  // ELEM: the lane's current sequence (its meta in mm)
         SeqMeta mm{};
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
+        for (uint32_t t = 0; t < W; ++t) {
             const uint32_t q = (qs[t >> 2] >> (8 * (t & 3))) & 0xFFu;
             if (q >= G) continue;
             uint32_t f = 0;
@@ -1883,7 +1900,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                 s_eh[f] = eh;
                 s_el[f] = (el & ~0xFFFFull) | bks[t];  // the bucket id rides in the offset field until the split
             } else {
-                s_out[f] = (16u * lane + (uint32_t)t) | (bks[t] << 10);
+                s_out[f] = (W * lane + t) | (bks[t] << 10);
             }
         }
         wave_sync();
@@ -1906,7 +1923,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
         }
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) run[q] += qa[q + 1] - qa[q];
-        wave_sync();  // s_out is rewritten by the next tile
+        wave_sync();  // the staging is rewritten by the next tile
     }
 }
 
@@ -5536,10 +5553,10 @@ constexpr uint64_t PASS_BYTES = 88;    // recs 16 + tmp 16 + chain lens/jobs ~10
 inline bool elems_on(const skm_build* b) { return b->tune.emit_elems && b->owner_bits + b->b1_bits <= 16; }
 // HBM a shard's work buffers take for passes of at most m elements: PASS_BYTES per element (+16
 // for the received buffer at world > 1), with key-range passes also the entries of a pass group
-// (G = min(P, 4) slots of 8 B per element -- 16 B when k_pass_emit writes elements, size_local)
+// (G = min(P, 4) slots of 8 B per element; with elements min(P, 2) slots of 16 B, size_local)
 // and the pass-id byte per residue.
 inline uint64_t pass_work(uint64_t m, int pb, uint64_t rp, int world, bool elems) {
-    const uint64_t G = pb ? std::min<uint64_t>(1ull << pb, 4) : 0;
+    const uint64_t G = pb ? std::min<uint64_t>(1ull << pb, elems ? 2 : 4) : 0;
     return m * (PASS_BYTES + (world > 1 ? 16 : 0) + (elems ? 16 : 8) * G) + (pb ? rp : 0);
 }
 // the work buffers may take 5/8 of the budget; the kept arena (18 B per kept k-mer) and the
@@ -5632,8 +5649,8 @@ void size_local(skm_build* b) {
     if (b->pass_bits > 0) {
         const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
         const uint32_t P = 1u << b->pass_bits;
-        b->emit_g = std::max<uint32_t>(1, std::min<uint32_t>(P, 4u));
         b->elems = elems_on(b);
+        b->emit_g = std::max<uint32_t>(1, std::min<uint32_t>(P, b->elems ? 2u : 4u));
         b->d_posg.ensure(8 * W * b->emit_g);
         if (b->elems) b->d_posg_lo.ensure(8 * W * b->emit_g);
         b->d_ids.ensure(((b->rp + 15) & ~15ull) + 64);
