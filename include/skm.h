@@ -203,9 +203,7 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   their own streams; 0 = off; default: 14 with one pass or world_size > 1, off with key-range
  *   passes on one GPU),
  *   "giant_passes", "prefetch" (the next pass group's positions, k_pass_emit, during the group-by of the group's
- *   last pass, 1), "emit_elems" (1: k_pass_emit writes each pass's finished 16-byte occurrence
- *   elements, so the staged scatter streams them instead of gathering every window's residues and
- *   sequence record; 0: window positions; 1 applies where the owner + level-1 bucket bits fit 16),
+ *   last pass, 1),
  *   "overflow_grid" / "split_grid" / "chain_grid" (persistent-grid sizes), "stream_priority"
  *   (1: the group-by stream at the highest priority), "chain_batches" (key-range passes: the
  *   stashed long chains leave in this many batches, 4) / "chain_streams" (over 1..4 streams, 1),

@@ -1771,63 +1771,31 @@ __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ 
 constexpr uint32_t EMIT_THREADS = 64;
 constexpr int POS_BITS = 36;                 // pass entry: position | level-1 bucket << POS_BITS
 constexpr uint64_t POS_MASK = (1ull << POS_BITS) - 1ull;
-// ELEM (option emit_elems, the default where the bucket id fits 16 bits): the entries are the
-// pass's finished 16-byte occurrence elements (hi in pos, lo in pos_lo; the level-1 bucket rides
-// in lo's low 16 bits as in k_extract_stage_pos), built here where the window's residues are
-// already in registers -- the wave walks its span in order, so each lane finds its windows'
-// sequence with one blk2seq / meta lookup per tile.  The staged scatter that follows then streams
-// elements instead of gathering 8 residue bytes, a blk2seq word and a SeqMeta per window.
-struct EmitElemArgs {
-    uint64_t* pos_lo;
-    const uint32_t* blk2seq;
-    const SeqMeta* meta;
-    uint32_t s_base;
-    int pass_bits;
-};
-template <uint32_t G, bool ELEM>
+template <uint32_t G>
 __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __restrict__ res, const uint8_t* __restrict__ ids,
                                                            uint64_t rp, uint32_t pass0, uint64_t span,
                                                            const uint64_t* __restrict__ seloff,
                                                            uint64_t* __restrict__ pos, uint64_t cap, int rem_bits,
-                                                           uint32_t NB, EmitElemArgs EA) {
-    // W windows per lane per tile: 16 for positions (4 KB of staging per wave); 8 for elements, whose
-    // 16-byte staging would otherwise take 16 KB per wave and cap the kernel at 10 waves per CU
-    constexpr uint32_t W = ELEM ? 8 : 16;
-    constexpr uint32_t TILE = W * 64;
-    __shared__ uint32_t s_out[ELEM ? 1 : TILE];  // the tile's entries, pass-major: window (10 bits) | bucket << 10
-    __shared__ uint64_t s_eh[ELEM ? TILE : 1];   // ELEM: the tile's elements, pass-major
-    __shared__ uint64_t s_el[ELEM ? TILE : 1];
+                                                           uint32_t NB) {
+    __shared__ uint32_t s_out[16 * 64];  // the tile's entries, pass-major: window (10 bits) | bucket << 10
     const uint32_t lane = threadIdx.x;
-    const uint64_t rem_mask = (1ull << rem_bits) - 1ull;
     uint64_t run[G];
 #pragma unroll
     for (uint32_t q = 0; q < G; ++q) run[q] = seloff[(uint64_t)(pass0 + q) * (SEL_WG + 1) + blockIdx.x];
     const uint64_t a = (uint64_t)blockIdx.x * span, e = min(rp, a + span);
-    for (uint64_t t0 = a; t0 < e; t0 += TILE) {
-        const uint64_t base = t0 + (uint64_t)W * lane;
-        uint32_t qs[W / 4];                     // byte t: the window's pass within the group (0xFF: none)
-#pragma unroll
-        for (uint32_t i = 0; i < W / 4; ++i) qs[i] = ~0u;
-        uint32_t bks[W];                        // the window's level-1 bucket
-        uint64_t hs[ELEM ? W : 1];              // ELEM: the window's mix43
+    for (uint64_t t0 = a; t0 < e; t0 += 16ull * 64) {
+        const uint64_t base = t0 + 16ull * lane;
+        uint32_t qs[4] = {~0u, ~0u, ~0u, ~0u};  // byte t: the window's pass within the group (0xFF: none)
+        uint32_t bks[16];                       // the window's level-1 bucket
         uint32_t cnt[G];
-        uint32_t s_blk = 0;                     // ELEM: the sequence holding the lane's first window
-        if constexpr (ELEM)
-            if (base < e) s_blk = EA.blk2seq[base >> 6];  // issued early: the meta lookup depends on it
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) cnt[q] = 0;
         if (base < e) {
-            uint32_t idw[W / 4];
-            if constexpr (W == 16) {
-                const uint4 id4 = *reinterpret_cast<const uint4*>(ids + base);
-                idw[0] = id4.x; idw[1] = id4.y; idw[2] = id4.z; idw[3] = id4.w;
-            } else {
-                const uint2 id2 = *reinterpret_cast<const uint2*>(ids + base);
-                idw[0] = id2.x; idw[1] = id2.y;
-            }
+            const uint4 id4 = *reinterpret_cast<const uint4*>(ids + base);
+            const uint32_t idw[4] = {id4.x, id4.y, id4.z, id4.w};
             uint32_t any = 0;
 #pragma unroll
-            for (uint32_t t = 0; t < W; ++t) {
+            for (int t = 0; t < 16; ++t) {
                 const uint32_t q = ((idw[t >> 2] >> (8 * (t & 3))) & 0xFFu) - pass0;  // 0xFF (no window): >= G
                 if (q < G && base + t < e) {
                     any |= 1u << t;
@@ -1837,18 +1805,13 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                     for (uint32_t j = 0; j < G; ++j) cnt[j] += q == j ? 1u : 0u;
                 }
             }
-            if (any) {  // the W keys rolled from the lane's W + 7 residues, mixed for the group's windows
-                constexpr uint32_t NW = W == 16 ? 8 : 4;  // residue words loaded (32 / 16 bytes)
-                uint32_t w[NW];
+            if (any) {  // the 16 keys rolled from the lane's 24 residues, mixed for the group's windows
+                const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
+                const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
+                const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+                uint32_t code[24];
 #pragma unroll
-                for (uint32_t i = 0; i < NW / 2; ++i) {  // 8-byte loads (base is a multiple of 8)
-                    const uint2 v = *reinterpret_cast<const uint2*>(res + base + 8 * i);
-                    w[2 * i] = v.x;
-                    w[2 * i + 1] = v.y;
-                }
-                uint32_t code[4 * NW];
-#pragma unroll
-                for (uint32_t j = 0; j < 4 * NW; ++j) {
+                for (int j = 0; j < 24; ++j) {
                     const uint32_t cd = residue_code((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
                     code[j] = cd < 40u ? cd : 0u;
                 }
@@ -1857,11 +1820,9 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                 for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
                 constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
 #pragma unroll
-                for (uint32_t t = 0; t < W; ++t) {
+                for (int t = 0; t < 16; ++t) {
                     if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
-                    const uint64_t h = mix43(k);
-                    bks[t] = ((any >> t) & 1u) ? (uint32_t)(h >> rem_bits) & (NB - 1) : 0u;
-                    if constexpr (ELEM) hs[t] = h;
+                    bks[t] = ((any >> t) & 1u) ? (uint32_t)(mix43(k) >> rem_bits) & (NB - 1) : 0u;
                 }
             }
         }
@@ -1875,33 +1836,15 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
             off[q] = qa[q] + inc - cnt[q];
             qa[q + 1] = qa[q] + tot;
         }
-        uint32_t ms = 0xFFFFFFFFu;  // ELEM: the lane's current sequence (its meta in mm)
-        SeqMeta mm{};
 #pragma unroll
-        for (uint32_t t = 0; t < W; ++t) {
+        for (int t = 0; t < 16; ++t) {
             const uint32_t q = (qs[t >> 2] >> (8 * (t & 3))) & 0xFFu;
             if (q >= G) continue;
             uint32_t f = 0;
 #pragma unroll
             for (uint32_t j = 0; j < G; ++j)
                 if (q == j) f = off[j]++;
-            if constexpr (ELEM) {
-                const uint64_t p = base + (uint64_t)t;
-                if (ms == 0xFFFFFFFFu) {
-                    ms = s_blk;
-                    mm = EA.meta[ms];
-                }
-                while (p > mm.pstart + mm.len) mm = EA.meta[++ms];  // valid windows never span a separator
-                const uint64_t h = hs[t];
-                // a heavy key routed in from a later pass keeps (natural ^ this pass) above its rem
-                const uint64_t route = (uint64_t)((uint32_t)(h >> (KEY_BITS - EA.pass_bits)) ^ (pass0 + q)) << rem_bits;
-                uint64_t eh, el;
-                make_elem((h & rem_mask) | route, EA.s_base + ms, (uint32_t)(p - mm.pstart), mm, eh, el);
-                s_eh[f] = eh;
-                s_el[f] = (el & ~0xFFFFull) | bks[t];  // the bucket id rides in the offset field until the split
-            } else {
-                s_out[f] = (W * lane + t) | (bks[t] << 10);
-            }
+            s_out[f] = (16u * lane + (uint32_t)t) | (bks[t] << 10);
         }
         wave_sync();
         for (uint32_t j = lane; j < qa[G]; j += 64) {
@@ -1912,25 +1855,18 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 #pragma unroll
             for (uint32_t k = 0; k < G; ++k)
                 if (q == k) o = run[k] + (j - qa[k]);
-            if (o >= cap) continue;
-            if constexpr (ELEM) {
-                pos[(uint64_t)q * cap + o] = s_eh[j];
-                EA.pos_lo[(uint64_t)q * cap + o] = s_el[j];
-            } else {
-                const uint32_t v = s_out[j];
-                pos[(uint64_t)q * cap + o] = (t0 + (v & 1023u)) | ((uint64_t)(v >> 10) << POS_BITS);
-            }
+            const uint32_t v = s_out[j];
+            if (o < cap) pos[(uint64_t)q * cap + o] = (t0 + (v & 1023u)) | ((uint64_t)(v >> 10) << POS_BITS);
         }
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) run[q] += qa[q + 1] - qa[q];
-        wave_sync();  // the staging is rewritten by the next tile
+        wave_sync();  // s_out is rewritten by the next tile
     }
 }
 
 // The level-1 histogram of each pass of a group from its entries' bucket bits: blockIdx.y = the
 // pass within the group, blockIdx.x strides over its list; NB counters in LDS, merged once.
 constexpr uint32_t PH_THREADS = 512;
-template <bool ELEM>  // ELEM: the entries are elements, the bucket in the low 16 bits of lo (pos = the lo array)
 __global__ __launch_bounds__(PH_THREADS) void k_pass_hist(const uint64_t* __restrict__ pos, uint64_t cap,
                                                           const unsigned long long* __restrict__ npos, uint32_t NB,
                                                           uint32_t* __restrict__ hist) {
@@ -1950,7 +1886,7 @@ __global__ __launch_bounds__(PH_THREADS) void k_pass_hist(const uint64_t* __rest
         }
 #pragma unroll
         for (uint32_t u = 0; u < U; ++u)
-            if (v[u] != ~0ull) atomicAdd(&s_h[ELEM ? (uint32_t)(v[u] & 0xFFFFu) : (uint32_t)(v[u] >> POS_BITS)], 1u);
+            if (v[u] != ~0ull) atomicAdd(&s_h[(uint32_t)(v[u] >> POS_BITS)], 1u);
     }
     __syncthreads();
     uint32_t* hq = hist + (uint64_t)q * NB;
@@ -2149,15 +2085,12 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
 // The staged level-0 scatter over a key-range pass's positions pos[0..n) (same staging rounds
 // as k_extract_stage; each position finds its sequence through blk2seq, reusing the previous
 // one while it still contains the window).
-// With ELEM (k_pass_emit wrote finished elements: pos = hi, pos_lo = lo with the bucket in the
-// low 16 bits) it only stages and scatters them.
-template <int R, int MINB, bool ELEM>
+template <int R, int MINB>
 __global__ __launch_bounds__(EX_THREADS, MINB) void k_extract_stage_pos(ExtractArgs X, const uint64_t* __restrict__ pos,
                                                                         const unsigned long long* __restrict__ np,
                                                                         unsigned long long* __restrict__ cur0,
                                                                         uint64_t* __restrict__ out_hi,
-                                                                        uint64_t* __restrict__ out_lo,
-                                                                        const uint64_t* __restrict__ pos_lo) {
+                                                                        uint64_t* __restrict__ out_lo) {
     constexpr int SC_POS = R / EX_THREADS;
     const uint64_t n = min((uint64_t)*np, X.pos_cap);
     __shared__ StageLdsT<R> L;
@@ -2167,45 +2100,6 @@ __global__ __launch_bounds__(EX_THREADS, MINB) void k_extract_stage_pos(ExtractA
     const uint64_t rem_mask = (1ull << rem_bits) - 1;
     const int l0_shift = nbits - SC_L0_BITS;
     const uint64_t begin = (uint64_t)blockIdx.x * X.span, end = min(begin + X.span, n);
-    if constexpr (ELEM) {
-        for (uint64_t base = begin; base < end; base += R) {
-            if (threadIdx.x < 128) L.cnt[threadIdx.x] = 0;
-            __syncthreads();
-            uint64_t eh[SC_POS], el[SC_POS];
-            uint32_t rk[SC_POS], l0[SC_POS];
-#pragma unroll
-            for (int t = 0; t < SC_POS; ++t) {
-                const uint64_t j = base + (uint64_t)t * EX_THREADS + threadIdx.x;  // coalesced
-                eh[t] = j < end ? __builtin_nontemporal_load(pos + j) : 0ull;
-                el[t] = j < end ? __builtin_nontemporal_load(pos_lo + j) : 0ull;
-            }
-#pragma unroll
-            for (int t = 0; t < SC_POS; ++t) {
-                const uint64_t j = base + (uint64_t)t * EX_THREADS + threadIdx.x;
-                l0[t] = (uint32_t)(el[t] & 0xFFFFu) >> l0_shift;
-                rk[t] = j < end ? atomicAdd(&L.cnt[l0[t]], 1u) : 0u;
-            }
-            __syncthreads();
-            const uint32_t tot = stage_reserve(L, 1u << SC_L0_BITS, cur0, 0);
-#pragma unroll
-            for (int t = 0; t < SC_POS; ++t)
-                if (base + (uint64_t)t * EX_THREADS + threadIdx.x < end) {
-                    const uint32_t slot = L.off[l0[t]] + rk[t];
-                    L.hi[slot] = eh[t];
-                    L.lo[slot] = el[t];
-                    L.dst[slot] = (uint8_t)l0[t];
-                }
-            __syncthreads();
-            for (uint32_t j = threadIdx.x; j < tot; j += blockDim.x) {
-                const uint32_t d = L.dst[j];
-                const uint64_t o = L.base[d] + (j - L.off[d]);
-                out_hi[o] = L.hi[j];
-                out_lo[o] = L.lo[j];
-            }
-            __syncthreads();
-        }
-        return;
-    }
     uint32_t s = 0xFFFFFFFFu;
     SeqMeta m{};
     // the next round's entries are loaded before this round's gathers and LDS work (one level
@@ -2752,15 +2646,14 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     __syncthreads();
     SKM_STAMP(3);
     // 3. singletons resolved in place; multi-occurrence groups get a slice of `order` (each thread
-    //    owns LPER elements strided by the workgroup -- consecutive lanes touch consecutive LDS
-    //    words; a thread's LPER consecutive elements put lanes 8 apart on one bank -- and one
-    //    workgroup scan orders the groups by (thread, element): any fixed order will do)
+    //    owns LPER consecutive elements: one workgroup scan for the whole batch)
     uint32_t M = 0, G = 0;
     {
+        const uint32_t j0 = tid * LPER;
         uint32_t ev[LPER], loc = 0;
 #pragma unroll
         for (uint32_t u = 0; u < LPER; ++u) {
-            const uint32_t j = tid + u * BPK_THREADS;
+            const uint32_t j = j0 + u;
             ev[u] = j < n ? L.tab[L.slot[j]] : 0u;
             const uint32_t cnt = ev[u] & 0xFFFFu;
             loc += (cnt > 1 && (ev[u] >> 16) == j) ? ((cnt << 13) | 1u) : 0u;
@@ -2770,7 +2663,7 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         uint32_t ms[LPER];  // the singletons' sequences, flagged after the loop
 #pragma unroll
         for (uint32_t u = 0; u < LPER; ++u) {
-            const uint32_t j = tid + u * BPK_THREADS;
+            const uint32_t j = j0 + u;
             const uint32_t cnt = ev[u] & 0xFFFFu;
             ms[u] = 0xFFFFFFFFu;
             if (j < n && cnt > 1 && (ev[u] >> 16) == j) {
@@ -2905,10 +2798,11 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
     //    a job's kept position) so consecutive lanes write consecutive records
     constexpr uint32_t EMIT_PER = CAP / BPK_THREADS;
     unsigned long long* s_base = reinterpret_cast<unsigned long long*>(L.wave + 36);
-    uint32_t cnt = 0;  // (elements strided by the workgroup, as in the classify phase)
+    const uint32_t j0 = tid * EMIT_PER;
+    uint32_t cnt = 0;
 #pragma unroll
     for (uint32_t u = 0; u < EMIT_PER; ++u) {
-        const uint32_t j = tid + u * BPK_THREADS;
+        const uint32_t j = j0 + u;
         const uint32_t jb = j < n ? jobinfo[j] : 0u;
         cnt += ((jb & JOB_KEPT) ? 1u : 0u) | ((jb & JOB_COUNT_MASK) ? 0x10000u : 0u);
     }
@@ -2922,13 +2816,12 @@ __device__ __forceinline__ void process_sub(const uint64_t* __restrict__ src_hi,
         uint32_t pk = pos & 0xFFFFu, pj = pos >> 16;
 #pragma unroll
         for (uint32_t u = 0; u < EMIT_PER; ++u) {
-            const uint32_t j = tid + u * BPK_THREADS;
-            const uint32_t jb = j < n ? jobinfo[j] : 0u;
+            const uint32_t jb = j0 + u < n ? jobinfo[j0 + u] : 0u;
             if (!(jb & JOB_KEPT)) continue;
-            L.slot[pk] = (uint16_t)j;
+            L.slot[pk] = (uint16_t)(j0 + u);
             if (jb & JOB_COUNT_MASK) {
-                L.order[pj++] = (uint16_t)j;
-                L.rank[j] = (uint16_t)pk;
+                L.order[pj++] = (uint16_t)(j0 + u);
+                L.rank[j0 + u] = (uint16_t)pk;
             }
             ++pk;
         }
@@ -3352,17 +3245,7 @@ __global__ __launch_bounds__(PT_THREADS, MINB) void k_partition(BucketArgs A) {
     for (uint32_t p = 0; p < nseg; ++p) {
         uint64_t base, len;
         seg(p, base, len);
-        // eight loads in flight per thread before their LDS atomics (a rolled loop waited for each)
-        constexpr uint32_t CU = 8;
-        uint64_t j0 = threadIdx.x;
-        for (; j0 + (uint64_t)(CU - 1) * PT_THREADS < len; j0 += (uint64_t)CU * PT_THREADS) {
-            uint64_t h[CU];
-#pragma unroll
-            for (uint32_t u = 0; u < CU; ++u) h[u] = A.recs_hi[base + j0 + (uint64_t)u * PT_THREADS];
-#pragma unroll
-            for (uint32_t u = 0; u < CU; ++u) atomicAdd(&s_cur[(uint32_t)(((h[u] >> 16) & rem_mask) >> shift)], 1u);
-        }
-        for (uint64_t j = j0; j < len; j += PT_THREADS) {
+        for (uint64_t j = threadIdx.x; j < len; j += blockDim.x) {
             const uint64_t h = A.recs_hi[base + j];
             atomicAdd(&s_cur[(uint32_t)(((h >> 16) & rem_mask) >> shift)], 1u);
         }
@@ -4877,8 +4760,6 @@ struct Tune {
     int giant_class = -1;
     int giant_passes = 0;            // giant chains only in the last N passes (0: all)
     int prefetch = 1;                // next pass group's positions (k_pass_emit) during this group-by
-    int emit_elems = 1;              // k_pass_emit writes finished 16-byte elements (1; where the bucket id
-                                     //   fits 16 bits) instead of window positions (0)
     int heavy_grid = (int)HEAVY_GRID; // persistent grids: k_heavy,
     int ovf_grid = 1024;             //   k_overflow (per stream),
     int split_grid = 512;            //   k_ovf_split,
@@ -5059,8 +4940,6 @@ struct skm_build {
     // residue scan per group), in emit_g slots; the next group's scan runs on stx once the group's
     // last pass has staged its elements (ev_staged), beside that pass's group-by
     DevBuf d_posg, d_histg, d_npos;      // d_npos: every pass's window count (k_sel_scan)
-    DevBuf d_posg_lo;                    // emit_elems: the elements' lo words (d_posg holds hi)
-    bool elems = false;                  // this run's k_pass_emit writes elements (emit_elems)
     uint32_t emit_g = 1;
     DevBuf d_selrows, d_seloff;          // per-workgroup windows of each pass, their scanned offsets
     uint64_t sel_span = 0;               // windows per k_pass_ids / k_pass_emit workgroup
@@ -5547,17 +5426,13 @@ void prepare_local(skm_build* b) {
 // the smallest power of two whose largest pass fits the 32-bit element indexing and whose
 // per-pass work buffers (~PASS_BYTES per element) leave room for the kept arena (18 B per kept
 // k-mer, accumulated over all passes).
-constexpr uint64_t PASS_BYTES = 88;    // recs 16 + tmp 16 + chain lens/jobs ~10 + overflow scratch ~40 (+ received 16 at world > 1)
-// emit_elems applies to this shard: the level-1 bucket id (owner and bucket bits) fits the 16 bits
-// the element's offset field carries it in until the split
-inline bool elems_on(const skm_build* b) { return b->tune.emit_elems && b->owner_bits + b->b1_bits <= 16; }
-// HBM a shard's work buffers take for passes of at most m elements: PASS_BYTES per element (+16
-// for the received buffer at world > 1), with key-range passes also the entries of a pass group
-// (G = min(P, 4) slots of 8 B per element; with elements min(P, 2) slots of 16 B, size_local)
-// and the pass-id byte per residue.
-inline uint64_t pass_work(uint64_t m, int pb, uint64_t rp, int world, bool elems) {
-    const uint64_t G = pb ? std::min<uint64_t>(1ull << pb, elems ? 2 : 4) : 0;
-    return m * (PASS_BYTES + (world > 1 ? 16 : 0) + (elems ? 16 : 8) * G) + (pb ? rp : 0);
+constexpr uint64_t PASS_BYTES = 104;   // recs 16 + tmp 16 + received 16 (world > 1) + chain lens/jobs ~10 + overflow scratch ~40
+// HBM a shard's work buffers take for passes of at most m elements: PASS_BYTES per element, with
+// key-range passes also the window-position slots of a pass group (8 B per element and slot,
+// G = min(P, 4) slots, size_local) and the pass-id byte per residue.
+inline uint64_t pass_work(uint64_t m, int pb, uint64_t rp) {
+    const uint64_t G = pb ? std::min<uint64_t>(1ull << pb, 4) : 0;
+    return m * (PASS_BYTES + 8 * G) + (pb ? rp : 0);
 }
 // the work buffers may take 5/8 of the budget; the kept arena (18 B per kept k-mer) and the
 // grow-and-redo reserve share the rest
@@ -5600,7 +5475,7 @@ void size_passes(skm_build* b, int forced_pb = -1) {
         // exchange (skewed owners); 2^32 - 2^28 leaves the same slack for the 32-bit indexing
         while (pb < 6) {
             const uint64_t m = pass_max(pb);
-            if (m < (1ull << 32) - (1ull << 28) && work_fits(pass_work(m, pb, b->rp, b->world, elems_on(b)), budget)) break;
+            if (m < (1ull << 32) - (1ull << 28) && work_fits(pass_work(m, pb, b->rp), budget)) break;
             ++pb;
         }
     }
@@ -5649,10 +5524,8 @@ void size_local(skm_build* b) {
     if (b->pass_bits > 0) {
         const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
         const uint32_t P = 1u << b->pass_bits;
-        b->elems = elems_on(b);
-        b->emit_g = std::max<uint32_t>(1, std::min<uint32_t>(P, b->elems ? 2u : 4u));
+        b->emit_g = std::max<uint32_t>(1, std::min<uint32_t>(P, 4u));
         b->d_posg.ensure(8 * W * b->emit_g);
-        if (b->elems) b->d_posg_lo.ensure(8 * W * b->emit_g);
         b->d_ids.ensure(((b->rp + 15) & ~15ull) + 64);
         SKM_HIP(hipMemsetAsync(b->d_ids.p, 0xFF, ((b->rp + 15) & ~15ull) + 64, b->stream));  // padding: no window
         b->d_histg.ensure(sizeof(uint32_t) * (uint64_t)NB * b->emit_g);
@@ -5686,7 +5559,7 @@ void size_arena(skm_build* b) {
     uint64_t cap = std::min<uint64_t>(b->valid_total + 16, avail / (8 + sizeof(skm_stored_kmer_data)));
     if (b->tune.mem_budget_mb > 0) {
         const uint64_t budget = (uint64_t)b->tune.mem_budget_mb << 20;
-        const uint64_t used = pass_work(b->pass_max, b->pass_bits, b->rp, b->world, elems_on(b));
+        const uint64_t used = pass_work(b->pass_max, b->pass_bits, b->rp);
         cap = std::min<uint64_t>(cap, budget > used ? (budget - used) / 18 : 0);
     }
     cap = std::max<uint64_t>(cap, b->pass_max + 16);
@@ -5780,7 +5653,7 @@ void route_plan(const Ranks& bs) {
         SKM_HIP(hipMemGetInfo(&fr, &tot));
         const uint64_t budget = b->tune.mem_budget_mb > 0 ? (uint64_t)b->tune.mem_budget_mb << 20 : (uint64_t)fr;
         const bool forced = b->tune.passes > 0;
-        ok[k] = m < (1ull << 32) - (1ull << 28) && (forced || m <= b->pass_max || work_fits(pass_work(m, pb, b->rp, b->world, elems_on(b)), budget));
+        ok[k] = m < (1ull << 32) - (1ull << 28) && (forced || m <= b->pass_max || work_fits(pass_work(m, pb, b->rp), budget));
         routed_m[k] = m;
         routed_n[k] = natural_late - late;
     }
@@ -5929,42 +5802,21 @@ void emit_group(skm_build* b, uint32_t g, hipStream_t st) {
     const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
     const int rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
     const uint64_t cap = std::max<uint64_t>(b->pass_max, 1);
-    EmitElemArgs EA;
-    EA.pos_lo = b->elems ? b->d_posg_lo.as<uint64_t>() : nullptr;
-    EA.blk2seq = b->d_blk2seq.as<uint32_t>();
-    EA.meta = b->d_meta.as<SeqMeta>();
-    EA.s_base = b->s_base;
-    EA.pass_bits = b->pass_bits;
-#define SKM_EMIT(GG, EL)                                                                                                \
-    SKM_LAUNCH_AS(b, "k_pass_emit", (k_pass_emit<GG, EL>), dim3(SEL_WG), dim3(EMIT_THREADS), 0, st, b->d_res.as<uint8_t>(), \
+#define SKM_EMIT(GG)                                                                                                    \
+    SKM_LAUNCH_AS(b, "k_pass_emit", k_pass_emit<GG>, dim3(SEL_WG), dim3(EMIT_THREADS), 0, st, b->d_res.as<uint8_t>(), \
                   b->d_ids.as<uint8_t>(), b->rp, g * G, b->sel_span, b->d_seloff.as<uint64_t>(), b->d_posg.as<uint64_t>(), \
-                  cap, rem_bits, NB, EA)
-    if (b->elems) {
-        if (G == 4)
-            SKM_EMIT(4, true);
-        else if (G == 2)
-            SKM_EMIT(2, true);
-        else
-            SKM_EMIT(1, true);
-    } else {
-        if (G == 4)
-            SKM_EMIT(4, false);
-        else if (G == 2)
-            SKM_EMIT(2, false);
-        else
-            SKM_EMIT(1, false);
-    }
+                  cap, rem_bits, NB)
+    if (G == 4)
+        SKM_EMIT(4);
+    else if (G == 2)
+        SKM_EMIT(2);
+    else
+        SKM_EMIT(1);
 #undef SKM_EMIT
     // the group's histograms from the entries' bucket bits (8 B per window read, no residues)
     SKM_HIP(hipMemsetAsync(b->d_histg.p, 0, sizeof(uint32_t) * NB * G, st));
-    if (b->elems)
-        SKM_LAUNCH_AS(b, "k_pass_hist", k_pass_hist<true>, dim3(256, G), dim3(PH_THREADS), 4u * NB, st,
-                      b->d_posg_lo.as<uint64_t>(), cap, b->d_npos.as<unsigned long long>() + (uint64_t)g * G, NB,
-                      b->d_histg.as<uint32_t>());
-    else
-        SKM_LAUNCH_AS(b, "k_pass_hist", k_pass_hist<false>, dim3(256, G), dim3(PH_THREADS), 4u * NB, st,
-                      b->d_posg.as<uint64_t>(), cap, b->d_npos.as<unsigned long long>() + (uint64_t)g * G, NB,
-                      b->d_histg.as<uint32_t>());
+    SKM_LAUNCH(b, k_pass_hist, dim3(256, G), dim3(PH_THREADS), 4u * NB, st, b->d_posg.as<uint64_t>(), cap,
+               b->d_npos.as<unsigned long long>() + (uint64_t)g * G, NB, b->d_histg.as<uint32_t>());
     SKM_HIP(hipGetLastError());
     if (st != b->stream) SKM_HIP(hipEventRecord(b->ev_emit, st));
 }
@@ -6051,20 +5903,16 @@ void phase_extract(skm_build* b, uint32_t pass) {
     b->d_slices.ensure(4 * 80);
     SKM_LAUNCH(b, k_stage_init, dim3((NB + 255) / 256), dim3(256), 0, st, b->d_bstart.as<uint64_t>(), NB, l0_shift,
                        b->d_cur0.as<unsigned long long>(), b->d_cur1.as<unsigned long long>(), b->d_slices.as<uint32_t>());
-    const uint64_t slot_off = (uint64_t)(pass % b->emit_g) * std::max<uint64_t>(b->pass_max, 1);
-    const uint64_t* slot_lo = b->elems ? b->d_posg_lo.as<uint64_t>() + slot_off : nullptr;
-    if (b->pass_bits && b->elems)
-        SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND, 2, true>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
-                   b->d_posg.as<uint64_t>() + slot_off, b->d_npos.as<unsigned long long>() + pass,
-                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass), slot_lo);
-    else if (b->pass_bits && b->tune.stage_round == 1)
-        SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND_HALF, 4, false>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
-                   b->d_posg.as<uint64_t>() + slot_off, b->d_npos.as<unsigned long long>() + pass,
-                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass), slot_lo);
+    if (b->pass_bits && b->tune.stage_round == 1)
+        SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND_HALF, 4>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
+                   b->d_posg.as<uint64_t>() + (uint64_t)(pass % b->emit_g) * std::max<uint64_t>(b->pass_max, 1),
+                   b->d_npos.as<unsigned long long>() + pass,
+                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass));
     else if (b->pass_bits)
-        SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND, 2, false>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
-                   b->d_posg.as<uint64_t>() + slot_off, b->d_npos.as<unsigned long long>() + pass,
-                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass), slot_lo);
+        SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND, 2>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
+                   b->d_posg.as<uint64_t>() + (uint64_t)(pass % b->emit_g) * std::max<uint64_t>(b->pass_max, 1),
+                   b->d_npos.as<unsigned long long>() + pass,
+                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass));
     else
         SKM_LAUNCH(b, k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
                            tmp_hi(b, pass), tmp_lo(b, pass));
@@ -7287,7 +7135,6 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "giant_passes" ? &t.giant_passes
                : n == "heavy_lsd" ? &t.heavy_lsd
                : n == "prefetch" ? &t.prefetch
-               : n == "emit_elems" ? &t.emit_elems
                : n == "overflow_grid" ? &t.ovf_grid
                : n == "split_grid" ? &t.split_grid
                : n == "chain_grid" ? &t.chain_grid

@@ -90,8 +90,7 @@ def test_overflow_inline_chains(skm, gpu, inline_min):
                                                    (4, 8, {"side_cus": 64}),
                                                    (4, 8, {"overlap": 1}), (16, 8, {"overlap": 1}),
                                                    (4, 8, {"overlap": 1, "serial_overflow": 1}),
-                                                   (4, 8, {"lane_long": 0}), (16, 8, {"lane_long": 600}),
-                                                   (4, 8, {"emit_elems": 0}), (16, 8, {"emit_elems": 0, "stage_round": 0})])
+                                                   (4, 8, {"lane_long": 0}), (16, 8, {"lane_long": 600})])
 def test_key_range_passes(skm, gpu, passes, long_class, opts):
     """Out-of-core build: P passes over disjoint k-mer ranges (each k-mer in exactly one pass)
     give the single-pass result bit for bit, overflow sub-buckets and chains included, and a
@@ -101,9 +100,7 @@ def test_key_range_passes(skm, gpu, passes, long_class, opts):
     partition_round 1, 2: rounds of 4096 with 512 / 1024 threads), flag_check, serial_overflow, chain_cus / side_cus (the long-chain / overflow
     and selection streams on a subset of the CUs), overlap 1 (pipelined passes: a second element
     buffer set, the pass's overflow path beside the next pass), lane_long 0 / 600 (every stashed long
-    chain on a wave pair / the ones of >= 600 samples: the others one lane each, k_chains), emit_elems 0
-    (k_pass_emit writes window positions and the staged scatter gathers the windows, round 4's
-    path, instead of finished elements)."""
+    chain on a wave pair / the ones of >= 600 samples: the others one lane each, k_chains)."""
     p = synth.generate_arrays(60000, 60, per_file=2000, seed=6)
     r, o, l, f, i, funcs = synth.build_inputs(p)
     ref = oracle_ref.build(r, o, l, f, i, len(funcs))
