@@ -7100,8 +7100,9 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                 }
             SKM_HIP(hipExtStreamCreateWithCUMask(&x, (uint32_t)mask.size(), mask.data()));
         };
-        if (n == "chain_cus") {
+        if (n == "chain_cus") {  // the wave-pair chains' stream and the per-lane stash streams
             remake(b->chain_st);
+            for (int k = 0; k < skm_build::LANE_ST; ++k) remake(b->lane_st[k]);
             t.chain_cus = (int)value;
         } else {
             remake(b->stream2);
