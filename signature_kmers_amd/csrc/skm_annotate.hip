@@ -7,8 +7,8 @@
 //   k_lookup   one thread per 16 windows: window validity (no 'X'/'*' in the window or the byte
 //              after it), jenkins lookup2 -> 3 vertices -> 2-bit g -> rank (popcount over u32
 //              words of g) -> 10-byte record gather; writes func<<16|mean per window position
-//   k_calls_scan   one thread per query sequence: the HitSet state machine over its window hits,
-//              emitting one segment per HitSet::process
+//   k_calls_scan_wave   one wave per query sequence: the HitSet state machine over its window
+//              hits (runs of one function walked in bulk), one segment per HitSet::process
 //   k_seg_process  one wave per segment: statistics (Boost.Math mean / median / MAD) in LDS,
 //              the length test, the KmerCall
 //   scan + k_gather   CSR compaction of the calls
@@ -304,80 +304,11 @@ __device__ void hitset_process(const CallArgs& A, const uint32_t* hit, uint16_t*
     }
 }
 
-// HitSet state machine (call_functions.tcc:259-338), thread per sequence.  Each HitSet::process
-// event becomes a segment {sequence, first window, last window, current function}; the
-// statistics of a segment never feed back into the state machine, so they run afterwards one
-// wave per segment (k_seg_process) instead of divergently inside this loop.
-__global__ void k_calls_scan(CallArgs A, uint4* __restrict__ segs) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= A.nseq) return;
-    const QMeta m = A.meta[s];
-    const uint32_t nwin = m.len >= 8 ? m.len - 7 : 0;
-    const uint32_t* hit = A.hits + m.pstart;
-    uint4* out = segs + A.cap_off[s];
-    uint32_t nseg = 0;
-    // HitSet: all usable hits in window range [first, last_pos]; pair = (prev, last); ncur = the
-    // hits of the current function (HitSet::process's fI_count).  A process() event with
-    // ncur < min_hits emits no call (call_functions.tcc:60), so it yields no segment.
-    uint32_t count = 0, ncur = 0, first = 0, last_pos = 0, prev_pos = 0, last_f = 0, prev_f = 0, cur = 0xFFFFu;
-    auto process = [&]() {
-        if ((int)ncur >= A.min_hits) out[nseg++] = make_uint4(s, first, last_pos, cur);
-        if (prev_f != cur && prev_f == last_f) {
-            cur = prev_f;
-            first = prev_pos;
-            count = 2;
-            ncur = 2;  // the kept pair has the new current function
-        } else {
-            count = 0;
-            ncur = 0;
-        }
-    };
-    // the next 16 hits are loaded while these 16 are walked (the walk is a per-thread chain;
-    // the loads of one thread are 64 contiguous bytes)
-    uint32_t nb[16];
-#pragma unroll
-    for (uint32_t k = 0; k < 16; ++k) nb[k] = k < nwin ? hit[k] : NO_HIT;
-    for (uint32_t i0 = 0; i0 < nwin; i0 += 16) {
-        uint32_t hb[16];
-#pragma unroll
-        for (uint32_t k = 0; k < 16; ++k) hb[k] = nb[k];
-        if (i0 + 16 < nwin) {
-#pragma unroll
-            for (uint32_t k = 0; k < 16; ++k) nb[k] = i0 + 16 + k < nwin ? hit[i0 + 16 + k] : NO_HIT;
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < 16; ++k) {
-            const uint32_t h = hb[k], i = i0 + k;
-            if (!usable(h, A)) continue;
-            const uint32_t f = h >> 16;
-            if (count > 0 && (uint64_t)last_pos + (uint64_t)A.max_gap < (uint64_t)i) {
-                if ((int)count >= A.min_hits) {
-                    process();
-                } else {
-                    count = 0;
-                    ncur = 0;
-                }
-            }
-            if (count == 0) {
-                cur = f;
-                first = i;
-            }
-            prev_pos = last_pos;
-            prev_f = last_f;
-            last_pos = i;
-            last_f = f;
-            ++count;
-            ncur += f == cur;
-            if (count > 1 && cur != f && prev_f == f) process();
-        }
-    }
-    if ((int)count >= A.min_hits && (int)ncur >= A.min_hits) out[nseg++] = make_uint4(s, first, last_pos, cur);
-    A.counts[s] = nseg;
-}
-
-// The same state machine, one wave per sequence (the default since round 5).  The thread-per-
-// sequence form ran each wave as long as its longest sequence and walked every hit serially.
-// Here lanes take 64 windows at a time (one coalesced load) and split the usable hits into
+// HitSet state machine (call_functions.tcc:259-338), one wave per query sequence.  Each
+// HitSet::process event becomes a segment {sequence, first window, last window, current
+// function}; the statistics of a segment never feed back into the state machine, so they run
+// afterwards one wave per segment (k_seg_process).  (Round 4 ran one thread per sequence: each
+// wave as long as its longest sequence, every hit walked serially.)  Lanes take 64 windows at a time (one coalesced load) and split the usable hits into
 // RUNS: maximal chains of consecutive usable hits with one function and no gap > max_gap.
 // Only a run's first two hits can change the state machine's course (gap check, a new current
 // function, the process() trigger); after its second hit cur == the run's function, so its
@@ -394,7 +325,10 @@ __global__ __launch_bounds__(256) void k_calls_scan_wave(CallArgs A, uint4* __re
     uint4* out = segs + A.cap_off[s];
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
     uint32_t nseg = 0;
-    // wave-uniform state of the reference's loop (see k_calls_scan)
+    // wave-uniform state of the reference's loop: all usable hits in window range [first,
+    // last_pos]; pair = (prev, last); ncur = the hits of the current function (HitSet::process's
+    // fI_count).  A process() event with ncur < min_hits emits no call (call_functions.tcc:60),
+    // so it yields no segment.
     uint32_t count = 0, ncur = 0, first = 0, last_pos = 0, prev_pos = 0, last_f = 0, prev_f = 0, cur = 0xFFFFu;
     bool seen = false;   // a usable hit has been seen (last_pos / last_f hold it)
     uint32_t run_k = 0;  // hits of the run that the last usable hit belongs to, so far
