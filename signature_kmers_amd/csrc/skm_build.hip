@@ -5555,7 +5555,10 @@ void size_arena(skm_build* b) {
     // the work buffers are allocated by now (alloc_caps); keep 32 B per element of the largest pass
     // in reserve for a redo that grows them (and for the received buffers at world > 1)
     const uint64_t reserve = b->pass_max * 32 + (1ull << 30);
-    const uint64_t avail = fr > reserve ? fr - reserve : 0;
+    // a re-prepare (an option set after a run) reuses the arena it already holds: its bytes are
+    // free for this plan too (counting them as used shrank the cap below the kept count)
+    const uint64_t held = (uint64_t)b->d_keys.bytes + (uint64_t)b->d_data.bytes;
+    const uint64_t avail = fr + held > reserve ? fr + held - reserve : 0;
     uint64_t cap = std::min<uint64_t>(b->valid_total + 16, avail / (8 + sizeof(skm_stored_kmer_data)));
     if (b->tune.mem_budget_mb > 0) {
         const uint64_t budget = (uint64_t)b->tune.mem_budget_mb << 20;
