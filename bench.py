@@ -317,6 +317,7 @@ def main():
         "prepare_seconds": prep_s,
     }
     out["chain_tail_ms"] = head["chain_tail_ms"]
+    out["giant_chains"] = head["giant_chains"]
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         n = a.seqs_total // max(1, a.cpu_shard_div)
         log(f"CPU baseline: first {n:,} proteins (1/{a.cpu_shard_div} shard of C3)")
@@ -525,6 +526,12 @@ def _measure(skm, b, steps, warmup, shard, world, dist):
                      "kernels_ms_per_step": {k: round(v[0], 2) for k, v in top},
                      "largest_gpu_time": largest},
         "chain_tail_ms": phase.get("chain_tail"),
+        # the run's first giant-chain launch (k_heavy's chains of >= 2^giant_class samples; with
+        # route_first the heavy-only pass 0's): start / end from the step's start, rank 0
+        "giant_chains": None if phase.get("giant_start", -1) < 0 else {
+            "start_ms": phase["giant_start"], "end_ms": phase["giant_end"],
+            "chains": ctrs.get("giant_chains"), "longest_samples": ctrs.get("giant_max"),
+            "routed_occurrences": ctrs.get("routed")},
         "pipeline": {"alg_bytes": pipe_alg, "ms": 1000.0 * t_max / steps, "GBs": pipe_gbs,
                      "frac": pipe_gbs / HBM_PEAK_GBS / max(1, world), "phase_ms_rank0": phase},
     }

@@ -123,7 +123,10 @@ int skm_build_run(skm_build* b);
  * returns entries written. */
 int skm_build_last_timings(skm_build* b, float* ms, int cap);
 /* [12] of skm_build_last_timings: the long-chain tail -- device time from the end of the last
- * key-range pass on the group-by stream until the last stashed P^2 / variance chain is done. */
+ * key-range pass on the group-by stream until the last stashed P^2 / variance chain is done.
+ * [13], [14]: the start and end of the run's first giant-chain launch (k_heavy's chains of
+ * >= 2^giant_class samples; with route_first the heavy-only pass 0's), in ms from the run's
+ * start; -1 when no giant chain ran. */
 /* Per-kernel device time (diagnostics and the bench's roofline): with enable != 0 every kernel
  * launch of a run -- or only the launches of the kernel named `only` (e.g. "k_bucket_process";
  * NULL = all) -- is bracketed by an event pair on its stream, and after the run's host

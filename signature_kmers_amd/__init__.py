@@ -303,10 +303,10 @@ class SignatureBuilder:
         _check(lib().skm_build_run(self._h))
 
     def timings(self) -> dict:
-        ms = (C.c_float * 13)()
-        n = lib().skm_build_last_timings(self._h, ms, 13)
+        ms = (C.c_float * 15)()
+        n = lib().skm_build_last_timings(self._h, ms, 15)
         names = ["extract_count", "scan", "extract_scatter", "bucket_process", "overflow", "chains", "stats", "total",
-                 "exchange", "partition", "bucket_kernel", "big_groups", "chain_tail"]
+                 "exchange", "partition", "bucket_kernel", "big_groups", "chain_tail", "giant_start", "giant_end"]
         return {names[i]: float(ms[i]) for i in range(n)}
 
     def set_kernel_timing(self, enable: bool, only: str | None = None):

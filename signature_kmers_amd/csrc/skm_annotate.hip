@@ -7,8 +7,8 @@
 //   k_lookup   one thread per 16 windows: window validity (no 'X'/'*' in the window or the byte
 //              after it), jenkins lookup2 -> 3 vertices -> 2-bit g -> rank (popcount over u32
 //              words of g) -> 10-byte record gather; writes func<<16|mean per window position
-//   k_calls_scan_wave   one wave per query sequence: the HitSet state machine over its window
-//              hits (runs of one function walked in bulk), one segment per HitSet::process
+//   k_calls_scan   one thread per query sequence: the HitSet state machine over its window hits,
+//              emitting one segment per HitSet::process
 //   k_seg_process  one wave per segment: statistics (Boost.Math mean / median / MAD) in LDS,
 //              the length test, the KmerCall
 //   scan + k_gather   CSR compaction of the calls
@@ -304,129 +304,75 @@ __device__ void hitset_process(const CallArgs& A, const uint32_t* hit, uint16_t*
     }
 }
 
-// HitSet state machine (call_functions.tcc:259-338), one wave per query sequence.  Each
-// HitSet::process event becomes a segment {sequence, first window, last window, current
-// function}; the statistics of a segment never feed back into the state machine, so they run
-// afterwards one wave per segment (k_seg_process).  (Round 4 ran one thread per sequence: each
-// wave as long as its longest sequence, every hit walked serially.)  Lanes take 64 windows at a time (one coalesced load) and split the usable hits into
-// RUNS: maximal chains of consecutive usable hits with one function and no gap > max_gap.
-// Only a run's first two hits can change the state machine's course (gap check, a new current
-// function, the process() trigger); after its second hit cur == the run's function, so its
-// remaining hits just add to count / ncur and move last_pos / prev_pos -- applied in bulk from
-// ballot masks.  The wave walks the "special" hits (run index 0 or 1) in order with
-// wave-uniform scalar state; segments are written by lane 0.
-__global__ __launch_bounds__(256) void k_calls_scan_wave(CallArgs A, uint4* __restrict__ segs) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t s = blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (s >= A.nseq) return;  // wave-uniform
+// HitSet state machine (call_functions.tcc:259-338), thread per sequence.  Each HitSet::process
+// event becomes a segment {sequence, first window, last window, current function}; the
+// statistics of a segment never feed back into the state machine, so they run afterwards one
+// wave per segment (k_seg_process) instead of divergently inside this loop.
+__global__ void k_calls_scan(CallArgs A, uint4* __restrict__ segs) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= A.nseq) return;
     const QMeta m = A.meta[s];
     const uint32_t nwin = m.len >= 8 ? m.len - 7 : 0;
     const uint32_t* hit = A.hits + m.pstart;
     uint4* out = segs + A.cap_off[s];
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
     uint32_t nseg = 0;
-    // wave-uniform state of the reference's loop: all usable hits in window range [first,
-    // last_pos]; pair = (prev, last); ncur = the hits of the current function (HitSet::process's
-    // fI_count).  A process() event with ncur < min_hits emits no call (call_functions.tcc:60),
-    // so it yields no segment.
+    // HitSet: all usable hits in window range [first, last_pos]; pair = (prev, last); ncur = the
+    // hits of the current function (HitSet::process's fI_count).  A process() event with
+    // ncur < min_hits emits no call (call_functions.tcc:60), so it yields no segment.
     uint32_t count = 0, ncur = 0, first = 0, last_pos = 0, prev_pos = 0, last_f = 0, prev_f = 0, cur = 0xFFFFu;
-    bool seen = false;   // a usable hit has been seen (last_pos / last_f hold it)
-    uint32_t run_k = 0;  // hits of the run that the last usable hit belongs to, so far
-    auto emit = [&](uint32_t a, uint32_t b, uint32_t c) {
-        if (lane == 0) out[nseg] = make_uint4(s, a, b, c);
-        ++nseg;
-    };
     auto process = [&]() {
-        if ((int)ncur >= A.min_hits) emit(first, last_pos, cur);
+        if ((int)ncur >= A.min_hits) out[nseg++] = make_uint4(s, first, last_pos, cur);
         if (prev_f != cur && prev_f == last_f) {
             cur = prev_f;
             first = prev_pos;
             count = 2;
-            ncur = 2;
+            ncur = 2;  // the kept pair has the new current function
         } else {
             count = 0;
             ncur = 0;
         }
     };
-    auto step = [&](uint32_t i, uint32_t f) {  // one usable hit through the full state machine
-        if (count > 0 && (uint64_t)last_pos + (uint64_t)A.max_gap < (uint64_t)i) {
-            if ((int)count >= A.min_hits) {
-                process();
-            } else {
-                count = 0;
-                ncur = 0;
+    // the next 16 hits are loaded while these 16 are walked (the walk is a per-thread chain;
+    // the loads of one thread are 64 contiguous bytes)
+    uint32_t nb[16];
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) nb[k] = k < nwin ? hit[k] : NO_HIT;
+    for (uint32_t i0 = 0; i0 < nwin; i0 += 16) {
+        uint32_t hb[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) hb[k] = nb[k];
+        if (i0 + 16 < nwin) {
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) nb[k] = i0 + 16 + k < nwin ? hit[i0 + 16 + k] : NO_HIT;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t h = hb[k], i = i0 + k;
+            if (!usable(h, A)) continue;
+            const uint32_t f = h >> 16;
+            if (count > 0 && (uint64_t)last_pos + (uint64_t)A.max_gap < (uint64_t)i) {
+                if ((int)count >= A.min_hits) {
+                    process();
+                } else {
+                    count = 0;
+                    ncur = 0;
+                }
             }
+            if (count == 0) {
+                cur = f;
+                first = i;
+            }
+            prev_pos = last_pos;
+            prev_f = last_f;
+            last_pos = i;
+            last_f = f;
+            ++count;
+            ncur += f == cur;
+            if (count > 1 && cur != f && prev_f == f) process();
         }
-        if (count == 0) {
-            cur = f;
-            first = i;
-        }
-        prev_pos = last_pos;
-        prev_f = last_f;
-        last_pos = i;
-        last_f = f;
-        ++count;
-        ncur += f == cur;
-        if (count > 1 && cur != f && prev_f == f) process();
-    };
-    uint32_t hn = lane < nwin ? hit[lane] : NO_HIT;
-    for (uint32_t c0 = 0; c0 < nwin; c0 += 64) {
-        const uint32_t h = hn;
-        if (c0 + 64 < nwin) hn = c0 + 64 + lane < nwin ? hit[c0 + 64 + lane] : NO_HIT;
-        const bool u = usable(h, A);
-        const uint32_t f = h >> 16;
-        const uint64_t U = __ballot(u);
-        if (!U) continue;  // wave-uniform
-        // the previous usable hit (in this chunk, else the carried one) and run heads
-        const uint64_t below = U & lt;
-        const int p = below ? 63 - __clzll((long long)below) : -1;
-        const uint32_t pf_in = (uint32_t)__shfl((int)f, p >= 0 ? p : 0, 64);
-        const bool has_prev = p >= 0 || seen;
-        const uint32_t pf = p >= 0 ? pf_in : last_f;
-        const uint32_t pi = p >= 0 ? c0 + (uint32_t)p : last_pos;
-        const uint32_t i = c0 + lane;
-        const bool head = u && (!has_prev || pf != f || (uint64_t)pi + (uint64_t)A.max_gap < (uint64_t)i);
-        const uint64_t H = __ballot(head);
-        // index of each usable hit within its run
-        const uint64_t hle = H & (lt | (1ull << lane));
-        uint32_t k;
-        if (hle) {
-            const int hl = 63 - __clzll((long long)hle);
-            k = (uint32_t)__popcll(U & lt & ~((1ull << hl) - 1ull));
-        } else {
-            k = run_k + (uint32_t)__popcll(U & lt);
-        }
-        const uint64_t SP = __ballot(u && k <= 1u);
-        const uint64_t PL = U & ~SP;  // plain hits: the third and later of their run
-        uint32_t from = 0;            // lanes below `from` are applied
-        auto apply_plain = [&](uint32_t to) {  // the plain hits of lanes [from, to)
-            if (from >= 64) return;  // (a shift by 64 is undefined)
-            const uint64_t span = (to >= 64 ? ~0ull : ((1ull << to) - 1ull)) & ~((1ull << from) - 1ull);
-            const uint64_t M = PL & span;
-            if (!M) return;
-            const uint32_t c = (uint32_t)__popcll(M);
-            const int a = 63 - __clzll((long long)M);
-            const uint64_t M2 = M & ~(1ull << a);
-            prev_pos = M2 ? c0 + (uint32_t)(63 - __clzll((long long)M2)) : last_pos;
-            last_pos = c0 + (uint32_t)a;
-            prev_f = last_f;  // the run's function (cur == it after the run's second hit)
-            count += c;
-            ncur += c;
-        };
-        for (uint64_t sp = SP; sp;) {
-            const int q = __ffsll((long long)sp) - 1;
-            sp &= sp - 1;
-            apply_plain((uint32_t)q);
-            step(c0 + (uint32_t)q, (uint32_t)__builtin_amdgcn_readlane((int)f, q));
-            from = (uint32_t)q + 1;
-        }
-        apply_plain(64);
-        const int lu = 63 - __clzll((long long)U);
-        run_k = (uint32_t)__builtin_amdgcn_readlane((int)k, lu) + 1u;
-        seen = true;
     }
-    if ((int)count >= A.min_hits && (int)ncur >= A.min_hits) emit(first, last_pos, cur);
-    if (lane == 0) A.counts[s] = nseg;
+    if ((int)count >= A.min_hits && (int)ncur >= A.min_hits) out[nseg++] = make_uint4(s, first, last_pos, cur);
+    A.counts[s] = nseg;
 }
 
 // dense segment list: segments of sequence s at seg_off[s]..
@@ -1058,7 +1004,7 @@ void query_run(skm_query* q, const skm_annot_opts* o) {
         A.mad_mode = o->mad_mode;
         A.hypo = o->hypo_index >= 0 ? (uint32_t)o->hypo_index : 0xFFFFFFFFu;
         SKM_HIP(hipEventRecord(q->ev[2], st));
-        hipLaunchKernelGGL(k_calls_scan_wave, dim3(ceil_div(ns, 4)), dim3(256), 0, st, A, q->d_slots.as<uint4>());
+        hipLaunchKernelGGL(k_calls_scan, dim3(ceil_div(ns, 64)), dim3(64), 0, st, A, q->d_slots.as<uint4>());
         SKM_HIP(hipGetLastError());
         q->scan.run(q->d_counts.as<uint32_t>(), ns, q->d_seg_off.as<uint64_t>(), st);
         uint64_t nseg = 0;

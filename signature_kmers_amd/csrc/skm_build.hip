@@ -1565,6 +1565,7 @@ constexpr int BLOOM_BITS = 18;      // Bloom filter of the heavy keys: 2^18 bits
                                     // (C3: ~2*10^4 routed keys -> ~2 % false positives, harmless light
                                     // keys routed too)
 constexpr int ROUTE_SAMPLE = 6;     // 1 in 2^6 window positions are sampled
+constexpr uint32_t ROUTE_FIRST = 0x80000000u;  // k_pass_ids' vac flag: a heavy-only first pass
 
 __device__ __forceinline__ uint32_t cms_slot(uint64_t h, int row) {
     return row == 0 ? (uint32_t)(h & ((1u << CMS_BITS) - 1u)) : (uint32_t)((h >> 21) & ((1u << CMS_BITS) - 1u));
@@ -1672,7 +1673,11 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
     __syncthreads();
     const uint32_t half = pass_bits >= 1 ? 1u << (pass_bits - 1) : 0u;
     // routing vacates the last R passes: R = half (vac 0) maps pass p to p - P/2; any other R
-    // spreads the heavy keys of the last R passes over the first P - R by 16 hash bits
+    // spreads the heavy keys of the last R passes over the first P - R by 16 hash bits.
+    // vac & ROUTE_FIRST: pass 0 holds the heavy keys only -- every heavy key goes to pass 0 and
+    // the light keys of pass 0 spread over passes 1 .. P-1 by 16 hash bits
+    const bool first = (vac & ROUTE_FIRST) != 0;
+    vac &= ~ROUTE_FIRST;
     const uint32_t R = vac ? min(vac, (1u << pass_bits) - 1u) : half, keep = (1u << pass_bits) - R;
     const uint64_t nchunk = (rp + 15) >> 4;
     const uint64_t c0 = rows ? ((uint64_t)blockIdx.x * span >> 4) + threadIdx.x : (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1706,8 +1711,14 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
                     if (counts) atomicAdd(&s_cnt[(uint32_t)(h >> (KEY_BITS - 6))], 1u);
                 } else {
                     id = pass_bits ? (uint32_t)(h >> (KEY_BITS - pass_bits)) : 0u;
-                    if (route && id >= keep && bloom_has(s_bloom, h))
+                    if (route && first) {
+                        if (bloom_has(s_bloom, h))
+                            id = 0;
+                        else if (id == 0)
+                            id = 1u + (uint32_t)(((uint32_t)(h & 0xFFFFu) * ((1u << pass_bits) - 1u)) >> 16);
+                    } else if (route && id >= keep && bloom_has(s_bloom, h)) {
                         id = R == half ? id - half : (uint32_t)(((uint32_t)(h & 0xFFFFu) * keep) >> 16);
+                    }
                     if (tally) {
                         const uint32_t own = (uint32_t)(h >> (KEY_BITS - pass_bits - owner_bits)) & ((1u << owner_bits) - 1u);
                         atomicAdd(&s_cnt[(id << owner_bits) | own], 1u);
@@ -4769,6 +4780,11 @@ struct Tune {
     int chain_streams = 1;           //   over this many streams (1..4)
     int poison_jobs = 0;             // tests: every slot of the run's long-job list starts as a canary job
     int route_vacate = 0;            // routing: the last this many passes hold no heavy key (0: half)
+    // routing: pass 0 holds only the heavy keys, so their chains start a heavy-only pass into the
+    // step (-1, the default: on at world > 1, where one or two passes per rank would otherwise
+    // start the heaviest chain half a step in -- the pass count is doubled below four passes;
+    // 0: off; 1: on)
+    int route_first = -1;
     int route_heavy_min = 1 << 14;   // key-range passes: k-mers of >= this many occurrences are routed into
                                      //   the first half of the passes (0: off; k_pass_ids)
     int overlap = 0;                 // key-range passes, one GPU: pipelined passes (a second element set)
@@ -4823,7 +4839,7 @@ struct skm_build {
     hipEvent_t* ev = nullptr;           // the current pass's set
     hipEvent_t* ev_o = nullptr;
     hipEvent_t* ev_o3 = nullptr;
-    float last_ms[13] = {};
+    float last_ms[15] = {};
     uint64_t ovf_elems = 0, ovf_kept = 0;
 
     // host staging (reference emission order, only sequences with a kept function)
@@ -4935,7 +4951,8 @@ struct skm_build {
     DevBuf d_bloom;                     // heavy-key routing filter (route)
     std::vector<uint64_t> cnt64;        // valid windows by the top 6 hash bits (size_passes)
     bool route = false;
-    uint64_t routed = 0;                // occurrences routed into the first half of the passes
+    bool route_first = false;           // routing into a heavy-only pass 0 (route_plan; every rank alike)
+    uint64_t routed = 0;                // occurrences routed into the first half of the passes (or pass 0)
     // the window positions and level-1 histograms of a group of emit_g passes (k_pass_emit: one
     // residue scan per group), in emit_g slots; the next group's scan runs on stx once the group's
     // last pass has staged its elements (ev_staged), beside that pass's group-by
@@ -5008,6 +5025,8 @@ struct skm_build {
     std::vector<uint64_t> kt_n;
     // the long-chain tail: from the end of the last pass on the group-by stream to the last chain
     hipEvent_t ev_tail[2] = {};
+    hipEvent_t ev_giant[2] = {};        // the run's first giant-chain launch: start, end (timings [13], [14])
+    bool giant_timed = false;
 };
 
 namespace {
@@ -5574,6 +5593,15 @@ void size_arena(skm_build* b) {
 void alloc_caps(skm_build* b);
 void pass_peer_counts(const Ranks& bs);
 
+// the heavy-only first pass (option route_first): asked for by default at world > 1
+bool route_first_on(const skm_build* b) {
+    return b->tune.route_first > 0 || (b->tune.route_first < 0 && b->world > 1);
+}
+// k_pass_ids' routing argument: the vacated pass count, or ROUTE_FIRST (as route_plan agreed)
+uint32_t route_arg(const skm_build* b) {
+    return b->route_first ? ROUTE_FIRST : (uint32_t)std::max(0, b->tune.route_vacate);
+}
+
 // Heavy-key routing plan, after the ranks agreed on the pass count (one GPU: at least 4 passes;
 // world > 1: at least 2).  Every rank sketches 1/64 of its windows into a count-min sketch; at
 // world > 1 the sketches are summed over the ranks (all-reduce, 32 MB), so a key's estimate is
@@ -5585,19 +5613,28 @@ void pass_peer_counts(const Ranks& bs);
 // no longer fits turns routing off on every rank (the ranks must route alike).
 void route_plan(const Ranks& bs) {
     skm_build* b0 = bs[0];
-    const int pb = b0->pass_bits, W = b0->world;
+    int pb = b0->pass_bits;
+    const int W = b0->world;
     for (auto* b : bs) {
         b->route = false;
+        b->route_first = false;
         b->routed = 0;
     }
-    uint64_t want = (pb >= (W > 1 ? 1 : 2) && b0->tune.route_heavy_min > 0) ? 1u : 0u;
-    {   // the option is per handle: route only if every rank asks for it
-        std::vector<uint64_t> mine(bs.size(), want);
-        for (size_t k = 0; k < bs.size(); ++k) mine[k] = (pb >= (W > 1 ? 1 : 2) && bs[k]->tune.route_heavy_min > 0) ? 1u : 0u;
+    // bit 0: route; bit 1: into a heavy-only pass 0 (from one pass up: the pass count is doubled)
+    auto wish = [&](const skm_build* b) -> uint64_t {
+        const bool first = route_first_on(b);
+        if (b->tune.route_heavy_min <= 0 || pb < (first ? (W > 1 ? 1 : 0) : (W > 1 ? 1 : 2))) return 0u;
+        return first ? 3u : 1u;
+    };
+    uint64_t want = 3u;
+    {   // the options are per handle: route (first) only if every rank asks for it
+        std::vector<uint64_t> mine(bs.size());
+        for (size_t k = 0; k < bs.size(); ++k) mine[k] = wish(bs[k]);
         const std::vector<uint64_t> all = W > 1 ? allgather_u64(bs, mine) : mine;
         for (auto v : all) want &= v;
     }
-    if (!want) return;
+    if (!(want & 1u)) return;
+    const bool first = (want & 2u) != 0;
     const size_t ncms = 2ull << CMS_BITS, nbl = 1ull << BLOOM_BITS;
     std::vector<DevBuf> cms(bs.size()), bl8(bs.size());
     std::vector<void*> pc, pb8;
@@ -5625,45 +5662,78 @@ void route_plan(const Ranks& bs) {
         SKM_HIP(hipGetLastError());
     }
     if (W > 1) allreduce(bs, pb8, nbl, Red::MaxU8);
-    std::vector<uint64_t> ok(bs.size(), 1);
-    std::vector<uint64_t> routed_m(bs.size()), routed_n(bs.size());
     for (size_t k = 0; k < bs.size(); ++k) {
         skm_build* b = bs[k];
+        b->route_first = first;  // route_arg
         b->d_bloom.ensure(nbl / 8);
         hipLaunchKernelGGL(k_bloom_pack, dim3((uint32_t)(nbl / 32 + 255) / 256), dim3(256), 0, b->stream,
                            bl8[k].as<uint8_t>(), b->d_bloom.as<uint32_t>());
-        // the routed pass sizes of this shard
-        const uint32_t P = 1u << pb;
-        DevBuf d_cnt;
-        d_cnt.ensure(8 * 64);
-        SKM_HIP(hipMemsetAsync(d_cnt.p, 0, 8 * 64, b->stream));
-        if (b->rp)
-            hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 4u * 64 + (uint32_t)(nbl / 8), b->stream,
-                               b->d_res.as<uint8_t>(), b->rp, pb, 0, nullptr, d_cnt.as<unsigned long long>(),
-                               b->d_bloom.as<uint32_t>(), 64u, nullptr, 0, (uint32_t)std::max(0, b->tune.route_vacate));
         SKM_HIP(hipGetLastError());
-        uint64_t cnt[64];
-        SKM_HIP(hipMemcpyAsync(cnt, d_cnt.p, sizeof(cnt), hipMemcpyDeviceToHost, b->stream));
-        SKM_HIP(hipStreamSynchronize(b->stream));
-        const int R = b->tune.route_vacate > 0 ? std::min(b->tune.route_vacate, (int)P - 1) : (int)(P >> 1);
-        uint64_t natural_late = 0, late = 0, m = 0;  // occurrences of the vacated passes before / after routing
-        for (int p = (int)P - R; p < (int)P; ++p) {
-            for (int i = 0; i < (64 >> pb); ++i) natural_late += b->cnt64[p * (64 >> pb) + i];
-            late += cnt[p];
+    }
+    std::vector<uint64_t> ok(bs.size(), 1), heavy(bs.size(), 0);
+    std::vector<uint64_t> routed_m(bs.size()), routed_n(bs.size());
+    // the routed pass sizes of every shard at pass_bits pb
+    auto count_routed = [&]() {
+        for (size_t k = 0; k < bs.size(); ++k) {
+            skm_build* b = bs[k];
+            const uint32_t P = 1u << pb;
+            DevBuf d_cnt;
+            d_cnt.ensure(8 * 64);
+            SKM_HIP(hipMemsetAsync(d_cnt.p, 0, 8 * 64, b->stream));
+            if (b->rp)
+                hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 4u * 64 + (uint32_t)(nbl / 8), b->stream,
+                                   b->d_res.as<uint8_t>(), b->rp, pb, 0, nullptr, d_cnt.as<unsigned long long>(),
+                                   b->d_bloom.as<uint32_t>(), 64u, nullptr, 0, route_arg(b));
+            SKM_HIP(hipGetLastError());
+            uint64_t cnt[64];
+            SKM_HIP(hipMemcpyAsync(cnt, d_cnt.p, sizeof(cnt), hipMemcpyDeviceToHost, b->stream));
+            SKM_HIP(hipStreamSynchronize(b->stream));
+            const int R = b->tune.route_vacate > 0 ? std::min(b->tune.route_vacate, (int)P - 1) : (int)(P >> 1);
+            uint64_t natural_late = 0, late = 0, m = 0;  // occurrences of the vacated passes before / after routing
+            if (first) {
+                natural_late = cnt[0];  // the heavy-only pass
+            } else {
+                for (int p = (int)P - R; p < (int)P; ++p) {
+                    for (int i = 0; i < (64 >> pb); ++i) natural_late += b->cnt64[p * (64 >> pb) + i];
+                    late += cnt[p];
+                }
+            }
+            for (uint32_t p = 0; p < P; ++p) m = std::max<uint64_t>(m, cnt[p]);
+            size_t fr = 0, tot = 0;
+            SKM_HIP(hipMemGetInfo(&fr, &tot));
+            const uint64_t budget = b->tune.mem_budget_mb > 0 ? (uint64_t)b->tune.mem_budget_mb << 20 : (uint64_t)fr;
+            const bool forced = b->tune.passes > 0;
+            ok[k] = m < (1ull << 32) - (1ull << 28) && (forced || m <= b->pass_max || work_fits(pass_work(m, pb, b->rp), budget));
+            routed_m[k] = m;
+            routed_n[k] = natural_late - late;
+            heavy[k] = first ? cnt[0] : 0;
         }
-        for (uint32_t p = 0; p < P; ++p) m = std::max<uint64_t>(m, cnt[p]);
-        size_t fr = 0, tot = 0;
-        SKM_HIP(hipMemGetInfo(&fr, &tot));
-        const uint64_t budget = b->tune.mem_budget_mb > 0 ? (uint64_t)b->tune.mem_budget_mb << 20 : (uint64_t)fr;
-        const bool forced = b->tune.passes > 0;
-        ok[k] = m < (1ull << 32) - (1ull << 28) && (forced || m <= b->pass_max || work_fits(pass_work(m, pb, b->rp), budget));
-        routed_m[k] = m;
-        routed_n[k] = natural_late - late;
+    };
+    auto turn_off = [&]() {
+        for (auto* b : bs) b->route_first = false;
+    };
+    count_routed();
+    if (first) {
+        // no heavy key on any rank: no heavy-only pass (and no routing)
+        const std::vector<uint64_t> all = W > 1 ? allgather_u64(bs, heavy) : heavy;
+        uint64_t any = 0;
+        for (auto v : all) any |= v;
+        if (!any) return turn_off();
+        // below four passes the light keys of pass 0 would crowd one pass: twice the passes
+        // (size_passes re-counts; the forced pass count of the option stands)
+        if (pb < 2 && b0->tune.passes <= 0 && pb < 6) {
+            ++pb;
+            for (auto* b : bs) {
+                size_passes(b, pb);
+                b->route_first = true;
+            }
+            count_routed();
+        }
     }
     {
         const std::vector<uint64_t> all = W > 1 ? allgather_u64(bs, ok) : ok;
         for (auto v : all)
-            if (!v) return;  // routing off on every rank: the unrouted pass sizes stand
+            if (!v) return turn_off();  // routing off on every rank: the unrouted pass sizes stand
     }
     for (size_t k = 0; k < bs.size(); ++k) {
         bs[k]->pass_max = routed_m[k];
@@ -6005,7 +6075,7 @@ void pass_peer_counts(const Ranks& bs) {
             hipLaunchKernelGGL(k_pass_ids, dim3(1024), dim3(256), 4u * P * W + (b->route ? (1u << BLOOM_BITS) / 8 : 0u),
                                b->stream, b->d_res.as<uint8_t>(), b->rp, b->pass_bits, b->owner_bits, nullptr,
                                cnt.as<unsigned long long>(), b->route ? b->d_bloom.as<uint32_t>() : nullptr, P * W,
-                               nullptr, 0, (uint32_t)std::max(0, b->tune.route_vacate));
+                               nullptr, 0, route_arg(b));
         SKM_HIP(hipGetLastError());
         std::vector<uint64_t> c(P * W), t(P * W);
         SKM_HIP(hipMemcpyAsync(c.data(), cnt.p, 8ull * P * W, hipMemcpyDeviceToHost, b->stream));
@@ -6056,15 +6126,12 @@ void pass_peer_counts(const Ranks& bs) {
 // run's long arena and they run on the chain stream, overlapping the following passes.  The
 // per-lane chains run on st (or st_short) within the pass.  Fixed grids that read the counts on
 // the device: no host round trip.
-// Giant chains (k_heavy's chains of >= 2^class samples start on a chain stream right after it):
-// the option, or by default 14 with one pass (C2: -0.5 ms, the longest P^2 chain is that path's
-// end) and off with key-range passes (C3: +60..80 ms, the FP64 chain waves slow the passes).
 // Giant chains (>= 2^class samples) start on their own streams right after k_heavy instead of
 // waiting for the stash batches.  Default on with one pass, and at world > 1 (verdict r04 #4): the
 // owner split leaves each rank few passes (two at 8 GPUs), routing puts the heaviest k-mers into
 // the first, and their stashed chains would only start after that pass's group-by (~0.08 s of a
 // ~0.2 s step) -- the multi-GPU step's floor.  Off on one GPU with key-range passes, where the
-// stash batches overlap the later passes (measured round 3).
+// stash batches overlap the later passes (C3: +60..80 ms, the FP64 chain waves slow the passes).
 int giant_class(const skm_build* b) {
     return b->tune.giant_class >= 0 ? b->tune.giant_class : (b->pass_bits == 0 || b->world > 1 ? 14 : 0);
 }
@@ -6297,9 +6364,12 @@ void phase_group(skm_build* b, uint32_t pass) {
     if (H.giant_min) {
         SKM_HIP(hipEventRecord(b->gev_ready[gs], st2));
         SKM_HIP(hipStreamWaitEvent(b->gst[gs], b->gev_ready[gs], 0));
+        if (!b->giant_timed) SKM_HIP(hipEventRecord(b->ev_giant[0], b->gst[gs]));
         SKM_LAUNCH(b, k_chain_dyn, dim3(1024), dim3(128), 0, b->gst[gs], H.gjobs, H.gcount, A.out_data,
                            b->tune.chain_prio);
         SKM_HIP(hipGetLastError());
+        if (!b->giant_timed) SKM_HIP(hipEventRecord(b->ev_giant[1], b->gst[gs]));
+        b->giant_timed = true;
         SKM_HIP(hipEventRecord(b->gev_done[gs], b->gst[gs]));
         b->gused[gs] = true;
     }
@@ -6449,6 +6519,7 @@ void begin_run(skm_build* b) {
     alloc_caps(b);
     b->chainq_next = 0;
     b->emit_q = -1;  // no pass group's positions are queued from an earlier (possibly aborted) run
+    b->giant_timed = false;
     SKM_HIP(hipEventRecord(b->ev_start, st));
     SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 3 * 256, st));
     b->ovf_pending[0] = b->ovf_pending[1] = false;
@@ -6467,7 +6538,7 @@ void begin_run(skm_build* b) {
         SKM_LAUNCH(b, k_pass_ids, dim3(SEL_WG), dim3(256), 4u * P + (b->route ? (1u << BLOOM_BITS) / 8 : 0u), st,
                    b->d_res.as<uint8_t>(), b->rp, b->pass_bits, 0, b->d_ids.as<uint8_t>(), nullptr,
                    b->route ? b->d_bloom.as<uint32_t>() : nullptr, P, b->d_selrows.as<uint32_t>(), b->sel_span,
-                   (uint32_t)std::max(0, b->tune.route_vacate));
+                   route_arg(b));
         SKM_LAUNCH(b, k_sel_scan, dim3(P), dim3(1024), 0, st, b->d_selrows.as<uint32_t>(), SEL_WG, P,
                    b->d_seloff.as<uint64_t>(), b->d_npos.as<unsigned long long>(), b->pass_max,
                    b->d_run.as<unsigned long long>());
@@ -6638,6 +6709,11 @@ void phase_final(skm_build* b) {
     SKM_HIP(hipEventElapsedTime(&b->last_ms[6], b->ev[7], b->ev[8]));      // stats (+ reductions)
     SKM_HIP(hipEventElapsedTime(&b->last_ms[7], b->ev_start, b->ev[8]));   // whole run
     SKM_HIP(hipEventElapsedTime(&b->last_ms[12], b->ev_tail[0], b->ev_tail[1]));  // long-chain tail
+    b->last_ms[13] = b->last_ms[14] = -1.0f;  // the first giant chains' start / end from the run's start
+    if (b->giant_timed) {
+        SKM_HIP(hipEventElapsedTime(&b->last_ms[13], b->ev_start, b->ev_giant[0]));
+        SKM_HIP(hipEventElapsedTime(&b->last_ms[14], b->ev_start, b->ev_giant[1]));
+    }
     b->long_samples = R[RUN_LONG_CUR];
     kt_collect(b);
     // run totals for counters() / finish()
@@ -6791,6 +6867,7 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
         SKM_HIP(hipEventCreateWithFlags(&b->ev_main_done[k], hipEventDisableTiming));
     }
     for (auto& e : b->ev_tail) SKM_HIP(hipEventCreate(&e));
+    for (auto& e : b->ev_giant) SKM_HIP(hipEventCreate(&e));
     for (int i = 0; i < 2; ++i) {
         SKM_HIP(hipHostMalloc(reinterpret_cast<void**>(&b->st_pin[i]), STAGE_BYTES, hipHostMallocDefault));
         SKM_HIP(hipEventCreateWithFlags(&b->st_ev[i], hipEventDisableTiming));
@@ -7160,7 +7237,8 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "serial_overflow" ? &t.serial_overflow
                : n == "overlap" ? &t.overlap
                : n == "heavy_grid" ? &t.heavy_grid
-               : n == "route_vacate" ? &t.route_vacate : nullptr;
+               : n == "route_vacate" ? &t.route_vacate
+               : n == "route_first" ? &t.route_first : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")
@@ -7341,7 +7419,7 @@ int skm_build_kernel_timings(skm_build* b, char* names, size_t names_cap, float*
 
 int skm_build_last_timings(skm_build* b, float* ms, int cap) {
     if (!b || !ms) return SKM_E_ARG;
-    int n = std::min(cap, 13);
+    int n = std::min(cap, 15);
     for (int i = 0; i < n; ++i) ms[i] = b->last_ms[i];
     return n;
 }
@@ -7570,6 +7648,8 @@ void skm_build_destroy(skm_build* b) {
         if (b->ev_main_done[k]) (void)hipEventDestroy(b->ev_main_done[k]);
     }
     for (auto& e : b->ev_tail)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : b->ev_giant)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : b->kt_pool) (void)hipEventDestroy(e);
     for (int i = 0; i < 2; ++i) {

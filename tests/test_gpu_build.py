@@ -121,28 +121,39 @@ def test_key_range_passes(skm, gpu, passes, long_class, opts):
     assert c1["overflow_subbuckets"] > 0 and c1["grouped"] == oracle_ref.count_windows(l, f) - _invalid(r, o, l, f)
 
 
-@pytest.mark.parametrize("passes,route_min,vacate", [(4, 256, 0), (16, 64, 0), (64, 1024, 0), (16, 64, 4), (16, 64, 1)])
+@pytest.mark.parametrize("passes,route_min,vacate", [(4, 256, 0), (16, 64, 0), (64, 1024, 0), (16, 64, 4), (16, 64, 1),
+                                                     (4, 256, -1), (64, 1024, -1), (0, 256, -1)])
 def test_heavy_key_routing(skm, gpu, passes, route_min, vacate):
     """Heavy-key routing (route_heavy_min): the k-mers whose sampled occurrence estimate reaches the
     threshold are grouped in the first half of the key-range passes, their elements carrying
     (natural pass ^ routed pass) above the rem bits so the key decodes back -- the kept set is the
-    oracle's bit for bit, and many occurrences were actually routed."""
+    oracle's bit for bit, and many occurrences were actually routed.  vacate = -1: route_first, a
+    heavy-only pass 0 (the light keys of pass 0 spread over the others; passes = 0 -> one pass by
+    the budget, doubled to two)."""
     p = synth.generate_arrays(60000, 60, per_file=2000, seed=6)
     r, o, l, f, i, funcs = synth.build_inputs(p)
     ref = oracle_ref.build(r, o, l, f, i, len(funcs))
     b = skm.SignatureBuilder(len(funcs))
     b.set_option("key_range_passes", passes)
     b.set_option("route_heavy_min", route_min)
-    b.set_option("route_vacate", vacate)  # 0: the second half; else the last `vacate` passes, spread
+    if vacate >= 0:
+        b.set_option("route_vacate", vacate)  # 0: the second half; else the last `vacate` passes, spread
+    else:
+        b.set_option("route_first", 1)
+        b.set_option("giant_class", 8)  # the heavy pass's chains on the giant streams, timed
     b.set_option("main_long_class", 8)
     b.set_option("overflow_long_class", 8)
     b.add_batch(r, o, l, f, i)
     b.run()
     c = b.counters()
+    t = b.timings()
     got = b.finish()
     b.close()
     assert c["routed"] > 100_000, c
     assert c["grouped"] == c["valid"]
+    if vacate < 0:
+        assert c["passes"] == (passes or 2) and c["giant_chains"] > 0, c
+        assert 0 <= t["giant_start"] <= t["giant_end"] <= t["total"], t
     assert_same(got, ref)
 
 
