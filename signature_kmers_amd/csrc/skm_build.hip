@@ -1358,6 +1358,55 @@ __global__ __launch_bounds__(128) void k_chain_long(const Job* __restrict__ jobs
     }
 }
 
+// Giant chains of one pass, longest first: k_heavy appends a key's job when the key is done, so the
+// heaviest keys (the longest reads) come late in the list, and k_chain_dyn's workgroups would
+// start them after a first round of shorter chains.  One workgroup sorts the first GORD_MAX jobs
+// in place by samples, descending (ties by list order): a bitonic network over (~n, index) keys
+// in LDS, then every job moves to its rank.  The order of the chains does not change any result.
+constexpr uint32_t GORD_MAX = 4096;
+__global__ __launch_bounds__(1024) void k_giant_order(Job* __restrict__ jobs, const unsigned long long* __restrict__ njobs) {
+    __shared__ uint64_t s_key[GORD_MAX];
+    __shared__ uint32_t s_pos[GORD_MAX];
+    constexpr uint32_t PER = GORD_MAX / 1024;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nj = (uint32_t)min((unsigned long long)GORD_MAX, *njobs);
+    if (nj < 2) return;  // uniform
+    Job mine[PER];
+#pragma unroll
+    for (uint32_t r = 0; r < PER; ++r) {
+        const uint32_t i = tid + r * 1024u;
+        if (i < nj) mine[r] = jobs[i];
+        s_key[i] = i < nj ? ((uint64_t)(0xFFFFFFFFu - mine[r].n) << 32) | i : ~0ull;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= GORD_MAX; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (uint32_t r = 0; r < PER; ++r) {
+                const uint32_t i = tid + r * 1024u, l = i ^ j;
+                if (l > i) {
+                    const uint64_t a = s_key[i], c = s_key[l];
+                    if (((i & k) == 0) == (a > c)) {
+                        s_key[i] = c;
+                        s_key[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+#pragma unroll
+    for (uint32_t r = 0; r < PER; ++r) {
+        const uint32_t p = tid + r * 1024u;
+        if (p < nj) s_pos[(uint32_t)s_key[p]] = p;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < PER; ++r) {
+        const uint32_t i = tid + r * 1024u;
+        if (i < nj) jobs[s_pos[i]] = mine[r];
+    }
+}
+
 // Giant chains of one pass (k_heavy's slot list): the job count is read on the device, so the
 // launch needs no host round trip; one wave pair per job, idle workgroups exit at once.
 __global__ __launch_bounds__(128) void k_chain_dyn(const Job* __restrict__ jobs, const unsigned long long* __restrict__ njobs,
@@ -4785,6 +4834,8 @@ struct Tune {
     // start the heaviest chain half a step in -- the pass count is doubled below four passes;
     // 0: off; 1: on)
     int route_first = -1;
+    int route_first_min = 1 << 17;   // route_first: k-mers of >= this many occurrences make pass 0 (C3: ~4.5 %
+                                     //   of the windows; those of >= 2^14 hold ~17 %, too many for a short pass)
     int route_heavy_min = 1 << 14;   // key-range passes: k-mers of >= this many occurrences are routed into
                                      //   the first half of the passes (0: off; k_pass_ids)
     int overlap = 0;                 // key-range passes, one GPU: pipelined passes (a second element set)
@@ -5654,8 +5705,8 @@ void route_plan(const Ranks& bs) {
     if (W > 1) allreduce(bs, pc, ncms, Red::SumU32);
     for (size_t k = 0; k < bs.size(); ++k) {
         skm_build* b = bs[k];
-        const uint32_t thresh =
-            std::max<uint32_t>(8, (uint32_t)(((uint64_t)b->tune.route_heavy_min >> ROUTE_SAMPLE) * 85 / 100));
+        const uint64_t hmin = first ? (uint64_t)std::max(1, b->tune.route_first_min) : (uint64_t)b->tune.route_heavy_min;
+        const uint32_t thresh = std::max<uint32_t>(8, (uint32_t)((hmin >> ROUTE_SAMPLE) * 85 / 100));
         if (b->rp)
             hipLaunchKernelGGL(k_route_sketch, dim3(2048), dim3(256), 0, b->stream, b->d_res.as<uint8_t>(), b->rp,
                                cms[k].as<uint32_t>(), thresh, bl8[k].as<uint8_t>());
@@ -6132,6 +6183,11 @@ void pass_peer_counts(const Ranks& bs) {
 // the first, and their stashed chains would only start after that pass's group-by (~0.08 s of a
 // ~0.2 s step) -- the multi-GPU step's floor.  Off on one GPU with key-range passes, where the
 // stash batches overlap the later passes (C3: +60..80 ms, the FP64 chain waves slow the passes).
+// samples a pass's giant-chain buffer holds (k_heavy: a key that no longer fits takes the job path):
+// the split capacity, at most 2^28 (1 GB per pass: C3's heavy-only pass 0 holds ~7 * 10^8 samples
+// of keys of >= 2^17 occurrences; the longest chains come first in k_heavy's list, mostly)
+uint64_t giant_cap(const skm_build* b) { return std::min<uint64_t>(std::max<uint64_t>(b->split_cap, 1), 1ull << 28); }
+
 int giant_class(const skm_build* b) {
     return b->tune.giant_class >= 0 ? b->tune.giant_class : (b->pass_bits == 0 || b->world > 1 ? 14 : 0);
 }
@@ -6344,7 +6400,7 @@ void phase_group(skm_build* b, uint32_t pass) {
         H.gsamples = b->gsamples[pass].as<uint32_t>();
         H.gjobs = b->gjobs[pass].as<Job>();
         H.gcount = b->gcount[pass].as<unsigned long long>();
-        H.gcap = b->split_cap;
+        H.gcap = giant_cap(b);
         H.gstat = b->d_gstat.as<unsigned long long>();
     }
     // issued before the group-by (concurrent with it), or after it (option serial_overflow: the
@@ -6364,6 +6420,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     if (H.giant_min) {
         SKM_HIP(hipEventRecord(b->gev_ready[gs], st2));
         SKM_HIP(hipStreamWaitEvent(b->gst[gs], b->gev_ready[gs], 0));
+        SKM_LAUNCH(b, k_giant_order, dim3(1), dim3(1024), 0, b->gst[gs], H.gjobs, H.gcount);
         if (!b->giant_timed) SKM_HIP(hipEventRecord(b->ev_giant[0], b->gst[gs]));
         SKM_LAUNCH(b, k_chain_dyn, dim3(1024), dim3(128), 0, b->gst[gs], H.gjobs, H.gcount, A.out_data,
                            b->tune.chain_prio);
@@ -6506,8 +6563,8 @@ void alloc_caps(skm_build* b) {
             b->gcount.emplace_back();
         }
         for (uint32_t p = 0; p < NP; ++p) {
-            b->gsamples[p].ensure(4 * Sp);
-            b->gjobs[p].ensure(sizeof(Job) * (Sp / (1u << giant_class(b)) + 16));
+            b->gsamples[p].ensure(4 * giant_cap(b));
+            b->gjobs[p].ensure(sizeof(Job) * (giant_cap(b) / (1u << giant_class(b)) + 16));
             b->gcount[p].ensure(16);
         }
     }
@@ -7238,7 +7295,8 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "overlap" ? &t.overlap
                : n == "heavy_grid" ? &t.heavy_grid
                : n == "route_vacate" ? &t.route_vacate
-               : n == "route_first" ? &t.route_first : nullptr;
+               : n == "route_first" ? &t.route_first
+               : n == "route_first_min" ? &t.route_first_min : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
         if (n == "overflow_long_class" || n == "main_long_class")

@@ -54,11 +54,14 @@ def build(skm, dist, rank, world):
     idx = np.nonzero(np.isin(p.file_of, files))[0]
     ref = oracle_ref.build(r, o, l, f, i, len(funcs)) if rank == 0 else None
     T = skm.GlooTransport()
-    for passes, route in ((1, 0), (2, 0), (2, 64), (4, 64)):
-        # route > 0: heavy-key routing over the transport (summed sketches, OR-ed filters)
+    for passes, route, first in ((1, 0, 1), (2, 0, 1), (2, 64, 1), (4, 64, 1), (4, 64, 0)):
+        # route > 0: heavy-key routing over the transport (summed sketches, OR-ed filters); first:
+        # into a heavy-only pass 0 (the world > 1 default), else into the first half of the passes
         b = skm.SignatureBuilder(len(funcs), device=0, rank=rank, world_size=world)
         b.set_option("key_range_passes", passes)
         b.set_option("route_heavy_min", route)
+        b.set_option("route_first_min", route or 1 << 17)
+        b.set_option("route_first", first)
         if len(idx):
             b.add_batch(r, o[idx], l[idx], f[idx], i[idx])
         b.set_transport(T)
@@ -67,6 +70,7 @@ def build(skm, dist, rank, world):
         c = b.counters()
         b.close()
         assert c["passes"] == passes
+        assert (c["routed"] > 0) == (route > 0 and passes > 1), c
         if rank == 0:
             assert np.array_equal(got.keys, ref["keys"])
             assert np.array_equal(got.data.view(np.uint8), ref["data"].view(np.uint8))

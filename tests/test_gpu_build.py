@@ -140,6 +140,7 @@ def test_heavy_key_routing(skm, gpu, passes, route_min, vacate):
         b.set_option("route_vacate", vacate)  # 0: the second half; else the last `vacate` passes, spread
     else:
         b.set_option("route_first", 1)
+        b.set_option("route_first_min", route_min)
         b.set_option("giant_class", 8)  # the heavy pass's chains on the giant streams, timed
     b.set_option("main_long_class", 8)
     b.set_option("overflow_long_class", 8)

@@ -116,6 +116,8 @@ def test_group_heavy_key_routing(skm, gpu, world, passes, first):
     opts = {"key_range_passes": passes, "route_heavy_min": 256, "main_long_class": 8, "overflow_long_class": 8}
     if first >= 0:
         opts["route_first"] = first
+    if first != 0:
+        opts["route_first_min"] = 256
     if passes == 0:
         opts["device_memory_budget_mb"] = 1000
     outs = run_group(skm, (r, o, l, f, i), len(funcs), world, lambda k: shard(p, world, k), opts, ctrs)

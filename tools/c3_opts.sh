@@ -15,6 +15,6 @@ for set in "$@"; do
     || { tail -5 $O/c3_opts_$i.log; exit 1; }
   python3 -c "
 import json,sys; d=json.load(open('$O/c3_opts_$i.json')); r=d['roofline']; k=r.get('kernels_ms_per_step') or {}
-print(sys.argv[1] or 'defaults', round(d['ms_per_step'],1), 'tail', round(d.get('chain_tail_ms') or 0,1), {n: round(v) for n, v in sorted(k.items(), key=lambda x: -x[1])[:10]})" "$set"
+print(sys.argv[1] or 'defaults', round(d['ms_per_step'],1), 'tail', round(d.get('chain_tail_ms') or 0,1), 'giant', d.get('giant_chains'), {n: round(v) for n, v in sorted(k.items(), key=lambda x: -x[1])[:10]})" "$set"
   i=$((i+1))
 done

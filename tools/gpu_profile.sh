@@ -30,7 +30,7 @@ C3="python3 -u $R/bench.py --cache-dir /tmp/c3 --weak-seqs 0 --annot-queries 0 -
 C2="python3 -u $R/tools/c3_diag.py --cache-dir /tmp/c3 --files 250"
 LEGS="python3 -u $R/bench.py --seqs-total 1000000 --cache-dir /tmp/legs --cli-seqs 0 --finish 0 --no-cpu-baseline"
 # PHASE: all | trace (stamps + C3/C2 traces) | pmc (C3/C2 counters) | legs (legs trace + counters)
-#        | legs_trace (the legs' kernel trace only)
+#        | legs_trace (the legs' kernel trace only) | sq (SQ counters of a C3 build)
 if [ "$P" = all ] || [ "$P" = trace ]; then
   step c3_stamps 300 python3 -u $R/tools/c3_diag.py --cache-dir /tmp/c3 --runs 1 --stamps
   step prof_c3 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_c3" -o run -- $C3 --steps 2 --warmup 1 --json-out "$O/bench_c3_trace.json"
@@ -42,6 +42,12 @@ if [ "$P" = all ] || [ "$P" = pmc ]; then
     step pmc_c3_$lc 500 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_c3_$lc" -o run -- python3 -u $R/tools/c3_diag.py --cache-dir /tmp/c3 --runs 1
     step pmc_c2_$lc 300 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_c2_$lc" -o run -- $C2 --runs 1
   done
+fi
+if [ "$P" = sq ]; then  # SQ counters of one C3 build (k_bucket_process at C3 size; dispatches serialised)
+  cd "$R"
+  SQ_CMD="python3 -u $R/tools/c3_diag.py --cache-dir /tmp/c3 --runs 1" SQ_OUT=pmc_sq_c3 SKM_PROBE_ANNOT=0 \
+    bash tools/pmc_sq.sh || exit 1
+  echo done; exit 0
 fi
 if [ "$P" = all ] || [ "$P" = legs ] || [ "$P" = legs_trace ]; then
   cd "$R"

@@ -7,7 +7,7 @@ and the ratios that say what bounds it --
   active_frac    SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES share of wave time issuing
   lds_conflict   SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS  bank-conflict cycles per LDS-issue cycle
   valu_per_vmem  SQ_INSTS_VALU / SQ_INSTS_VMEM
-usage: python tools/sq_summary.py [gpurun_out/pmc_sq] [round]
+usage: python tools/sq_summary.py [gpurun_out/pmc_sq] [round] [workload text] [output name]
 """
 import collections
 import csv
@@ -33,8 +33,10 @@ def main():
                 continue
             acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
             launches[(k, p)].add(row["Dispatch_Id"])
-    out = {"round": rnd, "workload": "C2 probe build (tools/pmc_probe.py: 1,000,000 proteins, 2 runs) + "
-                                     "annotate of 1,000,000 fresh queries against its DB (2 runs)",
+    wl = sys.argv[3] if len(sys.argv) > 3 else ("C2 probe build (tools/pmc_probe.py: 1,000,000 proteins, 2 runs) + "
+                                                 "annotate of 1,000,000 fresh queries against its DB (2 runs)")
+    name = sys.argv[4] if len(sys.argv) > 4 else f"{rnd}_sq_counters.json"
+    out = {"round": rnd, "workload": wl,
            "script": "tools/pmc_sq.sh", "kernels": {}}
     for k, c in acc.items():
         wc = c.get("SQ_WAVE_CYCLES", 0.0)
@@ -47,7 +49,7 @@ def main():
         if c.get("SQ_INSTS_VMEM"):
             r["valu_per_vmem"] = c.get("SQ_INSTS_VALU", 0.0) / c["SQ_INSTS_VMEM"]
         out["kernels"][k] = r
-    json.dump(out, open(os.path.join(ROOT, "profiles", f"{rnd}_sq_counters.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(ROOT, "profiles", name), "w"), indent=1)
     rank = sorted(out["kernels"].items(), key=lambda kv: -kv[1]["counters"].get("SQ_WAVE_CYCLES", 0))
     for k, r in rank[:10]:
         print(f"{k:24s} wave_cycles {r['counters'].get('SQ_WAVE_CYCLES', 0):.3g} "
