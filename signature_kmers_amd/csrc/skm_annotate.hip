@@ -313,7 +313,6 @@ __global__ void k_calls_scan(CallArgs A, uint4* __restrict__ segs) {
     if (s >= A.nseq) return;
     const QMeta m = A.meta[s];
     const uint32_t nwin = m.len >= 8 ? m.len - 7 : 0;
-    const uint32_t* hit = A.hits + m.pstart;
     uint4* out = segs + A.cap_off[s];
     uint32_t nseg = 0;
     // HitSet: all usable hits in window range [first, last_pos]; pair = (prev, last); ncur = the
@@ -332,23 +331,33 @@ __global__ void k_calls_scan(CallArgs A, uint4* __restrict__ segs) {
             ncur = 0;
         }
     };
-    // the next 16 hits are loaded while these 16 are walked (the walk is a per-thread chain;
-    // the loads of one thread are 64 contiguous bytes)
-    uint32_t nb[16];
+    // the next 16 hits are loaded while these 16 are walked (the walk is a per-thread chain): four
+    // 16-byte loads from the 16-byte aligned slot below the sequence's first hit (slots outside
+    // [0, nwin) are skipped; the hit array is padded by 16 slots), so a wave's load instruction
+    // covers 64 lines four times fewer times than with 16 dword loads
+    const uint32_t mis = (uint32_t)(m.pstart & 3u);
+    const uint4* h4 = reinterpret_cast<const uint4*>(A.hits + (m.pstart - mis));
+    const uint32_t tot = nwin ? nwin + mis : 0u;
+    uint4 nb[4];
 #pragma unroll
-    for (uint32_t k = 0; k < 16; ++k) nb[k] = k < nwin ? hit[k] : NO_HIT;
-    for (uint32_t i0 = 0; i0 < nwin; i0 += 16) {
+    for (uint32_t k = 0; k < 4; ++k) nb[k] = 4u * k < tot ? h4[k] : make_uint4(NO_HIT, NO_HIT, NO_HIT, NO_HIT);
+    for (uint32_t j0 = 0; j0 < tot; j0 += 16) {
         uint32_t hb[16];
 #pragma unroll
-        for (uint32_t k = 0; k < 16; ++k) hb[k] = nb[k];
-        if (i0 + 16 < nwin) {
+        for (uint32_t k = 0; k < 4; ++k) {
+            hb[4 * k] = nb[k].x;
+            hb[4 * k + 1] = nb[k].y;
+            hb[4 * k + 2] = nb[k].z;
+            hb[4 * k + 3] = nb[k].w;
+        }
+        if (j0 + 16 < tot) {
 #pragma unroll
-            for (uint32_t k = 0; k < 16; ++k) nb[k] = i0 + 16 + k < nwin ? hit[i0 + 16 + k] : NO_HIT;
+            for (uint32_t k = 0; k < 4; ++k) nb[k] = h4[(j0 >> 2) + 4 + k];
         }
 #pragma unroll
         for (uint32_t k = 0; k < 16; ++k) {
-            const uint32_t h = hb[k], i = i0 + k;
-            if (!usable(h, A)) continue;
+            const uint32_t h = hb[k], i = j0 + k - mis;  // wraps above nwin before the first window
+            if (i >= nwin || !usable(h, A)) continue;
             const uint32_t f = h >> 16;
             if (count > 0 && (uint64_t)last_pos + (uint64_t)A.max_gap < (uint64_t)i) {
                 if ((int)count >= A.min_hits) {
@@ -524,16 +533,36 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
     const double seqlen = (double)m.len;
     uint32_t* buf = sv[wave];
     uint32_t n = 0, last_cur = first;
-    uint32_t hn = first + lane <= last ? hit[first + lane] : NO_HIT;  // the next 64 hits in flight
-    for (uint32_t i0 = first; i0 <= last; i0 += 64) {
-        const uint32_t h = hn, i1 = i0 + 64u + lane;
-        hn = i1 <= last ? hit[i1] : NO_HIT;
+    auto take64 = [&](uint32_t i0, uint32_t h) {  // the usable hits of cur among windows i0 + lane
         const bool take = usable(h, A) && (h >> 16) == cur;
         const uint64_t bal = __ballot(take);
         const uint32_t pos = n + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
         if (take && pos < SEG_CAP) buf[pos] = h & 0xFFFFu;
         if (bal) last_cur = i0 + 63u - (uint32_t)__clzll(bal);
         n += (uint32_t)__popcll(bal);
+    };
+    // the first SEG_CAP windows' hits loaded together (one memory latency per segment instead of
+    // one per 64 windows); a longer window range walks the rest 64 at a time, the next in flight
+    constexpr uint32_t SEG_PRE = SEG_CAP / 64;
+    const uint32_t span = last - first + 1u;
+    uint32_t hv[SEG_PRE];
+#pragma unroll
+    for (uint32_t e = 0; e < SEG_PRE; ++e) {
+        const uint32_t i = first + e * 64u + lane;
+        hv[e] = e * 64u < span && i <= last ? hit[i] : NO_HIT;
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < SEG_PRE; ++e) {
+        if (e * 64u >= span) break;  // wave-uniform
+        take64(first + e * 64u, hv[e]);
+    }
+    if (span > SEG_CAP) {
+        uint32_t hn = first + SEG_CAP + lane <= last ? hit[first + SEG_CAP + lane] : NO_HIT;
+        for (uint32_t i0 = first + SEG_CAP; i0 <= last; i0 += 64) {
+            const uint32_t h = hn, i1 = i0 + 64u + lane;
+            hn = i1 <= last ? hit[i1] : NO_HIT;
+            take64(i0, h);
+        }
     }
     if (n > SEG_CAP) {  // long run: the sequential restatement on a private scratch
         if (lane == 0) {
@@ -620,16 +649,21 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
     // segment).  A segment's lengths span a few hundred values, so both selects read a histogram of
     // x - min in the wave's LDS buffer (two per segment); a wider span takes MSD radix selects on
     // ballots.
+    // (loops bounded by the wave-uniform item count, lane conditions as selects: the LDS reads
+    // stay inside the buffer, so no exec-mask branches)
     uint32_t x[SEG_CAP / 64];
     uint32_t vmin = 0xFFFFu, vmax = 0u;
 #pragma unroll
+    for (int e = 0; e < (int)(SEG_CAP / 64); ++e) x[e] = 0u;
+#pragma unroll
     for (int e = 0; e < (int)(SEG_CAP / 64); ++e) {
+        if ((uint32_t)e * 64u >= n) break;  // wave-uniform
         const uint32_t i = (uint32_t)e * 64u + lane;
-        x[e] = i < n ? buf[i] : 0u;
-        if (i < n) {
-            vmin = min(vmin, x[e]);
-            vmax = max(vmax, x[e]);
-        }
+        const uint32_t v = buf[i];
+        const bool in = i < n;
+        x[e] = in ? v : 0u;
+        vmin = min(vmin, in ? v : 0xFFFFu);
+        vmax = max(vmax, in ? v : 0u);
     }
     vmin = wave_min_u32(vmin);
     vmax = wave_max_u32(vmax);
@@ -647,7 +681,8 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
 #pragma unroll
         for (uint32_t t = 0; t < HBMAX; ++t) {
             if (t >= B) break;  // wave-uniform
-            c[t] = b0 + t < R ? buf[b0 + t] : 0u;
+            const uint32_t v = buf[min(b0 + t, SEG_CAP - 1u)];
+            c[t] = b0 + t < R ? v : 0u;
         }
         hist_kth2(c, B, k1, k2, a, b);
         const uint32_t C2 = a + b;
@@ -659,8 +694,9 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_process(CallArgs A, cons
         for (uint32_t t = 0; t < HBMAX; ++t) {
             if (t >= B) break;
             const uint32_t i = b0 + t;
-            uint32_t d = up + i < R ? buf[up + i] : 0u;
-            if ((i > 0 || p) && i <= lo) d += buf[lo - i];
+            const bool hi_in = up + i < R, lo_in = (i > 0 || p) && i <= lo;
+            const uint32_t vu = buf[min(up + i, SEG_CAP - 1u)], vl = buf[lo_in ? lo - i : 0u];
+            const uint32_t d = (hi_in ? vu : 0u) + (lo_in ? vl : 0u);
             c[t] = i < R ? d : 0u;
         }
         hist_kth2(c, B, k1, k2, a, b);
