@@ -4833,6 +4833,10 @@ struct Tune {
     // step (-1, the default: on at world > 1, where one or two passes per rank would otherwise
     // start the heaviest chain half a step in -- the pass count is doubled below four passes;
     // 0: off; 1: on)
+    // key-range passes on one GPU: a pass's tail (k_big_groups, the group-by's chains, the pass
+    // accounting) runs on its own stream beside the next pass's staging, which writes a buffer of
+    // its own (the split waits for the tail: it overwrites the slots the tail reads)
+    int tail_async = 1;
     int route_first = -1;
     int route_first_min = 1 << 17;   // route_first: k-mers of >= this many occurrences make pass 0 (C3: ~4.5 %
                                      //   of the windows; those of >= 2^14 hold ~17 %, too many for a short pass)
@@ -4932,6 +4936,7 @@ struct skm_build {
     // device work
     DevBuf d_hist, d_offs, d_partial, d_rbbase, d_bstart32, d_bstart, d_owner_start;
     DevBuf d_recs_hi, d_recs_lo, d_tmp_hi, d_tmp_lo;
+    DevBuf d_stg_hi, d_stg_lo;          // tail_async: the level-0 staging (else tmp holds it)
     DevBuf d_cur0, d_cur1, d_slices;   // staged scatter cursors
     DevBuf d_flagbits;
     DevBuf d_chainq;              // k_chains work queues: two counters per launch of a run
@@ -4968,6 +4973,9 @@ struct skm_build {
 
     // second stream: overflow sub-buckets + their chains, concurrent with the group-by
     hipStream_t stream2 = nullptr, stream3 = nullptr;
+    hipStream_t stream_tail = nullptr;  // tail_async: a pass's big groups, main chains and accounting
+    hipEvent_t ev_tail_bp = nullptr, ev_tail_done = nullptr;
+    bool tail_pending = false;          // the last pass's tail is still in flight on stream_tail
     hipEvent_t ev_part = nullptr, ev_split = nullptr;
     DevBuf d_hv_keys, d_hv_hi, d_hv_lo, d_hv_s0, d_hv_s1;   // heavy keys of the split overflow
     DevBuf d_sub_tab, d_jobs2, d_jobs3;
@@ -5559,7 +5567,14 @@ void size_passes(skm_build* b, int forced_pb = -1) {
 }
 
 // buffers sized by the number of elements this rank groups in one pass
+bool tail_async_on(const skm_build* b) { return b->tune.tail_async && b->world == 1 && b->pass_bits && !b->overlap; }
+
 void ensure_local(skm_build* b, uint64_t n) {
+    if (tail_async_on(b)) {  // within PASS_BYTES: the 16 B/element of the received set (world > 1) are free
+        const uint64_t cs = std::max<uint64_t>(n + n / 16, 1);
+        b->d_stg_hi.ensure(8 * cs);
+        b->d_stg_lo.ensure(8 * cs);
+    }
     if (n <= b->cap_local && b->cap_local) return;
     const uint64_t c = std::max<uint64_t>(n + n / 16, 1);
     if (b->world > 1) {
@@ -5956,6 +5971,15 @@ inline unsigned long long* pass_ctr(skm_build* b, uint32_t pass) {
     return b->d_ctr.as<unsigned long long>() + 32 * (1 + pset(b, pass));
 }
 
+// the main stream waits for the previous pass's tail (tail_async) before it overwrites what the tail
+// reads (the split's recs, then the partition's tmp, the counters, the job lists) or reads what it
+// writes (the stash cursors, the kept arena's totals)
+void join_tail(skm_build* b) {
+    if (!b->tail_pending) return;
+    SKM_HIP(hipStreamWaitEvent(b->stream, b->ev_tail_done, 0));
+    b->tail_pending = false;
+}
+
 void phase_extract(skm_build* b, uint32_t pass) {
     hipStream_t st = b->stream;
     const int nbits = b->owner_bits + b->b1_bits;
@@ -6027,22 +6051,29 @@ void phase_extract(skm_build* b, uint32_t pass) {
     b->d_slices.ensure(4 * 80);
     SKM_LAUNCH(b, k_stage_init, dim3((NB + 255) / 256), dim3(256), 0, st, b->d_bstart.as<uint64_t>(), NB, l0_shift,
                        b->d_cur0.as<unsigned long long>(), b->d_cur1.as<unsigned long long>(), b->d_slices.as<uint32_t>());
+    // the level-0 staging: tmp, or (tail_async) a buffer of its own, so it overlaps the previous
+    // pass's tail, which still reads tmp and recs
+    const bool sep = tail_async_on(b);
+    uint64_t* stg_hi = sep ? b->d_stg_hi.as<uint64_t>() : tmp_hi(b, pass);
+    uint64_t* stg_lo = sep ? b->d_stg_lo.as<uint64_t>() : tmp_lo(b, pass);
+    if (!sep) join_tail(b);
     if (b->pass_bits && b->tune.stage_round == 1)
         SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND_HALF, 4>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
                    b->d_posg.as<uint64_t>() + (uint64_t)(pass % b->emit_g) * std::max<uint64_t>(b->pass_max, 1),
                    b->d_npos.as<unsigned long long>() + pass,
-                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass));
+                   b->d_cur0.as<unsigned long long>(), stg_hi, stg_lo);
     else if (b->pass_bits)
         SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND, 2>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
                    b->d_posg.as<uint64_t>() + (uint64_t)(pass % b->emit_g) * std::max<uint64_t>(b->pass_max, 1),
                    b->d_npos.as<unsigned long long>() + pass,
-                   b->d_cur0.as<unsigned long long>(), tmp_hi(b, pass), tmp_lo(b, pass));
+                   b->d_cur0.as<unsigned long long>(), stg_hi, stg_lo);
     else
         SKM_LAUNCH(b, k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
-                           tmp_hi(b, pass), tmp_lo(b, pass));
+                           stg_hi, stg_lo);
+    join_tail(b);
     const uint32_t nsl = (uint32_t)(ceil_div(b->pass_max, SC_SLICE) + (1u << SC_L0_BITS));
-    SKM_LAUNCH(b, k_split_stage, dim3(nsl), dim3(EX_THREADS), 0, st, tmp_hi(b, pass),
-                       tmp_lo(b, pass), b->d_bstart.as<uint64_t>(), nbits, b->d_slices.as<uint32_t>(),
+    SKM_LAUNCH(b, k_split_stage, dim3(nsl), dim3(EX_THREADS), 0, st, stg_hi,
+                       stg_lo, b->d_bstart.as<uint64_t>(), nbits, b->d_slices.as<uint32_t>(),
                        b->d_cur1.as<unsigned long long>(), recs_hi(b, pass), recs_lo(b, pass));
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[3], st));
@@ -6462,11 +6493,19 @@ void phase_group(skm_build* b, uint32_t pass) {
         emit_group(b, (pass + 1) / b->emit_g, b->stx);
         b->emit_q = (pass + 1) / b->emit_g;
     }
-    SKM_LAUNCH(b, k_big_groups<false>, dim3(2048), dim3(BIG_WG), 0, st, BA);
-    SKM_LAUNCH(b, k_big_groups<true>, dim3(512), dim3(BIG_WG), 0, st, BA);
-    SKM_LAUNCH(b, k_big_append, dim3(256), dim3(BIG_WG), 0, st, BA.out, BA, A);
+    // the pass's tail: on the main stream, or (tail_async) on its own stream beside the next pass's
+    // staging -- the next split waits for it (join_tail)
+    const bool tail_async = tail_async_on(b);
+    hipStream_t tt = tail_async ? b->stream_tail : st;
+    if (tail_async) {
+        SKM_HIP(hipEventRecord(b->ev_tail_bp, st));
+        SKM_HIP(hipStreamWaitEvent(tt, b->ev_tail_bp, 0));
+    }
+    SKM_LAUNCH(b, k_big_groups<false>, dim3(2048), dim3(BIG_WG), 0, tt, BA);
+    SKM_LAUNCH(b, k_big_groups<true>, dim3(512), dim3(BIG_WG), 0, tt, BA);
+    SKM_LAUNCH(b, k_big_append, dim3(256), dim3(BIG_WG), 0, tt, BA.out, BA, A);
     SKM_HIP(hipGetLastError());
-    SKM_HIP(hipEventRecord(b->ev[12], st));
+    SKM_HIP(hipEventRecord(b->ev[12], tt));
     // ---- 6. deferred P^2 / variance chains: the overflow's as soon as both parts are grouped
     //      (the long ones on stream 2, the per-lane ones on stream 3), the group-by's on st ----
     SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
@@ -6475,7 +6514,7 @@ void phase_group(skm_build* b, uint32_t pass) {
                   A.out_data, (uint32_t)b->tune.ovf_long_class, st3, b->ev_o3[2], (uint32_t)b->tune.ovf_chain_wgs);
     SKM_HIP(hipEventRecord(b->ev_o[2], st2));
     SKM_HIP(hipEventRecord(b->ev_o3[1], st3));
-    launch_chains(b, st, A.jobs, ctr_d + 3, b->jobs_cap, b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
+    launch_chains(b, tt, A.jobs, ctr_d + 3, b->jobs_cap, b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
                   reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, (uint32_t)b->tune.main_long_class);
     if (b->overlap) {
         // the pass ends on the main stream here; its overflow path and accounting finish on
@@ -6492,14 +6531,18 @@ void phase_group(skm_build* b, uint32_t pass) {
         SKM_HIP(hipEventRecord(b->ev[7], st));
         return;
     }
-    SKM_HIP(hipStreamWaitEvent(st, b->ev_o[2], 0));
-    SKM_HIP(hipStreamWaitEvent(st, b->ev_o3[1], 0));
-    SKM_HIP(hipEventRecord(b->ev[6], st));
+    SKM_HIP(hipStreamWaitEvent(tt, b->ev_o[2], 0));
+    SKM_HIP(hipStreamWaitEvent(tt, b->ev_o3[1], 0));
+    SKM_HIP(hipEventRecord(b->ev[6], tt));
     // ---- 7. run totals and the chain lists' bounds ----
-    SKM_LAUNCH(b, k_pass_account, dim3(1), dim3(1), 0, st, ctr_d, run_d, b->jobs_cap, b->jobs2_cap, b->big_cap,
+    SKM_LAUNCH(b, k_pass_account, dim3(1), dim3(1), 0, tt, ctr_d, run_d, b->jobs_cap, b->jobs2_cap, b->big_cap,
                        b->lens_cap);
     SKM_HIP(hipGetLastError());
-    SKM_HIP(hipEventRecord(b->ev[7], st));
+    SKM_HIP(hipEventRecord(b->ev[7], tt));
+    if (tail_async) {
+        SKM_HIP(hipEventRecord(b->ev_tail_done, tt));
+        b->tail_pending = true;
+    }
 }
 
 // overlap: the main stream waits for every pass's overflow path still in flight
@@ -6577,6 +6620,7 @@ void begin_run(skm_build* b) {
     b->chainq_next = 0;
     b->emit_q = -1;  // no pass group's positions are queued from an earlier (possibly aborted) run
     b->giant_timed = false;
+    b->tail_pending = false;
     SKM_HIP(hipEventRecord(b->ev_start, st));
     SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 3 * 256, st));
     b->ovf_pending[0] = b->ovf_pending[1] = false;
@@ -6657,6 +6701,7 @@ hipStream_t chain_stream(skm_build* b, int slot) {
 }
 
 void flush_long_chains(skm_build* b, int slot) {
+    join_tail(b);  // the stash of the last pass's chains (k_long_stash) is part of its tail
     unsigned long long* run_d = b->d_run.as<unsigned long long>();
     unsigned long long* rng = run_d + RUN_SNAP + 2 * slot;
     SKM_LAUNCH(b, k_long_snap, dim3(1), dim3(1), 0, b->stream, run_d, rng, b->long_jobs_cap);
@@ -6696,6 +6741,7 @@ void phase_stats(skm_build* b) {
     hipStream_t st = b->stream;
     const uint32_t F = b->opts.n_functions;
     SKM_HIP(hipEventRecord(b->ev_tail[0], st));  // the last pass is issued: the tail starts here
+    join_tail(b);
     drain_overflow(b);
     if (b->tune.flag_bits && b->n_total)
         SKM_LAUNCH(b, k_flags_from_bits, dim3(1024), dim3(256), 0, st, b->d_flagbits.as<uint32_t>(),
@@ -6902,6 +6948,9 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     SKM_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
     SKM_HIP(hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking));
     SKM_HIP(hipStreamCreateWithFlags(&b->stream3, hipStreamNonBlocking));
+    SKM_HIP(hipStreamCreateWithFlags(&b->stream_tail, hipStreamNonBlocking));
+    SKM_HIP(hipEventCreateWithFlags(&b->ev_tail_bp, hipEventDisableTiming));
+    SKM_HIP(hipEventCreateWithFlags(&b->ev_tail_done, hipEventDisableTiming));
     use_evset(b, 0);
     SKM_HIP(hipEventCreate(&b->ev_start));
     SKM_HIP(hipStreamCreateWithFlags(&b->chain_st, hipStreamNonBlocking));
@@ -7245,6 +7294,7 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
             remake(b->stream2);
             remake(b->stream3);
             remake(b->stx);
+            remake(b->stream_tail);
             t.side_cus = (int)value;
         }
     } else if (n == "work_buffer_elements") {
@@ -7296,6 +7346,7 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "heavy_grid" ? &t.heavy_grid
                : n == "route_vacate" ? &t.route_vacate
                : n == "route_first" ? &t.route_first
+               : n == "tail_async" ? &t.tail_async
                : n == "route_first_min" ? &t.route_first_min : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
@@ -7691,6 +7742,7 @@ void skm_build_destroy(skm_build* b) {
         if (x != b) x->group.clear();
     if (b->stream2) (void)hipStreamSynchronize(b->stream2);
     if (b->stream3) (void)hipStreamSynchronize(b->stream3);
+    if (b->stream_tail) (void)hipStreamSynchronize(b->stream_tail);
     if (b->chain_st) (void)hipStreamSynchronize(b->chain_st);
     for (auto& set : b->evsets) {
         for (auto& e : set.ev)
@@ -7749,6 +7801,9 @@ void skm_build_destroy(skm_build* b) {
     if (b->stream) (void)hipStreamDestroy(b->stream);
     if (b->stream2) (void)hipStreamDestroy(b->stream2);
     if (b->stream3) (void)hipStreamDestroy(b->stream3);
+    if (b->stream_tail) (void)hipStreamDestroy(b->stream_tail);
+    if (b->ev_tail_bp) (void)hipEventDestroy(b->ev_tail_bp);
+    if (b->ev_tail_done) (void)hipEventDestroy(b->ev_tail_done);
     delete b;
 }
 
