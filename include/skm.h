@@ -217,7 +217,12 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   windows -- are grouped in the first half of the passes, so their long P^2 chains run beside
  *   the later passes instead of after the last one; 16384; 0 = off), "route_vacate" (the last
  *   this many passes hold no routed heavy key, whose keys are spread over the others by hash;
- *   0 = the second half, mapped to pass - P/2), "stage_round" (key-range
+ *   0 = the second half, mapped to pass - P/2), "route_first" (every routed heavy k-mer in a
+ *   heavy-only pass 0, the light keys of pass 0 spread over the others, the pass count doubled
+ *   below four passes: 1 = on, 0 = off; default on at world_size > 1), "route_first_min" (its
+ *   occurrence threshold, 131072), "tail_async" (one GPU, key-range passes: a pass's big groups,
+ *   chains and accounting on their own stream beside the next pass's staging; 1),
+ *   "stage_round" (key-range
  *   passes: 1 = the staged position scatter in half rounds of 2048 elements, four workgroups
  *   per CU, the default; 0 = rounds of 4096), "partition_round"
  *   (k_partition staging rounds: 0 = 2048 elements, three 512-thread workgroups per CU (default);
