@@ -4837,6 +4837,8 @@ struct Tune {
     // accounting) runs on its own stream beside the next pass's staging, which writes a buffer of
     // its own (the split waits for the tail: it overwrites the slots the tail reads)
     int tail_async = 1;
+    int big_grid = 2048;             // k_big_groups' persistent grids: groups of 65..1024 members,
+    int big_grid_large = 512;        //   and of 1025..CAP
     int route_first = -1;
     int route_first_min = 1 << 17;   // route_first: k-mers of >= this many occurrences make pass 0 (C3: ~4.5 %
                                      //   of the windows; those of >= 2^14 hold ~17 %, too many for a short pass)
@@ -6501,8 +6503,8 @@ void phase_group(skm_build* b, uint32_t pass) {
         SKM_HIP(hipEventRecord(b->ev_tail_bp, st));
         SKM_HIP(hipStreamWaitEvent(tt, b->ev_tail_bp, 0));
     }
-    SKM_LAUNCH(b, k_big_groups<false>, dim3(2048), dim3(BIG_WG), 0, tt, BA);
-    SKM_LAUNCH(b, k_big_groups<true>, dim3(512), dim3(BIG_WG), 0, tt, BA);
+    SKM_LAUNCH(b, k_big_groups<false>, dim3((uint32_t)std::max(1, b->tune.big_grid)), dim3(BIG_WG), 0, tt, BA);
+    SKM_LAUNCH(b, k_big_groups<true>, dim3((uint32_t)std::max(1, b->tune.big_grid_large)), dim3(BIG_WG), 0, tt, BA);
     SKM_LAUNCH(b, k_big_append, dim3(256), dim3(BIG_WG), 0, tt, BA.out, BA, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[12], tt));
@@ -7294,7 +7296,6 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
             remake(b->stream2);
             remake(b->stream3);
             remake(b->stx);
-            remake(b->stream_tail);
             t.side_cus = (int)value;
         }
     } else if (n == "work_buffer_elements") {
@@ -7347,6 +7348,8 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "route_vacate" ? &t.route_vacate
                : n == "route_first" ? &t.route_first
                : n == "tail_async" ? &t.tail_async
+               : n == "big_grid" ? &t.big_grid
+               : n == "big_grid_large" ? &t.big_grid_large
                : n == "route_first_min" ? &t.route_first_min : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");

@@ -54,18 +54,28 @@ public:
             job_ = std::move(f);
             parts_ = n;
             next_.store(0);
+            done_parts_.store(0, std::memory_order_relaxed);
             gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         work();
+        // every part done: return without a futex round trip (a worker still leaving work() only
+        // finds the part counter exhausted; the next run waits for it under the lock above)
+        const auto t0 = std::chrono::steady_clock::now();
+        while (done_parts_.load(std::memory_order_acquire) < n &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(SPIN_US))
+            __builtin_ia32_pause();
+        if (done_parts_.load(std::memory_order_acquire) >= n) return;
         std::unique_lock<std::mutex> l(m_);
         done_.wait(l, [&] { return active_ == 0; });
-        job_ = nullptr;
     }
 
 private:
     void work() {
-        for (int p; (p = next_.fetch_add(1)) < parts_;) job_(p);
+        for (int p; (p = next_.fetch_add(1)) < parts_;) {
+            job_(p);
+            done_parts_.fetch_add(1, std::memory_order_release);
+        }
     }
     void loop() {
         uint64_t seen = 0;
@@ -92,7 +102,7 @@ private:
     std::mutex m_;
     std::condition_variable cv_, done_;
     std::function<void(int)> job_;
-    std::atomic<int> next_{0};
+    std::atomic<int> next_{0}, done_parts_{0};
     int parts_ = 0, active_ = 0;
     std::atomic<uint64_t> gen_{0};
     bool stop_ = false;
