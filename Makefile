@@ -15,7 +15,7 @@ LIB      = signature_kmers_amd/libskm.so
 TOOLS    = bin/kmers-build-signatures bin/kmers-call-functions bin/kmers-annotate-seqs bin/kmers-matrix-distance bin/skm-front-probe
 ORACLE   = oracle/liboracle_skm.so
 FRONT    = $(OBJDIR)/front/skm_front.o $(OBJDIR)/front/skm_caller.o $(OBJDIR)/front/skm_mesh.o
-FRONTH   = $(wildcard $(SRC)/front/*.h) include/skm.h
+FRONTH   = $(wildcard $(SRC)/front/*.h) $(SRC)/skm_strutil.h include/skm.h
 
 all: $(LIB) $(ORACLE) $(TOOLS)
 tools: $(TOOLS)

@@ -36,8 +36,9 @@ extern "C" {
 #define SKM_UNDEFINED_FUNCTION 0xFFFFu /* kmer_data.h:23 UndefinedFunction */
 
 /* StoredKmerData (kmer_data.h:114-128): five little-endian u16, 10 bytes, the kmer_data.dat
- * record (perfect_hash.h:62 writes sizeof(StoredKmerData)=10 per MPH slot). */
-#pragma pack(push, 1)
+ * record (perfect_hash.h:62 writes sizeof(StoredKmerData)=10 per MPH slot).  Natural layout:
+ * sizeof 10, alignof 2, offsets 0/2/4/6/8 -- equal to the reference as g++ compiles it
+ * (tests/golden/ref_split.npz `layout`, tests/test_ref_pin_cpu.py). */
 typedef struct skm_stored_kmer_data {
     uint16_t avg_from_end;
     uint16_t function_index;
@@ -45,7 +46,6 @@ typedef struct skm_stored_kmer_data {
     uint16_t median;
     uint16_t var;
 } skm_stored_kmer_data;
-#pragma pack(pop)
 
 /* KmerCall (call_functions.h:23-48). 24 bytes. */
 typedef struct skm_kmer_call {

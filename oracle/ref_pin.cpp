@@ -2,10 +2,13 @@
 //  oracle/ref_pin.cpp  --  TEST INFRASTRUCTURE ONLY (generates golden vectors; never shipped)
 // ============================================================================================
 //
-//  A driver around the two parts of the reference that compile here UNCHANGED with the image's
-//  g++ (std-only headers, no Boost / TBB / CMPH):
-//    kmer_data.h        for_each_kmer<N>  (kmer_data.h:76-102), the annotate window iterator
+//  A driver around the parts of the reference that compile here UNCHANGED with the image's g++
+//  (std-only headers, no Boost / TBB / CMPH):
+//    kmer_data.h        for_each_kmer<N>  (kmer_data.h:76-102), the annotate window iterator, and
+//                       the StoredKmerData / KmerAttributes records (kmer_data.h:105-128)
 //    fasta_parser.h/.cc FastaParser       (fasta_parser.h:38-144, fasta_parser.cc:17-36)
+//    operators.h        split()           (operators.h:80-91), used by read_function_index
+//                       (call_functions.tcc:143) and find_best_call's fusion keys (:487)
 //  They are compiled from where they lie under /root/reference/src by oracle/Makefile.ref into
 //  oracle/_ref/ref_pin (git-ignored).  Nothing of the reference is copied into this repository:
 //  this file only #includes the reference headers and calls them.
@@ -24,15 +27,24 @@
 //                   "E <line> <hex message> <hex id>" in call order, then "END"
 //    S <hex file>   FastaParser as function_map.h:128-237 / call_functions.tcc:165-182 drive it
 //                   (set_callback (id, seq) only), the same output with "-" for the definition
+//    P <hex s> <hex delim>   split(s, delim) -> "P <n> <hex part> ..." (n parts, "-" = empty)
+//    L -            the record layouts -> "L <sizeof StoredKmerData> <alignof> <offsetof
+//                   avg_from_end function_index mean median var> <sizeof KmerAttributes>
+//                   <alignof> <offsetof func_index otu_index offset seq_id protein_length>"
 // ============================================================================================
+#include <algorithm>
+#include <cstddef>
 #include <cstdio>
 #include <iostream>
+#include <iterator>
+#include <map>
 #include <sstream>
 #include <string>
 #include <vector>
 
 #include "fasta_parser.h"
 #include "kmer_data.h"
+#include "operators.h"  // needs <vector>, <map>, <algorithm> from the includer (as call_functions.h does)
 
 namespace {
 
@@ -85,6 +97,23 @@ void run_fasta(const std::string& data, bool with_def) {
     std::cout << "END\n";
 }
 
+void run_split(const std::string& s, const std::string& delim) {
+    const std::vector<std::string> parts = split(s, delim);
+    std::cout << "P " << parts.size();
+    for (const auto& p : parts) std::cout << " " << hex(p);
+    std::cout << "\n";
+}
+
+void run_layout() {
+    std::cout << "L " << sizeof(StoredKmerData) << " " << alignof(StoredKmerData) << " "
+              << offsetof(StoredKmerData, avg_from_end) << " " << offsetof(StoredKmerData, function_index) << " "
+              << offsetof(StoredKmerData, mean) << " " << offsetof(StoredKmerData, median) << " "
+              << offsetof(StoredKmerData, var) << " " << sizeof(KmerAttributes) << " " << alignof(KmerAttributes)
+              << " " << offsetof(KmerAttributes, func_index) << " " << offsetof(KmerAttributes, otu_index) << " "
+              << offsetof(KmerAttributes, offset) << " " << offsetof(KmerAttributes, seq_id) << " "
+              << offsetof(KmerAttributes, protein_length) << "\n";
+}
+
 }  // namespace
 
 int main() {
@@ -93,6 +122,15 @@ int main() {
     while (std::getline(std::cin, line)) {
         if (line.size() < 3) continue;
         const char op = line[0];
+        if (op == 'P') {  // two hex fields
+            const size_t sp = line.find(' ', 2);
+            run_split(unhex(line.substr(2, sp - 2)), unhex(line.substr(sp + 1)));
+            continue;
+        }
+        if (op == 'L') {
+            run_layout();
+            continue;
+        }
         const std::string arg = unhex(line.substr(2));
         if (op == 'W')
             run_windows(arg);

@@ -1081,6 +1081,22 @@ static std::vector<std::string> split_str(const std::string& s, const std::strin
     return result;
 }
 
+// split (operators.h:80-91) as the tests see it: the parts' [begin, end) byte ranges of s into
+// se[2 * k], se[2 * k + 1] for k < cap; returns the number of parts (pinned by ref_split.npz)
+extern "C" uint64_t oracle_split(const char* s, uint64_t n, const char* d, uint64_t dn, uint64_t* se, uint64_t cap) {
+    const std::string str(s ? s : "", n), delim(d ? d : "", dn);
+    const std::vector<std::string> parts = split_str(str, delim);
+    uint64_t pos = 0;
+    for (uint64_t k = 0; k < parts.size(); ++k) {
+        if (k < cap) {
+            se[2 * k] = pos;
+            se[2 * k + 1] = pos + parts[k].size();
+        }
+        pos += parts[k].size() + delim.size();
+    }
+    return parts.size();
+}
+
 void oracle_find_best_call(const oracle_call* calls_in, uint64_t ncalls, const char* const* function_index,
                            uint64_t nfunc, uint16_t* out_fi, float* out_score, float* out_offset,
                            char* out_func, uint64_t out_func_cap) {

@@ -1,6 +1,8 @@
 // skm_caller.cpp -- see skm_caller.h.
 #include "skm_caller.h"
 
+#include "../skm_strutil.h"
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -12,6 +14,9 @@
 namespace skmf {
 
 bool read_function_index(const std::string& path, std::vector<std::string>& table, std::string& err) {
+    // call_functions.tcc:123-148: max id over the lines, then function_index_[stoi(parts[0])] =
+    // parts[1] with parts = split(line, "\t") (operators.h:80-91).  One read instead of two; a
+    // line without a tab (parts[1] out of range in the reference) names the empty string.
     std::ifstream f(path);
     if (!f) {
         err = "cannot read " + path;
@@ -21,15 +26,20 @@ bool read_function_index(const std::string& path, std::vector<std::string>& tabl
     int max_id = 0;
     std::string line;
     while (std::getline(f, line, '\n')) {
-        size_t tab = line.find('\t');
-        int id = std::stoi(line.substr(0, tab));
-        std::string name;
-        if (tab != std::string::npos) {
-            size_t t2 = line.find('\t', tab + 1);
-            name = line.substr(tab + 1, t2 == std::string::npos ? std::string::npos : t2 - tab - 1);
+        const std::vector<std::string> parts = skm_str::split(line, "\t");
+        int id = 0;
+        try {
+            id = std::stoi(parts[0]);
+        } catch (const std::exception&) {
+            err = "bad function.index line in " + path + ": '" + line + "'";
+            return false;
+        }
+        if (id < 0) {
+            err = "negative function index in " + path + ": '" + line + "'";
+            return false;
         }
         max_id = std::max(max_id, id);
-        rows.emplace_back(id, name);
+        rows.emplace_back(id, parts.size() > 1 ? parts[1] : std::string());
     }
     table.assign((size_t)max_id + 1, std::string());
     for (auto& r : rows) table[(size_t)r.first] = r.second;

@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "skm_strutil.h"
 #include "skm_util.h"
 
 namespace skm {
@@ -18,18 +19,6 @@ static thread_local std::string g_last_error;
 void set_last_error(const std::string& msg) { g_last_error = msg; }
 
 namespace {
-
-// operators.h:183-194 split(): empty fields kept, delimiter is a whole string
-std::vector<std::string> split_all(const std::string& s, const std::string& delim) {
-    std::vector<std::string> out;
-    std::string::size_type start = 0, end = 0;
-    while (end != std::string::npos) {
-        end = s.find(delim, start);
-        out.push_back(s.substr(start, end == std::string::npos ? std::string::npos : end - start));
-        start = end + delim.size();
-    }
-    return out;
-}
 
 // Matcher for boost::regex("^W?A[A|W]*W[B|W]*BW?") under regex_match (whole string).
 // Character classes include '|'.  Implemented as the NFA it denotes.
@@ -155,7 +144,7 @@ int skm_find_best_call(const skm_kmer_call* calls_in, size_t ncalls, const char*
         for (const auto& c : merged) {
             sum_scores += c.count;
             std::string f = fname(c.function_index);
-            std::vector<std::string> parts = split_all(f, " / ");
+            std::vector<std::string> parts = skm_str::split(f, " / ");  // call_functions.tcc:487
             std::string fk;
             for (const auto& p : parts) {
                 if (!func_key.count(p)) func_key[p] = next_func_key++;

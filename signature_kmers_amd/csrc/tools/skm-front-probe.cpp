@@ -9,11 +9,16 @@
 // image, one line per record "R <hex id> <hex def> <hex residues>" and one per parse error the
 // parser reported "E <line> <hex message> <hex id>", in the order the parser produced them, then
 // "END" (the shape of oracle/ref_pin's output, so tests compare with the reference's FastaParser).
+// skm-front-probe --split: one "<hex s> <hex delim>" per stdin line -> "P <n> <hex part> ..." from
+// the shared split (skm_strutil.h; oracle/ref_pin's P output shape).
+// skm-front-probe --function-index FILE: read_function_index -> one "<index> <hex name>" per slot.
 #include <cstdio>
 #include <iostream>
 #include <sstream>
 #include <string>
 
+#include "../skm_strutil.h"
+#include "skm_caller.h"
 #include "skm_front.h"
 
 using namespace skmf;
@@ -42,7 +47,28 @@ int main(int argc, char** argv) {
         std::cout << "n_residues " << f.n_residues << " residues " << f.residues.size() << "\n";
         return 0;
     }
+    if (argc == 3 && std::string(argv[1]) == "--function-index") {
+        std::vector<std::string> table;
+        std::string err;
+        if (!read_function_index(argv[2], table, err)) {
+            std::cerr << err << "\n";
+            return 1;
+        }
+        for (size_t i = 0; i < table.size(); ++i) std::cout << i << " " << hex(table[i]) << "\n";
+        return 0;
+    }
     std::string line;
+    if (argc == 2 && std::string(argv[1]) == "--split") {
+        while (std::getline(std::cin, line)) {
+            const size_t sp = line.find(' ');
+            const auto un = [](const std::string& h) { return h == "-" ? std::string() : unhex(h); };
+            const auto parts = skm_str::split(un(line.substr(0, sp)), un(line.substr(sp + 1)));
+            std::cout << "P " << parts.size();
+            for (const auto& p : parts) std::cout << " " << hex(p);
+            std::cout << "\n";
+        }
+        return 0;
+    }
     if (argc == 2 && std::string(argv[1]) == "--fasta-hex") {
         while (std::getline(std::cin, line)) {
             const std::string img = line == "-" ? std::string() : unhex(line);

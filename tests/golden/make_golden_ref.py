@@ -10,6 +10,12 @@ ref_windows.npz  seqs (concatenated bytes) / seq_off [n+1]; win (concatenated of
                  [n+1] = for_each_kmer<8>'s offsets per sequence.  The sequences put 'X' / '*'
                  at every offset of a window and at the sequence end, pairs of them, runs, lower
                  case 'x' (not ambiguous), B / Z / U / O / J, lengths 0..40, and long random ones.
+ref_split.npz    split(s, delim) of operators.h:80-91 over adversarial strings: strs / str_off,
+                 delims / delim_off, parts / part_off (the parts of all cases concatenated) and
+                 nparts [n] (parts per case); plus `layout` = sizeof, alignof and offsetof of
+                 StoredKmerData (avg_from_end, function_index, mean, median, var) and of
+                 KmerAttributes (func_index, otu_index, offset, seq_id, protein_length),
+                 kmer_data.h:105-128, as the reference compiles them.
 ref_fasta.npz    blobs / blob_off [n+1] (FASTA file images); out / out_off [n+1] = ref_pin's
                  lines per blob for the load_kmers_from_fasta driving ("F": def callback, parse,
                  then the caller's second parse_complete) and sout / sout_off for the (id, seq)
@@ -115,12 +121,35 @@ def fasta_inputs(rng):
     return blobs
 
 
+def split_inputs(rng):
+    """(s, delim) cases: the two delimiters the path splits on -- " / " (find_best_call's fusion
+    parts, call_functions.tcc:487) and "\\t" (read_function_index, :143) -- over empty fields,
+    leading / trailing / doubled delimiters, near-miss delimiters and names containing '/'."""
+    fixed = [b"", b" / ", b"a / ", b" / a", b"a / / b", b"a /  / b", b"a / b / c", b"a  /  b", b"a/b", b"a /b",
+             b"a/ b", b" /  / ", b"a / b / ", b" / / ", b"/", b"//", b" /", b"/ ", b"a / b/c / d", b"and/or / x",
+             b"1,3-beta / 1,4-alpha / ", b"x // y", b"a  / b", b"a /\tb", b"function 00001 / function 00003"]
+    cases = [(s, b" / ") for s in fixed]
+    tabs = [b"", b"\t", b"a\t", b"\ta", b"a\t\tb", b"0\talpha\t3\t1\t1\t0\t0", b"2\tgamma / delta\t9",
+            b"12\t\t", b"7\tx\ty\tz\t", b"\t\t\t", b"5\tname with / slash\t1", b"a b\tc d"]
+    cases += [(s, b"\t") for s in tabs]
+    alphabet = list(b"ab /\t")
+    for _ in range(400):
+        L = int(rng.integers(0, 24))
+        s = bytes(rng.choice(alphabet, size=L).astype(np.uint8))
+        cases.append((s, b" / " if rng.random() < 0.6 else b"\t"))
+    cases += [(b"a--b----c--", b"--"), (b"xyz", b"xyz"), (b"xyzxyz", b"xyz"), (b"aaa", b"aa")]
+    return cases
+
+
 def hexs(b: bytes) -> str:
     return b.hex() if b else "-"
 
 
 def run(reqs):
-    inp = "".join(f"{op} {hexs(b)}\n" for op, b in reqs)
+    return run_lines("".join(f"{op} {hexs(b)}\n" for op, b in reqs))
+
+
+def run_lines(inp: str):
     return subprocess.run([REF_PIN], input=inp.encode(), capture_output=True, check=True).stdout
 
 
@@ -146,6 +175,24 @@ def main():
     w_flat, w_off = cat(wins, np.int32)
     np.savez_compressed(os.path.join(HERE, "ref_windows.npz"), seqs=s_flat, seq_off=s_off, win=w_flat, win_off=w_off)
 
+    cases = split_inputs(np.random.default_rng(20261018))  # own stream: ref_fasta stays as it was
+    text = run_lines("".join(f"P {hexs(a)} {hexs(d)}\n" for a, d in cases) + "L -\n").decode().splitlines()
+    assert len(text) == len(cases) + 1
+    parts, nparts = [], []
+    for ln in text[:-1]:
+        c = ln.split(" ")
+        assert c[0] == "P" and len(c) == int(c[1]) + 2
+        nparts.append(int(c[1]))
+        parts += [b"" if h == "-" else bytes.fromhex(h) for h in c[2:]]
+    lay = text[-1].split(" ")
+    assert lay[0] == "L"
+    st_flat, st_off = cat([a for a, _ in cases])
+    de_flat, de_off = cat([d for _, d in cases])
+    pa_flat, pa_off = cat(parts)
+    np.savez_compressed(os.path.join(HERE, "ref_split.npz"), strs=st_flat, str_off=st_off, delims=de_flat,
+                        delim_off=de_off, parts=pa_flat, part_off=pa_off, nparts=np.array(nparts, np.int32),
+                        layout=np.array([int(x) for x in lay[1:]], np.int32))
+
     blobs = fasta_inputs(rng)
     outs = {}
     for op in ("F", "S"):
@@ -158,7 +205,8 @@ def main():
     g_flat, g_off = cat(outs["S"])
     np.savez_compressed(os.path.join(HERE, "ref_fasta.npz"), blobs=b_flat, blob_off=b_off, out=f_flat, out_off=f_off,
                         sout=g_flat, sout_off=g_off)
-    print(f"ref_windows: {len(seqs)} sequences, {len(w_flat)} windows; ref_fasta: {len(blobs)} blobs")
+    print(f"ref_windows: {len(seqs)} sequences, {len(w_flat)} windows; ref_split: {len(cases)} cases; "
+          f"ref_fasta: {len(blobs)} blobs")
 
 
 if __name__ == "__main__":

@@ -64,6 +64,8 @@ def olib():
         _lib.oracle_matrix_distance_mt.argtypes = [P, P, P, P, P, P, C.c_uint64, C.c_int32, P, C.c_uint64, C.c_int]
         _lib.oracle_kmer_windows.restype = C.c_uint32
         _lib.oracle_kmer_windows.argtypes = [C.c_char_p, C.c_uint32, P]
+        _lib.oracle_split.restype = C.c_uint64
+        _lib.oracle_split.argtypes = [C.c_char_p, C.c_uint64, C.c_char_p, C.c_uint64, P, C.c_uint64]
         _lib.oracle_find_best_call.argtypes = [P, C.c_uint64, C.POINTER(C.c_char_p), C.c_uint64, P, P, P,
                                                C.c_char_p, C.c_uint64]
     return _lib
@@ -78,6 +80,14 @@ def kmer_windows(seq: bytes) -> np.ndarray:
     out = np.zeros(max(len(seq), 1), np.uint32)
     n = olib().oracle_kmer_windows(seq, len(seq), _p(out))
     return out[:n]
+
+
+def split(s: bytes, delim: bytes) -> list:
+    """The oracle's restatement of split() (operators.h:80-91)."""
+    cap = len(s) + 2
+    se = np.zeros(2 * cap, np.uint64)
+    n = olib().oracle_split(s, len(s), delim, len(delim), _p(se), cap)
+    return [s[int(se[2 * k]):int(se[2 * k + 1])] for k in range(n)]
 
 
 def build(residues, seq_off, seq_len, seq_func, seq_id, n_functions):

@@ -185,3 +185,27 @@ def test_malformed_bdz_images_are_rejected_before_any_device_use(skm, tmp_path):
     for b in bad:
         rc, msg = open_err(b)
         assert rc != 0 and "kmer_data.mph" in msg, msg
+
+
+# function names that stress split(" / ") in the fusion keys (call_functions.tcc:487;
+# split itself is pinned against the reference in test_ref_pin_cpu.py)
+FUNCS_SPLIT = sorted(["alpha", "beta", "alpha / beta", "alpha / ", " / beta", "alpha / / beta", "x // y",
+                      "alpha /  / beta", "beta / alpha", "alpha / beta / ", "a/b", "hypothetical protein", ""],
+                     key=lambda s: s.encode())
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_find_best_call_split_edge_names_vs_oracle(skm, seed):
+    import signature_kmers_amd as skm_pkg
+    rng = np.random.default_rng(1000 + seed)
+    rows = [(int(rng.integers(0, len(FUNCS_SPLIT))), int(rng.integers(1, 15)), int(rng.integers(80, 900)))
+            for _ in range(int(rng.integers(1, 7)))]
+    if seed % 3 == 0:  # A W B shaped around the edge names
+        i = {f: k for k, f in enumerate(FUNCS_SPLIT)}
+        w = ["alpha / beta", "alpha / / beta", "alpha / ", " / beta"][seed % 4]
+        rows = [(i["alpha"], 6, 200), (i[w], 9, 500), (i["beta"], 6, 300)] + rows[:2]
+    c = mk_calls(rows)
+    a = skm_pkg.find_best_call(c, FUNCS_SPLIT)
+    b = oracle_ref.find_best_call(c, FUNCS_SPLIT)
+    assert a[0] == b[0] and a[1] == b[1], (rows, a, b)
+    assert np.float32(a[2]) == np.float32(b[2]) and np.float32(a[3]) == np.float32(b[3]), (rows, a, b)

@@ -108,3 +108,95 @@ def test_product_fasta_parser_matches_reference(probe):
         assert grecs == [r for r in recs if r[0]], b
         # the same error reports (message, line number, current id), in order
         assert gerrs == errs, b
+
+
+# ------------------------------------------------------------------ split / record layout
+# tests/golden/ref_split.npz: the reference's own split() (operators.h:80-91) over adversarial
+# strings and its StoredKmerData / KmerAttributes layout (kmer_data.h:105-128), from oracle/_ref.
+def ref_split():
+    z = np.load(os.path.join(GOLD, "ref_split.npz"))
+    strs, delims = _split(z["strs"], z["str_off"]), _split(z["delims"], z["delim_off"])
+    flat = _split(z["parts"], z["part_off"])
+    parts, k = [], 0
+    for n in z["nparts"]:
+        parts.append(flat[k:k + int(n)])
+        k += int(n)
+    return list(zip(strs, delims, parts)), [int(x) for x in z["layout"]]
+
+
+def test_split_vectors_cover_the_edge_cases():
+    cases, _ = ref_split()
+    got = {(s, d): p for s, d, p in cases}
+    assert got[(b"", b" / ")] == [b""]                      # empty string: one empty field
+    assert got[(b"a / ", b" / ")] == [b"a", b""]            # trailing delimiter: trailing empty field
+    assert got[(b" / a", b" / ")] == [b"", b"a"]
+    assert got[(b"a / / b", b" / ")] == [b"a", b"/ b"]      # the delimiter is a whole string
+    assert got[(b"12\t\t", b"\t")] == [b"12", b"", b""]
+    assert len(cases) > 400
+
+
+def test_oracle_split_matches_reference():
+    cases, _ = ref_split()
+    for s, d, p in cases:
+        assert oracle_ref.split(s, d) == p, (s, d)
+
+
+def test_product_split_matches_reference(probe):
+    cases, _ = ref_split()
+    inp = "".join(f"{s.hex() or '-'} {d.hex() or '-'}\n" for s, d, _ in cases).encode()
+    out = subprocess.run([probe, "--split"], input=inp, capture_output=True, check=True).stdout.decode().splitlines()
+    assert len(out) == len(cases)
+    for ln, (s, d, p) in zip(out, cases):
+        c = ln.split(" ")
+        assert c[0] == "P" and int(c[1]) == len(p), (s, d, ln)
+        assert [b"" if h == "-" else bytes.fromhex(h) for h in c[2:]] == p, (s, d)
+
+
+def test_product_read_function_index_matches_reference_split(probe, tmp_path):
+    """read_function_index (call_functions.tcc:123-148) restated from the pinned split: slot
+    stoi(parts[0]) = parts[1] of split(line, "\\t"), max id + 1 slots, later lines win."""
+    cases, _ = ref_split()
+    rng = np.random.default_rng(5)
+    names = [p[1] for s, d, p in cases if d == b"\t" and len(p) > 1] + \
+            [b"a / b", b"", b"x / ", b"name with / slash", b"  padded  "]
+    lines, want = [], {}
+    for k, nm in enumerate(names):
+        idx = int(rng.integers(0, 60)) if k % 3 else k
+        extra = b"\t".join(bytes(rng.choice(list(b"0123 /"), size=int(rng.integers(0, 4))).astype(np.uint8))
+                           for _ in range(int(rng.integers(0, 4))))
+        line = str(idx).encode() + b"\t" + nm + (b"\t" + extra if extra or k % 2 else b"")
+        lines.append(line)
+        parts = oracle_ref.split(line, b"\t")   # == the reference's split (test above)
+        want[int(parts[0])] = parts[1]
+    f = tmp_path / "function.index"
+    f.write_bytes(b"\n".join(lines) + b"\n")
+    out = subprocess.run([probe, "--function-index", str(f)], capture_output=True, check=True).stdout.decode()
+    got = [ln.split(" ") for ln in out.splitlines()]
+    assert len(got) == max(want) + 1
+    for i, h in got:
+        assert (b"" if h == "-" else bytes.fromhex(h)) == want.get(int(i), b""), i
+
+
+def test_stored_kmer_data_layout_matches_reference(tmp_path):
+    """skm_stored_kmer_data (include/skm.h), the Python mirror STORED_DTYPE and the oracle's
+    record all have the reference's StoredKmerData layout: the 10-byte kmer_data.dat record."""
+    import signature_kmers_amd as skm_pkg
+    _, lay = ref_split()
+    size, align, offs = lay[0], lay[1], lay[2:7]
+    assert (size, offs) == (10, [0, 2, 4, 6, 8])
+    for dt in (skm_pkg.STORED_DTYPE, oracle_ref.STORED_DTYPE):
+        assert dt.itemsize == size
+        assert [dt.fields[n][1] for n in ("avg_from_end", "function_index", "mean", "median", "var")] == offs
+    src = tmp_path / "lay.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "skm.h"\nint main(void) {\n'
+                   '  printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(skm_stored_kmer_data), _Alignof(skm_stored_kmer_data),\n'
+                   '    offsetof(skm_stored_kmer_data, avg_from_end), offsetof(skm_stored_kmer_data, function_index),\n'
+                   '    offsetof(skm_stored_kmer_data, mean), offsetof(skm_stored_kmer_data, median),\n'
+                   '    offsetof(skm_stored_kmer_data, var));\n  return 0;\n}\n')
+    exe = tmp_path / "lay"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert got == [size, align] + offs
+    # KmerAttributes (kmer_data.h:105-112) is the reference's in-memory build record; the build
+    # keeps its fields in the 16-byte element instead (DESIGN.md section 2) -- pinned for the record
+    assert lay[7:] == [16, 4, 0, 2, 4, 8, 12]
