@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--cli-queries", type=int, default=10_000_000,
                     help="cli_call leg: bin/kmers-call-functions end to end on this many query proteins (FASTA) "
                          "against the cli_build leg's DB (BASELINE configs[3]); 0 = off")
+    ap.add_argument("--mph", type=int, default=1,
+                    help="with --finish: the device BDZ over the whole headline kept set, checked on the device; N=1")
     ap.add_argument("--finish", type=int, default=1,
                     help="time skm_build_finish (the kept-set hand-off to host arrays) on the headline build; N=1")
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
@@ -282,8 +284,20 @@ def main():
                   "host_copy_s": c["finish_copy_us"] / 1e6,
                   "note": "skm_build_finish: device radix sort in key-range chunks, D2H through pinned staging, "
                           "copied out by the host pool; keys ascending in malloc'd host arrays"}
-        del k
         log(f"finish (hand-off of {finish['kept']:,} kept k-mers): {dt:.2f} s")
+        b.close()
+        if a.mph:  # the drop-in build's MPH + .dat over the whole kept set (kmers-build-signatures.cc:253-264)
+            t = time.perf_counter()
+            st = skm.mph_build_device(k.keys, k.data, None, None, seed=1, device=device, verify=True)
+            mph = {"seconds": time.perf_counter() - t, **st,
+                   "note": "skm_mph_build_device_ex over the whole headline kept set from host arrays (H2D of keys "
+                           "and records included, image files not written): GPU peeling, assignment, rank table, "
+                           "record placement, then the on-device check (slots a permutation of [0, n_keys), the "
+                           "annotate kernels' pair-line search == bdz_search for every key, .dat[slot] == record)"}
+            log(f"mph over {st['n_keys']:,} keys ({st['n_vertices']:,} vertices): {mph['seconds']:.2f} s, "
+                f"verified={st['verified']}")
+            finish["mph"] = mph
+        del k
     b.close()
     per_gpu = a.seqs_total // world
     out = {

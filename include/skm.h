@@ -160,7 +160,8 @@ int skm_build_kernel_timings(skm_build* b, char* names, size_t names_cap, float*
  * hand-off (device radix sort in key-range chunks, streamed through pinned staging): [33] its
  * host microseconds, [34] of them waiting for the device / PCIe, [35] copying pieces out on the
  * host pool, [36] chunks, and its device microseconds summed over the chunks: [37] selection,
- * [38] radix sort, [39] gather, [40] the D2H pieces; returns entries written. */
+ * [38] radix sort, [39] gather, [40] the D2H pieces; [41] the largest hand-off chunk (k-mers),
+ * [42] 1 if the hand-off used 64-bit arena indices (>= 2^32 k-mers); returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Host transport: the rank collectives of a multi-process build run by the caller on host
  * buffers, for ranks joined by a channel other than RCCL (the tests drive it with
@@ -340,6 +341,24 @@ int skm_mph_build(const uint64_t* keys, const skm_stored_kmer_data* data, size_t
  * device < 0 (or fewer than 1024 keys) runs the host builder.                                */
 int skm_mph_build_device(const uint64_t* keys, const skm_stored_kmer_data* data, size_t n, uint32_t seed,
                          const char* mph_path, const char* dat_path, int device);
+
+/* skm_mph_build_device with phase times and an optional on-device check, for builds up to the
+ * headline kept set (cmph's 32-bit m, n = 3r: n < 2^32, i.e. about 3.4 G keys).  mph_path /
+ * dat_path may be NULL (that image is not written).  verify != 0: every key's slot is < n and
+ * distinct (a slot bitmap), the annotate kernels' b == 7 pair-line search equals the generic
+ * bdz_search for every key, and .dat[slot] equals the key's record; a failure returns
+ * SKM_E_STATE.  Replaces build_perfect_hash (perfect_hash.h:11-69) as kmers-build-signatures
+ * runs it over the whole kept set (kmers-build-signatures.cc:253-264). */
+typedef struct skm_mph_stats {
+    double upload_s, peel_s, assign_s, rank_s, place_s, verify_s, write_s, total_s;
+    uint64_t n_keys, n_vertices;
+    uint32_t attempts, peel_rounds;
+    int32_t verified;      /* 1: the check above ran and passed */
+    int32_t pad;
+} skm_mph_stats;
+int skm_mph_build_device_ex(const uint64_t* keys, const skm_stored_kmer_data* data, size_t n, uint32_t seed,
+                            const char* mph_path, const char* dat_path, int device, int verify,
+                            skm_mph_stats* stats);
 
 /* ------------------------------------------------------------------------------------------
  * Function calling.  Replaces FunctionCaller<CmphKmerDb>::process_aa_seq for a batch of query

@@ -120,6 +120,8 @@ _SIGS = {
     "skm_db_close": (None, [_P]),
     "skm_mph_build": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_char_p, C.c_char_p]),
     "skm_mph_build_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_char_p, C.c_char_p, C.c_int]),
+    "skm_mph_build_device_ex": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_char_p, C.c_char_p, C.c_int, C.c_int,
+                                          C.c_void_p]),
     "skm_query_create": (C.c_int, [C.POINTER(_P), _P, _P, _P, _P, C.c_size_t]),
     "skm_query_run": (C.c_int, [_P, C.POINTER(_AnnotOpts)]),
     "skm_query_last_timings": (C.c_int, [_P, C.POINTER(C.c_float), C.c_int]),
@@ -335,8 +337,8 @@ class SignatureBuilder:
         return self.counters()["passes"]
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 41)()
-        n = lib().skm_build_counters(self._h, v, 41)
+        v = (C.c_uint64 * 43)()
+        n = lib().skm_build_counters(self._h, v, 43)
         names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped",
                  "overflow_elements", "overflow_kept", "big_groups", "big_kept", "passes", "valid", "giant_chains",
                  "giant_max", "redone", "cap_overflow_scratch", "cap_split", "cap_long_samples", "cap_long_jobs",
@@ -344,7 +346,7 @@ class SignatureBuilder:
                  "long_samples", "routed", "add_batch_us", "prepare_upload_us", "prepare_plan_us", "prepare_rest_us",
                  "pass_groups", "add_pack_us", "add_dma_wait_us", "finish_us", "finish_wait_us", "finish_copy_us",
                  "finish_chunks", "finish_select_dev_us", "finish_sort_dev_us", "finish_gather_dev_us",
-                 "finish_d2h_dev_us"]
+                 "finish_d2h_dev_us", "finish_max_chunk", "finish_wide_index"]
         return {names[i]: int(v[i]) for i in range(n)}
 
     def debug_jobs(self, k: int = 64) -> list:
@@ -527,6 +529,29 @@ def mph_build(keys: np.ndarray, data: np.ndarray, mph_path: str, dat_path: str, 
     else:
         _check(lib().skm_mph_build_device(_ptr(keys), _ptr(data), len(keys), seed, mph_path.encode(),
                                           dat_path.encode(), device))
+
+
+class _MphStats(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("upload_s", "peel_s", "assign_s", "rank_s", "place_s", "verify_s",
+                                          "write_s", "total_s")] + \
+               [("n_keys", C.c_uint64), ("n_vertices", C.c_uint64), ("attempts", C.c_uint32),
+                ("peel_rounds", C.c_uint32), ("verified", C.c_int32), ("pad", C.c_int32)]
+
+
+def mph_build_device(keys: np.ndarray, data: np.ndarray, mph_path: str | None = None, dat_path: str | None = None,
+                     seed: int = 1, device: int = 0, verify: bool = True) -> dict:
+    """skm_mph_build_device_ex: the device BDZ construction (perfect_hash.h:11-69) up to cmph's
+    32-bit vertex space, with its phase times; None paths skip writing that image; verify checks
+    on the device that the slots are a permutation, that the annotate kernels' pair-line search
+    agrees with bdz_search for every key and that every .dat record is its key's."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    data = np.ascontiguousarray(data, dtype=STORED_DTYPE)
+    st = _MphStats()
+    _check(lib().skm_mph_build_device_ex(_ptr(keys), _ptr(data), len(keys), seed,
+                                         mph_path.encode() if mph_path else None,
+                                         dat_path.encode() if dat_path else None, device, 1 if verify else 0,
+                                         C.byref(st)))
+    return {n: getattr(st, n) for n, _ in _MphStats._fields_ if n != "pad"}
 
 
 class CmphKmerDb:

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <cmath>
 #include <fstream>
@@ -1404,9 +1405,19 @@ void skm_calls_free(skm_calls* c) {
 //                   (unassigned = 3 = 0 mod 3); edges of one round never share a free vertex
 //                   and their other vertices were freed in later rounds, so a round is parallel
 //   rank table on the host from g; records placed by the device lookup.
-// Any acyclic peel order gives a valid minimal perfect hash; this one is deterministic.
+// Any acyclic peel order gives a valid minimal perfect hash; this one is deterministic (the
+// frontier ORDER depends on atomics, the peeled SET of a round and the g values do not).
+//
+// Sized for the headline build's kept set (C3: 2.89 G keys, 3.55 G vertices): cmph's BDZ keeps
+// m, n and r as cmph_uint32, so every key, edge and vertex index here is a u32 and the limit is
+// n = 3r < 2^32 (MPH_MAX_KEYS).  An edge's vertices are recomputed from its key where they are
+// needed (8 random bytes instead of a 12-byte edge array: 35 GB less HBM at C3); a peeled entry is
+// the edge id plus its free position in a byte array beside it; the peel state (degrees, XORs,
+// frontiers) is freed before the records are uploaded and placed.
 // ------------------------------------------------------------------------------------------
 namespace skm {
+
+constexpr uint64_t MPH_MAX_KEYS = 3400000000ull;  // n = 3 * ceil(1.23 m / 3) (+ retries) < 2^32 - 2^12
 
 struct MphDev {
     uint32_t r;
@@ -1422,15 +1433,15 @@ __device__ __forceinline__ void mph_verts(const MphDev& P, uint64_t k, uint32_t 
     v[2] = fastmod(c, P.r_magic, P.r) + 2u * P.r;
 }
 
-__global__ void k_mph_edges(const uint64_t* __restrict__ keys, uint32_t m, MphDev P, uint32_t* __restrict__ ev,
-                            uint32_t* __restrict__ deg, uint32_t* __restrict__ xr) {
+// (grids: m, n < 2^32 - 2^12, so a u32 global thread index never wraps)
+__global__ void k_mph_edges(const uint64_t* __restrict__ keys, uint32_t m, MphDev P, uint32_t* __restrict__ deg,
+                            uint32_t* __restrict__ xr) {
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= m) return;
     uint32_t v[3];
     mph_verts(P, keys[e], v);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        ev[3ull * e + j] = v[j];
         atomicAdd(&deg[v[j]], 1u);
         atomicXor(&xr[v[j]], e);
     }
@@ -1448,22 +1459,23 @@ __global__ void k_mph_frontier(const uint32_t* __restrict__ deg, uint32_t nv, ui
     if (one) fr[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = v;
 }
 
-// peeled entry: e << 2 | position of the free vertex in the edge
-__global__ void k_mph_peel(const uint32_t* __restrict__ fr, uint32_t nf, const uint32_t* __restrict__ ev,
-                           const uint32_t* __restrict__ deg, const uint32_t* __restrict__ xr,
-                           uint32_t* __restrict__ peeled, uint32_t* __restrict__ npeeled) {
+// peeled entry: the edge id in pe[], the position of its free vertex in pp[]
+__global__ void k_mph_peel(const uint32_t* __restrict__ fr, uint32_t nf, const uint64_t* __restrict__ keys, MphDev P,
+                           const uint32_t* __restrict__ deg, const uint32_t* __restrict__ xr, uint32_t* __restrict__ pe,
+                           uint8_t* __restrict__ pp, uint32_t* __restrict__ npeeled) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool take = false;
-    uint32_t ent = 0;
+    uint32_t e = 0, pos = 0;
     if (i < nf) {
         const uint32_t v = fr[i];
         if (deg[v] == 1u) {
-            const uint32_t e = xr[v];
+            e = xr[v];
+            uint32_t u[3];
+            mph_verts(P, keys[e], u);
             for (uint32_t p = 0; p < 3; ++p) {
-                const uint32_t u = ev[3ull * e + p];
-                if (deg[u] == 1u) {  // first degree-1 vertex of e peels it
-                    take = u == v;
-                    ent = (e << 2) | p;
+                if (deg[u[p]] == 1u) {  // first degree-1 vertex of e peels it
+                    take = u[p] == v;
+                    pos = p;
                     break;
                 }
             }
@@ -1474,21 +1486,26 @@ __global__ void k_mph_peel(const uint32_t* __restrict__ fr, uint32_t nf, const u
     uint32_t base = 0;
     if (lane == 0 && bal) base = atomicAdd(npeeled, (uint32_t)__popcll(bal));
     base = __shfl(base, 0);
-    if (take) peeled[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = ent;
+    if (take) {
+        const uint32_t o = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        pe[o] = e;
+        pp[o] = (uint8_t)pos;
+    }
 }
 
-__global__ void k_mph_apply(const uint32_t* __restrict__ peeled, uint32_t p0, uint32_t p1,
-                            const uint32_t* __restrict__ ev, uint32_t* __restrict__ deg, uint32_t* __restrict__ xr,
-                            uint32_t* __restrict__ fr, uint32_t* __restrict__ nfr) {
-    const uint32_t i = p0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= p1) return;
-    const uint32_t e = peeled[i] >> 2;
+__global__ void k_mph_apply(const uint32_t* __restrict__ pe, uint32_t p0, uint32_t p1, const uint64_t* __restrict__ keys,
+                            MphDev P, uint32_t* __restrict__ deg, uint32_t* __restrict__ xr, uint32_t* __restrict__ fr,
+                            uint32_t* __restrict__ nfr) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= p1 - p0) return;
+    const uint32_t e = pe[p0 + t];
+    uint32_t u[3];
+    mph_verts(P, keys[e], u);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const uint32_t u = ev[3ull * e + j];
-        const uint32_t old = atomicSub(&deg[u], 1u);
-        atomicXor(&xr[u], e);
-        if (old == 2u) fr[atomicAdd(nfr, 1u)] = u;
+        const uint32_t old = atomicSub(&deg[u[j]], 1u);
+        atomicXor(&xr[u[j]], e);
+        if (old == 2u) fr[atomicAdd(nfr, 1u)] = u[j];
     }
 }
 
@@ -1497,27 +1514,30 @@ __device__ __forceinline__ uint32_t gmod3(const uint32_t* g, uint32_t i) {
     return x == 3u ? 0u : x;
 }
 
-__global__ void k_mph_assign(const uint32_t* __restrict__ peeled, uint32_t p0, uint32_t p1,
-                             const uint32_t* __restrict__ ev, uint32_t* __restrict__ g) {
-    const uint32_t i = p0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= p1) return;
-    const uint32_t ent = peeled[i], e = ent >> 2, p = ent & 3u;
+__global__ void k_mph_assign(const uint32_t* __restrict__ pe, const uint8_t* __restrict__ pp, uint32_t p0, uint32_t p1,
+                             const uint64_t* __restrict__ keys, MphDev P, uint32_t* __restrict__ g) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= p1 - p0) return;
+    const uint32_t e = pe[p0 + t], p = pp[p0 + t];
+    uint32_t u[3];
+    mph_verts(P, keys[e], u);
     uint32_t s = 0, fv = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 3; ++j) {
-        const uint32_t u = ev[3ull * e + j];
         if (j == p)
-            fv = u;
+            fv = u[j];
         else
-            s += gmod3(g, u);
+            s += gmod3(g, u[j]);
     }
     const uint32_t val = (p + 6u - s) % 3u;
     // entries start at 3 (0b11): clear the bits that are 0 in val
     atomicAnd(&g[fv >> 4], ~((3u & ~val) << ((fv & 15u) * 2)));
 }
 
+// bad: 1 = a key's slot >= m, 2 = two keys on one slot (the slot bitmap), 4 = the pair-line
+// search disagrees with the generic one, 8 = a .dat record differs from its key's record
 __global__ void k_mph_place(const uint64_t* __restrict__ keys, uint32_t m, DevBdz D, const uint16_t* __restrict__ data,
-                            uint16_t* __restrict__ dat, uint32_t* __restrict__ bad) {
+                            uint16_t* __restrict__ dat, uint32_t* __restrict__ bits, uint32_t* __restrict__ bad) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     const uint64_t k = keys[i];
@@ -1526,18 +1546,80 @@ __global__ void k_mph_place(const uint64_t* __restrict__ keys, uint32_t m, DevBd
         atomicOr(bad, 1u);
         return;
     }
+    if (bits) {
+        const uint32_t bit = 1u << (idx & 31u);
+        if (atomicOr(&bits[idx >> 5], bit) & bit) atomicOr(bad, 2u);
+    }
 #pragma unroll
     for (int j = 0; j < 5; ++j) dat[5ull * idx + j] = data[5ull * i + j];
 }
 
+// the b == 7 (g word, rank) pair lines of the annotate lookup (db_upload's layout), built on the
+// device from g and the rank table: one thread per 128-vertex block
+__global__ void k_mph_blk(const uint32_t* __restrict__ g, uint64_t gwords, const uint32_t* __restrict__ rank,
+                          uint64_t nrank, uint64_t nblk, uint32_t* __restrict__ blk) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nblk) return;
+    uint32_t r = q < nrank ? rank[q] : 0u;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const uint64_t gi = 8 * q + (uint64_t)w;
+        const uint32_t x = gi < gwords ? g[gi] : 0xFFFFFFFFu;
+        blk[16 * q + 2 * (uint64_t)w] = x;
+        blk[16 * q + 2 * (uint64_t)w + 1] = r;
+        r += 16u - (uint32_t)__popc(x & (x >> 1) & 0x55555555u);
+    }
+}
+
+__global__ void k_mph_verify(const uint64_t* __restrict__ keys, uint32_t m, DevBdz D, const uint16_t* __restrict__ data,
+                             const uint16_t* __restrict__ dat, uint32_t* __restrict__ bad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint64_t k = keys[i];
+    const uint32_t idx = bdz_lookup(D, (uint32_t)k, (uint32_t)(k >> 32));
+    const uint32_t idx7 = bdz7_lookup(D, (uint32_t)k, (uint32_t)(k >> 32));
+    if (idx7 != idx) atomicOr(bad, 4u);
+    if (idx >= m) return;
+    bool same = true;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) same &= dat[5ull * idx + j] == data[5ull * i + j];
+    if (!same) atomicOr(bad, 8u);
+}
+
+// keys ascending?  [0] |= 1 if some adjacent pair is out of order, 2 if some adjacent pair is equal
+__global__ void k_mph_adjacent(const uint64_t* __restrict__ keys, uint32_t m, uint32_t* __restrict__ flags) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i + 1 >= m) return;
+    const uint64_t a = keys[i], b = keys[i + 1];
+    if (a > b) atomicOr(flags, 1u);
+    if (a == b) atomicOr(flags, 2u);
+}
+
 }  // namespace skm
 
-extern "C" int skm_mph_build_device(const uint64_t* keys, const skm_stored_kmer_data* data, size_t nkeys, uint32_t seed,
-                                    const char* mph_path, const char* dat_path, int device) {
+namespace {
+double secs_since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+}
+}  // namespace
+
+extern "C" int skm_mph_build_device_ex(const uint64_t* keys, const skm_stored_kmer_data* data, size_t nkeys,
+                                       uint32_t seed, const char* mph_path, const char* dat_path, int device, int verify,
+                                       skm_mph_stats* stats) {
     SKM_API_BEGIN
-    SKM_CHECK((nkeys == 0 || (keys && data)) && mph_path && dat_path, SKM_E_ARG, "null argument");
-    if (device < 0 || nkeys < 1024) return skm_mph_build(keys, data, nkeys, seed, mph_path, dat_path);
-    SKM_CHECK(nkeys < (1ull << 30), SKM_E_ARG, "too many keys for one BDZ (edge ids are 30 bits)");
+    SKM_CHECK(nkeys == 0 || (keys && data), SKM_E_ARG, "null argument");
+    const auto t_all = std::chrono::steady_clock::now();
+    skm_mph_stats st{};
+    st.n_keys = nkeys;
+    if (device < 0 || nkeys < 1024) {
+        SKM_CHECK(mph_path && dat_path, SKM_E_ARG, "the host builder writes both files");
+        const int rc = skm_mph_build(keys, data, nkeys, seed, mph_path, dat_path);
+        st.total_s = secs_since(t_all);
+        if (stats) *stats = st;
+        return rc;
+    }
+    SKM_CHECK(nkeys <= MPH_MAX_KEYS, SKM_E_ARG,
+              "too many keys for one BDZ: cmph keeps m, n = 3r as 32-bit words (n = 1.23 m < 2^32)");
     SKM_HIP(hipSetDevice(device));
     const uint32_t m = (uint32_t)nkeys;
     Bdz h;
@@ -1546,30 +1628,40 @@ extern "C" int skm_mph_build_device(const uint64_t* keys, const skm_stored_kmer_
     if (h.r % 2 == 0) h.r += 1;
     h.b = 7;
     h.k = 1u << h.b;
-    DevBuf dkeys, ddata, dev_, ddeg, dxr, dfr0, dfr1, dpeel, dcnt, dg;
+    auto t = std::chrono::steady_clock::now();
+    DevBuf dkeys, ddata, ddeg, dxr, dfr0, dfr1, dpe, dpp, dcnt, dg;
     dkeys.ensure(8ull * m);
-    ddata.ensure(10ull * m);
     SKM_HIP(hipMemcpy(dkeys.p, keys, 8ull * m, hipMemcpyHostToDevice));
-    SKM_HIP(hipMemcpy(ddata.p, data, 10ull * m, hipMemcpyHostToDevice));
-    dev_.ensure(12ull * m);
-    dpeel.ensure(4ull * m);
+    st.upload_s = secs_since(t);
+    t = std::chrono::steady_clock::now();
+    dpe.ensure(4ull * m);
+    dpp.ensure(m);
     dcnt.ensure(64);
-    uint32_t* cnt = dcnt.as<uint32_t>();  // [0] frontier A, [1] frontier B, [2] peeled, [3] bad
+    uint32_t* cnt = dcnt.as<uint32_t>();  // [0] frontier A, [1] frontier B, [2] peeled, [3] bad, [4] order
     std::mt19937 rng(seed);
     bool ok = false;
     std::vector<uint32_t> rounds;  // peel-list boundaries
+    MphDev P{};
     for (int attempt = 0; attempt < 1000 && !ok; ++attempt) {
         if (attempt > 0 && attempt % 20 == 0) h.r += 2;
         if (attempt == 1) {  // duplicate keys never give an acyclic graph: check once
-            std::vector<uint64_t> sk(keys, keys + nkeys);
-            std::sort(sk.begin(), sk.end());
-            SKM_CHECK(std::adjacent_find(sk.begin(), sk.end()) == sk.end(), SKM_E_ARG,
-                      "BDZ construction failed: duplicate keys");
+            SKM_HIP(hipMemset(cnt + 4, 0, 4));
+            hipLaunchKernelGGL(k_mph_adjacent, dim3(ceil_div(m, 256)), dim3(256), 0, 0, dkeys.as<uint64_t>(), m, cnt + 4);
+            uint32_t order = 0;
+            SKM_HIP(hipMemcpy(&order, cnt + 4, 4, hipMemcpyDeviceToHost));
+            bool dup = (order & 2u) != 0;
+            if (order & 1u) {  // not ascending: sort a host copy
+                std::vector<uint64_t> sk(keys, keys + nkeys);
+                std::sort(sk.begin(), sk.end());
+                dup = std::adjacent_find(sk.begin(), sk.end()) != sk.end();
+            }
+            SKM_CHECK(!dup, SKM_E_ARG, "BDZ construction failed: duplicate keys");
         }
         h.n = 3 * h.r;
+        SKM_CHECK((uint64_t)3 * h.r < 0xFFFFF000ull, SKM_E_ARG, "BDZ vertex count exceeds 32 bits");
         h.ranktablesize = (uint32_t)std::ceil(h.n / (double)h.k);
         h.seed = rng();
-        MphDev P{h.r, ~0ull / h.r + 1, h.seed};
+        P = MphDev{h.r, ~0ull / h.r + 1, h.seed};
         const uint32_t nv = h.n;
         ddeg.ensure(4ull * nv);
         dxr.ensure(4ull * nv);
@@ -1579,7 +1671,7 @@ extern "C" int skm_mph_build_device(const uint64_t* keys, const skm_stored_kmer_
         SKM_HIP(hipMemset(dxr.p, 0, 4ull * nv));
         SKM_HIP(hipMemset(dcnt.p, 0, 64));
         hipLaunchKernelGGL(k_mph_edges, dim3(ceil_div(m, 256)), dim3(256), 0, 0, dkeys.as<uint64_t>(), m, P,
-                           dev_.as<uint32_t>(), ddeg.as<uint32_t>(), dxr.as<uint32_t>());
+                           ddeg.as<uint32_t>(), dxr.as<uint32_t>());
         hipLaunchKernelGGL(k_mph_frontier, dim3(ceil_div(nv, 256)), dim3(256), 0, 0, ddeg.as<uint32_t>(), nv,
                            dfr0.as<uint32_t>(), cnt + 0);
         SKM_HIP(hipGetLastError());
@@ -1592,14 +1684,14 @@ extern "C" int skm_mph_build_device(const uint64_t* keys, const skm_stored_kmer_
         int fcur = 0;
         while (nf > 0) {
             hipLaunchKernelGGL(k_mph_peel, dim3(ceil_div(nf, 256)), dim3(256), 0, 0, cur->as<uint32_t>(), nf,
-                               dev_.as<uint32_t>(), ddeg.as<uint32_t>(), dxr.as<uint32_t>(), dpeel.as<uint32_t>(),
-                               cnt + 2);
+                               dkeys.as<uint64_t>(), P, ddeg.as<uint32_t>(), dxr.as<uint32_t>(), dpe.as<uint32_t>(),
+                               dpp.as<uint8_t>(), cnt + 2);
             SKM_HIP(hipMemset(cnt + (1 - fcur), 0, 4));
             uint32_t np = 0;
             SKM_HIP(hipMemcpy(&np, cnt + 2, 4, hipMemcpyDeviceToHost));
             if (np == npeeled) break;
-            hipLaunchKernelGGL(k_mph_apply, dim3(ceil_div(np - npeeled, 256)), dim3(256), 0, 0, dpeel.as<uint32_t>(),
-                               npeeled, np, dev_.as<uint32_t>(), ddeg.as<uint32_t>(), dxr.as<uint32_t>(),
+            hipLaunchKernelGGL(k_mph_apply, dim3(ceil_div(np - npeeled, 256)), dim3(256), 0, 0, dpe.as<uint32_t>(),
+                               npeeled, np, dkeys.as<uint64_t>(), P, ddeg.as<uint32_t>(), dxr.as<uint32_t>(),
                                nxt->as<uint32_t>(), cnt + (1 - fcur));
             SKM_HIP(hipGetLastError());
             rounds.push_back(np);
@@ -1609,40 +1701,61 @@ extern "C" int skm_mph_build_device(const uint64_t* keys, const skm_stored_kmer_
             fcur = 1 - fcur;
         }
         ok = npeeled == m;
+        st.attempts = (uint32_t)attempt + 1;
     }
     SKM_CHECK(ok, SKM_E_ARG, "BDZ construction failed: no acyclic 3-graph in 1000 attempts");
+    st.peel_rounds = (uint32_t)rounds.size() - 1;
+    st.n_vertices = h.n;
+    ddeg.release();
+    dxr.release();
+    dfr0.release();
+    dfr1.release();
+    st.peel_s = secs_since(t);
     // assignment, rounds in reverse
+    t = std::chrono::steady_clock::now();
     const uint64_t gwords = ceil_div(h.n, 16) + 1;
     dg.ensure(4 * gwords);
     SKM_HIP(hipMemset(dg.p, 0xFF, 4 * gwords));
     for (size_t ri = rounds.size() - 1; ri >= 1; --ri) {
         const uint32_t p0 = rounds[ri - 1], p1 = rounds[ri];
-        hipLaunchKernelGGL(k_mph_assign, dim3(ceil_div(p1 - p0, 256)), dim3(256), 0, 0, dpeel.as<uint32_t>(), p0, p1,
-                           dev_.as<uint32_t>(), dg.as<uint32_t>());
+        hipLaunchKernelGGL(k_mph_assign, dim3(ceil_div(p1 - p0, 256)), dim3(256), 0, 0, dpe.as<uint32_t>(),
+                           dpp.as<uint8_t>(), p0, p1, dkeys.as<uint64_t>(), P, dg.as<uint32_t>());
     }
     SKM_HIP(hipGetLastError());
+    dpe.release();
+    dpp.release();
     std::vector<uint32_t> gw(gwords);
     SKM_HIP(hipMemcpy(gw.data(), dg.p, 4 * gwords, hipMemcpyDeviceToHost));
+    st.assign_s = secs_since(t);
+    t = std::chrono::steady_clock::now();
     h.g.assign((size_t)std::ceil(h.n / 4.0), 0xFF);
     std::memcpy(h.g.data(), gw.data(), h.g.size());
     h.ranktable.assign(h.ranktablesize, 0);
     {
-        uint32_t count = 0;
-        for (uint32_t i = 0; i < h.ranktablesize; ++i) {
-            h.ranktable[i] = count;
-            const uint32_t v0 = i * h.k, v1 = std::min<uint32_t>(h.n, v0 + h.k);
-            for (uint32_t v = v0; v < v1; v += 16) {  // k = 128: whole words; entries past n stay 3
+        uint64_t count = 0;
+        for (uint64_t i = 0; i < h.ranktablesize; ++i) {
+            h.ranktable[i] = (uint32_t)count;
+            const uint64_t v0 = i * h.k, v1 = std::min<uint64_t>(h.n, v0 + h.k);
+            for (uint64_t v = v0; v < v1; v += 16) {  // k = 128: whole words; entries past n stay 3
                 const uint32_t w = gw[v >> 4];
                 count += 16u - (uint32_t)__builtin_popcount(w & (w >> 1) & 0x55555555u);
             }
         }
         SKM_CHECK(count == m, SKM_E_ARG, "BDZ construction: assigned vertex count != number of keys");
     }
+    st.rank_s = secs_since(t);
     // place the records: dat[search(key)] = data
-    DevBuf drank, ddat;
+    t = std::chrono::steady_clock::now();
+    DevBuf drank, ddat, dbits;
     drank.ensure(4ull * std::max<uint32_t>(h.ranktablesize, 1));
     SKM_HIP(hipMemcpy(drank.p, h.ranktable.data(), 4ull * h.ranktablesize, hipMemcpyHostToDevice));
+    ddata.ensure(10ull * m);
+    SKM_HIP(hipMemcpy(ddata.p, data, 10ull * m, hipMemcpyHostToDevice));
     ddat.ensure(10ull * m);
+    if (verify) {
+        dbits.ensure(4 * (ceil_div(m, 32) + 1));
+        SKM_HIP(hipMemset(dbits.p, 0, 4 * (ceil_div(m, 32) + 1)));
+    }
     DevBdz D{};
     D.g = dg.as<uint32_t>();
     D.ranktable = drank.as<uint32_t>();
@@ -1653,20 +1766,58 @@ extern "C" int skm_mph_build_device(const uint64_t* keys, const skm_stored_kmer_
     D.r_magic = ~0ull / h.r + 1;
     SKM_HIP(hipMemset(cnt + 3, 0, 4));
     hipLaunchKernelGGL(k_mph_place, dim3(ceil_div(m, 256)), dim3(256), 0, 0, dkeys.as<uint64_t>(), m, D,
-                       ddata.as<uint16_t>(), ddat.as<uint16_t>(), cnt + 3);
+                       ddata.as<uint16_t>(), ddat.as<uint16_t>(), verify ? dbits.as<uint32_t>() : nullptr, cnt + 3);
     SKM_HIP(hipGetLastError());
     uint32_t bad = 0;
     SKM_HIP(hipMemcpy(&bad, cnt + 3, 4, hipMemcpyDeviceToHost));
-    SKM_CHECK(!bad, SKM_E_ARG, "BDZ construction produced an out-of-range slot");
-    std::vector<skm_stored_kmer_data> kd(m);
-    SKM_HIP(hipMemcpy(kd.data(), ddat.p, 10ull * m, hipMemcpyDeviceToHost));
-    std::vector<uint8_t> img = bdz_dump(h);
-    std::ofstream fm(mph_path, std::ios::binary);
-    SKM_CHECK((bool)fm, SKM_E_IO, std::string("cannot write ") + mph_path);
-    fm.write((const char*)img.data(), (std::streamsize)img.size());
-    std::ofstream fd(dat_path, std::ios::binary);
-    SKM_CHECK((bool)fd, SKM_E_IO, std::string("cannot write ") + dat_path);
-    fd.write((const char*)kd.data(), (std::streamsize)(10ull * m));
-    SKM_CHECK((bool)fm && (bool)fd, SKM_E_IO, "write failed");
+    SKM_CHECK(!(bad & 1u), SKM_E_ARG, "BDZ construction produced an out-of-range slot");
+    SKM_CHECK(!(bad & 2u), SKM_E_STATE, "BDZ construction mapped two keys to one slot");
+    st.place_s = secs_since(t);
+    if (verify) {  // the annotate path's b == 7 pair-line search over every key, and the records
+        t = std::chrono::steady_clock::now();
+        dbits.release();
+        const uint64_t nblk = (uint64_t)h.n / 128 + 2;
+        DevBuf dblk;
+        dblk.ensure(64 * nblk);
+        hipLaunchKernelGGL(k_mph_blk, dim3(ceil_div(nblk, 256)), dim3(256), 0, 0, dg.as<uint32_t>(), gwords,
+                           drank.as<uint32_t>(), (uint64_t)h.ranktablesize, nblk, dblk.as<uint32_t>());
+        D.blk = dblk.as<uint32_t>();
+        hipLaunchKernelGGL(k_mph_verify, dim3(ceil_div(m, 256)), dim3(256), 0, 0, dkeys.as<uint64_t>(), m, D,
+                           ddata.as<uint16_t>(), ddat.as<uint16_t>(), cnt + 3);
+        SKM_HIP(hipGetLastError());
+        SKM_HIP(hipMemcpy(&bad, cnt + 3, 4, hipMemcpyDeviceToHost));
+        SKM_CHECK(!(bad & 4u), SKM_E_STATE, "BDZ pair-line search differs from the generic search");
+        SKM_CHECK(!(bad & 8u), SKM_E_STATE, "BDZ .dat record differs from its key's record");
+        st.verified = 1;
+        st.verify_s = secs_since(t);
+    }
+    t = std::chrono::steady_clock::now();
+    if (mph_path) {
+        std::vector<uint8_t> img = bdz_dump(h);
+        std::ofstream fm(mph_path, std::ios::binary);
+        SKM_CHECK((bool)fm, SKM_E_IO, std::string("cannot write ") + mph_path);
+        fm.write((const char*)img.data(), (std::streamsize)img.size());
+        SKM_CHECK((bool)fm, SKM_E_IO, "write failed");
+    }
+    if (dat_path) {
+        std::vector<skm_stored_kmer_data> kd(m);
+        SKM_HIP(hipMemcpy(kd.data(), ddat.p, 10ull * m, hipMemcpyDeviceToHost));
+        std::ofstream fd(dat_path, std::ios::binary);
+        SKM_CHECK((bool)fd, SKM_E_IO, std::string("cannot write ") + dat_path);
+        fd.write((const char*)kd.data(), (std::streamsize)(10ull * m));
+        SKM_CHECK((bool)fd, SKM_E_IO, "write failed");
+    }
+    st.write_s = secs_since(t);
+    st.total_s = secs_since(t_all);
+    if (stats) *stats = st;
     SKM_API_END
+}
+
+extern "C" int skm_mph_build_device(const uint64_t* keys, const skm_stored_kmer_data* data, size_t nkeys, uint32_t seed,
+                                    const char* mph_path, const char* dat_path, int device) {
+    if (!mph_path || !dat_path) {
+        skm::set_last_error("null argument");
+        return SKM_E_ARG;
+    }
+    return skm_mph_build_device_ex(keys, data, nkeys, seed, mph_path, dat_path, device, 0, nullptr);
 }

@@ -4871,6 +4871,9 @@ struct Tune {
                                      //   2 = k_heavy without its sequence-index sort, 4 = no chain kernels,
                                      //   8 = no stashed long chains, 16 = no per-pass k_chains,
                                      //   32 / 64 = k_overflow skips its entries of <= / > CAP elements
+    int handoff_index_limit = 0;     // tests: finish hand-offs of >= this many k-mers take u64 arena
+                                     //   indices (0: 2^32, where they are needed)
+    int handoff_max_chunk = 0;       // tests: cap on the hand-off's chunk size (0: memory-planned)
 };
 
 }  // namespace skm
@@ -7350,6 +7353,8 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "tail_async" ? &t.tail_async
                : n == "big_grid" ? &t.big_grid
                : n == "big_grid_large" ? &t.big_grid_large
+               : n == "handoff_index_limit" ? &t.handoff_index_limit
+               : n == "handoff_max_chunk" ? &t.handoff_max_chunk
                : n == "route_first_min" ? &t.route_first_min : nullptr;
         SKM_CHECK(f != nullptr, SKM_E_ARG, "unknown build option: " + n);
         SKM_CHECK(value >= 0 && value <= 0x7FFFFFFF, SKM_E_ARG, "option value out of range");
@@ -7486,7 +7491,7 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
     auto us = [](double sec) { return (uint64_t)(sec * 1e6); };
-    const uint64_t v[41] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+    const uint64_t v[43] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
                             b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total,
                             b->giant_jobs, b->giant_max, b->n_redo, b->tot_cap, b->split_cap, b->long_cap,
                             b->long_jobs_cap, b->demand[0], b->demand[1], b->demand[2], b->demand[3],
@@ -7495,8 +7500,9 @@ int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
                             us(b->add_wait_s), us(b->handoff.total_s), us(b->handoff.wait_s),
                             us(b->handoff.copy_s), b->handoff.chunks, (uint64_t)(1e3 * b->handoff.select_ms),
                             (uint64_t)(1e3 * b->handoff.sort_ms), (uint64_t)(1e3 * b->handoff.gather_ms),
-                            (uint64_t)(1e3 * b->handoff.d2h_ms)};
-    int n = std::min(cap, 41);
+                            (uint64_t)(1e3 * b->handoff.d2h_ms), b->handoff.max_chunk,
+                            (uint64_t)b->handoff.wide_index};
+    int n = std::min(cap, 43);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }
@@ -7632,7 +7638,8 @@ int skm_build_finish(skm_build* b, skm_kept* out) {
     SKM_HIP(hipStreamSynchronize(b->stream));
     // keys ascending: device radix sort in chunks, streamed to the host arrays (skm_output.hip)
     if (!b->pool) b->pool.reset(new HostPool(HostPool::default_threads()));
-    kept_handoff(src_k, src_d, n, b->stream, b->pool.get(), &out->keys, &out->data, &b->handoff);
+    kept_handoff(src_k, src_d, n, b->stream, b->pool.get(), &out->keys, &out->data, &b->handoff,
+                 (uint64_t)b->tune.handoff_index_limit, (uint64_t)b->tune.handoff_max_chunk);
     out->n = n;
     out->n_functions = F;
     out->distinct_signatures = total;
@@ -7698,7 +7705,7 @@ int skm_build_finish_slice(skm_build* b, int slice_bits, uint32_t slice, skm_kep
     // keys ascending: the slice sorted on the device and streamed out (skm_output.hip)
     if (!b->pool) b->pool.reset(new HostPool(HostPool::default_threads()));
     kept_handoff(dk.as<uint64_t>(), dd.as<skm_stored_kmer_data>(), n, st, b->pool.get(), &out->keys, &out->data,
-                 &b->handoff);
+                 &b->handoff, (uint64_t)b->tune.handoff_index_limit, (uint64_t)b->tune.handoff_max_chunk);
     out->n = n;
     out->n_functions = F;
     uint64_t total = b->n_kept;

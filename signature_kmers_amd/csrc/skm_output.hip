@@ -65,10 +65,13 @@ __global__ __launch_bounds__(OUT_THREADS) void k_out_hist(const uint64_t* __rest
 // over its waves and reserved with ONE atomic per tile -- a chunk selects ~1/22 of the arena's
 // keys, spread over it in hash order, so a per-wave reservation put ~40 M atomics on one address
 // per chunk at C3 (0.5 s per chunk)
+// per chunk -- the arena index is a u32 below 2^32 kept k-mers, a u64 from there (a multi-GPU
+// build hands rank 0 the union of every rank's kept set)
 constexpr int SEL_ITEMS = 16;
+template <class IdxT>
 __global__ __launch_bounds__(OUT_THREADS) void k_out_select(const uint64_t* __restrict__ keys, uint64_t n, uint32_t lo,
                                                             uint32_t hi, unsigned long long* __restrict__ cur,
-                                                            uint64_t* __restrict__ code, uint32_t* __restrict__ idx) {
+                                                            uint64_t* __restrict__ code, IdxT* __restrict__ idx) {
     constexpr int NW = OUT_THREADS / 64;
     __shared__ uint32_t wsum[NW];
     __shared__ unsigned long long base_s;
@@ -106,20 +109,21 @@ __global__ __launch_bounds__(OUT_THREADS) void k_out_select(const uint64_t* __re
         for (int j = 0; j < SEL_ITEMS; ++j)
             if ((mask >> j) & 1u) {
                 code[o] = c[j];
-                idx[o] = (uint32_t)(t0 + (uint64_t)j * OUT_THREADS + tid);
+                idx[o] = (IdxT)(t0 + (uint64_t)j * OUT_THREADS + tid);
                 ++o;
             }
         __syncthreads();  // wsum / base_s are rewritten by the next tile
     }
 }
 
+template <class IdxT>
 __global__ __launch_bounds__(OUT_THREADS) void k_out_gather(const uint64_t* __restrict__ keys,
                                                             const skm_stored_kmer_data* __restrict__ data,
-                                                            const uint32_t* __restrict__ idx, uint64_t m,
+                                                            const IdxT* __restrict__ idx, uint64_t m,
                                                             uint64_t* __restrict__ okeys,
                                                             skm_stored_kmer_data* __restrict__ odata) {
     for (uint64_t j = (uint64_t)blockIdx.x * OUT_THREADS + threadIdx.x; j < m; j += (uint64_t)gridDim.x * OUT_THREADS) {
-        const uint32_t i = idx[j];
+        const IdxT i = idx[j];
         okeys[j] = keys[i];
         odata[j] = data[i];
     }
@@ -141,11 +145,14 @@ void* host_alloc(size_t bytes) {
 
 }  // namespace
 
-void kept_handoff(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint64_t n, hipStream_t st,
-                  HostPool* pool, uint64_t** keys_out, skm_stored_kmer_data** data_out, HandoffStats* stats) {
+namespace {
+
+template <class IdxT>
+void kept_handoff_t(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint64_t n, hipStream_t st,
+                    HostPool* pool, uint64_t** keys_out, skm_stored_kmer_data** data_out, HandoffStats* stats,
+                    uint64_t max_chunk) {
     auto now = [] { return std::chrono::steady_clock::now(); };
     const auto t0 = now();
-    SKM_CHECK(n < 0xFFFFFFFFull, SKM_E_ARG, "more than 2^32 - 1 kept k-mers in one hand-off");
     uint64_t* hk = (uint64_t*)host_alloc(8 * n);
     skm_stored_kmer_data* hd = (skm_stored_kmer_data*)host_alloc(sizeof(skm_stored_kmer_data) * n);
     if (!hk || !hd) {
@@ -172,7 +179,15 @@ void kept_handoff(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint
     std::vector<uint32_t> hist(OUT_BINS);
     SKM_HIP(hipMemcpyAsync(hist.data(), d_hist.p, 4ull * OUT_BINS, hipMemcpyDeviceToHost, st));
     SKM_HIP(hipStreamSynchronize(st));
-    const uint64_t target = std::max<uint64_t>(1ull << 22, std::min<uint64_t>(1ull << 27, ceil_div(n, 4)));
+    // chunk target: <= 2^27 k-mers, and its device scratch (sort pairs in and out, the double-
+    // buffered gather, the radix sort's temporary ~ one more pair array) within 3/4 of the memory
+    // free now -- the builder's work buffers are still allocated at finish
+    const uint64_t per = 2 * (8 + sizeof(IdxT)) + 2 * (8 + sizeof(skm_stored_kmer_data)) + (8 + sizeof(IdxT));
+    size_t free_b = 0, total_b = 0;
+    SKM_HIP(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t fit = std::max<uint64_t>(1ull << 16, (uint64_t)(0.75 * (double)free_b) / per);
+    uint64_t target = std::max<uint64_t>(1ull << 22, std::min<uint64_t>(1ull << 27, ceil_div(n, 4)));
+    target = std::min(target, std::min(fit, max_chunk));
     std::vector<Chunk> chunks;
     uint64_t tot = 0, cmax = 0;
     for (uint32_t b = 0; b < OUT_BINS;) {
@@ -187,15 +202,16 @@ void kept_handoff(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint
     }
     SKM_CHECK(tot == n, SKM_E_STATE, "kept-set hand-off: histogram does not cover the arena");
     S.chunks = chunks.size();
+    S.max_chunk = cmax;
     // 2. device scratch for the largest chunk; double-buffered gather output
     DevBuf kin, kout, vin, vout, tmp, gk[2], gd[2];
     kin.ensure(8 * cmax);
     kout.ensure(8 * cmax);
-    vin.ensure(4 * cmax);
-    vout.ensure(4 * cmax);
+    vin.ensure(sizeof(IdxT) * cmax);
+    vout.ensure(sizeof(IdxT) * cmax);
     size_t tmp_bytes = 0;
-    SKM_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, kin.as<uint64_t>(), kout.as<uint64_t>(), vin.as<uint32_t>(),
-                                      vout.as<uint32_t>(), (size_t)cmax, 0, KEY_BITS, st));
+    SKM_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, kin.as<uint64_t>(), kout.as<uint64_t>(), vin.as<IdxT>(),
+                                      vout.as<IdxT>(), (size_t)cmax, 0, KEY_BITS, st));
     tmp.ensure(std::max<size_t>(tmp_bytes, 16));
     for (int k = 0; k < 2; ++k) {
         gk[k].ensure(8 * cmax);
@@ -243,16 +259,16 @@ void kept_handoff(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint
             if (c >= 2) SKM_HIP(hipStreamWaitEvent(st, ev_d[k], 0));  // chunk c-2 has left gk/gd[k]
             cmark.push_back(tmark(st));
             SKM_HIP(hipMemsetAsync(d_cur.p, 0, 8, st));
-            hipLaunchKernelGGL(k_out_select, dim3(grid), dim3(OUT_THREADS), 0, st, dkeys, n, C.lo, C.hi,
-                               d_cur.as<unsigned long long>(), kin.as<uint64_t>(), vin.as<uint32_t>());
+            hipLaunchKernelGGL(k_out_select<IdxT>, dim3(grid), dim3(OUT_THREADS), 0, st, dkeys, n, C.lo, C.hi,
+                               d_cur.as<unsigned long long>(), kin.as<uint64_t>(), vin.as<IdxT>());
             SKM_HIP(hipGetLastError());
             tmark(st);
             size_t tb = tmp.bytes;
-            SKM_HIP(rocprim::radix_sort_pairs(tmp.p, tb, kin.as<uint64_t>(), kout.as<uint64_t>(), vin.as<uint32_t>(),
-                                              vout.as<uint32_t>(), (size_t)C.n, 0, KEY_BITS, st));
+            SKM_HIP(rocprim::radix_sort_pairs(tmp.p, tb, kin.as<uint64_t>(), kout.as<uint64_t>(), vin.as<IdxT>(),
+                                              vout.as<IdxT>(), (size_t)C.n, 0, KEY_BITS, st));
             tmark(st);
             const uint32_t gg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(C.n, OUT_THREADS), 4096));
-            hipLaunchKernelGGL(k_out_gather, dim3(gg), dim3(OUT_THREADS), 0, st, dkeys, ddata, vout.as<uint32_t>(), C.n,
+            hipLaunchKernelGGL(k_out_gather<IdxT>, dim3(gg), dim3(OUT_THREADS), 0, st, dkeys, ddata, vout.as<IdxT>(), C.n,
                                gk[k].as<uint64_t>(), gd[k].as<skm_stored_kmer_data>());
             SKM_HIP(hipGetLastError());
             tmark(st);
@@ -337,6 +353,20 @@ void kept_handoff(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint
     cleanup();
     S.total_s = std::chrono::duration<double>(now() - t0).count();
     if (stats) *stats = S;
+}
+
+}  // namespace
+
+void kept_handoff(const uint64_t* dkeys, const skm_stored_kmer_data* ddata, uint64_t n, hipStream_t st,
+                  HostPool* pool, uint64_t** keys_out, skm_stored_kmer_data** data_out, HandoffStats* stats,
+                  uint64_t index_limit, uint64_t max_chunk) {
+    // index_limit (test hook, 0 = 2^32): hand-offs of at least that many k-mers take u64 arena indices
+    const uint64_t lim = index_limit ? index_limit : (1ull << 32);
+    if (n < lim)
+        kept_handoff_t<uint32_t>(dkeys, ddata, n, st, pool, keys_out, data_out, stats, max_chunk ? max_chunk : ~0ull);
+    else
+        kept_handoff_t<uint64_t>(dkeys, ddata, n, st, pool, keys_out, data_out, stats, max_chunk ? max_chunk : ~0ull);
+    if (stats) stats->wide_index = n >= lim ? 1 : 0;
 }
 
 }  // namespace skm

@@ -68,6 +68,11 @@ struct DevBuf {
         SKM_HIP(hipMalloc(&p, alloc));
         bytes = alloc;
     }
+    void release() {
+        if (p) SKM_HIP(hipFree(p));
+        p = nullptr;
+        bytes = 0;
+    }
     template <typename T>
     T* as() const {
         return reinterpret_cast<T*>(p);

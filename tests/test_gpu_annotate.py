@@ -200,6 +200,29 @@ def test_device_mph_build_is_minimal_perfect(skm, gpu, tmp_path, n):
     np.testing.assert_array_equal(db.lookup_keys(keys), idx)
 
 
+def test_device_mph_build_ex_verifies_and_matches(skm, gpu, tmp_path):
+    """skm_mph_build_device_ex: the same image as skm_mph_build_device; its on-device check
+    passes; NULL paths build and check without writing; duplicate keys are refused."""
+    rng = np.random.default_rng(11)
+    keys = np.unique(rng.integers(1, 2**63, size=400000, dtype=np.uint64))  # ascending
+    data = np.zeros(len(keys), skm.STORED_DTYPE)
+    data["function_index"] = np.arange(len(keys)) % 50000
+    data["var"] = np.arange(len(keys)) % 65521
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    skm.mph_build(keys, data, a + ".mph", a + ".dat", seed=5, device=0)
+    st = skm.mph_build_device(keys, data, b + ".mph", b + ".dat", seed=5, device=0, verify=True)
+    assert st["verified"] == 1 and st["n_keys"] == len(keys) and st["attempts"] >= 1 and st["peel_rounds"] > 0
+    assert st["n_vertices"] >= 1.23 * len(keys) - 3
+    assert open(a + ".mph", "rb").read() == open(b + ".mph", "rb").read()
+    assert open(a + ".dat", "rb").read() == open(b + ".dat", "rb").read()
+    st2 = skm.mph_build_device(keys, data, None, None, seed=5, device=0, verify=True)
+    assert st2["verified"] == 1 and st2["n_vertices"] == st["n_vertices"]
+    dup = keys.copy()
+    dup[1000] = dup[999]
+    with pytest.raises(skm.SkmError):
+        skm.mph_build_device(dup, data, None, None, seed=5, device=0)
+
+
 def _long_family(rng, n_copies, length, func, first_id):
     """n_copies ~1 %-mutated variants of one random protein of `length` residues, one function:
     their k-mers are kept with a mean length near `length`, so a query of that length makes a

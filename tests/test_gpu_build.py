@@ -300,6 +300,27 @@ def test_rerun_is_idempotent(skm, gpu):
     np.testing.assert_array_equal(a.data, c.data)
 
 
+def test_handoff_wide_index_and_small_chunks(skm, gpu):
+    """The finish hand-off's u64-index form (used from 2^32 kept k-mers, e.g. rank 0's gathered set
+    of a multi-GPU build) and memory-capped small chunks give the same sorted kept set."""
+    p = synth.generate_arrays(20000, 400, per_file=500, seed=8)
+    r, o, l, f, i, funcs = synth.build_inputs(p)
+    b = skm.SignatureBuilder(len(funcs))
+    b.add_batch(r, o, l, f, i)
+    a = b.finish()
+    assert b.counters()["finish_wide_index"] == 0
+    b.set_option("handoff_index_limit", 1)
+    b.set_option("handoff_max_chunk", 1 << 14)
+    c = b.finish()
+    k = b.counters()
+    b.close()
+    assert k["finish_wide_index"] == 1 and k["finish_chunks"] > 4 and len(a.keys) > 1 << 16
+    np.testing.assert_array_equal(a.keys, c.keys)
+    np.testing.assert_array_equal(a.data.view(np.uint8), c.data.view(np.uint8))
+    ref = oracle_ref.build(r, o, l, f, i, len(funcs))
+    assert_same(c, ref)
+
+
 def test_device_exact_division(skm, gpu):
     # reciprocal of every integer up to 2^22 (both signs) and 2^22 * 64 random quotients
     assert skm.debug_div_check(1 << 22, 64) == 0

@@ -16,7 +16,8 @@ reference's way (~780 GB for the multimap), so the check is split:
   lane_tail = 2^14 runs the deepest chains on wave pairs (k_chain_long, the tail batch included)
   and must give the same slice;
 * the whole kept set through skm_build_finish (2.9 G k-mers, the device-sorted hand-off): keys
-  strictly ascending, as many as the run kept, and its slice equal to finish_slice's;
+  strictly ascending, as many as the run kept, and its slice equal to finish_slice's; the BDZ
+  minimal perfect hash over all of it (skm_mph_build_device_ex), checked on the device;
 * size-independent properties over the whole build: the occurrences grouped equal the oracle's
   count of valid windows of the whole input (every window extracted once, none lost by the
   key-range passes or the per-pass compaction), seqs_with_func equals the per-function sequence
@@ -103,7 +104,7 @@ def test_c3_slice_bit_exact_and_whole_build_properties(skm, gpu):
         sel_d.append(k.data[a:a + (1 << 27)][m])
     assert np.array_equal(np.concatenate(sel_k), got.keys)
     assert np.array_equal(np.concatenate(sel_d).view(np.uint8), got.data.view(np.uint8))
-    del k, sel_k, sel_d
+    del sel_k, sel_d
     print("C3 finish: sorted, complete, slice consistent", flush=True)
     # the same build with the deepest chains on wave pairs (k_chain_long, the tail batch included)
     b.set_option("lane_long", 1 << 18)
@@ -113,6 +114,14 @@ def test_c3_slice_bit_exact_and_whole_build_properties(skm, gpu):
     got2 = b.finish_slice(SLICE_BITS, SLICE)
     b.close()
     print("C3 build (wave-pair chains) done", flush=True)
+    # the drop-in build's BDZ over the WHOLE kept set (kmers-build-signatures.cc:253-264,
+    # perfect_hash.h:11-69): ~2.9 G keys, ~3.55 G vertices -- within 20 % of cmph's 32-bit vertex
+    # space; checked on the device (slots a permutation, pair-line search == bdz_search for every
+    # key, .dat[slot] == the key's record)
+    st = skm.mph_build_device(k.keys, k.data, None, None, seed=1, device=0, verify=True)
+    assert st["verified"] == 1 and st["n_keys"] == c["kept"] and st["n_vertices"] > 1 << 31, st
+    print(f"C3 BDZ: {st['n_keys']:,} keys, {st['n_vertices']:,} vertices, {st['total_s']:.1f} s, verified", flush=True)
+    del k
     assert c["passes"] >= 8, c  # the headline's out-of-core path (16 passes at 288 GB)
     # pack the input for the oracle (16.5 GB of residues)
     lens = np.concatenate([p[2] for p in parts])
