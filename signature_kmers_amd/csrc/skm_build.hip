@@ -1793,7 +1793,8 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
 // pass p at off[p * (nwg + 1) + w] (exclusive scan over w), npos[p] = the pass's window count
 // (checked against the list's capacity: a larger pass fails the run, SKM_E_STATE).  One workgroup
 // per pass.
-constexpr uint32_t SEL_WG = 8192;   // tally rows: k_pass_ids workgroups = k_pass_emit waves
+constexpr uint32_t SEL_WG = 8192;   // tally rows: k_pass_ids workgroups = k_pass_emit waves (at least;
+                                    //   more when a row's span would pass 2^REL_BITS residues)
 __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ rows, uint32_t nwg, uint32_t P,
                                                    uint64_t* __restrict__ off, unsigned long long* __restrict__ npos,
                                                    uint64_t cap, unsigned long long* __restrict__ run) {
@@ -1825,28 +1826,31 @@ __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ 
 // scans, stages the tile's entries in its own 4 KB of LDS and writes one contiguous run per pass
 // at its k_sel_scan offset -- no workgroup barrier anywhere (round-4 first form: 1024-thread
 // workgroups hashing every window of every group, ~50 ms per group at C3).  An entry is the
-// window's position with its level-1 bucket above POS_BITS, so the pass's histogram (k_pass_hist)
-// needs no second look at the residues.  Reads 1 B of id + 1 B of residue per window per group,
-// writes 8 B per window of the group.
+// window's 43-bit key hash with the window's offset in its row's span above it (REL_BITS):
+// the pass's histogram (k_pass_hist) and the staged scatter (k_extract_stage_pos) take the bucket
+// and the rem bits from the hash, so neither looks at the residues again (round 6: the staging
+// re-read every residue line and re-hashed every window once per pass -- 16.5 GB per pass at C3);
+// the staging finds the window's position as row * span + offset, the row from k_sel_scan's
+// offsets.  Reads 1 B of id + 1 B of residue per window per group, writes 8 B per window of the group.
 constexpr uint32_t EMIT_THREADS = 64;
-constexpr int POS_BITS = 36;                 // pass entry: position | level-1 bucket << POS_BITS
-constexpr uint64_t POS_MASK = (1ull << POS_BITS) - 1ull;
+constexpr int REL_BITS = 21;                      // pass entry: offset in the row's span << 43 | mix43(key)
+constexpr uint64_t H43_MASK = (1ull << KEY_BITS) - 1ull;
+static_assert(KEY_BITS + REL_BITS == 64, "the pass entry is one u64");
 template <uint32_t G>
 __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __restrict__ res, const uint8_t* __restrict__ ids,
                                                            uint64_t rp, uint32_t pass0, uint64_t span,
-                                                           const uint64_t* __restrict__ seloff,
-                                                           uint64_t* __restrict__ pos, uint64_t cap, int rem_bits,
-                                                           uint32_t NB) {
-    __shared__ uint32_t s_out[16 * 64];  // the tile's entries, pass-major: window (10 bits) | bucket << 10
+                                                           const uint64_t* __restrict__ seloff, uint32_t nrows,
+                                                           uint64_t* __restrict__ pos, uint64_t cap) {
+    __shared__ uint64_t s_out[16 * 64];  // the tile's entries, pass-major: window in the tile << 43 | hash
     const uint32_t lane = threadIdx.x;
     uint64_t run[G];
 #pragma unroll
-    for (uint32_t q = 0; q < G; ++q) run[q] = seloff[(uint64_t)(pass0 + q) * (SEL_WG + 1) + blockIdx.x];
+    for (uint32_t q = 0; q < G; ++q) run[q] = seloff[(uint64_t)(pass0 + q) * (nrows + 1) + blockIdx.x];
     const uint64_t a = (uint64_t)blockIdx.x * span, e = min(rp, a + span);
     for (uint64_t t0 = a; t0 < e; t0 += 16ull * 64) {
         const uint64_t base = t0 + 16ull * lane;
         uint32_t qs[4] = {~0u, ~0u, ~0u, ~0u};  // byte t: the window's pass within the group (0xFF: none)
-        uint32_t bks[16];                       // the window's level-1 bucket
+        uint64_t hs[16];                        // the window's key hash
         uint32_t cnt[G];
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) cnt[q] = 0;
@@ -1882,7 +1886,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
                     if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
-                    bks[t] = ((any >> t) & 1u) ? (uint32_t)(mix43(k) >> rem_bits) & (NB - 1) : 0u;
+                    hs[t] = ((any >> t) & 1u) ? mix43(k) : 0ull;
                 }
             }
         }
@@ -1904,7 +1908,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 #pragma unroll
             for (uint32_t j = 0; j < G; ++j)
                 if (q == j) f = off[j]++;
-            s_out[f] = (16u * lane + (uint32_t)t) | (bks[t] << 10);
+            s_out[f] = ((uint64_t)(16u * lane + (uint32_t)t) << KEY_BITS) | hs[t];
         }
         wave_sync();
         for (uint32_t j = lane; j < qa[G]; j += 64) {
@@ -1915,8 +1919,8 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 #pragma unroll
             for (uint32_t k = 0; k < G; ++k)
                 if (q == k) o = run[k] + (j - qa[k]);
-            const uint32_t v = s_out[j];
-            if (o < cap) pos[(uint64_t)q * cap + o] = (t0 + (v & 1023u)) | ((uint64_t)(v >> 10) << POS_BITS);
+            const uint64_t v = s_out[j];
+            if (o < cap) pos[(uint64_t)q * cap + o] = ((t0 - a + (v >> KEY_BITS)) << KEY_BITS) | (v & H43_MASK);
         }
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) run[q] += qa[q + 1] - qa[q];
@@ -1929,7 +1933,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 constexpr uint32_t PH_THREADS = 512;
 __global__ __launch_bounds__(PH_THREADS) void k_pass_hist(const uint64_t* __restrict__ pos, uint64_t cap,
                                                           const unsigned long long* __restrict__ npos, uint32_t NB,
-                                                          uint32_t* __restrict__ hist) {
+                                                          int rem_bits, uint32_t* __restrict__ hist) {
     extern __shared__ uint32_t s_h[];  // [NB]
     const uint32_t q = blockIdx.y;
     for (uint32_t k = threadIdx.x; k < NB; k += PH_THREADS) s_h[k] = 0;
@@ -1946,7 +1950,7 @@ __global__ __launch_bounds__(PH_THREADS) void k_pass_hist(const uint64_t* __rest
         }
 #pragma unroll
         for (uint32_t u = 0; u < U; ++u)
-            if (v[u] != ~0ull) atomicAdd(&s_h[(uint32_t)(v[u] >> POS_BITS)], 1u);
+            if (v[u] != ~0ull) atomicAdd(&s_h[(uint32_t)((v[u] & H43_MASK) >> rem_bits) & (NB - 1)], 1u);
     }
     __syncthreads();
     uint32_t* hq = hist + (uint64_t)q * NB;
@@ -2142,12 +2146,17 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_extract_stage(ExtractArgs X, 
     }
 }
 
-// The staged level-0 scatter over a key-range pass's positions pos[0..n) (same staging rounds
-// as k_extract_stage; each position finds its sequence through blk2seq, reusing the previous
-// one while it still contains the window).
+// The staged level-0 scatter over a key-range pass's entries pos[0..n) (same staging rounds as
+// k_extract_stage).  An entry carries the window's key hash (bucket and rem bits, no residue
+// read) and its offset in its emission row's span; the row is found from the pass's row offsets
+// sel[0..nrows] (k_sel_scan): each thread's entries ascend, so it walks its row forward -- one
+// binary search per thread at the start, then a compare per entry.  Each position finds its
+// sequence through blk2seq, reusing the previous one while it still contains the window.
 template <int R, int MINB>
 __global__ __launch_bounds__(EX_THREADS, MINB) void k_extract_stage_pos(ExtractArgs X, const uint64_t* __restrict__ pos,
                                                                         const unsigned long long* __restrict__ np,
+                                                                        const uint64_t* __restrict__ sel, uint32_t nrows,
+                                                                        uint64_t sel_span,
                                                                         unsigned long long* __restrict__ cur0,
                                                                         uint64_t* __restrict__ out_hi,
                                                                         uint64_t* __restrict__ out_lo) {
@@ -2162,8 +2171,22 @@ __global__ __launch_bounds__(EX_THREADS, MINB) void k_extract_stage_pos(ExtractA
     const uint64_t begin = (uint64_t)blockIdx.x * X.span, end = min(begin + X.span, n);
     uint32_t s = 0xFFFFFFFFu;
     SeqMeta m{};
-    // the next round's entries are loaded before this round's gathers and LDS work (one level
-    // less of the entry -> window / sequence -> record chain in each round's latency)
+    // the emission row of this thread's first entry: the last row whose offset is <= it
+    uint32_t row = 0;
+    {
+        const uint64_t j0 = begin + (uint64_t)threadIdx.x * SC_POS;
+        uint32_t lo = 0, hi = nrows;  // sel[lo] <= j0 < sel[hi] (sel[nrows] = n)
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sel[mid] <= j0)
+                lo = mid;
+            else
+                hi = mid;
+        }
+        row = lo;
+    }
+    uint64_t row_end = sel[row + 1];
+    // the next round's entries are loaded before this round's sequence gathers and LDS work
     uint64_t nxt[SC_POS];
 #pragma unroll
     for (int t = 0; t < SC_POS; ++t) {
@@ -2173,31 +2196,30 @@ __global__ __launch_bounds__(EX_THREADS, MINB) void k_extract_stage_pos(ExtractA
     for (uint64_t base = begin; base < end; base += R) {
         if (threadIdx.x < 128) L.cnt[threadIdx.x] = 0;
         __syncthreads();
-        uint64_t pp[SC_POS], raw[SC_POS];
+        uint64_t ent[SC_POS];
 #pragma unroll
-        for (int t = 0; t < SC_POS; ++t)
-            pp[t] = nxt[t] != ~0ull ? nxt[t] & POS_MASK : ~0ull;  // k_pass_emit's entry: position | bucket << POS_BITS
+        for (int t = 0; t < SC_POS; ++t) ent[t] = nxt[t];
 #pragma unroll
         for (int t = 0; t < SC_POS; ++t) {
             const uint64_t j = base + R + (uint64_t)threadIdx.x * SC_POS + t;
             nxt[t] = j < end ? pos[j] : ~0ull;
         }
-#pragma unroll
-        for (int t = 0; t < SC_POS; ++t) raw[t] = pp[t] != ~0ull ? load_window(X.res, pp[t]) : 0ull;
         uint64_t eh[SC_POS], el[SC_POS];
         uint32_t rk[SC_POS], l0[SC_POS];
 #pragma unroll
         for (int t = 0; t < SC_POS; ++t) {
             eh[t] = el[t] = 0;
             rk[t] = l0[t] = 0;
-            const uint64_t p = pp[t];
-            if (p != ~0ull) {
+            if (ent[t] != ~0ull) {
+                const uint64_t j = base + (uint64_t)threadIdx.x * SC_POS + t;
+                while (j >= row_end) row_end = sel[++row + 1];  // rows without entries are skipped
+                const uint64_t p = (uint64_t)row * sel_span + (ent[t] >> KEY_BITS);
                 if (s == 0xFFFFFFFFu || p < m.pstart || p > m.pstart + m.len) {
                     s = X.blk2seq[p >> 6];
                     m = X.meta[s];
                 }
                 while (p > m.pstart + m.len) m = X.meta[++s];
-                const uint64_t h = window_hash(raw[t]);
+                const uint64_t h = ent[t] & H43_MASK;
                 const uint32_t bucket = (uint32_t)(h >> rem_bits) & (NB - 1);
                 // a heavy key routed in from a later pass keeps (natural ^ this pass) above its rem
                 const uint64_t route = (uint64_t)((uint32_t)(h >> (KEY_BITS - X.pass_bits)) ^ X.pass_id) << rem_bits;
@@ -2211,7 +2233,7 @@ __global__ __launch_bounds__(EX_THREADS, MINB) void k_extract_stage_pos(ExtractA
         const uint32_t tot = stage_reserve(L, 1u << SC_L0_BITS, cur0, 0);
 #pragma unroll
         for (int t = 0; t < SC_POS; ++t)
-            if (pp[t] != ~0ull) {
+            if (ent[t] != ~0ull) {
                 const uint32_t slot = L.off[l0[t]] + rk[t];
                 L.hi[slot] = eh[t];
                 L.lo[slot] = el[t];
@@ -3769,8 +3791,9 @@ struct HeavyArgs {
     unsigned long long* cursor;
     unsigned long long* queue;    // k_heavy's work queue (cleared per pass): keys are taken in list
                                   //   order, largest sub-buckets first (k_ovf_plan / k_ovf_split)
-    uint64_t* hi;                 // heavy elements, key-contiguous
-    uint64_t* lo;
+    uint64_t* rec;                // heavy members, key-contiguous: heavy_rec() (8 B) ...
+    uint32_t* len;                //   ... and the protein length (4 B) -- 12 B per member instead
+                                  //   of the 16-byte element; k_heavy's first read takes rec only
     uint32_t* s0;                 // radix-sort ping-pong of the best members' sequence indices
     uint32_t* s1;
     // giant chains (>= 2^giant_class samples): samples and jobs in this pass's slot buffers, run
@@ -3788,6 +3811,16 @@ struct HeavyArgs {
 };
 
 __device__ __forceinline__ uint32_t split_hash(uint32_t rem) { return (rem * 0x9E3779B1u) >> (32 - 12); }
+
+// A heavy member as k_heavy reads it: everything but the key (one key per range) and the length:
+//   s << 36 | (len - i) mod 2^16 << 16 | function     (s = global sequence index, 28 bits)
+// bits 32..35 stay 0, so ~0 never is a record (the kernels' "no member" marker)
+__device__ __forceinline__ uint64_t heavy_rec(uint64_t hi, uint64_t lo) {
+    return (lo & ~((1ull << 36) - 1ull)) | ((lo & 0xFFFFull) << 16) | (hi & 0xFFFFull);
+}
+__device__ __forceinline__ uint32_t hr_func(uint64_t x) { return (uint32_t)x & 0xFFFFu; }
+__device__ __forceinline__ uint32_t hr_off(uint64_t x) { return (uint32_t)(x >> 16) & 0xFFFFu; }
+__device__ __forceinline__ uint32_t hr_seq(uint64_t x) { return (uint32_t)(x >> 36); }
 
 constexpr uint32_t SPLIT_U = 8;   // elements per thread per iteration (loads issued together)
 
@@ -3927,8 +3960,8 @@ __global__ __launch_bounds__(BP_THREADS) void k_ovf_split(BucketArgs A, OvfScrat
                 if (v && hid != 0xFFFFu) {
                     const uint32_t pos = hid == h0 ? hbase + (uint32_t)__popcll(hm & lt) : atomicAdd(&s_hcur[hid], 1u);
                     const uint64_t o = s_hbase[hid] + pos;
-                    H.hi[o] = eh[u];
-                    H.lo[o] = el[u];
+                    H.rec[o] = heavy_rec(eh[u], el[u]);
+                    H.len[o] = elem_len(eh[u], el[u], A.glen);
                 }
             }
         }
@@ -4137,8 +4170,8 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
         const uint32_t q = s_key;
         if (q >= nkeys) break;
         const HeavyKey K = H.keys[q];
-        const uint64_t* hi = H.hi + K.off;
-        const uint64_t* lo = H.lo + K.off;
+        const uint64_t* rec = H.rec + K.off;
+        const uint32_t* rlen = H.len + K.off;
         const uint32_t n = K.n;
         uint32_t best_f = 0, cb = 0, NBK = 0;
         bool bucketed = false;
@@ -4151,24 +4184,23 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
             for (uint32_t d = tid; d < 256; d += nt) s_oh[d] = 0;
             __syncthreads();
             for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
-                uint64_t h[U], l[U];
+                uint64_t x[U];
 #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) {
                     const uint32_t j = j0 + u * nt + tid;
-                    h[u] = j < n ? hi[j] : ~0ull;
-                    l[u] = j < n ? lo[j] : 0ull;
+                    x[u] = j < n ? rec[j] : ~0ull;
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) {
-                    const bool v = h[u] != ~0ull;
-                    const uint32_t f = v ? (uint32_t)(h[u] & 0xFFFFu) : 0xFFFFFFFFu;
+                    const bool v = x[u] != ~0ull;
+                    const uint32_t f = v ? hr_func(x[u]) : 0xFFFFFFFFu;
                     // the lanes sharing lane 0's function add once (a heavy key is mostly one function)
                     const uint32_t f0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)f);
                     const uint64_t same = __ballot(v && f == f0);
                     if (v && f != f0) atomicAdd(&s_fb[f], 1u);
                     if (v && f == f0 && (same & lt) == 0) atomicAdd(&s_fb[f], (uint32_t)__popcll(same));
-                    wave_hist_add(s_oh, (uint32_t)(l[u] >> 8) & 255u, v);
-                    if (v) atomicAdd(&s_bk[(uint32_t)(((l[u] >> 36) * NBK) / H.n_total)], 1u);
+                    wave_hist_add(s_oh, hr_off(x[u]) >> 8, v);
+                    if (v) atomicAdd(&s_bk[(uint32_t)(((uint64_t)hr_seq(x[u]) * NBK) / H.n_total)], 1u);
                 }
             }
             __syncthreads();
@@ -4195,7 +4227,7 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
     #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) {
                     const uint32_t j = j0 + u * nt + tid;
-                    f[u] = j < n ? (uint32_t)(hi[j] & 0xFFFFu) : 0xFFFFFFFFu;
+                    f[u] = j < n ? hr_func(rec[j]) : 0xFFFFFFFFu;
                 }
     #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) {
@@ -4239,7 +4271,7 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
     #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) {
                     const uint32_t j = j0 + u * nt + tid;
-                    f[u] = j < n ? (uint32_t)(hi[j] & 0xFFFFu) : 0xFFFFFFFFu;
+                    f[u] = j < n ? hr_func(rec[j]) : 0xFFFFFFFFu;
                 }
     #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) cb += f[u] == best_f;
@@ -4280,27 +4312,28 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
             uint32_t* ls = H.s1 + K.off;
             uint32_t sum = 0;
             for (uint32_t j0 = 0; j0 < n; j0 += nt * U) {
-                uint64_t h[U], l[U];
+                uint64_t x[U];
+                uint32_t ln[U];
 #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) {
                     const uint32_t j = j0 + u * nt + tid;
-                    h[u] = j < n ? hi[j] : ~0ull;
-                    l[u] = j < n ? lo[j] : 0ull;
+                    x[u] = j < n ? rec[j] : ~0ull;
+                    ln[u] = j < n ? rlen[j] : 0u;
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) {
-                    if (h[u] == ~0ull) continue;
-                    const uint32_t sq = (uint32_t)(l[u] >> 36);
+                    if (x[u] == ~0ull) continue;
+                    const uint32_t sq = hr_seq(x[u]);
                     const uint32_t bk = (uint32_t)(((uint64_t)sq * NBK) / H.n_total);
-                    const uint32_t off = (uint32_t)(l[u] & 0xFFFFu);
+                    const uint32_t off = hr_off(x[u]);
                     if ((off >> 8) == hb) atomicAdd(&s_ol[off & 255u], 1u);
-                    const bool best = (uint32_t)(h[u] & 0xFFFFu) == best_f;
+                    const bool best = hr_func(x[u]) == best_f;
                     const uint32_t slot = atomicAdd(&s_bk[bk], 1u);
                     if (best) {
-                        sum += (uint32_t)(h[u] >> 48);  // the u16 accumulator needs len mod 2^16 only
+                        sum += ln[u] & 0xFFFFu;  // the u16 accumulator needs len mod 2^16 only
                         atomicAdd(&s_fb[bk], 1u);
                         ks[slot] = sq + 1u;
-                        ls[slot] = elem_len(h[u], l[u], A.glen);
+                        ls[slot] = ln[u];
                     } else {
                         ks[slot] = 0u;
                         ls[slot] = 0u;
@@ -4346,22 +4379,21 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
     #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) {
                     const uint32_t j = j0 + u * nt + tid;
-                    const uint64_t h = j < n ? hi[j] : ~0ull;
-                    f[u] = j < n ? (uint32_t)(h & 0xFFFFu) : 0xFFFFFFFFu;
-                    // the mean's accumulator is a u16: the element's length mod 2^16 (bits 48..63 of
-                    // the heavy copy, which keeps the length bits) is all it needs -- no glen gather
-                    gl[u] = (uint32_t)(h >> 48);
-                    l[u] = j < n ? lo[j] : 0ull;
+                    const uint64_t x = j < n ? rec[j] : ~0ull;
+                    f[u] = j < n ? hr_func(x) : 0xFFFFFFFFu;
+                    // the mean's accumulator is a u16: the length mod 2^16 is all it needs
+                    gl[u] = j < n ? rlen[j] & 0xFFFFu : 0u;
+                    l[u] = x;
                 }
     #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) gl[u] = f[u] == best_f ? gl[u] : 0u;
     #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) {
                     const bool v = f[u] != 0xFFFFFFFFu;
-                    const uint32_t s = (uint32_t)(l[u] >> 36);
+                    const uint32_t s = hr_seq(l[u]);
                     const bool best = f[u] == best_f;
                     if (v && !best && A.flags) mark_seq(A.flags, s);  // the best members' flags go out in sorted order below
-                    wave_hist_add(s_hist, (uint32_t)(l[u] >> 8) & 255u, v);
+                    wave_hist_add(s_hist, hr_off(l[u]) >> 8, v);
                     if (best) {
                         sum += gl[u];
                         smax = max(smax, s);
@@ -4390,7 +4422,7 @@ __global__ __launch_bounds__(HEAVY_WG) void k_heavy(BucketArgs A, HeavyArgs H) {
     #pragma unroll
                         for (uint32_t u = 0; u < U; ++u) {
                             const uint32_t j = j0 + u * nt + tid;
-                            o[u] = j < n ? (uint32_t)(lo[j] & 0xFFFFu) : 0xFFFFFFFFu;
+                            o[u] = j < n ? hr_off(rec[j]) : 0xFFFFFFFFu;
                         }
     #pragma unroll
                         for (uint32_t u = 0; u < U; ++u)
@@ -4982,7 +5014,7 @@ struct skm_build {
     hipEvent_t ev_tail_bp = nullptr, ev_tail_done = nullptr;
     bool tail_pending = false;          // the last pass's tail is still in flight on stream_tail
     hipEvent_t ev_part = nullptr, ev_split = nullptr;
-    DevBuf d_hv_keys, d_hv_hi, d_hv_lo, d_hv_s0, d_hv_s1;   // heavy keys of the split overflow
+    DevBuf d_hv_keys, d_hv_rec, d_hv_len, d_hv_s0, d_hv_s1;   // heavy keys of the split overflow
     DevBuf d_sub_tab, d_jobs2, d_jobs3;
 
     // pinned host staging for the pipeline's small readbacks
@@ -5023,7 +5055,8 @@ struct skm_build {
     DevBuf d_posg, d_histg, d_npos;      // d_npos: every pass's window count (k_sel_scan)
     uint32_t emit_g = 1;
     DevBuf d_selrows, d_seloff;          // per-workgroup windows of each pass, their scanned offsets
-    uint64_t sel_span = 0;               // windows per k_pass_ids / k_pass_emit workgroup
+    uint64_t sel_span = 0;               // windows per k_pass_ids / k_pass_emit workgroup (< 2^REL_BITS)
+    uint32_t sel_wg = SEL_WG;            // k_pass_ids / k_pass_emit workgroups (tally rows)
     hipStream_t stx = nullptr;
     hipEvent_t ev_staged = nullptr, ev_emit = nullptr;
     // pipelined passes (option overlap, one GPU, key-range passes): a second element buffer set,
@@ -5620,9 +5653,13 @@ void size_local(skm_build* b) {
         SKM_HIP(hipMemsetAsync(b->d_ids.p, 0xFF, ((b->rp + 15) & ~15ull) + 64, b->stream));  // padding: no window
         b->d_histg.ensure(sizeof(uint32_t) * (uint64_t)NB * b->emit_g);
         b->d_npos.ensure(8ull * P);
-        b->d_selrows.ensure(4ull * SEL_WG * P);
-        b->d_seloff.ensure(8ull * P * (SEL_WG + 1));
-        b->sel_span = ceil_div(ceil_div(std::max<uint64_t>(b->rp, 1), SEL_WG), 16) * 16;
+        // rows of at most 2^REL_BITS - 16 residues: an entry keeps its window's offset in the row
+        const uint64_t rmax = (1ull << REL_BITS) - 16;
+        b->sel_wg = (uint32_t)std::max<uint64_t>(SEL_WG, ceil_div(std::max<uint64_t>(b->rp, 1), rmax));
+        b->d_selrows.ensure(4ull * b->sel_wg * P);
+        b->d_seloff.ensure(8ull * P * (b->sel_wg + 1));
+        b->sel_span = ceil_div(ceil_div(std::max<uint64_t>(b->rp, 1), b->sel_wg), 16) * 16;
+        SKM_CHECK(b->sel_span < (1ull << REL_BITS), SKM_E_STATE, "pass entry row span exceeds REL_BITS");
         // count-kernel geometry from the largest pass (the kernels read the pass's own count)
         // (the pass's histogram comes from k_pass_emit: this grid is the staged scatter's alone;
         // the half-round variant runs four workgroups per CU)
@@ -5947,9 +5984,9 @@ void emit_group(skm_build* b, uint32_t g, hipStream_t st) {
     const int rem_bits = KEY_BITS - b->pass_bits - b->owner_bits - b->b1_bits;
     const uint64_t cap = std::max<uint64_t>(b->pass_max, 1);
 #define SKM_EMIT(GG)                                                                                                    \
-    SKM_LAUNCH_AS(b, "k_pass_emit", k_pass_emit<GG>, dim3(SEL_WG), dim3(EMIT_THREADS), 0, st, b->d_res.as<uint8_t>(), \
-                  b->d_ids.as<uint8_t>(), b->rp, g * G, b->sel_span, b->d_seloff.as<uint64_t>(), b->d_posg.as<uint64_t>(), \
-                  cap, rem_bits, NB)
+    SKM_LAUNCH_AS(b, "k_pass_emit", k_pass_emit<GG>, dim3(b->sel_wg), dim3(EMIT_THREADS), 0, st, b->d_res.as<uint8_t>(), \
+                  b->d_ids.as<uint8_t>(), b->rp, g * G, b->sel_span, b->d_seloff.as<uint64_t>(), b->sel_wg, \
+                  b->d_posg.as<uint64_t>(), cap)
     if (G == 4)
         SKM_EMIT(4);
     else if (G == 2)
@@ -5960,7 +5997,7 @@ void emit_group(skm_build* b, uint32_t g, hipStream_t st) {
     // the group's histograms from the entries' bucket bits (8 B per window read, no residues)
     SKM_HIP(hipMemsetAsync(b->d_histg.p, 0, sizeof(uint32_t) * NB * G, st));
     SKM_LAUNCH(b, k_pass_hist, dim3(256, G), dim3(PH_THREADS), 4u * NB, st, b->d_posg.as<uint64_t>(), cap,
-               b->d_npos.as<unsigned long long>() + (uint64_t)g * G, NB, b->d_histg.as<uint32_t>());
+               b->d_npos.as<unsigned long long>() + (uint64_t)g * G, NB, rem_bits, b->d_histg.as<uint32_t>());
     SKM_HIP(hipGetLastError());
     if (st != b->stream) SKM_HIP(hipEventRecord(b->ev_emit, st));
 }
@@ -6066,11 +6103,13 @@ void phase_extract(skm_build* b, uint32_t pass) {
         SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND_HALF, 4>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
                    b->d_posg.as<uint64_t>() + (uint64_t)(pass % b->emit_g) * std::max<uint64_t>(b->pass_max, 1),
                    b->d_npos.as<unsigned long long>() + pass,
+                   b->d_seloff.as<uint64_t>() + (uint64_t)pass * (b->sel_wg + 1), b->sel_wg, b->sel_span,
                    b->d_cur0.as<unsigned long long>(), stg_hi, stg_lo);
     else if (b->pass_bits)
         SKM_LAUNCH_AS(b, "k_extract_stage_pos", (k_extract_stage_pos<SC_ROUND, 2>), dim3(nwg), dim3(EX_THREADS), 0, st, X,
                    b->d_posg.as<uint64_t>() + (uint64_t)(pass % b->emit_g) * std::max<uint64_t>(b->pass_max, 1),
                    b->d_npos.as<unsigned long long>() + pass,
+                   b->d_seloff.as<uint64_t>() + (uint64_t)pass * (b->sel_wg + 1), b->sel_wg, b->sel_span,
                    b->d_cur0.as<unsigned long long>(), stg_hi, stg_lo);
     else
         SKM_LAUNCH(b, k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
@@ -6412,8 +6451,8 @@ void phase_group(skm_build* b, uint32_t pass) {
     H.nkeys = ctr_d + 18;  // cleared with the pass's counters
     H.cursor = ctr_d + 19;
     H.queue = ctr_d + 20;
-    H.hi = b->d_hv_hi.as<uint64_t>();
-    H.lo = b->d_hv_lo.as<uint64_t>();
+    H.rec = b->d_hv_rec.as<uint64_t>();
+    H.len = b->d_hv_len.as<uint32_t>();
     H.s0 = b->d_hv_s0.as<uint32_t>();
     H.s1 = b->d_hv_s1.as<uint32_t>();
     H.nosort = (b->tune.diag & 2) ? 1u : 0u;
@@ -6574,8 +6613,8 @@ void alloc_caps(skm_build* b) {
     b->d_jobs2.ensure(sizeof(Job) * b->jobs2_cap);
     const uint32_t key_min = (uint32_t)std::max(b->tune.heavy_min, 2);
     b->d_hv_keys.ensure(sizeof(HeavyKey) * (Sp / key_min + 16));
-    b->d_hv_hi.ensure(8 * Sp);
-    b->d_hv_lo.ensure(8 * Sp);
+    b->d_hv_rec.ensure(8 * Sp);
+    b->d_hv_len.ensure(4 * Sp);
     b->d_hv_s0.ensure(4 * Sp);
     b->d_hv_s1.ensure(4 * Sp);
     b->d_ovf2.ensure(sizeof(OvfEntry) * std::max<uint64_t>(b->ovf_cap, 1));
@@ -6641,11 +6680,11 @@ void begin_run(skm_build* b) {
     if (b->pass_bits) {
         const uint32_t P = 1u << b->pass_bits;
         // every window's pass id and every workgroup's windows per pass (k_pass_emit's input and offsets)
-        SKM_LAUNCH(b, k_pass_ids, dim3(SEL_WG), dim3(256), 4u * P + (b->route ? (1u << BLOOM_BITS) / 8 : 0u), st,
+        SKM_LAUNCH(b, k_pass_ids, dim3(b->sel_wg), dim3(256), 4u * P + (b->route ? (1u << BLOOM_BITS) / 8 : 0u), st,
                    b->d_res.as<uint8_t>(), b->rp, b->pass_bits, 0, b->d_ids.as<uint8_t>(), nullptr,
                    b->route ? b->d_bloom.as<uint32_t>() : nullptr, P, b->d_selrows.as<uint32_t>(), b->sel_span,
                    route_arg(b));
-        SKM_LAUNCH(b, k_sel_scan, dim3(P), dim3(1024), 0, st, b->d_selrows.as<uint32_t>(), SEL_WG, P,
+        SKM_LAUNCH(b, k_sel_scan, dim3(P), dim3(1024), 0, st, b->d_selrows.as<uint32_t>(), b->sel_wg, P,
                    b->d_seloff.as<uint64_t>(), b->d_npos.as<unsigned long long>(), b->pass_max,
                    b->d_run.as<unsigned long long>());
     }
