@@ -55,120 +55,142 @@ void set_boost_math_modes(int mean_mode, int mad_mode) {
     g_mad_mode = mad_mode;
 }
 
-int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std::vector<std::string>& function_index,
-               bool ignore_hypo, int n_threads, std::vector<std::vector<SeqCall>>& out, std::string& err,
-               double* device_ms, uint64_t max_batch_residues, double* host_ms) {
-    const auto t_begin = std::chrono::steady_clock::now();
-    double dev_ms = 0;
+bool annot_opts_for(const std::vector<std::string>& function_index, bool ignore_hypo, skm_annot_opts& o,
+                    std::string& err) {
     auto hit = std::find(function_index.begin(), function_index.end(), "hypothetical protein");
     if (hit == function_index.end()) {  // process_aa_seq exits here (call_functions.tcc:269-274)
         err = "Cannot find hypothetical protein index";
-        return SKM_E_ARG;
+        return false;
     }
-    skm_annot_opts o{};
+    o = skm_annot_opts{};
     o.min_hits = 5;
     o.max_gap = 200;
     o.ignore_hypo = ignore_hypo ? 1 : 0;
     o.hypo_index = (int32_t)(hit - function_index.begin());
     o.mean_mode = g_mean_mode;
     o.mad_mode = g_mad_mode;
+    return true;
+}
+
+int annotate_batch(skm_db* db, const std::vector<const FastaFile*>& files, const skm_annot_opts& o, int n_threads,
+                   skm_calls* calls, std::string& err) {
+    *calls = skm_calls{};
+    uint64_t nres = 0, nseq = 0;
+    for (auto* f : files) {
+        nres += f->residues.size();
+        nseq += f->size();
+    }
+    std::vector<uint8_t> res;
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len;
+    const uint8_t* rp = nullptr;
+    if (files.size() == 1) {  // single file: its buffer directly
+        rp = files[0]->residues.data();
+        off = files[0]->off;
+        len = files[0]->len;
+    } else if (!files.empty()) {  // the batch's files side by side, copied by the host threads
+        std::vector<uint64_t> rbase(files.size() + 1, 0), sbase(files.size() + 1, 0);
+        for (size_t f = 0; f < files.size(); ++f) {
+            rbase[f + 1] = rbase[f] + files[f]->residues.size();
+            sbase[f + 1] = sbase[f] + files[f]->size();
+        }
+        res.resize(nres);
+        off.resize(nseq);
+        len.resize(nseq);
+        std::atomic<size_t> nextf{0};
+        auto cp = [&]() {
+            for (size_t f; (f = nextf.fetch_add(1)) < files.size();) {
+                const FastaFile& F = *files[f];
+                std::memcpy(res.data() + rbase[f], F.residues.data(), F.residues.size());
+                for (size_t r = 0; r < F.size(); ++r) {
+                    off[sbase[f] + r] = rbase[f] + F.off[r];
+                    len[sbase[f] + r] = F.len[r];
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < std::max(1, std::min<int>(n_threads, (int)files.size())); ++t) th.emplace_back(cp);
+        cp();
+        for (auto& t : th) t.join();
+        rp = res.data();
+    }
+    const int rc = skm_annotate(db, rp, off.data(), len.data(), off.size(), &o, calls);
+    if (rc) err = skm_last_error();
+    return rc;
+}
+
+int best_calls_batch(const skm_calls& calls, const std::vector<const FastaFile*>& files,
+                     const std::vector<const char*>& fidx, int n_threads, const std::vector<std::vector<SeqCall>*>& out,
+                     std::string& err) {
+    std::vector<std::pair<size_t, size_t>> where;  // (file, record) per batch sequence
+    for (size_t f = 0; f < files.size(); ++f)
+        for (size_t r = 0; r < files[f]->size(); ++r) where.emplace_back(f, r);
+    if (where.size() != calls.n_seqs) {
+        err = "find_best_call: call list does not match the batch";
+        return SKM_E_STATE;
+    }
+    std::atomic<size_t> next{0};
+    std::atomic<int> first_rc{0};
+    std::mutex err_mu;  // skm_last_error() is per thread: the failing worker records its own message
+    std::string worker_err;
+    auto work = [&]() {
+        std::vector<char> fb(1 << 16);
+        const size_t chunk = 4096;
+        for (size_t s0; (s0 = next.fetch_add(chunk)) < where.size();) {
+            for (size_t s = s0; s < std::min(where.size(), s0 + chunk); ++s) {
+                SeqCall& c = (*out[where[s].first])[where[s].second];
+                float offset = 0;
+                int r = skm_find_best_call(calls.calls + calls.call_off[s], calls.call_off[s + 1] - calls.call_off[s],
+                                           fidx.data(), fidx.size(), &c.fi, &c.score, &offset, fb.data(), fb.size());
+                if (r) {
+                    std::lock_guard<std::mutex> lk(err_mu);
+                    if (!first_rc) {
+                        first_rc = r;
+                        worker_err = skm_last_error();
+                    }
+                }
+                c.func = fb.data();
+            }
+        }
+    };
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, n_threads), where.size() / 4096 + 1));
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    if (first_rc) err = worker_err.empty() ? std::string("find_best_call failed") : worker_err;
+    return first_rc;
+}
+
+int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std::vector<std::string>& function_index,
+               bool ignore_hypo, int n_threads, std::vector<std::vector<SeqCall>>& out, std::string& err,
+               double* device_ms, uint64_t max_batch_residues, double* host_ms) {
+    const auto t_begin = std::chrono::steady_clock::now();
+    double dev_ms = 0;
+    skm_annot_opts o{};
+    if (!annot_opts_for(function_index, ignore_hypo, o, err)) return SKM_E_ARG;
     std::vector<const char*> fidx(function_index.size());
     for (size_t i = 0; i < function_index.size(); ++i) fidx[i] = function_index[i].c_str();
-
     out.assign(files.size(), std::vector<SeqCall>());
     for (size_t f = 0; f < files.size(); ++f) out[f].resize(files[f]->size());
-
     size_t f0 = 0;
     while (f0 < files.size()) {
         // one device batch: whole files up to max_batch_residues residues
         size_t f1 = f0;
-        uint64_t nres = 0, nseq = 0;
-        while (f1 < files.size() && (f1 == f0 || nres + files[f1]->residues.size() <= max_batch_residues)) {
-            nres += files[f1]->residues.size();
-            nseq += files[f1]->size();
-            ++f1;
-        }
-        std::vector<uint8_t> res;
-        std::vector<uint64_t> off;
-        std::vector<uint32_t> len;
-        const uint8_t* rp = nullptr;
-        if (f1 == f0 + 1) {  // single file: use its buffer directly
-            rp = files[f0]->residues.data();
-            off = files[f0]->off;
-            len = files[f0]->len;
-        } else {  // the batch's files side by side, copied by the host threads
-            std::vector<uint64_t> rbase(f1 - f0 + 1, 0), sbase(f1 - f0 + 1, 0);
-            for (size_t f = f0; f < f1; ++f) {
-                rbase[f - f0 + 1] = rbase[f - f0] + files[f]->residues.size();
-                sbase[f - f0 + 1] = sbase[f - f0] + files[f]->size();
-            }
-            res.resize(nres);
-            off.resize(nseq);
-            len.resize(nseq);
-            std::atomic<size_t> nextf{f0};
-            auto cp = [&]() {
-                for (size_t f; (f = nextf.fetch_add(1)) < f1;) {
-                    const FastaFile& F = *files[f];
-                    std::memcpy(res.data() + rbase[f - f0], F.residues.data(), F.residues.size());
-                    for (size_t r = 0; r < F.size(); ++r) {
-                        off[sbase[f - f0] + r] = rbase[f - f0] + F.off[r];
-                        len[sbase[f - f0] + r] = F.len[r];
-                    }
-                }
-            };
-            std::vector<std::thread> th;
-            for (int t = 1; t < std::max(1, std::min<int>(n_threads, (int)(f1 - f0))); ++t) th.emplace_back(cp);
-            cp();
-            for (auto& t : th) t.join();
-            rp = res.data();
-        }
+        uint64_t nres = 0;
+        while (f1 < files.size() && (f1 == f0 || nres + files[f1]->residues.size() <= max_batch_residues))
+            nres += files[f1++]->residues.size();
+        const std::vector<const FastaFile*> batch(files.begin() + f0, files.begin() + f1);
         skm_calls calls{};
         auto t0 = std::chrono::steady_clock::now();
-        int rc = skm_annotate(db, rp, off.data(), len.data(), off.size(), &o, &calls);
+        int rc = annotate_batch(db, batch, o, n_threads, &calls, err);
         dev_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        if (rc) {
-            err = skm_last_error();
-            return rc;
-        }
-        // host find_best_call per sequence
-        std::vector<std::pair<size_t, size_t>> where;  // (file, record) per batch sequence
-        where.reserve(off.size());
-        for (size_t f = f0; f < f1; ++f)
-            for (size_t r = 0; r < files[f]->size(); ++r) where.emplace_back(f, r);
-        std::atomic<size_t> next{0};
-        std::atomic<int> first_rc{0};
-        std::mutex err_mu;  // skm_last_error() is per thread: the failing worker records its own message
-        std::string worker_err;
-        auto work = [&]() {
-            std::vector<char> fb(1 << 16);
-            const size_t chunk = 4096;
-            for (size_t s0; (s0 = next.fetch_add(chunk)) < where.size();) {
-                for (size_t s = s0; s < std::min(where.size(), s0 + chunk); ++s) {
-                    SeqCall& c = out[where[s].first][where[s].second];
-                    float offset = 0;
-                    int r = skm_find_best_call(calls.calls + calls.call_off[s], calls.call_off[s + 1] - calls.call_off[s],
-                                               fidx.data(), fidx.size(), &c.fi, &c.score, &offset, fb.data(), fb.size());
-                    if (r) {
-                        std::lock_guard<std::mutex> lk(err_mu);
-                        if (!first_rc) {
-                            first_rc = r;
-                            worker_err = skm_last_error();
-                        }
-                    }
-                    c.func = fb.data();
-                }
-            }
-        };
-        int nt = std::max(1, n_threads);
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) th.emplace_back(work);
-        work();
-        for (auto& t : th) t.join();
+        if (rc) return rc;
+        std::vector<std::vector<SeqCall>*> outp;
+        for (size_t f = f0; f < f1; ++f) outp.push_back(&out[f]);
+        rc = best_calls_batch(calls, batch, fidx, n_threads, outp, err);
         skm_calls_free(&calls);
-        if (first_rc) {
-            err = worker_err.empty() ? std::string("find_best_call failed") : worker_err;
-            return first_rc;
-        }
+        if (rc) return rc;
         f0 = f1;
     }
     if (device_ms) *device_ms = dev_ms;

@@ -35,4 +35,21 @@ int call_files(skm_db* db, const std::vector<const FastaFile*>& files, const std
                bool ignore_hypo, int n_threads, std::vector<std::vector<SeqCall>>& out, std::string& err,
                double* device_ms = nullptr, uint64_t max_batch_residues = 2000000000ull, double* host_ms = nullptr);
 
+// The two halves of call_files, for callers that pipeline them (kmers-call-functions overlaps
+// parsing, the device and find_best_call over groups of files, as the reference overlaps its
+// per-file tasks with its writer thread, kmers-call-functions.cc:147-189).
+// annot_opts_for: process_aa_seq's options (min_hits 5, max_gap 200, the hypothetical-protein
+// index -- an error when the function index has none, call_functions.tcc:269-274).
+bool annot_opts_for(const std::vector<std::string>& function_index, bool ignore_hypo, skm_annot_opts& o,
+                    std::string& err);
+// the device half for one batch of whole files: the windows looked up and the HitSet calls made
+// (skm_annotate over their sequences, in file order); *calls is released with skm_calls_free
+int annotate_batch(skm_db* db, const std::vector<const FastaFile*>& files, const skm_annot_opts& o, int n_threads,
+                   skm_calls* calls, std::string& err);
+// the host half: find_best_call per sequence on n_threads threads; out[f] is the call vector of
+// files[f] (sized by the caller)
+int best_calls_batch(const skm_calls& calls, const std::vector<const FastaFile*>& files,
+                     const std::vector<const char*>& fidx, int n_threads, const std::vector<std::vector<SeqCall>*>& out,
+                     std::string& err);
+
 }  // namespace skmf

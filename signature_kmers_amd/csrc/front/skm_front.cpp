@@ -4,6 +4,7 @@
 #include <cerrno>
 #include <dirent.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -13,6 +14,7 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <sstream>
 #include <stdexcept>
 #include <thread>
 
@@ -418,6 +420,23 @@ void FloatStats::add(float x) {
         float tmp = x - mean;
         variance = variance * (float)(count - 1) / (float)count + tmp * tmp / (float)(count - 1);
     }
+}
+
+double process_age_s() {
+    // /proc/self/stat field 22: start time in clock ticks after boot; /proc/uptime: seconds after boot
+    std::ifstream st("/proc/self/stat"), up("/proc/uptime");
+    std::string line;
+    double uptime = 0;
+    if (!std::getline(st, line) || !(up >> uptime)) return 0;
+    const size_t rp = line.rfind(')');  // the command name may hold spaces
+    if (rp == std::string::npos) return 0;
+    std::istringstream is(line.substr(rp + 2));
+    std::string tok;
+    unsigned long long start = 0;
+    for (int field = 3; field <= 22 && (is >> tok); ++field)
+        if (field == 22) start = std::strtoull(tok.c_str(), nullptr, 10);
+    const long hz = sysconf(_SC_CLK_TCK);
+    return hz > 0 ? std::max(0.0, uptime - (double)start / (double)hz) : 0.0;
 }
 
 std::string fmt_g(double v) {

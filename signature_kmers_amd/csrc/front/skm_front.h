@@ -117,6 +117,8 @@ void select_build_sequences(const FunctionMap& fm, const FastaFile& f, unsigned 
                             unsigned max_seqs_per_file, const std::set<std::string>& deleted_fids,
                             BuildBatch& out);
 
+// seconds since this process started (the CLIs' "startup" phase: loader, libskm, HIP runtime)
+double process_age_s();
 // ostream << float/double with the default format (precision 6, %g), incl. "-nan"/"inf".
 std::string fmt_g(double v);
 

@@ -32,8 +32,10 @@
 
 namespace skm {
 
-__global__ void k_exact_insert(const uint64_t* __restrict__ keys, uint64_t n, unsigned long long* __restrict__ tk,
-                               uint32_t* __restrict__ ti, uint64_t mask, uint32_t shift, uint32_t* __restrict__ bad) {
+// the kept keys into the 16-byte-slot table (exact_slot): the key by CAS on its slot's first 8
+// bytes, then its record index and record word; bad |= 1 for a key 0, 2 for a duplicate key
+__global__ void k_exact_insert(const uint64_t* __restrict__ keys, const uint16_t* __restrict__ dat, uint64_t n,
+                               uint4* __restrict__ tab, uint64_t mask, uint32_t shift, uint32_t* __restrict__ bad) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const unsigned long long k = keys[i];
@@ -43,9 +45,12 @@ __global__ void k_exact_insert(const uint64_t* __restrict__ keys, uint64_t n, un
     }
     uint64_t h = xmix(k) >> shift;
     for (;;) {
-        const unsigned long long prev = atomicCAS(&tk[h], 0ull, k);
+        unsigned long long* key = reinterpret_cast<unsigned long long*>(tab + h);
+        const unsigned long long prev = atomicCAS(key, 0ull, k);
         if (prev == 0ull) {
-            ti[h] = (uint32_t)i;
+            uint32_t* rest = reinterpret_cast<uint32_t*>(tab + h) + 2;
+            rest[0] = (uint32_t)i;
+            rest[1] = ((uint32_t)dat[5 * i + 1] << 16) | (uint32_t)dat[5 * i + 2];  // function_index, mean
             return;
         }
         if (prev == k) {
@@ -78,7 +83,35 @@ __global__ __launch_bounds__(LK_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             bad |= ((a || c == 0) ? 1u : 0u) << j;
         }
         uint32_t out[LK_POS];
-        if constexpr (MODE != LK_BDZ7) {
+        if constexpr (MODE == LK_EXACT) {
+            // the 16 windows' first probes issued together (one 16-byte slot each: key and record
+            // word); the few that land on another key walk on (linear probing, load <= 1/2)
+            uint4 sl[LK_POS];
+            uint64_t hp[LK_POS];
+            uint32_t live = 0;
+#pragma unroll
+            for (int t = 0; t < LK_POS; ++t) {
+                const uint64_t p = base + t;
+                uint32_t lo, hi;
+                key_at(w, t, lo, hi);
+                const bool ok = p < rp && ((bad >> t) & 0xFFu) == 0 && ((amb >> (t + 8)) & 1u) == 0;
+                hp[t] = xmix(((uint64_t)hi << 32) | lo) >> D.xshift;
+                sl[t] = ok ? D.xtab[hp[t]] : make_uint4(0u, 0u, 0u, 0u);
+                live |= (ok ? 1u : 0u) << t;
+            }
+#pragma unroll
+            for (int t = 0; t < LK_POS; ++t) {
+                uint32_t lo, hi;
+                key_at(w, t, lo, hi);
+                uint4 q = sl[t];
+                uint64_t h = hp[t];
+                while (((live >> t) & 1u) && !(q.x == lo && q.y == hi) && (q.x | q.y) != 0u) {
+                    h = (h + 1) & D.xmask;
+                    q = D.xtab[h];
+                }
+                out[t] = ((live >> t) & 1u) && (q.x | q.y) != 0u ? q.w : NO_HIT;  // function_index << 16 | mean
+            }
+        } else if constexpr (MODE != LK_BDZ7) {
 #pragma unroll
             for (int t = 0; t < LK_POS; ++t) {
                 const uint64_t p = base + t;
@@ -86,7 +119,7 @@ __global__ __launch_bounds__(LK_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                 if (p < rp && ((bad >> t) & 0xFFu) == 0 && ((amb >> (t + 8)) & 1u) == 0) {
                     uint32_t lo, hi;
                     key_at(w, t, lo, hi);
-                    const uint32_t idx = MODE == LK_EXACT ? exact_lookup(D, lo, hi) : bdz_lookup(D, lo, hi);
+                    const uint32_t idx = bdz_lookup(D, lo, hi);
                     if (idx < D.m) o = D.fm[idx];  // function_index << 16 | mean
                 }
                 out[t] = o;
@@ -952,19 +985,18 @@ void db_upload_kept(skm_db* db, const uint64_t* keys, const skm_stored_kmer_data
     db->dat_records = n;
     int lg = std::max(4, ilog2_ceil(2 * (uint64_t)std::max<size_t>(n, 1)));  // load factor <= 1/2
     const uint64_t T = 1ull << lg;
-    db->d_xkeys.ensure(8 * T);
-    db->d_xidx.ensure(4 * T);
+    db->d_xtab.ensure(16 * T);
     db->d_dat.ensure(std::max<size_t>(10 * n, 16));
-    SKM_HIP(hipMemset(db->d_xkeys.p, 0, 8 * T));
+    SKM_HIP(hipMemset(db->d_xtab.p, 0, 16 * T));
     if (n) SKM_HIP(hipMemcpy(db->d_dat.p, data, 10 * n, hipMemcpyHostToDevice));
     DevBdz& D = db->dev;
     D = DevBdz{};
     D.dat = db->d_dat.as<uint16_t>();
     D.m = (uint32_t)n;
-    D.xkeys = db->d_xkeys.as<unsigned long long>();
-    D.xidx = db->d_xidx.as<uint32_t>();
+    D.xtab = db->d_xtab.as<uint4>();
     D.xmask = T - 1;
     D.xshift = 64u - (uint32_t)lg;
+    D.fm = nullptr;  // the exact path reads the record word from the slot
     if (n) {
         DevBuf dk, dbad;
         dk.ensure(8 * n);
@@ -972,15 +1004,14 @@ void db_upload_kept(skm_db* db, const uint64_t* keys, const skm_stored_kmer_data
         SKM_HIP(hipMemcpy(dk.p, keys, 8 * n, hipMemcpyHostToDevice));
         SKM_HIP(hipMemset(dbad.p, 0, 4));
         hipLaunchKernelGGL(k_exact_insert, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, 0, dk.as<uint64_t>(),
-                           (uint64_t)n, db->d_xkeys.as<unsigned long long>(), db->d_xidx.as<uint32_t>(), T - 1,
-                           64u - (uint32_t)lg, dbad.as<uint32_t>());
+                           db->d_dat.as<uint16_t>(), (uint64_t)n, db->d_xtab.as<uint4>(), T - 1, 64u - (uint32_t)lg,
+                           dbad.as<uint32_t>());
         SKM_HIP(hipGetLastError());
         uint32_t bad = 0;
         SKM_HIP(hipMemcpy(&bad, dbad.p, 4, hipMemcpyDeviceToHost));
         SKM_CHECK(!(bad & 1u), SKM_E_ARG, "kept k-mer key 0 is not a valid k-mer");
         SKM_CHECK(!(bad & 2u), SKM_E_ARG, "duplicate kept k-mer keys");
     }
-    upload_fm(db, reinterpret_cast<const uint8_t*>(data), n);
 }
 
 bool read_file(const char* path, std::vector<uint8_t>& out) {

@@ -32,9 +32,12 @@ struct DevBdz {
     const uint32_t* blk;
     uint32_t m, r, b, seed;
     uint64_t r_magic;           // fastmod: ceil(2^64 / r)
-    // exact-key mode (KeptKmerDB, kept_kmer_db.h:20-27): open-addressing table of the kept keys
-    const unsigned long long* xkeys;  // [mask+1], 0 = empty (a k-mer key is never 0)
-    const uint32_t* xidx;             // record index of the key in xkeys[h]
+    // exact-key mode (KeptKmerDB, kept_kmer_db.h:20-27): open-addressing table of the kept keys,
+    // 16-byte slots (x, y = the key's low / high word, 0 = empty: a k-mer key is never 0; z = its
+    // record index; w = the record's function_index << 16 | mean), eight to a 128-byte line: a
+    // probe and the call path's record word arrive in one load (round 5 had the keys, the record
+    // indices and the records in three arrays: three lines per window)
+    const uint4* xtab;                // [mask+1]
     uint64_t xmask;
     uint32_t xshift;
 };
@@ -48,16 +51,20 @@ __device__ __forceinline__ uint64_t xmix(uint64_t k) {  // murmur3 fmix64 (bijec
     return k;
 }
 
-// KeptKmerDB::fetch: a hit iff the key is a kept k-mer; returns D.m on a miss.
-__device__ __forceinline__ uint32_t exact_lookup(const DevBdz& D, uint32_t lo, uint32_t hi) {
+// KeptKmerDB::fetch: the slot of the key, or an empty slot (x == y == 0) on a miss
+__device__ __forceinline__ uint4 exact_slot(const DevBdz& D, uint32_t lo, uint32_t hi) {
     const uint64_t k = ((uint64_t)hi << 32) | lo;
     uint64_t h = xmix(k) >> D.xshift;
     for (;;) {
-        const uint64_t t = D.xkeys[h];
-        if (t == k) return D.xidx[h];
-        if (t == 0) return D.m;
+        const uint4 t = D.xtab[h];
+        if ((t.x == lo && t.y == hi) || (t.x | t.y) == 0u) return t;
         h = (h + 1) & D.xmask;
     }
+}
+// the record index of a kept k-mer; D.m on a miss
+__device__ __forceinline__ uint32_t exact_lookup(const DevBdz& D, uint32_t lo, uint32_t hi) {
+    const uint4 t = exact_slot(D, lo, hi);
+    return (t.x | t.y) ? t.z : D.m;
 }
 
 __device__ __forceinline__ uint32_t fastmod(uint32_t a, uint64_t M, uint32_t d) {
@@ -166,6 +173,6 @@ struct skm_db {
     uint32_t m = 0;              // hash size (BDZ) or number of kept keys (exact)
     skm::Bdz bdz;
     uint64_t dat_records = 0;
-    skm::DevBuf d_g, d_rank, d_dat, d_xkeys, d_xidx, d_fm, d_blk;
+    skm::DevBuf d_g, d_rank, d_dat, d_xtab, d_fm, d_blk;
     skm::DevBdz dev{};
 };

@@ -180,6 +180,7 @@ int main(int argc, char** argv) {
         return 1;
     }
     const double t_start = now_s();
+    const double t_startup = process_age_s();  // before main: loader, libskm, HIP runtime
     // ranks: forked here (before any thread or GPU use), or given by an external launcher
     Mesh mesh;
     const std::string comm = op.get("comm", "rccl");
@@ -450,19 +451,30 @@ int main(int argc, char** argv) {
     double recall_dev_ms = 0;
     if (call_files(kdb, fptr, fidx, false, n_threads, calls, err, &recall_dev_ms)) die(err);
     skm_db_close(kdb);
-    for (size_t f = 0; f < files.size(); ++f) {
-        std::map<std::string, std::string> data;  // saver::data (first emplace wins), sorted by id
-        for (size_t r = 0; r < files[f].size(); ++r) {
-            const std::string& id = files[f].ids[r];
-            const SeqCall& c = calls[f][r];
-            std::string orig, orig_stripped;
-            fm.lookup_original_assignment(id, orig, orig_stripped);
-            if (orig_stripped != c.func && !data.count(id))
-                data.emplace(id, id + "\t" + orig + "\t" + orig_stripped + "\t" + c.func + "\t" +
-                                     std::to_string((int)c.fi) + "\t" + fmt_g(c.score) + "\n");
-        }
-        std::ofstream of(path_join(report_dir, files[f].filename));
-        for (auto& e : data) of << e.second;
+    {  // one report per file (kmers-build-signatures.cc:300-349), the files on the host threads
+        std::atomic<size_t> next_f{0};
+        auto report = [&]() {
+            for (size_t f; (f = next_f.fetch_add(1)) < files.size();) {
+                std::map<std::string, std::string> data;  // saver::data (first emplace wins), sorted by id
+                for (size_t r = 0; r < files[f].size(); ++r) {
+                    const std::string& id = files[f].ids[r];
+                    const SeqCall& c = calls[f][r];
+                    std::string orig, orig_stripped;
+                    fm.lookup_original_assignment(id, orig, orig_stripped);
+                    if (orig_stripped != c.func && !data.count(id))
+                        data.emplace(id, id + "\t" + orig + "\t" + orig_stripped + "\t" + c.func + "\t" +
+                                             std::to_string((int)c.fi) + "\t" + fmt_g(c.score) + "\n");
+                }
+                std::string text;
+                for (auto& e : data) text += e.second;
+                std::ofstream of(path_join(report_dir, files[f].filename));
+                of.write(text.data(), (std::streamsize)text.size());
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < std::min<int>(n_threads, (int)files.size()); ++t) th.emplace_back(report);
+        report();
+        for (auto& t : th) t.join();
     }
     const double t_recall = now_s() - t0;
     const double t_recall_dev = recall_dev_ms / 1000.0;
@@ -484,7 +496,8 @@ int main(int argc, char** argv) {
     // one machine-readable line of the phases (bench.py's cli_build leg)
     std::cerr << "phases: parse " << t_parse << " add " << t_add << " prepare " << t_prepare << " run " << t_run
               << " finish " << t_finish << " final_kmers " << t_final_kmers << " mph " << t_mph << " recall "
-              << t_recall << " recall_device " << t_recall_dev << " total " << now_s() - t_start << "\n";
+              << t_recall << " recall_device " << t_recall_dev << " total " << now_s() - t_start << " startup "
+              << t_startup << "\n";
     std::cerr << "all done\n";
     return 0;
 }

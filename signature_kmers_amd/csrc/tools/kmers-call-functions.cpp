@@ -6,7 +6,8 @@
 // "id\tfunc\tfunc_index\tscore\n" (kmers-call-functions.cc:178), files in input order, to -o or
 // stdout.  Window lookups and HitSet calls run on the GPU (skm_annotate), find_best_call on host.
 // --debug-hits prints the per-hit lines of the reference's debug hit callback
-// (kmers-call-functions.cc:109-118) before each file's calls.
+// (kmers-call-functions.cc:109-118) before each file's calls.  Parsing, the device, find_best_call
+// and the writer run as a pipeline over groups of files (see main).
 // Extra options: --device N; --boost-math-stats current|legacy (the Boost.Math mean / MAD the
 // reference was compiled against, call_functions.tcc:51-53: current = >= 1.76, legacy = the older
 // single running mean and |x(mid)| MAD).
@@ -20,6 +21,8 @@
 #include <iostream>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 
 #include "skm.h"
@@ -79,6 +82,7 @@ void debug_hits(skm_db* db, const std::vector<uint8_t>& dat, const FastaFile& f,
 }  // namespace
 
 int main(int argc, char** argv) {
+    const double t_startup = process_age_s();  // before main: loader, libskm, HIP runtime
     {  // libskm runs up to 8 streams at once: at least 8 hardware queues (read at the first HIP call)
         const char* q = getenv("GPU_MAX_HW_QUEUES");
         if (!q || atoi(q) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
@@ -124,26 +128,13 @@ int main(int argc, char** argv) {
     const std::string db_base = path_join(data_dir, "kmer_data");
     const std::string mph = db_base + ".mph", dat = db_base + ".dat";
     if (!file_exists(mph)) die("Database \"" + db_base + "\" does not exist");
-    skm_db* db = nullptr;
-    const auto t_open0 = std::chrono::steady_clock::now();
-    if (skm_db_open(&db, mph.c_str(), dat.c_str(), device)) die(skm_last_error());
-    const double t_open = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_open0).count();
     std::vector<std::string> fidx;
     if (!read_function_index(path_join(data_dir, "function.index"), fidx, err)) die(err);
     const bool ignore_hypo = op.has("ignore-hypo");
-
-    auto now_s = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-    double t0 = now_s();
-    std::vector<FastaFile> files;
-    if (!parse_fasta_files(inputs, files, n_threads, err)) die(err);
-    const double t_parse = now_s() - t0;
-    std::vector<const FastaFile*> fptr;
-    for (auto& f : files) fptr.push_back(&f);
-    std::vector<std::vector<SeqCall>> calls;
-    double dev_ms = 0, host_ms = 0;
-    if (call_files(db, fptr, fidx, ignore_hypo, n_threads, calls, err, &dev_ms, 2000000000ull, &host_ms)) die(err);
-    t0 = now_s();
-
+    skm_annot_opts aopts{};
+    if (!annot_opts_for(fidx, ignore_hypo, aopts, err)) die(err);
+    std::vector<const char*> fptr_idx(fidx.size());
+    for (size_t i = 0; i < fidx.size(); ++i) fptr_idx[i] = fidx[i].c_str();
     std::ofstream ofs;
     std::ostream* out = &std::cout;
     if (op.has("output-files")) {
@@ -156,49 +147,157 @@ int main(int argc, char** argv) {
     if (op.has("debug-hits")) {
         std::ifstream df(dat, std::ios::binary);
         datbuf.assign(std::istreambuf_iterator<char>(df), std::istreambuf_iterator<char>());
-        for (size_t i = 0; i < fidx.size(); ++i)
-            if (fidx[i] == "hypothetical protein") {
-                hypo = (int)i;
-                break;
-            }
+        hypo = aopts.hypo_index;
     }
-    // each file's lines formatted on the host threads, written in file order
-    std::vector<std::string> text(files.size());
-    {
-        std::atomic<size_t> next{0};
-        auto fmt = [&]() {
-            for (size_t f; (f = next.fetch_add(1)) < files.size();) {
-                std::string& buf = text[f];
-                for (size_t r = 0; r < files[f].size(); ++r) {
-                    const SeqCall& c = calls[f][r];
-                    buf += files[f].ids[r];
-                    buf += '\t';
-                    buf += c.func;
-                    buf += '\t';
-                    buf += std::to_string((unsigned)c.fi);
-                    buf += '\t';
-                    buf += fmt_g(c.score);
-                    buf += '\n';
+    // Pipelined over groups of input files, as the reference overlaps its per-file tasks with its
+    // writer thread (kmers-call-functions.cc:147-189): a parse stage (the files of a group on the
+    // host threads), the device stage (skm_annotate of the group), a host stage (find_best_call
+    // and each file's lines) and this thread writing the groups in input order.  The DB is opened
+    // (read + uploaded to HBM) while the first groups parse.  Output bytes are those of the
+    // one-phase-at-a-time form.
+    using clk = std::chrono::steady_clock;
+    auto secs = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
+    const auto t_all = clk::now();
+    const size_t per_group = std::max<size_t>(1, std::min<size_t>(128, (inputs.size() + 7) / 8));
+    const size_t ng = (inputs.size() + per_group - 1) / per_group;
+    struct Group {
+        std::vector<FastaFile> files;
+        std::vector<std::vector<SeqCall>> calls;
+        skm_calls dev{};
+        std::string text;
+        int state = 0;  // 1 parsed, 2 on-device done, 3 calls + text ready; -1 failed
+        std::string err;
+    };
+    std::vector<Group> groups(ng);
+    std::mutex mu;
+    std::condition_variable cv;
+    auto set_state = [&](size_t g, int st, const std::string& e = std::string()) {
+        std::lock_guard<std::mutex> lk(mu);
+        groups[g].state = st;
+        if (st < 0) groups[g].err = e;
+        cv.notify_all();
+    };
+    auto wait_state = [&](size_t g, int st) {  // false: the group failed
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return groups[g].state >= st || groups[g].state < 0; });
+        return groups[g].state >= 0;
+    };
+    skm_db* db = nullptr;
+    double t_open = 0, t_parse = 0, t_dev = 0, t_best = 0, t_write = 0;
+    std::string db_err;
+    std::thread db_thread([&] {
+        const auto t = clk::now();
+        if (skm_db_open(&db, mph.c_str(), dat.c_str(), device)) db_err = skm_last_error();
+        t_open = secs(t);
+    });
+    std::thread parser([&] {
+        for (size_t g = 0; g < ng; ++g) {
+            const auto t = clk::now();
+            const std::vector<std::string> paths(inputs.begin() + g * per_group,
+                                                 inputs.begin() + std::min(inputs.size(), (g + 1) * per_group));
+            std::string e;
+            if (!parse_fasta_files(paths, groups[g].files, n_threads, e)) {
+                for (size_t h = g; h < ng; ++h) set_state(h, -1, e);
+                return;
+            }
+            t_parse += secs(t);
+            set_state(g, 1);
+        }
+    });
+    std::thread device_stage([&] {
+        db_thread.join();
+        for (size_t g = 0; g < ng; ++g) {
+            if (!db_err.empty()) {
+                set_state(g, -1, db_err);
+                continue;
+            }
+            if (!wait_state(g, 1)) continue;
+            const auto t = clk::now();
+            std::vector<const FastaFile*> fp;
+            for (auto& f : groups[g].files) fp.push_back(&f);
+            std::string e;
+            if (annotate_batch(db, fp, aopts, n_threads, &groups[g].dev, e)) {
+                set_state(g, -1, e);
+                continue;
+            }
+            t_dev += secs(t);
+            set_state(g, 2);
+        }
+    });
+    std::thread host_stage([&] {
+        for (size_t g = 0; g < ng; ++g) {
+            if (!wait_state(g, 2)) continue;
+            const auto t = clk::now();
+            Group& G = groups[g];
+            std::vector<const FastaFile*> fp;
+            std::vector<std::vector<SeqCall>*> op_;
+            G.calls.resize(G.files.size());
+            for (size_t f = 0; f < G.files.size(); ++f) {
+                fp.push_back(&G.files[f]);
+                G.calls[f].resize(G.files[f].size());
+                op_.push_back(&G.calls[f]);
+            }
+            std::string e;
+            const int rc = best_calls_batch(G.dev, fp, fptr_idx, n_threads, op_, e);
+            skm_calls_free(&G.dev);
+            if (rc) {
+                set_state(g, -1, e);
+                continue;
+            }
+            // the group's lines, its files in order ("id\tfunc\tfunc_index\tscore\n", :178)
+            for (size_t f = 0; f < G.files.size(); ++f)
+                for (size_t r = 0; r < G.files[f].size(); ++r) {
+                    const SeqCall& c = G.calls[f][r];
+                    G.text += G.files[f].ids[r];
+                    G.text += '\t';
+                    G.text += c.func;
+                    G.text += '\t';
+                    G.text += std::to_string((unsigned)c.fi);
+                    G.text += '\t';
+                    G.text += fmt_g(c.score);
+                    G.text += '\n';
                 }
-            }
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < std::min<int>(n_threads, (int)files.size()); ++t) th.emplace_back(fmt);
-        fmt();
-        for (auto& t : th) t.join();
-    }
-    for (size_t f = 0; f < files.size(); ++f) {
-        if (op.has("debug-hits")) debug_hits(db, datbuf, files[f], fidx, ignore_hypo, hypo, std::cout);
-        out->write(text[f].data(), (std::streamsize)text[f].size());
-        std::string().swap(text[f]);
-    }
-    out->flush();
-    const double t_write = now_s() - t0;
-    skm_db_close(db);
+            std::vector<std::vector<SeqCall>>().swap(G.calls);
+            t_best += secs(t);
+            set_state(g, 3);
+        }
+    });
     uint64_t nrec = 0;
-    for (auto& f : files) nrec += f.size();
-    // one machine-readable line of the phases (bench.py's cli_call leg)
-    std::cerr << "phases: sequences " << nrec << " db_open " << t_open << " parse " << t_parse << " device " << dev_ms / 1e3 << " best_call "
-              << host_ms / 1e3 << " write " << t_write << "\n";
+    std::string fail;
+    for (size_t g = 0; g < ng; ++g) {
+        if (!wait_state(g, 3)) {
+            fail = groups[g].err;
+            break;
+        }
+        const auto t = clk::now();
+        Group& G = groups[g];
+        if (op.has("debug-hits")) {  // per file: its hit lines, then its calls (the reference's order)
+            size_t at = 0;
+            for (auto& f : G.files) {
+                debug_hits(db, datbuf, f, fidx, ignore_hypo, hypo, std::cout);
+                size_t end = at;
+                for (size_t r = 0; r < f.size(); ++r) end = G.text.find('\n', end) + 1;
+                out->write(G.text.data() + at, (std::streamsize)(end - at));
+                at = end;
+            }
+        } else {
+            out->write(G.text.data(), (std::streamsize)G.text.size());
+        }
+        for (auto& f : G.files) nrec += f.size();
+        std::string().swap(G.text);
+        std::vector<FastaFile>().swap(G.files);
+        t_write += secs(t);
+    }
+    parser.join();
+    device_stage.join();
+    host_stage.join();
+    if (!fail.empty()) die(fail);
+    out->flush();
+    if (db) skm_db_close(db);
+    // one machine-readable line of the phases (bench.py's cli_call leg): busy seconds per stage
+    // (the stages overlap) and the pipeline's wall time
+    std::cerr << "phases: sequences " << nrec << " db_open " << t_open << " parse " << t_parse << " device " << t_dev
+              << " best_call " << t_best << " write " << t_write << " groups " << ng << " wall " << secs(t_all)
+              << " startup " << t_startup << "\n";
     return 0;
 }
