@@ -11,6 +11,7 @@
 #include <cctype>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
@@ -420,6 +421,15 @@ void FloatStats::add(float x) {
         float tmp = x - mean;
         variance = variance * (float)(count - 1) / (float)count + tmp * tmp / (float)(count - 1);
     }
+}
+
+void fast_exit(int code) {
+    std::cout.flush();
+    std::cerr.flush();
+    std::fflush(nullptr);
+    const char* full = std::getenv("SKM_CLI_FULL_EXIT");
+    if (full && std::atoi(full) != 0) std::exit(code);
+    std::_Exit(code);
 }
 
 double process_age_s() {

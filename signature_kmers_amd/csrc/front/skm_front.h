@@ -117,6 +117,11 @@ void select_build_sequences(const FunctionMap& fm, const FastaFile& f, unsigned 
                             unsigned max_seqs_per_file, const std::set<std::string>& deleted_fids,
                             BuildBatch& out);
 
+// End the process with status `code` once its output is written: std::_Exit after flushing
+// stdout / stderr, skipping the destructors of the host-side tables (FunctionMap, parsed files:
+// millions of strings) and the HIP runtime's teardown (~1.4 s at C2 for kmers-build-signatures).
+// SKM_CLI_FULL_EXIT=1 (e.g. under a profiler that writes its trace at exit) returns normally.
+[[noreturn]] void fast_exit(int code);
 // seconds since this process started (the CLIs' "startup" phase: loader, libskm, HIP runtime)
 double process_age_s();
 // ostream << float/double with the default format (precision 6, %g), incl. "-nan"/"inf".

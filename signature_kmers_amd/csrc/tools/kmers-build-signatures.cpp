@@ -499,5 +499,5 @@ int main(int argc, char** argv) {
               << t_recall << " recall_device " << t_recall_dev << " total " << now_s() - t_start << " startup "
               << t_startup << "\n";
     std::cerr << "all done\n";
-    return 0;
+    fast_exit(0);  // every output file is closed by now
 }

@@ -299,5 +299,6 @@ int main(int argc, char** argv) {
     std::cerr << "phases: sequences " << nrec << " db_open " << t_open << " parse " << t_parse << " device " << t_dev
               << " best_call " << t_best << " write " << t_write << " groups " << ng << " wall " << secs(t_all)
               << " startup " << t_startup << "\n";
-    return 0;
+    if (ofs.is_open()) ofs.close();
+    fast_exit(0);
 }
