@@ -4857,7 +4857,11 @@ struct Tune {
     int split_grid = 512;            //   k_ovf_split,
     int chain_grid = 4096;           //   k_chains
     int stream_prio = 0;             // 1: the group-by stream at the highest priority
-    int chain_batches = 4;           // key-range passes: stashed long chains leave in this many batches
+    // key-range passes: stashed long chains leave in this many batches.  Round 6 (C3, one box,
+    // after the staging stopped re-reading the residues): 2 -> 1404-1426 ms/step, chain tail 11 ms;
+    // 4 -> 1536-1541 ms, tail 92-105 ms (the batch flushed after pass 11 still ran when the last
+    // pass ended); 1 -> 1835 ms; 8 -> 2464 ms
+    int chain_batches = 2;
     int chain_streams = 1;           //   over this many streams (1..4)
     int poison_jobs = 0;             // tests: every slot of the run's long-job list starts as a canary job
     int route_vacate = 0;            // routing: the last this many passes hold no heavy key (0: half)
@@ -5546,9 +5550,13 @@ constexpr uint64_t PASS_BYTES = 104;   // recs 16 + tmp 16 + received 16 (world 
 // HBM a shard's work buffers take for passes of at most m elements: PASS_BYTES per element, with
 // key-range passes also the window-position slots of a pass group (8 B per element and slot,
 // G = min(P, 4) slots, size_local) and the pass-id byte per residue.
-inline uint64_t pass_work(uint64_t m, int pb, uint64_t rp) {
+// giant: giant chains on (giant_class), whose per-pass sample slots (alloc_caps: 4 B x giant_cap,
+// giant_cap = min(split_cap ~ 5/16 of the pass, 2^28), and their job lists) count too.
+inline uint64_t pass_work(uint64_t m, int pb, uint64_t rp, bool giant = false) {
     const uint64_t G = pb ? std::min<uint64_t>(1ull << pb, 4) : 0;
-    return m * (PASS_BYTES + 8 * G) + (pb ? rp : 0);
+    const uint64_t gcap = std::min<uint64_t>(m / 16 * 5 + (1u << 15), 1ull << 28);
+    const uint64_t gw = giant ? (1ull << pb) * (4 * gcap + sizeof(Job) * (gcap >> 10) + 4096) : 0;
+    return m * (PASS_BYTES + 8 * G) + (pb ? rp : 0) + gw;
 }
 // the work buffers may take 5/8 of the budget; the kept arena (18 B per kept k-mer) and the
 // grow-and-redo reserve share the rest
@@ -5591,7 +5599,8 @@ void size_passes(skm_build* b, int forced_pb = -1) {
         // exchange (skewed owners); 2^32 - 2^28 leaves the same slack for the 32-bit indexing
         while (pb < 6) {
             const uint64_t m = pass_max(pb);
-            if (m < (1ull << 32) - (1ull << 28) && work_fits(pass_work(m, pb, b->rp), budget)) break;
+            const bool giant = b->tune.giant_class > 0 || (b->tune.giant_class < 0 && (pb == 0 || b->world > 1));
+            if (m < (1ull << 32) - (1ull << 28) && work_fits(pass_work(m, pb, b->rp, giant), budget)) break;
             ++pb;
         }
     }
@@ -5689,7 +5698,8 @@ void size_arena(skm_build* b) {
     uint64_t cap = std::min<uint64_t>(b->valid_total + 16, avail / (8 + sizeof(skm_stored_kmer_data)));
     if (b->tune.mem_budget_mb > 0) {
         const uint64_t budget = (uint64_t)b->tune.mem_budget_mb << 20;
-        const uint64_t used = pass_work(b->pass_max, b->pass_bits, b->rp);
+        const bool giant = b->tune.giant_class > 0 || (b->tune.giant_class < 0 && (b->pass_bits == 0 || b->world > 1));
+        const uint64_t used = pass_work(b->pass_max, b->pass_bits, b->rp, giant);
         cap = std::min<uint64_t>(cap, budget > used ? (budget - used) / 18 : 0);
     }
     cap = std::max<uint64_t>(cap, b->pass_max + 16);
@@ -5811,7 +5821,9 @@ void route_plan(const Ranks& bs) {
             SKM_HIP(hipMemGetInfo(&fr, &tot));
             const uint64_t budget = b->tune.mem_budget_mb > 0 ? (uint64_t)b->tune.mem_budget_mb << 20 : (uint64_t)fr;
             const bool forced = b->tune.passes > 0;
-            ok[k] = m < (1ull << 32) - (1ull << 28) && (forced || m <= b->pass_max || work_fits(pass_work(m, pb, b->rp), budget));
+            const bool giant = b->tune.giant_class > 0 || (b->tune.giant_class < 0 && (pb == 0 || b->world > 1));
+            ok[k] = m < (1ull << 32) - (1ull << 28) &&
+                    (forced || m <= b->pass_max || work_fits(pass_work(m, pb, b->rp, giant), budget));
             routed_m[k] = m;
             routed_n[k] = natural_late - late;
             heavy[k] = first ? cnt[0] : 0;
@@ -5837,6 +5849,9 @@ void route_plan(const Ranks& bs) {
             }
             count_routed();
         }
+        // a forced single pass stays one pass: with no pass bits k_pass_ids routes nothing, so
+        // routing is off and the routed counter stays 0
+        if (pb == 0) return turn_off();
     }
     {
         const std::vector<uint64_t> all = W > 1 ? allgather_u64(bs, ok) : ok;
@@ -6959,15 +6974,15 @@ Ranks ranks_of(skm_build* b) {
 
 }  // namespace
 
-// A build drives up to 8 streams at once (group-by, two overflow streams, the stashed-chain
-// stream and four giant-chain slots).  HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues
-// (default 4); streams sharing a queue execute in order, which would serialise a pass behind the
-// previous pass's long chains.  Ask for at least 8 (read at HIP init, so
-// this only takes effect when libskm is loaded before the first HIP call; bench.py, the tests and
-// the CLIs set it themselves).
+// A build drives up to 10 streams at once (group-by, two overflow streams, the pass tail, the
+// next group's emission, the stashed-chain stream and the giant-chain slots).  HIP maps streams
+// onto GPU_MAX_HW_QUEUES hardware queues (default 4); streams sharing a queue execute in order,
+// which would serialise a pass behind the previous pass's long chains.  Ask for at least 16, as
+// bench.py and the tests run with (read at HIP init, so this only takes effect when libskm is
+// loaded before the first HIP call; the CLIs set it themselves).
 __attribute__((constructor)) static void skm_hw_queues() {
     const char* q = getenv("GPU_MAX_HW_QUEUES");
-    if (!q || atoi(q) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
+    if (!q || atoi(q) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
 }
 
 extern "C" {

@@ -139,9 +139,9 @@ void dump_extract(const std::string& path, const std::vector<FastaFile>& files, 
 }  // namespace
 
 int main(int argc, char** argv) {
-    {  // libskm runs up to 8 streams at once: at least 8 hardware queues (read at the first HIP call)
+    {  // libskm runs up to 10 streams at once: 16 hardware queues (read at the first HIP call)
         const char* q = getenv("GPU_MAX_HW_QUEUES");
-        if (!q || atoi(q) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
+        if (!q || atoi(q) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
     }
     Options op;
     op.specs = {{"definition-dir", 'D', false, true},  {"fasta-dir", 'F', false, true},
@@ -212,6 +212,15 @@ int main(int argc, char** argv) {
     std::string final_kmers = op.get("final-kmers");
     std::string ph_file = op.get("perfect-hash"), ph_data = op.get("perfect-hash-data");
 
+    // the HIP runtime initialises on a thread of its own while the host parses (the first HIP call
+    // of a process costs ~0.3-0.5 s)
+    double t_hip_init = 0;
+    std::thread hip_warm([&] {
+        const double th = now_s();
+        int ndev = 0;
+        (void)skm_device_count(&ndev);
+        t_hip_init = now_s() - th;
+    });
     std::vector<std::string> definition_files, fasta_files, keep_files;
     auto populate = [&](const std::vector<std::string>& dirs, std::vector<std::string>& out) {
         for (const auto& d : dirs)
@@ -242,22 +251,10 @@ int main(int argc, char** argv) {
         good_roles.insert(good_roles.end(), v.begin(), v.end());
     }
 
-    FunctionMap fm;
-    fm.add_good_roles(good_roles);
-    fm.add_good_functions(good_functions);
-    for (auto& d : definition_files) fm.load_id_assignments(d);
-
-    std::set<std::string> deleted_fids, ignored_functions;
-    if (op.has("deleted-features-file"))
-        for (auto& l : load_lines(op.get("deleted-features-file"))) deleted_fids.insert(l);
-    if (op.has("ignored-functions-file"))
-        for (auto& l : load_lines(op.get("ignored-functions-file"))) ignored_functions.insert(l);
-
-    if (!kmer_data_dir.empty() && !ensure_directory(kmer_data_dir)) die("Error creating " + quoted(kmer_data_dir));
-
-    // all_fasta_data_ = fasta-dir files, then keep-dir files (signature_build.tcc:26-35)
+    // the FASTA files parse on the host threads while this thread loads the definitions (the two are
+    // independent until the FunctionMap reads the records, below)
     std::cerr << "load fasta\n";
-    std::vector<std::string> all_paths = fasta_files;
+    std::vector<std::string> all_paths = fasta_files;  // fasta-dir files, then keep-dir files (signature_build.tcc:26-35)
     all_paths.insert(all_paths.end(), keep_files.begin(), keep_files.end());
     std::vector<FastaFile> files;
     // this rank's contiguous range of files (global file numbering keeps seq_id = file*100000+k)
@@ -269,7 +266,26 @@ int main(int argc, char** argv) {
     std::vector<char> keep_res(all_paths.size(), 0);
     for (size_t f = 0; f < all_paths.size(); ++f) keep_res[f] = rank == 0 || dump || (f >= f0 && f < f1);
     double t0 = now_s();
-    if (!parse_fasta_files(all_paths, files, n_threads, err, &keep_res)) die(err);
+    bool parsed_ok = true;
+    std::string parse_err;
+    std::thread parser([&] { parsed_ok = parse_fasta_files(all_paths, files, n_threads, parse_err, &keep_res); });
+    const double td = now_s();
+    FunctionMap fm;
+    fm.add_good_roles(good_roles);
+    fm.add_good_functions(good_functions);
+    for (auto& d : definition_files) fm.load_id_assignments(d);
+    const double t_defs = now_s() - td;
+
+    std::set<std::string> deleted_fids, ignored_functions;
+    if (op.has("deleted-features-file"))
+        for (auto& l : load_lines(op.get("deleted-features-file"))) deleted_fids.insert(l);
+    if (op.has("ignored-functions-file"))
+        for (auto& l : load_lines(op.get("ignored-functions-file"))) ignored_functions.insert(l);
+
+    if (!kmer_data_dir.empty() && !ensure_directory(kmer_data_dir)) die("Error creating " + quoted(kmer_data_dir));
+
+    parser.join();
+    if (!parsed_ok) die(parse_err);
     try {
         for (auto& f : files) fm.load_fasta_file(f, deleted_fids);
     } catch (const std::exception& e) {
@@ -311,6 +327,7 @@ int main(int argc, char** argv) {
             if (t.joinable()) t.join();
     };
     if (dump) {
+        hip_warm.join();
         join_selection();
         if (rank != 0) return 0;
         dump_extract(op.get("dump-extract"), files, batches);
@@ -330,6 +347,8 @@ int main(int argc, char** argv) {
     auto check = [](int rc, const char* what) {
         if (rc) die(std::string(what) + ": " + skm_last_error());
     };
+    hip_warm.join();
+    const double t_create0 = now_s();
     check(skm_build_create(&b, &device, 1, &bo), "skm_build_create");
     {
         uint64_t nres = 0, nseq = 0;
@@ -356,6 +375,7 @@ int main(int argc, char** argv) {
         }
         check(skm_build_set_comm(b, id), "skm_build_set_comm");
     }
+    const double t_create = now_s() - t_create0;
     const double t_add0 = now_s();
     for (size_t f = f0; f < f1; ++f) {
         {
@@ -497,7 +517,7 @@ int main(int argc, char** argv) {
     std::cerr << "phases: parse " << t_parse << " add " << t_add << " prepare " << t_prepare << " run " << t_run
               << " finish " << t_finish << " final_kmers " << t_final_kmers << " mph " << t_mph << " recall "
               << t_recall << " recall_device " << t_recall_dev << " total " << now_s() - t_start << " startup "
-              << t_startup << "\n";
+              << t_startup << " defs " << t_defs << " hip_init " << t_hip_init << " create " << t_create << "\n";
     std::cerr << "all done\n";
     fast_exit(0);  // every output file is closed by now
 }

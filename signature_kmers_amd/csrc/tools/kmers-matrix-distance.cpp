@@ -53,9 +53,9 @@ bool file_exists(const std::string& p) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    {  // libskm runs up to 8 streams at once: at least 8 hardware queues (read at the first HIP call)
+    {  // libskm runs up to 10 streams at once: 16 hardware queues (read at the first HIP call)
         const char* q = getenv("GPU_MAX_HW_QUEUES");
-        if (!q || atoi(q) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
+        if (!q || atoi(q) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
     }
     Options op;
     op.specs = {{"data-dir", 'd', false, false},   {"input-file", 'i', false, false}, {"output-file", 'o', false, false},
