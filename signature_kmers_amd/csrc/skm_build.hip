@@ -4875,6 +4875,7 @@ struct Tune {
     int tail_async = 1;
     int big_grid = 2048;             // k_big_groups' persistent grids: groups of 65..1024 members,
     int big_grid_large = 512;        //   and of 1025..CAP
+    int big_split = 1;               // tail_async: the 1025..CAP class on a second tail stream
     int route_first = -1;
     int route_first_min = 1 << 17;   // route_first: k-mers of >= this many occurrences make pass 0 (C3: ~4.5 %
                                      //   of the windows; those of >= 2^14 hold ~17 %, too many for a short pass)
@@ -5015,7 +5016,8 @@ struct skm_build {
     // second stream: overflow sub-buckets + their chains, concurrent with the group-by
     hipStream_t stream2 = nullptr, stream3 = nullptr;
     hipStream_t stream_tail = nullptr;  // tail_async: a pass's big groups, main chains and accounting
-    hipEvent_t ev_tail_bp = nullptr, ev_tail_done = nullptr;
+    hipStream_t stream_tail2 = nullptr; //   the groups of 1025..CAP members beside the smaller big groups
+    hipEvent_t ev_tail_bp = nullptr, ev_tail_done = nullptr, ev_tail2 = nullptr;
     bool tail_pending = false;          // the last pass's tail is still in flight on stream_tail
     hipEvent_t ev_part = nullptr, ev_split = nullptr;
     DevBuf d_hv_keys, d_hv_rec, d_hv_len, d_hv_s0, d_hv_s1;   // heavy keys of the split overflow
@@ -6560,8 +6562,19 @@ void phase_group(skm_build* b, uint32_t pass) {
         SKM_HIP(hipEventRecord(b->ev_tail_bp, st));
         SKM_HIP(hipStreamWaitEvent(tt, b->ev_tail_bp, 0));
     }
-    SKM_LAUNCH(b, k_big_groups<false>, dim3((uint32_t)std::max(1, b->tune.big_grid)), dim3(BIG_WG), 0, tt, BA);
-    SKM_LAUNCH(b, k_big_groups<true>, dim3((uint32_t)std::max(1, b->tune.big_grid_large)), dim3(BIG_WG), 0, tt, BA);
+    if (tail_async && b->tune.big_split) {
+        // the two size classes of big groups are independent (disjoint descriptors and outputs):
+        // the large class on a stream of its own, joined before the append
+        SKM_HIP(hipStreamWaitEvent(b->stream_tail2, b->ev_tail_bp, 0));
+        SKM_LAUNCH(b, k_big_groups<true>, dim3((uint32_t)std::max(1, b->tune.big_grid_large)), dim3(BIG_WG), 0,
+                   b->stream_tail2, BA);
+        SKM_HIP(hipEventRecord(b->ev_tail2, b->stream_tail2));
+        SKM_LAUNCH(b, k_big_groups<false>, dim3((uint32_t)std::max(1, b->tune.big_grid)), dim3(BIG_WG), 0, tt, BA);
+        SKM_HIP(hipStreamWaitEvent(tt, b->ev_tail2, 0));
+    } else {
+        SKM_LAUNCH(b, k_big_groups<false>, dim3((uint32_t)std::max(1, b->tune.big_grid)), dim3(BIG_WG), 0, tt, BA);
+        SKM_LAUNCH(b, k_big_groups<true>, dim3((uint32_t)std::max(1, b->tune.big_grid_large)), dim3(BIG_WG), 0, tt, BA);
+    }
     SKM_LAUNCH(b, k_big_append, dim3(256), dim3(BIG_WG), 0, tt, BA.out, BA, A);
     SKM_HIP(hipGetLastError());
     SKM_HIP(hipEventRecord(b->ev[12], tt));
@@ -7008,6 +7021,8 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     SKM_HIP(hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking));
     SKM_HIP(hipStreamCreateWithFlags(&b->stream3, hipStreamNonBlocking));
     SKM_HIP(hipStreamCreateWithFlags(&b->stream_tail, hipStreamNonBlocking));
+    SKM_HIP(hipStreamCreateWithFlags(&b->stream_tail2, hipStreamNonBlocking));
+    SKM_HIP(hipEventCreateWithFlags(&b->ev_tail2, hipEventDisableTiming));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_tail_bp, hipEventDisableTiming));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_tail_done, hipEventDisableTiming));
     use_evset(b, 0);
@@ -7407,6 +7422,7 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "tail_async" ? &t.tail_async
                : n == "big_grid" ? &t.big_grid
                : n == "big_grid_large" ? &t.big_grid_large
+               : n == "big_split" ? &t.big_split
                : n == "handoff_index_limit" ? &t.handoff_index_limit
                : n == "handoff_max_chunk" ? &t.handoff_max_chunk
                : n == "route_first_min" ? &t.route_first_min : nullptr;
@@ -7807,6 +7823,7 @@ void skm_build_destroy(skm_build* b) {
     if (b->stream2) (void)hipStreamSynchronize(b->stream2);
     if (b->stream3) (void)hipStreamSynchronize(b->stream3);
     if (b->stream_tail) (void)hipStreamSynchronize(b->stream_tail);
+    if (b->stream_tail2) (void)hipStreamSynchronize(b->stream_tail2);
     if (b->chain_st) (void)hipStreamSynchronize(b->chain_st);
     for (auto& set : b->evsets) {
         for (auto& e : set.ev)
@@ -7866,6 +7883,8 @@ void skm_build_destroy(skm_build* b) {
     if (b->stream2) (void)hipStreamDestroy(b->stream2);
     if (b->stream3) (void)hipStreamDestroy(b->stream3);
     if (b->stream_tail) (void)hipStreamDestroy(b->stream_tail);
+    if (b->stream_tail2) (void)hipStreamDestroy(b->stream_tail2);
+    if (b->ev_tail2) (void)hipEventDestroy(b->ev_tail2);
     if (b->ev_tail_bp) (void)hipEventDestroy(b->ev_tail_bp);
     if (b->ev_tail_done) (void)hipEventDestroy(b->ev_tail_done);
     delete b;
