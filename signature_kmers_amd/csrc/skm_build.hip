@@ -4875,7 +4875,10 @@ struct Tune {
     int tail_async = 1;
     int big_grid = 2048;             // k_big_groups' persistent grids: groups of 65..1024 members,
     int big_grid_large = 512;        //   and of 1025..CAP
-    int big_split = 1;               // tail_async: the 1025..CAP class on a second tail stream
+    // tail_async: the 1025..CAP class on a second tail stream.  Measured slower at C3 (round 6,
+    // one box: 1445 / 1474 vs 1391 / 1429 ms/step): the concurrent classes slow the chains after them
+    int big_split = 0;
+    int emit_group = 0;              // key-range passes emitted per residue scan (0: 4; 1, 2, 4, 8 or 16)
     int route_first = -1;
     int route_first_min = 1 << 17;   // route_first: k-mers of >= this many occurrences make pass 0 (C3: ~4.5 %
                                      //   of the windows; those of >= 2^14 hold ~17 %, too many for a short pass)
@@ -5658,7 +5661,8 @@ void size_local(skm_build* b) {
     if (b->pass_bits > 0) {
         const uint32_t NB = 1u << (b->owner_bits + b->b1_bits);
         const uint32_t P = 1u << b->pass_bits;
-        b->emit_g = std::max<uint32_t>(1, std::min<uint32_t>(P, 4u));
+        const uint32_t eg = b->tune.emit_group > 0 ? (uint32_t)b->tune.emit_group : 4u;
+        b->emit_g = std::max<uint32_t>(1, std::min<uint32_t>(P, eg));
         b->d_posg.ensure(8 * W * b->emit_g);
         b->d_ids.ensure(((b->rp + 15) & ~15ull) + 64);
         SKM_HIP(hipMemsetAsync(b->d_ids.p, 0xFF, ((b->rp + 15) & ~15ull) + 64, b->stream));  // padding: no window
@@ -6004,7 +6008,11 @@ void emit_group(skm_build* b, uint32_t g, hipStream_t st) {
     SKM_LAUNCH_AS(b, "k_pass_emit", k_pass_emit<GG>, dim3(b->sel_wg), dim3(EMIT_THREADS), 0, st, b->d_res.as<uint8_t>(), \
                   b->d_ids.as<uint8_t>(), b->rp, g * G, b->sel_span, b->d_seloff.as<uint64_t>(), b->sel_wg, \
                   b->d_posg.as<uint64_t>(), cap)
-    if (G == 4)
+    if (G == 16)
+        SKM_EMIT(16);
+    else if (G == 8)
+        SKM_EMIT(8);
+    else if (G == 4)
         SKM_EMIT(4);
     else if (G == 2)
         SKM_EMIT(2);
@@ -7423,6 +7431,7 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "big_grid" ? &t.big_grid
                : n == "big_grid_large" ? &t.big_grid_large
                : n == "big_split" ? &t.big_split
+               : n == "emit_group" ? &t.emit_group
                : n == "handoff_index_limit" ? &t.handoff_index_limit
                : n == "handoff_max_chunk" ? &t.handoff_max_chunk
                : n == "route_first_min" ? &t.route_first_min : nullptr;
@@ -7431,6 +7440,9 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
         if (n == "overflow_long_class" || n == "main_long_class")
             SKM_CHECK(value >= 1 && value < 32, SKM_E_ARG, "long chain classes in [1, 32)");
         if (n == "giant_class") SKM_CHECK(value < 32, SKM_E_ARG, "giant_class in [0, 32)");
+        if (n == "emit_group")
+            SKM_CHECK(value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16, SKM_E_ARG,
+                      "emit_group must be 0, 1, 2, 4, 8 or 16");
         *f = (int)value;
     }
     b->prepared = false;  // pass geometry and buffers are re-planned on the next prepare/run
