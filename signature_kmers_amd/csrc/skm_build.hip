@@ -2040,6 +2040,35 @@ using StageLds = StageLdsT<SC_ROUND>;
 // chain (C3 step 2046 -> 1950 ms, the kernel 435 -> 320 ms per step)
 constexpr int SC_ROUND_HALF = SC_ROUND / 2;
 
+// The rank of a lane's element among its destination's elements (LDS counter cnt[d]), called by
+// every lane of the wave (v: the lane has an element): the lanes that share the first live lane's
+// destination reserve together with one atomic, the rest one each.  A heavy key crowds its
+// elements into one destination, and same-address LDS atomics serialise lane by lane.
+__device__ __forceinline__ uint32_t agg_rank(uint32_t* cnt, uint32_t d, bool v) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t act = __ballot(v);
+    if (act == 0) return 0u;
+    const uint32_t l0 = (uint32_t)__ffsll((long long)act) - 1u;
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)l0);
+    const uint64_t same = __ballot(v && d == d0);
+    uint32_t base = 0;
+    if (lane == l0) base = atomicAdd(&cnt[d0], (uint32_t)__popcll(same));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)l0);
+    if (v && d == d0) return base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+    return v ? atomicAdd(&cnt[d], 1u) : 0u;
+}
+// the same aggregation for a count (no ranks)
+__device__ __forceinline__ void agg_count(uint32_t* cnt, uint32_t d, bool v) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t act = __ballot(v);
+    if (act == 0) return;
+    const uint32_t l0 = (uint32_t)__ffsll((long long)act) - 1u;
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)l0);
+    const uint64_t same = __ballot(v && d == d0);
+    if (lane == l0) atomicAdd(&cnt[d0], (uint32_t)__popcll(same));
+    if (v && d != d0) atomicAdd(&cnt[d], 1u);
+}
+
 // counts already in L.cnt[0..nd): exclusive offsets, then one global reservation per destination
 template <class Lds>
 __device__ __forceinline__ uint32_t stage_reserve(Lds& L, uint32_t nd, unsigned long long* __restrict__ cur,
@@ -2226,9 +2255,10 @@ __global__ __launch_bounds__(EX_THREADS, MINB) void k_extract_stage_pos(ExtractA
                 make_elem((h & rem_mask) | route, X.s_base + s, (uint32_t)(p - m.pstart), m, eh[t], el[t]);
                 el[t] = (el[t] & ~0xFFFFull) | bucket;  // bucket id rides in the offset field until pass 2
                 l0[t] = bucket >> l0_shift;
-                rk[t] = atomicAdd(&L.cnt[l0[t]], 1u);
             }
         }
+#pragma unroll
+        for (int t = 0; t < SC_POS; ++t) rk[t] = agg_rank(L.cnt, l0[t], ent[t] != ~0ull);
         __syncthreads();
         const uint32_t tot = stage_reserve(L, 1u << SC_L0_BITS, cur0, 0);
 #pragma unroll
@@ -2317,9 +2347,11 @@ __global__ __launch_bounds__(EX_THREADS, 2) void k_split_stage(const uint64_t* _
                 sb[t] = (uint32_t)(el[t] & 0xFFFFu) & (nsub - 1);
                 const uint32_t i = (uint32_t)(el[t] >> 16) & ((1u << ELEM_I_BITS) - 1);
                 el[t] = (el[t] & ~0xFFFFull) | (((uint32_t)(eh[t] >> 48) - i) & 0xFFFFu);  // restore (len - i) mod 2^16
-                rk[t] = atomicAdd(&L.cnt[sb[t]], 1u);
             }
         }
+#pragma unroll
+        for (int t = 0; t < SC_POS; ++t)
+            rk[t] = agg_rank(L.cnt, sb[t], base + threadIdx.x + (uint64_t)t * EX_THREADS < end);
         __syncthreads();
         const uint32_t tot = stage_reserve(L, nsub, cur1, b0 << sub_bits);
 #pragma unroll
@@ -3327,9 +3359,11 @@ __global__ __launch_bounds__(PT_THREADS, MINB) void k_partition(BucketArgs A) {
     for (uint32_t p = 0; p < nseg; ++p) {
         uint64_t base, len;
         seg(p, base, len);
-        for (uint64_t j = threadIdx.x; j < len; j += blockDim.x) {
-            const uint64_t h = A.recs_hi[base + j];
-            atomicAdd(&s_cur[(uint32_t)(((h >> 16) & rem_mask) >> shift)], 1u);
+        for (uint64_t j0 = 0; j0 < len; j0 += blockDim.x) {  // wave-uniform trip count (agg_count)
+            const uint64_t j = j0 + threadIdx.x;
+            const bool v = j < len;
+            const uint64_t h = v ? A.recs_hi[base + j] : 0ull;
+            agg_count(s_cur, (uint32_t)(((h >> 16) & rem_mask) >> shift), v);
         }
     }
     __syncthreads();
@@ -3401,10 +3435,9 @@ __global__ __launch_bounds__(PT_THREADS, MINB) void k_partition(BucketArgs A) {
 #pragma unroll
             for (uint32_t u = 0; u < PER; ++u) {
                 const uint64_t j = rb + threadIdx.x + (uint64_t)u * PT_THREADS;
-                if (j < len) {
-                    sb[u] = (uint32_t)(((eh[u] >> 16) & rem_mask) >> shift);
-                    rk[u] = atomicAdd(&s_rc[sb[u]], 1u);
-                }
+                const bool v = j < len;
+                if (v) sb[u] = (uint32_t)(((eh[u] >> 16) & rem_mask) >> shift);
+                rk[u] = agg_rank(s_rc, v ? sb[u] : 0u, v);
             }
             __syncthreads();
             {   // exclusive scan of the round counts over the sub-buckets
