@@ -1847,15 +1847,31 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
 #pragma unroll
     for (uint32_t q = 0; q < G; ++q) run[q] = seloff[(uint64_t)(pass0 + q) * (nrows + 1) + blockIdx.x];
     const uint64_t a = (uint64_t)blockIdx.x * span, e = min(rp, a + span);
+    // the next tile's ids and residues are loaded before this tile is processed (round 5 loaded
+    // the residues only after the ids showed a window of the group: two serial latencies a tile)
+    uint4 nid = make_uint4(~0u, ~0u, ~0u, ~0u), nr0 = make_uint4(0u, 0u, 0u, 0u), nr1 = nr0;
+    if (a + 16ull * lane < e) {
+        nid = *reinterpret_cast<const uint4*>(ids + a + 16ull * lane);
+        nr0 = *reinterpret_cast<const uint4*>(res + a + 16ull * lane);
+        nr1 = *reinterpret_cast<const uint4*>(res + a + 16ull * lane + 16);
+    }
     for (uint64_t t0 = a; t0 < e; t0 += 16ull * 64) {
         const uint64_t base = t0 + 16ull * lane;
+        const uint4 id4 = nid, v0 = nr0, v1 = nr1;
+        {
+            const uint64_t nb = base + 16ull * 64;
+            if (nb < e) {  // the residue buffer is padded past rp, the id buffer to a multiple of 16
+                nid = *reinterpret_cast<const uint4*>(ids + nb);
+                nr0 = *reinterpret_cast<const uint4*>(res + nb);
+                nr1 = *reinterpret_cast<const uint4*>(res + nb + 16);
+            }
+        }
         uint32_t qs[4] = {~0u, ~0u, ~0u, ~0u};  // byte t: the window's pass within the group (0xFF: none)
         uint64_t hs[16];                        // the window's key hash
         uint32_t cnt[G];
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) cnt[q] = 0;
         if (base < e) {
-            const uint4 id4 = *reinterpret_cast<const uint4*>(ids + base);
             const uint32_t idw[4] = {id4.x, id4.y, id4.z, id4.w};
             uint32_t any = 0;
 #pragma unroll
@@ -1870,8 +1886,6 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                 }
             }
             if (any) {  // the 16 keys rolled from the lane's 24 residues, mixed for the group's windows
-                const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
-                const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
                 const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
                 uint32_t code[24];
 #pragma unroll
