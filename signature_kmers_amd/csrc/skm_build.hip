@@ -1732,10 +1732,19 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
     const uint64_t c0 = rows ? ((uint64_t)blockIdx.x * span >> 4) + threadIdx.x : (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t cend = rows ? min(nchunk, ((uint64_t)blockIdx.x + 1) * span >> 4) : nchunk;
     const uint64_t cstep = rows ? (uint64_t)blockDim.x : (uint64_t)gridDim.x * blockDim.x;
+    // the next chunk's residues are loaded before this chunk is hashed
+    uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
+    if (c0 < cend) {
+        n0 = *reinterpret_cast<const uint4*>(res + (c0 << 4));
+        n1 = *reinterpret_cast<const uint4*>(res + (c0 << 4) + 16);
+    }
     for (uint64_t c = c0; c < cend; c += cstep) {
         const uint64_t base = c << 4;
-        const uint4 v0 = *reinterpret_cast<const uint4*>(res + base);
-        const uint4 v1 = *reinterpret_cast<const uint4*>(res + base + 16);
+        const uint4 v0 = n0, v1 = n1;
+        if (c + cstep < cend) {
+            n0 = *reinterpret_cast<const uint4*>(res + ((c + cstep) << 4));
+            n1 = *reinterpret_cast<const uint4*>(res + ((c + cstep) << 4) + 16);
+        }
         const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
         uint32_t code[24];
         uint32_t valid = 0;
@@ -6873,8 +6882,20 @@ void phase_stats(skm_build* b) {
     if (b->tune.flag_bits && b->n_total)
         SKM_LAUNCH(b, k_flags_from_bits, dim3(1024), dim3(256), 0, st, b->d_flagbits.as<uint32_t>(),
                    (uint32_t)b->n_total, b->d_flags.as<uint8_t>());
+    // the arena's keys decoded and distinct_functions counted while the last chains run: neither
+    // reads what the chains write (the records' median / var), and every pass's kept k-mers are in
+    // the arena once the main stream is here
+    SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
+    SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
+    const size_t lds_f = F <= 16384 ? sizeof(uint32_t) * F : 0;
+    if (b->pass_bits) flush_long_chains(b, 16);  // the last batch of long chains first, on the chain streams
+    SKM_LAUNCH(b, k_kept_finalize, dim3(2048), dim3(256), lds_f, st, b->d_keys.as<uint64_t>(),
+                       b->d_data.as<skm_stored_kmer_data>(), b->d_ctr.as<unsigned long long>(), F,
+                       b->d_dfunc.as<uint32_t>());
+    if (b->nseq)
+        SKM_LAUNCH(b, k_func_hist_seqs, dim3(256), dim3(256), lds_f, st, b->d_meta.as<SeqMeta>(), b->nseq, F,
+                           b->d_swf.as<uint32_t>());
     if (b->pass_bits) {  // the long chains of every pass (the last batch on the chain stream)
-        flush_long_chains(b, 16);
         for (int k = 0; k < skm_build::LANE_ST; ++k) {
             if (!b->lane_used[k]) continue;
             SKM_HIP(hipEventRecord(b->lane_ev[k], b->lane_st[k]));
@@ -6893,15 +6914,6 @@ void phase_stats(skm_build* b) {
         if (b->gused[g]) SKM_HIP(hipStreamWaitEvent(st, b->gev_done[g], 0));
     SKM_HIP(hipEventRecord(b->ev_tail[1], st));
     SKM_HIP(hipEventRecord(b->ev[7], st));
-    SKM_HIP(hipMemsetAsync(b->d_dfunc.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
-    SKM_HIP(hipMemsetAsync(b->d_swf.p, 0, sizeof(uint32_t) * (F ? F : 1), st));
-    const size_t lds_f = F <= 16384 ? sizeof(uint32_t) * F : 0;
-    SKM_LAUNCH(b, k_kept_finalize, dim3(2048), dim3(256), lds_f, st, b->d_keys.as<uint64_t>(),
-                       b->d_data.as<skm_stored_kmer_data>(), b->d_ctr.as<unsigned long long>(), F,
-                       b->d_dfunc.as<uint32_t>());
-    if (b->nseq)
-        SKM_LAUNCH(b, k_func_hist_seqs, dim3(256), dim3(256), lds_f, st, b->d_meta.as<SeqMeta>(), b->nseq, F,
-                           b->d_swf.as<uint32_t>());
     SKM_HIP(hipGetLastError());
 }
 
