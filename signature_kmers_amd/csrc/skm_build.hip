@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -1625,6 +1626,24 @@ __device__ __forceinline__ bool bloom_has(const uint32_t* bloom, uint64_t h) {
     return ((bloom[b1 >> 5] >> (b1 & 31u)) & (bloom[b2 >> 5] >> (b2 & 31u)) & 1u) != 0;
 }
 
+// The base-40 keys of the 16 windows starting at codes[0..15] (24 codes): k = H * 40^4 + L with
+// H, L the base-40 numbers of the window's first and last four codes, each rolled in 32-bit
+// integer arithmetic (< 40^4 < 2^22: 24-bit multiply-adds), one 32 x 32 -> 64 multiply-add per
+// key instead of a rolled 64-bit key (the emission and pass-id kernels are VALU-bound)
+__device__ __forceinline__ void roll_keys16(const uint32_t (&code)[24], uint64_t (&k)[16]) {
+    constexpr uint32_t P3 = 64000u, P4 = 2560000u;  // 40^3, 40^4
+    uint32_t H = ((code[0] * 40u + code[1]) * 40u + code[2]) * 40u + code[3];
+    uint32_t L = ((code[4] * 40u + code[5]) * 40u + code[6]) * 40u + code[7];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        if (t > 0) {
+            H = (H - code[t - 1] * P3) * 40u + code[t + 3];
+            L = (L - code[t + 3] * P3) * 40u + code[t + 7];
+        }
+        k[t] = (uint64_t)H * P4 + L;
+    }
+}
+
 // mix43 of the (valid) window at packed position p, or ~0 when the window is not valid
 __device__ __forceinline__ uint64_t sampled_hash(const uint8_t* __restrict__ res, uint64_t p, uint64_t rp) {
     if (p >= rp) return ~0ull;
@@ -1754,37 +1773,47 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
             valid |= (cd < 40u ? 1u : 0u) << j;
             code[j] = cd < 40u ? cd : 0u;
         }
-        uint64_t k = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
-        constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
+        uint64_t kk[16];
+        roll_keys16(code, kk);
         uint32_t out[4] = {0u, 0u, 0u, 0u};
+        // every lane computes every window's id with selects, one loop per (uniform) mode: the kernel
+        // is VALU-bound, and per-window exec-mask branches cost more than the work they skip
+        auto windows = [&](auto mode) {
+            constexpr int M = decltype(mode)::value;  // 0: prepare counts, 1: no routing, 2: routing, 3: route_first
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
-            uint32_t id = 0xFFu;
-            if (((valid >> t) & 0xFFu) == 0xFFu && base + t < rp) {
-                const uint64_t h = mix43(k);
-                if (pass_bits == 0 && owner_bits == 0) {
-                    if (counts) atomicAdd(&s_cnt[(uint32_t)(h >> (KEY_BITS - 6))], 1u);
+            for (int t = 0; t < 16; ++t) {
+                const bool v = ((valid >> t) & 0xFFu) == 0xFFu && base + t < rp;
+                const uint64_t h = mix43(kk[t]);
+                uint32_t id = 0xFFu;
+                if constexpr (M == 0) {
+                    if (counts && v) atomicAdd(&s_cnt[(uint32_t)(h >> (KEY_BITS - 6))], 1u);
                 } else {
                     id = pass_bits ? (uint32_t)(h >> (KEY_BITS - pass_bits)) : 0u;
-                    if (route && first) {
-                        if (bloom_has(s_bloom, h))
-                            id = 0;
-                        else if (id == 0)
-                            id = 1u + (uint32_t)(((uint32_t)(h & 0xFFFFu) * ((1u << pass_bits) - 1u)) >> 16);
-                    } else if (route && id >= keep && bloom_has(s_bloom, h)) {
-                        id = R == half ? id - half : (uint32_t)(((uint32_t)(h & 0xFFFFu) * keep) >> 16);
+                    if constexpr (M >= 2) {
+                        const bool hb = bloom_has(s_bloom, h);
+                        const uint32_t h16 = (uint32_t)(h & 0xFFFFu);
+                        if constexpr (M == 3)
+                            id = hb ? 0u : (id == 0 ? 1u + ((h16 * ((1u << pass_bits) - 1u)) >> 16) : id);
+                        else
+                            id = (id >= keep && hb) ? (R == half ? id - half : (h16 * keep) >> 16) : id;
                     }
-                    if (tally) {
+                    if (tally && v) {
                         const uint32_t own = (uint32_t)(h >> (KEY_BITS - pass_bits - owner_bits)) & ((1u << owner_bits) - 1u);
                         atomicAdd(&s_cnt[(id << owner_bits) | own], 1u);
                     }
+                    id = v ? id : 0xFFu;
                 }
+                out[t >> 2] |= id << (8 * (t & 3));
             }
-            out[t >> 2] |= id << (8 * (t & 3));
-        }
+        };
+        if (pass_bits == 0 && owner_bits == 0)
+            windows(std::integral_constant<int, 0>{});
+        else if (!route)
+            windows(std::integral_constant<int, 1>{});
+        else if (first)
+            windows(std::integral_constant<int, 3>{});
+        else
+            windows(std::integral_constant<int, 2>{});
         if (!counts && ids) *reinterpret_cast<uint4*>(ids + base) = make_uint4(out[0], out[1], out[2], out[3]);
     }
     if (counts) {
@@ -1880,6 +1909,8 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
         uint32_t cnt[G];
 #pragma unroll
         for (uint32_t q = 0; q < G; ++q) cnt[q] = 0;
+        constexpr bool PACK = G <= 4;  // the lane's counts as 8-bit fields of one word
+        uint32_t pc = 0;
         if (base < e) {
             const uint32_t idw[4] = {id4.x, id4.y, id4.z, id4.w};
             uint32_t any = 0;
@@ -1890,8 +1921,12 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                     any |= 1u << t;
                     qs[t >> 2] &= ~(0xFFu << (8 * (t & 3)));
                     qs[t >> 2] |= q << (8 * (t & 3));
+                    if constexpr (PACK) {
+                        pc += 1u << (8u * q);
+                    } else {
 #pragma unroll
-                    for (uint32_t j = 0; j < G; ++j) cnt[j] += q == j ? 1u : 0u;
+                        for (uint32_t j = 0; j < G; ++j) cnt[j] += q == j ? 1u : 0u;
+                    }
                 }
             }
             if (any) {  // the 16 keys rolled from the lane's 24 residues, mixed for the group's windows
@@ -1902,16 +1937,15 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                     const uint32_t cd = residue_code((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
                     code[j] = cd < 40u ? cd : 0u;
                 }
-                uint64_t k = 0;
+                uint64_t k[16];
+                roll_keys16(code, k);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) k = k * 40u + code[j];
-                constexpr uint64_t P7 = 6553600000000ull / 40u;  // 40^7
-#pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    if (t > 0) k = (k - (uint64_t)code[t - 1] * P7) * 40u + code[t + 7];
-                    hs[t] = ((any >> t) & 1u) ? mix43(k) : 0ull;
-                }
+                for (int t = 0; t < 16; ++t) hs[t] = ((any >> t) & 1u) ? mix43(k[t]) : 0ull;
             }
+        }
+        if constexpr (PACK) {
+#pragma unroll
+            for (uint32_t q = 0; q < G; ++q) cnt[q] = (pc >> (8u * q)) & 0xFFu;
         }
         // pass-major ranks of the wave's tile: one DPP scan per pass of the group
         uint32_t off[G], qa[G + 1];
@@ -1923,15 +1957,29 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
             off[q] = qa[q] + inc - cnt[q];
             qa[q + 1] = qa[q] + tot;
         }
+        if constexpr (PACK) {  // the lane's running offsets as 16-bit fields of one u64 (< 1024 each)
+            uint64_t op = 0;
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const uint32_t q = (qs[t >> 2] >> (8 * (t & 3))) & 0xFFu;
-            if (q >= G) continue;
-            uint32_t f = 0;
+            for (uint32_t q = 0; q < G; ++q) op |= (uint64_t)off[q] << (16u * q);
 #pragma unroll
-            for (uint32_t j = 0; j < G; ++j)
-                if (q == j) f = off[j]++;
-            s_out[f] = ((uint64_t)(16u * lane + (uint32_t)t) << KEY_BITS) | hs[t];
+            for (int t = 0; t < 16; ++t) {
+                const uint32_t q = (qs[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+                if (q >= G) continue;
+                const uint32_t f = (uint32_t)(op >> (16u * q)) & 0xFFFFu;
+                op += 1ull << (16u * q);
+                s_out[f] = ((uint64_t)(16u * lane + (uint32_t)t) << KEY_BITS) | hs[t];
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const uint32_t q = (qs[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+                if (q >= G) continue;
+                uint32_t f = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < G; ++j)
+                    if (q == j) f = off[j]++;
+                s_out[f] = ((uint64_t)(16u * lane + (uint32_t)t) << KEY_BITS) | hs[t];
+            }
         }
         wave_sync();
         for (uint32_t j = lane; j < qa[G]; j += 64) {
