@@ -1626,6 +1626,23 @@ __device__ __forceinline__ bool bloom_has(const uint32_t* bloom, uint64_t h) {
     return ((bloom[b1 >> 5] >> (b1 & 31u)) & (bloom[b2 >> 5] >> (b2 & 31u)) & 1u) != 0;
 }
 
+// residue_code of every byte value in LDS (0xFF: not an ok_prot_ residue): the VALU-bound scans
+// look a residue's code up instead of computing it (~10 VALU operations per byte)
+__device__ __forceinline__ void fill_code_lut(uint8_t* lut) {
+    for (uint32_t c = threadIdx.x; c < 256; c += blockDim.x) lut[c] = (uint8_t)residue_code(c);
+}
+// the 24 codes of a lane's 32 residue bytes (w[0..5] hold the first 24) and their validity bits
+__device__ __forceinline__ uint32_t lut_codes24(const uint8_t* lut, const uint32_t (&w)[8], uint32_t (&code)[24]) {
+    uint32_t valid = 0;
+#pragma unroll
+    for (int j = 0; j < 24; ++j) {
+        const uint32_t cd = lut[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu];
+        valid |= (cd < 40u ? 1u : 0u) << j;
+        code[j] = cd < 40u ? cd : 0u;
+    }
+    return valid;
+}
+
 // The base-40 keys of the 16 windows starting at codes[0..15] (24 codes): k = H * 40^4 + L with
 // H, L the base-40 numbers of the window's first and last four codes, each rolled in 32-bit
 // integer arithmetic (< 40^4 < 2^22: 24-bit multiply-adds), one 32 x 32 -> 64 multiply-add per
@@ -1730,8 +1747,10 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
                                                   uint32_t* __restrict__ rows = nullptr, uint64_t span = 0,
                                                   uint32_t vac = 0) {
     extern __shared__ uint32_t s_dyn[];
+    __shared__ uint8_t s_code[256];
     uint32_t* s_cnt = s_dyn;
     uint32_t* s_bloom = s_dyn + ncnt;  // (1 << BLOOM_BITS) / 32 words when routing
+    fill_code_lut(s_code);
     const bool tally = counts != nullptr || rows != nullptr;
     if (tally)
         for (uint32_t c = threadIdx.x; c < ncnt; c += blockDim.x) s_cnt[c] = 0;
@@ -1766,13 +1785,7 @@ __global__ __launch_bounds__(256) void k_pass_ids(const uint8_t* __restrict__ re
         }
         const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
         uint32_t code[24];
-        uint32_t valid = 0;
-#pragma unroll
-        for (int j = 0; j < 24; ++j) {
-            const uint32_t cd = residue_code((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
-            valid |= (cd < 40u ? 1u : 0u) << j;
-            code[j] = cd < 40u ? cd : 0u;
-        }
+        const uint32_t valid = lut_codes24(s_code, w, code);
         uint64_t kk[16];
         roll_keys16(code, kk);
         uint32_t out[4] = {0u, 0u, 0u, 0u};
@@ -1880,7 +1893,10 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
                                                            const uint64_t* __restrict__ seloff, uint32_t nrows,
                                                            uint64_t* __restrict__ pos, uint64_t cap) {
     __shared__ uint64_t s_out[16 * 64];  // the tile's entries, pass-major: window in the tile << 43 | hash
+    __shared__ uint8_t s_code[256];
     const uint32_t lane = threadIdx.x;
+    fill_code_lut(s_code);
+    wave_sync();
     uint64_t run[G];
 #pragma unroll
     for (uint32_t q = 0; q < G; ++q) run[q] = seloff[(uint64_t)(pass0 + q) * (nrows + 1) + blockIdx.x];
@@ -1932,11 +1948,7 @@ __global__ __launch_bounds__(EMIT_THREADS) void k_pass_emit(const uint8_t* __res
             if (any) {  // the 16 keys rolled from the lane's 24 residues, mixed for the group's windows
                 const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
                 uint32_t code[24];
-#pragma unroll
-                for (int j = 0; j < 24; ++j) {
-                    const uint32_t cd = residue_code((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
-                    code[j] = cd < 40u ? cd : 0u;
-                }
+                (void)lut_codes24(s_code, w, code);
                 uint64_t k[16];
                 roll_keys16(code, k);
 #pragma unroll
