@@ -332,6 +332,9 @@ def main():
     }
     out["chain_tail_ms"] = head["chain_tail_ms"]
     out["giant_chains"] = head["giant_chains"]
+    keep = ("overflow_subbuckets", "overflow_elements", "overflow_kept", "big_groups", "big_kept", "chain_jobs",
+            "chain_samples", "long_samples", "routed", "pass_groups", "kept_cap", "free_after_prepare", "recs_rot")
+    out["build_counters_rank0"] = {k: int(v) for k, v in head["counters"].items() if k in keep}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         n = a.seqs_total // max(1, a.cpu_shard_div)
         log(f"CPU baseline: first {n:,} proteins (1/{a.cpu_shard_div} shard of C3)")

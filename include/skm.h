@@ -161,7 +161,9 @@ int skm_build_kernel_timings(skm_build* b, char* names, size_t names_cap, float*
  * host microseconds, [34] of them waiting for the device / PCIe, [35] copying pieces out on the
  * host pool, [36] chunks, and its device microseconds summed over the chunks: [37] selection,
  * [38] radix sort, [39] gather, [40] the D2H pieces; [41] the largest hand-off chunk (k-mers),
- * [42] 1 if the hand-off used 64-bit arena indices (>= 2^32 k-mers); returns entries written. */
+ * [42] 1 if the hand-off used 64-bit arena indices (>= 2^32 k-mers); [43] the kept arena's
+ * capacity (k-mers); [44] device bytes free after prepare; [45] 1 if the passes alternate two
+ * element buffers ("recs_rot"); returns entries written. */
 int skm_build_counters(skm_build* b, uint64_t* out, int cap);
 /* Host transport: the rank collectives of a multi-process build run by the caller on host
  * buffers, for ranks joined by a channel other than RCCL (the tests drive it with

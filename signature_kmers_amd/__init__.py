@@ -337,8 +337,8 @@ class SignatureBuilder:
         return self.counters()["passes"]
 
     def counters(self) -> dict:
-        v = (C.c_uint64 * 43)()
-        n = lib().skm_build_counters(self._h, v, 43)
+        v = (C.c_uint64 * 46)()
+        n = lib().skm_build_counters(self._h, v, 46)
         names = ["windows", "kept", "overflow_subbuckets", "chain_jobs", "chain_samples", "sequences", "grouped",
                  "overflow_elements", "overflow_kept", "big_groups", "big_kept", "passes", "valid", "giant_chains",
                  "giant_max", "redone", "cap_overflow_scratch", "cap_split", "cap_long_samples", "cap_long_jobs",
@@ -346,7 +346,8 @@ class SignatureBuilder:
                  "long_samples", "routed", "add_batch_us", "prepare_upload_us", "prepare_plan_us", "prepare_rest_us",
                  "pass_groups", "add_pack_us", "add_dma_wait_us", "finish_us", "finish_wait_us", "finish_copy_us",
                  "finish_chunks", "finish_select_dev_us", "finish_sort_dev_us", "finish_gather_dev_us",
-                 "finish_d2h_dev_us", "finish_max_chunk", "finish_wide_index"]
+                 "finish_d2h_dev_us", "finish_max_chunk", "finish_wide_index", "kept_cap",
+                 "free_after_prepare", "recs_rot"]
         return {names[i]: int(v[i]) for i in range(n)}
 
     def debug_jobs(self, k: int = 64) -> list:

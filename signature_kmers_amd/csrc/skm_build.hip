@@ -30,6 +30,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <numeric>
 #include <string>
@@ -4994,6 +4995,17 @@ struct Tune {
     // tail_async: the 1025..CAP class on a second tail stream.  Measured slower at C3 (round 6,
     // one box: 1445 / 1474 vs 1391 / 1429 ms/step): the concurrent classes slow the chains after them
     int big_split = 0;
+    // tail_async: the tail is issued after the next pass's scan kernels (k_colsum .. k_stage_init),
+    // which otherwise wait ~2 ms per pass behind k_big_groups' persistent grid for their workgroups.
+    // Within noise at C3 (round 6, one box: 1434 / 1387 vs 1414 / 1377 ms/step): the scan's 25 ms
+    // per step go, the tail then slows the staging more
+    int tail_defer = 0;
+    // tail_async: the split writes the pass's elements into one of two element buffers by pass
+    // parity, so the next pass's split no longer waits for this pass's tail (which reads them);
+    // the wait moves to the partition.  Costs 16 B per element of the largest pass (when it fits
+    // beside a kept arena of a quarter of the valid windows).  With tail_defer, within noise at C3
+    // (1396 / 1405 vs 1414 / 1377 ms/step): the device is busy either way, the tail's work moves
+    int recs_rot = 0;
     int emit_group = 0;              // key-range passes emitted per residue scan (0: 4; 1, 2, 4, 8 or 16)
     int route_first = -1;
     int route_first_min = 1 << 17;   // route_first: k-mers of >= this many occurrences make pass 0 (C3: ~4.5 %
@@ -5138,6 +5150,10 @@ struct skm_build {
     hipStream_t stream_tail2 = nullptr; //   the groups of 1025..CAP members beside the smaller big groups
     hipEvent_t ev_tail_bp = nullptr, ev_tail_done = nullptr, ev_tail2 = nullptr;
     bool tail_pending = false;          // the last pass's tail is still in flight on stream_tail
+    std::function<void()> tail_issue;   // tail_defer: the last pass's tail, not yet issued
+    hipEvent_t ev_scan = nullptr;       // tail_defer: the next pass's scan kernels are done
+    bool rot = false;                   // recs_rot: odd passes split into d_recs_*2
+    uint64_t free_after_prepare = 0;    // device bytes free after prepare (counters [44])
     hipEvent_t ev_part = nullptr, ev_split = nullptr;
     DevBuf d_hv_keys, d_hv_rec, d_hv_len, d_hv_s0, d_hv_s1;   // heavy keys of the split overflow
     DevBuf d_sub_tab, d_jobs2, d_jobs3;
@@ -6081,6 +6097,24 @@ void prepare(const Ranks& bs) {
             b->long_cap = b->pass_bits ? b->valid_total / 8 + (1u << 16) : 0;
         }
         alloc_caps(b);
+        // recs_rot: the second element buffer, before the kept arena takes the rest of the memory
+        b->rot = false;
+        if (b->tune.recs_rot && b->tune.tail_async && !b->tune.overlap && b->world == 1 && b->pass_bits > 0) {
+            const uint64_t W = std::max<uint64_t>(b->pass_max, 1);
+            if (b->d_recs_hi2.bytes >= 8 * W && b->d_recs_lo2.bytes >= 8 * W) {
+                b->rot = true;
+            } else {
+                size_t fr = 0, tot = 0;
+                SKM_HIP(hipMemGetInfo(&fr, &tot));
+                const uint64_t held = (uint64_t)b->d_keys.bytes + (uint64_t)b->d_data.bytes;
+                const uint64_t need = 16 * W + 32 * W + (1ull << 30) + 18 * (b->valid_total / 4);
+                if ((uint64_t)fr + held > need) {
+                    b->d_recs_hi2.ensure(8 * W);
+                    b->d_recs_lo2.ensure(8 * W);
+                    b->rot = true;
+                }
+            }
+        }
         size_arena(b);
         b->d_flags.ensure(std::max<uint64_t>(b->n_total, 1));
         b->d_flagbits.ensure(4 * ((b->n_total + 31) / 32 + 1));
@@ -6101,6 +6135,11 @@ void prepare(const Ranks& bs) {
                 b->overlap = true;
             }
             if (b->overlap) b->d_ovf2b.ensure(sizeof(OvfEntry) * std::max<uint64_t>(b->ovf_cap, 1));
+        }
+        {
+            size_t fr = 0, tot = 0;
+            SKM_HIP(hipMemGetInfo(&fr, &tot));
+            b->free_after_prepare = fr;
         }
         SKM_HIP(hipStreamSynchronize(b->stream));
         b->prepared = true;
@@ -6145,8 +6184,9 @@ void emit_group(skm_build* b, uint32_t g, hipStream_t st) {
 
 // the element buffer set, counter block, plan and overflow list of a pass (set 0 unless overlap)
 inline int pset(const skm_build* b, uint32_t pass) { return b->overlap ? (int)(pass & 1u) : 0; }
-inline uint64_t* recs_hi(skm_build* b, uint32_t pass) { return (pset(b, pass) ? b->d_recs_hi2 : b->d_recs_hi).as<uint64_t>(); }
-inline uint64_t* recs_lo(skm_build* b, uint32_t pass) { return (pset(b, pass) ? b->d_recs_lo2 : b->d_recs_lo).as<uint64_t>(); }
+inline bool rset(const skm_build* b, uint32_t pass) { return pset(b, pass) || (b->rot && (pass & 1u)); }
+inline uint64_t* recs_hi(skm_build* b, uint32_t pass) { return (rset(b, pass) ? b->d_recs_hi2 : b->d_recs_hi).as<uint64_t>(); }
+inline uint64_t* recs_lo(skm_build* b, uint32_t pass) { return (rset(b, pass) ? b->d_recs_lo2 : b->d_recs_lo).as<uint64_t>(); }
 inline uint64_t* tmp_hi(skm_build* b, uint32_t pass) { return (pset(b, pass) ? b->d_tmp_hi2 : b->d_tmp_hi).as<uint64_t>(); }
 inline uint64_t* tmp_lo(skm_build* b, uint32_t pass) { return (pset(b, pass) ? b->d_tmp_lo2 : b->d_tmp_lo).as<uint64_t>(); }
 // d_ctr: [0] the kept arena cursor, [2] the flag count (run-level); per-set pass counters at 32, 64
@@ -6157,7 +6197,20 @@ inline unsigned long long* pass_ctr(skm_build* b, uint32_t pass) {
 // the main stream waits for the previous pass's tail (tail_async) before it overwrites what the tail
 // reads (the split's recs, then the partition's tmp, the counters, the job lists) or reads what it
 // writes (the stash cursors, the kept arena's totals)
+// tail_defer: the last pass's tail is issued now (after_scan: behind the next pass's scan kernels)
+void issue_tail(skm_build* b, bool after_scan) {
+    if (!b->tail_issue) return;
+    if (after_scan) {
+        SKM_HIP(hipEventRecord(b->ev_scan, b->stream));
+        SKM_HIP(hipStreamWaitEvent(b->stream_tail, b->ev_scan, 0));
+    }
+    std::function<void()> f;
+    f.swap(b->tail_issue);
+    f();
+}
+
 void join_tail(skm_build* b) {
+    issue_tail(b, false);
     if (!b->tail_pending) return;
     SKM_HIP(hipStreamWaitEvent(b->stream, b->ev_tail_done, 0));
     b->tail_pending = false;
@@ -6234,6 +6287,7 @@ void phase_extract(skm_build* b, uint32_t pass) {
     b->d_slices.ensure(4 * 80);
     SKM_LAUNCH(b, k_stage_init, dim3((NB + 255) / 256), dim3(256), 0, st, b->d_bstart.as<uint64_t>(), NB, l0_shift,
                        b->d_cur0.as<unsigned long long>(), b->d_cur1.as<unsigned long long>(), b->d_slices.as<uint32_t>());
+    issue_tail(b, true);
     // the level-0 staging: tmp, or (tail_async) a buffer of its own, so it overlaps the previous
     // pass's tail, which still reads tmp and recs
     const bool sep = tail_async_on(b);
@@ -6255,7 +6309,8 @@ void phase_extract(skm_build* b, uint32_t pass) {
     else
         SKM_LAUNCH(b, k_extract_stage, dim3(nwg), dim3(EX_THREADS), 0, st, X, b->d_cur0.as<unsigned long long>(),
                            stg_hi, stg_lo);
-    join_tail(b);
+    // recs_rot: the split writes the other element buffer; the wait moves to the partition
+    if (!b->rot) join_tail(b);
     const uint32_t nsl = (uint32_t)(ceil_div(b->pass_max, SC_SLICE) + (1u << SC_L0_BITS));
     SKM_LAUNCH(b, k_split_stage, dim3(nsl), dim3(EX_THREADS), 0, st, stg_hi,
                        stg_lo, b->d_bstart.as<uint64_t>(), nbits, b->d_slices.as<uint32_t>(),
@@ -6479,6 +6534,7 @@ void phase_group(skm_build* b, uint32_t pass) {
     hipStream_t st = b->stream, st2 = b->stream2, st3 = b->stream3;
     const bool multi = b->world > 1;
     const uint32_t NB1 = 1u << b->b1_bits;
+    join_tail(b);  // recs_rot: the previous pass's tail still read tmp, the counters and the job lists
     SKM_HIP(hipEventRecord(b->ev[4], st));
     // per-pass counters; [0] (kept k-mers: the arena cursor) and the signature flags run over
     // all passes (begin_run clears them)
@@ -6686,6 +6742,8 @@ void phase_group(skm_build* b, uint32_t pass) {
         SKM_HIP(hipEventRecord(b->ev_tail_bp, st));
         SKM_HIP(hipStreamWaitEvent(tt, b->ev_tail_bp, 0));
     }
+    hipEvent_t* ev = b->ev;  // this pass's events (the deferred tail is issued after use_evset(pass + 1))
+    auto big_tail = [=]() {
     if (tail_async && b->tune.big_split) {
         // the two size classes of big groups are independent (disjoint descriptors and outputs):
         // the large class on a stream of its own, joined before the append
@@ -6701,7 +6759,8 @@ void phase_group(skm_build* b, uint32_t pass) {
     }
     SKM_LAUNCH(b, k_big_append, dim3(256), dim3(BIG_WG), 0, tt, BA.out, BA, A);
     SKM_HIP(hipGetLastError());
-    SKM_HIP(hipEventRecord(b->ev[12], tt));
+    SKM_HIP(hipEventRecord(ev[12], tt));
+    };
     // ---- 6. deferred P^2 / variance chains: the overflow's as soon as both parts are grouped
     //      (the long ones on stream 2, the per-lane ones on stream 3), the group-by's on st ----
     SKM_HIP(hipEventRecord(b->ev_o3[0], st3));
@@ -6710,35 +6769,45 @@ void phase_group(skm_build* b, uint32_t pass) {
                   A.out_data, (uint32_t)b->tune.ovf_long_class, st3, b->ev_o3[2], (uint32_t)b->tune.ovf_chain_wgs);
     SKM_HIP(hipEventRecord(b->ev_o[2], st2));
     SKM_HIP(hipEventRecord(b->ev_o3[1], st3));
+    hipEvent_t* ev_o = b->ev_o;
+    hipEvent_t* ev_o3 = b->ev_o3;
+    auto main_tail = [=]() {
+    big_tail();
     launch_chains(b, tt, A.jobs, ctr_d + 3, b->jobs_cap, b->cs_main, A.lens, reinterpret_cast<const uint32_t*>(A.recs_hi),
                   reinterpret_cast<const uint32_t*>(A.tmp_hi), nullptr, A.out_data, (uint32_t)b->tune.main_long_class);
     if (b->overlap) {
         // the pass ends on the main stream here; its overflow path and accounting finish on
         // stream 2 beside the next pass, whose staging into this set waits for ev_ovf_done
         SKM_HIP(hipEventRecord(b->ev_main_done[ks], st));
-        SKM_HIP(hipEventRecord(b->ev[6], st));
-        SKM_HIP(hipStreamWaitEvent(st2, b->ev_o3[1], 0));
+        SKM_HIP(hipEventRecord(ev[6], st));
+        SKM_HIP(hipStreamWaitEvent(st2, ev_o3[1], 0));
         SKM_HIP(hipStreamWaitEvent(st2, b->ev_main_done[ks], 0));
         SKM_LAUNCH(b, k_pass_account, dim3(1), dim3(1), 0, st2, ctr_d, run_d, b->jobs_cap, b->jobs2_cap, b->big_cap,
                    b->lens_cap);
         SKM_HIP(hipGetLastError());
         SKM_HIP(hipEventRecord(b->ev_ovf_done[ks], st2));
         b->ovf_pending[ks] = true;
-        SKM_HIP(hipEventRecord(b->ev[7], st));
+        SKM_HIP(hipEventRecord(ev[7], st));
         return;
     }
-    SKM_HIP(hipStreamWaitEvent(tt, b->ev_o[2], 0));
-    SKM_HIP(hipStreamWaitEvent(tt, b->ev_o3[1], 0));
-    SKM_HIP(hipEventRecord(b->ev[6], tt));
+    SKM_HIP(hipStreamWaitEvent(tt, ev_o[2], 0));
+    SKM_HIP(hipStreamWaitEvent(tt, ev_o3[1], 0));
+    SKM_HIP(hipEventRecord(ev[6], tt));
     // ---- 7. run totals and the chain lists' bounds ----
     SKM_LAUNCH(b, k_pass_account, dim3(1), dim3(1), 0, tt, ctr_d, run_d, b->jobs_cap, b->jobs2_cap, b->big_cap,
                        b->lens_cap);
     SKM_HIP(hipGetLastError());
-    SKM_HIP(hipEventRecord(b->ev[7], tt));
+    SKM_HIP(hipEventRecord(ev[7], tt));
     if (tail_async) {
         SKM_HIP(hipEventRecord(b->ev_tail_done, tt));
         b->tail_pending = true;
     }
+    };
+    // tail_defer: issued by the next pass's phase_extract after its scan kernels (or by join_tail)
+    if (tail_async && b->tune.tail_defer && pass + 1 < NP && !b->overlap)
+        b->tail_issue = main_tail;
+    else
+        main_tail();
 }
 
 // overlap: the main stream waits for every pass's overflow path still in flight
@@ -6817,6 +6886,7 @@ void begin_run(skm_build* b) {
     b->emit_q = -1;  // no pass group's positions are queued from an earlier (possibly aborted) run
     b->giant_timed = false;
     b->tail_pending = false;
+    b->tail_issue = nullptr;
     SKM_HIP(hipEventRecord(b->ev_start, st));
     SKM_HIP(hipMemsetAsync(b->d_ctr.p, 0, 3 * 256, st));
     b->ovf_pending[0] = b->ovf_pending[1] = false;
@@ -7152,6 +7222,7 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     SKM_HIP(hipEventCreateWithFlags(&b->ev_tail2, hipEventDisableTiming));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_tail_bp, hipEventDisableTiming));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_tail_done, hipEventDisableTiming));
+    SKM_HIP(hipEventCreateWithFlags(&b->ev_scan, hipEventDisableTiming));
     use_evset(b, 0);
     SKM_HIP(hipEventCreate(&b->ev_start));
     SKM_HIP(hipStreamCreateWithFlags(&b->chain_st, hipStreamNonBlocking));
@@ -7550,6 +7621,8 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "big_grid" ? &t.big_grid
                : n == "big_grid_large" ? &t.big_grid_large
                : n == "big_split" ? &t.big_split
+               : n == "tail_defer" ? &t.tail_defer
+               : n == "recs_rot" ? &t.recs_rot
                : n == "emit_group" ? &t.emit_group
                : n == "handoff_index_limit" ? &t.handoff_index_limit
                : n == "handoff_max_chunk" ? &t.handoff_max_chunk
@@ -7692,7 +7765,7 @@ int skm_debug_div_check(uint64_t nm, uint32_t per, uint64_t* mismatches) {
 int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
     if (!b || !out) return SKM_E_ARG;
     auto us = [](double sec) { return (uint64_t)(sec * 1e6); };
-    const uint64_t v[43] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
+    const uint64_t v[46] = {b->n_windows, b->n_kept, b->n_overflow, b->n_jobs, b->n_lens, b->nseq, b->n_local,
                             b->ovf_elems, b->ovf_kept, b->n_big, b->big_kept, 1ull << b->pass_bits, b->valid_total,
                             b->giant_jobs, b->giant_max, b->n_redo, b->tot_cap, b->split_cap, b->long_cap,
                             b->long_jobs_cap, b->demand[0], b->demand[1], b->demand[2], b->demand[3],
@@ -7702,8 +7775,9 @@ int skm_build_counters(skm_build* b, uint64_t* out, int cap) {
                             us(b->handoff.copy_s), b->handoff.chunks, (uint64_t)(1e3 * b->handoff.select_ms),
                             (uint64_t)(1e3 * b->handoff.sort_ms), (uint64_t)(1e3 * b->handoff.gather_ms),
                             (uint64_t)(1e3 * b->handoff.d2h_ms), b->handoff.max_chunk,
-                            (uint64_t)b->handoff.wide_index};
-    int n = std::min(cap, 43);
+                            (uint64_t)b->handoff.wide_index, b->kept_cap, b->free_after_prepare,
+                            (uint64_t)b->rot};
+    int n = std::min(cap, 46);
     for (int i = 0; i < n; ++i) out[i] = v[i];
     return n;
 }
@@ -8018,6 +8092,7 @@ void skm_build_destroy(skm_build* b) {
     if (b->ev_tail2) (void)hipEventDestroy(b->ev_tail2);
     if (b->ev_tail_bp) (void)hipEventDestroy(b->ev_tail_bp);
     if (b->ev_tail_done) (void)hipEventDestroy(b->ev_tail_done);
+    if (b->ev_scan) (void)hipEventDestroy(b->ev_scan);
     delete b;
 }
 

@@ -90,7 +90,9 @@ def test_overflow_inline_chains(skm, gpu, inline_min):
                                                    (4, 8, {"side_cus": 64}),
                                                    (4, 8, {"overlap": 1}), (16, 8, {"overlap": 1}),
                                                    (4, 8, {"overlap": 1, "serial_overflow": 1}),
-                                                   (4, 8, {"lane_long": 0}), (16, 8, {"lane_long": 600})])
+                                                   (4, 8, {"lane_long": 0}), (16, 8, {"lane_long": 600}),
+                                                   (16, 8, {"tail_defer": 1, "recs_rot": 1}), (4, 8, {"recs_rot": 1}),
+                                                   (16, 8, {"big_split": 1, "emit_group": 16})])
 def test_key_range_passes(skm, gpu, passes, long_class, opts):
     """Out-of-core build: P passes over disjoint k-mer ranges (each k-mer in exactly one pass)
     give the single-pass result bit for bit, overflow sub-buckets and chains included, and a
@@ -100,7 +102,9 @@ def test_key_range_passes(skm, gpu, passes, long_class, opts):
     partition_round 1, 2: rounds of 4096 with 512 / 1024 threads), flag_check, serial_overflow, chain_cus / side_cus (the long-chain / overflow
     and selection streams on a subset of the CUs), overlap 1 (pipelined passes: a second element
     buffer set, the pass's overflow path beside the next pass), lane_long 0 / 600 (every stashed long
-    chain on a wave pair / the ones of >= 600 samples: the others one lane each, k_chains)."""
+    chain on a wave pair / the ones of >= 600 samples: the others one lane each, k_chains),
+    tail_defer / recs_rot (the pass tail issued after the next pass's scan; the split alternating two
+    element buffers), big_split with emit_group 16 (one residue scan for all 16 passes)."""
     p = synth.generate_arrays(60000, 60, per_file=2000, seed=6)
     r, o, l, f, i, funcs = synth.build_inputs(p)
     ref = oracle_ref.build(r, o, l, f, i, len(funcs))
@@ -119,6 +123,8 @@ def test_key_range_passes(skm, gpu, passes, long_class, opts):
     b.close()
     assert_same(got, ref)
     assert c1["overflow_subbuckets"] > 0 and c1["grouped"] == oracle_ref.count_windows(l, f) - _invalid(r, o, l, f)
+    if opts.get("recs_rot") and passes > 1:
+        assert c1["recs_rot"] == 1  # the second element buffer fits at this size
 
 
 @pytest.mark.parametrize("passes,route_min,vacate", [(4, 256, 0), (16, 64, 0), (64, 1024, 0), (16, 64, 4), (16, 64, 1),
