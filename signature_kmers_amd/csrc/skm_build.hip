@@ -64,7 +64,11 @@ constexpr int BPK_THREADS = SKM_BPK_THREADS;
 constexpr int BPK_WAVES_EU = BPK_THREADS == 512 ? 4 : 2;  // two workgroups per CU (LDS ~78 KB each)
 constexpr int TAB_BITS = 12;
 constexpr int TAB = 1 << TAB_BITS;     // LDS hash slots per sub-bucket (load <= 0.5)
-constexpr int SUB_TARGET = 1024;       // target records per level-2 sub-bucket
+// target records per level-2 sub-bucket.  768 (round 6, C3 A/B on one box, three alternations each):
+// k_bucket_process 642 -> 617, overflow path 500 -> 450 ms of GPU time per step; the step itself
+// 1357 -> 1349 ms (within noise: the partition's 200 / 245 ms spread between runs dominates);
+// 512 takes the group-by to 600 ms but slows the partition as much
+constexpr int SUB_TARGET = 768;
 constexpr int MAX_B2 = 11;             // <= 2048 sub-buckets per level-1 bucket
 constexpr int SUB_TAB = (1 << MAX_B2) + 2;  // per-bucket sub-bucket table: count + offsets
 
