@@ -882,7 +882,7 @@ def _per_launch(traffic, passes):
     return None if traffic is None else traffic / max(1, passes)
 
 
-_PMC_FILE = "r05_pmc_traffic.json"
+_PMC_FILE = "r06_pmc_traffic.json"
 
 
 def src_sha16() -> str:
@@ -899,7 +899,7 @@ def src_sha16() -> str:
 
 
 def _pmc_traffic(kernel: str, workload: str, seqs: int):
-    """HBM bytes of `kernel` from the committed rocprofv3 PMC summary (profiles/r04_pmc_traffic.json,
+    """HBM bytes of `kernel` from the committed rocprofv3 PMC summary (profiles/r06_pmc_traffic.json,
     tools/gpu_profile.sh + tools/pmc_summary.py): per build run (all launches of a step)
     or per launch (legs), when it was measured on this kernel and workload size AND on the same
     device sources as this run (src_sha16); else None.  Streaming kernels count FETCH_SIZE x2,
