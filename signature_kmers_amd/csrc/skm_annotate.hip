@@ -1426,8 +1426,9 @@ void skm_calls_free(skm_calls* c) {
 // BDZ construction on the device (build_perfect_hash, perfect_hash.h:11-69, via cmph_new
 // CMPH_BDZ): same parameters as the host builder (r = ceil(1.23 m / 3) made odd, n = 3r,
 // jenkins seeds from mt19937(seed)), 3-hypergraph peeled in parallel rounds:
-//   k_mph_edges     one thread per key: 3 vertices, degree += 1, incident-edge XOR ^= e
-//   k_mph_frontier  vertices of degree 1
+//   k_mph_edges     one thread per key: 3 vertices, (degree, incident edge-id sum) += (1, e) in
+//                   one 64-bit atomic each
+//   k_mph_frontier  vertices of degree 1 (one reservation per wave of 8 x 64 vertices)
 //   k_mph_peel      a frontier vertex v peels its only edge e iff v is the first degree-1
 //                   vertex of e (deterministic: one peeler per edge, no atomics on e)
 //   k_mph_apply     the peeled edges leave their vertices; vertices that drop to degree 1 form
@@ -1464,47 +1465,71 @@ __device__ __forceinline__ void mph_verts(const MphDev& P, uint64_t k, uint32_t 
     v[2] = fastmod(c, P.r_magic, P.r) + 2u * P.r;
 }
 
+// A vertex's peel state is one u64: its degree << 40 | the sum of its incident edge ids.  One
+// 64-bit atomic adds or removes an edge (the degree and the id sum move together, half the
+// atomics of separate degree and XOR words); at degree 1 the sum is the edge.  The sum stays below
+// 2^40 while the degree is below 256: a vertex reaching MPH_DEG_MAX fails the attempt (never seen
+// at 2.89 G keys: the degrees are ~Poisson(2.4)).
+constexpr int MPH_SUM_BITS = 40;
+constexpr uint64_t MPH_ONE = 1ull << MPH_SUM_BITS;
+constexpr uint32_t MPH_DEG_MAX = 255;
+__device__ __forceinline__ uint32_t vdeg(uint64_t x) { return (uint32_t)(x >> MPH_SUM_BITS); }
+
 // (grids: m, n < 2^32 - 2^12, so a u32 global thread index never wraps)
-__global__ void k_mph_edges(const uint64_t* __restrict__ keys, uint32_t m, MphDev P, uint32_t* __restrict__ deg,
-                            uint32_t* __restrict__ xr) {
+__global__ void k_mph_edges(const uint64_t* __restrict__ keys, uint32_t m, MphDev P, unsigned long long* __restrict__ dx,
+                            uint32_t* __restrict__ bad) {
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= m) return;
     uint32_t v[3];
     mph_verts(P, keys[e], v);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        atomicAdd(&deg[v[j]], 1u);
-        atomicXor(&xr[v[j]], e);
-    }
+    for (int j = 0; j < 3; ++j)
+        if (vdeg(atomicAdd(&dx[v[j]], MPH_ONE + e)) + 1u >= MPH_DEG_MAX) atomicOr(bad, 1u);
 }
 
-__global__ void k_mph_frontier(const uint32_t* __restrict__ deg, uint32_t nv, uint32_t* __restrict__ fr,
-                               uint32_t* __restrict__ nfr) {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool one = v < nv && deg[v] == 1u;
-    const uint64_t bal = __ballot(one);
-    uint32_t base = 0;
+// MPH_FR_PER vertices per thread, one frontier reservation per wave (a single counter: at C3's
+// 3.55 G vertices one atomic per 64 vertices was 55 M atomics on one address per attempt)
+constexpr uint32_t MPH_FR_PER = 8;
+__global__ __launch_bounds__(256) void k_mph_frontier(const unsigned long long* __restrict__ dx, uint32_t nv,
+                                                      uint32_t* __restrict__ fr, uint32_t* __restrict__ nfr) {
+    const uint64_t v0 = (uint64_t)blockIdx.x * (256u * MPH_FR_PER) + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
-    if (lane == 0 && bal) base = atomicAdd(nfr, (uint32_t)__popcll(bal));
-    base = __shfl(base, 0);
-    if (one) fr[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = v;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t bal[MPH_FR_PER];
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < MPH_FR_PER; ++j) {
+        const uint64_t v = v0 + 256u * j;
+        bal[j] = __ballot(v < nv && vdeg(dx[v]) == 1u);
+        tot += (uint32_t)__popcll(bal[j]);
+    }
+    if (tot == 0) return;  // wave-uniform
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(nfr, tot);
+    base = (uint32_t)__shfl((int)base, 0);
+#pragma unroll
+    for (uint32_t j = 0; j < MPH_FR_PER; ++j) {
+        if ((bal[j] >> lane) & 1ull) fr[base + (uint32_t)__popcll(bal[j] & lt)] = (uint32_t)(v0 + 256u * j);
+        base += (uint32_t)__popcll(bal[j]);
+    }
 }
 
 // peeled entry: the edge id in pe[], the position of its free vertex in pp[]
 __global__ void k_mph_peel(const uint32_t* __restrict__ fr, uint32_t nf, const uint64_t* __restrict__ keys, MphDev P,
-                           const uint32_t* __restrict__ deg, const uint32_t* __restrict__ xr, uint32_t* __restrict__ pe,
+                           const unsigned long long* __restrict__ dx, uint32_t* __restrict__ pe,
                            uint8_t* __restrict__ pp, uint32_t* __restrict__ npeeled) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool take = false;
     uint32_t e = 0, pos = 0;
     if (i < nf) {
         const uint32_t v = fr[i];
-        if (deg[v] == 1u) {
-            e = xr[v];
+        const uint64_t xv = dx[v];
+        if (vdeg(xv) == 1u) {
+            e = (uint32_t)xv;
             uint32_t u[3];
             mph_verts(P, keys[e], u);
             for (uint32_t p = 0; p < 3; ++p) {
-                if (deg[u[p]] == 1u) {  // first degree-1 vertex of e peels it
+                if (vdeg(dx[u[p]]) == 1u) {  // first degree-1 vertex of e peels it
                     take = u[p] == v;
                     pos = p;
                     break;
@@ -1525,18 +1550,37 @@ __global__ void k_mph_peel(const uint32_t* __restrict__ fr, uint32_t nf, const u
 }
 
 __global__ void k_mph_apply(const uint32_t* __restrict__ pe, uint32_t p0, uint32_t p1, const uint64_t* __restrict__ keys,
-                            MphDev P, uint32_t* __restrict__ deg, uint32_t* __restrict__ xr, uint32_t* __restrict__ fr,
+                            MphDev P, unsigned long long* __restrict__ dx, uint32_t* __restrict__ fr,
                             uint32_t* __restrict__ nfr) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= p1 - p0) return;
-    const uint32_t e = pe[p0 + t];
-    uint32_t u[3];
-    mph_verts(P, keys[e], u);
+    const bool live = t < p1 - p0;
+    const uint32_t e = live ? pe[p0 + t] : 0u;
+    uint32_t u[3] = {0u, 0u, 0u};
+    if (live) mph_verts(P, keys[e], u);
+    bool add[3] = {false, false, false};
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+        if (live) {
+            add[j] = vdeg(atomicAdd(&dx[u[j]], 0ull - (MPH_ONE + e))) == 2u;
+        }
+    // the vertices that dropped to degree 1: one frontier reservation per wave (a single counter)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t bal[3];
+    uint32_t tot = 0;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const uint32_t old = atomicSub(&deg[u[j]], 1u);
-        atomicXor(&xr[u[j]], e);
-        if (old == 2u) fr[atomicAdd(nfr, 1u)] = u[j];
+        bal[j] = __ballot(add[j]);
+        tot += (uint32_t)__popcll(bal[j]);
+    }
+    if (tot == 0) return;  // wave-uniform
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(nfr, tot);
+    base = (uint32_t)__shfl((int)base, 0);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        if (add[j]) fr[base + (uint32_t)__popcll(bal[j] & lt)] = u[j];
+        base += (uint32_t)__popcll(bal[j]);
     }
 }
 
@@ -1660,7 +1704,7 @@ extern "C" int skm_mph_build_device_ex(const uint64_t* keys, const skm_stored_km
     h.b = 7;
     h.k = 1u << h.b;
     auto t = std::chrono::steady_clock::now();
-    DevBuf dkeys, ddata, ddeg, dxr, dfr0, dfr1, dpe, dpp, dcnt, dg;
+    DevBuf dkeys, ddata, ddx, dfr0, dfr1, dpe, dpp, dcnt, dg;
     dkeys.ensure(8ull * m);
     SKM_HIP(hipMemcpy(dkeys.p, keys, 8ull * m, hipMemcpyHostToDevice));
     st.upload_s = secs_since(t);
@@ -1694,35 +1738,33 @@ extern "C" int skm_mph_build_device_ex(const uint64_t* keys, const skm_stored_km
         h.seed = rng();
         P = MphDev{h.r, ~0ull / h.r + 1, h.seed};
         const uint32_t nv = h.n;
-        ddeg.ensure(4ull * nv);
-        dxr.ensure(4ull * nv);
+        ddx.ensure(8ull * nv);
         dfr0.ensure(4ull * nv);
         dfr1.ensure(4ull * nv);
-        SKM_HIP(hipMemset(ddeg.p, 0, 4ull * nv));
-        SKM_HIP(hipMemset(dxr.p, 0, 4ull * nv));
+        SKM_HIP(hipMemset(ddx.p, 0, 8ull * nv));
         SKM_HIP(hipMemset(dcnt.p, 0, 64));
         hipLaunchKernelGGL(k_mph_edges, dim3(ceil_div(m, 256)), dim3(256), 0, 0, dkeys.as<uint64_t>(), m, P,
-                           ddeg.as<uint32_t>(), dxr.as<uint32_t>());
-        hipLaunchKernelGGL(k_mph_frontier, dim3(ceil_div(nv, 256)), dim3(256), 0, 0, ddeg.as<uint32_t>(), nv,
+                           ddx.as<unsigned long long>(), cnt + 3);
+        hipLaunchKernelGGL(k_mph_frontier, dim3(ceil_div(nv, 256 * MPH_FR_PER)), dim3(256), 0, 0, ddx.as<unsigned long long>(), nv,
                            dfr0.as<uint32_t>(), cnt + 0);
         SKM_HIP(hipGetLastError());
         uint32_t hc[4] = {0, 0, 0, 0};
         SKM_HIP(hipMemcpy(hc, cnt, 16, hipMemcpyDeviceToHost));
-        uint32_t nf = hc[0], npeeled = 0;
+        uint32_t nf = hc[3] ? 0u : hc[0], npeeled = 0;  // a vertex of degree >= MPH_DEG_MAX: next seed
         rounds.assign(1, 0);
         DevBuf* cur = &dfr0;
         DevBuf* nxt = &dfr1;
         int fcur = 0;
         while (nf > 0) {
             hipLaunchKernelGGL(k_mph_peel, dim3(ceil_div(nf, 256)), dim3(256), 0, 0, cur->as<uint32_t>(), nf,
-                               dkeys.as<uint64_t>(), P, ddeg.as<uint32_t>(), dxr.as<uint32_t>(), dpe.as<uint32_t>(),
+                               dkeys.as<uint64_t>(), P, ddx.as<unsigned long long>(), dpe.as<uint32_t>(),
                                dpp.as<uint8_t>(), cnt + 2);
             SKM_HIP(hipMemset(cnt + (1 - fcur), 0, 4));
             uint32_t np = 0;
             SKM_HIP(hipMemcpy(&np, cnt + 2, 4, hipMemcpyDeviceToHost));
             if (np == npeeled) break;
             hipLaunchKernelGGL(k_mph_apply, dim3(ceil_div(np - npeeled, 256)), dim3(256), 0, 0, dpe.as<uint32_t>(),
-                               npeeled, np, dkeys.as<uint64_t>(), P, ddeg.as<uint32_t>(), dxr.as<uint32_t>(),
+                               npeeled, np, dkeys.as<uint64_t>(), P, ddx.as<unsigned long long>(),
                                nxt->as<uint32_t>(), cnt + (1 - fcur));
             SKM_HIP(hipGetLastError());
             rounds.push_back(np);
@@ -1737,8 +1779,7 @@ extern "C" int skm_mph_build_device_ex(const uint64_t* keys, const skm_stored_km
     SKM_CHECK(ok, SKM_E_ARG, "BDZ construction failed: no acyclic 3-graph in 1000 attempts");
     st.peel_rounds = (uint32_t)rounds.size() - 1;
     st.n_vertices = h.n;
-    ddeg.release();
-    dxr.release();
+    ddx.release();
     dfr0.release();
     dfr1.release();
     st.peel_s = secs_since(t);
