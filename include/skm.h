@@ -212,7 +212,7 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   last pass, 1),
  *   "overflow_grid" / "split_grid" / "chain_grid" (persistent-grid sizes), "stream_priority"
  *   (1: the group-by stream at the highest priority), "chain_batches" (key-range passes: the
- *   stashed long chains leave in this many batches, 4) / "chain_streams" (over 1..4 streams, 1),
+ *   stashed long chains leave in this many batches, 2) / "chain_streams" (over 1..4 streams, 1),
  *   "work_buffer_elements" (capacity of the data-sized work buffers; tests force the
  *   grow-and-redo path with a small value; 0 = automatic), "poison_jobs" (tests: canary jobs in
  *   the stashed long-job list), "route_heavy_min" (one GPU, >= 4 key-range passes: k-mers with at
@@ -243,7 +243,14 @@ int skm_debug_transport_check(const skm_transport* tp, int rank, int world);
  *   "lane_streams" (their batches rotate over 1..4 streams, 1), "chain_queue" (1: chain waves take
  *   64-job blocks from a work queue instead of a fixed stride), "flag_bits" (1: signature flags
  *   kept as bits during the run, read before an atomic set; 0: a byte store per kept
- *   occurrence), "sub_target" (k_partition's target elements per level-2 sub-bucket; 0 = 1024),
+ *   occurrence), "sub_target" (k_partition's target elements per level-2 sub-bucket; 0 = 768),
+ *   "big_split" (tail_async: the two big-group size classes on two tail streams; 0),
+ *   "emit_group" (key-range passes emitted per residue scan: 0 = 4, or 1, 2, 4, 8, 16),
+ *   "tail_defer" (tail_async: a pass's tail issued after the next pass's scan kernels; 0),
+ *   "recs_rot" (tail_async: the passes alternate two element buffers, so a split does not wait
+ *   for the previous pass's tail; +16 B per element of the largest pass when it fits; 0),
+ *   "handoff_index_limit" / "handoff_max_chunk" (tests: force the hand-off's 64-bit indices /
+ *   small chunks),
  *   "diag" (diagnostics only, wrong results: skips of flag stores / the heavy sort / chain
  *   kernels / overflow entry classes).
  * Unknown names and out-of-range values return SKM_E_ARG. */
