@@ -9,6 +9,9 @@
 #include <algorithm>
 #include <atomic>
 #include <cctype>
+#include <cstdint>
+#include <functional>
+#include <iterator>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -458,26 +461,179 @@ std::string fmt_g(double v) {
 // ---------------------------------------------------------------------------------------------
 // FunctionMap
 // ---------------------------------------------------------------------------------------------
-void FunctionMap::load_id_assignments(const std::string& path) {
-    std::ifstream f(path);
-    std::string line;
-    int lineno = 0;
-    while (std::getline(f, line)) {
-        lineno++;
-        size_t s = line.find('\t');
-        if (s == std::string::npos) {
-            std::cerr << "bad line " << lineno << " in file \"" << path << "\"\n";
-            continue;
+namespace {
+// one definition line's fields (load_id_assignments)
+struct IdLine {
+    std::string id, func, stripped;
+    bool bad = false, truncated = false;
+};
+void parse_id_line(const char* b, const char* e, IdLine& x) {
+    const std::string line(b, e);
+    const size_t s = line.find('\t');
+    if (s == std::string::npos) {
+        x.bad = true;
+        return;
+    }
+    const size_t s2 = line.find('\t', s + 1);
+    x.id = line.substr(0, s);
+    x.func = s2 == std::string::npos ? line.substr(s + 1) : line.substr(s + 1, s2 - s - 1);
+    std::string delim, comment;
+    split_func_comment(x.func, x.stripped, delim, comment);
+    x.truncated = delim == "#" && is_truncated_comment(comment);
+}
+// f(0..n-1) on up to `threads` std::threads (the caller's included)
+void par_for(int n, int threads, const std::function<void(int)>& f) {
+    std::vector<std::thread> th;
+    std::atomic<int> next{0};
+    auto work = [&] {
+        for (int i; (i = next.fetch_add(1)) < n;) f(i);
+    };
+    for (int t = 1; t < std::min(threads, n); ++t) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+}
+}  // namespace
+
+void FunctionMap::load_id_assignments(const std::string& path, int threads) {
+    load_id_assignments(std::vector<std::string>{path}, threads);
+}
+
+void FunctionMap::load_id_assignments(const std::vector<std::string>& paths, int threads) {
+    // every file's lines, split as std::getline returns them ('\n'; a last line without one
+    // included) and parsed on the host threads, file by file
+    std::vector<std::vector<IdLine>> lines(paths.size());
+    par_for((int)paths.size(), std::max(1, threads), [&](int fi) {
+        std::ifstream f(paths[(size_t)fi], std::ios::binary);
+        if (!f) return;
+        const std::string buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        std::vector<IdLine>& out = lines[(size_t)fi];
+        for (size_t p = 0; p < buf.size();) {
+            const size_t q = buf.find('\n', p);
+            const size_t e = q == std::string::npos ? buf.size() : q;
+            out.emplace_back();
+            parse_id_line(buf.data() + p, buf.data() + e, out.back());
+            p = q == std::string::npos ? buf.size() : q + 1;
         }
-        size_t s2 = line.find('\t', s + 1);
-        std::string id = line.substr(0, s);
-        std::string func = s2 == std::string::npos ? line.substr(s + 1) : line.substr(s + 1, s2 - s - 1);
-        std::string stripped, delim, comment;
-        split_func_comment(func, stripped, delim, comment);
-        original_assignment_stripped_[id] = stripped;
-        original_assignment_[id] = func;
-        if (delim == "#" && is_truncated_comment(comment)) continue;
-        id_function_map_[id] = stripped;
+    });
+    size_t n = 0;
+    for (size_t fi = 0; fi < paths.size(); ++fi) {
+        n += lines[fi].size();
+        for (size_t i = 0; i < lines[fi].size(); ++i)
+            if (lines[fi][i].bad) std::cerr << "bad line " << i + 1 << " in file \"" << paths[fi] << "\"\n";
+    }
+    // the three tables are independent: one thread each, every one in file and line order (a
+    // later assignment of an id replaces an earlier one, as operator[] = does)
+    par_for(3, threads > 1 ? 3 : 1, [&](int k) {
+        auto& tab = k == 0 ? original_assignment_stripped_ : k == 1 ? original_assignment_ : id_function_map_;
+        tab.reserve(tab.size() + n);
+        for (const auto& fl : lines)
+            for (const IdLine& x : fl) {
+                if (x.bad) continue;
+                if (k == 0) tab[x.id] = x.stripped;
+                if (k == 1) tab[x.id] = x.func;
+                if (k == 2 && !x.truncated) tab[x.id] = x.stripped;
+            }
+    });
+}
+
+void FunctionMap::load_fasta_files(const std::vector<FastaFile>& files, const std::set<std::string>& deleted_fids,
+                                   int threads) {
+    // per file: the kept records' (index, function before the id table) and the file's genome --
+    // set by its first record that passes the checks and never changed after (load_fasta_file)
+    struct FileRecs {
+        std::vector<uint32_t> rec;
+        std::vector<std::string> func;
+        std::string genome, msg;
+        size_t bad = SIZE_MAX;  // the first blank definition line (load_fasta_file throws there)
+    };
+    std::vector<FileRecs> out(files.size());
+    par_for((int)files.size(), std::max(1, threads), [&](int fi) {
+        const FastaFile& f = files[(size_t)fi];
+        FileRecs& o = out[(size_t)fi];
+        o.rec.reserve(f.size());
+        o.func.reserve(f.size());
+        std::string genome;
+        for (size_t r = 0; r < f.size(); ++r) {
+            const std::string& id = f.ids[r];
+            const std::string& def = f.defs[r];
+            if (deleted_fids.count(id)) continue;
+            std::string func;
+            if (!def.empty()) {
+                const size_t x = def.find_first_not_of(" \t");
+                if (x == std::string::npos) {
+                    o.bad = r;
+                    break;
+                }
+                func = def.substr(x);
+            }
+            std::string genome_loc, fpart, g;
+            if (match_genome_defline(def, fpart, g)) {
+                std::string delim, comment;
+                split_func_comment(fpart, func, delim, comment);
+                if (delim == "#" && is_truncated_comment(comment)) continue;
+                genome_loc = g;
+            }
+            if (genome.empty()) {
+                if (def.empty())
+                    search_fig_genome(id, genome);
+                else if (!genome_loc.empty())
+                    genome = genome_loc;
+            }
+            if (genome.empty()) {
+                genome = f.filename;
+                if (!match_genome_id(genome)) o.msg += "cannot determine genome from file \"" + f.path + "\"\n";
+            }
+            o.rec.push_back((uint32_t)r);
+            o.func.push_back(std::move(func));
+        }
+        o.genome = genome;
+    });
+    size_t total = 0;
+    for (const auto& o : out) total += o.rec.size();
+    id_function_map_.reserve(id_function_map_.size() + total);
+    // the ids' table entries found on the host threads (no writer yet; the entries an insert adds
+    // below do not move the others); the ones not found are added in record order below
+    std::vector<std::vector<std::string*>> cur_of(files.size());
+    par_for((int)files.size(), std::max(1, threads), [&](int fi) {
+        const FileRecs& o = out[(size_t)fi];
+        auto& c = cur_of[(size_t)fi];
+        c.resize(o.rec.size());
+        for (size_t k = 0; k < o.rec.size(); ++k) {
+            auto it = id_function_map_.find(files[(size_t)fi].ids[o.rec[k]]);
+            c[k] = it == id_function_map_.end() ? nullptr : &it->second;
+        }
+    });
+    // the function tables' entries of each function name, found once (std::map nodes are stable),
+    // and the genome last added to its set (an equal insert is a no-op)
+    struct FuncRef {
+        std::set<std::string>* genomes;
+        FloatStats* acc;
+        const std::string* last;
+    };
+    std::unordered_map<std::string, FuncRef> fref;
+    for (size_t fi = 0; fi < files.size(); ++fi) {
+        const FastaFile& f = files[fi];
+        FileRecs& o = out[fi];
+        std::cerr << o.msg;
+        for (size_t k = 0; k < o.rec.size(); ++k) {
+            const uint32_t r = o.rec[k];
+            std::string& func = o.func[k];
+            std::string& cur = cur_of[fi][k] ? *cur_of[fi][k] : id_function_map_[f.ids[r]];
+            if (cur.empty()) {
+                if (!func.empty()) cur = func;
+            } else {
+                func = cur;
+            }
+            if (func.empty()) continue;
+            auto it = fref.find(func);
+            if (it == fref.end())
+                it = fref.emplace(func, FuncRef{&function_genome_map_[func], &function_accumulators_[func], nullptr}).first;
+            FuncRef& x = it->second;
+            if (!x.last || *x.last != o.genome) x.last = &*x.genomes->insert(o.genome).first;
+            x.acc->add((float)f.len[r]);
+        }
+        if (o.bad != SIZE_MAX)
+            throw std::out_of_range("blank definition line for " + f.ids[o.bad] + " in " + f.path);
     }
 }
 

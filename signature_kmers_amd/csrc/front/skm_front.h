@@ -77,11 +77,17 @@ class FunctionMap {
 public:
     void add_good_functions(const std::vector<std::string>& v) { good_functions_.insert(v.begin(), v.end()); }
     void add_good_roles(const std::vector<std::string>& v) { good_roles_.insert(v.begin(), v.end()); }
-    // function_map.h:62-104
-    void load_id_assignments(const std::string& path);
+    // function_map.h:62-104.  threads > 1: the lines are split on that many host threads, then
+    // the three tables are filled in line order, one thread per table (same tables, same messages)
+    void load_id_assignments(const std::string& path, int threads = 1);
+    void load_id_assignments(const std::vector<std::string>& paths, int threads);  // in path order
     // function_map.h:119-238 over an already parsed file (keep flag: signature_build.tcc:32
     // always passes false)
     void load_fasta_file(const FastaFile& f, const std::set<std::string>& deleted_fids);
+    // load_fasta_file over every file in order, the per-record parsing (definition line, function /
+    // comment split, the file's genome) on `threads` host threads and the table updates in record
+    // order on the caller's: the same tables, messages and first exception as the loop
+    void load_fasta_files(const std::vector<FastaFile>& files, const std::set<std::string>& deleted_fids, int threads);
     // function_map.h:257-332; returns the number of kept functions ("kept N functions")
     unsigned process_kept_functions(int min_reps_required, const std::set<std::string>& ignored);
     // function_map.h:389-411

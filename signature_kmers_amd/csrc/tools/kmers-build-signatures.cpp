@@ -268,12 +268,16 @@ int main(int argc, char** argv) {
     double t0 = now_s();
     bool parsed_ok = true;
     std::string parse_err;
-    std::thread parser([&] { parsed_ok = parse_fasta_files(all_paths, files, n_threads, parse_err, &keep_res); });
+    double t_files = 0;  // the parser thread's own time
+    std::thread parser([&] {
+        parsed_ok = parse_fasta_files(all_paths, files, n_threads, parse_err, &keep_res);
+        t_files = now_s() - t0;
+    });
     const double td = now_s();
     FunctionMap fm;
     fm.add_good_roles(good_roles);
     fm.add_good_functions(good_functions);
-    for (auto& d : definition_files) fm.load_id_assignments(d);
+    fm.load_id_assignments(definition_files, n_threads);
     const double t_defs = now_s() - td;
 
     std::set<std::string> deleted_fids, ignored_functions;
@@ -286,12 +290,13 @@ int main(int argc, char** argv) {
 
     parser.join();
     if (!parsed_ok) die(parse_err);
+    const double t_fm0 = now_s();
     try {
-        for (auto& f : files) fm.load_fasta_file(f, deleted_fids);
+        fm.load_fasta_files(files, deleted_fids, n_threads);
     } catch (const std::exception& e) {
         die(std::string("terminate called after throwing an instance of 'std::out_of_range': ") + e.what());
     }
-    const double t_parse = now_s() - t0;
+    const double t_parse = now_s() - t0, t_fm = now_s() - t_fm0;
 
     unsigned nkept_f = fm.process_kept_functions(min_reps_required, ignored_functions);
     std::cout << "kept " << nkept_f << " functions\n";
@@ -332,6 +337,8 @@ int main(int argc, char** argv) {
         if (rank != 0) return 0;
         dump_extract(op.get("dump-extract"), files, batches);
         std::cerr << "wrote build input to " << op.get("dump-extract") << "\n";
+        std::cerr << "phases: parse " << t_parse << " parse_files " << t_files << " defs " << t_defs << " fm_load " << t_fm
+                  << "\n";
         if (!mesh.wait_children(err)) die(err);
         return 0;
     }
@@ -517,7 +524,8 @@ int main(int argc, char** argv) {
     std::cerr << "phases: parse " << t_parse << " add " << t_add << " prepare " << t_prepare << " run " << t_run
               << " finish " << t_finish << " final_kmers " << t_final_kmers << " mph " << t_mph << " recall "
               << t_recall << " recall_device " << t_recall_dev << " total " << now_s() - t_start << " startup "
-              << t_startup << " defs " << t_defs << " hip_init " << t_hip_init << " create " << t_create << "\n";
+              << t_startup << " defs " << t_defs << " hip_init " << t_hip_init << " create " << t_create
+              << " parse_files " << t_files << " fm_load " << t_fm << "\n";
     std::cerr << "all done\n";
     fast_exit(0);  // every output file is closed by now
 }

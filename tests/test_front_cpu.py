@@ -138,3 +138,29 @@ def test_front_end_synthetic_layout_matches_generator(tools, tmp_path):
     last = p.residues[(p.seq_off + p.seq_len - 1).astype(np.int64)]
     lost = int(((p.seq_len % 60 == 1) & (last == ord("*"))).sum())
     assert int(ln.astype(np.int64).sum()) == int(p.seq_len.astype(np.int64).sum()) - lost
+
+
+def test_definition_bad_lines_reported_in_order(tools, tmp_path):
+    """load_id_assignments (function_map.h:62-104) parses the definition files on host threads:
+    lines without a tab -- an empty line and a last line without a newline included -- are reported
+    as "bad line N" with getline's numbering, in line order within a file (the files in directory
+    listing order, as before), and the assignments of the good lines still apply."""
+    defs = tmp_path / "defs"
+    seqs = tmp_path / "seqs"
+    defs.mkdir()
+    seqs.mkdir()
+    (defs / "a").write_bytes(b"fig|1.1.peg.1\talpha protein\nnotab line\n\nfig|1.1.peg.2\tbeta protein # note\nlast")
+    (defs / "b").write_bytes(b"fig|1.1.peg.3\tgamma protein\n\n")
+    (seqs / "1.1").write_bytes(b">fig|1.1.peg.1\nMKVLAAGIVGLLLAWQ\n>fig|1.1.peg.2\nMKTAYIAKQRQISFVK\n"
+                               b">fig|1.1.peg.3\nMSTNPKPQRKTKRNTNRR\n")
+    out = tmp_path / "out"
+    cmd = [os.path.join(tools, "kmers-build-signatures"), "-D", str(defs), "-F", str(seqs), "--kmer-data-dir", str(out),
+           "--min-reps-required", "1", "--dump-extract", str(out / "extract.bin")]
+    p = subprocess.run(cmd, capture_output=True, check=True)
+    bad = [ln for ln in p.stderr.decode().splitlines() if ln.startswith("bad line")]
+    in_a = [ln for ln in bad if ln.endswith(f'"{defs / "a"}"')]
+    assert in_a == [f'bad line 2 in file "{defs / "a"}"', f'bad line 3 in file "{defs / "a"}"',
+                    f'bad line 5 in file "{defs / "a"}"']
+    assert [ln for ln in bad if ln not in in_a] == [f'bad line 2 in file "{defs / "b"}"']
+    names = {ln.split(b"\t")[1] for ln in (out / "function.index").read_bytes().splitlines()}
+    assert {b"alpha protein", b"beta protein", b"gamma protein"} <= names

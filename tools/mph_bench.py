@@ -29,3 +29,6 @@ for n in a.n:
         skm.mph_build(keys, data, f"{a.out}/h.mph", f"{a.out}/h.dat", seed=1)
         th = time.time() - t
     print(f"n={len(keys)} device {td:.2f} s" + (f", host {th:.2f} s" if th else ""), flush=True)
+    st = skm.mph_build_device(keys, data, f"{a.out}/e.mph", f"{a.out}/e.dat", seed=1, device=0, verify=False)
+    print("  skm_mph_build_device_ex phases (s):", {k: round(v, 3) if isinstance(v, float) else v for k, v in st.items()},
+          flush=True)
