@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cstring>
 #include <fstream>
+#include <memory>
 #include <mutex>
 #include <thread>
 
@@ -75,46 +76,38 @@ bool annot_opts_for(const std::vector<std::string>& function_index, bool ignore_
 int annotate_batch(skm_db* db, const std::vector<const FastaFile*>& files, const skm_annot_opts& o, int n_threads,
                    skm_calls* calls, std::string& err) {
     *calls = skm_calls{};
-    uint64_t nres = 0, nseq = 0;
-    for (auto* f : files) {
-        nres += f->residues.size();
-        nseq += f->size();
+    // the batch packed as skm_annotate lays it out on the device (every sequence followed by a 0,
+    // back to back), so the library uploads it as it is instead of packing a second copy; files
+    // are copied by the host threads
+    std::vector<uint64_t> rbase(files.size() + 1, 0), sbase(files.size() + 1, 0);
+    for (size_t f = 0; f < files.size(); ++f) {
+        uint64_t nb = 0;
+        for (size_t r = 0; r < files[f]->size(); ++r) nb += (uint64_t)files[f]->len[r] + 1;
+        rbase[f + 1] = rbase[f] + nb;
+        sbase[f + 1] = sbase[f] + files[f]->size();
     }
-    std::vector<uint8_t> res;
-    std::vector<uint64_t> off;
-    std::vector<uint32_t> len;
-    const uint8_t* rp = nullptr;
-    if (files.size() == 1) {  // single file: its buffer directly
-        rp = files[0]->residues.data();
-        off = files[0]->off;
-        len = files[0]->len;
-    } else if (!files.empty()) {  // the batch's files side by side, copied by the host threads
-        std::vector<uint64_t> rbase(files.size() + 1, 0), sbase(files.size() + 1, 0);
-        for (size_t f = 0; f < files.size(); ++f) {
-            rbase[f + 1] = rbase[f] + files[f]->residues.size();
-            sbase[f + 1] = sbase[f] + files[f]->size();
-        }
-        res.resize(nres);
-        off.resize(nseq);
-        len.resize(nseq);
-        std::atomic<size_t> nextf{0};
-        auto cp = [&]() {
-            for (size_t f; (f = nextf.fetch_add(1)) < files.size();) {
-                const FastaFile& F = *files[f];
-                std::memcpy(res.data() + rbase[f], F.residues.data(), F.residues.size());
-                for (size_t r = 0; r < F.size(); ++r) {
-                    off[sbase[f] + r] = rbase[f] + F.off[r];
-                    len[sbase[f] + r] = F.len[r];
-                }
+    std::unique_ptr<uint8_t[]> res(new uint8_t[std::max<uint64_t>(rbase.back(), 1)]);
+    std::vector<uint64_t> off(sbase.back());
+    std::vector<uint32_t> len(sbase.back());
+    std::atomic<size_t> nextf{0};
+    auto cp = [&]() {
+        for (size_t f; (f = nextf.fetch_add(1)) < files.size();) {
+            const FastaFile& F = *files[f];
+            uint64_t p = rbase[f];
+            for (size_t r = 0; r < F.size(); ++r) {
+                std::memcpy(res.get() + p, F.residues.data() + F.off[r], F.len[r]);
+                res[p + F.len[r]] = 0;
+                off[sbase[f] + r] = p;
+                len[sbase[f] + r] = F.len[r];
+                p += (uint64_t)F.len[r] + 1;
             }
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < std::max(1, std::min<int>(n_threads, (int)files.size())); ++t) th.emplace_back(cp);
-        cp();
-        for (auto& t : th) t.join();
-        rp = res.data();
-    }
-    const int rc = skm_annotate(db, rp, off.data(), len.data(), off.size(), &o, calls);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < std::max(1, std::min<int>(n_threads, (int)files.size())); ++t) th.emplace_back(cp);
+    cp();
+    for (auto& t : th) t.join();
+    const int rc = skm_annotate(db, res.get(), off.data(), len.data(), off.size(), &o, calls);
     if (rc) err = skm_last_error();
     return rc;
 }

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -898,6 +899,24 @@ void Scanner::run(const uint32_t* in, uint64_t n, uint64_t* out, hipStream_t st)
     SKM_HIP(hipGetLastError());
 }
 
+// fm[i] = function_index << 16 | mean of .dat record i (u16 words 1 and 2 of its 10 bytes): the 4
+// aligned bytes the call path reads per hit (one gather instead of two 2-byte loads)
+__global__ void k_dat_fm(const uint16_t* __restrict__ dat, uint64_t n, uint32_t* __restrict__ fm) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fm[i] = ((uint32_t)dat[5 * i + 1] << 16) | (uint32_t)dat[5 * i + 2];
+}
+
+// the 0 after every query sequence of a batch uploaded as the caller packed it
+__global__ void k_zero_seps(const QMeta* __restrict__ meta, uint32_t n, uint8_t* __restrict__ res) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < n) res[meta[s].pstart + meta[s].len] = 0;
+}
+
+// the b == 7 (g word, rank) pair lines from g and the rank table (defined with the BDZ builder)
+__global__ void k_mph_blk(const uint32_t* __restrict__ g, uint64_t gwords, const uint32_t* __restrict__ rank,
+                          uint64_t nrank, uint64_t nblk, uint32_t* __restrict__ blk);
+
 }  // namespace skm
 
 using namespace skm;
@@ -914,24 +933,10 @@ struct skm_query {
     Scanner scan;
     uint64_t n_calls = 0;
     bool ran = false;
+    std::unique_ptr<HostPool> pool;  // packs the residues (created on first use)
 };
 
 namespace {
-
-// fm[i] = function_index << 16 | mean of record i: the 4 aligned bytes the call path reads per hit
-// (one gather instead of two 2-byte loads from the 10-byte records)
-void upload_fm(skm_db* db, const uint8_t* dat, uint64_t nrec) {
-    std::vector<uint32_t> fm(std::max<uint64_t>(nrec, 1), 0u);
-    for (uint64_t i = 0; i < nrec; ++i) {
-        uint16_t f, mn;
-        std::memcpy(&f, dat + 10 * i + 2, 2);
-        std::memcpy(&mn, dat + 10 * i + 4, 2);
-        fm[i] = ((uint32_t)f << 16) | (uint32_t)mn;
-    }
-    db->d_fm.ensure(4 * fm.size());
-    SKM_HIP(hipMemcpy(db->d_fm.p, fm.data(), 4 * fm.size(), hipMemcpyHostToDevice));
-    db->dev.fm = db->d_fm.as<uint32_t>();
-}
 
 void db_upload(skm_db* db, const uint8_t* dat, size_t dat_len) {
     SKM_HIP(hipSetDevice(db->device));
@@ -958,29 +963,28 @@ void db_upload(skm_db* db, const uint8_t* dat, size_t dat_len) {
     D.seed = h.seed;
     D.r_magic = h.r ? (~0ull / h.r + 1) : 0;
     db->m = h.m;
-    upload_fm(db, dat, dat_len / 10);
-    // b == 7: g and the rank table interleaved, one 64-byte line per 128 vertices
+    // the record words from the uploaded records, on the device
+    const uint64_t nrec = dat_len / 10;
+    db->d_fm.ensure(4 * std::max<uint64_t>(nrec, 1));
+    if (nrec)
+        hipLaunchKernelGGL(k_dat_fm, dim3((uint32_t)ceil_div(nrec, 256)), dim3(256), 0, 0, db->d_dat.as<uint16_t>(), nrec,
+                           db->d_fm.as<uint32_t>());
+    D.fm = db->d_fm.as<uint32_t>();
+    // b == 7: g and the rank table interleaved, one 64-byte line per 128 vertices -- pairs (g word
+    // w, rank of its first vertex = rank table entry plus the assigned vertices of the words before
+    // it), so one 8-byte load gives a vertex's g value and rank; built on the device from the
+    // uploaded g (padded with 0xFF) and rank table
     D.blk = nullptr;
     if (h.b == 7) {
         const uint64_t nblk = (uint64_t)h.n / 128 + 2;
-        std::vector<uint32_t> blk(16 * nblk, 0);
-        const uint32_t* gw = reinterpret_cast<const uint32_t*>(g.data());  // padded with 0xFF
-        for (uint64_t q = 0; q < nblk; ++q) {
-            // pairs (g word w, rank of its first vertex = rank table entry plus the assigned
-            // vertices of the words before it): one 8-byte load gives a vertex's g value and rank
-            uint32_t r = q < h.ranktable.size() ? h.ranktable[q] : 0u;
-            for (int w = 0; w < 8; ++w) {
-                const uint64_t gi = 8 * q + (uint64_t)w;
-                const uint32_t x = 4 * gi + 4 <= g.size() ? gw[gi] : 0xFFFFFFFFu;
-                blk[16 * q + 2 * (uint64_t)w] = x;
-                blk[16 * q + 2 * (uint64_t)w + 1] = r;
-                r += 16u - (uint32_t)__builtin_popcount(x & (x >> 1) & 0x55555555u);
-            }
-        }
-        db->d_blk.ensure(4 * blk.size());
-        SKM_HIP(hipMemcpy(db->d_blk.p, blk.data(), 4 * blk.size(), hipMemcpyHostToDevice));
+        db->d_blk.ensure(64 * nblk);
+        hipLaunchKernelGGL(k_mph_blk, dim3((uint32_t)ceil_div(nblk, 256)), dim3(256), 0, 0, db->d_g.as<uint32_t>(),
+                           (uint64_t)(gbytes / 4), db->d_rank.as<uint32_t>(), (uint64_t)h.ranktable.size(), nblk,
+                           db->d_blk.as<uint32_t>());
         D.blk = db->d_blk.as<uint32_t>();
     }
+    SKM_HIP(hipGetLastError());
+    SKM_HIP(hipDeviceSynchronize());
 }
 
 void db_upload_kept(skm_db* db, const uint64_t* keys, const skm_stored_kmer_data* data, size_t n) {
@@ -1029,6 +1033,40 @@ bool read_file(const char* path, std::vector<uint8_t>& out) {
     out.resize((size_t)n);
     if (n) f.read((char*)out.data(), n);
     return (bool)f;
+}
+
+// a whole file into an uninitialised buffer, read by a few threads with pread (the C2 DB's .dat is
+// 1.7 GB: one zero-filled vector and one stream read took half of skm_db_open)
+bool read_file_par(const char* path, std::unique_ptr<uint8_t[]>& out, uint64_t& n) {
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) return false;
+    struct stat sb;
+    if (::fstat(fd, &sb) != 0) {
+        ::close(fd);
+        return false;
+    }
+    n = (uint64_t)sb.st_size;
+    out.reset(new uint8_t[std::max<uint64_t>(n, 1)]);
+    const uint64_t piece = std::max<uint64_t>(64ull << 20, (n + 7) / 8);
+    const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, (n + piece - 1) / piece));
+    std::atomic<bool> ok{true};
+    auto part = [&](int t) {
+        const uint64_t a = (uint64_t)t * piece, b = std::min(n, a + piece);
+        for (uint64_t o = a; o < b;) {
+            const ssize_t r = ::pread(fd, out.get() + o, (size_t)std::min<uint64_t>(b - o, 1ull << 30), (off_t)o);
+            if (r <= 0) {
+                ok = false;
+                return;
+            }
+            o += (uint64_t)r;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(part, t);
+    part(0);
+    for (auto& x : th) x.join();
+    ::close(fd);
+    return ok.load();
 }
 
 void query_run(skm_query* q, const skm_annot_opts* o) {
@@ -1149,10 +1187,12 @@ int skm_db_open_mem(skm_db** out, const uint8_t* mph, size_t mph_len, const uint
 int skm_db_open(skm_db** out, const char* mph_path, const char* dat_path, int device) {
     SKM_API_BEGIN
     SKM_CHECK(out && mph_path && dat_path, SKM_E_ARG, "null argument");
-    std::vector<uint8_t> mph, dat;
+    std::vector<uint8_t> mph;
+    std::unique_ptr<uint8_t[]> dat;
+    uint64_t dat_len = 0;
     SKM_CHECK(read_file(mph_path, mph), SKM_E_IO, std::string("cannot read ") + mph_path);
-    SKM_CHECK(read_file(dat_path, dat), SKM_E_IO, std::string("cannot read ") + dat_path);
-    int rc = skm_db_open_mem(out, mph.data(), mph.size(), dat.data(), dat.size(), device);
+    SKM_CHECK(read_file_par(dat_path, dat, dat_len), SKM_E_IO, std::string("cannot read ") + dat_path);
+    int rc = skm_db_open_mem(out, mph.data(), mph.size(), dat.get(), dat_len, device);
     if (rc) return rc;
     SKM_API_END
 }
@@ -1224,7 +1264,11 @@ int skm_debug_db_lookup_generic(skm_db* db, const uint64_t* keys, size_t n, uint
     return db_lookup(db, keys, n, idx_out, true);
 }
 
-void skm_db_close(skm_db* db) { delete db; }
+void skm_db_close(skm_db* db) {
+    if (!db) return;
+    skm_query_destroy(db->aq);
+    delete db;
+}
 
 int skm_mph_build(const uint64_t* keys, const skm_stored_kmer_data* data, size_t n, uint32_t seed, const char* mph_path,
                   const char* dat_path) {
@@ -1254,71 +1298,100 @@ int skm_mph_build(const uint64_t* keys, const skm_stored_kmer_data* data, size_t
     SKM_API_END
 }
 
+namespace {
+// (Re)loads a query object with a batch of sequences: the packed residues (one 0 after each
+// sequence) and the per-sequence tables on the device; the buffers only grow, so a reused query
+// (skm_annotate's, one per DB) allocates nothing once it has seen its largest batch.  Input that is
+// already packed (sequence s at sum_{t<s} (len_t + 1), a 0 after each) is uploaded as it is.
+void query_setup(skm_query* q, const uint8_t* residues, const uint64_t* seq_off, const uint32_t* seq_len,
+                 size_t n_seqs) {
+    SKM_HIP(hipSetDevice(q->db->device));
+    if (!q->stream) {
+        SKM_HIP(hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking));
+        for (auto& e : q->ev) SKM_HIP(hipEventCreate(&e));
+    }
+    q->ran = false;
+    q->n_calls = 0;
+    std::vector<QMeta> meta(n_seqs);
+    std::vector<uint64_t> scr_off(n_seqs);
+    uint64_t total = 0, nwin_tot = 0;
+    // packed offsets: the caller's bytes [0, max_end) -- which hold every sequence, so the buffer
+    // spans them -- go to the device as they are, and the separators are zeroed there (no byte
+    // outside a sequence is relied on)
+    bool packed = true;
+    uint64_t max_end = 0;
+    for (size_t s = 0; s < n_seqs; ++s) {
+        meta[s].pstart = total;
+        meta[s].len = seq_len[s];
+        meta[s].pad = 0;
+        packed = packed && seq_off[s] == total;
+        if (seq_len[s]) max_end = std::max<uint64_t>(max_end, seq_off[s] + seq_len[s]);
+        total += (uint64_t)seq_len[s] + 1;
+        scr_off[s] = nwin_tot;
+        nwin_tot += seq_len[s] >= 8 ? seq_len[s] - 7 : 0;
+    }
+    // otherwise the packed residues, copied by the host pool in byte-balanced sequence ranges
+    // (10 M queries are ~3 GB)
+    std::vector<uint8_t> res;
+    const uint8_t* src = residues;
+    if (!packed) {
+        res.resize(total);
+        if (!q->pool) q->pool.reset(new HostPool(n_seqs > 4096 ? HostPool::default_threads() : 1));
+        const int parts = std::max(1, std::min<int>(4 * q->pool->threads(), (int)(total >> 20)));
+        q->pool->run(parts, [&](int p) {
+            const uint64_t lo = total * (uint64_t)p / (uint64_t)parts, hi = total * (uint64_t)(p + 1) / (uint64_t)parts;
+            auto first_at = [&](uint64_t x) {  // first sequence starting at or after byte x
+                size_t a = 0, e = n_seqs;
+                while (a < e) {
+                    const size_t mid = (a + e) / 2;
+                    if (meta[mid].pstart < x) a = mid + 1; else e = mid;
+                }
+                return a;
+            };
+            for (size_t s = first_at(lo), e = first_at(hi); s < e; ++s) {
+                std::memcpy(res.data() + meta[s].pstart, residues + seq_off[s], seq_len[s]);
+                res[meta[s].pstart + seq_len[s]] = 0;
+            }
+        });
+        src = res.data();
+    }
+    q->nseq = (uint32_t)n_seqs;
+    q->rp = total;
+    q->n_windows = nwin_tot;
+    // hits are written in 16-window groups: pad to a multiple of 16 positions
+    const uint64_t rp_pad = ceil_div(q->rp + 1, LK_POS) * LK_POS;
+    q->d_res.ensure(rp_pad + 64);
+    const uint64_t body = packed ? max_end : q->rp;
+    SKM_HIP(hipMemsetAsync(q->d_res.as<uint8_t>() + body, 0, rp_pad + 64 - body, q->stream));
+    if (body) SKM_HIP(hipMemcpyAsync(q->d_res.p, src, body, hipMemcpyHostToDevice, q->stream));
+    q->d_meta.ensure(sizeof(QMeta) * std::max<size_t>(n_seqs, 1));
+    if (n_seqs) SKM_HIP(hipMemcpyAsync(q->d_meta.p, meta.data(), sizeof(QMeta) * n_seqs, hipMemcpyHostToDevice, q->stream));
+    if (packed && n_seqs)
+        hipLaunchKernelGGL(k_zero_seps, dim3((uint32_t)ceil_div(n_seqs, 256)), dim3(256), 0, q->stream,
+                           q->d_meta.as<QMeta>(), (uint32_t)n_seqs, q->d_res.as<uint8_t>());
+    q->d_hits.ensure(4 * (rp_pad + 16));
+    q->d_scr.ensure(2 * std::max<uint64_t>(nwin_tot, 1));
+    q->d_scr_off.ensure(8 * std::max<size_t>(n_seqs, 1));
+    if (n_seqs) SKM_HIP(hipMemcpyAsync(q->d_scr_off.p, scr_off.data(), 8 * n_seqs, hipMemcpyHostToDevice, q->stream));
+    q->d_caps.ensure(4 * std::max<size_t>(n_seqs, 1));
+    q->d_cap_off.ensure(8 * (n_seqs + 1));
+    q->d_counts.ensure(4 * std::max<size_t>(n_seqs, 1));
+    q->d_call_off.ensure(8 * (n_seqs + 1));
+    q->d_seg_off.ensure(8 * (n_seqs + 1));
+    SKM_HIP(hipStreamSynchronize(q->stream));  // the host arrays above go out of scope
+}
+}  // namespace
+
 int skm_query_create(skm_query** out, skm_db* db, const uint8_t* residues, const uint64_t* seq_off,
                      const uint32_t* seq_len, size_t n_seqs) {
     SKM_API_BEGIN
     SKM_CHECK(out && db, SKM_E_ARG, "null argument");
     SKM_CHECK(n_seqs == 0 || (residues && seq_off && seq_len), SKM_E_ARG, "null array");
     SKM_CHECK(n_seqs < 0xFFFFFFFFull, SKM_E_ARG, "too many query sequences in one batch");
-    SKM_HIP(hipSetDevice(db->device));
     auto* q = new skm_query();
     q->db = db;
     try {
-        SKM_HIP(hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking));
-        for (auto& e : q->ev) SKM_HIP(hipEventCreate(&e));
-        std::vector<QMeta> meta(n_seqs);
-        std::vector<uint64_t> scr_off(n_seqs);
-        uint64_t total = 0, nwin_tot = 0;
-        for (size_t s = 0; s < n_seqs; ++s) {
-            meta[s].pstart = total;
-            meta[s].len = seq_len[s];
-            meta[s].pad = 0;
-            total += (uint64_t)seq_len[s] + 1;
-            scr_off[s] = nwin_tot;
-            nwin_tot += seq_len[s] >= 8 ? seq_len[s] - 7 : 0;
-        }
-        // the packed residues (one 0 after each sequence), copied by the host pool in
-        // byte-balanced sequence ranges (10 M queries are ~3 GB)
-        std::vector<uint8_t> res(total);
-        {
-            HostPool pool(n_seqs > 4096 ? HostPool::default_threads() : 1);
-            const int parts = std::max(1, std::min<int>(4 * pool.threads(), (int)(total >> 20)));
-            pool.run(parts, [&](int p) {
-                const uint64_t lo = total * (uint64_t)p / (uint64_t)parts, hi = total * (uint64_t)(p + 1) / (uint64_t)parts;
-                auto first_at = [&](uint64_t x) {  // first sequence starting at or after byte x
-                    size_t a = 0, e = n_seqs;
-                    while (a < e) {
-                        const size_t mid = (a + e) / 2;
-                        if (meta[mid].pstart < x) a = mid + 1; else e = mid;
-                    }
-                    return a;
-                };
-                for (size_t s = first_at(lo), e = first_at(hi); s < e; ++s) {
-                    std::memcpy(res.data() + meta[s].pstart, residues + seq_off[s], seq_len[s]);
-                    res[meta[s].pstart + seq_len[s]] = 0;
-                }
-            });
-        }
-        q->nseq = (uint32_t)n_seqs;
-        q->rp = res.size();
-        q->n_windows = nwin_tot;
-        // hits are written in 16-window groups: pad to a multiple of 16 positions
-        const uint64_t rp_pad = ceil_div(q->rp + 1, LK_POS) * LK_POS;
-        q->d_res.ensure(rp_pad + 64);
-        SKM_HIP(hipMemsetAsync(q->d_res.p, 0, rp_pad + 64, q->stream));
-        if (q->rp) SKM_HIP(hipMemcpyAsync(q->d_res.p, res.data(), q->rp, hipMemcpyHostToDevice, q->stream));
-        q->d_meta.ensure(sizeof(QMeta) * std::max<size_t>(n_seqs, 1));
-        if (n_seqs) SKM_HIP(hipMemcpyAsync(q->d_meta.p, meta.data(), sizeof(QMeta) * n_seqs, hipMemcpyHostToDevice, q->stream));
-        q->d_hits.ensure(4 * (rp_pad + 16));
-        q->d_scr.ensure(2 * std::max<uint64_t>(nwin_tot, 1));
-        q->d_scr_off.ensure(8 * std::max<size_t>(n_seqs, 1));
-        if (n_seqs) SKM_HIP(hipMemcpyAsync(q->d_scr_off.p, scr_off.data(), 8 * n_seqs, hipMemcpyHostToDevice, q->stream));
-        q->d_caps.ensure(4 * std::max<size_t>(n_seqs, 1));
-        q->d_cap_off.ensure(8 * (n_seqs + 1));
-        q->d_counts.ensure(4 * std::max<size_t>(n_seqs, 1));
-        q->d_call_off.ensure(8 * (n_seqs + 1));
-        q->d_seg_off.ensure(8 * (n_seqs + 1));
-        SKM_HIP(hipStreamSynchronize(q->stream));
+        query_setup(q, residues, seq_off, seq_len, n_seqs);
     } catch (...) {
         skm_query_destroy(q);
         throw;
@@ -1408,14 +1481,28 @@ void skm_query_destroy(skm_query* q) {
     delete q;
 }
 
+namespace {
+int annotate_setup(skm_db* db, const uint8_t* residues, const uint64_t* seq_off, const uint32_t* seq_len, size_t n_seqs) {
+    SKM_API_BEGIN
+    SKM_CHECK(db, SKM_E_ARG, "null argument");
+    SKM_CHECK(n_seqs == 0 || (residues && seq_off && seq_len), SKM_E_ARG, "null array");
+    SKM_CHECK(n_seqs < 0xFFFFFFFFull, SKM_E_ARG, "too many query sequences in one batch");
+    if (!db->aq) {
+        db->aq = new skm_query();
+        db->aq->db = db;
+    }
+    query_setup(db->aq, residues, seq_off, seq_len, n_seqs);
+    SKM_API_END
+}
+}  // namespace
+
+// one batch through the DB's own reused query (its device buffers, stream and host pool persist
+// from call to call: a batch of the annotate CLI used to create and free all of them)
 int skm_annotate(skm_db* db, const uint8_t* residues, const uint64_t* seq_off, const uint32_t* seq_len, size_t n_seqs,
                  const skm_annot_opts* opts, skm_calls* out) {
-    skm_query* q = nullptr;
-    int rc = skm_query_create(&q, db, residues, seq_off, seq_len, n_seqs);
-    if (rc) return rc;
-    rc = skm_query_run(q, opts);
-    if (!rc) rc = skm_query_calls(q, out);
-    skm_query_destroy(q);
+    int rc = annotate_setup(db, residues, seq_off, seq_len, n_seqs);
+    if (!rc) rc = skm_query_run(db->aq, opts);
+    if (!rc) rc = skm_query_calls(db->aq, out);
     return rc;
 }
 

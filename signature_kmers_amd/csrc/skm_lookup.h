@@ -166,8 +166,11 @@ struct Scanner {
 
 }  // namespace skm
 
+struct skm_query;
+
 // CmphKmerDb<StoredKmerData,8> / KeptKmerDB<8> resident in HBM (skm_db_open*, skm_annotate.hip)
 struct skm_db {
+    skm_query* aq = nullptr;     // skm_annotate's query, reused call to call (its buffers, stream)
     int device = 0;
     bool exact = false;          // KeptKmerDB semantics (skm_db_open_kept)
     uint32_t m = 0;              // hash size (BDZ) or number of kept keys (exact)

@@ -22,13 +22,16 @@
 // rank 0 gathers the kept k-mers and writes every output, exactly as one process would.
 // --comm host joins the forked ranks through socketpairs instead of RCCL (several ranks may then
 // share one GPU: --device is every rank's device; used by the tests).
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <iostream>
 #include <map>
 #include <sstream>
@@ -62,13 +65,13 @@ void die(const std::string& m) {
 std::string quoted(const std::string& p) { return "\"" + p + "\""; }
 
 // final.kmers (kmers-build-signatures.cc:212-216): "KMER\tavg_from_end\tfunction_index\t\n" per
-// kept k-mer.  Blocks of lines are formatted on `threads` threads and written in order.
+// kept k-mer.  Blocks of lines are sized first (the decimal widths), then formatted and written
+// at their offsets (pwrite) by `threads` threads, so formatting and writing overlap.
 void write_final_kmers(const std::string& path, const skm_kept& kept, int threads) {
-    std::ofstream kf(path, std::ios::binary);
     const uint64_t B = 1u << 20;  // lines per block
     const uint64_t nb = (kept.n + B - 1) / B;
-    const int T = std::max(1, threads);
-    std::vector<std::string> buf(T);
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, threads), nb));
+    auto ndig = [](unsigned v) { return v < 10 ? 1 : v < 100 ? 2 : v < 1000 ? 3 : v < 10000 ? 4 : 5; };
     auto fmt_u = [](char* p, unsigned v) {  // decimal, returns the digits written
         char t[8];
         int n = 0;
@@ -79,32 +82,50 @@ void write_final_kmers(const std::string& path, const skm_kept& kept, int thread
         for (int i = 0; i < n; ++i) p[i] = t[n - 1 - i];
         return n;
     };
-    for (uint64_t g = 0; g < nb; g += (uint64_t)T) {
-        const int m = (int)std::min<uint64_t>((uint64_t)T, nb - g);
-        auto work = [&](int t) {
-            const uint64_t a = (g + (uint64_t)t) * B, e = std::min<uint64_t>(kept.n, a + B);
-            std::string& o = buf[t];
-            o.resize((e - a) * 24);
-            char* p = &o[0];
-            for (uint64_t i = a; i < e; ++i) {
-                std::memcpy(p, &kept.keys[i], 8);
-                p[8] = '\t';
-                p += 9;
-                p += fmt_u(p, kept.data[i].avg_from_end);
-                *p++ = '\t';
-                p += fmt_u(p, kept.data[i].function_index);
-                *p++ = '\t';
-                *p++ = '\n';
-            }
-            o.resize((size_t)(p - &o[0]));
+    std::vector<uint64_t> off(nb + 1, 0);
+    auto par = [&](const std::function<void(uint64_t)>& f) {
+        std::atomic<uint64_t> next{0};
+        auto work = [&] {
+            for (uint64_t b; (b = next.fetch_add(1)) < nb;) f(b);
         };
         std::vector<std::thread> th;
-        for (int t = 1; t < m; ++t) th.emplace_back(work, t);
-        work(0);
+        for (int t = 1; t < T; ++t) th.emplace_back(work);
+        work();
         for (auto& x : th) x.join();
-        for (int t = 0; t < m; ++t) kf.write(buf[t].data(), (std::streamsize)buf[t].size());
-    }
-    if (!kf) die("cannot write " + path);
+    };
+    par([&](uint64_t b) {
+        uint64_t n = 0;
+        for (uint64_t i = b * B, e = std::min<uint64_t>(kept.n, i + B); i < e; ++i)
+            n += 12 + ndig(kept.data[i].avg_from_end) + ndig(kept.data[i].function_index);
+        off[b + 1] = n;
+    });
+    for (uint64_t b = 0; b < nb; ++b) off[b + 1] += off[b];
+    const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) die("cannot write " + path);
+    std::atomic<bool> ok{true};
+    par([&](uint64_t b) {
+        std::string o(off[b + 1] - off[b], '\0');
+        char* p = &o[0];
+        for (uint64_t i = b * B, e = std::min<uint64_t>(kept.n, i + B); i < e; ++i) {
+            std::memcpy(p, &kept.keys[i], 8);
+            p[8] = '\t';
+            p += 9;
+            p += fmt_u(p, kept.data[i].avg_from_end);
+            *p++ = '\t';
+            p += fmt_u(p, kept.data[i].function_index);
+            *p++ = '\t';
+            *p++ = '\n';
+        }
+        for (uint64_t w = 0; w < o.size();) {
+            const ssize_t r = ::pwrite(fd, o.data() + w, o.size() - w, (off_t)(off[b] + w));
+            if (r <= 0) {
+                ok = false;
+                return;
+            }
+            w += (uint64_t)r;
+        }
+    });
+    if (::close(fd) != 0 || !ok) die("cannot write " + path);
 }
 
 // binary dump of the build input (--dump-extract): u64 n_seqs, u64 n_residues, then
