@@ -244,19 +244,36 @@ int main(int argc, char** argv) {
                 set_state(g, -1, e);
                 continue;
             }
-            // the group's lines, its files in order ("id\tfunc\tfunc_index\tscore\n", :178)
-            for (size_t f = 0; f < G.files.size(); ++f)
-                for (size_t r = 0; r < G.files[f].size(); ++r) {
-                    const SeqCall& c = G.calls[f][r];
-                    G.text += G.files[f].ids[r];
-                    G.text += '\t';
-                    G.text += c.func;
-                    G.text += '\t';
-                    G.text += std::to_string((unsigned)c.fi);
-                    G.text += '\t';
-                    G.text += fmt_g(c.score);
-                    G.text += '\n';
+            // the group's lines, its files in order ("id\tfunc\tfunc_index\tscore\n", :178): each
+            // file's lines formatted on the host threads, then joined in order
+            std::vector<std::string> ftext(G.files.size());
+            std::atomic<size_t> nextf{0};
+            auto fmt = [&]() {
+                for (size_t f; (f = nextf.fetch_add(1)) < G.files.size();) {
+                    std::string& o = ftext[f];
+                    for (size_t r = 0; r < G.files[f].size(); ++r) {
+                        const SeqCall& c = G.calls[f][r];
+                        o += G.files[f].ids[r];
+                        o += '\t';
+                        o += c.func;
+                        o += '\t';
+                        o += std::to_string((unsigned)c.fi);
+                        o += '\t';
+                        o += fmt_g(c.score);
+                        o += '\n';
+                    }
                 }
+            };
+            {
+                std::vector<std::thread> th;
+                for (int t = 1; t < std::max(1, std::min<int>(n_threads, (int)G.files.size())); ++t) th.emplace_back(fmt);
+                fmt();
+                for (auto& x : th) x.join();
+            }
+            size_t tl = 0;
+            for (auto& x : ftext) tl += x.size();
+            G.text.reserve(tl);
+            for (auto& x : ftext) G.text += x;
             std::vector<std::vector<SeqCall>>().swap(G.calls);
             t_best += secs(t);
             set_state(g, 3);
