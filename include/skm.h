@@ -409,7 +409,12 @@ int skm_query_calls(skm_query* q, skm_calls* out);
  * *n_out = the total number of hits. */
 int skm_query_window_hits(skm_query* q, uint64_t* hit_off, uint32_t* pos, uint32_t* fm, uint64_t cap, uint64_t* n_out);
 void skm_query_destroy(skm_query* q);
-/* Convenience: create + run + calls + destroy. */
+/* Convenience: create + run + calls, through one query object the DB keeps for these calls (its
+ * device buffers, stream and host threads reused from batch to batch; released by
+ * skm_db_close).  A batch laid out packed -- seq_off[s] = sum over t < s of (seq_len[t] + 1),
+ * i.e. one byte after every sequence -- is uploaded as it is (the bytes between sequences are not
+ * read as residues); any other layout is packed on the host first.  Like every call on a handle,
+ * from one host thread at a time per DB. */
 int skm_annotate(skm_db* db, const uint8_t* residues, const uint64_t* seq_off, const uint32_t* seq_len,
                  size_t n_seqs, const skm_annot_opts* opts, skm_calls* out);
 void skm_calls_free(skm_calls* c);
