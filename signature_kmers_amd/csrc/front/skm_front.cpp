@@ -31,8 +31,12 @@ inline bool is_digit(unsigned char c) { return c >= '0' && c <= '9'; }
 
 struct CharClass {
     bool alpha[256];
+    bool res[256];  // a residue byte inside a data line: a letter or '*'
     CharClass() {
-        for (int c = 0; c < 256; ++c) alpha[c] = (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z');
+        for (int c = 0; c < 256; ++c) {
+            alpha[c] = (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z');
+            res[c] = alpha[c] || c == '*';
+        }
     }
 };
 const CharClass kCls;
@@ -90,22 +94,36 @@ void parse_fasta_impl(const char* buf, size_t n, FastaFile& out) {
                 } else if (c == '\n') {
                     st = S_DATA;
                 } else {
+                    // the rest of the id in one append (the bytes the per-byte states would add)
+                    const unsigned char* q = p;
+                    while (q < end && *q != ' ' && *q != '\t' && *q != '\n' && *q != '\r') ++q;
                     id.push_back((char)c);
+                    id.append(reinterpret_cast<const char*>(p), (size_t)(q - p));
+                    p = q;
                 }
                 break;
             case S_DEF:
-                if (c == '\n')
+                if (c == '\n') {
                     st = S_DATA;
-                else
+                } else {
+                    const unsigned char* q = p;
+                    while (q < end && *q != '\n' && *q != '\r') ++q;
                     def.push_back((char)c);
+                    def.append(reinterpret_cast<const char*>(p), (size_t)(q - p));
+                    p = q;
+                }
                 break;
             case S_DATA:
                 if (c == '\n') {
                     st = S_ID_OR_DATA;
-                } else if (kCls.alpha[c] || c == '*') {
+                } else if (kCls.res[c]) {
                     // fast path: the rest of a residue run
                     const unsigned char* q = p;
-                    while (q < end && (kCls.alpha[*q] || *q == '*')) ++q;
+                    // eight table lookups per step (independent loads), then byte by byte
+                    while (end - q >= 8 && (kCls.res[q[0]] & kCls.res[q[1]] & kCls.res[q[2]] & kCls.res[q[3]] &
+                                            kCls.res[q[4]] & kCls.res[q[5]] & kCls.res[q[6]] & kCls.res[q[7]]))
+                        q += 8;
+                    while (q < end && kCls.res[*q]) ++q;
                     if (Keep) {
                         out.residues.push_back(c);
                         out.residues.insert(out.residues.end(), p, q);
