@@ -6,6 +6,8 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <emmintrin.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cctype>
@@ -40,6 +42,23 @@ struct CharClass {
     }
 };
 const CharClass kCls;
+
+// the first byte at or after q (< end) that is not a residue byte (letter or '*'): 16 bytes per
+// step (SSE2 compares), then byte by byte
+inline const unsigned char* residue_run_end(const unsigned char* q, const unsigned char* end) {
+    const __m128i k20 = _mm_set1_epi8(0x20), ka = _mm_set1_epi8('a'), k25 = _mm_set1_epi8(25),
+                  kst = _mm_set1_epi8('*');
+    while (end - q >= 16) {
+        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(q));
+        const __m128i t = _mm_sub_epi8(_mm_or_si128(v, k20), ka);  // 0..25 for a letter of either case
+        const __m128i ok = _mm_or_si128(_mm_cmpeq_epi8(_mm_min_epu8(t, k25), t), _mm_cmpeq_epi8(v, kst));
+        const unsigned m = (unsigned)_mm_movemask_epi8(ok);
+        if (m != 0xFFFFu) return q + __builtin_ctz(~m);
+        q += 16;
+    }
+    while (q < end && kCls.res[*q]) ++q;
+    return q;
+}
 
 }  // namespace
 
@@ -117,19 +136,21 @@ void parse_fasta_impl(const char* buf, size_t n, FastaFile& out) {
                 if (c == '\n') {
                     st = S_ID_OR_DATA;
                 } else if (kCls.res[c]) {
-                    // fast path: the rest of a residue run
-                    const unsigned char* q = p;
-                    // eight table lookups per step (independent loads), then byte by byte
-                    while (end - q >= 8 && (kCls.res[q[0]] & kCls.res[q[1]] & kCls.res[q[2]] & kCls.res[q[3]] &
-                                            kCls.res[q[4]] & kCls.res[q[5]] & kCls.res[q[6]] & kCls.res[q[7]]))
-                        q += 8;
-                    while (q < end && kCls.res[*q]) ++q;
-                    if (Keep) {
-                        out.residues.push_back(c);
-                        out.residues.insert(out.residues.end(), p, q);
+                    // fast path: the rest of the sequence body while it is residue lines -- each
+                    // line's run, its '\n', and the next line's first byte when it is a letter
+                    // (what S_DATA -> S_ID_OR_DATA -> S_DATA would do byte by byte); anything else
+                    // goes back to the states above
+                    const unsigned char* a = p - 1;
+                    for (;;) {
+                        const unsigned char* q = residue_run_end(p, end);
+                        if (Keep) out.residues.insert(out.residues.end(), a, q);
+                        nres += (uint64_t)(q - a);
+                        p = q;
+                        if (!(end - p >= 2 && p[0] == '\n' && kCls.alpha[p[1]])) break;
+                        ++line;
+                        a = p + 1;
+                        p += 2;
                     }
-                    nres += (uint64_t)(q - p) + 1;
-                    p = q;
                 } else {
                     error(std::string("Bad data character '") + (char)c + "'");
                 }
