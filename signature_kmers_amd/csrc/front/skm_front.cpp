@@ -3,6 +3,7 @@
 
 #include <cerrno>
 #include <dirent.h>
+#include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -20,6 +21,7 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <memory>
 #include <sstream>
 #include <stdexcept>
 #include <thread>
@@ -186,15 +188,25 @@ bool parse_fasta_file(const std::string& path, FastaFile& out, bool keep_residue
     out = FastaFile();
     out.path = path;
     out.filename = path_filename(path);
-    std::ifstream f(path, std::ios::binary);
-    if (!f) return false;
-    f.seekg(0, std::ios::end);
-    std::streamoff n = f.tellg();
-    f.seekg(0);
-    std::string buf((size_t)std::max<std::streamoff>(n, 0), '\0');
-    if (n > 0) f.read(&buf[0], n);
-    if (keep_residues) out.residues.reserve((size_t)n);
-    parse_fasta_buffer(buf.data(), buf.size(), out, keep_residues);
+    // the whole file into an uninitialised buffer (no zero fill: ~1.3 MB per genome file)
+    const int fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) return false;
+    struct stat sb;
+    if (::fstat(fd, &sb) != 0) {
+        ::close(fd);
+        return false;
+    }
+    const size_t n = (size_t)std::max<off_t>(sb.st_size, 0);
+    std::unique_ptr<char[]> buf(new char[std::max<size_t>(n, 1)]);
+    size_t got = 0;
+    while (got < n) {
+        const ssize_t r = ::read(fd, buf.get() + got, n - got);
+        if (r <= 0) break;
+        got += (size_t)r;
+    }
+    ::close(fd);
+    if (keep_residues) out.residues.reserve(got);
+    parse_fasta_buffer(buf.get(), got, out, keep_residues);
     out.residues.shrink_to_fit();
     return true;
 }
