@@ -124,6 +124,12 @@ int main(int argc, char** argv) {
         set_boost_math_modes(bm == "legacy", bm == "legacy");
     }
     const int device = std::atoi(op.get("device", "0").c_str());
+    // the HIP runtime initialises on a thread of its own while the DB files are read (the first
+    // HIP call of a process costs ~0.1-0.3 s; skm_db_open's uploads then find it done)
+    std::thread hip_warm([] {
+        int ndev = 0;
+        (void)skm_device_count(&ndev);
+    });
     const std::string data_dir = op.get("data-dir");
     const std::string db_base = path_join(data_dir, "kmer_data");
     const std::string mph = db_base + ".mph", dat = db_base + ".dat";
@@ -206,6 +212,7 @@ int main(int argc, char** argv) {
     });
     std::thread device_stage([&] {
         db_thread.join();
+        hip_warm.join();
         for (size_t g = 0; g < ng; ++g) {
             if (!db_err.empty()) {
                 set_state(g, -1, db_err);
