@@ -2573,6 +2573,7 @@ struct BucketArgs {
     const uint32_t* skip;      // k_ovf_plan's verdict for the pass (nonzero: the run is being abandoned)
     uint32_t sub_target;       // k_partition: target elements per level-2 sub-bucket (0: SUB_TARGET)
     int diag;                  // option diag (diagnostics only)
+    const uint32_t* order;     // k_partition: bucket of each workgroup (k_part_order; null: blockIdx.x)
 };
 
 #define SKM_STAMP(i)                                                          \
@@ -3408,6 +3409,30 @@ __global__ __launch_bounds__(BIG_WG) void k_big_append(const BigOut* __restrict_
 // staged, and the running write offsets double as the sub-bucket table); 4096 (option
 // partition_round = 1, 2): one per CU, but each round's run per sub-bucket is twice as long, so
 // fewer 128-byte lines leave L2 partly written.
+// k_partition's workgroup order: the buckets of more than twice the mean size first, then the rest,
+// each class in bucket order.  One workgroup walks a whole bucket, and a routed heavy k-mer makes
+// its bucket several times the mean (C3: ~1 M occurrences beside a mean of ~230 K): started late in
+// bucket order, those workgroups were the kernel's tail in the passes holding heavy keys.
+__global__ __launch_bounds__(1024) void k_part_order(const uint64_t* __restrict__ bstart, uint32_t nb,
+                                                     uint32_t* __restrict__ order) {
+    __shared__ uint32_t s_wave[48];
+    const uint64_t total = bstart[nb] - bstart[0];
+    const uint64_t thr = 2 * (total / max(nb, 1u));
+    const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;
+    const uint32_t b0 = min(nb, threadIdx.x * per), b1 = min(nb, b0 + per);
+    uint32_t loc = 0;
+    for (uint32_t b = b0; b < b1; ++b) loc += bstart[b + 1] - bstart[b] > thr ? 1u : 0u;
+    uint32_t nbig;
+    uint32_t pos = wg_exclusive_scan(loc, s_wave, nbig);
+    uint32_t sp = b0 - pos;  // the small buckets before b0
+    for (uint32_t b = b0; b < b1; ++b) {
+        if (bstart[b + 1] - bstart[b] > thr)
+            order[pos++] = b;
+        else
+            order[nbig + sp++] = b;
+    }
+}
+
 template <uint32_t PT_ROUND, uint32_t PT_THREADS, int MINB>
 __global__ __launch_bounds__(PT_THREADS, MINB) void k_partition(BucketArgs A) {
     __shared__ uint32_t s_cur[(1 << MAX_B2) + 1];   // counts, then running write offsets
@@ -3416,8 +3441,8 @@ __global__ __launch_bounds__(PT_THREADS, MINB) void k_partition(BucketArgs A) {
     __shared__ uint64_t s_sh[PT_ROUND];
     __shared__ uint64_t s_sl[PT_ROUND];
     __shared__ __align__(16) uint32_t s_wave[48];
-    const uint32_t bucket = blockIdx.x;
-    if (bucket >= A.nbuckets) return;
+    if (blockIdx.x >= A.nbuckets) return;
+    const uint32_t bucket = A.order ? A.order[blockIdx.x] : blockIdx.x;
     const uint64_t r0 = A.bstart[bucket], r1 = A.bstart[bucket + 1];
     const uint64_t n = r1 - r0;
     uint32_t* tab = A.sub_tab + (uint64_t)bucket * SUB_TAB;
@@ -5004,6 +5029,7 @@ struct Tune {
     // Within noise at C3 (round 6, one box: 1434 / 1387 vs 1414 / 1377 ms/step): the scan's 25 ms
     // per step go, the tail then slows the staging more
     int tail_defer = 0;
+    int part_order = 1;              // k_partition: the buckets of > 2x the mean size first (k_part_order)
     // tail_async: the split writes the pass's elements into one of two element buffers by pass
     // parity, so the next pass's split no longer waits for this pass's tail (which reads them);
     // the wait moves to the partition.  Costs 16 B per element of the largest pass (when it fits
@@ -5114,6 +5140,7 @@ struct skm_build {
     DevBuf d_hist, d_offs, d_partial, d_rbbase, d_bstart32, d_bstart, d_owner_start;
     DevBuf d_recs_hi, d_recs_lo, d_tmp_hi, d_tmp_lo;
     DevBuf d_stg_hi, d_stg_lo;          // tail_async: the level-0 staging (else tmp holds it)
+    DevBuf d_part_order;                // k_part_order's workgroup -> bucket map
     DevBuf d_cur0, d_cur1, d_slices;   // staged scatter cursors
     DevBuf d_flagbits;
     DevBuf d_chainq;              // k_chains work queues: two counters per launch of a run
@@ -6586,7 +6613,13 @@ void phase_group(skm_build* b, uint32_t pass) {
         SKM_HIP(hipMemsetAsync(b->d_stamps.p, 0, 32 * 8, st));
         A.stamps = b->d_stamps.as<unsigned long long>();
     }
-    // ---- 4a. level-2 partition ----
+    // ---- 4a. level-2 partition (the oversized buckets' workgroups first) ----
+    A.order = nullptr;
+    if (b->tune.part_order) {
+        b->d_part_order.ensure(4ull * NB1);
+        SKM_LAUNCH(b, k_part_order, dim3(1), dim3(1024), 0, st, A.bstart, NB1, b->d_part_order.as<uint32_t>());
+        A.order = b->d_part_order.as<uint32_t>();
+    }
     if (b->tune.partition_round == 1)
         SKM_LAUNCH_AS(b, "k_partition", (k_partition<4096, 512, 1>), dim3(NB1), dim3(512), 0, st, A);
     else if (b->tune.partition_round == 2)
@@ -7626,6 +7659,7 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "big_grid_large" ? &t.big_grid_large
                : n == "big_split" ? &t.big_split
                : n == "tail_defer" ? &t.tail_defer
+               : n == "part_order" ? &t.part_order
                : n == "recs_rot" ? &t.recs_rot
                : n == "emit_group" ? &t.emit_group
                : n == "handoff_index_limit" ? &t.handoff_index_limit
