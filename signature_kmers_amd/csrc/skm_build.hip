@@ -2574,6 +2574,7 @@ struct BucketArgs {
     uint32_t sub_target;       // k_partition: target elements per level-2 sub-bucket (0: SUB_TARGET)
     int diag;                  // option diag (diagnostics only)
     const uint32_t* order;     // k_partition: bucket of each workgroup (k_part_order; null: blockIdx.x)
+    int part_class;            // k_partition: 0 all buckets, 1 the oversized ones (order[nb] of them), 2 the rest
 };
 
 #define SKM_STAMP(i)                                                          \
@@ -3431,6 +3432,7 @@ __global__ __launch_bounds__(1024) void k_part_order(const uint64_t* __restrict_
         else
             order[nbig + sp++] = b;
     }
+    if (threadIdx.x == 0) order[nb] = nbig;  // the oversized buckets: order[0, nbig)
 }
 
 template <uint32_t PT_ROUND, uint32_t PT_THREADS, int MINB>
@@ -3442,7 +3444,17 @@ __global__ __launch_bounds__(PT_THREADS, MINB) void k_partition(BucketArgs A) {
     __shared__ uint64_t s_sl[PT_ROUND];
     __shared__ __align__(16) uint32_t s_wave[48];
     if (blockIdx.x >= A.nbuckets) return;
-    const uint32_t bucket = A.order ? A.order[blockIdx.x] : blockIdx.x;
+    // part_class 1: the oversized buckets only (order[0, nbig)), 2: the others (order[nbig, nb))
+    uint32_t slot = blockIdx.x;
+    if (A.part_class) {
+        const uint32_t nbig = A.order[A.nbuckets];
+        if (A.part_class == 1 && slot >= nbig) return;
+        if (A.part_class == 2) {
+            slot += nbig;
+            if (slot >= A.nbuckets) return;
+        }
+    }
+    const uint32_t bucket = A.order ? A.order[slot] : slot;
     const uint64_t r0 = A.bstart[bucket], r1 = A.bstart[bucket + 1];
     const uint64_t n = r1 - r0;
     uint32_t* tab = A.sub_tab + (uint64_t)bucket * SUB_TAB;
@@ -5030,6 +5042,10 @@ struct Tune {
     // per step go, the tail then slows the staging more
     int tail_defer = 0;
     int part_order = 1;              // k_partition: the buckets of > 2x the mean size first (k_part_order)
+    // part_order: those buckets by 1024-thread workgroups on stream 2, beside the rest.  Within noise
+    // at C3 (round 6, one box, three alternations: 1353 / 1378 / 1378 vs 1374 / 1371 / 1353 ms/step):
+    // the heavy buckets' workgroups stay as long, now beside the rest
+    int part_split = 0;
     // tail_async: the split writes the pass's elements into one of two element buffers by pass
     // parity, so the next pass's split no longer waits for this pass's tail (which reads them);
     // the wait moves to the partition.  Costs 16 B per element of the largest pass (when it fits
@@ -5185,7 +5201,7 @@ struct skm_build {
     hipEvent_t ev_scan = nullptr;       // tail_defer: the next pass's scan kernels are done
     bool rot = false;                   // recs_rot: odd passes split into d_recs_*2
     uint64_t free_after_prepare = 0;    // device bytes free after prepare (counters [44])
-    hipEvent_t ev_part = nullptr, ev_split = nullptr;
+    hipEvent_t ev_part = nullptr, ev_split = nullptr, ev_part_heavy = nullptr;
     DevBuf d_hv_keys, d_hv_rec, d_hv_len, d_hv_s0, d_hv_s1;   // heavy keys of the split overflow
     DevBuf d_sub_tab, d_jobs2, d_jobs3;
 
@@ -6615,12 +6631,27 @@ void phase_group(skm_build* b, uint32_t pass) {
     }
     // ---- 4a. level-2 partition (the oversized buckets' workgroups first) ----
     A.order = nullptr;
+    A.part_class = 0;
     if (b->tune.part_order) {
-        b->d_part_order.ensure(4ull * NB1);
+        b->d_part_order.ensure(4ull * (NB1 + 1));
         SKM_LAUNCH(b, k_part_order, dim3(1), dim3(1024), 0, st, A.bstart, NB1, b->d_part_order.as<uint32_t>());
         A.order = b->d_part_order.as<uint32_t>();
     }
-    if (b->tune.partition_round == 1)
+    if (A.order && b->tune.part_split && b->tune.partition_round == 0 && !b->overlap) {
+        // part_split: the oversized buckets on stream 2 by 1024-thread workgroups (rounds of 4096),
+        // beside the others on the main stream -- a heavy bucket's workgroup no longer sets the
+        // kernel's length (stream 2's earlier work is joined: the split waited for the last tail)
+        BucketArgs AH = A;
+        AH.part_class = 1;
+        SKM_HIP(hipEventRecord(b->ev_part, st));
+        SKM_HIP(hipStreamWaitEvent(st2, b->ev_part, 0));
+        SKM_LAUNCH_AS(b, "k_partition", (k_partition<4096, 1024, 1>), dim3(NB1), dim3(1024), 0, st2, AH);
+        SKM_HIP(hipEventRecord(b->ev_part_heavy, st2));
+        A.part_class = 2;
+        SKM_LAUNCH_AS(b, "k_partition", (k_partition<2048, BP_THREADS, 3>), dim3(NB1), dim3(BP_THREADS), 0, st, A);
+        SKM_HIP(hipStreamWaitEvent(st, b->ev_part_heavy, 0));
+        A.part_class = 0;
+    } else if (b->tune.partition_round == 1)
         SKM_LAUNCH_AS(b, "k_partition", (k_partition<4096, 512, 1>), dim3(NB1), dim3(512), 0, st, A);
     else if (b->tune.partition_round == 2)
         SKM_LAUNCH_AS(b, "k_partition", (k_partition<4096, 1024, 1>), dim3(NB1), dim3(1024), 0, st, A);
@@ -7277,6 +7308,7 @@ int skm_build_create(skm_build** out, const int* devices, int n_devices, const s
     }
     for (auto& e : b->chain_ev) SKM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     SKM_HIP(hipEventCreateWithFlags(&b->ev_part, hipEventDisableTiming));
+    SKM_HIP(hipEventCreateWithFlags(&b->ev_part_heavy, hipEventDisableTiming));
     for (int k = 0; k < 2; ++k) {
         SKM_HIP(hipEventCreateWithFlags(&b->ev_ovf_done[k], hipEventDisableTiming));
         SKM_HIP(hipEventCreateWithFlags(&b->ev_main_done[k], hipEventDisableTiming));
@@ -7660,6 +7692,7 @@ int skm_build_set_option(skm_build* b, const char* name, int64_t value) {
                : n == "big_split" ? &t.big_split
                : n == "tail_defer" ? &t.tail_defer
                : n == "part_order" ? &t.part_order
+               : n == "part_split" ? &t.part_split
                : n == "recs_rot" ? &t.recs_rot
                : n == "emit_group" ? &t.emit_group
                : n == "handoff_index_limit" ? &t.handoff_index_limit
@@ -8077,6 +8110,7 @@ void skm_build_destroy(skm_build* b) {
             if (e) (void)hipEventDestroy(e);
     }
     if (b->ev_part) (void)hipEventDestroy(b->ev_part);
+    if (b->ev_part_heavy) (void)hipEventDestroy(b->ev_part_heavy);
     for (int k = 0; k < 2; ++k) {
         if (b->ev_ovf_done[k]) (void)hipEventDestroy(b->ev_ovf_done[k]);
         if (b->ev_main_done[k]) (void)hipEventDestroy(b->ev_main_done[k]);

@@ -92,7 +92,8 @@ def test_overflow_inline_chains(skm, gpu, inline_min):
                                                    (4, 8, {"overlap": 1, "serial_overflow": 1}),
                                                    (4, 8, {"lane_long": 0}), (16, 8, {"lane_long": 600}),
                                                    (16, 8, {"tail_defer": 1, "recs_rot": 1}), (4, 8, {"recs_rot": 1}),
-                                                   (16, 8, {"big_split": 1, "emit_group": 16})])
+                                                   (16, 8, {"big_split": 1, "emit_group": 16}),
+                                                   (16, 8, {"part_order": 0}), (16, 8, {"part_split": 0})])
 def test_key_range_passes(skm, gpu, passes, long_class, opts):
     """Out-of-core build: P passes over disjoint k-mer ranges (each k-mer in exactly one pass)
     give the single-pass result bit for bit, overflow sub-buckets and chains included, and a
@@ -104,7 +105,8 @@ def test_key_range_passes(skm, gpu, passes, long_class, opts):
     buffer set, the pass's overflow path beside the next pass), lane_long 0 / 600 (every stashed long
     chain on a wave pair / the ones of >= 600 samples: the others one lane each, k_chains),
     tail_defer / recs_rot (the pass tail issued after the next pass's scan; the split alternating two
-    element buffers), big_split with emit_group 16 (one residue scan for all 16 passes)."""
+    element buffers), big_split with emit_group 16 (one residue scan for all 16 passes), part_order 0
+    / part_split 0 (k_partition in bucket order / the oversized buckets not split off to stream 2)."""
     p = synth.generate_arrays(60000, 60, per_file=2000, seed=6)
     r, o, l, f, i, funcs = synth.build_inputs(p)
     ref = oracle_ref.build(r, o, l, f, i, len(funcs))
